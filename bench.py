@@ -1,0 +1,160 @@
+#!/usr/bin/env python3
+"""Benchmark of the subtree-dissemination hot path (BASELINE.json metric).
+
+A step = one ps_run over one batch of synthetic publishes of the workload
+(default cfg3: 1M peers, 64 topics with Zipf subscriptions, 100k messages),
+topology already resident in HBM.  Prints ONE JSON line (rank 0).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3]
+
+N > 1 is launched by torch.distributed.run (one process per GPU); peers are
+hash-partitioned (owner(p) = splitmix64(p) mod N) and the per-round frontier
+exchange runs over RCCL (see psengine/dist.py).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "go-libp2p-pubsub_amd"))
+
+import psengine as PE  # noqa: E402
+from psengine import workloads as WL  # noqa: E402
+
+METRIC = "deliveries/sec (peer×msg) at 1M peers, 1/2/4/8 GPU; % of HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PAIR_BYTES = 28.375  # SURVEY.md §8d bytes/delivery of the (peer,msg)-pair formulation
+
+DESCR = {
+    "cfg2": "100k peers, 1 topic, TreeOpts{8,20}, 10k-message burst",
+    "cfg3": "1M peers, 64 topics, Zipf(1) subscriptions, W=2/MaxW=5, 100k msgs Zipf(1) over topics",
+    "cfg4": "16M peers, 1 topic, W=8/MaxW=20, 1k-message burst",
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(eng, wl, sizes, budget_s: float = 10.0):
+    """The CPU restatement (oracle/, a port) on a bounded sample of the same
+    workload: per-message BFS over the same trees, OpenMP over messages."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    graphs = {}
+    for t in range(len(wl.topics)):
+        rp, cl = O.parents_to_csr(eng.parents(t))
+        graphs[t] = (rp, cl)
+    live = np.ones(wl.n_peers, dtype=np.uint8)
+    counts = np.bincount(wl.msg_topics, minlength=len(wl.topics)).astype(np.float64)
+    frac = 0.0005
+    done_deliv, done_msgs, spent = 0, 0, 0.0
+    while spent < budget_s and frac <= 1.0:
+        per_topic = np.maximum(1, np.round(counts * frac)).astype(int)
+        per_topic[counts == 0] = 0
+        t0 = time.perf_counter()
+        for t, k in enumerate(per_topic):
+            if k:
+                tot, _, _ = O.disseminate(*graphs[t], wl.topics[t].root, live, int(k),
+                                          want_hops=False, threads=threads)
+                done_deliv += tot
+                done_msgs += int(k)
+        spent += time.perf_counter() - t0
+        frac *= 2
+    return {"value": done_deliv / spent, "unit": "deliveries/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{done_msgs} of the workload's messages (topic mix kept), "
+                      f"{done_deliv} deliveries, {spent:.1f} s on {threads} host threads; "
+                      "oracle/psoracle.c or_disseminate (per-message BFS restating "
+                      "subtree.go:319-354 + client.go:100-132); Go reference not buildable (no go)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="cfg3", choices=sorted(DESCR))
+    ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 or world > 1:
+        from psengine import dist
+
+        return dist.bench_main(args, DESCR, METRIC)
+
+    wl = WL.CONFIGS[args.workload]() if args.scale == 1.0 else WL.scaled(args.workload, args.scale)
+    t0 = time.perf_counter()
+    eng = PE.Engine(wl.n_peers, len(wl.topics), time_kernels=True, seed=wl.seed)
+    sizes = WL.build_engine_topics(eng, wl)
+    deliv_expected = wl.expected_deliveries(sizes)
+    log(f"[bench] {wl.name}: {wl.n_peers} peers, {len(wl.topics)} topics, {sum(sizes)} "
+        f"subscriptions, {wl.n_msgs} msgs, setup {time.perf_counter() - t0:.1f}s")
+
+    def step():
+        eng.publish(wl.msg_topics)
+        return eng.run()
+
+    for _ in range(args.warmup):
+        st = step()
+        assert st.deliveries == deliv_expected, (st.deliveries, deliv_expected)
+    tot_deliv = tot_bytes = 0
+    tot_expand_ms = 0.0
+    launches = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        st = step()
+        tot_deliv += st.deliveries
+        tot_bytes += st.expand_bytes
+        tot_expand_ms += st.expand_ms
+        launches += st.expand_launches
+    wall = time.perf_counter() - t0
+    assert tot_deliv == deliv_expected * args.steps
+    value = tot_deliv / wall
+    achieved = tot_bytes / (tot_expand_ms * 1e-3) / 1e9
+    pair_gbs = value * PAIR_BYTES / 1e9
+    out = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "deliveries/s",
+        "n_gpus": 1,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic",
+        "config": {"workload": f"{wl.name}: {DESCR[wl.name]}", "peers": wl.n_peers,
+                   "topics": len(wl.topics), "subscriptions": int(sum(sizes)),
+                   "messages": wl.n_msgs, "deliveries_per_step": deliv_expected,
+                   "parallelism": "1 GPU"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "kernel": "k_expand", "avg_launch_us": tot_expand_ms * 1e3 / max(1, launches),
+                     "bytes_per_launch": tot_bytes / max(1, launches)},
+        "pair_model": {"bytes_per_delivery": PAIR_BYTES, "equiv_GBs": pair_gbs,
+                       "equiv_frac": pair_gbs / HBM_PEAK_GBS},
+        "last_step": {"rounds": st.rounds, "windows": st.windows, "run_ms": st.run_ms,
+                      "expand_ms": st.expand_ms, "edge_words": st.edge_words},
+    }
+    if not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(eng, wl, sizes, args.cpu_budget)
+    print(json.dumps(out), flush=True)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

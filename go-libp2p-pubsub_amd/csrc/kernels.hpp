@@ -1,0 +1,88 @@
+// kernels.hpp -- device data layout shared by the HIP kernels and the host
+// runtime.  See DESIGN.md §4 (HBM layout) and §5 (kernels).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace psamd {
+
+// node_flags bits (one byte per tree node)
+enum : uint8_t {
+  kNodeLive = 1,      // subscribed and live: receives and forwards
+  kNodeInternal = 2,  // has at least one child: enters the next frontier
+};
+
+// TopicDev.flags
+enum : uint32_t {
+  kTopicMesh = 1,  // a node may have several parents: seen/arrival via atomics
+};
+
+// One topic of the fused node space.  Node u of topic t (nbase <= u <
+// nbase + n_nodes) owns the 64-message words [wbase + (u-nbase)*W, +W) of the
+// seen bitset and of the two arrival buffers.
+struct TopicDev {
+  uint64_t wbase;     // first word of the topic's mask block
+  uint64_t magic;     // ceil(2^32 / W): item -> (child, word) split
+  uint32_t nbase;     // first node of the topic
+  uint32_t n_nodes;   // nodes in the topic
+  uint32_t W;         // 64-message words per node in this window (0 = idle)
+  uint32_t flags;     // kTopic*
+};
+
+// One root injection: words of a topic root that start flooding in a round.
+struct SeedDev {
+  uint64_t woff;  // word offset (root row + word)
+  uint64_t mask;  // messages entering at this round
+  uint32_t node;  // root node index
+  uint32_t pad;
+};
+
+// Per-wave counters written by the expand kernel, reduced per round.
+enum : int {
+  kCtrDeliveries = 0,
+  kCtrDuplicates,
+  kCtrEntries,
+  kCtrEntryWords,
+  kCtrChildren,
+  kCtrItemReads,
+  kCtrSeenWrites,
+  kCtrArrivalWrites,
+  kNumCtr
+};
+
+struct ExpandArgs {
+  const uint32_t* frontier;
+  const uint32_t* n_front;
+  const uint32_t* row_ptr;
+  const uint32_t* col;
+  const uint16_t* node_topic;
+  const uint8_t* node_flags;
+  const TopicDev* topics;
+  uint64_t* a_cur;   // arrivals of the current frontier (read, then cleared)
+  uint64_t* a_next;  // arrivals for the next frontier
+  uint64_t* seen;    // per-node delivered bitset (the dedup record)
+  uint8_t* next_flag;
+  uint64_t* partials;  // [n_waves][kNumCtr]
+  uint8_t* hop_rec;    // [word*64 + bit] = round, record mode only
+};
+
+constexpr int kBlock = 256;
+constexpr int kFlagsPerThread = 16;
+constexpr int kFlagsPerBlock = kBlock * kFlagsPerThread;
+
+// host-side launchers (kernels.hip)
+hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t* arrivals,
+                       uint64_t* seen, uint8_t* next_flag, hipStream_t s);
+hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid,
+                         hipStream_t s);
+hipError_t launch_flag_count(const uint8_t* flags, uint32_t n_pad, uint32_t* wg_count,
+                             const uint64_t* partials, uint32_t n_waves, uint64_t* round_stats,
+                             hipStream_t s);
+hipError_t launch_flag_compact(uint8_t* flags, uint32_t n_pad, const uint32_t* wg_count,
+                               uint32_t* frontier, uint32_t* n_front, hipStream_t s);
+hipError_t launch_digest(const uint64_t* seen, const uint32_t* node_peer,
+                         const uint16_t* node_topic, const TopicDev* topics, uint32_t n_nodes,
+                         uint64_t* out, hipStream_t s);
+
+}  // namespace psamd

@@ -1,0 +1,67 @@
+// tree.hpp -- host-side subscription tree of one topic (product code).
+//
+// Restates the reference's tree maintenance (subtree.go:16-307,356-375,
+// client.go:36-98) under the quiescent rules Q1-Q5 documented in DESIGN.md
+// §3.  This is the *input generator* for the GPU hot path: it decides which
+// peer hangs below which; the dissemination itself never runs here.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace psamd {
+
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+enum class PeerState : uint8_t { Out = 0, In = 1, Dead = 2, Failed = 3, Orphan = 4 };
+
+// The parent's record of one child (subtree.go:36-44).
+struct ChildRec {
+  uint32_t id;
+  uint32_t last_state;  // `children` of the last State message (one peer)
+  int64_t redirects;    // `size`: reset to NumPeers+1 = 1 by State, ++ per redirect
+  bool parted;          // `dead`: set by a Part message
+};
+
+class SubscriptionTree {
+ public:
+  SubscriptionTree() = default;
+  SubscriptionTree(uint32_t n_peers, uint32_t root, uint32_t width, uint32_t max_width,
+                   uint64_t seed);
+
+  // 0 or a negative PS_E_* code.
+  int subscribe(uint32_t peer);
+  int close_client(uint32_t peer);  // graceful: Part
+  int close_host(uint32_t peer);    // abrupt
+  // Called once per message that floods this topic: lazy prune and repair of
+  // failed writes at every node the message reached (rule Q3).
+  void after_message();
+  bool has_pending_failures() const { return pending_failures_; }
+  // a Part or a host failure happened since the last after_message()
+  bool needs_message_pass() const { return needs_pass_; }
+
+  // Attached structure: parent of every peer reachable from the root through
+  // subscribed peers, kNone elsewhere.
+  void attached_parents(std::vector<uint32_t>& parent) const;
+  // Peers reachable for the NEXT message (failed hosts cut their subtree).
+  // Children lists in insertion order.
+  const std::vector<ChildRec>& children(uint32_t p) const { return kids_[p]; }
+  PeerState state(uint32_t p) const { return state_[p]; }
+  uint32_t root() const { return root_; }
+  uint32_t n_peers() const { return n_; }
+
+ private:
+  int attach(uint32_t at, uint32_t joiner, bool prio);
+  void depart(uint32_t at, uint32_t gone, uint32_t rescue);
+  uint64_t next_random();
+
+  uint32_t n_ = 0, root_ = 0, width_ = 2, max_width_ = 5;
+  uint64_t rng_ = 0;
+  bool pending_failures_ = false;
+  bool needs_pass_ = false;
+  std::vector<PeerState> state_;
+  std::vector<uint32_t> up_;  // upstream peer (the other end of `in`)
+  std::vector<std::vector<ChildRec>> kids_;
+};
+
+}  // namespace psamd

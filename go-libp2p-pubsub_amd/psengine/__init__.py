@@ -1,0 +1,254 @@
+"""ctypes binding of libpsengine.so (include/psengine.h).
+
+This is plumbing for tests and bench.py: every call goes straight into the
+C ABI, whose hot path runs only as HIP kernels on the GPU.  There is no CPU
+fallback: if the library or a GPU is missing, construction fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _build
+
+NONE = 0xFFFFFFFF
+HOP_NONE = 0xFF
+MAX_ROUNDS = 256
+
+PS_OK = 0
+ERRORS = {
+    -1: "PS_E_INVAL", -2: "PS_E_NOMEM", -3: "PS_E_STATE", -4: "PS_E_NOPARENT",
+    -5: "PS_E_UNREACHABLE", -6: "PS_E_DEVICE", -7: "PS_E_RANGE", -8: "PS_E_NOTREADY",
+}
+F_RECORD_HOPS = 0x1
+F_TIME_KERNELS = 0x2
+F_NO_LAZY_SEEN = 0x4
+
+# C prototypes exported by libpsengine.so: (name, restype, argtypes)
+_P = C.c_void_p
+_u32 = C.c_uint32
+_u32p = C.POINTER(C.c_uint32)
+_i32p = C.POINTER(C.c_int32)
+_u8p = C.POINTER(C.c_uint8)
+_u64p = C.POINTER(C.c_uint64)
+
+
+class Config(C.Structure):
+    _fields_ = [("n_peers", C.c_uint32), ("n_topics", C.c_uint32), ("tree_width", C.c_uint32),
+                ("tree_max_width", C.c_uint32), ("msg_window", C.c_uint32), ("device", C.c_int32),
+                ("flags", C.c_uint32), ("reserved", C.c_uint32), ("seed", C.c_uint64)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("deliveries", C.c_uint64), ("duplicates", C.c_uint64),
+                ("frontier_entries", C.c_uint64), ("child_visits", C.c_uint64),
+                ("edge_words", C.c_uint64), ("expand_bytes", C.c_uint64),
+                ("windows", C.c_uint64), ("rounds", C.c_uint64), ("expand_launches", C.c_uint64),
+                ("run_ms", C.c_double), ("expand_ms", C.c_double),
+                ("deliveries_per_round", C.c_uint64 * MAX_ROUNDS)]
+
+    def as_dict(self) -> dict:
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "deliveries_per_round"}
+        per = list(self.deliveries_per_round)
+        while per and per[-1] == 0:
+            per.pop()
+        d["deliveries_per_round"] = per
+        return d
+
+
+PROTOTYPES = [
+    ("ps_version", C.c_char_p, []),
+    ("ps_create", C.c_int, [C.POINTER(Config), C.POINTER(_P)]),
+    ("ps_destroy", None, [_P]),
+    ("ps_last_error", C.c_char_p, [_P]),
+    ("ps_topic_create", C.c_int, [_P, _u32, _u32, _u32, _u32]),
+    ("ps_topic_close", C.c_int, [_P, _u32]),
+    ("ps_topic_join", C.c_int, [_P, _u32, _u32p, C.c_size_t, _i32p]),
+    ("ps_topic_leave", C.c_int, [_P, _u32, _u32p, C.c_size_t]),
+    ("ps_topic_drop", C.c_int, [_P, _u32, _u32p, C.c_size_t]),
+    ("ps_topic_set_tree", C.c_int, [_P, _u32, _u32, _u32p]),
+    ("ps_topic_set_children", C.c_int, [_P, _u32, _u32, _u32p, _u32p]),
+    ("ps_topic_get_parents", C.c_int, [_P, _u32, _u32p]),
+    ("ps_topic_depth", C.c_int, [_P, _u32, _u32p, _u32p]),
+    ("ps_set_live", C.c_int, [_P, _u8p]),
+    ("ps_publish", C.c_int, [_P, _u32p, C.c_size_t, _u32p]),
+    ("ps_publish_at", C.c_int, [_P, _u32p, _u32p, C.c_size_t, _u32p]),
+    ("ps_run", C.c_int, [_P, C.POINTER(Stats)]),
+    ("ps_read_hops", C.c_int, [_P, _u32, _u8p]),
+    ("ps_read_delivered", C.c_int, [_P, _u32, _u8p]),
+    ("ps_seen_digest", C.c_int, [_P, _u64p]),
+]
+
+_lib = None
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def load(build_if_missing: bool = False):
+    """Loads libpsengine.so and binds every prototype (raises if absent)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_build.LIB):
+            if not build_if_missing:
+                raise FileNotFoundError(
+                    f"{_build.LIB} missing: run __graft_entry__.build() (no CPU fallback exists)")
+            _build.build()
+        L = C.CDLL(_build.LIB)
+        for name, res, args in PROTOTYPES:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+class EngineError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+def _u32arr(a) -> np.ndarray:
+    return np.ascontiguousarray(a, dtype=np.uint32)
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+class Engine:
+    """One engine = one GPU's worth of topics (NewTopicManager, pubsub.go:26-31)."""
+
+    def __init__(self, n_peers: int, n_topics: int = 1, tree_width: int = 2,
+                 tree_max_width: int = 5, msg_window: int = 65536, device: int = 0,
+                 record_hops: bool = False, time_kernels: bool = False, seed: int = 1,
+                 flags: int = 0):
+        L = load()
+        self.n_peers = n_peers
+        self.n_topics = n_topics
+        self.seed = seed
+        f = flags | (F_RECORD_HOPS if record_hops else 0) | (F_TIME_KERNELS if time_kernels else 0)
+        cfg = Config(n_peers, n_topics, tree_width, tree_max_width, msg_window, device, f, 0, seed)
+        h = _P()
+        rc = L.ps_create(C.byref(cfg), C.byref(h))
+        if rc != PS_OK:
+            raise EngineError(rc, "ps_create failed (is a GPU visible?)")
+        self._h = h
+        self._L = L
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.ps_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, rc: int) -> int:
+        if rc < 0:
+            raise EngineError(rc, self._L.ps_last_error(self._h).decode())
+        return rc
+
+    @staticmethod
+    def topic_seed(seed: int, topic: int) -> int:
+        """Redirect tie-break seed of a topic created with ps_topic_create."""
+        return (seed ^ (0xA5A5A5A5 * (topic + 1))) & ((1 << 64) - 1)
+
+    # topics
+    def topic_create(self, topic: int, root: int, tree_width: int = 0, tree_max_width: int = 0):
+        self._check(self._L.ps_topic_create(self._h, topic, root, tree_width, tree_max_width))
+
+    def topic_close(self, topic: int):
+        self._check(self._L.ps_topic_close(self._h, topic))
+
+    def join(self, topic: int, peers, check: bool = True) -> np.ndarray:
+        p = _u32arr(peers)
+        st = np.zeros(p.shape[0], dtype=np.int32)
+        rc = self._L.ps_topic_join(self._h, topic, _p(p, C.c_uint32), p.shape[0],
+                                   _p(st, C.c_int32))
+        if check:
+            self._check(rc)
+        return st
+
+    def leave(self, topic: int, peers):
+        p = _u32arr(peers)
+        self._check(self._L.ps_topic_leave(self._h, topic, _p(p, C.c_uint32), p.shape[0]))
+
+    def drop(self, topic: int, peers):
+        p = _u32arr(peers)
+        self._check(self._L.ps_topic_drop(self._h, topic, _p(p, C.c_uint32), p.shape[0]))
+
+    def set_tree(self, topic: int, root: int, parent):
+        par = _u32arr(parent)
+        assert par.shape[0] == self.n_peers
+        self._check(self._L.ps_topic_set_tree(self._h, topic, root, _p(par, C.c_uint32)))
+
+    def set_children(self, topic: int, root: int, row_ptr, col):
+        rp, cl = _u32arr(row_ptr), _u32arr(col)
+        assert rp.shape[0] == self.n_peers + 1
+        if cl.shape[0] == 0:
+            cl = np.zeros(1, dtype=np.uint32)
+        self._check(self._L.ps_topic_set_children(self._h, topic, root, _p(rp, C.c_uint32),
+                                                  _p(cl, C.c_uint32)))
+
+    def parents(self, topic: int) -> np.ndarray:
+        out = np.empty(self.n_peers, dtype=np.uint32)
+        self._check(self._L.ps_topic_get_parents(self._h, topic, _p(out, C.c_uint32)))
+        return out
+
+    def depth(self, topic: int) -> tuple[int, int]:
+        d, n = C.c_uint32(), C.c_uint32()
+        self._check(self._L.ps_topic_depth(self._h, topic, C.byref(d), C.byref(n)))
+        return d.value, n.value
+
+    def set_live(self, live):
+        lv = np.ascontiguousarray(live, dtype=np.uint8)
+        assert lv.shape[0] == self.n_peers
+        self._check(self._L.ps_set_live(self._h, _p(lv, C.c_uint8)))
+
+    # hot path
+    def publish(self, topics, start_rounds=None) -> int:
+        t = _u32arr(topics)
+        first = C.c_uint32()
+        if start_rounds is None:
+            self._check(self._L.ps_publish(self._h, _p(t, C.c_uint32), t.shape[0], C.byref(first)))
+        else:
+            s = _u32arr(start_rounds)
+            assert s.shape == t.shape
+            self._check(self._L.ps_publish_at(self._h, _p(t, C.c_uint32), _p(s, C.c_uint32),
+                                              t.shape[0], C.byref(first)))
+        return first.value
+
+    def run(self) -> Stats:
+        st = Stats()
+        self._check(self._L.ps_run(self._h, C.byref(st)))
+        return st
+
+    def hops(self, msg: int) -> np.ndarray:
+        out = np.empty(self.n_peers, dtype=np.uint8)
+        self._check(self._L.ps_read_hops(self._h, msg, _p(out, C.c_uint8)))
+        return out
+
+    def delivered(self, msg: int) -> np.ndarray:
+        out = np.empty(self.n_peers, dtype=np.uint8)
+        self._check(self._L.ps_read_delivered(self._h, msg, _p(out, C.c_uint8)))
+        return out
+
+    def seen_digest(self) -> int:
+        d = C.c_uint64()
+        self._check(self._L.ps_seen_digest(self._h, C.byref(d)))
+        return d.value
+
+
+def version() -> str:
+    return load().ps_version().decode()

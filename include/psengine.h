@@ -1,0 +1,151 @@
+/*
+ * psengine.h -- C ABI of the MI355X subtree-dissemination engine.
+ *
+ * Drop-in boundary for the one hot path of go-libp2p-pubsub v0: flooding
+ * published messages down each topic's subscription tree (subtree.go).
+ * Plain C types only (no torch, no HIP types): a cgo shim, ctypes or C++ binds
+ * it directly.  Every entry point names the reference interface it replaces.
+ *
+ * Conventions:
+ *  - return codes: 0 = PS_OK, negative = PS_E_*; the cgo shim turns a negative
+ *    code plus ps_last_error() into a Go `error`.
+ *  - caller arrays are borrowed for the duration of the call and copied;
+ *    the engine owns all device memory.
+ *  - an engine is NOT thread-safe; the caller serialises calls, as
+ *    subtree.chlock does in the reference (subtree.go:18,320).
+ *  - peers are dense u32 ids [0, n_peers) standing in for peer.ID
+ *    (go-libp2p-peer); messages are u32 publish indices returned by
+ *    ps_publish (the reference's Message has no ID, pubsub.go:146-153).
+ */
+#ifndef PSENGINE_H
+#define PSENGINE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PS_NONE 0xFFFFFFFFu
+#define PS_HOP_NONE 0xFFu
+#define PS_MAX_ROUNDS 256
+
+enum ps_status {
+  PS_OK = 0,
+  PS_E_INVAL = -1,       /* bad argument                                        */
+  PS_E_NOMEM = -2,       /* host or device allocation failed                    */
+  PS_E_STATE = -3,       /* peer/topic in the wrong state for the request       */
+  PS_E_NOPARENT = -4,    /* redirectJoin found no live child (subtree.go:172)   */
+  PS_E_UNREACHABLE = -5, /* join redirected into a closed host (subtree.go:302) */
+  PS_E_DEVICE = -6,      /* HIP runtime error                                   */
+  PS_E_RANGE = -7,       /* message id / topic id out of range                  */
+  PS_E_NOTREADY = -8     /* no completed run holds the requested record         */
+};
+
+/* ps_config.flags */
+#define PS_F_RECORD_HOPS 0x1u  /* keep (peer,msg)->hop for ps_read_hops (parity) */
+#define PS_F_TIME_KERNELS 0x2u /* HIP-event time every expand launch            */
+#define PS_F_NO_LAZY_SEEN 0x4u /* clear the seen bitset eagerly per window      */
+
+typedef struct ps_config {
+  uint32_t n_peers;        /* peer id space [0, n_peers)                       */
+  uint32_t n_topics;       /* topic slots [0, n_topics)                        */
+  uint32_t tree_width;     /* DefaultTreeWidth  (pubsub.go:16), 0 -> 2         */
+  uint32_t tree_max_width; /* DefaultTreeMaxWidth (pubsub.go:17), 0 -> 5       */
+  uint32_t msg_window;     /* max messages per topic per window, 0 -> 65536    */
+  int32_t device;          /* HIP device ordinal                               */
+  uint32_t flags;          /* PS_F_*                                           */
+  uint32_t reserved;
+  uint64_t seed;           /* redirect tie-break stream (Go map order, Q2)     */
+} ps_config;
+
+typedef struct ps_stats {
+  uint64_t deliveries;         /* (peer,msg) pairs delivered by this run        */
+  uint64_t duplicates;         /* bits suppressed by the seen test (0 on trees)  */
+  uint64_t frontier_entries;   /* frontier nodes expanded                        */
+  uint64_t child_visits;       /* (frontier node, child) pairs                   */
+  uint64_t edge_words;         /* (child, 64-message word) pairs tested          */
+  uint64_t expand_bytes;       /* algorithmic HBM bytes of the expand kernel     */
+  uint64_t windows;            /* propagation windows                            */
+  uint64_t rounds;             /* synchronous rounds launched                    */
+  uint64_t expand_launches;    /* expand kernel launches                         */
+  double run_ms;               /* device time of the whole run (HIP events)      */
+  double expand_ms;            /* summed expand-kernel device time (TIME flag)   */
+  uint64_t deliveries_per_round[PS_MAX_ROUNDS];
+} ps_stats;
+
+typedef struct ps_engine ps_engine;
+
+/* ---- lifecycle: NewTopicManager (pubsub.go:26-31) ------------------------ */
+int ps_create(const ps_config* cfg, ps_engine** out);
+void ps_destroy(ps_engine* e);
+const char* ps_last_error(const ps_engine* e);
+const char* ps_version(void);
+
+/* ---- topics: TopicManager.NewTopic + TreeOpts (pubsub.go:49-97),
+ *      Topic.Close (pubsub.go:99-103).  width 0 -> engine default.            */
+int ps_topic_create(ps_engine* e, uint32_t topic, uint32_t root,
+                    uint32_t tree_width, uint32_t tree_max_width);
+int ps_topic_close(ps_engine* e, uint32_t topic);
+
+/* ---- membership, restated on the host (sequential by nature):
+ * ps_topic_join:  TopicManager.Subscribe -> joinToPeer -> handleJoin /
+ *                 redirectJoin / joinParents (client.go:65-94,
+ *                 subtree.go:100-307).  status_out[i] (nullable) gets the
+ *                 per-peer PS_* code; the call returns the first failure.
+ * ps_topic_leave: client.Close -> Part -> redistributeChildren
+ *                 (client.go:30-34, subtree.go:46-98,356-375).
+ * ps_topic_drop:  host.Close(): abrupt; the parent notices on its next write
+ *                 (subtree.go:333-351); that message is lost below the peer. */
+int ps_topic_join(ps_engine* e, uint32_t topic, const uint32_t* peers, size_t n,
+                  int32_t* status_out);
+int ps_topic_leave(ps_engine* e, uint32_t topic, const uint32_t* peers, size_t n);
+int ps_topic_drop(ps_engine* e, uint32_t topic, const uint32_t* peers, size_t n);
+
+/* ---- explicit topology (harness / parity inputs) ---------------------------
+ * set_tree:     parent[p] for every peer (PS_NONE = not in the tree); the tree
+ *               printTree walks (pubsub_test.go:204-229).
+ * set_children: general child lists in peer space (row_ptr[n_peers+1],
+ *               col[row_ptr[n_peers]]); a peer may have several parents
+ *               (mesh), in which case the seen bitset deduplicates.
+ * get_parents:  current attached tree (PS_NONE = not attached / orphaned).   */
+int ps_topic_set_tree(ps_engine* e, uint32_t topic, uint32_t root, const uint32_t* parent);
+int ps_topic_set_children(ps_engine* e, uint32_t topic, uint32_t root,
+                          const uint32_t* row_ptr, const uint32_t* col);
+int ps_topic_get_parents(ps_engine* e, uint32_t topic, uint32_t* parent_out);
+int ps_topic_depth(ps_engine* e, uint32_t topic, uint32_t* depth_out, uint32_t* n_nodes_out);
+
+/* Subscribed-and-live mask over peers (1 = receives and forwards).  A peer
+ * whose client stopped reading (client.go:103-131) is 0. Default: all 1. */
+int ps_set_live(ps_engine* e, const uint8_t* live);
+
+/* ---- the hot path ----------------------------------------------------------
+ * ps_publish:    Topic.PublishMessage (pubsub.go:111-120) for a batch; message
+ *                i of the batch gets id *first_msg_id_out + i.
+ * ps_publish_at: same, message i enters its topic root at round start_round[i]
+ *                (paced / pipelined publishing; hop = round - start_round).
+ * ps_run:        forwardMessage (subtree.go:319-354) + processMessages
+ *                (client.go:100-132) for every enqueued message, as
+ *                synchronous rounds on the GPU, to quiescence.               */
+int ps_publish(ps_engine* e, const uint32_t* topic_of_msg, size_t n_msgs,
+               uint32_t* first_msg_id_out);
+int ps_publish_at(ps_engine* e, const uint32_t* topic_of_msg, const uint32_t* start_round,
+                  size_t n_msgs, uint32_t* first_msg_id_out);
+int ps_run(ps_engine* e, ps_stats* out);
+
+/* ---- results of the last ps_run (client.Messages, client.go:26-28) --------
+ * ps_read_hops: hop of message `msg` at every peer (PS_HOP_NONE = not
+ *               delivered); needs PS_F_RECORD_HOPS.
+ * ps_read_delivered: 1 where `msg` was delivered (seen bit set), any mode,
+ *               for messages of the last window of the last run.            */
+int ps_read_hops(ps_engine* e, uint32_t msg, uint8_t* hop_per_peer);
+int ps_read_delivered(ps_engine* e, uint32_t msg, uint8_t* delivered_per_peer);
+/* Order-independent digest of the final seen state of the last window:
+ * sum over (peer, topic, word) of mix64(peer, topic, word, seen bits). */
+int ps_seen_digest(ps_engine* e, uint64_t* digest_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSENGINE_H */
