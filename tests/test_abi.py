@@ -1,0 +1,75 @@
+"""CPU checks of the drop-in boundary: libpsengine.so builds for gfx950,
+loads, and exports every entry point include/psengine.h declares; the ctypes
+structs match the C layout.  No compute calls (no GPU here)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import psengine as PE
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "psengine.h")
+
+
+def declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(ps_[a-z_0-9]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from psengine import _build
+
+    _build.build()
+    return PE.load()
+
+
+def test_header_symbols_exported(lib):
+    names = declared()
+    assert len(names) >= 20
+    out = subprocess.run(["nm", "-D", "--defined-only", PE.lib_path()], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (ps_\w+)", out))
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+    bound = {p[0] for p in PE.PROTOTYPES}
+    assert set(names) == bound, set(names) ^ bound
+
+
+def test_code_object_is_gfx950(lib):
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading",
+                          PE.lib_path()], capture_output=True, text=True)
+    text = out.stdout + out.stderr
+    assert "gfx950" in text
+
+
+def test_struct_layouts(lib):
+    assert ctypes.sizeof(PE.Config) == 40
+    assert ctypes.sizeof(PE.Stats) == 9 * 8 + 2 * 8 + PE.MAX_ROUNDS * 8
+    src = open(HEADER).read()
+    assert f"#define PS_MAX_ROUNDS {PE.MAX_ROUNDS}" in src
+    for name, val in [("PS_F_RECORD_HOPS", PE.F_RECORD_HOPS), ("PS_F_TIME_KERNELS", PE.F_TIME_KERNELS)]:
+        assert re.search(rf"#define {name} 0x{val:x}u", src)
+
+
+def test_version_and_error_paths(lib):
+    assert b"gfx950" in lib.ps_version()
+    assert lib.ps_create(None, None) == -1  # PS_E_INVAL
+    assert lib.ps_last_error(None) == b"null engine"
+    cfg = PE.Config(0, 1, 2, 5, 0, 0, 0, 0, 1)
+    h = ctypes.c_void_p()
+    assert lib.ps_create(ctypes.byref(cfg), ctypes.byref(h)) == -1  # n_peers == 0
+
+
+def test_no_cpu_fallback_without_gpu(lib):
+    """On a machine without a GPU the engine refuses to start (PS_E_DEVICE):
+    there is no silent CPU path."""
+    if os.path.exists("/dev/kfd"):
+        pytest.skip("GPU driver present")
+    with pytest.raises(PE.EngineError) as ei:
+        PE.Engine(8)
+    assert ei.value.code == -6

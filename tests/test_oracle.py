@@ -1,0 +1,183 @@
+"""CPU tests of the oracle (test infrastructure): the C restatement
+(oracle/psoracle.c) is pinned against the independent Python restatement
+(oracle/event_sim.py), the committed golden fixtures and the reference's own
+test assertions (pubsub_test.go:101-325)."""
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import event_sim as ES
+import oracle as O
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def load(name):
+    with open(os.path.join(GOLD, name)) as f:
+        return json.load(f)
+
+
+def unhex(s):
+    return np.frombuffer(bytes.fromhex(s), dtype=np.uint8)
+
+
+def unhex32(s):
+    return np.frombuffer(bytes.fromhex(s), dtype=np.uint32)
+
+
+@pytest.mark.parametrize("trial", range(150))
+def test_c_tree_matches_python_restatement(oracle_lib, trial):
+    """Random join / leave / drop / message sequences: the two independent
+    restatements agree on every attach decision, repair and delivered hop."""
+    rng = random.Random(trial)
+    n = rng.randint(4, 60)
+    W = rng.randint(1, 4)
+    MW = W + rng.randint(0, 4)
+    seed = rng.randint(0, 2**63)
+    ct = O.Tree(n, 0, W, MW, seed)
+    pt = ES.Topic(n, 0, W, MW, seed)
+    for step in range(rng.randint(5, 80)):
+        op = rng.random()
+        if op < 0.55:
+            p = rng.randrange(1, n)
+            rc = ct.join(p)
+            try:
+                pt.subscribe(p)
+                prc = 0
+            except (ValueError, ConnectionError, RuntimeError):
+                prc = -1
+            assert (rc == 0) == (prc == 0), (trial, step, p, rc)
+        elif op < 0.7:
+            ins = [p for p in range(1, n) if ct.state(p) == O.IN]
+            if ins:
+                p = rng.choice(ins)
+                ct.leave(p)
+                pt.leave(p)
+        elif op < 0.8:
+            ins = [p for p in range(1, n) if ct.state(p) == O.IN]
+            if ins:
+                p = rng.choice(ins)
+                ct.drop(p)
+                pt.drop(p)
+        else:
+            h = ct.message()
+            got = pt.publish([b"x"], random.Random(step))
+            ph = np.full(n, 255, np.uint8)
+            for peer, lst in enumerate(got):
+                for _, hop in lst:
+                    ph[peer] = hop
+            assert np.array_equal(h, ph), (trial, step)
+        assert np.array_equal(ct.parents(), np.array(pt.parents(), np.uint32)), (trial, step)
+
+
+def test_golden_cfg1(oracle_lib):
+    g = load("cfg1.json")
+    t = O.Tree(g["n_peers"], g["root"], g["width"], g["max_width"], g["seed"])
+    t.join_all(g["join_order"])
+    par = t.parents()
+    assert par.tolist() == g["parent"]
+    rp, cl = O.parents_to_csr(par)
+    total, hops, _ = O.disseminate(rp, cl, g["root"], np.ones(g["n_peers"], np.uint8), g["n_msgs"])
+    assert total == g["deliveries"] == 15000
+    exp = unhex(g["hops_per_message"])
+    assert all(np.array_equal(hops[m], exp) for m in range(g["n_msgs"]))
+
+
+def test_golden_multitopic(oracle_lib):
+    g = load("multitopic_1k.json")
+    n = g["n_peers"]
+    for tp in g["topics"]:
+        t = O.Tree(n, tp["root"], tp["width"], tp["max_width"], tp["seed"])
+        t.join_all(tp["join_order"])
+        assert t.parents().tolist() == tp["parent"]
+        assert np.array_equal(t.message(), unhex(tp["hops"]))
+
+
+def test_golden_churn(oracle_lib):
+    g = load("churn_300.json")
+    t = O.Tree(g["n_peers"], g["root"], g["width"], g["max_width"], g["seed"])
+    for k, op in enumerate(g["ops"]):
+        if op["op"] == "join":
+            assert (t.join(op["peer"]) == 0) == op["ok"], k
+        elif op["op"] == "leave":
+            assert t.leave(op["peer"]) == 0, k
+        elif op["op"] == "drop":
+            assert t.drop(op["peer"]) == 0, k
+        else:
+            assert np.array_equal(t.message(), unhex(op["hops"])), k
+            assert np.array_equal(t.parents(), unhex32(op["parent"])), k
+
+
+def test_reference_scenarios(oracle_lib):
+    """pubsub_test.go's four tests, restated: for every tie-break seed the C
+    restatement reproduces the fixture, and the fixture satisfies the
+    reference test's own assertion (each non-skipped subscriber receives)."""
+    g = load("scenarios.json")
+    for sc in g["scenarios"]:
+        n = sc["hosts"]
+        for run in sc["runs"]:
+            t = O.Tree(n, 0, g["width"], g["max_width"], run["seed"])
+            t.join_all(range(1, n))
+            assert t.parents().tolist() == run["parent"], (sc["name"], run["seed"])
+            pubs = iter(run["publishes"])
+            for step in sc["steps"]:
+                if step[0] == "drop":
+                    t.drop(step[1])
+                elif step[0] == "leave":
+                    t.leave(step[1])
+                else:
+                    for mid in step[1]:
+                        rec = next(pubs)
+                        assert rec["mid"] == mid
+                        h = t.message()
+                        assert np.array_equal(h, unhex(rec["hops"])), (sc["name"], mid)
+                        for i in range(n - 1):
+                            if i not in step[2]:
+                                assert h[i + 1] != 255, (sc["name"], run["seed"], mid, i)
+
+
+def test_disseminate_edge_cases(oracle_lib):
+    # root alone; dead child cuts its subtree; self-loop and cycle back to root
+    rp = np.array([0, 0], np.uint32)
+    tot, h, _ = O.disseminate(rp, np.zeros(0, np.uint32), 0, np.ones(1, np.uint8), 3)
+    assert tot == 0 and (h == 255).all()
+    par = np.array([O.NONE, 0, 1, 2, 0], np.uint32)
+    rp, cl = O.parents_to_csr(par)
+    live = np.array([1, 1, 0, 1, 1], np.uint8)
+    tot, h, hist = O.disseminate(rp, cl, 0, live, 2)
+    assert h[0].tolist() == [255, 1, 255, 255, 1] and tot == 4 and hist[1] == 4
+    # mesh: 0 -> 1, 0 -> 2, 1 -> 2, 2 -> 0, 2 -> 2
+    rp = np.array([0, 2, 3, 5], np.uint32)
+    cl = np.array([1, 2, 2, 0, 2], np.uint32)
+    tot, h, _ = O.disseminate(rp, cl, 0, np.ones(3, np.uint8), 1)
+    assert h[0].tolist() == [255, 1, 1] and tot == 2
+
+
+def test_async_flood_equals_round_synchronous(oracle_lib):
+    """asynchronous FIFO flooding with random latencies gives
+    hop = depth and per-peer publish order, i.e. the round-synchronous model."""
+    for seed in range(5):
+        n = 200
+        t = ES.build_join_tree(n, 0, 3, 6, seed)
+        got = t.publish([b"a"] * 30, random.Random(seed), pace=0.0)
+        par = np.array(t.parents(), np.uint32)
+        d = ES.depths(list(par), 0)
+        for peer in range(1, n):
+            assert [m for m, _ in got[peer]] == list(range(30))
+            assert all(hop == d[peer] for _, hop in got[peer])
+        rp, cl = O.parents_to_csr(par)
+        _, hops, _ = O.disseminate(rp, cl, 0, np.ones(n, np.uint8), 1)
+        assert hops[0][1:].tolist() == d[1:]
+
+
+def test_splitmix_matches_workload_generator(oracle_lib):
+    import ctypes
+
+    from psengine import workloads as WL
+
+    s = ctypes.c_uint64(12345)
+    vals = [O.lib().or_splitmix64(ctypes.byref(s)) for _ in range(5)]
+    assert vals == [int(x) for x in WL.stream(12345, np.arange(5))]
