@@ -148,7 +148,8 @@ def main():
         "pair_model": {"bytes_per_delivery": PAIR_BYTES, "equiv_GBs": pair_gbs,
                        "equiv_frac": pair_gbs / HBM_PEAK_GBS},
         "last_step": {"rounds": st.rounds, "windows": st.windows, "run_ms": st.run_ms,
-                      "expand_ms": st.expand_ms, "edge_words": st.edge_words},
+                      "expand_ms": st.expand_ms, "host_ms": st.host_ms,
+                      "edge_words": st.edge_words},
     }
     if not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(eng, wl, sizes, args.cpu_budget)

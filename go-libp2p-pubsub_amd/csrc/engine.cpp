@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -102,8 +103,9 @@ struct ps_engine {
   std::vector<uint8_t> node_flags;
 
   DevBuf d_row_ptr, d_col, d_node_topic, d_node_flags, d_node_peer;
-  DevBuf d_seen, d_arr0, d_arr1, d_hop, d_flags, d_frontier, d_nfront, d_wgcount, d_partials,
-      d_stats, d_topics, d_seeds, d_digest;
+  DevBuf d_seen, d_arr0, d_arr1, d_hop, d_flags, d_blk, d_gen, d_frontier, d_nfront, d_wgcount,
+      d_partials, d_stats, d_topics, d_seeds, d_digest;
+  uint32_t gen_cur = 0;  // window generation stamped into d_gen (1..255)
 
   // publishes not yet run
   std::vector<RunMsg> pending;
@@ -281,6 +283,12 @@ int upload_graph(ps_engine* e) {
     const size_t flag_bytes = static_cast<size_t>(ceil_div(e->n_pad, kFlagsPerBlock)) * kFlagsPerBlock;
     HIP_TRY(e->d_flags.ensure(flag_bytes, &fresh), "alloc flags");
     HIP_TRY(hipMemsetAsync(e->d_flags.p, 0, e->d_flags.bytes, e->stream), "clear flags");
+    const size_t n_blk = ceil_div(e->n_pad, kFlagsPerBlock);
+    HIP_TRY(e->d_blk.ensure(n_blk), "alloc block flags");
+    HIP_TRY(hipMemsetAsync(e->d_blk.p, 0, e->d_blk.bytes, e->stream), "clear block flags");
+    HIP_TRY(e->d_gen.ensure(e->n_pad), "alloc generations");
+    HIP_TRY(hipMemsetAsync(e->d_gen.p, 0, e->d_gen.bytes, e->stream), "clear generations");
+    e->gen_cur = 0;  // node ids changed: every row is stale
     HIP_TRY(e->d_frontier.ensure(std::max<size_t>(nn, 1) * 4), "alloc frontier");
     HIP_TRY(e->d_wgcount.ensure(static_cast<size_t>(ceil_div(e->n_pad, kFlagsPerBlock)) * 4),
             "alloc wg_count");
@@ -327,12 +335,11 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
   }
   if (wtot == 0) return PS_OK;
   const bool record = (e->cfg.flags & PS_F_RECORD_HOPS) != 0;
-  bool fresh0 = false, fresh1 = false;
   HIP_TRY(e->d_seen.ensure(wtot * 8), "alloc seen");
-  HIP_TRY(e->d_arr0.ensure(wtot * 8, &fresh0), "alloc arrivals");
-  HIP_TRY(e->d_arr1.ensure(wtot * 8, &fresh1), "alloc arrivals");
-  if (fresh0) HIP_TRY(hipMemsetAsync(e->d_arr0.p, 0, e->d_arr0.bytes, e->stream), "clear arrivals");
-  if (fresh1) HIP_TRY(hipMemsetAsync(e->d_arr1.p, 0, e->d_arr1.bytes, e->stream), "clear arrivals");
+  HIP_TRY(e->d_arr0.ensure(wtot * 8), "alloc arrivals");
+  HIP_TRY(e->d_arr1.ensure(wtot * 8), "alloc arrivals");
+  bool any_mesh = false;
+  for (uint32_t t = 0; t < nt; ++t) any_mesh |= (tab[t].W && (tab[t].flags & kTopicMesh));
   if (record) HIP_TRY(e->d_hop.ensure(wtot * 64), "alloc hop record");
   const uint32_t n_waves = e->expand_grid * (kBlock / 64);
   HIP_TRY(e->d_partials.ensure(static_cast<size_t>(n_waves) * kNumCtr * 8), "alloc partials");
@@ -371,7 +378,22 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
                          hipMemcpyHostToDevice, s),
           "upload seeds");
   HIP_TRY(hipEventRecord(e->ev_run0, s), "event");
-  HIP_TRY(hipMemsetAsync(e->d_seen.p, 0, wtot * 8, s), "clear seen");
+  // new window generation: every tree row from older windows becomes stale
+  if (++e->gen_cur > 255) {
+    HIP_TRY(hipMemsetAsync(e->d_gen.p, 0, e->d_gen.bytes, s), "clear generations");
+    e->gen_cur = 1;
+  }
+  HIP_TRY(launch_window_init(e->d_topics.as<TopicDev>(), nt, e->d_seen.as<uint64_t>(),
+                             e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>(),
+                             e->d_gen.as<uint8_t>(), e->gen_cur, any_mesh, s),
+          "window init");
+  if (e->cfg.flags & PS_F_NO_LAZY_SEEN) {
+    // eager variant: clear every row and mark every node current, so the
+    // expand kernel reads each child's seen word before it tests and sets it
+    HIP_TRY(hipMemsetAsync(e->d_seen.p, 0, wtot * 8, s), "clear seen");
+    HIP_TRY(hipMemsetAsync(e->d_gen.p, static_cast<int>(e->gen_cur), e->d_gen.bytes, s),
+            "stamp generations");
+  }
   if (record) HIP_TRY(hipMemsetAsync(e->d_hop.p, 0xFF, wtot * 64, s), "clear hop record");
 
   ExpandArgs a{};
@@ -383,7 +405,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
   a.node_flags = e->d_node_flags.as<uint8_t>();
   a.topics = e->d_topics.as<TopicDev>();
   a.seen = e->d_seen.as<uint64_t>();
+  a.gen = e->d_gen.as<uint8_t>();
+  a.gen_cur = e->gen_cur;
   a.next_flag = e->d_flags.as<uint8_t>();
+  a.blk_flag = e->d_blk.as<uint8_t>();
   a.partials = e->d_partials.as<uint64_t>();
   a.hop_rec = record ? e->d_hop.as<uint8_t>() : nullptr;
   uint64_t* arr[2] = {e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>()};
@@ -393,14 +418,15 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
   auto seed_round = [&](uint32_t r, uint64_t* into) -> hipError_t {
     if (r > max_start) return hipSuccess;
     return launch_seed(e->d_seeds.as<SeedDev>(), seed_off[r], seed_off[r + 1], into,
-                       a.seen, a.next_flag, s);
+                       a.seen, a.next_flag, a.blk_flag, s);
   };
   auto compact = [&](uint32_t r) -> hipError_t {
-    hipError_t x = launch_flag_count(a.next_flag, e->n_pad, e->d_wgcount.as<uint32_t>(),
-                                     a.partials, n_waves, r ? stats + r * kNumCtr : nullptr, s);
+    hipError_t x = launch_flag_count(a.next_flag, a.blk_flag, e->n_pad,
+                                     e->d_wgcount.as<uint32_t>(), a.partials, n_waves,
+                                     r ? stats + r * kNumCtr : nullptr, s);
     if (x != hipSuccess) return x;
-    return launch_flag_compact(a.next_flag, e->n_pad, e->d_wgcount.as<uint32_t>(), e->d_frontier.as<uint32_t>(),
-                               e->d_nfront.as<uint32_t>(), s);
+    return launch_flag_compact(a.next_flag, a.blk_flag, e->n_pad, e->d_wgcount.as<uint32_t>(),
+                               e->d_frontier.as<uint32_t>(), e->d_nfront.as<uint32_t>(), s);
   };
 
   HIP_TRY(seed_round(0, arr[0]), "seed");
@@ -457,10 +483,15 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
     st->duplicates += c[kCtrDuplicates];
     st->frontier_entries += c[kCtrEntries];
     st->child_visits += c[kCtrChildren];
-    st->edge_words += c[kCtrItemReads];
-    // algorithmic bytes of the expand kernel (DESIGN.md §5.1 byte model)
-    st->expand_bytes += c[kCtrEntries] * 14 + c[kCtrEntryWords] * 16 + c[kCtrChildren] * 5 +
-                        c[kCtrItemReads] * 8 + c[kCtrSeenWrites] * 8 + c[kCtrArrivalWrites] * 9;
+    st->edge_words += c[kCtrSeenWrites];
+    // algorithmic bytes of the expand kernel (DESIGN.md §5.1 byte model):
+    // per entry frontier id 4 + topic 2 + row_ptr pair 8 + first child 4;
+    // per entry word the arrival read 8 (+ 8 when cleared); per child its
+    // flag byte + generation read/write (tree) or col id 4 (mesh); per
+    // seen read / seen write / arrival write 8.
+    st->expand_bytes += c[kCtrEntries] * 18 + c[kCtrEntryWords] * 8 + c[kCtrClearWords] * 8 +
+                        c[kCtrChildren] * 3 + c[kCtrMeshChildren] * 4 + c[kCtrSeenReads] * 8 +
+                        c[kCtrSeenWrites] * 8 + c[kCtrArrivalWrites] * 8;
     if (q < PS_MAX_ROUNDS) st->deliveries_per_round[q] += c[kCtrDeliveries];
   }
   st->rounds += r;
@@ -547,7 +578,9 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess &&
       cus > 0)
     e->n_cus = static_cast<uint32_t>(cus);
-  e->expand_grid = e->n_cus * 8;  // 8 x 256-thread blocks = 32 waves per CU
+  // 7 x 256-thread blocks per CU: k_expand needs 92 SGPRs, which admits 7
+  // (not the 8 the occupancy API reports), MI355X_MICROARCH.md §Residency
+  e->expand_grid = e->n_cus * 7;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess) {
     delete e;
@@ -768,6 +801,7 @@ int ps_publish(ps_engine* e, const uint32_t* topic_of_msg, size_t n, uint32_t* f
 
 int ps_run(ps_engine* e, ps_stats* out) {
   if (!e) return PS_E_INVAL;
+  const auto t_host0 = std::chrono::steady_clock::now();
   ps_stats st{};
   if (hipSetDevice(e->cfg.device) != hipSuccess) return e->fail(PS_E_DEVICE, "hipSetDevice");
   std::vector<RunMsg> msgs;
@@ -809,9 +843,12 @@ int ps_run(ps_engine* e, ps_stats* out) {
     }
   }
   std::vector<uint32_t> rest;
-  for (uint32_t t = 0; t < nt; ++t)
-    for (size_t q = head[t]; q < queue[t].size(); ++q) rest.push_back(queue[t][q]);
-  std::sort(rest.begin(), rest.end());
+  rest.reserve(nmsg);
+  {
+    std::vector<size_t> seen_in_topic(nt, 0);  // publish order, minus the solo'd heads
+    for (uint32_t i = 0; i < nmsg; ++i)
+      if (seen_in_topic[msgs[i].topic]++ >= head[msgs[i].topic]) rest.push_back(i);
+  }
   if (!rest.empty()) {
     int rc = run_phase(e, msgs, rest, &st);
     if (rc) return rc;
@@ -826,6 +863,7 @@ int ps_run(ps_engine* e, ps_stats* out) {
     }
   }
   e->have_hops = record;
+  st.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
   if (out) *out = st;
   return PS_OK;
 }
@@ -856,10 +894,15 @@ int ps_read_delivered(ps_engine* e, uint32_t msg, uint8_t* out) {
   HIP_TRY(hipMemcpy2DAsync(col.data(), 8, e->d_seen.as<uint64_t>() + d.wbase + (li >> 6),
                            d.W * 8ull, 8, d.n_nodes, hipMemcpyDeviceToHost, e->stream),
           "read seen");
+  std::vector<uint8_t> gen(d.n_nodes);
+  HIP_TRY(hipMemcpyAsync(gen.data(), e->d_gen.as<uint8_t>() + d.nbase, d.n_nodes,
+                         hipMemcpyDeviceToHost, e->stream),
+          "read generations");
   HIP_TRY(hipStreamSynchronize(e->stream), "sync");
+  const bool mesh = (d.flags & kTopicMesh) != 0;
   const uint64_t bit = 1ull << (li & 63);
   for (uint32_t u = 1; u < d.n_nodes; ++u)  // the root is not a recipient
-    if (col[u] & bit) out[e->node_peer[d.nbase + u]] = 1;
+    if ((mesh || gen[u] == e->gen_cur) && (col[u] & bit)) out[e->node_peer[d.nbase + u]] = 1;
   return PS_OK;
 }
 
@@ -867,7 +910,8 @@ int ps_seen_digest(ps_engine* e, uint64_t* digest_out) {
   if (!e || !digest_out) return PS_E_INVAL;
   if (!e->have_window) return e->fail(PS_E_NOTREADY, "no completed run");
   HIP_TRY(hipMemsetAsync(e->d_digest.p, 0, 8, e->stream), "clear digest");
-  HIP_TRY(launch_digest(e->d_seen.as<uint64_t>(), e->d_node_peer.as<uint32_t>(),
+  HIP_TRY(launch_digest(e->d_seen.as<uint64_t>(), e->d_gen.as<uint8_t>(), e->gen_cur,
+                        e->d_node_peer.as<uint32_t>(),
                         e->d_node_topic.as<uint16_t>(), e->d_topics.as<TopicDev>(), e->n_nodes,
                         e->d_digest.as<uint64_t>(), e->stream),
           "digest");

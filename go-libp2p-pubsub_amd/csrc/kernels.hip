@@ -72,28 +72,129 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
   return z ^ (z >> 31);
 }
 
+// ----------------------------------------------------------- window init ---
+// Per window: zero every topic root's rows (seen and both arrival buffers;
+// the root is node 0 of its topic) and stamp its generation; mesh topics get
+// all their rows zeroed (they do not use generations).  Grid: x = chunk, y =
+// topic.
+__global__ __launch_bounds__(kBlock) void k_window_init(const TopicDev* __restrict__ topics,
+                                                        uint64_t* __restrict__ seen,
+                                                        uint64_t* __restrict__ a0,
+                                                        uint64_t* __restrict__ a1,
+                                                        uint8_t* __restrict__ gen,
+                                                        uint32_t gen_cur) {
+  const TopicDev T = topics[blockIdx.y];
+  if (T.W == 0 || T.n_nodes == 0) return;
+  const bool mesh = (T.flags & kTopicMesh) != 0;
+  const uint64_t n_words = mesh ? static_cast<uint64_t>(T.n_nodes) * T.W : T.W;
+  if (!mesh && blockIdx.x != 0) return;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n_words;
+       i += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    seen[T.wbase + i] = 0;
+    a0[T.wbase + i] = 0;
+    a1[T.wbase + i] = 0;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) gen[T.nbase] = static_cast<uint8_t>(gen_cur);
+}
+
 // ---------------------------------------------------------------- seeds ---
 // Topic.PublishMessage (pubsub.go:111-120): the root "has" its own messages
 // (it is not a recipient) and forwards them in the next round.
 __global__ __launch_bounds__(kBlock) void k_seed(const SeedDev* __restrict__ seeds, uint32_t lo,
                                                  uint32_t hi, uint64_t* __restrict__ arrivals,
                                                  uint64_t* __restrict__ seen,
-                                                 uint8_t* __restrict__ next_flag) {
+                                                 uint8_t* __restrict__ next_flag,
+                                                 uint8_t* __restrict__ blk_flag) {
   const uint32_t i = lo + blockIdx.x * kBlock + threadIdx.x;
   if (i >= hi) return;
   const SeedDev s = seeds[i];
   arrivals[s.woff] |= s.mask;
   seen[s.woff] |= s.mask;
   next_flag[s.node] = 1;
+  blk_flag[s.node >> kFlagBlockShift] = 1;
 }
 
 // --------------------------------------------------------------- expand ---
-// One wave per frontier node p (grid-stride).  The wave flattens p's
-// (child j, word w) pairs, deg*W of them, over its 64 lanes: for W >= 64 one
-// iteration touches 512 contiguous bytes of the children's seen rows (BFS
-// numbering puts siblings next to each other).  Tree topics own each child
-// row exclusively (one parent), so the test-and-set is a plain RMW; mesh
-// topics use returning 64-bit atomicOr so exactly one parent wins each bit.
+// Tree topics: every child has exactly one parent, so p's wave owns the
+// child's rows this round.  The seen test is lazy: a child whose generation
+// byte is not the window's has seen nothing yet (its row is stale from an
+// older window), so it is tested against 0 and its whole row is written; a
+// current child is tested against its stored row.  Arrival rows of internal
+// children are written whole (zeros included), so they need no clearing.
+// Mesh topics: returning 64-bit atomicOr decides which parent wins each bit;
+// arrival rows are OR-accumulated and consumed-and-cleared.
+
+// per-lane counters of one launch (a lane handles < 2^26 words per launch)
+struct ExpandCtr {
+  uint32_t deliv = 0, dup = 0, sr = 0, sw = 0, aw = 0;
+};
+
+// Test-and-set of one (child, word): returns the newly delivered bits.
+template <bool kRecord>
+__device__ __forceinline__ uint64_t deliver_word(const ExpandArgs& a, bool mesh, bool stale,
+                                                 bool internal, uint64_t cw, uint64_t m,
+                                                 uint32_t round, ExpandCtr& k) {
+  uint64_t old = 0, nm;
+  if (mesh) {
+    if (m == 0) return 0;
+    old = atomicOr(reinterpret_cast<unsigned long long*>(a.seen + cw),
+                   static_cast<unsigned long long>(m));
+    nm = m & ~old;
+    k.sr += 1;
+    k.sw += 1;
+    if (nm && internal) {
+      atomicOr(reinterpret_cast<unsigned long long*>(a.a_next + cw),
+               static_cast<unsigned long long>(nm));
+      k.aw += 1;
+    }
+  } else {
+    if (!stale && m) {
+      old = a.seen[cw];
+      k.sr += 1;
+    }
+    nm = m & ~old;
+    if (stale || nm) {
+      a.seen[cw] = old | nm;
+      k.sw += 1;
+    }
+    if (internal) {
+      a.a_next[cw] = nm;
+      k.aw += 1;
+    }
+  }
+  k.dup += __popcll(m & old);
+  k.deliv += __popcll(nm);
+  if constexpr (kRecord) {
+    uint8_t* h = a.hop_rec + cw * 64;
+    uint64_t b = nm;
+    while (b) {
+      const int q = __ffsll(static_cast<long long>(b)) - 1;
+      h[q] = static_cast<uint8_t>(round);
+      b &= b - 1;
+    }
+  }
+  return nm;
+}
+
+__device__ __forceinline__ void mark_next(const ExpandArgs& a, uint32_t c) {
+  a.next_flag[c] = 1;
+  a.blk_flag[c >> kFlagBlockShift] = 1;
+}
+
+__device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(lane)));
+}
+
+// Frontier entries are dealt to waves round-robin (entry e -> wave e mod
+// n_waves).  A wave prefetches the metadata of its next 64 entries into lane
+// registers (frontier id, topic, row range, first child) and broadcasts them
+// with readlane, so the dependent-load chain is paid once per 64 entries.
+//  W >= 64: word blocks outer, children inner: a child is wave-uniform
+//    (flags and generation by readlane), each lane owns one word, so every
+//    child costs one 512-B contiguous store burst per array.
+//  W <  64: lanes split into 64/Wp groups of Wp = pow2ceil(W) lanes, one
+//    child per group per pass.
+// One lane per child raises the child's frontier flag.
 template <bool kRecord>
 __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round) {
   const uint32_t lane = threadIdx.x & 63;
@@ -101,115 +202,126 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
       __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) >> 6);
   const uint32_t n_waves = (gridDim.x * kBlock) >> 6;
   const uint32_t n = *a.n_front;
+  const uint32_t cur = a.gen_cur & 0xFF;
 
-  uint64_t c_deliv = 0, c_dup = 0, c_items = 0, c_seen_w = 0, c_arr_w = 0;
-  uint32_t c_ent = 0, c_ent_words = 0, c_kids = 0;
+  ExpandCtr k;
+  uint32_t c_ent = 0, c_ent_words = 0, c_kids = 0, c_mesh_kids = 0, c_clear = 0;
 
-  for (uint32_t e = wave; e < n; e += n_waves) {
-    const uint32_t p = __builtin_amdgcn_readfirstlane(a.frontier[e]);
-    const uint32_t t = __builtin_amdgcn_readfirstlane(a.node_topic[p]);
-    const TopicDev T = a.topics[t];
-    const uint32_t rs = __builtin_amdgcn_readfirstlane(a.row_ptr[p]);
-    const uint32_t deg = __builtin_amdgcn_readfirstlane(a.row_ptr[p + 1]) - rs;
-    const uint32_t W = T.W;
-    if (W == 0) continue;  // idle topic in this window (never seeded)
-    const uint64_t pw = T.wbase + static_cast<uint64_t>(p - T.nbase) * W;
-    const uint64_t cbase = T.wbase - static_cast<uint64_t>(T.nbase) * W;
-    const bool mesh = (T.flags & kTopicMesh) != 0;
-    c_ent += 1;
-    c_ent_words += W;
-    c_kids += deg;
-    // children in chunks of <= 2^16/W so that it * W < 2^32 and the
-    // multiply-high split below is exact (one chunk for any tree)
-    const uint32_t chunk = W >= 65536 ? 1u : (65536u / W);
-    for (uint32_t j0 = 0; j0 < deg; j0 += chunk) {
-    const uint32_t items = min(chunk, deg - j0) * W;
-    for (uint32_t it = lane; it < items; it += 64) {
-      const uint32_t j = j0 + static_cast<uint32_t>((static_cast<uint64_t>(it) * T.magic) >> 32);
-      const uint32_t w = it - (j - j0) * W;
-      const uint32_t c = a.col[rs + j];
-      const uint8_t f = a.node_flags[c];
-      const uint64_t m = a.a_cur[pw + w];
-      if (!(f & kNodeLive) || m == 0) continue;
-      const uint64_t cw = cbase + static_cast<uint64_t>(c) * W + w;
-      const bool internal = (f & kNodeInternal) != 0;
-      uint64_t old, nm;
-      if (mesh) {
-        old = atomicOr(reinterpret_cast<unsigned long long*>(a.seen + cw),
-                       static_cast<unsigned long long>(m));
-        nm = m & ~old;
-        if (nm && internal)
-          atomicOr(reinterpret_cast<unsigned long long*>(a.a_next + cw),
-                   static_cast<unsigned long long>(nm));
-      } else {
-        old = a.seen[cw];
-        nm = m & ~old;
-        if (nm) {
-          a.seen[cw] = old | nm;
-          if (internal) a.a_next[cw] = nm;
+  for (uint64_t e0 = wave; e0 < n; e0 += 64ull * n_waves) {
+    const uint64_t el = e0 + static_cast<uint64_t>(lane) * n_waves;
+    uint32_t bp = 0, bt = 0, brs = 0, bdeg = 0, bc0 = 0;
+    if (el < n) {
+      bp = a.frontier[el];
+      bt = a.node_topic[bp];
+      brs = a.row_ptr[bp];
+      bdeg = a.row_ptr[bp + 1] - brs;
+      if (bdeg) bc0 = a.col[brs];
+    }
+    const uint32_t nb = static_cast<uint32_t>(__popcll(__ballot(el < n)));
+    for (uint32_t q = 0; q < nb; ++q) {
+      const uint32_t p = rl(bp, q), t = rl(bt, q), rs = rl(brs, q), deg = rl(bdeg, q);
+      const uint32_t c0 = rl(bc0, q);
+      const TopicDev T = a.topics[t];
+      const uint32_t W = T.W;
+      if (W == 0) continue;  // idle topic in this window (never seeded)
+      const bool mesh = (T.flags & kTopicMesh) != 0;
+      const uint64_t pw = T.wbase + static_cast<uint64_t>(p - T.nbase) * W;
+      const uint64_t cbase = T.wbase - static_cast<uint64_t>(T.nbase) * W;
+      c_ent += 1;
+      c_ent_words += W;
+      c_kids += deg;
+      if (mesh) c_mesh_kids += deg;
+      for (uint32_t j0 = 0; j0 < deg; j0 += 64) {
+        const uint32_t cd = min(64u, deg - j0);
+        // lane j < cd: child j0+j (BFS trees: contiguous from c0)
+        uint32_t cj = 0, fj = 0, gj = 0;
+        if (lane < cd) {
+          cj = mesh ? a.col[rs + j0 + lane] : c0 + j0 + lane;
+          fj = a.node_flags[cj];
+          gj = mesh ? 0u : a.gen[cj];
         }
-      }
-      c_items += 1;
-      c_dup += __popcll(m & old);
-      if (nm) {
-        c_deliv += __popcll(nm);
-        c_seen_w += 1;
-        if (internal) {
-          c_arr_w += 1;
-          a.next_flag[c] = 1;
-        }
-        if constexpr (kRecord) {
-          uint8_t* h = a.hop_rec + cw * 64;
-          uint64_t b = nm;
-          while (b) {
-            const int k = __ffsll(static_cast<long long>(b)) - 1;
-            h[k] = static_cast<uint8_t>(round);
-            b &= b - 1;
+        if (W >= 64) {
+          for (uint32_t wb = 0; wb < W; wb += 64) {
+            const uint32_t w = wb + lane;
+            const bool active = w < W;
+            const uint64_t m = active ? a.a_cur[pw + w] : 0ull;
+            for (uint32_t jj = 0; jj < cd; ++jj) {
+              const uint32_t f = rl(fj, jj);
+              if (!(f & kNodeLive)) continue;
+              const uint32_t c = rl(cj, jj);
+              const bool stale = !mesh && rl(gj, jj) != cur;
+              const bool internal = (f & kNodeInternal) != 0;
+              uint64_t nm = 0;
+              if (active)
+                nm = deliver_word<kRecord>(a, mesh, stale, internal,
+                                           cbase + static_cast<uint64_t>(c) * W + w, m, round, k);
+              if (internal && __ballot(nm != 0) && lane == 0) mark_next(a, c);
+            }
+          }
+        } else {
+          const uint32_t sh = 32u - __clz(W - 1u);  // Wp = 1 << sh >= W
+          const uint32_t wp = 1u << sh;
+          const uint32_t w = lane & (wp - 1u);
+          const uint32_t jl = lane >> sh;
+          const uint32_t groups = 64u >> sh;
+          const uint64_t gmask = (wp == 64u ? ~0ull : ((1ull << wp) - 1ull)) << (jl << sh);
+          const uint64_t m = w < W ? a.a_cur[pw + w] : 0ull;
+          for (uint32_t jb = 0; jb < cd; jb += groups) {
+            const uint32_t jj = jb + jl;
+            const uint32_t c = static_cast<uint32_t>(__shfl(static_cast<int>(cj), static_cast<int>(jj), 64));
+            const uint32_t f = static_cast<uint32_t>(__shfl(static_cast<int>(fj), static_cast<int>(jj), 64));
+            const uint32_t g = static_cast<uint32_t>(__shfl(static_cast<int>(gj), static_cast<int>(jj), 64));
+            const bool live = (w < W) && (jj < cd) && (f & kNodeLive);
+            uint64_t nm = 0;
+            if (live)
+              nm = deliver_word<kRecord>(a, mesh, !mesh && g != cur, (f & kNodeInternal) != 0,
+                                         cbase + static_cast<uint64_t>(c) * W + w, m, round, k);
+            const uint64_t bal = __ballot(nm != 0);
+            if (live && w == 0 && (f & kNodeInternal) && (bal & gmask)) mark_next(a, c);
           }
         }
+        // this chunk's live tree children hold current rows now
+        if (!mesh && lane < cd && (fj & kNodeLive)) a.gen[cj] = static_cast<uint8_t>(cur);
+      }
+      if (mesh || p == T.nbase) {
+        // consume-and-clear: mesh rows are OR-accumulated, root rows are seeded
+        for (uint32_t w = lane; w < W; w += 64) a.a_cur[pw + w] = 0;
+        c_clear += W;
       }
     }
-    }
-    // consume-and-clear: arrival rows are zero outside the frontier
-    for (uint32_t w = lane; w < W; w += 64) a.a_cur[pw + w] = 0;
   }
 
-  c_deliv = wave_sum_u64(c_deliv);
-  c_dup = wave_sum_u64(c_dup);
-  c_items = wave_sum_u64(c_items);
-  c_seen_w = wave_sum_u64(c_seen_w);
-  c_arr_w = wave_sum_u64(c_arr_w);
+  const uint64_t s_deliv = wave_sum_u64(k.deliv);
+  const uint64_t s_dup = wave_sum_u64(k.dup);
+  const uint64_t s_sr = wave_sum_u64(k.sr);
+  const uint64_t s_sw = wave_sum_u64(k.sw);
+  const uint64_t s_aw = wave_sum_u64(k.aw);
   if (lane == 0) {
     uint64_t* out = a.partials + static_cast<uint64_t>(wave) * kNumCtr;
-    out[kCtrDeliveries] = c_deliv;
-    out[kCtrDuplicates] = c_dup;
+    out[kCtrDeliveries] = s_deliv;
+    out[kCtrDuplicates] = s_dup;
     out[kCtrEntries] = c_ent;
     out[kCtrEntryWords] = c_ent_words;
     out[kCtrChildren] = c_kids;
-    out[kCtrItemReads] = c_items;
-    out[kCtrSeenWrites] = c_seen_w;
-    out[kCtrArrivalWrites] = c_arr_w;
+    out[kCtrMeshChildren] = c_mesh_kids;
+    out[kCtrSeenReads] = s_sr;
+    out[kCtrSeenWrites] = s_sw;
+    out[kCtrArrivalWrites] = s_aw;
+    out[kCtrClearWords] = c_clear;
   }
 }
 
 // ------------------------------------------------------------ compaction ---
 // Pass 1: per-block count of flagged nodes (16 one-byte flags per lane, one
-// 16-B load).  Block 0 also folds the expand kernel's per-wave counters into
-// this round's statistics.
+// 16-B load); blocks whose blk_flag byte is clear exit at once.  Block 0 also
+// folds the expand kernel's per-wave counters into this round's statistics.
 __global__ __launch_bounds__(kBlock) void k_flag_count(const uint8_t* __restrict__ flags,
+                                                       const uint8_t* __restrict__ blk_flag,
                                                        uint32_t n_pad,
                                                        uint32_t* __restrict__ wg_count,
                                                        const uint64_t* __restrict__ partials,
                                                        uint32_t n_waves,
                                                        uint64_t* __restrict__ round_stats) {
-  const uint32_t base = blockIdx.x * kFlagsPerBlock + threadIdx.x * kFlagsPerThread;
-  uint32_t c = 0;
-  if (base < n_pad) {
-    const uint4 v = *reinterpret_cast<const uint4*>(flags + base);
-    c = __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
-  }
-  c = block_sum_u32(c);
-  if (threadIdx.x == 0) wg_count[blockIdx.x] = c;
   if (blockIdx.x == 0 && round_stats != nullptr) {
     __shared__ uint64_t red[kNumCtr][kBlock / 64];
     uint64_t acc[kNumCtr];
@@ -230,23 +342,39 @@ __global__ __launch_bounds__(kBlock) void k_flag_count(const uint8_t* __restrict
       round_stats[threadIdx.x] = s;
     }
   }
+  if (blk_flag[blockIdx.x] == 0) {
+    if (threadIdx.x == 0) wg_count[blockIdx.x] = 0;
+    return;
+  }
+  const uint32_t base = blockIdx.x * kFlagsPerBlock + threadIdx.x * kFlagsPerThread;
+  uint32_t c = 0;
+  if (base < n_pad) {
+    const uint4 v = *reinterpret_cast<const uint4*>(flags + base);
+    c = __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+  }
+  c = block_sum_u32(c);
+  if (threadIdx.x == 0) wg_count[blockIdx.x] = c;
 }
 
-// Pass 2: ordered compaction.  Each block sums the counts of the blocks
-// before it, scans its lanes' counts, writes the flagged node ids in node
-// order (so the next frontier is sorted: siblings stay adjacent) and clears
-// the flags.  The last block publishes the frontier length.
+// Pass 2: ordered compaction.  Each non-empty block sums the counts of the
+// blocks before it, scans its lanes' counts, writes the flagged node ids in
+// node order (so the next frontier is sorted: siblings stay adjacent) and
+// clears its flags.  The last block publishes the frontier length.
 __global__ __launch_bounds__(kBlock) void k_flag_compact(uint8_t* __restrict__ flags,
+                                                         uint8_t* __restrict__ blk_flag,
                                                          uint32_t n_pad,
                                                          const uint32_t* __restrict__ wg_count,
                                                          uint32_t* __restrict__ frontier,
                                                          uint32_t* __restrict__ n_front) {
+  const bool last = blockIdx.x == gridDim.x - 1;
+  const bool busy = blk_flag[blockIdx.x] != 0;
+  if (!busy && !last) return;
   uint32_t pre = 0;
   for (uint32_t i = threadIdx.x; i < blockIdx.x; i += kBlock) pre += wg_count[i];
   pre = block_sum_u32(pre);
   const uint32_t base = blockIdx.x * kFlagsPerBlock + threadIdx.x * kFlagsPerThread;
   uint4 v = make_uint4(0, 0, 0, 0);
-  if (base < n_pad) v = *reinterpret_cast<const uint4*>(flags + base);
+  if (busy && base < n_pad) v = *reinterpret_cast<const uint4*>(flags + base);
   const uint32_t c = __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
   uint32_t total;
   uint32_t pos = pre + block_excl_scan(c, &total);
@@ -263,11 +391,16 @@ __global__ __launch_bounds__(kBlock) void k_flag_compact(uint8_t* __restrict__ f
     }
     *reinterpret_cast<uint4*>(flags + base) = make_uint4(0, 0, 0, 0);
   }
-  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) *n_front = pre + total;
+  if (busy && threadIdx.x == 0) blk_flag[blockIdx.x] = 0;
+  if (last && threadIdx.x == 0) *n_front = pre + total;
 }
 
 // ---------------------------------------------------------------- digest ---
+// Order-independent digest of the window's delivered state: a tree node whose
+// generation is not the window's holds nothing (its row is stale).
 __global__ __launch_bounds__(kBlock) void k_digest(const uint64_t* __restrict__ seen,
+                                                   const uint8_t* __restrict__ gen,
+                                                   uint32_t gen_cur,
                                                    const uint32_t* __restrict__ node_peer,
                                                    const uint16_t* __restrict__ node_topic,
                                                    const TopicDev* __restrict__ topics,
@@ -277,9 +410,11 @@ __global__ __launch_bounds__(kBlock) void k_digest(const uint64_t* __restrict__ 
     const uint32_t t = node_topic[u];
     const TopicDev T = topics[t];
     if (T.W == 0) continue;
+    const bool valid = (T.flags & kTopicMesh) || gen[u] == static_cast<uint8_t>(gen_cur);
     const uint64_t row = T.wbase + static_cast<uint64_t>(u - T.nbase) * T.W;
     const uint64_t key0 = (static_cast<uint64_t>(node_peer[u]) << 32) | (static_cast<uint64_t>(t) << 16);
-    for (uint32_t w = 0; w < T.W; ++w) acc += mix64((key0 | w) ^ mix64(seen[row + w]));
+    for (uint32_t w = 0; w < T.W; ++w)
+      acc += mix64((key0 | w) ^ mix64(valid ? seen[row + w] : 0ull));
   }
   acc = wave_sum_u64(acc);
   if ((threadIdx.x & 63) == 0)
@@ -288,12 +423,21 @@ __global__ __launch_bounds__(kBlock) void k_digest(const uint64_t* __restrict__ 
 
 }  // namespace
 
+hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_t* seen,
+                              uint64_t* a0, uint64_t* a1, uint8_t* gen, uint32_t gen_cur,
+                              bool any_mesh, hipStream_t s) {
+  if (n_topics == 0) return hipSuccess;
+  const dim3 grid(any_mesh ? 64 : 1, n_topics);
+  hipLaunchKernelGGL(k_window_init, grid, dim3(kBlock), 0, s, topics, seen, a0, a1, gen, gen_cur);
+  return hipGetLastError();
+}
+
 hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t* arrivals,
-                       uint64_t* seen, uint8_t* next_flag, hipStream_t s) {
+                       uint64_t* seen, uint8_t* next_flag, uint8_t* blk_flag, hipStream_t s) {
   if (hi <= lo) return hipSuccess;
   const uint32_t grid = (hi - lo + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(k_seed, dim3(grid), dim3(kBlock), 0, s, seeds, lo, hi, arrivals, seen,
-                     next_flag);
+                     next_flag, blk_flag);
   return hipGetLastError();
 }
 
@@ -306,31 +450,32 @@ hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, uint3
   return hipGetLastError();
 }
 
-hipError_t launch_flag_count(const uint8_t* flags, uint32_t n_pad, uint32_t* wg_count,
-                             const uint64_t* partials, uint32_t n_waves, uint64_t* round_stats,
-                             hipStream_t s) {
+hipError_t launch_flag_count(const uint8_t* flags, const uint8_t* blk_flag, uint32_t n_pad,
+                             uint32_t* wg_count, const uint64_t* partials, uint32_t n_waves,
+                             uint64_t* round_stats, hipStream_t s) {
   const uint32_t grid = (n_pad + kFlagsPerBlock - 1) / kFlagsPerBlock;
-  hipLaunchKernelGGL(k_flag_count, dim3(grid), dim3(kBlock), 0, s, flags, n_pad, wg_count,
-                     partials, n_waves, round_stats);
+  hipLaunchKernelGGL(k_flag_count, dim3(grid), dim3(kBlock), 0, s, flags, blk_flag, n_pad,
+                     wg_count, partials, n_waves, round_stats);
   return hipGetLastError();
 }
 
-hipError_t launch_flag_compact(uint8_t* flags, uint32_t n_pad, const uint32_t* wg_count,
-                               uint32_t* frontier, uint32_t* n_front, hipStream_t s) {
+hipError_t launch_flag_compact(uint8_t* flags, uint8_t* blk_flag, uint32_t n_pad,
+                               const uint32_t* wg_count, uint32_t* frontier, uint32_t* n_front,
+                               hipStream_t s) {
   const uint32_t grid = (n_pad + kFlagsPerBlock - 1) / kFlagsPerBlock;
-  hipLaunchKernelGGL(k_flag_compact, dim3(grid), dim3(kBlock), 0, s, flags, n_pad, wg_count,
-                     frontier, n_front);
+  hipLaunchKernelGGL(k_flag_compact, dim3(grid), dim3(kBlock), 0, s, flags, blk_flag, n_pad,
+                     wg_count, frontier, n_front);
   return hipGetLastError();
 }
 
-hipError_t launch_digest(const uint64_t* seen, const uint32_t* node_peer,
-                         const uint16_t* node_topic, const TopicDev* topics, uint32_t n_nodes,
-                         uint64_t* out, hipStream_t s) {
+hipError_t launch_digest(const uint64_t* seen, const uint8_t* gen, uint32_t gen_cur,
+                         const uint32_t* node_peer, const uint16_t* node_topic,
+                         const TopicDev* topics, uint32_t n_nodes, uint64_t* out, hipStream_t s) {
   uint32_t grid = (n_nodes + kBlock - 1) / kBlock;
   if (grid > 4096) grid = 4096;
   if (grid == 0) grid = 1;
-  hipLaunchKernelGGL(k_digest, dim3(grid), dim3(kBlock), 0, s, seen, node_peer, node_topic,
-                     topics, n_nodes, out);
+  hipLaunchKernelGGL(k_digest, dim3(grid), dim3(kBlock), 0, s, seen, gen, gen_cur, node_peer,
+                     node_topic, topics, n_nodes, out);
   return hipGetLastError();
 }
 

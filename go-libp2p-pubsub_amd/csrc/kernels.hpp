@@ -15,19 +15,23 @@ enum : uint8_t {
 
 // TopicDev.flags
 enum : uint32_t {
-  kTopicMesh = 1,  // a node may have several parents: seen/arrival via atomics
+  // A node may have several parents (general child lists): the seen
+  // test-and-set and the arrival OR are 64-bit atomics, rows are cleared
+  // eagerly per window and consumed-and-cleared per round.
+  kTopicMesh = 1,
 };
 
 // One topic of the fused node space.  Node u of topic t (nbase <= u <
 // nbase + n_nodes) owns the 64-message words [wbase + (u-nbase)*W, +W) of the
-// seen bitset and of the two arrival buffers.
+// seen bitset and of the two arrival buffers.  Tree topics are numbered in
+// BFS order, so the children of a node are consecutive node ids.
 struct TopicDev {
-  uint64_t wbase;     // first word of the topic's mask block
-  uint64_t magic;     // ceil(2^32 / W): item -> (child, word) split
-  uint32_t nbase;     // first node of the topic
-  uint32_t n_nodes;   // nodes in the topic
-  uint32_t W;         // 64-message words per node in this window (0 = idle)
-  uint32_t flags;     // kTopic*
+  uint64_t wbase;    // first word of the topic's mask block
+  uint64_t magic;    // ceil(2^32 / W): item -> (child, word) split
+  uint32_t nbase;    // first node of the topic (its root)
+  uint32_t n_nodes;  // nodes in the topic
+  uint32_t W;        // 64-message words per node in this window (0 = idle)
+  uint32_t flags;    // kTopic*
 };
 
 // One root injection: words of a topic root that start flooding in a round.
@@ -38,16 +42,19 @@ struct SeedDev {
   uint32_t pad;
 };
 
-// Per-wave counters written by the expand kernel, reduced per round.
+// Per-wave counters written by the expand kernel, reduced per round; they
+// also feed the algorithmic byte model.
 enum : int {
   kCtrDeliveries = 0,
   kCtrDuplicates,
   kCtrEntries,
   kCtrEntryWords,
   kCtrChildren,
-  kCtrItemReads,
+  kCtrMeshChildren,
+  kCtrSeenReads,
   kCtrSeenWrites,
   kCtrArrivalWrites,
+  kCtrClearWords,
   kNumCtr
 };
 
@@ -59,30 +66,38 @@ struct ExpandArgs {
   const uint16_t* node_topic;
   const uint8_t* node_flags;
   const TopicDev* topics;
-  uint64_t* a_cur;   // arrivals of the current frontier (read, then cleared)
+  uint64_t* a_cur;   // arrivals of the current frontier
   uint64_t* a_next;  // arrivals for the next frontier
   uint64_t* seen;    // per-node delivered bitset (the dedup record)
+  uint8_t* gen;      // per-node window generation of its seen row (tree topics)
   uint8_t* next_flag;
+  uint8_t* blk_flag;  // one byte per kFlagsPerBlock nodes: some flag set
   uint64_t* partials;  // [n_waves][kNumCtr]
   uint8_t* hop_rec;    // [word*64 + bit] = round, record mode only
+  uint32_t gen_cur;
 };
 
 constexpr int kBlock = 256;
 constexpr int kFlagsPerThread = 16;
-constexpr int kFlagsPerBlock = kBlock * kFlagsPerThread;
+constexpr int kFlagsPerBlock = kBlock * kFlagsPerThread;  // 4096 nodes
+constexpr int kFlagBlockShift = 12;
 
 // host-side launchers (kernels.hip)
+hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_t* seen,
+                              uint64_t* a0, uint64_t* a1, uint8_t* gen, uint32_t gen_cur,
+                              bool any_mesh, hipStream_t s);
 hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t* arrivals,
-                       uint64_t* seen, uint8_t* next_flag, hipStream_t s);
+                       uint64_t* seen, uint8_t* next_flag, uint8_t* blk_flag, hipStream_t s);
 hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid,
                          hipStream_t s);
-hipError_t launch_flag_count(const uint8_t* flags, uint32_t n_pad, uint32_t* wg_count,
-                             const uint64_t* partials, uint32_t n_waves, uint64_t* round_stats,
-                             hipStream_t s);
-hipError_t launch_flag_compact(uint8_t* flags, uint32_t n_pad, const uint32_t* wg_count,
-                               uint32_t* frontier, uint32_t* n_front, hipStream_t s);
-hipError_t launch_digest(const uint64_t* seen, const uint32_t* node_peer,
-                         const uint16_t* node_topic, const TopicDev* topics, uint32_t n_nodes,
-                         uint64_t* out, hipStream_t s);
+hipError_t launch_flag_count(const uint8_t* flags, const uint8_t* blk_flag, uint32_t n_pad,
+                             uint32_t* wg_count, const uint64_t* partials, uint32_t n_waves,
+                             uint64_t* round_stats, hipStream_t s);
+hipError_t launch_flag_compact(uint8_t* flags, uint8_t* blk_flag, uint32_t n_pad,
+                               const uint32_t* wg_count, uint32_t* frontier, uint32_t* n_front,
+                               hipStream_t s);
+hipError_t launch_digest(const uint64_t* seen, const uint8_t* gen, uint32_t gen_cur,
+                         const uint32_t* node_peer, const uint16_t* node_topic,
+                         const TopicDev* topics, uint32_t n_nodes, uint64_t* out, hipStream_t s);
 
 }  // namespace psamd

@@ -46,7 +46,7 @@ class Stats(C.Structure):
                 ("frontier_entries", C.c_uint64), ("child_visits", C.c_uint64),
                 ("edge_words", C.c_uint64), ("expand_bytes", C.c_uint64),
                 ("windows", C.c_uint64), ("rounds", C.c_uint64), ("expand_launches", C.c_uint64),
-                ("run_ms", C.c_double), ("expand_ms", C.c_double),
+                ("run_ms", C.c_double), ("expand_ms", C.c_double), ("host_ms", C.c_double),
                 ("deliveries_per_round", C.c_uint64 * MAX_ROUNDS)]
 
     def as_dict(self) -> dict:

@@ -72,6 +72,7 @@ typedef struct ps_stats {
   uint64_t expand_launches;    /* expand kernel launches                         */
   double run_ms;               /* device time of the whole run (HIP events)      */
   double expand_ms;            /* summed expand-kernel device time (TIME flag)   */
+  double host_ms;              /* wall time of the ps_run call                   */
   uint64_t deliveries_per_round[PS_MAX_ROUNDS];
 } ps_stats;
 

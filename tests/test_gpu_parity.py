@@ -51,8 +51,9 @@ def check_topic(eng, first, msg_idx, row_ptr, col, root, live):
     return total
 
 
+@pytest.mark.parametrize("eager", [False, True])
 @pytest.mark.parametrize("seed", range(8))
-def test_tree_parity_random(seed):
+def test_tree_parity_random(seed, eager):
     rng = np.random.default_rng(seed)
     n = int(rng.integers(2, 3000))
     root = int(rng.integers(0, n))
@@ -60,7 +61,8 @@ def test_tree_parity_random(seed):
     live = (rng.random(n) > 0.1).astype(np.uint8)
     n_msgs = int(rng.integers(1, 300))
     starts = rng.integers(0, 6, size=n_msgs) if seed % 2 else None
-    with PE.Engine(n, 1, record_hops=True) as eng:
+    flags = PE.F_NO_LAZY_SEEN if eager else 0
+    with PE.Engine(n, 1, record_hops=True, flags=flags) as eng:
         eng.set_tree(0, root, parent)
         eng.set_live(live)
         first = eng.publish(np.zeros(n_msgs), starts)
@@ -255,3 +257,26 @@ def test_cfg3_full_size_properties():
         assert per[1:] == [int(x) for x in exp[1:len(per)]]
         assert int(exp[len(per):].sum()) == 0
         assert eng.seen_digest() == digest
+
+
+def test_many_windows_generation_wrap_and_reuse():
+    """> 255 windows on one engine: generation bytes wrap, stale rows from
+    older windows never leak into a new window (lazy seen reset)."""
+    rng = np.random.default_rng(21)
+    n = 700
+    par = random_tree(rng, n, 0)
+    rp, cl = O.parents_to_csr(par)
+    live = (rng.random(n) > 0.1).astype(np.uint8)
+    with PE.Engine(n, 2, record_hops=True, msg_window=64) as eng:
+        eng.set_tree(0, 0, par)
+        eng.set_tree(1, 5, random_tree(rng, n, 5))
+        eng.set_live(live)
+        _, hops, _ = O.disseminate(rp, cl, 0, live, 1)
+        for rep in range(3):
+            k = 64 * 100 + 7  # 101 windows of topic 0 per run
+            first = eng.publish(np.zeros(k), rng.integers(0, 3, size=k))
+            st = eng.run()
+            assert st.windows == 101
+            for m in (0, 63, 64, 5000, k - 1):
+                assert np.array_equal(eng.hops(first + m), hops[0]), (rep, m)
+            assert st.deliveries == k * int((hops[0] != 255).sum())
