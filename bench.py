@@ -86,6 +86,7 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--no-check", action="store_true", help="skip delivery assertions (experiments)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -108,7 +109,7 @@ def main():
 
     for _ in range(args.warmup):
         st = step()
-        assert st.deliveries == deliv_expected, (st.deliveries, deliv_expected)
+        assert args.no_check or st.deliveries == deliv_expected, (st.deliveries, deliv_expected)
     tot_deliv = tot_bytes = 0
     tot_expand_ms = 0.0
     launches = 0
@@ -120,7 +121,7 @@ def main():
         tot_expand_ms += st.expand_ms
         launches += st.expand_launches
     wall = time.perf_counter() - t0
-    assert tot_deliv == deliv_expected * args.steps
+    assert args.no_check or tot_deliv == deliv_expected * args.steps
     value = tot_deliv / wall
     achieved = tot_bytes / (tot_expand_ms * 1e-3) / 1e9
     pair_gbs = value * PAIR_BYTES / 1e9
@@ -149,7 +150,10 @@ def main():
                        "equiv_frac": pair_gbs / HBM_PEAK_GBS},
         "last_step": {"rounds": st.rounds, "windows": st.windows, "run_ms": st.run_ms,
                       "expand_ms": st.expand_ms, "host_ms": st.host_ms,
-                      "edge_words": st.edge_words},
+                      "edge_words": st.edge_words,
+                      "frontier_per_round": st.as_dict()["frontier_per_round"],
+                      "expand_us_per_round": [round(x * 1e3, 1) for x in
+                                              st.as_dict()["expand_ms_per_round"]]},
     }
     if not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(eng, wl, sizes, args.cpu_budget)

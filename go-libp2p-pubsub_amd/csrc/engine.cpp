@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -267,7 +268,8 @@ int upload_graph(ps_engine* e) {
     HIP_TRY(e->d_col.ensure(std::max<size_t>(e->col.size(), 1) * 4), "alloc col");
     HIP_TRY(e->d_node_topic.ensure(std::max<size_t>(nn, 1) * 2), "alloc node_topic");
     HIP_TRY(e->d_node_peer.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_peer");
-    HIP_TRY(e->d_node_flags.ensure(std::max<size_t>(nn, 1)), "alloc node_flags");
+    // padded to n_pad: the expand kernel stages flag bytes as whole dwords
+    HIP_TRY(e->d_node_flags.ensure(e->n_pad + 16), "alloc node_flags");
     HIP_TRY(hipMemcpyAsync(e->d_row_ptr.p, e->row_ptr.data(), (nn + 1) * 4, hipMemcpyHostToDevice, e->stream),
             "upload row_ptr");
     if (!e->col.empty())
@@ -286,7 +288,7 @@ int upload_graph(ps_engine* e) {
     const size_t n_blk = ceil_div(e->n_pad, kFlagsPerBlock);
     HIP_TRY(e->d_blk.ensure(n_blk), "alloc block flags");
     HIP_TRY(hipMemsetAsync(e->d_blk.p, 0, e->d_blk.bytes, e->stream), "clear block flags");
-    HIP_TRY(e->d_gen.ensure(e->n_pad), "alloc generations");
+    HIP_TRY(e->d_gen.ensure(e->n_pad + 16), "alloc generations");
     HIP_TRY(hipMemsetAsync(e->d_gen.p, 0, e->d_gen.bytes, e->stream), "clear generations");
     e->gen_cur = 0;  // node ids changed: every row is stale
     HIP_TRY(e->d_frontier.ensure(std::max<size_t>(nn, 1) * 4), "alloc frontier");
@@ -409,6 +411,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
   a.gen_cur = e->gen_cur;
   a.next_flag = e->d_flags.as<uint8_t>();
   a.blk_flag = e->d_blk.as<uint8_t>();
+  a.dbg = 0;
+  if (const char* v = std::getenv("PSAMD_DEBUG_EXPAND")) a.dbg = static_cast<uint32_t>(std::atoi(v));
   a.partials = e->d_partials.as<uint64_t>();
   a.hop_rec = record ? e->d_hop.as<uint8_t>() : nullptr;
   uint64_t* arr[2] = {e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>()};
@@ -473,6 +477,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
     float k = 0.f;
     HIP_TRY(hipEventElapsedTime(&k, e->ev_k[i], e->ev_k[i + 1]), "elapsed");
     st->expand_ms += k;
+    const size_t q = i / 2 + 1;  // round of this launch
+    if (q < PS_MAX_ROUNDS) st->expand_ms_per_round[q] += k;
   }
   std::vector<uint64_t> hs(static_cast<size_t>(r + 1) * kNumCtr);
   HIP_TRY(hipMemcpyAsync(hs.data(), stats, hs.size() * 8, hipMemcpyDeviceToHost, s), "read stats");
@@ -492,7 +498,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
     st->expand_bytes += c[kCtrEntries] * 18 + c[kCtrEntryWords] * 8 + c[kCtrClearWords] * 8 +
                         c[kCtrChildren] * 3 + c[kCtrMeshChildren] * 4 + c[kCtrSeenReads] * 8 +
                         c[kCtrSeenWrites] * 8 + c[kCtrArrivalWrites] * 8;
-    if (q < PS_MAX_ROUNDS) st->deliveries_per_round[q] += c[kCtrDeliveries];
+    if (q < PS_MAX_ROUNDS) {
+      st->deliveries_per_round[q] += c[kCtrDeliveries];
+      st->frontier_per_round[q] += static_cast<uint32_t>(c[kCtrEntries]);
+    }
   }
   st->rounds += r;
   st->expand_launches += r;
@@ -578,9 +587,11 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) == hipSuccess &&
       cus > 0)
     e->n_cus = static_cast<uint32_t>(cus);
-  // 7 x 256-thread blocks per CU: k_expand needs 92 SGPRs, which admits 7
-  // (not the 8 the occupancy API reports), MI355X_MICROARCH.md §Residency
-  e->expand_grid = e->n_cus * 7;
+  // resident 256-thread blocks per CU: k_expand needs 80 VGPRs / 106 SGPRs,
+  // which admits 6 (MI355X_MICROARCH.md §Residency); PSAMD_EXPAND_BPC overrides
+  uint32_t bpc = 6;
+  if (const char* v = std::getenv("PSAMD_EXPAND_BPC")) bpc = std::max(1, std::atoi(v));
+  e->expand_grid = e->n_cus * bpc;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess) {
     delete e;

@@ -153,11 +153,11 @@ __device__ __forceinline__ uint64_t deliver_word(const ExpandArgs& a, bool mesh,
       k.sr += 1;
     }
     nm = m & ~old;
-    if (stale || nm) {
+    if ((stale || nm) && !(a.dbg & kDbgNoSeenStore)) {
       a.seen[cw] = old | nm;
       k.sw += 1;
     }
-    if (internal) {
+    if (internal && !(a.dbg & kDbgNoArrivalStore)) {
       a.a_next[cw] = nm;
       k.aw += 1;
     }
@@ -177,6 +177,7 @@ __device__ __forceinline__ uint64_t deliver_word(const ExpandArgs& a, bool mesh,
 }
 
 __device__ __forceinline__ void mark_next(const ExpandArgs& a, uint32_t c) {
+  if (a.dbg & kDbgNoByteStores) return;
   a.next_flag[c] = 1;
   a.blk_flag[c >> kFlagBlockShift] = 1;
 }
@@ -185,109 +186,265 @@ __device__ __forceinline__ uint32_t rl(uint32_t v, uint32_t lane) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(lane)));
 }
 
+__device__ __forceinline__ uint32_t pow2_shift(uint32_t W) { return 32u - __clz(W - 1u); }
+
+// LDS-DMA: lane i copies N bytes from its own global address into
+// lds_base + i * N (lds_base wave-uniform); no VGPR destination.
+#define PSAMD_LDS_DMA(g, lds_base, N)                                            \
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g), \
+                                   (__attribute__((address_space(3))) void*)(lds_base), N, 0, 0)
+
+// Per-wave LDS slice of the staged path: arrival words of a sub-batch of
+// entries, plus the flag and generation bytes of their children.
+constexpr uint32_t kStageWords = 704;  // 5.5 KiB
+constexpr uint32_t kStageBytes = 512;  // 2 x 512 B of child flag / generation dwords
+struct WaveStage {
+  uint64_t words[kStageWords];
+  uint8_t flags[kStageBytes];
+  uint8_t gens[kStageBytes];
+};
+
+struct EntryCtr {
+  uint32_t ent = 0, ent_words = 0, kids = 0, mesh_kids = 0, clear = 0;
+};
+
+// Direct path: one entry with its loads inline (mesh topics, rows wider than
+// the stage, fan-out above 64).
+template <bool kRecord>
+__device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint32_t deg,
+                              uint32_t c0, uint32_t W, uint32_t nbase, uint32_t tflags,
+                              uint64_t wbase, uint32_t lane, uint32_t cur, uint32_t round,
+                              ExpandCtr& k, EntryCtr& ec) {
+  const bool mesh = (tflags & kTopicMesh) != 0;
+  const uint64_t pw = wbase + static_cast<uint64_t>(p - nbase) * W;
+  const uint64_t cbase = wbase - static_cast<uint64_t>(nbase) * W;
+  ec.ent += 1;
+  ec.ent_words += W;
+  ec.kids += deg;
+  if (mesh) ec.mesh_kids += deg;
+  for (uint32_t j0 = 0; j0 < deg; j0 += 64) {
+    const uint32_t cd = min(64u, deg - j0);
+    uint32_t cj = 0, fj = 0, gj = 0;
+    if (lane < cd) {
+      cj = mesh ? a.col[rs + j0 + lane] : c0 + j0 + lane;
+      fj = a.node_flags[cj];
+      gj = mesh ? 0u : a.gen[cj];
+    }
+    if (W >= 64) {
+      for (uint32_t wb = 0; wb < W; wb += 64) {
+        const uint32_t w = wb + lane;
+        const bool active = w < W;
+        const uint64_t m = active ? a.a_cur[pw + w] : 0ull;
+        for (uint32_t jj = 0; jj < cd; ++jj) {
+          const uint32_t f = rl(fj, jj);
+          if (!(f & kNodeLive)) continue;
+          const uint32_t c = rl(cj, jj);
+          const bool stale = !mesh && rl(gj, jj) != cur;
+          const bool internal = (f & kNodeInternal) != 0;
+          uint64_t nm = 0;
+          if (active)
+            nm = deliver_word<kRecord>(a, mesh, stale, internal,
+                                       cbase + static_cast<uint64_t>(c) * W + w, m, round, k);
+          if (internal && __ballot(nm != 0) && lane == 0) mark_next(a, c);
+        }
+      }
+    } else {
+      const uint32_t sh = pow2_shift(W);
+      const uint32_t wp = 1u << sh;
+      const uint32_t w = lane & (wp - 1u);
+      const uint32_t jl = lane >> sh;
+      const uint32_t groups = 64u >> sh;
+      const uint64_t gmask = (wp == 64u ? ~0ull : ((1ull << wp) - 1ull)) << (jl << sh);
+      const uint64_t m = w < W ? a.a_cur[pw + w] : 0ull;
+      for (uint32_t jb = 0; jb < cd; jb += groups) {
+        const uint32_t jj = jb + jl;
+        const uint32_t c = static_cast<uint32_t>(__shfl(static_cast<int>(cj), static_cast<int>(jj), 64));
+        const uint32_t f = static_cast<uint32_t>(__shfl(static_cast<int>(fj), static_cast<int>(jj), 64));
+        const uint32_t g = static_cast<uint32_t>(__shfl(static_cast<int>(gj), static_cast<int>(jj), 64));
+        const bool live = (w < W) && (jj < cd) && (f & kNodeLive);
+        uint64_t nm = 0;
+        if (live)
+          nm = deliver_word<kRecord>(a, mesh, !mesh && g != cur, (f & kNodeInternal) != 0,
+                                     cbase + static_cast<uint64_t>(c) * W + w, m, round, k);
+        const uint64_t bal = __ballot(nm != 0);
+        if (live && w == 0 && (f & kNodeInternal) && (bal & gmask)) mark_next(a, c);
+      }
+    }
+    if (!mesh && lane < cd && (fj & kNodeLive) && !(a.dbg & kDbgNoByteStores))
+      a.gen[cj] = static_cast<uint8_t>(cur);
+  }
+  if (mesh || p == nbase) {
+    // consume-and-clear: mesh rows are OR-accumulated, root rows are seeded
+    for (uint32_t w = lane; w < W; w += 64) a.a_cur[pw + w] = 0;
+    ec.clear += W;
+  }
+}
+
 // Frontier entries are dealt to waves round-robin (entry e -> wave e mod
-// n_waves).  A wave prefetches the metadata of its next 64 entries into lane
-// registers (frontier id, topic, row range, first child) and broadcasts them
-// with readlane, so the dependent-load chain is paid once per 64 entries.
-//  W >= 64: word blocks outer, children inner: a child is wave-uniform
-//    (flags and generation by readlane), each lane owns one word, so every
-//    child costs one 512-B contiguous store burst per array.
-//  W <  64: lanes split into 64/Wp groups of Wp = pow2ceil(W) lanes, one
-//    child per group per pass.
-// One lane per child raises the child's frontier flag.
+// n_waves).  A wave loads the metadata of its next 64 entries into lane
+// registers (frontier id, row range, first child, topic fields) and
+// broadcasts them with readlane.  Tree entries then go through the staged
+// path in sub-batches that fit the wave's LDS slice:
+//   phase A  LDS-DMA of every arrival row and of the children's flag and
+//            generation bytes (BFS numbering: contiguous), one vmcnt(0) wait;
+//   phase B  stores only: W >= 64 child-outer / word-block-inner (512-B
+//            contiguous bursts, child wave-uniform), W < 64 Wp-lane groups.
+// The waves therefore wait once per sub-batch, not once per word block.
 template <bool kRecord>
 __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round) {
+  __shared__ WaveStage stage_lds[kBlock / 64];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave =
       __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) >> 6);
+  WaveStage& ws = stage_lds[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
   const uint32_t n_waves = (gridDim.x * kBlock) >> 6;
   const uint32_t n = *a.n_front;
   const uint32_t cur = a.gen_cur & 0xFF;
 
   ExpandCtr k;
-  uint32_t c_ent = 0, c_ent_words = 0, c_kids = 0, c_mesh_kids = 0, c_clear = 0;
+  EntryCtr ec;
 
   for (uint64_t e0 = wave; e0 < n; e0 += 64ull * n_waves) {
     const uint64_t el = e0 + static_cast<uint64_t>(lane) * n_waves;
-    uint32_t bp = 0, bt = 0, brs = 0, bdeg = 0, bc0 = 0;
+    uint32_t bp = 0, brs = 0, bdeg = 0, bc0 = 0, bW = 0, bnb = 0, bfl = 0, bwl = 0, bwh = 0;
     if (el < n) {
       bp = a.frontier[el];
-      bt = a.node_topic[bp];
+      const uint32_t t = a.node_topic[bp];
       brs = a.row_ptr[bp];
       bdeg = a.row_ptr[bp + 1] - brs;
-      if (bdeg) bc0 = a.col[brs];
+      const TopicDev T = a.topics[t];
+      bW = T.W;
+      bnb = T.nbase;
+      bfl = T.flags;
+      bwl = static_cast<uint32_t>(T.wbase);
+      bwh = static_cast<uint32_t>(T.wbase >> 32);
+      if (bdeg && T.W) bc0 = a.col[brs];
     }
     const uint32_t nb = static_cast<uint32_t>(__popcll(__ballot(el < n)));
-    for (uint32_t q = 0; q < nb; ++q) {
-      const uint32_t p = rl(bp, q), t = rl(bt, q), rs = rl(brs, q), deg = rl(bdeg, q);
-      const uint32_t c0 = rl(bc0, q);
-      const TopicDev T = a.topics[t];
-      const uint32_t W = T.W;
-      if (W == 0) continue;  // idle topic in this window (never seeded)
-      const bool mesh = (T.flags & kTopicMesh) != 0;
-      const uint64_t pw = T.wbase + static_cast<uint64_t>(p - T.nbase) * W;
-      const uint64_t cbase = T.wbase - static_cast<uint64_t>(T.nbase) * W;
-      c_ent += 1;
-      c_ent_words += W;
-      c_kids += deg;
-      if (mesh) c_mesh_kids += deg;
-      for (uint32_t j0 = 0; j0 < deg; j0 += 64) {
-        const uint32_t cd = min(64u, deg - j0);
-        // lane j < cd: child j0+j (BFS trees: contiguous from c0)
-        uint32_t cj = 0, fj = 0, gj = 0;
-        if (lane < cd) {
-          cj = mesh ? a.col[rs + j0 + lane] : c0 + j0 + lane;
-          fj = a.node_flags[cj];
-          gj = mesh ? 0u : a.gen[cj];
+    uint32_t q = 0;
+    while (q < nb) {
+      const uint32_t W0 = rl(bW, q), d0 = rl(bdeg, q), f0 = rl(bfl, q);
+      if (W0 == 0) {
+        ++q;
+        continue;
+      }
+      if ((f0 & kTopicMesh) || W0 > kStageWords || d0 > 64) {
+        expand_direct<kRecord>(a, rl(bp, q), rl(brs, q), d0, rl(bc0, q), W0, rl(bnb, q), f0,
+                               (static_cast<uint64_t>(rl(bwh, q)) << 32) | rl(bwl, q), lane, cur,
+                               round, k, ec);
+        ++q;
+        continue;
+      }
+      // sub-batch [q, q + nq) that fits the stage; a child's flag and
+      // generation bytes are staged as the dwords enclosing [c0, c0 + deg)
+      // (sub-dword LDS-DMA does not pack lanes byte by byte)
+      uint32_t nq = 0, sw = 0, sd = 0;
+      while (q + nq < nb) {
+        const uint32_t Wn = rl(bW, q + nq), dn = rl(bdeg, q + nq), fn = rl(bfl, q + nq);
+        const uint32_t cn = rl(bc0, q + nq);
+        const uint32_t bn = 4u * (((cn + dn + 3u) >> 2) - (cn >> 2));
+        if ((fn & kTopicMesh) || Wn > kStageWords || dn > 64) break;
+        if (sw + Wn > kStageWords || sd + bn > kStageBytes) break;
+        sw += Wn;
+        sd += bn;
+        ++nq;
+      }
+      // phase A: LDS-DMA of arrival rows and child flag / generation bytes
+      {
+        uint32_t off = 0, doff = 0;
+        for (uint32_t i = q; i < q + nq; ++i) {
+          const uint32_t W = rl(bW, i), deg = rl(bdeg, i);
+          if (W == 0) continue;
+          const uint32_t p = rl(bp, i), nbase = rl(bnb, i), c0 = rl(bc0, i);
+          const uint64_t wbase = (static_cast<uint64_t>(rl(bwh, i)) << 32) | rl(bwl, i);
+          const uint32_t* row =
+              reinterpret_cast<const uint32_t*>(a.a_cur + wbase + static_cast<uint64_t>(p - nbase) * W);
+          uint32_t* dst = reinterpret_cast<uint32_t*>(ws.words + off);
+          for (uint32_t d = 0; d < 2 * W; d += 64)
+            if (d + lane < 2 * W) PSAMD_LDS_DMA(row + d + lane, dst + d, 4);
+          const uint32_t nd = ((c0 + deg + 3u) >> 2) - (c0 >> 2);
+          if (lane < nd) {
+            PSAMD_LDS_DMA(reinterpret_cast<const uint32_t*>(a.node_flags) + (c0 >> 2) + lane,
+                          ws.flags + doff, 4);
+            PSAMD_LDS_DMA(reinterpret_cast<const uint32_t*>(a.gen) + (c0 >> 2) + lane,
+                          ws.gens + doff, 4);
+          }
+          off += W;
+          doff += 4u * nd;
         }
-        if (W >= 64) {
-          for (uint32_t wb = 0; wb < W; wb += 64) {
-            const uint32_t w = wb + lane;
-            const bool active = w < W;
-            const uint64_t m = active ? a.a_cur[pw + w] : 0ull;
-            for (uint32_t jj = 0; jj < cd; ++jj) {
-              const uint32_t f = rl(fj, jj);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if (a.dbg & kDbgNoArrivalLoad)
+        for (uint32_t i = lane; i < sw; i += 64) ws.words[i] = ~0ull;
+      // phase B: stores
+      {
+        uint32_t off = 0, doff = 0;
+        for (uint32_t i = q; i < q + nq; ++i) {
+          const uint32_t W = rl(bW, i), deg = rl(bdeg, i);
+          if (W == 0) continue;
+          const uint32_t p = rl(bp, i), nbase = rl(bnb, i), c0 = rl(bc0, i);
+          const uint64_t wbase = (static_cast<uint64_t>(rl(bwh, i)) << 32) | rl(bwl, i);
+          const uint64_t cbase = wbase - static_cast<uint64_t>(nbase) * W;
+          const uint32_t nd = ((c0 + deg + 3u) >> 2) - (c0 >> 2);
+          const uint32_t fo = doff + (c0 & 3u);  // byte of child 0
+          ec.ent += 1;
+          ec.ent_words += W;
+          ec.kids += deg;
+          if (W >= 64) {
+            for (uint32_t jj = 0; jj < deg; ++jj) {
+              const uint32_t f = ws.flags[fo + jj];
               if (!(f & kNodeLive)) continue;
-              const uint32_t c = rl(cj, jj);
-              const bool stale = !mesh && rl(gj, jj) != cur;
+              const bool stale = ws.gens[fo + jj] != cur;
               const bool internal = (f & kNodeInternal) != 0;
+              const uint32_t c = c0 + jj;
+              const uint64_t row = cbase + static_cast<uint64_t>(c) * W;
+              bool any = false;
+              for (uint32_t wb = 0; wb < W; wb += 64) {
+                const uint32_t w = wb + lane;
+                if (w < W) {
+                  const uint64_t nm =
+                      deliver_word<kRecord>(a, false, stale, internal, row + w, ws.words[off + w], round, k);
+                  any |= nm != 0;
+                }
+              }
+              if (internal && __ballot(any) && lane == 0) mark_next(a, c);
+            }
+          } else {
+            const uint32_t sh = pow2_shift(W);
+            const uint32_t wp = 1u << sh;
+            const uint32_t w = lane & (wp - 1u);
+            const uint32_t jl = lane >> sh;
+            const uint32_t groups = 64u >> sh;
+            const uint64_t gmask = (wp == 64u ? ~0ull : ((1ull << wp) - 1ull)) << (jl << sh);
+            const uint64_t m = w < W ? ws.words[off + w] : 0ull;
+            for (uint32_t jb = 0; jb < deg; jb += groups) {
+              const uint32_t jj = jb + jl;
+              const bool valid = (w < W) && (jj < deg);
+              const uint32_t f = valid ? ws.flags[fo + jj] : 0u;
+              const bool live = valid && (f & kNodeLive);
+              const uint32_t c = c0 + jj;
               uint64_t nm = 0;
-              if (active)
-                nm = deliver_word<kRecord>(a, mesh, stale, internal,
+              if (live)
+                nm = deliver_word<kRecord>(a, false, ws.gens[fo + jj] != cur,
+                                           (f & kNodeInternal) != 0,
                                            cbase + static_cast<uint64_t>(c) * W + w, m, round, k);
-              if (internal && __ballot(nm != 0) && lane == 0) mark_next(a, c);
+              const uint64_t bal = __ballot(nm != 0);
+              if (live && w == 0 && (f & kNodeInternal) && (bal & gmask)) mark_next(a, c);
             }
           }
-        } else {
-          const uint32_t sh = 32u - __clz(W - 1u);  // Wp = 1 << sh >= W
-          const uint32_t wp = 1u << sh;
-          const uint32_t w = lane & (wp - 1u);
-          const uint32_t jl = lane >> sh;
-          const uint32_t groups = 64u >> sh;
-          const uint64_t gmask = (wp == 64u ? ~0ull : ((1ull << wp) - 1ull)) << (jl << sh);
-          const uint64_t m = w < W ? a.a_cur[pw + w] : 0ull;
-          for (uint32_t jb = 0; jb < cd; jb += groups) {
-            const uint32_t jj = jb + jl;
-            const uint32_t c = static_cast<uint32_t>(__shfl(static_cast<int>(cj), static_cast<int>(jj), 64));
-            const uint32_t f = static_cast<uint32_t>(__shfl(static_cast<int>(fj), static_cast<int>(jj), 64));
-            const uint32_t g = static_cast<uint32_t>(__shfl(static_cast<int>(gj), static_cast<int>(jj), 64));
-            const bool live = (w < W) && (jj < cd) && (f & kNodeLive);
-            uint64_t nm = 0;
-            if (live)
-              nm = deliver_word<kRecord>(a, mesh, !mesh && g != cur, (f & kNodeInternal) != 0,
-                                         cbase + static_cast<uint64_t>(c) * W + w, m, round, k);
-            const uint64_t bal = __ballot(nm != 0);
-            if (live && w == 0 && (f & kNodeInternal) && (bal & gmask)) mark_next(a, c);
+          // live children hold current rows now
+          if (lane < deg && (ws.flags[fo + lane] & kNodeLive) && !(a.dbg & kDbgNoByteStores))
+            a.gen[c0 + lane] = static_cast<uint8_t>(cur);
+          if (p == nbase) {  // root rows are seeded with |=: consume-and-clear
+            const uint64_t pw = wbase + static_cast<uint64_t>(p - nbase) * W;
+            for (uint32_t w = lane; w < W; w += 64) a.a_cur[pw + w] = 0;
+            ec.clear += W;
           }
+          off += W;
+          doff += 4u * nd;
         }
-        // this chunk's live tree children hold current rows now
-        if (!mesh && lane < cd && (fj & kNodeLive)) a.gen[cj] = static_cast<uint8_t>(cur);
       }
-      if (mesh || p == T.nbase) {
-        // consume-and-clear: mesh rows are OR-accumulated, root rows are seeded
-        for (uint32_t w = lane; w < W; w += 64) a.a_cur[pw + w] = 0;
-        c_clear += W;
-      }
+      q += nq;
     }
   }
 
@@ -300,14 +457,14 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
     uint64_t* out = a.partials + static_cast<uint64_t>(wave) * kNumCtr;
     out[kCtrDeliveries] = s_deliv;
     out[kCtrDuplicates] = s_dup;
-    out[kCtrEntries] = c_ent;
-    out[kCtrEntryWords] = c_ent_words;
-    out[kCtrChildren] = c_kids;
-    out[kCtrMeshChildren] = c_mesh_kids;
+    out[kCtrEntries] = ec.ent;
+    out[kCtrEntryWords] = ec.ent_words;
+    out[kCtrChildren] = ec.kids;
+    out[kCtrMeshChildren] = ec.mesh_kids;
     out[kCtrSeenReads] = s_sr;
     out[kCtrSeenWrites] = s_sw;
     out[kCtrArrivalWrites] = s_aw;
-    out[kCtrClearWords] = c_clear;
+    out[kCtrClearWords] = ec.clear;
   }
 }
 

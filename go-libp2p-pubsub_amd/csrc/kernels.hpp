@@ -75,6 +75,15 @@ struct ExpandArgs {
   uint64_t* partials;  // [n_waves][kNumCtr]
   uint8_t* hop_rec;    // [word*64 + bit] = round, record mode only
   uint32_t gen_cur;
+  uint32_t dbg;  // experiment knobs (kDbg*), 0 in production
+};
+
+// k_expand experiment knobs (PSAMD_DEBUG_EXPAND); results are wrong when set
+enum : uint32_t {
+  kDbgNoArrivalLoad = 1,   // arrival words read as all-ones
+  kDbgNoArrivalStore = 2,  // skip arrival-row stores
+  kDbgNoByteStores = 4,    // skip frontier-flag and generation byte stores
+  kDbgNoSeenStore = 8,     // skip seen-row stores
 };
 
 constexpr int kBlock = 256;

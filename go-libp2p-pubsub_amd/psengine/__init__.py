@@ -47,14 +47,20 @@ class Stats(C.Structure):
                 ("edge_words", C.c_uint64), ("expand_bytes", C.c_uint64),
                 ("windows", C.c_uint64), ("rounds", C.c_uint64), ("expand_launches", C.c_uint64),
                 ("run_ms", C.c_double), ("expand_ms", C.c_double), ("host_ms", C.c_double),
-                ("deliveries_per_round", C.c_uint64 * MAX_ROUNDS)]
+                ("deliveries_per_round", C.c_uint64 * MAX_ROUNDS),
+                ("expand_ms_per_round", C.c_float * MAX_ROUNDS),
+                ("frontier_per_round", C.c_uint32 * MAX_ROUNDS)]
+
+    PER_ROUND = ("deliveries_per_round", "expand_ms_per_round", "frontier_per_round")
 
     def as_dict(self) -> dict:
-        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "deliveries_per_round"}
-        per = list(self.deliveries_per_round)
-        while per and per[-1] == 0:
-            per.pop()
-        d["deliveries_per_round"] = per
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k not in self.PER_ROUND}
+        n = int(self.rounds) + 1 if self.windows == 1 else MAX_ROUNDS
+        for k in self.PER_ROUND:
+            per = list(getattr(self, k))[:min(n, MAX_ROUNDS)]
+            while per and per[-1] == 0:
+                per.pop()
+            d[k] = per
         return d
 
 

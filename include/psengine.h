@@ -74,6 +74,8 @@ typedef struct ps_stats {
   double expand_ms;            /* summed expand-kernel device time (TIME flag)   */
   double host_ms;              /* wall time of the ps_run call                   */
   uint64_t deliveries_per_round[PS_MAX_ROUNDS];
+  float expand_ms_per_round[PS_MAX_ROUNDS];   /* TIME flag, summed over windows  */
+  uint32_t frontier_per_round[PS_MAX_ROUNDS]; /* expanded entries per round      */
 } ps_stats;
 
 typedef struct ps_engine ps_engine;
