@@ -69,6 +69,7 @@ struct TopicHost {
   // node space (set by build_graph)
   uint32_t nbase = 0, n_nodes = 0, depth = 0;
   bool mesh = false;
+  std::vector<uint32_t> level_internal;  // BFS level -> nodes with children
 };
 
 struct RunMsg {
@@ -220,6 +221,21 @@ int build_graph(ps_engine* e) {
     }
     if (order.size() > level_end) ++depth;
     T.depth = depth;
+    // internal nodes per BFS level: bounds the frontier of every round
+    T.level_internal.assign(depth + 1, 0);
+    {
+      std::vector<uint32_t> lvl(order.size(), 0);
+      for (uint32_t u = 0; u < order.size(); ++u) {
+        const uint32_t p = order[u];
+        bool internal = false;
+        for (uint32_t k = rp[p]; k < rp[p + 1]; ++k) {
+          const uint32_t lc = local[cl[k]];
+          if (lc > u && lvl[lc] == 0) lvl[lc] = lvl[u] + 1;  // BFS discovery
+          internal = true;
+        }
+        if (internal) T.level_internal[lvl[u]]++;
+      }
+    }
     T.n_nodes = static_cast<uint32_t>(order.size());
     if (n_total + order.size() >= 0xFFFFFFF0ull)
       return e->fail(PS_E_NOMEM, "node space exceeds 2^32 nodes");
@@ -329,7 +345,11 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
     d.flags = T.mesh ? kTopicMesh : 0;
     if (!T.exists || win[t].empty() || T.n_nodes == 0) continue;
     d.W = ceil_div(win[t].size(), 64);
-    d.magic = ((1ull << 32) + d.W - 1) / d.W;
+    d.w_msgs = d.W;
+    // rows of >= 64 words are padded to an even length so that every row
+    // starts 16-B aligned (the expand kernel stores them as dwordx4)
+    if (d.W >= 64) d.W += d.W & 1u;
+    wtot = (wtot + 15) & ~15ull;  // topic blocks start on a 128-B line
     d.wbase = wtot;
     wtot += static_cast<uint64_t>(T.n_nodes) * d.W;
     max_depth = std::max(max_depth, T.depth);
@@ -371,6 +391,34 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
     seed_off[r + 1] = static_cast<uint32_t>(seeds.size());
   }
   HIP_TRY(e->d_seeds.ensure(seeds.size() * sizeof(SeedDev)), "alloc seeds");
+
+  // Upper bound of the frontier expanded in round r (tree topics: a node at
+  // BFS level d receives a message started at round s in round s + d), used
+  // to size each round's grid; mesh topics (paths lengthen under the live
+  // mask) use the full grid.
+  bool any_mesh_active = false;
+  std::vector<std::vector<uint8_t>> starts_of(nt);
+  for (uint32_t t = 0; t < nt; ++t) {
+    if (tab[t].W == 0) continue;
+    if (e->topics[t].mesh) any_mesh_active = true;
+    starts_of[t].assign(max_start + 1, 0);
+    for (uint32_t i : win[t]) starts_of[t][msgs[i].start] = 1;
+  }
+  auto round_grid = [&](uint32_t r) -> uint32_t {
+    if (any_mesh_active) return e->expand_grid;
+    uint64_t bound = 0;
+    for (uint32_t t = 0; t < nt; ++t) {
+      if (tab[t].W == 0) continue;
+      const auto& li = e->topics[t].level_internal;
+      for (uint32_t s0 = 0; s0 <= max_start; ++s0) {
+        if (!starts_of[t][s0] || r < 1 + s0) continue;
+        const uint32_t d = r - 1 - s0;
+        if (d < li.size()) bound += li[d];
+      }
+    }
+    const uint64_t blocks = (bound + 3) / 4;  // ~1 entry per wave at least
+    return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(e->expand_grid, blocks)));
+  };
 
   hipStream_t s = e->stream;
   HIP_TRY(hipMemcpyAsync(e->d_topics.p, tab.data(), tab.size() * sizeof(TopicDev),
@@ -424,9 +472,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
     return launch_seed(e->d_seeds.as<SeedDev>(), seed_off[r], seed_off[r + 1], into,
                        a.seen, a.next_flag, a.blk_flag, s);
   };
-  auto compact = [&](uint32_t r) -> hipError_t {
+  auto compact = [&](uint32_t r, uint32_t waves_r) -> hipError_t {
     hipError_t x = launch_flag_count(a.next_flag, a.blk_flag, e->n_pad,
-                                     e->d_wgcount.as<uint32_t>(), a.partials, n_waves,
+                                     e->d_wgcount.as<uint32_t>(), a.partials, waves_r,
                                      r ? stats + r * kNumCtr : nullptr, s);
     if (x != hipSuccess) return x;
     return launch_flag_compact(a.next_flag, a.blk_flag, e->n_pad, e->d_wgcount.as<uint32_t>(),
@@ -434,7 +482,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
   };
 
   HIP_TRY(seed_round(0, arr[0]), "seed");
-  HIP_TRY(compact(0), "compact");
+  HIP_TRY(compact(0, 0), "compact");
   uint32_t planned = max_depth + max_start + 1;
   uint32_t r = 0;
   size_t ev_used = 0;
@@ -453,11 +501,12 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
         }
         HIP_TRY(hipEventRecord(e->ev_k[ev_used], s), "event");
       }
-      HIP_TRY(launch_expand(a, r, record, e->expand_grid, s), "expand");
+      const uint32_t grid_r = r <= planned ? round_grid(r) : e->expand_grid;
+      HIP_TRY(launch_expand(a, r, record, grid_r, s), "expand");
       if (timed) HIP_TRY(hipEventRecord(e->ev_k[ev_used + 1], s), "event");
       if (timed) ev_used += 2;
       HIP_TRY(seed_round(r, a.a_next), "seed");
-      HIP_TRY(compact(r), "compact");
+      HIP_TRY(compact(r, grid_r * (kBlock / 64)), "compact");
     }
     uint32_t left = 0;
     HIP_TRY(hipMemcpyAsync(&left, e->d_nfront.p, 4, hipMemcpyDeviceToHost, s), "read frontier");

@@ -176,6 +176,53 @@ __device__ __forceinline__ uint64_t deliver_word(const ExpandArgs& a, bool mesh,
   return nm;
 }
 
+// A child whose row is stale (nothing seen this window): every arriving bit is
+// new, the whole row is written, no load -- so no vmcnt wait in the burst.
+template <bool kRecord>
+__device__ __forceinline__ void deliver_fresh(const ExpandArgs& a, bool internal, uint64_t cw,
+                                              uint64_t m, uint32_t round, ExpandCtr& k) {
+  if (!(a.dbg & kDbgNoSeenStore)) a.seen[cw] = m;
+  k.sw += 1;
+  if (internal && !(a.dbg & kDbgNoArrivalStore)) {
+    a.a_next[cw] = m;
+    k.aw += 1;
+  }
+  k.deliv += __popcll(m);
+  if constexpr (kRecord) {
+    uint8_t* h = a.hop_rec + cw * 64;
+    uint64_t b = m;
+    while (b) {
+      const int q = __ffsll(static_cast<long long>(b)) - 1;
+      h[q] = static_cast<uint8_t>(round);
+      b &= b - 1;
+    }
+  }
+}
+
+// Two adjacent words of a fresh row (16-B aligned): one dwordx4 store each.
+template <bool kRecord>
+__device__ __forceinline__ void deliver_fresh2(const ExpandArgs& a, bool internal, uint64_t cw,
+                                               uint4 v, uint32_t round, ExpandCtr& k) {
+  if (!(a.dbg & kDbgNoSeenStore)) *reinterpret_cast<uint4*>(a.seen + cw) = v;
+  k.sw += 2;
+  if (internal && !(a.dbg & kDbgNoArrivalStore)) {
+    *reinterpret_cast<uint4*>(a.a_next + cw) = v;
+    k.aw += 2;
+  }
+  k.deliv += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+  if constexpr (kRecord) {
+    for (int h = 0; h < 2; ++h) {
+      uint8_t* rec = a.hop_rec + (cw + h) * 64;
+      uint64_t b = h ? (static_cast<uint64_t>(v.w) << 32 | v.z) : (static_cast<uint64_t>(v.y) << 32 | v.x);
+      while (b) {
+        const int q = __ffsll(static_cast<long long>(b)) - 1;
+        rec[q] = static_cast<uint8_t>(round);
+        b &= b - 1;
+      }
+    }
+  }
+}
+
 __device__ __forceinline__ void mark_next(const ExpandArgs& a, uint32_t c) {
   if (a.dbg & kDbgNoByteStores) return;
   a.next_flag[c] = 1;
@@ -198,7 +245,7 @@ __device__ __forceinline__ uint32_t pow2_shift(uint32_t W) { return 32u - __clz(
 // entries, plus the flag and generation bytes of their children.
 constexpr uint32_t kStageWords = 704;  // 5.5 KiB
 constexpr uint32_t kStageBytes = 512;  // 2 x 512 B of child flag / generation dwords
-struct WaveStage {
+struct __attribute__((aligned(16))) WaveStage {
   uint64_t words[kStageWords];
   uint8_t flags[kStageBytes];
   uint8_t gens[kStageBytes];
@@ -344,8 +391,8 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
         const uint32_t cn = rl(bc0, q + nq);
         const uint32_t bn = 4u * (((cn + dn + 3u) >> 2) - (cn >> 2));
         if ((fn & kTopicMesh) || Wn > kStageWords || dn > 64) break;
-        if (sw + Wn > kStageWords || sd + bn > kStageBytes) break;
-        sw += Wn;
+        if (sw + Wn + (Wn & 1u) > kStageWords || sd + bn > kStageBytes) break;
+        sw += Wn + (Wn & 1u);
         sd += bn;
         ++nq;
       }
@@ -369,7 +416,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
             PSAMD_LDS_DMA(reinterpret_cast<const uint32_t*>(a.gen) + (c0 >> 2) + lane,
                           ws.gens + doff, 4);
           }
-          off += W;
+          off += W + (W & 1u);  // keep every staged row 16-B aligned
           doff += 4u * nd;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -399,12 +446,25 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
               const uint32_t c = c0 + jj;
               const uint64_t row = cbase + static_cast<uint64_t>(c) * W;
               bool any = false;
-              for (uint32_t wb = 0; wb < W; wb += 64) {
-                const uint32_t w = wb + lane;
-                if (w < W) {
-                  const uint64_t nm =
-                      deliver_word<kRecord>(a, false, stale, internal, row + w, ws.words[off + w], round, k);
-                  any |= nm != 0;
+              if (stale) {
+                // W even, row and stage offset even: two words per lane,
+                // 1 KiB per store instruction
+                for (uint32_t wb = 0; wb < W; wb += 128) {
+                  const uint32_t w = wb + 2 * lane;
+                  if (w < W) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(ws.words + off + w);
+                    deliver_fresh2<kRecord>(a, internal, row + w, v, round, k);
+                    any |= (v.x | v.y | v.z | v.w) != 0;
+                  }
+                }
+              } else {
+                for (uint32_t wb = 0; wb < W; wb += 64) {
+                  const uint32_t w = wb + lane;
+                  if (w < W) {
+                    const uint64_t nm = deliver_word<kRecord>(a, false, false, internal, row + w,
+                                                              ws.words[off + w], round, k);
+                    any |= nm != 0;
+                  }
                 }
               }
               if (internal && __ballot(any) && lane == 0) mark_next(a, c);
@@ -422,12 +482,18 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
               const bool valid = (w < W) && (jj < deg);
               const uint32_t f = valid ? ws.flags[fo + jj] : 0u;
               const bool live = valid && (f & kNodeLive);
+              const bool stale = ws.gens[fo + jj] != cur;
               const uint32_t c = c0 + jj;
+              const uint64_t cw = cbase + static_cast<uint64_t>(c) * W + w;
               uint64_t nm = 0;
-              if (live)
-                nm = deliver_word<kRecord>(a, false, ws.gens[fo + jj] != cur,
-                                           (f & kNodeInternal) != 0,
-                                           cbase + static_cast<uint64_t>(c) * W + w, m, round, k);
+              if (__ballot(live && !stale) == 0) {  // burst: every live child fresh
+                if (live) {
+                  deliver_fresh<kRecord>(a, (f & kNodeInternal) != 0, cw, m, round, k);
+                  nm = m;
+                }
+              } else if (live) {
+                nm = deliver_word<kRecord>(a, false, stale, (f & kNodeInternal) != 0, cw, m, round, k);
+              }
               const uint64_t bal = __ballot(nm != 0);
               if (live && w == 0 && (f & kNodeInternal) && (bal & gmask)) mark_next(a, c);
             }
@@ -440,7 +506,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
             for (uint32_t w = lane; w < W; w += 64) a.a_cur[pw + w] = 0;
             ec.clear += W;
           }
-          off += W;
+          off += W + (W & 1u);
           doff += 4u * nd;
         }
       }
@@ -570,7 +636,7 @@ __global__ __launch_bounds__(kBlock) void k_digest(const uint64_t* __restrict__ 
     const bool valid = (T.flags & kTopicMesh) || gen[u] == static_cast<uint8_t>(gen_cur);
     const uint64_t row = T.wbase + static_cast<uint64_t>(u - T.nbase) * T.W;
     const uint64_t key0 = (static_cast<uint64_t>(node_peer[u]) << 32) | (static_cast<uint64_t>(t) << 16);
-    for (uint32_t w = 0; w < T.W; ++w)
+    for (uint32_t w = 0; w < T.w_msgs; ++w)
       acc += mix64((key0 | w) ^ mix64(valid ? seen[row + w] : 0ull));
   }
   acc = wave_sum_u64(acc);

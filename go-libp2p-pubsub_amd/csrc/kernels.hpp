@@ -27,7 +27,8 @@ enum : uint32_t {
 // BFS order, so the children of a node are consecutive node ids.
 struct TopicDev {
   uint64_t wbase;    // first word of the topic's mask block
-  uint64_t magic;    // ceil(2^32 / W): item -> (child, word) split
+  uint32_t w_msgs;   // message words in use (W may carry one pad word)
+  uint32_t pad;
   uint32_t nbase;    // first node of the topic (its root)
   uint32_t n_nodes;  // nodes in the topic
   uint32_t W;        // 64-message words per node in this window (0 = idle)
