@@ -1,0 +1,192 @@
+// dist.cpp -- RCCL and in-process loopback frontier-exchange transports.
+#include "dist.hpp"
+
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+
+namespace psamd {
+
+// ------------------------------------------------------------------ RCCL ---
+namespace {
+
+class RcclTransport final : public Transport {
+ public:
+  RcclTransport(int rank, int world, ncclComm_t comm) : rank_(rank), world_(world), comm_(comm) {}
+  ~RcclTransport() override {
+    if (comm_) ncclCommDestroy(comm_);
+  }
+  int rank() const override { return rank_; }
+  int world() const override { return world_; }
+  const char* name() const override { return "rccl"; }
+  hipError_t exchange(const uint8_t* send, const std::vector<uint64_t>& send_off,
+                      const std::vector<uint64_t>& send_len, uint8_t* recv,
+                      const std::vector<uint64_t>& recv_off, const std::vector<uint64_t>& recv_len,
+                      hipStream_t s, std::string* err) override {
+    ncclResult_t r = ncclGroupStart();
+    for (int p = 0; p < world_ && r == ncclSuccess; ++p) {
+      if (p == rank_) continue;
+      if (send_len[p])
+        r = ncclSend(send + send_off[p], send_len[p], ncclUint8, p, comm_, s);
+      if (r == ncclSuccess && recv_len[p])
+        r = ncclRecv(recv + recv_off[p], recv_len[p], ncclUint8, p, comm_, s);
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r == ncclSuccess) r = r2;
+    if (r != ncclSuccess) {
+      if (err) *err = std::string("rccl exchange: ") + ncclGetErrorString(r);
+      return hipErrorUnknown;
+    }
+    return hipSuccess;
+  }
+
+ private:
+  int rank_, world_;
+  ncclComm_t comm_;
+};
+
+}  // namespace
+
+int rccl_unique_id(uint8_t id_out[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "NCCL unique id size");
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return -1;
+  std::memcpy(id_out, &id, sizeof(id));
+  return 0;
+}
+
+std::unique_ptr<Transport> make_rccl_transport(int rank, int world, const uint8_t id_bytes[128],
+                                               std::string* err) {
+  ncclUniqueId id;
+  std::memcpy(&id, id_bytes, sizeof(id));
+  ncclComm_t comm = nullptr;
+  ncclResult_t r = ncclCommInitRank(&comm, world, id, rank);
+  if (r != ncclSuccess) {
+    if (err) *err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+    return nullptr;
+  }
+  return std::make_unique<RcclTransport>(rank, world, comm);
+}
+
+// -------------------------------------------------------------- loopback ---
+struct LoopbackGroup {
+  int world;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  uint64_t generation = 0;
+  struct Slot {
+    const uint8_t* send = nullptr;
+    const std::vector<uint64_t>* send_off = nullptr;
+    hipEvent_t sent = nullptr;  // send regions complete (stream order)
+    hipEvent_t read = nullptr;  // this rank finished copying from the others
+  };
+  std::vector<Slot> slot;
+
+  explicit LoopbackGroup(int w) : world(w), slot(w) {}
+
+  bool broken = false;
+
+  // false when a rank did not arrive within 60 s (it failed): the group is
+  // broken for good and every later exchange fails instead of hanging
+  bool barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    if (broken) return false;
+    const uint64_t gen = generation;
+    if (++arrived == world) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+      return true;
+    }
+    if (!cv.wait_for(lk, std::chrono::seconds(60), [&] { return generation != gen || broken; }) ||
+        broken) {
+      broken = true;
+      cv.notify_all();
+      return false;
+    }
+    return true;
+  }
+};
+
+LoopbackGroup* loopback_create(int world) {
+  if (world < 1) return nullptr;
+  return new LoopbackGroup(world);
+}
+
+void loopback_destroy(LoopbackGroup* g) { delete g; }
+
+namespace {
+
+class LoopbackTransport final : public Transport {
+ public:
+  LoopbackTransport(LoopbackGroup* g, int rank, int device) : g_(g), rank_(rank), device_(device) {
+    (void)hipSetDevice(device_);
+    (void)hipEventCreateWithFlags(&sent_, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&read_, hipEventDisableTiming);
+  }
+  ~LoopbackTransport() override {
+    if (sent_) (void)hipEventDestroy(sent_);
+    if (read_) (void)hipEventDestroy(read_);
+  }
+  int rank() const override { return rank_; }
+  int world() const override { return g_->world; }
+  const char* name() const override { return "loopback"; }
+
+  hipError_t exchange(const uint8_t* send, const std::vector<uint64_t>& send_off,
+                      const std::vector<uint64_t>& send_len, uint8_t* recv,
+                      const std::vector<uint64_t>& recv_off, const std::vector<uint64_t>& recv_len,
+                      hipStream_t s, std::string* err) override {
+    (void)send_len;
+    hipError_t e = hipEventRecord(sent_, s);
+    if (e != hipSuccess) return fail(e, err);
+    auto& me = g_->slot[rank_];
+    me.send = send;
+    me.send_off = &send_off;
+    me.sent = sent_;
+    me.read = read_;
+    if (!g_->barrier()) return timeout(err);  // every rank published regions + `sent`
+    for (int src = 0; src < g_->world; ++src) {
+      if (src == rank_ || recv_len[src] == 0) continue;
+      const auto& o = g_->slot[src];
+      if ((e = hipStreamWaitEvent(s, o.sent, 0)) != hipSuccess) return fail(e, err);
+      e = hipMemcpyAsync(recv + recv_off[src], o.send + (*o.send_off)[rank_], recv_len[src],
+                         hipMemcpyDeviceToDevice, s);
+      if (e != hipSuccess) return fail(e, err);
+    }
+    if ((e = hipEventRecord(read_, s)) != hipSuccess) return fail(e, err);
+    if (!g_->barrier()) return timeout(err);  // every rank enqueued copies + `read`
+    // our send regions may be rewritten only after every reader copied them
+    for (int q = 0; q < g_->world; ++q) {
+      if (q == rank_) continue;
+      if ((e = hipStreamWaitEvent(s, g_->slot[q].read, 0)) != hipSuccess) return fail(e, err);
+    }
+    if (!g_->barrier()) return timeout(err);  // `read` events may be re-recorded
+    return hipSuccess;
+  }
+
+ private:
+  static hipError_t timeout(std::string* err) {
+    if (err) *err = "loopback exchange: a rank did not arrive (group broken)";
+    return hipErrorUnknown;
+  }
+  static hipError_t fail(hipError_t e, std::string* err) {
+    if (err) *err = std::string("loopback exchange: ") + hipGetErrorString(e);
+    return e;
+  }
+  LoopbackGroup* g_;
+  int rank_, device_;
+  hipEvent_t sent_ = nullptr, read_ = nullptr;
+};
+
+}  // namespace
+
+std::unique_ptr<Transport> make_loopback_transport(LoopbackGroup* g, int rank, int device) {
+  if (!g || rank < 0 || rank >= g->world) return nullptr;
+  return std::make_unique<LoopbackTransport>(g, rank, device);
+}
+
+}  // namespace psamd

@@ -1,0 +1,46 @@
+// dist.hpp -- frontier-exchange transports of the multi-GPU engine.
+//
+// One engine per GPU (rank).  Each synchronous round the ranks exchange the
+// deliveries addressed to tree nodes owned by another rank: every rank sends
+// rank d one region of fixed, host-known size (header + capacity items), so
+// the exchange is stream-ordered and needs no host synchronisation.
+//   RcclTransport      ncclSend / ncclRecv pairs in one group (all-to-allv over
+//                      xGMI), the production transport.
+//   LoopbackTransport  `world` engines of one process (threads) copy each
+//                      other's regions device-to-device; lets the real kernels
+//                      and routing be tested on a single GPU.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace psamd {
+
+class Transport {
+ public:
+  virtual ~Transport() = default;
+  virtual int rank() const = 0;
+  virtual int world() const = 0;
+  // All-to-allv of device byte ranges on stream s: region d of `send` goes to
+  // rank d, region s of `recv` comes from rank s (sizes agree pairwise).
+  virtual hipError_t exchange(const uint8_t* send, const std::vector<uint64_t>& send_off,
+                              const std::vector<uint64_t>& send_len, uint8_t* recv,
+                              const std::vector<uint64_t>& recv_off,
+                              const std::vector<uint64_t>& recv_len, hipStream_t s,
+                              std::string* err) = 0;
+  virtual const char* name() const = 0;
+};
+
+std::unique_ptr<Transport> make_rccl_transport(int rank, int world, const uint8_t id[128],
+                                               std::string* err);
+int rccl_unique_id(uint8_t id_out[128]);
+
+struct LoopbackGroup;
+LoopbackGroup* loopback_create(int world);
+void loopback_destroy(LoopbackGroup* g);
+std::unique_ptr<Transport> make_loopback_transport(LoopbackGroup* g, int rank, int device);
+
+}  // namespace psamd

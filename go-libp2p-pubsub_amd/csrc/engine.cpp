@@ -9,9 +9,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <memory>
 #include <string>
+#include <tuple>
 #include <vector>
 
+#include "dist.hpp"
 #include "kernels.hpp"
 #include "psengine.h"
 #include "tree.hpp"
@@ -69,7 +73,14 @@ struct TopicHost {
   // node space (set by build_graph)
   uint32_t nbase = 0, n_nodes = 0, depth = 0;
   bool mesh = false;
-  std::vector<uint32_t> level_internal;  // BFS level -> nodes with children
+  bool root_local = true;                // this rank owns the root
+  uint32_t max_deg = 0;
+  std::vector<uint32_t> level_internal;  // BFS level -> owned nodes with children
+  // cross-rank edges by the parent's BFS level: (level, from rank, to rank, count)
+  struct Cross {
+    uint32_t level, from, to, count;
+  };
+  std::vector<Cross> cross;
 };
 
 struct RunMsg {
@@ -77,9 +88,11 @@ struct RunMsg {
   uint32_t start;
 };
 
-struct WindowMsg {
-  uint32_t run_idx;  // index into the run's message list
-  uint32_t local;    // bit index within the topic's window block
+// Messages of one topic in one window: a slice of the run's topic-sorted
+// message index array (bit li of the topic block = message idx[li]).
+struct WinSlice {
+  const uint32_t* idx = nullptr;
+  uint32_t n = 0;
 };
 
 uint32_t ceil_div(uint64_t a, uint64_t b) { return static_cast<uint32_t>((a + b - 1) / b); }
@@ -108,6 +121,14 @@ struct ps_engine {
   DevBuf d_seen, d_arr0, d_arr1, d_hop, d_flags, d_blk, d_gen, d_frontier, d_nfront, d_wgcount,
       d_partials, d_stats, d_topics, d_seeds, d_digest;
   uint32_t gen_cur = 0;  // window generation stamped into d_gen (1..255)
+  DevBuf d_remote_fed, d_send, d_recv, d_apply_stats;
+  uint32_t n_remote_fed = 0;
+  std::vector<uint32_t> remote_fed;  // owned nodes whose parent is on another rank
+
+  // multi-GPU: this engine owns a hash-partitioned share of every topic
+  int32_t rank = 0, world = 1;
+  uint32_t partition = PS_PART_SUBTREE, split_depth = 0;
+  std::unique_ptr<Transport> transport;
 
   // publishes not yet run
   std::vector<RunMsg> pending;
@@ -117,8 +138,11 @@ struct ps_engine {
   uint32_t last_first = 0, last_n = 0;
   bool have_hops = false;
   std::vector<uint8_t> hops;  // [msg][peer]
-  std::vector<RunMsg> last_msgs;
-  std::vector<int32_t> last_win_local;  // per run msg: bit index in the last window, -1 if not there
+  std::vector<RunMsg> last_msgs;        // messages of the last run, publish order
+  std::vector<uint32_t> run_sorted;     // run message indices grouped by topic
+  std::vector<uint32_t> run_topic_off;  // topic -> first position in run_sorted
+  std::vector<uint32_t> run_rank;       // message -> position within its topic
+  std::vector<uint32_t> last_lo, last_cnt;  // topic -> last window's rank range
   std::vector<TopicDev> last_topics;
   bool have_window = false;
 
@@ -180,35 +204,76 @@ void peer_children(const ps_engine* e, const TopicHost& T, std::vector<uint32_t>
   }
 }
 
-// Builds the fused node space: per topic, the nodes reachable from the root
-// in BFS order (siblings contiguous, root = first node), CSR over node ids.
+// Ownership of one topic's nodes (positions in its BFS order) among `world`
+// ranks.  PS_PART_PEER: owner = splitmix64(peer) mod world.
+// PS_PART_SUBTREE: nodes at BFS level >= L belong to the owner of their
+// ancestor at level L, hashed as splitmix64(topic<<32 | ancestor peer); the
+// few nodes above L hash by peer.  L = split_depth, or (0) the first level
+// holding >= 64*world nodes, so only edges out of levels < L cross ranks.
+void partition_topic(const std::vector<uint32_t>& order, const std::vector<uint32_t>& bfs_parent,
+                     const std::vector<uint32_t>& level, uint32_t topic, int32_t world,
+                     uint32_t part, uint32_t split_depth, std::vector<int32_t>& owner) {
+  const size_t n = order.size();
+  owner.assign(n, 0);
+  if (world <= 1) return;
+  auto mix = [](uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  };
+  uint32_t L = split_depth;
+  if (part == PS_PART_SUBTREE && L == 0) {
+    std::vector<uint64_t> cnt;
+    for (size_t u = 0; u < n; ++u) {
+      if (level[u] >= cnt.size()) cnt.resize(level[u] + 1, 0);
+      cnt[level[u]]++;
+    }
+    L = static_cast<uint32_t>(cnt.size() ? cnt.size() - 1 : 0);
+    for (uint32_t d = 0; d < cnt.size(); ++d)
+      if (cnt[d] >= 64ull * world) {
+        L = d;
+        break;
+      }
+  }
+  std::vector<uint32_t> anc(n, kNone);
+  for (size_t u = 0; u < n; ++u) {
+    if (part == PS_PART_SUBTREE && level[u] >= L && L > 0) {
+      anc[u] = level[u] == L ? static_cast<uint32_t>(u) : anc[bfs_parent[u]];
+      owner[u] = static_cast<int32_t>(mix((static_cast<uint64_t>(topic) << 32) | order[anc[u]]) %
+                                      static_cast<uint64_t>(world));
+    } else {
+      owner[u] = static_cast<int32_t>(mix(order[u]) % static_cast<uint64_t>(world));
+    }
+  }
+}
+
+// Builds this rank's node space: per topic, the owned nodes among those
+// reachable from the root, in global BFS order (siblings contiguous, the root
+// first when owned), CSR over node ids; a child owned by another rank is
+// encoded kRemoteBit | rank << 27 | its id at that rank.
 int build_graph(ps_engine* e) {
   const uint32_t n = e->cfg.n_peers;
+  const int32_t world = e->world, me = e->rank;
   e->node_peer.clear();
   e->node_topic.clear();
   e->row_ptr.assign(1, 0);
   e->col.clear();
-  std::vector<uint32_t> local(n, kNone);
-  std::vector<uint32_t> rp, cl, order, indeg;
-  uint64_t n_total = 0;
-  for (uint32_t t = 0; t < e->topics.size(); ++t) {
-    TopicHost& T = e->topics[t];
-    T.nbase = static_cast<uint32_t>(n_total);
-    T.n_nodes = 0;
-    T.depth = 0;
-    T.mesh = false;
-    if (!T.exists) continue;
+  e->remote_fed.clear();
+  std::vector<uint32_t> local(n, kNone);  // peer -> BFS position
+  std::vector<uint32_t> rp, cl, order, indeg, bfs_parent, level, loc;
+  std::vector<int32_t> owner;
+  // node-space base of every topic at every rank (multi-GPU: a remote child
+  // is addressed by its fused node id at its owner)
+  const uint32_t ntop = static_cast<uint32_t>(e->topics.size());
+  std::vector<uint64_t> base_at(static_cast<size_t>(ntop) * std::max(world, 1), 0);
+  auto topic_bfs = [&](TopicHost& T, uint32_t t) -> int {
     peer_children(e, T, rp, cl);
-    order.clear();
-    order.push_back(T.root);
+    order.assign(1, T.root);
+    bfs_parent.assign(1, kNone);
+    level.assign(1, 0);
     local[T.root] = 0;
-    size_t level_end = 1;
-    uint32_t depth = 0;
     for (size_t qi = 0; qi < order.size(); ++qi) {
-      if (qi == level_end) {
-        level_end = order.size();
-        ++depth;
-      }
       const uint32_t p = order[qi];
       for (uint32_t k = rp[p]; k < rp[p + 1]; ++k) {
         const uint32_t c = cl[k];
@@ -216,46 +281,94 @@ int build_graph(ps_engine* e) {
         if (local[c] == kNone) {
           local[c] = static_cast<uint32_t>(order.size());
           order.push_back(c);
+          bfs_parent.push_back(static_cast<uint32_t>(qi));
+          level.push_back(level[qi] + 1);
         }
       }
     }
-    if (order.size() > level_end) ++depth;
-    T.depth = depth;
-    // internal nodes per BFS level: bounds the frontier of every round
-    T.level_internal.assign(depth + 1, 0);
+    partition_topic(order, bfs_parent, level, t, world, e->partition, e->split_depth, owner);
+    return PS_OK;
+  };
+  if (world > 1) {
+    std::vector<uint64_t> run(world, 0);
+    for (uint32_t t = 0; t < ntop; ++t) {
+      for (int32_t q = 0; q < world; ++q) base_at[static_cast<size_t>(t) * world + q] = run[q];
+      TopicHost& T = e->topics[t];
+      if (!T.exists) continue;
+      int rc = topic_bfs(T, t);
+      if (rc) return rc;
+      for (size_t u = 0; u < order.size(); ++u) run[owner[u]]++;
+      for (uint32_t p : order) local[p] = kNone;
+    }
+  }
+  uint64_t n_total = 0;
+  for (uint32_t t = 0; t < e->topics.size(); ++t) {
+    TopicHost& T = e->topics[t];
+    T.nbase = static_cast<uint32_t>(n_total);
+    T.n_nodes = 0;
+    T.depth = 0;
+    T.mesh = false;
+    T.root_local = true;
+    T.max_deg = 0;
+    T.cross.clear();
+    T.level_internal.clear();
+    if (!T.exists) continue;
     {
-      std::vector<uint32_t> lvl(order.size(), 0);
-      for (uint32_t u = 0; u < order.size(); ++u) {
-        const uint32_t p = order[u];
-        bool internal = false;
-        for (uint32_t k = rp[p]; k < rp[p + 1]; ++k) {
-          const uint32_t lc = local[cl[k]];
-          if (lc > u && lvl[lc] == 0) lvl[lc] = lvl[u] + 1;  // BFS discovery
-          internal = true;
-        }
-        if (internal) T.level_internal[lvl[u]]++;
-      }
+      int rc = topic_bfs(T, t);
+      if (rc) return rc;
     }
-    T.n_nodes = static_cast<uint32_t>(order.size());
-    if (n_total + order.size() >= 0xFFFFFFF0ull)
-      return e->fail(PS_E_NOMEM, "node space exceeds 2^32 nodes");
-    indeg.assign(order.size(), 0);
-    for (uint32_t u = 0; u < order.size(); ++u) {
+    for (uint32_t p : order) T.max_deg = std::max(T.max_deg, rp[p + 1] - rp[p]);
+    const uint32_t N = static_cast<uint32_t>(order.size());
+    T.depth = level.back();
+    indeg.assign(N, 0);
+    for (uint32_t u = 0; u < N; ++u)
+      for (uint32_t k = rp[order[u]]; k < rp[order[u] + 1]; ++k) indeg[local[cl[k]]]++;
+    for (uint32_t u = 0; u < N; ++u)
+      if (indeg[u] > (u == 0 ? 0u : 1u)) T.mesh = true;
+    if (T.mesh && world > 1) return e->fail(PS_E_STATE, "multi-GPU engines support tree topics only");
+    // local ids at every rank: rank of each position among its owner's nodes
+    loc.assign(N, 0);
+    {
+      std::vector<uint32_t> next(std::max(world, 1), 0);
+      for (uint32_t u = 0; u < N; ++u) loc[u] = next[owner[u]]++;
+    }
+    T.root_local = owner[0] == me;
+    T.level_internal.assign(T.depth + 1, 0);
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> cross;
+    uint32_t n_own = 0;
+    for (uint32_t u = 0; u < N; ++u) {
       const uint32_t p = order[u];
+      const uint32_t deg = rp[p + 1] - rp[p];
+      for (uint32_t k = rp[p]; k < rp[p + 1]; ++k) {
+        const uint32_t v = local[cl[k]];
+        if (owner[v] != owner[u]) cross[{level[u], static_cast<uint32_t>(owner[u]), static_cast<uint32_t>(owner[v])}]++;
+      }
+      if (owner[u] != me) continue;
+      ++n_own;
       e->node_peer.push_back(p);
       e->node_topic.push_back(static_cast<uint16_t>(t));
       for (uint32_t k = rp[p]; k < rp[p + 1]; ++k) {
-        const uint32_t lc = local[cl[k]];
-        e->col.push_back(T.nbase + lc);
-        indeg[lc]++;
+        const uint32_t v = local[cl[k]];
+        if (owner[v] == me) {
+          e->col.push_back(T.nbase + loc[v]);
+        } else {
+          const uint64_t id = base_at[static_cast<size_t>(t) * world + owner[v]] + loc[v];
+          if (id > kRemoteIdMask) return e->fail(PS_E_NOMEM, "rank node space exceeds 2^27");
+          e->col.push_back(kRemoteBit | (static_cast<uint32_t>(owner[v]) << kRemoteRankShift) |
+                           static_cast<uint32_t>(id));
+        }
       }
       e->row_ptr.push_back(static_cast<uint32_t>(e->col.size()));
+      if (deg) T.level_internal[level[u]]++;
+      if (u && owner[bfs_parent[u]] != me) e->remote_fed.push_back(T.nbase + loc[u]);
       if (e->col.size() >= 0xFFFFFFF0ull) return e->fail(PS_E_NOMEM, "edge space exceeds 2^32");
     }
-    for (uint32_t u = 0; u < order.size(); ++u)
-      if (indeg[u] > (u == 0 ? 0u : 1u)) T.mesh = true;
+    for (const auto& kv : cross)
+      T.cross.push_back({std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first), kv.second});
+    T.n_nodes = n_own;
     for (uint32_t p : order) local[p] = kNone;
-    n_total += order.size();
+    n_total += n_own;
+    if (n_total >= 0xFFFFFFF0ull) return e->fail(PS_E_NOMEM, "node space exceeds 2^32 nodes");
   }
   e->n_nodes = static_cast<uint32_t>(n_total);
   e->n_pad = ((e->n_nodes + 15) / 16) * 16;
@@ -269,10 +382,15 @@ void build_flags(ps_engine* e) {
     const uint32_t p = e->node_peer[u];
     uint8_t f = e->live[p] ? kNodeLive : 0;
     if (e->row_ptr[u + 1] > e->row_ptr[u]) f |= kNodeInternal;
+    for (uint32_t k = e->row_ptr[u]; k < e->row_ptr[u + 1]; ++k)
+      if (e->col[k] & kRemoteBit) {
+        f |= kNodeSplit;
+        break;
+      }
     e->node_flags[u] = f;
   }
   for (const auto& T : e->topics)
-    if (T.exists && T.n_nodes) e->node_flags[T.nbase] |= kNodeLive;  // roots always forward
+    if (T.exists && T.n_nodes && T.root_local) e->node_flags[T.nbase] |= kNodeLive;  // roots forward
 }
 
 int upload_graph(ps_engine* e) {
@@ -305,6 +423,12 @@ int upload_graph(ps_engine* e) {
     HIP_TRY(e->d_blk.ensure(n_blk), "alloc block flags");
     HIP_TRY(hipMemsetAsync(e->d_blk.p, 0, e->d_blk.bytes, e->stream), "clear block flags");
     HIP_TRY(e->d_gen.ensure(e->n_pad + 16), "alloc generations");
+    e->n_remote_fed = static_cast<uint32_t>(e->remote_fed.size());
+    HIP_TRY(e->d_remote_fed.ensure(std::max<size_t>(e->remote_fed.size(), 1) * 4), "alloc remote list");
+    if (!e->remote_fed.empty())
+      HIP_TRY(hipMemcpyAsync(e->d_remote_fed.p, e->remote_fed.data(), e->remote_fed.size() * 4,
+                             hipMemcpyHostToDevice, e->stream),
+              "upload remote list");
     HIP_TRY(hipMemsetAsync(e->d_gen.p, 0, e->d_gen.bytes, e->stream), "clear generations");
     e->gen_cur = 0;  // node ids changed: every row is stale
     HIP_TRY(e->d_frontier.ensure(std::max<size_t>(nn, 1) * 4), "alloc frontier");
@@ -328,23 +452,30 @@ int upload_graph(ps_engine* e) {
 
 // Propagates one window: per topic t, win[t] lists the messages (indices into
 // `msgs`) whose bits form t's block of W_t = ceil(|win[t]|/64) words.
-int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
-               const std::vector<std::vector<uint32_t>>& win, ps_stats* st) {
+int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<WinSlice>& win,
+               ps_stats* st) {
   int rc = upload_graph(e);
   if (rc) return rc;
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
+  const int32_t world = e->world, me = e->rank;
   std::vector<TopicDev> tab(std::max<uint32_t>(nt, 1));
   uint64_t wtot = 0;
   uint32_t max_depth = 0, max_start = 0;
+  bool need_direct = world > 1;
   for (uint32_t t = 0; t < nt; ++t) {
     const TopicHost& T = e->topics[t];
     TopicDev& d = tab[t];
     d = TopicDev{};
     d.nbase = T.nbase;
     d.n_nodes = T.n_nodes;
-    d.flags = T.mesh ? kTopicMesh : 0;
-    if (!T.exists || win[t].empty() || T.n_nodes == 0) continue;
-    d.W = ceil_div(win[t].size(), 64);
+    d.flags = (T.mesh ? kTopicMesh : 0u) | (T.root_local ? kTopicRootLocal : 0u);
+    if (!T.exists || win[t].n == 0) continue;
+    // every rank plans the same rounds: global depth, global start rounds
+    max_depth = std::max(max_depth, T.depth);
+    for (uint32_t li = 0; li < win[t].n; ++li)
+      max_start = std::max(max_start, msgs[win[t].idx[li]].start);
+    if (T.n_nodes == 0) continue;
+    d.W = ceil_div(win[t].n, 64);
     d.w_msgs = d.W;
     // rows of >= 64 words are padded to an even length so that every row
     // starts 16-B aligned (the expand kernel stores them as dwordx4)
@@ -352,10 +483,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
     wtot = (wtot + 15) & ~15ull;  // topic blocks start on a 128-B line
     d.wbase = wtot;
     wtot += static_cast<uint64_t>(T.n_nodes) * d.W;
-    max_depth = std::max(max_depth, T.depth);
-    for (uint32_t i : win[t]) max_start = std::max(max_start, msgs[i].start);
+    if (T.mesh || T.max_deg > 64 || d.W > kStageMaxWords) need_direct = true;
   }
-  if (wtot == 0) return PS_OK;
+  if (wtot == 0 && world == 1) return PS_OK;
   const bool record = (e->cfg.flags & PS_F_RECORD_HOPS) != 0;
   HIP_TRY(e->d_seen.ensure(wtot * 8), "alloc seen");
   HIP_TRY(e->d_arr0.ensure(wtot * 8), "alloc arrivals");
@@ -364,25 +494,29 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
   for (uint32_t t = 0; t < nt; ++t) any_mesh |= (tab[t].W && (tab[t].flags & kTopicMesh));
   if (record) HIP_TRY(e->d_hop.ensure(wtot * 64), "alloc hop record");
   const uint32_t n_waves = e->expand_grid * (kBlock / 64);
-  HIP_TRY(e->d_partials.ensure(static_cast<size_t>(n_waves) * kNumCtr * 8), "alloc partials");
+  // staged + direct kernel counters side by side
+  HIP_TRY(e->d_partials.ensure(static_cast<size_t>(2) * n_waves * kNumCtr * 8), "alloc partials");
   HIP_TRY(e->d_stats.ensure(static_cast<size_t>(kMaxRoundsCap + 1) * kNumCtr * 8), "alloc stats");
+  HIP_TRY(e->d_apply_stats.ensure(static_cast<size_t>(kMaxRoundsCap + 1) * kNumCtr * 8),
+          "alloc apply stats");
   HIP_TRY(e->d_topics.ensure(tab.size() * sizeof(TopicDev)), "alloc topics");
   HIP_TRY(e->d_nfront.ensure(4), "alloc n_front");
 
-  // root injections, grouped by round: mask[t][round][word]
+  // root injections (owned roots only), grouped by round: mask[t][round][word]
   std::vector<std::vector<uint64_t>> inj(nt);
   for (uint32_t t = 0; t < nt; ++t) {
     const TopicDev& d = tab[t];
-    if (d.W == 0) continue;
+    if (d.W == 0 || !(d.flags & kTopicRootLocal)) continue;
     inj[t].assign(static_cast<size_t>(max_start + 1) * d.W, 0);
-    for (uint32_t li = 0; li < win[t].size(); ++li)
-      inj[t][static_cast<size_t>(msgs[win[t][li]].start) * d.W + (li >> 6)] |= 1ull << (li & 63);
+    for (uint32_t li = 0; li < win[t].n; ++li)
+      inj[t][static_cast<size_t>(msgs[win[t].idx[li]].start) * d.W + (li >> 6)] |= 1ull << (li & 63);
   }
   std::vector<SeedDev> seeds;
   std::vector<uint32_t> seed_off(max_start + 2, 0);
   for (uint32_t r = 0; r <= max_start; ++r) {
     for (uint32_t t = 0; t < nt; ++t) {
       const TopicDev& d = tab[t];
+      if (inj[t].empty()) continue;
       for (uint32_t w = 0; w < d.W; ++w) {
         const uint64_t m = inj[t][static_cast<size_t>(r) * d.W + w];
         if (m) seeds.push_back(SeedDev{d.wbase + w, m, d.nbase, 0});  // root = node 0
@@ -392,20 +526,18 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
   }
   HIP_TRY(e->d_seeds.ensure(seeds.size() * sizeof(SeedDev)), "alloc seeds");
 
-  // Upper bound of the frontier expanded in round r (tree topics: a node at
-  // BFS level d receives a message started at round s in round s + d), used
-  // to size each round's grid; mesh topics (paths lengthen under the live
-  // mask) use the full grid.
-  bool any_mesh_active = false;
+  // Start rounds present per topic.  A node at BFS level d receives a
+  // message started at round s in round s + d and is expanded in round
+  // s + d + 1: that bounds each round's frontier (grid size) and, for the
+  // multi-GPU exchange, each round's cross-rank traffic exactly.
   std::vector<std::vector<uint8_t>> starts_of(nt);
   for (uint32_t t = 0; t < nt; ++t) {
-    if (tab[t].W == 0) continue;
-    if (e->topics[t].mesh) any_mesh_active = true;
+    if (win[t].n == 0 || !e->topics[t].exists) continue;
     starts_of[t].assign(max_start + 1, 0);
-    for (uint32_t i : win[t]) starts_of[t][msgs[i].start] = 1;
+    for (uint32_t li = 0; li < win[t].n; ++li) starts_of[t][msgs[win[t].idx[li]].start] = 1;
   }
   auto round_grid = [&](uint32_t r) -> uint32_t {
-    if (any_mesh_active) return e->expand_grid;
+    if (any_mesh) return e->expand_grid;
     uint64_t bound = 0;
     for (uint32_t t = 0; t < nt; ++t) {
       if (tab[t].W == 0) continue;
@@ -419,14 +551,43 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
     const uint64_t blocks = (bound + 3) / 4;  // ~1 entry per wave at least
     return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(e->expand_grid, blocks)));
   };
+  const uint32_t planned0 = max_depth + max_start + 1;
+  // cross-rank capacities (items = node words) per round: cap[r][from*world+to]
+  std::vector<std::vector<uint64_t>> cap;
+  uint64_t max_send = 0, max_recv = 0;
+  if (world > 1) {
+    cap.assign(planned0 + 1, std::vector<uint64_t>(static_cast<size_t>(world) * world, 0));
+    for (uint32_t t = 0; t < nt; ++t) {
+      const TopicHost& T = e->topics[t];
+      if (starts_of[t].empty()) continue;
+      const uint64_t Wt = ceil_div(win[t].n, 64) + ((ceil_div(win[t].n, 64) >= 64) ? (ceil_div(win[t].n, 64) & 1u) : 0u);
+      for (const auto& c : T.cross)
+        for (uint32_t s0 = 0; s0 <= max_start; ++s0) {
+          const uint32_t r = c.level + 1 + s0;
+          if (starts_of[t][s0] && r <= planned0) cap[r][c.from * world + c.to] += c.count * Wt;
+        }
+    }
+    for (uint32_t r = 1; r <= planned0; ++r) {
+      uint64_t sb = 0, rb = 0;
+      for (int32_t q = 0; q < world; ++q) {
+        if (cap[r][me * world + q]) sb += kRegionHeader + cap[r][me * world + q] * sizeof(XItem);
+        if (cap[r][q * world + me]) rb += kRegionHeader + cap[r][q * world + me] * sizeof(XItem);
+      }
+      max_send = std::max(max_send, sb);
+      max_recv = std::max(max_recv, rb);
+    }
+    HIP_TRY(e->d_send.ensure(max_send), "alloc send regions");
+    HIP_TRY(e->d_recv.ensure(max_recv), "alloc recv regions");
+  }
 
   hipStream_t s = e->stream;
   HIP_TRY(hipMemcpyAsync(e->d_topics.p, tab.data(), tab.size() * sizeof(TopicDev),
                          hipMemcpyHostToDevice, s),
           "upload topics");
-  HIP_TRY(hipMemcpyAsync(e->d_seeds.p, seeds.data(), seeds.size() * sizeof(SeedDev),
-                         hipMemcpyHostToDevice, s),
-          "upload seeds");
+  if (!seeds.empty())
+    HIP_TRY(hipMemcpyAsync(e->d_seeds.p, seeds.data(), seeds.size() * sizeof(SeedDev),
+                           hipMemcpyHostToDevice, s),
+            "upload seeds");
   HIP_TRY(hipEventRecord(e->ev_run0, s), "event");
   // new window generation: every tree row from older windows becomes stale
   if (++e->gen_cur > 255) {
@@ -437,6 +598,12 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
                              e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>(),
                              e->d_gen.as<uint8_t>(), e->gen_cur, any_mesh, s),
           "window init");
+  if (e->n_remote_fed)
+    HIP_TRY(launch_init_nodes(e->d_remote_fed.as<uint32_t>(), e->n_remote_fed,
+                              e->d_node_topic.as<uint16_t>(), e->d_topics.as<TopicDev>(),
+                              e->d_seen.as<uint64_t>(), e->d_arr0.as<uint64_t>(),
+                              e->d_arr1.as<uint64_t>(), e->d_gen.as<uint8_t>(), e->gen_cur, s),
+            "init remote-fed rows");
   if (e->cfg.flags & PS_F_NO_LAZY_SEEN) {
     // eager variant: clear every row and mark every node current, so the
     // expand kernel reads each child's seen word before it tests and sets it
@@ -445,6 +612,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
             "stamp generations");
   }
   if (record) HIP_TRY(hipMemsetAsync(e->d_hop.p, 0xFF, wtot * 64, s), "clear hop record");
+  if (world > 1)
+    HIP_TRY(hipMemsetAsync(e->d_apply_stats.p, 0, static_cast<size_t>(planned0 + 1) * kNumCtr * 8, s),
+            "clear apply stats");
 
   ExpandArgs a{};
   a.frontier = e->d_frontier.as<uint32_t>();
@@ -461,8 +631,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
   a.blk_flag = e->d_blk.as<uint8_t>();
   a.dbg = 0;
   if (const char* v = std::getenv("PSAMD_DEBUG_EXPAND")) a.dbg = static_cast<uint32_t>(std::atoi(v));
-  a.partials = e->d_partials.as<uint64_t>();
   a.hop_rec = record ? e->d_hop.as<uint8_t>() : nullptr;
+  a.send = e->d_send.as<uint8_t>();
+  uint64_t* const partials = e->d_partials.as<uint64_t>();
   uint64_t* arr[2] = {e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>()};
   uint64_t* stats = e->d_stats.as<uint64_t>();
   const bool timed = (e->cfg.flags & PS_F_TIME_KERNELS) != 0;
@@ -474,16 +645,35 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
   };
   auto compact = [&](uint32_t r, uint32_t waves_r) -> hipError_t {
     hipError_t x = launch_flag_count(a.next_flag, a.blk_flag, e->n_pad,
-                                     e->d_wgcount.as<uint32_t>(), a.partials, waves_r,
+                                     e->d_wgcount.as<uint32_t>(), partials, waves_r,
                                      r ? stats + r * kNumCtr : nullptr, s);
     if (x != hipSuccess) return x;
     return launch_flag_compact(a.next_flag, a.blk_flag, e->n_pad, e->d_wgcount.as<uint32_t>(),
                                e->d_frontier.as<uint32_t>(), e->d_nfront.as<uint32_t>(), s);
   };
+  // multi-GPU round r: region layout, header reset, exchange, apply
+  std::vector<uint64_t> s_off(world, 0), s_len(world, 0), r_off(world, 0), r_len(world, 0);
+  auto layout = [&](uint32_t r) -> bool {
+    if (world <= 1 || r > planned0) return false;
+    uint64_t so = 0, ro = 0;
+    bool any = false;
+    for (int32_t q = 0; q < world; ++q) {
+      const uint64_t cs = cap[r][me * world + q], cr = cap[r][q * world + me];
+      s_off[q] = so;
+      s_len[q] = cs ? kRegionHeader + cs * sizeof(XItem) : 0;
+      so += s_len[q];
+      r_off[q] = ro;
+      r_len[q] = cr ? kRegionHeader + cr * sizeof(XItem) : 0;
+      ro += r_len[q];
+      for (int32_t z = 0; z < world; ++z) any |= cap[r][q * world + z] != 0;
+    }
+    for (int32_t q = 0; q < world && q < kMaxRanks; ++q) a.send_off[q] = s_off[q];
+    return any;  // the same verdict on every rank
+  };
 
   HIP_TRY(seed_round(0, arr[0]), "seed");
   HIP_TRY(compact(0, 0), "compact");
-  uint32_t planned = max_depth + max_start + 1;
+  uint32_t planned = planned0;
   uint32_t r = 0;
   size_t ev_used = 0;
   while (true) {
@@ -491,6 +681,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
       ++r;
       a.a_cur = arr[(r - 1) & 1];
       a.a_next = arr[r & 1];
+      const bool xr = layout(r);
+      if (xr)
+        for (int32_t q = 0; q < world; ++q)
+          if (s_len[q]) HIP_TRY(hipMemsetAsync(a.send + s_off[q], 0, kRegionHeader, s), "reset header");
       if (timed) {
         if (ev_used + 2 > e->ev_k.size()) {
           hipEvent_t x, y;
@@ -501,12 +695,43 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
         }
         HIP_TRY(hipEventRecord(e->ev_k[ev_used], s), "event");
       }
-      const uint32_t grid_r = r <= planned ? round_grid(r) : e->expand_grid;
+      const uint32_t grid_r = r <= planned0 ? round_grid(r) : e->expand_grid;
+      a.partials = partials;
       HIP_TRY(launch_expand(a, r, record, grid_r, s), "expand");
+      uint32_t waves_r = grid_r * (kBlock / 64);
+      if (need_direct) {
+        a.partials = partials + static_cast<size_t>(waves_r) * kNumCtr;
+        HIP_TRY(launch_expand_direct(a, r, record, e->expand_grid, s), "expand direct");
+        waves_r += n_waves;
+      }
       if (timed) HIP_TRY(hipEventRecord(e->ev_k[ev_used + 1], s), "event");
       if (timed) ev_used += 2;
+      if (xr) {
+        std::string xerr;
+        hipError_t xe = e->transport->exchange(a.send, s_off, s_len, e->d_recv.as<uint8_t>(), r_off,
+                                               r_len, s, &xerr);
+        if (xe != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
+        ApplyArgs ap{};
+        ap.recv = e->d_recv.as<uint8_t>();
+        ap.world = static_cast<uint32_t>(world);
+        ap.cap_pre[0] = 0;
+        for (int32_t q = 0; q < world; ++q) {
+          ap.recv_off[q] = r_off[q];
+          ap.cap_pre[q + 1] = ap.cap_pre[q] + cap[r][q * world + me];
+        }
+        ap.node_topic = a.node_topic;
+        ap.node_flags = a.node_flags;
+        ap.topics = a.topics;
+        ap.seen = a.seen;
+        ap.a_next = a.a_next;
+        ap.next_flag = a.next_flag;
+        ap.blk_flag = a.blk_flag;
+        ap.hop_rec = a.hop_rec;
+        ap.stats = e->d_apply_stats.as<uint64_t>() + static_cast<size_t>(r) * kNumCtr;
+        HIP_TRY(launch_apply(ap, r, record, s), "apply");
+      }
       HIP_TRY(seed_round(r, a.a_next), "seed");
-      HIP_TRY(compact(r, grid_r * (kBlock / 64)), "compact");
+      HIP_TRY(compact(r, waves_r), "compact");
     }
     uint32_t left = 0;
     HIP_TRY(hipMemcpyAsync(&left, e->d_nfront.p, 4, hipMemcpyDeviceToHost, s), "read frontier");
@@ -515,6 +740,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
       if (left) return e->fail(PS_E_STATE, "propagation did not converge");
       break;
     }
+    if (world > 1) return e->fail(PS_E_STATE, "multi-GPU frontier outlived the planned rounds");
     planned = r + 8;  // live mask lengthened a mesh path beyond the BFS depth
   }
   HIP_TRY(hipEventRecord(e->ev_run1, s), "event");
@@ -529,13 +755,20 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
     const size_t q = i / 2 + 1;  // round of this launch
     if (q < PS_MAX_ROUNDS) st->expand_ms_per_round[q] += k;
   }
-  std::vector<uint64_t> hs(static_cast<size_t>(r + 1) * kNumCtr);
+  std::vector<uint64_t> hs(static_cast<size_t>(r + 1) * kNumCtr), ha;
   HIP_TRY(hipMemcpyAsync(hs.data(), stats, hs.size() * 8, hipMemcpyDeviceToHost, s), "read stats");
+  if (world > 1) {
+    ha.resize(static_cast<size_t>(planned0 + 1) * kNumCtr);
+    HIP_TRY(hipMemcpyAsync(ha.data(), e->d_apply_stats.p, ha.size() * 8, hipMemcpyDeviceToHost, s),
+            "read apply stats");
+  }
   HIP_TRY(hipStreamSynchronize(s), "sync");
   for (uint32_t q = 1; q <= r; ++q) {
     const uint64_t* c = &hs[static_cast<size_t>(q) * kNumCtr];
-    st->deliveries += c[kCtrDeliveries];
-    st->duplicates += c[kCtrDuplicates];
+    const uint64_t app_d = (world > 1 && q <= planned0) ? ha[static_cast<size_t>(q) * kNumCtr + kCtrDeliveries] : 0;
+    const uint64_t app_u = (world > 1 && q <= planned0) ? ha[static_cast<size_t>(q) * kNumCtr + kCtrDuplicates] : 0;
+    st->deliveries += c[kCtrDeliveries] + app_d;
+    st->duplicates += c[kCtrDuplicates] + app_u;
     st->frontier_entries += c[kCtrEntries];
     st->child_visits += c[kCtrChildren];
     st->edge_words += c[kCtrSeenWrites];
@@ -548,7 +781,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
                         c[kCtrChildren] * 3 + c[kCtrMeshChildren] * 4 + c[kCtrSeenReads] * 8 +
                         c[kCtrSeenWrites] * 8 + c[kCtrArrivalWrites] * 8;
     if (q < PS_MAX_ROUNDS) {
-      st->deliveries_per_round[q] += c[kCtrDeliveries];
+      st->deliveries_per_round[q] += c[kCtrDeliveries] + app_d;
       st->frontier_per_round[q] += static_cast<uint32_t>(c[kCtrEntries]);
     }
   }
@@ -558,14 +791,16 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
 
   if (record) {
     std::vector<uint8_t> hr(wtot * 64);
-    HIP_TRY(hipMemcpyAsync(hr.data(), e->d_hop.p, hr.size(), hipMemcpyDeviceToHost, s), "read hops");
-    HIP_TRY(hipStreamSynchronize(s), "sync");
+    if (!hr.empty()) {
+      HIP_TRY(hipMemcpyAsync(hr.data(), e->d_hop.p, hr.size(), hipMemcpyDeviceToHost, s), "read hops");
+      HIP_TRY(hipStreamSynchronize(s), "sync");
+    }
     const uint32_t np = e->cfg.n_peers;
     for (uint32_t t = 0; t < nt; ++t) {
       const TopicDev& d = tab[t];
       if (d.W == 0) continue;
-      for (uint32_t li = 0; li < win[t].size(); ++li) {
-        const uint32_t mi = win[t][li];
+      for (uint32_t li = 0; li < win[t].n; ++li) {
+        const uint32_t mi = win[t].idx[li];
         const uint32_t s0 = msgs[mi].start;
         uint8_t* row = e->hops.data() + static_cast<size_t>(mi) * np;
         for (uint32_t u = 0; u < d.n_nodes; ++u) {
@@ -577,28 +812,28 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs,
   }
   // remember the last window for ps_read_delivered / ps_seen_digest
   e->last_topics = tab;
-  std::fill(e->last_win_local.begin(), e->last_win_local.end(), -1);
-  for (uint32_t t = 0; t < nt; ++t)
-    for (uint32_t li = 0; li < win[t].size(); ++li) e->last_win_local[win[t][li]] = static_cast<int32_t>(li);
+  for (uint32_t t = 0; t < nt; ++t) {
+    e->last_cnt[t] = tab[t].W ? win[t].n : 0;
+    e->last_lo[t] = win[t].n ? e->run_rank[win[t].idx[0]] : 0;
+  }
   e->have_window = true;
   return PS_OK;
 }
 
-// Messages of one phase, split into windows of at most msg_window per topic.
-int run_phase(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<uint32_t>& idx,
+// Messages of one phase (per topic, a slice of the run's topic-sorted index
+// array), split into windows of at most msg_window messages per topic.
+int run_phase(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<WinSlice>& per,
               ps_stats* st) {
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
-  std::vector<std::vector<uint32_t>> per(nt);
-  for (uint32_t i : idx) per[msgs[i].topic].push_back(i);
   const uint32_t cap = e->cfg.msg_window;
-  size_t n_win = 0;
-  for (const auto& v : per) n_win = std::max(n_win, (v.size() + cap - 1) / cap);
-  std::vector<std::vector<uint32_t>> win(nt);
-  for (size_t k = 0; k < n_win; ++k) {
+  uint32_t n_win = 0;
+  for (const auto& v : per) n_win = std::max(n_win, (v.n + cap - 1) / cap);
+  std::vector<WinSlice> win(nt);
+  for (uint32_t k = 0; k < n_win; ++k) {
     for (uint32_t t = 0; t < nt; ++t) {
-      win[t].clear();
-      const size_t lo = k * cap, hi = std::min(per[t].size(), lo + cap);
-      for (size_t q = lo; q < hi; ++q) win[t].push_back(per[t][q]);
+      const uint32_t lo = k * cap;
+      win[t].idx = per[t].idx + std::min(lo, per[t].n);
+      win[t].n = lo < per[t].n ? std::min(cap, per[t].n - lo) : 0;
     }
     int rc = run_window(e, msgs, win, st);
     if (rc) return rc;
@@ -864,13 +1099,12 @@ int ps_run(ps_engine* e, ps_stats* out) {
   const auto t_host0 = std::chrono::steady_clock::now();
   ps_stats st{};
   if (hipSetDevice(e->cfg.device) != hipSuccess) return e->fail(PS_E_DEVICE, "hipSetDevice");
-  std::vector<RunMsg> msgs;
-  msgs.swap(e->pending);
+  e->last_msgs.clear();
+  e->last_msgs.swap(e->pending);
+  const std::vector<RunMsg>& msgs = e->last_msgs;
   const uint32_t nmsg = static_cast<uint32_t>(msgs.size());
   e->last_first = e->next_msg - nmsg;
   e->last_n = nmsg;
-  e->last_msgs = msgs;
-  e->last_win_local.assign(nmsg, -1);
   e->have_hops = false;
   e->have_window = false;
   const bool record = (e->cfg.flags & PS_F_RECORD_HOPS) != 0;
@@ -880,43 +1114,71 @@ int ps_run(ps_engine* e, ps_stats* out) {
     e->hops.assign(bytes, PS_HOP_NONE);
   }
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
-  std::vector<std::vector<uint32_t>> queue(nt);
-  for (uint32_t i = 0; i < nmsg; ++i) queue[msgs[i].topic].push_back(i);
-  std::vector<size_t> head(nt, 0);
+  // one counting sort: message indices grouped by topic, publish order kept
+  auto& off = e->run_topic_off;
+  off.assign(nt + 1, 0);
+  for (uint32_t i = 0; i < nmsg; ++i) off[msgs[i].topic + 1]++;
+  for (uint32_t t = 0; t < nt; ++t) off[t + 1] += off[t];
+  e->run_sorted.resize(nmsg);
+  e->run_rank.resize(nmsg);
+  {
+    std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+    for (uint32_t i = 0; i < nmsg; ++i) {
+      const uint32_t t = msgs[i].topic;
+      e->run_rank[i] = fill[t] - off[t];
+      e->run_sorted[fill[t]++] = i;
+    }
+  }
+  e->last_lo.assign(nt, 0);
+  e->last_cnt.assign(nt, 0);
+  std::vector<uint32_t> head(nt, 0);
+  auto slice = [&](uint32_t t, uint32_t from, uint32_t n) {
+    WinSlice w;
+    w.idx = e->run_sorted.data() + off[t] + from;
+    w.n = n;
+    return w;
+  };
   // Abruptly dropped hosts: the first message through the failed edge is lost
   // below it, then the parent repairs (subtree.go:333-351): that message runs
   // on its own over the current tree, the rest over the repaired one.
   while (true) {
-    std::vector<uint32_t> solo;
+    std::vector<WinSlice> solo(nt);
+    bool any = false;
     for (uint32_t t = 0; t < nt; ++t) {
       TopicHost& T = e->topics[t];
-      if (T.exists && T.kind == Kind::Join && T.tree.has_pending_failures() &&
-          head[t] < queue[t].size())
-        solo.push_back(queue[t][head[t]++]);
+      const uint32_t cnt = off[t + 1] - off[t];
+      if (T.exists && T.kind == Kind::Join && T.tree.has_pending_failures() && head[t] < cnt) {
+        solo[t] = slice(t, head[t], 1);
+        head[t]++;
+        any = true;
+      }
     }
-    if (solo.empty()) break;
+    if (!any) break;
     int rc = run_phase(e, msgs, solo, &st);
     if (rc) return rc;
-    for (uint32_t i : solo) {
-      e->topics[msgs[i].topic].tree.after_message();
-      e->graph_dirty = true;
-    }
+    for (uint32_t t = 0; t < nt; ++t)
+      if (solo[t].n) {
+        e->topics[t].tree.after_message();
+        e->graph_dirty = true;
+      }
   }
-  std::vector<uint32_t> rest;
-  rest.reserve(nmsg);
   {
-    std::vector<size_t> seen_in_topic(nt, 0);  // publish order, minus the solo'd heads
-    for (uint32_t i = 0; i < nmsg; ++i)
-      if (seen_in_topic[msgs[i].topic]++ >= head[msgs[i].topic]) rest.push_back(i);
-  }
-  if (!rest.empty()) {
-    int rc = run_phase(e, msgs, rest, &st);
-    if (rc) return rc;
+    std::vector<WinSlice> rest(nt);
+    bool any = false;
+    for (uint32_t t = 0; t < nt; ++t) {
+      const uint32_t cnt = off[t + 1] - off[t];
+      rest[t] = slice(t, head[t], cnt - head[t]);
+      any |= rest[t].n > 0;
+    }
+    if (any) {
+      int rc = run_phase(e, msgs, rest, &st);
+      if (rc) return rc;
+    }
   }
   // lazy prune of Part'ed children at every forwarding node (subtree.go:326-331)
   for (uint32_t t = 0; t < nt; ++t) {
     TopicHost& T = e->topics[t];
-    if (T.exists && T.kind == Kind::Join && head[t] < queue[t].size() &&
+    if (T.exists && T.kind == Kind::Join && head[t] < off[t + 1] - off[t] &&
         T.tree.needs_message_pass()) {
       T.tree.after_message();
       e->graph_dirty = true;
@@ -944,9 +1206,11 @@ int ps_read_delivered(ps_engine* e, uint32_t msg, uint8_t* out) {
   if (msg < e->last_first || msg >= e->last_first + e->last_n)
     return e->fail(PS_E_RANGE, "message not in the last run");
   const uint32_t i = msg - e->last_first;
-  const int32_t li = e->last_win_local[i];
-  if (li < 0) return e->fail(PS_E_NOTREADY, "message not in the last window");
   const uint32_t t = e->last_msgs[i].topic;
+  const uint32_t rank = e->run_rank[i];
+  if (rank < e->last_lo[t] || rank >= e->last_lo[t] + e->last_cnt[t])
+    return e->fail(PS_E_NOTREADY, "message not in the last window");
+  const uint32_t li = rank - e->last_lo[t];
   const TopicDev& d = e->last_topics[t];
   std::memset(out, 0, e->cfg.n_peers);
   std::vector<uint64_t> col(d.n_nodes);
@@ -978,6 +1242,104 @@ int ps_seen_digest(ps_engine* e, uint64_t* digest_out) {
   HIP_TRY(hipMemcpyAsync(digest_out, e->d_digest.p, 8, hipMemcpyDeviceToHost, e->stream),
           "read digest");
   HIP_TRY(hipStreamSynchronize(e->stream), "sync");
+  return PS_OK;
+}
+
+int ps_dist_unique_id(uint8_t id_out[PS_UNIQUE_ID_BYTES]) {
+  if (!id_out) return PS_E_INVAL;
+  return rccl_unique_id(id_out) == 0 ? PS_OK : PS_E_DEVICE;
+}
+
+static int dist_common(ps_engine* e, const ps_dist_config* dc) {
+  if (!e || !dc) return PS_E_INVAL;
+  if (dc->world < 1 || dc->world > kMaxRanks || dc->rank < 0 || dc->rank >= dc->world)
+    return e->fail(PS_E_INVAL, "rank/world out of range (world <= 16)");
+  if (dc->partition != PS_PART_PEER && dc->partition != PS_PART_SUBTREE)
+    return e->fail(PS_E_INVAL, "unknown partition");
+  if (!e->pending.empty()) return e->fail(PS_E_STATE, "messages pending");
+  e->rank = dc->rank;
+  e->world = dc->world;
+  e->partition = dc->partition;
+  e->split_depth = dc->split_depth;
+  e->graph_dirty = true;
+  return PS_OK;
+}
+
+int ps_dist_init(ps_engine* e, const ps_dist_config* dc, const uint8_t id[PS_UNIQUE_ID_BYTES]) {
+  if (!id) return PS_E_INVAL;
+  int rc = dist_common(e, dc);
+  if (rc) return rc;
+  if (dc->world == 1) return PS_OK;
+  if (hipSetDevice(e->cfg.device) != hipSuccess) return e->fail(PS_E_DEVICE, "hipSetDevice");
+  std::string err;
+  e->transport = make_rccl_transport(dc->rank, dc->world, id, &err);
+  if (!e->transport) return e->fail(PS_E_DEVICE, err);
+  return PS_OK;
+}
+
+struct ps_loopback {
+  psamd::LoopbackGroup* g;
+};
+
+int ps_loopback_create(int32_t world, ps_loopback** out) {
+  if (!out || world < 1 || world > kMaxRanks) return PS_E_INVAL;
+  auto* lb = new (std::nothrow) ps_loopback{loopback_create(world)};
+  if (!lb || !lb->g) {
+    delete lb;
+    return PS_E_NOMEM;
+  }
+  *out = lb;
+  return PS_OK;
+}
+
+void ps_loopback_destroy(ps_loopback* lb) {
+  if (!lb) return;
+  loopback_destroy(lb->g);
+  delete lb;
+}
+
+int ps_dist_init_loopback(ps_engine* e, const ps_dist_config* dc, ps_loopback* lb) {
+  if (!lb) return PS_E_INVAL;
+  int rc = dist_common(e, dc);
+  if (rc) return rc;
+  if (dc->world == 1) return PS_OK;
+  e->transport = make_loopback_transport(lb->g, dc->rank, e->cfg.device);
+  if (!e->transport) return e->fail(PS_E_INVAL, "loopback group size != world");
+  return PS_OK;
+}
+
+int ps_partition_owner(uint32_t n_peers, uint32_t root, const uint32_t* parent, uint32_t topic,
+                       const ps_dist_config* dc, int32_t* owner_out) {
+  if (!parent || !dc || !owner_out || root >= n_peers) return PS_E_INVAL;
+  if (dc->world < 1 || dc->world > kMaxRanks) return PS_E_INVAL;
+  // children lists, then the same BFS the engine uses
+  std::vector<uint32_t> rp(n_peers + 1, 0), cl;
+  for (uint32_t c = 0; c < n_peers; ++c)
+    if (parent[c] != PS_NONE && c != root) {
+      if (parent[c] >= n_peers) return PS_E_INVAL;
+      rp[parent[c] + 1]++;
+    }
+  for (uint32_t i = 0; i < n_peers; ++i) rp[i + 1] += rp[i];
+  cl.assign(rp[n_peers], 0);
+  {
+    std::vector<uint32_t> fill(rp.begin(), rp.end() - 1);
+    for (uint32_t c = 0; c < n_peers; ++c)
+      if (parent[c] != PS_NONE && c != root) cl[fill[parent[c]]++] = c;
+  }
+  std::vector<uint32_t> order{root}, bfs_parent{kNone}, level{0}, local(n_peers, kNone);
+  local[root] = 0;
+  for (size_t qi = 0; qi < order.size(); ++qi)
+    for (uint32_t k = rp[order[qi]]; k < rp[order[qi] + 1]; ++k)
+      if (local[cl[k]] == kNone) {
+        local[cl[k]] = static_cast<uint32_t>(order.size());
+        order.push_back(cl[k]);
+        bfs_parent.push_back(static_cast<uint32_t>(qi));
+        level.push_back(level[qi] + 1);
+      }
+  std::vector<int32_t> owner;
+  partition_topic(order, bfs_parent, level, topic, dc->world, dc->partition, dc->split_depth, owner);
+  for (uint32_t p = 0; p < n_peers; ++p) owner_out[p] = -1;
+  for (size_t u = 0; u < order.size(); ++u) owner_out[order[u]] = owner[u];
   return PS_OK;
 }
 

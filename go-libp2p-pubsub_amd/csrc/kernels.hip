@@ -11,6 +11,8 @@
 // restricted to live (subscribed) children; seen[c] |= new; arrival'[c] = new.
 // Reference: subtree.forwardMessage (subtree.go:319-354) and
 // client.processMessages (client.go:100-132).  Design: DESIGN.md §5.
+#include <algorithm>
+
 #include "kernels.hpp"
 
 namespace psamd {
@@ -87,14 +89,42 @@ __global__ __launch_bounds__(kBlock) void k_window_init(const TopicDev* __restri
   if (T.W == 0 || T.n_nodes == 0) return;
   const bool mesh = (T.flags & kTopicMesh) != 0;
   const uint64_t n_words = mesh ? static_cast<uint64_t>(T.n_nodes) * T.W : T.W;
-  if (!mesh && blockIdx.x != 0) return;
+  if (!mesh && (blockIdx.x != 0 || !(T.flags & kTopicRootLocal))) return;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n_words;
        i += static_cast<uint64_t>(gridDim.x) * kBlock) {
     seen[T.wbase + i] = 0;
     a0[T.wbase + i] = 0;
     a1[T.wbase + i] = 0;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) gen[T.nbase] = static_cast<uint8_t>(gen_cur);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && (T.flags & kTopicRootLocal))
+    gen[T.nbase] = static_cast<uint8_t>(gen_cur);
+}
+
+// Nodes fed by a parent on another rank: rows zeroed, generation current, so
+// the apply kernel can test-and-set them with atomics.
+__global__ __launch_bounds__(kBlock) void k_init_nodes(const uint32_t* __restrict__ nodes,
+                                                       uint32_t n,
+                                                       const uint16_t* __restrict__ node_topic,
+                                                       const TopicDev* __restrict__ topics,
+                                                       uint64_t* __restrict__ seen,
+                                                       uint64_t* __restrict__ a0,
+                                                       uint64_t* __restrict__ a1,
+                                                       uint8_t* __restrict__ gen, uint32_t gen_cur) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
+  const uint32_t n_waves = (gridDim.x * kBlock) >> 6;
+  for (uint32_t i = wave; i < n; i += n_waves) {
+    const uint32_t u = nodes[i];
+    const TopicDev T = topics[node_topic[u]];
+    if (T.W == 0) continue;
+    const uint64_t row = T.wbase + static_cast<uint64_t>(u - T.nbase) * T.W;
+    for (uint32_t w = lane; w < T.W; w += 64) {
+      seen[row + w] = 0;
+      a0[row + w] = 0;
+      a1[row + w] = 0;
+    }
+    if (lane == 0) gen[u] = static_cast<uint8_t>(gen_cur);
+  }
 }
 
 // ---------------------------------------------------------------- seeds ---
@@ -263,6 +293,8 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
                               uint64_t wbase, uint32_t lane, uint32_t cur, uint32_t round,
                               ExpandCtr& k, EntryCtr& ec) {
   const bool mesh = (tflags & kTopicMesh) != 0;
+  const bool split = (tflags & kEntrySplit) != 0;  // some children live on other ranks
+  const bool listed = mesh || split;
   const uint64_t pw = wbase + static_cast<uint64_t>(p - nbase) * W;
   const uint64_t cbase = wbase - static_cast<uint64_t>(nbase) * W;
   ec.ent += 1;
@@ -273,9 +305,32 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
     const uint32_t cd = min(64u, deg - j0);
     uint32_t cj = 0, fj = 0, gj = 0;
     if (lane < cd) {
-      cj = mesh ? a.col[rs + j0 + lane] : c0 + j0 + lane;
-      fj = a.node_flags[cj];
-      gj = mesh ? 0u : a.gen[cj];
+      cj = listed ? a.col[rs + j0 + lane] : c0 + j0 + lane;
+      if (!(cj & kRemoteBit)) {  // a remote child is not live here: routed below
+        fj = a.node_flags[cj];
+        gj = mesh ? 0u : a.gen[cj];
+      }
+    }
+    if (split) {
+      // children owned by other ranks: the whole arrival row goes into the
+      // owner's send region (one reservation per child)
+      for (uint32_t jj = 0; jj < cd; ++jj) {
+        const uint32_t c = rl(cj, jj);
+        if (!(c & kRemoteBit)) continue;
+        const uint32_t dest = (c >> kRemoteRankShift) & 0xFu;
+        uint8_t* region = a.send + a.send_off[dest];
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(reinterpret_cast<uint32_t*>(region), W);
+        base = static_cast<uint32_t>(__shfl(static_cast<int>(base), 0, 64));
+        XItem* out = reinterpret_cast<XItem*>(region + kRegionHeader) + base;
+        for (uint32_t w = lane; w < W; w += 64) {
+          XItem it;
+          it.node = c & kRemoteIdMask;
+          it.word = w;
+          it.mask = a.a_cur[pw + w];
+          out[w] = it;
+        }
+      }
     }
     if (W >= 64) {
       for (uint32_t wb = 0; wb < W; wb += 64) {
@@ -320,7 +375,7 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
     if (!mesh && lane < cd && (fj & kNodeLive) && !(a.dbg & kDbgNoByteStores))
       a.gen[cj] = static_cast<uint8_t>(cur);
   }
-  if (mesh || p == nbase) {
+  if (mesh || (p == nbase && (tflags & kTopicRootLocal))) {
     // consume-and-clear: mesh rows are OR-accumulated, root rows are seeded
     for (uint32_t w = lane; w < W; w += 64) a.a_cur[pw + w] = 0;
     ec.clear += W;
@@ -337,13 +392,16 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
 //   phase B  stores only: W >= 64 child-outer / word-block-inner (512-B
 //            contiguous bursts, child wave-uniform), W < 64 Wp-lane groups.
 // The waves therefore wait once per sub-batch, not once per word block.
-template <bool kRecord>
+// kDirect = false: the staged path only (entries that need the direct path
+// are left to the second instance); kDirect = true: the direct path only.
+// Separate instances keep the hot staged kernel's register budget small.
+template <bool kRecord, bool kDirect>
 __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round) {
-  __shared__ WaveStage stage_lds[kBlock / 64];
+  __shared__ WaveStage stage_lds[kDirect ? 1 : kBlock / 64];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave =
       __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) >> 6);
-  WaveStage& ws = stage_lds[__builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
+  WaveStage& ws = stage_lds[kDirect ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6)];
   const uint32_t n_waves = (gridDim.x * kBlock) >> 6;
   const uint32_t n = *a.n_front;
   const uint32_t cur = a.gen_cur & 0xFF;
@@ -362,7 +420,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
       const TopicDev T = a.topics[t];
       bW = T.W;
       bnb = T.nbase;
-      bfl = T.flags;
+      bfl = T.flags | ((a.node_flags[bp] & kNodeSplit) ? kEntrySplit : 0u);
       bwl = static_cast<uint32_t>(T.wbase);
       bwh = static_cast<uint32_t>(T.wbase >> 32);
       if (bdeg && T.W) bc0 = a.col[brs];
@@ -375,10 +433,12 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
         ++q;
         continue;
       }
-      if ((f0 & kTopicMesh) || W0 > kStageWords || d0 > 64) {
-        expand_direct<kRecord>(a, rl(bp, q), rl(brs, q), d0, rl(bc0, q), W0, rl(bnb, q), f0,
-                               (static_cast<uint64_t>(rl(bwh, q)) << 32) | rl(bwl, q), lane, cur,
-                               round, k, ec);
+      const bool direct = (f0 & (kTopicMesh | kEntrySplit)) || W0 > kStageWords || d0 > 64;
+      if (direct || kDirect) {
+        if (direct && kDirect)
+          expand_direct<kRecord>(a, rl(bp, q), rl(brs, q), d0, rl(bc0, q), W0, rl(bnb, q), f0,
+                                 (static_cast<uint64_t>(rl(bwh, q)) << 32) | rl(bwl, q), lane,
+                                 cur, round, k, ec);
         ++q;
         continue;
       }
@@ -390,7 +450,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
         const uint32_t Wn = rl(bW, q + nq), dn = rl(bdeg, q + nq), fn = rl(bfl, q + nq);
         const uint32_t cn = rl(bc0, q + nq);
         const uint32_t bn = 4u * (((cn + dn + 3u) >> 2) - (cn >> 2));
-        if ((fn & kTopicMesh) || Wn > kStageWords || dn > 64) break;
+        if ((fn & (kTopicMesh | kEntrySplit)) || Wn > kStageWords || dn > 64) break;
         if (sw + Wn + (Wn & 1u) > kStageWords || sd + bn > kStageBytes) break;
         sw += Wn + (Wn & 1u);
         sd += bn;
@@ -501,7 +561,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
           // live children hold current rows now
           if (lane < deg && (ws.flags[fo + lane] & kNodeLive) && !(a.dbg & kDbgNoByteStores))
             a.gen[c0 + lane] = static_cast<uint8_t>(cur);
-          if (p == nbase) {  // root rows are seeded with |=: consume-and-clear
+          if (p == nbase && (rl(bfl, i) & kTopicRootLocal)) {  // seeded with |=: consume-and-clear
             const uint64_t pw = wbase + static_cast<uint64_t>(p - nbase) * W;
             for (uint32_t w = lane; w < W; w += 64) a.a_cur[pw + w] = 0;
             ec.clear += W;
@@ -531,6 +591,62 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
     out[kCtrSeenWrites] = s_sw;
     out[kCtrArrivalWrites] = s_aw;
     out[kCtrClearWords] = ec.clear;
+  }
+}
+
+// ----------------------------------------------------------------- apply ---
+// Deliveries received from other ranks: test-and-set into the owned node's
+// row (atomic: its row was zeroed at window init), arrival row written whole
+// (the sender ships every word of the parent's arrival row).
+template <bool kRecord>
+__global__ __launch_bounds__(kBlock) void k_apply(ApplyArgs a, uint32_t round) {
+  const uint64_t total = a.cap_pre[a.world];
+  uint64_t deliv = 0, dup = 0;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < total;
+       i += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    uint32_t src = 0;
+    while (i >= a.cap_pre[src + 1]) ++src;
+    const uint8_t* region = a.recv + a.recv_off[src];
+    const uint64_t k = i - a.cap_pre[src];
+    if (k >= *reinterpret_cast<const uint32_t*>(region)) continue;
+    const XItem it = reinterpret_cast<const XItem*>(region + kRegionHeader)[k];
+    const uint8_t f = a.node_flags[it.node];
+    if (!(f & kNodeLive) || it.mask == 0) {
+      if ((f & kNodeLive) && (f & kNodeInternal)) {
+        const TopicDev T = a.topics[a.node_topic[it.node]];
+        a.a_next[T.wbase + static_cast<uint64_t>(it.node - T.nbase) * T.W + it.word] = 0;
+      }
+      continue;
+    }
+    const TopicDev T = a.topics[a.node_topic[it.node]];
+    const uint64_t cw = T.wbase + static_cast<uint64_t>(it.node - T.nbase) * T.W + it.word;
+    const uint64_t old = atomicOr(reinterpret_cast<unsigned long long*>(a.seen + cw),
+                                  static_cast<unsigned long long>(it.mask));
+    const uint64_t nm = it.mask & ~old;
+    if (f & kNodeInternal) a.a_next[cw] = nm;
+    dup += __popcll(it.mask & old);
+    if (nm) {
+      deliv += __popcll(nm);
+      if (f & kNodeInternal) {
+        a.next_flag[it.node] = 1;
+        a.blk_flag[it.node >> kFlagBlockShift] = 1;
+      }
+      if constexpr (kRecord) {
+        uint8_t* h = a.hop_rec + cw * 64;
+        uint64_t b = nm;
+        while (b) {
+          const int q = __ffsll(static_cast<long long>(b)) - 1;
+          h[q] = static_cast<uint8_t>(round);
+          b &= b - 1;
+        }
+      }
+    }
+  }
+  deliv = wave_sum_u64(deliv);
+  dup = wave_sum_u64(dup);
+  if ((threadIdx.x & 63) == 0 && (deliv || dup)) {
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + kCtrDeliveries), deliv);
+    atomicAdd(reinterpret_cast<unsigned long long*>(a.stats + kCtrDuplicates), dup);
   }
 }
 
@@ -655,6 +771,27 @@ hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_
   return hipGetLastError();
 }
 
+hipError_t launch_init_nodes(const uint32_t* nodes, uint32_t n, const uint16_t* node_topic,
+                             const TopicDev* topics, uint64_t* seen, uint64_t* a0, uint64_t* a1,
+                             uint8_t* gen, uint32_t gen_cur, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint32_t grid = std::min<uint32_t>(1024, (n + 3) / 4);
+  hipLaunchKernelGGL(k_init_nodes, dim3(grid), dim3(kBlock), 0, s, nodes, n, node_topic, topics,
+                     seen, a0, a1, gen, gen_cur);
+  return hipGetLastError();
+}
+
+hipError_t launch_apply(const ApplyArgs& a, uint32_t round, bool record, hipStream_t s) {
+  const uint64_t total = a.cap_pre[a.world];
+  if (total == 0) return hipSuccess;
+  const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(2048, (total + kBlock - 1) / kBlock));
+  if (record)
+    hipLaunchKernelGGL(k_apply<true>, dim3(grid), dim3(kBlock), 0, s, a, round);
+  else
+    hipLaunchKernelGGL(k_apply<false>, dim3(grid), dim3(kBlock), 0, s, a, round);
+  return hipGetLastError();
+}
+
 hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t* arrivals,
                        uint64_t* seen, uint8_t* next_flag, uint8_t* blk_flag, hipStream_t s) {
   if (hi <= lo) return hipSuccess;
@@ -667,9 +804,18 @@ hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t*
 hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid,
                          hipStream_t s) {
   if (record)
-    hipLaunchKernelGGL(k_expand<true>, dim3(grid), dim3(kBlock), 0, s, a, round);
+    hipLaunchKernelGGL((k_expand<true, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
   else
-    hipLaunchKernelGGL(k_expand<false>, dim3(grid), dim3(kBlock), 0, s, a, round);
+    hipLaunchKernelGGL((k_expand<false, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
+  return hipGetLastError();
+}
+
+hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid,
+                                hipStream_t s) {
+  if (record)
+    hipLaunchKernelGGL((k_expand<true, true>), dim3(grid), dim3(kBlock), 0, s, a, round);
+  else
+    hipLaunchKernelGGL((k_expand<false, true>), dim3(grid), dim3(kBlock), 0, s, a, round);
   return hipGetLastError();
 }
 

@@ -11,7 +11,24 @@ namespace psamd {
 enum : uint8_t {
   kNodeLive = 1,      // subscribed and live: receives and forwards
   kNodeInternal = 2,  // has at least one child: enters the next frontier
+  kNodeSplit = 4,     // some child is owned by another rank (direct path)
 };
+
+// col[] entry of a child owned by another rank: rank and its local node id
+constexpr uint32_t kRemoteBit = 0x80000000u;
+constexpr uint32_t kRemoteRankShift = 27;
+constexpr uint32_t kRemoteIdMask = (1u << kRemoteRankShift) - 1u;
+constexpr int kMaxRanks = 16;
+
+// One delivery addressed to a node of another rank: node id at the owner,
+// word of its row, the arriving bits.  Regions: 16-B header (u32 count) +
+// capacity items.
+struct XItem {
+  uint32_t node;
+  uint32_t word;
+  uint64_t mask;
+};
+constexpr uint32_t kRegionHeader = 16;
 
 // TopicDev.flags
 enum : uint32_t {
@@ -19,7 +36,9 @@ enum : uint32_t {
   // test-and-set and the arrival OR are 64-bit atomics, rows are cleared
   // eagerly per window and consumed-and-cleared per round.
   kTopicMesh = 1,
+  kTopicRootLocal = 2,  // this rank owns the topic root (node nbase)
 };
+constexpr uint32_t kEntrySplit = 0x100;  // per-entry flag bit next to TopicDev.flags
 
 // One topic of the fused node space.  Node u of topic t (nbase <= u <
 // nbase + n_nodes) owns the 64-message words [wbase + (u-nbase)*W, +W) of the
@@ -77,6 +96,24 @@ struct ExpandArgs {
   uint8_t* hop_rec;    // [word*64 + bit] = round, record mode only
   uint32_t gen_cur;
   uint32_t dbg;  // experiment knobs (kDbg*), 0 in production
+  uint8_t* send;                  // send regions of this round (multi-GPU)
+  uint64_t send_off[kMaxRanks];   // byte offset of the region for each rank
+};
+
+struct ApplyArgs {
+  const uint8_t* recv;
+  uint64_t recv_off[kMaxRanks];  // region from each rank
+  uint64_t cap_pre[kMaxRanks + 1];  // prefix of region capacities (items)
+  uint32_t world;
+  const uint16_t* node_topic;
+  const uint8_t* node_flags;
+  const TopicDev* topics;
+  uint64_t* seen;
+  uint64_t* a_next;
+  uint8_t* next_flag;
+  uint8_t* blk_flag;
+  uint8_t* hop_rec;
+  uint64_t* stats;  // [kNumCtr] of this round (deliveries, duplicates)
 };
 
 // k_expand experiment knobs (PSAMD_DEBUG_EXPAND); results are wrong when set
@@ -96,10 +133,19 @@ constexpr int kFlagBlockShift = 12;
 hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_t* seen,
                               uint64_t* a0, uint64_t* a1, uint8_t* gen, uint32_t gen_cur,
                               bool any_mesh, hipStream_t s);
+hipError_t launch_init_nodes(const uint32_t* nodes, uint32_t n, const uint16_t* node_topic,
+                             const TopicDev* topics, uint64_t* seen, uint64_t* a0, uint64_t* a1,
+                             uint8_t* gen, uint32_t gen_cur, hipStream_t s);
+hipError_t launch_apply(const ApplyArgs& a, uint32_t round, bool record, hipStream_t s);
 hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t* arrivals,
                        uint64_t* seen, uint8_t* next_flag, uint8_t* blk_flag, hipStream_t s);
 hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid,
                          hipStream_t s);
+// second instance: entries the staged kernel leaves (mesh, split, wide rows,
+// fan-out > 64); writes the same counters to partials + n_waves*kNumCtr
+hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid,
+                                hipStream_t s);
+constexpr uint32_t kStageMaxWords = 704;  // widest row of the staged path
 hipError_t launch_flag_count(const uint8_t* flags, const uint8_t* blk_flag, uint32_t n_pad,
                              uint32_t* wg_count, const uint64_t* partials, uint32_t n_waves,
                              uint64_t* round_stats, hipStream_t s);

@@ -22,6 +22,8 @@ ERRORS = {
     -1: "PS_E_INVAL", -2: "PS_E_NOMEM", -3: "PS_E_STATE", -4: "PS_E_NOPARENT",
     -5: "PS_E_UNREACHABLE", -6: "PS_E_DEVICE", -7: "PS_E_RANGE", -8: "PS_E_NOTREADY",
 }
+PART_PEER = 0
+PART_SUBTREE = 1
 F_RECORD_HOPS = 0x1
 F_TIME_KERNELS = 0x2
 F_NO_LAZY_SEEN = 0x4
@@ -64,6 +66,11 @@ class Stats(C.Structure):
         return d
 
 
+class DistConfig(C.Structure):
+    _fields_ = [("rank", C.c_int32), ("world", C.c_int32), ("partition", C.c_uint32),
+                ("split_depth", C.c_uint32)]
+
+
 PROTOTYPES = [
     ("ps_version", C.c_char_p, []),
     ("ps_create", C.c_int, [C.POINTER(Config), C.POINTER(_P)]),
@@ -85,6 +92,12 @@ PROTOTYPES = [
     ("ps_read_hops", C.c_int, [_P, _u32, _u8p]),
     ("ps_read_delivered", C.c_int, [_P, _u32, _u8p]),
     ("ps_seen_digest", C.c_int, [_P, _u64p]),
+    ("ps_dist_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
+    ("ps_dist_init", C.c_int, [_P, C.POINTER(DistConfig), C.POINTER(C.c_uint8)]),
+    ("ps_loopback_create", C.c_int, [C.c_int32, C.POINTER(_P)]),
+    ("ps_loopback_destroy", None, [_P]),
+    ("ps_dist_init_loopback", C.c_int, [_P, C.POINTER(DistConfig), _P]),
+    ("ps_partition_owner", C.c_int, [_u32, _u32, _u32p, _u32, C.POINTER(DistConfig), _i32p]),
 ]
 
 _lib = None
@@ -254,6 +267,62 @@ class Engine:
         d = C.c_uint64()
         self._check(self._L.ps_seen_digest(self._h, C.byref(d)))
         return d.value
+
+
+    # multi-GPU
+    def dist_init(self, rank: int, world: int, unique_id: bytes, partition: int = PART_SUBTREE,
+                  split_depth: int = 0):
+        """RCCL-backed sharding: this engine owns a hash partition of every topic."""
+        dc = DistConfig(rank, world, partition, split_depth)
+        uid = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        self._check(self._L.ps_dist_init(self._h, C.byref(dc), uid))
+
+    def dist_init_loopback(self, group: "Loopback", rank: int, partition: int = PART_SUBTREE,
+                           split_depth: int = 0):
+        dc = DistConfig(rank, group.world, partition, split_depth)
+        self._check(self._L.ps_dist_init_loopback(self._h, C.byref(dc), group._h))
+
+
+def unique_id() -> bytes:
+    buf = (C.c_uint8 * 128)()
+    rc = load().ps_dist_unique_id(buf)
+    if rc != PS_OK:
+        raise EngineError(rc, "ps_dist_unique_id")
+    return bytes(buf)
+
+
+class Loopback:
+    """In-process transport: `world` engines (one thread each) exchange
+    frontier regions through device copies -- the multi-GPU path on one GPU."""
+
+    def __init__(self, world: int):
+        self.world = world
+        h = _P()
+        rc = load().ps_loopback_create(world, C.byref(h))
+        if rc != PS_OK:
+            raise EngineError(rc, "ps_loopback_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            load().ps_loopback_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()
+
+
+def partition_owner(parent, root: int, topic: int, world: int, partition: int = PART_SUBTREE,
+                    split_depth: int = 0) -> np.ndarray:
+    """Host-only: owner rank of every peer of a tree (-1 outside the tree)."""
+    par = _u32arr(parent)
+    out = np.empty(par.shape[0], dtype=np.int32)
+    dc = DistConfig(0, world, partition, split_depth)
+    rc = load().ps_partition_owner(par.shape[0], root, _p(par, C.c_uint32), topic, C.byref(dc),
+                                   _p(out, C.c_int32))
+    if rc != PS_OK:
+        raise EngineError(rc, "ps_partition_owner")
+    return out
 
 
 def version() -> str:

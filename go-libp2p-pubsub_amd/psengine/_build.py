@@ -12,8 +12,8 @@ LIB = os.path.join(LIBDIR, "libpsengine.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["kernels.hip", "engine.cpp", "tree.cpp"]
-HEADERS = ["kernels.hpp", "tree.hpp"]
+SOURCES = ["kernels.hip", "engine.cpp", "tree.cpp", "dist.cpp"]
+HEADERS = ["kernels.hpp", "tree.hpp", "dist.hpp"]
 
 
 def _stale() -> bool:
@@ -32,7 +32,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     cmd = [HIPCC, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared", "-Wall",
            "-I" + os.path.join(REPO, "include"), "-I" + CSRC]
     cmd += [os.path.join(CSRC, f) for f in SOURCES]
-    cmd += ["-o", LIB + ".tmp"]
+    cmd += ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-o", LIB + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

@@ -145,8 +145,45 @@ int ps_run(ps_engine* e, ps_stats* out);
 int ps_read_hops(ps_engine* e, uint32_t msg, uint8_t* hop_per_peer);
 int ps_read_delivered(ps_engine* e, uint32_t msg, uint8_t* delivered_per_peer);
 /* Order-independent digest of the final seen state of the last window:
- * sum over (peer, topic, word) of mix64(peer, topic, word, seen bits). */
+ * sum over (peer, topic, word < message words) of
+ * mix64(mix64(peer << 32 | topic << 16 | word) ^ mix64(seen word)); a
+ * multi-GPU engine sums its owned nodes (the ranks' digests add up). */
 int ps_seen_digest(ps_engine* e, uint64_t* digest_out);
+
+/* ---- multi-GPU: one engine (process) per GPU --------------------------------
+ * Every rank creates the same topics and memberships and publishes the same
+ * messages; each owns a hash partition of every topic's tree nodes and ps_run
+ * exchanges, each round, the deliveries addressed to other ranks' nodes
+ * (stream-ordered all-to-allv over RCCL / xGMI).  Stats and ps_read_* cover
+ * the owned nodes; sums over ranks give the job totals.
+ *   PS_PART_PEER     owner(p) = splitmix64(p) mod world
+ *   PS_PART_SUBTREE  a node below the split level belongs to the owner of its
+ *                    ancestor at that level (hash of topic and that peer), so
+ *                    only edges out of the top levels cross GPUs. */
+#define PS_PART_PEER 0u
+#define PS_PART_SUBTREE 1u
+#define PS_UNIQUE_ID_BYTES 128
+
+typedef struct ps_dist_config {
+  int32_t rank;
+  int32_t world;        /* <= 16 */
+  uint32_t partition;   /* PS_PART_*                                    */
+  uint32_t split_depth; /* PS_PART_SUBTREE: split level, 0 = automatic */
+} ps_dist_config;
+
+/* rank 0 creates the RCCL id; the caller ships it to every rank */
+int ps_dist_unique_id(uint8_t id_out[PS_UNIQUE_ID_BYTES]);
+int ps_dist_init(ps_engine* e, const ps_dist_config* dc, const uint8_t id[PS_UNIQUE_ID_BYTES]);
+/* in-process transport: `world` engines of one process (one thread each)
+ * exchange through device copies -- runs the multi-GPU path on one GPU */
+typedef struct ps_loopback ps_loopback;
+int ps_loopback_create(int32_t world, ps_loopback** out);
+void ps_loopback_destroy(ps_loopback* lb);
+int ps_dist_init_loopback(ps_engine* e, const ps_dist_config* dc, ps_loopback* lb);
+/* host-only: owner rank of every peer of a tree (parent array, PS_NONE =
+ * absent) under a partition; -1 for peers outside the tree */
+int ps_partition_owner(uint32_t n_peers, uint32_t root, const uint32_t* parent, uint32_t topic,
+                       const ps_dist_config* dc, int32_t* owner_out);
 
 #ifdef __cplusplus
 }

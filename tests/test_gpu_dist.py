@@ -1,0 +1,113 @@
+"""GPU: the multi-GPU path (hash-partitioned nodes, per-round all-to-allv
+exchange, apply kernel) on ONE GPU through the in-process loopback transport:
+`world` engines in `world` threads, the real kernels and routing, device-to-
+device copies in place of RCCL.  The union of the ranks' deliveries must equal
+the CPU restatement's bit for bit."""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle as O
+import psengine as PE
+from psengine import workloads as WL
+
+pytestmark = pytest.mark.gpu
+
+
+def random_tree(rng, n, root=0):
+    perm = rng.permutation(n)
+    perm = np.concatenate([[root], perm[perm != root]])
+    parent = np.full(n, O.NONE, dtype=np.uint32)
+    for i in range(1, n):
+        parent[perm[i]] = perm[rng.integers(0, i)]
+    return parent
+
+
+def run_ranks(engines):
+    stats = [None] * len(engines)
+    errs = []
+
+    def go(r):
+        try:
+            stats[r] = engines[r].run()
+        except Exception as ex:  # noqa: BLE001
+            errs.append((r, ex))
+
+    th = [threading.Thread(target=go, args=(r,)) for r in range(len(engines))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "rank thread hung"
+    assert not errs, errs
+    return stats
+
+
+def make_ranks(world, n, n_topics, partition, split_depth=0, **kw):
+    lb = PE.Loopback(world)
+    engines = [PE.Engine(n, n_topics, record_hops=True, **kw) for _ in range(world)]
+    for r, e in enumerate(engines):
+        e.dist_init_loopback(lb, r, partition, split_depth)
+    return lb, engines
+
+
+def merged_hops(engines, msg):
+    h = np.stack([e.hops(msg) for e in engines])
+    return h.min(axis=0)  # every peer is owned by exactly one rank per topic
+
+
+@pytest.mark.parametrize("world,partition", [(2, PE.PART_SUBTREE), (3, PE.PART_PEER),
+                                             (4, PE.PART_SUBTREE), (4, PE.PART_PEER)])
+def test_sharded_trees_match_oracle(world, partition):
+    rng = np.random.default_rng(world * 10 + partition)
+    n, n_topics = 2500, 3
+    lb, engines = make_ranks(world, n, n_topics, partition)
+    trees = [random_tree(rng, n, int(rng.integers(0, n))) for _ in range(n_topics)]
+    live = (rng.random(n) > 0.08).astype(np.uint8)
+    topics = rng.integers(0, n_topics, size=150)
+    starts = rng.integers(0, 4, size=150)
+    for e in engines:
+        for t in range(n_topics):
+            e.set_tree(t, int(np.nonzero(trees[t] == O.NONE)[0][0]), trees[t])
+        e.set_live(live)
+    firsts = [e.publish(topics, starts) for e in engines]
+    stats = run_ranks(engines)
+    total = 0
+    for t in range(n_topics):
+        root = int(np.nonzero(trees[t] == O.NONE)[0][0])
+        rp, cl = O.parents_to_csr(trees[t])
+        idx = np.nonzero(topics == t)[0]
+        tot, hops, _ = O.disseminate(rp, cl, root, live, len(idx))
+        total += tot
+        for k, m in enumerate(idx):
+            assert np.array_equal(merged_hops(engines, firsts[0] + m), hops[k]), (t, m)
+    assert sum(s.deliveries for s in stats) == total
+    assert sum(s.duplicates for s in stats) == 0
+    for e in engines:
+        e.close()
+    lb.close()
+
+
+def test_sharded_join_trees_and_digest_sum():
+    """cfg3-shaped (scaled): restated join trees on every rank, subtree
+    partition; per-rank digests add up to the single-engine digest."""
+    wl = WL.cfg3(20000, 8, 3000)
+    with PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed) as one:
+        sizes = WL.build_engine_topics(one, wl)
+        one.publish(wl.msg_topics)
+        st1 = one.run()
+        d1 = one.seen_digest()
+    world = 4
+    lb = PE.Loopback(world)
+    engines = [PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed) for _ in range(world)]
+    for r, e in enumerate(engines):
+        e.dist_init_loopback(lb, r, PE.PART_SUBTREE)
+        WL.build_engine_topics(e, wl)
+        e.publish(wl.msg_topics)
+    stats = run_ranks(engines)
+    assert sum(s.deliveries for s in stats) == st1.deliveries == wl.expected_deliveries(sizes)
+    assert sum(e.seen_digest() for e in engines) % (1 << 64) == d1
+    for e in engines:
+        e.close()
+    lb.close()
