@@ -87,10 +87,14 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-check", action="store_true", help="skip delivery assertions (experiments)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="use the torch.distributed driver even with one rank (testing)")
+    ap.add_argument("--partition", default="subtree", choices=["subtree", "peer"],
+                    help="multi-GPU node ownership: subtree hash (default) or peer hash")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus > 1 or world > 1:
+    if args.gpus > 1 or world > 1 or args.force_dist:
         from psengine import dist
 
         return dist.bench_main(args, DESCR, METRIC)

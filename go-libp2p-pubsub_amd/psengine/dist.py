@@ -1,0 +1,135 @@
+"""Multi-GPU driver for bench.py: one process per GPU, torch.distributed for
+bootstrap, barriers and the max-over-ranks clock; the frontier exchange itself
+runs inside the engine over its own RCCL communicator (ps_dist_init).
+
+Every rank builds the same topics (the restated joins are deterministic) and
+publishes the same messages; each owns a hash partition of every topic's tree
+nodes (PART_SUBTREE by default, PART_PEER = owner(p) = splitmix64(p) mod N).
+The job's deliveries are the sum over ranks; its time is the slowest rank's.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+from . import PART_PEER, PART_SUBTREE, Engine, unique_id
+from . import workloads as WL
+
+
+def env_ranks():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def init(backend: str):
+    """Initialises the default process group (rendezvous on 127.0.0.1)."""
+    import torch.distributed as dist
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29531")
+    if not dist.is_initialized():
+        dist.init_process_group(backend)
+    return dist
+
+
+def share_bytes(dist, make, rank: int) -> bytes:
+    """Rank 0 makes a byte string (the RCCL unique id); every rank gets it."""
+    obj = [make() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+def job_totals(dist, elapsed_s: float, local_count: int, device=None):
+    """(max elapsed over ranks, sum of counts over ranks)."""
+    import torch
+
+    t = torch.tensor([elapsed_s], dtype=torch.float64, device=device)
+    c = torch.tensor([float(local_count)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    return float(t.item()), int(round(c.item()))
+
+
+def bench_main(args, descr: dict, metric: str):
+    import torch
+
+    rank, world, local = env_ranks()
+    torch.cuda.set_device(local)
+    dist = init("nccl")  # RCCL on ROCm
+    dev = torch.device("cuda", local)
+    part = PART_PEER if getattr(args, "partition", "subtree") == "peer" else PART_SUBTREE
+    wl = WL.CONFIGS[args.workload]() if args.scale == 1.0 else WL.scaled(args.workload, args.scale)
+    uid = share_bytes(dist, unique_id, rank)
+    t0 = time.perf_counter()
+    eng = Engine(wl.n_peers, len(wl.topics), device=local, time_kernels=True, seed=wl.seed)
+    eng.dist_init(rank, world, uid, part)
+    sizes = WL.build_engine_topics(eng, wl)
+    expected = wl.expected_deliveries(sizes)
+    if rank == 0:
+        print(f"[bench] {wl.name} on {world} GPUs ({'peer' if part == PART_PEER else 'subtree'} "
+              f"partition), setup {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+
+    def step():
+        eng.publish(wl.msg_topics)
+        return eng.run()
+
+    for _ in range(args.warmup):
+        st = step()
+    _, warm = job_totals(dist, 0.0, st.deliveries if args.warmup else 0, dev)
+    if args.warmup and not args.no_check:
+        assert warm == expected, (warm, expected)
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    local_deliv = 0
+    bytes_, exp_ms, launches = 0, 0.0, 0
+    for _ in range(args.steps):
+        st = step()
+        local_deliv += st.deliveries
+        bytes_ += st.expand_bytes
+        exp_ms += st.expand_ms
+        launches += st.expand_launches
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    wall, total = job_totals(dist, elapsed, local_deliv, dev)
+    _, tot_bytes = job_totals(dist, 0.0, bytes_, dev)
+    slow_exp_ms, _ = job_totals(dist, exp_ms, 0, dev)
+    if not args.no_check:
+        assert total == expected * args.steps, (total, expected * args.steps)
+    if rank == 0:
+        value = total / wall
+        achieved = tot_bytes / max(1e-12, slow_exp_ms * 1e-3) / 1e9 / world  # per GPU
+        out = {
+            "metric": metric,
+            "value": value,
+            "unit": "deliveries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic",
+            "config": {"workload": f"{wl.name}: {descr[wl.name]}", "peers": wl.n_peers,
+                       "topics": len(wl.topics), "subscriptions": int(sum(sizes)),
+                       "messages": wl.n_msgs, "deliveries_per_step": expected,
+                       "parallelism": f"{world} GPUs, nodes hash-partitioned "
+                                      f"({'peer' if part == PART_PEER else 'subtree'}), "
+                                      "RCCL all-to-allv frontier exchange per round"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
+                         "frac": achieved / 8000.0, "traffic": None, "kernel": "k_expand",
+                         "note": "per-GPU: job expand bytes / slowest rank's expand time / N"},
+            "last_step_rank0": {"rounds": st.rounds, "run_ms": st.run_ms,
+                                "expand_ms": st.expand_ms, "host_ms": st.host_ms},
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    dist.barrier()
+    dist.destroy_process_group()
