@@ -106,6 +106,7 @@ struct ps_engine {
   hipEvent_t ev_run0 = nullptr, ev_run1 = nullptr;
   std::vector<hipEvent_t> ev_k;  // pairs around expand launches
   uint32_t n_cus = 256, expand_grid = 2048;
+  bool no_single_start = false;  // PSAMD_NO_SINGLE_START=1: keep arrival rows (A/B)
 
   std::vector<TopicHost> topics;
   std::vector<uint8_t> live;
@@ -472,8 +473,14 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     if (!T.exists || win[t].n == 0) continue;
     // every rank plans the same rounds: global depth, global start rounds
     max_depth = std::max(max_depth, T.depth);
-    for (uint32_t li = 0; li < win[t].n; ++li)
+    bool one_start = true;
+    for (uint32_t li = 0; li < win[t].n; ++li) {
       max_start = std::max(max_start, msgs[win[t].idx[li]].start);
+      one_start &= msgs[win[t].idx[li]].start == msgs[win[t].idx[0]].start;
+    }
+    // a tree topic whose window messages share one start round: every node
+    // receives once, so arrival rows are its seen rows (kTopicSingleStart)
+    if (one_start && !T.mesh && !e->no_single_start) d.flags |= kTopicSingleStart;
     if (T.n_nodes == 0) continue;
     d.W = ceil_div(win[t].n, 64);
     d.w_msgs = d.W;
@@ -876,6 +883,7 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   uint32_t bpc = 6;
   if (const char* v = std::getenv("PSAMD_EXPAND_BPC")) bpc = std::max(1, std::atoi(v));
   e->expand_grid = e->n_cus * bpc;
+  if (const char* v = std::getenv("PSAMD_NO_SINGLE_START")) e->no_single_start = std::atoi(v) != 0;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess) {
     delete e;

@@ -295,6 +295,10 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
   const bool mesh = (tflags & kTopicMesh) != 0;
   const bool split = (tflags & kEntrySplit) != 0;  // some children live on other ranks
   const bool listed = mesh || split;
+  const bool is_root = p == nbase && (tflags & kTopicRootLocal);
+  // single-start tree topic: arrival rows live in `seen` (roots: seeded rows)
+  const bool single = (tflags & kTopicSingleStart) && !mesh;
+  const uint64_t* src = (single && !is_root) ? a.seen : a.a_cur;
   const uint64_t pw = wbase + static_cast<uint64_t>(p - nbase) * W;
   const uint64_t cbase = wbase - static_cast<uint64_t>(nbase) * W;
   ec.ent += 1;
@@ -327,7 +331,7 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
           XItem it;
           it.node = c & kRemoteIdMask;
           it.word = w;
-          it.mask = a.a_cur[pw + w];
+          it.mask = src[pw + w];
           out[w] = it;
         }
       }
@@ -336,7 +340,7 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
       for (uint32_t wb = 0; wb < W; wb += 64) {
         const uint32_t w = wb + lane;
         const bool active = w < W;
-        const uint64_t m = active ? a.a_cur[pw + w] : 0ull;
+        const uint64_t m = active ? src[pw + w] : 0ull;
         for (uint32_t jj = 0; jj < cd; ++jj) {
           const uint32_t f = rl(fj, jj);
           if (!(f & kNodeLive)) continue;
@@ -345,7 +349,7 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
           const bool internal = (f & kNodeInternal) != 0;
           uint64_t nm = 0;
           if (active)
-            nm = deliver_word<kRecord>(a, mesh, stale, internal,
+            nm = deliver_word<kRecord>(a, mesh, stale, internal && !single,
                                        cbase + static_cast<uint64_t>(c) * W + w, m, round, k);
           if (internal && __ballot(nm != 0) && lane == 0) mark_next(a, c);
         }
@@ -357,7 +361,7 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
       const uint32_t jl = lane >> sh;
       const uint32_t groups = 64u >> sh;
       const uint64_t gmask = (wp == 64u ? ~0ull : ((1ull << wp) - 1ull)) << (jl << sh);
-      const uint64_t m = w < W ? a.a_cur[pw + w] : 0ull;
+      const uint64_t m = w < W ? src[pw + w] : 0ull;
       for (uint32_t jb = 0; jb < cd; jb += groups) {
         const uint32_t jj = jb + jl;
         const uint32_t c = static_cast<uint32_t>(__shfl(static_cast<int>(cj), static_cast<int>(jj), 64));
@@ -366,7 +370,8 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
         const bool live = (w < W) && (jj < cd) && (f & kNodeLive);
         uint64_t nm = 0;
         if (live)
-          nm = deliver_word<kRecord>(a, mesh, !mesh && g != cur, (f & kNodeInternal) != 0,
+          nm = deliver_word<kRecord>(a, mesh, !mesh && g != cur,
+                                     (f & kNodeInternal) != 0 && !single,
                                      cbase + static_cast<uint64_t>(c) * W + w, m, round, k);
         const uint64_t bal = __ballot(nm != 0);
         if (live && w == 0 && (f & kNodeInternal) && (bal & gmask)) mark_next(a, c);
@@ -375,7 +380,7 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
     if (!mesh && lane < cd && (fj & kNodeLive) && !(a.dbg & kDbgNoByteStores))
       a.gen[cj] = static_cast<uint8_t>(cur);
   }
-  if (mesh || (p == nbase && (tflags & kTopicRootLocal))) {
+  if (mesh || is_root) {
     // consume-and-clear: mesh rows are OR-accumulated, root rows are seeded
     for (uint32_t w = lane; w < W; w += 64) a.a_cur[pw + w] = 0;
     ec.clear += W;
@@ -464,8 +469,10 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
           if (W == 0) continue;
           const uint32_t p = rl(bp, i), nbase = rl(bnb, i), c0 = rl(bc0, i);
           const uint64_t wbase = (static_cast<uint64_t>(rl(bwh, i)) << 32) | rl(bwl, i);
-          const uint32_t* row =
-              reinterpret_cast<const uint32_t*>(a.a_cur + wbase + static_cast<uint64_t>(p - nbase) * W);
+          const uint32_t fl = rl(bfl, i);
+          const bool from_seen = (fl & kTopicSingleStart) && !(p == nbase && (fl & kTopicRootLocal));
+          const uint32_t* row = reinterpret_cast<const uint32_t*>(
+              (from_seen ? a.seen : a.a_cur) + wbase + static_cast<uint64_t>(p - nbase) * W);
           uint32_t* dst = reinterpret_cast<uint32_t*>(ws.words + off);
           for (uint32_t d = 0; d < 2 * W; d += 64)
             if (d + lane < 2 * W) PSAMD_LDS_DMA(row + d + lane, dst + d, 4);
@@ -494,6 +501,8 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
           const uint64_t cbase = wbase - static_cast<uint64_t>(nbase) * W;
           const uint32_t nd = ((c0 + deg + 3u) >> 2) - (c0 >> 2);
           const uint32_t fo = doff + (c0 & 3u);  // byte of child 0
+          // single-start topics keep no arrival rows (see kTopicSingleStart)
+          const bool keep = !(rl(bfl, i) & kTopicSingleStart);
           ec.ent += 1;
           ec.ent_words += W;
           ec.kids += deg;
@@ -503,6 +512,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
               if (!(f & kNodeLive)) continue;
               const bool stale = ws.gens[fo + jj] != cur;
               const bool internal = (f & kNodeInternal) != 0;
+              const bool store = internal && keep;
               const uint32_t c = c0 + jj;
               const uint64_t row = cbase + static_cast<uint64_t>(c) * W;
               bool any = false;
@@ -513,7 +523,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
                   const uint32_t w = wb + 2 * lane;
                   if (w < W) {
                     const uint4 v = *reinterpret_cast<const uint4*>(ws.words + off + w);
-                    deliver_fresh2<kRecord>(a, internal, row + w, v, round, k);
+                    deliver_fresh2<kRecord>(a, store, row + w, v, round, k);
                     any |= (v.x | v.y | v.z | v.w) != 0;
                   }
                 }
@@ -521,7 +531,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
                 for (uint32_t wb = 0; wb < W; wb += 64) {
                   const uint32_t w = wb + lane;
                   if (w < W) {
-                    const uint64_t nm = deliver_word<kRecord>(a, false, false, internal, row + w,
+                    const uint64_t nm = deliver_word<kRecord>(a, false, false, store, row + w,
                                                               ws.words[off + w], round, k);
                     any |= nm != 0;
                   }
@@ -548,11 +558,12 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
               uint64_t nm = 0;
               if (__ballot(live && !stale) == 0) {  // burst: every live child fresh
                 if (live) {
-                  deliver_fresh<kRecord>(a, (f & kNodeInternal) != 0, cw, m, round, k);
+                  deliver_fresh<kRecord>(a, keep && (f & kNodeInternal), cw, m, round, k);
                   nm = m;
                 }
               } else if (live) {
-                nm = deliver_word<kRecord>(a, false, stale, (f & kNodeInternal) != 0, cw, m, round, k);
+                nm = deliver_word<kRecord>(a, false, stale, keep && (f & kNodeInternal), cw, m,
+                                           round, k);
               }
               const uint64_t bal = __ballot(nm != 0);
               if (live && w == 0 && (f & kNodeInternal) && (bal & gmask)) mark_next(a, c);
@@ -614,7 +625,8 @@ __global__ __launch_bounds__(kBlock) void k_apply(ApplyArgs a, uint32_t round) {
     if (!(f & kNodeLive) || it.mask == 0) {
       if ((f & kNodeLive) && (f & kNodeInternal)) {
         const TopicDev T = a.topics[a.node_topic[it.node]];
-        a.a_next[T.wbase + static_cast<uint64_t>(it.node - T.nbase) * T.W + it.word] = 0;
+        if (!(T.flags & kTopicSingleStart))
+          a.a_next[T.wbase + static_cast<uint64_t>(it.node - T.nbase) * T.W + it.word] = 0;
       }
       continue;
     }
@@ -623,7 +635,7 @@ __global__ __launch_bounds__(kBlock) void k_apply(ApplyArgs a, uint32_t round) {
     const uint64_t old = atomicOr(reinterpret_cast<unsigned long long*>(a.seen + cw),
                                   static_cast<unsigned long long>(it.mask));
     const uint64_t nm = it.mask & ~old;
-    if (f & kNodeInternal) a.a_next[cw] = nm;
+    if ((f & kNodeInternal) && !(T.flags & kTopicSingleStart)) a.a_next[cw] = nm;
     dup += __popcll(it.mask & old);
     if (nm) {
       deliv += __popcll(nm);

@@ -37,6 +37,11 @@ enum : uint32_t {
   // eagerly per window and consumed-and-cleared per round.
   kTopicMesh = 1,
   kTopicRootLocal = 2,  // this rank owns the topic root (node nbase)
+  // Tree topic whose messages of this window all start in one round: every
+  // node receives exactly once, so a node's arrival row equals its freshly
+  // written seen row.  Arrival rows are then neither stored nor read: a
+  // (non-root) parent's row is read from `seen`.
+  kTopicSingleStart = 4,
 };
 constexpr uint32_t kEntrySplit = 0x100;  // per-entry flag bit next to TopicDev.flags
 
