@@ -76,6 +76,7 @@ struct TopicHost {
   bool root_local = true;                // this rank owns the root
   uint32_t max_deg = 0;
   std::vector<uint32_t> level_internal;  // BFS level -> owned nodes with children
+  std::vector<uint32_t> level_off;       // single rank: BFS level -> first node (topic-relative)
   // cross-rank edges by the parent's BFS level: (level, from rank, to rank, count)
   struct Cross {
     uint32_t level, from, to, count;
@@ -107,10 +108,17 @@ struct ps_engine {
   std::vector<hipEvent_t> ev_k;  // pairs around expand launches
   uint32_t n_cus = 256, expand_grid = 2048;
   bool no_single_start = false;  // PSAMD_NO_SINGLE_START=1: keep arrival rows (A/B)
+  bool no_level = false;         // PSAMD_NO_LEVEL=1: always compact the frontier (A/B)
 
   std::vector<TopicHost> topics;
   std::vector<uint8_t> live;
   bool graph_dirty = true, flags_dirty = true;
+  uint64_t graph_epoch = 0, flags_epoch = 0;  // bumped by every upload
+
+  // level mode: static per-round frontier of the window
+  std::vector<uint64_t> sched_key;  // (epochs, rounds, per-topic start) it was built for
+  std::vector<uint32_t> sched_host, sched_off, sched_cnt, woff_host;
+  DevBuf d_sched, d_sched_cnt, d_woff;
 
   // fused node space (host mirror)
   uint32_t n_nodes = 0, n_pad = 16;
@@ -335,6 +343,11 @@ int build_graph(ps_engine* e) {
     }
     T.root_local = owner[0] == me;
     T.level_internal.assign(T.depth + 1, 0);
+    T.level_off.assign(T.depth + 2, 0);
+    if (world == 1) {  // every node owned: BFS levels are contiguous node ranges
+      for (uint32_t u = 0; u < N; ++u) T.level_off[level[u] + 1]++;
+      for (uint32_t d = 0; d <= T.depth; ++d) T.level_off[d + 1] += T.level_off[d];
+    }
     std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> cross;
     uint32_t n_own = 0;
     for (uint32_t u = 0; u < N; ++u) {
@@ -438,8 +451,10 @@ int upload_graph(ps_engine* e) {
     e->graph_dirty = false;
     e->flags_dirty = true;
     e->have_window = false;  // the node space of the last window is gone
+    ++e->graph_epoch;
   }
   if (e->flags_dirty) {
+    ++e->flags_epoch;
     build_flags(e);
     if (e->n_nodes)
       HIP_TRY(hipMemcpyAsync(e->d_node_flags.p, e->node_flags.data(), e->n_nodes, hipMemcpyHostToDevice, e->stream),
@@ -448,6 +463,56 @@ int upload_graph(ps_engine* e) {
   }
   // host mirrors may be rebuilt by the next call: finish the uploads now
   HIP_TRY(hipStreamSynchronize(e->stream), "sync uploads");
+  return PS_OK;
+}
+
+// Level mode.  In a window whose topics are all trees with a
+// single start round s_t each, a node at BFS level d receives the window's
+// messages exactly in round s_t + d (if every ancestor is live) and forwards
+// them in round s_t + d + 1.  The frontier of round q is therefore known
+// before the window runs: the live internal nodes of level q - 1 - s_t of
+// every topic.  The schedule lists them round by round (node order inside a
+// topic, so siblings' rows stay adjacent); the expand kernel skips the
+// entries the messages did not reach, and no flags or compaction are needed.
+// Cached: rebuilt only when the node space, the flags or the start rounds
+// change.
+int build_schedule(ps_engine* e, const std::vector<TopicDev>& tab,
+                   const std::vector<uint32_t>& tstart, uint32_t rounds) {
+  const uint32_t nt = static_cast<uint32_t>(e->topics.size());
+  std::vector<uint64_t> key{e->graph_epoch, e->flags_epoch, rounds};
+  for (uint32_t t = 0; t < nt; ++t) key.push_back(tab[t].W ? tstart[t] : ~0ull);
+  if (key == e->sched_key) return PS_OK;
+  e->sched_key.clear();
+  auto& S = e->sched_host;
+  auto& off = e->sched_off;
+  S.clear();
+  off.assign(rounds + 2, 0);
+  for (uint32_t q = 1; q <= rounds; ++q) {
+    off[q] = static_cast<uint32_t>(S.size());
+    for (uint32_t t = 0; t < nt; ++t) {
+      const TopicHost& T = e->topics[t];
+      if (tab[t].W == 0 || q < tstart[t] + 1) continue;
+      const uint32_t d = q - 1 - tstart[t];
+      if (d + 1 >= T.level_off.size()) continue;
+      for (uint32_t u = T.level_off[d]; u < T.level_off[d + 1]; ++u) {
+        const uint32_t node = T.nbase + u;
+        if ((e->node_flags[node] & (kNodeLive | kNodeInternal)) == (kNodeLive | kNodeInternal))
+          S.push_back(node);
+      }
+    }
+  }
+  off[rounds + 1] = static_cast<uint32_t>(S.size());
+  e->sched_cnt.assign(rounds + 2, 0);
+  for (uint32_t q = 1; q <= rounds; ++q) e->sched_cnt[q] = off[q + 1] - off[q];
+  HIP_TRY(e->d_sched.ensure(std::max<size_t>(S.size(), 1) * 4), "alloc schedule");
+  HIP_TRY(e->d_sched_cnt.ensure(e->sched_cnt.size() * 4), "alloc schedule counts");
+  if (!S.empty())
+    HIP_TRY(hipMemcpyAsync(e->d_sched.p, S.data(), S.size() * 4, hipMemcpyHostToDevice, e->stream),
+            "upload schedule");
+  HIP_TRY(hipMemcpyAsync(e->d_sched_cnt.p, e->sched_cnt.data(), e->sched_cnt.size() * 4,
+                         hipMemcpyHostToDevice, e->stream),
+          "upload schedule counts");
+  e->sched_key = key;
   return PS_OK;
 }
 
@@ -463,6 +528,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   uint64_t wtot = 0;
   uint32_t max_depth = 0, max_start = 0;
   bool need_direct = world > 1;
+  std::vector<uint32_t> tstart(std::max<uint32_t>(nt, 1), 0);  // single-start topics
   for (uint32_t t = 0; t < nt; ++t) {
     const TopicHost& T = e->topics[t];
     TopicDev& d = tab[t];
@@ -481,6 +547,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     // a tree topic whose window messages share one start round: every node
     // receives once, so arrival rows are its seen rows (kTopicSingleStart)
     if (one_start && !T.mesh && !e->no_single_start) d.flags |= kTopicSingleStart;
+    tstart[t] = msgs[win[t].idx[0]].start;
     if (T.n_nodes == 0) continue;
     d.W = ceil_div(win[t].n, 64);
     d.w_msgs = d.W;
@@ -559,6 +626,28 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(e->expand_grid, blocks)));
   };
   const uint32_t planned0 = max_depth + max_start + 1;
+  // level mode: single rank, staged path only, every active topic a
+  // single-start tree
+  bool level = world == 1 && !need_direct && !any_mesh && !e->no_level &&
+               planned0 + 1 < kMaxRoundsCap;
+  for (uint32_t t = 0; t < nt && level; ++t)
+    if (tab[t].W && !(tab[t].flags & kTopicSingleStart)) level = false;
+  std::vector<uint32_t> lgrid;  // level mode: expand grid of every round
+  if (level) {
+    int rc2 = build_schedule(e, tab, tstart, planned0);
+    if (rc2) return rc2;
+    lgrid.assign(planned0 + 1, 0);
+    auto& woff = e->woff_host;
+    woff.assign(planned0 + 2, 0);
+    for (uint32_t q = 1; q <= planned0; ++q) {
+      const uint32_t cnt = e->sched_cnt[q];
+      lgrid[q] = cnt ? std::min<uint32_t>(e->expand_grid, ceil_div(cnt, 4)) : 0;  // >= 1 entry per wave
+      woff[q + 1] = woff[q] + lgrid[q] * (kBlock / 64);
+    }
+    HIP_TRY(e->d_partials.ensure(static_cast<size_t>(woff[planned0 + 1]) * kNumCtr * 8),
+            "alloc level partials");
+    HIP_TRY(e->d_woff.ensure(woff.size() * 4), "alloc wave offsets");
+  }
   // cross-rank capacities (items = node words) per round: cap[r][from*world+to]
   std::vector<std::vector<uint64_t>> cap;
   uint64_t max_send = 0, max_recv = 0;
@@ -647,8 +736,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
 
   auto seed_round = [&](uint32_t r, uint64_t* into) -> hipError_t {
     if (r > max_start) return hipSuccess;
-    return launch_seed(e->d_seeds.as<SeedDev>(), seed_off[r], seed_off[r + 1], into,
-                       a.seen, a.next_flag, a.blk_flag, s);
+    return launch_seed(e->d_seeds.as<SeedDev>(), seed_off[r], seed_off[r + 1], into, a.seen,
+                       level ? nullptr : a.next_flag, level ? nullptr : a.blk_flag, s);
   };
   auto compact = [&](uint32_t r, uint32_t waves_r) -> hipError_t {
     hipError_t x = launch_flag_count(a.next_flag, a.blk_flag, e->n_pad,
@@ -678,11 +767,48 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     return any;  // the same verdict on every rank
   };
 
-  HIP_TRY(seed_round(0, arr[0]), "seed");
-  HIP_TRY(compact(0, 0), "compact");
   uint32_t planned = planned0;
   uint32_t r = 0;
   size_t ev_used = 0;
+  auto time_mark = [&](bool begin) -> hipError_t {
+    if (!timed) return hipSuccess;
+    if (begin && ev_used + 2 > e->ev_k.size()) {
+      hipEvent_t x, y;
+      hipError_t c = hipEventCreate(&x);
+      if (c == hipSuccess) c = hipEventCreate(&y);
+      if (c != hipSuccess) return c;
+      e->ev_k.push_back(x);
+      e->ev_k.push_back(y);
+    }
+    const hipError_t c = hipEventRecord(e->ev_k[ev_used + (begin ? 0 : 1)], s);
+    if (!begin) ev_used += 2;
+    return c;
+  };
+  if (level) {
+    // static frontier: one expand launch per round, counters reduced once
+    HIP_TRY(hipMemcpyAsync(e->d_woff.p, e->woff_host.data(), e->woff_host.size() * 4,
+                           hipMemcpyHostToDevice, s),
+            "upload wave offsets");
+    HIP_TRY(seed_round(0, arr[0]), "seed");
+    for (r = 1; r <= planned0; ++r) {
+      a.a_cur = arr[(r - 1) & 1];
+      a.a_next = arr[r & 1];
+      HIP_TRY(time_mark(true), "event");
+      if (lgrid[r]) {
+        a.frontier = e->d_sched.as<uint32_t>() + e->sched_off[r];
+        a.n_front = e->d_sched_cnt.as<uint32_t>() + r;
+        a.partials = partials + static_cast<size_t>(e->woff_host[r]) * kNumCtr;
+        HIP_TRY(launch_expand(a, r, record, true, lgrid[r], s), "expand");
+      }
+      HIP_TRY(time_mark(false), "event");
+      HIP_TRY(seed_round(r, a.a_next), "seed");
+    }
+    r = planned0;
+    HIP_TRY(launch_reduce_rounds(partials, e->d_woff.as<uint32_t>(), planned0, stats, s),
+            "reduce rounds");
+  } else {
+  HIP_TRY(seed_round(0, arr[0]), "seed");
+  HIP_TRY(compact(0, 0), "compact");
   while (true) {
     for (; r < planned && r < kMaxRoundsCap; ) {
       ++r;
@@ -692,27 +818,17 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       if (xr)
         for (int32_t q = 0; q < world; ++q)
           if (s_len[q]) HIP_TRY(hipMemsetAsync(a.send + s_off[q], 0, kRegionHeader, s), "reset header");
-      if (timed) {
-        if (ev_used + 2 > e->ev_k.size()) {
-          hipEvent_t x, y;
-          HIP_TRY(hipEventCreate(&x), "event");
-          HIP_TRY(hipEventCreate(&y), "event");
-          e->ev_k.push_back(x);
-          e->ev_k.push_back(y);
-        }
-        HIP_TRY(hipEventRecord(e->ev_k[ev_used], s), "event");
-      }
+      HIP_TRY(time_mark(true), "event");
       const uint32_t grid_r = r <= planned0 ? round_grid(r) : e->expand_grid;
       a.partials = partials;
-      HIP_TRY(launch_expand(a, r, record, grid_r, s), "expand");
+      HIP_TRY(launch_expand(a, r, record, false, grid_r, s), "expand");
       uint32_t waves_r = grid_r * (kBlock / 64);
       if (need_direct) {
         a.partials = partials + static_cast<size_t>(waves_r) * kNumCtr;
         HIP_TRY(launch_expand_direct(a, r, record, e->expand_grid, s), "expand direct");
         waves_r += n_waves;
       }
-      if (timed) HIP_TRY(hipEventRecord(e->ev_k[ev_used + 1], s), "event");
-      if (timed) ev_used += 2;
+      HIP_TRY(time_mark(false), "event");
       if (xr) {
         std::string xerr;
         hipError_t xe = e->transport->exchange(a.send, s_off, s_len, e->d_recv.as<uint8_t>(), r_off,
@@ -749,6 +865,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     }
     if (world > 1) return e->fail(PS_E_STATE, "multi-GPU frontier outlived the planned rounds");
     planned = r + 8;  // live mask lengthened a mesh path beyond the BFS depth
+  }
   }
   HIP_TRY(hipEventRecord(e->ev_run1, s), "event");
   HIP_TRY(hipEventSynchronize(e->ev_run1), "sync");
@@ -884,6 +1001,7 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_EXPAND_BPC")) bpc = std::max(1, std::atoi(v));
   e->expand_grid = e->n_cus * bpc;
   if (const char* v = std::getenv("PSAMD_NO_SINGLE_START")) e->no_single_start = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_NO_LEVEL")) e->no_level = std::atoi(v) != 0;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess) {
     delete e;

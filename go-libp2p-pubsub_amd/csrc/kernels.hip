@@ -140,6 +140,7 @@ __global__ __launch_bounds__(kBlock) void k_seed(const SeedDev* __restrict__ see
   const SeedDev s = seeds[i];
   arrivals[s.woff] |= s.mask;
   seen[s.woff] |= s.mask;
+  if (next_flag == nullptr) return;  // level mode: the root is scheduled statically
   next_flag[s.node] = 1;
   blk_flag[s.node >> kFlagBlockShift] = 1;
 }
@@ -400,7 +401,12 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
 // kDirect = false: the staged path only (entries that need the direct path
 // are left to the second instance); kDirect = true: the direct path only.
 // Separate instances keep the hot staged kernel's register budget small.
-template <bool kRecord, bool kDirect>
+// kLevel = true (staged only): the frontier is the round's static level
+// schedule (live internal nodes of one BFS level per topic, single-start
+// tree windows); an entry the window's messages did not reach (generation
+// stale: a non-live ancestor) is skipped, and no frontier flags are raised
+// because the next round's frontier is known already.
+template <bool kRecord, bool kDirect, bool kLevel>
 __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round) {
   __shared__ WaveStage stage_lds[kDirect ? 1 : kBlock / 64];
   const uint32_t lane = threadIdx.x & 63;
@@ -429,6 +435,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
       bwl = static_cast<uint32_t>(T.wbase);
       bwh = static_cast<uint32_t>(T.wbase >> 32);
       if (bdeg && T.W) bc0 = a.col[brs];
+      if (kLevel && a.gen[bp] != cur) bW = bdeg = 0;  // not reached this window
     }
     const uint32_t nb = static_cast<uint32_t>(__popcll(__ballot(el < n)));
     uint32_t q = 0;
@@ -537,7 +544,8 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
                   }
                 }
               }
-              if (internal && __ballot(any) && lane == 0) mark_next(a, c);
+              if constexpr (!kLevel)
+                if (internal && __ballot(any) && lane == 0) mark_next(a, c);
             }
           } else {
             const uint32_t sh = pow2_shift(W);
@@ -565,8 +573,10 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
                 nm = deliver_word<kRecord>(a, false, stale, keep && (f & kNodeInternal), cw, m,
                                            round, k);
               }
-              const uint64_t bal = __ballot(nm != 0);
-              if (live && w == 0 && (f & kNodeInternal) && (bal & gmask)) mark_next(a, c);
+              if constexpr (!kLevel) {
+                const uint64_t bal = __ballot(nm != 0);
+                if (live && w == 0 && (f & kNodeInternal) && (bal & gmask)) mark_next(a, c);
+              }
             }
           }
           // live children hold current rows now
@@ -663,6 +673,39 @@ __global__ __launch_bounds__(kBlock) void k_apply(ApplyArgs a, uint32_t round) {
 }
 
 // ------------------------------------------------------------ compaction ---
+// One block folds the expand kernel's per-wave counters [w0, w1) into one
+// round's statistics.
+__device__ __forceinline__ void block_reduce_ctrs(const uint64_t* __restrict__ partials,
+                                                  uint32_t w0, uint32_t w1,
+                                                  uint64_t* __restrict__ out) {
+  __shared__ uint64_t red[kNumCtr][kBlock / 64];
+  uint64_t acc[kNumCtr];
+#pragma unroll
+  for (int k = 0; k < kNumCtr; ++k) acc[k] = 0;
+  for (uint32_t w = w0 + threadIdx.x; w < w1; w += kBlock)
+#pragma unroll
+    for (int k = 0; k < kNumCtr; ++k) acc[k] += partials[static_cast<uint64_t>(w) * kNumCtr + k];
+#pragma unroll
+  for (int k = 0; k < kNumCtr; ++k) {
+    uint64_t s = wave_sum_u64(acc[k]);
+    if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < kNumCtr) {
+    uint64_t s = 0;
+    for (int i = 0; i < kBlock / 64; ++i) s += red[threadIdx.x][i];
+    out[threadIdx.x] = s;
+  }
+}
+
+// Level mode: one block per round q = blockIdx.x + 1.
+__global__ __launch_bounds__(kBlock) void k_reduce_rounds(const uint64_t* __restrict__ partials,
+                                                          const uint32_t* __restrict__ woff,
+                                                          uint64_t* __restrict__ round_stats) {
+  const uint32_t q = blockIdx.x + 1;
+  block_reduce_ctrs(partials, woff[q], woff[q + 1], round_stats + static_cast<uint64_t>(q) * kNumCtr);
+}
+
 // Pass 1: per-block count of flagged nodes (16 one-byte flags per lane, one
 // 16-B load); blocks whose blk_flag byte is clear exit at once.  Block 0 also
 // folds the expand kernel's per-wave counters into this round's statistics.
@@ -673,26 +716,7 @@ __global__ __launch_bounds__(kBlock) void k_flag_count(const uint8_t* __restrict
                                                        const uint64_t* __restrict__ partials,
                                                        uint32_t n_waves,
                                                        uint64_t* __restrict__ round_stats) {
-  if (blockIdx.x == 0 && round_stats != nullptr) {
-    __shared__ uint64_t red[kNumCtr][kBlock / 64];
-    uint64_t acc[kNumCtr];
-#pragma unroll
-    for (int k = 0; k < kNumCtr; ++k) acc[k] = 0;
-    for (uint32_t w = threadIdx.x; w < n_waves; w += kBlock)
-#pragma unroll
-      for (int k = 0; k < kNumCtr; ++k) acc[k] += partials[static_cast<uint64_t>(w) * kNumCtr + k];
-#pragma unroll
-    for (int k = 0; k < kNumCtr; ++k) {
-      uint64_t s = wave_sum_u64(acc[k]);
-      if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = s;
-    }
-    __syncthreads();
-    if (threadIdx.x < kNumCtr) {
-      uint64_t s = 0;
-      for (int i = 0; i < kBlock / 64; ++i) s += red[threadIdx.x][i];
-      round_stats[threadIdx.x] = s;
-    }
-  }
+  if (blockIdx.x == 0 && round_stats != nullptr) block_reduce_ctrs(partials, 0, n_waves, round_stats);
   if (blk_flag[blockIdx.x] == 0) {
     if (threadIdx.x == 0) wg_count[blockIdx.x] = 0;
     return;
@@ -813,21 +837,33 @@ hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t*
   return hipGetLastError();
 }
 
-hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid,
-                         hipStream_t s) {
-  if (record)
-    hipLaunchKernelGGL((k_expand<true, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
+hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, bool level,
+                         uint32_t grid, hipStream_t s) {
+  if (record && level)
+    hipLaunchKernelGGL((k_expand<true, false, true>), dim3(grid), dim3(kBlock), 0, s, a, round);
+  else if (record)
+    hipLaunchKernelGGL((k_expand<true, false, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
+  else if (level)
+    hipLaunchKernelGGL((k_expand<false, false, true>), dim3(grid), dim3(kBlock), 0, s, a, round);
   else
-    hipLaunchKernelGGL((k_expand<false, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
+    hipLaunchKernelGGL((k_expand<false, false, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
   return hipGetLastError();
 }
 
 hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid,
                                 hipStream_t s) {
   if (record)
-    hipLaunchKernelGGL((k_expand<true, true>), dim3(grid), dim3(kBlock), 0, s, a, round);
+    hipLaunchKernelGGL((k_expand<true, true, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
   else
-    hipLaunchKernelGGL((k_expand<false, true>), dim3(grid), dim3(kBlock), 0, s, a, round);
+    hipLaunchKernelGGL((k_expand<false, true, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
+  return hipGetLastError();
+}
+
+hipError_t launch_reduce_rounds(const uint64_t* partials, const uint32_t* woff, uint32_t n_rounds,
+                                uint64_t* round_stats, hipStream_t s) {
+  if (n_rounds == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_reduce_rounds, dim3(n_rounds), dim3(kBlock), 0, s, partials, woff,
+                     round_stats);
   return hipGetLastError();
 }
 

@@ -142,10 +142,18 @@ hipError_t launch_init_nodes(const uint32_t* nodes, uint32_t n, const uint16_t* 
                              const TopicDev* topics, uint64_t* seen, uint64_t* a0, uint64_t* a1,
                              uint8_t* gen, uint32_t gen_cur, hipStream_t s);
 hipError_t launch_apply(const ApplyArgs& a, uint32_t round, bool record, hipStream_t s);
+// next_flag / blk_flag may be null (level mode: the root is in the schedule)
 hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t* arrivals,
                        uint64_t* seen, uint8_t* next_flag, uint8_t* blk_flag, hipStream_t s);
-hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid,
-                         hipStream_t s);
+// level = true: the frontier is a static level schedule (every entry a live
+// internal node of the round's BFS level): entries not reached this window
+// (stale generation) are skipped and no frontier flags are raised.
+hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, bool level,
+                         uint32_t grid, hipStream_t s);
+// Level mode: round q's counters = sum of the per-wave partials
+// [woff[q], woff[q+1]) for q = 1..n_rounds.
+hipError_t launch_reduce_rounds(const uint64_t* partials, const uint32_t* woff, uint32_t n_rounds,
+                                uint64_t* round_stats, hipStream_t s);
 // second instance: entries the staged kernel leaves (mesh, split, wide rows,
 // fan-out > 64); writes the same counters to partials + n_waves*kNumCtr
 hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid,
