@@ -109,6 +109,8 @@ struct ps_engine {
   uint32_t n_cus = 256, expand_grid = 2048;
   bool no_single_start = false;  // PSAMD_NO_SINGLE_START=1: keep arrival rows (A/B)
   bool no_level = false;         // PSAMD_NO_LEVEL=1: always compact the frontier (A/B)
+  bool level_push = false;       // PSAMD_LEVEL_PUSH=1: level mode with the push kernel (A/B)
+  uint32_t pull_words = kPullWords;  // words per pull chunk (PSAMD_PULL_WORDS)
 
   std::vector<TopicHost> topics;
   std::vector<uint8_t> live;
@@ -119,14 +121,20 @@ struct ps_engine {
   std::vector<uint64_t> sched_key;  // (epochs, rounds, per-topic start) it was built for
   std::vector<uint32_t> sched_host, sched_off, sched_cnt, woff_host;
   DevBuf d_sched, d_sched_cnt, d_woff;
+  // level mode, pull direction: per-round chunks of next-level nodes
+  std::vector<uint64_t> pull_key;
+  std::vector<PullChunk> pull_host;
+  std::vector<uint32_t> pull_off;
+  DevBuf d_pull, d_scratch;
 
   // fused node space (host mirror)
   uint32_t n_nodes = 0, n_pad = 16;
   std::vector<uint32_t> node_peer, row_ptr, col;
+  std::vector<uint32_t> node_parent;  // node-space parent on this rank (kNone: root / remote)
   std::vector<uint16_t> node_topic;
   std::vector<uint8_t> node_flags;
 
-  DevBuf d_row_ptr, d_col, d_node_topic, d_node_flags, d_node_peer;
+  DevBuf d_row_ptr, d_col, d_node_topic, d_node_flags, d_node_peer, d_node_parent;
   DevBuf d_seen, d_arr0, d_arr1, d_hop, d_flags, d_blk, d_gen, d_frontier, d_nfront, d_wgcount,
       d_partials, d_stats, d_topics, d_seeds, d_digest;
   uint32_t gen_cur = 0;  // window generation stamped into d_gen (1..255)
@@ -265,6 +273,7 @@ int build_graph(ps_engine* e) {
   const uint32_t n = e->cfg.n_peers;
   const int32_t world = e->world, me = e->rank;
   e->node_peer.clear();
+  e->node_parent.clear();
   e->node_topic.clear();
   e->row_ptr.assign(1, 0);
   e->col.clear();
@@ -360,6 +369,7 @@ int build_graph(ps_engine* e) {
       if (owner[u] != me) continue;
       ++n_own;
       e->node_peer.push_back(p);
+      e->node_parent.push_back(u && owner[bfs_parent[u]] == me ? T.nbase + loc[bfs_parent[u]] : kNone);
       e->node_topic.push_back(static_cast<uint16_t>(t));
       for (uint32_t k = rp[p]; k < rp[p + 1]; ++k) {
         const uint32_t v = local[cl[k]];
@@ -416,6 +426,7 @@ int upload_graph(ps_engine* e) {
     HIP_TRY(e->d_col.ensure(std::max<size_t>(e->col.size(), 1) * 4), "alloc col");
     HIP_TRY(e->d_node_topic.ensure(std::max<size_t>(nn, 1) * 2), "alloc node_topic");
     HIP_TRY(e->d_node_peer.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_peer");
+    HIP_TRY(e->d_node_parent.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_parent");
     // padded to n_pad: the expand kernel stages flag bytes as whole dwords
     HIP_TRY(e->d_node_flags.ensure(e->n_pad + 16), "alloc node_flags");
     HIP_TRY(hipMemcpyAsync(e->d_row_ptr.p, e->row_ptr.data(), (nn + 1) * 4, hipMemcpyHostToDevice, e->stream),
@@ -428,6 +439,9 @@ int upload_graph(ps_engine* e) {
               "upload node_topic");
       HIP_TRY(hipMemcpyAsync(e->d_node_peer.p, e->node_peer.data(), nn * 4, hipMemcpyHostToDevice, e->stream),
               "upload node_peer");
+      HIP_TRY(hipMemcpyAsync(e->d_node_parent.p, e->node_parent.data(), nn * 4, hipMemcpyHostToDevice,
+                             e->stream),
+              "upload node_parent");
     }
     bool fresh = false;
     const size_t flag_bytes = static_cast<size_t>(ceil_div(e->n_pad, kFlagsPerBlock)) * kFlagsPerBlock;
@@ -516,6 +530,47 @@ int build_schedule(ps_engine* e, const std::vector<TopicDev>& tab,
   return PS_OK;
 }
 
+// Level mode, pull direction: round q writes the rows of
+// BFS level q - s_t of every active topic t (children pull from their
+// parents), cut into chunks of at most kPullMaxKids nodes and about
+// kPullWords words, one wave each.  Cached like the schedule.
+int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
+                      const std::vector<uint32_t>& tstart, uint32_t rounds) {
+  const uint32_t nt = static_cast<uint32_t>(e->topics.size());
+  std::vector<uint64_t> key{e->graph_epoch, rounds, e->pull_words};
+  for (uint32_t t = 0; t < nt; ++t) {
+    key.push_back(tab[t].W ? tstart[t] : ~0ull);
+    key.push_back(tab[t].W);
+  }
+  if (key == e->pull_key) return PS_OK;
+  e->pull_key.clear();
+  auto& C = e->pull_host;
+  auto& off = e->pull_off;
+  C.clear();
+  off.assign(rounds + 2, 0);
+  for (uint32_t q = 1; q <= rounds; ++q) {
+    off[q] = static_cast<uint32_t>(C.size());
+    for (uint32_t t = 0; t < nt; ++t) {
+      const TopicHost& T = e->topics[t];
+      const uint32_t W = tab[t].W;
+      if (W == 0 || q < tstart[t] + 1) continue;
+      const uint32_t d = q - tstart[t];  // level of the nodes written this round
+      if (d + 1 >= T.level_off.size()) continue;
+      const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, e->pull_words / W));
+      for (uint32_t u = T.level_off[d]; u < T.level_off[d + 1]; u += per)
+        C.push_back(PullChunk{T.nbase + u, T.nbase + std::min(u + per, T.level_off[d + 1]), t, 0});
+    }
+  }
+  off[rounds + 1] = static_cast<uint32_t>(C.size());
+  HIP_TRY(e->d_pull.ensure(std::max<size_t>(C.size(), 1) * sizeof(PullChunk)), "alloc pull chunks");
+  if (!C.empty())
+    HIP_TRY(hipMemcpyAsync(e->d_pull.p, C.data(), C.size() * sizeof(PullChunk),
+                           hipMemcpyHostToDevice, e->stream),
+            "upload pull chunks");
+  e->pull_key = key;
+  return PS_OK;
+}
+
 // Propagates one window: per topic t, win[t] lists the messages (indices into
 // `msgs`) whose bits form t's block of W_t = ceil(|win[t]|/64) words.
 int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<WinSlice>& win,
@@ -557,7 +612,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     wtot = (wtot + 15) & ~15ull;  // topic blocks start on a 128-B line
     d.wbase = wtot;
     wtot += static_cast<uint64_t>(T.n_nodes) * d.W;
-    if (T.mesh || T.max_deg > 64 || d.W > kStageMaxWords) need_direct = true;
+    if (T.mesh || T.max_deg > 64) need_direct = true;
   }
   if (wtot == 0 && world == 1) return PS_OK;
   const bool record = (e->cfg.flags & PS_F_RECORD_HOPS) != 0;
@@ -633,20 +688,29 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   for (uint32_t t = 0; t < nt && level; ++t)
     if (tab[t].W && !(tab[t].flags & kTopicSingleStart)) level = false;
   std::vector<uint32_t> lgrid;  // level mode: expand grid of every round
+  const bool pull = level && !e->level_push;
   if (level) {
-    int rc2 = build_schedule(e, tab, tstart, planned0);
+    int rc2 = pull ? build_pull_chunks(e, tab, tstart, planned0)
+                   : build_schedule(e, tab, tstart, planned0);
     if (rc2) return rc2;
     lgrid.assign(planned0 + 1, 0);
     auto& woff = e->woff_host;
     woff.assign(planned0 + 2, 0);
     for (uint32_t q = 1; q <= planned0; ++q) {
-      const uint32_t cnt = e->sched_cnt[q];
-      lgrid[q] = cnt ? std::min<uint32_t>(e->expand_grid, ceil_div(cnt, 4)) : 0;  // >= 1 entry per wave
+      if (pull) {  // one wave per chunk, one partial slot per block
+        lgrid[q] = ceil_div(e->pull_off[q + 1] - e->pull_off[q], kBlock / 64);
+        woff[q + 1] = woff[q] + lgrid[q];
+        continue;
+      } else {
+        const uint32_t cnt = e->sched_cnt[q];
+        lgrid[q] = cnt ? std::min<uint32_t>(e->expand_grid, ceil_div(cnt, 4)) : 0;  // >= 1 entry per wave
+      }
       woff[q + 1] = woff[q] + lgrid[q] * (kBlock / 64);
     }
     HIP_TRY(e->d_partials.ensure(static_cast<size_t>(woff[planned0 + 1]) * kNumCtr * 8),
             "alloc level partials");
     HIP_TRY(e->d_woff.ensure(woff.size() * 4), "alloc wave offsets");
+    HIP_TRY(e->d_scratch.ensure(1024 * 1024), "alloc scratch");
   }
   // cross-rank capacities (items = node words) per round: cap[r][from*world+to]
   std::vector<std::vector<uint64_t>> cap;
@@ -794,7 +858,23 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       a.a_cur = arr[(r - 1) & 1];
       a.a_next = arr[r & 1];
       HIP_TRY(time_mark(true), "event");
-      if (lgrid[r]) {
+      if (lgrid[r] && pull) {
+        PullArgs pa{};
+        pa.node_parent = e->d_node_parent.as<uint32_t>();
+        pa.node_flags = a.node_flags;
+        pa.topics = a.topics;
+        pa.a_cur = a.a_cur;
+        pa.seen = a.seen;
+        pa.gen = a.gen;
+        pa.hop_rec = a.hop_rec;
+        pa.partials = partials + static_cast<size_t>(e->woff_host[r]) * kNumCtr;
+        pa.gen_cur = a.gen_cur;
+        pa.scratch = e->d_scratch.as<uint64_t>();
+        pa.dbg = a.dbg;
+        HIP_TRY(launch_pull(pa, e->d_pull.as<PullChunk>() + e->pull_off[r],
+                            e->pull_off[r + 1] - e->pull_off[r], r, record, s),
+                "pull");
+      } else if (lgrid[r]) {
         a.frontier = e->d_sched.as<uint32_t>() + e->sched_off[r];
         a.n_front = e->d_sched_cnt.as<uint32_t>() + r;
         a.partials = partials + static_cast<size_t>(e->woff_host[r]) * kNumCtr;
@@ -901,9 +981,14 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     // per entry word the arrival read 8 (+ 8 when cleared); per child its
     // flag byte + generation read/write (tree) or col id 4 (mesh); per
     // seen read / seen write / arrival write 8.
-    st->expand_bytes += c[kCtrEntries] * 18 + c[kCtrEntryWords] * 8 + c[kCtrClearWords] * 8 +
-                        c[kCtrChildren] * 3 + c[kCtrMeshChildren] * 4 + c[kCtrSeenReads] * 8 +
-                        c[kCtrSeenWrites] * 8 + c[kCtrArrivalWrites] * 8;
+    if (pull)  // pull model: per node parent id 4 + flag 1 + parent generation 1, per
+               // reached node its generation write 1; parent rows read once; rows written
+      st->expand_bytes += c[kCtrChildren] * 6 + c[kCtrMeshChildren] * 1 +
+                          c[kCtrEntryWords] * 8 + c[kCtrSeenWrites] * 8;
+    else
+      st->expand_bytes += c[kCtrEntries] * 18 + c[kCtrEntryWords] * 8 + c[kCtrClearWords] * 8 +
+                          c[kCtrChildren] * 3 + c[kCtrMeshChildren] * 4 + c[kCtrSeenReads] * 8 +
+                          c[kCtrSeenWrites] * 8 + c[kCtrArrivalWrites] * 8;
     if (q < PS_MAX_ROUNDS) {
       st->deliveries_per_round[q] += c[kCtrDeliveries] + app_d;
       st->frontier_per_round[q] += static_cast<uint32_t>(c[kCtrEntries]);
@@ -1002,6 +1087,8 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   e->expand_grid = e->n_cus * bpc;
   if (const char* v = std::getenv("PSAMD_NO_SINGLE_START")) e->no_single_start = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_NO_LEVEL")) e->no_level = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_LEVEL_PUSH")) e->level_push = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_PULL_WORDS")) e->pull_words = std::max(64, std::atoi(v));
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess) {
     delete e;

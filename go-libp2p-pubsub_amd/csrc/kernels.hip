@@ -388,6 +388,76 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
   }
 }
 
+// One tree entry whose row is wider than the stage (W > kStageWords, so W is
+// even and 16-B aligned): the row goes through the stage in slices of
+// kStageWords words, each slice stored to every live child before the next
+// is loaded.  The children's flag and generation bytes are read once, before
+// any store, so every slice sees the same staleness.
+template <bool kRecord, bool kLevel>
+__device__ void expand_wide(const ExpandArgs& a, WaveStage& ws, uint32_t p, uint32_t deg,
+                            uint32_t c0, uint32_t W, uint32_t nbase, uint32_t fl, uint64_t wbase,
+                            uint32_t lane, uint32_t cur, uint32_t round, ExpandCtr& k,
+                            EntryCtr& ec) {
+  const bool is_root = p == nbase && (fl & kTopicRootLocal);
+  const bool from_seen = (fl & kTopicSingleStart) && !is_root;
+  const bool keep = !(fl & kTopicSingleStart);
+  const uint64_t pw = wbase + static_cast<uint64_t>(p - nbase) * W;
+  const uint64_t cbase = wbase - static_cast<uint64_t>(nbase) * W;
+  const uint32_t* row = reinterpret_cast<const uint32_t*>((from_seen ? a.seen : a.a_cur) + pw);
+  uint32_t fj = 0, gj = 0;
+  if (lane < deg) {  // deg <= 64
+    fj = a.node_flags[c0 + lane];
+    gj = a.gen[c0 + lane];
+  }
+  ec.ent += 1;
+  ec.ent_words += W;
+  ec.kids += deg;
+  uint64_t got = 0;  // bit j: child j received something
+  for (uint32_t w0 = 0; w0 < W; w0 += kStageWords) {
+    const uint32_t len = min(kStageWords, W - w0);  // even
+    uint32_t* dst = reinterpret_cast<uint32_t*>(ws.words);
+    for (uint32_t d = 0; d < 2 * len; d += 256)
+      if (d + 4 * lane < 2 * len) PSAMD_LDS_DMA(row + 2 * w0 + d + 4 * lane, dst + d, 16);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (uint32_t jj = 0; jj < deg; ++jj) {
+      const uint32_t f = rl(fj, jj);
+      if (!(f & kNodeLive)) continue;
+      const bool stale = rl(gj, jj) != cur;
+      const bool store = (f & kNodeInternal) && keep;
+      const uint64_t crow = cbase + static_cast<uint64_t>(c0 + jj) * W + w0;
+      bool any = false;
+      if (stale) {
+        for (uint32_t wb = 0; wb < len; wb += 128) {
+          const uint32_t w = wb + 2 * lane;
+          if (w < len) {
+            const uint4 v = *reinterpret_cast<const uint4*>(ws.words + w);
+            deliver_fresh2<kRecord>(a, store, crow + w, v, round, k);
+            any |= (v.x | v.y | v.z | v.w) != 0;
+          }
+        }
+      } else {
+        for (uint32_t wb = 0; wb < len; wb += 64) {
+          const uint32_t w = wb + lane;
+          if (w < len) {
+            const uint64_t nm =
+                deliver_word<kRecord>(a, false, false, store, crow + w, ws.words[w], round, k);
+            any |= nm != 0;
+          }
+        }
+      }
+      if (__ballot(any)) got |= 1ull << jj;
+    }
+  }
+  if constexpr (!kLevel)
+    if (lane < deg && (fj & kNodeInternal) && ((got >> lane) & 1ull)) mark_next(a, c0 + lane);
+  if (lane < deg && (fj & kNodeLive) && !(a.dbg & kDbgNoByteStores))
+    a.gen[c0 + lane] = static_cast<uint8_t>(cur);
+  if (is_root) {  // seeded with |=: consume-and-clear
+    for (uint32_t w = lane; w < W; w += 64) a.a_cur[pw + w] = 0;
+    ec.clear += W;
+  }
+}
+
 // Frontier entries are dealt to waves round-robin (entry e -> wave e mod
 // n_waves).  A wave loads the metadata of its next 64 entries into lane
 // registers (frontier id, row range, first child, topic fields) and
@@ -445,12 +515,19 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
         ++q;
         continue;
       }
-      const bool direct = (f0 & (kTopicMesh | kEntrySplit)) || W0 > kStageWords || d0 > 64;
+      const bool direct = (f0 & (kTopicMesh | kEntrySplit)) || d0 > 64;
       if (direct || kDirect) {
         if (direct && kDirect)
           expand_direct<kRecord>(a, rl(bp, q), rl(brs, q), d0, rl(bc0, q), W0, rl(bnb, q), f0,
                                  (static_cast<uint64_t>(rl(bwh, q)) << 32) | rl(bwl, q), lane,
                                  cur, round, k, ec);
+        ++q;
+        continue;
+      }
+      if (W0 > kStageWords) {  // wide row: staged slice by slice
+        expand_wide<kRecord, kLevel>(a, ws, rl(bp, q), d0, rl(bc0, q), W0, rl(bnb, q), f0,
+                                     (static_cast<uint64_t>(rl(bwh, q)) << 32) | rl(bwl, q), lane,
+                                     cur, round, k, ec);
         ++q;
         continue;
       }
@@ -481,8 +558,18 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
           const uint32_t* row = reinterpret_cast<const uint32_t*>(
               (from_seen ? a.seen : a.a_cur) + wbase + static_cast<uint64_t>(p - nbase) * W);
           uint32_t* dst = reinterpret_cast<uint32_t*>(ws.words + off);
-          for (uint32_t d = 0; d < 2 * W; d += 64)
-            if (d + lane < 2 * W) PSAMD_LDS_DMA(row + d + lane, dst + d, 4);
+          if (a.dbg & kDbgNoArrivalLoad) {
+            // experiment: no row loads (the words are set to all-ones below)
+          } else if ((W & 1u) == 0) {
+            // even W: the row and its stage slot are 16-B aligned (topic
+            // blocks start on 128-B lines, slots keep even offsets): one
+            // dwordx4 DMA per lane, 1 KiB per wave instruction
+            for (uint32_t d = 0; d < 2 * W; d += 256)
+              if (d + 4 * lane < 2 * W) PSAMD_LDS_DMA(row + d + 4 * lane, dst + d, 16);
+          } else {
+            for (uint32_t d = 0; d < 2 * W; d += 64)
+              if (d + lane < 2 * W) PSAMD_LDS_DMA(row + d + lane, dst + d, 4);
+          }
           const uint32_t nd = ((c0 + deg + 3u) >> 2) - (c0 >> 2);
           if (lane < nd) {
             PSAMD_LDS_DMA(reinterpret_cast<const uint32_t*>(a.node_flags) + (c0 >> 2) + lane,
@@ -612,6 +699,218 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
     out[kCtrSeenWrites] = s_sw;
     out[kCtrArrivalWrites] = s_aw;
     out[kCtrClearWords] = ec.clear;
+  }
+}
+
+// ------------------------------------------------------------------ pull ---
+// Level mode, pull direction.  In a single-start tree
+// window a node of BFS level d receives, in round s + d, exactly its parent's
+// arrival set -- if the parent was reached and the node is live -- and it is
+// fresh (it has seen nothing this window), so the seen test-and-set is
+// new = arrival(parent) & ~0 and the whole row is written.  This kernel runs
+// that step child-parallel (the bottom-up direction of BFS): a wave owns a
+// contiguous run of next-level nodes, whose rows form one contiguous output
+// stream, and
+//   phase 1  resolves each node's source into a wave-private LDS table: its
+//            parent if the parent is in the frontier (generation current:
+//            reached this window) and the node is live, else none; the node's
+//            generation is stamped;
+//   phase 2  streams the run's rows in order with 16-B stores, each lane's
+//            16-B load taken from its node's parent row (siblings read the
+//            same parent row: L2 hits).  Loads are unconditional (a skipped
+//            node reads its own row) so the unrolled body keeps several in
+//            flight; only the stores are predicated.
+// Counters: deliveries, seen writes, nodes visited, nodes reached, parents
+// expanded (a reached parent counts at its first child) and their row words.
+__device__ __forceinline__ uint32_t popc4(uint4 v) {
+  return __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
+}
+
+template <bool kRecord>
+__device__ __forceinline__ void record_word(uint8_t* hop_rec, uint64_t cw, uint64_t m,
+                                            uint32_t round) {
+  uint8_t* h = hop_rec + cw * 64;
+  while (m) {
+    const int q = __ffsll(static_cast<long long>(m)) - 1;
+    h[q] = static_cast<uint8_t>(round);
+    m &= m - 1;
+  }
+}
+
+struct PullVec {
+  bool go;
+  uint4 v;
+};
+
+template <bool kRecord>
+__global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __restrict__ chunks,
+                                                 uint32_t n_chunks, uint32_t round) {
+  __shared__ uint32_t src_lds[kBlock / 64][kPullMaxKids];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wave = blockIdx.x * (kBlock / 64) + wid;
+  uint32_t* src = src_lds[wid];
+  const uint32_t cur = a.gen_cur & 0xFF;
+  uint64_t deliv = 0;
+  uint32_t sw = 0, kids = 0, reached = 0, parents = 0, pwords = 0;
+  if (wave < n_chunks) {
+    const PullChunk ch = chunks[wave];
+    const TopicDev T = a.topics[ch.topic];
+    const uint32_t W = T.W;
+    const uint32_t nb = ch.node_begin, nk = ch.node_end - ch.node_begin;
+    const uint64_t base = T.wbase - static_cast<uint64_t>(T.nbase) * W;  // row of u: base + u*W
+    const uint32_t root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
+    // phase 1: source table
+    for (uint32_t j0 = 0; j0 < nk; j0 += 64) {
+      const uint32_t j = j0 + lane;
+      const bool in = j < nk;
+      uint32_t p = kNoneNode, f = 0;
+      if (in) {
+        p = a.node_parent[nb + j];
+        f = a.node_flags[nb + j];
+      }
+      uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
+      if (lane == 0) prev = nb + j0 > T.nbase ? a.node_parent[nb + j0 - 1] : kNoneNode;
+      bool up = false;  // the parent was reached this window
+      if (in && p != kNoneNode) up = a.gen[p] == cur;
+      const bool ok = up && (f & kNodeLive);
+      if (in) src[j] = ok ? p : kNoneNode;
+      if (ok && !(a.dbg & kDbgNoByteStores)) a.gen[nb + j] = static_cast<uint8_t>(cur);
+      kids += in;
+      reached += ok;
+      if (up && p != prev) {
+        parents += 1;
+        pwords += W;
+      }
+    }
+    // phase 2: the run's rows as one output stream (LDS ops of a wave are
+    // processed in order: the table is visible to the reads below)
+    const uint32_t total = nk * W;
+    uint64_t* const out = a.seen + base + static_cast<uint64_t>(nb) * W;
+    if (!(W & 1u)) {
+      // even W: every row 16-B aligned, a 2-word pair never straddles rows
+      const float rw = 1.0f / static_cast<float>(W);
+      auto one = [&](uint32_t i, bool valid) {
+        // row kk = i / W and word r of the run, branch-free (float estimate
+        // off by at most one; i < 2^24)
+        int32_t kk = static_cast<int32_t>(static_cast<float>(i) * rw);
+        int32_t r = static_cast<int32_t>(i) - kk * static_cast<int32_t>(W);
+        const int32_t lo = r < 0, hi = r >= static_cast<int32_t>(W);
+        kk += hi - lo;
+        r += (lo - hi) * static_cast<int32_t>(W);
+        const uint32_t p = valid ? src[kk] : kNoneNode;
+        const bool go = p != kNoneNode;
+        // unconditional load: a skipped lane reads its own output row
+        const uint64_t* s = go ? (p == root ? a.a_cur : a.seen) + base + static_cast<uint64_t>(p) * W + r
+                               : out + (valid ? i : 0);
+        const uint4 v = *reinterpret_cast<const uint4*>(s);
+        return PullVec{go, v};
+      };
+      uint32_t i0 = 0;
+      if constexpr (!kRecord) {
+        // 8 loads in flight, then 8 stores, all unconditional and branch-free
+        // (a skipped lane writes its own row back unchanged; a lane past the
+        // run's end reads the run's first word and writes a scratch slot), so
+        // the compiler counts vmcnt exactly instead of draining at branches
+        constexpr uint32_t kU = 8;
+        uint64_t* const dummy = a.scratch + static_cast<uint64_t>(wave & 1023u) * 128;
+        for (; i0 < total; i0 += kU * 128) {
+          PullVec x[kU];
+#pragma unroll
+          for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t i = i0 + u * 128 + 2 * lane;
+            x[u] = one(i, i < total);
+          }
+#pragma unroll
+          for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t i = i0 + u * 128 + 2 * lane;
+            uint64_t* const dst = i < total ? out + i : dummy + 2 * lane;
+            *reinterpret_cast<uint4*>(dst) = x[u].v;
+            deliv += x[u].go ? popc4(x[u].v) : 0u;
+            sw += x[u].go ? 2u : 0u;
+          }
+        }
+      }
+      for (; i0 < total; i0 += 128) {
+        const uint32_t i = i0 + 2 * lane;
+        const auto x = one(i, i < total);
+        if (x.go) {
+          if (!(a.dbg & kDbgNoSeenStore)) *reinterpret_cast<uint4*>(out + i) = x.v;
+          deliv += popc4(x.v);
+          sw += 2;
+          if constexpr (kRecord) {
+            const uint64_t cw = (out - a.seen) + i;
+            record_word<kRecord>(a.hop_rec, cw, static_cast<uint64_t>(x.v.y) << 32 | x.v.x, round);
+            record_word<kRecord>(a.hop_rec, cw + 1, static_cast<uint64_t>(x.v.w) << 32 | x.v.z, round);
+          }
+        }
+      }
+    } else {
+      // odd W: one word (8 B) per lane, the same branch-free pipeline
+      const float rw = 1.0f / static_cast<float>(W);
+      auto one1 = [&](uint32_t i, bool valid, bool& go) -> uint64_t {
+        int32_t kk = static_cast<int32_t>(static_cast<float>(i) * rw);
+        int32_t r = static_cast<int32_t>(i) - kk * static_cast<int32_t>(W);
+        const int32_t lo = r < 0, hi = r >= static_cast<int32_t>(W);
+        kk += hi - lo;
+        r += (lo - hi) * static_cast<int32_t>(W);
+        const uint32_t p = valid ? src[kk] : kNoneNode;
+        go = p != kNoneNode;
+        const uint64_t* s = go ? (p == root ? a.a_cur : a.seen) + base + static_cast<uint64_t>(p) * W + r
+                               : out + (valid ? i : 0);
+        return *s;
+      };
+      constexpr uint32_t kU = 8;
+      uint64_t* const dummy = a.scratch + static_cast<uint64_t>(wave & 1023u) * 128;
+      for (uint32_t i0 = 0; i0 < total; i0 += kU * 64) {
+        uint64_t m[kU];
+        bool go[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+          const uint32_t i = i0 + u * 64 + lane;
+          m[u] = one1(i, i < total, go[u]);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+          const uint32_t i = i0 + u * 64 + lane;
+          if constexpr (kRecord) {
+            if (go[u] && i < total) {
+              out[i] = m[u];
+              record_word<kRecord>(a.hop_rec, (out - a.seen) + i, m[u], round);
+            }
+          } else {
+            *(i < total ? out + i : dummy + lane) = m[u];
+          }
+          deliv += go[u] ? __popcll(m[u]) : 0u;
+          sw += go[u] ? 1u : 0u;
+        }
+      }
+    }
+  }
+  // block-level counters: one partial slot per block (fewer for the reduce)
+  __shared__ uint64_t red[kBlock / 64][6];
+  const uint64_t v6[6] = {wave_sum_u64(deliv), wave_sum_u64(sw), wave_sum_u64(kids),
+                          wave_sum_u64(reached), wave_sum_u64(parents), wave_sum_u64(pwords)};
+  if (lane == 0)
+#pragma unroll
+    for (int q = 0; q < 6; ++q) red[wid][q] = v6[q];
+  __syncthreads();
+  if (threadIdx.x < kNumCtr) {
+    uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+    for (int w = 0; w < kBlock / 64; ++w)
+#pragma unroll
+      for (int q = 0; q < 6; ++q) t[q] += red[w][q];
+    uint64_t v = 0;
+    switch (threadIdx.x) {
+      case kCtrDeliveries: v = t[0]; break;
+      case kCtrEntries: v = t[4]; break;
+      case kCtrEntryWords: v = t[5]; break;
+      case kCtrChildren: v = t[2]; break;
+      case kCtrMeshChildren: v = t[3]; break;  // pull mode: nodes reached (generation writes)
+      case kCtrSeenWrites: v = t[1]; break;
+      default: v = 0;
+    }
+    a.partials[static_cast<uint64_t>(blockIdx.x) * kNumCtr + threadIdx.x] = v;
   }
 }
 
@@ -856,6 +1155,17 @@ hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record
     hipLaunchKernelGGL((k_expand<true, true, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
   else
     hipLaunchKernelGGL((k_expand<false, true, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
+  return hipGetLastError();
+}
+
+hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
+                       uint32_t round, bool record, hipStream_t s) {
+  if (n_chunks == 0) return hipSuccess;
+  const uint32_t grid = (n_chunks + kBlock / 64 - 1) / (kBlock / 64);
+  if (record)
+    hipLaunchKernelGGL(k_pull<true>, dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
+  else
+    hipLaunchKernelGGL(k_pull<false>, dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
   return hipGetLastError();
 }
 

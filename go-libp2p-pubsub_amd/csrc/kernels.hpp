@@ -105,6 +105,30 @@ struct ExpandArgs {
   uint64_t send_off[kMaxRanks];   // byte offset of the region for each rank
 };
 
+// Level mode, pull direction: one wave copies the parents' rows into the
+// rows of a contiguous run of next-level nodes [node_begin, node_end) of one
+// topic (at most kPullMaxKids nodes, about kPullWords words).
+struct PullChunk {
+  uint32_t node_begin, node_end, topic, pad;
+};
+constexpr uint32_t kPullMaxKids = 512;
+constexpr uint32_t kNoneNode = 0xFFFFFFFFu;
+constexpr uint32_t kPullWords = 1024;  // default; PSAMD_PULL_WORDS overrides
+
+struct PullArgs {
+  const uint32_t* node_parent;  // node-space parent (kNone for roots)
+  const uint8_t* node_flags;
+  const TopicDev* topics;
+  const uint64_t* a_cur;  // arrivals of round-1 (topic roots' seeded rows)
+  uint64_t* seen;
+  uint8_t* gen;
+  uint8_t* hop_rec;
+  uint64_t* partials;  // [n_blocks][kNumCtr]
+  uint64_t* scratch;   // 1024 x 1 KiB: stores of lanes past a run's end
+  uint32_t gen_cur;
+  uint32_t dbg;
+};
+
 struct ApplyArgs {
   const uint8_t* recv;
   uint64_t recv_off[kMaxRanks];  // region from each rank
@@ -150,6 +174,9 @@ hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t*
 // (stale generation) are skipped and no frontier flags are raised.
 hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, bool level,
                          uint32_t grid, hipStream_t s);
+// Level mode, pull direction: one wave per chunk (grid = ceil(n_chunks / 4)).
+hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
+                       uint32_t round, bool record, hipStream_t s);
 // Level mode: round q's counters = sum of the per-wave partials
 // [woff[q], woff[q+1]) for q = 1..n_rounds.
 hipError_t launch_reduce_rounds(const uint64_t* partials, const uint32_t* woff, uint32_t n_rounds,

@@ -73,6 +73,30 @@ def test_tree_parity_random(seed, eager):
         assert st.duplicates == 0
 
 
+@pytest.mark.parametrize("staggered", [False, True])
+def test_wide_rows_parity(staggered):
+    """Rows wider than the expand kernel's LDS stage (W > 704 words): staged
+    slice by slice (expand_wide); single-start (level mode) and staggered."""
+    rng = np.random.default_rng(40 + staggered)
+    n = 600
+    parent = random_tree(rng, n, 3)
+    live = (rng.random(n) > 0.1).astype(np.uint8)
+    n_msgs = 64 * 800 + 17  # W = 801 words: two slices
+    starts = rng.integers(0, 3, size=n_msgs) if staggered else None
+    with PE.Engine(n, 1, record_hops=True) as eng:
+        eng.set_tree(0, 3, parent)
+        eng.set_live(live)
+        first = eng.publish(np.zeros(n_msgs), starts)
+        st = eng.run()
+        rp, cl = O.parents_to_csr(parent)
+        # every message floods the same tree: hop = depth below the root
+        _, hops, _ = O.disseminate(rp, cl, 3, live, 1)
+        for m in list(range(0, n_msgs, 97)) + [n_msgs - 1]:
+            assert np.array_equal(eng.hops(first + m), hops[0]), m
+        assert st.deliveries == n_msgs * int((hops[0] != 0xFF).sum())
+        assert st.duplicates == 0
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_mesh_parity_dedup(seed):
     rng = np.random.default_rng(100 + seed)

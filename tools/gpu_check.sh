@@ -1,6 +1,6 @@
 #!/bin/bash
-# One GPU session: parity tests, bench A/B, kernel-trace profile.
-#   tools/gpu_check.sh <tag> [pytest -k expr]
+# One GPU session: parity tests, bench, optional A/B, kernel trace, PMC passes.
+#   [AB="ENV=1 ..."] [PMC=1] [TRACE=0] [TESTS=0] [BENCH_ARGS=...] tools/gpu_check.sh <tag> [pytest -k expr]
 # Every GPU step has its own time limit; the script stops at the first
 # failure (set -e), so nothing runs on the GPU after a fault or a timeout.
 set -euo pipefail
@@ -8,24 +8,44 @@ TAG=${1:-x}
 KEXPR=${2:-}
 ROOT=${GRAFT_REPO_ROOT:-/root/repo}
 OUT=$ROOT/gpurun_out/$TAG
+BARGS=${BENCH_ARGS:-}
 mkdir -p "$OUT"
 cd "$ROOT"
-echo "[gpu_check] tests $(date +%T)"
-if [ -n "$KEXPR" ]; then
-  timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -k "$KEXPR" > "$OUT/pytest.log" 2>&1
-else
-  timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > "$OUT/pytest.log" 2>&1
+if [ "${TESTS:-1}" = 1 ]; then
+  echo "[gpu_check] tests $(date +%T)"
+  KARGS=()
+  [ -n "$KEXPR" ] && KARGS=(-k "$KEXPR")
+  timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread "${KARGS[@]}" > "$OUT/pytest.log" 2>&1
+  tail -2 "$OUT/pytest.log"
 fi
-tail -3 "$OUT/pytest.log"
 echo "[gpu_check] bench $(date +%T)"
-timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 $BARGS > "$OUT/bench.json" 2> "$OUT/bench.err"
 cat "$OUT/bench.json"
-echo "[gpu_check] bench A/B (PSAMD_NO_LEVEL=1) $(date +%T)"
-PSAMD_NO_LEVEL=1 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu > "$OUT/bench_nolevel.json" 2> "$OUT/bench_nolevel.err"
-cat "$OUT/bench_nolevel.json"
-echo "[gpu_check] trace $(date +%T)"
+if [ -n "${AB:-}" ]; then
+  echo "[gpu_check] bench A/B ($AB) $(date +%T)"
+  env $AB timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu $BARGS > "$OUT/bench_ab.json" 2> "$OUT/bench_ab.err"
+  cat "$OUT/bench_ab.json"
+fi
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- \
-  python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err"
-find "$OUT/trace" -name "*kernel_stats.csv" -exec cat {} \;
+if [ "${TRACE:-1}" = 1 ]; then
+  echo "[gpu_check] trace $(date +%T)"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- \
+    python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu $BARGS > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err"
+  find "$OUT/trace" -name "*kernel_stats.csv" -exec cat {} \;
+fi
+if [ "${PMC:-0}" = 1 ]; then
+  for C in FETCH_SIZE WRITE_SIZE; do
+    echo "[gpu_check] pmc $C $(date +%T)"
+    timeout -s KILL 180 rocprofv3 --pmc $C -f csv -d "$OUT/pmc_$C" -o run -- \
+      python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu $BARGS > "$OUT/pmc_$C.json" 2> "$OUT/pmc_$C.err"
+  done
+  python3 "$ROOT/tools/pmc_summary.py" "$OUT" > "$OUT/pmc_summary.json"
+  python3 - "$OUT/pmc_summary.json" <<'EOF'
+import json, sys
+d = json.load(open(sys.argv[1]))
+for k, v in d.items():
+    if "k_expand" in k:
+        print(k[:60], {x: v.get(x) for x in ("hbm_read_bytes_per_dispatch_x2", "hbm_write_bytes_per_dispatch")})
+EOF
+fi
 echo "[gpu_check] done $(date +%T)"
