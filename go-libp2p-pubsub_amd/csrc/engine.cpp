@@ -109,6 +109,8 @@ struct ps_engine {
   uint32_t n_cus = 256, expand_grid = 2048;
   bool no_single_start = false;  // PSAMD_NO_SINGLE_START=1: keep arrival rows (A/B)
   bool no_level = false;         // PSAMD_NO_LEVEL=1: always compact the frontier (A/B)
+  bool host_timing = false;      // PSAMD_HOST_TIMING=1: host phase times to stderr
+  std::chrono::steady_clock::time_point t_run0;
   bool level_push = false;       // PSAMD_LEVEL_PUSH=1: level mode with the push kernel (A/B)
   uint32_t pull_words = kPullWords;  // words per pull chunk (PSAMD_PULL_WORDS)
 
@@ -149,6 +151,8 @@ struct ps_engine {
 
   // publishes not yet run
   std::vector<RunMsg> pending;
+  bool pending_nonzero_start = false;  // some pending message starts after round 0
+  bool run_zero_start = true;          // every message of the current run starts in round 0
   uint32_t next_msg = 0;
 
   // results of the last run
@@ -579,6 +583,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   if (rc) return rc;
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
   const int32_t world = e->world, me = e->rank;
+  const auto t_w0 = std::chrono::steady_clock::now();
   std::vector<TopicDev> tab(std::max<uint32_t>(nt, 1));
   uint64_t wtot = 0;
   uint32_t max_depth = 0, max_start = 0;
@@ -595,10 +600,11 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     // every rank plans the same rounds: global depth, global start rounds
     max_depth = std::max(max_depth, T.depth);
     bool one_start = true;
-    for (uint32_t li = 0; li < win[t].n; ++li) {
-      max_start = std::max(max_start, msgs[win[t].idx[li]].start);
-      one_start &= msgs[win[t].idx[li]].start == msgs[win[t].idx[0]].start;
-    }
+    if (!e->run_zero_start)  // else: every message of the run starts in round 0
+      for (uint32_t li = 0; li < win[t].n; ++li) {
+        max_start = std::max(max_start, msgs[win[t].idx[li]].start);
+        one_start &= msgs[win[t].idx[li]].start == msgs[win[t].idx[0]].start;
+      }
     // a tree topic whose window messages share one start round: every node
     // receives once, so arrival rows are its seen rows (kTopicSingleStart)
     if (one_start && !T.mesh && !e->no_single_start) d.flags |= kTopicSingleStart;
@@ -615,6 +621,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     if (T.mesh || T.max_deg > 64) need_direct = true;
   }
   if (wtot == 0 && world == 1) return PS_OK;
+  const auto t_w1 = std::chrono::steady_clock::now();
   const bool record = (e->cfg.flags & PS_F_RECORD_HOPS) != 0;
   HIP_TRY(e->d_seen.ensure(wtot * 8), "alloc seen");
   HIP_TRY(e->d_arr0.ensure(wtot * 8), "alloc arrivals");
@@ -637,8 +644,13 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     const TopicDev& d = tab[t];
     if (d.W == 0 || !(d.flags & kTopicRootLocal)) continue;
     inj[t].assign(static_cast<size_t>(max_start + 1) * d.W, 0);
-    for (uint32_t li = 0; li < win[t].n; ++li)
-      inj[t][static_cast<size_t>(msgs[win[t].idx[li]].start) * d.W + (li >> 6)] |= 1ull << (li & 63);
+    if (e->run_zero_start) {  // bits 0 .. n-1 of round 0
+      for (uint32_t w = 0; w < win[t].n / 64; ++w) inj[t][w] = ~0ull;
+      if (win[t].n % 64) inj[t][win[t].n / 64] = (1ull << (win[t].n % 64)) - 1;
+    } else {
+      for (uint32_t li = 0; li < win[t].n; ++li)
+        inj[t][static_cast<size_t>(msgs[win[t].idx[li]].start) * d.W + (li >> 6)] |= 1ull << (li & 63);
+    }
   }
   std::vector<SeedDev> seeds;
   std::vector<uint32_t> seed_off(max_start + 2, 0);
@@ -654,6 +666,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     seed_off[r + 1] = static_cast<uint32_t>(seeds.size());
   }
   HIP_TRY(e->d_seeds.ensure(seeds.size() * sizeof(SeedDev)), "alloc seeds");
+  const auto t_w2 = std::chrono::steady_clock::now();
 
   // Start rounds present per topic.  A node at BFS level d receives a
   // message started at round s in round s + d and is expanded in round
@@ -663,7 +676,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   for (uint32_t t = 0; t < nt; ++t) {
     if (win[t].n == 0 || !e->topics[t].exists) continue;
     starts_of[t].assign(max_start + 1, 0);
-    for (uint32_t li = 0; li < win[t].n; ++li) starts_of[t][msgs[win[t].idx[li]].start] = 1;
+    if (e->run_zero_start)
+      starts_of[t][0] = 1;
+    else
+      for (uint32_t li = 0; li < win[t].n; ++li) starts_of[t][msgs[win[t].idx[li]].start] = 1;
   }
   auto round_grid = [&](uint32_t r) -> uint32_t {
     if (any_mesh) return e->expand_grid;
@@ -740,6 +756,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     HIP_TRY(e->d_recv.ensure(max_recv), "alloc recv regions");
   }
 
+  const auto t_w3 = std::chrono::steady_clock::now();
   hipStream_t s = e->stream;
   HIP_TRY(hipMemcpyAsync(e->d_topics.p, tab.data(), tab.size() * sizeof(TopicDev),
                          hipMemcpyHostToDevice, s),
@@ -749,6 +766,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
                            hipMemcpyHostToDevice, s),
             "upload seeds");
   HIP_TRY(hipEventRecord(e->ev_run0, s), "event");
+  const auto t_first = std::chrono::steady_clock::now();
   // new window generation: every tree row from older windows becomes stale
   if (++e->gen_cur > 255) {
     HIP_TRY(hipMemsetAsync(e->d_gen.p, 0, e->d_gen.bytes, s), "clear generations");
@@ -948,7 +966,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   }
   }
   HIP_TRY(hipEventRecord(e->ev_run1, s), "event");
+  const auto t_enq = std::chrono::steady_clock::now();
   HIP_TRY(hipEventSynchronize(e->ev_run1), "sync");
+  const auto t_sync = std::chrono::steady_clock::now();
   float ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, e->ev_run0, e->ev_run1), "elapsed");
   st->run_ms += ms;
@@ -997,6 +1017,14 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   st->rounds += r;
   st->expand_launches += r;
   st->windows += 1;
+  if (e->host_timing) {
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    std::fprintf(stderr, "[psengine] window: plan %.3f ms (run->window %.3f, topics %.3f, seeds %.3f, "
+                 "schedule %.3f, uploads %.3f), enqueue %.3f ms, wait %.3f ms, tail %.3f ms\n",
+                 ms(e->t_run0, t_first), ms(e->t_run0, t_w0), ms(t_w0, t_w1), ms(t_w1, t_w2),
+                 ms(t_w2, t_w3), ms(t_w3, t_first), ms(t_first, t_enq), ms(t_enq, t_sync),
+                 ms(t_sync, std::chrono::steady_clock::now()));
+  }
 
   if (record) {
     std::vector<uint8_t> hr(wtot * 64);
@@ -1087,6 +1115,7 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   e->expand_grid = e->n_cus * bpc;
   if (const char* v = std::getenv("PSAMD_NO_SINGLE_START")) e->no_single_start = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_NO_LEVEL")) e->no_level = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_HOST_TIMING")) e->host_timing = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_LEVEL_PUSH")) e->level_push = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_WORDS")) e->pull_words = std::max(64, std::atoi(v));
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -1297,8 +1326,13 @@ int ps_publish_at(ps_engine* e, const uint32_t* topic_of_msg, const uint32_t* st
   if (static_cast<uint64_t>(e->next_msg) + n >= 0xFFFFFFF0ull)
     return e->fail(PS_E_RANGE, "message id space exhausted");
   if (first) *first = e->next_msg;
-  for (size_t i = 0; i < n; ++i)
-    e->pending.push_back(RunMsg{topic_of_msg[i], start_round ? start_round[i] : 0u});
+  const size_t old = e->pending.size();
+  e->pending.resize(old + n);
+  RunMsg* out = e->pending.data() + old;
+  for (size_t i = 0; i < n; ++i) {
+    out[i] = RunMsg{topic_of_msg[i], start_round ? start_round[i] : 0u};
+    e->pending_nonzero_start |= out[i].start != 0;
+  }
   e->next_msg += static_cast<uint32_t>(n);
   return PS_OK;
 }
@@ -1310,10 +1344,13 @@ int ps_publish(ps_engine* e, const uint32_t* topic_of_msg, size_t n, uint32_t* f
 int ps_run(ps_engine* e, ps_stats* out) {
   if (!e) return PS_E_INVAL;
   const auto t_host0 = std::chrono::steady_clock::now();
+  e->t_run0 = t_host0;
   ps_stats st{};
   if (hipSetDevice(e->cfg.device) != hipSuccess) return e->fail(PS_E_DEVICE, "hipSetDevice");
   e->last_msgs.clear();
   e->last_msgs.swap(e->pending);
+  e->run_zero_start = !e->pending_nonzero_start;
+  e->pending_nonzero_start = false;
   const std::vector<RunMsg>& msgs = e->last_msgs;
   const uint32_t nmsg = static_cast<uint32_t>(msgs.size());
   e->last_first = e->next_msg - nmsg;
