@@ -28,6 +28,7 @@ import psengine as PE  # noqa: E402
 from psengine import workloads as WL  # noqa: E402
 
 METRIC = "deliveries/sec (peer×msg) at 1M peers, 1/2/4/8 GPU; % of HBM roofline"
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PAIR_BYTES = 28.375  # SURVEY.md §8d bytes/delivery of the (peer,msg)-pair formulation
 
@@ -77,6 +78,34 @@ def cpu_baseline(eng, wl, sizes, budget_s: float = 10.0):
                       "subtree.go:319-354 + client.go:100-132); Go reference not buildable (no go)"}
 
 
+def pmc_traffic(kernel: str, workload: str):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from separate
+    FETCH_SIZE / WRITE_SIZE runs of this bench), or None."""
+    try:
+        with open(TRAFFIC_FILE) as fh:
+            d = json.load(fh)
+    except (OSError, ValueError):
+        return None, None
+    if d.get("kernel") != kernel or d.get("workload") != workload:
+        return None, None
+    return d.get("traffic_bytes_per_launch"), d.get("source")
+
+
+def instrumented(eng, step, n):
+    """Roofline pass: n steps with HIP events around every hot-kernel launch
+    on the engine's stream (PS_F_TIME_KERNELS); the timed steps run without."""
+    eng.set_time_kernels(True)
+    tot_bytes, tot_ms, launches, st = 0, 0.0, 0, None
+    for _ in range(n):
+        st = step()
+        tot_bytes += st.expand_bytes
+        tot_ms += st.expand_ms
+        launches += st.expand_launches
+    eng.set_time_kernels(False)
+    return tot_bytes, tot_ms, launches, st
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -101,7 +130,7 @@ def main():
 
     wl = WL.CONFIGS[args.workload]() if args.scale == 1.0 else WL.scaled(args.workload, args.scale)
     t0 = time.perf_counter()
-    eng = PE.Engine(wl.n_peers, len(wl.topics), time_kernels=True, seed=wl.seed)
+    eng = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed)
     sizes = WL.build_engine_topics(eng, wl)
     deliv_expected = wl.expected_deliveries(sizes)
     log(f"[bench] {wl.name}: {wl.n_peers} peers, {len(wl.topics)} topics, {sum(sizes)} "
@@ -114,20 +143,19 @@ def main():
     for _ in range(args.warmup):
         st = step()
         assert args.no_check or st.deliveries == deliv_expected, (st.deliveries, deliv_expected)
-    tot_deliv = tot_bytes = 0
-    tot_expand_ms = 0.0
-    launches = 0
+    tot_deliv = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         st = step()
         tot_deliv += st.deliveries
-        tot_bytes += st.expand_bytes
-        tot_expand_ms += st.expand_ms
-        launches += st.expand_launches
     wall = time.perf_counter() - t0
     assert args.no_check or tot_deliv == deliv_expected * args.steps
     value = tot_deliv / wall
+    tot_bytes, tot_expand_ms, launches, st = instrumented(eng, step, max(3, min(args.steps, 5)))
+    assert args.no_check or st.deliveries == deliv_expected
     achieved = tot_bytes / (tot_expand_ms * 1e-3) / 1e9
+    kernel = PE.MODE_KERNEL.get(st.expand_mode, "k_expand")
+    traffic, traffic_src = pmc_traffic(kernel, wl.name)
     pair_gbs = value * PAIR_BYTES / 1e9
     out = {
         "metric": METRIC,
@@ -147,9 +175,12 @@ def main():
                    "messages": wl.n_msgs, "deliveries_per_step": deliv_expected,
                    "parallelism": "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "k_expand", "avg_launch_us": tot_expand_ms * 1e3 / max(1, launches),
-                     "bytes_per_launch": tot_bytes / max(1, launches)},
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": kernel, "avg_launch_us": tot_expand_ms * 1e3 / max(1, launches),
+                     "bytes_per_launch": tot_bytes / max(1, launches),
+                     "timing": "HIP events around every launch on the engine stream, "
+                               "separate instrumented steps after the timed region",
+                     "traffic_source": traffic_src},
         "pair_model": {"bytes_per_delivery": PAIR_BYTES, "equiv_GBs": pair_gbs,
                        "equiv_frac": pair_gbs / HBM_PEAK_GBS},
         "last_step": {"rounds": st.rounds, "windows": st.windows, "run_ms": st.run_ms,

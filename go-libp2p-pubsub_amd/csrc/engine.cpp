@@ -113,6 +113,7 @@ struct ps_engine {
   std::chrono::steady_clock::time_point t_run0;
   bool level_push = false;       // PSAMD_LEVEL_PUSH=1: level mode with the push kernel (A/B)
   uint32_t pull_words = kPullWords;  // words per pull chunk (PSAMD_PULL_WORDS)
+  uint32_t pull_unroll = 8;          // loads in flight per lane (PSAMD_PULL_UNROLL: 4 or 8)
 
   std::vector<TopicHost> topics;
   std::vector<uint8_t> live;
@@ -121,11 +122,13 @@ struct ps_engine {
 
   // level mode: static per-round frontier of the window
   std::vector<uint64_t> sched_key;  // (epochs, rounds, per-topic start) it was built for
-  std::vector<uint32_t> sched_host, sched_off, sched_cnt, woff_host;
+  std::vector<uint32_t> sched_host, sched_off, sched_cnt, woff_host, desc_host;
   DevBuf d_sched, d_sched_cnt, d_woff;
   // level mode, pull direction: per-round chunks of next-level nodes
   std::vector<uint64_t> pull_key;
   std::vector<PullChunk> pull_host;
+  bool pull_fused = false;  // the cached chunks are fused (two levels per launch)
+  bool no_fuse = true;      // PSAMD_PULL_FUSE=1: two levels per pull launch (A/B; slower)
   std::vector<uint32_t> pull_off;
   DevBuf d_pull, d_scratch;
 
@@ -539,33 +542,72 @@ int build_schedule(ps_engine* e, const std::vector<TopicDev>& tab,
 // parents), cut into chunks of at most kPullMaxKids nodes and about
 // kPullWords words, one wave each.  Cached like the schedule.
 int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
-                      const std::vector<uint32_t>& tstart, uint32_t rounds) {
+                      const std::vector<uint32_t>& tstart, uint32_t rounds, bool* fuse) {
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
-  std::vector<uint64_t> key{e->graph_epoch, rounds, e->pull_words};
+  std::vector<uint64_t> key{e->graph_epoch, rounds, e->pull_words, *fuse ? 1ull : 0ull};
   for (uint32_t t = 0; t < nt; ++t) {
     key.push_back(tab[t].W ? tstart[t] : ~0ull);
     key.push_back(tab[t].W);
   }
-  if (key == e->pull_key) return PS_OK;
+  if (key == e->pull_key) {
+    *fuse = e->pull_fused;
+    return PS_OK;
+  }
   e->pull_key.clear();
   auto& C = e->pull_host;
   auto& off = e->pull_off;
-  C.clear();
-  off.assign(rounds + 2, 0);
-  for (uint32_t q = 1; q <= rounds; ++q) {
-    off[q] = static_cast<uint32_t>(C.size());
-    for (uint32_t t = 0; t < nt; ++t) {
-      const TopicHost& T = e->topics[t];
-      const uint32_t W = tab[t].W;
-      if (W == 0 || q < tstart[t] + 1) continue;
-      const uint32_t d = q - tstart[t];  // level of the nodes written this round
-      if (d + 1 >= T.level_off.size()) continue;
-      const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, e->pull_words / W));
-      for (uint32_t u = T.level_off[d]; u < T.level_off[d + 1]; u += per)
-        C.push_back(PullChunk{T.nbase + u, T.nbase + std::min(u + per, T.level_off[d + 1]), t, 0});
+  auto build = [&](bool fused) -> bool {
+    C.clear();
+    off.assign(rounds + 2, 0);
+    for (uint32_t q = 1; q <= rounds; ++q) {
+      off[q] = static_cast<uint32_t>(C.size());
+      for (uint32_t t = 0; t < nt; ++t) {
+        const TopicHost& T = e->topics[t];
+        const uint32_t W = tab[t].W;
+        if (W == 0 || q < tstart[t] + 1) continue;
+        const uint32_t d = q - tstart[t];  // level of the nodes written this round
+        if (fused && (d & 1u) == 0) continue;  // fused: launches write levels (1,2), (3,4), ...
+        if (d + 1 >= T.level_off.size()) continue;
+        const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
+        if (!fused) {
+          const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, e->pull_words / W));
+          for (uint32_t u = lo; u < hi; u += per)
+            C.push_back(PullChunk{T.nbase + u, T.nbase + std::min(u + per, hi), 0, 0, t,
+                                  e->node_parent[T.nbase + u],
+                                  e->node_parent[T.nbase + std::min(u + per, hi) - 1], 0});
+          continue;
+        }
+        // fused: a run of level-d nodes plus their children (consecutive ids:
+        // BFS numbering), at most kPullMaxKids nodes and ~pull_words words
+        for (uint32_t u = lo; u < hi;) {
+          const uint32_t b = u;
+          uint32_t n1 = 0, n2 = 0;
+          while (u < hi) {
+            const uint32_t deg = e->row_ptr[T.nbase + u + 1] - e->row_ptr[T.nbase + u];
+            const uint64_t nn = static_cast<uint64_t>(n1) + 1 + n2 + deg;
+            if (n1 && (nn > kPullMaxKids || nn * W > e->pull_words)) break;
+            if (nn > kPullMaxKids) return false;  // one node's children do not fit a chunk
+            ++n1;
+            n2 += deg;
+            ++u;
+          }
+          uint32_t gb = 0;
+          if (n2) {
+            const uint32_t k0 = e->row_ptr[T.nbase + b], k1 = e->row_ptr[T.nbase + u];
+            gb = e->col[k0];
+            if (e->col[k1 - 1] != gb + n2 - 1) return false;  // children not consecutive
+          }
+          C.push_back(PullChunk{T.nbase + b, T.nbase + u, gb, gb + n2, t, e->node_parent[T.nbase + b],
+                                e->node_parent[T.nbase + u - 1], 0});
+        }
+      }
     }
-  }
-  off[rounds + 1] = static_cast<uint32_t>(C.size());
+    off[rounds + 1] = static_cast<uint32_t>(C.size());
+    return true;
+  };
+  if (*fuse && !build(true)) *fuse = false;
+  if (!*fuse) build(false);
+  e->pull_fused = *fuse;
   HIP_TRY(e->d_pull.ensure(std::max<size_t>(C.size(), 1) * sizeof(PullChunk)), "alloc pull chunks");
   if (!C.empty())
     HIP_TRY(hipMemcpyAsync(e->d_pull.p, C.data(), C.size() * sizeof(PullChunk),
@@ -705,27 +747,46 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     if (tab[t].W && !(tab[t].flags & kTopicSingleStart)) level = false;
   std::vector<uint32_t> lgrid;  // level mode: expand grid of every round
   const bool pull = level && !e->level_push;
+  // fused pull (two levels per launch): every active topic starts together
+  bool fuse = pull && !e->no_fuse;
+  for (uint32_t t = 0; t < nt && fuse; ++t)
+    if (tab[t].W && tstart[t] != max_start) fuse = false;
   if (level) {
-    int rc2 = pull ? build_pull_chunks(e, tab, tstart, planned0)
+    int rc2 = pull ? build_pull_chunks(e, tab, tstart, planned0, &fuse)
                    : build_schedule(e, tab, tstart, planned0);
     if (rc2) return rc2;
     lgrid.assign(planned0 + 1, 0);
+    // partial counter slots: launch of round q owns [woff[q], woff[q+1]);
+    // desc[3q..]: round q's (first, end, stride) for the reduce
     auto& woff = e->woff_host;
     woff.assign(planned0 + 2, 0);
     for (uint32_t q = 1; q <= planned0; ++q) {
-      if (pull) {  // one wave per chunk, one partial slot per block
+      if (pull) {  // one wave per chunk; a partial slot per block (and level)
         lgrid[q] = ceil_div(e->pull_off[q + 1] - e->pull_off[q], kBlock / 64);
-        woff[q + 1] = woff[q] + lgrid[q];
-        continue;
+        woff[q + 1] = woff[q] + lgrid[q] * (fuse ? 2 : 1);
       } else {
         const uint32_t cnt = e->sched_cnt[q];
         lgrid[q] = cnt ? std::min<uint32_t>(e->expand_grid, ceil_div(cnt, 4)) : 0;  // >= 1 entry per wave
+        woff[q + 1] = woff[q] + lgrid[q] * (kBlock / 64);
       }
-      woff[q + 1] = woff[q] + lgrid[q] * (kBlock / 64);
+    }
+    auto& desc = e->desc_host;
+    desc.assign(3 * (planned0 + 2), 0);
+    for (uint32_t q = 1; q <= planned0; ++q) {
+      desc[3 * q] = woff[q];
+      desc[3 * q + 1] = woff[q + 1];
+      desc[3 * q + 2] = 1;
+      if (fuse) {
+        const bool second = q > max_start && (q - max_start) % 2 == 0;  // written by launch q - 1
+        const uint32_t L = second ? q - 1 : q;
+        desc[3 * q] = woff[L] + (second ? 1 : 0);
+        desc[3 * q + 1] = woff[L + 1];
+        desc[3 * q + 2] = 2;
+      }
     }
     HIP_TRY(e->d_partials.ensure(static_cast<size_t>(woff[planned0 + 1]) * kNumCtr * 8),
             "alloc level partials");
-    HIP_TRY(e->d_woff.ensure(woff.size() * 4), "alloc wave offsets");
+    HIP_TRY(e->d_woff.ensure(desc.size() * 4), "alloc reduce descriptors");
     HIP_TRY(e->d_scratch.ensure(1024 * 1024), "alloc scratch");
   }
   // cross-rank capacities (items = node words) per round: cap[r][from*world+to]
@@ -852,8 +913,11 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   uint32_t planned = planned0;
   uint32_t r = 0;
   size_t ev_used = 0;
+  std::vector<uint32_t> ev_round;  // round of every timed launch pair
+  uint32_t launches = 0;
   auto time_mark = [&](bool begin) -> hipError_t {
     if (!timed) return hipSuccess;
+    if (begin) ev_round.push_back(r);
     if (begin && ev_used + 2 > e->ev_k.size()) {
       hipEvent_t x, y;
       hipError_t c = hipEventCreate(&x);
@@ -868,14 +932,17 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   };
   if (level) {
     // static frontier: one expand launch per round, counters reduced once
-    HIP_TRY(hipMemcpyAsync(e->d_woff.p, e->woff_host.data(), e->woff_host.size() * 4,
+    HIP_TRY(hipMemcpyAsync(e->d_woff.p, e->desc_host.data(), e->desc_host.size() * 4,
                            hipMemcpyHostToDevice, s),
             "upload wave offsets");
     HIP_TRY(seed_round(0, arr[0]), "seed");
     for (r = 1; r <= planned0; ++r) {
       a.a_cur = arr[(r - 1) & 1];
       a.a_next = arr[r & 1];
-      HIP_TRY(time_mark(true), "event");
+      if (lgrid[r]) {
+        HIP_TRY(time_mark(true), "event");
+        ++launches;
+      }
       if (lgrid[r] && pull) {
         PullArgs pa{};
         pa.node_parent = e->d_node_parent.as<uint32_t>();
@@ -890,7 +957,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         pa.scratch = e->d_scratch.as<uint64_t>();
         pa.dbg = a.dbg;
         HIP_TRY(launch_pull(pa, e->d_pull.as<PullChunk>() + e->pull_off[r],
-                            e->pull_off[r + 1] - e->pull_off[r], r, record, s),
+                            e->pull_off[r + 1] - e->pull_off[r], lgrid[r], r, record, fuse,
+                            e->pull_unroll, s),
                 "pull");
       } else if (lgrid[r]) {
         a.frontier = e->d_sched.as<uint32_t>() + e->sched_off[r];
@@ -898,7 +966,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         a.partials = partials + static_cast<size_t>(e->woff_host[r]) * kNumCtr;
         HIP_TRY(launch_expand(a, r, record, true, lgrid[r], s), "expand");
       }
-      HIP_TRY(time_mark(false), "event");
+      if (lgrid[r]) HIP_TRY(time_mark(false), "event");
       HIP_TRY(seed_round(r, a.a_next), "seed");
     }
     r = planned0;
@@ -917,6 +985,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         for (int32_t q = 0; q < world; ++q)
           if (s_len[q]) HIP_TRY(hipMemsetAsync(a.send + s_off[q], 0, kRegionHeader, s), "reset header");
       HIP_TRY(time_mark(true), "event");
+      ++launches;
       const uint32_t grid_r = r <= planned0 ? round_grid(r) : e->expand_grid;
       a.partials = partials;
       HIP_TRY(launch_expand(a, r, record, false, grid_r, s), "expand");
@@ -976,7 +1045,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     float k = 0.f;
     HIP_TRY(hipEventElapsedTime(&k, e->ev_k[i], e->ev_k[i + 1]), "elapsed");
     st->expand_ms += k;
-    const size_t q = i / 2 + 1;  // round of this launch
+    const size_t q = ev_round[i / 2];  // round of this launch
     if (q < PS_MAX_ROUNDS) st->expand_ms_per_round[q] += k;
   }
   std::vector<uint64_t> hs(static_cast<size_t>(r + 1) * kNumCtr), ha;
@@ -1015,7 +1084,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     }
   }
   st->rounds += r;
-  st->expand_launches += r;
+  st->expand_launches += launches;
+  st->expand_mode = pull ? PS_MODE_LEVEL_PULL : level ? PS_MODE_LEVEL_PUSH : PS_MODE_COMPACT;
   st->windows += 1;
   if (e->host_timing) {
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -1118,6 +1188,8 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_HOST_TIMING")) e->host_timing = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_LEVEL_PUSH")) e->level_push = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_WORDS")) e->pull_words = std::max(64, std::atoi(v));
+  if (const char* v = std::getenv("PSAMD_PULL_FUSE")) e->no_fuse = std::atoi(v) == 0;
+  if (const char* v = std::getenv("PSAMD_PULL_UNROLL")) e->pull_unroll = std::atoi(v) <= 4 ? 4 : 8;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess) {
     delete e;
@@ -1305,6 +1377,14 @@ int ps_topic_depth(ps_engine* e, uint32_t topic, uint32_t* depth_out, uint32_t* 
   if (rc) return rc;
   if (depth_out) *depth_out = e->topics[topic].depth;
   if (n_nodes_out) *n_nodes_out = e->topics[topic].n_nodes;
+  return PS_OK;
+}
+
+int ps_set_flags(ps_engine* e, uint32_t flags) {
+  if (!e) return PS_E_INVAL;
+  if (flags & ~(PS_F_RECORD_HOPS | PS_F_TIME_KERNELS | PS_F_NO_LAZY_SEEN))
+    return e->fail(PS_E_INVAL, "unknown flag");
+  e->cfg.flags = flags;
   return PS_OK;
 }
 

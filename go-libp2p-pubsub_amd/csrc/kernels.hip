@@ -742,155 +742,179 @@ struct PullVec {
   uint4 v;
 };
 
-template <bool kRecord>
-__global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __restrict__ chunks,
-                                                 uint32_t n_chunks, uint32_t round) {
-  __shared__ uint32_t src_lds[kBlock / 64][kPullMaxKids];
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t wave = blockIdx.x * (kBlock / 64) + wid;
-  uint32_t* src = src_lds[wid];
-  const uint32_t cur = a.gen_cur & 0xFF;
+// One wave's counters for one level of a pull launch.
+struct PullCtr {
   uint64_t deliv = 0;
   uint32_t sw = 0, kids = 0, reached = 0, parents = 0, pwords = 0;
-  if (wave < n_chunks) {
-    const PullChunk ch = chunks[wave];
-    const TopicDev T = a.topics[ch.topic];
-    const uint32_t W = T.W;
-    const uint32_t nb = ch.node_begin, nk = ch.node_end - ch.node_begin;
-    const uint64_t base = T.wbase - static_cast<uint64_t>(T.nbase) * W;  // row of u: base + u*W
-    const uint32_t root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
-    // phase 1: source table
-    for (uint32_t j0 = 0; j0 < nk; j0 += 64) {
-      const uint32_t j = j0 + lane;
-      const bool in = j < nk;
-      uint32_t p = kNoneNode, f = 0;
-      if (in) {
-        p = a.node_parent[nb + j];
-        f = a.node_flags[nb + j];
+};
+
+// Topic constants of a chunk: row of node u = base + u * W.
+struct PullTopic {
+  uint64_t base;
+  uint32_t W, nbase, root;
+};
+
+// Phase 1 for the nodes [nb, nb + nk) of one level: src[j] = the node whose
+// row node nb + j copies, or kNoneNode.  Level 1 (kSecond = false): the
+// parent, if the parent was reached this window (generation current) and the
+// node is live.  Level 2 of a fused launch (kSecond = true): the node's
+// parent pc is level 1 of the same chunk, whose row is being written from
+// src1[pc - b1]; the node copies that same source row (the row pc receives)
+// if pc was reached and the node is live.  Reached nodes get their
+// generation stamped.  A parent counts once, at its first child.
+template <bool kSecond>
+__device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic& P, uint32_t nb,
+                                             uint32_t nk, uint32_t p_lo, uint32_t p_hi,
+                                             uint32_t* src, const uint32_t* src1, uint32_t b1,
+                                             uint8_t* genl, uint32_t lane, uint32_t cur,
+                                             PullCtr& c) {
+  // Level 1: the parents of a run are consecutive node ids [p_lo, p_hi]
+  // (BFS numbering), known to the host: their generation bytes are staged
+  // into LDS by loads issued together with the nodes' own metadata, so phase
+  // 1 costs one memory round trip.
+  uint32_t g0 = 0;
+  const bool staged = !kSecond && p_lo != kNoneNode && p_hi - p_lo < kPullMaxKids;
+  if (staged) {
+    g0 = p_lo & ~3u;
+    const uint32_t nd = ((p_hi + 4u) & ~3u) - g0;  // bytes, whole dwords
+    const uint32_t* gsrc = reinterpret_cast<const uint32_t*>(a.gen + g0);
+    for (uint32_t d = lane; 4 * d < nd; d += 64) reinterpret_cast<uint32_t*>(genl)[d] = gsrc[d];
+  }
+  for (uint32_t j0 = 0; j0 < nk; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    const bool in = j < nk;
+    uint32_t p = kNoneNode, f = 0;
+    if (in) {
+      p = a.node_parent[nb + j];
+      f = a.node_flags[nb + j];
+    }
+    uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
+    if (lane == 0) prev = nb + j0 > P.nbase ? a.node_parent[nb + j0 - 1] : kNoneNode;
+    uint32_t from = kNoneNode;
+    bool up = false;  // the parent was reached this window
+    if constexpr (kSecond) {
+      if (in) from = src1[p - b1];
+      up = from != kNoneNode;
+    } else {
+      if (in && p != kNoneNode) up = (staged ? genl[p - g0] : a.gen[p]) == cur;
+      from = p;
+    }
+    const bool ok = up && (f & kNodeLive);
+    if (in) src[j] = ok ? from : kNoneNode;
+    if (ok && !(a.dbg & kDbgNoByteStores)) a.gen[nb + j] = static_cast<uint8_t>(cur);
+    c.kids += in;
+    c.reached += ok;
+    if (up && p != prev) {
+      c.parents += 1;
+      if constexpr (!kSecond) c.pwords += P.W;  // fused level 2 re-reads the level-1 source
+    }
+  }
+}
+
+// Phase 2: the rows of nodes [nb, nb + nk) as one output stream, each lane's
+// load from the row its node copies (src[], kNoneNode = skip).
+template <bool kRecord, uint32_t kU>
+__device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& P, uint32_t nb,
+                                            uint32_t nk, const uint32_t* src, uint32_t lane,
+                                            uint32_t wave, uint32_t round, PullCtr& c) {
+  const uint32_t W = P.W;
+  const uint64_t base = P.base;
+  const uint32_t root = P.root;
+  const uint32_t total = nk * W;
+  uint64_t* const out = a.seen + base + static_cast<uint64_t>(nb) * W;
+  uint64_t* const dummy = a.scratch + static_cast<uint64_t>(wave & 1023u) * 128;
+  const float rw = 1.0f / static_cast<float>(W);
+  // row kk = i / W and word r of the run, branch-free (float estimate off by
+  // at most one; i < 2^24)
+  auto split = [&](uint32_t i, int32_t& kk, int32_t& r) {
+    kk = static_cast<int32_t>(static_cast<float>(i) * rw);
+    r = static_cast<int32_t>(i) - kk * static_cast<int32_t>(W);
+    const int32_t lo = r < 0, hi = r >= static_cast<int32_t>(W);
+    kk += hi - lo;
+    r += (lo - hi) * static_cast<int32_t>(W);
+  };
+  if (!(W & 1u)) {
+    // even W: every row 16-B aligned, a 2-word pair never straddles rows
+    auto one = [&](uint32_t i, bool valid) {
+      int32_t kk, r;
+      split(i, kk, r);
+      const uint32_t p = valid ? src[kk] : kNoneNode;
+      const bool go = p != kNoneNode;
+      // unconditional load: a skipped lane reads its own output row
+      const uint64_t* s = go ? (p == root ? a.a_cur : a.seen) + base + static_cast<uint64_t>(p) * W + r
+                             : out + (valid ? i : 0);
+      return PullVec{go, *reinterpret_cast<const uint4*>(s)};
+    };
+    // 8 loads in flight, then 8 stores, unconditional and branch-free (a
+    // skipped lane writes its own row back unchanged, a lane past the run's
+    // end writes a scratch slot), so the compiler counts vmcnt exactly
+    // instead of draining at branches
+    for (uint32_t i0 = 0; i0 < total; i0 += kU * 128) {
+      PullVec x[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t i = i0 + u * 128 + 2 * lane;
+        x[u] = one(i, i < total);
       }
-      uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
-      if (lane == 0) prev = nb + j0 > T.nbase ? a.node_parent[nb + j0 - 1] : kNoneNode;
-      bool up = false;  // the parent was reached this window
-      if (in && p != kNoneNode) up = a.gen[p] == cur;
-      const bool ok = up && (f & kNodeLive);
-      if (in) src[j] = ok ? p : kNoneNode;
-      if (ok && !(a.dbg & kDbgNoByteStores)) a.gen[nb + j] = static_cast<uint8_t>(cur);
-      kids += in;
-      reached += ok;
-      if (up && p != prev) {
-        parents += 1;
-        pwords += W;
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t i = i0 + u * 128 + 2 * lane;
+        if constexpr (kRecord) {
+          if (x[u].go && i < total) {
+            *reinterpret_cast<uint4*>(out + i) = x[u].v;
+            const uint64_t cw = (out - a.seen) + i;
+            record_word<kRecord>(a.hop_rec, cw, static_cast<uint64_t>(x[u].v.y) << 32 | x[u].v.x, round);
+            record_word<kRecord>(a.hop_rec, cw + 1, static_cast<uint64_t>(x[u].v.w) << 32 | x[u].v.z,
+                                 round);
+          }
+        } else {
+          *reinterpret_cast<uint4*>(i < total ? out + i : dummy + 2 * lane) = x[u].v;
+        }
+        c.deliv += x[u].go ? popc4(x[u].v) : 0u;
+        c.sw += x[u].go ? 2u : 0u;
       }
     }
-    // phase 2: the run's rows as one output stream (LDS ops of a wave are
-    // processed in order: the table is visible to the reads below)
-    const uint32_t total = nk * W;
-    uint64_t* const out = a.seen + base + static_cast<uint64_t>(nb) * W;
-    if (!(W & 1u)) {
-      // even W: every row 16-B aligned, a 2-word pair never straddles rows
-      const float rw = 1.0f / static_cast<float>(W);
-      auto one = [&](uint32_t i, bool valid) {
-        // row kk = i / W and word r of the run, branch-free (float estimate
-        // off by at most one; i < 2^24)
-        int32_t kk = static_cast<int32_t>(static_cast<float>(i) * rw);
-        int32_t r = static_cast<int32_t>(i) - kk * static_cast<int32_t>(W);
-        const int32_t lo = r < 0, hi = r >= static_cast<int32_t>(W);
-        kk += hi - lo;
-        r += (lo - hi) * static_cast<int32_t>(W);
+  } else {
+    // odd W: one word (8 B) per lane, the same pipeline
+    for (uint32_t i0 = 0; i0 < total; i0 += kU * 64) {
+      uint64_t m[kU];
+      bool go[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t i = i0 + u * 64 + lane;
+        const bool valid = i < total;
+        int32_t kk, r;
+        split(i, kk, r);
         const uint32_t p = valid ? src[kk] : kNoneNode;
-        const bool go = p != kNoneNode;
-        // unconditional load: a skipped lane reads its own output row
-        const uint64_t* s = go ? (p == root ? a.a_cur : a.seen) + base + static_cast<uint64_t>(p) * W + r
-                               : out + (valid ? i : 0);
-        const uint4 v = *reinterpret_cast<const uint4*>(s);
-        return PullVec{go, v};
-      };
-      uint32_t i0 = 0;
-      if constexpr (!kRecord) {
-        // 8 loads in flight, then 8 stores, all unconditional and branch-free
-        // (a skipped lane writes its own row back unchanged; a lane past the
-        // run's end reads the run's first word and writes a scratch slot), so
-        // the compiler counts vmcnt exactly instead of draining at branches
-        constexpr uint32_t kU = 8;
-        uint64_t* const dummy = a.scratch + static_cast<uint64_t>(wave & 1023u) * 128;
-        for (; i0 < total; i0 += kU * 128) {
-          PullVec x[kU];
-#pragma unroll
-          for (uint32_t u = 0; u < kU; ++u) {
-            const uint32_t i = i0 + u * 128 + 2 * lane;
-            x[u] = one(i, i < total);
-          }
-#pragma unroll
-          for (uint32_t u = 0; u < kU; ++u) {
-            const uint32_t i = i0 + u * 128 + 2 * lane;
-            uint64_t* const dst = i < total ? out + i : dummy + 2 * lane;
-            *reinterpret_cast<uint4*>(dst) = x[u].v;
-            deliv += x[u].go ? popc4(x[u].v) : 0u;
-            sw += x[u].go ? 2u : 0u;
-          }
-        }
+        go[u] = p != kNoneNode;
+        const uint64_t* s = go[u] ? (p == root ? a.a_cur : a.seen) + base + static_cast<uint64_t>(p) * W + r
+                                  : out + (valid ? i : 0);
+        m[u] = *s;
       }
-      for (; i0 < total; i0 += 128) {
-        const uint32_t i = i0 + 2 * lane;
-        const auto x = one(i, i < total);
-        if (x.go) {
-          if (!(a.dbg & kDbgNoSeenStore)) *reinterpret_cast<uint4*>(out + i) = x.v;
-          deliv += popc4(x.v);
-          sw += 2;
-          if constexpr (kRecord) {
-            const uint64_t cw = (out - a.seen) + i;
-            record_word<kRecord>(a.hop_rec, cw, static_cast<uint64_t>(x.v.y) << 32 | x.v.x, round);
-            record_word<kRecord>(a.hop_rec, cw + 1, static_cast<uint64_t>(x.v.w) << 32 | x.v.z, round);
-          }
-        }
-      }
-    } else {
-      // odd W: one word (8 B) per lane, the same branch-free pipeline
-      const float rw = 1.0f / static_cast<float>(W);
-      auto one1 = [&](uint32_t i, bool valid, bool& go) -> uint64_t {
-        int32_t kk = static_cast<int32_t>(static_cast<float>(i) * rw);
-        int32_t r = static_cast<int32_t>(i) - kk * static_cast<int32_t>(W);
-        const int32_t lo = r < 0, hi = r >= static_cast<int32_t>(W);
-        kk += hi - lo;
-        r += (lo - hi) * static_cast<int32_t>(W);
-        const uint32_t p = valid ? src[kk] : kNoneNode;
-        go = p != kNoneNode;
-        const uint64_t* s = go ? (p == root ? a.a_cur : a.seen) + base + static_cast<uint64_t>(p) * W + r
-                               : out + (valid ? i : 0);
-        return *s;
-      };
-      constexpr uint32_t kU = 8;
-      uint64_t* const dummy = a.scratch + static_cast<uint64_t>(wave & 1023u) * 128;
-      for (uint32_t i0 = 0; i0 < total; i0 += kU * 64) {
-        uint64_t m[kU];
-        bool go[kU];
 #pragma unroll
-        for (uint32_t u = 0; u < kU; ++u) {
-          const uint32_t i = i0 + u * 64 + lane;
-          m[u] = one1(i, i < total, go[u]);
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kU; ++u) {
-          const uint32_t i = i0 + u * 64 + lane;
-          if constexpr (kRecord) {
-            if (go[u] && i < total) {
-              out[i] = m[u];
-              record_word<kRecord>(a.hop_rec, (out - a.seen) + i, m[u], round);
-            }
-          } else {
-            *(i < total ? out + i : dummy + lane) = m[u];
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t i = i0 + u * 64 + lane;
+        if constexpr (kRecord) {
+          if (go[u] && i < total) {
+            out[i] = m[u];
+            record_word<kRecord>(a.hop_rec, (out - a.seen) + i, m[u], round);
           }
-          deliv += go[u] ? __popcll(m[u]) : 0u;
-          sw += go[u] ? 1u : 0u;
+        } else {
+          *(i < total ? out + i : dummy + lane) = m[u];
         }
+        c.deliv += go[u] ? __popcll(m[u]) : 0u;
+        c.sw += go[u] ? 1u : 0u;
       }
     }
   }
-  // block-level counters: one partial slot per block (fewer for the reduce)
+}
+
+// Block-level counters of one level into partial slot `slot`.
+__device__ __forceinline__ void pull_flush(const PullCtr& c, uint64_t* partials, uint64_t slot,
+                                           uint32_t lane, uint32_t wid) {
   __shared__ uint64_t red[kBlock / 64][6];
-  const uint64_t v6[6] = {wave_sum_u64(deliv), wave_sum_u64(sw), wave_sum_u64(kids),
-                          wave_sum_u64(reached), wave_sum_u64(parents), wave_sum_u64(pwords)};
+  const uint64_t v6[6] = {wave_sum_u64(c.deliv), wave_sum_u64(c.sw), wave_sum_u64(c.kids),
+                          wave_sum_u64(c.reached), wave_sum_u64(c.parents), wave_sum_u64(c.pwords)};
   if (lane == 0)
 #pragma unroll
     for (int q = 0; q < 6; ++q) red[wid][q] = v6[q];
@@ -910,7 +934,53 @@ __global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __
       case kCtrSeenWrites: v = t[1]; break;
       default: v = 0;
     }
-    a.partials[static_cast<uint64_t>(blockIdx.x) * kNumCtr + threadIdx.x] = v;
+    partials[slot * kNumCtr + threadIdx.x] = v;
+  }
+  __syncthreads();  // `red` is reused by the next level's flush
+}
+
+// kFuse: the chunk also carries the children [g_begin, g_end) of its nodes,
+// written in the same launch (round + 1) from the same source rows, so the
+// rows of level d + 1 are never read back.  Partial slots: one per block and
+// level (fused: 2 * block + level).
+template <bool kRecord, bool kFuse, uint32_t kU>
+__global__ __launch_bounds__(kBlock, kU <= 4 ? 8 : 1) void k_pull(PullArgs a, const PullChunk* __restrict__ chunks,
+                                                 uint32_t n_chunks, uint32_t round) {
+  __shared__ uint32_t src_lds[kBlock / 64][kPullMaxKids];
+  __shared__ uint32_t gen_lds[kBlock / 64][kPullMaxKids / 4 + 2];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wave = blockIdx.x * (kBlock / 64) + wid;
+  uint32_t* src = src_lds[wid];
+  uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds[wid]);
+  const uint32_t cur = a.gen_cur & 0xFF;
+  PullCtr c1, c2;
+  if (wave < n_chunks) {  // one chunk per wave
+    const PullChunk ch = chunks[wave];
+    const TopicDev T = a.topics[ch.topic];
+    PullTopic P;
+    P.W = T.W;
+    P.nbase = T.nbase;
+    P.base = T.wbase - static_cast<uint64_t>(T.nbase) * T.W;
+    P.root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
+    const uint32_t n1 = ch.node_end - ch.node_begin;
+    const uint32_t n2 = kFuse ? ch.g_end - ch.g_begin : 0u;
+    // LDS ops of a wave are processed in order: the tables written in phase
+    // 1 are visible to the reads that follow
+    pull_resolve<false>(a, P, ch.node_begin, n1, ch.p_lo, ch.p_hi, src, nullptr, 0, genl, lane,
+                        cur, c1);
+    if constexpr (kFuse)
+      pull_resolve<true>(a, P, ch.g_begin, n2, kNoneNode, kNoneNode, src + n1, src, ch.node_begin,
+                         genl, lane, cur, c2);
+    pull_stream<kRecord, kU>(a, P, ch.node_begin, n1, src, lane, wave, round, c1);
+    if constexpr (kFuse)
+      pull_stream<kRecord, kU>(a, P, ch.g_begin, n2, src + n1, lane, wave, round + 1, c2);
+  }
+  if constexpr (kFuse) {
+    pull_flush(c1, a.partials, 2ull * blockIdx.x, lane, wid);
+    pull_flush(c2, a.partials, 2ull * blockIdx.x + 1, lane, wid);
+  } else {
+    pull_flush(c1, a.partials, blockIdx.x, lane, wid);
   }
 }
 
@@ -972,16 +1042,16 @@ __global__ __launch_bounds__(kBlock) void k_apply(ApplyArgs a, uint32_t round) {
 }
 
 // ------------------------------------------------------------ compaction ---
-// One block folds the expand kernel's per-wave counters [w0, w1) into one
-// round's statistics.
+// One block folds the partial counter slots w0, w0 + stride, ... (< w1) into
+// one round's statistics.
 __device__ __forceinline__ void block_reduce_ctrs(const uint64_t* __restrict__ partials,
-                                                  uint32_t w0, uint32_t w1,
+                                                  uint32_t w0, uint32_t w1, uint32_t stride,
                                                   uint64_t* __restrict__ out) {
   __shared__ uint64_t red[kNumCtr][kBlock / 64];
   uint64_t acc[kNumCtr];
 #pragma unroll
   for (int k = 0; k < kNumCtr; ++k) acc[k] = 0;
-  for (uint32_t w = w0 + threadIdx.x; w < w1; w += kBlock)
+  for (uint32_t w = w0 + threadIdx.x * stride; w < w1; w += kBlock * stride)
 #pragma unroll
     for (int k = 0; k < kNumCtr; ++k) acc[k] += partials[static_cast<uint64_t>(w) * kNumCtr + k];
 #pragma unroll
@@ -997,12 +1067,22 @@ __device__ __forceinline__ void block_reduce_ctrs(const uint64_t* __restrict__ p
   }
 }
 
-// Level mode: one block per round q = blockIdx.x + 1.
+// Level mode: grid (rounds, kReduceSplit); block (q-1, y) folds every
+// kReduceSplit-th partial slot of round q (desc[3q..3q+2] = first slot, end
+// slot, stride) and adds its sums into the round's (zeroed) statistics.
+constexpr uint32_t kReduceSplit = 32;
 __global__ __launch_bounds__(kBlock) void k_reduce_rounds(const uint64_t* __restrict__ partials,
-                                                          const uint32_t* __restrict__ woff,
+                                                          const uint32_t* __restrict__ desc,
                                                           uint64_t* __restrict__ round_stats) {
+  __shared__ uint64_t sums[kNumCtr];
   const uint32_t q = blockIdx.x + 1;
-  block_reduce_ctrs(partials, woff[q], woff[q + 1], round_stats + static_cast<uint64_t>(q) * kNumCtr);
+  const uint32_t stride = desc[3 * q + 2];
+  block_reduce_ctrs(partials, desc[3 * q] + blockIdx.y * stride, desc[3 * q + 1],
+                    stride * kReduceSplit, sums);
+  if (threadIdx.x < kNumCtr && sums[threadIdx.x])
+    atomicAdd(reinterpret_cast<unsigned long long*>(round_stats + static_cast<uint64_t>(q) * kNumCtr +
+                                                    threadIdx.x),
+              static_cast<unsigned long long>(sums[threadIdx.x]));
 }
 
 // Pass 1: per-block count of flagged nodes (16 one-byte flags per lane, one
@@ -1015,7 +1095,7 @@ __global__ __launch_bounds__(kBlock) void k_flag_count(const uint8_t* __restrict
                                                        const uint64_t* __restrict__ partials,
                                                        uint32_t n_waves,
                                                        uint64_t* __restrict__ round_stats) {
-  if (blockIdx.x == 0 && round_stats != nullptr) block_reduce_ctrs(partials, 0, n_waves, round_stats);
+  if (blockIdx.x == 0 && round_stats != nullptr) block_reduce_ctrs(partials, 0, n_waves, 1, round_stats);
   if (blk_flag[blockIdx.x] == 0) {
     if (threadIdx.x == 0) wg_count[blockIdx.x] = 0;
     return;
@@ -1159,21 +1239,38 @@ hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record
 }
 
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                       uint32_t round, bool record, hipStream_t s) {
-  if (n_chunks == 0) return hipSuccess;
-  const uint32_t grid = (n_chunks + kBlock / 64 - 1) / (kBlock / 64);
-  if (record)
-    hipLaunchKernelGGL(k_pull<true>, dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
-  else
-    hipLaunchKernelGGL(k_pull<false>, dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
+                       uint32_t grid, uint32_t round, bool record, bool fuse, uint32_t unroll,
+                       hipStream_t s) {
+  if (n_chunks == 0 || grid == 0) return hipSuccess;
+#define PSAMD_PULL(R, F, U) \
+  hipLaunchKernelGGL((k_pull<R, F, U>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round)
+  if (record) {  // parity runs: one variant
+    if (fuse)
+      PSAMD_PULL(true, true, 8);
+    else
+      PSAMD_PULL(true, false, 8);
+  } else if (unroll <= 4) {
+    if (fuse)
+      PSAMD_PULL(false, true, 4);
+    else
+      PSAMD_PULL(false, false, 4);
+  } else {
+    if (fuse)
+      PSAMD_PULL(false, true, 8);
+    else
+      PSAMD_PULL(false, false, 8);
+  }
+#undef PSAMD_PULL
   return hipGetLastError();
 }
 
-hipError_t launch_reduce_rounds(const uint64_t* partials, const uint32_t* woff, uint32_t n_rounds,
+hipError_t launch_reduce_rounds(const uint64_t* partials, const uint32_t* desc, uint32_t n_rounds,
                                 uint64_t* round_stats, hipStream_t s) {
   if (n_rounds == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_reduce_rounds, dim3(n_rounds), dim3(kBlock), 0, s, partials, woff,
-                     round_stats);
+  hipError_t e = hipMemsetAsync(round_stats, 0, (n_rounds + 1ull) * kNumCtr * 8, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_reduce_rounds, dim3(n_rounds, kReduceSplit), dim3(kBlock), 0, s, partials,
+                     desc, round_stats);
   return hipGetLastError();
 }
 

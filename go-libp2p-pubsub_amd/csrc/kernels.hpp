@@ -109,7 +109,11 @@ struct ExpandArgs {
 // rows of a contiguous run of next-level nodes [node_begin, node_end) of one
 // topic (at most kPullMaxKids nodes, about kPullWords words).
 struct PullChunk {
-  uint32_t node_begin, node_end, topic, pad;
+  uint32_t node_begin, node_end;  // nodes written in round r (level d)
+  uint32_t g_begin, g_end;        // fused launches: their children, written as round r + 1
+  uint32_t topic;
+  uint32_t p_lo, p_hi;  // parents of [node_begin, node_end) (consecutive ids), kNone: unknown
+  uint32_t pad;
 };
 constexpr uint32_t kPullMaxKids = 512;
 constexpr uint32_t kNoneNode = 0xFFFFFFFFu;
@@ -174,12 +178,16 @@ hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t*
 // (stale generation) are skipped and no frontier flags are raised.
 hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, bool level,
                          uint32_t grid, hipStream_t s);
-// Level mode, pull direction: one wave per chunk (grid = ceil(n_chunks / 4)).
+// Level mode, pull direction: one wave per chunk (grid = ceil(n_chunks / 4));
+// fuse: each chunk also writes its nodes' children (two levels per launch).
+// unroll: 16-B loads in flight per lane (4: 8 waves/SIMD, 8: 6 waves/SIMD)
+// grid: blocks, one chunk per wave (ceil(n_chunks / 4))
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                       uint32_t round, bool record, hipStream_t s);
-// Level mode: round q's counters = sum of the per-wave partials
-// [woff[q], woff[q+1]) for q = 1..n_rounds.
-hipError_t launch_reduce_rounds(const uint64_t* partials, const uint32_t* woff, uint32_t n_rounds,
+                       uint32_t grid, uint32_t round, bool record, bool fuse, uint32_t unroll,
+                       hipStream_t s);
+// Level mode: round q's counters = sum of the partial slots desc[3q],
+// desc[3q] + desc[3q+2], ... < desc[3q+1], for q = 1..n_rounds.
+hipError_t launch_reduce_rounds(const uint64_t* partials, const uint32_t* desc, uint32_t n_rounds,
                                 uint64_t* round_stats, hipStream_t s);
 // second instance: entries the staged kernel leaves (mesh, split, wide rows,
 // fan-out > 64); writes the same counters to partials + n_waves*kNumCtr

@@ -27,6 +27,8 @@ PART_SUBTREE = 1
 F_RECORD_HOPS = 0x1
 F_TIME_KERNELS = 0x2
 F_NO_LAZY_SEEN = 0x4
+MODE_COMPACT, MODE_LEVEL_PUSH, MODE_LEVEL_PULL = 0, 1, 2
+MODE_KERNEL = {MODE_COMPACT: "k_expand", MODE_LEVEL_PUSH: "k_expand", MODE_LEVEL_PULL: "k_pull"}
 
 # C prototypes exported by libpsengine.so: (name, restype, argtypes)
 _P = C.c_void_p
@@ -49,6 +51,7 @@ class Stats(C.Structure):
                 ("edge_words", C.c_uint64), ("expand_bytes", C.c_uint64),
                 ("windows", C.c_uint64), ("rounds", C.c_uint64), ("expand_launches", C.c_uint64),
                 ("run_ms", C.c_double), ("expand_ms", C.c_double), ("host_ms", C.c_double),
+                ("expand_mode", C.c_uint32), ("reserved", C.c_uint32),
                 ("deliveries_per_round", C.c_uint64 * MAX_ROUNDS),
                 ("expand_ms_per_round", C.c_float * MAX_ROUNDS),
                 ("frontier_per_round", C.c_uint32 * MAX_ROUNDS)]
@@ -86,6 +89,7 @@ PROTOTYPES = [
     ("ps_topic_get_parents", C.c_int, [_P, _u32, _u32p]),
     ("ps_topic_depth", C.c_int, [_P, _u32, _u32p, _u32p]),
     ("ps_set_live", C.c_int, [_P, _u8p]),
+    ("ps_set_flags", C.c_int, [_P, _u32]),
     ("ps_publish", C.c_int, [_P, _u32p, C.c_size_t, _u32p]),
     ("ps_publish_at", C.c_int, [_P, _u32p, _u32p, C.c_size_t, _u32p]),
     ("ps_run", C.c_int, [_P, C.POINTER(Stats)]),
@@ -152,6 +156,7 @@ class Engine:
         self.seed = seed
         f = flags | (F_RECORD_HOPS if record_hops else 0) | (F_TIME_KERNELS if time_kernels else 0)
         cfg = Config(n_peers, n_topics, tree_width, tree_max_width, msg_window, device, f, 0, seed)
+        self.flags = f
         h = _P()
         rc = L.ps_create(C.byref(cfg), C.byref(h))
         if rc != PS_OK:
@@ -229,6 +234,14 @@ class Engine:
         d, n = C.c_uint32(), C.c_uint32()
         self._check(self._L.ps_topic_depth(self._h, topic, C.byref(d), C.byref(n)))
         return d.value, n.value
+
+    def set_flags(self, flags: int):
+        """Replaces the PS_F_* flags for the next runs (ps_set_flags)."""
+        self._check(self._L.ps_set_flags(self._h, flags))
+        self.flags = flags
+
+    def set_time_kernels(self, on: bool):
+        self.set_flags((self.flags & ~F_TIME_KERNELS) | (F_TIME_KERNELS if on else 0))
 
     def set_live(self, live):
         lv = np.ascontiguousarray(live, dtype=np.uint8)

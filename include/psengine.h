@@ -60,6 +60,11 @@ typedef struct ps_config {
   uint64_t seed;           /* redirect tie-break stream (Go map order, Q2)     */
 } ps_config;
 
+/* ps_stats.expand_mode: how the last window's rounds ran */
+#define PS_MODE_COMPACT 0u     /* k_expand over a compacted frontier (flags + scan) */
+#define PS_MODE_LEVEL_PUSH 1u  /* k_expand over a static level schedule              */
+#define PS_MODE_LEVEL_PULL 2u  /* k_pull: next level pulls its parents' rows         */
+
 typedef struct ps_stats {
   uint64_t deliveries;         /* (peer,msg) pairs delivered by this run        */
   uint64_t duplicates;         /* bits suppressed by the seen test (0 on trees)  */
@@ -73,6 +78,8 @@ typedef struct ps_stats {
   double run_ms;               /* device time of the whole run (HIP events)      */
   double expand_ms;            /* summed expand-kernel device time (TIME flag)   */
   double host_ms;              /* wall time of the ps_run call                   */
+  uint32_t expand_mode;        /* hot kernel of the last window: PS_MODE_*       */
+  uint32_t reserved;
   uint64_t deliveries_per_round[PS_MAX_ROUNDS];
   float expand_ms_per_round[PS_MAX_ROUNDS];   /* TIME flag, summed over windows  */
   uint32_t frontier_per_round[PS_MAX_ROUNDS]; /* expanded entries per round      */
@@ -118,6 +125,10 @@ int ps_topic_set_children(ps_engine* e, uint32_t topic, uint32_t root,
                           const uint32_t* row_ptr, const uint32_t* col);
 int ps_topic_get_parents(ps_engine* e, uint32_t topic, uint32_t* parent_out);
 int ps_topic_depth(ps_engine* e, uint32_t topic, uint32_t* depth_out, uint32_t* n_nodes_out);
+
+/* Replace the engine's PS_F_* flags (e.g. PS_F_TIME_KERNELS for an
+ * instrumented run between untimed ones); applies to the next ps_run. */
+int ps_set_flags(ps_engine* e, uint32_t flags);
 
 /* Subscribed-and-live mask over peers (1 = receives and forwards).  A peer
  * whose client stopped reading (client.go:103-131) is 0. Default: all 1. */

@@ -16,7 +16,7 @@ from psengine import workloads as WL  # noqa: E402
 name = sys.argv[1] if len(sys.argv) > 1 else "cfg3"
 steps = int(sys.argv[2]) if len(sys.argv) > 2 else 6
 wl = WL.CONFIGS[name]()
-eng = PE.Engine(wl.n_peers, len(wl.topics), time_kernels=True, seed=wl.seed)
+eng = PE.Engine(wl.n_peers, len(wl.topics), time_kernels=os.environ.get("TIMEK", "1") == "1", seed=wl.seed)
 WL.build_engine_topics(eng, wl)
 for i in range(steps):
     t0 = time.perf_counter()
