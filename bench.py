@@ -120,6 +120,9 @@ def main():
                     help="use the torch.distributed driver even with one rank (testing)")
     ap.add_argument("--partition", default="subtree", choices=["subtree", "peer"],
                     help="multi-GPU node ownership: subtree hash (default) or peer hash")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="N>1: weak = N x the messages on the same topology (per-GPU work of "
+                         "N=1), strong = the N=1 workload unchanged")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -166,7 +169,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": wall * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "strong",
+        "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic",

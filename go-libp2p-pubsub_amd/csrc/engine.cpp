@@ -127,6 +127,8 @@ struct ps_engine {
   // level mode, pull direction: per-round chunks of next-level nodes
   std::vector<uint64_t> pull_key;
   std::vector<PullChunk> pull_host;
+  std::vector<uint32_t> split_host, split_off;  // multi-GPU: split parents per round
+  DevBuf d_split;
   bool pull_fused = false;  // the cached chunks are fused (two levels per launch)
   bool no_fuse = true;      // PSAMD_PULL_FUSE=1: two levels per pull launch (A/B; slower)
   std::vector<uint32_t> pull_off;
@@ -359,11 +361,11 @@ int build_graph(ps_engine* e) {
     }
     T.root_local = owner[0] == me;
     T.level_internal.assign(T.depth + 1, 0);
+    // owned nodes are numbered in BFS order: each level is a contiguous range
     T.level_off.assign(T.depth + 2, 0);
-    if (world == 1) {  // every node owned: BFS levels are contiguous node ranges
-      for (uint32_t u = 0; u < N; ++u) T.level_off[level[u] + 1]++;
-      for (uint32_t d = 0; d <= T.depth; ++d) T.level_off[d + 1] += T.level_off[d];
-    }
+    for (uint32_t u = 0; u < N; ++u)
+      if (owner[u] == me) T.level_off[level[u] + 1]++;
+    for (uint32_t d = 0; d <= T.depth; ++d) T.level_off[d + 1] += T.level_off[d];
     std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> cross;
     uint32_t n_own = 0;
     for (uint32_t u = 0; u < N; ++u) {
@@ -544,7 +546,7 @@ int build_schedule(ps_engine* e, const std::vector<TopicDev>& tab,
 int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
                       const std::vector<uint32_t>& tstart, uint32_t rounds, bool* fuse) {
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
-  std::vector<uint64_t> key{e->graph_epoch, rounds, e->pull_words, *fuse ? 1ull : 0ull};
+  std::vector<uint64_t> key{e->graph_epoch, e->flags_epoch, rounds, e->pull_words, *fuse ? 1ull : 0ull};
   for (uint32_t t = 0; t < nt; ++t) {
     key.push_back(tab[t].W ? tstart[t] : ~0ull);
     key.push_back(tab[t].W);
@@ -559,8 +561,11 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
   auto build = [&](bool fused) -> bool {
     C.clear();
     off.assign(rounds + 2, 0);
+    e->split_host.clear();
+    e->split_off.assign(rounds + 2, 0);
     for (uint32_t q = 1; q <= rounds; ++q) {
       off[q] = static_cast<uint32_t>(C.size());
+      e->split_off[q] = static_cast<uint32_t>(e->split_host.size());
       for (uint32_t t = 0; t < nt; ++t) {
         const TopicHost& T = e->topics[t];
         const uint32_t W = tab[t].W;
@@ -570,6 +575,11 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
         if (d + 1 >= T.level_off.size()) continue;
         const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
         if (!fused) {
+          // split parents of this round (children owned by other ranks)
+          if (e->world > 1)
+            for (uint32_t u = T.level_off[d - 1]; u < T.level_off[d]; ++u)
+              if ((e->node_flags[T.nbase + u] & (kNodeSplit | kNodeLive)) == (kNodeSplit | kNodeLive))
+                e->split_host.push_back(T.nbase + u);
           const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, e->pull_words / W));
           for (uint32_t u = lo; u < hi; u += per)
             C.push_back(PullChunk{T.nbase + u, T.nbase + std::min(u + per, hi), 0, 0, t,
@@ -603,11 +613,17 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
       }
     }
     off[rounds + 1] = static_cast<uint32_t>(C.size());
+    e->split_off[rounds + 1] = static_cast<uint32_t>(e->split_host.size());
     return true;
   };
   if (*fuse && !build(true)) *fuse = false;
   if (!*fuse) build(false);
   e->pull_fused = *fuse;
+  HIP_TRY(e->d_split.ensure(std::max<size_t>(e->split_host.size(), 1) * 4), "alloc split list");
+  if (!e->split_host.empty())
+    HIP_TRY(hipMemcpyAsync(e->d_split.p, e->split_host.data(), e->split_host.size() * 4,
+                           hipMemcpyHostToDevice, e->stream),
+            "upload split list");
   HIP_TRY(e->d_pull.ensure(std::max<size_t>(C.size(), 1) * sizeof(PullChunk)), "alloc pull chunks");
   if (!C.empty())
     HIP_TRY(hipMemcpyAsync(e->d_pull.p, C.data(), C.size() * sizeof(PullChunk),
@@ -741,14 +757,16 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   const uint32_t planned0 = max_depth + max_start + 1;
   // level mode: single rank, staged path only, every active topic a
   // single-start tree
-  bool level = world == 1 && !need_direct && !any_mesh && !e->no_level &&
-               planned0 + 1 < kMaxRoundsCap;
+  // (pull: any rank count and fan-out; the push kernel's level schedule needs
+  // the staged path: one rank, fan-out <= 64)
+  bool level = !any_mesh && !e->no_level && planned0 + 1 < kMaxRoundsCap;
   for (uint32_t t = 0; t < nt && level; ++t)
     if (tab[t].W && !(tab[t].flags & kTopicSingleStart)) level = false;
+  if (level && e->level_push && need_direct) level = false;
   std::vector<uint32_t> lgrid;  // level mode: expand grid of every round
   const bool pull = level && !e->level_push;
   // fused pull (two levels per launch): every active topic starts together
-  bool fuse = pull && !e->no_fuse;
+  bool fuse = pull && !e->no_fuse && world == 1;
   for (uint32_t t = 0; t < nt && fuse; ++t)
     if (tab[t].W && tstart[t] != max_start) fuse = false;
   if (level) {
@@ -841,7 +859,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     HIP_TRY(launch_init_nodes(e->d_remote_fed.as<uint32_t>(), e->n_remote_fed,
                               e->d_node_topic.as<uint16_t>(), e->d_topics.as<TopicDev>(),
                               e->d_seen.as<uint64_t>(), e->d_arr0.as<uint64_t>(),
-                              e->d_arr1.as<uint64_t>(), e->d_gen.as<uint8_t>(), e->gen_cur, s),
+                              e->d_arr1.as<uint64_t>(), e->d_gen.as<uint8_t>(), e->gen_cur, !level, s),
             "init remote-fed rows");
   if (e->cfg.flags & PS_F_NO_LAZY_SEEN) {
     // eager variant: clear every row and mark every node current, so the
@@ -930,6 +948,34 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     if (!begin) ev_used += 2;
     return c;
   };
+  // all-to-allv of this round's send regions, then the apply kernel
+  auto xchg = [&](uint32_t rr) -> int {
+    std::string xerr;
+    hipError_t xe = e->transport->exchange(a.send, s_off, s_len, e->d_recv.as<uint8_t>(), r_off,
+                                           r_len, s, &xerr);
+    if (xe != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
+    ApplyArgs ap{};
+    ap.recv = e->d_recv.as<uint8_t>();
+    ap.world = static_cast<uint32_t>(world);
+    ap.cap_pre[0] = 0;
+    for (int32_t q = 0; q < world; ++q) {
+      ap.recv_off[q] = r_off[q];
+      ap.cap_pre[q + 1] = ap.cap_pre[q] + cap[rr][q * world + me];
+    }
+    ap.node_topic = a.node_topic;
+    ap.node_flags = a.node_flags;
+    ap.topics = a.topics;
+    ap.seen = a.seen;
+    ap.a_next = a.a_next;
+    ap.next_flag = level ? nullptr : a.next_flag;
+    ap.blk_flag = level ? nullptr : a.blk_flag;
+    ap.hop_rec = a.hop_rec;
+    ap.stats = e->d_apply_stats.as<uint64_t>() + static_cast<size_t>(rr) * kNumCtr;
+    ap.gen = level ? a.gen : nullptr;
+    ap.gen_cur = a.gen_cur;
+    HIP_TRY(launch_apply(ap, rr, record, s), "apply");
+    return PS_OK;
+  };
   if (level) {
     // static frontier: one expand launch per round, counters reduced once
     HIP_TRY(hipMemcpyAsync(e->d_woff.p, e->desc_host.data(), e->desc_host.size() * 4,
@@ -939,6 +985,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     for (r = 1; r <= planned0; ++r) {
       a.a_cur = arr[(r - 1) & 1];
       a.a_next = arr[r & 1];
+      const bool xr = layout(r);
+      if (xr)
+        for (int32_t q = 0; q < world; ++q)
+          if (s_len[q]) HIP_TRY(hipMemsetAsync(a.send + s_off[q], 0, kRegionHeader, s), "reset header");
       if (lgrid[r]) {
         HIP_TRY(time_mark(true), "event");
         ++launches;
@@ -967,6 +1017,14 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         HIP_TRY(launch_expand(a, r, record, true, lgrid[r], s), "expand");
       }
       if (lgrid[r]) HIP_TRY(time_mark(false), "event");
+      if (pull && world > 1 && e->split_off[r + 1] > e->split_off[r])
+        HIP_TRY(launch_send(a, e->d_split.as<uint32_t>() + e->split_off[r],
+                            e->split_off[r + 1] - e->split_off[r], s),
+                "send");
+      if (xr) {
+        const int rc3 = xchg(r);
+        if (rc3) return rc3;
+      }
       HIP_TRY(seed_round(r, a.a_next), "seed");
     }
     r = planned0;
@@ -997,28 +1055,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       }
       HIP_TRY(time_mark(false), "event");
       if (xr) {
-        std::string xerr;
-        hipError_t xe = e->transport->exchange(a.send, s_off, s_len, e->d_recv.as<uint8_t>(), r_off,
-                                               r_len, s, &xerr);
-        if (xe != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
-        ApplyArgs ap{};
-        ap.recv = e->d_recv.as<uint8_t>();
-        ap.world = static_cast<uint32_t>(world);
-        ap.cap_pre[0] = 0;
-        for (int32_t q = 0; q < world; ++q) {
-          ap.recv_off[q] = r_off[q];
-          ap.cap_pre[q + 1] = ap.cap_pre[q] + cap[r][q * world + me];
-        }
-        ap.node_topic = a.node_topic;
-        ap.node_flags = a.node_flags;
-        ap.topics = a.topics;
-        ap.seen = a.seen;
-        ap.a_next = a.a_next;
-        ap.next_flag = a.next_flag;
-        ap.blk_flag = a.blk_flag;
-        ap.hop_rec = a.hop_rec;
-        ap.stats = e->d_apply_stats.as<uint64_t>() + static_cast<size_t>(r) * kNumCtr;
-        HIP_TRY(launch_apply(ap, r, record, s), "apply");
+        const int rc3 = xchg(r);
+        if (rc3) return rc3;
       }
       HIP_TRY(seed_round(r, a.a_next), "seed");
       HIP_TRY(compact(r, waves_r), "compact");

@@ -100,8 +100,11 @@ __global__ __launch_bounds__(kBlock) void k_window_init(const TopicDev* __restri
     gen[T.nbase] = static_cast<uint8_t>(gen_cur);
 }
 
-// Nodes fed by a parent on another rank: rows zeroed, generation current, so
-// the apply kernel can test-and-set them with atomics.
+// Nodes fed by a parent on another rank: rows zeroed, so the apply kernel can
+// test-and-set them with atomics.  Compaction mode stamps their generation
+// here (their rows are current from the start); level mode leaves that to
+// the apply kernel, which stamps a node when something reaches it, so that
+// "generation current" keeps meaning "reached this window".
 __global__ __launch_bounds__(kBlock) void k_init_nodes(const uint32_t* __restrict__ nodes,
                                                        uint32_t n,
                                                        const uint16_t* __restrict__ node_topic,
@@ -109,7 +112,8 @@ __global__ __launch_bounds__(kBlock) void k_init_nodes(const uint32_t* __restric
                                                        uint64_t* __restrict__ seen,
                                                        uint64_t* __restrict__ a0,
                                                        uint64_t* __restrict__ a1,
-                                                       uint8_t* __restrict__ gen, uint32_t gen_cur) {
+                                                       uint8_t* __restrict__ gen, uint32_t gen_cur,
+                                                       bool stamp) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = (blockIdx.x * kBlock + threadIdx.x) >> 6;
   const uint32_t n_waves = (gridDim.x * kBlock) >> 6;
@@ -123,7 +127,7 @@ __global__ __launch_bounds__(kBlock) void k_init_nodes(const uint32_t* __restric
       a0[row + w] = 0;
       a1[row + w] = 0;
     }
-    if (lane == 0) gen[u] = static_cast<uint8_t>(gen_cur);
+    if (lane == 0 && stamp) gen[u] = static_cast<uint8_t>(gen_cur);
   }
 }
 
@@ -984,6 +988,46 @@ __global__ __launch_bounds__(kBlock, kU <= 4 ? 8 : 1) void k_pull(PullArgs a, co
   }
 }
 
+// ------------------------------------------------------------------ send ---
+// Level mode, multi-GPU: the rows of this round's split parents (nodes with
+// children owned by other ranks) go to those children's owners.  One wave per
+// parent: a parent the window's messages reached (generation current) ships
+// its whole row, (child id at the owner, word, bits) per word, into the
+// owner's send region (one reservation per child).  Local children pull.
+__global__ __launch_bounds__(kBlock) void k_send(ExpandArgs a, const uint32_t* __restrict__ list,
+                                                 uint32_t n) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) >> 6);
+  const uint32_t n_waves = (gridDim.x * kBlock) >> 6;
+  const uint32_t cur = a.gen_cur & 0xFF;
+  for (uint32_t i = wave; i < n; i += n_waves) {
+    const uint32_t p = list[i];
+    if (a.gen[p] != cur) continue;  // not reached: nothing to forward
+    const TopicDev T = a.topics[a.node_topic[p]];
+    const uint32_t W = T.W;
+    const bool is_root = p == T.nbase && (T.flags & kTopicRootLocal);
+    const uint64_t* src = ((T.flags & kTopicSingleStart) && !is_root ? a.seen : a.a_cur) + T.wbase +
+                          static_cast<uint64_t>(p - T.nbase) * W;
+    for (uint32_t k = a.row_ptr[p]; k < a.row_ptr[p + 1]; ++k) {
+      const uint32_t c = a.col[k];
+      if (!(c & kRemoteBit)) continue;
+      const uint32_t dest = (c >> kRemoteRankShift) & 0xFu;
+      uint8_t* region = a.send + a.send_off[dest];
+      uint32_t base = 0;
+      if (lane == 0) base = atomicAdd(reinterpret_cast<uint32_t*>(region), W);
+      base = static_cast<uint32_t>(__shfl(static_cast<int>(base), 0, 64));
+      XItem* out = reinterpret_cast<XItem*>(region + kRegionHeader) + base;
+      for (uint32_t w = lane; w < W; w += 64) {
+        XItem it;
+        it.node = c & kRemoteIdMask;
+        it.word = w;
+        it.mask = src[w];
+        out[w] = it;
+      }
+    }
+  }
+}
+
 // ----------------------------------------------------------------- apply ---
 // Deliveries received from other ranks: test-and-set into the owned node's
 // row (atomic: its row was zeroed at window init), arrival row written whole
@@ -1014,11 +1058,12 @@ __global__ __launch_bounds__(kBlock) void k_apply(ApplyArgs a, uint32_t round) {
     const uint64_t old = atomicOr(reinterpret_cast<unsigned long long*>(a.seen + cw),
                                   static_cast<unsigned long long>(it.mask));
     const uint64_t nm = it.mask & ~old;
+    if (a.gen != nullptr && nm) a.gen[it.node] = static_cast<uint8_t>(a.gen_cur);  // reached
     if ((f & kNodeInternal) && !(T.flags & kTopicSingleStart)) a.a_next[cw] = nm;
     dup += __popcll(it.mask & old);
     if (nm) {
       deliv += __popcll(nm);
-      if (f & kNodeInternal) {
+      if ((f & kNodeInternal) && a.next_flag != nullptr) {
         a.next_flag[it.node] = 1;
         a.blk_flag[it.node >> kFlagBlockShift] = 1;
       }
@@ -1188,11 +1233,11 @@ hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_
 
 hipError_t launch_init_nodes(const uint32_t* nodes, uint32_t n, const uint16_t* node_topic,
                              const TopicDev* topics, uint64_t* seen, uint64_t* a0, uint64_t* a1,
-                             uint8_t* gen, uint32_t gen_cur, hipStream_t s) {
+                             uint8_t* gen, uint32_t gen_cur, bool stamp, hipStream_t s) {
   if (n == 0) return hipSuccess;
   const uint32_t grid = std::min<uint32_t>(1024, (n + 3) / 4);
   hipLaunchKernelGGL(k_init_nodes, dim3(grid), dim3(kBlock), 0, s, nodes, n, node_topic, topics,
-                     seen, a0, a1, gen, gen_cur);
+                     seen, a0, a1, gen, gen_cur, stamp);
   return hipGetLastError();
 }
 
@@ -1204,6 +1249,13 @@ hipError_t launch_apply(const ApplyArgs& a, uint32_t round, bool record, hipStre
     hipLaunchKernelGGL(k_apply<true>, dim3(grid), dim3(kBlock), 0, s, a, round);
   else
     hipLaunchKernelGGL(k_apply<false>, dim3(grid), dim3(kBlock), 0, s, a, round);
+  return hipGetLastError();
+}
+
+hipError_t launch_send(const ExpandArgs& a, const uint32_t* list, uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint32_t grid = std::min<uint32_t>(1024, (n + 3) / 4);
+  hipLaunchKernelGGL(k_send, dim3(grid), dim3(kBlock), 0, s, a, list, n);
   return hipGetLastError();
 }
 

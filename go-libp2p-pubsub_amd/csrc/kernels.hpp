@@ -147,6 +147,8 @@ struct ApplyArgs {
   uint8_t* blk_flag;
   uint8_t* hop_rec;
   uint64_t* stats;  // [kNumCtr] of this round (deliveries, duplicates)
+  uint8_t* gen;     // level mode: stamp a node reached (null: compaction mode)
+  uint32_t gen_cur;
 };
 
 // k_expand experiment knobs (PSAMD_DEBUG_EXPAND); results are wrong when set
@@ -166,9 +168,13 @@ constexpr int kFlagBlockShift = 12;
 hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_t* seen,
                               uint64_t* a0, uint64_t* a1, uint8_t* gen, uint32_t gen_cur,
                               bool any_mesh, hipStream_t s);
+// stamp: mark the nodes' generation current (compaction mode)
 hipError_t launch_init_nodes(const uint32_t* nodes, uint32_t n, const uint16_t* node_topic,
                              const TopicDev* topics, uint64_t* seen, uint64_t* a0, uint64_t* a1,
-                             uint8_t* gen, uint32_t gen_cur, hipStream_t s);
+                             uint8_t* gen, uint32_t gen_cur, bool stamp, hipStream_t s);
+// level mode, multi-GPU: rows of the reached split parents `list` to the
+// send regions of their remote children's owners
+hipError_t launch_send(const ExpandArgs& a, const uint32_t* list, uint32_t n, hipStream_t s);
 hipError_t launch_apply(const ApplyArgs& a, uint32_t round, bool record, hipStream_t s);
 // next_flag / blk_flag may be null (level mode: the root is in the schedule)
 hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t* arrivals,

@@ -6,6 +6,11 @@ Every rank builds the same topics (the restated joins are deterministic) and
 publishes the same messages; each owns a hash partition of every topic's tree
 nodes (PART_SUBTREE by default, PART_PEER = owner(p) = splitmix64(p) mod N).
 The job's deliveries are the sum over ranks; its time is the slowest rank's.
+
+Scaling: "weak" (default) keeps the per-GPU work of the N=1
+workload: the same topology, N x the messages (each rank holds 1/N of every
+tree, so it moves as many row words as one GPU does at N=1); "strong" runs
+the N=1 workload unchanged.
 """
 from __future__ import annotations
 
@@ -14,7 +19,7 @@ import os
 import sys
 import time
 
-from . import PART_PEER, PART_SUBTREE, Engine, unique_id
+from . import MODE_KERNEL, PART_PEER, PART_SUBTREE, Engine, unique_id
 from . import workloads as WL
 
 
@@ -31,6 +36,8 @@ def init(backend: str):
 
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29531")
+    os.environ.setdefault("RANK", "0")  # a single process (bench.py --force-dist)
+    os.environ.setdefault("WORLD_SIZE", "1")
     if not dist.is_initialized():
         dist.init_process_group(backend)
     return dist
@@ -54,18 +61,34 @@ def job_totals(dist, elapsed_s: float, local_count: int, device=None):
     return float(t.item()), int(round(c.item()))
 
 
+def workload(args, world: int):
+    """The bench workload at `world` ranks (weak scaling: N x the messages)."""
+    wl = WL.CONFIGS[args.workload]() if args.scale == 1.0 else WL.scaled(args.workload, args.scale)
+    if getattr(args, "scaling", "weak") == "weak" and world > 1:
+        import numpy as np
+
+        wl.msg_topics = np.tile(wl.msg_topics, world)
+    return wl
+
+
 def bench_main(args, descr: dict, metric: str):
     import torch
 
+    # RCCL prints its version banner on stdout when a communicator comes up:
+    # keep stdout for the one JSON line (rank 0), everything else to stderr
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
     rank, world, local = env_ranks()
     torch.cuda.set_device(local)
     dist = init("nccl")  # RCCL on ROCm
     dev = torch.device("cuda", local)
     part = PART_PEER if getattr(args, "partition", "subtree") == "peer" else PART_SUBTREE
-    wl = WL.CONFIGS[args.workload]() if args.scale == 1.0 else WL.scaled(args.workload, args.scale)
+    wl = workload(args, world)
+    scaling = getattr(args, "scaling", "weak") if world > 1 else "weak"
     uid = share_bytes(dist, unique_id, rank)
     t0 = time.perf_counter()
-    eng = Engine(wl.n_peers, len(wl.topics), device=local, time_kernels=True, seed=wl.seed)
+    # one window per topic (pull kernels take rows of any width)
+    eng = Engine(wl.n_peers, len(wl.topics), device=local, seed=wl.seed, msg_window=1 << 20)
     eng.dist_init(rank, world, uid, part)
     sizes = WL.build_engine_topics(eng, wl)
     expected = wl.expected_deliveries(sizes)
@@ -86,24 +109,30 @@ def bench_main(args, descr: dict, metric: str):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     local_deliv = 0
-    bytes_, exp_ms, launches = 0, 0.0, 0
     for _ in range(args.steps):
         st = step()
         local_deliv += st.deliveries
-        bytes_ += st.expand_bytes
-        exp_ms += st.expand_ms
-        launches += st.expand_launches
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
     wall, total = job_totals(dist, elapsed, local_deliv, dev)
+    # roofline pass: HIP events around every hot-kernel launch (untimed above)
+    eng.set_time_kernels(True)
+    bytes_, exp_ms, launches = 0, 0.0, 0
+    for _ in range(3):
+        st = step()
+        bytes_ += st.expand_bytes
+        exp_ms += st.expand_ms
+        launches += st.expand_launches
+    eng.set_time_kernels(False)
     _, tot_bytes = job_totals(dist, 0.0, bytes_, dev)
     slow_exp_ms, _ = job_totals(dist, exp_ms, 0, dev)
     if not args.no_check:
         assert total == expected * args.steps, (total, expected * args.steps)
     if rank == 0:
         value = total / wall
-        achieved = tot_bytes / max(1e-12, slow_exp_ms * 1e-3) / 1e9 / world  # per GPU
+        # per GPU: the job's expand bytes over the slowest rank's expand time / N
+        achieved = tot_bytes / max(1e-12, slow_exp_ms * 1e-3) / 1e9 / world
         out = {
             "metric": metric,
             "value": value,
@@ -113,7 +142,7 @@ def bench_main(args, descr: dict, metric: str):
             "warmup": args.warmup,
             "ms_per_step": wall * 1e3 / args.steps,
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic",
@@ -124,12 +153,14 @@ def bench_main(args, descr: dict, metric: str):
                                       f"({'peer' if part == PART_PEER else 'subtree'}), "
                                       "RCCL all-to-allv frontier exchange per round"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
-                         "frac": achieved / 8000.0, "traffic": None, "kernel": "k_expand",
+                         "frac": achieved / 8000.0, "traffic": None,
+                         "kernel": MODE_KERNEL.get(st.expand_mode, "k_expand"),
                          "note": "per-GPU: job expand bytes / slowest rank's expand time / N"},
             "last_step_rank0": {"rounds": st.rounds, "run_ms": st.run_ms,
                                 "expand_ms": st.expand_ms, "host_ms": st.host_ms},
         }
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     eng.close()
     dist.barrier()
     dist.destroy_process_group()

@@ -57,16 +57,20 @@ def merged_hops(engines, msg):
     return h.min(axis=0)  # every peer is owned by exactly one rank per topic
 
 
+@pytest.mark.parametrize("staggered", [True, False])
 @pytest.mark.parametrize("world,partition", [(2, PE.PART_SUBTREE), (3, PE.PART_PEER),
                                              (4, PE.PART_SUBTREE), (4, PE.PART_PEER)])
-def test_sharded_trees_match_oracle(world, partition):
-    rng = np.random.default_rng(world * 10 + partition)
+def test_sharded_trees_match_oracle(world, partition, staggered):
+    """Staggered starts run the compaction path; a single start round runs
+    level mode (pull kernel + split-parent send + apply stamping reached
+    remote-fed nodes), with dead peers cutting subtrees across ranks."""
+    rng = np.random.default_rng(world * 10 + partition + 100 * staggered)
     n, n_topics = 2500, 3
     lb, engines = make_ranks(world, n, n_topics, partition)
     trees = [random_tree(rng, n, int(rng.integers(0, n))) for _ in range(n_topics)]
     live = (rng.random(n) > 0.08).astype(np.uint8)
     topics = rng.integers(0, n_topics, size=150)
-    starts = rng.integers(0, 4, size=150)
+    starts = rng.integers(0, 4, size=150) if staggered else np.full(150, 2)
     for e in engines:
         for t in range(n_topics):
             e.set_tree(t, int(np.nonzero(trees[t] == O.NONE)[0][0]), trees[t])
