@@ -1,6 +1,7 @@
 // tree.cpp -- host-side subscription tree maintenance (see tree.hpp).
 #include "tree.hpp"
 
+#include <algorithm>
 #include <deque>
 
 #include "psengine.h"
@@ -10,8 +11,31 @@ namespace psamd {
 SubscriptionTree::SubscriptionTree(uint32_t n_peers, uint32_t root, uint32_t width,
                                    uint32_t max_width, uint64_t seed)
     : n_(n_peers), root_(root), width_(width), max_width_(max_width), rng_(seed),
-      state_(n_peers, PeerState::Out), up_(n_peers, kNone), kids_(n_peers) {
+      touched_mark_(n_peers, 0), state_(n_peers, PeerState::Out), up_(n_peers, kNone),
+      kids_(n_peers) {
   state_[root] = PeerState::In;
+}
+
+void SubscriptionTree::touch(uint32_t p) {
+  if (!touched_mark_[p]) {
+    touched_mark_[p] = 1;
+    touched_.push_back(p);
+  }
+}
+
+void SubscriptionTree::take_touched(std::vector<uint32_t>& out) {
+  out.swap(touched_);
+  touched_.clear();
+  for (uint32_t p : out) touched_mark_[p] = 0;
+}
+
+bool SubscriptionTree::reachable(uint32_t p) const {
+  for (uint32_t hops = 0; hops <= n_; ++hops) {
+    if (p == root_) return true;
+    if (state_[p] != PeerState::In || up_[p] == kNone) return false;
+    p = up_[p];
+  }
+  return false;
 }
 
 // SplitMix64: stands in for Go's randomised map iteration (rule Q2).
@@ -33,6 +57,7 @@ int SubscriptionTree::attach(uint32_t at, uint32_t joiner, bool prio) {
       list.push_back(ChildRec{joiner, kNone, 0, false});
       up_[joiner] = at;
       state_[joiner] = PeerState::In;
+      touch(joiner);
       // State{Peers:[joiner], NumPeers: sub.size(=0)} upstream (137-147);
       // only a node holding a live `in` stream sends it (client.go:106).
       const uint32_t gp = up_[at];
@@ -87,11 +112,15 @@ int SubscriptionTree::subscribe(uint32_t peer) {
 // (redistributeChildren, subtree.go:356-375); the rest are orphaned (Q5).
 void SubscriptionTree::depart(uint32_t at, uint32_t gone, uint32_t rescue) {
   for (const auto& r : kids_[gone])
-    if (r.id != rescue && state_[r.id] == PeerState::In) state_[r.id] = PeerState::Orphan;
+    if (r.id != rescue && state_[r.id] == PeerState::In) {
+      state_[r.id] = PeerState::Orphan;
+      touch(r.id);
+    }
   kids_[gone].clear();
   if (rescue == kNone) return;
   if (state_[rescue] != PeerState::In || up_[rescue] != gone) return;
   state_[rescue] = PeerState::Out;
+  touch(rescue);
   if (attach(at, rescue, true) != PS_OK) {
     state_[rescue] = PeerState::Orphan;
     up_[rescue] = gone;
@@ -103,6 +132,7 @@ int SubscriptionTree::close_client(uint32_t peer) {
   if (peer == root_ || state_[peer] != PeerState::In) return PS_E_STATE;
   const uint32_t at = up_[peer];
   state_[peer] = PeerState::Dead;
+  touch(peer);
   ChildRec* rec = nullptr;
   if (at != kNone && state_[at] != PeerState::Failed)  // a Part to a closed host is lost
     for (auto& r : kids_[at])
@@ -116,6 +146,7 @@ int SubscriptionTree::close_client(uint32_t peer) {
   }
   rec->parted = true;  // handleChildMessages Part (subtree.go:62-70)
   needs_pass_ = true;
+  parted_at_.push_back(at);
   depart(at, peer, rec->last_state);
   return PS_OK;
 }
@@ -125,6 +156,7 @@ int SubscriptionTree::close_host(uint32_t peer) {
   if (peer == root_) return PS_E_STATE;
   if (state_[peer] != PeerState::In && state_[peer] != PeerState::Orphan) return PS_E_STATE;
   state_[peer] = PeerState::Failed;
+  touch(peer);
   pending_failures_ = true;
   needs_pass_ = true;
   return PS_OK;
@@ -132,6 +164,39 @@ int SubscriptionTree::close_host(uint32_t peer) {
 
 void SubscriptionTree::after_message() {
   if (!needs_pass_) return;
+  if (!pending_failures_) {
+    // Parts only: the lazy prune at each forwarding node deletes Part'ed
+    // entries (subtree.go:329-331), draws nothing from the tie-break stream,
+    // so the order does not matter -- visit just the parents holding one,
+    // if the message reached them (an In-state path from the root).
+    std::sort(parted_at_.begin(), parted_at_.end());
+    parted_at_.erase(std::unique(parted_at_.begin(), parted_at_.end()), parted_at_.end());
+    std::vector<uint32_t> keep;
+    for (uint32_t p : parted_at_) {
+      if (p >= n_ || !reachable(p)) {
+        if (p < n_) keep.push_back(p);  // pruned by a later message that reaches it
+        continue;
+      }
+      auto& list = kids_[p];
+      size_t w = 0;
+      for (size_t i = 0; i < list.size(); ++i) {
+        const ChildRec r = list[i];
+        if (r.parted) {
+          if (state_[r.id] == PeerState::Dead) {
+            state_[r.id] = PeerState::Out;
+            up_[r.id] = kNone;
+            touch(r.id);
+          }
+          continue;
+        }
+        list[w++] = r;
+      }
+      list.resize(w);
+    }
+    parted_at_.swap(keep);
+    needs_pass_ = !parted_at_.empty();
+    return;
+  }
   // forwarding nodes in BFS order over subscribed peers
   std::vector<uint32_t> order;
   order.reserve(64);
@@ -153,6 +218,7 @@ void SubscriptionTree::after_message() {
         if (state_[r.id] == PeerState::Dead) {
           state_[r.id] = PeerState::Out;
           up_[r.id] = kNone;
+          touch(r.id);
         }
         continue;
       }
@@ -167,6 +233,16 @@ void SubscriptionTree::after_message() {
   }
   pending_failures_ = false;
   needs_pass_ = false;
+  // Part'ed entries under parents this message did not reach stay listed
+  std::vector<uint32_t> keep;
+  for (uint32_t p : parted_at_)
+    for (const auto& r : kids_[p])
+      if (r.parted) {
+        keep.push_back(p);
+        needs_pass_ = true;
+        break;
+      }
+  parted_at_.swap(keep);
   for (uint32_t p = 0; p < n_ && !pending_failures_; ++p)
     if (state_[p] == PeerState::Failed && up_[p] != kNone) {
       for (const auto& r : kids_[up_[p]])

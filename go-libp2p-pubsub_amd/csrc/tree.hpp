@@ -43,6 +43,11 @@ class SubscriptionTree {
   // Attached structure: parent of every peer reachable from the root through
   // subscribed peers, kNone elsewhere.
   void attached_parents(std::vector<uint32_t>& parent) const;
+  // Upstream of every subscribed (In) peer, kNone elsewhere; reachability from
+  // the root is left to the consumer (the GPU rebuild).  take_touched() hands
+  // out the peers whose entry may have changed since the last call.
+  uint32_t in_parent(uint32_t p) const { return state_[p] == PeerState::In && p != root_ ? up_[p] : kNone; }
+  void take_touched(std::vector<uint32_t>& out);
   // Peers reachable for the NEXT message (failed hosts cut their subtree).
   // Children lists in insertion order.
   const std::vector<ChildRec>& children(uint32_t p) const { return kids_[p]; }
@@ -55,10 +60,16 @@ class SubscriptionTree {
   void depart(uint32_t at, uint32_t gone, uint32_t rescue);
   uint64_t next_random();
 
+  bool reachable(uint32_t p) const;  // In-state path from the root
+  void touch(uint32_t p);             // (state, upstream) of p may have changed
+
   uint32_t n_ = 0, root_ = 0, width_ = 2, max_width_ = 5;
   uint64_t rng_ = 0;
   bool pending_failures_ = false;
   bool needs_pass_ = false;
+  std::vector<uint32_t> parted_at_;  // parents holding a Part'ed child entry
+  std::vector<uint32_t> touched_;    // peers whose attachment may have changed
+  std::vector<uint8_t> touched_mark_;
   std::vector<PeerState> state_;
   std::vector<uint32_t> up_;  // upstream peer (the other end of `in`)
   std::vector<std::vector<ChildRec>> kids_;

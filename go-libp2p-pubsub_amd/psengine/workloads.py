@@ -110,11 +110,41 @@ def cfg4(n_peers: int = 1 << 24, n_msgs: int = 1000) -> Workload:
                     np.zeros(n_msgs, dtype=np.uint32), 4)
 
 
-def cfg5(n_peers: int = 1_000_000, batches: int = 100, per_batch: int = 1000) -> Workload:
-    w = Workload("cfg5", n_peers, [TopicSpec(0, 2, 5, np.arange(1, n_peers, dtype=np.uint32))],
-                 np.zeros(batches * per_batch, dtype=np.uint32), 5)
-    w.notes = {"batches": batches, "per_batch": per_batch, "churn": 0.01}
+def cfg5(n_peers: int = 1_000_000, batches: int = 100, per_batch: int = 1000,
+         members: float = 0.9, churn: float = 0.01) -> Workload:
+    """Churn workload: peers 1..N-1 subscribe with probability `members` (join
+    order = peer order); then `batches` batches, each preceded by churn_plan's
+    leaves (churn x N current members, graceful Part) and joins (churn x N
+    current non-members)."""
+    peers = np.arange(1, n_peers, dtype=np.uint64)
+    sub = uniform(5, peers) < members
+    w = Workload("cfg5", n_peers, [TopicSpec(0, 2, 5, peers[sub].astype(np.uint32))],
+                 np.zeros(per_batch, dtype=np.uint32), 5)
+    w.notes = {"batches": batches, "per_batch": per_batch, "churn": churn}
     return w
+
+
+def churn_plan(wl: Workload, batches: int, seed: int = 5):
+    """Leave / join sets before each batch, from the generator's own member set
+    (a peer that leaves is a non-member from then on; a join makes a member).
+    The engine may refuse some (a leave of an orphaned peer): the plan does not
+    depend on that, so it is computed up front, outside any timed region."""
+    rng = np.random.default_rng(seed)
+    n = wl.n_peers
+    k = max(1, int(round(n * wl.notes["churn"])))
+    member = np.zeros(n, dtype=bool)
+    member[wl.topics[0].join_order] = True
+    plan = []
+    for _ in range(batches):
+        ins = np.nonzero(member)[0]
+        outs = np.nonzero(~member)[0]
+        outs = outs[outs != wl.topics[0].root]
+        leave = np.sort(rng.choice(ins, size=min(k, ins.size), replace=False)).astype(np.uint32)
+        join = np.sort(rng.choice(outs, size=min(k, outs.size), replace=False)).astype(np.uint32)
+        member[leave] = False
+        member[join] = True
+        plan.append((leave, join))
+    return plan
 
 
 CONFIGS = {"cfg1": cfg1, "cfg2": cfg2, "cfg3": cfg3, "cfg4": cfg4, "cfg5": cfg5}
@@ -128,6 +158,8 @@ def scaled(name: str, scale: float) -> Workload:
         return cfg3(max(256, int(1_000_000 * scale)), 64, max(64, int(100_000 * scale)))
     if name == "cfg4":
         return cfg4(max(16, int((1 << 24) * scale)), max(1, int(1000 * scale)))
+    if name == "cfg5":
+        return cfg5(max(256, int(1_000_000 * scale)), 100, max(16, int(1000 * scale)))
     return CONFIGS[name]()
 
 
