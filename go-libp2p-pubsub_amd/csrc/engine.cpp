@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "dist.hpp"
+#include "gbuild.hpp"
 #include "kernels.hpp"
 #include "psengine.h"
 #include "tree.hpp"
@@ -77,6 +78,10 @@ struct TopicHost {
   uint32_t max_deg = 0;
   std::vector<uint32_t> level_internal;  // BFS level -> owned nodes with children
   std::vector<uint32_t> level_off;       // single rank: BFS level -> first node (topic-relative)
+  // GPU rebuild: the upstream of every peer as last shipped to the device
+  std::vector<uint32_t> par_mirror;
+  bool par_dev_valid = false;  // the device parent array holds par_mirror
+  bool par_full_dirty = true;  // Kind::Parent: re-diff the whole array
   // cross-rank edges by the parent's BFS level: (level, from rank, to rank, count)
   struct Cross {
     uint32_t level, from, to, count;
@@ -110,6 +115,15 @@ struct ps_engine {
   bool no_single_start = false;  // PSAMD_NO_SINGLE_START=1: keep arrival rows (A/B)
   bool no_level = false;         // PSAMD_NO_LEVEL=1: always compact the frontier (A/B)
   bool host_timing = false;      // PSAMD_HOST_TIMING=1: host phase times to stderr
+  // GPU rebuild of the node space: on by default for one
+  // rank and tree topics (PSAMD_GPU_BUILD=0: host build)
+  bool gpu_build_on = true;
+  bool gpu_graph = false;     // the current node space was built on the GPU
+  bool mirrors_valid = true;  // host copies of node_peer / flags / CSR are current
+  std::vector<uint32_t> pairs_host, gstat_host, lvl_host, roots_host;
+  std::vector<size_t> pair_off;
+  DevBuf d_tpar, d_anc0, d_anc1, d_dep0, d_dep1, d_keys0, d_keys1, d_skeys, d_local, d_deg, d_first, d_lvl,
+      d_gstat, d_cub, d_pairs, d_live, d_roots;
   std::chrono::steady_clock::time_point t_run0;
   bool level_push = false;       // PSAMD_LEVEL_PUSH=1: level mode with the push kernel (A/B)
   uint32_t pull_words = kPullWords;  // words per pull chunk (PSAMD_PULL_WORDS)
@@ -426,32 +440,283 @@ void build_flags(ps_engine* e) {
     if (T.exists && T.n_nodes && T.root_local) e->node_flags[T.nbase] |= kNodeLive;  // roots forward
 }
 
+// Host copies of the node space when it was built on the GPU (record-mode
+// readback, ps_read_delivered, the push kernel's level schedule).
+int ensure_mirrors(ps_engine* e) {
+  if (e->mirrors_valid) return PS_OK;
+  const size_t nn = e->n_nodes;
+  e->node_peer.resize(nn);
+  e->node_parent.resize(nn);
+  e->node_topic.resize(nn);
+  e->node_flags.resize(nn);
+  e->row_ptr.resize(nn + 1);
+  hipStream_t s = e->stream;
+  HIP_TRY(hipMemcpyAsync(e->row_ptr.data(), e->d_row_ptr.p, (nn + 1) * 4, hipMemcpyDeviceToHost, s), "read row_ptr");
+  HIP_TRY(hipStreamSynchronize(s), "sync");
+  e->col.resize(e->row_ptr[nn]);
+  if (nn) {
+    HIP_TRY(hipMemcpyAsync(e->node_peer.data(), e->d_node_peer.p, nn * 4, hipMemcpyDeviceToHost, s), "read node_peer");
+    HIP_TRY(hipMemcpyAsync(e->node_parent.data(), e->d_node_parent.p, nn * 4, hipMemcpyDeviceToHost, s),
+            "read node_parent");
+    HIP_TRY(hipMemcpyAsync(e->node_topic.data(), e->d_node_topic.p, nn * 2, hipMemcpyDeviceToHost, s), "read node_topic");
+    HIP_TRY(hipMemcpyAsync(e->node_flags.data(), e->d_node_flags.p, nn, hipMemcpyDeviceToHost, s), "read node_flags");
+  }
+  if (!e->col.empty())
+    HIP_TRY(hipMemcpyAsync(e->col.data(), e->d_col.p, e->col.size() * 4, hipMemcpyDeviceToHost, s), "read col");
+  HIP_TRY(hipStreamSynchronize(s), "sync");
+  e->mirrors_valid = true;
+  return PS_OK;
+}
+
+bool can_gpu_build(const ps_engine* e) {
+  if (!e->gpu_build_on || e->world != 1 || e->cfg.n_peers >= (1u << kBuildPeerBits)) return false;
+  bool any = false;
+  for (const auto& T : e->topics) {
+    if (!T.exists) continue;
+    if (T.kind != Kind::Join && T.kind != Kind::Parent) return false;
+    any = true;
+  }
+  return any;
+}
+
+// GPU rebuild of the node space (gbuild.hip): ship the
+// changed upstream entries, then per topic depth (pointer jumping) -> sort
+// of (depth, parent, peer) -> node ids, parents, fan-out; one scan for the
+// CSR, flags from the live mask.  Two small readbacks: reachable counts and
+// depths (to lay out the topics), then the level tables.  *fallback: a tree
+// deeper than the sort key allows -- the caller builds on the host.
+int gpu_build_graph(ps_engine* e, bool* fallback) {
+  *fallback = false;
+  const uint32_t n = e->cfg.n_peers;
+  const uint32_t nt = static_cast<uint32_t>(e->topics.size());
+  hipStream_t s = e->stream;
+  HIP_TRY(e->d_tpar.ensure(static_cast<size_t>(nt) * n * 4), "alloc parents");
+  // 1. parent deltas of every topic, one upload
+  auto& pairs = e->pairs_host;
+  pairs.clear();
+  e->pair_off.assign(nt + 1, 0);
+  std::vector<uint32_t> cand;
+  for (uint32_t t = 0; t < nt; ++t) {
+    TopicHost& T = e->topics[t];
+    e->pair_off[t] = pairs.size() / 2;
+    if (!T.exists) continue;
+    uint32_t* par_t = e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n;
+    bool full = false;
+    if (!T.par_dev_valid) {
+      HIP_TRY(hipMemsetAsync(par_t, 0xFF, static_cast<size_t>(n) * 4, s), "clear parents");
+      T.par_mirror.assign(n, kNone);
+      T.par_dev_valid = true;
+      full = true;
+    }
+    auto diff = [&](uint32_t p, uint32_t v) {
+      if (T.par_mirror[p] != v) {
+        T.par_mirror[p] = v;
+        pairs.push_back(p);
+        pairs.push_back(v);
+      }
+    };
+    if (T.kind == Kind::Join) {
+      T.tree.take_touched(cand);
+      if (full)
+        for (uint32_t p = 0; p < n; ++p) diff(p, T.tree.in_parent(p));
+      else
+        for (uint32_t p : cand) diff(p, T.tree.in_parent(p));
+    } else if (T.par_full_dirty || full) {
+      for (uint32_t p = 0; p < n; ++p) diff(p, p == T.root ? kNone : T.parent[p]);
+      T.par_full_dirty = false;
+    }
+  }
+  e->pair_off[nt] = pairs.size() / 2;
+  if (!pairs.empty()) {
+    HIP_TRY(e->d_pairs.ensure(pairs.size() * 4), "alloc deltas");
+    HIP_TRY(hipMemcpyAsync(e->d_pairs.p, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, s),
+            "upload deltas");
+    for (uint32_t t = 0; t < nt; ++t)
+      HIP_TRY(launch_scatter_pairs(e->d_pairs.as<uint32_t>() + 2 * e->pair_off[t],
+                                   static_cast<uint32_t>(e->pair_off[t + 1] - e->pair_off[t]),
+                                   e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n, s),
+              "scatter deltas");
+  }
+  // 2. depth keys and sort per topic
+  HIP_TRY(e->d_anc0.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
+  HIP_TRY(e->d_anc1.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
+  HIP_TRY(e->d_dep0.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
+  HIP_TRY(e->d_dep1.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
+  HIP_TRY(e->d_keys0.ensure(static_cast<size_t>(n) * 8), "alloc keys");
+  HIP_TRY(e->d_skeys.ensure(static_cast<size_t>(nt) * n * 8), "alloc sorted keys");
+  HIP_TRY(e->d_gstat.ensure(static_cast<size_t>(nt) * 3 * 4), "alloc build stats");
+  HIP_TRY(e->d_lvl.ensure(static_cast<size_t>(nt) * 512 * 4), "alloc level tables");
+  HIP_TRY(hipMemsetAsync(e->d_lvl.p, 0, static_cast<size_t>(nt) * 512 * 4, s), "clear level tables");
+  HIP_TRY(e->d_keys1.ensure(static_cast<size_t>(n) * 8), "alloc keys");
+  HIP_TRY(hipMemsetAsync(e->d_gstat.p, 0, static_cast<size_t>(nt) * 3 * 4, s), "clear build stats");
+  size_t cub_bytes = 0, scan_bytes = 0;
+  HIP_TRY(sort_keys(nullptr, &cub_bytes, nullptr, nullptr, n, s), "sort size");
+  uint32_t* gstat = e->d_gstat.as<uint32_t>();  // [t][reach, max depth, max fan-out]
+  for (uint32_t t = 0; t < nt; ++t) {
+    const TopicHost& T = e->topics[t];
+    if (!T.exists) continue;
+    HIP_TRY(launch_depth_keys(e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n, n, T.root,
+                              e->d_anc0.as<uint32_t>(), e->d_anc1.as<uint32_t>(),
+                              e->d_dep0.as<uint32_t>(), e->d_dep1.as<uint32_t>(),
+                              e->d_keys0.as<uint64_t>(), gstat + 3 * t, gstat + 3 * t + 1, s),
+            "depth");
+    HIP_TRY(e->d_cub.ensure(std::max<size_t>(cub_bytes, 16)), "alloc sort temp");
+    size_t tb = e->d_cub.bytes;
+    HIP_TRY(sort_keys(e->d_cub.p, &tb, e->d_keys0.as<uint64_t>(),
+                      e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n, s),
+            "sort");
+    HIP_TRY(launch_level_starts(e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n,
+                                e->d_lvl.as<uint32_t>() + 512 * t, s),
+            "level starts");
+  }
+  // (level starts of unreachable peers' keys land in slot 255: ignored)
+  auto& gs = e->gstat_host;
+  gs.assign(static_cast<size_t>(nt) * 3, 0);
+  auto& lh = e->lvl_host;
+  lh.assign(static_cast<size_t>(nt) * 512, 0);
+  HIP_TRY(hipMemcpyAsync(gs.data(), gstat, gs.size() * 4, hipMemcpyDeviceToHost, s), "read build stats");
+  HIP_TRY(hipMemcpyAsync(lh.data(), e->d_lvl.p, lh.size() * 4, hipMemcpyDeviceToHost, s), "read level starts");
+  HIP_TRY(hipStreamSynchronize(s), "sync");
+  for (uint32_t t = 0; t < nt; ++t)
+    if (e->topics[t].exists && gs[3 * t + 1] >= kBuildMaxDepth) {
+      *fallback = true;  // deeper than the key's depth field
+      return PS_OK;
+    }
+  // 3. layout: topic t's nodes at [nbase_t, nbase_t + R_t)
+  uint64_t n_total = 0;
+  e->roots_host.clear();
+  for (uint32_t t = 0; t < nt; ++t) {
+    TopicHost& T = e->topics[t];
+    T.nbase = static_cast<uint32_t>(n_total);
+    T.n_nodes = T.exists ? gs[3 * t] : 0;
+    if (T.n_nodes) e->roots_host.push_back(T.nbase);
+    n_total += T.n_nodes;
+  }
+  if (n_total >= 0xFFFFFFF0ull) return e->fail(PS_E_NOMEM, "node space exceeds 2^32 nodes");
+  const uint32_t nn = static_cast<uint32_t>(n_total);
+  e->n_nodes = nn;
+  e->n_pad = std::max<uint32_t>(16, ((nn + 15) / 16) * 16);
+  HIP_TRY(e->d_row_ptr.ensure((static_cast<size_t>(nn) + 1) * 4), "alloc row_ptr");
+  HIP_TRY(e->d_col.ensure(std::max<size_t>(nn, 1) * 4), "alloc col");
+  HIP_TRY(e->d_node_topic.ensure(std::max<size_t>(nn, 1) * 2), "alloc node_topic");
+  HIP_TRY(e->d_node_peer.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_peer");
+  HIP_TRY(e->d_node_parent.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_parent");
+  HIP_TRY(e->d_node_flags.ensure(e->n_pad + 16), "alloc node_flags");
+  HIP_TRY(e->d_deg.ensure((static_cast<size_t>(nn) + 1) * 4), "alloc fan-out");
+  HIP_TRY(e->d_first.ensure(std::max<size_t>(nn, 1) * 4), "alloc first child");
+  HIP_TRY(e->d_local.ensure(static_cast<size_t>(n) * 4), "alloc local ids");
+  HIP_TRY(hipMemsetAsync(e->d_deg.p, 0, (static_cast<size_t>(nn) + 1) * 4, s), "clear fan-out");
+  HIP_TRY(hipMemsetAsync(e->d_first.p, 0xFF, std::max<size_t>(nn, 1) * 4, s), "clear first child");
+  uint32_t* lvl = e->d_lvl.as<uint32_t>();  // [t][0..255] level start, [t][256..511] internal count
+  // BFS placement, level by level: level d re-keyed by its parents' node ids
+  // (placed with level d - 1) and sorted, so siblings are consecutive and in
+  // their parents' order
+  for (uint32_t t = 0; t < nt; ++t) {
+    TopicHost& T = e->topics[t];
+    if (!T.n_nodes) continue;
+    const uint32_t depth = gs[3 * t + 1];
+    const uint64_t* keys = e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n;
+    for (uint32_t d = 0; d <= depth; ++d) {
+      const uint32_t lo = lh[512 * t + d];
+      const uint32_t hi = d == depth ? T.n_nodes : lh[512 * t + d + 1];
+      const uint32_t cnt = hi - lo;
+      if (d == 0) {
+        HIP_TRY(launch_place(keys, 1, T.nbase, static_cast<uint16_t>(t), true, e->d_node_peer.as<uint32_t>(),
+                             e->d_node_topic.as<uint16_t>(), e->d_local.as<uint32_t>(),
+                             e->d_node_parent.as<uint32_t>(), e->d_deg.as<uint32_t>(),
+                             e->d_first.as<uint32_t>(), s),
+                "place root");
+        continue;
+      }
+      HIP_TRY(launch_rekey(keys + lo, cnt, e->d_local.as<uint32_t>(), e->d_keys0.as<uint64_t>(), s), "rekey");
+      size_t tb = e->d_cub.bytes;
+      HIP_TRY(sort_keys(e->d_cub.p, &tb, e->d_keys0.as<uint64_t>(), e->d_keys1.as<uint64_t>(), cnt, s),
+              "sort level");
+      HIP_TRY(launch_place(e->d_keys1.as<uint64_t>(), cnt, T.nbase + lo, static_cast<uint16_t>(t), false,
+                           e->d_node_peer.as<uint32_t>(), e->d_node_topic.as<uint16_t>(),
+                           e->d_local.as<uint32_t>(), e->d_node_parent.as<uint32_t>(),
+                           e->d_deg.as<uint32_t>(), e->d_first.as<uint32_t>(), s),
+              "place level");
+    }
+  }
+  for (uint32_t t = 0; t < nt; ++t) {
+    const TopicHost& T = e->topics[t];
+    if (!T.n_nodes) continue;
+    HIP_TRY(launch_level_internal(e->d_deg.as<uint32_t>(), T.nbase, T.n_nodes, lvl + 512 * t, gs[3 * t + 1],
+                                  lvl + 512 * t + 256, gstat + 3 * t + 2, s),
+            "level stats");
+  }
+  // 4. CSR: row_ptr = exclusive scan of the fan-out; children consecutive
+  HIP_TRY(scan_u32(nullptr, &scan_bytes, nullptr, nullptr, nn + 1, s), "scan size");
+  HIP_TRY(e->d_cub.ensure(std::max<size_t>(scan_bytes, 16)), "alloc scan temp");
+  size_t tb = e->d_cub.bytes;
+  HIP_TRY(scan_u32(e->d_cub.p, &tb, e->d_deg.as<uint32_t>(), e->d_row_ptr.as<uint32_t>(), nn + 1, s), "scan");
+  HIP_TRY(launch_fill_col(e->d_row_ptr.as<uint32_t>(), e->d_first.as<uint32_t>(), nn, e->d_col.as<uint32_t>(), s),
+          "fill col");
+  // 5. level tables back to the host (rounds, chunks, grid bounds)
+  HIP_TRY(hipMemcpyAsync(lh.data(), lvl, lh.size() * 4, hipMemcpyDeviceToHost, s), "read level tables");
+  HIP_TRY(hipMemcpyAsync(gs.data(), gstat, gs.size() * 4, hipMemcpyDeviceToHost, s), "read build stats");
+  HIP_TRY(hipStreamSynchronize(s), "sync");
+  for (uint32_t t = 0; t < nt; ++t) {
+    TopicHost& T = e->topics[t];
+    T.mesh = false;
+    T.root_local = true;
+    T.cross.clear();
+    T.depth = T.n_nodes ? gs[3 * t + 1] : 0;
+    T.max_deg = gs[3 * t + 2];
+    T.level_off.assign(T.depth + 2, 0);
+    T.level_internal.assign(T.depth + 1, 0);
+    if (!T.n_nodes) continue;
+    for (uint32_t d = 0; d <= T.depth; ++d) {
+      T.level_off[d] = lh[512 * t + d];
+      T.level_internal[d] = lh[512 * t + 256 + d];
+    }
+    T.level_off[T.depth + 1] = T.n_nodes;
+  }
+  e->remote_fed.clear();
+  e->gpu_graph = true;
+  e->mirrors_valid = false;
+  return PS_OK;
+}
+
 int upload_graph(ps_engine* e) {
   if (e->graph_dirty) {
-    int rc = build_graph(e);
-    if (rc) return rc;
-    const size_t nn = e->n_nodes;
-    HIP_TRY(e->d_row_ptr.ensure((nn + 1) * 4), "alloc row_ptr");
-    HIP_TRY(e->d_col.ensure(std::max<size_t>(e->col.size(), 1) * 4), "alloc col");
-    HIP_TRY(e->d_node_topic.ensure(std::max<size_t>(nn, 1) * 2), "alloc node_topic");
-    HIP_TRY(e->d_node_peer.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_peer");
-    HIP_TRY(e->d_node_parent.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_parent");
-    // padded to n_pad: the expand kernel stages flag bytes as whole dwords
-    HIP_TRY(e->d_node_flags.ensure(e->n_pad + 16), "alloc node_flags");
-    HIP_TRY(hipMemcpyAsync(e->d_row_ptr.p, e->row_ptr.data(), (nn + 1) * 4, hipMemcpyHostToDevice, e->stream),
-            "upload row_ptr");
-    if (!e->col.empty())
-      HIP_TRY(hipMemcpyAsync(e->d_col.p, e->col.data(), e->col.size() * 4, hipMemcpyHostToDevice, e->stream),
-              "upload col");
-    if (nn) {
-      HIP_TRY(hipMemcpyAsync(e->d_node_topic.p, e->node_topic.data(), nn * 2, hipMemcpyHostToDevice, e->stream),
-              "upload node_topic");
-      HIP_TRY(hipMemcpyAsync(e->d_node_peer.p, e->node_peer.data(), nn * 4, hipMemcpyHostToDevice, e->stream),
-              "upload node_peer");
-      HIP_TRY(hipMemcpyAsync(e->d_node_parent.p, e->node_parent.data(), nn * 4, hipMemcpyHostToDevice,
-                             e->stream),
-              "upload node_parent");
+    bool built = false;
+    if (can_gpu_build(e)) {
+      bool fallback = false;
+      int rc = gpu_build_graph(e, &fallback);
+      if (rc) return rc;
+      built = !fallback;
     }
+    if (!built) {
+      int rc = build_graph(e);
+      if (rc) return rc;
+      e->gpu_graph = false;
+      e->mirrors_valid = true;
+      const size_t nn = e->n_nodes;
+      HIP_TRY(e->d_row_ptr.ensure((nn + 1) * 4), "alloc row_ptr");
+      HIP_TRY(e->d_col.ensure(std::max<size_t>(e->col.size(), 1) * 4), "alloc col");
+      HIP_TRY(e->d_node_topic.ensure(std::max<size_t>(nn, 1) * 2), "alloc node_topic");
+      HIP_TRY(e->d_node_peer.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_peer");
+      HIP_TRY(e->d_node_parent.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_parent");
+      // padded to n_pad: the expand kernel stages flag bytes as whole dwords
+      HIP_TRY(e->d_node_flags.ensure(e->n_pad + 16), "alloc node_flags");
+      HIP_TRY(hipMemcpyAsync(e->d_row_ptr.p, e->row_ptr.data(), (nn + 1) * 4, hipMemcpyHostToDevice, e->stream),
+              "upload row_ptr");
+      if (!e->col.empty())
+        HIP_TRY(hipMemcpyAsync(e->d_col.p, e->col.data(), e->col.size() * 4, hipMemcpyHostToDevice, e->stream),
+                "upload col");
+      if (nn) {
+        HIP_TRY(hipMemcpyAsync(e->d_node_topic.p, e->node_topic.data(), nn * 2, hipMemcpyHostToDevice, e->stream),
+                "upload node_topic");
+        HIP_TRY(hipMemcpyAsync(e->d_node_peer.p, e->node_peer.data(), nn * 4, hipMemcpyHostToDevice, e->stream),
+                "upload node_peer");
+        HIP_TRY(hipMemcpyAsync(e->d_node_parent.p, e->node_parent.data(), nn * 4, hipMemcpyHostToDevice,
+                               e->stream),
+                "upload node_parent");
+      }
+    }
+    const size_t nn = e->n_nodes;
     bool fresh = false;
     const size_t flag_bytes = static_cast<size_t>(ceil_div(e->n_pad, kFlagsPerBlock)) * kFlagsPerBlock;
     HIP_TRY(e->d_flags.ensure(flag_bytes, &fresh), "alloc flags");
@@ -478,10 +743,28 @@ int upload_graph(ps_engine* e) {
   }
   if (e->flags_dirty) {
     ++e->flags_epoch;
-    build_flags(e);
-    if (e->n_nodes)
-      HIP_TRY(hipMemcpyAsync(e->d_node_flags.p, e->node_flags.data(), e->n_nodes, hipMemcpyHostToDevice, e->stream),
-              "upload node_flags");
+    if (e->gpu_graph) {
+      const uint32_t n = e->cfg.n_peers;
+      HIP_TRY(e->d_live.ensure(n), "alloc live mask");
+      HIP_TRY(e->d_roots.ensure(std::max<size_t>(e->roots_host.size(), 1) * 4), "alloc roots");
+      HIP_TRY(hipMemcpyAsync(e->d_live.p, e->live.data(), n, hipMemcpyHostToDevice, e->stream), "upload live");
+      if (!e->roots_host.empty())
+        HIP_TRY(hipMemcpyAsync(e->d_roots.p, e->roots_host.data(), e->roots_host.size() * 4,
+                               hipMemcpyHostToDevice, e->stream),
+                "upload roots");
+      HIP_TRY(launch_node_flags(e->d_node_peer.as<uint32_t>(), e->d_row_ptr.as<uint32_t>(),
+                                e->d_live.as<uint8_t>(), e->n_nodes, e->d_roots.as<uint32_t>(),
+                                static_cast<uint32_t>(e->roots_host.size()), e->d_node_flags.as<uint8_t>(),
+                                e->stream),
+              "node flags");
+      e->mirrors_valid = false;
+    } else {
+      build_flags(e);
+      if (e->n_nodes)
+        HIP_TRY(hipMemcpyAsync(e->d_node_flags.p, e->node_flags.data(), e->n_nodes, hipMemcpyHostToDevice,
+                               e->stream),
+                "upload node_flags");
+    }
     e->flags_dirty = false;
   }
   // host mirrors may be rebuilt by the next call: finish the uploads now
@@ -506,6 +789,10 @@ int build_schedule(ps_engine* e, const std::vector<TopicDev>& tab,
   for (uint32_t t = 0; t < nt; ++t) key.push_back(tab[t].W ? tstart[t] : ~0ull);
   if (key == e->sched_key) return PS_OK;
   e->sched_key.clear();
+  {
+    int rc = ensure_mirrors(e);
+    if (rc) return rc;
+  }
   auto& S = e->sched_host;
   auto& off = e->sched_off;
   S.clear();
@@ -556,6 +843,10 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
     return PS_OK;
   }
   e->pull_key.clear();
+  // parent-range staging and fused launches read host mirrors of the node
+  // space; a GPU-built one (BFS order too) is used without them
+  const bool gpu = e->gpu_graph;
+  if (gpu) *fuse = false;
   auto& C = e->pull_host;
   auto& off = e->pull_off;
   auto build = [&](bool fused) -> bool {
@@ -583,8 +874,8 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
           const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, e->pull_words / W));
           for (uint32_t u = lo; u < hi; u += per)
             C.push_back(PullChunk{T.nbase + u, T.nbase + std::min(u + per, hi), 0, 0, t,
-                                  e->node_parent[T.nbase + u],
-                                  e->node_parent[T.nbase + std::min(u + per, hi) - 1], 0});
+                                  gpu ? kNone : e->node_parent[T.nbase + u],
+                                  gpu ? kNone : e->node_parent[T.nbase + std::min(u + per, hi) - 1], 0});
           continue;
         }
         // fused: a run of level-d nodes plus their children (consecutive ids:
@@ -1135,6 +1426,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   }
 
   if (record) {
+    {
+      int rcm = ensure_mirrors(e);
+      if (rcm) return rcm;
+    }
     std::vector<uint8_t> hr(wtot * 64);
     if (!hr.empty()) {
       HIP_TRY(hipMemcpyAsync(hr.data(), e->d_hop.p, hr.size(), hipMemcpyDeviceToHost, s), "read hops");
@@ -1224,6 +1519,7 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_NO_SINGLE_START")) e->no_single_start = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_NO_LEVEL")) e->no_level = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_HOST_TIMING")) e->host_timing = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_LEVEL_PUSH")) e->level_push = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_WORDS")) e->pull_words = std::max(64, std::atoi(v));
   if (const char* v = std::getenv("PSAMD_PULL_FUSE")) e->no_fuse = std::atoi(v) == 0;
@@ -1354,6 +1650,7 @@ int ps_topic_set_tree(ps_engine* e, uint32_t topic, uint32_t root, const uint32_
   T.kind = Kind::Parent;
   T.root = root;
   T.parent.assign(parent, parent + e->cfg.n_peers);
+  T.par_full_dirty = true;
   e->graph_dirty = true;
   return PS_OK;
 }
@@ -1580,6 +1877,10 @@ int ps_read_delivered(ps_engine* e, uint32_t msg, uint8_t* out) {
     return e->fail(PS_E_NOTREADY, "message not in the last window");
   const uint32_t li = rank - e->last_lo[t];
   const TopicDev& d = e->last_topics[t];
+  {
+    int rcm = ensure_mirrors(e);
+    if (rcm) return rcm;
+  }
   std::memset(out, 0, e->cfg.n_peers);
   std::vector<uint64_t> col(d.n_nodes);
   // one word per node: strided copy of this message's word column

@@ -1,0 +1,345 @@
+// gbuild.hip -- gfx950 kernels of the GPU node-space rebuild (gbuild.hpp).
+// Integer work over peer-indexed arrays: coalesced, HBM/latency-bound; the
+// sort and the scan are hipcub's (rocPRIM) device primitives.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+
+#include "gbuild.hpp"
+#include "kernels.hpp"
+
+namespace psamd {
+
+namespace {
+
+constexpr uint32_t kB = 256;
+constexpr uint32_t kNoneP = 0xFFFFFFFFu;
+constexpr uint64_t kPeerMask = (1ull << kBuildPeerBits) - 1ull;
+
+uint32_t blocks(uint64_t n) { return static_cast<uint32_t>(std::max<uint64_t>(1, (n + kB - 1) / kB)); }
+
+__global__ __launch_bounds__(kB) void k_scatter_pairs(const uint32_t* __restrict__ pairs, uint32_t n,
+                                                      uint32_t* __restrict__ par) {
+  const uint32_t i = blockIdx.x * kB + threadIdx.x;
+  if (i < n) par[pairs[2 * i]] = pairs[2 * i + 1];
+}
+
+// anc = upstream (root: itself), dep = 1 (root: 0)
+__global__ __launch_bounds__(kB) void k_depth_init(const uint32_t* __restrict__ par, uint32_t n,
+                                                   uint32_t root, uint32_t* __restrict__ anc,
+                                                   uint32_t* __restrict__ dep) {
+  const uint32_t p = blockIdx.x * kB + threadIdx.x;
+  if (p >= n) return;
+  anc[p] = p == root ? root : par[p];
+  dep[p] = p == root ? 0u : 1u;
+}
+
+// One pointer-jumping step: dep += dep[anc], anc = anc[anc]; the root is a
+// fixed point, kNone (not subscribed / cut) absorbs.
+__global__ __launch_bounds__(kB) void k_depth_jump(const uint32_t* __restrict__ ai,
+                                                   const uint32_t* __restrict__ di,
+                                                   uint32_t* __restrict__ ao, uint32_t* __restrict__ dout,
+                                                   uint32_t n, uint32_t root) {
+  const uint32_t p = blockIdx.x * kB + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t a = ai[p];
+  if (a == kNoneP || a == root) {
+    ao[p] = a;
+    dout[p] = di[p];
+    return;
+  }
+  ao[p] = ai[a];
+  dout[p] = di[p] + di[a];
+}
+
+__global__ __launch_bounds__(kB) void k_depth_keys(const uint32_t* __restrict__ anc,
+                                                   const uint32_t* __restrict__ dep,
+                                                   const uint32_t* __restrict__ par, uint32_t n,
+                                                   uint32_t root, uint64_t* __restrict__ keys,
+                                                   uint32_t* __restrict__ reach,
+                                                   uint32_t* __restrict__ max_depth) {
+  const uint32_t p = blockIdx.x * kB + threadIdx.x;
+  bool ok = false;
+  uint32_t d = 0;
+  if (p < n) {
+    ok = anc[p] == root;
+    uint64_t k = ~0ull;
+    if (ok) {
+      d = dep[p];
+      const uint64_t pp = p == root ? 0ull : par[p];
+      k = (static_cast<uint64_t>(min(d, kBuildMaxDepth)) << 56) | (pp << kBuildPeerBits) | p;
+    }
+    keys[p] = k;
+  }
+  const uint64_t b = __ballot(ok);
+  uint32_t m = d;
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), s, 64)));
+  if ((threadIdx.x & 63) == 0) {
+    if (b) atomicAdd(reach, static_cast<uint32_t>(__popcll(b)));
+    if (m) atomicMax(max_depth, m);
+  }
+}
+
+__global__ __launch_bounds__(kB) void k_layout(const uint64_t* __restrict__ keys, uint32_t R,
+                                               uint32_t nbase, uint16_t topic,
+                                               uint32_t* __restrict__ node_peer,
+                                               uint16_t* __restrict__ node_topic,
+                                               uint32_t* __restrict__ local) {
+  const uint32_t u = blockIdx.x * kB + threadIdx.x;
+  if (u >= R) return;
+  const uint32_t peer = static_cast<uint32_t>(keys[u] & kPeerMask);
+  node_peer[nbase + u] = peer;
+  node_topic[nbase + u] = topic;
+  local[peer] = nbase + u;
+}
+
+__global__ __launch_bounds__(kB) void k_link(const uint64_t* __restrict__ keys, uint32_t R,
+                                             uint32_t nbase, const uint32_t* __restrict__ local,
+                                             uint32_t* __restrict__ node_parent,
+                                             uint32_t* __restrict__ deg, uint32_t* __restrict__ first,
+                                             uint32_t* __restrict__ lvl_start) {
+  const uint32_t u = blockIdx.x * kB + threadIdx.x;
+  if (u >= R) return;
+  const uint64_t k = keys[u];
+  const uint32_t d = static_cast<uint32_t>(k >> 56);
+  if (u == 0 || static_cast<uint32_t>(keys[u - 1] >> 56) != d) lvl_start[d] = u;
+  if (u == 0) {  // depth 0: the root, alone
+    node_parent[nbase] = kNoneP;
+    return;
+  }
+  const uint32_t pu = local[static_cast<uint32_t>((k >> kBuildPeerBits) & kPeerMask)];
+  node_parent[nbase + u] = pu;
+  atomicAdd(deg + pu, 1u);
+  atomicMin(first + pu, nbase + u);
+}
+
+__global__ __launch_bounds__(kB) void k_level_stats(const uint64_t* __restrict__ keys, uint32_t R,
+                                                    uint32_t nbase, const uint32_t* __restrict__ deg,
+                                                    uint32_t* __restrict__ lvl_internal,
+                                                    uint32_t* __restrict__ max_deg) {
+  const uint32_t u = blockIdx.x * kB + threadIdx.x;
+  uint32_t dg = 0;
+  if (u < R) {
+    dg = deg[nbase + u];
+    if (dg) atomicAdd(lvl_internal + static_cast<uint32_t>(keys[u] >> 56), 1u);
+  }
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) dg = max(dg, static_cast<uint32_t>(__shfl_xor(static_cast<int>(dg), s, 64)));
+  if ((threadIdx.x & 63) == 0 && dg) atomicMax(max_deg, dg);
+}
+
+__global__ __launch_bounds__(kB) void k_fill_col(const uint32_t* __restrict__ row_ptr,
+                                                 const uint32_t* __restrict__ first, uint32_t n_nodes,
+                                                 uint32_t* __restrict__ col) {
+  const uint32_t u = blockIdx.x * kB + threadIdx.x;
+  if (u >= n_nodes) return;
+  const uint32_t b = row_ptr[u], e = row_ptr[u + 1];
+  for (uint32_t k = b; k < e; ++k) col[k] = first[u] + (k - b);
+}
+
+__global__ __launch_bounds__(kB) void k_node_flags(const uint32_t* __restrict__ node_peer,
+                                                   const uint32_t* __restrict__ row_ptr,
+                                                   const uint8_t* __restrict__ live, uint32_t n_nodes,
+                                                   uint8_t* __restrict__ flags) {
+  const uint32_t u = blockIdx.x * kB + threadIdx.x;
+  if (u >= n_nodes) return;
+  uint8_t f = live[node_peer[u]] ? kNodeLive : 0;
+  if (row_ptr[u + 1] > row_ptr[u]) f |= kNodeInternal;
+  flags[u] = f;
+}
+
+__global__ __launch_bounds__(kB) void k_root_flags(const uint32_t* __restrict__ roots, uint32_t n,
+                                                   uint8_t* __restrict__ flags) {
+  const uint32_t i = blockIdx.x * kB + threadIdx.x;
+  if (i < n) flags[roots[i]] |= kNodeLive;  // roots forward (they are not recipients)
+}
+
+// Level starts of a topic's (depth, parent, peer)-sorted keys (first R valid).
+__global__ __launch_bounds__(kB) void k_level_starts(const uint64_t* __restrict__ keys, uint32_t R,
+                                                     uint32_t* __restrict__ lvl_start) {
+  const uint32_t u = blockIdx.x * kB + threadIdx.x;
+  if (u >= R) return;
+  const uint32_t d = static_cast<uint32_t>(keys[u] >> 56);
+  if (u == 0 || static_cast<uint32_t>(keys[u - 1] >> 56) != d) lvl_start[d] = u;
+}
+
+// Level d's keys re-keyed by the parent's node id (placed with level d - 1):
+// sorting them gives BFS order (siblings consecutive, in parent order).
+__global__ __launch_bounds__(kB) void k_rekey(const uint64_t* __restrict__ keys, uint32_t n,
+                                              const uint32_t* __restrict__ local,
+                                              uint64_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * kB + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k = keys[i];
+  const uint32_t pu = local[static_cast<uint32_t>((k >> kBuildPeerBits) & kPeerMask)];
+  out[i] = (static_cast<uint64_t>(pu) << kBuildPeerBits) | (k & kPeerMask);
+}
+
+// Place one level: node ids [node0, node0 + n) in key order; key = parent
+// node << 28 | peer (root: parent kNone).
+__global__ __launch_bounds__(kB) void k_place(const uint64_t* __restrict__ keys, uint32_t n,
+                                              uint32_t node0, uint16_t topic, bool root,
+                                              uint32_t* __restrict__ node_peer,
+                                              uint16_t* __restrict__ node_topic,
+                                              uint32_t* __restrict__ local,
+                                              uint32_t* __restrict__ node_parent,
+                                              uint32_t* __restrict__ deg, uint32_t* __restrict__ first) {
+  const uint32_t i = blockIdx.x * kB + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k = keys[i];
+  const uint32_t peer = static_cast<uint32_t>(k & kPeerMask);
+  const uint32_t node = node0 + i;
+  node_peer[node] = peer;
+  node_topic[node] = topic;
+  local[peer] = node;
+  if (root) {
+    node_parent[node] = kNoneP;
+    return;
+  }
+  const uint32_t pu = static_cast<uint32_t>(k >> kBuildPeerBits);
+  node_parent[node] = pu;
+  atomicAdd(deg + pu, 1u);
+  atomicMin(first + pu, node);
+}
+
+// Internal nodes per level and the largest fan-out of a topic placed at
+// [nbase, nbase + R) with level starts lvl_start[0..depth] (topic-relative).
+__global__ __launch_bounds__(kB) void k_level_internal(const uint32_t* __restrict__ deg, uint32_t nbase,
+                                                       uint32_t R, const uint32_t* __restrict__ lvl_start,
+                                                       uint32_t depth, uint32_t* __restrict__ lvl_internal,
+                                                       uint32_t* __restrict__ max_deg) {
+  const uint32_t u = blockIdx.x * kB + threadIdx.x;
+  uint32_t dg = 0;
+  if (u < R) {
+    dg = deg[nbase + u];
+    if (dg) {
+      uint32_t lo = 0, hi = depth;  // last level whose start <= u
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) / 2;
+        if (lvl_start[mid] <= u)
+          lo = mid;
+        else
+          hi = mid - 1;
+      }
+      atomicAdd(lvl_internal + lo, 1u);
+    }
+  }
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) dg = max(dg, static_cast<uint32_t>(__shfl_xor(static_cast<int>(dg), s, 64)));
+  if ((threadIdx.x & 63) == 0 && dg) atomicMax(max_deg, dg);
+}
+
+}  // namespace
+
+hipError_t launch_level_starts(const uint64_t* keys, uint32_t R, uint32_t* lvl_start, hipStream_t s) {
+  if (R == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_level_starts, dim3(blocks(R)), dim3(kB), 0, s, keys, R, lvl_start);
+  return hipGetLastError();
+}
+
+hipError_t launch_rekey(const uint64_t* keys, uint32_t n, const uint32_t* local, uint64_t* out,
+                        hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_rekey, dim3(blocks(n)), dim3(kB), 0, s, keys, n, local, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_place(const uint64_t* keys, uint32_t n, uint32_t node0, uint16_t topic, bool root,
+                        uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
+                        uint32_t* node_parent, uint32_t* deg, uint32_t* first, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_place, dim3(blocks(n)), dim3(kB), 0, s, keys, n, node0, topic, root, node_peer,
+                     node_topic, local, node_parent, deg, first);
+  return hipGetLastError();
+}
+
+hipError_t launch_level_internal(const uint32_t* deg, uint32_t nbase, uint32_t R,
+                                 const uint32_t* lvl_start, uint32_t depth, uint32_t* lvl_internal,
+                                 uint32_t* max_deg, hipStream_t s) {
+  if (R == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_level_internal, dim3(blocks(R)), dim3(kB), 0, s, deg, nbase, R, lvl_start, depth,
+                     lvl_internal, max_deg);
+  return hipGetLastError();
+}
+
+hipError_t launch_scatter_pairs(const uint32_t* pairs, uint32_t n, uint32_t* par, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scatter_pairs, dim3(blocks(n)), dim3(kB), 0, s, pairs, n, par);
+  return hipGetLastError();
+}
+
+hipError_t launch_depth_keys(const uint32_t* par, uint32_t n, uint32_t root, uint32_t* anc0,
+                             uint32_t* anc1, uint32_t* dep0, uint32_t* dep1, uint64_t* keys,
+                             uint32_t* reach, uint32_t* max_depth, hipStream_t s) {
+  hipLaunchKernelGGL(k_depth_init, dim3(blocks(n)), dim3(kB), 0, s, par, n, root, anc0, dep0);
+  // after j steps every peer's ancestor is 2^j levels up: log2(n) + 1 steps
+  // reach the root from any depth
+  uint32_t steps = 1;
+  while ((1ull << steps) < n) ++steps;
+  uint32_t *ai = anc0, *ao = anc1, *di = dep0, *dout = dep1;
+  for (uint32_t j = 0; j <= steps; ++j) {
+    hipLaunchKernelGGL(k_depth_jump, dim3(blocks(n)), dim3(kB), 0, s, ai, di, ao, dout, n, root);
+    std::swap(ai, ao);
+    std::swap(di, dout);
+  }
+  hipLaunchKernelGGL(k_depth_keys, dim3(blocks(n)), dim3(kB), 0, s, ai, di, par, n, root, keys,
+                     reach, max_depth);
+  return hipGetLastError();
+}
+
+hipError_t sort_keys(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
+                     hipStream_t s) {
+  return hipcub::DeviceRadixSort::SortKeys(temp, *temp_bytes, in, out, n, 0, 64, s);
+}
+
+hipError_t scan_u32(void* temp, size_t* temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n,
+                    hipStream_t s) {
+  return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, in, out, n, s);
+}
+
+hipError_t launch_layout(const uint64_t* keys, uint32_t R, uint32_t nbase, uint16_t topic,
+                         uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
+                         hipStream_t s) {
+  if (R == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_layout, dim3(blocks(R)), dim3(kB), 0, s, keys, R, nbase, topic, node_peer,
+                     node_topic, local);
+  return hipGetLastError();
+}
+
+hipError_t launch_link(const uint64_t* keys, uint32_t R, uint32_t nbase, const uint32_t* local,
+                       uint32_t* node_parent, uint32_t* deg, uint32_t* first, uint32_t* lvl_start,
+                       hipStream_t s) {
+  if (R == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_link, dim3(blocks(R)), dim3(kB), 0, s, keys, R, nbase, local, node_parent,
+                     deg, first, lvl_start);
+  return hipGetLastError();
+}
+
+hipError_t launch_level_stats(const uint64_t* keys, uint32_t R, uint32_t nbase, const uint32_t* deg,
+                              uint32_t* lvl_internal, uint32_t* max_deg, hipStream_t s) {
+  if (R == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_level_stats, dim3(blocks(R)), dim3(kB), 0, s, keys, R, nbase, deg,
+                     lvl_internal, max_deg);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_col(const uint32_t* row_ptr, const uint32_t* first, uint32_t n_nodes,
+                           uint32_t* col, hipStream_t s) {
+  if (n_nodes == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fill_col, dim3(blocks(n_nodes)), dim3(kB), 0, s, row_ptr, first, n_nodes, col);
+  return hipGetLastError();
+}
+
+hipError_t launch_node_flags(const uint32_t* node_peer, const uint32_t* row_ptr,
+                             const uint8_t* live, uint32_t n_nodes, const uint32_t* roots,
+                             uint32_t n_roots, uint8_t* flags, hipStream_t s) {
+  if (n_nodes)
+    hipLaunchKernelGGL(k_node_flags, dim3(blocks(n_nodes)), dim3(kB), 0, s, node_peer, row_ptr, live,
+                       n_nodes, flags);
+  if (n_roots)
+    hipLaunchKernelGGL(k_root_flags, dim3(blocks(n_roots)), dim3(kB), 0, s, roots, n_roots, flags);
+  return hipGetLastError();
+}
+
+}  // namespace psamd

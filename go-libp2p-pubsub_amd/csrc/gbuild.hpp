@@ -1,0 +1,70 @@
+// gbuild.hpp -- GPU rebuild of the node space from per-topic parent arrays
+// (DESIGN.md §4.1).  Single rank, tree topics.
+//
+// For each topic: the upstream of every subscribed peer (kNone otherwise,
+// maintained on the host by the restated join / leave protocol and shipped as
+// deltas) -> depth of every peer reachable from the root (pointer jumping) ->
+// one radix sort of (depth, parent, peer) keys -> node ids: each BFS level is
+// a contiguous range, siblings are consecutive -> node_parent, CSR, flags.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace psamd {
+
+constexpr uint32_t kBuildMaxDepth = 255;  // depth bits of the sort key
+constexpr uint32_t kBuildPeerBits = 28;   // peer / parent bits of the sort key
+
+// (peer, value) pairs scattered into a parent array
+hipError_t launch_scatter_pairs(const uint32_t* pairs, uint32_t n, uint32_t* par, hipStream_t s);
+
+// Depth of every peer (pointer jumping): keys[p] = depth << 56 | parent << 28
+// | p for peers reachable from root, ~0 otherwise; *reach += reachable
+// count, *max_depth = max(depth).  Scratch: anc[2][n], dep[2][n].
+hipError_t launch_depth_keys(const uint32_t* par, uint32_t n, uint32_t root, uint32_t* anc0,
+                             uint32_t* anc1, uint32_t* dep0, uint32_t* dep1, uint64_t* keys,
+                             uint32_t* reach, uint32_t* max_depth, hipStream_t s);
+
+// hipcub radix sort of n keys (in -> out); temp queried when temp == nullptr
+hipError_t sort_keys(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
+                     hipStream_t s);
+// exclusive scan of n u32 (in -> out)
+hipError_t scan_u32(void* temp, size_t* temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n,
+                    hipStream_t s);
+
+// Node ids of one topic from its sorted keys (first R valid): node_peer,
+// node_topic, local[peer] = node; then node_parent, fan-out / first child of
+// every parent node and the level starts (lvl_start[d], topic-relative).
+// deg[] must be zeroed and first[] set to ~0 by the caller.
+hipError_t launch_layout(const uint64_t* keys, uint32_t R, uint32_t nbase, uint16_t topic,
+                         uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
+                         hipStream_t s);
+hipError_t launch_link(const uint64_t* keys, uint32_t R, uint32_t nbase, const uint32_t* local,
+                       uint32_t* node_parent, uint32_t* deg, uint32_t* first, uint32_t* lvl_start,
+                       hipStream_t s);
+// BFS placement, level by level: level starts of the sorted keys; level d's
+// keys re-keyed by their parent's node id (parent node << 28 | peer), sorted,
+// then placed at node0.. (node_peer, node_topic, local, node_parent, fan-out
+// and first child of the parents)
+hipError_t launch_level_starts(const uint64_t* keys, uint32_t R, uint32_t* lvl_start, hipStream_t s);
+hipError_t launch_rekey(const uint64_t* keys, uint32_t n, const uint32_t* local, uint64_t* out,
+                        hipStream_t s);
+hipError_t launch_place(const uint64_t* keys, uint32_t n, uint32_t node0, uint16_t topic, bool root,
+                        uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
+                        uint32_t* node_parent, uint32_t* deg, uint32_t* first, hipStream_t s);
+hipError_t launch_level_internal(const uint32_t* deg, uint32_t nbase, uint32_t R,
+                                 const uint32_t* lvl_start, uint32_t depth, uint32_t* lvl_internal,
+                                 uint32_t* max_deg, hipStream_t s);
+// per-level internal-node counts and the topic's largest fan-out
+hipError_t launch_level_stats(const uint64_t* keys, uint32_t R, uint32_t nbase, const uint32_t* deg,
+                              uint32_t* lvl_internal, uint32_t* max_deg, hipStream_t s);
+// col[row_ptr[u] + j] = first[u] + j
+hipError_t launch_fill_col(const uint32_t* row_ptr, const uint32_t* first, uint32_t n_nodes,
+                           uint32_t* col, hipStream_t s);
+// node flags from the live mask (per peer) and the fan-out; roots[] forced live
+hipError_t launch_node_flags(const uint32_t* node_peer, const uint32_t* row_ptr,
+                             const uint8_t* live, uint32_t n_nodes, const uint32_t* roots,
+                             uint32_t n_roots, uint8_t* flags, hipStream_t s);
+
+}  // namespace psamd

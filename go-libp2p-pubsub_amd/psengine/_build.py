@@ -12,8 +12,8 @@ LIB = os.path.join(LIBDIR, "libpsengine.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["kernels.hip", "engine.cpp", "tree.cpp", "dist.cpp"]
-HEADERS = ["kernels.hpp", "tree.hpp", "dist.hpp"]
+SOURCES = ["kernels.hip", "gbuild.hip", "engine.cpp", "tree.cpp", "dist.cpp"]
+HEADERS = ["kernels.hpp", "gbuild.hpp", "tree.hpp", "dist.hpp"]
 
 
 def _stale() -> bool:
