@@ -81,6 +81,39 @@ def cpu_baseline(eng, wl, sizes, budget_s: float = 10.0):
                       "subtree.go:319-354 + client.go:100-132); Go reference not buildable (no go)"}
 
 
+def cpu_baseline_cfg5(wl, plan, budget_s: float = 10.0):
+    """cfg5 on the CPU restatement (oracle/, a port), end to end per batch:
+    the restated leaves / joins (psoracle.c Tree), the attached tree as CSR,
+    the batch's messages by per-message BFS (OpenMP over messages) and the
+    lazy prune pass -- as many batches of the plan as fit the budget."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    ot = O.Tree(wl.n_peers, 0, 2, 5, PE.Engine.topic_seed(wl.seed, 0))
+    ot.join_all(wl.topics[0].join_order)
+    live = np.ones(wl.n_peers, dtype=np.uint8)
+    deliv, spent, batches = 0, 0.0, 0
+    for leave, join in plan:
+        if spent >= budget_s:
+            break
+        t0 = time.perf_counter()
+        for p in leave:
+            ot.leave(int(p))
+        for p in join:
+            ot.join(int(p))
+        rp, cl = O.parents_to_csr(ot.parents())
+        tot, _, _ = O.disseminate(rp, cl, 0, live, wl.n_msgs, want_hops=False, threads=threads)
+        ot.message()  # lazy prune / repair after the batch's first message
+        spent += time.perf_counter() - t0
+        deliv += tot
+        batches += 1
+    return {"value": deliv / spent, "unit": "deliveries/s", "cores": threads, "kind": "port",
+            "sample": f"{batches} batches of the cfg5 churn plan from the initial tree "
+                      f"({deliv} deliveries, {spent:.1f} s on {threads} host threads): "
+                      "oracle/psoracle.c tree restatement + or_disseminate"}
+
+
 def pmc_traffic(kernel: str, workload: str):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC passes
     (profiles/pmc_traffic.json, written by tools/pmc_traffic.py from separate
@@ -168,6 +201,8 @@ def bench_cfg5(args):
         "last_step": {"deliveries": st.deliveries, "rounds": st.rounds, "host_ms": st.host_ms,
                       "run_ms": st.run_ms},
     }
+    if not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline_cfg5(wl, plan, args.cpu_budget)
     print(json.dumps(out), flush=True)
     eng.close()
 
