@@ -544,41 +544,58 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   HIP_TRY(e->d_dep1.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
   HIP_TRY(e->d_keys0.ensure(static_cast<size_t>(n) * 8), "alloc keys");
   HIP_TRY(e->d_skeys.ensure(static_cast<size_t>(nt) * n * 8), "alloc sorted keys");
-  HIP_TRY(e->d_gstat.ensure(static_cast<size_t>(nt) * 3 * 4), "alloc build stats");
+  HIP_TRY(e->d_gstat.ensure(static_cast<size_t>(nt) * 4 * 4), "alloc build stats");
   HIP_TRY(e->d_lvl.ensure(static_cast<size_t>(nt) * 512 * 4), "alloc level tables");
-  HIP_TRY(hipMemsetAsync(e->d_lvl.p, 0, static_cast<size_t>(nt) * 512 * 4, s), "clear level tables");
   HIP_TRY(e->d_keys1.ensure(static_cast<size_t>(n) * 8), "alloc keys");
-  HIP_TRY(hipMemsetAsync(e->d_gstat.p, 0, static_cast<size_t>(nt) * 3 * 4, s), "clear build stats");
   size_t cub_bytes = 0, scan_bytes = 0;
   HIP_TRY(sort_keys(nullptr, &cub_bytes, nullptr, nullptr, n, s), "sort size");
-  uint32_t* gstat = e->d_gstat.as<uint32_t>();  // [t][reach, max depth, max fan-out]
-  for (uint32_t t = 0; t < nt; ++t) {
-    const TopicHost& T = e->topics[t];
-    if (!T.exists) continue;
-    HIP_TRY(launch_depth_keys(e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n, n, T.root,
-                              e->d_anc0.as<uint32_t>(), e->d_anc1.as<uint32_t>(),
-                              e->d_dep0.as<uint32_t>(), e->d_dep1.as<uint32_t>(),
-                              e->d_keys0.as<uint64_t>(), gstat + 3 * t, gstat + 3 * t + 1, s),
-            "depth");
-    HIP_TRY(e->d_cub.ensure(std::max<size_t>(cub_bytes, 16)), "alloc sort temp");
-    size_t tb = e->d_cub.bytes;
-    HIP_TRY(sort_keys(e->d_cub.p, &tb, e->d_keys0.as<uint64_t>(),
-                      e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n, s),
-            "sort");
-    HIP_TRY(launch_level_starts(e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n,
-                                e->d_lvl.as<uint32_t>() + 512 * t, s),
-            "level starts");
-  }
-  // (level starts of unreachable peers' keys land in slot 255: ignored)
+  HIP_TRY(e->d_cub.ensure(std::max<size_t>(cub_bytes, 16)), "alloc sort temp");
+  // [t][reach, max depth, max fan-out, unresolved]
+  uint32_t* gstat = e->d_gstat.as<uint32_t>();
   auto& gs = e->gstat_host;
-  gs.assign(static_cast<size_t>(nt) * 3, 0);
   auto& lh = e->lvl_host;
-  lh.assign(static_cast<size_t>(nt) * 512, 0);
-  HIP_TRY(hipMemcpyAsync(gs.data(), gstat, gs.size() * 4, hipMemcpyDeviceToHost, s), "read build stats");
-  HIP_TRY(hipMemcpyAsync(lh.data(), e->d_lvl.p, lh.size() * 4, hipMemcpyDeviceToHost, s), "read level starts");
-  HIP_TRY(hipStreamSynchronize(s), "sync");
+  // pointer jumping sized from the last build's depth (x4 headroom); a topic
+  // that grew deeper reports unresolved peers and is redone with full jumps
+  std::vector<uint32_t> jumps(nt, depth_jumps_full(n));
+  for (uint32_t t = 0; t < nt; ++t) {
+    const uint32_t d = e->topics[t].depth;
+    if (d) jumps[t] = std::min(jumps[t], depth_jumps_full(4 * d));
+  }
+  for (int pass = 0; pass < 2; ++pass) {
+    HIP_TRY(hipMemsetAsync(e->d_gstat.p, 0, static_cast<size_t>(nt) * 4 * 4, s), "clear build stats");
+    HIP_TRY(hipMemsetAsync(e->d_lvl.p, 0, static_cast<size_t>(nt) * 512 * 4, s), "clear level tables");
+    for (uint32_t t = 0; t < nt; ++t) {
+      const TopicHost& T = e->topics[t];
+      if (!T.exists) continue;
+      HIP_TRY(launch_depth_keys(e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n, n, T.root, jumps[t],
+                                e->d_anc0.as<uint32_t>(), e->d_anc1.as<uint32_t>(),
+                                e->d_dep0.as<uint32_t>(), e->d_dep1.as<uint32_t>(),
+                                e->d_keys0.as<uint64_t>(), gstat + 4 * t, s),
+              "depth");
+      size_t tb = e->d_cub.bytes;
+      HIP_TRY(sort_keys(e->d_cub.p, &tb, e->d_keys0.as<uint64_t>(),
+                        e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n, s),
+              "sort");
+      HIP_TRY(launch_level_starts(e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n,
+                                  e->d_lvl.as<uint32_t>() + 512 * t, s),
+              "level starts");
+    }
+    // (level starts of unreachable peers' keys land in slot 255: ignored)
+    gs.assign(static_cast<size_t>(nt) * 4, 0);
+    lh.assign(static_cast<size_t>(nt) * 512, 0);
+    HIP_TRY(hipMemcpyAsync(gs.data(), gstat, gs.size() * 4, hipMemcpyDeviceToHost, s), "read build stats");
+    HIP_TRY(hipMemcpyAsync(lh.data(), e->d_lvl.p, lh.size() * 4, hipMemcpyDeviceToHost, s), "read level starts");
+    HIP_TRY(hipStreamSynchronize(s), "sync");
+    bool redo = false;
+    for (uint32_t t = 0; t < nt; ++t)
+      if (e->topics[t].exists && gs[4 * t + 3]) {
+        jumps[t] = depth_jumps_full(n);
+        redo = true;
+      }
+    if (!redo) break;
+  }
   for (uint32_t t = 0; t < nt; ++t)
-    if (e->topics[t].exists && gs[3 * t + 1] >= kBuildMaxDepth) {
+    if (e->topics[t].exists && gs[4 * t + 1] >= kBuildMaxDepth) {
       *fallback = true;  // deeper than the key's depth field
       return PS_OK;
     }
@@ -588,7 +605,7 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   for (uint32_t t = 0; t < nt; ++t) {
     TopicHost& T = e->topics[t];
     T.nbase = static_cast<uint32_t>(n_total);
-    T.n_nodes = T.exists ? gs[3 * t] : 0;
+    T.n_nodes = T.exists ? gs[4 * t] : 0;
     if (T.n_nodes) e->roots_host.push_back(T.nbase);
     n_total += T.n_nodes;
   }
@@ -614,7 +631,7 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   for (uint32_t t = 0; t < nt; ++t) {
     TopicHost& T = e->topics[t];
     if (!T.n_nodes) continue;
-    const uint32_t depth = gs[3 * t + 1];
+    const uint32_t depth = gs[4 * t + 1];
     const uint64_t* keys = e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n;
     for (uint32_t d = 0; d <= depth; ++d) {
       const uint32_t lo = lh[512 * t + d];
@@ -642,8 +659,8 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   for (uint32_t t = 0; t < nt; ++t) {
     const TopicHost& T = e->topics[t];
     if (!T.n_nodes) continue;
-    HIP_TRY(launch_level_internal(e->d_deg.as<uint32_t>(), T.nbase, T.n_nodes, lvl + 512 * t, gs[3 * t + 1],
-                                  lvl + 512 * t + 256, gstat + 3 * t + 2, s),
+    HIP_TRY(launch_level_internal(e->d_deg.as<uint32_t>(), T.nbase, T.n_nodes, lvl + 512 * t, gs[4 * t + 1],
+                                  lvl + 512 * t + 256, gstat + 4 * t + 2, s),
             "level stats");
   }
   // 4. CSR: row_ptr = exclusive scan of the fan-out; children consecutive
@@ -662,8 +679,8 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
     T.mesh = false;
     T.root_local = true;
     T.cross.clear();
-    T.depth = T.n_nodes ? gs[3 * t + 1] : 0;
-    T.max_deg = gs[3 * t + 2];
+    T.depth = T.n_nodes ? gs[4 * t + 1] : 0;
+    T.max_deg = gs[4 * t + 2];
     T.level_off.assign(T.depth + 2, 0);
     T.level_internal.assign(T.depth + 1, 0);
     if (!T.n_nodes) continue;
@@ -1896,6 +1913,55 @@ int ps_read_delivered(ps_engine* e, uint32_t msg, uint8_t* out) {
   const uint64_t bit = 1ull << (li & 63);
   for (uint32_t u = 1; u < d.n_nodes; ++u)  // the root is not a recipient
     if ((mesh || gen[u] == e->gen_cur) && (col[u] & bit)) out[e->node_peer[d.nbase + u]] = 1;
+  return PS_OK;
+}
+
+int ps_read_peer_messages(ps_engine* e, uint32_t topic, uint32_t peer, uint32_t* msg_out, size_t cap,
+                          size_t* n_out) {
+  if (!e || !n_out || (cap && !msg_out)) return PS_E_INVAL;
+  *n_out = 0;
+  if (!e->have_window) return e->fail(PS_E_NOTREADY, "no completed run");
+  if (topic >= e->topics.size() || peer >= e->cfg.n_peers) return e->fail(PS_E_RANGE, "topic or peer out of range");
+  const TopicDev& d = e->last_topics[topic];
+  if (!d.W || !e->last_cnt[topic]) return PS_OK;
+  {
+    int rcm = ensure_mirrors(e);
+    if (rcm) return rcm;
+  }
+  // the peer's node in this topic (the root is the publisher, not a recipient)
+  uint32_t u = kNone;
+  for (uint32_t k = 1; k < d.n_nodes; ++k)
+    if (e->node_peer[d.nbase + k] == peer) {
+      u = k;
+      break;
+    }
+  if (u == kNone) return PS_OK;  // not subscribed (or not owned by this rank)
+  std::vector<uint64_t> row(d.W);
+  uint8_t g = 0;
+  HIP_TRY(hipMemcpyAsync(row.data(), e->d_seen.as<uint64_t>() + d.wbase + static_cast<uint64_t>(u) * d.W,
+                         d.W * 8ull, hipMemcpyDeviceToHost, e->stream),
+          "read seen row");
+  HIP_TRY(hipMemcpyAsync(&g, e->d_gen.as<uint8_t>() + d.nbase + u, 1, hipMemcpyDeviceToHost, e->stream),
+          "read generation");
+  HIP_TRY(hipStreamSynchronize(e->stream), "sync");
+  if (!(d.flags & kTopicMesh) && g != e->gen_cur) return PS_OK;  // stale row: saw nothing
+  // window slot li -> message: the window holds the topic's ranks
+  // [last_lo, last_lo + last_cnt)
+  const uint32_t lo = e->last_lo[topic], cnt = e->last_cnt[topic];
+  std::vector<std::pair<uint64_t, uint32_t>> got;  // (start round << 32 | id, id)
+  for (uint32_t i = 0; i < e->last_n; ++i) {
+    if (e->last_msgs[i].topic != topic) continue;
+    const uint32_t r = e->run_rank[i];
+    if (r < lo || r >= lo + cnt) continue;
+    const uint32_t li = r - lo;
+    if (row[li >> 6] >> (li & 63) & 1ull)
+      got.emplace_back((static_cast<uint64_t>(e->last_msgs[i].start) << 32) | i, e->last_first + i);
+  }
+  // arrival order: paced messages by entry round, then publish order
+  std::sort(got.begin(), got.end());
+  *n_out = got.size();
+  if (got.size() > cap) return e->fail(PS_E_RANGE, "output buffer too small");
+  for (size_t k = 0; k < got.size(); ++k) msg_out[k] = got[k].second;
   return PS_OK;
 }
 

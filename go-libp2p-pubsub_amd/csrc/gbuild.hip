@@ -16,6 +16,8 @@ constexpr uint32_t kB = 256;
 constexpr uint32_t kNoneP = 0xFFFFFFFFu;
 constexpr uint64_t kPeerMask = (1ull << kBuildPeerBits) - 1ull;
 
+constexpr uint32_t kStatBlocks = 1024;  // grid of the reducing kernels
+
 uint32_t blocks(uint64_t n) { return static_cast<uint32_t>(std::max<uint64_t>(1, (n + kB - 1) / kB)); }
 
 __global__ __launch_bounds__(kB) void k_scatter_pairs(const uint32_t* __restrict__ pairs, uint32_t n,
@@ -52,81 +54,56 @@ __global__ __launch_bounds__(kB) void k_depth_jump(const uint32_t* __restrict__ 
   dout[p] = di[p] + di[a];
 }
 
+// Block-wide max / sum through LDS: one global atomic per block (thousands of
+// same-address atomics, one per wave, serialise in one L2 channel).
+template <bool kMax>
+__device__ uint32_t block_reduce(uint32_t v, uint32_t* lds) {
+#pragma unroll
+  for (int s = 32; s >= 1; s >>= 1) {
+    const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), s, 64));
+    v = kMax ? max(v, o) : v + o;
+  }
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  v = lds[0];
+  for (uint32_t w = 1; w < kB / 64; ++w) v = kMax ? max(v, lds[w]) : v + lds[w];
+  __syncthreads();
+  return v;
+}
+
+// Keys of the reachable peers (grid-stride): depth << 56 | parent << 28 |
+// peer, ~0 otherwise.  gstat[0] += reachable, gstat[1] = max depth,
+// gstat[3] += peers whose ancestor is neither the root nor cut (the jump
+// steps did not cover their depth: the caller repeats with more steps).
 __global__ __launch_bounds__(kB) void k_depth_keys(const uint32_t* __restrict__ anc,
                                                    const uint32_t* __restrict__ dep,
                                                    const uint32_t* __restrict__ par, uint32_t n,
                                                    uint32_t root, uint64_t* __restrict__ keys,
-                                                   uint32_t* __restrict__ reach,
-                                                   uint32_t* __restrict__ max_depth) {
-  const uint32_t p = blockIdx.x * kB + threadIdx.x;
-  bool ok = false;
-  uint32_t d = 0;
-  if (p < n) {
-    ok = anc[p] == root;
+                                                   uint32_t* __restrict__ gstat) {
+  __shared__ uint32_t lds[kB / 64];
+  uint32_t cnt = 0, far = 0, m = 0;
+  for (uint32_t p = blockIdx.x * kB + threadIdx.x; p < n; p += gridDim.x * kB) {
+    const uint32_t a = anc[p];
     uint64_t k = ~0ull;
-    if (ok) {
-      d = dep[p];
+    if (a == root) {
+      const uint32_t d = dep[p];
       const uint64_t pp = p == root ? 0ull : par[p];
       k = (static_cast<uint64_t>(min(d, kBuildMaxDepth)) << 56) | (pp << kBuildPeerBits) | p;
+      ++cnt;
+      m = max(m, d);
+    } else if (a != kNoneP) {
+      ++far;
     }
     keys[p] = k;
   }
-  const uint64_t b = __ballot(ok);
-  uint32_t m = d;
-#pragma unroll
-  for (int s = 32; s >= 1; s >>= 1) m = max(m, static_cast<uint32_t>(__shfl_xor(static_cast<int>(m), s, 64)));
-  if ((threadIdx.x & 63) == 0) {
-    if (b) atomicAdd(reach, static_cast<uint32_t>(__popcll(b)));
-    if (m) atomicMax(max_depth, m);
+  cnt = block_reduce<false>(cnt, lds);
+  m = block_reduce<true>(m, lds);
+  far = block_reduce<false>(far, lds);
+  if (threadIdx.x == 0) {
+    if (cnt) atomicAdd(gstat + 0, cnt);
+    if (m) atomicMax(gstat + 1, m);
+    if (far) atomicAdd(gstat + 3, far);
   }
-}
-
-__global__ __launch_bounds__(kB) void k_layout(const uint64_t* __restrict__ keys, uint32_t R,
-                                               uint32_t nbase, uint16_t topic,
-                                               uint32_t* __restrict__ node_peer,
-                                               uint16_t* __restrict__ node_topic,
-                                               uint32_t* __restrict__ local) {
-  const uint32_t u = blockIdx.x * kB + threadIdx.x;
-  if (u >= R) return;
-  const uint32_t peer = static_cast<uint32_t>(keys[u] & kPeerMask);
-  node_peer[nbase + u] = peer;
-  node_topic[nbase + u] = topic;
-  local[peer] = nbase + u;
-}
-
-__global__ __launch_bounds__(kB) void k_link(const uint64_t* __restrict__ keys, uint32_t R,
-                                             uint32_t nbase, const uint32_t* __restrict__ local,
-                                             uint32_t* __restrict__ node_parent,
-                                             uint32_t* __restrict__ deg, uint32_t* __restrict__ first,
-                                             uint32_t* __restrict__ lvl_start) {
-  const uint32_t u = blockIdx.x * kB + threadIdx.x;
-  if (u >= R) return;
-  const uint64_t k = keys[u];
-  const uint32_t d = static_cast<uint32_t>(k >> 56);
-  if (u == 0 || static_cast<uint32_t>(keys[u - 1] >> 56) != d) lvl_start[d] = u;
-  if (u == 0) {  // depth 0: the root, alone
-    node_parent[nbase] = kNoneP;
-    return;
-  }
-  const uint32_t pu = local[static_cast<uint32_t>((k >> kBuildPeerBits) & kPeerMask)];
-  node_parent[nbase + u] = pu;
-  atomicAdd(deg + pu, 1u);
-  atomicMin(first + pu, nbase + u);
-}
-
-__global__ __launch_bounds__(kB) void k_level_stats(const uint64_t* __restrict__ keys, uint32_t R,
-                                                    uint32_t nbase, const uint32_t* __restrict__ deg,
-                                                    uint32_t* __restrict__ lvl_internal,
-                                                    uint32_t* __restrict__ max_deg) {
-  const uint32_t u = blockIdx.x * kB + threadIdx.x;
-  uint32_t dg = 0;
-  if (u < R) {
-    dg = deg[nbase + u];
-    if (dg) atomicAdd(lvl_internal + static_cast<uint32_t>(keys[u] >> 56), 1u);
-  }
-#pragma unroll
-  for (int s = 32; s >= 1; s >>= 1) dg = max(dg, static_cast<uint32_t>(__shfl_xor(static_cast<int>(dg), s, 64)));
-  if ((threadIdx.x & 63) == 0 && dg) atomicMax(max_deg, dg);
 }
 
 __global__ __launch_bounds__(kB) void k_fill_col(const uint32_t* __restrict__ row_ptr,
@@ -204,30 +181,39 @@ __global__ __launch_bounds__(kB) void k_place(const uint64_t* __restrict__ keys,
 }
 
 // Internal nodes per level and the largest fan-out of a topic placed at
-// [nbase, nbase + R) with level starts lvl_start[0..depth] (topic-relative).
+// [nbase, nbase + R) with level starts lvl_start[0..depth] (topic-relative):
+// a per-block LDS histogram over the levels, flushed with one atomic per
+// non-empty bin (a tree has a few dozen levels: per-node global atomics on
+// them serialise).
 __global__ __launch_bounds__(kB) void k_level_internal(const uint32_t* __restrict__ deg, uint32_t nbase,
                                                        uint32_t R, const uint32_t* __restrict__ lvl_start,
                                                        uint32_t depth, uint32_t* __restrict__ lvl_internal,
                                                        uint32_t* __restrict__ max_deg) {
-  const uint32_t u = blockIdx.x * kB + threadIdx.x;
-  uint32_t dg = 0;
-  if (u < R) {
-    dg = deg[nbase + u];
-    if (dg) {
-      uint32_t lo = 0, hi = depth;  // last level whose start <= u
-      while (lo < hi) {
-        const uint32_t mid = (lo + hi + 1) / 2;
-        if (lvl_start[mid] <= u)
-          lo = mid;
-        else
-          hi = mid - 1;
-      }
-      atomicAdd(lvl_internal + lo, 1u);
+  __shared__ uint32_t hist[kBuildMaxDepth + 1];
+  __shared__ uint32_t starts[kBuildMaxDepth + 2];
+  __shared__ uint32_t lds[kB / 64];
+  for (uint32_t d = threadIdx.x; d <= kBuildMaxDepth; d += kB) hist[d] = 0;
+  for (uint32_t d = threadIdx.x; d <= depth; d += kB) starts[d] = lvl_start[d];
+  __syncthreads();
+  uint32_t m = 0;
+  for (uint32_t u = blockIdx.x * kB + threadIdx.x; u < R; u += gridDim.x * kB) {
+    const uint32_t dg = deg[nbase + u];
+    if (!dg) continue;
+    m = max(m, dg);
+    uint32_t lo = 0, hi = depth;  // last level whose start <= u
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1) / 2;
+      if (starts[mid] <= u)
+        lo = mid;
+      else
+        hi = mid - 1;
     }
+    atomicAdd(hist + lo, 1u);
   }
-#pragma unroll
-  for (int s = 32; s >= 1; s >>= 1) dg = max(dg, static_cast<uint32_t>(__shfl_xor(static_cast<int>(dg), s, 64)));
-  if ((threadIdx.x & 63) == 0 && dg) atomicMax(max_deg, dg);
+  m = block_reduce<true>(m, lds);  // includes the barrier after the histogram
+  for (uint32_t d = threadIdx.x; d <= depth; d += kB)
+    if (hist[d]) atomicAdd(lvl_internal + d, hist[d]);
+  if (threadIdx.x == 0 && m) atomicMax(max_deg, m);
 }
 
 }  // namespace
@@ -258,7 +244,9 @@ hipError_t launch_level_internal(const uint32_t* deg, uint32_t nbase, uint32_t R
                                  const uint32_t* lvl_start, uint32_t depth, uint32_t* lvl_internal,
                                  uint32_t* max_deg, hipStream_t s) {
   if (R == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_level_internal, dim3(blocks(R)), dim3(kB), 0, s, deg, nbase, R, lvl_start, depth,
+  if (depth > kBuildMaxDepth) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_level_internal, dim3(std::min(blocks(R), kStatBlocks)), dim3(kB), 0, s, deg, nbase,
+                     R, lvl_start, depth,
                      lvl_internal, max_deg);
   return hipGetLastError();
 }
@@ -269,22 +257,19 @@ hipError_t launch_scatter_pairs(const uint32_t* pairs, uint32_t n, uint32_t* par
   return hipGetLastError();
 }
 
-hipError_t launch_depth_keys(const uint32_t* par, uint32_t n, uint32_t root, uint32_t* anc0,
-                             uint32_t* anc1, uint32_t* dep0, uint32_t* dep1, uint64_t* keys,
-                             uint32_t* reach, uint32_t* max_depth, hipStream_t s) {
+hipError_t launch_depth_keys(const uint32_t* par, uint32_t n, uint32_t root, uint32_t jumps,
+                             uint32_t* anc0, uint32_t* anc1, uint32_t* dep0, uint32_t* dep1,
+                             uint64_t* keys, uint32_t* gstat, hipStream_t s) {
   hipLaunchKernelGGL(k_depth_init, dim3(blocks(n)), dim3(kB), 0, s, par, n, root, anc0, dep0);
-  // after j steps every peer's ancestor is 2^j levels up: log2(n) + 1 steps
-  // reach the root from any depth
-  uint32_t steps = 1;
-  while ((1ull << steps) < n) ++steps;
+  // after j jumps every peer's ancestor is 2^j levels up (or the root / cut)
   uint32_t *ai = anc0, *ao = anc1, *di = dep0, *dout = dep1;
-  for (uint32_t j = 0; j <= steps; ++j) {
+  for (uint32_t j = 0; j < jumps; ++j) {
     hipLaunchKernelGGL(k_depth_jump, dim3(blocks(n)), dim3(kB), 0, s, ai, di, ao, dout, n, root);
     std::swap(ai, ao);
     std::swap(di, dout);
   }
-  hipLaunchKernelGGL(k_depth_keys, dim3(blocks(n)), dim3(kB), 0, s, ai, di, par, n, root, keys,
-                     reach, max_depth);
+  hipLaunchKernelGGL(k_depth_keys, dim3(std::min(blocks(n), kStatBlocks)), dim3(kB), 0, s, ai, di, par, n,
+                     root, keys, gstat);
   return hipGetLastError();
 }
 
@@ -296,32 +281,6 @@ hipError_t sort_keys(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_
 hipError_t scan_u32(void* temp, size_t* temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n,
                     hipStream_t s) {
   return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, in, out, n, s);
-}
-
-hipError_t launch_layout(const uint64_t* keys, uint32_t R, uint32_t nbase, uint16_t topic,
-                         uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
-                         hipStream_t s) {
-  if (R == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_layout, dim3(blocks(R)), dim3(kB), 0, s, keys, R, nbase, topic, node_peer,
-                     node_topic, local);
-  return hipGetLastError();
-}
-
-hipError_t launch_link(const uint64_t* keys, uint32_t R, uint32_t nbase, const uint32_t* local,
-                       uint32_t* node_parent, uint32_t* deg, uint32_t* first, uint32_t* lvl_start,
-                       hipStream_t s) {
-  if (R == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_link, dim3(blocks(R)), dim3(kB), 0, s, keys, R, nbase, local, node_parent,
-                     deg, first, lvl_start);
-  return hipGetLastError();
-}
-
-hipError_t launch_level_stats(const uint64_t* keys, uint32_t R, uint32_t nbase, const uint32_t* deg,
-                              uint32_t* lvl_internal, uint32_t* max_deg, hipStream_t s) {
-  if (R == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_level_stats, dim3(blocks(R)), dim3(kB), 0, s, keys, R, nbase, deg,
-                     lvl_internal, max_deg);
-  return hipGetLastError();
 }
 
 hipError_t launch_fill_col(const uint32_t* row_ptr, const uint32_t* first, uint32_t n_nodes,

@@ -19,12 +19,20 @@ constexpr uint32_t kBuildPeerBits = 28;   // peer / parent bits of the sort key
 // (peer, value) pairs scattered into a parent array
 hipError_t launch_scatter_pairs(const uint32_t* pairs, uint32_t n, uint32_t* par, hipStream_t s);
 
-// Depth of every peer (pointer jumping): keys[p] = depth << 56 | parent << 28
-// | p for peers reachable from root, ~0 otherwise; *reach += reachable
-// count, *max_depth = max(depth).  Scratch: anc[2][n], dep[2][n].
-hipError_t launch_depth_keys(const uint32_t* par, uint32_t n, uint32_t root, uint32_t* anc0,
-                             uint32_t* anc1, uint32_t* dep0, uint32_t* dep1, uint64_t* keys,
-                             uint32_t* reach, uint32_t* max_depth, hipStream_t s);
+// Depth of every peer (pointer jumping, `jumps` steps: depths up to 2^jumps
+// resolve): keys[p] = depth << 56 | parent << 28 | p for peers reachable from
+// root, ~0 otherwise; gstat[0] += reachable count, gstat[1] = max(depth),
+// gstat[3] += unresolved peers (more jumps needed).  Scratch: anc[2][n],
+// dep[2][n].
+hipError_t launch_depth_keys(const uint32_t* par, uint32_t n, uint32_t root, uint32_t jumps,
+                             uint32_t* anc0, uint32_t* anc1, uint32_t* dep0, uint32_t* dep1,
+                             uint64_t* keys, uint32_t* gstat, hipStream_t s);
+// jumps that resolve any depth below n
+inline uint32_t depth_jumps_full(uint32_t n) {
+  uint32_t j = 1;
+  while ((1ull << j) < n) ++j;
+  return j + 1;
+}
 
 // hipcub radix sort of n keys (in -> out); temp queried when temp == nullptr
 hipError_t sort_keys(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
@@ -33,16 +41,6 @@ hipError_t sort_keys(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_
 hipError_t scan_u32(void* temp, size_t* temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n,
                     hipStream_t s);
 
-// Node ids of one topic from its sorted keys (first R valid): node_peer,
-// node_topic, local[peer] = node; then node_parent, fan-out / first child of
-// every parent node and the level starts (lvl_start[d], topic-relative).
-// deg[] must be zeroed and first[] set to ~0 by the caller.
-hipError_t launch_layout(const uint64_t* keys, uint32_t R, uint32_t nbase, uint16_t topic,
-                         uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
-                         hipStream_t s);
-hipError_t launch_link(const uint64_t* keys, uint32_t R, uint32_t nbase, const uint32_t* local,
-                       uint32_t* node_parent, uint32_t* deg, uint32_t* first, uint32_t* lvl_start,
-                       hipStream_t s);
 // BFS placement, level by level: level starts of the sorted keys; level d's
 // keys re-keyed by their parent's node id (parent node << 28 | peer), sorted,
 // then placed at node0.. (node_peer, node_topic, local, node_parent, fan-out
@@ -56,9 +54,6 @@ hipError_t launch_place(const uint64_t* keys, uint32_t n, uint32_t node0, uint16
 hipError_t launch_level_internal(const uint32_t* deg, uint32_t nbase, uint32_t R,
                                  const uint32_t* lvl_start, uint32_t depth, uint32_t* lvl_internal,
                                  uint32_t* max_deg, hipStream_t s);
-// per-level internal-node counts and the topic's largest fan-out
-hipError_t launch_level_stats(const uint64_t* keys, uint32_t R, uint32_t nbase, const uint32_t* deg,
-                              uint32_t* lvl_internal, uint32_t* max_deg, hipStream_t s);
 // col[row_ptr[u] + j] = first[u] + j
 hipError_t launch_fill_col(const uint32_t* row_ptr, const uint32_t* first, uint32_t n_nodes,
                            uint32_t* col, hipStream_t s);

@@ -74,6 +74,21 @@ class DistConfig(C.Structure):
                 ("split_depth", C.c_uint32)]
 
 
+class MessageC(C.Structure):
+    """ps_message (include/psengine.h): pubsub.go:146-153 Message."""
+    _fields_ = [("type", C.c_int32), ("data", _u8p), ("data_len", C.c_size_t),
+                ("peers", C.POINTER(C.c_char_p)), ("n_peers", C.c_size_t),
+                ("tree_width", C.c_int64), ("tree_max_width", C.c_int64), ("num_peers", C.c_int64)]
+
+
+class MessageBuf(C.Structure):
+    """ps_message_buf: caller-owned decode target."""
+    _fields_ = [("type", C.c_int32), ("reserved", C.c_int32), ("data", _u8p),
+                ("data_cap", C.c_size_t), ("data_len", C.c_size_t), ("peers", C.c_char_p),
+                ("peers_cap", C.c_size_t), ("peers_len", C.c_size_t), ("n_peers", C.c_size_t),
+                ("tree_width", C.c_int64), ("tree_max_width", C.c_int64), ("num_peers", C.c_int64)]
+
+
 PROTOTYPES = [
     ("ps_version", C.c_char_p, []),
     ("ps_create", C.c_int, [C.POINTER(Config), C.POINTER(_P)]),
@@ -95,7 +110,10 @@ PROTOTYPES = [
     ("ps_run", C.c_int, [_P, C.POINTER(Stats)]),
     ("ps_read_hops", C.c_int, [_P, _u32, _u8p]),
     ("ps_read_delivered", C.c_int, [_P, _u32, _u8p]),
+    ("ps_read_peer_messages", C.c_int, [_P, _u32, _u32, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]),
     ("ps_seen_digest", C.c_int, [_P, _u64p]),
+    ("ps_msg_encode", C.c_int, [C.POINTER(MessageC), C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("ps_msg_decode", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(MessageBuf), C.POINTER(C.c_size_t)]),
     ("ps_dist_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("ps_dist_init", C.c_int, [_P, C.POINTER(DistConfig), C.POINTER(C.c_uint8)]),
     ("ps_loopback_create", C.c_int, [C.c_int32, C.POINTER(_P)]),
@@ -276,11 +294,24 @@ class Engine:
         self._check(self._L.ps_read_delivered(self._h, msg, _p(out, C.c_uint8)))
         return out
 
+    def peer_messages(self, topic: int, peer: int) -> np.ndarray:
+        """Message ids `peer`'s client.Messages() yields for `topic` from the
+        last window, in arrival order (ps_read_peer_messages)."""
+        n = C.c_size_t()
+        cap = 1024
+        while True:
+            out = np.empty(cap, dtype=np.uint32)
+            rc = self._L.ps_read_peer_messages(self._h, topic, peer, _p(out, C.c_uint32), cap, C.byref(n))
+            if rc == -7 and n.value > cap:
+                cap = n.value
+                continue
+            self._check(rc)
+            return out[:n.value].copy()
+
     def seen_digest(self) -> int:
         d = C.c_uint64()
         self._check(self._L.ps_seen_digest(self._h, C.byref(d)))
         return d.value
-
 
     # multi-GPU
     def dist_init(self, rank: int, world: int, unique_id: bytes, partition: int = PART_SUBTREE,

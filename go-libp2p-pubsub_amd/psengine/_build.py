@@ -12,7 +12,7 @@ LIB = os.path.join(LIBDIR, "libpsengine.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["kernels.hip", "gbuild.hip", "engine.cpp", "tree.cpp", "dist.cpp"]
+SOURCES = ["kernels.hip", "gbuild.hip", "engine.cpp", "tree.cpp", "dist.cpp", "codec.cpp"]
 HEADERS = ["kernels.hpp", "gbuild.hpp", "tree.hpp", "dist.hpp"]
 
 

@@ -155,6 +155,14 @@ int ps_run(ps_engine* e, ps_stats* out);
  *               for messages of the last window of the last run.            */
 int ps_read_hops(ps_engine* e, uint32_t msg, uint8_t* hop_per_peer);
 int ps_read_delivered(ps_engine* e, uint32_t msg, uint8_t* delivered_per_peer);
+/* ps_read_peer_messages: what one subscriber's client.Messages() channel
+ *               (client.go:26-28, fed by processMessages client.go:124-128)
+ *               yields for `topic` from the last window of the last run: the
+ *               delivered message ids in publish order (a tree path is FIFO,
+ *               so publish order is arrival order).  *n_out = count; returns
+ *               PS_E_RANGE (with *n_out set) when cap is too small. */
+int ps_read_peer_messages(ps_engine* e, uint32_t topic, uint32_t peer, uint32_t* msg_out,
+                          size_t cap, size_t* n_out);
 /* Order-independent digest of the final seen state of the last window:
  * sum over (peer, topic, word < message words) of
  * mix64(mix64(peer << 32 | topic << 16 | word) ^ mix64(seen word)); a
@@ -195,6 +203,55 @@ int ps_dist_init_loopback(ps_engine* e, const ps_dist_config* dc, ps_loopback* l
  * absent) under a partition; -1 for peers outside the tree */
 int ps_partition_owner(uint32_t n_peers, uint32_t root, const uint32_t* parent, uint32_t topic,
                        const ps_dist_config* dc, int32_t* owner_out);
+
+/* ---- wire codec (host only, no engine needed) --------------------------------
+ * The reference's stream framing, pubsub.go:122-153: writeMessage is
+ * json.NewEncoder(s).Encode(m) and readMessage json.NewDecoder(r).Decode(m)
+ * over
+ *   type Message struct { Type MessageType; Data []byte `json:"data,omitempty"`;
+ *     Peers []string `json:"parents,omitempty"`; TreeWidth, TreeMaxWidth,
+ *     NumPeers int `json:"...,omitempty"` }
+ * so a Go peer and this engine exchange byte-identical lines. */
+#define PS_MSG_DATA 0   /* MessageType, pubsub.go:138-144 */
+#define PS_MSG_JOIN 1
+#define PS_MSG_PART 2
+#define PS_MSG_UPDATE 3
+#define PS_MSG_STATE 4
+
+typedef struct ps_message {
+  int32_t type;
+  const uint8_t* data;      /* Data (base64 on the wire) */
+  size_t data_len;
+  const char* const* peers; /* Peers: NUL-terminated peer id strings */
+  size_t n_peers;
+  int64_t tree_width;
+  int64_t tree_max_width;
+  int64_t num_peers;
+} ps_message;
+
+/* decode target: caller-owned buffers; *_len / n_peers are always set, and
+ * PS_E_RANGE is returned when data_cap / peers_cap is too small */
+typedef struct ps_message_buf {
+  int32_t type;
+  int32_t reserved;
+  uint8_t* data;
+  size_t data_cap;
+  size_t data_len;
+  char* peers;              /* n_peers NUL-terminated strings, back to back */
+  size_t peers_cap;
+  size_t peers_len;
+  size_t n_peers;
+  int64_t tree_width;
+  int64_t tree_max_width;
+  int64_t num_peers;
+} ps_message_buf;
+
+/* one JSON line, '\n'-terminated; *len_out = bytes needed (PS_E_RANGE if cap
+ * is short, nothing written) */
+int ps_msg_encode(const ps_message* m, char* out, size_t cap, size_t* len_out);
+/* one JSON value from in[0..len); *consumed = bytes up to the next value
+ * (trailing whitespace included); PS_E_INVAL on malformed input */
+int ps_msg_decode(const char* in, size_t len, ps_message_buf* out, size_t* consumed);
 
 #ifdef __cplusplus
 }
