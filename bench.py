@@ -161,20 +161,22 @@ def bench_cfg5(args):
             eng.leave(0, leave)
         except PE.EngineError:
             pass  # orphaned peers cannot Part (their client panicked, client.go:96-98)
+        tl = time.perf_counter()
         eng.join(0, join, check=False)
         tj = time.perf_counter()
         eng.publish(wl.msg_topics)
         st = eng.run()
-        return st, tj - tc
+        return st, (tl - tc, tj - tl)
 
     for b in range(args.warmup):
         step(b)
-    tot, churn_s, run_host, run_gpu = 0, 0.0, 0.0, 0.0
+    tot, leave_s, join_s, run_host, run_gpu = 0, 0.0, 0.0, 0.0, 0.0
     t0 = time.perf_counter()
     for b in range(args.warmup, args.warmup + args.steps):
-        st, c = step(b)
+        st, (cl, cj) = step(b)
         tot += st.deliveries
-        churn_s += c
+        leave_s += cl
+        join_s += cj
         run_host += st.host_ms
         run_gpu += st.run_ms
     wall = time.perf_counter() - t0
@@ -192,7 +194,8 @@ def bench_cfg5(args):
         "data": "synthetic",
         "config": {"workload": f"cfg5: {DESCR['cfg5']}", "peers": wl.n_peers,
                    "messages_per_batch": wl.n_msgs, "parallelism": "1 GPU"},
-        "breakdown_ms_per_step": {"churn_host": churn_s * 1e3 / args.steps,
+        "breakdown_ms_per_step": {"leave_host": leave_s * 1e3 / args.steps,
+                                  "join_host": join_s * 1e3 / args.steps,
                                   "ps_run_wall": run_host / args.steps,
                                   "ps_run_gpu": run_gpu / args.steps},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

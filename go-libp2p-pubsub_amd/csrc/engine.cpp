@@ -487,6 +487,7 @@ bool can_gpu_build(const ps_engine* e) {
 // deeper than the sort key allows -- the caller builds on the host.
 int gpu_build_graph(ps_engine* e, bool* fallback) {
   *fallback = false;
+  const auto tb0 = std::chrono::steady_clock::now();
   const uint32_t n = e->cfg.n_peers;
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
   hipStream_t s = e->stream;
@@ -537,6 +538,8 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
                                    e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n, s),
               "scatter deltas");
   }
+  using clk = std::chrono::steady_clock;
+  const auto tb1 = clk::now();
   // 2. depth keys and sort per topic
   HIP_TRY(e->d_anc0.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
   HIP_TRY(e->d_anc1.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
@@ -594,6 +597,7 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
       }
     if (!redo) break;
   }
+  const auto tb2 = clk::now();
   for (uint32_t t = 0; t < nt; ++t)
     if (e->topics[t].exists && gs[4 * t + 1] >= kBuildMaxDepth) {
       *fallback = true;  // deeper than the key's depth field
@@ -671,9 +675,16 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   HIP_TRY(launch_fill_col(e->d_row_ptr.as<uint32_t>(), e->d_first.as<uint32_t>(), nn, e->d_col.as<uint32_t>(), s),
           "fill col");
   // 5. level tables back to the host (rounds, chunks, grid bounds)
+  const auto tb3 = clk::now();
   HIP_TRY(hipMemcpyAsync(lh.data(), lvl, lh.size() * 4, hipMemcpyDeviceToHost, s), "read level tables");
   HIP_TRY(hipMemcpyAsync(gs.data(), gstat, gs.size() * 4, hipMemcpyDeviceToHost, s), "read build stats");
   HIP_TRY(hipStreamSynchronize(s), "sync");
+  if (e->host_timing) {
+    auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+    std::fprintf(stderr, "[psengine] gpu build: deltas %.3f ms (%zu), depth+sort+readback %.3f ms, "
+                 "placement enqueue %.3f ms, drain %.3f ms\n", ms(tb0, tb1), pairs.size() / 2,
+                 ms(tb1, tb2), ms(tb2, tb3), ms(tb3, clk::now()));
+  }
   for (uint32_t t = 0; t < nt; ++t) {
     TopicHost& T = e->topics[t];
     T.mesh = false;
@@ -945,11 +956,16 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
 // `msgs`) whose bits form t's block of W_t = ceil(|win[t]|/64) words.
 int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<WinSlice>& win,
                ps_stats* st) {
+  const auto t_g0 = std::chrono::steady_clock::now();
   int rc = upload_graph(e);
   if (rc) return rc;
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
   const int32_t world = e->world, me = e->rank;
   const auto t_w0 = std::chrono::steady_clock::now();
+  if (e->host_timing)
+    std::fprintf(stderr, "[psengine] graph upload/build %.3f ms (%s)\n",
+                 std::chrono::duration<double, std::milli>(t_w0 - t_g0).count(),
+                 e->gpu_graph ? "gpu" : "host");
   std::vector<TopicDev> tab(std::max<uint32_t>(nt, 1));
   uint64_t wtot = 0;
   uint32_t max_depth = 0, max_start = 0;
@@ -1858,6 +1874,7 @@ int ps_run(ps_engine* e, ps_stats* out) {
     }
   }
   // lazy prune of Part'ed children at every forwarding node (subtree.go:326-331)
+  const auto t_am = std::chrono::steady_clock::now();
   for (uint32_t t = 0; t < nt; ++t) {
     TopicHost& T = e->topics[t];
     if (T.exists && T.kind == Kind::Join && head[t] < off[t + 1] - off[t] &&
@@ -1867,6 +1884,9 @@ int ps_run(ps_engine* e, ps_stats* out) {
     }
   }
   e->have_hops = record;
+  if (e->host_timing)
+    std::fprintf(stderr, "[psengine] after-message prune %.3f ms\n",
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_am).count());
   st.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
   if (out) *out = st;
   return PS_OK;
