@@ -1875,11 +1875,31 @@ int ps_run(ps_engine* e, ps_stats* out) {
   }
   // lazy prune of Part'ed children at every forwarding node (subtree.go:326-331)
   const auto t_am = std::chrono::steady_clock::now();
+  const bool gpu_reach = e->gpu_graph && !e->graph_dirty;  // the node space the messages ran on
   for (uint32_t t = 0; t < nt; ++t) {
     TopicHost& T = e->topics[t];
     if (T.exists && T.kind == Kind::Join && head[t] < off[t + 1] - off[t] &&
         T.tree.needs_message_pass()) {
-      T.tree.after_message();
+      // on a GPU-built node space the message's reach is a lookup there (a
+      // host walk to the root per Part'ed parent costs ~0.2 us each)
+      SubscriptionTree::ReachQuery q = [e, &T](const std::vector<uint32_t>& peers,
+                                               std::vector<uint8_t>& outv) -> int {
+        const uint32_t k = static_cast<uint32_t>(peers.size());
+        if (!k) return PS_OK;
+        HIP_TRY(e->d_pairs.ensure(static_cast<size_t>(k) * 4 + k + 16), "alloc reach query");
+        uint32_t* dp = e->d_pairs.as<uint32_t>();
+        uint8_t* dout = reinterpret_cast<uint8_t*>(dp + k);
+        HIP_TRY(hipMemcpyAsync(dp, peers.data(), static_cast<size_t>(k) * 4, hipMemcpyHostToDevice, e->stream),
+                "upload reach query");
+        HIP_TRY(launch_reach_query(dp, k, e->cfg.n_peers, e->d_local.as<uint32_t>(),
+                                   e->d_node_peer.as<uint32_t>(), T.nbase, T.n_nodes, dout, e->stream),
+                "reach query");
+        HIP_TRY(hipMemcpyAsync(outv.data(), dout, k, hipMemcpyDeviceToHost, e->stream), "read reach query");
+        HIP_TRY(hipStreamSynchronize(e->stream), "sync");
+        return PS_OK;
+      };
+      int rc = T.tree.after_message(gpu_reach ? &q : nullptr);
+      if (rc) return rc;
       e->graph_dirty = true;
     }
   }

@@ -216,7 +216,33 @@ __global__ __launch_bounds__(kB) void k_level_internal(const uint32_t* __restric
   if (threadIdx.x == 0 && m) atomicMax(max_deg, m);
 }
 
+// out[i] = 1 iff peers[i] holds a node of the topic placed at [nbase, nbase +
+// n_nodes) by the last build (local[] may hold stale ids: node_peer confirms)
+__global__ __launch_bounds__(kB) void k_reach_query(const uint32_t* __restrict__ peers, uint32_t n,
+                                                    uint32_t n_peers, const uint32_t* __restrict__ local,
+                                                    const uint32_t* __restrict__ node_peer, uint32_t nbase,
+                                                    uint32_t n_nodes, uint8_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * kB + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t p = peers[i];
+  uint8_t r = 0;
+  if (p < n_peers) {
+    const uint32_t u = local[p];
+    r = u >= nbase && u - nbase < n_nodes && node_peer[u] == p;
+  }
+  out[i] = r;
+}
+
 }  // namespace
+
+hipError_t launch_reach_query(const uint32_t* peers, uint32_t n, uint32_t n_peers, const uint32_t* local,
+                              const uint32_t* node_peer, uint32_t nbase, uint32_t n_nodes, uint8_t* out,
+                              hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_reach_query, dim3(blocks(n)), dim3(kB), 0, s, peers, n, n_peers, local, node_peer,
+                     nbase, n_nodes, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_level_starts(const uint64_t* keys, uint32_t R, uint32_t* lvl_start, hipStream_t s) {
   if (R == 0) return hipSuccess;

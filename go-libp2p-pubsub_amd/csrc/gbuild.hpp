@@ -54,6 +54,11 @@ hipError_t launch_place(const uint64_t* keys, uint32_t n, uint32_t node0, uint16
 hipError_t launch_level_internal(const uint32_t* deg, uint32_t nbase, uint32_t R,
                                  const uint32_t* lvl_start, uint32_t depth, uint32_t* lvl_internal,
                                  uint32_t* max_deg, hipStream_t s);
+// out[i] = 1 iff peer peers[i] holds a node of the topic at [nbase, nbase +
+// n_nodes) in the last GPU build (the message's reach, for the lazy prune)
+hipError_t launch_reach_query(const uint32_t* peers, uint32_t n, uint32_t n_peers, const uint32_t* local,
+                              const uint32_t* node_peer, uint32_t nbase, uint32_t n_nodes, uint8_t* out,
+                              hipStream_t s);
 // col[row_ptr[u] + j] = first[u] + j
 hipError_t launch_fill_col(const uint32_t* row_ptr, const uint32_t* first, uint32_t n_nodes,
                            uint32_t* col, hipStream_t s);

@@ -29,10 +29,27 @@ void SubscriptionTree::take_touched(std::vector<uint32_t>& out) {
   for (uint32_t p : out) touched_mark_[p] = 0;
 }
 
-bool SubscriptionTree::reachable(uint32_t p) const {
+bool SubscriptionTree::reachable_memo(uint32_t p) {
+  const uint32_t yes = 2 * reach_pass_, no = yes + 1;
+  walk_.clear();
+  bool ok = false;
   for (uint32_t hops = 0; hops <= n_; ++hops) {
-    if (p == root_) return true;
-    if (state_[p] != PeerState::In || up_[p] == kNone) return false;
+    if (p == root_ || reach_stamp_[p] == yes) {
+      ok = true;
+      break;
+    }
+    if (reach_stamp_[p] == no || state_[p] != PeerState::In || up_[p] == kNone) break;
+    walk_.push_back(p);
+    p = up_[p];
+  }
+  for (uint32_t q : walk_) reach_stamp_[q] = ok ? yes : no;
+  return ok;
+}
+
+bool SubscriptionTree::below_orphan(uint32_t p) const {
+  for (uint32_t hops = 0; hops <= n_ && p != root_ && p != kNone; ++hops) {
+    if (state_[p] == PeerState::Orphan) return true;
+    if (state_[p] != PeerState::In) return false;
     p = up_[p];
   }
   return false;
@@ -162,8 +179,8 @@ int SubscriptionTree::close_host(uint32_t peer) {
   return PS_OK;
 }
 
-void SubscriptionTree::after_message() {
-  if (!needs_pass_) return;
+int SubscriptionTree::after_message(const ReachQuery* reach) {
+  if (!needs_pass_) return PS_OK;
   if (!pending_failures_) {
     // Parts only: the lazy prune at each forwarding node deletes Part'ed
     // entries (subtree.go:329-331), draws nothing from the tie-break stream,
@@ -171,16 +188,35 @@ void SubscriptionTree::after_message() {
     // if the message reached them (an In-state path from the root).
     std::sort(parted_at_.begin(), parted_at_.end());
     parted_at_.erase(std::unique(parted_at_.begin(), parted_at_.end()), parted_at_.end());
+    // reachability of the message's tree, before this pass mutates anything
+    // (the prune below only edits child lists of reached parents and puts Dead
+    // children Out: no reached peer's path changes)
+    if (reach_stamp_.size() != n_) reach_stamp_.assign(n_, 0xFFFFFFFFu);
+    if (++reach_pass_ >= 0x7FFFFFF0u) {
+      std::fill(reach_stamp_.begin(), reach_stamp_.end(), 0xFFFFFFFFu);
+      reach_pass_ = 1;
+    }
+    std::vector<uint8_t> reached(parted_at_.size());
+    if (reach) {
+      int rc = (*reach)(parted_at_, reached);
+      if (rc) return rc;
+    } else {
+      for (size_t i = 0; i < parted_at_.size(); ++i)
+        reached[i] = parted_at_[i] < n_ && reachable_memo(parted_at_[i]);
+    }
     std::vector<uint32_t> keep;
-    for (uint32_t p : parted_at_) {
-      if (p >= n_ || !reachable(p)) {
-        if (p < n_) keep.push_back(p);  // pruned by a later message that reaches it
+    for (size_t i = 0; i < parted_at_.size(); ++i) {
+      const uint32_t p = parted_at_[i];
+      if (!reached[i]) {
+        // pruned by a later message that reaches it -- unless an orphan cuts
+        // it off for good (an Orphan never becomes In again, Q5)
+        if (p < n_ && !below_orphan(p)) keep.push_back(p);
         continue;
       }
       auto& list = kids_[p];
       size_t w = 0;
-      for (size_t i = 0; i < list.size(); ++i) {
-        const ChildRec r = list[i];
+      for (size_t k = 0; k < list.size(); ++k) {
+        const ChildRec r = list[k];
         if (r.parted) {
           if (state_[r.id] == PeerState::Dead) {
             state_[r.id] = PeerState::Out;
@@ -195,7 +231,7 @@ void SubscriptionTree::after_message() {
     }
     parted_at_.swap(keep);
     needs_pass_ = !parted_at_.empty();
-    return;
+    return PS_OK;
   }
   // forwarding nodes in BFS order over subscribed peers
   std::vector<uint32_t> order;
@@ -252,6 +288,7 @@ void SubscriptionTree::after_message() {
           break;
         }
     }
+  return PS_OK;
 }
 
 void SubscriptionTree::attached_parents(std::vector<uint32_t>& parent) const {

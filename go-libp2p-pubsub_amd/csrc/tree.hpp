@@ -6,6 +6,7 @@
 // peer hangs below which; the dissemination itself never runs here.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -34,8 +35,12 @@ class SubscriptionTree {
   int close_client(uint32_t peer);  // graceful: Part
   int close_host(uint32_t peer);    // abrupt
   // Called once per message that floods this topic: lazy prune and repair of
-  // failed writes at every node the message reached (rule Q3).
-  void after_message();
+  // failed writes at every node the message reached (rule Q3).  `reach`, if
+  // given, answers "did the message reach peer p" for a batch of peers (the
+  // engine asks the node space the message ran on); otherwise the tree walks
+  // up from each peer.
+  using ReachQuery = std::function<int(const std::vector<uint32_t>& peers, std::vector<uint8_t>& out)>;
+  int after_message(const ReachQuery* reach = nullptr);
   bool has_pending_failures() const { return pending_failures_; }
   // a Part or a host failure happened since the last after_message()
   bool needs_message_pass() const { return needs_pass_; }
@@ -60,7 +65,10 @@ class SubscriptionTree {
   void depart(uint32_t at, uint32_t gone, uint32_t rescue);
   uint64_t next_random();
 
-  bool reachable(uint32_t p) const;  // In-state path from the root
+  // In-state path from the root?  Memoised over one pass: every peer on a
+  // walked path is stamped reachable / unreachable (top levels are shared).
+  bool reachable_memo(uint32_t p);
+  bool below_orphan(uint32_t p) const;  // an Orphan on the upstream path (cut for good)
   void touch(uint32_t p);             // (state, upstream) of p may have changed
 
   uint32_t n_ = 0, root_ = 0, width_ = 2, max_width_ = 5;
@@ -70,6 +78,9 @@ class SubscriptionTree {
   std::vector<uint32_t> parted_at_;  // parents holding a Part'ed child entry
   std::vector<uint32_t> touched_;    // peers whose attachment may have changed
   std::vector<uint8_t> touched_mark_;
+  std::vector<uint32_t> reach_stamp_;  // 2*pass: reachable, 2*pass+1: not (reachable_memo)
+  uint32_t reach_pass_ = 0;
+  std::vector<uint32_t> walk_;
   std::vector<PeerState> state_;
   std::vector<uint32_t> up_;  // upstream peer (the other end of `in`)
   std::vector<std::vector<ChildRec>> kids_;
