@@ -283,6 +283,29 @@ def test_cfg3_full_size_properties():
         assert eng.seen_digest() == digest
 
 
+def test_cfg4_full_size_properties():
+    """BASELINE cfg4 at full size on one GPU (16,777,216 peers, TreeOpts{8,20}
+    built by the restated join protocol and rebuilt on the GPU, 1k burst):
+    exact deliveries, per-hop histogram, no duplicates, seen-state digest
+    (host side summed in slices to bound memory)."""
+    wl = WL.cfg4()
+    with PE.Engine(wl.n_peers, 1, seed=wl.seed) as eng:
+        WL.build_engine_topics(eng, wl)
+        eng.publish(wl.msg_topics)
+        st = eng.run()
+        assert st.deliveries == (wl.n_peers - 1) * wl.n_msgs == 16_777_215_000
+        assert st.duplicates == 0
+        rp, cl = O.parents_to_csr(eng.parents(0))
+        _, _, hist = O.disseminate(rp, cl, 0, np.ones(wl.n_peers, np.uint8), 1, want_hops=False)
+        per = st.as_dict()["deliveries_per_round"]
+        assert per[1:] == [int(h) * wl.n_msgs for h in hist[1:len(per)]]
+        digest = 0
+        for lo in range(0, wl.n_peers, 1 << 21):
+            part = np.arange(lo, min(wl.n_peers, lo + (1 << 21)))
+            digest = (digest + _digest_full_tree(part, 0, wl.n_msgs)) % (1 << 64)
+        assert eng.seen_digest() == digest
+
+
 def test_many_windows_generation_wrap_and_reuse():
     """> 255 windows on one engine: generation bytes wrap, stale rows from
     older windows never leak into a new window (lazy seen reset)."""
