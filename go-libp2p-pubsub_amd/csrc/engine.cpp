@@ -114,6 +114,7 @@ struct ps_engine {
   uint32_t n_cus = 256, expand_grid = 2048;
   bool no_single_start = false;  // PSAMD_NO_SINGLE_START=1: keep arrival rows (A/B)
   bool no_level = false;         // PSAMD_NO_LEVEL=1: always compact the frontier (A/B)
+  bool pull_nt = true;           // non-temporal row stores in k_pull (PSAMD_PULL_NT=0: plain, A/B)
   bool host_timing = false;      // PSAMD_HOST_TIMING=1: host phase times to stderr
   // GPU rebuild of the node space: on by default for one
   // rank and tree topics (PSAMD_GPU_BUILD=0: host build)
@@ -1332,7 +1333,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         pa.dbg = a.dbg;
         HIP_TRY(launch_pull(pa, e->d_pull.as<PullChunk>() + e->pull_off[r],
                             e->pull_off[r + 1] - e->pull_off[r], lgrid[r], r, record, fuse,
-                            e->pull_unroll, s),
+                            e->pull_unroll, e->pull_nt, s),
                 "pull");
       } else if (lgrid[r]) {
         a.frontier = e->d_sched.as<uint32_t>() + e->sched_off[r];
@@ -1552,6 +1553,7 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_NO_SINGLE_START")) e->no_single_start = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_NO_LEVEL")) e->no_level = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_HOST_TIMING")) e->host_timing = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_PULL_NT")) e->pull_nt = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_LEVEL_PUSH")) e->level_push = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_WORDS")) e->pull_words = std::max(64, std::atoi(v));

@@ -817,7 +817,28 @@ __device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic&
 
 // Phase 2: the rows of nodes [nb, nb + nk) as one output stream, each lane's
 // load from the row its node copies (src[], kNoneNode = skip).
-template <bool kRecord, uint32_t kU>
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+// row store of the pull stream: plain, or non-temporal (`nt`: no L2 / MALL
+// allocation for rows nobody re-reads within the launch)
+template <bool kNT>
+__device__ __forceinline__ void store_row16(uint64_t* p, const uint4& v) {
+  if constexpr (kNT) {
+    u32x4_t x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x4_t*>(p));
+  } else {
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+}
+template <bool kNT>
+__device__ __forceinline__ void store_row8(uint64_t* p, uint64_t v) {
+  if constexpr (kNT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
+template <bool kRecord, uint32_t kU, bool kNT>
 __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& P, uint32_t nb,
                                             uint32_t nk, const uint32_t* src, uint32_t lane,
                                             uint32_t wave, uint32_t round, PullCtr& c) {
@@ -872,7 +893,7 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
                                  round);
           }
         } else {
-          *reinterpret_cast<uint4*>(i < total ? out + i : dummy + 2 * lane) = x[u].v;
+          store_row16<kNT>(i < total ? out + i : dummy + 2 * lane, x[u].v);
         }
         c.deliv += x[u].go ? popc4(x[u].v) : 0u;
         c.sw += x[u].go ? 2u : 0u;
@@ -904,7 +925,7 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
             record_word<kRecord>(a.hop_rec, (out - a.seen) + i, m[u], round);
           }
         } else {
-          *(i < total ? out + i : dummy + lane) = m[u];
+          store_row8<kNT>(i < total ? out + i : dummy + lane, m[u]);
         }
         c.deliv += go[u] ? __popcll(m[u]) : 0u;
         c.sw += go[u] ? 1u : 0u;
@@ -947,7 +968,7 @@ __device__ __forceinline__ void pull_flush(const PullCtr& c, uint64_t* partials,
 // written in the same launch (round + 1) from the same source rows, so the
 // rows of level d + 1 are never read back.  Partial slots: one per block and
 // level (fused: 2 * block + level).
-template <bool kRecord, bool kFuse, uint32_t kU>
+template <bool kRecord, bool kFuse, uint32_t kU, bool kNT = false>
 __global__ __launch_bounds__(kBlock, kU <= 4 ? 8 : 1) void k_pull(PullArgs a, const PullChunk* __restrict__ chunks,
                                                  uint32_t n_chunks, uint32_t round) {
   __shared__ uint32_t src_lds[kBlock / 64][kPullMaxKids];
@@ -976,9 +997,9 @@ __global__ __launch_bounds__(kBlock, kU <= 4 ? 8 : 1) void k_pull(PullArgs a, co
     if constexpr (kFuse)
       pull_resolve<true>(a, P, ch.g_begin, n2, kNoneNode, kNoneNode, src + n1, src, ch.node_begin,
                          genl, lane, cur, c2);
-    pull_stream<kRecord, kU>(a, P, ch.node_begin, n1, src, lane, wave, round, c1);
+    pull_stream<kRecord, kU, kNT>(a, P, ch.node_begin, n1, src, lane, wave, round, c1);
     if constexpr (kFuse)
-      pull_stream<kRecord, kU>(a, P, ch.g_begin, n2, src + n1, lane, wave, round + 1, c2);
+      pull_stream<kRecord, kU, kNT>(a, P, ch.g_begin, n2, src + n1, lane, wave, round + 1, c2);
   }
   if constexpr (kFuse) {
     pull_flush(c1, a.partials, 2ull * blockIdx.x, lane, wid);
@@ -1292,7 +1313,7 @@ hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record
 
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
                        uint32_t grid, uint32_t round, bool record, bool fuse, uint32_t unroll,
-                       hipStream_t s) {
+                       bool nt, hipStream_t s) {
   if (n_chunks == 0 || grid == 0) return hipSuccess;
 #define PSAMD_PULL(R, F, U) \
   hipLaunchKernelGGL((k_pull<R, F, U>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round)
@@ -1301,6 +1322,8 @@ hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_ch
       PSAMD_PULL(true, true, 8);
     else
       PSAMD_PULL(true, false, 8);
+  } else if (nt && !fuse && unroll > 4) {
+    hipLaunchKernelGGL((k_pull<false, false, 8, true>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
   } else if (unroll <= 4) {
     if (fuse)
       PSAMD_PULL(false, true, 4);
