@@ -114,7 +114,9 @@ struct ps_engine {
   uint32_t n_cus = 256, expand_grid = 2048;
   bool no_single_start = false;  // PSAMD_NO_SINGLE_START=1: keep arrival rows (A/B)
   bool no_level = false;         // PSAMD_NO_LEVEL=1: always compact the frontier (A/B)
-  bool pull_nt = true;           // non-temporal row stores in k_pull (PSAMD_PULL_NT=0: plain, A/B)
+  uint32_t pull_nt = 1;          // k_pull cache policy: 1 nt row stores, 2 nt parent loads, 3 both, 0 plain (PSAMD_PULL_NT)
+  uint64_t pull_nt_min = 64ull << 20;  // nt only for rounds writing >= this many row bytes, and the last round
+  std::vector<uint64_t> pull_bytes;    // row bytes written per round (pull chunks)
   bool host_timing = false;      // PSAMD_HOST_TIMING=1: host phase times to stderr
   // GPU rebuild of the node space: on by default for one
   // rank and tree topics (PSAMD_GPU_BUILD=0: host build)
@@ -881,6 +883,7 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
   auto build = [&](bool fused) -> bool {
     C.clear();
     off.assign(rounds + 2, 0);
+    e->pull_bytes.assign(rounds + 2, 0);
     e->split_host.clear();
     e->split_off.assign(rounds + 2, 0);
     for (uint32_t q = 1; q <= rounds; ++q) {
@@ -901,6 +904,7 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
               if ((e->node_flags[T.nbase + u] & (kNodeSplit | kNodeLive)) == (kNodeSplit | kNodeLive))
                 e->split_host.push_back(T.nbase + u);
           const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, e->pull_words / W));
+          e->pull_bytes[q] += static_cast<uint64_t>(hi - lo) * W * 8;
           for (uint32_t u = lo; u < hi; u += per)
             C.push_back(PullChunk{T.nbase + u, T.nbase + std::min(u + per, hi), 0, 0, t,
                                   gpu ? kNone : e->node_parent[T.nbase + u],
@@ -1333,7 +1337,14 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         pa.dbg = a.dbg;
         HIP_TRY(launch_pull(pa, e->d_pull.as<PullChunk>() + e->pull_off[r],
                             e->pull_off[r + 1] - e->pull_off[r], lgrid[r], r, record, fuse,
-                            e->pull_unroll, e->pull_nt, s),
+                            e->pull_unroll,
+                            // rows a later level re-reads while they can still sit in the
+                            // 256 MB MALL keep the default policy
+                            r < e->pull_bytes.size() &&
+                                    (e->pull_bytes[r] >= e->pull_nt_min || r == planned0)
+                                ? e->pull_nt
+                                : 0u,
+                            s),
                 "pull");
       } else if (lgrid[r]) {
         a.frontier = e->d_sched.as<uint32_t>() + e->sched_off[r];
@@ -1553,7 +1564,8 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_NO_SINGLE_START")) e->no_single_start = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_NO_LEVEL")) e->no_level = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_HOST_TIMING")) e->host_timing = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_PULL_NT")) e->pull_nt = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_PULL_NT")) e->pull_nt = static_cast<uint32_t>(std::atoi(v)) & 3u;
+  if (const char* v = std::getenv("PSAMD_PULL_NT_MB")) e->pull_nt_min = std::strtoull(v, nullptr, 10) << 20;
   if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_LEVEL_PUSH")) e->level_push = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_WORDS")) e->pull_words = std::max(64, std::atoi(v));

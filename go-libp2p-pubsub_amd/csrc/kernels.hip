@@ -838,7 +838,25 @@ __device__ __forceinline__ void store_row8(uint64_t* p, uint64_t v) {
     *p = v;
 }
 
-template <bool kRecord, uint32_t kU, bool kNT>
+template <bool kNTL>
+__device__ __forceinline__ uint4 load_row16(const uint64_t* p) {
+  if constexpr (kNTL) {
+    const u32x4_t x = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+    return uint4{x.x, x.y, x.z, x.w};
+  } else {
+    return *reinterpret_cast<const uint4*>(p);
+  }
+}
+template <bool kNTL>
+__device__ __forceinline__ uint64_t load_row8(const uint64_t* p) {
+  if constexpr (kNTL)
+    return __builtin_nontemporal_load(p);
+  else
+    return *p;
+}
+
+// kNT: bit 0 non-temporal row stores, bit 1 non-temporal parent-row loads
+template <bool kRecord, uint32_t kU, uint32_t kNT>
 __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& P, uint32_t nb,
                                             uint32_t nk, const uint32_t* src, uint32_t lane,
                                             uint32_t wave, uint32_t round, PullCtr& c) {
@@ -868,7 +886,7 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
       // unconditional load: a skipped lane reads its own output row
       const uint64_t* s = go ? (p == root ? a.a_cur : a.seen) + base + static_cast<uint64_t>(p) * W + r
                              : out + (valid ? i : 0);
-      return PullVec{go, *reinterpret_cast<const uint4*>(s)};
+      return PullVec{go, load_row16<(kNT & 2u) != 0>(s)};
     };
     // 8 loads in flight, then 8 stores, unconditional and branch-free (a
     // skipped lane writes its own row back unchanged, a lane past the run's
@@ -893,7 +911,7 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
                                  round);
           }
         } else {
-          store_row16<kNT>(i < total ? out + i : dummy + 2 * lane, x[u].v);
+          store_row16<(kNT & 1u) != 0>(i < total ? out + i : dummy + 2 * lane, x[u].v);
         }
         c.deliv += x[u].go ? popc4(x[u].v) : 0u;
         c.sw += x[u].go ? 2u : 0u;
@@ -914,7 +932,7 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
         go[u] = p != kNoneNode;
         const uint64_t* s = go[u] ? (p == root ? a.a_cur : a.seen) + base + static_cast<uint64_t>(p) * W + r
                                   : out + (valid ? i : 0);
-        m[u] = *s;
+        m[u] = load_row8<(kNT & 2u) != 0>(s);
       }
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
@@ -925,7 +943,7 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
             record_word<kRecord>(a.hop_rec, (out - a.seen) + i, m[u], round);
           }
         } else {
-          store_row8<kNT>(i < total ? out + i : dummy + lane, m[u]);
+          store_row8<(kNT & 1u) != 0>(i < total ? out + i : dummy + lane, m[u]);
         }
         c.deliv += go[u] ? __popcll(m[u]) : 0u;
         c.sw += go[u] ? 1u : 0u;
@@ -968,7 +986,7 @@ __device__ __forceinline__ void pull_flush(const PullCtr& c, uint64_t* partials,
 // written in the same launch (round + 1) from the same source rows, so the
 // rows of level d + 1 are never read back.  Partial slots: one per block and
 // level (fused: 2 * block + level).
-template <bool kRecord, bool kFuse, uint32_t kU, bool kNT = false>
+template <bool kRecord, bool kFuse, uint32_t kU, uint32_t kNT = 0>
 __global__ __launch_bounds__(kBlock, kU <= 4 ? 8 : 1) void k_pull(PullArgs a, const PullChunk* __restrict__ chunks,
                                                  uint32_t n_chunks, uint32_t round) {
   __shared__ uint32_t src_lds[kBlock / 64][kPullMaxKids];
@@ -1313,7 +1331,7 @@ hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record
 
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
                        uint32_t grid, uint32_t round, bool record, bool fuse, uint32_t unroll,
-                       bool nt, hipStream_t s) {
+                       uint32_t nt, hipStream_t s) {
   if (n_chunks == 0 || grid == 0) return hipSuccess;
 #define PSAMD_PULL(R, F, U) \
   hipLaunchKernelGGL((k_pull<R, F, U>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round)
@@ -1323,7 +1341,12 @@ hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_ch
     else
       PSAMD_PULL(true, false, 8);
   } else if (nt && !fuse && unroll > 4) {
-    hipLaunchKernelGGL((k_pull<false, false, 8, true>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
+    if (nt == 1)
+      hipLaunchKernelGGL((k_pull<false, false, 8, 1>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
+    else if (nt == 2)
+      hipLaunchKernelGGL((k_pull<false, false, 8, 2>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
+    else
+      hipLaunchKernelGGL((k_pull<false, false, 8, 3>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
   } else if (unroll <= 4) {
     if (fuse)
       PSAMD_PULL(false, true, 4);

@@ -189,7 +189,7 @@ hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, bool 
 // unroll: 16-B loads in flight per lane (4: 8 waves/SIMD, 8: 6 waves/SIMD)
 // grid: blocks, one chunk per wave (ceil(n_chunks / 4))
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                       uint32_t grid, uint32_t round, bool record, bool fuse, uint32_t unroll, bool nt,
+                       uint32_t grid, uint32_t round, bool record, bool fuse, uint32_t unroll, uint32_t nt,
                        hipStream_t s);
 // Level mode: round q's counters = sum of the partial slots desc[3q],
 // desc[3q] + desc[3q+2], ... < desc[3q+1], for q = 1..n_rounds.
