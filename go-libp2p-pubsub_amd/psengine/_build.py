@@ -12,7 +12,7 @@ LIB = os.path.join(LIBDIR, "libpsengine.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["kernels.hip", "gbuild.hip", "engine.cpp", "tree.cpp", "dist.cpp", "codec.cpp"]
+SOURCES = ["kernels.hip", "gbuild.hip", "engine.cpp", "tree.cpp", "dist.cpp", "codec.cpp", "pubsub.cpp"]
 HEADERS = ["kernels.hpp", "gbuild.hpp", "tree.hpp", "dist.hpp"]
 
 
@@ -22,6 +22,7 @@ def _stale() -> bool:
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     deps.append(os.path.join(REPO, "include", "psengine.h"))
+    deps.append(os.path.join(REPO, "include", "pubsub.hpp"))
     return any(os.path.getmtime(d) > t for d in deps)
 
 
@@ -38,3 +39,26 @@ def build(force: bool = False, verbose: bool = False) -> str:
     subprocess.run(cmd, check=True)
     os.replace(LIB + ".tmp", LIB)
     return LIB
+
+
+CPP_TESTS = os.path.join(REPO, "tests", "cpp")
+CPP_TEST_BIN = os.path.join(CPP_TESTS, "bin", "pubsub_test")
+
+
+def build_cpp_tests(force: bool = False, verbose: bool = False) -> str:
+    """tests/cpp/pubsub_test.cpp (the reference's tests against the C++ API
+    mirror, include/pubsub.hpp) -> tests/cpp/bin/pubsub_test, linked to the
+    in-tree libpsengine.so.  Host C++ only (g++)."""
+    src = os.path.join(CPP_TESTS, "pubsub_test.cpp")
+    hdr = os.path.join(REPO, "include", "pubsub.hpp")
+    if (not force and os.path.exists(CPP_TEST_BIN) and
+            os.path.getmtime(CPP_TEST_BIN) >= max(os.path.getmtime(src), os.path.getmtime(hdr))):
+        return CPP_TEST_BIN
+    os.makedirs(os.path.dirname(CPP_TEST_BIN), exist_ok=True)
+    cmd = [os.environ.get("CXX", "g++"), "-O2", "-std=c++17", "-Wall", "-I" + os.path.join(REPO, "include"),
+           src, "-L" + LIBDIR, "-lpsengine", "-Wl,-rpath," + LIBDIR, "-o", CPP_TEST_BIN + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(CPP_TEST_BIN + ".tmp", CPP_TEST_BIN)
+    return CPP_TEST_BIN

@@ -119,3 +119,13 @@ def test_encode_sizing_and_empty_fields():
     buf = C.create_string_buffer(n.value - 1)
     assert L.ps_msg_encode(C.byref(cm), buf, n.value - 1, C.byref(n)) == -7  # short: nothing written
     assert L.ps_msg_encode(None, None, 0, C.byref(n)) == -1
+
+
+def test_cpp_api_mirror_codec():
+    """writeMessage / readMessage of the C++ API mirror (include/pubsub.hpp),
+    host only: the native test binary's codec case."""
+    import subprocess
+    from psengine import _build
+    exe = _build.build_cpp_tests()
+    p = subprocess.run([exe, "TestWireCodec"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0 and "--- PASS: TestWireCodec" in p.stdout, p.stdout + p.stderr
