@@ -224,6 +224,9 @@ def main():
                     help="use the torch.distributed driver even with one rank (testing)")
     ap.add_argument("--partition", default="subtree", choices=["subtree", "peer"],
                     help="multi-GPU node ownership: subtree hash (default) or peer hash")
+    ap.add_argument("--sync", action="store_true",
+                    help="one blocking ps_run per step (default: pipelined ps_run_async / ps_wait, "
+                         "the next batch is published and planned while the previous one's kernels run)")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="N>1: weak = N x the messages on the same topology (per-GPU work of "
                          "N=1), strong = the N=1 workload unchanged")
@@ -249,15 +252,28 @@ def main():
         eng.publish(wl.msg_topics)
         return eng.run()
 
-    for _ in range(args.warmup):
-        st = step()
+    def steps_pipelined(n):
+        """n steps, each batch published and enqueued while the previous
+        batch's kernels run; every batch completes inside the call."""
+        out = []
+        for i in range(n):
+            eng.publish(wl.msg_topics)
+            eng.run_async()
+            if i:
+                out.append(eng.wait())
+        if n:
+            out.append(eng.wait())
+        return out
+
+    def steps(n):
+        return [step() for _ in range(n)] if args.sync else steps_pipelined(n)
+
+    for st in steps(args.warmup):
         assert args.no_check or st.deliveries == deliv_expected, (st.deliveries, deliv_expected)
-    tot_deliv = 0
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        st = step()
-        tot_deliv += st.deliveries
+    sts = steps(args.steps)
     wall = time.perf_counter() - t0
+    tot_deliv = sum(st.deliveries for st in sts)
     assert args.no_check or tot_deliv == deliv_expected * args.steps
     value = tot_deliv / wall
     tot_bytes, tot_expand_ms, launches, st = instrumented(eng, step, max(3, min(args.steps, 5)))
@@ -282,7 +298,9 @@ def main():
         "config": {"workload": f"{wl.name}: {DESCR[wl.name]}", "peers": wl.n_peers,
                    "topics": len(wl.topics), "subscriptions": int(sum(sizes)),
                    "messages": wl.n_msgs, "deliveries_per_step": deliv_expected,
-                   "parallelism": "1 GPU"},
+                   "parallelism": "1 GPU",
+                   "steps_issue": "blocking ps_run" if args.sync else
+                   "pipelined ps_run_async/ps_wait (<= 2 batches in flight)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kernel, "avg_launch_us": tot_expand_ms * 1e3 / max(1, launches),

@@ -189,6 +189,24 @@ struct ps_engine {
   std::vector<TopicDev> last_topics;
   bool have_window = false;
 
+  // asynchronous runs (ps_run_async / ps_wait): the last window of a run may
+  // leave its stats on the stream (pinned readback) so that the host plans
+  // the next run while this one's kernels execute
+  struct Inflight {
+    ps_stats st{};
+    bool deferred = false;
+    uint32_t r = 0, launches = 0;
+    bool pull = false, level = false;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the window's kernels
+    hipEvent_t done = nullptr;                // after the counters' readback
+    uint64_t* hs = nullptr;  // pinned: (PS_MAX_ROUNDS + 1) x kNumCtr counters
+  };
+  Inflight infl[2];
+  uint32_t infl_head = 0, infl_count = 0;
+  bool defer_phase = false;  // the current phase may defer its last window's stats
+  bool defer_last = false;   // ... and this window is that last window
+  Inflight* defer_into = nullptr;
+
   int fail(int code, const std::string& m) {
     err = m;
     return code;
@@ -957,6 +975,43 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
   return PS_OK;
 }
 
+// Counters of one window (rows r x kNumCtr, apply rows for multi-GPU) into
+// the run's stats.
+void accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uint32_t r,
+                       uint32_t planned0, bool pull, bool level, uint32_t launches, int32_t world) {
+  for (uint32_t q = 1; q <= r; ++q) {
+    const uint64_t* c = &hs[static_cast<size_t>(q) * kNumCtr];
+    const uint64_t app_d = (world > 1 && q <= planned0) ? ha[static_cast<size_t>(q) * kNumCtr + kCtrDeliveries] : 0;
+    const uint64_t app_u = (world > 1 && q <= planned0) ? ha[static_cast<size_t>(q) * kNumCtr + kCtrDuplicates] : 0;
+    st->deliveries += c[kCtrDeliveries] + app_d;
+    st->duplicates += c[kCtrDuplicates] + app_u;
+    st->frontier_entries += c[kCtrEntries];
+    st->child_visits += c[kCtrChildren];
+    st->edge_words += c[kCtrSeenWrites];
+    // algorithmic bytes of the expand kernel (DESIGN.md §5.1 byte model):
+    // per entry frontier id 4 + topic 2 + row_ptr pair 8 + first child 4;
+    // per entry word the arrival read 8 (+ 8 when cleared); per child its
+    // flag byte + generation read/write (tree) or col id 4 (mesh); per
+    // seen read / seen write / arrival write 8.
+    if (pull)  // pull model: per node parent id 4 + flag 1 + parent generation 1, per
+               // reached node its generation write 1; parent rows read once; rows written
+      st->expand_bytes += c[kCtrChildren] * 6 + c[kCtrMeshChildren] * 1 +
+                          c[kCtrEntryWords] * 8 + c[kCtrSeenWrites] * 8;
+    else
+      st->expand_bytes += c[kCtrEntries] * 18 + c[kCtrEntryWords] * 8 + c[kCtrClearWords] * 8 +
+                          c[kCtrChildren] * 3 + c[kCtrMeshChildren] * 4 + c[kCtrSeenReads] * 8 +
+                          c[kCtrSeenWrites] * 8 + c[kCtrArrivalWrites] * 8;
+    if (q < PS_MAX_ROUNDS) {
+      st->deliveries_per_round[q] += c[kCtrDeliveries] + app_d;
+      st->frontier_per_round[q] += static_cast<uint32_t>(c[kCtrEntries]);
+    }
+  }
+  st->rounds += r;
+  st->expand_launches += launches;
+  st->expand_mode = pull ? PS_MODE_LEVEL_PULL : level ? PS_MODE_LEVEL_PUSH : PS_MODE_COMPACT;
+  st->windows += 1;
+}
+
 // Propagates one window: per topic t, win[t] lists the messages (indices into
 // `msgs`) whose bits form t's block of W_t = ceil(|win[t]|/64) words.
 int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<WinSlice>& win,
@@ -1410,6 +1465,26 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   }
   HIP_TRY(hipEventRecord(e->ev_run1, s), "event");
   const auto t_enq = std::chrono::steady_clock::now();
+  if (e->defer_last && e->defer_into && world == 1 && !record && !timed) {
+    // asynchronous run: the counters follow the kernels on the stream into
+    // pinned memory; ps_wait accumulates them
+    ps_engine::Inflight& f = *e->defer_into;
+    HIP_TRY(hipMemcpyAsync(f.hs, stats, static_cast<size_t>(r + 1) * kNumCtr * 8, hipMemcpyDeviceToHost, s),
+            "read stats");
+    HIP_TRY(hipEventRecord(f.done, s), "event");
+    f.deferred = true;
+    f.r = r;
+    f.launches = launches;
+    f.pull = pull;
+    f.level = level;
+    e->last_topics = tab;
+    for (uint32_t t = 0; t < nt; ++t) {
+      e->last_cnt[t] = tab[t].W ? win[t].n : 0;
+      e->last_lo[t] = win[t].n ? e->run_rank[win[t].idx[0]] : 0;
+    }
+    e->have_window = true;
+    return PS_OK;
+  }
   HIP_TRY(hipEventSynchronize(e->ev_run1), "sync");
   const auto t_sync = std::chrono::steady_clock::now();
   float ms = 0.f;
@@ -1430,37 +1505,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
             "read apply stats");
   }
   HIP_TRY(hipStreamSynchronize(s), "sync");
-  for (uint32_t q = 1; q <= r; ++q) {
-    const uint64_t* c = &hs[static_cast<size_t>(q) * kNumCtr];
-    const uint64_t app_d = (world > 1 && q <= planned0) ? ha[static_cast<size_t>(q) * kNumCtr + kCtrDeliveries] : 0;
-    const uint64_t app_u = (world > 1 && q <= planned0) ? ha[static_cast<size_t>(q) * kNumCtr + kCtrDuplicates] : 0;
-    st->deliveries += c[kCtrDeliveries] + app_d;
-    st->duplicates += c[kCtrDuplicates] + app_u;
-    st->frontier_entries += c[kCtrEntries];
-    st->child_visits += c[kCtrChildren];
-    st->edge_words += c[kCtrSeenWrites];
-    // algorithmic bytes of the expand kernel (DESIGN.md §5.1 byte model):
-    // per entry frontier id 4 + topic 2 + row_ptr pair 8 + first child 4;
-    // per entry word the arrival read 8 (+ 8 when cleared); per child its
-    // flag byte + generation read/write (tree) or col id 4 (mesh); per
-    // seen read / seen write / arrival write 8.
-    if (pull)  // pull model: per node parent id 4 + flag 1 + parent generation 1, per
-               // reached node its generation write 1; parent rows read once; rows written
-      st->expand_bytes += c[kCtrChildren] * 6 + c[kCtrMeshChildren] * 1 +
-                          c[kCtrEntryWords] * 8 + c[kCtrSeenWrites] * 8;
-    else
-      st->expand_bytes += c[kCtrEntries] * 18 + c[kCtrEntryWords] * 8 + c[kCtrClearWords] * 8 +
-                          c[kCtrChildren] * 3 + c[kCtrMeshChildren] * 4 + c[kCtrSeenReads] * 8 +
-                          c[kCtrSeenWrites] * 8 + c[kCtrArrivalWrites] * 8;
-    if (q < PS_MAX_ROUNDS) {
-      st->deliveries_per_round[q] += c[kCtrDeliveries] + app_d;
-      st->frontier_per_round[q] += static_cast<uint32_t>(c[kCtrEntries]);
-    }
-  }
-  st->rounds += r;
-  st->expand_launches += launches;
-  st->expand_mode = pull ? PS_MODE_LEVEL_PULL : level ? PS_MODE_LEVEL_PUSH : PS_MODE_COMPACT;
-  st->windows += 1;
+  accumulate_window(st, hs.data(), ha.data(), r, planned0, pull, level, launches, world);
   if (e->host_timing) {
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     std::fprintf(stderr, "[psengine] window: plan %.3f ms (run->window %.3f, topics %.3f, seeds %.3f, "
@@ -1520,7 +1565,9 @@ int run_phase(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<W
       win[t].idx = per[t].idx + std::min(lo, per[t].n);
       win[t].n = lo < per[t].n ? std::min(cap, per[t].n - lo) : 0;
     }
+    e->defer_last = e->defer_phase && k + 1 == n_win;
     int rc = run_window(e, msgs, win, st);
+    e->defer_last = false;
     if (rc) return rc;
   }
   return PS_OK;
@@ -1576,6 +1623,16 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
     delete e;
     return PS_E_DEVICE;
   }
+  for (auto& f : e->infl) {
+    void* h = nullptr;
+    if (hipEventCreate(&f.ev0) != hipSuccess || hipEventCreate(&f.ev1) != hipSuccess ||
+        hipEventCreateWithFlags(&f.done, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc(&h, (PS_MAX_ROUNDS + 1) * kNumCtr * 8, hipHostMallocDefault) != hipSuccess) {
+      ps_destroy(e);
+      return PS_E_DEVICE;
+    }
+    f.hs = static_cast<uint64_t*>(h);
+  }
   e->topics.resize(cfg->n_topics);
   e->live.assign(cfg->n_peers, 1);
   if (e->d_digest.ensure(8) != hipSuccess) {
@@ -1593,6 +1650,12 @@ void ps_destroy(ps_engine* e) {
   for (auto ev : e->ev_k) (void)hipEventDestroy(ev);
   if (e->ev_run0) (void)hipEventDestroy(e->ev_run0);
   if (e->ev_run1) (void)hipEventDestroy(e->ev_run1);
+  for (auto& f : e->infl) {
+    if (f.ev0) (void)hipEventDestroy(f.ev0);
+    if (f.ev1) (void)hipEventDestroy(f.ev1);
+    if (f.done) (void)hipEventDestroy(f.done);
+    if (f.hs) (void)hipHostFree(f.hs);
+  }
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -1803,11 +1866,16 @@ int ps_publish(ps_engine* e, const uint32_t* topic_of_msg, size_t n, uint32_t* f
   return ps_publish_at(e, topic_of_msg, nullptr, n, first);
 }
 
-int ps_run(ps_engine* e, ps_stats* out) {
-  if (!e) return PS_E_INVAL;
+}  // extern "C"
+
+namespace {
+
+// ps_run's body.  may_defer: the last window of the final phase may leave its
+// counters on the stream (ps_run_async); *stp is completed by ps_wait then.
+int run_body(ps_engine* e, ps_stats* stp, bool may_defer) {
   const auto t_host0 = std::chrono::steady_clock::now();
   e->t_run0 = t_host0;
-  ps_stats st{};
+  ps_stats& st = *stp;
   if (hipSetDevice(e->cfg.device) != hipSuccess) return e->fail(PS_E_DEVICE, "hipSetDevice");
   e->last_msgs.clear();
   e->last_msgs.swap(e->pending);
@@ -1883,7 +1951,9 @@ int ps_run(ps_engine* e, ps_stats* out) {
       any |= rest[t].n > 0;
     }
     if (any) {
+      e->defer_phase = may_defer && !record && e->world == 1;
       int rc = run_phase(e, msgs, rest, &st);
+      e->defer_phase = false;
       if (rc) return rc;
     }
   }
@@ -1922,7 +1992,60 @@ int ps_run(ps_engine* e, ps_stats* out) {
     std::fprintf(stderr, "[psengine] after-message prune %.3f ms\n",
                  std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_am).count());
   st.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
+  return PS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ps_run(ps_engine* e, ps_stats* out) {
+  if (!e) return PS_E_INVAL;
+  if (e->infl_count) return e->fail(PS_E_STATE, "asynchronous runs pending: ps_wait first");
+  ps_stats st{};
+  const int rc = run_body(e, &st, false);
+  if (rc) return rc;
   if (out) *out = st;
+  return PS_OK;
+}
+
+int ps_run_async(ps_engine* e) {
+  if (!e) return PS_E_INVAL;
+  if (e->infl_count >= 2) return e->fail(PS_E_STATE, "two runs in flight: ps_wait first");
+  ps_engine::Inflight& f = e->infl[(e->infl_head + e->infl_count) % 2];
+  f.st = ps_stats{};
+  f.deferred = false;
+  hipEvent_t ev0 = e->ev_run0, ev1 = e->ev_run1;
+  e->ev_run0 = f.ev0;  // this run's window events belong to its slot
+  e->ev_run1 = f.ev1;
+  e->defer_into = &f;
+  const int rc = run_body(e, &f.st, true);
+  e->ev_run0 = ev0;
+  e->ev_run1 = ev1;
+  e->defer_into = nullptr;
+  if (rc) {
+    (void)hipStreamSynchronize(e->stream);
+    return rc;
+  }
+  ++e->infl_count;
+  return PS_OK;
+}
+
+int ps_wait(ps_engine* e, ps_stats* out) {
+  if (!e) return PS_E_INVAL;
+  if (!e->infl_count) return e->fail(PS_E_NOTREADY, "no asynchronous run pending");
+  ps_engine::Inflight& f = e->infl[e->infl_head];
+  e->infl_head = (e->infl_head + 1) % 2;
+  --e->infl_count;
+  if (f.deferred) {
+    HIP_TRY(hipEventSynchronize(f.done), "sync");
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, f.ev0, f.ev1), "elapsed");
+    f.st.run_ms += ms;
+    accumulate_window(&f.st, f.hs, nullptr, f.r, 0, f.pull, f.level, f.launches, 1);
+    f.deferred = false;
+  }
+  if (out) *out = f.st;
   return PS_OK;
 }
 

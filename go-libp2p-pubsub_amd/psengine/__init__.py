@@ -108,6 +108,8 @@ PROTOTYPES = [
     ("ps_publish", C.c_int, [_P, _u32p, C.c_size_t, _u32p]),
     ("ps_publish_at", C.c_int, [_P, _u32p, _u32p, C.c_size_t, _u32p]),
     ("ps_run", C.c_int, [_P, C.POINTER(Stats)]),
+    ("ps_run_async", C.c_int, [_P]),
+    ("ps_wait", C.c_int, [_P, C.POINTER(Stats)]),
     ("ps_read_hops", C.c_int, [_P, _u32, _u8p]),
     ("ps_read_delivered", C.c_int, [_P, _u32, _u8p]),
     ("ps_read_peer_messages", C.c_int, [_P, _u32, _u32, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]),
@@ -282,6 +284,15 @@ class Engine:
     def run(self) -> Stats:
         st = Stats()
         self._check(self._L.ps_run(self._h, C.byref(st)))
+        return st
+
+    def run_async(self):
+        """Enqueues the run (ps_run_async); ps_wait / wait() completes it."""
+        self._check(self._L.ps_run_async(self._h))
+
+    def wait(self) -> Stats:
+        st = Stats()
+        self._check(self._L.ps_wait(self._h, C.byref(st)))
         return st
 
     def hops(self, msg: int) -> np.ndarray:

@@ -147,6 +147,14 @@ int ps_publish(ps_engine* e, const uint32_t* topic_of_msg, size_t n_msgs,
 int ps_publish_at(ps_engine* e, const uint32_t* topic_of_msg, const uint32_t* start_round,
                   size_t n_msgs, uint32_t* first_msg_id_out);
 int ps_run(ps_engine* e, ps_stats* out);
+/* ps_run in two halves, for pipelined batches: ps_run_async plans and enqueues
+ * the run and returns while its last window's kernels execute (at most two runs
+ * in flight), so the caller can publish and enqueue the next batch; ps_wait
+ * completes the oldest run in flight and returns its stats.  Reads
+ * (ps_read_*, ps_seen_digest) and membership changes stay stream-ordered
+ * behind the runs in flight; ps_run refuses while any is pending. */
+int ps_run_async(ps_engine* e);
+int ps_wait(ps_engine* e, ps_stats* out);
 
 /* ---- results of the last ps_run (client.Messages, client.go:26-28) --------
  * ps_read_hops: hop of message `msg` at every peer (PS_HOP_NONE = not

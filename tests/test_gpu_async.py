@@ -1,0 +1,112 @@
+"""GPU: pipelined runs (ps_run_async / ps_wait) deliver exactly what blocking
+ps_run does, batch by batch; readbacks stay stream-ordered behind runs in
+flight; the engine refuses the calls that would break the pairing."""
+import numpy as np
+import pytest
+
+import oracle as O
+import psengine as PE
+from psengine import workloads as WL
+
+pytestmark = pytest.mark.gpu
+
+
+def stats_key(st):
+    d = st.as_dict()
+    return (st.deliveries, st.duplicates, st.rounds, st.windows, st.expand_bytes,
+            tuple(d["deliveries_per_round"]))
+
+
+def test_pipelined_equals_blocking_multi_topic():
+    wl = WL.cfg3(50_000, 16, 3000)
+    rng = np.random.default_rng(3)
+    batches = [rng.permutation(wl.msg_topics)[: 1000 + 300 * b] for b in range(6)]
+    out = []
+    for pipelined in (False, True):
+        e = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed)
+        WL.build_engine_topics(e, wl)
+        res = []
+        if pipelined:
+            for i, b in enumerate(batches):
+                e.publish(b)
+                e.run_async()
+                if i:
+                    res.append(stats_key(e.wait()))
+            res.append(stats_key(e.wait()))
+        else:
+            for b in batches:
+                e.publish(b)
+                res.append(stats_key(e.run()))
+        out.append((res, e.seen_digest()))
+        e.close()
+    assert out[0] == out[1]
+
+
+def test_readback_behind_run_in_flight():
+    """ps_read_delivered right after ps_run_async sees that run's result (the
+    readback is stream-ordered behind the kernels)."""
+    rng = np.random.default_rng(5)
+    n, root = 3000, 0
+    perm = rng.permutation(np.arange(1, n))
+    parent = np.full(n, O.NONE, dtype=np.uint32)
+    order = np.concatenate([[root], perm])
+    for i in range(1, n):
+        parent[order[i]] = order[rng.integers(0, i)]
+    live = (rng.random(n) > 0.2).astype(np.uint8)
+    rp, cl = O.parents_to_csr(parent)
+    _, hops, _ = O.disseminate(rp, cl, root, live, 1)
+    with PE.Engine(n, 1) as e:
+        e.set_tree(0, root, parent)
+        e.set_live(live)
+        first = e.publish(np.zeros(100))
+        e.run_async()
+        got = e.delivered(first + 37)  # before ps_wait
+        exp = (hops[0] != 0xFF).astype(np.uint8)
+        assert np.array_equal(got, exp)
+        st = e.wait()
+        assert st.deliveries == 100 * int(exp.sum())
+
+
+def test_pairing_rules():
+    with PE.Engine(64, 1) as e:
+        e.topic_create(0, 0)
+        e.join(0, np.arange(1, 64))
+        with pytest.raises(PE.EngineError):
+            e.wait()  # nothing in flight
+        e.publish(np.zeros(10))
+        e.run_async()
+        e.publish(np.zeros(10))
+        e.run_async()
+        with pytest.raises(PE.EngineError):
+            e.run_async()  # two in flight already
+        with pytest.raises(PE.EngineError):
+            e.run()  # blocking run while runs are pending
+        assert e.wait().deliveries == 630
+        assert e.wait().deliveries == 630
+        e.publish(np.zeros(3))
+        assert e.run().deliveries == 189
+
+
+def test_async_with_hop_record_and_churn():
+    """Runs that cannot defer (hop record) or that prune after the message
+    (Parts) stay exact through the asynchronous entry points."""
+    n = 500
+    with PE.Engine(n, 1, record_hops=True, seed=9) as e:
+        ot = O.Tree(n, 0, 2, 5, PE.Engine.topic_seed(9, 0))
+        e.topic_create(0, 0, 2, 5)
+        e.join(0, np.arange(1, n))
+        ot.join_all(range(1, n))
+        for step in range(4):
+            leave = np.arange(10 + step, n, 37)
+            try:
+                e.leave(0, leave)
+            except PE.EngineError:
+                pass
+            for p in leave:
+                ot.leave(int(p))
+            first = e.publish(np.zeros(20))
+            e.run_async()
+            st = e.wait()
+            exp = ot.message()
+            assert np.array_equal(e.hops(first), exp), step
+            assert st.deliveries == 20 * int((exp != 0xFF).sum())
