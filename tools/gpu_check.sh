@@ -44,7 +44,7 @@ if [ "${PMC:-0}" = 1 ]; then
 import json, sys
 d = json.load(open(sys.argv[1]))
 for k, v in d.items():
-    if "k_expand" in k:
+    if "k_expand" in k or "k_pull" in k:
         print(k[:60], {x: v.get(x) for x in ("hbm_read_bytes_per_dispatch_x2", "hbm_write_bytes_per_dispatch")})
 EOF
 fi

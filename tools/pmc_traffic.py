@@ -21,19 +21,20 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def main():
     run_dir, kernel, workload, rtag = sys.argv[1:5]
     summ = json.load(open(os.path.join(run_dir, "pmc_summary.json")))
-    # production instance: no hop record (first template argument false)
+    # production instances: no hop record (first template argument false);
+    # the cache-policy variants (plain / nt stores) are one kernel to the
+    # roofline, so their traffic is averaged over all of their dispatches
     names = [k for k in summ if f"{kernel}<false" in k and "hbm_write_bytes_per_dispatch" in summ[k]]
     if not names:
         sys.exit(f"no {kernel}<false ...> dispatches with both counters in {run_dir}")
-    names.sort(key=lambda k: -summ[k]["WRITE_SIZE"]["dispatches"])
-    d = summ[names[0]]
-    rd = d["hbm_read_bytes_per_dispatch_x2"]
-    wr = d["hbm_write_bytes_per_dispatch"]
+    disp = sum(summ[k]["WRITE_SIZE"]["dispatches"] for k in names)
+    rd = sum(summ[k]["hbm_read_bytes_per_dispatch_x2"] * summ[k]["WRITE_SIZE"]["dispatches"] for k in names) / disp
+    wr = sum(summ[k]["hbm_write_bytes_per_dispatch"] * summ[k]["WRITE_SIZE"]["dispatches"] for k in names) / disp
     os.makedirs(os.path.join(REPO, "profiles", rtag), exist_ok=True)
     dst = os.path.join("profiles", rtag, "pmc_summary.json")
     shutil.copy(os.path.join(run_dir, "pmc_summary.json"), os.path.join(REPO, dst))
-    out = {"kernel": kernel, "workload": workload, "instance": names[0],
-           "dispatches": d["WRITE_SIZE"]["dispatches"],
+    out = {"kernel": kernel, "workload": workload, "instances": names,
+           "dispatches": disp,
            "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
            "traffic_bytes_per_launch": rd + wr,
            "source": f"rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) of "
