@@ -200,6 +200,9 @@ struct ps_engine {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the window's kernels
     hipEvent_t done = nullptr;                // after the counters' readback
     uint64_t* hs = nullptr;  // pinned: (PS_MAX_ROUNDS + 1) x kNumCtr counters
+    uint64_t* ha = nullptr;  // pinned: apply counters of a multi-GPU window
+    uint32_t planned0 = 0;
+    int32_t world = 1;
   };
   Inflight infl[2];
   uint32_t infl_head = 0, infl_count = 0;
@@ -1465,14 +1468,21 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   }
   HIP_TRY(hipEventRecord(e->ev_run1, s), "event");
   const auto t_enq = std::chrono::steady_clock::now();
-  if (e->defer_last && e->defer_into && world == 1 && !record && !timed) {
+  if (e->defer_last && e->defer_into && !record && !timed && r <= PS_MAX_ROUNDS &&
+      (world == 1 || planned0 <= PS_MAX_ROUNDS)) {  // the pinned slots hold PS_MAX_ROUNDS + 1 rows
     // asynchronous run: the counters follow the kernels on the stream into
     // pinned memory; ps_wait accumulates them
     ps_engine::Inflight& f = *e->defer_into;
     HIP_TRY(hipMemcpyAsync(f.hs, stats, static_cast<size_t>(r + 1) * kNumCtr * 8, hipMemcpyDeviceToHost, s),
             "read stats");
+    if (world > 1)
+      HIP_TRY(hipMemcpyAsync(f.ha, e->d_apply_stats.p, static_cast<size_t>(planned0 + 1) * kNumCtr * 8,
+                             hipMemcpyDeviceToHost, s),
+              "read apply stats");
     HIP_TRY(hipEventRecord(f.done, s), "event");
     f.deferred = true;
+    f.planned0 = planned0;
+    f.world = world;
     f.r = r;
     f.launches = launches;
     f.pull = pull;
@@ -1627,11 +1637,12 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
     void* h = nullptr;
     if (hipEventCreate(&f.ev0) != hipSuccess || hipEventCreate(&f.ev1) != hipSuccess ||
         hipEventCreateWithFlags(&f.done, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc(&h, (PS_MAX_ROUNDS + 1) * kNumCtr * 8, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc(&h, 2 * (PS_MAX_ROUNDS + 1) * kNumCtr * 8, hipHostMallocDefault) != hipSuccess) {
       ps_destroy(e);
       return PS_E_DEVICE;
     }
     f.hs = static_cast<uint64_t*>(h);
+    f.ha = f.hs + (PS_MAX_ROUNDS + 1) * kNumCtr;
   }
   e->topics.resize(cfg->n_topics);
   e->live.assign(cfg->n_peers, 1);
@@ -1951,7 +1962,7 @@ int run_body(ps_engine* e, ps_stats* stp, bool may_defer) {
       any |= rest[t].n > 0;
     }
     if (any) {
-      e->defer_phase = may_defer && !record && e->world == 1;
+      e->defer_phase = may_defer && !record;
       int rc = run_phase(e, msgs, rest, &st);
       e->defer_phase = false;
       if (rc) return rc;
@@ -2042,7 +2053,7 @@ int ps_wait(ps_engine* e, ps_stats* out) {
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, f.ev0, f.ev1), "elapsed");
     f.st.run_ms += ms;
-    accumulate_window(&f.st, f.hs, nullptr, f.r, 0, f.pull, f.level, f.launches, 1);
+    accumulate_window(&f.st, f.hs, f.ha, f.r, f.planned0, f.pull, f.level, f.launches, f.world);
     f.deferred = false;
   }
   if (out) *out = f.st;

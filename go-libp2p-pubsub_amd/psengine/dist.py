@@ -109,9 +109,20 @@ def bench_main(args, descr: dict, metric: str):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     local_deliv = 0
-    for _ in range(args.steps):
-        st = step()
-        local_deliv += st.deliveries
+    if getattr(args, "sync", False):
+        for _ in range(args.steps):
+            st = step()
+            local_deliv += st.deliveries
+    else:
+        # pipelined like bench.py: batch k + 1 is published and enqueued (its
+        # RCCL exchanges included, stream-ordered) while batch k runs
+        for i in range(args.steps):
+            eng.publish(wl.msg_topics)
+            eng.run_async()
+            if i:
+                local_deliv += eng.wait().deliveries
+        if args.steps:
+            local_deliv += eng.wait().deliveries
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0

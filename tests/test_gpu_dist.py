@@ -115,3 +115,52 @@ def test_sharded_join_trees_and_digest_sum():
     for e in engines:
         e.close()
     lb.close()
+
+
+def test_sharded_pipelined_batches():
+    """Pipelined runs (ps_run_async / ps_wait) on 3 ranks: every batch's job
+    total equals the single engine's, and the final digests add up."""
+    wl = WL.cfg3(20000, 8, 2000)
+    rng = np.random.default_rng(8)
+    batches = [rng.permutation(wl.msg_topics)[: 500 + 250 * b] for b in range(5)]
+    with PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed) as one:
+        WL.build_engine_topics(one, wl)
+        exp = []
+        for b in batches:
+            one.publish(b)
+            exp.append(one.run().deliveries)
+        d1 = one.seen_digest()
+    world = 3
+    lb = PE.Loopback(world)
+    engines = [PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed, msg_window=1 << 20)
+               for _ in range(world)]
+    for r, e in enumerate(engines):
+        e.dist_init_loopback(lb, r, PE.PART_SUBTREE)
+        WL.build_engine_topics(e, wl)
+    got = [[] for _ in range(world)]
+    errs = []
+
+    def go(r):
+        try:
+            e = engines[r]
+            for i, b in enumerate(batches):
+                e.publish(b)
+                e.run_async()
+                if i:
+                    got[r].append(e.wait().deliveries)
+            got[r].append(e.wait().deliveries)
+        except Exception as ex:  # noqa: BLE001
+            errs.append((r, ex))
+
+    th = [threading.Thread(target=go, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in th), "rank thread hung"
+    assert not errs, errs
+    assert [sum(g[i] for g in got) for i in range(len(batches))] == exp
+    assert sum(e.seen_digest() for e in engines) % (1 << 64) == d1
+    for e in engines:
+        e.close()
+    lb.close()
