@@ -1737,7 +1737,14 @@ int ps_topic_leave(ps_engine* e, uint32_t topic, const uint32_t* peers, size_t n
   TopicHost* T = join_topic(e, topic);
   if (!T) return PS_E_STATE;
   int first = PS_OK;
+  // leaving peers are scattered over the tree: their entries are fetched a
+  // few peers ahead (two stages: the peer, then the lists it points to)
+  constexpr size_t kAhead0 = 16, kAhead1 = 8;
+  for (size_t i = 0; i < std::min(n, kAhead0); ++i) T->tree.prefetch_leave(peers[i], 0);
+  for (size_t i = 0; i < std::min(n, kAhead1); ++i) T->tree.prefetch_leave(peers[i], 1);
   for (size_t i = 0; i < n; ++i) {
+    if (i + kAhead0 < n) T->tree.prefetch_leave(peers[i + kAhead0], 0);
+    if (i + kAhead1 < n) T->tree.prefetch_leave(peers[i + kAhead1], 1);
     int rc = T->tree.close_client(peers[i]);
     if (rc && !first) first = rc;
   }

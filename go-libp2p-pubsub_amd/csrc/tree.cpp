@@ -89,6 +89,12 @@ int SubscriptionTree::attach(uint32_t at, uint32_t joiner, bool prio) {
       return PS_OK;
     }
     if (list.empty()) return PS_E_NOPARENT;
+    // the walk continues at one of these children: start fetching their
+    // entries while the redirect choice is made
+    for (const auto& r : list) {
+      __builtin_prefetch(&kids_[r.id]);
+      __builtin_prefetch(&state_[r.id]);
+    }
     int64_t best = 10000000000ll;
     uint32_t ties = 0;
     for (const auto& r : list) {
@@ -166,6 +172,23 @@ int SubscriptionTree::close_client(uint32_t peer) {
   parted_at_.push_back(at);
   depart(at, peer, rec->last_state);
   return PS_OK;
+}
+
+void SubscriptionTree::prefetch_leave(uint32_t peer, int stage) const {
+  if (peer >= n_) return;
+  if (stage == 0) {
+    __builtin_prefetch(&state_[peer]);
+    __builtin_prefetch(&up_[peer]);
+    __builtin_prefetch(&kids_[peer]);
+    return;
+  }
+  if (!kids_[peer].empty()) __builtin_prefetch(kids_[peer].data());
+  const uint32_t at = up_[peer];
+  if (at < n_) {
+    __builtin_prefetch(&kids_[at]);
+    __builtin_prefetch(&state_[at]);
+    if (!kids_[at].empty()) __builtin_prefetch(kids_[at].data());
+  }
 }
 
 int SubscriptionTree::close_host(uint32_t peer) {

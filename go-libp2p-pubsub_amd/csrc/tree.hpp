@@ -33,6 +33,10 @@ class SubscriptionTree {
   // 0 or a negative PS_E_* code.
   int subscribe(uint32_t peer);
   int close_client(uint32_t peer);  // graceful: Part
+  // Cache hint for a batch of leaves (no state change): stage 0 touches the
+  // peer's own entries, stage 1 (a few peers later) its child lists and its
+  // parent's list, so close_client() finds them resident.
+  void prefetch_leave(uint32_t peer, int stage) const;
   int close_host(uint32_t peer);    // abrupt
   // Called once per message that floods this topic: lazy prune and repair of
   // failed writes at every node the message reached (rule Q3).  `reach`, if
