@@ -125,8 +125,8 @@ struct ps_engine {
   bool mirrors_valid = true;  // host copies of node_peer / flags / CSR are current
   std::vector<uint32_t> pairs_host, gstat_host, lvl_host, roots_host;
   std::vector<size_t> pair_off;
-  DevBuf d_tpar, d_anc0, d_anc1, d_dep0, d_dep1, d_keys0, d_keys1, d_skeys, d_local, d_deg, d_first, d_lvl,
-      d_gstat, d_cub, d_pairs, d_live, d_roots;
+  DevBuf d_tpar, d_anc0, d_anc1, d_dep0, d_dep1, d_keys0, d_skeys, d_local, d_deg, d_first, d_lvl,
+      d_gstat, d_cub, d_pairs, d_live, d_roots, d_cnt, d_fidx, d_childoff;
   std::chrono::steady_clock::time_point t_run0;
   bool level_push = false;       // PSAMD_LEVEL_PUSH=1: level mode with the push kernel (A/B)
   uint32_t pull_words = kPullWords;  // words per pull chunk (PSAMD_PULL_WORDS)
@@ -573,7 +573,6 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   HIP_TRY(e->d_skeys.ensure(static_cast<size_t>(nt) * n * 8), "alloc sorted keys");
   HIP_TRY(e->d_gstat.ensure(static_cast<size_t>(nt) * 4 * 4), "alloc build stats");
   HIP_TRY(e->d_lvl.ensure(static_cast<size_t>(nt) * 512 * 4), "alloc level tables");
-  HIP_TRY(e->d_keys1.ensure(static_cast<size_t>(n) * 8), "alloc keys");
   size_t cub_bytes = 0, scan_bytes = 0;
   HIP_TRY(sort_keys(nullptr, &cub_bytes, nullptr, nullptr, n, s), "sort size");
   HIP_TRY(e->d_cub.ensure(std::max<size_t>(cub_bytes, 16)), "alloc sort temp");
@@ -653,34 +652,45 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   HIP_TRY(hipMemsetAsync(e->d_deg.p, 0, (static_cast<size_t>(nn) + 1) * 4, s), "clear fan-out");
   HIP_TRY(hipMemsetAsync(e->d_first.p, 0xFF, std::max<size_t>(nn, 1) * 4, s), "clear first child");
   uint32_t* lvl = e->d_lvl.as<uint32_t>();  // [t][0..255] level start, [t][256..511] internal count
-  // BFS placement, level by level: level d re-keyed by its parents' node ids
-  // (placed with level d - 1) and sorted, so siblings are consecutive and in
-  // their parents' order
+  // BFS placement, level by level and without sorting: the keys are already
+  // grouped by level and, within a level, by parent peer with siblings in peer
+  // order; the groups go in parent node order (an exclusive scan of the
+  // parents' fan-out), each child at its sibling rank
+  HIP_TRY(e->d_cnt.ensure(static_cast<size_t>(n) * 4), "alloc fan-out by peer");
+  HIP_TRY(e->d_fidx.ensure(static_cast<size_t>(n) * 4), "alloc first child index");
+  HIP_TRY(e->d_childoff.ensure(static_cast<size_t>(n) * 4 + 4), "alloc child offsets");
+  {
+    size_t sb = 0;
+    HIP_TRY(scan_u32(nullptr, &sb, nullptr, nullptr, n, s), "scan size");
+    HIP_TRY(e->d_cub.ensure(std::max<size_t>(sb, 16)), "alloc scan temp");
+  }
+  uint32_t* cnt = e->d_cnt.as<uint32_t>();
+  uint32_t* fidx = e->d_fidx.as<uint32_t>();
+  uint32_t* childoff = e->d_childoff.as<uint32_t>();
   for (uint32_t t = 0; t < nt; ++t) {
     TopicHost& T = e->topics[t];
     if (!T.n_nodes) continue;
     const uint32_t depth = gs[4 * t + 1];
     const uint64_t* keys = e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n;
-    for (uint32_t d = 0; d <= depth; ++d) {
+    const uint16_t tt = static_cast<uint16_t>(t);
+    HIP_TRY(hipMemsetAsync(cnt, 0, static_cast<size_t>(n) * 4, s), "clear fan-out by peer");
+    HIP_TRY(hipMemsetAsync(fidx, 0xFF, static_cast<size_t>(n) * 4, s), "clear first child index");
+    HIP_TRY(launch_child_stats(keys, T.n_nodes, cnt, fidx, s), "child stats");
+    HIP_TRY(launch_place_root(keys, T.nbase, tt, cnt, e->d_node_peer.as<uint32_t>(),
+                              e->d_node_topic.as<uint16_t>(), e->d_local.as<uint32_t>(),
+                              e->d_node_parent.as<uint32_t>(), e->d_deg.as<uint32_t>(), s),
+            "place root");
+    for (uint32_t d = 1; d <= depth; ++d) {
+      const uint32_t plo = lh[512 * t + d - 1];
       const uint32_t lo = lh[512 * t + d];
       const uint32_t hi = d == depth ? T.n_nodes : lh[512 * t + d + 1];
-      const uint32_t cnt = hi - lo;
-      if (d == 0) {
-        HIP_TRY(launch_place(keys, 1, T.nbase, static_cast<uint16_t>(t), true, e->d_node_peer.as<uint32_t>(),
-                             e->d_node_topic.as<uint16_t>(), e->d_local.as<uint32_t>(),
-                             e->d_node_parent.as<uint32_t>(), e->d_deg.as<uint32_t>(),
-                             e->d_first.as<uint32_t>(), s),
-                "place root");
-        continue;
-      }
-      HIP_TRY(launch_rekey(keys + lo, cnt, e->d_local.as<uint32_t>(), e->d_keys0.as<uint64_t>(), s), "rekey");
       size_t tb = e->d_cub.bytes;
-      HIP_TRY(sort_keys(e->d_cub.p, &tb, e->d_keys0.as<uint64_t>(), e->d_keys1.as<uint64_t>(), cnt, s),
-              "sort level");
-      HIP_TRY(launch_place(e->d_keys1.as<uint64_t>(), cnt, T.nbase + lo, static_cast<uint16_t>(t), false,
-                           e->d_node_peer.as<uint32_t>(), e->d_node_topic.as<uint16_t>(),
-                           e->d_local.as<uint32_t>(), e->d_node_parent.as<uint32_t>(),
-                           e->d_deg.as<uint32_t>(), e->d_first.as<uint32_t>(), s),
+      HIP_TRY(scan_u32(e->d_cub.p, &tb, e->d_deg.as<uint32_t>() + T.nbase + plo, childoff, lo - plo, s),
+              "scan fan-out");
+      HIP_TRY(launch_place_level(keys, lo, hi, T.nbase, T.nbase + plo, childoff, cnt, fidx, tt,
+                                 e->d_node_peer.as<uint32_t>(), e->d_node_topic.as<uint16_t>(),
+                                 e->d_local.as<uint32_t>(), e->d_node_parent.as<uint32_t>(),
+                                 e->d_deg.as<uint32_t>(), e->d_first.as<uint32_t>(), s),
               "place level");
     }
   }

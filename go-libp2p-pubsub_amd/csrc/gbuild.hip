@@ -141,45 +141,6 @@ __global__ __launch_bounds__(kB) void k_level_starts(const uint64_t* __restrict_
   if (u == 0 || static_cast<uint32_t>(keys[u - 1] >> 56) != d) lvl_start[d] = u;
 }
 
-// Level d's keys re-keyed by the parent's node id (placed with level d - 1):
-// sorting them gives BFS order (siblings consecutive, in parent order).
-__global__ __launch_bounds__(kB) void k_rekey(const uint64_t* __restrict__ keys, uint32_t n,
-                                              const uint32_t* __restrict__ local,
-                                              uint64_t* __restrict__ out) {
-  const uint32_t i = blockIdx.x * kB + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t k = keys[i];
-  const uint32_t pu = local[static_cast<uint32_t>((k >> kBuildPeerBits) & kPeerMask)];
-  out[i] = (static_cast<uint64_t>(pu) << kBuildPeerBits) | (k & kPeerMask);
-}
-
-// Place one level: node ids [node0, node0 + n) in key order; key = parent
-// node << 28 | peer (root: parent kNone).
-__global__ __launch_bounds__(kB) void k_place(const uint64_t* __restrict__ keys, uint32_t n,
-                                              uint32_t node0, uint16_t topic, bool root,
-                                              uint32_t* __restrict__ node_peer,
-                                              uint16_t* __restrict__ node_topic,
-                                              uint32_t* __restrict__ local,
-                                              uint32_t* __restrict__ node_parent,
-                                              uint32_t* __restrict__ deg, uint32_t* __restrict__ first) {
-  const uint32_t i = blockIdx.x * kB + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t k = keys[i];
-  const uint32_t peer = static_cast<uint32_t>(k & kPeerMask);
-  const uint32_t node = node0 + i;
-  node_peer[node] = peer;
-  node_topic[node] = topic;
-  local[peer] = node;
-  if (root) {
-    node_parent[node] = kNoneP;
-    return;
-  }
-  const uint32_t pu = static_cast<uint32_t>(k >> kBuildPeerBits);
-  node_parent[node] = pu;
-  atomicAdd(deg + pu, 1u);
-  atomicMin(first + pu, node);
-}
-
 // Internal nodes per level and the largest fan-out of a topic placed at
 // [nbase, nbase + R) with level starts lvl_start[0..depth] (topic-relative):
 // a per-block LDS histogram over the levels, flushed with one atomic per
@@ -216,6 +177,58 @@ __global__ __launch_bounds__(kB) void k_level_internal(const uint32_t* __restric
   if (threadIdx.x == 0 && m) atomicMax(max_deg, m);
 }
 
+// Fan-out and first child of every parent peer in one topic's (depth, parent,
+// peer)-sorted keys (first R valid; keys[0] is the root): cnt[parent] += 1,
+// firstidx[parent] = min index.  Siblings are contiguous and sorted by peer.
+__global__ __launch_bounds__(kB) void k_child_stats(const uint64_t* __restrict__ keys, uint32_t R,
+                                                    uint32_t* __restrict__ cnt,
+                                                    uint32_t* __restrict__ firstidx) {
+  const uint32_t i = blockIdx.x * kB + threadIdx.x;
+  if (i == 0 || i >= R) return;
+  const uint32_t pp = static_cast<uint32_t>((keys[i] >> kBuildPeerBits) & kPeerMask);
+  atomicAdd(cnt + pp, 1u);
+  atomicMin(firstidx + pp, i);
+}
+
+__global__ void k_place_root(const uint64_t* __restrict__ keys, uint32_t nbase, uint16_t topic,
+                             const uint32_t* __restrict__ cnt, uint32_t* __restrict__ node_peer,
+                             uint16_t* __restrict__ node_topic, uint32_t* __restrict__ local,
+                             uint32_t* __restrict__ node_parent, uint32_t* __restrict__ deg) {
+  if (threadIdx.x) return;
+  const uint32_t peer = static_cast<uint32_t>(keys[0] & kPeerMask);
+  node_peer[nbase] = peer;
+  node_topic[nbase] = topic;
+  local[peer] = nbase;
+  node_parent[nbase] = kNoneP;
+  deg[nbase] = cnt[peer];
+}
+
+// BFS placement of level d (keys [lo, hi), nodes nbase + [lo, hi)) without a
+// sort: the children of parent node u form one group at nbase + lo +
+// childoff[u - prev0] (exclusive scan of the parents' fan-out, in parent node
+// order), each child at its rank among its siblings (index - first index).
+__global__ __launch_bounds__(kB) void k_place_level(
+    const uint64_t* __restrict__ keys, uint32_t lo, uint32_t hi, uint32_t nbase, uint32_t prev0,
+    const uint32_t* __restrict__ childoff, const uint32_t* __restrict__ cnt,
+    const uint32_t* __restrict__ firstidx, uint16_t topic, uint32_t* __restrict__ node_peer,
+    uint16_t* __restrict__ node_topic, uint32_t* __restrict__ local, uint32_t* __restrict__ node_parent,
+    uint32_t* __restrict__ deg, uint32_t* __restrict__ first) {
+  const uint32_t i = lo + blockIdx.x * kB + threadIdx.x;
+  if (i >= hi) return;
+  const uint64_t k = keys[i];
+  const uint32_t peer = static_cast<uint32_t>(k & kPeerMask);
+  const uint32_t pp = static_cast<uint32_t>((k >> kBuildPeerBits) & kPeerMask);
+  const uint32_t pu = local[pp];
+  const uint32_t f = firstidx[pp];
+  const uint32_t node = nbase + lo + childoff[pu - prev0] + (i - f);
+  node_peer[node] = peer;
+  node_topic[node] = topic;
+  local[peer] = node;
+  node_parent[node] = pu;
+  deg[node] = cnt[peer];
+  if (i == f) first[pu] = node;
+}
+
 // out[i] = 1 iff peers[i] holds a node of the topic placed at [nbase, nbase +
 // n_nodes) by the last build (local[] may hold stale ids: node_peer confirms)
 __global__ __launch_bounds__(kB) void k_reach_query(const uint32_t* __restrict__ peers, uint32_t n,
@@ -244,25 +257,34 @@ hipError_t launch_reach_query(const uint32_t* peers, uint32_t n, uint32_t n_peer
   return hipGetLastError();
 }
 
+hipError_t launch_child_stats(const uint64_t* keys, uint32_t R, uint32_t* cnt, uint32_t* firstidx,
+                              hipStream_t s) {
+  if (R < 2) return hipSuccess;
+  hipLaunchKernelGGL(k_child_stats, dim3(blocks(R)), dim3(kB), 0, s, keys, R, cnt, firstidx);
+  return hipGetLastError();
+}
+
+hipError_t launch_place_root(const uint64_t* keys, uint32_t nbase, uint16_t topic, const uint32_t* cnt,
+                             uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
+                             uint32_t* node_parent, uint32_t* deg, hipStream_t s) {
+  hipLaunchKernelGGL(k_place_root, dim3(1), dim3(64), 0, s, keys, nbase, topic, cnt, node_peer, node_topic,
+                     local, node_parent, deg);
+  return hipGetLastError();
+}
+
+hipError_t launch_place_level(const uint64_t* keys, uint32_t lo, uint32_t hi, uint32_t nbase, uint32_t prev0,
+                              const uint32_t* childoff, const uint32_t* cnt, const uint32_t* firstidx,
+                              uint16_t topic, uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
+                              uint32_t* node_parent, uint32_t* deg, uint32_t* first, hipStream_t s) {
+  if (hi <= lo) return hipSuccess;
+  hipLaunchKernelGGL(k_place_level, dim3(blocks(hi - lo)), dim3(kB), 0, s, keys, lo, hi, nbase, prev0,
+                     childoff, cnt, firstidx, topic, node_peer, node_topic, local, node_parent, deg, first);
+  return hipGetLastError();
+}
+
 hipError_t launch_level_starts(const uint64_t* keys, uint32_t R, uint32_t* lvl_start, hipStream_t s) {
   if (R == 0) return hipSuccess;
   hipLaunchKernelGGL(k_level_starts, dim3(blocks(R)), dim3(kB), 0, s, keys, R, lvl_start);
-  return hipGetLastError();
-}
-
-hipError_t launch_rekey(const uint64_t* keys, uint32_t n, const uint32_t* local, uint64_t* out,
-                        hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_rekey, dim3(blocks(n)), dim3(kB), 0, s, keys, n, local, out);
-  return hipGetLastError();
-}
-
-hipError_t launch_place(const uint64_t* keys, uint32_t n, uint32_t node0, uint16_t topic, bool root,
-                        uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
-                        uint32_t* node_parent, uint32_t* deg, uint32_t* first, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_place, dim3(blocks(n)), dim3(kB), 0, s, keys, n, node0, topic, root, node_peer,
-                     node_topic, local, node_parent, deg, first);
   return hipGetLastError();
 }
 

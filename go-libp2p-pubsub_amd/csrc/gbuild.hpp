@@ -4,8 +4,10 @@
 // For each topic: the upstream of every subscribed peer (kNone otherwise,
 // maintained on the host by the restated join / leave protocol and shipped as
 // deltas) -> depth of every peer reachable from the root (pointer jumping) ->
-// one radix sort of (depth, parent, peer) keys -> node ids: each BFS level is
-// a contiguous range, siblings are consecutive -> node_parent, CSR, flags.
+// one radix sort of (depth, parent, peer) keys: each BFS level is a
+// contiguous range, siblings consecutive -> node ids level by level (the
+// sibling groups in parent node order: a scan of the parents' fan-out, no
+// further sort) -> node_parent, CSR, flags.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -41,19 +43,24 @@ hipError_t sort_keys(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_
 hipError_t scan_u32(void* temp, size_t* temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n,
                     hipStream_t s);
 
-// BFS placement, level by level: level starts of the sorted keys; level d's
-// keys re-keyed by their parent's node id (parent node << 28 | peer), sorted,
-// then placed at node0.. (node_peer, node_topic, local, node_parent, fan-out
-// and first child of the parents)
+// level starts of a topic's sorted keys (lvl_start[d], topic-relative)
 hipError_t launch_level_starts(const uint64_t* keys, uint32_t R, uint32_t* lvl_start, hipStream_t s);
-hipError_t launch_rekey(const uint64_t* keys, uint32_t n, const uint32_t* local, uint64_t* out,
-                        hipStream_t s);
-hipError_t launch_place(const uint64_t* keys, uint32_t n, uint32_t node0, uint16_t topic, bool root,
-                        uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
-                        uint32_t* node_parent, uint32_t* deg, uint32_t* first, hipStream_t s);
 hipError_t launch_level_internal(const uint32_t* deg, uint32_t nbase, uint32_t R,
                                  const uint32_t* lvl_start, uint32_t depth, uint32_t* lvl_internal,
                                  uint32_t* max_deg, hipStream_t s);
+// Sort-free BFS placement: fan-out / first child index of every parent peer
+// from the (depth, parent, peer)-sorted keys; the root; then level by level,
+// each child at nbase + lo + childoff[parent node - prev0] + sibling rank,
+// where childoff is the exclusive scan of the parents' fan-out (deg).
+hipError_t launch_child_stats(const uint64_t* keys, uint32_t R, uint32_t* cnt, uint32_t* firstidx,
+                              hipStream_t s);
+hipError_t launch_place_root(const uint64_t* keys, uint32_t nbase, uint16_t topic, const uint32_t* cnt,
+                             uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
+                             uint32_t* node_parent, uint32_t* deg, hipStream_t s);
+hipError_t launch_place_level(const uint64_t* keys, uint32_t lo, uint32_t hi, uint32_t nbase, uint32_t prev0,
+                              const uint32_t* childoff, const uint32_t* cnt, const uint32_t* firstidx,
+                              uint16_t topic, uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
+                              uint32_t* node_parent, uint32_t* deg, uint32_t* first, hipStream_t s);
 // out[i] = 1 iff peer peers[i] holds a node of the topic at [nbase, nbase +
 // n_nodes) in the last GPU build (the message's reach, for the lazy prune)
 hipError_t launch_reach_query(const uint32_t* peers, uint32_t n, uint32_t n_peers, const uint32_t* local,
