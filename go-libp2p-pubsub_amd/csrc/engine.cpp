@@ -118,6 +118,7 @@ struct ps_engine {
   uint64_t pull_nt_min = 64ull << 20;  // nt only for rounds writing >= this many row bytes, and the last round
   std::vector<uint64_t> pull_bytes;    // row bytes written per round (pull chunks)
   bool host_timing = false;      // PSAMD_HOST_TIMING=1: host phase times to stderr
+  uint32_t small_place = 512;    // top levels up to this many nodes placed by one block (PSAMD_SMALL_PLACE, 0 = off)
   // GPU rebuild of the node space: on by default for one
   // rank and tree topics (PSAMD_GPU_BUILD=0: host build)
   bool gpu_build_on = true;
@@ -545,7 +546,13 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
       if (full)
         for (uint32_t p = 0; p < n; ++p) diff(p, T.tree.in_parent(p));
       else
-        for (uint32_t p : cand) diff(p, T.tree.in_parent(p));
+        for (size_t i = 0; i < cand.size(); ++i) {
+          if (i + 16 < cand.size()) {  // touched peers are scattered: fetch ahead
+            T.tree.prefetch_peer(cand[i + 16]);
+            __builtin_prefetch(&T.par_mirror[cand[i + 16]]);
+          }
+          diff(cand[i], T.tree.in_parent(cand[i]));
+        }
     } else if (T.par_full_dirty || full) {
       for (uint32_t p = 0; p < n; ++p) diff(p, p == T.root ? kNone : T.parent[p]);
       T.par_full_dirty = false;
@@ -676,11 +683,25 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
     HIP_TRY(hipMemsetAsync(cnt, 0, static_cast<size_t>(n) * 4, s), "clear fan-out by peer");
     HIP_TRY(hipMemsetAsync(fidx, 0xFF, static_cast<size_t>(n) * 4, s), "clear first child index");
     HIP_TRY(launch_child_stats(keys, T.n_nodes, cnt, fidx, s), "child stats");
-    HIP_TRY(launch_place_root(keys, T.nbase, tt, cnt, e->d_node_peer.as<uint32_t>(),
-                              e->d_node_topic.as<uint16_t>(), e->d_local.as<uint32_t>(),
-                              e->d_node_parent.as<uint32_t>(), e->d_deg.as<uint32_t>(), s),
-            "place root");
-    for (uint32_t d = 1; d <= depth; ++d) {
+    // the small top levels (and their parents) go in one single-block launch
+    auto lvl_end = [&](uint32_t d) { return d == depth ? T.n_nodes : lh[512 * t + d + 1]; };
+    uint32_t d_small = 1;
+    while (d_small <= depth && lvl_end(d_small) - lh[512 * t + d_small] <= e->small_place &&
+           lh[512 * t + d_small] - lh[512 * t + d_small - 1] <= e->small_place)
+      ++d_small;
+    if (d_small > 1) {
+      HIP_TRY(launch_place_small(keys, e->d_lvl.as<uint32_t>() + 512 * t, d_small, depth, T.n_nodes, T.nbase, tt,
+                                 cnt, fidx, e->d_node_peer.as<uint32_t>(), e->d_node_topic.as<uint16_t>(),
+                                 e->d_local.as<uint32_t>(), e->d_node_parent.as<uint32_t>(),
+                                 e->d_deg.as<uint32_t>(), e->d_first.as<uint32_t>(), s),
+              "place small levels");
+    } else {
+      HIP_TRY(launch_place_root(keys, T.nbase, tt, cnt, e->d_node_peer.as<uint32_t>(),
+                                e->d_node_topic.as<uint16_t>(), e->d_local.as<uint32_t>(),
+                                e->d_node_parent.as<uint32_t>(), e->d_deg.as<uint32_t>(), s),
+              "place root");
+    }
+    for (uint32_t d = d_small; d <= depth; ++d) {
       const uint32_t plo = lh[512 * t + d - 1];
       const uint32_t lo = lh[512 * t + d];
       const uint32_t hi = d == depth ? T.n_nodes : lh[512 * t + d + 1];
@@ -1631,6 +1652,8 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_NO_SINGLE_START")) e->no_single_start = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_NO_LEVEL")) e->no_level = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_HOST_TIMING")) e->host_timing = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_SMALL_PLACE"))
+    e->small_place = std::min<uint32_t>(static_cast<uint32_t>(std::atoi(v)), kBuildSmallLevel);
   if (const char* v = std::getenv("PSAMD_PULL_NT")) e->pull_nt = static_cast<uint32_t>(std::atoi(v)) & 3u;
   if (const char* v = std::getenv("PSAMD_PULL_NT_MB")) e->pull_nt_min = std::strtoull(v, nullptr, 10) << 20;
   if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;

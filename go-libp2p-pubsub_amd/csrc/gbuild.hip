@@ -229,6 +229,86 @@ __global__ __launch_bounds__(kB) void k_place_level(
   if (i == f) first[pu] = node;
 }
 
+// The small top levels of one topic in ONE block (one launch for what would be
+// 3 launches per level): root, then each level 1 .. d_end - 1 (at most
+// kBuildSmallLevel nodes and parents) with the parents' fan-out scanned in
+// LDS.  Nodes placed by other waves of the block are read back through L1-
+// bypassing loads after the barrier.
+constexpr uint32_t kSmallB = 1024;
+constexpr uint32_t kSmallPer = kBuildSmallLevel / kSmallB;
+
+__device__ __forceinline__ uint32_t load_agent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kSmallB) void k_place_small(
+    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ lvl, uint32_t d_end, uint32_t depth, uint32_t n_nodes,
+    uint32_t nbase, uint16_t topic, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ firstidx,
+    uint32_t* __restrict__ node_peer, uint16_t* __restrict__ node_topic, uint32_t* local,
+    uint32_t* __restrict__ node_parent, uint32_t* deg, uint32_t* __restrict__ first) {
+  __shared__ uint32_t off[kBuildSmallLevel];
+  __shared__ uint32_t wsum[kSmallB / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (tid == 0) {
+    const uint32_t peer = static_cast<uint32_t>(keys[0] & kPeerMask);
+    node_peer[nbase] = peer;
+    node_topic[nbase] = topic;
+    local[peer] = nbase;
+    node_parent[nbase] = kNoneP;
+    deg[nbase] = cnt[peer];
+  }
+  __threadfence_block();
+  __syncthreads();
+  for (uint32_t d = 1; d < d_end; ++d) {
+    const uint32_t plo = lvl[d - 1], lo = lvl[d];
+    const uint32_t hi = d == depth ? n_nodes : lvl[d + 1];
+    const uint32_t np = lo - plo;
+    // exclusive scan of the parents' fan-out: kSmallPer per thread, then waves
+    uint32_t v[kSmallPer];
+    uint32_t run = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPer; ++k) {
+      const uint32_t j = tid * kSmallPer + k;
+      v[k] = j < np ? load_agent(deg + nbase + plo + j) : 0u;
+      run += v[k];
+    }
+    uint32_t incl = run;
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) {
+      const uint32_t o = static_cast<uint32_t>(__shfl_up(static_cast<int>(incl), sh, 64));
+      if (lane >= static_cast<uint32_t>(sh)) incl += o;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t base = 0;
+    for (uint32_t q = 0; q < w; ++q) base += wsum[q];
+    uint32_t acc = base + incl - run;
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPer; ++k) {
+      const uint32_t j = tid * kSmallPer + k;
+      if (j < np) off[j] = acc;
+      acc += v[k];
+    }
+    __syncthreads();
+    for (uint32_t i = lo + tid; i < hi; i += kSmallB) {
+      const uint64_t kk = keys[i];
+      const uint32_t peer = static_cast<uint32_t>(kk & kPeerMask);
+      const uint32_t pp = static_cast<uint32_t>((kk >> kBuildPeerBits) & kPeerMask);
+      const uint32_t pu = load_agent(local + pp);
+      const uint32_t f = firstidx[pp];
+      const uint32_t node = nbase + lo + off[pu - nbase - plo] + (i - f);
+      node_peer[node] = peer;
+      node_topic[node] = topic;
+      local[peer] = node;
+      node_parent[node] = pu;
+      deg[node] = cnt[peer];
+      if (i == f) first[pu] = node;
+    }
+    __threadfence_block();
+    __syncthreads();
+  }
+}
+
 // out[i] = 1 iff peers[i] holds a node of the topic placed at [nbase, nbase +
 // n_nodes) by the last build (local[] may hold stale ids: node_peer confirms)
 __global__ __launch_bounds__(kB) void k_reach_query(const uint32_t* __restrict__ peers, uint32_t n,
@@ -269,6 +349,16 @@ hipError_t launch_place_root(const uint64_t* keys, uint32_t nbase, uint16_t topi
                              uint32_t* node_parent, uint32_t* deg, hipStream_t s) {
   hipLaunchKernelGGL(k_place_root, dim3(1), dim3(64), 0, s, keys, nbase, topic, cnt, node_peer, node_topic,
                      local, node_parent, deg);
+  return hipGetLastError();
+}
+
+hipError_t launch_place_small(const uint64_t* keys, const uint32_t* lvl, uint32_t d_end, uint32_t depth, uint32_t n_nodes,
+                              uint32_t nbase, uint16_t topic, const uint32_t* cnt, const uint32_t* firstidx,
+                              uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
+                              uint32_t* node_parent, uint32_t* deg, uint32_t* first, hipStream_t s) {
+  if (d_end > depth + 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_place_small, dim3(1), dim3(kSmallB), 0, s, keys, lvl, d_end, depth, n_nodes, nbase, topic, cnt,
+                     firstidx, node_peer, node_topic, local, node_parent, deg, first);
   return hipGetLastError();
 }
 

@@ -17,6 +17,7 @@ namespace psamd {
 
 constexpr uint32_t kBuildMaxDepth = 255;  // depth bits of the sort key
 constexpr uint32_t kBuildPeerBits = 28;   // peer / parent bits of the sort key
+constexpr uint32_t kBuildSmallLevel = 8192;  // levels placed by the one-block kernel
 
 // (peer, value) pairs scattered into a parent array
 hipError_t launch_scatter_pairs(const uint32_t* pairs, uint32_t n, uint32_t* par, hipStream_t s);
@@ -57,6 +58,13 @@ hipError_t launch_child_stats(const uint64_t* keys, uint32_t R, uint32_t* cnt, u
 hipError_t launch_place_root(const uint64_t* keys, uint32_t nbase, uint16_t topic, const uint32_t* cnt,
                              uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
                              uint32_t* node_parent, uint32_t* deg, hipStream_t s);
+// root and levels 1 .. d_end - 1 in one block; every one of those levels and
+// its parent level has at most kBuildSmallLevel nodes.  lvl: the topic's level
+// starts on the device (level d ends at lvl[d + 1], the last one at n_nodes).
+hipError_t launch_place_small(const uint64_t* keys, const uint32_t* lvl, uint32_t d_end, uint32_t depth, uint32_t n_nodes,
+                              uint32_t nbase, uint16_t topic, const uint32_t* cnt, const uint32_t* firstidx,
+                              uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
+                              uint32_t* node_parent, uint32_t* deg, uint32_t* first, hipStream_t s);
 hipError_t launch_place_level(const uint64_t* keys, uint32_t lo, uint32_t hi, uint32_t nbase, uint32_t prev0,
                               const uint32_t* childoff, const uint32_t* cnt, const uint32_t* firstidx,
                               uint16_t topic, uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,

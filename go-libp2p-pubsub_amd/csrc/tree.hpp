@@ -37,6 +37,10 @@ class SubscriptionTree {
   // peer's own entries, stage 1 (a few peers later) its child lists and its
   // parent's list, so close_client() finds them resident.
   void prefetch_leave(uint32_t peer, int stage) const;
+  void prefetch_peer(uint32_t peer) const {  // state and upstream (in_parent)
+    __builtin_prefetch(&state_[peer]);
+    __builtin_prefetch(&up_[peer]);
+  }
   int close_host(uint32_t peer);    // abrupt
   // Called once per message that floods this topic: lazy prune and repair of
   // failed writes at every node the message reached (rule Q3).  `reach`, if
