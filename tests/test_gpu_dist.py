@@ -164,3 +164,43 @@ def test_sharded_pipelined_batches():
     for e in engines:
         e.close()
     lb.close()
+
+
+def test_sharded_churn_batches():
+    """Joins and graceful leaves between batches on 2 ranks (host-built node
+    space on every rank): per-batch job totals and digests equal the single
+    engine's (GPU-built) on the same operation sequence."""
+    wl = WL.cfg5(6000, batches=4, per_batch=90)
+    plan = WL.churn_plan(wl, 4)
+
+    def drive(e, b):
+        leave, join = plan[b]
+        try:
+            e.leave(0, leave)
+        except PE.EngineError:
+            pass
+        e.join(0, join, check=False)
+        e.publish(np.zeros(wl.n_msgs))
+
+    one = PE.Engine(wl.n_peers, 1, seed=wl.seed)
+    WL.build_engine_topics(one, wl)
+    exp = []
+    for b in range(4):
+        drive(one, b)
+        exp.append((one.run().deliveries, one.seen_digest()))
+    one.close()
+    world = 2
+    lb = PE.Loopback(world)
+    engines = [PE.Engine(wl.n_peers, 1, seed=wl.seed) for _ in range(world)]
+    for r, e in enumerate(engines):
+        e.dist_init_loopback(lb, r, PE.PART_SUBTREE)
+        WL.build_engine_topics(e, wl)
+    for b in range(4):
+        for e in engines:
+            drive(e, b)
+        stats = run_ranks(engines)
+        got = (sum(s.deliveries for s in stats), sum(e.seen_digest() for e in engines) % (1 << 64))
+        assert got == exp[b], b
+    for e in engines:
+        e.close()
+    lb.close()
