@@ -189,6 +189,8 @@ struct ps_engine {
   std::vector<uint32_t> last_lo, last_cnt;  // topic -> last window's rank range
   std::vector<TopicDev> last_topics;
   bool have_window = false;
+  std::map<uint32_t, std::vector<uint32_t>> peer_node;  // topic -> peer -> node (ps_read_peer_messages)
+  std::vector<uint64_t> peer_node_epoch;                 // graph_epoch each map was built for
 
   // asynchronous runs (ps_run_async / ps_wait): the last window of a run may
   // leave its stats on the stream (pinned readback) so that the host plans
@@ -1104,7 +1106,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   HIP_TRY(e->d_arr1.ensure(wtot * 8), "alloc arrivals");
   bool any_mesh = false;
   for (uint32_t t = 0; t < nt; ++t) any_mesh |= (tab[t].W && (tab[t].flags & kTopicMesh));
-  if (record) HIP_TRY(e->d_hop.ensure(wtot * 64), "alloc hop record");
+  if (record) HIP_TRY(e->d_hop.ensure(wtot * 64 * 2), "alloc hop record");
   const uint32_t n_waves = e->expand_grid * (kBlock / 64);
   // staged + direct kernel counters side by side
   HIP_TRY(e->d_partials.ensure(static_cast<size_t>(2) * n_waves * kNumCtr * 8), "alloc partials");
@@ -1286,7 +1288,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     HIP_TRY(hipMemsetAsync(e->d_gen.p, static_cast<int>(e->gen_cur), e->d_gen.bytes, s),
             "stamp generations");
   }
-  if (record) HIP_TRY(hipMemsetAsync(e->d_hop.p, 0xFF, wtot * 64, s), "clear hop record");
+  if (record) HIP_TRY(hipMemsetAsync(e->d_hop.p, 0xFF, wtot * 64 * 2, s), "clear hop record");
   if (world > 1)
     HIP_TRY(hipMemsetAsync(e->d_apply_stats.p, 0, static_cast<size_t>(planned0 + 1) * kNumCtr * 8, s),
             "clear apply stats");
@@ -1306,7 +1308,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   a.blk_flag = e->d_blk.as<uint8_t>();
   a.dbg = 0;
   if (const char* v = std::getenv("PSAMD_DEBUG_EXPAND")) a.dbg = static_cast<uint32_t>(std::atoi(v));
-  a.hop_rec = record ? e->d_hop.as<uint8_t>() : nullptr;
+  a.hop_rec = record ? e->d_hop.as<uint16_t>() : nullptr;
   a.send = e->d_send.as<uint8_t>();
   uint64_t* const partials = e->d_partials.as<uint64_t>();
   uint64_t* arr[2] = {e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>()};
@@ -1561,9 +1563,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       int rcm = ensure_mirrors(e);
       if (rcm) return rcm;
     }
-    std::vector<uint8_t> hr(wtot * 64);
+    std::vector<uint16_t> hr(wtot * 64);
     if (!hr.empty()) {
-      HIP_TRY(hipMemcpyAsync(hr.data(), e->d_hop.p, hr.size(), hipMemcpyDeviceToHost, s), "read hops");
+      HIP_TRY(hipMemcpyAsync(hr.data(), e->d_hop.p, hr.size() * 2, hipMemcpyDeviceToHost, s), "read hops");
       HIP_TRY(hipStreamSynchronize(s), "sync");
     }
     const uint32_t np = e->cfg.n_peers;
@@ -1575,8 +1577,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         const uint32_t s0 = msgs[mi].start;
         uint8_t* row = e->hops.data() + static_cast<size_t>(mi) * np;
         for (uint32_t u = 0; u < d.n_nodes; ++u) {
-          const uint8_t v = hr[(d.wbase + static_cast<uint64_t>(u) * d.W + (li >> 6)) * 64 + (li & 63)];
-          if (v != 0xFF) row[e->node_peer[d.nbase + u]] = static_cast<uint8_t>(v - s0);
+          const uint16_t v = hr[(d.wbase + static_cast<uint64_t>(u) * d.W + (li >> 6)) * 64 + (li & 63)];
+          // hop = round - start round, saturated at 254 (0xFF: not delivered)
+          if (v != kHopRecNone) row[e->node_peer[d.nbase + u]] = static_cast<uint8_t>(std::min<uint32_t>(v - s0, 254u));
         }
       }
     }
@@ -2156,13 +2159,16 @@ int ps_read_peer_messages(ps_engine* e, uint32_t topic, uint32_t peer, uint32_t*
     int rcm = ensure_mirrors(e);
     if (rcm) return rcm;
   }
-  // the peer's node in this topic (the root is the publisher, not a recipient)
-  uint32_t u = kNone;
-  for (uint32_t k = 1; k < d.n_nodes; ++k)
-    if (e->node_peer[d.nbase + k] == peer) {
-      u = k;
-      break;
-    }
+  // the peer's node in this topic (the root is the publisher, not a recipient):
+  // a peer -> node map per topic, built once per node space
+  auto& pm = e->peer_node[topic];
+  if (e->peer_node_epoch.size() != e->topics.size()) e->peer_node_epoch.assign(e->topics.size(), ~0ull);
+  if (e->peer_node_epoch[topic] != e->graph_epoch) {
+    pm.assign(e->cfg.n_peers, kNone);
+    for (uint32_t k = 1; k < d.n_nodes; ++k) pm[e->node_peer[d.nbase + k]] = k;
+    e->peer_node_epoch[topic] = e->graph_epoch;
+  }
+  const uint32_t u = pm[peer];
   if (u == kNone) return PS_OK;  // not subscribed (or not owned by this rank)
   std::vector<uint64_t> row(d.W);
   uint8_t g = 0;

@@ -200,11 +200,11 @@ __device__ __forceinline__ uint64_t deliver_word(const ExpandArgs& a, bool mesh,
   k.dup += __popcll(m & old);
   k.deliv += __popcll(nm);
   if constexpr (kRecord) {
-    uint8_t* h = a.hop_rec + cw * 64;
+    uint16_t* h = a.hop_rec + cw * 64;
     uint64_t b = nm;
     while (b) {
       const int q = __ffsll(static_cast<long long>(b)) - 1;
-      h[q] = static_cast<uint8_t>(round);
+      h[q] = hop_round(round);
       b &= b - 1;
     }
   }
@@ -224,11 +224,11 @@ __device__ __forceinline__ void deliver_fresh(const ExpandArgs& a, bool internal
   }
   k.deliv += __popcll(m);
   if constexpr (kRecord) {
-    uint8_t* h = a.hop_rec + cw * 64;
+    uint16_t* h = a.hop_rec + cw * 64;
     uint64_t b = m;
     while (b) {
       const int q = __ffsll(static_cast<long long>(b)) - 1;
-      h[q] = static_cast<uint8_t>(round);
+      h[q] = hop_round(round);
       b &= b - 1;
     }
   }
@@ -247,11 +247,11 @@ __device__ __forceinline__ void deliver_fresh2(const ExpandArgs& a, bool interna
   k.deliv += __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
   if constexpr (kRecord) {
     for (int h = 0; h < 2; ++h) {
-      uint8_t* rec = a.hop_rec + (cw + h) * 64;
+      uint16_t* rec = a.hop_rec + (cw + h) * 64;
       uint64_t b = h ? (static_cast<uint64_t>(v.w) << 32 | v.z) : (static_cast<uint64_t>(v.y) << 32 | v.x);
       while (b) {
         const int q = __ffsll(static_cast<long long>(b)) - 1;
-        rec[q] = static_cast<uint8_t>(round);
+        rec[q] = hop_round(round);
         b &= b - 1;
       }
     }
@@ -731,12 +731,12 @@ __device__ __forceinline__ uint32_t popc4(uint4 v) {
 }
 
 template <bool kRecord>
-__device__ __forceinline__ void record_word(uint8_t* hop_rec, uint64_t cw, uint64_t m,
+__device__ __forceinline__ void record_word(uint16_t* hop_rec, uint64_t cw, uint64_t m,
                                             uint32_t round) {
-  uint8_t* h = hop_rec + cw * 64;
+  uint16_t* h = hop_rec + cw * 64;
   while (m) {
     const int q = __ffsll(static_cast<long long>(m)) - 1;
-    h[q] = static_cast<uint8_t>(round);
+    h[q] = hop_round(round);
     m &= m - 1;
   }
 }
@@ -1107,11 +1107,11 @@ __global__ __launch_bounds__(kBlock) void k_apply(ApplyArgs a, uint32_t round) {
         a.blk_flag[it.node >> kFlagBlockShift] = 1;
       }
       if constexpr (kRecord) {
-        uint8_t* h = a.hop_rec + cw * 64;
+        uint16_t* h = a.hop_rec + cw * 64;
         uint64_t b = nm;
         while (b) {
           const int q = __ffsll(static_cast<long long>(b)) - 1;
-          h[q] = static_cast<uint8_t>(round);
+          h[q] = hop_round(round);
           b &= b - 1;
         }
       }

@@ -49,6 +49,13 @@ constexpr uint32_t kEntrySplit = 0x100;  // per-entry flag bit next to TopicDev.
 // nbase + n_nodes) owns the 64-message words [wbase + (u-nbase)*W, +W) of the
 // seen bitset and of the two arrival buffers.  Tree topics are numbered in
 // BFS order, so the children of a node are consecutive node ids.
+// Hop record (parity mode): the delivery round of every (node, message) as
+// u16, so paths deeper than 254 hops stay exact up to the host's saturation.
+constexpr uint16_t kHopRecNone = 0xFFFF;
+__host__ __device__ inline uint16_t hop_round(uint32_t round) {
+  return static_cast<uint16_t>(round < 0xFFFEu ? round : 0xFFFEu);
+}
+
 struct TopicDev {
   uint64_t wbase;    // first word of the topic's mask block
   uint32_t w_msgs;   // message words in use (W may carry one pad word)
@@ -98,7 +105,7 @@ struct ExpandArgs {
   uint8_t* next_flag;
   uint8_t* blk_flag;  // one byte per kFlagsPerBlock nodes: some flag set
   uint64_t* partials;  // [n_waves][kNumCtr]
-  uint8_t* hop_rec;    // [word*64 + bit] = round, record mode only
+  uint16_t* hop_rec;   // [word*64 + bit] = round (kHopRecNone: none), record mode only
   uint32_t gen_cur;
   uint32_t dbg;  // experiment knobs (kDbg*), 0 in production
   uint8_t* send;                  // send regions of this round (multi-GPU)
@@ -126,7 +133,7 @@ struct PullArgs {
   const uint64_t* a_cur;  // arrivals of round-1 (topic roots' seeded rows)
   uint64_t* seen;
   uint8_t* gen;
-  uint8_t* hop_rec;
+  uint16_t* hop_rec;
   uint64_t* partials;  // [n_blocks][kNumCtr]
   uint64_t* scratch;   // 1024 x 1 KiB: stores of lanes past a run's end
   uint32_t gen_cur;
@@ -145,7 +152,7 @@ struct ApplyArgs {
   uint64_t* a_next;
   uint8_t* next_flag;
   uint8_t* blk_flag;
-  uint8_t* hop_rec;
+  uint16_t* hop_rec;
   uint64_t* stats;  // [kNumCtr] of this round (deliveries, duplicates)
   uint8_t* gen;     // level mode: stamp a node reached (null: compaction mode)
   uint32_t gen_cur;

@@ -158,7 +158,7 @@ int ps_wait(ps_engine* e, ps_stats* out);
 
 /* ---- results of the last ps_run (client.Messages, client.go:26-28) --------
  * ps_read_hops: hop of message `msg` at every peer (PS_HOP_NONE = not
- *               delivered); needs PS_F_RECORD_HOPS.
+ *               delivered; hops beyond 254 read as 254); needs PS_F_RECORD_HOPS.
  * ps_read_delivered: 1 where `msg` was delivered (seen bit set), any mode,
  *               for messages of the last window of the last run.            */
 int ps_read_hops(ps_engine* e, uint32_t msg, uint8_t* hop_per_peer);

@@ -130,3 +130,27 @@ def test_abi_error_behaviour():
             e.publish(np.array([0]))
         with pytest.raises(PE.EngineError):
             e.hops(0)  # no hop record on this engine
+
+
+@pytest.mark.parametrize("staggered", [False, True])
+def test_deep_chain_beyond_255_hops(staggered):
+    """A 700-deep chain: more rounds than a hop byte holds.  Deliveries are
+    exact; hops read back saturated at 254, as the restatement reports them;
+    the host build takes over from the GPU rebuild (depth > 254)."""
+    n = 700
+    parent = np.full(n, O.NONE, dtype=np.uint32)
+    parent[1:] = np.arange(n - 1)
+    live = np.ones(n, dtype=np.uint8)
+    k = 70
+    starts = np.arange(k) % 3 if staggered else None
+    with PE.Engine(n, 1, record_hops=True) as e:
+        e.set_tree(0, 0, parent)
+        first = e.publish(np.zeros(k), starts)
+        st = e.run()
+        assert st.deliveries == k * (n - 1)
+        rp, cl = O.parents_to_csr(parent)
+        _, hops, _ = O.disseminate(rp, cl, 0, live, 1)
+        assert hops[0][300] == 254 and hops[0][200] == 200
+        for m in (0, 1, k - 1):
+            assert np.array_equal(e.hops(first + m), hops[0]), m
+        assert e.depth(0) == (n - 1, n)

@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""Randomised differential run of the HIP path against the CPU restatement
+(oracle/psoracle.c), wider than the pytest suite: random trees and meshes,
+live masks, staggered or single start rounds, several topics, small windows
+(many windows per run), record / no-record, eager / lazy seen, pipelined runs,
+and churn sequences on restated join trees.  Every case is bit-exact or the
+script reports it (seed and case) and exits non-zero.
+
+    python tools/fuzz_gpu.py [--cases 300] [--seed 0] [--max-peers 4000]
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "go-libp2p-pubsub_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+
+import oracle as O  # noqa: E402
+import psengine as PE  # noqa: E402
+
+
+def random_tree(rng, n, root):
+    perm = rng.permutation(n)
+    perm = np.concatenate([[root], perm[perm != root]])
+    parent = np.full(n, O.NONE, dtype=np.uint32)
+    shape = rng.integers(0, 3)
+    for i in range(1, n):
+        if shape == 0:  # random recursive tree
+            j = rng.integers(0, i)
+        elif shape == 1:  # deep: mostly the previous few
+            j = max(0, i - 1 - int(rng.integers(0, 3)))
+        else:  # wide: bounded fan-out levels
+            j = (i - 1) // int(rng.integers(2, 9))
+        parent[perm[i]] = perm[j]
+    return parent
+
+
+def random_mesh(rng, n, max_out):
+    deg = rng.integers(0, max_out + 1, size=n)
+    row_ptr = np.zeros(n + 1, dtype=np.uint32)
+    np.cumsum(deg, out=row_ptr[1:])
+    col = rng.integers(0, n, size=int(row_ptr[-1])).astype(np.uint32)
+    return row_ptr, col
+
+
+def case_topology(rng, max_peers):
+    n = int(rng.integers(2, max_peers))
+    n_topics = int(rng.integers(1, 5))
+    live = (rng.random(n) > rng.choice([0.0, 0.05, 0.3])).astype(np.uint8)
+    n_msgs = int(rng.integers(1, 700))
+    staggered = rng.random() < 0.4
+    starts = rng.integers(0, 5, size=n_msgs) if staggered else None
+    topics = rng.integers(0, n_topics, size=n_msgs)
+    window = int(rng.choice([64, 200, 65536]))
+    flags = PE.F_NO_LAZY_SEEN if rng.random() < 0.2 else 0
+    record = True
+    pipelined = rng.random() < 0.3
+    with PE.Engine(n, n_topics, record_hops=record, msg_window=window, flags=flags) as e:
+        graphs = []
+        for t in range(n_topics):
+            root = int(rng.integers(0, n))
+            if rng.random() < 0.25:
+                rp, cl = random_mesh(rng, n, int(rng.integers(1, 5)))
+                e.set_children(t, root, rp, cl)
+            else:
+                par = random_tree(rng, n, root)
+                e.set_tree(t, root, par)
+                rp, cl = O.parents_to_csr(par)
+            graphs.append((rp, cl, root))
+        e.set_live(live)
+        first = e.publish(topics, starts)
+        if pipelined:
+            e.run_async()
+            st = e.wait()
+        else:
+            st = e.run()
+        total = 0
+        for t, (rp, cl, root) in enumerate(graphs):
+            idx = np.nonzero(topics == t)[0]
+            if not len(idx):
+                continue
+            # the oracle floods each message from its start round; hops are
+            # relative to it, so one call per distinct start suffices
+            tot, hops, _ = O.disseminate(rp, cl, root, live, 1)
+            total += tot * len(idx)
+            for m in idx[: 40]:
+                got = e.hops(first + int(m))
+                if not np.array_equal(got, hops[0]):
+                    bad = np.nonzero(got != hops[0])[0][:8]
+                    return f"topic {t} msg {m}: peers {bad} engine {got[bad]} oracle {hops[0][bad]}"
+        if st.deliveries != total:
+            return f"deliveries {st.deliveries} != oracle {total}"
+    return None
+
+
+def case_churn(rng, max_peers):
+    n = int(rng.integers(20, max_peers))
+    seed = int(rng.integers(1, 1 << 30))
+    w, mw = int(rng.integers(1, 5)), int(rng.integers(5, 9))
+    with PE.Engine(n, 1, record_hops=True, seed=seed) as e:
+        ot = O.Tree(n, 0, w, mw, PE.Engine.topic_seed(seed, 0))
+        e.topic_create(0, 0, w, mw)
+        members = set()
+        for step in range(12):
+            op = rng.random()
+            if op < 0.5 or not members:
+                outs = [p for p in range(1, n) if p not in members]
+                if outs:
+                    peers = rng.choice(outs, size=min(len(outs), int(rng.integers(1, 30))), replace=False)
+                    st = e.join(0, peers, check=False)
+                    for p, s in zip(peers, st):
+                        if ot.join(int(p)) != s:
+                            return f"join status differs at step {step} peer {p}"
+                        if s == 0:
+                            members.add(int(p))
+            elif op < 0.8:
+                peers = rng.choice(sorted(members), size=min(len(members), int(rng.integers(1, 10))), replace=False)
+                try:
+                    e.leave(0, peers)
+                except PE.EngineError:
+                    pass
+                for p in peers:
+                    ot.leave(int(p))
+                    members.discard(int(p))
+            else:
+                p = int(rng.choice(sorted(members)))
+                try:
+                    e.drop(0, [p])
+                except PE.EngineError:
+                    pass
+                ot.drop(p)
+                members.discard(p)
+            k = int(rng.integers(1, 4))
+            first = e.publish(np.zeros(k))
+            e.run()
+            for m in range(k):
+                exp = ot.message()
+                got = e.hops(first + m)
+                if not np.array_equal(got, exp):
+                    bad = np.nonzero(got != exp)[0][:8]
+                    return f"churn step {step} msg {m}: peers {bad} engine {got[bad]} oracle {exp[bad]}"
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", type=int, default=300)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--max-peers", type=int, default=4000)
+    args = ap.parse_args()
+    fails = 0
+    t0 = time.time()
+    for c in range(args.cases):
+        rng = np.random.default_rng([args.seed, c])
+        kind = "churn" if c % 4 == 3 else "topology"
+        try:
+            err = (case_churn if kind == "churn" else case_topology)(rng, args.max_peers)
+        except PE.EngineError as ex:
+            err = f"engine error: {ex}"
+        if err:
+            fails += 1
+            print(f"FAIL case {c} ({kind}, seed {args.seed}): {err}", flush=True)
+        if c % 25 == 0:
+            print(f"[fuzz] {c + 1}/{args.cases} cases, {fails} failures, {time.time() - t0:.0f} s", flush=True)
+    print(f"[fuzz] done: {args.cases} cases, {fails} failures, {time.time() - t0:.0f} s", flush=True)
+    return 1 if fails else 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
