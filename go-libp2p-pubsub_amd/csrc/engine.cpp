@@ -25,7 +25,7 @@ using namespace psamd;
 
 namespace {
 
-constexpr uint32_t kMaxRoundsCap = 4096;
+constexpr uint32_t kMaxRoundsCap = 4096;  // round buffers' minimum size (deeper windows grow them)
 constexpr uint32_t kMaxStartRound = 200;
 constexpr uint32_t kDefaultWindow = 65536;
 
@@ -1110,8 +1110,16 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   const uint32_t n_waves = e->expand_grid * (kBlock / 64);
   // staged + direct kernel counters side by side
   HIP_TRY(e->d_partials.ensure(static_cast<size_t>(2) * n_waves * kNumCtr * 8), "alloc partials");
-  HIP_TRY(e->d_stats.ensure(static_cast<size_t>(kMaxRoundsCap + 1) * kNumCtr * 8), "alloc stats");
-  HIP_TRY(e->d_apply_stats.ensure(static_cast<size_t>(kMaxRoundsCap + 1) * kNumCtr * 8),
+  // no simple path is longer than a topic's peers: a window ends within
+  // n_peers + the latest start round (chains of any depth run to the end; the
+  // bound is the same on every rank)
+  const uint32_t round_cap = static_cast<uint32_t>(
+      std::max<uint64_t>(kMaxRoundsCap, static_cast<uint64_t>(e->cfg.n_peers) + max_start + 2));
+  // per-round counter rows: the planned rounds plus slack, grown (content kept)
+  // if a mesh path outlives them
+  uint32_t stats_rows = std::min<uint32_t>(round_cap, std::max<uint32_t>(kMaxRoundsCap, max_depth + max_start + 32));
+  HIP_TRY(e->d_stats.ensure(static_cast<size_t>(stats_rows + 1) * kNumCtr * 8), "alloc stats");
+  HIP_TRY(e->d_apply_stats.ensure(static_cast<size_t>(stats_rows + 1) * kNumCtr * 8),
           "alloc apply stats");
   HIP_TRY(e->d_topics.ensure(tab.size() * sizeof(TopicDev)), "alloc topics");
   HIP_TRY(e->d_nfront.ensure(4), "alloc n_front");
@@ -1179,7 +1187,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // single-start tree
   // (pull: any rank count and fan-out; the push kernel's level schedule needs
   // the staged path: one rank, fan-out <= 64)
-  bool level = !any_mesh && !e->no_level && planned0 + 1 < kMaxRoundsCap;
+  bool level = !any_mesh && !e->no_level && planned0 + 1 < round_cap;
   for (uint32_t t = 0; t < nt && level; ++t)
     if (tab[t].W && !(tab[t].flags & kTopicSingleStart)) level = false;
   if (level && e->level_push && need_direct) level = false;
@@ -1461,7 +1469,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   HIP_TRY(seed_round(0, arr[0]), "seed");
   HIP_TRY(compact(0, 0), "compact");
   while (true) {
-    for (; r < planned && r < kMaxRoundsCap; ) {
+    for (; r < planned && r < round_cap; ) {
       ++r;
       a.a_cur = arr[(r - 1) & 1];
       a.a_next = arr[r & 1];
@@ -1491,12 +1499,25 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     uint32_t left = 0;
     HIP_TRY(hipMemcpyAsync(&left, e->d_nfront.p, 4, hipMemcpyDeviceToHost, s), "read frontier");
     HIP_TRY(hipStreamSynchronize(s), "sync");
-    if (left == 0 || r >= kMaxRoundsCap) {
+    if (left == 0 || r >= round_cap) {
       if (left) return e->fail(PS_E_STATE, "propagation did not converge");
       break;
     }
     if (world > 1) return e->fail(PS_E_STATE, "multi-GPU frontier outlived the planned rounds");
     planned = r + 8;  // live mask lengthened a mesh path beyond the BFS depth
+    if (planned + 1 > stats_rows) {  // grow the round rows, keeping the counted ones
+      const uint32_t rows = std::min<uint32_t>(round_cap, std::max(planned + 1, 2 * stats_rows));
+      DevBuf grown;
+      HIP_TRY(grown.ensure(static_cast<size_t>(rows + 1) * kNumCtr * 8), "grow stats");
+      HIP_TRY(hipMemcpyAsync(grown.p, e->d_stats.p, static_cast<size_t>(stats_rows + 1) * kNumCtr * 8,
+                             hipMemcpyDeviceToDevice, s),
+              "keep stats");
+      HIP_TRY(hipStreamSynchronize(s), "sync");
+      std::swap(grown.p, e->d_stats.p);
+      std::swap(grown.bytes, e->d_stats.bytes);
+      stats = e->d_stats.as<uint64_t>();
+      stats_rows = rows;
+    }
   }
   }
   HIP_TRY(hipEventRecord(e->ev_run1, s), "event");

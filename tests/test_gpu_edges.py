@@ -132,12 +132,13 @@ def test_abi_error_behaviour():
             e.hops(0)  # no hop record on this engine
 
 
+@pytest.mark.parametrize("n", [700, 5000])
 @pytest.mark.parametrize("staggered", [False, True])
-def test_deep_chain_beyond_255_hops(staggered):
-    """A 700-deep chain: more rounds than a hop byte holds.  Deliveries are
-    exact; hops read back saturated at 254, as the restatement reports them;
-    the host build takes over from the GPU rebuild (depth > 254)."""
-    n = 700
+def test_deep_chain_beyond_255_hops(staggered, n):
+    """Chains 700 and 5000 deep: more rounds than a hop byte holds and than
+    the 4096 preallocated round rows.  Deliveries are exact; hops read back
+    saturated at 254, as the restatement reports them; the host build takes
+    over from the GPU rebuild (depth > 254)."""
     parent = np.full(n, O.NONE, dtype=np.uint32)
     parent[1:] = np.arange(n - 1)
     live = np.ones(n, dtype=np.uint8)
