@@ -2,8 +2,9 @@
 """Randomised differential run of the HIP path against the CPU restatement
 (oracle/psoracle.c), wider than the pytest suite: random trees and meshes,
 live masks, staggered or single start rounds, several topics, small windows
-(many windows per run), record / no-record, eager / lazy seen, pipelined runs,
-and churn sequences on restated join trees.  Every case is bit-exact or the
+(many windows per run), eager / lazy seen, pipelined runs, churn sequences
+on restated join trees, 2-4 ranks on the loopback transport, and
+per-subscriber drains.  Every case is bit-exact or the
 script reports it (seed and case) and exits non-zero.
 
     python tools/fuzz_gpu.py [--cases 300] [--seed 0] [--max-peers 4000]
@@ -146,6 +147,98 @@ def case_churn(rng, max_peers):
     return None
 
 
+def case_dist(rng, max_peers):
+    """world 2-4 engines on the loopback transport (one thread each), random
+    trees, live masks, single or staggered starts, either partition: the
+    union of the ranks' hops equals the oracle's."""
+    import threading
+    world = int(rng.integers(2, 5))
+    n = int(rng.integers(world + 2, max(world + 3, max_peers // 2)))
+    n_topics = int(rng.integers(1, 4))
+    part = int(rng.integers(0, 2))
+    live = (rng.random(n) > rng.choice([0.0, 0.1])).astype(np.uint8)
+    n_msgs = int(rng.integers(1, 300))
+    starts = rng.integers(0, 4, size=n_msgs) if rng.random() < 0.4 else None
+    topics = rng.integers(0, n_topics, size=n_msgs)
+    trees = []
+    for _ in range(n_topics):
+        root = int(rng.integers(0, n))
+        trees.append((random_tree(rng, n, root), root))
+    lb = PE.Loopback(world)
+    engines = [PE.Engine(n, n_topics, record_hops=True) for _ in range(world)]
+    try:
+        for r, e in enumerate(engines):
+            e.dist_init_loopback(lb, r, part)
+            for t, (par, root) in enumerate(trees):
+                e.set_tree(t, root, par)
+            e.set_live(live)
+        firsts = [e.publish(topics, starts) for e in engines]
+        stats, errs = [None] * world, []
+
+        def go(r):
+            try:
+                stats[r] = engines[r].run()
+            except Exception as ex:  # noqa: BLE001
+                errs.append(ex)
+
+        th = [threading.Thread(target=go, args=(r,)) for r in range(world)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(timeout=120)
+        if any(x.is_alive() for x in th):
+            return "rank thread hung"
+        if errs:
+            return f"rank error: {errs[0]}"
+        total = 0
+        for t, (par, root) in enumerate(trees):
+            idx = np.nonzero(topics == t)[0]
+            if not len(idx):
+                continue
+            rp, cl = O.parents_to_csr(par)
+            tot, hops, _ = O.disseminate(rp, cl, root, live, 1)
+            total += tot * len(idx)
+            for m in idx[:20]:
+                got = np.stack([e.hops(firsts[0] + int(m)) for e in engines]).min(axis=0)
+                if not np.array_equal(got, hops[0]):
+                    bad = np.nonzero(got != hops[0])[0][:8]
+                    return f"world {world} part {part} topic {t} msg {m}: peers {bad} {got[bad]} vs {hops[0][bad]}"
+        if sum(st.deliveries for st in stats) != total:
+            return f"world {world}: deliveries {sum(st.deliveries for st in stats)} != {total}"
+    finally:
+        for e in engines:
+            e.close()
+        lb.close()
+    return None
+
+
+def case_drain(rng, max_peers):
+    """ps_read_peer_messages against the hops: a peer's drain is exactly the
+    messages that reached it, ordered by (start round, publish order)."""
+    n = int(rng.integers(2, max_peers))
+    n_topics = int(rng.integers(1, 4))
+    live = (rng.random(n) > 0.1).astype(np.uint8)
+    n_msgs = int(rng.integers(1, 400))
+    starts = rng.integers(0, 6, size=n_msgs) if rng.random() < 0.5 else np.zeros(n_msgs, dtype=np.int64)
+    topics = rng.integers(0, n_topics, size=n_msgs)
+    with PE.Engine(n, n_topics, record_hops=True) as e:
+        for t in range(n_topics):
+            root = int(rng.integers(0, n))
+            e.set_tree(t, root, random_tree(rng, n, root))
+        e.set_live(live)
+        first = e.publish(topics, starts)
+        e.run()
+        hops = np.stack([e.hops(first + m) for m in range(n_msgs)])  # [msg][peer]
+        for p in rng.choice(n, size=min(n, 12), replace=False):
+            for t in range(n_topics):
+                ids = [m for m in range(n_msgs) if topics[m] == t and hops[m, p] != 0xFF]
+                exp = [first + m for m in sorted(ids, key=lambda m: (int(starts[m]), m))]
+                got = e.peer_messages(t, int(p)).tolist()
+                if got != exp:
+                    return f"peer {p} topic {t}: drain {got[:6]}... != {exp[:6]}..."
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", type=int, default=300)
@@ -156,9 +249,10 @@ def main():
     t0 = time.time()
     for c in range(args.cases):
         rng = np.random.default_rng([args.seed, c])
-        kind = "churn" if c % 4 == 3 else "topology"
+        kind = ("topology", "churn", "dist", "topology", "drain")[c % 5]
+        fn = {"topology": case_topology, "churn": case_churn, "dist": case_dist, "drain": case_drain}[kind]
         try:
-            err = (case_churn if kind == "churn" else case_topology)(rng, args.max_peers)
+            err = fn(rng, args.max_peers)
         except PE.EngineError as ex:
             err = f"engine error: {ex}"
         if err:
