@@ -274,9 +274,10 @@ void peer_children(const ps_engine* e, const TopicHost& T, std::vector<uint32_t>
 // Ownership of one topic's nodes (positions in its BFS order) among `world`
 // ranks.  PS_PART_PEER: owner = splitmix64(peer) mod world.
 // PS_PART_SUBTREE: nodes at BFS level >= L belong to the owner of their
-// ancestor at level L, hashed as splitmix64(topic<<32 | ancestor peer); the
-// few nodes above L hash by peer.  L = split_depth, or (0) the first level
-// holding >= 64*world nodes, so only edges out of levels < L cross ranks.
+// ancestor at level L; the level-L subtrees are dealt largest first to the
+// least-loaded rank; the few nodes above L hash by peer.  L = split_depth, or
+// (0) the first level holding >= 64*world nodes, so only edges out of levels
+// < L cross ranks.
 void partition_topic(const std::vector<uint32_t>& order, const std::vector<uint32_t>& bfs_parent,
                      const std::vector<uint32_t>& level, uint32_t topic, int32_t world,
                      uint32_t part, uint32_t split_depth, std::vector<int32_t>& owner) {
@@ -304,15 +305,38 @@ void partition_topic(const std::vector<uint32_t>& order, const std::vector<uint3
       }
   }
   std::vector<uint32_t> anc(n, kNone);
+  const bool subtree = part == PS_PART_SUBTREE && L > 0;
+  // subtree mode: the level-L subtrees go to ranks largest first, each to the
+  // least-loaded rank (LPT), so every rank holds the same share of this
+  // topic's nodes whatever the topic's message weight (hashing the subtree
+  // roots left 14 % imbalance at 8 ranks on cfg3)
+  std::vector<uint64_t> size(subtree ? n : 0, 0);
   for (size_t u = 0; u < n; ++u) {
-    if (part == PS_PART_SUBTREE && level[u] >= L && L > 0) {
+    if (subtree && level[u] >= L) {
       anc[u] = level[u] == L ? static_cast<uint32_t>(u) : anc[bfs_parent[u]];
-      owner[u] = static_cast<int32_t>(mix((static_cast<uint64_t>(topic) << 32) | order[anc[u]]) %
-                                      static_cast<uint64_t>(world));
+      size[anc[u]]++;
     } else {
       owner[u] = static_cast<int32_t>(mix(order[u]) % static_cast<uint64_t>(world));
     }
   }
+  if (!subtree) return;
+  std::vector<uint32_t> roots;
+  for (size_t u = 0; u < n; ++u)
+    if (level[u] == L) roots.push_back(static_cast<uint32_t>(u));
+  std::sort(roots.begin(), roots.end(), [&](uint32_t a, uint32_t b) {
+    return size[a] != size[b] ? size[a] > size[b] : order[a] < order[b];
+  });
+  std::vector<uint64_t> load(world, 0);
+  for (uint32_t u : roots) {
+    int32_t best = 0;
+    for (int32_t q = 1; q < world; ++q)
+      if (load[q] < load[best]) best = q;
+    owner[u] = best;
+    load[best] += size[u];
+  }
+  (void)topic;
+  for (size_t u = 0; u < n; ++u)
+    if (level[u] > L) owner[u] = owner[anc[u]];
 }
 
 // Builds this rank's node space: per topic, the owned nodes among those

@@ -185,8 +185,9 @@ int ps_seen_digest(ps_engine* e, uint64_t* digest_out);
  * the owned nodes; sums over ranks give the job totals.
  *   PS_PART_PEER     owner(p) = splitmix64(p) mod world
  *   PS_PART_SUBTREE  a node below the split level belongs to the owner of its
- *                    ancestor at that level (hash of topic and that peer), so
- *                    only edges out of the top levels cross GPUs. */
+ *                    ancestor at that level (the subtrees dealt largest first
+ *                    to the least-loaded rank), so only edges out of the top
+ *                    levels cross GPUs. */
 #define PS_PART_PEER 0u
 #define PS_PART_SUBTREE 1u
 #define PS_UNIQUE_ID_BYTES 128

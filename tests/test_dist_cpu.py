@@ -60,7 +60,8 @@ def test_subtree_partition_keeps_subtrees_whole(oracle_lib):
         cross = [(p, c) for p in range(n) for c in cl[rp[p]:rp[p + 1]] if own[p] != own[c]]
         assert all(d[p] < L for p, _ in cross)  # only top-level edges cross ranks
         share = np.bincount(own, minlength=world) / n
-        assert share.min() > 0.5 / world  # hash over >= 64*world subtrees: balanced
+        # >= 64*world subtrees dealt largest first to the least-loaded rank
+        assert share.min() > 0.9 / world and share.max() < 1.1 / world, share
 
 
 def _free_port():
