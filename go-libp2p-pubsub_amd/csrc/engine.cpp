@@ -131,6 +131,8 @@ struct ps_engine {
   std::chrono::steady_clock::time_point t_run0;
   bool level_push = false;       // PSAMD_LEVEL_PUSH=1: level mode with the push kernel (A/B)
   uint32_t pull_words = kPullWords;  // words per pull chunk (PSAMD_PULL_WORDS)
+  uint64_t pull_top_max = 32ull << 20;  // top launch: leading rounds writing <= this many row bytes each (PSAMD_PULL_TOP_MB, 0 = off)
+  uint32_t pull_top_first = 0, pull_top_last = 0;  // rounds of the cached top launch (0: none)
   uint32_t pull_unroll = 8;          // loads in flight per lane (PSAMD_PULL_UNROLL: 4 or 8)
 
   std::vector<TopicHost> topics;
@@ -209,6 +211,22 @@ struct ps_engine {
   };
   Inflight infl[2];
   uint32_t infl_head = 0, infl_count = 0;
+
+  // per-window uploads (topic table, seeds, reduce descriptors) go through
+  // pinned staging: a copy from pageable memory blocks the host until the
+  // stream has drained, so the next batch's launches would only be issued
+  // once the previous batch had finished (a ~35 us bubble per pipelined
+  // step).  Two slots alternate; a slot is rewritten only after the copies
+  // of its previous use have completed (event).
+  struct Staging {
+    uint8_t* h = nullptr;
+    uint8_t* d = nullptr;  // the slot's device-mapped address
+    size_t cap = 0;
+    hipEvent_t used = nullptr;
+    bool pending = false;
+  };
+  Staging stg[2];
+  uint32_t stg_next = 0;
   bool defer_phase = false;  // the current phase may defer its last window's stats
   bool defer_last = false;   // ... and this window is that last window
   Inflight* defer_into = nullptr;
@@ -789,6 +807,9 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
 }
 
 int upload_graph(ps_engine* e) {
+  // nothing changed: no uploads, and no stream sync (a pipelined run must not
+  // wait here for the previous run's kernels)
+  if (!e->graph_dirty && !e->flags_dirty) return PS_OK;
   if (e->graph_dirty) {
     bool built = false;
     if (can_gpu_build(e)) {
@@ -940,9 +961,10 @@ int build_schedule(ps_engine* e, const std::vector<TopicDev>& tab,
 // parents), cut into chunks of at most kPullMaxKids nodes and about
 // kPullWords words, one wave each.  Cached like the schedule.
 int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
-                      const std::vector<uint32_t>& tstart, uint32_t rounds, bool* fuse) {
+                      const std::vector<uint32_t>& tstart, uint32_t rounds, bool* fuse, bool top_ok) {
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
-  std::vector<uint64_t> key{e->graph_epoch, e->flags_epoch, rounds, e->pull_words, *fuse ? 1ull : 0ull};
+  std::vector<uint64_t> key{e->graph_epoch, e->flags_epoch, rounds, e->pull_words, *fuse ? 1ull : 0ull,
+                            top_ok ? e->pull_top_max : 0ull};
   for (uint32_t t = 0; t < nt; ++t) {
     key.push_back(tab[t].W ? tstart[t] : ~0ull);
     key.push_back(tab[t].W);
@@ -958,6 +980,33 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
   if (gpu) *fuse = false;
   auto& C = e->pull_host;
   auto& off = e->pull_off;
+  // top launch: the leading rounds (from the common start) that each write at
+  // most pull_top_max row bytes go into one k_pull_top launch
+  e->pull_top_first = e->pull_top_last = 0;
+  if (top_ok && !*fuse && e->pull_top_max) {
+    uint32_t s0 = ~0u;
+    for (uint32_t t = 0; t < nt; ++t)
+      if (tab[t].W) s0 = std::min(s0, tstart[t]);
+    std::vector<uint64_t> rb(rounds + 2, 0);
+    for (uint32_t t = 0; t < nt; ++t) {
+      if (!tab[t].W) continue;
+      const TopicHost& T = e->topics[t];
+      for (uint32_t q = tstart[t] + 1; q <= rounds; ++q) {
+        const uint32_t d = q - tstart[t];
+        if (d + 1 >= T.level_off.size()) break;
+        rb[q] += static_cast<uint64_t>(T.level_off[d + 1] - T.level_off[d]) * tab[t].W * 8;
+      }
+    }
+    uint32_t last = 0;
+    for (uint32_t q = s0 + 1; s0 != ~0u && q <= rounds && q <= s0 + kPullTopLevels && rb[q] &&
+                            rb[q] <= e->pull_top_max;
+         ++q)
+      last = q;
+    if (last > s0 + 1) {
+      e->pull_top_first = s0 + 1;
+      e->pull_top_last = last;
+    }
+  }
   auto build = [&](bool fused) -> bool {
     C.clear();
     off.assign(rounds + 2, 0);
@@ -965,6 +1014,10 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
     e->split_host.clear();
     e->split_off.assign(rounds + 2, 0);
     for (uint32_t q = 1; q <= rounds; ++q) {
+      // top launch: every round's chunks fill whole blocks (one partial slot
+      // per block and round)
+      if (q > e->pull_top_first && q <= e->pull_top_last + 1)
+        while (C.size() % (kBlock / 64)) C.push_back(PullChunk{0, 0, 0, 0, 0, kNone, kNone, q - 1});
       off[q] = static_cast<uint32_t>(C.size());
       e->split_off[q] = static_cast<uint32_t>(e->split_host.size());
       for (uint32_t t = 0; t < nt; ++t) {
@@ -986,7 +1039,7 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
           for (uint32_t u = lo; u < hi; u += per)
             C.push_back(PullChunk{T.nbase + u, T.nbase + std::min(u + per, hi), 0, 0, t,
                                   gpu ? kNone : e->node_parent[T.nbase + u],
-                                  gpu ? kNone : e->node_parent[T.nbase + std::min(u + per, hi) - 1], 0});
+                                  gpu ? kNone : e->node_parent[T.nbase + std::min(u + per, hi) - 1], q});
           continue;
         }
         // fused: a run of level-d nodes plus their children (consecutive ids:
@@ -1074,6 +1127,58 @@ void accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uin
 
 // Propagates one window: per topic t, win[t] lists the messages (indices into
 // `msgs`) whose bits form t's block of W_t = ceil(|win[t]|/64) words.
+// Host -> device copies of one window through a pinned staging slot
+// (ps_engine::Staging): asynchronous for the host, stream-ordered.
+struct Upload {
+  void* dst;
+  const void* src;
+  size_t bytes;
+};
+int stage_uploads(ps_engine* e, const Upload* ups, size_t n, hipStream_t s) {
+  size_t need = 0;
+  for (size_t i = 0; i < n; ++i) need += (ups[i].bytes + 255) & ~size_t(255);
+  if (need == 0) return PS_OK;
+  ps_engine::Staging& g = e->stg[e->stg_next];
+  e->stg_next ^= 1u;
+  if (g.pending) HIP_TRY(hipEventSynchronize(g.used), "sync staging");
+  g.pending = false;
+  if (need > g.cap) {
+    if (g.h) HIP_TRY(hipHostFree(g.h), "free staging");
+    g.h = nullptr;
+    g.cap = 0;
+    const size_t cap = std::max<size_t>(need, 64 << 10);
+    void* h = nullptr;
+    HIP_TRY(hipHostMalloc(&h, cap, hipHostMallocMapped), "alloc staging");
+    g.h = static_cast<uint8_t*>(h);
+    g.cap = cap;
+    void* d = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&d, h, 0), "map staging");
+    g.d = static_cast<uint8_t*>(d);
+  }
+  // one copy kernel for up to kStageMax arrays of whole u32 words; blits
+  // otherwise
+  bool kernel = n <= kStageMax;
+  for (size_t i = 0; i < n; ++i) kernel = kernel && ups[i].bytes % 4 == 0;
+  StageCopy c{};
+  size_t off = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (!ups[i].bytes) continue;
+    std::memcpy(g.h + off, ups[i].src, ups[i].bytes);
+    if (kernel) {
+      c.src[c.n] = reinterpret_cast<const uint32_t*>(g.d + off);
+      c.dst[c.n] = static_cast<uint32_t*>(ups[i].dst);
+      c.words[c.n++] = static_cast<uint32_t>(ups[i].bytes / 4);
+    } else {
+      HIP_TRY(hipMemcpyAsync(ups[i].dst, g.h + off, ups[i].bytes, hipMemcpyHostToDevice, s), "upload");
+    }
+    off += (ups[i].bytes + 255) & ~size_t(255);
+  }
+  if (kernel) HIP_TRY(launch_stage_copy(c, s), "stage copy");
+  HIP_TRY(hipEventRecord(g.used, s), "event");
+  g.pending = true;
+  return PS_OK;
+}
+
 int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<WinSlice>& win,
                ps_stats* st) {
   const auto t_g0 = std::chrono::steady_clock::now();
@@ -1222,7 +1327,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   for (uint32_t t = 0; t < nt && fuse; ++t)
     if (tab[t].W && tstart[t] != max_start) fuse = false;
   if (level) {
-    int rc2 = pull ? build_pull_chunks(e, tab, tstart, planned0, &fuse)
+    bool top_ok = pull && world == 1;  // one launch for the leading small rounds
+    for (uint32_t t = 0; t < nt && top_ok; ++t)
+      if (tab[t].W && tstart[t] != max_start) top_ok = false;
+    int rc2 = pull ? build_pull_chunks(e, tab, tstart, planned0, &fuse, top_ok)
                    : build_schedule(e, tab, tstart, planned0);
     if (rc2) return rc2;
     lgrid.assign(planned0 + 1, 0);
@@ -1232,8 +1340,15 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     woff.assign(planned0 + 2, 0);
     for (uint32_t q = 1; q <= planned0; ++q) {
       if (pull) {  // one wave per chunk; a partial slot per block (and level)
-        lgrid[q] = ceil_div(e->pull_off[q + 1] - e->pull_off[q], kBlock / 64);
-        woff[q + 1] = woff[q] + lgrid[q] * (fuse ? 2 : 1);
+        const uint32_t tf = e->pull_top_first, tl = e->pull_top_last;
+        const bool in_top = tf && q >= tf && q <= tl;
+        if (in_top)  // the top launch, issued in round tf: one slot per block
+          lgrid[q] = q == tf ? ceil_div(e->pull_off[tl + 1] - e->pull_off[tf], kBlock / 64) : 0;
+        else
+          lgrid[q] = ceil_div(e->pull_off[q + 1] - e->pull_off[q], kBlock / 64);
+        const uint32_t slots = in_top ? (q == tf ? (tl - tf + 1) * kPullSlots : 0)
+                                      : std::min<uint32_t>(lgrid[q], kPullSlots);
+        woff[q + 1] = woff[q] + slots * (fuse ? 2 : 1);
       } else {
         const uint32_t cnt = e->sched_cnt[q];
         lgrid[q] = cnt ? std::min<uint32_t>(e->expand_grid, ceil_div(cnt, 4)) : 0;  // >= 1 entry per wave
@@ -1246,6 +1361,11 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       desc[3 * q] = woff[q];
       desc[3 * q + 1] = woff[q + 1];
       desc[3 * q + 2] = 1;
+      if (pull && e->pull_top_first && q >= e->pull_top_first && q <= e->pull_top_last) {
+        const uint32_t tf = e->pull_top_first;
+        desc[3 * q] = woff[tf] + (q - tf) * kPullSlots;
+        desc[3 * q + 1] = desc[3 * q] + kPullSlots;
+      }
       if (fuse) {
         const bool second = q > max_start && (q - max_start) % 2 == 0;  // written by launch q - 1
         const uint32_t L = second ? q - 1 : q;
@@ -1289,13 +1409,14 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
 
   const auto t_w3 = std::chrono::steady_clock::now();
   hipStream_t s = e->stream;
-  HIP_TRY(hipMemcpyAsync(e->d_topics.p, tab.data(), tab.size() * sizeof(TopicDev),
-                         hipMemcpyHostToDevice, s),
-          "upload topics");
-  if (!seeds.empty())
-    HIP_TRY(hipMemcpyAsync(e->d_seeds.p, seeds.data(), seeds.size() * sizeof(SeedDev),
-                           hipMemcpyHostToDevice, s),
-            "upload seeds");
+  {
+    const Upload ups[3] = {
+        {e->d_topics.p, tab.data(), tab.size() * sizeof(TopicDev)},
+        {e->d_seeds.p, seeds.data(), seeds.size() * sizeof(SeedDev)},
+        {e->d_woff.p, e->desc_host.data(), level ? e->desc_host.size() * 4 : 0}};
+    const int rcu = stage_uploads(e, ups, 3, s);
+    if (rcu) return rcu;
+  }
   HIP_TRY(hipEventRecord(e->ev_run0, s), "event");
   const auto t_first = std::chrono::steady_clock::now();
   // new window generation: every tree row from older windows becomes stale
@@ -1430,9 +1551,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   };
   if (level) {
     // static frontier: one expand launch per round, counters reduced once
-    HIP_TRY(hipMemcpyAsync(e->d_woff.p, e->desc_host.data(), e->desc_host.size() * 4,
-                           hipMemcpyHostToDevice, s),
-            "upload wave offsets");
+    if (pull)  // pull blocks add into shared partial slots
+      HIP_TRY(hipMemsetAsync(partials, 0, static_cast<size_t>(e->woff_host[planned0 + 1]) * kNumCtr * 8, s),
+              "clear partials");
     HIP_TRY(seed_round(0, arr[0]), "seed");
     for (r = 1; r <= planned0; ++r) {
       a.a_cur = arr[(r - 1) & 1];
@@ -1446,6 +1567,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         ++launches;
       }
       if (lgrid[r] && pull) {
+        const bool top = e->pull_top_first == r;
         PullArgs pa{};
         pa.node_parent = e->d_node_parent.as<uint32_t>();
         pa.node_flags = a.node_flags;
@@ -1458,17 +1580,20 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         pa.gen_cur = a.gen_cur;
         pa.scratch = e->d_scratch.as<uint64_t>();
         pa.dbg = a.dbg;
-        HIP_TRY(launch_pull(pa, e->d_pull.as<PullChunk>() + e->pull_off[r],
-                            e->pull_off[r + 1] - e->pull_off[r], lgrid[r], r, record, fuse,
-                            e->pull_unroll,
-                            // rows a later level re-reads while they can still sit in the
-                            // 256 MB MALL keep the default policy
-                            r < e->pull_bytes.size() &&
-                                    (e->pull_bytes[r] >= e->pull_nt_min || r == planned0)
-                                ? e->pull_nt
-                                : 0u,
-                            s),
-                "pull");
+        pa.slot_mod = kPullSlots;
+        pa.slot_base = r;
+        const PullChunk* ch = e->d_pull.as<PullChunk>() + e->pull_off[r];
+        if (top) {
+          HIP_TRY(launch_pull_top(pa, ch, e->pull_off[e->pull_top_last + 1] - e->pull_off[r], record, s),
+                  "pull top");
+        } else {
+          // rows a later level re-reads while they can still sit in the 256 MB
+          // MALL keep the default policy
+          const bool nt = r < e->pull_bytes.size() && (e->pull_bytes[r] >= e->pull_nt_min || r == planned0);
+          HIP_TRY(launch_pull(pa, ch, e->pull_off[r + 1] - e->pull_off[r], lgrid[r], r, record, fuse,
+                              e->pull_unroll, nt ? e->pull_nt : 0u, s),
+                  "pull");
+        }
       } else if (lgrid[r]) {
         a.frontier = e->d_sched.as<uint32_t>() + e->sched_off[r];
         a.n_front = e->d_sched_cnt.as<uint32_t>() + r;
@@ -1571,6 +1696,13 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       e->last_lo[t] = win[t].n ? e->run_rank[win[t].idx[0]] : 0;
     }
     e->have_window = true;
+    if (e->host_timing) {
+      auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+      std::fprintf(stderr, "[psengine] async window: plan %.3f ms (run->window %.3f, topics %.3f, seeds %.3f, "
+                   "schedule %.3f, uploads %.3f), enqueue %.3f ms\n",
+                   ms(e->t_run0, t_first), ms(e->t_run0, t_w0), ms(t_w0, t_w1), ms(t_w1, t_w2),
+                   ms(t_w2, t_w3), ms(t_w3, t_first), ms(t_first, t_enq));
+    }
     return PS_OK;
   }
   HIP_TRY(hipEventSynchronize(e->ev_run1), "sync");
@@ -1707,6 +1839,7 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_LEVEL_PUSH")) e->level_push = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_WORDS")) e->pull_words = std::max(64, std::atoi(v));
+  if (const char* v = std::getenv("PSAMD_PULL_TOP_MB")) e->pull_top_max = std::strtoull(v, nullptr, 10) << 20;
   if (const char* v = std::getenv("PSAMD_PULL_FUSE")) e->no_fuse = std::atoi(v) == 0;
   if (const char* v = std::getenv("PSAMD_PULL_UNROLL")) e->pull_unroll = std::atoi(v) <= 4 ? 4 : 8;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
@@ -1725,6 +1858,11 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
     f.hs = static_cast<uint64_t*>(h);
     f.ha = f.hs + (PS_MAX_ROUNDS + 1) * kNumCtr;
   }
+  for (auto& g : e->stg)
+    if (hipEventCreateWithFlags(&g.used, hipEventDisableTiming) != hipSuccess) {
+      ps_destroy(e);
+      return PS_E_DEVICE;
+    }
   e->topics.resize(cfg->n_topics);
   e->live.assign(cfg->n_peers, 1);
   if (e->d_digest.ensure(8) != hipSuccess) {
@@ -1747,6 +1885,10 @@ void ps_destroy(ps_engine* e) {
     if (f.ev1) (void)hipEventDestroy(f.ev1);
     if (f.done) (void)hipEventDestroy(f.done);
     if (f.hs) (void)hipHostFree(f.hs);
+  }
+  for (auto& g : e->stg) {
+    if (g.used) (void)hipEventDestroy(g.used);
+    if (g.h) (void)hipHostFree(g.h);
   }
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;

@@ -977,7 +977,9 @@ __device__ __forceinline__ void pull_flush(const PullCtr& c, uint64_t* partials,
       case kCtrSeenWrites: v = t[1]; break;
       default: v = 0;
     }
-    partials[slot * kNumCtr + threadIdx.x] = v;
+    // blocks share a slot (slot_mod): partials are zeroed per window
+    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(partials + slot * kNumCtr + threadIdx.x),
+                     static_cast<unsigned long long>(v));
   }
   __syncthreads();  // `red` is reused by the next level's flush
 }
@@ -1020,11 +1022,91 @@ __global__ __launch_bounds__(kBlock, kU <= 4 ? 8 : 1) void k_pull(PullArgs a, co
       pull_stream<kRecord, kU, kNT>(a, P, ch.g_begin, n2, src + n1, lane, wave, round + 1, c2);
   }
   if constexpr (kFuse) {
-    pull_flush(c1, a.partials, 2ull * blockIdx.x, lane, wid);
-    pull_flush(c2, a.partials, 2ull * blockIdx.x + 1, lane, wid);
+    pull_flush(c1, a.partials, 2ull * (blockIdx.x % a.slot_mod), lane, wid);
+    pull_flush(c2, a.partials, 2ull * (blockIdx.x % a.slot_mod) + 1, lane, wid);
   } else {
-    pull_flush(c1, a.partials, blockIdx.x, lane, wid);
+    pull_flush(c1, a.partials, blockIdx.x % a.slot_mod, lane, wid);
   }
+}
+
+// Top levels in one launch (one rank, every active topic starting together):
+// the chunks of levels 1..K (small rounds, latency-bound as separate
+// launches: ~6 us each for a few MB) run side by side, ch.pad = the round a
+// chunk's nodes are written in.  A node is reached iff the root was reached
+// and the node and every ancestor below the root are live (the per-level
+// rule "parent reached and node live", unrolled along the path), and then
+// receives exactly the root's arrival row, so it copies that row instead of
+// its parent's row written in the same launch.  The host pads every round's
+// chunk list to whole blocks, so a block's partial slot belongs to one round.
+__device__ __forceinline__ void pull_resolve_top(const PullArgs& a, const PullTopic& P, uint32_t nb,
+                                                 uint32_t nk, uint32_t* src, uint32_t lane,
+                                                 uint32_t cur, PullCtr& c) {
+  const bool root_up = P.root != kNoneNode && a.gen[P.root] == cur;
+  for (uint32_t j0 = 0; j0 < nk; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    const bool in = j < nk;
+    uint32_t p = kNoneNode, f = 0;
+    if (in) {
+      p = a.node_parent[nb + j];
+      f = a.node_flags[nb + j];
+    }
+    uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
+    if (lane == 0) prev = nb + j0 > P.nbase ? a.node_parent[nb + j0 - 1] : kNoneNode;
+    // up: the parent was reached (root reached, every ancestor below it live)
+    bool up = in && root_up && p != kNoneNode;
+    uint32_t q = p;
+    for (uint32_t step = 0; up && q != P.root; ++step) {
+      const uint32_t fq = a.node_flags[q];
+      const uint32_t pq = a.node_parent[q];
+      up = (fq & kNodeLive) && pq != kNoneNode && step < 2 * kPullTopLevels;  // a walk spans < kPullTopLevels
+      q = pq;
+    }
+    const bool ok = up && (f & kNodeLive);
+    if (in) src[j] = ok ? P.root : kNoneNode;
+    if (ok && !(a.dbg & kDbgNoByteStores)) a.gen[nb + j] = static_cast<uint8_t>(cur);
+    c.kids += in;
+    c.reached += ok;
+    if (up && p != prev) {
+      c.parents += 1;
+      if (p == P.root) c.pwords += P.W;  // the only row this launch reads
+    }
+  }
+}
+
+template <bool kRecord>
+__global__ __launch_bounds__(kBlock, 8) void k_pull_top(PullArgs a, const PullChunk* __restrict__ chunks,
+                                                        uint32_t n_chunks) {
+  __shared__ uint32_t src_lds[kBlock / 64][kPullMaxKids];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wave = blockIdx.x * (kBlock / 64) + wid;
+  uint32_t* src = src_lds[wid];
+  const uint32_t cur = a.gen_cur & 0xFF;
+  PullCtr c1;
+  // every chunk of a block belongs to one round (the host pads the rounds to
+  // whole blocks): the block adds into that round's kPullSlots slots
+  const uint32_t q0 = chunks[blockIdx.x * (kBlock / 64)].pad;
+  if (wave < n_chunks) {
+    const PullChunk ch = chunks[wave];
+    if (ch.node_end > ch.node_begin) {  // padding chunks are empty
+      const TopicDev T = a.topics[ch.topic];
+      PullTopic P;
+      P.W = T.W;
+      P.nbase = T.nbase;
+      P.base = T.wbase - static_cast<uint64_t>(T.nbase) * T.W;
+      P.root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
+      const uint32_t n1 = ch.node_end - ch.node_begin;
+      pull_resolve_top(a, P, ch.node_begin, n1, src, lane, cur, c1);
+      pull_stream<kRecord, 8, 0>(a, P, ch.node_begin, n1, src, lane, wave, ch.pad, c1);
+    }
+  }
+  pull_flush(c1, a.partials, (q0 - a.slot_base) * kPullSlots + blockIdx.x % kPullSlots, lane, wid);
+}
+
+__global__ __launch_bounds__(kBlock) void k_stage_copy(StageCopy c) {
+  const uint32_t tid = blockIdx.x * kBlock + threadIdx.x, nth = gridDim.x * kBlock;
+  for (uint32_t k = 0; k < c.n; ++k)
+    for (uint32_t i = tid; i < c.words[k]; i += nth) c.dst[k][i] = c.src[k][i];
 }
 
 // ------------------------------------------------------------------ send ---
@@ -1151,22 +1233,41 @@ __device__ __forceinline__ void block_reduce_ctrs(const uint64_t* __restrict__ p
   }
 }
 
-// Level mode: grid (rounds, kReduceSplit); block (q-1, y) folds every
-// kReduceSplit-th partial slot of round q (desc[3q..3q+2] = first slot, end
-// slot, stride) and adds its sums into the round's (zeroed) statistics.
-constexpr uint32_t kReduceSplit = 32;
+// Level mode: one block per round q (block 0: the unused row 0) folds the
+// round's partial slots (desc[3q..3q+2] = first slot, end slot, stride) as
+// one coalesced stream of counters (kAct threads, each on one counter index)
+// and writes the round's statistics row.  Pull launches share at most
+// kPullSlots slots per round between their blocks, so the streams are short.
 __global__ __launch_bounds__(kBlock) void k_reduce_rounds(const uint64_t* __restrict__ partials,
                                                           const uint32_t* __restrict__ desc,
                                                           uint64_t* __restrict__ round_stats) {
-  __shared__ uint64_t sums[kNumCtr];
-  const uint32_t q = blockIdx.x + 1;
-  const uint32_t stride = desc[3 * q + 2];
-  block_reduce_ctrs(partials, desc[3 * q] + blockIdx.y * stride, desc[3 * q + 1],
-                    stride * kReduceSplit, sums);
-  if (threadIdx.x < kNumCtr && sums[threadIdx.x])
-    atomicAdd(reinterpret_cast<unsigned long long*>(round_stats + static_cast<uint64_t>(q) * kNumCtr +
-                                                    threadIdx.x),
-              static_cast<unsigned long long>(sums[threadIdx.x]));
+  constexpr uint32_t kAct = (kBlock / kNumCtr) * kNumCtr;
+  __shared__ uint64_t red[kBlock];
+  const uint32_t q = blockIdx.x;
+  const uint32_t first = desc[3 * q], end = desc[3 * q + 1], stride = desc[3 * q + 2];
+  uint64_t acc = 0;
+  if (q && stride && threadIdx.x < kAct) {
+    const uint32_t e1 = end * kNumCtr;
+    uint32_t i = first * kNumCtr + threadIdx.x;
+    if (stride == 1) {
+      uint64_t x[4] = {0, 0, 0, 0};
+      for (; i + 3 * kAct < e1; i += 4 * kAct)
+#pragma unroll
+        for (int u = 0; u < 4; ++u) x[u] += partials[i + u * kAct];
+      for (; i < e1; i += kAct) x[0] += partials[i];
+      acc = x[0] + x[1] + x[2] + x[3];
+    } else {
+      for (; i < e1; i += kAct)
+        if ((i / kNumCtr - first) % stride == 0) acc += partials[i];
+    }
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x < kNumCtr) {
+    uint64_t t = 0;
+    for (uint32_t k = threadIdx.x; k < kAct; k += kNumCtr) t += red[k];
+    round_stats[static_cast<uint64_t>(q) * kNumCtr + threadIdx.x] = t;
+  }
 }
 
 // Pass 1: per-block count of flagged nodes (16 one-byte flags per lane, one
@@ -1362,13 +1463,31 @@ hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_ch
   return hipGetLastError();
 }
 
+hipError_t launch_pull_top(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
+                           bool record, hipStream_t s) {
+  if (n_chunks == 0) return hipSuccess;
+  const uint32_t grid = (n_chunks + kBlock / 64 - 1) / (kBlock / 64);
+  if (record)
+    hipLaunchKernelGGL(k_pull_top<true>, dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks);
+  else
+    hipLaunchKernelGGL(k_pull_top<false>, dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks);
+  return hipGetLastError();
+}
+
+hipError_t launch_stage_copy(const StageCopy& c, hipStream_t s) {
+  uint32_t most = 0;
+  for (uint32_t k = 0; k < c.n; ++k) most = c.words[k] > most ? c.words[k] : most;
+  if (most == 0) return hipSuccess;
+  uint32_t grid = (most + kBlock - 1) / kBlock;
+  grid = grid > 64 ? 64 : grid;
+  hipLaunchKernelGGL(k_stage_copy, dim3(grid), dim3(kBlock), 0, s, c);
+  return hipGetLastError();
+}
+
 hipError_t launch_reduce_rounds(const uint64_t* partials, const uint32_t* desc, uint32_t n_rounds,
                                 uint64_t* round_stats, hipStream_t s) {
   if (n_rounds == 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(round_stats, 0, (n_rounds + 1ull) * kNumCtr * 8, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_reduce_rounds, dim3(n_rounds, kReduceSplit), dim3(kBlock), 0, s, partials,
-                     desc, round_stats);
+  hipLaunchKernelGGL(k_reduce_rounds, dim3(n_rounds + 1), dim3(kBlock), 0, s, partials, desc, round_stats);
   return hipGetLastError();
 }
 

@@ -123,6 +123,7 @@ struct PullChunk {
   uint32_t pad;
 };
 constexpr uint32_t kPullMaxKids = 512;
+constexpr uint32_t kPullTopLevels = 32;  // levels of one top launch at most (ancestor walks)
 constexpr uint32_t kNoneNode = 0xFFFFFFFFu;
 constexpr uint32_t kPullWords = 1024;  // default; PSAMD_PULL_WORDS overrides
 
@@ -138,7 +139,10 @@ struct PullArgs {
   uint64_t* scratch;   // 1024 x 1 KiB: stores of lanes past a run's end
   uint32_t gen_cur;
   uint32_t dbg;
+  uint32_t slot_mod;   // block b adds its counters into partial slot b % slot_mod (zeroed per window)
+  uint32_t slot_base;  // top launch: round q's slots start at (q - slot_base) * kPullSlots
 };
+constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch
 
 struct ApplyArgs {
   const uint8_t* recv;
@@ -198,6 +202,22 @@ hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, bool 
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
                        uint32_t grid, uint32_t round, bool record, bool fuse, uint32_t unroll, uint32_t nt,
                        hipStream_t s);
+// Per-window parameters (topic table, seeds, reduce descriptors) copied by
+// one small kernel straight from the pinned staging slot (device-mapped host
+// memory): one launch instead of a blit per array and its barrier packets.
+constexpr uint32_t kStageMax = 4;
+struct StageCopy {
+  const uint32_t* src[kStageMax];
+  uint32_t* dst[kStageMax];
+  uint32_t words[kStageMax];
+  uint32_t n;
+};
+hipError_t launch_stage_copy(const StageCopy& c, hipStream_t s);
+// Level mode, top levels in one launch (one rank, every active topic
+// starting together): chunks of several rounds (PullChunk::pad = round),
+// each round's list padded to whole blocks of kBlock / 64 chunks.
+hipError_t launch_pull_top(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
+                           bool record, hipStream_t s);
 // Level mode: round q's counters = sum of the partial slots desc[3q],
 // desc[3q] + desc[3q+2], ... < desc[3q+1], for q = 1..n_rounds.
 hipError_t launch_reduce_rounds(const uint64_t* partials, const uint32_t* desc, uint32_t n_rounds,

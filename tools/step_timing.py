@@ -28,3 +28,21 @@ for i in range(steps):
           f"(host_ms {st.host_ms:.3f}, gpu run_ms {st.run_ms:.3f}, expand {st.expand_ms:.3f})",
           file=sys.stderr, flush=True)
 eng.close()
+
+# pipelined loop (bench.py's default): where the host spends a step
+if os.environ.get("PIPE", "1") == "1":
+    eng = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed)
+    WL.build_engine_topics(eng, wl)
+    for i in range(steps + 1):
+        t0 = time.perf_counter()
+        eng.publish(wl.msg_topics)
+        t1 = time.perf_counter()
+        eng.run_async()
+        t2 = time.perf_counter()
+        if i:
+            st = eng.wait()
+        t3 = time.perf_counter()
+        print(f"pipe {i}: publish {1e3 * (t1 - t0):.3f} ms, run_async {1e3 * (t2 - t1):.3f} ms, "
+              f"wait {1e3 * (t3 - t2):.3f} ms", file=sys.stderr, flush=True)
+    eng.wait()
+    eng.close()
