@@ -132,6 +132,7 @@ struct ps_engine {
   bool level_push = false;       // PSAMD_LEVEL_PUSH=1: level mode with the push kernel (A/B)
   uint32_t pull_words = kPullWords;  // words per pull chunk (PSAMD_PULL_WORDS)
   uint64_t pull_top_max = 32ull << 20;  // top launch: leading rounds writing <= this many row bytes each (PSAMD_PULL_TOP_MB, 0 = off)
+  bool fold_window = true;  // PSAMD_FOLD_WINDOW=0: separate copy / seed / clear launches (A/B)
   uint32_t pull_top_first = 0, pull_top_last = 0;  // rounds of the cached top launch (0: none)
   uint32_t pull_unroll = 8;          // loads in flight per lane (PSAMD_PULL_UNROLL: 4 or 8)
 
@@ -152,7 +153,7 @@ struct ps_engine {
   bool pull_fused = false;  // the cached chunks are fused (two levels per launch)
   bool no_fuse = true;      // PSAMD_PULL_FUSE=1: two levels per pull launch (A/B; slower)
   std::vector<uint32_t> pull_off;
-  DevBuf d_pull, d_scratch;
+  DevBuf d_pull;
 
   // fused node space (host mirror)
   uint32_t n_nodes = 0, n_pad = 16;
@@ -203,8 +204,8 @@ struct ps_engine {
     uint32_t r = 0, launches = 0;
     bool pull = false, level = false;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the window's kernels
-    hipEvent_t done = nullptr;                // after the counters' readback
     uint64_t* hs = nullptr;  // pinned: (PS_MAX_ROUNDS + 1) x kNumCtr counters
+    uint64_t* hs_dev = nullptr;  // hs, device-mapped (k_reduce_rounds writes it)
     uint64_t* ha = nullptr;  // pinned: apply counters of a multi-GPU window
     uint32_t planned0 = 0;
     int32_t world = 1;
@@ -217,16 +218,14 @@ struct ps_engine {
   // stream has drained, so the next batch's launches would only be issued
   // once the previous batch had finished (a ~35 us bubble per pipelined
   // step).  Two slots alternate; a slot is rewritten only after the copies
-  // of its previous use have completed (event).
+  // of its previous use have completed: slot i belongs to asynchronous run
+  // slot i (synchronous runs use slot 0 with nothing in flight).
   struct Staging {
     uint8_t* h = nullptr;
     uint8_t* d = nullptr;  // the slot's device-mapped address
     size_t cap = 0;
-    hipEvent_t used = nullptr;
-    bool pending = false;
   };
   Staging stg[2];
-  uint32_t stg_next = 0;
   bool defer_phase = false;  // the current phase may defer its last window's stats
   bool defer_last = false;   // ... and this window is that last window
   Inflight* defer_into = nullptr;
@@ -1134,21 +1133,27 @@ struct Upload {
   const void* src;
   size_t bytes;
 };
-int stage_uploads(ps_engine* e, const Upload* ups, size_t n, hipStream_t s) {
+// With `fold` set and the copy-kernel form, nothing is launched: *fold gets
+// the copies for a kernel that folds them in, and staged[i] the device-mapped
+// address of upload i's staged bytes (else its destination).
+int stage_uploads(ps_engine* e, const Upload* ups, size_t n, hipStream_t s, StageCopy* fold = nullptr,
+                  const void** staged = nullptr) {
+  if (fold) *fold = StageCopy{};
+  for (size_t i = 0; staged && i < n; ++i) staged[i] = ups[i].dst;
   size_t need = 0;
   for (size_t i = 0; i < n; ++i) need += (ups[i].bytes + 255) & ~size_t(255);
   if (need == 0) return PS_OK;
-  ps_engine::Staging& g = e->stg[e->stg_next];
-  e->stg_next ^= 1u;
-  if (g.pending) HIP_TRY(hipEventSynchronize(g.used), "sync staging");
-  g.pending = false;
+  // the slot of the asynchronous run being enqueued (its previous user was
+  // waited for before the run slot was reused); synchronous runs start with
+  // nothing in flight
+  ps_engine::Staging& g = e->stg[e->defer_into ? e->defer_into - e->infl : 0];
   if (need > g.cap) {
     if (g.h) HIP_TRY(hipHostFree(g.h), "free staging");
     g.h = nullptr;
     g.cap = 0;
     const size_t cap = std::max<size_t>(need, 64 << 10);
     void* h = nullptr;
-    HIP_TRY(hipHostMalloc(&h, cap, hipHostMallocMapped), "alloc staging");
+    HIP_TRY(hipHostMalloc(&h, cap, hipHostMallocMapped | hipHostMallocCoherent), "alloc staging");
     g.h = static_cast<uint8_t*>(h);
     g.cap = cap;
     void* d = nullptr;
@@ -1165,6 +1170,7 @@ int stage_uploads(ps_engine* e, const Upload* ups, size_t n, hipStream_t s) {
     if (!ups[i].bytes) continue;
     std::memcpy(g.h + off, ups[i].src, ups[i].bytes);
     if (kernel) {
+      if (staged && fold) staged[i] = g.d + off;
       c.src[c.n] = reinterpret_cast<const uint32_t*>(g.d + off);
       c.dst[c.n] = static_cast<uint32_t*>(ups[i].dst);
       c.words[c.n++] = static_cast<uint32_t>(ups[i].bytes / 4);
@@ -1173,9 +1179,10 @@ int stage_uploads(ps_engine* e, const Upload* ups, size_t n, hipStream_t s) {
     }
     off += (ups[i].bytes + 255) & ~size_t(255);
   }
-  if (kernel) HIP_TRY(launch_stage_copy(c, s), "stage copy");
-  HIP_TRY(hipEventRecord(g.used, s), "event");
-  g.pending = true;
+  if (kernel && fold)
+    *fold = c;
+  else if (kernel)
+    HIP_TRY(launch_stage_copy(c, s), "stage copy");
   return PS_OK;
 }
 
@@ -1271,12 +1278,14 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   std::vector<uint32_t> seed_off(max_start + 2, 0);
   for (uint32_t r = 0; r <= max_start; ++r) {
     for (uint32_t t = 0; t < nt; ++t) {
-      const TopicDev& d = tab[t];
+      TopicDev& d = tab[t];
+      if (r == 0) d.seed_lo = static_cast<uint32_t>(seeds.size());
       if (inj[t].empty()) continue;
       for (uint32_t w = 0; w < d.W; ++w) {
         const uint64_t m = inj[t][static_cast<size_t>(r) * d.W + w];
         if (m) seeds.push_back(SeedDev{d.wbase + w, m, d.nbase, 0});  // root = node 0
       }
+      if (r == 0) d.seed_n = static_cast<uint32_t>(seeds.size()) - d.seed_lo;
     }
     seed_off[r + 1] = static_cast<uint32_t>(seeds.size());
   }
@@ -1377,7 +1386,6 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     HIP_TRY(e->d_partials.ensure(static_cast<size_t>(woff[planned0 + 1]) * kNumCtr * 8),
             "alloc level partials");
     HIP_TRY(e->d_woff.ensure(desc.size() * 4), "alloc reduce descriptors");
-    HIP_TRY(e->d_scratch.ensure(1024 * 1024), "alloc scratch");
   }
   // cross-rank capacities (items = node words) per round: cap[r][from*world+to]
   std::vector<std::vector<uint64_t>> cap;
@@ -1409,14 +1417,29 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
 
   const auto t_w3 = std::chrono::steady_clock::now();
   hipStream_t s = e->stream;
+  // the window's first kernel also copies the staged uploads, applies the
+  // round-0 seeds of tree roots and clears the pull partial slots (level
+  // mode without meshes; the eager seen clear below would erase the seeds)
+  const bool fold = e->fold_window && level && !any_mesh && !(e->cfg.flags & PS_F_NO_LAZY_SEEN);
+  WindowStart ws{};
+  const void* staged[3] = {nullptr, nullptr, nullptr};
   {
     const Upload ups[3] = {
         {e->d_topics.p, tab.data(), tab.size() * sizeof(TopicDev)},
         {e->d_seeds.p, seeds.data(), seeds.size() * sizeof(SeedDev)},
         {e->d_woff.p, e->desc_host.data(), level ? e->desc_host.size() * 4 : 0}};
-    const int rcu = stage_uploads(e, ups, 3, s);
+    const int rcu = stage_uploads(e, ups, 3, s, fold ? &ws.copy : nullptr, staged);
     if (rcu) return rcu;
   }
+  if (fold) {
+    if (seed_off[1] > 0) ws.seeds = static_cast<const SeedDev*>(staged[1]);
+    if (pull) {
+      ws.zero = e->d_partials.as<uint64_t>();
+      ws.zero_words = static_cast<uint64_t>(e->woff_host[planned0 + 1]) * kNumCtr;
+    }
+  }
+  const bool seeds0_done = ws.seeds != nullptr;
+  const bool partials_done = ws.zero != nullptr;
   HIP_TRY(hipEventRecord(e->ev_run0, s), "event");
   const auto t_first = std::chrono::steady_clock::now();
   // new window generation: every tree row from older windows becomes stale
@@ -1424,9 +1447,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     HIP_TRY(hipMemsetAsync(e->d_gen.p, 0, e->d_gen.bytes, s), "clear generations");
     e->gen_cur = 1;
   }
-  HIP_TRY(launch_window_init(e->d_topics.as<TopicDev>(), nt, e->d_seen.as<uint64_t>(),
-                             e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>(),
-                             e->d_gen.as<uint8_t>(), e->gen_cur, any_mesh, s),
+  HIP_TRY(launch_window_init(static_cast<const TopicDev*>(fold ? staged[0] : e->d_topics.p), nt,
+                             e->d_seen.as<uint64_t>(), e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>(),
+                             e->d_gen.as<uint8_t>(), e->gen_cur, any_mesh, ws, s),
           "window init");
   if (e->n_remote_fed)
     HIP_TRY(launch_init_nodes(e->d_remote_fed.as<uint32_t>(), e->n_remote_fed,
@@ -1447,6 +1470,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
             "clear apply stats");
 
   ExpandArgs a{};
+  bool host_stats_written = false;  // the reduce wrote the deferred slot's pinned rows
   a.frontier = e->d_frontier.as<uint32_t>();
   a.n_front = e->d_nfront.as<uint32_t>();
   a.row_ptr = e->d_row_ptr.as<uint32_t>();
@@ -1551,10 +1575,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   };
   if (level) {
     // static frontier: one expand launch per round, counters reduced once
-    if (pull)  // pull blocks add into shared partial slots
+    if (pull && !partials_done)  // pull blocks add into shared partial slots
       HIP_TRY(hipMemsetAsync(partials, 0, static_cast<size_t>(e->woff_host[planned0 + 1]) * kNumCtr * 8, s),
               "clear partials");
-    HIP_TRY(seed_round(0, arr[0]), "seed");
+    if (!seeds0_done) HIP_TRY(seed_round(0, arr[0]), "seed");
     for (r = 1; r <= planned0; ++r) {
       a.a_cur = arr[(r - 1) & 1];
       a.a_next = arr[r & 1];
@@ -1578,7 +1602,6 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         pa.hop_rec = a.hop_rec;
         pa.partials = partials + static_cast<size_t>(e->woff_host[r]) * kNumCtr;
         pa.gen_cur = a.gen_cur;
-        pa.scratch = e->d_scratch.as<uint64_t>();
         pa.dbg = a.dbg;
         pa.slot_mod = kPullSlots;
         pa.slot_base = r;
@@ -1612,7 +1635,12 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       HIP_TRY(seed_round(r, a.a_next), "seed");
     }
     r = planned0;
-    HIP_TRY(launch_reduce_rounds(partials, e->d_woff.as<uint32_t>(), planned0, stats, s),
+    // a deferred window's counters go straight into its pinned rows
+    const bool direct = e->defer_last && e->defer_into && !record && !timed && r <= PS_MAX_ROUNDS &&
+                        (world == 1 || planned0 <= PS_MAX_ROUNDS);
+    host_stats_written = direct;
+    HIP_TRY(launch_reduce_rounds(partials, e->d_woff.as<uint32_t>(), planned0, stats,
+                                 direct ? e->defer_into->hs_dev : nullptr, s),
             "reduce rounds");
   } else {
   HIP_TRY(seed_round(0, arr[0]), "seed");
@@ -1669,20 +1697,23 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     }
   }
   }
-  HIP_TRY(hipEventRecord(e->ev_run1, s), "event");
+  const bool defer = e->defer_last && e->defer_into && !record && !timed && r <= PS_MAX_ROUNDS &&
+                     (world == 1 || planned0 <= PS_MAX_ROUNDS);  // the pinned slots hold PS_MAX_ROUNDS + 1 rows
+  if (!defer) HIP_TRY(hipEventRecord(e->ev_run1, s), "event");
   const auto t_enq = std::chrono::steady_clock::now();
-  if (e->defer_last && e->defer_into && !record && !timed && r <= PS_MAX_ROUNDS &&
-      (world == 1 || planned0 <= PS_MAX_ROUNDS)) {  // the pinned slots hold PS_MAX_ROUNDS + 1 rows
+  if (defer) {
     // asynchronous run: the counters follow the kernels on the stream into
-    // pinned memory; ps_wait accumulates them
+    // pinned memory (level mode: written there by the reduce itself); the
+    // window's end event marks their arrival; ps_wait accumulates them
     ps_engine::Inflight& f = *e->defer_into;
-    HIP_TRY(hipMemcpyAsync(f.hs, stats, static_cast<size_t>(r + 1) * kNumCtr * 8, hipMemcpyDeviceToHost, s),
-            "read stats");
+    if (!host_stats_written)
+      HIP_TRY(hipMemcpyAsync(f.hs, stats, static_cast<size_t>(r + 1) * kNumCtr * 8, hipMemcpyDeviceToHost, s),
+              "read stats");
     if (world > 1)
       HIP_TRY(hipMemcpyAsync(f.ha, e->d_apply_stats.p, static_cast<size_t>(planned0 + 1) * kNumCtr * 8,
                              hipMemcpyDeviceToHost, s),
               "read apply stats");
-    HIP_TRY(hipEventRecord(f.done, s), "event");
+    HIP_TRY(hipEventRecord(e->ev_run1, s), "event");
     f.deferred = true;
     f.planned0 = planned0;
     f.world = world;
@@ -1839,6 +1870,7 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_LEVEL_PUSH")) e->level_push = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_WORDS")) e->pull_words = std::max(64, std::atoi(v));
+  if (const char* v = std::getenv("PSAMD_FOLD_WINDOW")) e->fold_window = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_TOP_MB")) e->pull_top_max = std::strtoull(v, nullptr, 10) << 20;
   if (const char* v = std::getenv("PSAMD_PULL_FUSE")) e->no_fuse = std::atoi(v) == 0;
   if (const char* v = std::getenv("PSAMD_PULL_UNROLL")) e->pull_unroll = std::atoi(v) <= 4 ? 4 : 8;
@@ -1850,19 +1882,20 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   for (auto& f : e->infl) {
     void* h = nullptr;
     if (hipEventCreate(&f.ev0) != hipSuccess || hipEventCreate(&f.ev1) != hipSuccess ||
-        hipEventCreateWithFlags(&f.done, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc(&h, 2 * (PS_MAX_ROUNDS + 1) * kNumCtr * 8, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc(&h, 2 * (PS_MAX_ROUNDS + 1) * kNumCtr * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
       ps_destroy(e);
       return PS_E_DEVICE;
     }
     f.hs = static_cast<uint64_t*>(h);
-    f.ha = f.hs + (PS_MAX_ROUNDS + 1) * kNumCtr;
-  }
-  for (auto& g : e->stg)
-    if (hipEventCreateWithFlags(&g.used, hipEventDisableTiming) != hipSuccess) {
+    void* hd = nullptr;
+    if (hipHostGetDevicePointer(&hd, h, 0) != hipSuccess) {
       ps_destroy(e);
       return PS_E_DEVICE;
     }
+    f.hs_dev = static_cast<uint64_t*>(hd);
+    f.ha = f.hs + (PS_MAX_ROUNDS + 1) * kNumCtr;
+  }
+
   e->topics.resize(cfg->n_topics);
   e->live.assign(cfg->n_peers, 1);
   if (e->d_digest.ensure(8) != hipSuccess) {
@@ -1883,13 +1916,10 @@ void ps_destroy(ps_engine* e) {
   for (auto& f : e->infl) {
     if (f.ev0) (void)hipEventDestroy(f.ev0);
     if (f.ev1) (void)hipEventDestroy(f.ev1);
-    if (f.done) (void)hipEventDestroy(f.done);
     if (f.hs) (void)hipHostFree(f.hs);
   }
-  for (auto& g : e->stg) {
-    if (g.used) (void)hipEventDestroy(g.used);
+  for (auto& g : e->stg)
     if (g.h) (void)hipHostFree(g.h);
-  }
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -2279,7 +2309,7 @@ int ps_wait(ps_engine* e, ps_stats* out) {
   e->infl_head = (e->infl_head + 1) % 2;
   --e->infl_count;
   if (f.deferred) {
-    HIP_TRY(hipEventSynchronize(f.done), "sync");
+    HIP_TRY(hipEventSynchronize(f.ev1), "sync");
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, f.ev0, f.ev1), "elapsed");
     f.st.run_ms += ms;

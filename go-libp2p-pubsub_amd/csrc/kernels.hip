@@ -84,7 +84,17 @@ __global__ __launch_bounds__(kBlock) void k_window_init(const TopicDev* __restri
                                                         uint64_t* __restrict__ a0,
                                                         uint64_t* __restrict__ a1,
                                                         uint8_t* __restrict__ gen,
-                                                        uint32_t gen_cur) {
+                                                        uint32_t gen_cur, WindowStart ws) {
+  // folded-in work (one launch instead of three): the staged copies and the
+  // partial-slot clear, grid-stride over every block
+  const uint32_t nb = gridDim.x * gridDim.y;
+  const uint32_t bid = blockIdx.y * gridDim.x + blockIdx.x;
+  for (uint32_t k = 0; k < ws.copy.n; ++k)
+    for (uint32_t i = bid * kBlock + threadIdx.x; i < ws.copy.words[k]; i += nb * kBlock)
+      ws.copy.dst[k][i] = ws.copy.src[k][i];
+  for (uint64_t i = static_cast<uint64_t>(bid) * kBlock + threadIdx.x; i < ws.zero_words;
+       i += static_cast<uint64_t>(nb) * kBlock)
+    ws.zero[i] = 0;
   const TopicDev T = topics[blockIdx.y];
   if (T.W == 0 || T.n_nodes == 0) return;
   const bool mesh = (T.flags & kTopicMesh) != 0;
@@ -98,6 +108,16 @@ __global__ __launch_bounds__(kBlock) void k_window_init(const TopicDev* __restri
   }
   if (blockIdx.x == 0 && threadIdx.x == 0 && (T.flags & kTopicRootLocal))
     gen[T.nbase] = static_cast<uint8_t>(gen_cur);
+  if (ws.seeds && !mesh) {
+    // Topic.PublishMessage (pubsub.go:111-120), round 0: this block zeroed
+    // the root's row above; the barrier orders the seeds after it
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < T.seed_n; i += kBlock) {
+      const SeedDev sd = ws.seeds[T.seed_lo + i];
+      a0[sd.woff] |= sd.mask;
+      seen[sd.woff] |= sd.mask;
+    }
+  }
 }
 
 // Nodes fed by a parent on another rank: rows zeroed, so the apply kernel can
@@ -865,7 +885,6 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
   const uint32_t root = P.root;
   const uint32_t total = nk * W;
   uint64_t* const out = a.seen + base + static_cast<uint64_t>(nb) * W;
-  uint64_t* const dummy = a.scratch + static_cast<uint64_t>(wave & 1023u) * 128;
   const float rw = 1.0f / static_cast<float>(W);
   // row kk = i / W and word r of the run, branch-free (float estimate off by
   // at most one; i < 2^24)
@@ -878,26 +897,28 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
   };
   if (!(W & 1u)) {
     // even W: every row 16-B aligned, a 2-word pair never straddles rows
-    auto one = [&](uint32_t i, bool valid) {
+    // i: a pair of words of the run; a lane past the run's end repeats the
+    // run's last pair (same source, same value, same address)
+    auto one = [&](uint32_t i) {
       int32_t kk, r;
       split(i, kk, r);
-      const uint32_t p = valid ? src[kk] : kNoneNode;
+      const uint32_t p = src[kk];
       const bool go = p != kNoneNode;
       // unconditional load: a skipped lane reads its own output row
       const uint64_t* s = go ? (p == root ? a.a_cur : a.seen) + base + static_cast<uint64_t>(p) * W + r
-                             : out + (valid ? i : 0);
+                             : out + i;
       return PullVec{go, load_row16<(kNT & 2u) != 0>(s)};
     };
     // 8 loads in flight, then 8 stores, unconditional and branch-free (a
     // skipped lane writes its own row back unchanged, a lane past the run's
-    // end writes a scratch slot), so the compiler counts vmcnt exactly
-    // instead of draining at branches
+    // end stores the run's last pair again with the value its owner stores),
+    // so the compiler counts vmcnt exactly instead of draining at branches
     for (uint32_t i0 = 0; i0 < total; i0 += kU * 128) {
       PullVec x[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
         const uint32_t i = i0 + u * 128 + 2 * lane;
-        x[u] = one(i, i < total);
+        x[u] = one(i < total ? i : total - 2);
       }
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
@@ -911,10 +932,11 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
                                  round);
           }
         } else {
-          store_row16<(kNT & 1u) != 0>(i < total ? out + i : dummy + 2 * lane, x[u].v);
+          store_row16<(kNT & 1u) != 0>(out + (i < total ? i : total - 2), x[u].v);
         }
-        c.deliv += x[u].go ? popc4(x[u].v) : 0u;
-        c.sw += x[u].go ? 2u : 0u;
+        const bool own = x[u].go && i < total;
+        c.deliv += own ? popc4(x[u].v) : 0u;
+        c.sw += own ? 2u : 0u;
       }
     }
   } else {
@@ -925,13 +947,13 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
         const uint32_t i = i0 + u * 64 + lane;
-        const bool valid = i < total;
+        const uint32_t ic = i < total ? i : total - 1;  // past the end: the run's last word again
         int32_t kk, r;
-        split(i, kk, r);
-        const uint32_t p = valid ? src[kk] : kNoneNode;
+        split(ic, kk, r);
+        const uint32_t p = src[kk];
         go[u] = p != kNoneNode;
         const uint64_t* s = go[u] ? (p == root ? a.a_cur : a.seen) + base + static_cast<uint64_t>(p) * W + r
-                                  : out + (valid ? i : 0);
+                                  : out + ic;
         m[u] = load_row8<(kNT & 2u) != 0>(s);
       }
 #pragma unroll
@@ -943,10 +965,11 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
             record_word<kRecord>(a.hop_rec, (out - a.seen) + i, m[u], round);
           }
         } else {
-          store_row8<(kNT & 1u) != 0>(i < total ? out + i : dummy + lane, m[u]);
+          store_row8<(kNT & 1u) != 0>(out + (i < total ? i : total - 1), m[u]);
         }
-        c.deliv += go[u] ? __popcll(m[u]) : 0u;
-        c.sw += go[u] ? 1u : 0u;
+        const bool own = go[u] && i < total;
+        c.deliv += own ? __popcll(m[u]) : 0u;
+        c.sw += own ? 1u : 0u;
       }
     }
   }
@@ -1074,7 +1097,7 @@ __device__ __forceinline__ void pull_resolve_top(const PullArgs& a, const PullTo
 }
 
 template <bool kRecord>
-__global__ __launch_bounds__(kBlock, 8) void k_pull_top(PullArgs a, const PullChunk* __restrict__ chunks,
+__global__ __launch_bounds__(kBlock, 1) void k_pull_top(PullArgs a, const PullChunk* __restrict__ chunks,
                                                         uint32_t n_chunks) {
   __shared__ uint32_t src_lds[kBlock / 64][kPullMaxKids];
   const uint32_t lane = threadIdx.x & 63;
@@ -1240,7 +1263,8 @@ __device__ __forceinline__ void block_reduce_ctrs(const uint64_t* __restrict__ p
 // kPullSlots slots per round between their blocks, so the streams are short.
 __global__ __launch_bounds__(kBlock) void k_reduce_rounds(const uint64_t* __restrict__ partials,
                                                           const uint32_t* __restrict__ desc,
-                                                          uint64_t* __restrict__ round_stats) {
+                                                          uint64_t* __restrict__ round_stats,
+                                                          uint64_t* __restrict__ host_stats) {
   constexpr uint32_t kAct = (kBlock / kNumCtr) * kNumCtr;
   __shared__ uint64_t red[kBlock];
   const uint32_t q = blockIdx.x;
@@ -1267,6 +1291,11 @@ __global__ __launch_bounds__(kBlock) void k_reduce_rounds(const uint64_t* __rest
     uint64_t t = 0;
     for (uint32_t k = threadIdx.x; k < kAct; k += kNumCtr) t += red[k];
     round_stats[static_cast<uint64_t>(q) * kNumCtr + threadIdx.x] = t;
+    if (host_stats) {  // fine-grained pinned host rows: visible to the host once the kernel ends
+      __hip_atomic_store(host_stats + static_cast<uint64_t>(q) * kNumCtr + threadIdx.x, t, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __threadfence_system();
+    }
   }
 }
 
@@ -1364,10 +1393,10 @@ __global__ __launch_bounds__(kBlock) void k_digest(const uint64_t* __restrict__ 
 
 hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_t* seen,
                               uint64_t* a0, uint64_t* a1, uint8_t* gen, uint32_t gen_cur,
-                              bool any_mesh, hipStream_t s) {
+                              bool any_mesh, const WindowStart& ws, hipStream_t s) {
   if (n_topics == 0) return hipSuccess;
   const dim3 grid(any_mesh ? 64 : 1, n_topics);
-  hipLaunchKernelGGL(k_window_init, grid, dim3(kBlock), 0, s, topics, seen, a0, a1, gen, gen_cur);
+  hipLaunchKernelGGL(k_window_init, grid, dim3(kBlock), 0, s, topics, seen, a0, a1, gen, gen_cur, ws);
   return hipGetLastError();
 }
 
@@ -1485,9 +1514,10 @@ hipError_t launch_stage_copy(const StageCopy& c, hipStream_t s) {
 }
 
 hipError_t launch_reduce_rounds(const uint64_t* partials, const uint32_t* desc, uint32_t n_rounds,
-                                uint64_t* round_stats, hipStream_t s) {
+                                uint64_t* round_stats, uint64_t* host_stats, hipStream_t s) {
   if (n_rounds == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_reduce_rounds, dim3(n_rounds + 1), dim3(kBlock), 0, s, partials, desc, round_stats);
+  hipLaunchKernelGGL(k_reduce_rounds, dim3(n_rounds + 1), dim3(kBlock), 0, s, partials, desc, round_stats,
+                     host_stats);
   return hipGetLastError();
 }
 

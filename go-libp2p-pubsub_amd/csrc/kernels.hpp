@@ -64,6 +64,7 @@ struct TopicDev {
   uint32_t n_nodes;  // nodes in the topic
   uint32_t W;        // 64-message words per node in this window (0 = idle)
   uint32_t flags;    // kTopic*
+  uint32_t seed_lo, seed_n;  // the topic's round-0 seeds (k_window_init applies them when asked)
 };
 
 // One root injection: words of a topic root that start flooding in a round.
@@ -136,7 +137,6 @@ struct PullArgs {
   uint8_t* gen;
   uint16_t* hop_rec;
   uint64_t* partials;  // [n_blocks][kNumCtr]
-  uint64_t* scratch;   // 1024 x 1 KiB: stores of lanes past a run's end
   uint32_t gen_cur;
   uint32_t dbg;
   uint32_t slot_mod;   // block b adds its counters into partial slot b % slot_mod (zeroed per window)
@@ -176,9 +176,31 @@ constexpr int kFlagsPerBlock = kBlock * kFlagsPerThread;  // 4096 nodes
 constexpr int kFlagBlockShift = 12;
 
 // host-side launchers (kernels.hip)
+// Per-window parameters (topic table, seeds, reduce descriptors) copied by
+// one small kernel straight from the pinned staging slot (device-mapped host
+// memory): one launch instead of a blit per array and its barrier packets.
+constexpr uint32_t kStageMax = 4;
+struct StageCopy {
+  const uint32_t* src[kStageMax];
+  uint32_t* dst[kStageMax];
+  uint32_t words[kStageMax];
+  uint32_t n;
+};
+hipError_t launch_stage_copy(const StageCopy& c, hipStream_t s);
+// Window start: zero and stamp the roots' rows (every row of a mesh topic);
+// optionally in the same launch (WindowStart): the staged per-window copies
+// (topics_src / seeds_src then point at the staged sources), the round-0
+// seeds of tree roots (each topic's block, after its zeroing), and zeroing
+// of the pull partial slots.
+struct WindowStart {
+  StageCopy copy{};
+  const SeedDev* seeds = nullptr;  // apply round-0 seeds (tree topics only)
+  uint64_t* zero = nullptr;        // words to clear
+  uint64_t zero_words = 0;
+};
 hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_t* seen,
                               uint64_t* a0, uint64_t* a1, uint8_t* gen, uint32_t gen_cur,
-                              bool any_mesh, hipStream_t s);
+                              bool any_mesh, const WindowStart& ws, hipStream_t s);
 // stamp: mark the nodes' generation current (compaction mode)
 hipError_t launch_init_nodes(const uint32_t* nodes, uint32_t n, const uint16_t* node_topic,
                              const TopicDev* topics, uint64_t* seen, uint64_t* a0, uint64_t* a1,
@@ -202,17 +224,7 @@ hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, bool 
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
                        uint32_t grid, uint32_t round, bool record, bool fuse, uint32_t unroll, uint32_t nt,
                        hipStream_t s);
-// Per-window parameters (topic table, seeds, reduce descriptors) copied by
-// one small kernel straight from the pinned staging slot (device-mapped host
-// memory): one launch instead of a blit per array and its barrier packets.
-constexpr uint32_t kStageMax = 4;
-struct StageCopy {
-  const uint32_t* src[kStageMax];
-  uint32_t* dst[kStageMax];
-  uint32_t words[kStageMax];
-  uint32_t n;
-};
-hipError_t launch_stage_copy(const StageCopy& c, hipStream_t s);
+
 // Level mode, top levels in one launch (one rank, every active topic
 // starting together): chunks of several rounds (PullChunk::pad = round),
 // each round's list padded to whole blocks of kBlock / 64 chunks.
@@ -220,8 +232,10 @@ hipError_t launch_pull_top(const PullArgs& a, const PullChunk* chunks, uint32_t 
                            bool record, hipStream_t s);
 // Level mode: round q's counters = sum of the partial slots desc[3q],
 // desc[3q] + desc[3q+2], ... < desc[3q+1], for q = 1..n_rounds.
+// host_stats (nullable): device-mapped pinned rows that receive the same
+// counters, so an asynchronous run needs no readback copy
 hipError_t launch_reduce_rounds(const uint64_t* partials, const uint32_t* desc, uint32_t n_rounds,
-                                uint64_t* round_stats, hipStream_t s);
+                                uint64_t* round_stats, uint64_t* host_stats, hipStream_t s);
 // second instance: entries the staged kernel leaves (mesh, split, wide rows,
 // fan-out > 64); writes the same counters to partials + n_waves*kNumCtr
 hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid,

@@ -24,7 +24,9 @@ def main():
     # production instances: no hop record (first template argument false);
     # the cache-policy variants (plain / nt stores) are one kernel to the
     # roofline, so their traffic is averaged over all of their dispatches
-    names = [k for k in summ if f"{kernel}<false" in k and "hbm_write_bytes_per_dispatch" in summ[k]]
+    # (k_pull: its top-levels launch k_pull_top is one of the launches too)
+    names = [k for k in summ if (f"{kernel}<false" in k or f"{kernel}_top<false" in k)
+             and "hbm_write_bytes_per_dispatch" in summ[k]]
     if not names:
         sys.exit(f"no {kernel}<false ...> dispatches with both counters in {run_dir}")
     disp = sum(summ[k]["WRITE_SIZE"]["dispatches"] for k in names)
