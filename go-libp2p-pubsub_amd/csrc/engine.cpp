@@ -132,6 +132,7 @@ struct ps_engine {
   bool level_push = false;       // PSAMD_LEVEL_PUSH=1: level mode with the push kernel (A/B)
   uint32_t pull_words = kPullWords;  // words per pull chunk (PSAMD_PULL_WORDS)
   uint64_t pull_top_max = 32ull << 20;  // top launch: leading rounds writing <= this many row bytes each (PSAMD_PULL_TOP_MB, 0 = off)
+  bool pull_wave_flush = false;  // PSAMD_PULL_WAVE_FLUSH=1: per-wave counter atomics (A/B: -0.3 %)
   bool fold_window = true;  // PSAMD_FOLD_WINDOW=0: separate copy / seed / clear launches (A/B)
   uint32_t pull_top_first = 0, pull_top_last = 0;  // rounds of the cached top launch (0: none)
   uint32_t pull_unroll = 8;          // loads in flight per lane (PSAMD_PULL_UNROLL: 4 or 8)
@@ -1605,6 +1606,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         pa.dbg = a.dbg;
         pa.slot_mod = kPullSlots;
         pa.slot_base = r;
+        pa.wave_flush = e->pull_wave_flush;
         const PullChunk* ch = e->d_pull.as<PullChunk>() + e->pull_off[r];
         if (top) {
           HIP_TRY(launch_pull_top(pa, ch, e->pull_off[e->pull_top_last + 1] - e->pull_off[r], record, s),
@@ -1870,8 +1872,10 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_LEVEL_PUSH")) e->level_push = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_WORDS")) e->pull_words = std::max(64, std::atoi(v));
+  if (const char* v = std::getenv("PSAMD_PULL_WAVE_FLUSH")) e->pull_wave_flush = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FOLD_WINDOW")) e->fold_window = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_PULL_TOP_MB")) e->pull_top_max = std::strtoull(v, nullptr, 10) << 20;
+  if (const char* v = std::getenv("PSAMD_PULL_TOP_MB"))  // fractions allowed (tests split small windows)
+    e->pull_top_max = static_cast<uint64_t>(std::max(0.0, std::strtod(v, nullptr)) * 1048576.0);
   if (const char* v = std::getenv("PSAMD_PULL_FUSE")) e->no_fuse = std::atoi(v) == 0;
   if (const char* v = std::getenv("PSAMD_PULL_UNROLL")) e->pull_unroll = std::atoi(v) <= 4 ? 4 : 8;
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||

@@ -976,11 +976,31 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
 }
 
 // Block-level counters of one level into partial slot `slot`.
+__device__ __forceinline__ uint64_t pull_ctr_pick(const uint64_t* t, uint32_t k) {
+  switch (k) {
+    case kCtrDeliveries: return t[0];
+    case kCtrEntries: return t[4];
+    case kCtrEntryWords: return t[5];
+    case kCtrChildren: return t[2];
+    case kCtrMeshChildren: return t[3];  // pull mode: nodes reached (generation writes)
+    case kCtrSeenWrites: return t[1];
+    default: return 0;
+  }
+}
+
+// wave_flush: each wave adds its own sums (no block barrier, so a finished
+// wave retires at once); else the block folds its waves first
 __device__ __forceinline__ void pull_flush(const PullCtr& c, uint64_t* partials, uint64_t slot,
-                                           uint32_t lane, uint32_t wid) {
+                                           uint32_t lane, uint32_t wid, bool wave_flush) {
   __shared__ uint64_t red[kBlock / 64][6];
   const uint64_t v6[6] = {wave_sum_u64(c.deliv), wave_sum_u64(c.sw), wave_sum_u64(c.kids),
                           wave_sum_u64(c.reached), wave_sum_u64(c.parents), wave_sum_u64(c.pwords)};
+  if (wave_flush) {
+    const uint64_t v = lane < kNumCtr ? pull_ctr_pick(v6, lane) : 0;
+    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(partials + slot * kNumCtr + lane),
+                     static_cast<unsigned long long>(v));
+    return;
+  }
   if (lane == 0)
 #pragma unroll
     for (int q = 0; q < 6; ++q) red[wid][q] = v6[q];
@@ -990,16 +1010,7 @@ __device__ __forceinline__ void pull_flush(const PullCtr& c, uint64_t* partials,
     for (int w = 0; w < kBlock / 64; ++w)
 #pragma unroll
       for (int q = 0; q < 6; ++q) t[q] += red[w][q];
-    uint64_t v = 0;
-    switch (threadIdx.x) {
-      case kCtrDeliveries: v = t[0]; break;
-      case kCtrEntries: v = t[4]; break;
-      case kCtrEntryWords: v = t[5]; break;
-      case kCtrChildren: v = t[2]; break;
-      case kCtrMeshChildren: v = t[3]; break;  // pull mode: nodes reached (generation writes)
-      case kCtrSeenWrites: v = t[1]; break;
-      default: v = 0;
-    }
+    const uint64_t v = pull_ctr_pick(t, threadIdx.x);
     // blocks share a slot (slot_mod): partials are zeroed per window
     if (v) atomicAdd(reinterpret_cast<unsigned long long*>(partials + slot * kNumCtr + threadIdx.x),
                      static_cast<unsigned long long>(v));
@@ -1045,10 +1056,10 @@ __global__ __launch_bounds__(kBlock, kU <= 4 ? 8 : 1) void k_pull(PullArgs a, co
       pull_stream<kRecord, kU, kNT>(a, P, ch.g_begin, n2, src + n1, lane, wave, round + 1, c2);
   }
   if constexpr (kFuse) {
-    pull_flush(c1, a.partials, 2ull * (blockIdx.x % a.slot_mod), lane, wid);
-    pull_flush(c2, a.partials, 2ull * (blockIdx.x % a.slot_mod) + 1, lane, wid);
+    pull_flush(c1, a.partials, 2ull * (blockIdx.x % a.slot_mod), lane, wid, a.wave_flush);
+    pull_flush(c2, a.partials, 2ull * (blockIdx.x % a.slot_mod) + 1, lane, wid, a.wave_flush);
   } else {
-    pull_flush(c1, a.partials, blockIdx.x % a.slot_mod, lane, wid);
+    pull_flush(c1, a.partials, blockIdx.x % a.slot_mod, lane, wid, a.wave_flush);
   }
 }
 
@@ -1123,7 +1134,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_pull_top(PullArgs a, const PullCh
       pull_stream<kRecord, 8, 0>(a, P, ch.node_begin, n1, src, lane, wave, ch.pad, c1);
     }
   }
-  pull_flush(c1, a.partials, (q0 - a.slot_base) * kPullSlots + blockIdx.x % kPullSlots, lane, wid);
+  pull_flush(c1, a.partials, (q0 - a.slot_base) * kPullSlots + blockIdx.x % kPullSlots, lane, wid, a.wave_flush);
 }
 
 __global__ __launch_bounds__(kBlock) void k_stage_copy(StageCopy c) {

@@ -141,6 +141,7 @@ struct PullArgs {
   uint32_t dbg;
   uint32_t slot_mod;   // block b adds its counters into partial slot b % slot_mod (zeroed per window)
   uint32_t slot_base;  // top launch: round q's slots start at (q - slot_base) * kPullSlots
+  uint32_t wave_flush;  // counters added per wave (no block barrier) instead of per block
 };
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch
 
