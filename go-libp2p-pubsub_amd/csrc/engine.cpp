@@ -997,8 +997,19 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
         rb[q] += static_cast<uint64_t>(T.level_off[d + 1] - T.level_off[d]) * tab[t].W * 8;
       }
     }
+    // multi-GPU: the top launch ends above this rank's first remote-fed level
+    // (those rows arrive by the exchange of their round, after the launch);
+    // a rank owning no top nodes gets empty rounds
+    uint32_t cap = rounds;
+    if (e->world > 1)
+      for (uint32_t t = 0; t < nt; ++t) {
+        if (!tab[t].W) continue;
+        for (const auto& c : e->topics[t].cross)
+          if (c.to == static_cast<uint32_t>(e->rank) && c.from != c.to)
+            cap = std::min(cap, tstart[t] + c.level);  // level c.level + 1 is remote-fed here
+      }
     uint32_t last = 0;
-    for (uint32_t q = s0 + 1; s0 != ~0u && q <= rounds && q <= s0 + kPullTopLevels && rb[q] &&
+    for (uint32_t q = s0 + 1; s0 != ~0u && q <= cap && q <= s0 + kPullTopLevels && rb[q] &&
                             rb[q] <= e->pull_top_max;
          ++q)
       last = q;
@@ -1337,7 +1348,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   for (uint32_t t = 0; t < nt && fuse; ++t)
     if (tab[t].W && tstart[t] != max_start) fuse = false;
   if (level) {
-    bool top_ok = pull && world == 1;  // one launch for the leading small rounds
+    bool top_ok = pull;  // one launch for the leading small rounds
     for (uint32_t t = 0; t < nt && top_ok; ++t)
       if (tab[t].W && tstart[t] != max_start) top_ok = false;
     int rc2 = pull ? build_pull_chunks(e, tab, tstart, planned0, &fuse, top_ok)
