@@ -329,10 +329,19 @@ void partition_topic(const std::vector<uint32_t>& order, const std::vector<uint3
   // topic's nodes whatever the topic's message weight (hashing the subtree
   // roots left 14 % imbalance at 8 ranks on cfg3)
   std::vector<uint64_t> size(subtree ? n : 0, 0);
+  // subtree mode: the levels above L (< 64 * world nodes each) stay whole
+  // with the root's owner, so edges cross ranks only from level L - 1 into
+  // the level-L subtrees: one exchange round per topic, and that rank runs
+  // the top levels as one launch (k_pull_top)
+  const int32_t top_owner = n ? static_cast<int32_t>(mix(order[0]) % static_cast<uint64_t>(world)) : 0;
+  uint64_t n_top = 0;
   for (size_t u = 0; u < n; ++u) {
     if (subtree && level[u] >= L) {
       anc[u] = level[u] == L ? static_cast<uint32_t>(u) : anc[bfs_parent[u]];
       size[anc[u]]++;
+    } else if (subtree) {
+      owner[u] = top_owner;
+      ++n_top;
     } else {
       owner[u] = static_cast<int32_t>(mix(order[u]) % static_cast<uint64_t>(world));
     }
@@ -345,6 +354,7 @@ void partition_topic(const std::vector<uint32_t>& order, const std::vector<uint3
     return size[a] != size[b] ? size[a] > size[b] : order[a] < order[b];
   });
   std::vector<uint64_t> load(world, 0);
+  load[top_owner] = n_top;  // the dealing evens out the top levels too
   for (uint32_t u : roots) {
     int32_t best = 0;
     for (int32_t q = 1; q < world; ++q)

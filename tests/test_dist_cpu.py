@@ -58,7 +58,10 @@ def test_subtree_partition_keeps_subtrees_whole(oracle_lib):
         cnt = np.bincount(d[d >= 0])
         L = int(np.nonzero(cnt >= 64 * world)[0][0])
         cross = [(p, c) for p in range(n) for c in cl[rp[p]:rp[p + 1]] if own[p] != own[c]]
-        assert all(d[p] < L for p, _ in cross)  # only top-level edges cross ranks
+        # only edges into the level-L subtrees cross ranks; the levels above
+        # L stay with the root's owner
+        assert all(d[p] == L - 1 for p, _ in cross)
+        assert len(set(own[d < L].tolist())) == 1
         share = np.bincount(own, minlength=world) / n
         # >= 64*world subtrees dealt largest first to the least-loaded rank
         assert share.min() > 0.9 / world and share.max() < 1.1 / world, share
