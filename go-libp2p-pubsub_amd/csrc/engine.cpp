@@ -135,7 +135,7 @@ struct ps_engine {
   bool pull_wave_flush = false;  // PSAMD_PULL_WAVE_FLUSH=1: per-wave counter atomics (A/B: -0.3 %)
   bool fold_window = true;  // PSAMD_FOLD_WINDOW=0: separate copy / seed / clear launches (A/B)
   uint32_t pull_top_first = 0, pull_top_last = 0;  // rounds of the cached top launch (0: none)
-  uint32_t pull_unroll = 8;          // loads in flight per lane (PSAMD_PULL_UNROLL: 4 or 8)
+  uint32_t pull_unroll = 8;          // loads in flight per lane (PSAMD_PULL_UNROLL: 4, 8 or 16)
 
   std::vector<TopicHost> topics;
   std::vector<uint8_t> live;
@@ -1898,7 +1898,10 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_PULL_TOP_MB"))  // fractions allowed (tests split small windows)
     e->pull_top_max = static_cast<uint64_t>(std::max(0.0, std::strtod(v, nullptr)) * 1048576.0);
   if (const char* v = std::getenv("PSAMD_PULL_FUSE")) e->no_fuse = std::atoi(v) == 0;
-  if (const char* v = std::getenv("PSAMD_PULL_UNROLL")) e->pull_unroll = std::atoi(v) <= 4 ? 4 : 8;
+  if (const char* v = std::getenv("PSAMD_PULL_UNROLL")) {
+    const int u = std::atoi(v);
+    e->pull_unroll = u <= 4 ? 4 : (u >= 16 ? 16 : 8);
+  }
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess) {
     delete e;

@@ -1481,6 +1481,8 @@ hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_ch
       PSAMD_PULL(true, true, 8);
     else
       PSAMD_PULL(true, false, 8);
+  } else if (nt == 1 && !fuse && unroll >= 16) {  // A/B: 16 loads in flight (pair with 2048-word chunks)
+    hipLaunchKernelGGL((k_pull<false, false, 16, 1>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
   } else if (nt && !fuse && unroll > 4) {
     if (nt == 1)
       hipLaunchKernelGGL((k_pull<false, false, 8, 1>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
