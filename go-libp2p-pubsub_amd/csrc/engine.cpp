@@ -154,7 +154,7 @@ struct ps_engine {
   bool pull_fused = false;  // the cached chunks are fused (two levels per launch)
   bool no_fuse = true;      // PSAMD_PULL_FUSE=1: two levels per pull launch (A/B; slower)
   std::vector<uint32_t> pull_off;
-  DevBuf d_pull;
+  DevBuf d_pull, d_path_live;
 
   // fused node space (host mirror)
   uint32_t n_nodes = 0, n_pad = 16;
@@ -865,6 +865,11 @@ int upload_graph(ps_engine* e) {
     HIP_TRY(e->d_blk.ensure(n_blk), "alloc block flags");
     HIP_TRY(hipMemsetAsync(e->d_blk.p, 0, e->d_blk.bytes, e->stream), "clear block flags");
     HIP_TRY(e->d_gen.ensure(e->n_pad + 16), "alloc generations");
+    {
+      bool fresh_pl = false;  // stale entries carry older epochs; fresh memory is zeroed
+      HIP_TRY(e->d_path_live.ensure((static_cast<size_t>(e->n_pad) + 16) * 4, &fresh_pl), "alloc path-live");
+      if (fresh_pl) HIP_TRY(hipMemsetAsync(e->d_path_live.p, 0, e->d_path_live.bytes, e->stream), "clear path-live");
+    }
     e->n_remote_fed = static_cast<uint32_t>(e->remote_fed.size());
     HIP_TRY(e->d_remote_fed.ensure(std::max<size_t>(e->remote_fed.size(), 1) * 4), "alloc remote list");
     if (!e->remote_fed.empty())
@@ -1628,6 +1633,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         pa.slot_mod = kPullSlots;
         pa.slot_base = r;
         pa.wave_flush = e->pull_wave_flush;
+        pa.path_live = e->d_path_live.as<uint32_t>();
+        pa.pl_epoch = static_cast<uint32_t>(e->flags_epoch % ((1u << 30) - 1)) + 1;
         const PullChunk* ch = e->d_pull.as<PullChunk>() + e->pull_off[r];
         if (top) {
           HIP_TRY(launch_pull_top(pa, ch, e->pull_off[e->pull_top_last + 1] - e->pull_off[r], record, s),

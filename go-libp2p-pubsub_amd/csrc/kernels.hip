@@ -1086,15 +1086,27 @@ __device__ __forceinline__ void pull_resolve_top(const PullArgs& a, const PullTo
     }
     uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
     if (lane == 0) prev = nb + j0 > P.nbase ? a.node_parent[nb + j0 - 1] : kNoneNode;
-    // up: the parent was reached (root reached, every ancestor below it live)
-    bool up = in && root_up && p != kNoneNode;
-    uint32_t q = p;
-    for (uint32_t step = 0; up && q != P.root; ++step) {
-      const uint32_t fq = a.node_flags[q];
-      const uint32_t pq = a.node_parent[q];
-      up = (fq & kNodeLive) && pq != kNoneNode && step < 2 * kPullTopLevels;  // a walk spans < kPullTopLevels
-      q = pq;
+    // up_path: every ancestor between the root and the node is live (the
+    // parent is reached iff the root is).  Kept per node with the flags epoch
+    // (path_live: epoch << 2 | up_path << 1 | up_path && live), so only the
+    // first window after a graph or flags change walks.
+    const uint32_t e0 = in ? a.path_live[nb + j] : 0u;
+    bool up_path;
+    if (in && (e0 >> 2) == a.pl_epoch) {
+      up_path = (e0 >> 1) & 1u;
+    } else {
+      up_path = in && P.root != kNoneNode && p != kNoneNode;
+      uint32_t q = p;
+      for (uint32_t step = 0; up_path && q != P.root; ++step) {
+        const uint32_t fq = a.node_flags[q];
+        const uint32_t pq = a.node_parent[q];
+        up_path = (fq & kNodeLive) && pq != kNoneNode && step < 2 * kPullTopLevels;  // a walk spans < kPullTopLevels
+        q = pq;
+      }
+      if (in)
+        a.path_live[nb + j] = a.pl_epoch << 2 | (up_path ? 2u : 0u) | (up_path && (f & kNodeLive) ? 1u : 0u);
     }
+    const bool up = root_up && up_path;
     const bool ok = up && (f & kNodeLive);
     if (in) src[j] = ok ? P.root : kNoneNode;
     if (ok && !(a.dbg & kDbgNoByteStores)) a.gen[nb + j] = static_cast<uint8_t>(cur);

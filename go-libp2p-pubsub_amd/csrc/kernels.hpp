@@ -142,6 +142,8 @@ struct PullArgs {
   uint32_t slot_mod;   // block b adds its counters into partial slot b % slot_mod (zeroed per window)
   uint32_t slot_base;  // top launch: round q's slots start at (q - slot_base) * kPullSlots
   uint32_t wave_flush;  // counters added per wave (no block barrier) instead of per block
+  uint32_t* path_live;  // k_pull_top: per node, epoch << 2 | parent path live << 1 | node path live
+  uint32_t pl_epoch;    // current flags epoch (< 2^30, never 0)
 };
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch
 

@@ -108,3 +108,30 @@ def test_top_no_record_counts(monkeypatch):
     assert da["frontier_per_round"] == db["frontier_per_round"]
     assert da["deliveries_per_round"] == db["deliveries_per_round"]
     assert db["expand_launches"] < da["expand_launches"]  # the top launch replaced several
+
+
+def test_top_cache_follows_live_changes():
+    """The per-node path-liveness the top launch keeps between windows is
+    dropped when the live mask changes: kill and revive top-level peers
+    between runs of one engine, each run equal to the restatement."""
+    rng = np.random.default_rng(9)
+    n = 3000
+    parent = random_tree(rng, n, 0, fan=3)
+    rp, cl = O.parents_to_csr(parent)
+    live = np.ones(n, dtype=np.uint8)
+    kids = np.nonzero(parent == 0)[0]
+    grand = np.nonzero(np.isin(parent, kids))[0]
+    with PE.Engine(n, 1, record_hops=True) as eng:
+        eng.set_tree(0, 0, parent)
+        for step, change in enumerate([None, kids[:1], grand[:3], None, "revive"]):
+            if isinstance(change, str):
+                live[:] = 1
+            elif change is not None:
+                live[change] = 0
+            eng.set_live(live)
+            first = eng.publish(np.zeros(70))
+            st = eng.run()
+            total, oh, _ = O.disseminate(rp, cl, 0, live, 1)
+            assert st.deliveries == total * 70, step
+            for m in (0, 69):
+                assert np.array_equal(eng.hops(first + m), oh[0]), (step, m)
