@@ -133,6 +133,7 @@ struct ps_engine {
   uint32_t pull_words = kPullWords;  // words per pull chunk (PSAMD_PULL_WORDS)
   uint64_t pull_top_max = 32ull << 20;  // top launch: leading rounds writing <= this many row bytes each (PSAMD_PULL_TOP_MB, 0 = off)
   bool pull_wave_flush = false;  // PSAMD_PULL_WAVE_FLUSH=1: per-wave counter atomics (A/B: -0.3 %)
+  bool chunk_parents = true;  // PSAMD_CHUNK_PARENTS=0: GPU-built graphs without parent staging (A/B)
   bool fold_window = true;  // PSAMD_FOLD_WINDOW=0: separate copy / seed / clear launches (A/B)
   uint32_t pull_top_first = 0, pull_top_last = 0;  // rounds of the cached top launch (0: none)
   uint32_t pull_unroll = 8;          // loads in flight per lane (PSAMD_PULL_UNROLL: 4, 8 or 16)
@@ -1110,6 +1111,10 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
     HIP_TRY(hipMemcpyAsync(e->d_pull.p, C.data(), C.size() * sizeof(PullChunk),
                            hipMemcpyHostToDevice, e->stream),
             "upload pull chunks");
+  if (gpu && !C.empty() && e->chunk_parents)  // parent ranges for the generation staging
+    HIP_TRY(launch_chunk_parents(e->d_pull.as<PullChunk>(), static_cast<uint32_t>(C.size()),
+                                 e->d_node_parent.as<uint32_t>(), e->stream),
+            "chunk parents");
   e->pull_key = key;
   return PS_OK;
 }
@@ -1901,6 +1906,7 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_LEVEL_PUSH")) e->level_push = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_WORDS")) e->pull_words = std::max(64, std::atoi(v));
   if (const char* v = std::getenv("PSAMD_PULL_WAVE_FLUSH")) e->pull_wave_flush = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_CHUNK_PARENTS")) e->chunk_parents = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FOLD_WINDOW")) e->fold_window = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_TOP_MB"))  // fractions allowed (tests split small windows)
     e->pull_top_max = static_cast<uint64_t>(std::max(0.0, std::strtod(v, nullptr)) * 1048576.0);

@@ -1149,6 +1149,18 @@ __global__ __launch_bounds__(kBlock, 1) void k_pull_top(PullArgs a, const PullCh
   pull_flush(c1, a.partials, (q0 - a.slot_base) * kPullSlots + blockIdx.x % kPullSlots, lane, wid, a.wave_flush);
 }
 
+// GPU-built node spaces have no host mirror of node_parent: the chunks'
+// parent ranges (k_pull's generation staging) are filled in on the device.
+__global__ __launch_bounds__(kBlock) void k_chunk_parents(PullChunk* __restrict__ chunks, uint32_t n,
+                                                          const uint32_t* __restrict__ node_parent) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  PullChunk& c = chunks[i];
+  if (c.node_end <= c.node_begin) return;
+  c.p_lo = node_parent[c.node_begin];
+  c.p_hi = node_parent[c.node_end - 1];
+}
+
 __global__ __launch_bounds__(kBlock) void k_stage_copy(StageCopy c) {
   const uint32_t tid = blockIdx.x * kBlock + threadIdx.x, nth = gridDim.x * kBlock;
   for (uint32_t k = 0; k < c.n; ++k)
@@ -1525,6 +1537,12 @@ hipError_t launch_pull_top(const PullArgs& a, const PullChunk* chunks, uint32_t 
     hipLaunchKernelGGL(k_pull_top<true>, dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks);
   else
     hipLaunchKernelGGL(k_pull_top<false>, dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks);
+  return hipGetLastError();
+}
+
+hipError_t launch_chunk_parents(PullChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_chunk_parents, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, chunks, n, node_parent);
   return hipGetLastError();
 }
 

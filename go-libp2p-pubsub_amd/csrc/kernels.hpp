@@ -228,6 +228,8 @@ hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_ch
                        uint32_t grid, uint32_t round, bool record, bool fuse, uint32_t unroll, uint32_t nt,
                        hipStream_t s);
 
+// Fills PullChunk::p_lo / p_hi from the device node_parent (GPU-built graphs).
+hipError_t launch_chunk_parents(PullChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s);
 // Level mode, top levels in one launch (one rank, every active topic
 // starting together): chunks of several rounds (PullChunk::pad = round),
 // each round's list padded to whole blocks of kBlock / 64 chunks.
