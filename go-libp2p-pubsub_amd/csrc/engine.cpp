@@ -131,7 +131,7 @@ struct ps_engine {
   std::chrono::steady_clock::time_point t_run0;
   bool level_push = false;       // PSAMD_LEVEL_PUSH=1: level mode with the push kernel (A/B)
   uint32_t pull_words = kPullWords;  // words per pull chunk (PSAMD_PULL_WORDS)
-  uint64_t pull_top_max = 32ull << 20;  // top launch: leading rounds writing <= this many row bytes each (PSAMD_PULL_TOP_MB, 0 = off)
+  uint64_t pull_top_max = ~0ull;  // top launch: leading rounds writing <= this many row bytes each (PSAMD_PULL_TOP_MB, 0 = off)
   bool pull_wave_flush = false;  // PSAMD_PULL_WAVE_FLUSH=1: per-wave counter atomics (A/B: -0.3 %)
   bool chunk_parents = true;  // PSAMD_CHUNK_PARENTS=0: GPU-built graphs without parent staging (A/B)
   bool fold_window = true;  // PSAMD_FOLD_WINDOW=0: separate copy / seed / clear launches (A/B)
@@ -1642,6 +1642,12 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         pa.pl_epoch = static_cast<uint32_t>(e->flags_epoch % ((1u << 30) - 1)) + 1;
         const PullChunk* ch = e->d_pull.as<PullChunk>() + e->pull_off[r];
         if (top) {
+          // no row of the top launch is read back by it (every reached node
+          // copies the root's row): its large rounds store non-temporally
+          if (e->pull_nt & 1u)
+            for (uint32_t q = r; q <= e->pull_top_last && q - r < 32; ++q)
+              if (q < e->pull_bytes.size() && (e->pull_bytes[q] >= e->pull_nt_min || q == planned0))
+                pa.top_nt |= 1u << (q - r);
           HIP_TRY(launch_pull_top(pa, ch, e->pull_off[e->pull_top_last + 1] - e->pull_off[r], record, s),
                   "pull top");
         } else {

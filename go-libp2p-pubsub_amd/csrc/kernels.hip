@@ -1143,7 +1143,12 @@ __global__ __launch_bounds__(kBlock, 1) void k_pull_top(PullArgs a, const PullCh
       P.root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
       const uint32_t n1 = ch.node_end - ch.node_begin;
       pull_resolve_top(a, P, ch.node_begin, n1, src, lane, cur, c1);
-      pull_stream<kRecord, 8, 0>(a, P, ch.node_begin, n1, src, lane, wave, ch.pad, c1);
+      // wave-uniform: the large rounds (rows nobody reads back in this
+      // launch, and too many for the MALL) store non-temporally
+      if ((a.top_nt >> (ch.pad - a.slot_base)) & 1u)
+        pull_stream<kRecord, 8, 1>(a, P, ch.node_begin, n1, src, lane, wave, ch.pad, c1);
+      else
+        pull_stream<kRecord, 8, 0>(a, P, ch.node_begin, n1, src, lane, wave, ch.pad, c1);
     }
   }
   pull_flush(c1, a.partials, (q0 - a.slot_base) * kPullSlots + blockIdx.x % kPullSlots, lane, wid, a.wave_flush);

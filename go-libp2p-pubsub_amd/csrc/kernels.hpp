@@ -144,6 +144,7 @@ struct PullArgs {
   uint32_t wave_flush;  // counters added per wave (no block barrier) instead of per block
   uint32_t* path_live;  // k_pull_top: per node, epoch << 2 | parent path live << 1 | node path live
   uint32_t pl_epoch;    // current flags epoch (< 2^30, never 0)
+  uint32_t top_nt;      // k_pull_top: bit q - slot_base set = round q stores its rows non-temporally
 };
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch
 
