@@ -131,6 +131,8 @@ struct ps_engine {
   std::chrono::steady_clock::time_point t_run0;
   bool level_push = false;       // PSAMD_LEVEL_PUSH=1: level mode with the push kernel (A/B)
   uint32_t pull_words = kPullWords;  // words per pull chunk (PSAMD_PULL_WORDS)
+  uint32_t top_lds = 0;  // k_pull_top: reserved dynamic LDS per block, caps its occupancy (PSAMD_TOP_LDS_KB)
+  uint32_t top_odd_wide = 1;  // k_pull_top odd-W unroll 16 (PSAMD_TOP_ODD_WIDE=0: 8)
   uint64_t pull_top_max = ~0ull;  // top launch: leading rounds writing <= this many row bytes each (PSAMD_PULL_TOP_MB, 0 = off)
   bool pull_wave_flush = false;  // PSAMD_PULL_WAVE_FLUSH=1: per-wave counter atomics (A/B: -0.3 %)
   bool chunk_parents = true;  // PSAMD_CHUNK_PARENTS=0: GPU-built graphs without parent staging (A/B)
@@ -1648,7 +1650,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
             for (uint32_t q = r; q <= e->pull_top_last && q - r < 32; ++q)
               if (q < e->pull_bytes.size() && (e->pull_bytes[q] >= e->pull_nt_min || q == planned0))
                 pa.top_nt |= 1u << (q - r);
-          HIP_TRY(launch_pull_top(pa, ch, e->pull_off[e->pull_top_last + 1] - e->pull_off[r], record, s),
+          pa.top_odd_wide = e->top_odd_wide;
+          HIP_TRY(launch_pull_top(pa, ch, e->pull_off[e->pull_top_last + 1] - e->pull_off[r], record, s,
+                                  e->top_lds),
                   "pull top");
         } else {
           // rows a later level re-reads while they can still sit in the 256 MB
@@ -1914,6 +1918,9 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_PULL_WAVE_FLUSH")) e->pull_wave_flush = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_CHUNK_PARENTS")) e->chunk_parents = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FOLD_WINDOW")) e->fold_window = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_TOP_LDS_KB"))
+    e->top_lds = static_cast<uint32_t>(std::min(60, std::max(0, std::atoi(v)))) << 10;
+  if (const char* v = std::getenv("PSAMD_TOP_ODD_WIDE")) e->top_odd_wide = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_TOP_MB"))  // fractions allowed (tests split small windows)
     e->pull_top_max = static_cast<uint64_t>(std::max(0.0, std::strtod(v, nullptr)) * 1048576.0);
   if (const char* v = std::getenv("PSAMD_PULL_FUSE")) e->no_fuse = std::atoi(v) == 0;

@@ -1144,11 +1144,20 @@ __global__ __launch_bounds__(kBlock, 1) void k_pull_top(PullArgs a, const PullCh
       const uint32_t n1 = ch.node_end - ch.node_begin;
       pull_resolve_top(a, P, ch.node_begin, n1, src, lane, cur, c1);
       // wave-uniform: the large rounds (rows nobody reads back in this
-      // launch, and too many for the MALL) store non-temporally
-      if ((a.top_nt >> (ch.pad - a.slot_base)) & 1u)
+      // launch, and too many for the MALL) store non-temporally.  Odd W moves
+      // one word per lane per access: twice the unroll keeps the same bytes
+      // in flight per wave as the 16-B pairs of even W
+      const bool nt = (a.top_nt >> (ch.pad - a.slot_base)) & 1u;
+      if ((P.W & 1u) && a.top_odd_wide) {
+        if (nt)
+          pull_stream<kRecord, 16, 1>(a, P, ch.node_begin, n1, src, lane, wave, ch.pad, c1);
+        else
+          pull_stream<kRecord, 16, 0>(a, P, ch.node_begin, n1, src, lane, wave, ch.pad, c1);
+      } else if (nt) {
         pull_stream<kRecord, 8, 1>(a, P, ch.node_begin, n1, src, lane, wave, ch.pad, c1);
-      else
+      } else {
         pull_stream<kRecord, 8, 0>(a, P, ch.node_begin, n1, src, lane, wave, ch.pad, c1);
+      }
     }
   }
   pull_flush(c1, a.partials, (q0 - a.slot_base) * kPullSlots + blockIdx.x % kPullSlots, lane, wid, a.wave_flush);
@@ -1534,14 +1543,16 @@ hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_ch
   return hipGetLastError();
 }
 
+// lds_bytes: dynamic LDS the kernel does not use, reserved only to cap the
+// blocks per CU (waves per SIMD) of the store stream
 hipError_t launch_pull_top(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                           bool record, hipStream_t s) {
+                           bool record, hipStream_t s, uint32_t lds_bytes) {
   if (n_chunks == 0) return hipSuccess;
   const uint32_t grid = (n_chunks + kBlock / 64 - 1) / (kBlock / 64);
   if (record)
-    hipLaunchKernelGGL(k_pull_top<true>, dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks);
+    hipLaunchKernelGGL(k_pull_top<true>, dim3(grid), dim3(kBlock), lds_bytes, s, a, chunks, n_chunks);
   else
-    hipLaunchKernelGGL(k_pull_top<false>, dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks);
+    hipLaunchKernelGGL(k_pull_top<false>, dim3(grid), dim3(kBlock), lds_bytes, s, a, chunks, n_chunks);
   return hipGetLastError();
 }
 

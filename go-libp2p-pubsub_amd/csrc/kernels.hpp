@@ -145,6 +145,7 @@ struct PullArgs {
   uint32_t* path_live;  // k_pull_top: per node, epoch << 2 | parent path live << 1 | node path live
   uint32_t pl_epoch;    // current flags epoch (< 2^30, never 0)
   uint32_t top_nt;      // k_pull_top: bit q - slot_base set = round q stores its rows non-temporally
+  uint32_t top_odd_wide;  // k_pull_top: odd-W rows stream 16 words in flight per lane (else 8)
 };
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch
 
@@ -235,7 +236,7 @@ hipError_t launch_chunk_parents(PullChunk* chunks, uint32_t n, const uint32_t* n
 // starting together): chunks of several rounds (PullChunk::pad = round),
 // each round's list padded to whole blocks of kBlock / 64 chunks.
 hipError_t launch_pull_top(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                           bool record, hipStream_t s);
+                           bool record, hipStream_t s, uint32_t lds_bytes = 0);
 // Level mode: round q's counters = sum of the partial slots desc[3q],
 // desc[3q] + desc[3q+2], ... < desc[3q+1], for q = 1..n_rounds.
 // host_stats (nullable): device-mapped pinned rows that receive the same
