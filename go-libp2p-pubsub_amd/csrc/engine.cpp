@@ -132,7 +132,7 @@ struct ps_engine {
   bool level_push = false;       // PSAMD_LEVEL_PUSH=1: level mode with the push kernel (A/B)
   uint32_t pull_words = kPullWords;  // words per pull chunk (PSAMD_PULL_WORDS)
   uint32_t top_lds = 0;  // k_pull_top: reserved dynamic LDS per block, caps its occupancy (PSAMD_TOP_LDS_KB)
-  uint32_t top_odd_wide = 1;  // k_pull_top odd-W unroll 16 (PSAMD_TOP_ODD_WIDE=0: 8)
+  uint32_t top_odd_wide = 2;  // k_pull_top odd W: 2 16-B pair stores, 1 8-B words 16 in flight, 0 8 in flight (PSAMD_TOP_ODD_WIDE)
   uint64_t pull_top_max = ~0ull;  // top launch: leading rounds writing <= this many row bytes each (PSAMD_PULL_TOP_MB, 0 = off)
   bool pull_wave_flush = false;  // PSAMD_PULL_WAVE_FLUSH=1: per-wave counter atomics (A/B: -0.3 %)
   bool chunk_parents = true;  // PSAMD_CHUNK_PARENTS=0: GPU-built graphs without parent staging (A/B)
@@ -1920,7 +1920,7 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_FOLD_WINDOW")) e->fold_window = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_TOP_LDS_KB"))
     e->top_lds = static_cast<uint32_t>(std::min(60, std::max(0, std::atoi(v)))) << 10;
-  if (const char* v = std::getenv("PSAMD_TOP_ODD_WIDE")) e->top_odd_wide = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_TOP_ODD_WIDE")) e->top_odd_wide = static_cast<uint32_t>(std::min(2, std::max(0, std::atoi(v))));
   if (const char* v = std::getenv("PSAMD_PULL_TOP_MB"))  // fractions allowed (tests split small windows)
     e->pull_top_max = static_cast<uint64_t>(std::max(0.0, std::strtod(v, nullptr)) * 1048576.0);
   if (const char* v = std::getenv("PSAMD_PULL_FUSE")) e->no_fuse = std::atoi(v) == 0;

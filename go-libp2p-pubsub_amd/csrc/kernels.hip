@@ -975,6 +975,76 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
   }
 }
 
+// k_pull_top, odd W: 16-B stores over the run's 16-B aligned word pairs.  A
+// pair may straddle two rows, so its two words are loaded separately (8 B
+// each, from each node's own source: the root's row, an L2 hit, or the word
+// itself for a skipped node).  A head word (run start not 16-B aligned) and a
+// tail word go as 8-B stores by lanes 0 and 1.  Lanes past the last pair
+// repeat it (same sources, same value, same address).
+template <uint32_t kU, uint32_t kNT>
+__device__ __forceinline__ void pull_stream_odd16(const PullArgs& a, const PullTopic& P, uint32_t nb,
+                                                  uint32_t nk, const uint32_t* src, uint32_t lane,
+                                                  PullCtr& c) {
+  const uint32_t W = P.W;
+  const uint32_t total = nk * W;
+  uint64_t* const out = a.seen + P.base + static_cast<uint64_t>(nb) * W;
+  const uint32_t head = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out) >> 3) & 1u;
+  const float rw = 1.0f / static_cast<float>(W);
+  // word i of the run: its node kk = i / W and word r (as in pull_stream)
+  auto split = [&](uint32_t i, int32_t& kk, int32_t& r) {
+    kk = static_cast<int32_t>(static_cast<float>(i) * rw);
+    r = static_cast<int32_t>(i) - kk * static_cast<int32_t>(W);
+    const int32_t lo = r < 0, hi = r >= static_cast<int32_t>(W);
+    kk += hi - lo;
+    r += (lo - hi) * static_cast<int32_t>(W);
+  };
+  auto at = [&](int32_t kk, int32_t r, uint32_t i, bool& go) -> const uint64_t* {
+    const uint32_t p = src[kk];
+    go = p != kNoneNode;
+    return go ? (p == P.root ? a.a_cur : a.seen) + P.base + static_cast<uint64_t>(p) * W + r : out + i;
+  };
+  const uint32_t body = total - head;
+  if (lane < 2 && (lane == 0 ? head : (body & 1u))) {
+    const uint32_t i = lane == 0 ? 0u : total - 1;
+    int32_t kk, r;
+    split(i, kk, r);
+    bool g;
+    const uint64_t v = *at(kk, r, i, g);
+    store_row8<(kNT & 1u) != 0>(out + i, v);
+    c.deliv += g ? __popcll(v) : 0u;
+    c.sw += g;
+  }
+  const uint32_t np = body >> 1;
+  for (uint32_t j0 = 0; j0 < np; j0 += kU * 64) {
+    uint64_t lo[kU], hi[kU];
+    bool glo[kU], ghi[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t j = j0 + u * 64 + lane;
+      const uint32_t i = head + 2 * (j < np ? j : np - 1);
+      int32_t kk, r;
+      split(i, kk, r);
+      int32_t kk2 = kk, r2 = r + 1;
+      if (r2 == static_cast<int32_t>(W)) {
+        kk2 = kk + 1;
+        r2 = 0;
+      }
+      lo[u] = *at(kk, r, i, glo[u]);
+      hi[u] = *at(kk2, r2, i + 1, ghi[u]);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t j = j0 + u * 64 + lane;
+      const uint32_t i = head + 2 * (j < np ? j : np - 1);
+      store_row16<(kNT & 1u) != 0>(out + i, uint4{static_cast<uint32_t>(lo[u]), static_cast<uint32_t>(lo[u] >> 32),
+                                                   static_cast<uint32_t>(hi[u]), static_cast<uint32_t>(hi[u] >> 32)});
+      const bool own = j < np;
+      c.deliv += own ? (glo[u] ? __popcll(lo[u]) : 0u) + (ghi[u] ? __popcll(hi[u]) : 0u) : 0u;
+      c.sw += own ? static_cast<uint32_t>(glo[u]) + static_cast<uint32_t>(ghi[u]) : 0u;
+    }
+  }
+}
+
 // Block-level counters of one level into partial slot `slot`.
 __device__ __forceinline__ uint64_t pull_ctr_pick(const uint64_t* t, uint32_t k) {
   switch (k) {
@@ -1148,7 +1218,12 @@ __global__ __launch_bounds__(kBlock, 1) void k_pull_top(PullArgs a, const PullCh
       // one word per lane per access: twice the unroll keeps the same bytes
       // in flight per wave as the 16-B pairs of even W
       const bool nt = (a.top_nt >> (ch.pad - a.slot_base)) & 1u;
-      if ((P.W & 1u) && a.top_odd_wide) {
+      if (!kRecord && (P.W & 1u) && a.top_odd_wide == 2) {
+        if (nt)
+          pull_stream_odd16<8, 1>(a, P, ch.node_begin, n1, src, lane, c1);
+        else
+          pull_stream_odd16<8, 0>(a, P, ch.node_begin, n1, src, lane, c1);
+      } else if ((P.W & 1u) && a.top_odd_wide) {
         if (nt)
           pull_stream<kRecord, 16, 1>(a, P, ch.node_begin, n1, src, lane, wave, ch.pad, c1);
         else

@@ -135,3 +135,46 @@ def test_top_cache_follows_live_changes():
             assert st.deliveries == total * 70, step
             for m in (0, 69):
                 assert np.array_equal(eng.hops(first + m), oh[0]), (step, m)
+
+
+def _odd_digests(monkeypatch, odd_mode, record, n, topics, live, msg_topics):
+    """Seen digests and deliveries of two back-to-back runs (the second reads
+    the path-liveness cache) with PSAMD_TOP_ODD_WIDE = odd_mode."""
+    monkeypatch.delenv("PSAMD_PULL_TOP_MB", raising=False)
+    monkeypatch.setenv("PSAMD_TOP_ODD_WIDE", str(odd_mode))
+    out = []
+    with PE.Engine(n, len(topics), record_hops=record) as eng:
+        for t, (root, parent) in enumerate(topics):
+            eng.set_tree(t, root, parent)
+        eng.set_live(live)
+        for _ in range(2):
+            eng.publish(msg_topics)
+            st = eng.run()
+            out.append((st.deliveries, st.as_dict()["deliveries_per_round"], eng.seen_digest()))
+    return out
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_top_odd_row_stores(monkeypatch, seed):
+    """Odd W (rows of an odd number of 64-message words): the non-recording
+    launch stores aligned 16-B pairs that straddle two nodes' rows, with a
+    head and a tail word; its seen state must equal the per-word stream's and
+    the recording launch's (whose hops the oracle pins above), dead nodes
+    and odd run alignments included."""
+    rng = np.random.default_rng(700 + seed)
+    n = int(rng.integers(300, 3000))
+    nt = int(rng.integers(1, 4))
+    topics = []
+    for t in range(nt):
+        root = int(rng.integers(0, n))
+        topics.append((root, random_tree(rng, n, root, fan=int(rng.integers(2, 9)))))
+    live = rng.random(n) > 0.05
+    for root, _ in topics:
+        live[root] = True
+    # per topic an odd word count (1, 3, 5, 7, 9 words), last word ragged
+    counts = [64 * int(rng.choice([0, 2, 4, 6, 8])) + int(rng.integers(1, 65)) for _ in range(nt)]
+    msg_topics = rng.permutation(np.repeat(np.arange(nt), counts)).astype(np.uint32)
+    ref = _odd_digests(monkeypatch, 1, True, n, topics, live, msg_topics)
+    for mode in (2, 1, 0):
+        got = _odd_digests(monkeypatch, mode, False, n, topics, live, msg_topics)
+        assert got == ref, (mode, counts)
