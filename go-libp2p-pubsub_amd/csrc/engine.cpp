@@ -131,6 +131,7 @@ struct ps_engine {
   std::chrono::steady_clock::time_point t_run0;
   bool level_push = false;       // PSAMD_LEVEL_PUSH=1: level mode with the push kernel (A/B)
   uint32_t pull_words = kPullWords;  // words per pull chunk (PSAMD_PULL_WORDS)
+  uint32_t top_xcd = 0;  // k_pull_top: contiguous block range per XCD (PSAMD_TOP_XCD)
   uint32_t top_lds = 0;  // k_pull_top: reserved dynamic LDS per block, caps its occupancy (PSAMD_TOP_LDS_KB)
   uint32_t top_odd_wide = 2;  // k_pull_top odd W: 2 16-B pair stores, 1 8-B words 16 in flight, 0 8 in flight (PSAMD_TOP_ODD_WIDE)
   uint64_t pull_top_max = ~0ull;  // top launch: leading rounds writing <= this many row bytes each (PSAMD_PULL_TOP_MB, 0 = off)
@@ -1651,6 +1652,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
               if (q < e->pull_bytes.size() && (e->pull_bytes[q] >= e->pull_nt_min || q == planned0))
                 pa.top_nt |= 1u << (q - r);
           pa.top_odd_wide = e->top_odd_wide;
+          pa.xcd_remap = e->top_xcd;
           HIP_TRY(launch_pull_top(pa, ch, e->pull_off[e->pull_top_last + 1] - e->pull_off[r], record, s,
                                   e->top_lds),
                   "pull top");
@@ -1918,6 +1920,7 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_PULL_WAVE_FLUSH")) e->pull_wave_flush = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_CHUNK_PARENTS")) e->chunk_parents = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FOLD_WINDOW")) e->fold_window = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_TOP_XCD")) e->top_xcd = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_TOP_LDS_KB"))
     e->top_lds = static_cast<uint32_t>(std::min(60, std::max(0, std::atoi(v)))) << 10;
   if (const char* v = std::getenv("PSAMD_TOP_ODD_WIDE")) e->top_odd_wide = static_cast<uint32_t>(std::min(2, std::max(0, std::atoi(v))));

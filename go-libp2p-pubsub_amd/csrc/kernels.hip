@@ -1195,13 +1195,20 @@ __global__ __launch_bounds__(kBlock, 1) void k_pull_top(PullArgs a, const PullCh
   __shared__ uint32_t src_lds[kBlock / 64][kPullMaxKids];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t wave = blockIdx.x * (kBlock / 64) + wid;
+  // xcd_remap: blocks are dealt round-robin to the 8 XCDs; give XCD x one
+  // contiguous range of the chunk list (its own stretch of rows) instead
+  uint32_t blk = blockIdx.x;
+  if (a.xcd_remap) {
+    const uint32_t G = gridDim.x, q = G / 8, r = G % 8, x = blk % 8;
+    blk = x * q + (x < r ? x : r) + blk / 8;
+  }
+  const uint32_t wave = blk * (kBlock / 64) + wid;
   uint32_t* src = src_lds[wid];
   const uint32_t cur = a.gen_cur & 0xFF;
   PullCtr c1;
   // every chunk of a block belongs to one round (the host pads the rounds to
   // whole blocks): the block adds into that round's kPullSlots slots
-  const uint32_t q0 = chunks[blockIdx.x * (kBlock / 64)].pad;
+  const uint32_t q0 = chunks[blk * (kBlock / 64)].pad;
   if (wave < n_chunks) {
     const PullChunk ch = chunks[wave];
     if (ch.node_end > ch.node_begin) {  // padding chunks are empty
@@ -1235,7 +1242,7 @@ __global__ __launch_bounds__(kBlock, 1) void k_pull_top(PullArgs a, const PullCh
       }
     }
   }
-  pull_flush(c1, a.partials, (q0 - a.slot_base) * kPullSlots + blockIdx.x % kPullSlots, lane, wid, a.wave_flush);
+  pull_flush(c1, a.partials, (q0 - a.slot_base) * kPullSlots + blk % kPullSlots, lane, wid, a.wave_flush);
 }
 
 // GPU-built node spaces have no host mirror of node_parent: the chunks'

@@ -145,6 +145,7 @@ struct PullArgs {
   uint32_t* path_live;  // k_pull_top: per node, epoch << 2 | parent path live << 1 | node path live
   uint32_t pl_epoch;    // current flags epoch (< 2^30, never 0)
   uint32_t top_nt;      // k_pull_top: bit q - slot_base set = round q stores its rows non-temporally
+  uint32_t xcd_remap;  // k_pull_top: XCD x runs one contiguous range of the blocks
   uint32_t top_odd_wide;  // k_pull_top odd W: 2 = 16-B pair stores, 1 = 8-B words 16 in flight, 0 = 8 in flight
 };
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch

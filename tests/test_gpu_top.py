@@ -178,3 +178,7 @@ def test_top_odd_row_stores(monkeypatch, seed):
     for mode in (2, 1, 0):
         got = _odd_digests(monkeypatch, mode, False, n, topics, live, msg_topics)
         assert got == ref, (mode, counts)
+    # blocks dealt to the XCDs as contiguous ranges (PSAMD_TOP_XCD): same state
+    monkeypatch.setenv("PSAMD_TOP_XCD", "1")
+    assert _odd_digests(monkeypatch, 2, False, n, topics, live, msg_topics) == ref
+    assert _odd_digests(monkeypatch, 1, True, n, topics, live, msg_topics) == ref
