@@ -129,13 +129,10 @@ def pmc_traffic(kernel: str, workload: str):
 
 
 def hot_kernel(st):
-    """The launch family the roofline is quoted on: pull-mode windows that run
-    as one k_pull_top launch each (every level of the window) are labelled so,
-    to match the rocprofv3 kernel name."""
-    k = PE.MODE_KERNEL.get(st.expand_mode, "k_expand")
-    if k == "k_pull" and st.expand_launches == max(1, st.windows):
-        return "k_pull_top"
-    return k
+    """The kernel the roofline is quoted on (its rocprofv3 name): the one that
+    ran the window's rounds -- k_flood (one persistent launch per window),
+    k_pull (one launch per round) or k_expand (compaction mode)."""
+    return PE.MODE_KERNEL.get(st.expand_mode, "k_expand")
 
 
 def instrumented(eng, step, n):
@@ -318,8 +315,12 @@ def main():
                      "timing": "HIP events around every launch on the engine stream, "
                                "separate instrumented steps after the timed region",
                      "traffic_source": traffic_src},
-        "pair_model": {"bytes_per_delivery": PAIR_BYTES, "equiv_GBs": pair_gbs,
-                       "equiv_frac": pair_gbs / HBM_PEAK_GBS},
+        # SURVEY.md §8d's (peer,msg)-pair formulation: the HBM rate a pair-frontier
+        # engine would need for this delivery rate.  A model figure, NOT bandwidth
+        # this engine moves; compare roofline.frac, not this, with the peak.
+        "pair_model": {"bytes_per_delivery": PAIR_BYTES, "equiv_GBs_not_achievable": pair_gbs,
+                       "note": "model-equivalent rate of the 28.375 B/delivery pair formulation; "
+                               "this engine moves 64 messages per 8-B word (roofline.bytes_per_launch)"},
         "last_step": {"rounds": st.rounds, "windows": st.windows, "run_ms": st.run_ms,
                       "expand_ms": st.expand_ms, "host_ms": st.host_ms,
                       "edge_words": st.edge_words,

@@ -112,13 +112,9 @@ struct ps_engine {
   hipEvent_t ev_run0 = nullptr, ev_run1 = nullptr;
   std::vector<hipEvent_t> ev_k;  // pairs around expand launches
   uint32_t n_cus = 256, expand_grid = 2048;
-  bool no_single_start = false;  // PSAMD_NO_SINGLE_START=1: keep arrival rows (A/B)
-  bool no_level = false;         // PSAMD_NO_LEVEL=1: always compact the frontier (A/B)
-  uint32_t pull_nt = 1;          // k_pull cache policy: 1 nt row stores, 2 nt parent loads, 3 both, 0 plain (PSAMD_PULL_NT)
-  uint64_t pull_nt_min = 64ull << 20;  // nt only for rounds writing >= this many row bytes, and the last round
   std::vector<uint64_t> pull_bytes;    // row bytes written per round (pull chunks)
   bool host_timing = false;      // PSAMD_HOST_TIMING=1: host phase times to stderr
-  uint32_t small_place = 512;    // top levels up to this many nodes placed by one block (PSAMD_SMALL_PLACE, 0 = off)
+  uint32_t small_place = 512;    // top levels up to this many nodes placed by one block
   // GPU rebuild of the node space: on by default for one
   // rank and tree topics (PSAMD_GPU_BUILD=0: host build)
   bool gpu_build_on = true;
@@ -129,36 +125,35 @@ struct ps_engine {
   DevBuf d_tpar, d_anc0, d_anc1, d_dep0, d_dep1, d_keys0, d_skeys, d_local, d_deg, d_first, d_lvl,
       d_gstat, d_cub, d_pairs, d_live, d_roots, d_cnt, d_fidx, d_childoff;
   std::chrono::steady_clock::time_point t_run0;
-  bool level_push = false;       // PSAMD_LEVEL_PUSH=1: level mode with the push kernel (A/B)
-  uint32_t pull_words = kPullWords;  // words per pull chunk (PSAMD_PULL_WORDS)
-  uint32_t top_xcd = 0;  // k_pull_top: contiguous block range per XCD (PSAMD_TOP_XCD)
-  uint32_t top_lds = 0;  // k_pull_top: reserved dynamic LDS per block, caps its occupancy (PSAMD_TOP_LDS_KB)
-  uint32_t top_odd_wide = 2;  // k_pull_top odd W: 2 16-B pair stores, 1 8-B words 16 in flight, 0 8 in flight (PSAMD_TOP_ODD_WIDE)
-  uint64_t pull_top_max = ~0ull;  // top launch: leading rounds writing <= this many row bytes each (PSAMD_PULL_TOP_MB, 0 = off)
-  bool pull_wave_flush = false;  // PSAMD_PULL_WAVE_FLUSH=1: per-wave counter atomics (A/B: -0.3 %)
-  bool chunk_parents = true;  // PSAMD_CHUNK_PARENTS=0: GPU-built graphs without parent staging (A/B)
-  bool fold_window = true;  // PSAMD_FOLD_WINDOW=0: separate copy / seed / clear launches (A/B)
-  uint32_t pull_top_first = 0, pull_top_last = 0;  // rounds of the cached top launch (0: none)
-  uint32_t pull_unroll = 8;          // loads in flight per lane (PSAMD_PULL_UNROLL: 4, 8 or 16)
+  // k_flood: a single-rank level window in one persistent
+  // launch; PSAMD_FLOOD=0 runs one k_pull launch per round instead
+  bool flood_on = true;
+  bool flood_broken = false;  // a dependency wait timed out once: per-level launches from then on
+  uint32_t flood_grid = 0;    // resident blocks (0: k_flood unavailable)
+  uint32_t flood_words = kFloodWords;  // row words per task (PSAMD_FLOOD_WORDS)
+  uint32_t flood_epoch = 0;   // publish value of the last launch (done[] words never reset)
+  std::vector<uint64_t> flood_key;
+  std::vector<FloodTask> flood_tasks;
+  std::vector<FloodSeg> flood_segs;
+  std::vector<uint32_t> flood_slot0, flood_nslot;  // per round: partial counter slots
+  uint32_t flood_slots = 1;   // slots of a window (slot 0: the timeout word)
+  DevBuf d_flood_tasks, d_flood_segs, d_flood_done;
 
   std::vector<TopicHost> topics;
   std::vector<uint8_t> live;
   bool graph_dirty = true, flags_dirty = true;
   uint64_t graph_epoch = 0, flags_epoch = 0;  // bumped by every upload
 
-  // level mode: static per-round frontier of the window
-  std::vector<uint64_t> sched_key;  // (epochs, rounds, per-topic start) it was built for
-  std::vector<uint32_t> sched_host, sched_off, sched_cnt, woff_host, desc_host;
-  DevBuf d_sched, d_sched_cnt, d_woff;
+  // level mode, per-round counter slots and their reduce descriptors
+  std::vector<uint32_t> woff_host, desc_host;
+  DevBuf d_woff;
   // level mode, pull direction: per-round chunks of next-level nodes
   std::vector<uint64_t> pull_key;
   std::vector<PullChunk> pull_host;
   std::vector<uint32_t> split_host, split_off;  // multi-GPU: split parents per round
   DevBuf d_split;
-  bool pull_fused = false;  // the cached chunks are fused (two levels per launch)
-  bool no_fuse = true;      // PSAMD_PULL_FUSE=1: two levels per pull launch (A/B; slower)
   std::vector<uint32_t> pull_off;
-  DevBuf d_pull, d_path_live;
+  DevBuf d_pull;
 
   // fused node space (host mirror)
   uint32_t n_nodes = 0, n_pad = 16;
@@ -207,7 +202,7 @@ struct ps_engine {
     ps_stats st{};
     bool deferred = false;
     uint32_t r = 0, launches = 0;
-    bool pull = false, level = false;
+    uint32_t mode = PS_MODE_COMPACT;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the window's kernels
     uint64_t* hs = nullptr;  // pinned: (PS_MAX_ROUNDS + 1) x kNumCtr counters
     uint64_t* hs_dev = nullptr;  // hs, device-mapped (k_reduce_rounds writes it)
@@ -869,11 +864,6 @@ int upload_graph(ps_engine* e) {
     HIP_TRY(e->d_blk.ensure(n_blk), "alloc block flags");
     HIP_TRY(hipMemsetAsync(e->d_blk.p, 0, e->d_blk.bytes, e->stream), "clear block flags");
     HIP_TRY(e->d_gen.ensure(e->n_pad + 16), "alloc generations");
-    {
-      bool fresh_pl = false;  // stale entries carry older epochs; fresh memory is zeroed
-      HIP_TRY(e->d_path_live.ensure((static_cast<size_t>(e->n_pad) + 16) * 4, &fresh_pl), "alloc path-live");
-      if (fresh_pl) HIP_TRY(hipMemsetAsync(e->d_path_live.p, 0, e->d_path_live.bytes, e->stream), "clear path-live");
-    }
     e->n_remote_fed = static_cast<uint32_t>(e->remote_fed.size());
     HIP_TRY(e->d_remote_fed.ensure(std::max<size_t>(e->remote_fed.size(), 1) * 4), "alloc remote list");
     if (!e->remote_fed.empty())
@@ -921,189 +911,66 @@ int upload_graph(ps_engine* e) {
   return PS_OK;
 }
 
-// Level mode (DESIGN.md §5.4).  In a window whose topics are all trees with a
+// Level mode (DESIGN.md §5).  In a window whose topics are all trees with a
 // single start round s_t each, a node at BFS level d receives the window's
 // messages exactly in round s_t + d (if every ancestor is live) and forwards
-// them in round s_t + d + 1.  The frontier of round q is therefore known
-// before the window runs: the live internal nodes of level q - 1 - s_t of
-// every topic.  The schedule lists them round by round (node order inside a
-// topic, so siblings' rows stay adjacent); the expand kernel skips the
-// entries the messages did not reach, and no flags or compaction are needed.
-// Cached: rebuilt only when the node space, the flags or the start rounds
-// change.
-int build_schedule(ps_engine* e, const std::vector<TopicDev>& tab,
-                   const std::vector<uint32_t>& tstart, uint32_t rounds) {
+// them in round s_t + d + 1, so each round writes one BFS level per topic.
+//
+// Per-level launches (k_pull): round q writes the rows of BFS level q - s_t
+// of every active topic t (children pull from their parents), cut into
+// chunks of at most kPullMaxKids nodes and about kPullWords words, one wave
+// each.  Cached: rebuilt only when the node space, the flags or the start
+// rounds change.
+int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab, const std::vector<uint32_t>& tstart,
+                      uint32_t rounds) {
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
   std::vector<uint64_t> key{e->graph_epoch, e->flags_epoch, rounds};
-  for (uint32_t t = 0; t < nt; ++t) key.push_back(tab[t].W ? tstart[t] : ~0ull);
-  if (key == e->sched_key) return PS_OK;
-  e->sched_key.clear();
-  {
-    int rc = ensure_mirrors(e);
-    if (rc) return rc;
-  }
-  auto& S = e->sched_host;
-  auto& off = e->sched_off;
-  S.clear();
-  off.assign(rounds + 2, 0);
-  for (uint32_t q = 1; q <= rounds; ++q) {
-    off[q] = static_cast<uint32_t>(S.size());
-    for (uint32_t t = 0; t < nt; ++t) {
-      const TopicHost& T = e->topics[t];
-      if (tab[t].W == 0 || q < tstart[t] + 1) continue;
-      const uint32_t d = q - 1 - tstart[t];
-      if (d + 1 >= T.level_off.size()) continue;
-      for (uint32_t u = T.level_off[d]; u < T.level_off[d + 1]; ++u) {
-        const uint32_t node = T.nbase + u;
-        if ((e->node_flags[node] & (kNodeLive | kNodeInternal)) == (kNodeLive | kNodeInternal))
-          S.push_back(node);
-      }
-    }
-  }
-  off[rounds + 1] = static_cast<uint32_t>(S.size());
-  e->sched_cnt.assign(rounds + 2, 0);
-  for (uint32_t q = 1; q <= rounds; ++q) e->sched_cnt[q] = off[q + 1] - off[q];
-  HIP_TRY(e->d_sched.ensure(std::max<size_t>(S.size(), 1) * 4), "alloc schedule");
-  HIP_TRY(e->d_sched_cnt.ensure(e->sched_cnt.size() * 4), "alloc schedule counts");
-  if (!S.empty())
-    HIP_TRY(hipMemcpyAsync(e->d_sched.p, S.data(), S.size() * 4, hipMemcpyHostToDevice, e->stream),
-            "upload schedule");
-  HIP_TRY(hipMemcpyAsync(e->d_sched_cnt.p, e->sched_cnt.data(), e->sched_cnt.size() * 4,
-                         hipMemcpyHostToDevice, e->stream),
-          "upload schedule counts");
-  e->sched_key = key;
-  return PS_OK;
-}
-
-// Level mode, pull direction: round q writes the rows of
-// BFS level q - s_t of every active topic t (children pull from their
-// parents), cut into chunks of at most kPullMaxKids nodes and about
-// kPullWords words, one wave each.  Cached like the schedule.
-int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
-                      const std::vector<uint32_t>& tstart, uint32_t rounds, bool* fuse, bool top_ok) {
-  const uint32_t nt = static_cast<uint32_t>(e->topics.size());
-  std::vector<uint64_t> key{e->graph_epoch, e->flags_epoch, rounds, e->pull_words, *fuse ? 1ull : 0ull,
-                            top_ok ? e->pull_top_max : 0ull};
   for (uint32_t t = 0; t < nt; ++t) {
     key.push_back(tab[t].W ? tstart[t] : ~0ull);
     key.push_back(tab[t].W);
   }
-  if (key == e->pull_key) {
-    *fuse = e->pull_fused;
-    return PS_OK;
-  }
+  if (key == e->pull_key) return PS_OK;
   e->pull_key.clear();
-  // parent-range staging and fused launches read host mirrors of the node
-  // space; a GPU-built one (BFS order too) is used without them
+  // parent-range staging reads the host mirror of node_parent; a GPU-built
+  // node space (BFS order too) gets the ranges on the device
   const bool gpu = e->gpu_graph;
-  if (gpu) *fuse = false;
   auto& C = e->pull_host;
   auto& off = e->pull_off;
-  // top launch: the leading rounds (from the common start) that each write at
-  // most pull_top_max row bytes go into one k_pull_top launch
-  e->pull_top_first = e->pull_top_last = 0;
-  if (top_ok && !*fuse && e->pull_top_max) {
-    uint32_t s0 = ~0u;
-    for (uint32_t t = 0; t < nt; ++t)
-      if (tab[t].W) s0 = std::min(s0, tstart[t]);
-    std::vector<uint64_t> rb(rounds + 2, 0);
+  C.clear();
+  off.assign(rounds + 2, 0);
+  e->pull_bytes.assign(rounds + 2, 0);
+  e->split_host.clear();
+  e->split_off.assign(rounds + 2, 0);
+  for (uint32_t q = 1; q <= rounds; ++q) {
+    off[q] = static_cast<uint32_t>(C.size());
+    e->split_off[q] = static_cast<uint32_t>(e->split_host.size());
     for (uint32_t t = 0; t < nt; ++t) {
-      if (!tab[t].W) continue;
       const TopicHost& T = e->topics[t];
-      for (uint32_t q = tstart[t] + 1; q <= rounds; ++q) {
-        const uint32_t d = q - tstart[t];
-        if (d + 1 >= T.level_off.size()) break;
-        rb[q] += static_cast<uint64_t>(T.level_off[d + 1] - T.level_off[d]) * tab[t].W * 8;
+      const uint32_t W = tab[t].W;
+      if (W == 0 || q < tstart[t] + 1) continue;
+      const uint32_t d = q - tstart[t];  // level of the nodes written this round
+      if (d + 1 >= T.level_off.size()) continue;
+      const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
+      // split parents of this round (children owned by other ranks)
+      if (e->world > 1)
+        for (uint32_t u = T.level_off[d - 1]; u < T.level_off[d]; ++u)
+          if ((e->node_flags[T.nbase + u] & (kNodeSplit | kNodeLive)) == (kNodeSplit | kNodeLive))
+            e->split_host.push_back(T.nbase + u);
+      const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, kPullWords / W));
+      e->pull_bytes[q] += static_cast<uint64_t>(hi - lo) * W * 8;
+      for (uint32_t u = lo; u < hi; u += per) {
+        PullChunk c{};
+        c.node_begin = T.nbase + u;
+        c.node_end = T.nbase + std::min(u + per, hi);
+        c.topic = t;
+        c.p_lo = gpu ? kNone : e->node_parent[c.node_begin];
+        c.p_hi = gpu ? kNone : e->node_parent[c.node_end - 1];
+        C.push_back(c);
       }
-    }
-    // multi-GPU: the top launch ends above this rank's first remote-fed level
-    // (those rows arrive by the exchange of their round, after the launch);
-    // a rank owning no top nodes gets empty rounds
-    uint32_t cap = rounds;
-    if (e->world > 1)
-      for (uint32_t t = 0; t < nt; ++t) {
-        if (!tab[t].W) continue;
-        for (const auto& c : e->topics[t].cross)
-          if (c.to == static_cast<uint32_t>(e->rank) && c.from != c.to)
-            cap = std::min(cap, tstart[t] + c.level);  // level c.level + 1 is remote-fed here
-      }
-    uint32_t last = 0;
-    for (uint32_t q = s0 + 1; s0 != ~0u && q <= cap && q <= s0 + kPullTopLevels && rb[q] &&
-                            rb[q] <= e->pull_top_max;
-         ++q)
-      last = q;
-    if (last > s0 + 1) {
-      e->pull_top_first = s0 + 1;
-      e->pull_top_last = last;
     }
   }
-  auto build = [&](bool fused) -> bool {
-    C.clear();
-    off.assign(rounds + 2, 0);
-    e->pull_bytes.assign(rounds + 2, 0);
-    e->split_host.clear();
-    e->split_off.assign(rounds + 2, 0);
-    for (uint32_t q = 1; q <= rounds; ++q) {
-      // top launch: every round's chunks fill whole blocks (one partial slot
-      // per block and round)
-      if (q > e->pull_top_first && q <= e->pull_top_last + 1)
-        while (C.size() % (kBlock / 64)) C.push_back(PullChunk{0, 0, 0, 0, 0, kNone, kNone, q - 1});
-      off[q] = static_cast<uint32_t>(C.size());
-      e->split_off[q] = static_cast<uint32_t>(e->split_host.size());
-      for (uint32_t t = 0; t < nt; ++t) {
-        const TopicHost& T = e->topics[t];
-        const uint32_t W = tab[t].W;
-        if (W == 0 || q < tstart[t] + 1) continue;
-        const uint32_t d = q - tstart[t];  // level of the nodes written this round
-        if (fused && (d & 1u) == 0) continue;  // fused: launches write levels (1,2), (3,4), ...
-        if (d + 1 >= T.level_off.size()) continue;
-        const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
-        if (!fused) {
-          // split parents of this round (children owned by other ranks)
-          if (e->world > 1)
-            for (uint32_t u = T.level_off[d - 1]; u < T.level_off[d]; ++u)
-              if ((e->node_flags[T.nbase + u] & (kNodeSplit | kNodeLive)) == (kNodeSplit | kNodeLive))
-                e->split_host.push_back(T.nbase + u);
-          const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, e->pull_words / W));
-          e->pull_bytes[q] += static_cast<uint64_t>(hi - lo) * W * 8;
-          for (uint32_t u = lo; u < hi; u += per)
-            C.push_back(PullChunk{T.nbase + u, T.nbase + std::min(u + per, hi), 0, 0, t,
-                                  gpu ? kNone : e->node_parent[T.nbase + u],
-                                  gpu ? kNone : e->node_parent[T.nbase + std::min(u + per, hi) - 1], q});
-          continue;
-        }
-        // fused: a run of level-d nodes plus their children (consecutive ids:
-        // BFS numbering), at most kPullMaxKids nodes and ~pull_words words
-        for (uint32_t u = lo; u < hi;) {
-          const uint32_t b = u;
-          uint32_t n1 = 0, n2 = 0;
-          while (u < hi) {
-            const uint32_t deg = e->row_ptr[T.nbase + u + 1] - e->row_ptr[T.nbase + u];
-            const uint64_t nn = static_cast<uint64_t>(n1) + 1 + n2 + deg;
-            if (n1 && (nn > kPullMaxKids || nn * W > e->pull_words)) break;
-            if (nn > kPullMaxKids) return false;  // one node's children do not fit a chunk
-            ++n1;
-            n2 += deg;
-            ++u;
-          }
-          uint32_t gb = 0;
-          if (n2) {
-            const uint32_t k0 = e->row_ptr[T.nbase + b], k1 = e->row_ptr[T.nbase + u];
-            gb = e->col[k0];
-            if (e->col[k1 - 1] != gb + n2 - 1) return false;  // children not consecutive
-          }
-          C.push_back(PullChunk{T.nbase + b, T.nbase + u, gb, gb + n2, t, e->node_parent[T.nbase + b],
-                                e->node_parent[T.nbase + u - 1], 0});
-        }
-      }
-    }
-    off[rounds + 1] = static_cast<uint32_t>(C.size());
-    e->split_off[rounds + 1] = static_cast<uint32_t>(e->split_host.size());
-    return true;
-  };
-  if (*fuse && !build(true)) *fuse = false;
-  if (!*fuse) build(false);
-  e->pull_fused = *fuse;
+  off[rounds + 1] = static_cast<uint32_t>(C.size());
+  e->split_off[rounds + 1] = static_cast<uint32_t>(e->split_host.size());
   HIP_TRY(e->d_split.ensure(std::max<size_t>(e->split_host.size(), 1) * 4), "alloc split list");
   if (!e->split_host.empty())
     HIP_TRY(hipMemcpyAsync(e->d_split.p, e->split_host.data(), e->split_host.size() * 4,
@@ -1114,7 +981,7 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
     HIP_TRY(hipMemcpyAsync(e->d_pull.p, C.data(), C.size() * sizeof(PullChunk),
                            hipMemcpyHostToDevice, e->stream),
             "upload pull chunks");
-  if (gpu && !C.empty() && e->chunk_parents)  // parent ranges for the generation staging
+  if (gpu && !C.empty())  // parent ranges for the generation staging
     HIP_TRY(launch_chunk_parents(e->d_pull.as<PullChunk>(), static_cast<uint32_t>(C.size()),
                                  e->d_node_parent.as<uint32_t>(), e->stream),
             "chunk parents");
@@ -1122,10 +989,96 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
   return PS_OK;
 }
 
+// One persistent launch (k_flood, flood.hip): every level of every active
+// topic cut into tasks of at most kFloodMaxNodes nodes and about flood_words
+// row words, listed round by round -- a topological order of "reads the
+// parent rows the previous round wrote".  Each task records the parent
+// level's segment; k_flood_deps turns it into the parent range and the tasks
+// that write it.  Per round, the tasks share min(256, tasks) counter slots
+// (slot 0 is the window's timeout word).  Cached per node space, rounds,
+// start rounds and row widths.
+int build_flood_tasks(ps_engine* e, const std::vector<TopicDev>& tab, const std::vector<uint32_t>& tstart,
+                      uint32_t rounds) {
+  const uint32_t nt = static_cast<uint32_t>(e->topics.size());
+  std::vector<uint64_t> key{e->graph_epoch, rounds, e->flood_words};
+  for (uint32_t t = 0; t < nt; ++t) {
+    key.push_back(tab[t].W ? tstart[t] : ~0ull);
+    key.push_back(tab[t].W);
+  }
+  if (key == e->flood_key) return PS_OK;
+  e->flood_key.clear();
+  auto& TK = e->flood_tasks;
+  auto& SG = e->flood_segs;
+  TK.clear();
+  SG.clear();
+  e->flood_slot0.assign(rounds + 2, 0);
+  e->flood_nslot.assign(rounds + 2, 0);
+  std::vector<uint32_t> seg_prev(nt, kNone);  // each topic's segment of the previous round
+  uint32_t slot = 1;
+  for (uint32_t q = 1; q <= rounds; ++q) {
+    const size_t first = TK.size();
+    for (uint32_t t = 0; t < nt; ++t) {
+      const TopicHost& T = e->topics[t];
+      const uint32_t W = tab[t].W;
+      if (W == 0 || q < tstart[t] + 1) continue;
+      const uint32_t d = q - tstart[t];
+      if (d + 1 >= T.level_off.size()) continue;
+      const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
+      if (lo == hi) continue;
+      const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kFloodMaxNodes, e->flood_words / W));
+      const uint32_t pseg = d == 1 ? kNone : seg_prev[t];  // level 1: the seeded root
+      seg_prev[t] = static_cast<uint32_t>(SG.size());
+      SG.push_back(FloodSeg{static_cast<uint32_t>(TK.size()), T.nbase + lo, per, ceil_div(hi - lo, per)});
+      for (uint32_t u = lo; u < hi; u += per) {
+        FloodTask k{};
+        k.nb = T.nbase + u;
+        k.ne = T.nbase + std::min(u + per, hi);
+        k.dep_lo = pseg;
+        k.dep_hi = kNone;
+        k.topic = t;
+        k.round = q;
+        TK.push_back(k);
+      }
+    }
+    const uint32_t n_round = static_cast<uint32_t>(TK.size() - first);
+    if (!n_round) continue;
+    const uint32_t ns = std::min<uint32_t>(kPullSlots, n_round);
+    e->flood_slot0[q] = slot;
+    e->flood_nslot[q] = ns;
+    for (size_t i = first; i < TK.size(); ++i) {
+      TK[i].slot0 = slot;
+      TK[i].nslot = ns;
+    }
+    slot += ns;
+  }
+  e->flood_slots = slot;
+  const size_t n = TK.size();
+  HIP_TRY(e->d_flood_tasks.ensure(std::max<size_t>(n, 1) * sizeof(FloodTask)), "alloc flood tasks");
+  HIP_TRY(e->d_flood_segs.ensure(std::max<size_t>(SG.size(), 1) * sizeof(FloodSeg)), "alloc flood segments");
+  bool fresh = false;  // done words of a fresh allocation hold no epoch yet
+  HIP_TRY(e->d_flood_done.ensure(std::max<size_t>(n, 1) * 4, &fresh), "alloc flood done words");
+  if (fresh) HIP_TRY(hipMemsetAsync(e->d_flood_done.p, 0, e->d_flood_done.bytes, e->stream), "clear done words");
+  if (n) {
+    HIP_TRY(hipMemcpyAsync(e->d_flood_tasks.p, TK.data(), n * sizeof(FloodTask), hipMemcpyHostToDevice, e->stream),
+            "upload flood tasks");
+    HIP_TRY(hipMemcpyAsync(e->d_flood_segs.p, SG.data(), SG.size() * sizeof(FloodSeg), hipMemcpyHostToDevice,
+                           e->stream),
+            "upload flood segments");
+    HIP_TRY(launch_flood_deps(e->d_flood_tasks.as<FloodTask>(), static_cast<uint32_t>(n),
+                              e->d_flood_segs.as<FloodSeg>(), e->d_node_parent.as<uint32_t>(), e->stream),
+            "flood dependencies");
+  }
+  e->flood_key = key;
+  return PS_OK;
+}
+
 // Counters of one window (rows r x kNumCtr, apply rows for multi-GPU) into
 // the run's stats.
-void accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uint32_t r,
-                       uint32_t planned0, bool pull, bool level, uint32_t launches, int32_t world) {
+// Returns false when a k_flood dependency wait timed out (its timeout word
+// is folded into row 0).
+bool accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uint32_t r, uint32_t planned0,
+                       uint32_t mode, uint32_t launches, int32_t world) {
+  const bool pull = mode == PS_MODE_LEVEL_PULL || mode == PS_MODE_FLOOD;
   for (uint32_t q = 1; q <= r; ++q) {
     const uint64_t* c = &hs[static_cast<size_t>(q) * kNumCtr];
     const uint64_t app_d = (world > 1 && q <= planned0) ? ha[static_cast<size_t>(q) * kNumCtr + kCtrDeliveries] : 0;
@@ -1140,9 +1093,10 @@ void accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uin
     // per entry word the arrival read 8 (+ 8 when cleared); per child its
     // flag byte + generation read/write (tree) or col id 4 (mesh); per
     // seen read / seen write / arrival write 8.
-    if (pull)  // pull model: per node parent id 4 + flag 1 + parent generation 1, per
-               // reached node its generation write 1; parent rows read once; rows written
-      st->expand_bytes += c[kCtrChildren] * 6 + c[kCtrMeshChildren] * 1 +
+    if (pull)  // pull model: per node parent id 4 + flag 1 + parent generation 1 (k_flood:
+               // + its own generation 1, the seen test), per reached node its generation
+               // write 1; parent rows read once; rows written
+      st->expand_bytes += c[kCtrChildren] * (mode == PS_MODE_FLOOD ? 7 : 6) + c[kCtrMeshChildren] * 1 +
                           c[kCtrEntryWords] * 8 + c[kCtrSeenWrites] * 8;
     else
       st->expand_bytes += c[kCtrEntries] * 18 + c[kCtrEntryWords] * 8 + c[kCtrClearWords] * 8 +
@@ -1155,8 +1109,9 @@ void accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uin
   }
   st->rounds += r;
   st->expand_launches += launches;
-  st->expand_mode = pull ? PS_MODE_LEVEL_PULL : level ? PS_MODE_LEVEL_PUSH : PS_MODE_COMPACT;
+  st->expand_mode = mode;
   st->windows += 1;
+  return mode != PS_MODE_FLOOD || hs[kCtrDeliveries] == 0;
 }
 
 // Propagates one window: per topic t, win[t] lists the messages (indices into
@@ -1256,7 +1211,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       }
     // a tree topic whose window messages share one start round: every node
     // receives once, so arrival rows are its seen rows (kTopicSingleStart)
-    if (one_start && !T.mesh && !e->no_single_start) d.flags |= kTopicSingleStart;
+    if (one_start && !T.mesh) d.flags |= kTopicSingleStart;
     tstart[t] = msgs[win[t].idx[0]].start;
     if (T.n_nodes == 0) continue;
     d.W = ceil_div(win[t].n, 64);
@@ -1356,69 +1311,50 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(e->expand_grid, blocks)));
   };
   const uint32_t planned0 = max_depth + max_start + 1;
-  // level mode: single rank, staged path only, every active topic a
-  // single-start tree
-  // (pull: any rank count and fan-out; the push kernel's level schedule needs
-  // the staged path: one rank, fan-out <= 64)
-  bool level = !any_mesh && !e->no_level && planned0 + 1 < round_cap;
+  // level mode: every active topic a tree whose window messages share one
+  // start round.  One rank: the whole window is one k_flood launch; several
+  // ranks: one k_pull launch per round (the frontier exchange separates the
+  // rounds); PSAMD_FLOOD=0 selects the per-round launches on one rank too.
+  bool level = !any_mesh && planned0 + 1 < round_cap;
   for (uint32_t t = 0; t < nt && level; ++t)
     if (tab[t].W && !(tab[t].flags & kTopicSingleStart)) level = false;
-  if (level && e->level_push && need_direct) level = false;
-  std::vector<uint32_t> lgrid;  // level mode: expand grid of every round
-  const bool pull = level && !e->level_push;
-  // fused pull (two levels per launch): every active topic starts together
-  bool fuse = pull && !e->no_fuse && world == 1;
-  for (uint32_t t = 0; t < nt && fuse; ++t)
-    if (tab[t].W && tstart[t] != max_start) fuse = false;
+  const bool flood = level && world == 1 && e->flood_on && !e->flood_broken && e->flood_grid > 0 &&
+                     e->n_nodes < 0x80000000u;  // k_flood marks node ids with bit 31
+  const bool pull = level && !flood;
+  const uint32_t mode = flood ? PS_MODE_FLOOD : pull ? PS_MODE_LEVEL_PULL : PS_MODE_COMPACT;
+  std::vector<uint32_t> lgrid;  // per-round launches: grid of every round
+  uint32_t n_slots = 0;         // level mode: partial counter slots of the window
   if (level) {
-    bool top_ok = pull;  // one launch for the leading small rounds
-    for (uint32_t t = 0; t < nt && top_ok; ++t)
-      if (tab[t].W && tstart[t] != max_start) top_ok = false;
-    int rc2 = pull ? build_pull_chunks(e, tab, tstart, planned0, &fuse, top_ok)
-                   : build_schedule(e, tab, tstart, planned0);
+    int rc2 = flood ? build_flood_tasks(e, tab, tstart, planned0) : build_pull_chunks(e, tab, tstart, planned0);
     if (rc2) return rc2;
-    lgrid.assign(planned0 + 1, 0);
-    // partial counter slots: launch of round q owns [woff[q], woff[q+1]);
-    // desc[3q..]: round q's (first, end, stride) for the reduce
-    auto& woff = e->woff_host;
-    woff.assign(planned0 + 2, 0);
-    for (uint32_t q = 1; q <= planned0; ++q) {
-      if (pull) {  // one wave per chunk; a partial slot per block (and level)
-        const uint32_t tf = e->pull_top_first, tl = e->pull_top_last;
-        const bool in_top = tf && q >= tf && q <= tl;
-        if (in_top)  // the top launch, issued in round tf: one slot per block
-          lgrid[q] = q == tf ? ceil_div(e->pull_off[tl + 1] - e->pull_off[tf], kBlock / 64) : 0;
-        else
-          lgrid[q] = ceil_div(e->pull_off[q + 1] - e->pull_off[q], kBlock / 64);
-        const uint32_t slots = in_top ? (q == tf ? (tl - tf + 1) * kPullSlots : 0)
-                                      : std::min<uint32_t>(lgrid[q], kPullSlots);
-        woff[q + 1] = woff[q] + slots * (fuse ? 2 : 1);
-      } else {
-        const uint32_t cnt = e->sched_cnt[q];
-        lgrid[q] = cnt ? std::min<uint32_t>(e->expand_grid, ceil_div(cnt, 4)) : 0;  // >= 1 entry per wave
-        woff[q + 1] = woff[q] + lgrid[q] * (kBlock / 64);
-      }
-    }
+    // desc[3q..]: round q's partial slots (first, end, stride) for the reduce
     auto& desc = e->desc_host;
     desc.assign(3 * (planned0 + 2), 0);
-    for (uint32_t q = 1; q <= planned0; ++q) {
-      desc[3 * q] = woff[q];
-      desc[3 * q + 1] = woff[q + 1];
-      desc[3 * q + 2] = 1;
-      if (pull && e->pull_top_first && q >= e->pull_top_first && q <= e->pull_top_last) {
-        const uint32_t tf = e->pull_top_first;
-        desc[3 * q] = woff[tf] + (q - tf) * kPullSlots;
-        desc[3 * q + 1] = desc[3 * q] + kPullSlots;
+    if (flood) {
+      desc[0] = 0;  // row 0: k_flood's timeout word (slot 0)
+      desc[1] = 1;
+      desc[2] = 1;
+      for (uint32_t q = 1; q <= planned0; ++q) {
+        desc[3 * q] = e->flood_slot0[q];
+        desc[3 * q + 1] = e->flood_slot0[q] + e->flood_nslot[q];
+        desc[3 * q + 2] = e->flood_nslot[q] ? 1 : 0;
       }
-      if (fuse) {
-        const bool second = q > max_start && (q - max_start) % 2 == 0;  // written by launch q - 1
-        const uint32_t L = second ? q - 1 : q;
-        desc[3 * q] = woff[L] + (second ? 1 : 0);
-        desc[3 * q + 1] = woff[L + 1];
-        desc[3 * q + 2] = 2;
+      n_slots = e->flood_slots;
+    } else {
+      // launch of round q owns the slots [woff[q], woff[q+1]): one per block, at most kPullSlots
+      lgrid.assign(planned0 + 1, 0);
+      auto& woff = e->woff_host;
+      woff.assign(planned0 + 2, 0);
+      for (uint32_t q = 1; q <= planned0; ++q) {
+        lgrid[q] = ceil_div(e->pull_off[q + 1] - e->pull_off[q], kBlock / 64);
+        woff[q + 1] = woff[q] + std::min<uint32_t>(lgrid[q], kPullSlots);
+        desc[3 * q] = woff[q];
+        desc[3 * q + 1] = woff[q + 1];
+        desc[3 * q + 2] = 1;
       }
+      n_slots = woff[planned0 + 1];
     }
-    HIP_TRY(e->d_partials.ensure(static_cast<size_t>(woff[planned0 + 1]) * kNumCtr * 8),
+    HIP_TRY(e->d_partials.ensure(static_cast<size_t>(std::max<uint32_t>(n_slots, 1)) * kNumCtr * 8),
             "alloc level partials");
     HIP_TRY(e->d_woff.ensure(desc.size() * 4), "alloc reduce descriptors");
   }
@@ -1455,7 +1391,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // the window's first kernel also copies the staged uploads, applies the
   // round-0 seeds of tree roots and clears the pull partial slots (level
   // mode without meshes; the eager seen clear below would erase the seeds)
-  const bool fold = e->fold_window && level && !any_mesh && !(e->cfg.flags & PS_F_NO_LAZY_SEEN);
+  const bool fold = level && !any_mesh && !(e->cfg.flags & PS_F_NO_LAZY_SEEN);
   WindowStart ws{};
   const void* staged[3] = {nullptr, nullptr, nullptr};
   {
@@ -1468,10 +1404,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   }
   if (fold) {
     if (seed_off[1] > 0) ws.seeds = static_cast<const SeedDev*>(staged[1]);
-    if (pull) {
-      ws.zero = e->d_partials.as<uint64_t>();
-      ws.zero_words = static_cast<uint64_t>(e->woff_host[planned0 + 1]) * kNumCtr;
-    }
+    ws.zero = e->d_partials.as<uint64_t>();
+    ws.zero_words = static_cast<uint64_t>(n_slots) * kNumCtr;
   }
   const bool seeds0_done = ws.seeds != nullptr;
   const bool partials_done = ws.zero != nullptr;
@@ -1518,8 +1452,6 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   a.gen_cur = e->gen_cur;
   a.next_flag = e->d_flags.as<uint8_t>();
   a.blk_flag = e->d_blk.as<uint8_t>();
-  a.dbg = 0;
-  if (const char* v = std::getenv("PSAMD_DEBUG_EXPAND")) a.dbg = static_cast<uint32_t>(std::atoi(v));
   a.hop_rec = record ? e->d_hop.as<uint16_t>() : nullptr;
   a.send = e->d_send.as<uint8_t>();
   uint64_t* const partials = e->d_partials.as<uint64_t>();
@@ -1609,77 +1541,79 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     return PS_OK;
   };
   if (level) {
-    // static frontier: one expand launch per round, counters reduced once
-    if (pull && !partials_done)  // pull blocks add into shared partial slots
-      HIP_TRY(hipMemsetAsync(partials, 0, static_cast<size_t>(e->woff_host[planned0 + 1]) * kNumCtr * 8, s),
-              "clear partials");
+    // static frontier, counters reduced once per window
+    if (!partials_done)  // blocks / waves add into shared partial slots
+      HIP_TRY(hipMemsetAsync(partials, 0, static_cast<size_t>(n_slots) * kNumCtr * 8, s), "clear partials");
     if (!seeds0_done) HIP_TRY(seed_round(0, arr[0]), "seed");
-    for (r = 1; r <= planned0; ++r) {
-      a.a_cur = arr[(r - 1) & 1];
-      a.a_next = arr[r & 1];
-      const bool xr = layout(r);
-      if (xr)
-        for (int32_t q = 0; q < world; ++q)
-          if (s_len[q]) HIP_TRY(hipMemsetAsync(a.send + s_off[q], 0, kRegionHeader, s), "reset header");
-      if (lgrid[r]) {
-        HIP_TRY(time_mark(true), "event");
-        ++launches;
-      }
-      if (lgrid[r] && pull) {
-        const bool top = e->pull_top_first == r;
-        PullArgs pa{};
-        pa.node_parent = e->d_node_parent.as<uint32_t>();
-        pa.node_flags = a.node_flags;
-        pa.topics = a.topics;
-        pa.a_cur = a.a_cur;
-        pa.seen = a.seen;
-        pa.gen = a.gen;
-        pa.hop_rec = a.hop_rec;
-        pa.partials = partials + static_cast<size_t>(e->woff_host[r]) * kNumCtr;
-        pa.gen_cur = a.gen_cur;
-        pa.dbg = a.dbg;
-        pa.slot_mod = kPullSlots;
-        pa.slot_base = r;
-        pa.wave_flush = e->pull_wave_flush;
-        pa.path_live = e->d_path_live.as<uint32_t>();
-        pa.pl_epoch = static_cast<uint32_t>(e->flags_epoch % ((1u << 30) - 1)) + 1;
-        const PullChunk* ch = e->d_pull.as<PullChunk>() + e->pull_off[r];
-        if (top) {
-          // no row of the top launch is read back by it (every reached node
-          // copies the root's row): its large rounds store non-temporally
-          if (e->pull_nt & 1u)
-            for (uint32_t q = r; q <= e->pull_top_last && q - r < 32; ++q)
-              if (q < e->pull_bytes.size() && (e->pull_bytes[q] >= e->pull_nt_min || q == planned0))
-                pa.top_nt |= 1u << (q - r);
-          pa.top_odd_wide = e->top_odd_wide;
-          pa.xcd_remap = e->top_xcd;
-          HIP_TRY(launch_pull_top(pa, ch, e->pull_off[e->pull_top_last + 1] - e->pull_off[r], record, s,
-                                  e->top_lds),
-                  "pull top");
-        } else {
-          // rows a later level re-reads while they can still sit in the 256 MB
-          // MALL keep the default policy
-          const bool nt = r < e->pull_bytes.size() && (e->pull_bytes[r] >= e->pull_nt_min || r == planned0);
-          HIP_TRY(launch_pull(pa, ch, e->pull_off[r + 1] - e->pull_off[r], lgrid[r], r, record, fuse,
-                              e->pull_unroll, nt ? e->pull_nt : 0u, s),
+    if (flood) {
+      // topics starting after round 0: their roots' rows are seeded up front
+      // (k_flood reads every parent row, the roots' too, from `seen`)
+      if (max_start > 0)
+        HIP_TRY(launch_seed(e->d_seeds.as<SeedDev>(), seed_off[1], seed_off[max_start + 1], arr[0], a.seen,
+                            nullptr, nullptr, s),
+                "seed");
+      FloodArgs fa{};
+      fa.tasks = e->d_flood_tasks.as<FloodTask>();
+      fa.node_parent = e->d_node_parent.as<uint32_t>();
+      fa.node_flags = a.node_flags;
+      fa.topics = a.topics;
+      fa.seen = a.seen;
+      fa.gen = a.gen;
+      fa.hop_rec = a.hop_rec;
+      fa.done = e->d_flood_done.as<uint32_t>();
+      fa.partials = partials;
+      fa.err = reinterpret_cast<uint32_t*>(partials);  // slot 0, reduced into row 0
+      fa.n_tasks = static_cast<uint32_t>(e->flood_tasks.size());
+      if (++e->flood_epoch == 0) ++e->flood_epoch;  // done words from older launches hold older epochs
+      fa.epoch = e->flood_epoch;
+      fa.gen_cur = a.gen_cur;
+      fa.spin_ticks = 200000000u;  // 2 s of s_memrealtime (100 MHz)
+      r = 1;  // the per-round kernel times of a timed run go to round 1
+      HIP_TRY(time_mark(true), "event");
+      ++launches;
+      HIP_TRY(launch_flood(fa, std::min<uint32_t>(e->flood_grid, ceil_div(fa.n_tasks, kBlock / 64)), record, s),
+              "flood");
+      HIP_TRY(time_mark(false), "event");
+    } else {
+      for (r = 1; r <= planned0; ++r) {
+        a.a_cur = arr[(r - 1) & 1];
+        a.a_next = arr[r & 1];
+        const bool xr = layout(r);
+        if (xr)
+          for (int32_t q = 0; q < world; ++q)
+            if (s_len[q]) HIP_TRY(hipMemsetAsync(a.send + s_off[q], 0, kRegionHeader, s), "reset header");
+        if (lgrid[r]) {
+          HIP_TRY(time_mark(true), "event");
+          ++launches;
+          PullArgs pa{};
+          pa.node_parent = e->d_node_parent.as<uint32_t>();
+          pa.node_flags = a.node_flags;
+          pa.topics = a.topics;
+          pa.a_cur = a.a_cur;
+          pa.seen = a.seen;
+          pa.gen = a.gen;
+          pa.hop_rec = a.hop_rec;
+          pa.partials = partials + static_cast<size_t>(e->woff_host[r]) * kNumCtr;
+          pa.gen_cur = a.gen_cur;
+          pa.slot_mod = kPullSlots;
+          // rows nobody re-reads while they can still sit in the 256 MB MALL
+          // (large rounds and the last round) store non-temporally
+          const bool nt = r < e->pull_bytes.size() && (e->pull_bytes[r] >= (64ull << 20) || r == planned0);
+          HIP_TRY(launch_pull(pa, e->d_pull.as<PullChunk>() + e->pull_off[r], e->pull_off[r + 1] - e->pull_off[r],
+                              lgrid[r], r, record, nt, s),
                   "pull");
+          HIP_TRY(time_mark(false), "event");
         }
-      } else if (lgrid[r]) {
-        a.frontier = e->d_sched.as<uint32_t>() + e->sched_off[r];
-        a.n_front = e->d_sched_cnt.as<uint32_t>() + r;
-        a.partials = partials + static_cast<size_t>(e->woff_host[r]) * kNumCtr;
-        HIP_TRY(launch_expand(a, r, record, true, lgrid[r], s), "expand");
+        if (world > 1 && e->split_off[r + 1] > e->split_off[r])
+          HIP_TRY(launch_send(a, e->d_split.as<uint32_t>() + e->split_off[r], e->split_off[r + 1] - e->split_off[r],
+                              s),
+                  "send");
+        if (xr) {
+          const int rc3 = xchg(r);
+          if (rc3) return rc3;
+        }
+        HIP_TRY(seed_round(r, a.a_next), "seed");
       }
-      if (lgrid[r]) HIP_TRY(time_mark(false), "event");
-      if (pull && world > 1 && e->split_off[r + 1] > e->split_off[r])
-        HIP_TRY(launch_send(a, e->d_split.as<uint32_t>() + e->split_off[r],
-                            e->split_off[r + 1] - e->split_off[r], s),
-                "send");
-      if (xr) {
-        const int rc3 = xchg(r);
-        if (rc3) return rc3;
-      }
-      HIP_TRY(seed_round(r, a.a_next), "seed");
     }
     r = planned0;
     // a deferred window's counters go straight into its pinned rows
@@ -1705,7 +1639,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       ++launches;
       const uint32_t grid_r = r <= planned0 ? round_grid(r) : e->expand_grid;
       a.partials = partials;
-      HIP_TRY(launch_expand(a, r, record, false, grid_r, s), "expand");
+      HIP_TRY(launch_expand(a, r, record, grid_r, s), "expand");
       uint32_t waves_r = grid_r * (kBlock / 64);
       if (need_direct) {
         a.partials = partials + static_cast<size_t>(waves_r) * kNumCtr;
@@ -1766,8 +1700,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     f.world = world;
     f.r = r;
     f.launches = launches;
-    f.pull = pull;
-    f.level = level;
+    f.mode = mode;
     e->last_topics = tab;
     for (uint32_t t = 0; t < nt; ++t) {
       e->last_cnt[t] = tab[t].W ? win[t].n : 0;
@@ -1803,7 +1736,11 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
             "read apply stats");
   }
   HIP_TRY(hipStreamSynchronize(s), "sync");
-  accumulate_window(st, hs.data(), ha.data(), r, planned0, pull, level, launches, world);
+  if (!accumulate_window(st, hs.data(), ha.data(), r, planned0, mode, launches, world)) {
+    e->flood_broken = true;
+    return e->fail(PS_E_DEVICE, "k_flood: a dependency wait timed out (waves not co-resident?); "
+                                "per-round launches from now on");
+  }
   if (e->host_timing) {
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     std::fprintf(stderr, "[psengine] window: plan %.3f ms (run->window %.3f, topics %.3f, seeds %.3f, "
@@ -1903,34 +1840,22 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
       cus > 0)
     e->n_cus = static_cast<uint32_t>(cus);
   // resident 256-thread blocks per CU: k_expand needs 80 VGPRs / 106 SGPRs,
-  // which admits 6 (MI355X_MICROARCH.md §Residency); PSAMD_EXPAND_BPC overrides
-  uint32_t bpc = 6;
-  if (const char* v = std::getenv("PSAMD_EXPAND_BPC")) bpc = std::max(1, std::atoi(v));
-  e->expand_grid = e->n_cus * bpc;
-  if (const char* v = std::getenv("PSAMD_NO_SINGLE_START")) e->no_single_start = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_NO_LEVEL")) e->no_level = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_HOST_TIMING")) e->host_timing = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_SMALL_PLACE"))
-    e->small_place = std::min<uint32_t>(static_cast<uint32_t>(std::atoi(v)), kBuildSmallLevel);
-  if (const char* v = std::getenv("PSAMD_PULL_NT")) e->pull_nt = static_cast<uint32_t>(std::atoi(v)) & 3u;
-  if (const char* v = std::getenv("PSAMD_PULL_NT_MB")) e->pull_nt_min = std::strtoull(v, nullptr, 10) << 20;
-  if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_LEVEL_PUSH")) e->level_push = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_PULL_WORDS")) e->pull_words = std::max(64, std::atoi(v));
-  if (const char* v = std::getenv("PSAMD_PULL_WAVE_FLUSH")) e->pull_wave_flush = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_CHUNK_PARENTS")) e->chunk_parents = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_FOLD_WINDOW")) e->fold_window = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_TOP_XCD")) e->top_xcd = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_TOP_LDS_KB"))
-    e->top_lds = static_cast<uint32_t>(std::min(60, std::max(0, std::atoi(v)))) << 10;
-  if (const char* v = std::getenv("PSAMD_TOP_ODD_WIDE")) e->top_odd_wide = static_cast<uint32_t>(std::min(2, std::max(0, std::atoi(v))));
-  if (const char* v = std::getenv("PSAMD_PULL_TOP_MB"))  // fractions allowed (tests split small windows)
-    e->pull_top_max = static_cast<uint64_t>(std::max(0.0, std::strtod(v, nullptr)) * 1048576.0);
-  if (const char* v = std::getenv("PSAMD_PULL_FUSE")) e->no_fuse = std::atoi(v) == 0;
-  if (const char* v = std::getenv("PSAMD_PULL_UNROLL")) {
-    const int u = std::atoi(v);
-    e->pull_unroll = u <= 4 ? 4 : (u >= 16 ? 16 : 8);
+  // which admits 6 (MI355X_MICROARCH.md §Residency)
+  e->expand_grid = e->n_cus * 6;
+  // k_flood's waves must all be resident at once (its tasks wait on earlier
+  // tasks): the grid stays within the occupancy the runtime reports, capped
+  // at kFloodBlocksPerCu for margin (MI355X_MICROARCH.md §Residency)
+  {
+    int bpc = 0;
+    if (flood_blocks_per_cu(&bpc) == hipSuccess && bpc > 0)
+      e->flood_grid = e->n_cus * std::min<uint32_t>(static_cast<uint32_t>(bpc), kFloodBlocksPerCu);
   }
+  // switches: debug timing, and the modes the parity tests cover
+  if (const char* v = std::getenv("PSAMD_HOST_TIMING")) e->host_timing = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_FLOOD")) e->flood_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_FLOOD_WORDS"))
+    e->flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess) {
     delete e;
@@ -2370,8 +2295,12 @@ int ps_wait(ps_engine* e, ps_stats* out) {
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, f.ev0, f.ev1), "elapsed");
     f.st.run_ms += ms;
-    accumulate_window(&f.st, f.hs, f.ha, f.r, f.planned0, f.pull, f.level, f.launches, f.world);
     f.deferred = false;
+    if (!accumulate_window(&f.st, f.hs, f.ha, f.r, f.planned0, f.mode, f.launches, f.world)) {
+      e->flood_broken = true;
+      return e->fail(PS_E_DEVICE, "k_flood: a dependency wait timed out (waves not co-resident?); "
+                                  "per-round launches from now on");
+    }
   }
   if (out) *out = f.st;
   return PS_OK;

@@ -13,24 +13,14 @@
 // client.processMessages (client.go:100-132).  Design: DESIGN.md §5.
 #include <algorithm>
 
+#include "devutil.hpp"
 #include "kernels.hpp"
 
 namespace psamd {
 
 namespace {
 
-__device__ __forceinline__ uint64_t shfl_xor_u64(uint64_t v, int m) {
-  uint32_t lo = static_cast<uint32_t>(v), hi = static_cast<uint32_t>(v >> 32);
-  lo = __shfl_xor(lo, m, 64);
-  hi = __shfl_xor(hi, m, 64);
-  return (static_cast<uint64_t>(hi) << 32) | lo;
-}
-
-__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) v += shfl_xor_u64(v, m);
-  return v;
-}
+using namespace dev;
 
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
   const int lane = threadIdx.x & 63;
@@ -208,11 +198,11 @@ __device__ __forceinline__ uint64_t deliver_word(const ExpandArgs& a, bool mesh,
       k.sr += 1;
     }
     nm = m & ~old;
-    if ((stale || nm) && !(a.dbg & kDbgNoSeenStore)) {
+    if (stale || nm) {
       a.seen[cw] = old | nm;
       k.sw += 1;
     }
-    if (internal && !(a.dbg & kDbgNoArrivalStore)) {
+    if (internal) {
       a.a_next[cw] = nm;
       k.aw += 1;
     }
@@ -236,9 +226,9 @@ __device__ __forceinline__ uint64_t deliver_word(const ExpandArgs& a, bool mesh,
 template <bool kRecord>
 __device__ __forceinline__ void deliver_fresh(const ExpandArgs& a, bool internal, uint64_t cw,
                                               uint64_t m, uint32_t round, ExpandCtr& k) {
-  if (!(a.dbg & kDbgNoSeenStore)) a.seen[cw] = m;
+  a.seen[cw] = m;
   k.sw += 1;
-  if (internal && !(a.dbg & kDbgNoArrivalStore)) {
+  if (internal) {
     a.a_next[cw] = m;
     k.aw += 1;
   }
@@ -258,9 +248,9 @@ __device__ __forceinline__ void deliver_fresh(const ExpandArgs& a, bool internal
 template <bool kRecord>
 __device__ __forceinline__ void deliver_fresh2(const ExpandArgs& a, bool internal, uint64_t cw,
                                                uint4 v, uint32_t round, ExpandCtr& k) {
-  if (!(a.dbg & kDbgNoSeenStore)) *reinterpret_cast<uint4*>(a.seen + cw) = v;
+  *reinterpret_cast<uint4*>(a.seen + cw) = v;
   k.sw += 2;
-  if (internal && !(a.dbg & kDbgNoArrivalStore)) {
+  if (internal) {
     *reinterpret_cast<uint4*>(a.a_next + cw) = v;
     k.aw += 2;
   }
@@ -279,7 +269,6 @@ __device__ __forceinline__ void deliver_fresh2(const ExpandArgs& a, bool interna
 }
 
 __device__ __forceinline__ void mark_next(const ExpandArgs& a, uint32_t c) {
-  if (a.dbg & kDbgNoByteStores) return;
   a.next_flag[c] = 1;
   a.blk_flag[c >> kFlagBlockShift] = 1;
 }
@@ -402,7 +391,7 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
         if (live && w == 0 && (f & kNodeInternal) && (bal & gmask)) mark_next(a, c);
       }
     }
-    if (!mesh && lane < cd && (fj & kNodeLive) && !(a.dbg & kDbgNoByteStores))
+    if (!mesh && lane < cd && (fj & kNodeLive))
       a.gen[cj] = static_cast<uint8_t>(cur);
   }
   if (mesh || is_root) {
@@ -417,7 +406,7 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
 // kStageWords words, each slice stored to every live child before the next
 // is loaded.  The children's flag and generation bytes are read once, before
 // any store, so every slice sees the same staleness.
-template <bool kRecord, bool kLevel>
+template <bool kRecord>
 __device__ void expand_wide(const ExpandArgs& a, WaveStage& ws, uint32_t p, uint32_t deg,
                             uint32_t c0, uint32_t W, uint32_t nbase, uint32_t fl, uint64_t wbase,
                             uint32_t lane, uint32_t cur, uint32_t round, ExpandCtr& k,
@@ -472,9 +461,8 @@ __device__ void expand_wide(const ExpandArgs& a, WaveStage& ws, uint32_t p, uint
       if (__ballot(any)) got |= 1ull << jj;
     }
   }
-  if constexpr (!kLevel)
-    if (lane < deg && (fj & kNodeInternal) && ((got >> lane) & 1ull)) mark_next(a, c0 + lane);
-  if (lane < deg && (fj & kNodeLive) && !(a.dbg & kDbgNoByteStores))
+  if (lane < deg && (fj & kNodeInternal) && ((got >> lane) & 1ull)) mark_next(a, c0 + lane);
+  if (lane < deg && (fj & kNodeLive))
     a.gen[c0 + lane] = static_cast<uint8_t>(cur);
   if (is_root) {  // seeded with |=: consume-and-clear
     for (uint32_t w = lane; w < W; w += 64) a.a_cur[pw + w] = 0;
@@ -495,12 +483,7 @@ __device__ void expand_wide(const ExpandArgs& a, WaveStage& ws, uint32_t p, uint
 // kDirect = false: the staged path only (entries that need the direct path
 // are left to the second instance); kDirect = true: the direct path only.
 // Separate instances keep the hot staged kernel's register budget small.
-// kLevel = true (staged only): the frontier is the round's static level
-// schedule (live internal nodes of one BFS level per topic, single-start
-// tree windows); an entry the window's messages did not reach (generation
-// stale: a non-live ancestor) is skipped, and no frontier flags are raised
-// because the next round's frontier is known already.
-template <bool kRecord, bool kDirect, bool kLevel>
+template <bool kRecord, bool kDirect>
 __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round) {
   __shared__ WaveStage stage_lds[kDirect ? 1 : kBlock / 64];
   const uint32_t lane = threadIdx.x & 63;
@@ -529,7 +512,6 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
       bwl = static_cast<uint32_t>(T.wbase);
       bwh = static_cast<uint32_t>(T.wbase >> 32);
       if (bdeg && T.W) bc0 = a.col[brs];
-      if (kLevel && a.gen[bp] != cur) bW = bdeg = 0;  // not reached this window
     }
     const uint32_t nb = static_cast<uint32_t>(__popcll(__ballot(el < n)));
     uint32_t q = 0;
@@ -549,7 +531,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
         continue;
       }
       if (W0 > kStageWords) {  // wide row: staged slice by slice
-        expand_wide<kRecord, kLevel>(a, ws, rl(bp, q), d0, rl(bc0, q), W0, rl(bnb, q), f0,
+        expand_wide<kRecord>(a, ws, rl(bp, q), d0, rl(bc0, q), W0, rl(bnb, q), f0,
                                      (static_cast<uint64_t>(rl(bwh, q)) << 32) | rl(bwl, q), lane,
                                      cur, round, k, ec);
         ++q;
@@ -582,9 +564,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
           const uint32_t* row = reinterpret_cast<const uint32_t*>(
               (from_seen ? a.seen : a.a_cur) + wbase + static_cast<uint64_t>(p - nbase) * W);
           uint32_t* dst = reinterpret_cast<uint32_t*>(ws.words + off);
-          if (a.dbg & kDbgNoArrivalLoad) {
-            // experiment: no row loads (the words are set to all-ones below)
-          } else if ((W & 1u) == 0) {
+          if ((W & 1u) == 0) {
             // even W: the row and its stage slot are 16-B aligned (topic
             // blocks start on 128-B lines, slots keep even offsets): one
             // dwordx4 DMA per lane, 1 KiB per wave instruction
@@ -606,8 +586,6 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      if (a.dbg & kDbgNoArrivalLoad)
-        for (uint32_t i = lane; i < sw; i += 64) ws.words[i] = ~0ull;
       // phase B: stores
       {
         uint32_t off = 0, doff = 0;
@@ -655,8 +633,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
                   }
                 }
               }
-              if constexpr (!kLevel)
-                if (internal && __ballot(any) && lane == 0) mark_next(a, c);
+              if (internal && __ballot(any) && lane == 0) mark_next(a, c);
             }
           } else {
             const uint32_t sh = pow2_shift(W);
@@ -684,14 +661,12 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
                 nm = deliver_word<kRecord>(a, false, stale, keep && (f & kNodeInternal), cw, m,
                                            round, k);
               }
-              if constexpr (!kLevel) {
-                const uint64_t bal = __ballot(nm != 0);
-                if (live && w == 0 && (f & kNodeInternal) && (bal & gmask)) mark_next(a, c);
-              }
+              const uint64_t bal = __ballot(nm != 0);
+              if (live && w == 0 && (f & kNodeInternal) && (bal & gmask)) mark_next(a, c);
             }
           }
           // live children hold current rows now
-          if (lane < deg && (ws.flags[fo + lane] & kNodeLive) && !(a.dbg & kDbgNoByteStores))
+          if (lane < deg && (ws.flags[fo + lane] & kNodeLive))
             a.gen[c0 + lane] = static_cast<uint8_t>(cur);
           if (p == nbase && (rl(bfl, i) & kTopicRootLocal)) {  // seeded with |=: consume-and-clear
             const uint64_t pw = wbase + static_cast<uint64_t>(p - nbase) * W;
@@ -727,49 +702,27 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
 }
 
 // ------------------------------------------------------------------ pull ---
-// Level mode, pull direction.  In a single-start tree
-// window a node of BFS level d receives, in round s + d, exactly its parent's
-// arrival set -- if the parent was reached and the node is live -- and it is
-// fresh (it has seen nothing this window), so the seen test-and-set is
-// new = arrival(parent) & ~0 and the whole row is written.  This kernel runs
-// that step child-parallel (the bottom-up direction of BFS): a wave owns a
-// contiguous run of next-level nodes, whose rows form one contiguous output
-// stream, and
+// Level mode, pull direction, one launch per round (multi-GPU windows, whose
+// rounds are separated by the frontier exchange; PSAMD_FLOOD=0 on one GPU).
+// In a single-start tree window a node of BFS level d receives, in round
+// s + d, exactly its parent's row -- if the parent was reached this window
+// (generation current) and the node is live -- and it is fresh (it has seen
+// nothing this window), so the seen test-and-set is new = row(parent) & ~0
+// and the whole row is written.  A wave owns a contiguous run of next-level
+// nodes, whose rows form one contiguous output stream:
 //   phase 1  resolves each node's source into a wave-private LDS table: its
-//            parent if the parent is in the frontier (generation current:
-//            reached this window) and the node is live, else none; the node's
-//            generation is stamped;
-//   phase 2  streams the run's rows in order with 16-B stores, each lane's
-//            16-B load taken from its node's parent row (siblings read the
-//            same parent row: L2 hits).  Loads are unconditional (a skipped
-//            node reads its own row) so the unrolled body keeps several in
-//            flight; only the stores are predicated.
+//            parent if the parent is in the frontier (generation current) and
+//            the node is live, else none; the node's generation is stamped;
+//   phase 2  streams the run's rows in order with 16-B stores (8-B for odd
+//            W), each lane's load taken from its node's parent row (siblings
+//            read the same parent row: L2 hits).  Loads are unconditional (a
+//            skipped node reads its own row) so the unrolled body keeps
+//            several in flight.
 // Counters: deliveries, seen writes, nodes visited, nodes reached, parents
 // expanded (a reached parent counts at its first child) and their row words.
-__device__ __forceinline__ uint32_t popc4(uint4 v) {
-  return __popc(v.x) + __popc(v.y) + __popc(v.z) + __popc(v.w);
-}
-
-template <bool kRecord>
-__device__ __forceinline__ void record_word(uint16_t* hop_rec, uint64_t cw, uint64_t m,
-                                            uint32_t round) {
-  uint16_t* h = hop_rec + cw * 64;
-  while (m) {
-    const int q = __ffsll(static_cast<long long>(m)) - 1;
-    h[q] = hop_round(round);
-    m &= m - 1;
-  }
-}
-
 struct PullVec {
   bool go;
   uint4 v;
-};
-
-// One wave's counters for one level of a pull launch.
-struct PullCtr {
-  uint64_t deliv = 0;
-  uint32_t sw = 0, kids = 0, reached = 0, parents = 0, pwords = 0;
 };
 
 // Topic constants of a chunk: row of node u = base + u * W.
@@ -779,25 +732,15 @@ struct PullTopic {
 };
 
 // Phase 1 for the nodes [nb, nb + nk) of one level: src[j] = the node whose
-// row node nb + j copies, or kNoneNode.  Level 1 (kSecond = false): the
-// parent, if the parent was reached this window (generation current) and the
-// node is live.  Level 2 of a fused launch (kSecond = true): the node's
-// parent pc is level 1 of the same chunk, whose row is being written from
-// src1[pc - b1]; the node copies that same source row (the row pc receives)
-// if pc was reached and the node is live.  Reached nodes get their
-// generation stamped.  A parent counts once, at its first child.
-template <bool kSecond>
-__device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic& P, uint32_t nb,
-                                             uint32_t nk, uint32_t p_lo, uint32_t p_hi,
-                                             uint32_t* src, const uint32_t* src1, uint32_t b1,
-                                             uint8_t* genl, uint32_t lane, uint32_t cur,
-                                             PullCtr& c) {
-  // Level 1: the parents of a run are consecutive node ids [p_lo, p_hi]
-  // (BFS numbering), known to the host: their generation bytes are staged
-  // into LDS by loads issued together with the nodes' own metadata, so phase
-  // 1 costs one memory round trip.
+// row node nb + j copies, or kNoneNode.  The parents of a run are consecutive
+// node ids [p_lo, p_hi] (BFS numbering): their generation bytes are staged
+// into LDS by loads issued together with the nodes' own metadata, so phase 1
+// costs one memory round trip.
+__device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t nk,
+                                             uint32_t p_lo, uint32_t p_hi, uint32_t* src, uint8_t* genl,
+                                             uint32_t lane, uint32_t cur, PullCtr& c) {
   uint32_t g0 = 0;
-  const bool staged = !kSecond && p_lo != kNoneNode && p_hi - p_lo < kPullMaxKids;
+  const bool staged = p_lo != kNoneNode && p_hi - p_lo < kPullMaxKids;
   if (staged) {
     g0 = p_lo & ~3u;
     const uint32_t nd = ((p_hi + 4u) & ~3u) - g0;  // bytes, whole dwords
@@ -814,38 +757,27 @@ __device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic&
     }
     uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
     if (lane == 0) prev = nb + j0 > P.nbase ? a.node_parent[nb + j0 - 1] : kNoneNode;
-    uint32_t from = kNoneNode;
     bool up = false;  // the parent was reached this window
-    if constexpr (kSecond) {
-      if (in) from = src1[p - b1];
-      up = from != kNoneNode;
-    } else {
-      if (in && p != kNoneNode) up = (staged ? genl[p - g0] : a.gen[p]) == cur;
-      from = p;
-    }
+    if (in && p != kNoneNode) up = (staged ? genl[p - g0] : a.gen[p]) == cur;
     const bool ok = up && (f & kNodeLive);
-    if (in) src[j] = ok ? from : kNoneNode;
-    if (ok && !(a.dbg & kDbgNoByteStores)) a.gen[nb + j] = static_cast<uint8_t>(cur);
+    if (in) src[j] = ok ? p : kNoneNode;
+    if (ok) a.gen[nb + j] = static_cast<uint8_t>(cur);
     c.kids += in;
     c.reached += ok;
     if (up && p != prev) {
       c.parents += 1;
-      if constexpr (!kSecond) c.pwords += P.W;  // fused level 2 re-reads the level-1 source
+      c.pwords += P.W;
     }
   }
 }
 
-// Phase 2: the rows of nodes [nb, nb + nk) as one output stream, each lane's
-// load from the row its node copies (src[], kNoneNode = skip).
-typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
-
-// row store of the pull stream: plain, or non-temporal (`nt`: no L2 / MALL
-// allocation for rows nobody re-reads within the launch)
+// row store of the pull stream: plain, or non-temporal (`nt`: rows nobody
+// re-reads soon)
 template <bool kNT>
 __device__ __forceinline__ void store_row16(uint64_t* p, const uint4& v) {
   if constexpr (kNT) {
-    u32x4_t x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, reinterpret_cast<u32x4_t*>(p));
+    u32x4 x = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
   } else {
     *reinterpret_cast<uint4*>(p) = v;
   }
@@ -858,28 +790,16 @@ __device__ __forceinline__ void store_row8(uint64_t* p, uint64_t v) {
     *p = v;
 }
 
-template <bool kNTL>
-__device__ __forceinline__ uint4 load_row16(const uint64_t* p) {
-  if constexpr (kNTL) {
-    const u32x4_t x = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
-    return uint4{x.x, x.y, x.z, x.w};
-  } else {
-    return *reinterpret_cast<const uint4*>(p);
-  }
-}
-template <bool kNTL>
-__device__ __forceinline__ uint64_t load_row8(const uint64_t* p) {
-  if constexpr (kNTL)
-    return __builtin_nontemporal_load(p);
-  else
-    return *p;
-}
-
-// kNT: bit 0 non-temporal row stores, bit 1 non-temporal parent-row loads
-template <bool kRecord, uint32_t kU, uint32_t kNT>
-__device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& P, uint32_t nb,
-                                            uint32_t nk, const uint32_t* src, uint32_t lane,
-                                            uint32_t wave, uint32_t round, PullCtr& c) {
+// Phase 2: the rows of nodes [nb, nb + nk) as one output stream, each lane's
+// load from the row its node copies (src[], kNoneNode = skip).  8 loads in
+// flight, then 8 stores, unconditional and branch-free (a skipped lane writes
+// its own row back unchanged, a lane past the run's end stores the run's last
+// pair again with the value its owner stores), so the compiler counts vmcnt
+// exactly instead of draining at branches.
+template <bool kRecord, bool kNT>
+__device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t nk,
+                                            const uint32_t* src, uint32_t lane, uint32_t round, PullCtr& c) {
+  constexpr uint32_t kU = 8;
   const uint32_t W = P.W;
   const uint64_t base = P.base;
   const uint32_t root = P.root;
@@ -897,22 +817,15 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
   };
   if (!(W & 1u)) {
     // even W: every row 16-B aligned, a 2-word pair never straddles rows
-    // i: a pair of words of the run; a lane past the run's end repeats the
-    // run's last pair (same source, same value, same address)
     auto one = [&](uint32_t i) {
       int32_t kk, r;
       split(i, kk, r);
       const uint32_t p = src[kk];
       const bool go = p != kNoneNode;
-      // unconditional load: a skipped lane reads its own output row
       const uint64_t* s = go ? (p == root ? a.a_cur : a.seen) + base + static_cast<uint64_t>(p) * W + r
                              : out + i;
-      return PullVec{go, load_row16<(kNT & 2u) != 0>(s)};
+      return PullVec{go, *reinterpret_cast<const uint4*>(s)};
     };
-    // 8 loads in flight, then 8 stores, unconditional and branch-free (a
-    // skipped lane writes its own row back unchanged, a lane past the run's
-    // end stores the run's last pair again with the value its owner stores),
-    // so the compiler counts vmcnt exactly instead of draining at branches
     for (uint32_t i0 = 0; i0 < total; i0 += kU * 128) {
       PullVec x[kU];
 #pragma unroll
@@ -927,12 +840,11 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
           if (x[u].go && i < total) {
             *reinterpret_cast<uint4*>(out + i) = x[u].v;
             const uint64_t cw = (out - a.seen) + i;
-            record_word<kRecord>(a.hop_rec, cw, static_cast<uint64_t>(x[u].v.y) << 32 | x[u].v.x, round);
-            record_word<kRecord>(a.hop_rec, cw + 1, static_cast<uint64_t>(x[u].v.w) << 32 | x[u].v.z,
-                                 round);
+            record_word(a.hop_rec, cw, static_cast<uint64_t>(x[u].v.y) << 32 | x[u].v.x, round);
+            record_word(a.hop_rec, cw + 1, static_cast<uint64_t>(x[u].v.w) << 32 | x[u].v.z, round);
           }
         } else {
-          store_row16<(kNT & 1u) != 0>(out + (i < total ? i : total - 2), x[u].v);
+          store_row16<kNT>(out + (i < total ? i : total - 2), x[u].v);
         }
         const bool own = x[u].go && i < total;
         c.deliv += own ? popc4(x[u].v) : 0u;
@@ -954,7 +866,7 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
         go[u] = p != kNoneNode;
         const uint64_t* s = go[u] ? (p == root ? a.a_cur : a.seen) + base + static_cast<uint64_t>(p) * W + r
                                   : out + ic;
-        m[u] = load_row8<(kNT & 2u) != 0>(s);
+        m[u] = *s;
       }
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
@@ -962,10 +874,10 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
         if constexpr (kRecord) {
           if (go[u] && i < total) {
             out[i] = m[u];
-            record_word<kRecord>(a.hop_rec, (out - a.seen) + i, m[u], round);
+            record_word(a.hop_rec, (out - a.seen) + i, m[u], round);
           }
         } else {
-          store_row8<(kNT & 1u) != 0>(out + (i < total ? i : total - 1), m[u]);
+          store_row8<kNT>(out + (i < total ? i : total - 1), m[u]);
         }
         const bool own = go[u] && i < total;
         c.deliv += own ? __popcll(m[u]) : 0u;
@@ -975,125 +887,31 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
   }
 }
 
-// k_pull_top, odd W: 16-B stores over the run's 16-B aligned word pairs.  A
-// pair may straddle two rows, so its two words are loaded separately (8 B
-// each, from each node's own source: the root's row, an L2 hit, or the word
-// itself for a skipped node).  A head word (run start not 16-B aligned) and a
-// tail word go as 8-B stores by lanes 0 and 1.  Lanes past the last pair
-// repeat it (same sources, same value, same address).
-template <uint32_t kU, uint32_t kNT>
-__device__ __forceinline__ void pull_stream_odd16(const PullArgs& a, const PullTopic& P, uint32_t nb,
-                                                  uint32_t nk, const uint32_t* src, uint32_t lane,
-                                                  PullCtr& c) {
-  const uint32_t W = P.W;
-  const uint32_t total = nk * W;
-  uint64_t* const out = a.seen + P.base + static_cast<uint64_t>(nb) * W;
-  const uint32_t head = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out) >> 3) & 1u;
-  const float rw = 1.0f / static_cast<float>(W);
-  // word i of the run: its node kk = i / W and word r (as in pull_stream)
-  auto split = [&](uint32_t i, int32_t& kk, int32_t& r) {
-    kk = static_cast<int32_t>(static_cast<float>(i) * rw);
-    r = static_cast<int32_t>(i) - kk * static_cast<int32_t>(W);
-    const int32_t lo = r < 0, hi = r >= static_cast<int32_t>(W);
-    kk += hi - lo;
-    r += (lo - hi) * static_cast<int32_t>(W);
-  };
-  auto at = [&](int32_t kk, int32_t r, uint32_t i, bool& go) -> const uint64_t* {
-    const uint32_t p = src[kk];
-    go = p != kNoneNode;
-    return go ? (p == P.root ? a.a_cur : a.seen) + P.base + static_cast<uint64_t>(p) * W + r : out + i;
-  };
-  const uint32_t body = total - head;
-  if (lane < 2 && (lane == 0 ? head : (body & 1u))) {
-    const uint32_t i = lane == 0 ? 0u : total - 1;
-    int32_t kk, r;
-    split(i, kk, r);
-    bool g;
-    const uint64_t v = *at(kk, r, i, g);
-    store_row8<(kNT & 1u) != 0>(out + i, v);
-    c.deliv += g ? __popcll(v) : 0u;
-    c.sw += g;
-  }
-  const uint32_t np = body >> 1;
-  for (uint32_t j0 = 0; j0 < np; j0 += kU * 64) {
-    uint64_t lo[kU], hi[kU];
-    bool glo[kU], ghi[kU];
-#pragma unroll
-    for (uint32_t u = 0; u < kU; ++u) {
-      const uint32_t j = j0 + u * 64 + lane;
-      const uint32_t i = head + 2 * (j < np ? j : np - 1);
-      int32_t kk, r;
-      split(i, kk, r);
-      int32_t kk2 = kk, r2 = r + 1;
-      if (r2 == static_cast<int32_t>(W)) {
-        kk2 = kk + 1;
-        r2 = 0;
-      }
-      lo[u] = *at(kk, r, i, glo[u]);
-      hi[u] = *at(kk2, r2, i + 1, ghi[u]);
-    }
-#pragma unroll
-    for (uint32_t u = 0; u < kU; ++u) {
-      const uint32_t j = j0 + u * 64 + lane;
-      const uint32_t i = head + 2 * (j < np ? j : np - 1);
-      store_row16<(kNT & 1u) != 0>(out + i, uint4{static_cast<uint32_t>(lo[u]), static_cast<uint32_t>(lo[u] >> 32),
-                                                   static_cast<uint32_t>(hi[u]), static_cast<uint32_t>(hi[u] >> 32)});
-      const bool own = j < np;
-      c.deliv += own ? (glo[u] ? __popcll(lo[u]) : 0u) + (ghi[u] ? __popcll(hi[u]) : 0u) : 0u;
-      c.sw += own ? static_cast<uint32_t>(glo[u]) + static_cast<uint32_t>(ghi[u]) : 0u;
-    }
-  }
-}
-
-// Block-level counters of one level into partial slot `slot`.
-__device__ __forceinline__ uint64_t pull_ctr_pick(const uint64_t* t, uint32_t k) {
-  switch (k) {
-    case kCtrDeliveries: return t[0];
-    case kCtrEntries: return t[4];
-    case kCtrEntryWords: return t[5];
-    case kCtrChildren: return t[2];
-    case kCtrMeshChildren: return t[3];  // pull mode: nodes reached (generation writes)
-    case kCtrSeenWrites: return t[1];
-    default: return 0;
-  }
-}
-
-// wave_flush: each wave adds its own sums (no block barrier, so a finished
-// wave retires at once); else the block folds its waves first
-__device__ __forceinline__ void pull_flush(const PullCtr& c, uint64_t* partials, uint64_t slot,
-                                           uint32_t lane, uint32_t wid, bool wave_flush) {
-  __shared__ uint64_t red[kBlock / 64][6];
-  const uint64_t v6[6] = {wave_sum_u64(c.deliv), wave_sum_u64(c.sw), wave_sum_u64(c.kids),
-                          wave_sum_u64(c.reached), wave_sum_u64(c.parents), wave_sum_u64(c.pwords)};
-  if (wave_flush) {
-    const uint64_t v = lane < kNumCtr ? pull_ctr_pick(v6, lane) : 0;
-    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(partials + slot * kNumCtr + lane),
-                     static_cast<unsigned long long>(v));
-    return;
-  }
+// The block's counters of one launch into partial slot `slot` (blocks share
+// a slot: slots are zeroed per window).
+__device__ __forceinline__ void pull_flush(const PullCtr& c, uint64_t* partials, uint64_t slot, uint32_t lane,
+                                           uint32_t wid) {
+  __shared__ uint64_t red[kBlock / 64][7];
+  const uint64_t v7[7] = {wave_sum_u64(c.deliv),   wave_sum_u64(c.sw),      wave_sum_u64(c.kids),
+                          wave_sum_u64(c.reached), wave_sum_u64(c.parents), wave_sum_u64(c.pwords),
+                          wave_sum_u64(c.dup)};
   if (lane == 0)
 #pragma unroll
-    for (int q = 0; q < 6; ++q) red[wid][q] = v6[q];
+    for (int q = 0; q < 7; ++q) red[wid][q] = v7[q];
   __syncthreads();
   if (threadIdx.x < kNumCtr) {
-    uint64_t t[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t t[7] = {0, 0, 0, 0, 0, 0, 0};
     for (int w = 0; w < kBlock / 64; ++w)
 #pragma unroll
-      for (int q = 0; q < 6; ++q) t[q] += red[w][q];
+      for (int q = 0; q < 7; ++q) t[q] += red[w][q];
     const uint64_t v = pull_ctr_pick(t, threadIdx.x);
-    // blocks share a slot (slot_mod): partials are zeroed per window
     if (v) atomicAdd(reinterpret_cast<unsigned long long*>(partials + slot * kNumCtr + threadIdx.x),
                      static_cast<unsigned long long>(v));
   }
-  __syncthreads();  // `red` is reused by the next level's flush
 }
 
-// kFuse: the chunk also carries the children [g_begin, g_end) of its nodes,
-// written in the same launch (round + 1) from the same source rows, so the
-// rows of level d + 1 are never read back.  Partial slots: one per block and
-// level (fused: 2 * block + level).
-template <bool kRecord, bool kFuse, uint32_t kU, uint32_t kNT = 0>
-__global__ __launch_bounds__(kBlock, kU <= 4 ? 8 : 1) void k_pull(PullArgs a, const PullChunk* __restrict__ chunks,
+template <bool kRecord, bool kNT>
+__global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __restrict__ chunks,
                                                  uint32_t n_chunks, uint32_t round) {
   __shared__ uint32_t src_lds[kBlock / 64][kPullMaxKids];
   __shared__ uint32_t gen_lds[kBlock / 64][kPullMaxKids / 4 + 2];
@@ -1103,7 +921,7 @@ __global__ __launch_bounds__(kBlock, kU <= 4 ? 8 : 1) void k_pull(PullArgs a, co
   uint32_t* src = src_lds[wid];
   uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds[wid]);
   const uint32_t cur = a.gen_cur & 0xFF;
-  PullCtr c1, c2;
+  PullCtr c;
   if (wave < n_chunks) {  // one chunk per wave
     const PullChunk ch = chunks[wave];
     const TopicDev T = a.topics[ch.topic];
@@ -1113,136 +931,12 @@ __global__ __launch_bounds__(kBlock, kU <= 4 ? 8 : 1) void k_pull(PullArgs a, co
     P.base = T.wbase - static_cast<uint64_t>(T.nbase) * T.W;
     P.root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
     const uint32_t n1 = ch.node_end - ch.node_begin;
-    const uint32_t n2 = kFuse ? ch.g_end - ch.g_begin : 0u;
-    // LDS ops of a wave are processed in order: the tables written in phase
-    // 1 are visible to the reads that follow
-    pull_resolve<false>(a, P, ch.node_begin, n1, ch.p_lo, ch.p_hi, src, nullptr, 0, genl, lane,
-                        cur, c1);
-    if constexpr (kFuse)
-      pull_resolve<true>(a, P, ch.g_begin, n2, kNoneNode, kNoneNode, src + n1, src, ch.node_begin,
-                         genl, lane, cur, c2);
-    pull_stream<kRecord, kU, kNT>(a, P, ch.node_begin, n1, src, lane, wave, round, c1);
-    if constexpr (kFuse)
-      pull_stream<kRecord, kU, kNT>(a, P, ch.g_begin, n2, src + n1, lane, wave, round + 1, c2);
+    // LDS ops of a wave are processed in order: the table written in phase 1
+    // is visible to the reads that follow
+    pull_resolve(a, P, ch.node_begin, n1, ch.p_lo, ch.p_hi, src, genl, lane, cur, c);
+    pull_stream<kRecord, kNT>(a, P, ch.node_begin, n1, src, lane, round, c);
   }
-  if constexpr (kFuse) {
-    pull_flush(c1, a.partials, 2ull * (blockIdx.x % a.slot_mod), lane, wid, a.wave_flush);
-    pull_flush(c2, a.partials, 2ull * (blockIdx.x % a.slot_mod) + 1, lane, wid, a.wave_flush);
-  } else {
-    pull_flush(c1, a.partials, blockIdx.x % a.slot_mod, lane, wid, a.wave_flush);
-  }
-}
-
-// Top levels in one launch (one rank, every active topic starting together):
-// the chunks of levels 1..K (small rounds, latency-bound as separate
-// launches: ~6 us each for a few MB) run side by side, ch.pad = the round a
-// chunk's nodes are written in.  A node is reached iff the root was reached
-// and the node and every ancestor below the root are live (the per-level
-// rule "parent reached and node live", unrolled along the path), and then
-// receives exactly the root's arrival row, so it copies that row instead of
-// its parent's row written in the same launch.  The host pads every round's
-// chunk list to whole blocks, so a block's partial slot belongs to one round.
-__device__ __forceinline__ void pull_resolve_top(const PullArgs& a, const PullTopic& P, uint32_t nb,
-                                                 uint32_t nk, uint32_t* src, uint32_t lane,
-                                                 uint32_t cur, PullCtr& c) {
-  const bool root_up = P.root != kNoneNode && a.gen[P.root] == cur;
-  for (uint32_t j0 = 0; j0 < nk; j0 += 64) {
-    const uint32_t j = j0 + lane;
-    const bool in = j < nk;
-    uint32_t p = kNoneNode, f = 0;
-    if (in) {
-      p = a.node_parent[nb + j];
-      f = a.node_flags[nb + j];
-    }
-    uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
-    if (lane == 0) prev = nb + j0 > P.nbase ? a.node_parent[nb + j0 - 1] : kNoneNode;
-    // up_path: every ancestor between the root and the node is live (the
-    // parent is reached iff the root is).  Kept per node with the flags epoch
-    // (path_live: epoch << 2 | up_path << 1 | up_path && live), so only the
-    // first window after a graph or flags change walks.
-    const uint32_t e0 = in ? a.path_live[nb + j] : 0u;
-    bool up_path;
-    if (in && (e0 >> 2) == a.pl_epoch) {
-      up_path = (e0 >> 1) & 1u;
-    } else {
-      up_path = in && P.root != kNoneNode && p != kNoneNode;
-      uint32_t q = p;
-      for (uint32_t step = 0; up_path && q != P.root; ++step) {
-        const uint32_t fq = a.node_flags[q];
-        const uint32_t pq = a.node_parent[q];
-        up_path = (fq & kNodeLive) && pq != kNoneNode && step < 2 * kPullTopLevels;  // a walk spans < kPullTopLevels
-        q = pq;
-      }
-      if (in)
-        a.path_live[nb + j] = a.pl_epoch << 2 | (up_path ? 2u : 0u) | (up_path && (f & kNodeLive) ? 1u : 0u);
-    }
-    const bool up = root_up && up_path;
-    const bool ok = up && (f & kNodeLive);
-    if (in) src[j] = ok ? P.root : kNoneNode;
-    if (ok && !(a.dbg & kDbgNoByteStores)) a.gen[nb + j] = static_cast<uint8_t>(cur);
-    c.kids += in;
-    c.reached += ok;
-    if (up && p != prev) {
-      c.parents += 1;
-      if (p == P.root) c.pwords += P.W;  // the only row this launch reads
-    }
-  }
-}
-
-template <bool kRecord>
-__global__ __launch_bounds__(kBlock, 1) void k_pull_top(PullArgs a, const PullChunk* __restrict__ chunks,
-                                                        uint32_t n_chunks) {
-  __shared__ uint32_t src_lds[kBlock / 64][kPullMaxKids];
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // xcd_remap: blocks are dealt round-robin to the 8 XCDs; give XCD x one
-  // contiguous range of the chunk list (its own stretch of rows) instead
-  uint32_t blk = blockIdx.x;
-  if (a.xcd_remap) {
-    const uint32_t G = gridDim.x, q = G / 8, r = G % 8, x = blk % 8;
-    blk = x * q + (x < r ? x : r) + blk / 8;
-  }
-  const uint32_t wave = blk * (kBlock / 64) + wid;
-  uint32_t* src = src_lds[wid];
-  const uint32_t cur = a.gen_cur & 0xFF;
-  PullCtr c1;
-  // every chunk of a block belongs to one round (the host pads the rounds to
-  // whole blocks): the block adds into that round's kPullSlots slots
-  const uint32_t q0 = chunks[blk * (kBlock / 64)].pad;
-  if (wave < n_chunks) {
-    const PullChunk ch = chunks[wave];
-    if (ch.node_end > ch.node_begin) {  // padding chunks are empty
-      const TopicDev T = a.topics[ch.topic];
-      PullTopic P;
-      P.W = T.W;
-      P.nbase = T.nbase;
-      P.base = T.wbase - static_cast<uint64_t>(T.nbase) * T.W;
-      P.root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
-      const uint32_t n1 = ch.node_end - ch.node_begin;
-      pull_resolve_top(a, P, ch.node_begin, n1, src, lane, cur, c1);
-      // wave-uniform: the large rounds (rows nobody reads back in this
-      // launch, and too many for the MALL) store non-temporally.  Odd W moves
-      // one word per lane per access: twice the unroll keeps the same bytes
-      // in flight per wave as the 16-B pairs of even W
-      const bool nt = (a.top_nt >> (ch.pad - a.slot_base)) & 1u;
-      if (!kRecord && (P.W & 1u) && a.top_odd_wide == 2) {
-        if (nt)
-          pull_stream_odd16<8, 1>(a, P, ch.node_begin, n1, src, lane, c1);
-        else
-          pull_stream_odd16<8, 0>(a, P, ch.node_begin, n1, src, lane, c1);
-      } else if ((P.W & 1u) && a.top_odd_wide) {
-        if (nt)
-          pull_stream<kRecord, 16, 1>(a, P, ch.node_begin, n1, src, lane, wave, ch.pad, c1);
-        else
-          pull_stream<kRecord, 16, 0>(a, P, ch.node_begin, n1, src, lane, wave, ch.pad, c1);
-      } else if (nt) {
-        pull_stream<kRecord, 8, 1>(a, P, ch.node_begin, n1, src, lane, wave, ch.pad, c1);
-      } else {
-        pull_stream<kRecord, 8, 0>(a, P, ch.node_begin, n1, src, lane, wave, ch.pad, c1);
-      }
-    }
-  }
-  pull_flush(c1, a.partials, (q0 - a.slot_base) * kPullSlots + blk % kPullSlots, lane, wid, a.wave_flush);
+  pull_flush(c, a.partials, blockIdx.x % a.slot_mod, lane, wid);
 }
 
 // GPU-built node spaces have no host mirror of node_parent: the chunks'
@@ -1401,7 +1095,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_rounds(const uint64_t* __rest
   const uint32_t q = blockIdx.x;
   const uint32_t first = desc[3 * q], end = desc[3 * q + 1], stride = desc[3 * q + 2];
   uint64_t acc = 0;
-  if (q && stride && threadIdx.x < kAct) {
+  if (stride && threadIdx.x < kAct) {
     const uint32_t e1 = end * kNumCtr;
     uint32_t i = first * kNumCtr + threadIdx.x;
     if (stride == 1) {
@@ -1568,73 +1262,32 @@ hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t*
   return hipGetLastError();
 }
 
-hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, bool level,
-                         uint32_t grid, hipStream_t s) {
-  if (record && level)
-    hipLaunchKernelGGL((k_expand<true, false, true>), dim3(grid), dim3(kBlock), 0, s, a, round);
-  else if (record)
-    hipLaunchKernelGGL((k_expand<true, false, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
-  else if (level)
-    hipLaunchKernelGGL((k_expand<false, false, true>), dim3(grid), dim3(kBlock), 0, s, a, round);
+hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid, hipStream_t s) {
+  if (record)
+    hipLaunchKernelGGL((k_expand<true, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
   else
-    hipLaunchKernelGGL((k_expand<false, false, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
+    hipLaunchKernelGGL((k_expand<false, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
   return hipGetLastError();
 }
 
 hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid,
                                 hipStream_t s) {
   if (record)
-    hipLaunchKernelGGL((k_expand<true, true, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
+    hipLaunchKernelGGL((k_expand<true, true>), dim3(grid), dim3(kBlock), 0, s, a, round);
   else
-    hipLaunchKernelGGL((k_expand<false, true, false>), dim3(grid), dim3(kBlock), 0, s, a, round);
+    hipLaunchKernelGGL((k_expand<false, true>), dim3(grid), dim3(kBlock), 0, s, a, round);
   return hipGetLastError();
 }
 
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                       uint32_t grid, uint32_t round, bool record, bool fuse, uint32_t unroll,
-                       uint32_t nt, hipStream_t s) {
+                       uint32_t grid, uint32_t round, bool record, bool nt, hipStream_t s) {
   if (n_chunks == 0 || grid == 0) return hipSuccess;
-#define PSAMD_PULL(R, F, U) \
-  hipLaunchKernelGGL((k_pull<R, F, U>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round)
-  if (record) {  // parity runs: one variant
-    if (fuse)
-      PSAMD_PULL(true, true, 8);
-    else
-      PSAMD_PULL(true, false, 8);
-  } else if (nt == 1 && !fuse && unroll >= 16) {  // A/B: 16 loads in flight (pair with 2048-word chunks)
-    hipLaunchKernelGGL((k_pull<false, false, 16, 1>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
-  } else if (nt && !fuse && unroll > 4) {
-    if (nt == 1)
-      hipLaunchKernelGGL((k_pull<false, false, 8, 1>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
-    else if (nt == 2)
-      hipLaunchKernelGGL((k_pull<false, false, 8, 2>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
-    else
-      hipLaunchKernelGGL((k_pull<false, false, 8, 3>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
-  } else if (unroll <= 4) {
-    if (fuse)
-      PSAMD_PULL(false, true, 4);
-    else
-      PSAMD_PULL(false, false, 4);
-  } else {
-    if (fuse)
-      PSAMD_PULL(false, true, 8);
-    else
-      PSAMD_PULL(false, false, 8);
-  }
-#undef PSAMD_PULL
-  return hipGetLastError();
-}
-
-// lds_bytes: dynamic LDS the kernel does not use, reserved only to cap the
-// blocks per CU (waves per SIMD) of the store stream
-hipError_t launch_pull_top(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                           bool record, hipStream_t s, uint32_t lds_bytes) {
-  if (n_chunks == 0) return hipSuccess;
-  const uint32_t grid = (n_chunks + kBlock / 64 - 1) / (kBlock / 64);
-  if (record)
-    hipLaunchKernelGGL(k_pull_top<true>, dim3(grid), dim3(kBlock), lds_bytes, s, a, chunks, n_chunks);
+  if (record)  // parity runs: one variant
+    hipLaunchKernelGGL((k_pull<true, false>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
+  else if (nt)
+    hipLaunchKernelGGL((k_pull<false, true>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
   else
-    hipLaunchKernelGGL(k_pull_top<false>, dim3(grid), dim3(kBlock), lds_bytes, s, a, chunks, n_chunks);
+    hipLaunchKernelGGL((k_pull<false, false>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
   return hipGetLastError();
 }
 

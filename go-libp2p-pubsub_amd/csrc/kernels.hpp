@@ -108,7 +108,6 @@ struct ExpandArgs {
   uint64_t* partials;  // [n_waves][kNumCtr]
   uint16_t* hop_rec;   // [word*64 + bit] = round (kHopRecNone: none), record mode only
   uint32_t gen_cur;
-  uint32_t dbg;  // experiment knobs (kDbg*), 0 in production
   uint8_t* send;                  // send regions of this round (multi-GPU)
   uint64_t send_off[kMaxRanks];   // byte offset of the region for each rank
 };
@@ -118,15 +117,13 @@ struct ExpandArgs {
 // topic (at most kPullMaxKids nodes, about kPullWords words).
 struct PullChunk {
   uint32_t node_begin, node_end;  // nodes written in round r (level d)
-  uint32_t g_begin, g_end;        // fused launches: their children, written as round r + 1
   uint32_t topic;
   uint32_t p_lo, p_hi;  // parents of [node_begin, node_end) (consecutive ids), kNone: unknown
-  uint32_t pad;
+  uint32_t pad[3];
 };
 constexpr uint32_t kPullMaxKids = 512;
-constexpr uint32_t kPullTopLevels = 32;  // levels of one top launch at most (ancestor walks)
 constexpr uint32_t kNoneNode = 0xFFFFFFFFu;
-constexpr uint32_t kPullWords = 1024;  // default; PSAMD_PULL_WORDS overrides
+constexpr uint32_t kPullWords = 1024;
 
 struct PullArgs {
   const uint32_t* node_parent;  // node-space parent (kNone for roots)
@@ -138,17 +135,46 @@ struct PullArgs {
   uint16_t* hop_rec;
   uint64_t* partials;  // [n_blocks][kNumCtr]
   uint32_t gen_cur;
-  uint32_t dbg;
   uint32_t slot_mod;   // block b adds its counters into partial slot b % slot_mod (zeroed per window)
-  uint32_t slot_base;  // top launch: round q's slots start at (q - slot_base) * kPullSlots
-  uint32_t wave_flush;  // counters added per wave (no block barrier) instead of per block
-  uint32_t* path_live;  // k_pull_top: per node, epoch << 2 | parent path live << 1 | node path live
-  uint32_t pl_epoch;    // current flags epoch (< 2^30, never 0)
-  uint32_t top_nt;      // k_pull_top: bit q - slot_base set = round q stores its rows non-temporally
-  uint32_t xcd_remap;  // k_pull_top: XCD x runs one contiguous range of the blocks
-  uint32_t top_odd_wide;  // k_pull_top odd W: 2 = 16-B pair stores, 1 = 8-B words 16 in flight, 0 = 8 in flight
 };
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch
+
+// k_flood (flood.hip): every round of a single-start tree
+// window in one persistent launch.  A task = the nodes [nb, ne) of one BFS
+// level of one topic (at most kFloodMaxNodes nodes, about kFloodWords row
+// words), written in round `round`; tasks are listed level by level.
+struct FloodTask {
+  uint32_t nb, ne;          // nodes written (consecutive ids of one level)
+  uint32_t p_lo, p_hi;      // their parents (consecutive ids; k_flood_deps fills them)
+  uint32_t dep_lo, dep_hi;  // tasks writing p_lo .. p_hi (inclusive); kNoneNode: the seeded root
+  uint32_t topic, round;
+  uint32_t slot0, nslot;    // the round's partial counter slots
+  uint32_t pad[2];
+};
+// One level of one topic: its tasks are task0, task0 + 1, ... of `per` nodes
+// each, from node0 (k_flood_deps maps a parent to its task).
+struct FloodSeg {
+  uint32_t task0, node0, per, n_tasks;
+};
+struct FloodArgs {
+  const FloodTask* tasks;
+  const uint32_t* node_parent;
+  const uint8_t* node_flags;
+  const TopicDev* topics;
+  uint64_t* seen;
+  uint8_t* gen;
+  uint16_t* hop_rec;
+  uint32_t* done;       // per task: == epoch once its rows and generations are stored
+  uint64_t* partials;   // counter slots (FloodTask::slot0 ...), zeroed per window
+  uint32_t* err;        // set when a dependency wait times out
+  uint32_t n_tasks;
+  uint32_t epoch;       // this launch's publish value (never 0)
+  uint32_t gen_cur;
+  uint32_t spin_ticks;  // wait bound, s_memrealtime ticks (100 MHz)
+};
+constexpr uint32_t kFloodMaxNodes = 512;
+constexpr uint32_t kFloodWords = 2048;        // row words per task (16 KB)
+constexpr uint32_t kFloodBlocksPerCu = 4;     // resident 256-thread blocks per CU the grid uses
 
 struct ApplyArgs {
   const uint8_t* recv;
@@ -166,14 +192,6 @@ struct ApplyArgs {
   uint64_t* stats;  // [kNumCtr] of this round (deliveries, duplicates)
   uint8_t* gen;     // level mode: stamp a node reached (null: compaction mode)
   uint32_t gen_cur;
-};
-
-// k_expand experiment knobs (PSAMD_DEBUG_EXPAND); results are wrong when set
-enum : uint32_t {
-  kDbgNoArrivalLoad = 1,   // arrival words read as all-ones
-  kDbgNoArrivalStore = 2,  // skip arrival-row stores
-  kDbgNoByteStores = 4,    // skip frontier-flag and generation byte stores
-  kDbgNoSeenStore = 8,     // skip seen-row stores
 };
 
 constexpr int kBlock = 256;
@@ -218,26 +236,20 @@ hipError_t launch_apply(const ApplyArgs& a, uint32_t round, bool record, hipStre
 // next_flag / blk_flag may be null (level mode: the root is in the schedule)
 hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t* arrivals,
                        uint64_t* seen, uint8_t* next_flag, uint8_t* blk_flag, hipStream_t s);
-// level = true: the frontier is a static level schedule (every entry a live
-// internal node of the round's BFS level): entries not reached this window
-// (stale generation) are skipped and no frontier flags are raised.
-hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, bool level,
-                         uint32_t grid, hipStream_t s);
-// Level mode, pull direction: one wave per chunk (grid = ceil(n_chunks / 4));
-// fuse: each chunk also writes its nodes' children (two levels per launch).
-// unroll: 16-B loads in flight per lane (4: 8 waves/SIMD, 8: 6 waves/SIMD)
-// grid: blocks, one chunk per wave (ceil(n_chunks / 4))
+hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid, hipStream_t s);
+// Level mode, pull direction: one wave per chunk, grid = ceil(n_chunks / 4)
+// blocks; nt: the row stores are non-temporal (rounds nobody re-reads soon)
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                       uint32_t grid, uint32_t round, bool record, bool fuse, uint32_t unroll, uint32_t nt,
-                       hipStream_t s);
+                       uint32_t grid, uint32_t round, bool record, bool nt, hipStream_t s);
 
 // Fills PullChunk::p_lo / p_hi from the device node_parent (GPU-built graphs).
 hipError_t launch_chunk_parents(PullChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s);
-// Level mode, top levels in one launch (one rank, every active topic
-// starting together): chunks of several rounds (PullChunk::pad = round),
-// each round's list padded to whole blocks of kBlock / 64 chunks.
-hipError_t launch_pull_top(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                           bool record, hipStream_t s, uint32_t lds_bytes = 0);
+// k_flood (flood.hip): grid = resident blocks (<= flood_blocks_per_cu x CUs)
+hipError_t launch_flood(const FloodArgs& a, uint32_t grid, bool record, hipStream_t s);
+// FloodTask::p_lo / p_hi / dep_lo / dep_hi from node_parent and the segments
+hipError_t launch_flood_deps(FloodTask* tasks, uint32_t n, const FloodSeg* segs, const uint32_t* node_parent,
+                             hipStream_t s);
+hipError_t flood_blocks_per_cu(int* out);
 // Level mode: round q's counters = sum of the partial slots desc[3q],
 // desc[3q] + desc[3q+2], ... < desc[3q+1], for q = 1..n_rounds.
 // host_stats (nullable): device-mapped pinned rows that receive the same

@@ -27,8 +27,9 @@ PART_SUBTREE = 1
 F_RECORD_HOPS = 0x1
 F_TIME_KERNELS = 0x2
 F_NO_LAZY_SEEN = 0x4
-MODE_COMPACT, MODE_LEVEL_PUSH, MODE_LEVEL_PULL = 0, 1, 2
-MODE_KERNEL = {MODE_COMPACT: "k_expand", MODE_LEVEL_PUSH: "k_expand", MODE_LEVEL_PULL: "k_pull"}
+MODE_COMPACT, MODE_LEVEL_PULL, MODE_FLOOD = 0, 2, 3
+# ps_stats.expand_mode -> the kernel that ran the window's rounds
+MODE_KERNEL = {MODE_COMPACT: "k_expand", MODE_LEVEL_PULL: "k_pull", MODE_FLOOD: "k_flood"}
 
 # C prototypes exported by libpsengine.so: (name, restype, argtypes)
 _P = C.c_void_p

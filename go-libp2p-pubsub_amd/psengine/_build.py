@@ -12,8 +12,8 @@ LIB = os.path.join(LIBDIR, "libpsengine.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["kernels.hip", "gbuild.hip", "engine.cpp", "tree.cpp", "dist.cpp", "codec.cpp", "pubsub.cpp"]
-HEADERS = ["kernels.hpp", "gbuild.hpp", "tree.hpp", "dist.hpp"]
+SOURCES = ["kernels.hip", "flood.hip", "gbuild.hip", "engine.cpp", "tree.cpp", "dist.cpp", "codec.cpp", "pubsub.cpp"]
+HEADERS = ["kernels.hpp", "devutil.hpp", "gbuild.hpp", "tree.hpp", "dist.hpp"]
 
 
 def _stale() -> bool:
@@ -38,6 +38,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(LIB + ".tmp", LIB)
+    # hipcc leaves per-object offload bundles next to the output: not needed
+    for f in os.listdir(LIBDIR):
+        if f.startswith("libpsengine.so.") and not f.endswith(".tmp"):
+            os.remove(os.path.join(LIBDIR, f))
     return LIB
 
 

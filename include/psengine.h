@@ -62,8 +62,11 @@ typedef struct ps_config {
 
 /* ps_stats.expand_mode: how the last window's rounds ran */
 #define PS_MODE_COMPACT 0u     /* k_expand over a compacted frontier (flags + scan) */
-#define PS_MODE_LEVEL_PUSH 1u  /* k_expand over a static level schedule              */
-#define PS_MODE_LEVEL_PULL 2u  /* k_pull: next level pulls its parents' rows         */
+#define PS_MODE_LEVEL_PULL 2u  /* k_pull: one launch per round, each level pulls its
+                                  parents' rows (multi-GPU windows)                */
+#define PS_MODE_FLOOD 3u       /* k_flood: every round in one persistent launch,
+                                  each level pulls its parents' rows when the
+                                  tasks writing them have published               */
 
 typedef struct ps_stats {
   uint64_t deliveries;         /* (peer,msg) pairs delivered by this run        */

@@ -11,16 +11,19 @@ def _st(mode, launches, windows):
 
 
 def test_hot_kernel_labels():
-    # one k_pull_top launch per window (every level of a single-GPU window)
-    assert bench.hot_kernel(_st(PE.MODE_LEVEL_PULL, 1, 1)) == "k_pull_top"
-    assert bench.hot_kernel(_st(PE.MODE_LEVEL_PULL, 3, 3)) == "k_pull_top"
-    # per-level launches (multi-rank below the split level, deep windows)
+    # the kernel that ran the window's rounds, by ps_stats.expand_mode
+    assert bench.hot_kernel(_st(PE.MODE_FLOOD, 1, 1)) == "k_flood"
     assert bench.hot_kernel(_st(PE.MODE_LEVEL_PULL, 12, 1)) == "k_pull"
     assert bench.hot_kernel(_st(PE.MODE_COMPACT, 1, 1)) == "k_expand"
 
 
 def test_pmc_traffic_matches_kernel_and_workload():
-    t, src = bench.pmc_traffic("k_pull_top", "cfg3")
-    assert t is not None and t > 4.0e9 and "FETCH_SIZE" in src
-    assert bench.pmc_traffic("k_pull", "cfg3")[0] is None
-    assert bench.pmc_traffic("k_pull_top", "cfg4")[0] is None
+    """The committed PMC traffic is quoted only for the kernel and workload it
+    was measured on."""
+    import json
+    with open(bench.TRAFFIC_FILE) as fh:
+        d = json.load(fh)
+    t, src = bench.pmc_traffic(d["kernel"], d["workload"])
+    assert t is not None and t > 0 and "FETCH_SIZE" in src
+    assert bench.pmc_traffic(d["kernel"] + "_other", d["workload"])[0] is None
+    assert bench.pmc_traffic(d["kernel"], d["workload"] + "_other")[0] is None
