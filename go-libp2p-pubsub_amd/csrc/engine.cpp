@@ -131,13 +131,16 @@ struct ps_engine {
   bool flood_broken = false;  // a dependency wait timed out once: per-level launches from then on
   uint32_t flood_grid = 0;    // resident blocks (0: k_flood unavailable)
   uint32_t flood_words = kFloodWords;  // row words per task (PSAMD_FLOOD_WORDS)
-  uint32_t flood_epoch = 0;   // publish value of the last launch (done[] words never reset)
+  uint32_t flood_epoch = 0;   // granule tag of the last launch (granules are never reset)
   std::vector<uint64_t> flood_key;
   std::vector<FloodTask> flood_tasks;
   std::vector<FloodSeg> flood_segs;
   std::vector<uint32_t> flood_slot0, flood_nslot;  // per round: partial counter slots
   uint32_t flood_slots = 1;   // slots of a window (slot 0: the timeout word)
-  DevBuf d_flood_tasks, d_flood_segs, d_flood_done;
+  DevBuf d_flood_tasks, d_flood_segs, d_flood_gran;
+  bool flood_profile = false;  // PSAMD_FLOOD_PROFILE=1: per-wave phase times of k_flood to stderr (sync runs)
+  DevBuf d_flood_prof;
+  uint32_t flood_prof_waves = 0;
 
   std::vector<TopicHost> topics;
   std::vector<uint8_t> live;
@@ -992,11 +995,12 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab, const std:
 // One persistent launch (k_flood, flood.hip): every level of every active
 // topic cut into tasks of at most kFloodMaxNodes nodes and about flood_words
 // row words, listed round by round -- a topological order of "reads the
-// parent rows the previous round wrote".  Each task records the parent
-// level's segment; k_flood_deps turns it into the parent range and the tasks
-// that write it.  Per round, the tasks share min(256, tasks) counter slots
-// (slot 0 is the window's timeout word).  Cached per node space, rounds,
-// start rounds and row widths.
+// parent rows the previous round wrote".  A level's tasks publish granules of
+// gsz nodes (32, or the task size when smaller: a granule never spans two
+// tasks).  Each task records the parent level's segment; k_flood_deps turns it
+// into the parent range and its granules.  Per round, the tasks share
+// min(256, tasks) counter slots (slot 0 is the window's timeout word).
+// Cached per node space, rounds, start rounds and row widths.
 int build_flood_tasks(ps_engine* e, const std::vector<TopicDev>& tab, const std::vector<uint32_t>& tstart,
                       uint32_t rounds) {
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
@@ -1014,7 +1018,7 @@ int build_flood_tasks(ps_engine* e, const std::vector<TopicDev>& tab, const std:
   e->flood_slot0.assign(rounds + 2, 0);
   e->flood_nslot.assign(rounds + 2, 0);
   std::vector<uint32_t> seg_prev(nt, kNone);  // each topic's segment of the previous round
-  uint32_t slot = 1;
+  uint32_t slot = 1, gran = 0;
   for (uint32_t q = 1; q <= rounds; ++q) {
     const size_t first = TK.size();
     for (uint32_t t = 0; t < nt; ++t) {
@@ -1025,18 +1029,30 @@ int build_flood_tasks(ps_engine* e, const std::vector<TopicDev>& tab, const std:
       if (d + 1 >= T.level_off.size()) continue;
       const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
       if (lo == hi) continue;
-      const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kFloodMaxNodes, e->flood_words / W));
+      uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kFloodMaxNodes, e->flood_words / W));
+      const uint32_t gsz = std::min(per, kFloodGranule);
+      per -= per % gsz;  // whole granules per task
       const uint32_t pseg = d == 1 ? kNone : seg_prev[t];  // level 1: the seeded root
       seg_prev[t] = static_cast<uint32_t>(SG.size());
-      SG.push_back(FloodSeg{static_cast<uint32_t>(TK.size()), T.nbase + lo, per, ceil_div(hi - lo, per)});
+      FloodSeg sg{};
+      sg.task0 = static_cast<uint32_t>(TK.size());
+      sg.node0 = T.nbase + lo;
+      sg.per = per;
+      sg.n_tasks = ceil_div(hi - lo, per);
+      sg.gbase = gran;
+      sg.gsz = gsz;
+      sg.pad[0] = hi - lo;  // nodes of the level
+      SG.push_back(sg);
+      gran += ceil_div(hi - lo, gsz);
       for (uint32_t u = lo; u < hi; u += per) {
         FloodTask k{};
         k.nb = T.nbase + u;
         k.ne = T.nbase + std::min(u + per, hi);
-        k.dep_lo = pseg;
-        k.dep_hi = kNone;
         k.topic = t;
         k.round = q;
+        k.g_own = sg.gbase + (u - lo) / gsz;
+        k.gsz = gsz;
+        k.pseg = pseg;
         TK.push_back(k);
       }
     }
@@ -1055,9 +1071,9 @@ int build_flood_tasks(ps_engine* e, const std::vector<TopicDev>& tab, const std:
   const size_t n = TK.size();
   HIP_TRY(e->d_flood_tasks.ensure(std::max<size_t>(n, 1) * sizeof(FloodTask)), "alloc flood tasks");
   HIP_TRY(e->d_flood_segs.ensure(std::max<size_t>(SG.size(), 1) * sizeof(FloodSeg)), "alloc flood segments");
-  bool fresh = false;  // done words of a fresh allocation hold no epoch yet
-  HIP_TRY(e->d_flood_done.ensure(std::max<size_t>(n, 1) * 4, &fresh), "alloc flood done words");
-  if (fresh) HIP_TRY(hipMemsetAsync(e->d_flood_done.p, 0, e->d_flood_done.bytes, e->stream), "clear done words");
+  bool fresh = false;  // granules of a fresh allocation carry no epoch yet
+  HIP_TRY(e->d_flood_gran.ensure(std::max<size_t>(gran, 1) * 8, &fresh), "alloc flood granules");
+  if (fresh) HIP_TRY(hipMemsetAsync(e->d_flood_gran.p, 0, e->d_flood_gran.bytes, e->stream), "clear granules");
   if (n) {
     HIP_TRY(hipMemcpyAsync(e->d_flood_tasks.p, TK.data(), n * sizeof(FloodTask), hipMemcpyHostToDevice, e->stream),
             "upload flood tasks");
@@ -1174,6 +1190,35 @@ int stage_uploads(ps_engine* e, const Upload* ups, size_t n, hipStream_t s, Stag
   else if (kernel)
     HIP_TRY(launch_stage_copy(c, s), "stage copy");
   return PS_OK;
+}
+
+// Debug (PSAMD_FLOOD_PROFILE=1): where k_flood's waves spent the last launch.
+void flood_profile_report(ps_engine* e) {
+  const uint32_t nw = e->flood_prof_waves;
+  std::vector<uint64_t> p(static_cast<size_t>(nw) * kFloodProf);
+  if (hipMemcpy(p.data(), e->d_flood_prof.p, p.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+  uint64_t t0 = ~0ull, t1 = 0, smax = 0;
+  double sum[kFloodProf] = {};
+  std::vector<double> ends;
+  for (uint32_t w = 0; w < nw; ++w) {
+    const uint64_t* q = &p[static_cast<size_t>(w) * kFloodProf];
+    t0 = std::min(t0, q[0]);
+    t1 = std::max(t1, q[1]);
+    smax = std::max(smax, q[0]);
+    for (uint32_t k = 2; k < kFloodProf; ++k) sum[k] += static_cast<double>(q[k]);
+    ends.push_back(static_cast<double>(q[1]));
+  }
+  std::sort(ends.begin(), ends.end());
+  auto us = [](double ticks) { return ticks / 100.0; };  // s_memrealtime: 100 MHz
+  const double busy = sum[2] + sum[3] + sum[4] + sum[5];
+  std::fprintf(stderr,
+               "[psengine] k_flood profile: %u waves, span %.1f us, start skew %.1f us, ends p50 %.1f p90 %.1f "
+               "max %.1f us; per wave avg: wait %.1f resolve %.1f stream %.1f publish %.1f us (%.0f%%/%.0f%%/%.0f%%/"
+               "%.0f%%), %.1f tasks\n",
+               nw, us(static_cast<double>(t1 - t0)), us(static_cast<double>(smax - t0)),
+               us(ends[ends.size() / 2] - t0), us(ends[ends.size() * 9 / 10] - t0), us(ends.back() - t0),
+               us(sum[2] / nw), us(sum[3] / nw), us(sum[4] / nw), us(sum[5] / nw), 100 * sum[2] / busy,
+               100 * sum[3] / busy, 100 * sum[4] / busy, 100 * sum[5] / busy, sum[6] / nw);
 }
 
 int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<WinSlice>& win,
@@ -1560,19 +1605,25 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       fa.seen = a.seen;
       fa.gen = a.gen;
       fa.hop_rec = a.hop_rec;
-      fa.done = e->d_flood_done.as<uint32_t>();
+      fa.granules = e->d_flood_gran.as<uint64_t>();
       fa.partials = partials;
       fa.err = reinterpret_cast<uint32_t*>(partials);  // slot 0, reduced into row 0
       fa.n_tasks = static_cast<uint32_t>(e->flood_tasks.size());
-      if (++e->flood_epoch == 0) ++e->flood_epoch;  // done words from older launches hold older epochs
+      if (++e->flood_epoch == 0) ++e->flood_epoch;  // granules of older launches carry older epochs
       fa.epoch = e->flood_epoch;
       fa.gen_cur = a.gen_cur;
       fa.spin_ticks = 200000000u;  // 2 s of s_memrealtime (100 MHz)
+      if (const char* v = std::getenv("PSAMD_FLOOD_STORE")) fa.store_mode = static_cast<uint32_t>(std::atoi(v));
+      const uint32_t flood_blocks = std::min<uint32_t>(e->flood_grid, ceil_div(fa.n_tasks, kBlock / 64));
+      if (e->flood_profile) {
+        HIP_TRY(e->d_flood_prof.ensure(static_cast<size_t>(flood_blocks) * 4 * kFloodProf * 8), "alloc flood profile");
+        fa.prof = e->d_flood_prof.as<uint64_t>();
+        e->flood_prof_waves = flood_blocks * 4;
+      }
       r = 1;  // the per-round kernel times of a timed run go to round 1
       HIP_TRY(time_mark(true), "event");
       ++launches;
-      HIP_TRY(launch_flood(fa, std::min<uint32_t>(e->flood_grid, ceil_div(fa.n_tasks, kBlock / 64)), record, s),
-              "flood");
+      HIP_TRY(launch_flood(fa, flood_blocks, record, s), "flood");
       HIP_TRY(time_mark(false), "event");
     } else {
       for (r = 1; r <= planned0; ++r) {
@@ -1736,6 +1787,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
             "read apply stats");
   }
   HIP_TRY(hipStreamSynchronize(s), "sync");
+  if (mode == PS_MODE_FLOOD && e->flood_profile && e->flood_prof_waves) flood_profile_report(e);
   if (!accumulate_window(st, hs.data(), ha.data(), r, planned0, mode, launches, world)) {
     e->flood_broken = true;
     return e->fail(PS_E_DEVICE, "k_flood: a dependency wait timed out (waves not co-resident?); "
@@ -1849,11 +1901,14 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
     int bpc = 0;
     if (flood_blocks_per_cu(&bpc) == hipSuccess && bpc > 0)
       e->flood_grid = e->n_cus * std::min<uint32_t>(static_cast<uint32_t>(bpc), kFloodBlocksPerCu);
+    if (const char* v = std::getenv("PSAMD_FLOOD_BPC"))  // EXPERIMENT
+      e->flood_grid = e->n_cus * std::min<uint32_t>(static_cast<uint32_t>(bpc), static_cast<uint32_t>(std::atoi(v)));
   }
   // switches: debug timing, and the modes the parity tests cover
   if (const char* v = std::getenv("PSAMD_HOST_TIMING")) e->host_timing = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD")) e->flood_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_FLOOD_PROFILE")) e->flood_profile = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD_WORDS"))
     e->flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||

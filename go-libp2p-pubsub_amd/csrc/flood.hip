@@ -5,25 +5,29 @@
 // driven hop by hop by client.processMessages (client.go:100-132): round q
 // delivers to BFS level q - s_t of every active topic t.  A node's row of
 // 64-message words receives, in its round, its parent's row of the previous
-// round -- if the parent was reached this window (its generation byte was
-// stamped by the round that delivered to it) and the node is live (the dead
-// child is skipped, subtree.go:326-331) -- through the seen test-and-set
+// round -- if the parent was reached this window and the node is live (the
+// dead child is skipped, subtree.go:326-331) -- through the seen test-and-set
 // new = row(parent) & ~seen(node), seen(node) |= new, where a node whose
-// generation is stale has seen nothing yet (lazy reset).
+// generation byte is stale has seen nothing yet (lazy reset).
 //
-// Per-level launches (k_pull) separate the rounds by kernel boundaries.  Here
+// Per-round launches (k_pull) separate the rounds by kernel boundaries.  Here
 // the rounds are ordered by dataflow inside one launch:
-//   * the host cuts every level of every topic into tasks (a contiguous node
-//     run of one level, about kFloodWords row words), listed level by level: a
-//     topological order of "reads the rows the previous round wrote";
+//   * the host cuts every level of every topic into tasks (a run of at most
+//     64 consecutive nodes of one level, about kFloodWords row words), listed
+//     level by level: a topological order of "reads the rows the previous
+//     round wrote";
 //   * wave g of the G co-resident waves runs tasks g, g + G, g + 2G, ... in
-//     order.  A task first waits until every task writing its parents' rows
-//     has published done[task] == epoch, then pulls those rows;
-//   * a task publishes once its own rows and generation bytes have drained.
+//     order.  A task's lanes poll the granules of their parents -- 8-B words
+//     {epoch, reach bits} its parents' tasks published -- until every one
+//     carries this launch's epoch: that is both the dependency wait and the
+//     frontier test (parent reached this window), in one load;
+//   * the task then pulls the parents' rows, stores its own rows, and once
+//     they have drained publishes its own granules.
 // Hand-off (MI355X_MICROARCH.md §Workgroup dispatch... Valid forms; Guideline
-// 16 R1): rows are stored write-through (sc1 buffer stores), generation bytes
-// and the done word by agent-scope relaxed stores (sc1), and every load of a
-// handed-off byte is an sc1 load -- no fence, correct for any placement.
+// 16 R1/R2): rows are stored write-through (sc1 buffer stores) and drained
+// before the granule store; granules are single 8-B agent-scope stores (data
+// and tag together); every load of a handed-off byte is an sc1 load.  No
+// fence, correct for any placement.
 // Deadlock freedom: every dependency points to an earlier task, and the grid
 // never exceeds the resident capacity, so the wave holding the earliest
 // unfinished task always runs.  Every wait is bounded: a timeout sets *err
@@ -38,92 +42,29 @@ using namespace dev;
 
 constexpr uint32_t kMergeBit = 0x80000000u;  // src[]: the node already holds rows of this window
 
-// Waits until done[lo..hi] == epoch (relaxed sc1 polls, s_sleep back-off).
-// Bounded: past spin_ticks the wait sets *err and gives up; a wait longer
-// than 10 ms also gives up once another wave has set *err, so a launch whose
-// waves were not all resident drains in about one timeout.
-__device__ __forceinline__ bool flood_wait(const FloodArgs& a, uint32_t lo, uint32_t hi, uint32_t lane) {
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    bool ok = true;
-    for (uint32_t d = lo + lane; d <= hi; d += 64) ok &= ld_agent(a.done + d) == a.epoch;
-    if (__all(ok)) return true;
-    const uint64_t waited = __builtin_amdgcn_s_memrealtime() - t0;
-    if (waited > a.spin_ticks || (waited > 1000000u && ld_agent(a.err) != 0)) {
-      if (lane == 0) atomicOr(a.err, 1u);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
-
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // The task record, wave-uniform (scalar registers: buffer descriptors built
 // from it stay scalar, no per-lane loops).
-__device__ __forceinline__ FloodTask load_task(const FloodTask* p) {
-  FloodTask t = *p;
+__device__ __forceinline__ FloodTask uniform(FloodTask t) {
   t.nb = rfl(t.nb);
   t.ne = rfl(t.ne);
-  t.p_lo = rfl(t.p_lo);
-  t.p_hi = rfl(t.p_hi);
-  t.dep_lo = rfl(t.dep_lo);
-  t.dep_hi = rfl(t.dep_hi);
   t.topic = rfl(t.topic);
   t.round = rfl(t.round);
   t.slot0 = rfl(t.slot0);
   t.nslot = rfl(t.nslot);
+  t.g_own = rfl(t.g_own);
+  t.gsz = rfl(t.gsz);
+  t.p_lo = rfl(t.p_lo);
+  t.p_hi = rfl(t.p_hi);
+  t.pg_lo = rfl(t.pg_lo);
+  t.pnode0 = rfl(t.pnode0);
+  t.pgsz = rfl(t.pgsz);
   return t;
 }
 
-__device__ __forceinline__ uint8_t ld_agent_u8(const uint8_t* p) {
-  return __hip_atomic_load(const_cast<uint8_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Phase 1 for the task's nodes: src[j] = the parent whose row node nb + j
-// receives (| kMergeBit when the node already holds messages of this window),
-// or kNoneNode (parent not reached, or node not live).  Reached nodes get
-// their generation stamped (sc1: their children read it).  Returns whether
-// some node needs the merging path.
-__device__ __forceinline__ bool flood_resolve(const FloodArgs& a, const FloodTask& T, uint32_t nbase,
-                                              uint32_t W, uint32_t* src, uint8_t* genl, uint32_t lane,
-                                              uint32_t cur, PullCtr& c) {
-  const uint32_t nk = T.ne - T.nb;
-  // the parents' generation bytes, staged as whole dwords when the range is short
-  const bool staged = T.p_hi - T.p_lo < kFloodMaxNodes;
-  const uint32_t g0 = T.p_lo & ~3u;
-  if (staged) {
-    const uint32_t nd = (((T.p_hi + 4u) & ~3u) - g0) >> 2;
-    for (uint32_t d = lane; d < nd; d += 64)
-      reinterpret_cast<uint32_t*>(genl)[d] = ld_agent(reinterpret_cast<const uint32_t*>(a.gen + g0) + d);
-  }
-  bool merge = false;
-  for (uint32_t j0 = 0; j0 < nk; j0 += 64) {
-    const uint32_t j = j0 + lane;
-    const bool in = j < nk;
-    uint32_t p = kNoneNode, f = 0, own = 0;
-    if (in) {
-      p = a.node_parent[T.nb + j];
-      f = a.node_flags[T.nb + j];
-      own = a.gen[T.nb + j];  // only this wave writes this byte in this launch
-    }
-    uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
-    if (lane == 0) prev = T.nb + j0 > nbase ? a.node_parent[T.nb + j0 - 1] : kNoneNode;
-    bool up = in && p >= T.p_lo && p <= T.p_hi;  // (kNoneNode fails the range)
-    if (up) up = (staged ? genl[p - g0] : ld_agent_u8(a.gen + p)) == cur;
-    const bool ok = up && (f & kNodeLive);
-    const bool fresh = own != cur;
-    if (in) src[j] = ok ? (p | (fresh ? 0u : kMergeBit)) : kNoneNode;
-    if (ok) st_agent(a.gen + T.nb + j, static_cast<uint8_t>(cur));
-    merge |= ok && !fresh;
-    c.kids += in;
-    c.reached += ok;
-    if (up && p != prev) {  // a reached parent counts once, at its first child
-      c.parents += 1;
-      c.pwords += W;
-    }
-  }
-  return __any(merge);
+__device__ __forceinline__ uint64_t ld_agent64(const uint64_t* p) {
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Row kk = i / W and word r of word i of the run (float estimate, off by at
@@ -136,12 +77,12 @@ __device__ __forceinline__ void split_word(uint32_t i, float rw, uint32_t W, int
   r += (lo - hi) * static_cast<int32_t>(W);
 }
 
-// Phase 2, even W: the task's rows as one output stream of 16-B word pairs
+// Stream, even W: the task's rows as one output stream of 16-B word pairs
 // (rows and pairs 16-B aligned), each pair loaded from the parent row it
 // receives.  8 loads in flight per lane, then 8 stores; a skipped node's pair
 // and a lane past the end use an out-of-range offset (load 0, store dropped):
 // no branches, so the compiler counts vmcnt exactly.
-template <bool kRecord>
+template <bool kRecord, int kAux>
 __device__ __forceinline__ void flood_stream_even(const FloodArgs& a, uint64_t* out_row, uint32_t total,
                                                   uint32_t W, __amdgpu_buffer_rsrc_t in, uint32_t pbase,
                                                   const uint32_t* src, uint32_t lane, uint32_t round,
@@ -164,7 +105,7 @@ __device__ __forceinline__ void flood_stream_even(const FloodArgs& a, uint64_t* 
     }
 #pragma unroll
     for (uint32_t u = 0; u < kU; ++u) {
-      st16_sc1(out, so[u], v[u]);
+      st16_aux<kAux>(out, so[u], v[u]);
       const bool own = so[u] != kOutOfRange;
       c.deliv += own ? popc4(v[u]) : 0u;
       c.sw += own ? 2u : 0u;
@@ -179,7 +120,7 @@ __device__ __forceinline__ void flood_stream_even(const FloodArgs& a, uint64_t* 
   }
 }
 
-// Phase 2, odd W: 16-B stores over the run's 16-B aligned word pairs; a pair
+// Stream, odd W: 16-B stores over the run's 16-B aligned word pairs; a pair
 // may straddle two rows, so its two words are loaded separately (8 B each,
 // from each node's own source).  A head word (run not 16-B aligned) and a
 // tail word go as 8-B stores by lanes 0 and 1.  A pair with one skipped half
@@ -260,10 +201,9 @@ __device__ void flood_stream_merge(const FloodArgs& a, uint64_t* out_row, uint32
     const uint32_t s = src[kk];
     if (s == kNoneNode) continue;
     const uint32_t p = s & ~kMergeBit;
-    const uint64_t m = __hip_atomic_load(const_cast<uint64_t*>(prow) + static_cast<uint64_t>(p - pbase) * W + r,
-                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t m = ld_agent64(prow + static_cast<uint64_t>(p - pbase) * W + r);
     uint64_t* o = out_row + i;
-    const uint64_t own = (s & kMergeBit) ? __hip_atomic_load(o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    const uint64_t own = (s & kMergeBit) ? ld_agent64(o) : 0ull;
     const uint64_t nm = m & ~own;
     __hip_atomic_store(o, own | nm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     c.deliv += __popcll(nm);
@@ -286,59 +226,136 @@ __device__ __forceinline__ void flood_flush(const FloodArgs& a, PullCtr& c, uint
   c = PullCtr{};
 }
 
-template <bool kRecord>
+template <bool kRecord, int kAux>
 __global__ __launch_bounds__(kBlock, kFloodBlocksPerCu) void k_flood(FloodArgs a) {
   __shared__ uint32_t src_lds[kBlock / 64][kFloodMaxNodes];
-  __shared__ uint32_t gen_lds[kBlock / 64][kFloodMaxNodes / 4 + 2];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t wave = blockIdx.x * (kBlock / 64) + wid;
   const uint32_t nw = gridDim.x * (kBlock / 64);
   uint32_t* src = src_lds[wid];
-  uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds[wid]);
   const uint32_t cur = a.gen_cur & 0xFF;
   PullCtr c;
   uint32_t slot = kNoneNode, round = 0;
+  uint64_t pf[kFloodProf] = {0, 0, 0, 0, 0, 0, 0, 0};  // debug profile (a.prof)
+  auto stamp = [&]() -> uint64_t { return a.prof ? __builtin_amdgcn_s_memrealtime() : 0; };
+  uint64_t t_a = stamp();
+  pf[0] = t_a;
+  FloodTask T = uniform(a.tasks[wave < a.n_tasks ? wave : 0]);
   for (uint32_t ti = wave; ti < a.n_tasks; ti += nw) {
-    const FloodTask T = load_task(a.tasks + ti);
     if (T.round != round) {  // tasks come level by level: a wave's rounds only grow
       if (slot != kNoneNode) flood_flush(a, c, slot, lane);
       round = T.round;
       slot = T.slot0 + wave % T.nslot;
     }
-    // round - 1 must have written the parents' rows: wait for their tasks
-    if (T.dep_lo != kNoneNode) (void)flood_wait(a, T.dep_lo, T.dep_hi, lane);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the loads below the poll
+    const uint32_t nk = T.ne - T.nb;
+    // this task's nodes, one per lane (static data: loaded before the wait)
+    const bool in = lane < nk;
+    uint32_t p = kNoneNode, f = 0, own = 0, prev = kNoneNode;
+    if (in) {
+      p = a.node_parent[T.nb + lane];
+      f = a.node_flags[T.nb + lane];
+      own = a.gen[T.nb + lane];  // only this wave writes this byte in this launch
+    }
     const TopicDev D = a.topics[T.topic];
+    // the next task's record, consumed after this one
+    const FloodTask Tn = a.tasks[ti + nw < a.n_tasks ? ti + nw : ti];
+    if (lane == 0 && T.nb > 0) prev = a.node_parent[T.nb - 1];
+    // round - 1's granules of the parents: the dependency wait and the
+    // frontier test (parent reached this window) in one load
+    bool up = false;
+    if (T.pg_lo == kNoneNode) {
+      up = in;  // level 1: the parent is the topic root, seeded this window
+    } else {
+      const uint32_t rel = in ? p - T.pnode0 : T.p_lo - T.pnode0;
+      const uint64_t* gp = a.granules + T.pg_lo + (rel / T.pgsz - (T.p_lo - T.pnode0) / T.pgsz);
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      uint64_t g = 0;
+      bool have = !in;
+      for (;;) {
+        if (!have) {
+          g = ld_agent64(gp);
+          have = static_cast<uint32_t>(g >> 32) == a.epoch;
+        }
+        if (__all(have)) break;
+        const uint64_t waited = __builtin_amdgcn_s_memrealtime() - t0;
+        if (waited > a.spin_ticks || (waited > 1000000u && ld_agent(a.err) != 0)) {
+          if (lane == 0) atomicOr(a.err, 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      up = in && ((g >> (rel % T.pgsz)) & 1u);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the row loads below the poll
+    uint64_t t_b = stamp();
+    pf[2] += t_b - t_a;
     const uint32_t W = rfl(D.W), nbase = rfl(D.nbase);
     const uint64_t wbase = static_cast<uint64_t>(rfl(static_cast<uint32_t>(D.wbase >> 32))) << 32 |
                            rfl(static_cast<uint32_t>(D.wbase));
     const uint64_t base = wbase - static_cast<uint64_t>(nbase) * W;
-    const uint32_t total = (T.ne - T.nb) * W;
-    const bool merge = flood_resolve(a, T, nbase, W, src, genl, lane, cur, c);
+    // resolve: the parent whose row each node receives
+    const bool ok = up && (f & kNodeLive);
+    const bool fresh = own != cur;
+    if (in) src[lane] = ok ? (p | (fresh ? 0u : kMergeBit)) : kNoneNode;
+    const bool merge = __any(ok && !fresh);
+    {
+      uint32_t pv = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
+      if (lane == 0) pv = T.nb > nbase ? prev : kNoneNode;
+      c.kids += in;
+      c.reached += ok;
+      if (up && p != pv) {  // a reached parent counts once, at its first child
+        c.parents += 1;
+        c.pwords += W;
+      }
+    }
+    if (a.prof) {
+      const uint64_t t = stamp();
+      pf[3] += t - t_b;
+      t_b = t;
+    }
+    // stream the rows
+    const uint32_t total = nk * W;
     uint64_t* out_row = a.seen + base + static_cast<uint64_t>(T.nb) * W;
     const uint64_t* prow = a.seen + base + static_cast<uint64_t>(T.p_lo) * W;
     const uint64_t span = static_cast<uint64_t>(T.p_hi - T.p_lo + 1) * W * 8;
     if (merge || span >= kOutOfRange) {
       flood_stream_merge<kRecord>(a, out_row, total, W, prow, T.p_lo, src, lane, T.round, c);
     } else {
-      const __amdgpu_buffer_rsrc_t in = rsrc(prow, static_cast<uint32_t>(span));
+      const __amdgpu_buffer_rsrc_t rin = rsrc(prow, static_cast<uint32_t>(span));
       if (W & 1u)
-        flood_stream_odd<kRecord>(a, out_row, total, W, in, T.p_lo, src, lane, T.round, c);
+        flood_stream_odd<kRecord>(a, out_row, total, W, rin, T.p_lo, src, lane, T.round, c);
       else
-        flood_stream_even<kRecord>(a, out_row, total, W, in, T.p_lo, src, lane, T.round, c);
+        flood_stream_even<kRecord, kAux>(a, out_row, total, W, rin, T.p_lo, src, lane, T.round, c);
     }
-    // publish: every row and generation store of this wave has reached the
-    // device-coherent level before the done word does
+    // the node's generation (read by later windows and the readbacks only)
+    if (ok) a.gen[T.nb + lane] = static_cast<uint8_t>(cur);
+    const uint64_t reach = __ballot(ok);
+    const uint64_t t_c = stamp();
+    pf[4] += t_c - t_b;
+    // publish: every row store of this wave has reached the device-coherent
+    // level before the granules do
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) st_agent(a.done + ti, a.epoch);
+    const uint32_t ng = (nk + T.gsz - 1) / T.gsz;
+    if (lane < ng) {
+      const uint64_t bits = (reach >> (lane * T.gsz)) & (T.gsz >= 64 ? ~0ull : (1ull << T.gsz) - 1ull);
+      __hip_atomic_store(a.granules + T.g_own + lane, static_cast<uint64_t>(a.epoch) << 32 | bits,
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    T = uniform(Tn);
+    t_a = stamp();
+    pf[5] += t_a - t_c;
+    pf[6] += 1;
   }
   if (slot != kNoneNode) flood_flush(a, c, slot, lane);
+  if (a.prof && lane == 0) {
+    pf[1] = stamp();
+    for (uint32_t k = 0; k < kFloodProf; ++k) a.prof[static_cast<uint64_t>(wave) * kFloodProf + k] = pf[k];
+  }
 }
 
-// Parents and dependencies of every task: p_lo / p_hi from the node space,
-// and the tasks of the previous level that write them (FloodTask::dep_lo
-// holds that level's segment until then).
+// Parents of every task (p_lo / p_hi from the node space) and the granules
+// of the parent level that hold them.
 __global__ __launch_bounds__(kBlock) void k_flood_deps(FloodTask* __restrict__ tasks, uint32_t n,
                                                        const FloodSeg* __restrict__ segs,
                                                        const uint32_t* __restrict__ node_parent) {
@@ -347,13 +364,19 @@ __global__ __launch_bounds__(kBlock) void k_flood_deps(FloodTask* __restrict__ t
   FloodTask t = tasks[i];
   t.p_lo = node_parent[t.nb];
   t.p_hi = node_parent[t.ne - 1];
-  if (t.dep_lo != kNoneNode) {
-    const FloodSeg s = segs[t.dep_lo];
-    // (clamped to the segment: a malformed parent can only mis-order, never
-    // index outside the done words)
-    const uint32_t last = s.n_tasks - 1;
-    t.dep_lo = s.task0 + min(last, (t.p_lo >= s.node0 ? t.p_lo - s.node0 : 0u) / s.per);
-    t.dep_hi = s.task0 + min(last, (t.p_hi >= s.node0 ? t.p_hi - s.node0 : 0u) / s.per);
+  if (t.pseg == kNoneNode) {
+    t.pg_lo = kNoneNode;
+  } else {
+    const FloodSeg s = segs[t.pseg];
+    // a parent outside its level could only mis-order, never index outside
+    // the granules (clamped)
+    const uint32_t nodes = s.pad[0];
+    const uint32_t lo = t.p_lo >= s.node0 ? min(t.p_lo - s.node0, nodes - 1) : 0u;
+    if (t.p_hi < t.p_lo || t.p_hi - s.node0 >= nodes) t.p_hi = s.node0 + nodes - 1;
+    t.p_lo = s.node0 + lo;
+    t.pg_lo = s.gbase + lo / s.gsz;
+    t.pnode0 = s.node0;
+    t.pgsz = s.gsz;
   }
   tasks[i] = t;
 }
@@ -363,9 +386,13 @@ __global__ __launch_bounds__(kBlock) void k_flood_deps(FloodTask* __restrict__ t
 hipError_t launch_flood(const FloodArgs& a, uint32_t grid, bool record, hipStream_t s) {
   if (a.n_tasks == 0 || grid == 0) return hipSuccess;
   if (record)
-    hipLaunchKernelGGL(k_flood<true>, dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((k_flood<true, kAuxSC1>), dim3(grid), dim3(kBlock), 0, s, a);
+  else if (a.store_mode == 1)  // EXPERIMENT: plain even-W row stores
+    hipLaunchKernelGGL((k_flood<false, 0>), dim3(grid), dim3(kBlock), 0, s, a);
+  else if (a.store_mode == 2)  // EXPERIMENT: nt even-W row stores
+    hipLaunchKernelGGL((k_flood<false, 2>), dim3(grid), dim3(kBlock), 0, s, a);
   else
-    hipLaunchKernelGGL(k_flood<false>, dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((k_flood<false, kAuxSC1>), dim3(grid), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
@@ -380,8 +407,8 @@ hipError_t launch_flood_deps(FloodTask* tasks, uint32_t n, const FloodSeg* segs,
 // Resident k_flood blocks per CU (both instances; the smaller bounds the grid).
 hipError_t flood_blocks_per_cu(int* out) {
   int a = 0, b = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_flood<false>, kBlock, 0);
-  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_flood<true>, kBlock, 0);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_flood<false, kAuxSC1>, kBlock, 0);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_flood<true, kAuxSC1>, kBlock, 0);
   *out = a < b ? a : b;
   return e;
 }

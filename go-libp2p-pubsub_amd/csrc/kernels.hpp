@@ -141,20 +141,26 @@ constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launc
 
 // k_flood (flood.hip): every round of a single-start tree
 // window in one persistent launch.  A task = the nodes [nb, ne) of one BFS
-// level of one topic (at most kFloodMaxNodes nodes, about kFloodWords row
-// words), written in round `round`; tasks are listed level by level.
+// level of one topic (at most kFloodMaxNodes = one per lane, about
+// kFloodWords row words), written in round `round`; tasks are listed level by
+// level.  A task publishes which of its nodes were reached as granules: one
+// 8-B word {epoch << 32 | reach bits} per `gsz` consecutive nodes of its level
+// (data and flag in one store); its children's tasks poll those granules.
 struct FloodTask {
   uint32_t nb, ne;          // nodes written (consecutive ids of one level)
-  uint32_t p_lo, p_hi;      // their parents (consecutive ids; k_flood_deps fills them)
-  uint32_t dep_lo, dep_hi;  // tasks writing p_lo .. p_hi (inclusive); kNoneNode: the seeded root
   uint32_t topic, round;
   uint32_t slot0, nslot;    // the round's partial counter slots
-  uint32_t pad[2];
+  uint32_t g_own, gsz;      // granules written: g_own, g_own + 1, ... (gsz nodes each)
+  uint32_t p_lo, p_hi;      // parents of the run (consecutive ids)              [k_flood_deps]
+  uint32_t pg_lo, pg_hi;    // parent granules to poll; kNoneNode: parent = root [k_flood_deps]
+  uint32_t pnode0, pgsz;    // parent level: first node and nodes per granule    [k_flood_deps]
+  uint32_t pseg, pad;       // host: the parent level's segment (kNoneNode: root)
 };
-// One level of one topic: its tasks are task0, task0 + 1, ... of `per` nodes
-// each, from node0 (k_flood_deps maps a parent to its task).
+// One level of one topic: tasks task0 .. task0 + n_tasks - 1 of `per` nodes
+// each from node0, granules gbase .. of gsz nodes each.
 struct FloodSeg {
   uint32_t task0, node0, per, n_tasks;
+  uint32_t gbase, gsz, pad[2];
 };
 struct FloodArgs {
   const FloodTask* tasks;
@@ -164,15 +170,21 @@ struct FloodArgs {
   uint64_t* seen;
   uint8_t* gen;
   uint16_t* hop_rec;
-  uint32_t* done;       // per task: == epoch once its rows and generations are stored
+  uint64_t* granules;   // per granule: epoch << 32 | reach bits, once its task's rows are stored
   uint64_t* partials;   // counter slots (FloodTask::slot0 ...), zeroed per window
   uint32_t* err;        // set when a dependency wait times out
   uint32_t n_tasks;
-  uint32_t epoch;       // this launch's publish value (never 0)
+  uint32_t epoch;       // this launch's granule tag (never 0)
   uint32_t gen_cur;
   uint32_t spin_ticks;  // wait bound, s_memrealtime ticks (100 MHz)
+  uint32_t store_mode;  // EXPERIMENT (PSAMD_FLOOD_STORE): 0 sc1, 1 plain, 2 nt
+  uint64_t* prof;       // debug (PSAMD_FLOOD_PROFILE): per wave kFloodProf s_memrealtime stamps / sums
 };
-constexpr uint32_t kFloodMaxNodes = 512;
+// per-wave profile words: first task start, last task end, then summed ticks
+// waiting, resolving, streaming, publishing; tasks run
+constexpr uint32_t kFloodProf = 8;
+constexpr uint32_t kFloodMaxNodes = 64;       // one node per lane
+constexpr uint32_t kFloodGranule = 32;        // reach bits per granule at most
 constexpr uint32_t kFloodWords = 2048;        // row words per task (16 KB)
 constexpr uint32_t kFloodBlocksPerCu = 4;     // resident 256-thread blocks per CU the grid uses
 
@@ -246,7 +258,7 @@ hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_ch
 hipError_t launch_chunk_parents(PullChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s);
 // k_flood (flood.hip): grid = resident blocks (<= flood_blocks_per_cu x CUs)
 hipError_t launch_flood(const FloodArgs& a, uint32_t grid, bool record, hipStream_t s);
-// FloodTask::p_lo / p_hi / dep_lo / dep_hi from node_parent and the segments
+// FloodTask::p_lo / p_hi / pg_lo / pg_hi / pnode0 / pgsz from node_parent and the segments
 hipError_t launch_flood_deps(FloodTask* tasks, uint32_t n, const FloodSeg* segs, const uint32_t* node_parent,
                              hipStream_t s);
 hipError_t flood_blocks_per_cu(int* out);

@@ -47,6 +47,8 @@ def lib():
         L.or_disseminate.restype = C.c_int64
         L.or_disseminate.argtypes = [C.c_uint32, u32p, u32p, C.c_uint32, u8p, C.c_uint32,
                                      u32p, u8p, C.POINTER(C.c_uint64), C.c_uint32, C.c_int]
+        L.or_levels_bits.restype = C.c_int64
+        L.or_levels_bits.argtypes = [C.c_uint32, u32p, u32p, C.c_uint32, u8p, C.c_uint32, C.c_int]
         L.or_splitmix64.argtypes = [C.POINTER(C.c_uint64)]
         L.or_splitmix64.restype = C.c_uint64
         _lib = L
@@ -135,3 +137,16 @@ def disseminate(row_ptr, col, root: int, live, n_msgs: int, want_hops: bool = Tr
     if tot < 0:
         raise RuntimeError(f"or_disseminate -> {tot}")
     return int(tot), hops, hist
+
+
+def levels_bits(row_ptr, col, root: int, live, n_msgs: int, threads: int = 1) -> int:
+    """The hot path as the GPU engine computes it (messages as bits, rounds
+    level-synchronous, OpenMP over each level's nodes): total deliveries."""
+    row_ptr = np.ascontiguousarray(row_ptr, dtype=np.uint32)
+    col = np.ascontiguousarray(col, dtype=np.uint32)
+    live = np.ascontiguousarray(live, dtype=np.uint8)
+    tot = lib().or_levels_bits(row_ptr.shape[0] - 1, _ptr(row_ptr, C.c_uint32), _ptr(col, C.c_uint32), root,
+                               _ptr(live, C.c_uint8), n_msgs, threads)
+    if tot < 0:
+        raise RuntimeError(f"or_levels_bits -> {tot}")
+    return int(tot)

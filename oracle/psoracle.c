@@ -276,8 +276,20 @@ int or_tree_message(or_tree* t, uint8_t* hop_out) {
   for (uint32_t qi = 0; qi < nq; qi++) {
     uint32_t P = q[qi];
     or_clist* L = &t->ch[P];
-    uint32_t failed[64];
-    uint32_t failed_rep[64];
+    /* every failed child is repaired (subtree.go:342-349), however wide the
+     * fan-out: the list holds up to L->n entries */
+    uint32_t stack_f[64], stack_r[64];
+    uint32_t* failed = stack_f;
+    uint32_t* failed_rep = stack_r;
+    if (L->n > 64) {
+      failed = (uint32_t*)malloc((size_t)L->n * sizeof(uint32_t));
+      failed_rep = (uint32_t*)malloc((size_t)L->n * sizeof(uint32_t));
+      if (!failed || !failed_rep) {
+        free(failed);
+        free(failed_rep);
+        return OR_E_NOMEM;
+      }
+    }
     uint32_t nf = 0;
     uint32_t w = 0;
     for (uint32_t i = 0; i < L->n; i++) {
@@ -290,11 +302,9 @@ int or_tree_message(or_tree* t, uint8_t* hop_out) {
         continue;
       }
       if (t->state[e.id] == OR_FAILED) { /* write error, subtree.go:333-336 */
-        if (nf < 64) {
-          failed[nf] = e.id;
-          failed_rep[nf] = e.reported;
-          nf++;
-        }
+        failed[nf] = e.id;
+        failed_rep[nf] = e.reported;
+        nf++;
         continue;
       }
       L->v[w++] = e;
@@ -302,6 +312,10 @@ int or_tree_message(or_tree* t, uint8_t* hop_out) {
     L->n = w;
     for (uint32_t i = 0; i < nf; i++) /* subtree.go:342-349 */
       redistribute(t, P, failed[i], failed_rep[i]);
+    if (failed != stack_f) {
+      free(failed);
+      free(failed_rep);
+    }
   }
   return OR_OK;
 }
@@ -399,5 +413,81 @@ int64_t or_disseminate(uint32_t n, const uint32_t* row_ptr, const uint32_t* col,
     free(hist);
   }
   if (err) return OR_E_NOMEM;
+  return total;
+}
+
+/* The same hot path, restated the way the GPU engine computes it (CPU
+ * baseline, bench.py): messages as bits, 64 per u64 word, and the rounds
+ * level-synchronous -- round d writes every node of BFS level d, in parallel
+ * over the level's nodes (OpenMP): a node whose parent was reached and which
+ * is live receives new = row(parent) & ~seen(node) (seen is empty: each node
+ * is reached once on a tree, subtree.go:324-337 / client.go:124-130).  Rows
+ * are BFS-position major.  Returns total deliveries (popcount of every new
+ * word), or <0 on error. */
+int64_t or_levels_bits(uint32_t n, const uint32_t* row_ptr, const uint32_t* col, uint32_t root,
+                       const uint8_t* live, uint32_t n_msgs, int n_threads) {
+  if (root >= n) return OR_E_INVAL;
+  if (n_threads < 1) n_threads = 1;
+  if (n_msgs == 0) return 0;
+  const uint32_t W = (n_msgs + 63) / 64;
+  /* BFS numbering: order[], parent position, level starts */
+  uint32_t* order = (uint32_t*)malloc(sizeof(uint32_t) * n);
+  uint32_t* ppos = (uint32_t*)malloc(sizeof(uint32_t) * n);
+  uint32_t* pos = (uint32_t*)malloc(sizeof(uint32_t) * n);
+  uint32_t* lvl = (uint32_t*)malloc(sizeof(uint32_t) * (n + 2));
+  if (!order || !ppos || !pos || !lvl) {
+    free(order), free(ppos), free(pos), free(lvl);
+    return OR_E_NOMEM;
+  }
+  for (uint32_t i = 0; i < n; i++) pos[i] = OR_NONE;
+  uint32_t qt = 0, nl = 0;
+  order[qt] = root;
+  ppos[qt] = OR_NONE;
+  pos[root] = qt++;
+  lvl[nl++] = 0;
+  uint32_t lo = 0;
+  while (lo < qt) {
+    const uint32_t hi = qt;
+    lvl[nl++] = hi;
+    for (uint32_t i = lo; i < hi; i++)
+      for (uint32_t e = row_ptr[order[i]]; e < row_ptr[order[i] + 1]; e++) {
+        const uint32_t c = col[e];
+        if (pos[c] != OR_NONE) continue;
+        pos[c] = qt;
+        order[qt] = c;
+        ppos[qt++] = i;
+      }
+    lo = hi;
+  }
+  uint64_t* rows = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)qt * W);
+  uint8_t* reached = (uint8_t*)calloc(qt, 1);
+  if (!rows || !reached) {
+    free(order), free(ppos), free(pos), free(lvl), free(rows), free(reached);
+    return OR_E_NOMEM;
+  }
+  /* PublishMessage: the root holds the window's messages (not a recipient) */
+  for (uint32_t w = 0; w < W; w++) rows[w] = ~0ull;
+  if (n_msgs % 64) rows[W - 1] = (1ull << (n_msgs % 64)) - 1;
+  reached[0] = 1;
+  int64_t total = 0;
+  for (uint32_t d = 1; d + 1 < nl; d++) {
+    const int64_t a = lvl[d], b = lvl[d + 1];
+#pragma omp parallel for num_threads(n_threads) schedule(static, 256) reduction(+ : total)
+    for (int64_t u = a; u < b; u++) {
+      const uint32_t p = ppos[u];
+      if (!reached[p] || !live[order[u]]) continue;
+      reached[u] = 1;
+      const uint64_t* src = rows + (size_t)p * W;
+      uint64_t* dst = rows + (size_t)u * W;
+      int64_t k = 0;
+      for (uint32_t w = 0; w < W; w++) {
+        const uint64_t nw = src[w]; /* & ~seen(u): empty for a fresh node */
+        dst[w] = nw;
+        k += __builtin_popcountll(nw);
+      }
+      total += k;
+    }
+  }
+  free(order), free(ppos), free(pos), free(lvl), free(rows), free(reached);
   return total;
 }

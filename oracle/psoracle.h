@@ -83,6 +83,12 @@ int64_t or_disseminate(uint32_t n, const uint32_t* row_ptr, const uint32_t* col,
                        const uint32_t* start_round, uint8_t* hop_out,
                        uint64_t* hist_out, uint32_t hist_len, int n_threads);
 
+/* The hot path as the GPU engine computes it (bench CPU baseline): messages
+ * as bits (64 per u64), rounds level-synchronous, OpenMP over each level's
+ * nodes.  Returns total deliveries, or <0 on error. */
+int64_t or_levels_bits(uint32_t n, const uint32_t* row_ptr, const uint32_t* col, uint32_t root,
+                       const uint8_t* live, uint32_t n_msgs, int n_threads);
+
 /* SplitMix64 (shared definition with the engine and the synthetic workload
  * generator). */
 uint64_t or_splitmix64(uint64_t* state);

@@ -73,6 +73,40 @@ def test_c_tree_matches_python_restatement(oracle_lib, trial):
         assert np.array_equal(ct.parents(), np.array(pt.parents(), np.uint32)), (trial, step)
 
 
+@pytest.mark.parametrize("n_fail", [63, 64, 65, 100])
+def test_wide_fanout_every_failed_child_repaired(oracle_lib, n_fail):
+    """A parent with more than 64 children whose hosts all fail: the message
+    that meets them repairs every one (subtree.go:342-349 redistributes each
+    dead child), in the C restatement exactly as in the Python one -- the C
+    failed list once held only 64 entries."""
+    n = 2 * n_fail + 40
+    width = n_fail + 10
+    seed = 1234 + n_fail
+    ct = O.Tree(n, 0, width, width + 5, seed)
+    pt = ES.Topic(n, 0, width, width + 5, seed)
+    peers = list(range(1, n))
+    for p in peers:  # the first `width` peers attach to the root, the rest below them
+        rc = ct.join(p)
+        pt.subscribe(p)
+        assert rc == 0
+    kids = [p for p in range(1, n) if ct.parents()[p] == 0]
+    assert len(kids) >= n_fail
+    for p in kids[:n_fail]:
+        ct.drop(p)
+        pt.drop(p)
+    h = ct.message()
+    got = pt.publish([b"x"], random.Random(0))
+    ph = np.full(n, 255, np.uint8)
+    for peer, lst in enumerate(got):
+        for _, hop in lst:
+            ph[peer] = hop
+    assert np.array_equal(h, ph)
+    assert np.array_equal(ct.parents(), np.array(pt.parents(), np.uint32))
+    # every grandchild the failed children last reported is attached again
+    reattached = [p for p in range(1, n) if ct.parents()[p] == 0 and p not in kids]
+    assert len(reattached) > 0
+
+
 def test_golden_cfg1(oracle_lib):
     g = load("cfg1.json")
     t = O.Tree(g["n_peers"], g["root"], g["width"], g["max_width"], g["seed"])
@@ -181,3 +215,22 @@ def test_splitmix_matches_workload_generator(oracle_lib):
     s = ctypes.c_uint64(12345)
     vals = [O.lib().or_splitmix64(ctypes.byref(s)) for _ in range(5)]
     assert vals == [int(x) for x in WL.stream(12345, np.arange(5))]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_levels_bits_matches_per_message_bfs(oracle_lib, seed):
+    """The bit-sliced level-synchronous restatement (bench CPU baseline)
+    delivers exactly what the per-message BFS does, dead peers included."""
+    rng = np.random.default_rng(seed)
+    n = int(rng.integers(2, 3000))
+    root = int(rng.integers(0, n))
+    perm = rng.permutation(n)
+    perm = np.concatenate([[root], perm[perm != root]])
+    parent = np.full(n, O.NONE, dtype=np.uint32)
+    for i in range(1, n):
+        parent[perm[i]] = perm[rng.integers(0, i)]
+    live = (rng.random(n) > 0.1).astype(np.uint8)
+    rp, cl = O.parents_to_csr(parent)
+    for n_msgs in (1, 63, 64, 65, 300):
+        tot, _, _ = O.disseminate(rp, cl, root, live, n_msgs, want_hops=False)
+        assert O.levels_bits(rp, cl, root, live, n_msgs, threads=2) == tot
