@@ -262,6 +262,40 @@ def bench_cfg5(args):
     eng.close()
 
 
+def general_path(eng, wl, deliv_expected, steps: int, warmup: int = 1, max_start: int = 7):
+    """The general path (compaction mode): the same workload published with
+    staggered start rounds, uniform over 0..max_start -- paced publishing as
+    the reference's tests do it (pubsub_test.go:101-131) -- so every message
+    enters its root in its own round and the rounds run k_expand over a
+    compacted frontier with the seen test-and-set (client.go:103-131).  On a
+    tree every message still reaches every subscriber: the same deliveries."""
+    starts = (WL.stream(wl.seed ^ 0x57A6, np.arange(wl.n_msgs)) % np.uint64(max_start + 1)).astype(np.uint32)
+
+    def step():
+        eng.publish(wl.msg_topics, starts)
+        return eng.run()
+
+    for _ in range(warmup):
+        st = step()
+        assert st.deliveries == deliv_expected, (st.deliveries, deliv_expected)
+        assert st.expand_mode == PE.MODE_COMPACT
+    t0 = time.perf_counter()
+    tot = sum(step().deliveries for _ in range(steps))
+    wall = time.perf_counter() - t0
+    assert tot == deliv_expected * steps
+    tot_bytes, tot_ms, launches, st = instrumented(eng, step, 2)
+    achieved = tot_bytes / max(1e-12, tot_ms * 1e-3) / 1e9
+    return {"workload": f"{wl.name} with start rounds uniform over 0..{max_start} (paced publishing): "
+                        "compaction mode, k_expand + frontier compaction every round",
+            "value": tot / wall, "unit": "deliveries/s", "steps": steps, "ms_per_step": wall * 1e3 / steps,
+            "rounds": st.rounds, "deliveries_per_step": deliv_expected,
+            "roofline": {"bound": "hbm", "kernel": hot_kernel(st), "achieved": achieved, "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                         "avg_launch_us": tot_ms * 1e3 / max(1, launches),
+                         "bytes_per_launch": tot_bytes / max(1, launches),
+                         "expand_ms_per_step": tot_ms / 2}}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -272,10 +306,13 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--no-check", action="store_true", help="skip delivery assertions (experiments)")
+    ap.add_argument("--no-general", action="store_true",
+                    help="skip the general-path leg (staggered starts, compaction mode)")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the torch.distributed driver even with one rank (testing)")
-    ap.add_argument("--partition", default="subtree", choices=["subtree", "peer"],
-                    help="multi-GPU node ownership: subtree hash (default) or peer hash")
+    ap.add_argument("--partition", default="peer", choices=["peer", "subtree"],
+                    help="multi-GPU node ownership: peer hash owner(p) = splitmix64(p) mod N (default, "
+                         "SURVEY.md §8e) or level-L subtrees")
     ap.add_argument("--sync", action="store_true",
                     help="one blocking ps_run per step (default: pipelined ps_run_async / ps_wait, "
                          "the next batch is published and planned while the previous one's kernels run)")
@@ -374,6 +411,8 @@ def main():
                       "expand_us_per_round": [round(x * 1e3, 1) for x in
                                               st.as_dict()["expand_ms_per_round"]]},
     }
+    if not args.no_general and not args.no_check:
+        out["general_path"] = general_path(eng, wl, deliv_expected, max(2, min(args.steps, 4)))
     if not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(eng, wl, sizes, args.cpu_budget)
     print(json.dumps(out), flush=True)

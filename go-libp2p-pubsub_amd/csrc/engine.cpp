@@ -87,6 +87,13 @@ struct TopicHost {
     uint32_t level, from, to, count;
   };
   std::vector<Cross> cross;
+  // multi-GPU level mode: ghost parents.  gcnt[(d * world + a)
+  // * world + b] = parents at level d - 1 owned by rank a with a child at
+  // level d owned by rank b (a != b); each such row crosses once per round.
+  // This rank's parents to ship: send_node[i] (local node), send_dst[i]
+  // (dest rank << 27 | index among the a -> b ghosts of the level), grouped
+  // by level: send_lvl[d] .. send_lvl[d + 1].
+  std::vector<uint32_t> gcnt, send_node, send_dst, send_lvl;
 };
 
 struct RunMsg {
@@ -153,8 +160,6 @@ struct ps_engine {
   // level mode, pull direction: per-round chunks of next-level nodes
   std::vector<uint64_t> pull_key;
   std::vector<PullChunk> pull_host;
-  std::vector<uint32_t> split_host, split_off;  // multi-GPU: split parents per round
-  DevBuf d_split;
   std::vector<uint32_t> pull_off;
   DevBuf d_pull;
 
@@ -170,12 +175,27 @@ struct ps_engine {
       d_partials, d_stats, d_topics, d_seeds, d_digest;
   uint32_t gen_cur = 0;  // window generation stamped into d_gen (1..255)
   DevBuf d_remote_fed, d_send, d_recv, d_apply_stats;
+  // multi-GPU level mode: ghost parents
+  std::vector<uint32_t> ghost_ref;  // per node: remote parent's rank << 27 | ghost index, or kNone
+  std::vector<uint64_t> ghost_key;  // (graph, start rounds, row widths) the plan below was built for
+  struct GhostRound {
+    std::vector<uint64_t> s_off, s_len, r_off, r_len;  // transport regions, bytes
+    uint32_t pack0 = 0, pack1 = 0;                     // pack entries of the round
+    uint32_t seg0 = 0, seg1 = 0;                       // their (topic) segments
+    bool any = false;                                  // some rank ships rows this round
+  };
+  std::vector<GhostRound> ghost_rounds;
+  std::vector<PackEntry> pack_host;
+  std::vector<PackSeg> pack_seg_host;
+  std::vector<uint64_t> ghost_off_host;  // per node: flag byte << 40 | row word, in the recv buffer
+  DevBuf d_pack, d_pack_seg, d_ghost_off;
+  uint64_t ghost_send_max = 0, ghost_recv_max = 0;
   uint32_t n_remote_fed = 0;
   std::vector<uint32_t> remote_fed;  // owned nodes whose parent is on another rank
 
   // multi-GPU: this engine owns a hash-partitioned share of every topic
   int32_t rank = 0, world = 1;
-  uint32_t partition = PS_PART_SUBTREE, split_depth = 0;
+  uint32_t partition = PS_PART_PEER, split_depth = 0;
   std::unique_ptr<Transport> transport;
 
   // publishes not yet run
@@ -333,8 +353,7 @@ void partition_topic(const std::vector<uint32_t>& order, const std::vector<uint3
   std::vector<uint64_t> size(subtree ? n : 0, 0);
   // subtree mode: the levels above L (< 64 * world nodes each) stay whole
   // with the root's owner, so edges cross ranks only from level L - 1 into
-  // the level-L subtrees: one exchange round per topic, and that rank runs
-  // the top levels as one launch (k_pull_top)
+  // the level-L subtrees: one exchange round per topic
   const int32_t top_owner = n ? static_cast<int32_t>(mix(order[0]) % static_cast<uint64_t>(world)) : 0;
   uint64_t n_top = 0;
   for (size_t u = 0; u < n; ++u) {
@@ -382,6 +401,8 @@ int build_graph(ps_engine* e) {
   e->row_ptr.assign(1, 0);
   e->col.clear();
   e->remote_fed.clear();
+  e->ghost_ref.clear();
+  std::vector<uint32_t> ghost_of;  // per global BFS position: owner << 27 | ghost index, or kNone
   std::vector<uint32_t> local(n, kNone);  // peer -> BFS position
   std::vector<uint32_t> rp, cl, order, indeg, bfs_parent, level, loc;
   std::vector<int32_t> owner;
@@ -455,6 +476,40 @@ int build_graph(ps_engine* e) {
       for (uint32_t u = 0; u < N; ++u) loc[u] = next[owner[u]]++;
     }
     T.root_local = owner[0] == me;
+    // ghost parents: per parent in BFS order, one row per remote rank that
+    // owns one of its children (children are consecutive BFS positions)
+    T.gcnt.assign(world > 1 ? static_cast<size_t>(T.depth + 2) * world * world : 0, 0);
+    T.send_node.clear();
+    T.send_dst.clear();
+    T.send_lvl.assign(T.depth + 3, 0);
+    if (world > 1) {
+      ghost_of.assign(N, kNone);
+      for (uint32_t u = 0; u < N; ++u) {
+        const uint32_t p = order[u];
+        uint32_t mask = 0;
+        for (uint32_t k = rp[p]; k < rp[p + 1]; ++k) {
+          const uint32_t v = local[cl[k]];
+          if (owner[v] != owner[u]) mask |= 1u << owner[v];
+        }
+        const uint32_t d = level[u] + 1;
+        for (int32_t b = 0; mask; ++b, mask >>= 1) {
+          if (!(mask & 1u)) continue;
+          const uint32_t gk = T.gcnt[(static_cast<size_t>(d) * world + owner[u]) * world + b]++;
+          if (gk > kRemoteIdMask) return e->fail(PS_E_NOMEM, "ghost rows of one level exceed 2^27");
+          if (owner[u] == me) {
+            T.send_node.push_back(T.nbase + loc[u]);
+            T.send_dst.push_back(static_cast<uint32_t>(b) << kRemoteRankShift | gk);
+            T.send_lvl[d + 1] = static_cast<uint32_t>(T.send_node.size());
+          }
+          if (b == me)
+            for (uint32_t k = rp[p]; k < rp[p + 1]; ++k) {
+              const uint32_t v = local[cl[k]];
+              if (owner[v] == me) ghost_of[v] = static_cast<uint32_t>(owner[u]) << kRemoteRankShift | gk;
+            }
+        }
+      }
+      for (uint32_t d = 1; d < T.send_lvl.size(); ++d) T.send_lvl[d] = std::max(T.send_lvl[d], T.send_lvl[d - 1]);
+    }
     T.level_internal.assign(T.depth + 1, 0);
     // owned nodes are numbered in BFS order: each level is a contiguous range
     T.level_off.assign(T.depth + 2, 0);
@@ -473,6 +528,7 @@ int build_graph(ps_engine* e) {
       if (owner[u] != me) continue;
       ++n_own;
       e->node_peer.push_back(p);
+      if (world > 1) e->ghost_ref.push_back(u ? ghost_of[u] : kNone);
       e->node_parent.push_back(u && owner[bfs_parent[u]] == me ? T.nbase + loc[bfs_parent[u]] : kNone);
       e->node_topic.push_back(static_cast<uint16_t>(t));
       for (uint32_t k = rp[p]; k < rp[p + 1]; ++k) {
@@ -942,11 +998,8 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab, const std:
   C.clear();
   off.assign(rounds + 2, 0);
   e->pull_bytes.assign(rounds + 2, 0);
-  e->split_host.clear();
-  e->split_off.assign(rounds + 2, 0);
   for (uint32_t q = 1; q <= rounds; ++q) {
     off[q] = static_cast<uint32_t>(C.size());
-    e->split_off[q] = static_cast<uint32_t>(e->split_host.size());
     for (uint32_t t = 0; t < nt; ++t) {
       const TopicHost& T = e->topics[t];
       const uint32_t W = tab[t].W;
@@ -954,11 +1007,6 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab, const std:
       const uint32_t d = q - tstart[t];  // level of the nodes written this round
       if (d + 1 >= T.level_off.size()) continue;
       const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
-      // split parents of this round (children owned by other ranks)
-      if (e->world > 1)
-        for (uint32_t u = T.level_off[d - 1]; u < T.level_off[d]; ++u)
-          if ((e->node_flags[T.nbase + u] & (kNodeSplit | kNodeLive)) == (kNodeSplit | kNodeLive))
-            e->split_host.push_back(T.nbase + u);
       const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, kPullWords / W));
       e->pull_bytes[q] += static_cast<uint64_t>(hi - lo) * W * 8;
       for (uint32_t u = lo; u < hi; u += per) {
@@ -973,12 +1021,6 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab, const std:
     }
   }
   off[rounds + 1] = static_cast<uint32_t>(C.size());
-  e->split_off[rounds + 1] = static_cast<uint32_t>(e->split_host.size());
-  HIP_TRY(e->d_split.ensure(std::max<size_t>(e->split_host.size(), 1) * 4), "alloc split list");
-  if (!e->split_host.empty())
-    HIP_TRY(hipMemcpyAsync(e->d_split.p, e->split_host.data(), e->split_host.size() * 4,
-                           hipMemcpyHostToDevice, e->stream),
-            "upload split list");
   HIP_TRY(e->d_pull.ensure(std::max<size_t>(C.size(), 1) * sizeof(PullChunk)), "alloc pull chunks");
   if (!C.empty())
     HIP_TRY(hipMemcpyAsync(e->d_pull.p, C.data(), C.size() * sizeof(PullChunk),
@@ -989,6 +1031,144 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab, const std:
                                  e->d_node_parent.as<uint32_t>(), e->stream),
             "chunk parents");
   e->pull_key = key;
+  return PS_OK;
+}
+
+// Multi-GPU level mode: the per-round exchange of ghost
+// parents.  Region (a -> b, round q) holds, for the topics active in round q
+// in topic order, one record per a -> b ghost parent of that round's level:
+// [pad if W even][reach word][W row words] (ghost_record_words).  Every rank
+// computes every region from the same topology (gcnt) and message counts, so
+// sender and receiver agree on sizes and offsets without a handshake.  This
+// rank's pack entries (its parents to ship, with their record offsets in the
+// send buffer) and each ghost-fed node's row offset in the receive buffer
+// follow.  Cached per node space, start rounds and row widths.
+int build_ghost_plan(ps_engine* e, const std::vector<TopicDev>& tab, const std::vector<uint32_t>& tstart,
+                     uint32_t rounds) {
+  const uint32_t nt = static_cast<uint32_t>(e->topics.size());
+  const int32_t world = e->world, me = e->rank;
+  std::vector<uint64_t> key{e->graph_epoch, rounds};
+  for (uint32_t t = 0; t < nt; ++t) {
+    key.push_back(tab[t].W ? tstart[t] : ~0ull);
+    key.push_back(tab[t].W);
+  }
+  if (key == e->ghost_key) return PS_OK;
+  e->ghost_key.clear();
+  auto level_of = [&](uint32_t q, uint32_t t) -> uint32_t {  // level written in round q, 0: none
+    const TopicHost& T = e->topics[t];
+    if (!tab[t].W || !T.exists || q <= tstart[t] || T.gcnt.empty()) return 0;
+    const uint32_t d = q - tstart[t];
+    return d <= T.depth ? d : 0;
+  };
+  auto gcnt = [&](uint32_t t, uint32_t d, int32_t a, int32_t b) -> uint64_t {
+    return e->topics[t].gcnt[(static_cast<size_t>(d) * world + a) * world + b];
+  };
+  e->ghost_rounds.assign(rounds + 2, ps_engine::GhostRound{});
+  e->pack_host.clear();
+  e->pack_seg_host.clear();
+  e->ghost_off_host.assign(e->n_nodes, kGhostNone);
+  e->ghost_send_max = e->ghost_recv_max = 0;
+  std::vector<uint64_t> rec_off(static_cast<size_t>(world) * nt);  // per peer, per topic: first record (words)
+  for (uint32_t q = 1; q <= rounds; ++q) {
+    auto& R = e->ghost_rounds[q];
+    R.s_off.assign(world, 0);
+    R.s_len.assign(world, 0);
+    R.r_off.assign(world, 0);
+    R.r_len.assign(world, 0);
+    // region a -> b: bytes, and (into rec_off[peer]) each topic's first record
+    auto region = [&](int32_t a, int32_t b, int32_t peer) -> uint64_t {
+      uint64_t words = 0;
+      for (uint32_t t = 0; t < nt; ++t) {
+        rec_off[static_cast<size_t>(peer) * nt + t] = words;
+        const uint32_t d = level_of(q, t);
+        if (d) words += gcnt(t, d, a, b) * ghost_record_words(tab[t].W);
+      }
+      return words * 8;
+    };
+    for (int32_t a = 0; a < world && !R.any; ++a)
+      for (int32_t b = 0; b < world && !R.any; ++b)
+        for (uint32_t t = 0; t < nt && a != b; ++t) {
+          const uint32_t d = level_of(q, t);
+          if (d && gcnt(t, d, a, b)) {
+            R.any = true;
+            break;
+          }
+        }
+    // send regions (me -> b) and this rank's pack entries
+    uint64_t so = 0;
+    for (int32_t b = 0; b < world; ++b) {
+      if (b == me) continue;
+      R.s_off[b] = so;
+      R.s_len[b] = region(me, b, b);
+      so += R.s_len[b];
+    }
+    R.pack0 = static_cast<uint32_t>(e->pack_host.size());
+    R.seg0 = static_cast<uint32_t>(e->pack_seg_host.size());
+    uint64_t word0 = 0;
+    for (uint32_t t = 0; t < nt; ++t) {
+      const uint32_t d = level_of(q, t);
+      if (!d) continue;
+      const TopicHost& T = e->topics[t];
+      const uint32_t W = tab[t].W, rw = ghost_record_words(W);
+      const uint32_t e0 = static_cast<uint32_t>(e->pack_host.size());
+      for (uint32_t i = T.send_lvl[d]; i < T.send_lvl[d + 1]; ++i) {
+        const uint32_t b = T.send_dst[i] >> kRemoteRankShift, k = T.send_dst[i] & kRemoteIdMask;
+        PackEntry pe{};
+        pe.node = T.send_node[i];
+        pe.row_off = R.s_off[b] / 8 + rec_off[static_cast<size_t>(b) * nt + t] + static_cast<uint64_t>(k) * rw +
+                     (rw - W);
+        e->pack_host.push_back(pe);
+      }
+      const uint32_t e1 = static_cast<uint32_t>(e->pack_host.size());
+      if (e1 > e0) {
+        e->pack_seg_host.push_back(PackSeg{e0, e1, t, W, word0});
+        word0 += static_cast<uint64_t>(e1 - e0) * W;
+      }
+    }
+    R.pack1 = static_cast<uint32_t>(e->pack_host.size());
+    R.seg1 = static_cast<uint32_t>(e->pack_seg_host.size());
+    // receive regions (a -> me) and the rows the ghost-fed nodes read
+    uint64_t ro = 0;
+    for (int32_t a = 0; a < world; ++a) {
+      if (a == me) continue;
+      R.r_off[a] = ro;
+      R.r_len[a] = region(a, me, a);
+      ro += R.r_len[a];
+    }
+    for (uint32_t t = 0; t < nt; ++t) {
+      const uint32_t d = level_of(q, t);
+      if (!d) continue;
+      const TopicHost& T = e->topics[t];
+      const uint32_t W = tab[t].W, rw = ghost_record_words(W);
+      for (uint32_t u = T.nbase + T.level_off[d]; u < T.nbase + T.level_off[d + 1]; ++u) {
+        const uint32_t g = e->ghost_ref[u];
+        if (g == kNone) continue;
+        const uint32_t a = g >> kRemoteRankShift, k = g & kRemoteIdMask;
+        e->ghost_off_host[u] = R.r_off[a] / 8 + rec_off[static_cast<size_t>(a) * nt + t] +
+                               static_cast<uint64_t>(k) * rw + (rw - W);
+      }
+    }
+    e->ghost_send_max = std::max(e->ghost_send_max, so);
+    e->ghost_recv_max = std::max(e->ghost_recv_max, ro);
+  }
+  HIP_TRY(e->d_pack.ensure(std::max<size_t>(e->pack_host.size(), 1) * sizeof(PackEntry)), "alloc pack entries");
+  HIP_TRY(e->d_pack_seg.ensure(std::max<size_t>(e->pack_seg_host.size(), 1) * sizeof(PackSeg)), "alloc pack segments");
+  HIP_TRY(e->d_ghost_off.ensure(std::max<size_t>(e->n_nodes, 1) * 8), "alloc ghost offsets");
+  HIP_TRY(e->d_send.ensure(std::max<uint64_t>(e->ghost_send_max, 16)), "alloc send buffer");
+  HIP_TRY(e->d_recv.ensure(std::max<uint64_t>(e->ghost_recv_max, 16)), "alloc recv buffer");
+  if (!e->pack_host.empty())
+    HIP_TRY(hipMemcpyAsync(e->d_pack.p, e->pack_host.data(), e->pack_host.size() * sizeof(PackEntry),
+                           hipMemcpyHostToDevice, e->stream),
+            "upload pack entries");
+  if (!e->pack_seg_host.empty())
+    HIP_TRY(hipMemcpyAsync(e->d_pack_seg.p, e->pack_seg_host.data(), e->pack_seg_host.size() * sizeof(PackSeg),
+                           hipMemcpyHostToDevice, e->stream),
+            "upload pack segments");
+  if (e->n_nodes)
+    HIP_TRY(hipMemcpyAsync(e->d_ghost_off.p, e->ghost_off_host.data(), static_cast<size_t>(e->n_nodes) * 8,
+                           hipMemcpyHostToDevice, e->stream),
+            "upload ghost offsets");
+  e->ghost_key = key;
   return PS_OK;
 }
 
@@ -1214,11 +1394,11 @@ void flood_profile_report(ps_engine* e) {
   std::fprintf(stderr,
                "[psengine] k_flood profile: %u waves, span %.1f us, start skew %.1f us, ends p50 %.1f p90 %.1f "
                "max %.1f us; per wave avg: wait %.1f resolve %.1f stream %.1f publish %.1f us (%.0f%%/%.0f%%/%.0f%%/"
-               "%.0f%%), %.1f tasks\n",
+               "%.0f%%), %.1f tasks; waits in the last third of the rounds %.1f us\n",
                nw, us(static_cast<double>(t1 - t0)), us(static_cast<double>(smax - t0)),
                us(ends[ends.size() / 2] - t0), us(ends[ends.size() * 9 / 10] - t0), us(ends.back() - t0),
                us(sum[2] / nw), us(sum[3] / nw), us(sum[4] / nw), us(sum[5] / nw), 100 * sum[2] / busy,
-               100 * sum[3] / busy, 100 * sum[4] / busy, 100 * sum[5] / busy, sum[6] / nw);
+               100 * sum[3] / busy, 100 * sum[4] / busy, 100 * sum[5] / busy, sum[6] / nw, us(sum[7] / nw));
 }
 
 int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<WinSlice>& win,
@@ -1371,6 +1551,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   uint32_t n_slots = 0;         // level mode: partial counter slots of the window
   if (level) {
     int rc2 = flood ? build_flood_tasks(e, tab, tstart, planned0) : build_pull_chunks(e, tab, tstart, planned0);
+    if (!rc2 && world > 1) rc2 = build_ghost_plan(e, tab, tstart, planned0);
     if (rc2) return rc2;
     // desc[3q..]: round q's partial slots (first, end, stride) for the reduce
     auto& desc = e->desc_host;
@@ -1406,7 +1587,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // cross-rank capacities (items = node words) per round: cap[r][from*world+to]
   std::vector<std::vector<uint64_t>> cap;
   uint64_t max_send = 0, max_recv = 0;
-  if (world > 1) {
+  if (world > 1 && !level) {  // compaction mode: delivery items (level mode ships ghost rows)
     cap.assign(planned0 + 1, std::vector<uint64_t>(static_cast<size_t>(world) * world, 0));
     for (uint32_t t = 0; t < nt; ++t) {
       const TopicHost& T = e->topics[t];
@@ -1465,7 +1646,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
                              e->d_seen.as<uint64_t>(), e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>(),
                              e->d_gen.as<uint8_t>(), e->gen_cur, any_mesh, ws, s),
           "window init");
-  if (e->n_remote_fed)
+  if (e->n_remote_fed && !level)
     HIP_TRY(launch_init_nodes(e->d_remote_fed.as<uint32_t>(), e->n_remote_fed,
                               e->d_node_topic.as<uint16_t>(), e->d_topics.as<TopicDev>(),
                               e->d_seen.as<uint64_t>(), e->d_arr0.as<uint64_t>(),
@@ -1479,7 +1660,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
             "stamp generations");
   }
   if (record) HIP_TRY(hipMemsetAsync(e->d_hop.p, 0xFF, wtot * 64 * 2, s), "clear hop record");
-  if (world > 1)
+  if (world > 1)  // (level mode: stays zero; the pull kernels count every delivery)
     HIP_TRY(hipMemsetAsync(e->d_apply_stats.p, 0, static_cast<size_t>(planned0 + 1) * kNumCtr * 8, s),
             "clear apply stats");
 
@@ -1520,7 +1701,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // multi-GPU round r: region layout, header reset, exchange, apply
   std::vector<uint64_t> s_off(world, 0), s_len(world, 0), r_off(world, 0), r_len(world, 0);
   auto layout = [&](uint32_t r) -> bool {
-    if (world <= 1 || r > planned0) return false;
+    if (world <= 1 || r > planned0 || cap.empty()) return false;
     uint64_t so = 0, ro = 0;
     bool any = false;
     for (int32_t q = 0; q < world; ++q) {
@@ -1618,6 +1799,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       if (e->flood_profile) {
         HIP_TRY(e->d_flood_prof.ensure(static_cast<size_t>(flood_blocks) * 4 * kFloodProf * 8), "alloc flood profile");
         fa.prof = e->d_flood_prof.as<uint64_t>();
+        fa.prof_split = planned0 * 2 / 3;
         e->flood_prof_waves = flood_blocks * 4;
       }
       r = 1;  // the per-round kernel times of a timed run go to round 1
@@ -1629,10 +1811,22 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       for (r = 1; r <= planned0; ++r) {
         a.a_cur = arr[(r - 1) & 1];
         a.a_next = arr[r & 1];
-        const bool xr = layout(r);
-        if (xr)
-          for (int32_t q = 0; q < world; ++q)
-            if (s_len[q]) HIP_TRY(hipMemsetAsync(a.send + s_off[q], 0, kRegionHeader, s), "reset header");
+        // multi-GPU: this round's ghost parents (rows written last round, or
+        // seeded roots) to the ranks owning their children, then the exchange
+        if (world > 1 && e->ghost_rounds[r].any) {
+          const auto& R = e->ghost_rounds[r];
+          if (R.seg1 > R.seg0) {
+            const PackSeg& last = e->pack_seg_host[R.seg1 - 1];
+            HIP_TRY(launch_pack(e->d_pack.as<PackEntry>(), e->d_pack_seg.as<PackSeg>() + R.seg0, R.seg1 - R.seg0,
+                                last.word0 + static_cast<uint64_t>(last.e1 - last.e0) * last.W, a.topics, a.seen,
+                                a.gen, a.gen_cur, e->d_send.as<uint64_t>(), s),
+                    "pack");
+          }
+          std::string xerr;
+          const hipError_t xe = e->transport->exchange(e->d_send.as<uint8_t>(), R.s_off, R.s_len,
+                                                       e->d_recv.as<uint8_t>(), R.r_off, R.r_len, s, &xerr);
+          if (xe != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
+        }
         if (lgrid[r]) {
           HIP_TRY(time_mark(true), "event");
           ++launches;
@@ -1647,6 +1841,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
           pa.partials = partials + static_cast<size_t>(e->woff_host[r]) * kNumCtr;
           pa.gen_cur = a.gen_cur;
           pa.slot_mod = kPullSlots;
+          pa.ghost_off = world > 1 ? e->d_ghost_off.as<uint64_t>() : nullptr;
+          pa.recv = e->d_recv.as<uint64_t>();
           // rows nobody re-reads while they can still sit in the 256 MB MALL
           // (large rounds and the last round) store non-temporally
           const bool nt = r < e->pull_bytes.size() && (e->pull_bytes[r] >= (64ull << 20) || r == planned0);
@@ -1654,14 +1850,6 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
                               lgrid[r], r, record, nt, s),
                   "pull");
           HIP_TRY(time_mark(false), "event");
-        }
-        if (world > 1 && e->split_off[r + 1] > e->split_off[r])
-          HIP_TRY(launch_send(a, e->d_split.as<uint32_t>() + e->split_off[r], e->split_off[r + 1] - e->split_off[r],
-                              s),
-                  "send");
-        if (xr) {
-          const int rc3 = xchg(r);
-          if (rc3) return rc3;
         }
         HIP_TRY(seed_round(r, a.a_next), "seed");
       }

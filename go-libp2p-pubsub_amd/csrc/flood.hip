@@ -242,6 +242,10 @@ __global__ __launch_bounds__(kBlock, kFloodBlocksPerCu) void k_flood(FloodArgs a
   uint64_t t_a = stamp();
   pf[0] = t_a;
   FloodTask T = uniform(a.tasks[wave < a.n_tasks ? wave : 0]);
+  // the previous task's granules, published once its row stores are known
+  // to have drained (see below)
+  uint64_t pend_val = 0;
+  uint32_t pend_at = kNoneNode;
   for (uint32_t ti = wave; ti < a.n_tasks; ti += nw) {
     if (T.round != round) {  // tasks come level by level: a wave's rounds only grow
       if (slot != kNoneNode) flood_flush(a, c, slot, lane);
@@ -250,17 +254,29 @@ __global__ __launch_bounds__(kBlock, kFloodBlocksPerCu) void k_flood(FloodArgs a
     }
     const uint32_t nk = T.ne - T.nb;
     // this task's nodes, one per lane (static data: loaded before the wait)
+    // (unconditional loads, lanes past the run re-read its last node: no
+    // branch, so nothing waits for them before the poll)
     const bool in = lane < nk;
-    uint32_t p = kNoneNode, f = 0, own = 0, prev = kNoneNode;
-    if (in) {
-      p = a.node_parent[T.nb + lane];
-      f = a.node_flags[T.nb + lane];
-      own = a.gen[T.nb + lane];  // only this wave writes this byte in this launch
-    }
+    const uint32_t me = T.nb + (in ? lane : nk - 1);
+    const uint32_t p = a.node_parent[me];
+    const uint32_t f = a.node_flags[me];
+    const uint32_t own = a.gen[me];  // only this wave writes this byte in this launch
+    uint32_t prev = kNoneNode;
     const TopicDev D = a.topics[T.topic];
     // the next task's record, consumed after this one
     const FloodTask Tn = a.tasks[ti + nw < a.n_tasks ? ti + nw : ti];
     if (lane == 0 && T.nb > 0) prev = a.node_parent[T.nb - 1];
+    // The previous task's row stores were issued before these loads; the
+    // vector-memory counter retires in issue order, so once the parent id
+    // loaded above is in a register every older store has drained: publish
+    // the previous task's granules now (its drain overlapped these loads).
+    {
+      const uint32_t p_used = __builtin_amdgcn_readfirstlane(p);  // waits for the load of p
+      asm volatile("; publish after p %0" ::"s"(p_used) : "memory");
+      if (pend_at != kNoneNode)
+        __hip_atomic_store(a.granules + pend_at, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pend_at = kNoneNode;
+    }
     // round - 1's granules of the parents: the dependency wait and the
     // frontier test (parent reached this window) in one load
     bool up = false;
@@ -333,20 +349,25 @@ __global__ __launch_bounds__(kBlock, kFloodBlocksPerCu) void k_flood(FloodArgs a
     const uint64_t reach = __ballot(ok);
     const uint64_t t_c = stamp();
     pf[4] += t_c - t_b;
-    // publish: every row store of this wave has reached the device-coherent
-    // level before the granules do
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.prof && T.round > a.prof_split) pf[7] += t_b - t_a;  // waits of the later rounds
+    // publish: the granules wait until every row store of this task has
+    // reached the device-coherent level -- at the next task's first load, or
+    // below for a wave's last task
     const uint32_t ng = (nk + T.gsz - 1) / T.gsz;
     if (lane < ng) {
       const uint64_t bits = (reach >> (lane * T.gsz)) & (T.gsz >= 64 ? ~0ull : (1ull << T.gsz) - 1ull);
-      __hip_atomic_store(a.granules + T.g_own + lane, static_cast<uint64_t>(a.epoch) << 32 | bits,
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pend_val = static_cast<uint64_t>(a.epoch) << 32 | bits;
+      pend_at = T.g_own + lane;
     }
+    asm volatile("" ::: "memory");  // the next task's loads stay behind this task's stores
     T = uniform(Tn);
     t_a = stamp();
     pf[5] += t_a - t_c;
     pf[6] += 1;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (pend_at != kNoneNode)
+    __hip_atomic_store(a.granules + pend_at, pend_val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (slot != kNoneNode) flood_flush(a, c, slot, lane);
   if (a.prof && lane == 0) {
     pf[1] = stamp();

@@ -731,13 +731,14 @@ struct PullTopic {
   uint32_t W, nbase, root;
 };
 
-// Phase 1 for the nodes [nb, nb + nk) of one level: src[j] = the node whose
-// row node nb + j copies, or kNoneNode.  The parents of a run are consecutive
-// node ids [p_lo, p_hi] (BFS numbering): their generation bytes are staged
-// into LDS by loads issued together with the nodes' own metadata, so phase 1
-// costs one memory round trip.
+// Phase 1 for the nodes [nb, nb + nk) of one level: src[j] = the address of
+// the row node nb + j copies (its parent's row: the root's arrival row, a
+// seen row, or -- multi-GPU -- a ghost row in the receive buffer), or 0.  The
+// parents of a run are consecutive node ids [p_lo, p_hi] (BFS numbering):
+// their generation bytes are staged into LDS by loads issued together with
+// the nodes' own metadata, so phase 1 costs one memory round trip.
 __device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t nk,
-                                             uint32_t p_lo, uint32_t p_hi, uint32_t* src, uint8_t* genl,
+                                             uint32_t p_lo, uint32_t p_hi, uint64_t* src, uint8_t* genl,
                                              uint32_t lane, uint32_t cur, PullCtr& c) {
   uint32_t g0 = 0;
   const bool staged = p_lo != kNoneNode && p_hi - p_lo < kPullMaxKids;
@@ -755,16 +756,36 @@ __device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic&
       p = a.node_parent[nb + j];
       f = a.node_flags[nb + j];
     }
-    uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
-    if (lane == 0) prev = nb + j0 > P.nbase ? a.node_parent[nb + j0 - 1] : kNoneNode;
     bool up = false;  // the parent was reached this window
-    if (in && p != kNoneNode) up = (staged ? genl[p - g0] : a.gen[p]) == cur;
+    uint64_t row = 0;
+    uint32_t pid = p;  // the parent's identity for the once-per-parent count
+    if (in && p != kNoneNode) {
+      up = (staged ? genl[p - g0] : a.gen[p]) == cur;
+      row = reinterpret_cast<uint64_t>((p == P.root ? a.a_cur : a.seen) + P.base + static_cast<uint64_t>(p) * P.W);
+    } else if (in && a.ghost_off) {  // parent on another rank: its row arrived this round
+      const uint64_t g = a.ghost_off[nb + j];
+      if (g != kGhostNone) {
+        up = a.recv[g - 1] != 0;
+        row = reinterpret_cast<uint64_t>(a.recv + g);
+        pid = 0x80000000u | static_cast<uint32_t>(g);
+      }
+    }
+    uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(pid), 1, 64));
+    if (lane == 0) {
+      prev = kNoneNode;
+      const uint32_t q = nb + j0;
+      if (q > P.nbase) {
+        prev = a.node_parent[q - 1];
+        if (prev == kNoneNode && a.ghost_off && a.ghost_off[q - 1] != kGhostNone)
+          prev = 0x80000000u | static_cast<uint32_t>(a.ghost_off[q - 1]);
+      }
+    }
     const bool ok = up && (f & kNodeLive);
-    if (in) src[j] = ok ? p : kNoneNode;
+    if (in) src[j] = ok ? row : 0ull;
     if (ok) a.gen[nb + j] = static_cast<uint8_t>(cur);
     c.kids += in;
     c.reached += ok;
-    if (up && p != prev) {
+    if (up && pid != prev) {
       c.parents += 1;
       c.pwords += P.W;
     }
@@ -798,11 +819,10 @@ __device__ __forceinline__ void store_row8(uint64_t* p, uint64_t v) {
 // exactly instead of draining at branches.
 template <bool kRecord, bool kNT>
 __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t nk,
-                                            const uint32_t* src, uint32_t lane, uint32_t round, PullCtr& c) {
+                                            const uint64_t* src, uint32_t lane, uint32_t round, PullCtr& c) {
   constexpr uint32_t kU = 8;
   const uint32_t W = P.W;
   const uint64_t base = P.base;
-  const uint32_t root = P.root;
   const uint32_t total = nk * W;
   uint64_t* const out = a.seen + base + static_cast<uint64_t>(nb) * W;
   const float rw = 1.0f / static_cast<float>(W);
@@ -820,10 +840,9 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
     auto one = [&](uint32_t i) {
       int32_t kk, r;
       split(i, kk, r);
-      const uint32_t p = src[kk];
-      const bool go = p != kNoneNode;
-      const uint64_t* s = go ? (p == root ? a.a_cur : a.seen) + base + static_cast<uint64_t>(p) * W + r
-                             : out + i;
+      const uint64_t row = src[kk];
+      const bool go = row != 0;
+      const uint64_t* s = go ? reinterpret_cast<const uint64_t*>(row) + r : out + i;
       return PullVec{go, *reinterpret_cast<const uint4*>(s)};
     };
     for (uint32_t i0 = 0; i0 < total; i0 += kU * 128) {
@@ -862,10 +881,9 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
         const uint32_t ic = i < total ? i : total - 1;  // past the end: the run's last word again
         int32_t kk, r;
         split(ic, kk, r);
-        const uint32_t p = src[kk];
-        go[u] = p != kNoneNode;
-        const uint64_t* s = go[u] ? (p == root ? a.a_cur : a.seen) + base + static_cast<uint64_t>(p) * W + r
-                                  : out + ic;
+        const uint64_t row = src[kk];
+        go[u] = row != 0;
+        const uint64_t* s = go[u] ? reinterpret_cast<const uint64_t*>(row) + r : out + ic;
         m[u] = *s;
       }
 #pragma unroll
@@ -913,12 +931,12 @@ __device__ __forceinline__ void pull_flush(const PullCtr& c, uint64_t* partials,
 template <bool kRecord, bool kNT>
 __global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __restrict__ chunks,
                                                  uint32_t n_chunks, uint32_t round) {
-  __shared__ uint32_t src_lds[kBlock / 64][kPullMaxKids];
+  __shared__ uint64_t src_lds[kBlock / 64][kPullMaxKids];
   __shared__ uint32_t gen_lds[kBlock / 64][kPullMaxKids / 4 + 2];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t wave = blockIdx.x * (kBlock / 64) + wid;
-  uint32_t* src = src_lds[wid];
+  uint64_t* src = src_lds[wid];
   uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds[wid]);
   const uint32_t cur = a.gen_cur & 0xFF;
   PullCtr c;
@@ -939,6 +957,34 @@ __global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __
   pull_flush(c, a.partials, blockIdx.x % a.slot_mod, lane, wid);
 }
 
+// Multi-GPU level mode: the round's ghost rows.  Thread i of the flattened
+// stream copies word i: segment (one topic, constant W) by a short scan,
+// entry = offset / W.  A parent not reached this window (stale generation)
+// ships only its zero reach word; the receiver then skips its children.
+__global__ __launch_bounds__(kBlock) void k_pack(const PackEntry* __restrict__ entries,
+                                                 const PackSeg* __restrict__ segs, uint32_t n_segs,
+                                                 uint64_t total, const TopicDev* __restrict__ topics,
+                                                 const uint64_t* __restrict__ seen, const uint8_t* __restrict__ gen,
+                                                 uint32_t gen_cur, uint64_t* __restrict__ send) {
+  const uint8_t cur = static_cast<uint8_t>(gen_cur);
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < total;
+       i += static_cast<uint64_t>(gridDim.x) * kBlock) {
+    uint32_t k = 0;
+    while (k + 1 < n_segs && segs[k + 1].word0 <= i) ++k;
+    const PackSeg S = segs[k];
+    const uint64_t o = i - S.word0;
+    const uint32_t e = S.e0 + static_cast<uint32_t>(o / S.W);
+    const uint32_t w = static_cast<uint32_t>(o % S.W);
+    const PackEntry E = entries[e];
+    const bool reached = gen[E.node] == cur;
+    if (w == 0) send[E.row_off - 1] = reached ? 1 : 0;
+    if (reached) {
+      const TopicDev T = topics[S.topic];
+      send[E.row_off + w] = seen[T.wbase + static_cast<uint64_t>(E.node - T.nbase) * T.W + w];
+    }
+  }
+}
+
 // GPU-built node spaces have no host mirror of node_parent: the chunks'
 // parent ranges (k_pull's generation staging) are filled in on the device.
 __global__ __launch_bounds__(kBlock) void k_chunk_parents(PullChunk* __restrict__ chunks, uint32_t n,
@@ -955,46 +1001,6 @@ __global__ __launch_bounds__(kBlock) void k_stage_copy(StageCopy c) {
   const uint32_t tid = blockIdx.x * kBlock + threadIdx.x, nth = gridDim.x * kBlock;
   for (uint32_t k = 0; k < c.n; ++k)
     for (uint32_t i = tid; i < c.words[k]; i += nth) c.dst[k][i] = c.src[k][i];
-}
-
-// ------------------------------------------------------------------ send ---
-// Level mode, multi-GPU: the rows of this round's split parents (nodes with
-// children owned by other ranks) go to those children's owners.  One wave per
-// parent: a parent the window's messages reached (generation current) ships
-// its whole row, (child id at the owner, word, bits) per word, into the
-// owner's send region (one reservation per child).  Local children pull.
-__global__ __launch_bounds__(kBlock) void k_send(ExpandArgs a, const uint32_t* __restrict__ list,
-                                                 uint32_t n) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) >> 6);
-  const uint32_t n_waves = (gridDim.x * kBlock) >> 6;
-  const uint32_t cur = a.gen_cur & 0xFF;
-  for (uint32_t i = wave; i < n; i += n_waves) {
-    const uint32_t p = list[i];
-    if (a.gen[p] != cur) continue;  // not reached: nothing to forward
-    const TopicDev T = a.topics[a.node_topic[p]];
-    const uint32_t W = T.W;
-    const bool is_root = p == T.nbase && (T.flags & kTopicRootLocal);
-    const uint64_t* src = ((T.flags & kTopicSingleStart) && !is_root ? a.seen : a.a_cur) + T.wbase +
-                          static_cast<uint64_t>(p - T.nbase) * W;
-    for (uint32_t k = a.row_ptr[p]; k < a.row_ptr[p + 1]; ++k) {
-      const uint32_t c = a.col[k];
-      if (!(c & kRemoteBit)) continue;
-      const uint32_t dest = (c >> kRemoteRankShift) & 0xFu;
-      uint8_t* region = a.send + a.send_off[dest];
-      uint32_t base = 0;
-      if (lane == 0) base = atomicAdd(reinterpret_cast<uint32_t*>(region), W);
-      base = static_cast<uint32_t>(__shfl(static_cast<int>(base), 0, 64));
-      XItem* out = reinterpret_cast<XItem*>(region + kRegionHeader) + base;
-      for (uint32_t w = lane; w < W; w += 64) {
-        XItem it;
-        it.node = c & kRemoteIdMask;
-        it.word = w;
-        it.mask = src[w];
-        out[w] = it;
-      }
-    }
-  }
 }
 
 // ----------------------------------------------------------------- apply ---
@@ -1246,13 +1252,6 @@ hipError_t launch_apply(const ApplyArgs& a, uint32_t round, bool record, hipStre
   return hipGetLastError();
 }
 
-hipError_t launch_send(const ExpandArgs& a, const uint32_t* list, uint32_t n, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  const uint32_t grid = std::min<uint32_t>(1024, (n + 3) / 4);
-  hipLaunchKernelGGL(k_send, dim3(grid), dim3(kBlock), 0, s, a, list, n);
-  return hipGetLastError();
-}
-
 hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t* arrivals,
                        uint64_t* seen, uint8_t* next_flag, uint8_t* blk_flag, hipStream_t s) {
   if (hi <= lo) return hipSuccess;
@@ -1288,6 +1287,16 @@ hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_ch
     hipLaunchKernelGGL((k_pull<false, true>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
   else
     hipLaunchKernelGGL((k_pull<false, false>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack(const PackEntry* entries, const PackSeg* segs, uint32_t n_segs, uint64_t total_words,
+                       const TopicDev* topics, const uint64_t* seen, const uint8_t* gen, uint32_t gen_cur,
+                       uint64_t* send, hipStream_t s) {
+  if (total_words == 0 || n_segs == 0) return hipSuccess;
+  const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(4096, (total_words + kBlock - 1) / kBlock));
+  hipLaunchKernelGGL(k_pack, dim3(grid), dim3(kBlock), 0, s, entries, segs, n_segs, total_words, topics, seen, gen,
+                     gen_cur, send);
   return hipGetLastError();
 }
 

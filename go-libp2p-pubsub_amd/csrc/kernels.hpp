@@ -126,7 +126,7 @@ constexpr uint32_t kNoneNode = 0xFFFFFFFFu;
 constexpr uint32_t kPullWords = 1024;
 
 struct PullArgs {
-  const uint32_t* node_parent;  // node-space parent (kNone for roots)
+  const uint32_t* node_parent;  // node-space parent (kNone for roots and remote parents)
   const uint8_t* node_flags;
   const TopicDev* topics;
   const uint64_t* a_cur;  // arrivals of round-1 (topic roots' seeded rows)
@@ -134,8 +134,33 @@ struct PullArgs {
   uint8_t* gen;
   uint16_t* hop_rec;
   uint64_t* partials;  // [n_blocks][kNumCtr]
+  // multi-GPU: a node whose parent lives on another rank reads that parent's
+  // row from this round's receive buffer: ghost_off[node] = the row's first
+  // word in recv (its reach word is the word before), or kGhostNone
+  const uint64_t* ghost_off;  // null: one rank
+  const uint64_t* recv;
   uint32_t gen_cur;
   uint32_t slot_mod;   // block b adds its counters into partial slot b % slot_mod (zeroed per window)
+};
+constexpr uint64_t kGhostNone = ~0ull;
+
+// Multi-GPU level mode: before round q, each rank ships the
+// rows of its level-(q-1) parents that have children on other ranks -- once
+// per destination rank -- into that rank's region of the send buffer.  A
+// ghost record is [pad if W is even][reach word][W row words]: the row keeps
+// 16-B alignment and its reach word (parent reached this window) is the word
+// before it.  One entry per (parent, destination); the entries of one topic
+// form a segment (constant W).
+struct PackEntry {
+  uint32_t node;     // the parent (local node id)
+  uint32_t pad;
+  uint64_t row_off;  // row, words from the send buffer (reach word at row_off - 1)
+};
+__host__ __device__ inline uint32_t ghost_record_words(uint32_t W) { return W + ((W & 1u) ? 1u : 2u); }
+struct PackSeg {
+  uint32_t e0, e1;  // entries
+  uint32_t topic, W;
+  uint64_t word0;   // the segment's first word in the launch's flattened stream
 };
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch
 
@@ -179,9 +204,10 @@ struct FloodArgs {
   uint32_t spin_ticks;  // wait bound, s_memrealtime ticks (100 MHz)
   uint32_t store_mode;  // EXPERIMENT (PSAMD_FLOOD_STORE): 0 sc1, 1 plain, 2 nt
   uint64_t* prof;       // debug (PSAMD_FLOOD_PROFILE): per wave kFloodProf s_memrealtime stamps / sums
+  uint32_t prof_split;  // debug: pf[7] sums the waits of tasks of later rounds
 };
 // per-wave profile words: first task start, last task end, then summed ticks
-// waiting, resolving, streaming, publishing; tasks run
+// waiting, resolving, streaming, publishing; tasks run; waiting in rounds > prof_split
 constexpr uint32_t kFloodProf = 8;
 constexpr uint32_t kFloodMaxNodes = 64;       // one node per lane
 constexpr uint32_t kFloodGranule = 32;        // reach bits per granule at most
@@ -241,9 +267,6 @@ hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_
 hipError_t launch_init_nodes(const uint32_t* nodes, uint32_t n, const uint16_t* node_topic,
                              const TopicDev* topics, uint64_t* seen, uint64_t* a0, uint64_t* a1,
                              uint8_t* gen, uint32_t gen_cur, bool stamp, hipStream_t s);
-// level mode, multi-GPU: rows of the reached split parents `list` to the
-// send regions of their remote children's owners
-hipError_t launch_send(const ExpandArgs& a, const uint32_t* list, uint32_t n, hipStream_t s);
 hipError_t launch_apply(const ApplyArgs& a, uint32_t round, bool record, hipStream_t s);
 // next_flag / blk_flag may be null (level mode: the root is in the schedule)
 hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t* arrivals,
@@ -254,6 +277,10 @@ hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, uint3
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
                        uint32_t grid, uint32_t round, bool record, bool nt, hipStream_t s);
 
+// multi-GPU level mode: the round's ghost rows into the send buffer
+hipError_t launch_pack(const PackEntry* entries, const PackSeg* segs, uint32_t n_segs, uint64_t total_words,
+                       const TopicDev* topics, const uint64_t* seen, const uint8_t* gen, uint32_t gen_cur,
+                       uint64_t* send, hipStream_t s);
 // Fills PullChunk::p_lo / p_hi from the device node_parent (GPU-built graphs).
 hipError_t launch_chunk_parents(PullChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s);
 // k_flood (flood.hip): grid = resident blocks (<= flood_blocks_per_cu x CUs)

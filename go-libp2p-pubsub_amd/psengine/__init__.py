@@ -326,14 +326,14 @@ class Engine:
         return d.value
 
     # multi-GPU
-    def dist_init(self, rank: int, world: int, unique_id: bytes, partition: int = PART_SUBTREE,
+    def dist_init(self, rank: int, world: int, unique_id: bytes, partition: int = PART_PEER,
                   split_depth: int = 0):
         """RCCL-backed sharding: this engine owns a hash partition of every topic."""
         dc = DistConfig(rank, world, partition, split_depth)
         uid = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         self._check(self._L.ps_dist_init(self._h, C.byref(dc), uid))
 
-    def dist_init_loopback(self, group: "Loopback", rank: int, partition: int = PART_SUBTREE,
+    def dist_init_loopback(self, group: "Loopback", rank: int, partition: int = PART_PEER,
                            split_depth: int = 0):
         dc = DistConfig(rank, group.world, partition, split_depth)
         self._check(self._L.ps_dist_init_loopback(self._h, C.byref(dc), group._h))
@@ -368,7 +368,7 @@ class Loopback:
         self.close()
 
 
-def partition_owner(parent, root: int, topic: int, world: int, partition: int = PART_SUBTREE,
+def partition_owner(parent, root: int, topic: int, world: int, partition: int = PART_PEER,
                     split_depth: int = 0) -> np.ndarray:
     """Host-only: owner rank of every peer of a tree (-1 outside the tree)."""
     par = _u32arr(parent)

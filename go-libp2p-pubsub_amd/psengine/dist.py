@@ -4,7 +4,8 @@ runs inside the engine over its own RCCL communicator (ps_dist_init).
 
 Every rank builds the same topics (the restated joins are deterministic) and
 publishes the same messages; each owns a hash partition of every topic's tree
-nodes (PART_SUBTREE by default, PART_PEER = owner(p) = splitmix64(p) mod N).
+nodes (PART_PEER by default: owner(p) = splitmix64(p) mod N; PART_SUBTREE:
+level-L subtrees).
 The job's deliveries are the sum over ranks; its time is the slowest rank's.
 
 Scaling: "weak" (default) keeps the per-GPU work of the N=1
@@ -82,7 +83,7 @@ def bench_main(args, descr: dict, metric: str):
     torch.cuda.set_device(local)
     dist = init("nccl")  # RCCL on ROCm
     dev = torch.device("cuda", local)
-    part = PART_PEER if getattr(args, "partition", "subtree") == "peer" else PART_SUBTREE
+    part = PART_SUBTREE if getattr(args, "partition", "peer") == "subtree" else PART_PEER
     wl = workload(args, world)
     scaling = getattr(args, "scaling", "weak") if world > 1 else "weak"
     uid = share_bytes(dist, unique_id, rank)

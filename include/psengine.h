@@ -186,7 +186,9 @@ int ps_seen_digest(ps_engine* e, uint64_t* digest_out);
  * exchanges, each round, the deliveries addressed to other ranks' nodes
  * (stream-ordered all-to-allv over RCCL / xGMI).  Stats and ps_read_* cover
  * the owned nodes; sums over ranks give the job totals.
- *   PS_PART_PEER     owner(p) = splitmix64(p) mod world
+ *   PS_PART_PEER     owner(p) = splitmix64(p) mod world (the
+ *                    default): every round ships each parent row whose
+ *                    children live on other ranks once per such rank
  *   PS_PART_SUBTREE  a node below the split level belongs to the owner of its
  *                    ancestor at that level (the subtrees dealt largest first
  *                    to the least-loaded rank), so only edges out of the top

@@ -1,9 +1,9 @@
 """CPU tests of the multi-GPU path (no GPU): the partition function of the
 engine (ps_partition_owner, host-only C ABI) and the bootstrap / reduction
 helpers of psengine/dist.py under a world_size-2 gloo process group, plus a
-2-rank replay of the per-round exchange protocol (owned nodes expand, deliveries
-to other ranks' nodes cross via all_to_all) whose union must equal the
-single-process restatement."""
+2-rank replay of the per-round exchange protocol (ghost parents: a frontier
+row crosses once per remote rank owning a child, via all_to_all) whose union
+must equal the single-process restatement."""
 import os
 import socket
 
@@ -89,46 +89,55 @@ def _worker(rank, world, port, out):
         # bootstrap: rank 0's bytes reach every rank (the RCCL id path)
         uid = D.share_bytes(dist, lambda: bytes(range(128)), rank)
         assert uid == bytes(range(128))
-        # the replayed protocol: trees, ownership, rounds with all_to_all
+        # the replayed protocol: each round, a rank ships the
+        # row of every frontier parent it owns once to every other rank that
+        # owns one of that parent's children (a ghost parent, with its reach
+        # flag); the children read their parent's row locally or from the
+        # ghosts received -- rows of 128 message bits, as on the GPU
         rng = np.random.default_rng(11)
         n = 1500
         par = random_tree(rng, n)
         live = (rng.random(n) > 0.1).astype(np.uint8)
         rp, cl = O.parents_to_csr(par)
+        full = np.array([~0, ~0], dtype=np.int64)
         for part in (PE.PART_PEER, PE.PART_SUBTREE):
             own = PE.partition_owner(par, 0, 0, world, part)
             hop = np.full(n, 255, np.int64)
-            frontier = [0] if own[0] == rank else []
+            rows = {0: full} if own[0] == rank else {}  # this rank's frontier: node -> row
+            shipped = 0
             r = 0
             while True:
                 r += 1
-                out_local, outbox = [], [[] for _ in range(world)]
-                for p in frontier:
-                    for c in cl[rp[p]:rp[p + 1]]:
-                        c = int(c)
-                        if own[c] == rank:
-                            out_local.append(c)
-                        else:
-                            outbox[own[c]].append(c)
-                # all-to-all of the outboxes (object all_gather on gloo)
+                outbox = [[] for _ in range(world)]
+                for p, row in rows.items():
+                    dests = sorted({int(own[c]) for c in cl[rp[p]:rp[p + 1]]} - {rank})
+                    for b in dests:
+                        outbox[b].append((p, row.tolist(), 1))  # reached: flag 1
+                        shipped += 1
                 gathered = [None] * world
                 tdist.all_gather_object(gathered, outbox)
-                recv = [gathered[s][rank] for s in range(world)]
-                nxt = []
-                for c in out_local + [c for lst in recv for c in lst]:
-                    if live[c] and hop[c] == 255:
-                        hop[c] = r
-                        nxt.append(c)
-                frontier = nxt
-                alive = [len(frontier)]
+                ghosts = {p: np.array(row, np.int64) for s in range(world) for p, row, f in gathered[s][rank] if f}
+                nxt = {}
+                for src in (rows, ghosts):
+                    for p, row in src.items():
+                        for c in cl[rp[p]:rp[p + 1]]:
+                            c = int(c)
+                            if own[c] == rank and live[c] and hop[c] == 255:
+                                hop[c] = r
+                                nxt[c] = row  # new = row(parent) & ~seen(c), seen empty
+                rows = nxt
+                alive = [len(rows)]
                 tot = [None] * world
                 tdist.all_gather_object(tot, alive)
                 if sum(t[0] for t in tot) == 0:
                     break
             gathered = [None] * world
             tdist.all_gather_object(gathered, hop.tolist())
+            sh = [None] * world
+            tdist.all_gather_object(sh, [shipped])
             if rank == 0:
                 out[part] = np.min(np.array(gathered), axis=0)
+                out[(part, "shipped")] = sum(x[0] for x in sh)
         # job totals: max time, summed counts
         t, c = D.job_totals(dist, 1.0 + rank, 10 * (rank + 1))
         assert t == float(world) and c == 10 * world * (world + 1) // 2
@@ -150,5 +159,14 @@ def test_gloo_world2_protocol_matches_single_process(oracle_lib):
     live = (rng.random(n) > 0.1).astype(np.uint8)
     rp, cl = O.parents_to_csr(par)
     _, hops, _ = O.disseminate(rp, cl, 0, live, 1)
+    own_peer = PE.partition_owner(par, 0, 0, world, PE.PART_PEER)
     for part in (PE.PART_PEER, PE.PART_SUBTREE):
         assert np.array_equal(np.asarray(out[part]).astype(np.uint8), hops[0]), part
+    # one ghost row per (reached parent, remote rank owning a child): never
+    # more than the cross edges, and the subtree partition ships far fewer
+    reached = hops[0] != 255
+    reached[0] = True
+    cross = {(int(p), int(own_peer[c])) for p in range(n) if reached[p]
+             for c in cl[rp[p]:rp[p + 1]] if own_peer[c] != own_peer[p]}
+    assert out[(PE.PART_PEER, "shipped")] == len(cross)
+    assert out[(PE.PART_SUBTREE, "shipped")] < out[(PE.PART_PEER, "shipped")] / 4

@@ -126,3 +126,40 @@ def test_gpu_build_multi_topic_and_live_mask():
                     [e.depth(t) for t in range(len(wl.topics))]))
         e.close()
     assert out[0] == out[1]
+
+
+def test_cfg5_full_size_batches_match_oracle():
+    """BASELINE cfg5 at its stated size: 1M peers, 90 % members joined by the
+    restated protocol, then batches of 1 % graceful leaves (Part + repair,
+    subtree.go:46-98,356-375), 1 % joins (subtree.go:100-194) and a
+    1,000-message burst, the node space rebuilt on the GPU every batch.  Each
+    batch: the tree equals the restatement's, and the hops of sampled messages
+    equal oracle Tree.message()'s (peer by peer, 1M peers)."""
+    wl = WL.cfg5()
+    batches = 4
+    plan = WL.churn_plan(wl, batches)
+    eng = make_engine(wl.n_peers, True, record_hops=True, seed=wl.seed)
+    ot = O.Tree(wl.n_peers, 0, 2, 5, PE.Engine.topic_seed(wl.seed, 0))
+    WL.build_engine_topics(eng, wl)
+    ot.join_all(wl.topics[0].join_order)
+    for b, (leave, join) in enumerate(plan):
+        for p in leave:
+            assert ot.leave(int(p)) in (0, -3)  # an orphaned peer cannot Part
+        try:
+            eng.leave(0, leave)
+        except PE.EngineError:
+            pass
+        st = eng.join(0, join, check=False)
+        exp_st = np.array([ot.join(int(p)) for p in join], dtype=np.int32)
+        assert np.array_equal(st, exp_st), b
+        first = eng.publish(wl.msg_topics)
+        run = eng.run()
+        exp = ot.message()
+        assert run.deliveries == wl.n_msgs * int((exp != 0xFF).sum()), b
+        for m in (0, 63, 64, 500, wl.n_msgs - 1):
+            got = eng.hops(first + m)
+            if not np.array_equal(got, exp):
+                bad = np.nonzero(got != exp)[0][:8]
+                raise AssertionError(f"batch {b} msg {m}: peers {bad} got {got[bad]} want {exp[bad]}")
+        assert np.array_equal(eng.parents(0), ot.parents()), b
+    eng.close()

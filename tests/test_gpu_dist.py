@@ -204,3 +204,41 @@ def test_sharded_churn_batches():
     for e in engines:
         e.close()
     lb.close()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_cfg4_shaped_peer_partition(world):
+    """cfg4-shaped trees (TreeOpts{8,20} by the restated joins, scaled to
+    200k peers) under the peer hash (the default partition),
+    with ~3 % dead peers: every round ships ghost parents over the loopback
+    transport; the ranks' deliveries and seen digests add up to the single
+    engine's, and sampled messages' hops equal the restatement's."""
+    wl = WL.cfg4(200_000, 300)
+    rng = np.random.default_rng(40 + world)
+    live = (rng.random(wl.n_peers) > 0.03).astype(np.uint8)
+    live[0] = 1
+    with PE.Engine(wl.n_peers, 1, seed=wl.seed) as one:
+        WL.build_engine_topics(one, wl)
+        par = one.parents(0)
+        one.set_live(live)
+        one.publish(wl.msg_topics)
+        st1 = one.run()
+        d1 = one.seen_digest()
+    lb = PE.Loopback(world)
+    engines = [PE.Engine(wl.n_peers, 1, seed=wl.seed, record_hops=True) for _ in range(world)]
+    for r, e in enumerate(engines):
+        e.dist_init_loopback(lb, r)  # PART_PEER by default
+        WL.build_engine_topics(e, wl)
+        e.set_live(live)
+    firsts = [e.publish(wl.msg_topics) for e in engines]
+    stats = run_ranks(engines)
+    assert all(s.expand_mode == PE.MODE_LEVEL_PULL for s in stats)
+    assert sum(s.deliveries for s in stats) == st1.deliveries
+    assert sum(e.seen_digest() for e in engines) % (1 << 64) == d1
+    rp, cl = O.parents_to_csr(par)
+    _, hops, _ = O.disseminate(rp, cl, 0, live, 1)
+    for m in (0, 150, 299):
+        assert np.array_equal(merged_hops(engines, firsts[0] + m), hops[0]), m
+    for e in engines:
+        e.close()
+    lb.close()
