@@ -173,25 +173,62 @@ def pmc_traffic(kernel: str, workload: str):
     return d.get("traffic_bytes_per_launch"), d.get("source")
 
 
+def kernel_split(st):
+    """{kernel: (algorithmic bytes, device ms, launches)} of one run, by the
+    rocprofv3 names of the launches that ran its rounds: k_flood (the leading
+    rounds of a single-rank level window, one persistent launch, timed into
+    round 1), k_pull (one launch per remaining round) or k_expand
+    (compaction mode)."""
+    kern = PE.MODE_KERNEL.get(st.expand_mode, "k_expand")
+    fr = int(getattr(st, "flood_rounds", 0))
+    if st.expand_mode != PE.MODE_FLOOD or fr >= st.rounds or st.windows != 1:
+        return {kern: (st.expand_bytes, st.expand_ms, st.expand_launches)}
+    bf = sum(int(st.expand_bytes_per_round[q]) for q in range(1, fr + 1))
+    tf = float(st.expand_ms_per_round[1])
+    return {"k_flood": (bf, tf, 1),
+            "k_pull": (st.expand_bytes - bf, st.expand_ms - tf, st.expand_launches - 1)}
+
+
 def hot_kernel(st):
-    """The kernel the roofline is quoted on (its rocprofv3 name): the one that
-    ran the window's rounds -- k_flood (one persistent launch per window),
-    k_pull (one launch per round) or k_expand (compaction mode)."""
-    return PE.MODE_KERNEL.get(st.expand_mode, "k_expand")
+    """The kernel the roofline is quoted on: of kernel_split's launches, the
+    one with the most device time (by bytes when untimed)."""
+    sp = kernel_split(st)
+    return max(sp, key=lambda k: (sp[k][1], sp[k][0]))
 
 
 def instrumented(eng, step, n):
     """Roofline pass: n steps with HIP events around every hot-kernel launch
-    on the engine's stream (PS_F_TIME_KERNELS); the timed steps run without."""
+    on the engine's stream (PS_F_TIME_KERNELS); the timed steps run without.
+    Returns ({kernel: [bytes, ms, launches]}, last stats)."""
     eng.set_time_kernels(True)
-    tot_bytes, tot_ms, launches, st = 0, 0.0, 0, None
+    per, st = {}, None
     for _ in range(n):
         st = step()
-        tot_bytes += st.expand_bytes
-        tot_ms += st.expand_ms
-        launches += st.expand_launches
+        for k, v in kernel_split(st).items():
+            acc = per.setdefault(k, [0, 0.0, 0])
+            for i in range(3):
+                acc[i] += v[i]
     eng.set_time_kernels(False)
-    return tot_bytes, tot_ms, launches, st
+    return per, st
+
+
+def roofline_of(per, traffic=None, traffic_src=None):
+    """The roofline object for the dominant kernel of `per` (the most device
+    time), with every kernel's own figures under "kernels"."""
+    def fig(k):
+        b, ms, n = per[k]
+        gbs = b / max(1e-12, ms * 1e-3) / 1e9
+        return {"achieved": gbs, "frac": gbs / HBM_PEAK_GBS, "avg_launch_us": ms * 1e3 / max(1, n),
+                "bytes_per_launch": b / max(1, n), "launches": n, "device_ms": ms}
+    hot = max(per, key=lambda k: (per[k][1], per[k][0]))
+    f = fig(hot)
+    return {"bound": "hbm", "achieved": f["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": f["frac"], "traffic": traffic, "kernel": hot, "avg_launch_us": f["avg_launch_us"],
+            "bytes_per_launch": f["bytes_per_launch"],
+            "timing": "HIP events around every launch on the engine stream, "
+                      "separate instrumented steps after the timed region",
+            "traffic_source": traffic_src,
+            "kernels": {k: fig(k) for k in sorted(per)}}
 
 
 def bench_cfg5(args):
@@ -232,10 +269,8 @@ def bench_cfg5(args):
         run_host += st.host_ms
         run_gpu += st.run_ms
     wall = time.perf_counter() - t0
-    tot_bytes, tot_ms, launches, st = instrumented(
+    per, st = instrumented(
         eng, lambda it=iter(range(args.warmup + args.steps, args.warmup + args.steps + 3)): step(next(it))[0], 3)
-    achieved = tot_bytes / max(1e-12, tot_ms * 1e-3) / 1e9
-    kernel = hot_kernel(st)
     out = {
         "metric": METRIC + " [cfg5 end to end]",
         "value": tot / wall,
@@ -250,9 +285,7 @@ def bench_cfg5(args):
                                   "join_host": join_s * 1e3 / args.steps,
                                   "ps_run_wall": run_host / args.steps,
                                   "ps_run_gpu": run_gpu / args.steps},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "kernel": kernel,
-                     "avg_launch_us": tot_ms * 1e3 / max(1, launches)},
+        "roofline": roofline_of(per),
         "last_step": {"deliveries": st.deliveries, "rounds": st.rounds, "host_ms": st.host_ms,
                       "run_ms": st.run_ms},
     }
@@ -283,17 +316,14 @@ def general_path(eng, wl, deliv_expected, steps: int, warmup: int = 1, max_start
     tot = sum(step().deliveries for _ in range(steps))
     wall = time.perf_counter() - t0
     assert tot == deliv_expected * steps
-    tot_bytes, tot_ms, launches, st = instrumented(eng, step, 2)
-    achieved = tot_bytes / max(1e-12, tot_ms * 1e-3) / 1e9
+    per, st = instrumented(eng, step, 2)
+    roof = roofline_of(per)
+    roof["expand_ms_per_step"] = sum(v[1] for v in per.values()) / 2
     return {"workload": f"{wl.name} with start rounds uniform over 0..{max_start} (paced publishing): "
                         "compaction mode, k_expand + frontier compaction every round",
             "value": tot / wall, "unit": "deliveries/s", "steps": steps, "ms_per_step": wall * 1e3 / steps,
             "rounds": st.rounds, "deliveries_per_step": deliv_expected,
-            "roofline": {"bound": "hbm", "kernel": hot_kernel(st), "achieved": achieved, "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                         "avg_launch_us": tot_ms * 1e3 / max(1, launches),
-                         "bytes_per_launch": tot_bytes / max(1, launches),
-                         "expand_ms_per_step": tot_ms / 2}}
+            "roofline": roof}
 
 
 def main():
@@ -365,10 +395,9 @@ def main():
     tot_deliv = sum(st.deliveries for st in sts)
     assert args.no_check or tot_deliv == deliv_expected * args.steps
     value = tot_deliv / wall
-    tot_bytes, tot_expand_ms, launches, st = instrumented(eng, step, max(3, min(args.steps, 5)))
+    per, st = instrumented(eng, step, max(3, min(args.steps, 5)))
     assert args.no_check or st.deliveries == deliv_expected
-    achieved = tot_bytes / (tot_expand_ms * 1e-3) / 1e9
-    kernel = hot_kernel(st)
+    kernel = max(per, key=lambda k: (per[k][1], per[k][0]))
     traffic, traffic_src = pmc_traffic(kernel, wl.name)
     pair_gbs = value * PAIR_BYTES / 1e9
     out = {
@@ -390,20 +419,15 @@ def main():
                    "parallelism": "1 GPU",
                    "steps_issue": "blocking ps_run" if args.sync else
                    "pipelined ps_run_async/ps_wait (<= 2 batches in flight)"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": kernel, "avg_launch_us": tot_expand_ms * 1e3 / max(1, launches),
-                     "bytes_per_launch": tot_bytes / max(1, launches),
-                     "timing": "HIP events around every launch on the engine stream, "
-                               "separate instrumented steps after the timed region",
-                     "traffic_source": traffic_src},
+        "roofline": roofline_of(per, traffic, traffic_src),
         # SURVEY.md §8d's (peer,msg)-pair formulation: the HBM rate a pair-frontier
         # engine would need for this delivery rate.  A model figure, NOT bandwidth
         # this engine moves; compare roofline.frac, not this, with the peak.
         "pair_model": {"bytes_per_delivery": PAIR_BYTES, "equiv_GBs_not_achievable": pair_gbs,
                        "note": "model-equivalent rate of the 28.375 B/delivery pair formulation; "
                                "this engine moves 64 messages per 8-B word (roofline.bytes_per_launch)"},
-        "last_step": {"rounds": st.rounds, "windows": st.windows, "run_ms": st.run_ms,
+        "last_step": {"rounds": st.rounds, "windows": st.windows, "flood_rounds": st.flood_rounds,
+                      "run_ms": st.run_ms,
                       "expand_ms": st.expand_ms, "host_ms": st.host_ms,
                       "edge_words": st.edge_words,
                       "frontier_per_round": st.as_dict()["frontier_per_round"],

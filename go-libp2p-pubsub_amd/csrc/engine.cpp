@@ -138,6 +138,7 @@ struct ps_engine {
   bool flood_broken = false;  // a dependency wait timed out once: per-level launches from then on
   uint32_t flood_grid = 0;    // resident blocks (0: k_flood unavailable)
   uint32_t flood_words = kFloodWords;  // row words per task (PSAMD_FLOOD_WORDS)
+  uint64_t flood_top_bytes = 16ull << 20;  // k_flood runs the leading rounds writing at most this many row bytes
   uint32_t flood_epoch = 0;   // granule tag of the last launch (granules are never reset)
   std::vector<uint64_t> flood_key;
   std::vector<FloodTask> flood_tasks;
@@ -225,7 +226,7 @@ struct ps_engine {
     ps_stats st{};
     bool deferred = false;
     uint32_t r = 0, launches = 0;
-    uint32_t mode = PS_MODE_COMPACT;
+    uint32_t mode = PS_MODE_COMPACT, flood_rounds = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the window's kernels
     uint64_t* hs = nullptr;  // pinned: (PS_MAX_ROUNDS + 1) x kNumCtr counters
     uint64_t* hs_dev = nullptr;  // hs, device-mapped (k_reduce_rounds writes it)
@@ -1273,7 +1274,7 @@ int build_flood_tasks(ps_engine* e, const std::vector<TopicDev>& tab, const std:
 // Returns false when a k_flood dependency wait timed out (its timeout word
 // is folded into row 0).
 bool accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uint32_t r, uint32_t planned0,
-                       uint32_t mode, uint32_t launches, int32_t world) {
+                       uint32_t mode, uint32_t flood_rounds, uint32_t launches, int32_t world) {
   const bool pull = mode == PS_MODE_LEVEL_PULL || mode == PS_MODE_FLOOD;
   for (uint32_t q = 1; q <= r; ++q) {
     const uint64_t* c = &hs[static_cast<size_t>(q) * kNumCtr];
@@ -1289,16 +1290,18 @@ bool accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uin
     // per entry word the arrival read 8 (+ 8 when cleared); per child its
     // flag byte + generation read/write (tree) or col id 4 (mesh); per
     // seen read / seen write / arrival write 8.
+    uint64_t b;
     if (pull)  // pull model: per node parent id 4 + flag 1 + parent generation 1 (k_flood:
                // + its own generation 1, the seen test), per reached node its generation
                // write 1; parent rows read once; rows written
-      st->expand_bytes += c[kCtrChildren] * (mode == PS_MODE_FLOOD ? 7 : 6) + c[kCtrMeshChildren] * 1 +
-                          c[kCtrEntryWords] * 8 + c[kCtrSeenWrites] * 8;
+      b = c[kCtrChildren] * (q <= flood_rounds ? 7 : 6) + c[kCtrMeshChildren] * 1 + c[kCtrEntryWords] * 8 +
+          c[kCtrSeenWrites] * 8;
     else
-      st->expand_bytes += c[kCtrEntries] * 18 + c[kCtrEntryWords] * 8 + c[kCtrClearWords] * 8 +
-                          c[kCtrChildren] * 3 + c[kCtrMeshChildren] * 4 + c[kCtrSeenReads] * 8 +
-                          c[kCtrSeenWrites] * 8 + c[kCtrArrivalWrites] * 8;
+      b = c[kCtrEntries] * 18 + c[kCtrEntryWords] * 8 + c[kCtrClearWords] * 8 + c[kCtrChildren] * 3 +
+          c[kCtrMeshChildren] * 4 + c[kCtrSeenReads] * 8 + c[kCtrSeenWrites] * 8 + c[kCtrArrivalWrites] * 8;
+    st->expand_bytes += b;
     if (q < PS_MAX_ROUNDS) {
+      st->expand_bytes_per_round[q] += b;
       st->deliveries_per_round[q] += c[kCtrDeliveries] + app_d;
       st->frontier_per_round[q] += static_cast<uint32_t>(c[kCtrEntries]);
     }
@@ -1306,6 +1309,7 @@ bool accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uin
   st->rounds += r;
   st->expand_launches += launches;
   st->expand_mode = mode;
+  st->flood_rounds = flood_rounds;
   st->windows += 1;
   return mode != PS_MODE_FLOOD || hs[kCtrDeliveries] == 0;
 }
@@ -1537,49 +1541,56 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   };
   const uint32_t planned0 = max_depth + max_start + 1;
   // level mode: every active topic a tree whose window messages share one
-  // start round.  One rank: the whole window is one k_flood launch; several
-  // ranks: one k_pull launch per round (the frontier exchange separates the
-  // rounds); PSAMD_FLOOD=0 selects the per-round launches on one rank too.
+  // start round.  One rank: the leading rounds whose rows are small (latency
+  // bound: a launch each would cost more than their bytes) run as ONE
+  // persistent k_flood launch, the rest one k_pull launch per round
+  // (bandwidth bound); several ranks: one k_pull launch per round (the
+  // frontier exchange separates the rounds).  PSAMD_FLOOD=0 selects the
+  // per-round launches on one rank too.
   bool level = !any_mesh && planned0 + 1 < round_cap;
   for (uint32_t t = 0; t < nt && level; ++t)
     if (tab[t].W && !(tab[t].flags & kTopicSingleStart)) level = false;
-  const bool flood = level && world == 1 && e->flood_on && !e->flood_broken && e->flood_grid > 0 &&
-                     e->n_nodes < 0x80000000u;  // k_flood marks node ids with bit 31
-  const bool pull = level && !flood;
-  const uint32_t mode = flood ? PS_MODE_FLOOD : pull ? PS_MODE_LEVEL_PULL : PS_MODE_COMPACT;
+  const bool flood_ok = level && world == 1 && e->flood_on && !e->flood_broken && e->flood_grid > 0 &&
+                        e->n_nodes < 0x80000000u;  // k_flood marks node ids with bit 31
+  uint32_t flood_rounds = 0;    // rounds 1..flood_rounds: k_flood
   std::vector<uint32_t> lgrid;  // per-round launches: grid of every round
   uint32_t n_slots = 0;         // level mode: partial counter slots of the window
   if (level) {
-    int rc2 = flood ? build_flood_tasks(e, tab, tstart, planned0) : build_pull_chunks(e, tab, tstart, planned0);
+    int rc2 = build_pull_chunks(e, tab, tstart, planned0);
+    if (!rc2 && flood_ok) {
+      while (flood_rounds < planned0 && e->pull_bytes[flood_rounds + 1] <= e->flood_top_bytes) ++flood_rounds;
+      if (flood_rounds) rc2 = build_flood_tasks(e, tab, tstart, flood_rounds);
+    }
     if (!rc2 && world > 1) rc2 = build_ghost_plan(e, tab, tstart, planned0);
     if (rc2) return rc2;
     // desc[3q..]: round q's partial slots (first, end, stride) for the reduce
     auto& desc = e->desc_host;
     desc.assign(3 * (planned0 + 2), 0);
-    if (flood) {
+    uint32_t slot = 0;
+    if (flood_rounds) {
       desc[0] = 0;  // row 0: k_flood's timeout word (slot 0)
       desc[1] = 1;
       desc[2] = 1;
-      for (uint32_t q = 1; q <= planned0; ++q) {
+      for (uint32_t q = 1; q <= flood_rounds; ++q) {
         desc[3 * q] = e->flood_slot0[q];
         desc[3 * q + 1] = e->flood_slot0[q] + e->flood_nslot[q];
         desc[3 * q + 2] = e->flood_nslot[q] ? 1 : 0;
       }
-      n_slots = e->flood_slots;
-    } else {
-      // launch of round q owns the slots [woff[q], woff[q+1]): one per block, at most kPullSlots
-      lgrid.assign(planned0 + 1, 0);
-      auto& woff = e->woff_host;
-      woff.assign(planned0 + 2, 0);
-      for (uint32_t q = 1; q <= planned0; ++q) {
-        lgrid[q] = ceil_div(e->pull_off[q + 1] - e->pull_off[q], kBlock / 64);
-        woff[q + 1] = woff[q] + std::min<uint32_t>(lgrid[q], kPullSlots);
-        desc[3 * q] = woff[q];
-        desc[3 * q + 1] = woff[q + 1];
-        desc[3 * q + 2] = 1;
-      }
-      n_slots = woff[planned0 + 1];
+      slot = e->flood_slots;
     }
+    // k_pull launch of round q owns the slots [woff[q], woff[q+1]): one per block, at most kPullSlots
+    lgrid.assign(planned0 + 1, 0);
+    auto& woff = e->woff_host;
+    woff.assign(planned0 + 2, 0);
+    woff[flood_rounds + 1] = slot;
+    for (uint32_t q = flood_rounds + 1; q <= planned0; ++q) {
+      lgrid[q] = ceil_div(e->pull_off[q + 1] - e->pull_off[q], kBlock / 64);
+      woff[q + 1] = woff[q] + std::min<uint32_t>(lgrid[q], kPullSlots);
+      desc[3 * q] = woff[q];
+      desc[3 * q + 1] = woff[q + 1];
+      desc[3 * q + 2] = 1;
+    }
+    n_slots = woff[planned0 + 1];
     HIP_TRY(e->d_partials.ensure(static_cast<size_t>(std::max<uint32_t>(n_slots, 1)) * kNumCtr * 8),
             "alloc level partials");
     HIP_TRY(e->d_woff.ensure(desc.size() * 4), "alloc reduce descriptors");
@@ -1612,6 +1623,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     HIP_TRY(e->d_recv.ensure(max_recv), "alloc recv regions");
   }
 
+  const bool flood = flood_rounds > 0;
+  const uint32_t mode = flood ? PS_MODE_FLOOD : level ? PS_MODE_LEVEL_PULL : PS_MODE_COMPACT;
   const auto t_w3 = std::chrono::steady_clock::now();
   hipStream_t s = e->stream;
   // the window's first kernel also copies the staged uploads, applies the
@@ -1795,11 +1808,12 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       fa.gen_cur = a.gen_cur;
       fa.spin_ticks = 200000000u;  // 2 s of s_memrealtime (100 MHz)
       if (const char* v = std::getenv("PSAMD_FLOOD_STORE")) fa.store_mode = static_cast<uint32_t>(std::atoi(v));
+      if (const char* v = std::getenv("PSAMD_FLOOD_DB")) fa.db = static_cast<uint32_t>(std::atoi(v));
       const uint32_t flood_blocks = std::min<uint32_t>(e->flood_grid, ceil_div(fa.n_tasks, kBlock / 64));
       if (e->flood_profile) {
         HIP_TRY(e->d_flood_prof.ensure(static_cast<size_t>(flood_blocks) * 4 * kFloodProf * 8), "alloc flood profile");
         fa.prof = e->d_flood_prof.as<uint64_t>();
-        fa.prof_split = planned0 * 2 / 3;
+        fa.prof_split = flood_rounds * 2 / 3;
         e->flood_prof_waves = flood_blocks * 4;
       }
       r = 1;  // the per-round kernel times of a timed run go to round 1
@@ -1807,9 +1821,11 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       ++launches;
       HIP_TRY(launch_flood(fa, flood_blocks, record, s), "flood");
       HIP_TRY(time_mark(false), "event");
-    } else {
-      for (r = 1; r <= planned0; ++r) {
-        a.a_cur = arr[(r - 1) & 1];
+    }
+    {
+      for (r = flood_rounds + 1; r <= planned0; ++r) {
+        // (after k_flood every root is seeded in arr[0] already)
+        a.a_cur = flood ? arr[0] : arr[(r - 1) & 1];
         a.a_next = arr[r & 1];
         // multi-GPU: this round's ghost parents (rows written last round, or
         // seeded roots) to the ranks owning their children, then the exchange
@@ -1851,7 +1867,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
                   "pull");
           HIP_TRY(time_mark(false), "event");
         }
-        HIP_TRY(seed_round(r, a.a_next), "seed");
+        if (!flood) HIP_TRY(seed_round(r, a.a_next), "seed");
       }
     }
     r = planned0;
@@ -1940,6 +1956,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     f.r = r;
     f.launches = launches;
     f.mode = mode;
+    f.flood_rounds = flood_rounds;
     e->last_topics = tab;
     for (uint32_t t = 0; t < nt; ++t) {
       e->last_cnt[t] = tab[t].W ? win[t].n : 0;
@@ -1976,7 +1993,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   }
   HIP_TRY(hipStreamSynchronize(s), "sync");
   if (mode == PS_MODE_FLOOD && e->flood_profile && e->flood_prof_waves) flood_profile_report(e);
-  if (!accumulate_window(st, hs.data(), ha.data(), r, planned0, mode, launches, world)) {
+  if (!accumulate_window(st, hs.data(), ha.data(), r, planned0, mode, flood_rounds, launches, world)) {
     e->flood_broken = true;
     return e->fail(PS_E_DEVICE, "k_flood: a dependency wait timed out (waves not co-resident?); "
                                 "per-round launches from now on");
@@ -2099,6 +2116,8 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_FLOOD_PROFILE")) e->flood_profile = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD_WORDS"))
     e->flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
+  if (const char* v = std::getenv("PSAMD_FLOOD_TOP_BYTES"))  // the k_flood / k_pull split (tests: ~0 = all k_flood)
+    e->flood_top_bytes = std::strtoull(v, nullptr, 0);
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess) {
     delete e;
@@ -2539,7 +2558,7 @@ int ps_wait(ps_engine* e, ps_stats* out) {
     HIP_TRY(hipEventElapsedTime(&ms, f.ev0, f.ev1), "elapsed");
     f.st.run_ms += ms;
     f.deferred = false;
-    if (!accumulate_window(&f.st, f.hs, f.ha, f.r, f.planned0, f.mode, f.launches, f.world)) {
+    if (!accumulate_window(&f.st, f.hs, f.ha, f.r, f.planned0, f.mode, f.flood_rounds, f.launches, f.world)) {
       e->flood_broken = true;
       return e->fail(PS_E_DEVICE, "k_flood: a dependency wait timed out (waves not co-resident?); "
                                   "per-round launches from now on");

@@ -120,6 +120,59 @@ __device__ __forceinline__ void flood_stream_even(const FloodArgs& a, uint64_t* 
   }
 }
 
+// Stream, even W, double-buffered: batch b + 1's loads are issued before batch
+// b's stores, so a wave waits for its loads only -- never for its own store
+// acknowledgements, which retire in the background (the vector-memory
+// counter is in order: waiting for batch b + 1 waits for batch b - 1's
+// stores, two batches back).
+template <bool kRecord, int kAux, uint32_t kU>
+__device__ __forceinline__ void flood_stream_even_db(const FloodArgs& a, uint64_t* out_row, uint32_t total,
+                                                     uint32_t W, __amdgpu_buffer_rsrc_t in, uint32_t pbase,
+                                                     const uint32_t* src, uint32_t lane, uint32_t round,
+                                                     PullCtr& c) {
+  const __amdgpu_buffer_rsrc_t out = rsrc(out_row, total * 8u);
+  const float rw = 1.0f / static_cast<float>(W);
+  auto issue = [&](uint32_t i0, uint4 (&v)[kU], uint32_t (&so)[kU]) {
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t i = i0 + u * 128 + 2 * lane;
+      int32_t kk, r;
+      split_word(i < total ? i : total - 2, rw, W, kk, r);
+      const uint32_t p = i < total ? src[kk] : kNoneNode;
+      const bool go = p != kNoneNode;
+      v[u] = ld16_sc1(in, go ? ((p - pbase) * W + static_cast<uint32_t>(r)) * 8u : kOutOfRange);
+      so[u] = go ? i * 8u : kOutOfRange;
+    }
+  };
+  auto drain = [&](const uint4 (&v)[kU], const uint32_t (&so)[kU]) {
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      st16_aux<kAux>(out, so[u], v[u]);
+      const bool own = so[u] != kOutOfRange;
+      c.deliv += own ? popc4(v[u]) : 0u;
+      c.sw += own ? 2u : 0u;
+      if constexpr (kRecord) {
+        if (own) {
+          const uint64_t cw = (out_row - a.seen) + so[u] / 8u;
+          record_word(a.hop_rec, cw, static_cast<uint64_t>(v[u].y) << 32 | v[u].x, round);
+          record_word(a.hop_rec, cw + 1, static_cast<uint64_t>(v[u].w) << 32 | v[u].z, round);
+        }
+      }
+    }
+  };
+  constexpr uint32_t kStep = kU * 128;
+  uint4 va[kU], vb[kU];
+  uint32_t sa[kU], sb[kU];
+  issue(0, va, sa);
+  for (uint32_t i0 = 0; i0 < total; i0 += 2 * kStep) {
+    const bool more = i0 + kStep < total;
+    if (more) issue(i0 + kStep, vb, sb);
+    drain(va, sa);
+    if (i0 + 2 * kStep < total) issue(i0 + 2 * kStep, va, sa);
+    if (more) drain(vb, sb);
+  }
+}
+
 // Stream, odd W: 16-B stores over the run's 16-B aligned word pairs; a pair
 // may straddle two rows, so its two words are loaded separately (8 B each,
 // from each node's own source).  A head word (run not 16-B aligned) and a
@@ -226,13 +279,12 @@ __device__ __forceinline__ void flood_flush(const FloodArgs& a, PullCtr& c, uint
   c = PullCtr{};
 }
 
-template <bool kRecord, int kAux>
+template <bool kRecord, int kAux, uint32_t kDB = 0>
 __global__ __launch_bounds__(kBlock, kFloodBlocksPerCu) void k_flood(FloodArgs a) {
   __shared__ uint32_t src_lds[kBlock / 64][kFloodMaxNodes];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t wave = blockIdx.x * (kBlock / 64) + wid;
-  const uint32_t nw = gridDim.x * (kBlock / 64);
   uint32_t* src = src_lds[wid];
   const uint32_t cur = a.gen_cur & 0xFF;
   PullCtr c;
@@ -241,6 +293,10 @@ __global__ __launch_bounds__(kBlock, kFloodBlocksPerCu) void k_flood(FloodArgs a
   auto stamp = [&]() -> uint64_t { return a.prof ? __builtin_amdgcn_s_memrealtime() : 0; };
   uint64_t t_a = stamp();
   pf[0] = t_a;
+  // static round robin over the list (topological order): wave g runs tasks
+  // g, g + nw, ...; every wave is resident (grid <= occupancy), so the
+  // earliest unfinished task always has its parents done
+  const uint32_t nw = gridDim.x * (kBlock / 64);
   FloodTask T = uniform(a.tasks[wave < a.n_tasks ? wave : 0]);
   // the previous task's granules, published once its row stores are known
   // to have drained (see below)
@@ -341,6 +397,8 @@ __global__ __launch_bounds__(kBlock, kFloodBlocksPerCu) void k_flood(FloodArgs a
       const __amdgpu_buffer_rsrc_t rin = rsrc(prow, static_cast<uint32_t>(span));
       if (W & 1u)
         flood_stream_odd<kRecord>(a, out_row, total, W, rin, T.p_lo, src, lane, T.round, c);
+      else if constexpr (kDB > 0)  // EXPERIMENT
+        flood_stream_even_db<kRecord, kAux, kDB>(a, out_row, total, W, rin, T.p_lo, src, lane, T.round, c);
       else
         flood_stream_even<kRecord, kAux>(a, out_row, total, W, rin, T.p_lo, src, lane, T.round, c);
     }
@@ -408,6 +466,10 @@ hipError_t launch_flood(const FloodArgs& a, uint32_t grid, bool record, hipStrea
   if (a.n_tasks == 0 || grid == 0) return hipSuccess;
   if (record)
     hipLaunchKernelGGL((k_flood<true, kAuxSC1>), dim3(grid), dim3(kBlock), 0, s, a);
+  else if (a.db == 4)  // EXPERIMENT: double-buffered stream
+    hipLaunchKernelGGL((k_flood<false, kAuxSC1, 4>), dim3(grid), dim3(kBlock), 0, s, a);
+  else if (a.db == 8)
+    hipLaunchKernelGGL((k_flood<false, kAuxSC1, 8>), dim3(grid), dim3(kBlock), 0, s, a);
   else if (a.store_mode == 1)  // EXPERIMENT: plain even-W row stores
     hipLaunchKernelGGL((k_flood<false, 0>), dim3(grid), dim3(kBlock), 0, s, a);
   else if (a.store_mode == 2)  // EXPERIMENT: nt even-W row stores

@@ -203,6 +203,7 @@ struct FloodArgs {
   uint32_t gen_cur;
   uint32_t spin_ticks;  // wait bound, s_memrealtime ticks (100 MHz)
   uint32_t store_mode;  // EXPERIMENT (PSAMD_FLOOD_STORE): 0 sc1, 1 plain, 2 nt
+  uint32_t db;          // EXPERIMENT (PSAMD_FLOOD_DB): double-buffered even-W stream, 4 or 8 per batch
   uint64_t* prof;       // debug (PSAMD_FLOOD_PROFILE): per wave kFloodProf s_memrealtime stamps / sums
   uint32_t prof_split;  // debug: pf[7] sums the waits of tasks of later rounds
 };

@@ -52,12 +52,13 @@ class Stats(C.Structure):
                 ("edge_words", C.c_uint64), ("expand_bytes", C.c_uint64),
                 ("windows", C.c_uint64), ("rounds", C.c_uint64), ("expand_launches", C.c_uint64),
                 ("run_ms", C.c_double), ("expand_ms", C.c_double), ("host_ms", C.c_double),
-                ("expand_mode", C.c_uint32), ("reserved", C.c_uint32),
+                ("expand_mode", C.c_uint32), ("flood_rounds", C.c_uint32),
                 ("deliveries_per_round", C.c_uint64 * MAX_ROUNDS),
                 ("expand_ms_per_round", C.c_float * MAX_ROUNDS),
-                ("frontier_per_round", C.c_uint32 * MAX_ROUNDS)]
+                ("frontier_per_round", C.c_uint32 * MAX_ROUNDS),
+                ("expand_bytes_per_round", C.c_uint64 * MAX_ROUNDS)]
 
-    PER_ROUND = ("deliveries_per_round", "expand_ms_per_round", "frontier_per_round")
+    PER_ROUND = ("deliveries_per_round", "expand_ms_per_round", "frontier_per_round", "expand_bytes_per_round")
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in self.PER_ROUND}

@@ -82,10 +82,12 @@ typedef struct ps_stats {
   double expand_ms;            /* summed expand-kernel device time (TIME flag)   */
   double host_ms;              /* wall time of the ps_run call                   */
   uint32_t expand_mode;        /* hot kernel of the last window: PS_MODE_*       */
-  uint32_t reserved;
+  uint32_t flood_rounds;       /* PS_MODE_FLOOD: leading rounds of the last
+                                  window run by k_flood (the rest: k_pull)      */
   uint64_t deliveries_per_round[PS_MAX_ROUNDS];
   float expand_ms_per_round[PS_MAX_ROUNDS];   /* TIME flag, summed over windows  */
   uint32_t frontier_per_round[PS_MAX_ROUNDS]; /* expanded entries per round      */
+  uint64_t expand_bytes_per_round[PS_MAX_ROUNDS]; /* algorithmic bytes per round */
 } ps_stats;
 
 typedef struct ps_engine ps_engine;

@@ -49,7 +49,7 @@ def test_code_object_is_gfx950(lib):
 
 def test_struct_layouts(lib):
     assert ctypes.sizeof(PE.Config) == 40
-    assert ctypes.sizeof(PE.Stats) == 9 * 8 + 3 * 8 + 8 + PE.MAX_ROUNDS * 16
+    assert ctypes.sizeof(PE.Stats) == 9 * 8 + 3 * 8 + 8 + PE.MAX_ROUNDS * 24
     src = open(HEADER).read()
     assert f"#define PS_MAX_ROUNDS {PE.MAX_ROUNDS}" in src
     for name, val in [("PS_F_RECORD_HOPS", PE.F_RECORD_HOPS), ("PS_F_TIME_KERNELS", PE.F_TIME_KERNELS)]:

@@ -36,12 +36,16 @@ def random_tree(rng, n, root, fan):
     return parent
 
 
-def run_mode(monkeypatch, flood, n, topics, live, msg_topics, record=True, starts=None, words=None):
+def run_mode(monkeypatch, flood, n, topics, live, msg_topics, record=True, starts=None, words=None, top=None):
+    """One window; `top` (PSAMD_FLOOD_TOP_BYTES): k_flood runs the leading
+    rounds writing at most that many row bytes, k_pull the rest (default:
+    32 MB, every round of these small trees)."""
     monkeypatch.setenv("PSAMD_FLOOD", "1" if flood else "0")
-    if words is None:
-        monkeypatch.delenv("PSAMD_FLOOD_WORDS", raising=False)
-    else:
-        monkeypatch.setenv("PSAMD_FLOOD_WORDS", str(words))
+    for var, val in (("PSAMD_FLOOD_WORDS", words), ("PSAMD_FLOOD_TOP_BYTES", top)):
+        if val is None:
+            monkeypatch.delenv(var, raising=False)
+        else:
+            monkeypatch.setenv(var, str(val))
     with PE.Engine(n, len(topics), record_hops=record) as eng:
         for t, (root, parent) in enumerate(topics):
             eng.set_tree(t, root, parent)
@@ -49,6 +53,13 @@ def run_mode(monkeypatch, flood, n, topics, live, msg_topics, record=True, start
         first = eng.publish(msg_topics, starts)
         st = eng.run()
         assert st.expand_mode == (PE.MODE_FLOOD if flood else PE.MODE_LEVEL_PULL)
+        if flood:
+            assert 1 <= st.flood_rounds <= st.rounds
+            if top is None:
+                assert st.flood_rounds == st.rounds and st.expand_launches == 1
+            elif st.rounds < PE.MAX_ROUNDS:
+                assert st.expand_launches == 1 + sum(
+                    1 for q in range(st.flood_rounds + 1, st.rounds + 1) if st.expand_bytes_per_round[q])
         hops = [eng.hops(first + m) for m in range(len(msg_topics))] if record else None
         digest = eng.seen_digest()
     return st, hops, digest
@@ -86,9 +97,10 @@ def test_flood_parity(monkeypatch, seed):
     exp = oracle_hops(topics, live)
     total = sum(int((exp[t] != 0xFF).sum()) * int((msg_topics == t).sum()) for t in exp)
     ref = None
-    # small tasks (64 words) force many tasks and cross-task waits per level
-    for flood, words in ((False, None), (True, None), (True, 64)):
-        st, hops, digest = run_mode(monkeypatch, flood, n, topics, live, msg_topics, words=words)
+    # small tasks (64 words) force many tasks and cross-task waits per level;
+    # top=2048: k_flood for the first rounds only, k_pull launches after it
+    for flood, words, top in ((False, None, None), (True, None, None), (True, 64, None), (True, None, 2048)):
+        st, hops, digest = run_mode(monkeypatch, flood, n, topics, live, msg_topics, words=words, top=top)
         assert st.deliveries == total, (flood, words, st.deliveries, total)
         assert st.duplicates == 0
         for m, t in enumerate(msg_topics):
@@ -122,9 +134,11 @@ def test_flood_production_instance(monkeypatch, seed):
     counts = [64 * int(rng.integers(0, 9)) + int(rng.integers(1, 65)) for _ in range(nt)]
     msg_topics = rng.permutation(np.repeat(np.arange(nt), counts)).astype(np.uint32)
     outs = []
-    for flood, record, words in ((False, True, None), (True, True, None), (True, False, None),
-                                 (True, False, 128), (False, False, None)):
-        st, _, digest = run_mode(monkeypatch, flood, n, topics, live, msg_topics, record=record, words=words)
+    for flood, record, words, top in ((False, True, None, None), (True, True, None, None),
+                                      (True, False, None, None), (True, False, 128, None),
+                                      (True, False, None, 4096), (False, False, None, None)):
+        st, _, digest = run_mode(monkeypatch, flood, n, topics, live, msg_topics, record=record, words=words,
+                                 top=top)
         d = st.as_dict()
         outs.append((st.deliveries, st.duplicates, d["deliveries_per_round"], d["frontier_per_round"], digest))
     assert all(o == outs[0] for o in outs), (counts, outs)
@@ -142,10 +156,32 @@ def test_flood_topics_with_different_start_rounds(monkeypatch):
     msg_topics = rng.integers(0, 3, size=500).astype(np.uint32)
     starts = np.array([0, 3, 6], dtype=np.uint32)[msg_topics]
     exp = oracle_hops(topics, live)
-    for flood in (True, False):
-        st, hops, _ = run_mode(monkeypatch, flood, n, topics, live, msg_topics, starts=starts)
+    # top = round 1's row bytes: k_flood for the leading rounds that write no
+    # more than that; the later topics start inside the k_pull launches, from
+    # roots k_flood's launch seeded
+    per_round = {}
+    for t, (root, parent) in enumerate(topics):
+        w = -(-int((msg_topics == t).sum()) // 64)
+        depth = np.zeros(n, dtype=np.int64)
+        for v in range(n):  # depth by walking up (n is small)
+            d, u = 0, v
+            while u != root:
+                u, d = int(parent[u]), d + 1
+            depth[v] = d
+        for d, c in zip(*np.unique(depth[depth > 0], return_counts=True)):
+            q = int(d) + int(starts[msg_topics == t][0])
+            per_round[q] = per_round.get(q, 0) + int(c) * w * 8
+    top1 = per_round[1]
+    expect_fr = 0
+    while per_round.get(expect_fr + 1, 0) <= top1 and expect_fr < max(per_round):
+        expect_fr += 1
+    assert expect_fr < 6  # topic 2 (start 6) begins inside the k_pull launches
+    for flood, top in ((True, None), (True, top1), (False, None)):
+        st, hops, _ = run_mode(monkeypatch, flood, n, topics, live, msg_topics, starts=starts, top=top)
+        if top is not None:
+            assert st.flood_rounds == expect_fr
         for m, t in enumerate(msg_topics):
-            assert np.array_equal(hops[m], exp[int(t)]), (flood, m)
+            assert np.array_equal(hops[m], exp[int(t)]), (flood, top, m)
         assert st.deliveries == sum(int((exp[int(t)] != 0xFF).sum()) for t in msg_topics)
 
 

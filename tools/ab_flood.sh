@@ -15,7 +15,8 @@ for envs in "$@"; do
 import json,sys
 d=json.loads(open('$out/v$i.json').read().strip().splitlines()[-1])
 r=d['roofline']
-print(f\"  value {d['value']:.3e}  ms/step {d['ms_per_step']:.3f}  {r['kernel']} {r['avg_launch_us']:.1f} us  frac {r['frac']:.3f}\")
+ks='  '.join(f\"{k}: {v['launches']}x{v['avg_launch_us']:.1f} us frac {v['frac']:.3f}\" for k, v in r.get('kernels', {}).items())
+print(f\"  value {d['value']:.3e}  ms/step {d['ms_per_step']:.3f}  {r['kernel']} {r['avg_launch_us']:.1f} us  frac {r['frac']:.3f}  flood_rounds {d['last_step'].get('flood_rounds')}  [{ks}]\")
 " >> "$out/summary.txt"
 done
 cat "$out/summary.txt"
