@@ -296,34 +296,51 @@ def bench_cfg5(args):
 
 
 def general_path(eng, wl, deliv_expected, steps: int, warmup: int = 1, max_start: int = 7):
-    """The general path (compaction mode): the same workload published with
-    staggered start rounds, uniform over 0..max_start -- paced publishing as
-    the reference's tests do it (pubsub_test.go:101-131) -- so every message
-    enters its root in its own round and the rounds run k_expand over a
-    compacted frontier with the seen test-and-set (client.go:103-131).  On a
-    tree every message still reaches every subscriber: the same deliveries."""
+    """The general path: the same workload published with staggered start
+    rounds, uniform over 0..max_start -- paced publishing as the reference's
+    tests do it (pubsub_test.go:101-131).  Level mode runs each topic's
+    window as start groups (one word block per start round, k_pull per
+    round); the same steps forced through the compaction path (PS_F_COMPACT:
+    k_expand over a compacted frontier with the seen test-and-set,
+    client.go:103-131) are timed beside it.  On a tree every message still
+    reaches every subscriber: the same deliveries."""
     starts = (WL.stream(wl.seed ^ 0x57A6, np.arange(wl.n_msgs)) % np.uint64(max_start + 1)).astype(np.uint32)
 
     def step():
         eng.publish(wl.msg_topics, starts)
         return eng.run()
 
-    for _ in range(warmup):
-        st = step()
-        assert st.deliveries == deliv_expected, (st.deliveries, deliv_expected)
-        assert st.expand_mode == PE.MODE_COMPACT
-    t0 = time.perf_counter()
-    tot = sum(step().deliveries for _ in range(steps))
-    wall = time.perf_counter() - t0
-    assert tot == deliv_expected * steps
-    per, st = instrumented(eng, step, 2)
-    roof = roofline_of(per)
-    roof["expand_ms_per_step"] = sum(v[1] for v in per.values()) / 2
-    return {"workload": f"{wl.name} with start rounds uniform over 0..{max_start} (paced publishing): "
-                        "compaction mode, k_expand + frontier compaction every round",
-            "value": tot / wall, "unit": "deliveries/s", "steps": steps, "ms_per_step": wall * 1e3 / steps,
-            "rounds": st.rounds, "deliveries_per_step": deliv_expected,
-            "roofline": roof}
+    def leg(mode, n_steps):
+        for _ in range(warmup):
+            st = step()
+            assert st.deliveries == deliv_expected, (st.deliveries, deliv_expected)
+            assert st.expand_mode == mode, (st.expand_mode, mode)
+        t0 = time.perf_counter()
+        tot = sum(step().deliveries for _ in range(n_steps))
+        wall = time.perf_counter() - t0
+        assert tot == deliv_expected * n_steps
+        per, st = instrumented(eng, step, 2)
+        roof = roofline_of(per)
+        roof["device_ms_per_step"] = sum(v[1] for v in per.values()) / 2
+        d = st.as_dict()
+        return {"value": tot / wall, "unit": "deliveries/s", "steps": n_steps, "ms_per_step": wall * 1e3 / n_steps,
+                "rounds": st.rounds, "roofline": roof,
+                "expand_us_per_round": [round(x * 1e3, 1) for x in d["expand_ms_per_round"]],
+                "mbytes_per_round": [round(x / 1e6, 1) for x in d["expand_bytes_per_round"]]}
+
+    flags = eng.flags
+    out = leg(PE.MODE_LEVEL_PULL, steps)
+    out["workload"] = (f"{wl.name} with start rounds uniform over 0..{max_start} (paced publishing): "
+                       "start groups, one k_pull launch per round")
+    out["deliveries_per_step"] = deliv_expected
+    eng.set_flags(flags | PE.F_COMPACT)
+    try:
+        comp = leg(PE.MODE_COMPACT, max(1, steps // 2))
+    finally:
+        eng.set_flags(flags)
+    comp["workload"] = "the same steps through the compaction path (PS_F_COMPACT): k_expand + frontier compaction"
+    out["compaction"] = comp
+    return out
 
 
 def main():

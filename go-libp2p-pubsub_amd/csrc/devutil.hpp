@@ -88,11 +88,6 @@ __device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off,
   const u32x4 x = {v.x, v.y, v.z, v.w};
   __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, kAuxSC1);
 }
-template <int kAux>
-__device__ __forceinline__ void st16_aux(__amdgpu_buffer_rsrc_t r, uint32_t off, const uint4& v) {
-  const u32x4 x = {v.x, v.y, v.z, v.w};
-  __builtin_amdgcn_raw_buffer_store_b128(x, r, off, 0, kAux);
-}
 __device__ __forceinline__ void st8_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off, uint64_t v) {
   const u32x2 x = {static_cast<uint32_t>(v), static_cast<uint32_t>(v >> 32)};
   __builtin_amdgcn_raw_buffer_store_b64(x, r, off, 0, kAuxSC1);

@@ -108,6 +108,23 @@ struct WinSlice {
   uint32_t n = 0;
 };
 
+// One start round of a topic's window and its word block [w0, w0 + wn) of
+// every row: a tree node at level d receives the block in round start + d.
+// A topic whose window messages share one start round has one group, the
+// whole row.
+struct StartGroup {
+  uint32_t start, w0, wn;
+};
+
+// Word offset of virtual word w of row u (relative to the topic's first
+// node): node-major rows, or a kTopicGroups topic's group-major blocks.
+uint64_t phys_word(const TopicDev& d, const std::vector<StartGroup>& G, uint64_t u, uint32_t w) {
+  if (!(d.flags & kTopicGroups)) return d.wbase + u * d.W + w;
+  for (const StartGroup& g : G)
+    if (w < g.w0 + g.wn) return d.wbase + static_cast<uint64_t>(d.n_nodes) * g.w0 + u * g.wn + (w - g.w0);
+  return d.wbase;  // (w < W always)
+}
+
 uint32_t ceil_div(uint64_t a, uint64_t b) { return static_cast<uint32_t>((a + b - 1) / b); }
 
 }  // namespace
@@ -173,7 +190,7 @@ struct ps_engine {
 
   DevBuf d_row_ptr, d_col, d_node_topic, d_node_flags, d_node_peer, d_node_parent;
   DevBuf d_seen, d_arr0, d_arr1, d_hop, d_flags, d_blk, d_gen, d_frontier, d_nfront, d_wgcount,
-      d_partials, d_stats, d_topics, d_seeds, d_digest;
+      d_partials, d_stats, d_topics, d_seeds, d_digest, d_groups;
   uint32_t gen_cur = 0;  // window generation stamped into d_gen (1..255)
   DevBuf d_remote_fed, d_send, d_recv, d_apply_stats;
   // multi-GPU level mode: ghost parents
@@ -214,6 +231,10 @@ struct ps_engine {
   std::vector<uint32_t> run_topic_off;  // topic -> first position in run_sorted
   std::vector<uint32_t> run_rank;       // message -> position within its topic
   std::vector<uint32_t> last_lo, last_cnt;  // topic -> last window's rank range
+  // topic -> the last window's row bit of each window message (empty: bit li
+  // = the message's window slot; else the start-group layout, StartGroup)
+  std::vector<std::vector<uint32_t>> last_pos;
+  std::vector<std::vector<StartGroup>> last_groups;  // topic -> the last window's start groups
   std::vector<TopicDev> last_topics;
   bool have_window = false;
   std::map<uint32_t, std::vector<uint32_t>> peer_node;  // topic -> peer -> node (ps_read_peer_messages)
@@ -981,13 +1002,16 @@ int upload_graph(ps_engine* e) {
 // chunks of at most kPullMaxKids nodes and about kPullWords words, one wave
 // each.  Cached: rebuilt only when the node space, the flags or the start
 // rounds change.
-int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab, const std::vector<uint32_t>& tstart,
-                      uint32_t rounds) {
+int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
+                      const std::vector<std::vector<StartGroup>>& groups, uint32_t rounds) {
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
   std::vector<uint64_t> key{e->graph_epoch, e->flags_epoch, rounds};
   for (uint32_t t = 0; t < nt; ++t) {
-    key.push_back(tab[t].W ? tstart[t] : ~0ull);
+    key.push_back(tab[t].W ? groups[t].size() : ~0ull);
     key.push_back(tab[t].W);
+    key.push_back(tab[t].wbase << 1 | ((tab[t].flags & kTopicGroups) ? 1 : 0));
+    if (tab[t].W)
+      for (const StartGroup& g : groups[t]) key.push_back(static_cast<uint64_t>(g.start) << 32 | g.w0);
   }
   if (key == e->pull_key) return PS_OK;
   e->pull_key.clear();
@@ -1003,21 +1027,29 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab, const std:
     off[q] = static_cast<uint32_t>(C.size());
     for (uint32_t t = 0; t < nt; ++t) {
       const TopicHost& T = e->topics[t];
-      const uint32_t W = tab[t].W;
-      if (W == 0 || q < tstart[t] + 1) continue;
-      const uint32_t d = q - tstart[t];  // level of the nodes written this round
-      if (d + 1 >= T.level_off.size()) continue;
-      const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
-      const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, kPullWords / W));
-      e->pull_bytes[q] += static_cast<uint64_t>(hi - lo) * W * 8;
-      for (uint32_t u = lo; u < hi; u += per) {
-        PullChunk c{};
-        c.node_begin = T.nbase + u;
-        c.node_end = T.nbase + std::min(u + per, hi);
-        c.topic = t;
-        c.p_lo = gpu ? kNone : e->node_parent[c.node_begin];
-        c.p_hi = gpu ? kNone : e->node_parent[c.node_end - 1];
-        C.push_back(c);
+      if (tab[t].W == 0) continue;
+      for (const StartGroup& g : groups[t]) {
+        if (q < g.start + 1) continue;
+        const uint32_t d = q - g.start;  // level of the nodes whose block g is written this round
+        if (d + 1 >= T.level_off.size()) continue;
+        const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
+        const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, kPullWords / g.wn));
+        e->pull_bytes[q] += static_cast<uint64_t>(hi - lo) * g.wn * 8;
+        for (uint32_t u = lo; u < hi; u += per) {
+          PullChunk c{};
+          c.node_begin = T.nbase + u;
+          c.node_end = T.nbase + std::min(u + per, hi);
+          c.topic = t;
+          c.p_lo = gpu ? kNone : e->node_parent[c.node_begin];
+          c.p_hi = gpu ? kNone : e->node_parent[c.node_end - 1];
+          // the block rows: group-major blocks, or whole rows
+          const bool gm = (tab[t].flags & kTopicGroups) != 0;
+          const uint64_t row0 = tab[t].wbase + (gm ? static_cast<uint64_t>(tab[t].n_nodes) * g.w0 : 0);
+          c.W = gm ? g.wn : tab[t].W;
+          c.row0_lo = static_cast<uint32_t>(row0);
+          c.row0_hi = static_cast<uint32_t>(row0 >> 32);
+          C.push_back(c);
+        }
       }
     }
   }
@@ -1422,6 +1454,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   uint32_t max_depth = 0, max_start = 0;
   bool need_direct = world > 1;
   std::vector<uint32_t> tstart(std::max<uint32_t>(nt, 1), 0);  // single-start topics
+  std::vector<std::vector<StartGroup>> groups(std::max<uint32_t>(nt, 1));
+  std::vector<std::vector<uint32_t>> pos(std::max<uint32_t>(nt, 1));  // window slot -> row bit
   for (uint32_t t = 0; t < nt; ++t) {
     const TopicHost& T = e->topics[t];
     TopicDev& d = tab[t];
@@ -1432,22 +1466,58 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     if (!T.exists || win[t].n == 0) continue;
     // every rank plans the same rounds: global depth, global start rounds
     max_depth = std::max(max_depth, T.depth);
-    bool one_start = true;
+    uint32_t s_lo = ~0u, s_hi = 0;
     if (!e->run_zero_start)  // else: every message of the run starts in round 0
       for (uint32_t li = 0; li < win[t].n; ++li) {
-        max_start = std::max(max_start, msgs[win[t].idx[li]].start);
-        one_start &= msgs[win[t].idx[li]].start == msgs[win[t].idx[0]].start;
+        const uint32_t s0 = msgs[win[t].idx[li]].start;
+        s_lo = std::min(s_lo, s0);
+        s_hi = std::max(s_hi, s0);
       }
+    if (e->run_zero_start) s_lo = s_hi = 0;
+    max_start = std::max(max_start, s_hi);
+    const bool one_start = s_lo == s_hi;
     // a tree topic whose window messages share one start round: every node
     // receives once, so arrival rows are its seen rows (kTopicSingleStart)
     if (one_start && !T.mesh) d.flags |= kTopicSingleStart;
     tstart[t] = msgs[win[t].idx[0]].start;
     if (T.n_nodes == 0) continue;
-    d.W = ceil_div(win[t].n, 64);
-    d.w_msgs = d.W;
-    // rows of >= 64 words are padded to an even length so that every row
-    // starts 16-B aligned (the expand kernel stores them as dwordx4)
-    if (d.W >= 64) d.W += d.W & 1u;
+    if (one_start || T.mesh) {
+      d.W = ceil_div(win[t].n, 64);
+      d.w_msgs = d.W;
+      // rows of >= 64 words are padded to an even length so that every row
+      // starts 16-B aligned (the expand kernel stores them as dwordx4)
+      if (d.W >= 64) d.W += d.W & 1u;
+      groups[t].push_back(StartGroup{s_lo, 0, d.W});
+    } else {
+      // Start groups (a tree's messages entering at different rounds): the
+      // (virtual) row holds one word block per start round, in start order,
+      // each of an even number of words: a node at level d receives block s
+      // -- and only block s -- in round s + d.  Slot li's bit is its rank
+      // within its group from the block's first bit (counting sort by start,
+      // window order kept inside a group).  Level mode stores the blocks
+      // group-major (kTopicGroups, set below).
+      std::vector<uint32_t> cnt(s_hi - s_lo + 2, 0);
+      for (uint32_t li = 0; li < win[t].n; ++li) cnt[msgs[win[t].idx[li]].start - s_lo + 1]++;
+      std::vector<uint32_t> wfirst(s_hi - s_lo + 1, 0);
+      uint32_t w = 0;
+      for (uint32_t k = 0; k <= s_hi - s_lo; ++k) {
+        const uint32_t n_k = cnt[k + 1];
+        if (!n_k) continue;
+        const uint32_t wn = (ceil_div(n_k, 64) + 1) & ~1u;
+        wfirst[k] = w;
+        groups[t].push_back(StartGroup{s_lo + k, w, wn});
+        w += wn;
+      }
+      d.W = w;
+      d.w_msgs = w;  // every block's words (padding words stay zero)
+      auto& P = pos[t];
+      P.resize(win[t].n);
+      std::vector<uint32_t> fill(s_hi - s_lo + 1, 0);
+      for (uint32_t li = 0; li < win[t].n; ++li) {
+        const uint32_t k = msgs[win[t].idx[li]].start - s_lo;
+        P[li] = wfirst[k] * 64 + fill[k]++;
+      }
+    }
     wtot = (wtot + 15) & ~15ull;  // topic blocks start on a 128-B line
     d.wbase = wtot;
     wtot += static_cast<uint64_t>(T.n_nodes) * d.W;
@@ -1478,6 +1548,35 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
           "alloc apply stats");
   HIP_TRY(e->d_topics.ensure(tab.size() * sizeof(TopicDev)), "alloc topics");
   HIP_TRY(e->d_nfront.ensure(4), "alloc n_front");
+  const uint32_t planned0 = max_depth + max_start + 1;
+  // level mode: every active topic a tree.  One rank: the leading rounds
+  // whose rows are small (latency bound: a launch each would cost more than
+  // their bytes) run as ONE persistent k_flood launch, the rest one k_pull
+  // launch per round (bandwidth bound); several ranks: one k_pull launch per
+  // round (the frontier exchange separates the rounds).  PSAMD_FLOOD=0
+  // selects the per-round launches on one rank too.  A window with start
+  // groups (a tree's messages entering at several rounds) runs level mode on
+  // one rank, one k_pull launch per round over every group's level of that
+  // round, its blocks stored group-major; PS_F_COMPACT sends every window
+  // through the compaction path.
+  bool multi = false;
+  for (uint32_t t = 0; t < nt; ++t) multi |= tab[t].W && groups[t].size() > 1;
+  const bool level =
+      !(e->cfg.flags & PS_F_COMPACT) && !any_mesh && planned0 + 1 < round_cap && !(multi && world > 1);
+  std::vector<GroupDev> gtab;  // start groups of the group-major topics
+  for (uint32_t t = 0; t < nt; ++t) {
+    TopicDev& d = tab[t];
+    d.root_words = d.W;
+    if (!level || !d.W || groups[t].size() < 2) continue;
+    d.flags |= kTopicGroups;
+    d.group_lo = static_cast<uint32_t>(gtab.size());
+    d.group_n = static_cast<uint32_t>(groups[t].size());
+    d.root_words = groups[t][0].wn;
+    for (const StartGroup& g : groups[t]) gtab.push_back(GroupDev{g.w0, g.wn});
+  }
+  HIP_TRY(e->d_groups.ensure(std::max<size_t>(gtab.size(), 1) * sizeof(GroupDev)), "alloc groups");
+  // word offset of virtual word w of node u's row (u relative to the topic)
+  auto phys = [&](uint32_t t, uint64_t u, uint32_t w) { return phys_word(tab[t], groups[t], u, w); };
 
   // root injections (owned roots only), grouped by round: mask[t][round][word]
   std::vector<std::vector<uint64_t>> inj(nt);
@@ -1489,8 +1588,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       for (uint32_t w = 0; w < win[t].n / 64; ++w) inj[t][w] = ~0ull;
       if (win[t].n % 64) inj[t][win[t].n / 64] = (1ull << (win[t].n % 64)) - 1;
     } else {
-      for (uint32_t li = 0; li < win[t].n; ++li)
-        inj[t][static_cast<size_t>(msgs[win[t].idx[li]].start) * d.W + (li >> 6)] |= 1ull << (li & 63);
+      for (uint32_t li = 0; li < win[t].n; ++li) {
+        const uint32_t b = pos[t].empty() ? li : pos[t][li];
+        inj[t][static_cast<size_t>(msgs[win[t].idx[li]].start) * d.W + (b >> 6)] |= 1ull << (b & 63);
+      }
     }
   }
   std::vector<SeedDev> seeds;
@@ -1500,9 +1601,18 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       TopicDev& d = tab[t];
       if (r == 0) d.seed_lo = static_cast<uint32_t>(seeds.size());
       if (inj[t].empty()) continue;
-      for (uint32_t w = 0; w < d.W; ++w) {
-        const uint64_t m = inj[t][static_cast<size_t>(r) * d.W + w];
-        if (m) seeds.push_back(SeedDev{d.wbase + w, m, d.nbase, 0});  // root = node 0
+      if (d.flags & kTopicGroups) {
+        // group-major: the root's block of the group starting this round is
+        // set whole (k_window_init zeroes block 0 only)
+        for (const StartGroup& g : groups[t])
+          if (g.start == r)
+            for (uint32_t w = g.w0; w < g.w0 + g.wn; ++w)
+              seeds.push_back(SeedDev{phys(t, 0, w), inj[t][static_cast<size_t>(r) * d.W + w], d.nbase, 1});
+      } else {
+        for (uint32_t w = 0; w < d.W; ++w) {
+          const uint64_t m = inj[t][static_cast<size_t>(r) * d.W + w];
+          if (m) seeds.push_back(SeedDev{d.wbase + w, m, d.nbase, 0});  // root = node 0
+        }
       }
       if (r == 0) d.seed_n = static_cast<uint32_t>(seeds.size()) - d.seed_lo;
     }
@@ -1539,24 +1649,13 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     const uint64_t blocks = (bound + 3) / 4;  // ~1 entry per wave at least
     return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(e->expand_grid, blocks)));
   };
-  const uint32_t planned0 = max_depth + max_start + 1;
-  // level mode: every active topic a tree whose window messages share one
-  // start round.  One rank: the leading rounds whose rows are small (latency
-  // bound: a launch each would cost more than their bytes) run as ONE
-  // persistent k_flood launch, the rest one k_pull launch per round
-  // (bandwidth bound); several ranks: one k_pull launch per round (the
-  // frontier exchange separates the rounds).  PSAMD_FLOOD=0 selects the
-  // per-round launches on one rank too.
-  bool level = !any_mesh && planned0 + 1 < round_cap;
-  for (uint32_t t = 0; t < nt && level; ++t)
-    if (tab[t].W && !(tab[t].flags & kTopicSingleStart)) level = false;
-  const bool flood_ok = level && world == 1 && e->flood_on && !e->flood_broken && e->flood_grid > 0 &&
-                        e->n_nodes < 0x80000000u;  // k_flood marks node ids with bit 31
+  const bool flood_ok = level && !multi && world == 1 && e->flood_on && !e->flood_broken &&
+                        e->flood_grid > 0 && e->n_nodes < 0x80000000u;  // k_flood marks node ids with bit 31
   uint32_t flood_rounds = 0;    // rounds 1..flood_rounds: k_flood
   std::vector<uint32_t> lgrid;  // per-round launches: grid of every round
   uint32_t n_slots = 0;         // level mode: partial counter slots of the window
   if (level) {
-    int rc2 = build_pull_chunks(e, tab, tstart, planned0);
+    int rc2 = build_pull_chunks(e, tab, groups, planned0);
     if (!rc2 && flood_ok) {
       while (flood_rounds < planned0 && e->pull_bytes[flood_rounds + 1] <= e->flood_top_bytes) ++flood_rounds;
       if (flood_rounds) rc2 = build_flood_tasks(e, tab, tstart, flood_rounds);
@@ -1603,7 +1702,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     for (uint32_t t = 0; t < nt; ++t) {
       const TopicHost& T = e->topics[t];
       if (starts_of[t].empty()) continue;
-      const uint64_t Wt = ceil_div(win[t].n, 64) + ((ceil_div(win[t].n, 64) >= 64) ? (ceil_div(win[t].n, 64) & 1u) : 0u);
+      const uint64_t Wt = tab[t].W;
       for (const auto& c : T.cross)
         for (uint32_t s0 = 0; s0 <= max_start; ++s0) {
           const uint32_t r = c.level + 1 + s0;
@@ -1632,13 +1731,14 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // mode without meshes; the eager seen clear below would erase the seeds)
   const bool fold = level && !any_mesh && !(e->cfg.flags & PS_F_NO_LAZY_SEEN);
   WindowStart ws{};
-  const void* staged[3] = {nullptr, nullptr, nullptr};
+  const void* staged[4] = {nullptr, nullptr, nullptr, nullptr};
   {
-    const Upload ups[3] = {
+    const Upload ups[4] = {
         {e->d_topics.p, tab.data(), tab.size() * sizeof(TopicDev)},
         {e->d_seeds.p, seeds.data(), seeds.size() * sizeof(SeedDev)},
-        {e->d_woff.p, e->desc_host.data(), level ? e->desc_host.size() * 4 : 0}};
-    const int rcu = stage_uploads(e, ups, 3, s, fold ? &ws.copy : nullptr, staged);
+        {e->d_woff.p, e->desc_host.data(), level ? e->desc_host.size() * 4 : 0},
+        {e->d_groups.p, gtab.data(), gtab.size() * sizeof(GroupDev)}};
+    const int rcu = stage_uploads(e, ups, 4, s, fold ? &ws.copy : nullptr, staged);
     if (rcu) return rcu;
   }
   if (fold) {
@@ -1784,13 +1884,15 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     if (!partials_done)  // blocks / waves add into shared partial slots
       HIP_TRY(hipMemsetAsync(partials, 0, static_cast<size_t>(n_slots) * kNumCtr * 8, s), "clear partials");
     if (!seeds0_done) HIP_TRY(seed_round(0, arr[0]), "seed");
+    // k_flood, or start groups: every root row is seeded up front into arr[0]
+    // (and seen: k_flood reads parent rows from there), the blocks of later
+    // start rounds included -- a block is read only in its own rounds
+    const bool upfront = flood || multi;
+    if (upfront && max_start > 0)
+      HIP_TRY(launch_seed(e->d_seeds.as<SeedDev>(), seed_off[1], seed_off[max_start + 1], arr[0], a.seen, nullptr,
+                          nullptr, s),
+              "seed");
     if (flood) {
-      // topics starting after round 0: their roots' rows are seeded up front
-      // (k_flood reads every parent row, the roots' too, from `seen`)
-      if (max_start > 0)
-        HIP_TRY(launch_seed(e->d_seeds.as<SeedDev>(), seed_off[1], seed_off[max_start + 1], arr[0], a.seen,
-                            nullptr, nullptr, s),
-                "seed");
       FloodArgs fa{};
       fa.tasks = e->d_flood_tasks.as<FloodTask>();
       fa.node_parent = e->d_node_parent.as<uint32_t>();
@@ -1807,8 +1909,6 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       fa.epoch = e->flood_epoch;
       fa.gen_cur = a.gen_cur;
       fa.spin_ticks = 200000000u;  // 2 s of s_memrealtime (100 MHz)
-      if (const char* v = std::getenv("PSAMD_FLOOD_STORE")) fa.store_mode = static_cast<uint32_t>(std::atoi(v));
-      if (const char* v = std::getenv("PSAMD_FLOOD_DB")) fa.db = static_cast<uint32_t>(std::atoi(v));
       const uint32_t flood_blocks = std::min<uint32_t>(e->flood_grid, ceil_div(fa.n_tasks, kBlock / 64));
       if (e->flood_profile) {
         HIP_TRY(e->d_flood_prof.ensure(static_cast<size_t>(flood_blocks) * 4 * kFloodProf * 8), "alloc flood profile");
@@ -1824,8 +1924,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     }
     {
       for (r = flood_rounds + 1; r <= planned0; ++r) {
-        // (after k_flood every root is seeded in arr[0] already)
-        a.a_cur = flood ? arr[0] : arr[(r - 1) & 1];
+        a.a_cur = upfront ? arr[0] : arr[(r - 1) & 1];
         a.a_next = arr[r & 1];
         // multi-GPU: this round's ghost parents (rows written last round, or
         // seeded roots) to the ranks owning their children, then the exchange
@@ -1867,7 +1966,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
                   "pull");
           HIP_TRY(time_mark(false), "event");
         }
-        if (!flood) HIP_TRY(seed_round(r, a.a_next), "seed");
+        if (!upfront) HIP_TRY(seed_round(r, a.a_next), "seed");
       }
     }
     r = planned0;
@@ -1962,6 +2061,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       e->last_cnt[t] = tab[t].W ? win[t].n : 0;
       e->last_lo[t] = win[t].n ? e->run_rank[win[t].idx[0]] : 0;
     }
+    e->last_pos.swap(pos);
+    e->last_groups.swap(groups);
     e->have_window = true;
     if (e->host_timing) {
       auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -2024,9 +2125,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       for (uint32_t li = 0; li < win[t].n; ++li) {
         const uint32_t mi = win[t].idx[li];
         const uint32_t s0 = msgs[mi].start;
+        const uint32_t b = pos[t].empty() ? li : pos[t][li];
         uint8_t* row = e->hops.data() + static_cast<size_t>(mi) * np;
         for (uint32_t u = 0; u < d.n_nodes; ++u) {
-          const uint16_t v = hr[(d.wbase + static_cast<uint64_t>(u) * d.W + (li >> 6)) * 64 + (li & 63)];
+          const uint16_t v = hr[phys(t, u, b >> 6) * 64 + (b & 63)];
           // hop = round - start round, saturated at 254 (0xFF: not delivered)
           if (v != kHopRecNone) row[e->node_peer[d.nbase + u]] = static_cast<uint8_t>(std::min<uint32_t>(v - s0, 254u));
         }
@@ -2039,6 +2141,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     e->last_cnt[t] = tab[t].W ? win[t].n : 0;
     e->last_lo[t] = win[t].n ? e->run_rank[win[t].idx[0]] : 0;
   }
+  e->last_pos.swap(pos);
+  e->last_groups.swap(groups);
   e->have_window = true;
   return PS_OK;
 }
@@ -2106,8 +2210,6 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
     int bpc = 0;
     if (flood_blocks_per_cu(&bpc) == hipSuccess && bpc > 0)
       e->flood_grid = e->n_cus * std::min<uint32_t>(static_cast<uint32_t>(bpc), kFloodBlocksPerCu);
-    if (const char* v = std::getenv("PSAMD_FLOOD_BPC"))  // EXPERIMENT
-      e->flood_grid = e->n_cus * std::min<uint32_t>(static_cast<uint32_t>(bpc), static_cast<uint32_t>(std::atoi(v)));
   }
   // switches: debug timing, and the modes the parity tests cover
   if (const char* v = std::getenv("PSAMD_HOST_TIMING")) e->host_timing = std::atoi(v) != 0;
@@ -2342,7 +2444,7 @@ int ps_topic_depth(ps_engine* e, uint32_t topic, uint32_t* depth_out, uint32_t* 
 
 int ps_set_flags(ps_engine* e, uint32_t flags) {
   if (!e) return PS_E_INVAL;
-  if (flags & ~(PS_F_RECORD_HOPS | PS_F_TIME_KERNELS | PS_F_NO_LAZY_SEEN))
+  if (flags & ~(PS_F_RECORD_HOPS | PS_F_TIME_KERNELS | PS_F_NO_LAZY_SEEN | PS_F_COMPACT))
     return e->fail(PS_E_INVAL, "unknown flag");
   e->cfg.flags = flags;
   return PS_OK;
@@ -2589,6 +2691,7 @@ int ps_read_delivered(ps_engine* e, uint32_t msg, uint8_t* out) {
   if (rank < e->last_lo[t] || rank >= e->last_lo[t] + e->last_cnt[t])
     return e->fail(PS_E_NOTREADY, "message not in the last window");
   const uint32_t li = rank - e->last_lo[t];
+  const uint32_t b = t < e->last_pos.size() && !e->last_pos[t].empty() ? e->last_pos[t][li] : li;
   const TopicDev& d = e->last_topics[t];
   {
     int rcm = ensure_mirrors(e);
@@ -2596,9 +2699,19 @@ int ps_read_delivered(ps_engine* e, uint32_t msg, uint8_t* out) {
   }
   std::memset(out, 0, e->cfg.n_peers);
   std::vector<uint64_t> col(d.n_nodes);
-  // one word per node: strided copy of this message's word column
-  HIP_TRY(hipMemcpy2DAsync(col.data(), 8, e->d_seen.as<uint64_t>() + d.wbase + (li >> 6),
-                           d.W * 8ull, 8, d.n_nodes, hipMemcpyDeviceToHost, e->stream),
+  // one word per node: strided copy of this message's word column (row
+  // stride W, or its group's block width when group-major)
+  static const std::vector<StartGroup> kNoGroups;
+  const auto& G = t < e->last_groups.size() ? e->last_groups[t] : kNoGroups;
+  uint64_t stride = d.W;
+  if (d.flags & kTopicGroups)
+    for (const StartGroup& g : G)
+      if ((b >> 6) < g.w0 + g.wn) {
+        stride = g.wn;
+        break;
+      }
+  HIP_TRY(hipMemcpy2DAsync(col.data(), 8, e->d_seen.as<uint64_t>() + phys_word(d, G, 0, b >> 6), stride * 8ull, 8,
+                           d.n_nodes, hipMemcpyDeviceToHost, e->stream),
           "read seen");
   std::vector<uint8_t> gen(d.n_nodes);
   HIP_TRY(hipMemcpyAsync(gen.data(), e->d_gen.as<uint8_t>() + d.nbase, d.n_nodes,
@@ -2606,7 +2719,7 @@ int ps_read_delivered(ps_engine* e, uint32_t msg, uint8_t* out) {
           "read generations");
   HIP_TRY(hipStreamSynchronize(e->stream), "sync");
   const bool mesh = (d.flags & kTopicMesh) != 0;
-  const uint64_t bit = 1ull << (li & 63);
+  const uint64_t bit = 1ull << (b & 63);
   for (uint32_t u = 1; u < d.n_nodes; ++u)  // the root is not a recipient
     if ((mesh || gen[u] == e->gen_cur) && (col[u] & bit)) out[e->node_peer[d.nbase + u]] = 1;
   return PS_OK;
@@ -2637,9 +2750,16 @@ int ps_read_peer_messages(ps_engine* e, uint32_t topic, uint32_t peer, uint32_t*
   if (u == kNone) return PS_OK;  // not subscribed (or not owned by this rank)
   std::vector<uint64_t> row(d.W);
   uint8_t g = 0;
-  HIP_TRY(hipMemcpyAsync(row.data(), e->d_seen.as<uint64_t>() + d.wbase + static_cast<uint64_t>(u) * d.W,
-                         d.W * 8ull, hipMemcpyDeviceToHost, e->stream),
-          "read seen row");
+  if (d.flags & kTopicGroups) {  // the row's blocks, one per start group
+    for (const StartGroup& sg : e->last_groups[topic])
+      HIP_TRY(hipMemcpyAsync(row.data() + sg.w0, e->d_seen.as<uint64_t>() + phys_word(d, e->last_groups[topic], u, sg.w0),
+                             sg.wn * 8ull, hipMemcpyDeviceToHost, e->stream),
+              "read seen row");
+  } else {
+    HIP_TRY(hipMemcpyAsync(row.data(), e->d_seen.as<uint64_t>() + d.wbase + static_cast<uint64_t>(u) * d.W,
+                           d.W * 8ull, hipMemcpyDeviceToHost, e->stream),
+            "read seen row");
+  }
   HIP_TRY(hipMemcpyAsync(&g, e->d_gen.as<uint8_t>() + d.nbase + u, 1, hipMemcpyDeviceToHost, e->stream),
           "read generation");
   HIP_TRY(hipStreamSynchronize(e->stream), "sync");
@@ -2653,7 +2773,8 @@ int ps_read_peer_messages(ps_engine* e, uint32_t topic, uint32_t peer, uint32_t*
     const uint32_t r = e->run_rank[i];
     if (r < lo || r >= lo + cnt) continue;
     const uint32_t li = r - lo;
-    if (row[li >> 6] >> (li & 63) & 1ull)
+    const uint32_t b = topic < e->last_pos.size() && !e->last_pos[topic].empty() ? e->last_pos[topic][li] : li;
+    if (row[b >> 6] >> (b & 63) & 1ull)
       got.emplace_back((static_cast<uint64_t>(e->last_msgs[i].start) << 32) | i, e->last_first + i);
   }
   // arrival order: paced messages by entry round, then publish order
@@ -2670,7 +2791,8 @@ int ps_seen_digest(ps_engine* e, uint64_t* digest_out) {
   HIP_TRY(hipMemsetAsync(e->d_digest.p, 0, 8, e->stream), "clear digest");
   HIP_TRY(launch_digest(e->d_seen.as<uint64_t>(), e->d_gen.as<uint8_t>(), e->gen_cur,
                         e->d_node_peer.as<uint32_t>(),
-                        e->d_node_topic.as<uint16_t>(), e->d_topics.as<TopicDev>(), e->n_nodes,
+                        e->d_node_topic.as<uint16_t>(), e->d_topics.as<TopicDev>(), e->d_groups.as<GroupDev>(),
+                        e->n_nodes,
                         e->d_digest.as<uint64_t>(), e->stream),
           "digest");
   HIP_TRY(hipMemcpyAsync(digest_out, e->d_digest.p, 8, hipMemcpyDeviceToHost, e->stream),

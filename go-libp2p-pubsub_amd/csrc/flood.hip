@@ -82,7 +82,7 @@ __device__ __forceinline__ void split_word(uint32_t i, float rw, uint32_t W, int
 // receives.  8 loads in flight per lane, then 8 stores; a skipped node's pair
 // and a lane past the end use an out-of-range offset (load 0, store dropped):
 // no branches, so the compiler counts vmcnt exactly.
-template <bool kRecord, int kAux>
+template <bool kRecord>
 __device__ __forceinline__ void flood_stream_even(const FloodArgs& a, uint64_t* out_row, uint32_t total,
                                                   uint32_t W, __amdgpu_buffer_rsrc_t in, uint32_t pbase,
                                                   const uint32_t* src, uint32_t lane, uint32_t round,
@@ -105,7 +105,7 @@ __device__ __forceinline__ void flood_stream_even(const FloodArgs& a, uint64_t* 
     }
 #pragma unroll
     for (uint32_t u = 0; u < kU; ++u) {
-      st16_aux<kAux>(out, so[u], v[u]);
+      st16_sc1(out, so[u], v[u]);
       const bool own = so[u] != kOutOfRange;
       c.deliv += own ? popc4(v[u]) : 0u;
       c.sw += own ? 2u : 0u;
@@ -117,59 +117,6 @@ __device__ __forceinline__ void flood_stream_even(const FloodArgs& a, uint64_t* 
         }
       }
     }
-  }
-}
-
-// Stream, even W, double-buffered: batch b + 1's loads are issued before batch
-// b's stores, so a wave waits for its loads only -- never for its own store
-// acknowledgements, which retire in the background (the vector-memory
-// counter is in order: waiting for batch b + 1 waits for batch b - 1's
-// stores, two batches back).
-template <bool kRecord, int kAux, uint32_t kU>
-__device__ __forceinline__ void flood_stream_even_db(const FloodArgs& a, uint64_t* out_row, uint32_t total,
-                                                     uint32_t W, __amdgpu_buffer_rsrc_t in, uint32_t pbase,
-                                                     const uint32_t* src, uint32_t lane, uint32_t round,
-                                                     PullCtr& c) {
-  const __amdgpu_buffer_rsrc_t out = rsrc(out_row, total * 8u);
-  const float rw = 1.0f / static_cast<float>(W);
-  auto issue = [&](uint32_t i0, uint4 (&v)[kU], uint32_t (&so)[kU]) {
-#pragma unroll
-    for (uint32_t u = 0; u < kU; ++u) {
-      const uint32_t i = i0 + u * 128 + 2 * lane;
-      int32_t kk, r;
-      split_word(i < total ? i : total - 2, rw, W, kk, r);
-      const uint32_t p = i < total ? src[kk] : kNoneNode;
-      const bool go = p != kNoneNode;
-      v[u] = ld16_sc1(in, go ? ((p - pbase) * W + static_cast<uint32_t>(r)) * 8u : kOutOfRange);
-      so[u] = go ? i * 8u : kOutOfRange;
-    }
-  };
-  auto drain = [&](const uint4 (&v)[kU], const uint32_t (&so)[kU]) {
-#pragma unroll
-    for (uint32_t u = 0; u < kU; ++u) {
-      st16_aux<kAux>(out, so[u], v[u]);
-      const bool own = so[u] != kOutOfRange;
-      c.deliv += own ? popc4(v[u]) : 0u;
-      c.sw += own ? 2u : 0u;
-      if constexpr (kRecord) {
-        if (own) {
-          const uint64_t cw = (out_row - a.seen) + so[u] / 8u;
-          record_word(a.hop_rec, cw, static_cast<uint64_t>(v[u].y) << 32 | v[u].x, round);
-          record_word(a.hop_rec, cw + 1, static_cast<uint64_t>(v[u].w) << 32 | v[u].z, round);
-        }
-      }
-    }
-  };
-  constexpr uint32_t kStep = kU * 128;
-  uint4 va[kU], vb[kU];
-  uint32_t sa[kU], sb[kU];
-  issue(0, va, sa);
-  for (uint32_t i0 = 0; i0 < total; i0 += 2 * kStep) {
-    const bool more = i0 + kStep < total;
-    if (more) issue(i0 + kStep, vb, sb);
-    drain(va, sa);
-    if (i0 + 2 * kStep < total) issue(i0 + 2 * kStep, va, sa);
-    if (more) drain(vb, sb);
   }
 }
 
@@ -279,7 +226,7 @@ __device__ __forceinline__ void flood_flush(const FloodArgs& a, PullCtr& c, uint
   c = PullCtr{};
 }
 
-template <bool kRecord, int kAux, uint32_t kDB = 0>
+template <bool kRecord>
 __global__ __launch_bounds__(kBlock, kFloodBlocksPerCu) void k_flood(FloodArgs a) {
   __shared__ uint32_t src_lds[kBlock / 64][kFloodMaxNodes];
   const uint32_t lane = threadIdx.x & 63;
@@ -397,10 +344,8 @@ __global__ __launch_bounds__(kBlock, kFloodBlocksPerCu) void k_flood(FloodArgs a
       const __amdgpu_buffer_rsrc_t rin = rsrc(prow, static_cast<uint32_t>(span));
       if (W & 1u)
         flood_stream_odd<kRecord>(a, out_row, total, W, rin, T.p_lo, src, lane, T.round, c);
-      else if constexpr (kDB > 0)  // EXPERIMENT
-        flood_stream_even_db<kRecord, kAux, kDB>(a, out_row, total, W, rin, T.p_lo, src, lane, T.round, c);
       else
-        flood_stream_even<kRecord, kAux>(a, out_row, total, W, rin, T.p_lo, src, lane, T.round, c);
+        flood_stream_even<kRecord>(a, out_row, total, W, rin, T.p_lo, src, lane, T.round, c);
     }
     // the node's generation (read by later windows and the readbacks only)
     if (ok) a.gen[T.nb + lane] = static_cast<uint8_t>(cur);
@@ -465,17 +410,9 @@ __global__ __launch_bounds__(kBlock) void k_flood_deps(FloodTask* __restrict__ t
 hipError_t launch_flood(const FloodArgs& a, uint32_t grid, bool record, hipStream_t s) {
   if (a.n_tasks == 0 || grid == 0) return hipSuccess;
   if (record)
-    hipLaunchKernelGGL((k_flood<true, kAuxSC1>), dim3(grid), dim3(kBlock), 0, s, a);
-  else if (a.db == 4)  // EXPERIMENT: double-buffered stream
-    hipLaunchKernelGGL((k_flood<false, kAuxSC1, 4>), dim3(grid), dim3(kBlock), 0, s, a);
-  else if (a.db == 8)
-    hipLaunchKernelGGL((k_flood<false, kAuxSC1, 8>), dim3(grid), dim3(kBlock), 0, s, a);
-  else if (a.store_mode == 1)  // EXPERIMENT: plain even-W row stores
-    hipLaunchKernelGGL((k_flood<false, 0>), dim3(grid), dim3(kBlock), 0, s, a);
-  else if (a.store_mode == 2)  // EXPERIMENT: nt even-W row stores
-    hipLaunchKernelGGL((k_flood<false, 2>), dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((k_flood<true>), dim3(grid), dim3(kBlock), 0, s, a);
   else
-    hipLaunchKernelGGL((k_flood<false, kAuxSC1>), dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((k_flood<false>), dim3(grid), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 
@@ -490,8 +427,8 @@ hipError_t launch_flood_deps(FloodTask* tasks, uint32_t n, const FloodSeg* segs,
 // Resident k_flood blocks per CU (both instances; the smaller bounds the grid).
 hipError_t flood_blocks_per_cu(int* out) {
   int a = 0, b = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_flood<false, kAuxSC1>, kBlock, 0);
-  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_flood<true, kAuxSC1>, kBlock, 0);
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_flood<false>, kBlock, 0);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_flood<true>, kBlock, 0);
   *out = a < b ? a : b;
   return e;
 }

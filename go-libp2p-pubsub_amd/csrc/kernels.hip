@@ -88,7 +88,7 @@ __global__ __launch_bounds__(kBlock) void k_window_init(const TopicDev* __restri
   const TopicDev T = topics[blockIdx.y];
   if (T.W == 0 || T.n_nodes == 0) return;
   const bool mesh = (T.flags & kTopicMesh) != 0;
-  const uint64_t n_words = mesh ? static_cast<uint64_t>(T.n_nodes) * T.W : T.W;
+  const uint64_t n_words = mesh ? static_cast<uint64_t>(T.n_nodes) * T.W : T.root_words;
   if (!mesh && (blockIdx.x != 0 || !(T.flags & kTopicRootLocal))) return;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n_words;
        i += static_cast<uint64_t>(gridDim.x) * kBlock) {
@@ -104,8 +104,8 @@ __global__ __launch_bounds__(kBlock) void k_window_init(const TopicDev* __restri
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < T.seed_n; i += kBlock) {
       const SeedDev sd = ws.seeds[T.seed_lo + i];
-      a0[sd.woff] |= sd.mask;
-      seen[sd.woff] |= sd.mask;
+      a0[sd.woff] = sd.assign ? sd.mask : a0[sd.woff] | sd.mask;
+      seen[sd.woff] = sd.assign ? sd.mask : seen[sd.woff] | sd.mask;
     }
   }
 }
@@ -152,8 +152,8 @@ __global__ __launch_bounds__(kBlock) void k_seed(const SeedDev* __restrict__ see
   const uint32_t i = lo + blockIdx.x * kBlock + threadIdx.x;
   if (i >= hi) return;
   const SeedDev s = seeds[i];
-  arrivals[s.woff] |= s.mask;
-  seen[s.woff] |= s.mask;
+  arrivals[s.woff] = s.assign ? s.mask : arrivals[s.woff] | s.mask;
+  seen[s.woff] = s.assign ? s.mask : seen[s.woff] | s.mask;
   if (next_flag == nullptr) return;  // level mode: the root is scheduled statically
   next_flag[s.node] = 1;
   blk_flag[s.node >> kFlagBlockShift] = 1;
@@ -725,7 +725,8 @@ struct PullVec {
   uint4 v;
 };
 
-// Topic constants of a chunk: row of node u = base + u * W.
+// Chunk constants: row of node u = base + u * W (a start group's block row
+// for kTopicGroups topics).
 struct PullTopic {
   uint64_t base;
   uint32_t W, nbase, root;
@@ -944,9 +945,9 @@ __global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __
     const PullChunk ch = chunks[wave];
     const TopicDev T = a.topics[ch.topic];
     PullTopic P;
-    P.W = T.W;
+    P.W = ch.W;
     P.nbase = T.nbase;
-    P.base = T.wbase - static_cast<uint64_t>(T.nbase) * T.W;
+    P.base = (static_cast<uint64_t>(ch.row0_hi) << 32 | ch.row0_lo) - static_cast<uint64_t>(T.nbase) * ch.W;
     P.root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
     const uint32_t n1 = ch.node_end - ch.node_begin;
     // LDS ops of a wave are processed in order: the table written in phase 1
@@ -1203,6 +1204,7 @@ __global__ __launch_bounds__(kBlock) void k_digest(const uint64_t* __restrict__ 
                                                    const uint32_t* __restrict__ node_peer,
                                                    const uint16_t* __restrict__ node_topic,
                                                    const TopicDev* __restrict__ topics,
+                                                   const GroupDev* __restrict__ groups,
                                                    uint32_t n_nodes, uint64_t* out) {
   uint64_t acc = 0;
   for (uint32_t u = blockIdx.x * kBlock + threadIdx.x; u < n_nodes; u += gridDim.x * kBlock) {
@@ -1210,8 +1212,17 @@ __global__ __launch_bounds__(kBlock) void k_digest(const uint64_t* __restrict__ 
     const TopicDev T = topics[t];
     if (T.W == 0) continue;
     const bool valid = (T.flags & kTopicMesh) || gen[u] == static_cast<uint8_t>(gen_cur);
-    const uint64_t row = T.wbase + static_cast<uint64_t>(u - T.nbase) * T.W;
     const uint64_t key0 = (static_cast<uint64_t>(node_peer[u]) << 32) | (static_cast<uint64_t>(t) << 16);
+    if (T.flags & kTopicGroups) {  // virtual word w of the row from its group's block
+      for (uint32_t g = 0; g < T.group_n; ++g) {
+        const GroupDev G = groups[T.group_lo + g];
+        const uint64_t blk = T.wbase + static_cast<uint64_t>(T.n_nodes) * G.w0 + static_cast<uint64_t>(u - T.nbase) * G.wn;
+        for (uint32_t r = 0; r < G.wn && G.w0 + r < T.w_msgs; ++r)
+          acc += mix64((key0 | (G.w0 + r)) ^ mix64(valid ? seen[blk + r] : 0ull));
+      }
+      continue;
+    }
+    const uint64_t row = T.wbase + static_cast<uint64_t>(u - T.nbase) * T.W;
     for (uint32_t w = 0; w < T.w_msgs; ++w)
       acc += mix64((key0 | w) ^ mix64(valid ? seen[row + w] : 0ull));
   }
@@ -1344,12 +1355,13 @@ hipError_t launch_flag_compact(uint8_t* flags, uint8_t* blk_flag, uint32_t n_pad
 
 hipError_t launch_digest(const uint64_t* seen, const uint8_t* gen, uint32_t gen_cur,
                          const uint32_t* node_peer, const uint16_t* node_topic,
-                         const TopicDev* topics, uint32_t n_nodes, uint64_t* out, hipStream_t s) {
+                         const TopicDev* topics, const GroupDev* groups, uint32_t n_nodes, uint64_t* out,
+                         hipStream_t s) {
   uint32_t grid = (n_nodes + kBlock - 1) / kBlock;
   if (grid > 4096) grid = 4096;
   if (grid == 0) grid = 1;
   hipLaunchKernelGGL(k_digest, dim3(grid), dim3(kBlock), 0, s, seen, gen, gen_cur, node_peer,
-                     node_topic, topics, n_nodes, out);
+                     node_topic, topics, groups, n_nodes, out);
   return hipGetLastError();
 }
 

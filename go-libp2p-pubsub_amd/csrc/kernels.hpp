@@ -42,6 +42,15 @@ enum : uint32_t {
   // written seen row.  Arrival rows are then neither stored nor read: a
   // (non-root) parent's row is read from `seen`.
   kTopicSingleStart = 4,
+  // Tree topic whose window messages start in several rounds, laid out for
+  // level mode (one rank): start group g (GroupDev [group_lo, + group_n))
+  // owns the words [w0, w0 + wn) of every row -- "virtual" word w of node u
+  // -- stored group-major: block g of node u at wbase + n_nodes * w0 +
+  // (u - nbase) * wn, so a round's rows are contiguous per group.
+  kTopicGroups = 8,
+};
+struct GroupDev {
+  uint32_t w0, wn;
 };
 constexpr uint32_t kEntrySplit = 0x100;  // per-entry flag bit next to TopicDev.flags
 
@@ -59,20 +68,23 @@ __host__ __device__ inline uint16_t hop_round(uint32_t round) {
 struct TopicDev {
   uint64_t wbase;    // first word of the topic's mask block
   uint32_t w_msgs;   // message words in use (W may carry one pad word)
-  uint32_t pad;
+  uint32_t group_lo;  // kTopicGroups: the topic's start groups in the GroupDev table
   uint32_t nbase;    // first node of the topic (its root)
   uint32_t n_nodes;  // nodes in the topic
   uint32_t W;        // 64-message words per node in this window (0 = idle)
   uint32_t flags;    // kTopic*
   uint32_t seed_lo, seed_n;  // the topic's round-0 seeds (k_window_init applies them when asked)
+  uint32_t group_n;     // kTopicGroups: number of start groups
+  uint32_t root_words;  // words at wbase k_window_init zeroes for the root (W; group-major: block 0)
 };
 
 // One root injection: words of a topic root that start flooding in a round.
 struct SeedDev {
-  uint64_t woff;  // word offset (root row + word)
-  uint64_t mask;  // messages entering at this round
-  uint32_t node;  // root node index
-  uint32_t pad;
+  uint64_t woff;    // word offset (root row + word)
+  uint64_t mask;    // messages entering at this round
+  uint32_t node;    // root node index
+  uint32_t assign;  // 1: the word is set to mask (group-major root blocks, not zeroed by
+                    // k_window_init), 0: or-ed in
 };
 
 // Per-wave counters written by the expand kernel, reduced per round; they
@@ -119,7 +131,8 @@ struct PullChunk {
   uint32_t node_begin, node_end;  // nodes written in round r (level d)
   uint32_t topic;
   uint32_t p_lo, p_hi;  // parents of [node_begin, node_end) (consecutive ids), kNone: unknown
-  uint32_t pad[3];
+  uint32_t W;           // row words (a start group's block width for kTopicGroups)
+  uint32_t row0_lo, row0_hi;  // word offset of the row of the topic's first node (nbase)
 };
 constexpr uint32_t kPullMaxKids = 512;
 constexpr uint32_t kNoneNode = 0xFFFFFFFFu;
@@ -202,8 +215,6 @@ struct FloodArgs {
   uint32_t epoch;       // this launch's granule tag (never 0)
   uint32_t gen_cur;
   uint32_t spin_ticks;  // wait bound, s_memrealtime ticks (100 MHz)
-  uint32_t store_mode;  // EXPERIMENT (PSAMD_FLOOD_STORE): 0 sc1, 1 plain, 2 nt
-  uint32_t db;          // EXPERIMENT (PSAMD_FLOOD_DB): double-buffered even-W stream, 4 or 8 per batch
   uint64_t* prof;       // debug (PSAMD_FLOOD_PROFILE): per wave kFloodProf s_memrealtime stamps / sums
   uint32_t prof_split;  // debug: pf[7] sums the waits of tasks of later rounds
 };
@@ -309,6 +320,7 @@ hipError_t launch_flag_compact(uint8_t* flags, uint8_t* blk_flag, uint32_t n_pad
                                hipStream_t s);
 hipError_t launch_digest(const uint64_t* seen, const uint8_t* gen, uint32_t gen_cur,
                          const uint32_t* node_peer, const uint16_t* node_topic,
-                         const TopicDev* topics, uint32_t n_nodes, uint64_t* out, hipStream_t s);
+                         const TopicDev* topics, const GroupDev* groups, uint32_t n_nodes, uint64_t* out,
+                         hipStream_t s);
 
 }  // namespace psamd

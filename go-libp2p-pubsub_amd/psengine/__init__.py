@@ -27,6 +27,7 @@ PART_SUBTREE = 1
 F_RECORD_HOPS = 0x1
 F_TIME_KERNELS = 0x2
 F_NO_LAZY_SEEN = 0x4
+F_COMPACT = 0x8
 MODE_COMPACT, MODE_LEVEL_PULL, MODE_FLOOD = 0, 2, 3
 # ps_stats.expand_mode -> the kernel that ran the window's rounds
 MODE_KERNEL = {MODE_COMPACT: "k_expand", MODE_LEVEL_PULL: "k_pull", MODE_FLOOD: "k_flood"}

@@ -47,6 +47,8 @@ enum ps_status {
 #define PS_F_RECORD_HOPS 0x1u  /* keep (peer,msg)->hop for ps_read_hops (parity) */
 #define PS_F_TIME_KERNELS 0x2u /* HIP-event time every expand launch            */
 #define PS_F_NO_LAZY_SEEN 0x4u /* clear the seen bitset eagerly per window      */
+#define PS_F_COMPACT 0x8u      /* every window through the compaction path (the
+                                  general-graph k_expand rounds), trees too     */
 
 typedef struct ps_config {
   uint32_t n_peers;        /* peer id space [0, n_peers)                       */

@@ -1,0 +1,167 @@
+"""Start groups: tree windows whose messages enter at different rounds
+(ps_publish_at, paced publishing as in pubsub_test.go:101-131) run level mode
+-- one k_pull launch per round over each start group's word block -- and must
+equal the restatement (oracle/psoracle.c) and the compaction path
+(PS_F_COMPACT) exactly: hops, deliveries, per-round counts, seen digest and
+the readbacks.
+
+A message started at round s reaches a node of BFS level d in round s + d
+(subtree.forwardMessage, subtree.go:319-354; client.processMessages,
+client.go:100-132): each group is a single-start window of its own, laid out
+as an even-length word block of every row of its topic.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+import psengine as PE
+from psengine import workloads as WL
+
+pytestmark = pytest.mark.gpu
+
+
+def random_tree(rng, n, root, fan):
+    perm = rng.permutation(n)
+    perm = np.concatenate([[root], perm[perm != root]])
+    parent = np.full(n, O.NONE, dtype=np.uint32)
+    kids = np.zeros(n, dtype=np.int64)
+    for i in range(1, n):
+        while True:
+            p = perm[rng.integers(max(0, i - 4 * fan), i)]
+            if kids[p] < fan:
+                break
+        parent[perm[i]] = p
+        kids[p] += 1
+    return parent
+
+
+def run(level, n, topics, live, msg_topics, starts, record=True):
+    with PE.Engine(n, len(topics), record_hops=record, flags=0 if level else PE.F_COMPACT) as eng:
+        for t, (root, parent) in enumerate(topics):
+            eng.set_tree(t, root, parent)
+        eng.set_live(live)
+        first = eng.publish(msg_topics, starts)
+        st = eng.run()
+        if level:
+            assert st.expand_mode == PE.MODE_LEVEL_PULL
+        else:
+            assert st.expand_mode == PE.MODE_COMPACT
+        hops = [eng.hops(first + m) for m in range(len(msg_topics))] if record else None
+        deliv = [eng.delivered(first + m) for m in (0, len(msg_topics) // 2, len(msg_topics) - 1)]
+        peer_msgs = [eng.peer_messages(t, (topics[t][0] + 1) % n).tolist() for t in range(len(topics))]
+        return st, hops, deliv, peer_msgs, eng.seen_digest()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_groups_match_oracle_and_compaction(seed):
+    """Several topics, start rounds 0..7 drawn per message (some topics with
+    a single start), ~12 % dead peers: level mode with start groups and the
+    compaction path both equal the oracle message by message, and leave the
+    same counters, readbacks and seen digest."""
+    rng = np.random.default_rng(300 + seed)
+    n = int(rng.integers(400, 3000))
+    nt = int(rng.integers(1, 5))
+    topics = []
+    for t in range(nt):
+        root = int(rng.integers(0, n))
+        topics.append((root, random_tree(rng, n, root, fan=int(rng.integers(2, 7)))))
+    live = (rng.random(n) > 0.12).astype(np.uint8)
+    for root, _ in topics:
+        live[root] = 1
+    n_msgs = int(rng.integers(2, 900))
+    msg_topics = rng.integers(0, nt, size=n_msgs).astype(np.uint32)
+    starts = rng.integers(0, 8, size=n_msgs).astype(np.uint32)
+    if nt > 1:  # one topic single-start: a one-group topic beside grouped ones
+        starts[msg_topics == nt - 1] = 3
+    exp = {}
+    for t, (root, parent) in enumerate(topics):
+        rp, cl = O.parents_to_csr(parent)
+        exp[t] = O.disseminate(rp, cl, root, live, 1)[1][0]
+    outs = []
+    for level in (True, False):
+        st, hops, deliv, pm, digest = run(level, n, topics, live, msg_topics, starts)
+        for m, t in enumerate(msg_topics):
+            if not np.array_equal(hops[m], exp[int(t)]):
+                bad = np.nonzero(hops[m] != exp[int(t)])[0][:8]
+                raise AssertionError(f"level={level} msg {m} start {starts[m]}: peers {bad} "
+                                     f"got {hops[m][bad]} want {exp[int(t)][bad]}")
+        assert st.duplicates == 0
+        d = st.as_dict()
+        outs.append((st.deliveries, st.rounds, d["deliveries_per_round"], digest,
+                     [x.tobytes() for x in deliv], pm))
+    assert outs[0] == outs[1]
+    # per-round deliveries: message m reaches level d in round starts[m] + d
+    per = np.zeros(64, dtype=np.int64)
+    for m, t in enumerate(msg_topics):
+        h = exp[int(t)]
+        got = h[(h != 0xFF) & (h > 0)].astype(np.int64) + int(starts[m])
+        np.add.at(per, got, 1)
+    assert outs[0][2][1:] == [int(x) for x in per[1:len(outs[0][2])]]
+
+
+def test_groups_production_instance_and_windows():
+    """The non-recording instance, several windows per run (msg_window 200)
+    and ragged group sizes (1..130 messages per start round): level mode and
+    the compaction path leave the same deliveries, per-round counts and seen
+    digest; delivered() readbacks equal the oracle."""
+    rng = np.random.default_rng(77)
+    n = 2500
+    root = 11
+    parent = random_tree(rng, n, root, fan=4)
+    live = (rng.random(n) > 0.05).astype(np.uint8)
+    live[root] = 1
+    sizes = [1, 63, 64, 65, 130, 2, 127]
+    starts = np.concatenate([np.full(k, s, dtype=np.uint32) for s, k in enumerate(sizes)])
+    starts = starts[rng.permutation(len(starts))]
+    msg_topics = np.zeros(len(starts), dtype=np.uint32)
+    rp, cl = O.parents_to_csr(parent)
+    exp = O.disseminate(rp, cl, root, live, 1)[1][0]
+    outs = []
+    for level in (True, False):
+        with PE.Engine(n, 1, msg_window=200, flags=0 if level else PE.F_COMPACT) as eng:
+            eng.set_tree(0, root, parent)
+            eng.set_live(live)
+            first = eng.publish(msg_topics, starts)
+            st = eng.run()
+            assert st.windows >= 2
+            for m in (len(starts) - 1, len(starts) - 2, len(starts) - 50):  # the last window's
+                assert np.array_equal(eng.delivered(first + m), ((exp != 0xFF) & (exp > 0)).astype(np.uint8))
+            outs.append((st.deliveries, st.as_dict()["deliveries_per_round"], eng.seen_digest()))
+    assert outs[0] == outs[1]
+    assert outs[0][0] == len(starts) * int(((exp != 0xFF) & (exp > 0)).sum())
+
+
+def test_cfg3_staggered_full_size():
+    """BASELINE cfg3 at full size with start rounds uniform over 0..7 (the
+    bench's general-path workload): level mode with start groups delivers
+    exactly what the single-start window delivers, the per-round histogram
+    is the single-start one shifted per group, and 16 sampled messages per
+    topic class (hot 0, mid 8, cold 63) are delivered to exactly the tree."""
+    wl = WL.cfg3()
+    starts = (WL.stream(wl.seed ^ 0x57A6, np.arange(wl.n_msgs)) % np.uint64(8)).astype(np.uint32)
+    with PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed) as eng:
+        sizes = WL.build_engine_topics(eng, wl)
+        first = eng.publish(wl.msg_topics, starts)
+        st = eng.run()
+        assert st.expand_mode == PE.MODE_LEVEL_PULL
+        assert st.deliveries == wl.expected_deliveries(sizes) == 34_354_202_750
+        assert st.duplicates == 0
+        hist = np.zeros(80, dtype=np.int64)
+        ones = np.ones(wl.n_peers, np.uint8)
+        members = {}
+        for t in (0, 8, 63):
+            ts = wl.topics[t]
+            members[t] = np.zeros(wl.n_peers, dtype=np.uint8)
+            members[t][ts.join_order] = 1
+        for t, ts in enumerate(wl.topics):
+            rp, cl = O.parents_to_csr(eng.parents(t))
+            _, _, h = O.disseminate(rp, cl, ts.root, ones, 1, want_hops=False, hist_len=64)
+            for s0 in range(8):
+                k = int(((wl.msg_topics == t) & (starts == s0)).sum())
+                hist[s0:s0 + 64] += h.astype(np.int64) * k
+        per = st.as_dict()["deliveries_per_round"]
+        assert per[1:] == [int(x) for x in hist[1:len(per)]]
+        for t in (0, 8, 63):
+            ids = np.nonzero(wl.msg_topics == t)[0]
+            for m in ids[np.linspace(0, len(ids) - 1, 16).astype(int)]:
+                assert np.array_equal(eng.delivered(first + int(m)), members[t]), (t, m)

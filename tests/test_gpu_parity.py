@@ -51,9 +51,12 @@ def check_topic(eng, first, msg_idx, row_ptr, col, root, live):
     return total
 
 
+@pytest.mark.parametrize("level", [True, False])
 @pytest.mark.parametrize("eager", [False, True])
 @pytest.mark.parametrize("seed", range(8))
-def test_tree_parity_random(seed, eager):
+def test_tree_parity_random(seed, eager, level):
+    """Odd seeds publish at staggered start rounds: level mode runs them as
+    start groups, PS_F_COMPACT through the compaction path."""
     rng = np.random.default_rng(seed)
     n = int(rng.integers(2, 3000))
     root = int(rng.integers(0, n))
@@ -61,33 +64,38 @@ def test_tree_parity_random(seed, eager):
     live = (rng.random(n) > 0.1).astype(np.uint8)
     n_msgs = int(rng.integers(1, 300))
     starts = rng.integers(0, 6, size=n_msgs) if seed % 2 else None
-    flags = PE.F_NO_LAZY_SEEN if eager else 0
+    flags = (PE.F_NO_LAZY_SEEN if eager else 0) | (0 if level else PE.F_COMPACT)
     with PE.Engine(n, 1, record_hops=True, flags=flags) as eng:
         eng.set_tree(0, root, parent)
         eng.set_live(live)
         first = eng.publish(np.zeros(n_msgs), starts)
         st = eng.run()
+        if not level:
+            assert st.expand_mode == PE.MODE_COMPACT
         rp, cl = O.parents_to_csr(parent)
         total = check_topic(eng, first, list(range(n_msgs)), rp, cl, root, live)
         assert st.deliveries == total
         assert st.duplicates == 0
 
 
+@pytest.mark.parametrize("level", [True, False])
 @pytest.mark.parametrize("staggered", [False, True])
-def test_wide_rows_parity(staggered):
+def test_wide_rows_parity(staggered, level):
     """Rows wider than the expand kernel's LDS stage (W > 704 words): staged
-    slice by slice (expand_wide); single-start (level mode) and staggered."""
+    slice by slice (expand_wide, PS_F_COMPACT); single-start and staggered
+    (level mode: three start groups of ~268 words)."""
     rng = np.random.default_rng(40 + staggered)
     n = 600
     parent = random_tree(rng, n, 3)
     live = (rng.random(n) > 0.1).astype(np.uint8)
     n_msgs = 64 * 800 + 17  # W = 801 words: two slices
     starts = rng.integers(0, 3, size=n_msgs) if staggered else None
-    with PE.Engine(n, 1, record_hops=True) as eng:
+    with PE.Engine(n, 1, record_hops=True, flags=0 if level else PE.F_COMPACT) as eng:
         eng.set_tree(0, 3, parent)
         eng.set_live(live)
         first = eng.publish(np.zeros(n_msgs), starts)
         st = eng.run()
+        assert st.expand_mode != PE.MODE_COMPACT if level else st.expand_mode == PE.MODE_COMPACT
         rp, cl = O.parents_to_csr(parent)
         # every message floods the same tree: hop = depth below the root
         _, hops, _ = O.disseminate(rp, cl, 3, live, 1)

@@ -13,7 +13,7 @@ for W in cfg4 cfg5; do
   cut -c1-300 "$OUT/bench_$W.json"
 done
 echo "[other_cfgs] loopback $(date +%T)"
-timeout -k 10 300 python -u tools/loopback_bench.py 4 1.0 3 > "$OUT/loopback4.log" 2>&1
+timeout -k 10 300 python -u tools/loopback_bench.py --world 4 --workload cfg4 --scale 1.0 --steps 3 > "$OUT/loopback4.log" 2>&1
 tail -5 "$OUT/loopback4.log"
 cd /tmp && export TMPDIR=/tmp
 for W in cfg4 cfg5; do
