@@ -449,6 +449,7 @@ def main():
                       "edge_words": st.edge_words,
                       "frontier_per_round": st.as_dict()["frontier_per_round"],
                       "deliveries_per_round": st.as_dict()["deliveries_per_round"],
+                      "mbytes_per_round": [round(x / 1e6, 1) for x in st.as_dict()["expand_bytes_per_round"]],
                       "expand_us_per_round": [round(x * 1e3, 1) for x in
                                               st.as_dict()["expand_ms_per_round"]]},
     }

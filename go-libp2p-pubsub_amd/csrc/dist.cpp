@@ -1,6 +1,8 @@
 // dist.cpp -- RCCL and in-process loopback frontier-exchange transports.
 #include "dist.hpp"
 
+#include "kernels.hpp"
+
 #include <rccl/rccl.h>
 
 #include <chrono>
@@ -81,8 +83,9 @@ struct LoopbackGroup {
   struct Slot {
     const uint8_t* send = nullptr;
     const std::vector<uint64_t>* send_off = nullptr;
-    hipEvent_t sent = nullptr;  // send regions complete (stream order)
-    hipEvent_t read = nullptr;  // this rank finished copying from the others
+    hipEvent_t sent = nullptr;        // send regions complete (stream order)
+    hipEvent_t read[2] = {nullptr, nullptr};  // this rank finished copying from the others:
+                                              // exchange k records read[k & 1]
   };
   std::vector<Slot> slot;
 
@@ -126,11 +129,14 @@ class LoopbackTransport final : public Transport {
   LoopbackTransport(LoopbackGroup* g, int rank, int device) : g_(g), rank_(rank), device_(device) {
     (void)hipSetDevice(device_);
     (void)hipEventCreateWithFlags(&sent_, hipEventDisableTiming);
-    (void)hipEventCreateWithFlags(&read_, hipEventDisableTiming);
+    for (auto& r : read_) (void)hipEventCreateWithFlags(&r, hipEventDisableTiming);
+    g_->slot[rank_].read[0] = read_[0];
+    g_->slot[rank_].read[1] = read_[1];
   }
   ~LoopbackTransport() override {
     if (sent_) (void)hipEventDestroy(sent_);
-    if (read_) (void)hipEventDestroy(read_);
+    for (auto& r : read_)
+      if (r) (void)hipEventDestroy(r);
   }
   int rank() const override { return rank_; }
   int world() const override { return g_->world; }
@@ -140,31 +146,46 @@ class LoopbackTransport final : public Transport {
                       const std::vector<uint64_t>& send_len, uint8_t* recv,
                       const std::vector<uint64_t>& recv_off, const std::vector<uint64_t>& recv_len,
                       hipStream_t s, std::string* err) override {
+    // Two host barriers per exchange (every rank runs the same exchanges in
+    // the same order).  `sent` is re-recorded only after the next exchange's
+    // first barrier, which every rank reaches once it has enqueued its waits
+    // on it; the `read` events alternate, so one is re-recorded two exchanges
+    // later, after every rank's waits on it.
     (void)send_len;
+    const int par = parity_;
+    parity_ ^= 1;
+    hipEvent_t rd = read_[par];
     hipError_t e = hipEventRecord(sent_, s);
     if (e != hipSuccess) return fail(e, err);
     auto& me = g_->slot[rank_];
     me.send = send;
     me.send_off = &send_off;
     me.sent = sent_;
-    me.read = read_;
     if (!g_->barrier()) return timeout(err);  // every rank published regions + `sent`
+    CopyRegions c{};
     for (int src = 0; src < g_->world; ++src) {
       if (src == rank_ || recv_len[src] == 0) continue;
       const auto& o = g_->slot[src];
       if ((e = hipStreamWaitEvent(s, o.sent, 0)) != hipSuccess) return fail(e, err);
-      e = hipMemcpyAsync(recv + recv_off[src], o.send + (*o.send_off)[rank_], recv_len[src],
-                         hipMemcpyDeviceToDevice, s);
-      if (e != hipSuccess) return fail(e, err);
+      const uint8_t* from = o.send + (*o.send_off)[rank_];
+      uint8_t* to = recv + recv_off[src];
+      if (c.n < kMaxCopyRegions && recv_len[src] % 16 == 0 && reinterpret_cast<uintptr_t>(from) % 16 == 0 &&
+          reinterpret_cast<uintptr_t>(to) % 16 == 0) {  // (ghost records: whole 16-B units)
+        c.src[c.n] = reinterpret_cast<const uint4*>(from);
+        c.dst[c.n] = reinterpret_cast<uint4*>(to);
+        c.units[c.n++] = recv_len[src] / 16;
+      } else if ((e = hipMemcpyAsync(to, from, recv_len[src], hipMemcpyDeviceToDevice, s)) != hipSuccess) {
+        return fail(e, err);
+      }
     }
-    if ((e = hipEventRecord(read_, s)) != hipSuccess) return fail(e, err);
+    if ((e = launch_copy_regions(c, s)) != hipSuccess) return fail(e, err);
+    if ((e = hipEventRecord(rd, s)) != hipSuccess) return fail(e, err);
     if (!g_->barrier()) return timeout(err);  // every rank enqueued copies + `read`
     // our send regions may be rewritten only after every reader copied them
     for (int q = 0; q < g_->world; ++q) {
       if (q == rank_) continue;
-      if ((e = hipStreamWaitEvent(s, g_->slot[q].read, 0)) != hipSuccess) return fail(e, err);
+      if ((e = hipStreamWaitEvent(s, g_->slot[q].read[par], 0)) != hipSuccess) return fail(e, err);
     }
-    if (!g_->barrier()) return timeout(err);  // `read` events may be re-recorded
     return hipSuccess;
   }
 
@@ -179,7 +200,8 @@ class LoopbackTransport final : public Transport {
   }
   LoopbackGroup* g_;
   int rank_, device_;
-  hipEvent_t sent_ = nullptr, read_ = nullptr;
+  hipEvent_t sent_ = nullptr, read_[2] = {nullptr, nullptr};
+  int parity_ = 0;
 };
 
 }  // namespace

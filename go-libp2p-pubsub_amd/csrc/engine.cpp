@@ -155,6 +155,7 @@ struct ps_engine {
   bool flood_broken = false;  // a dependency wait timed out once: per-level launches from then on
   uint32_t flood_grid = 0;    // resident blocks (0: k_flood unavailable)
   uint32_t flood_words = kFloodWords;  // row words per task (PSAMD_FLOOD_WORDS)
+  uint32_t pull_words = kPullWords;    // row words per k_pull chunk (512..4096 measured: 1024 best)
   uint64_t flood_top_bytes = 16ull << 20;  // k_flood runs the leading rounds writing at most this many row bytes
   uint32_t flood_epoch = 0;   // granule tag of the last launch (granules are never reset)
   std::vector<uint64_t> flood_key;
@@ -1005,7 +1006,7 @@ int upload_graph(ps_engine* e) {
 int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
                       const std::vector<std::vector<StartGroup>>& groups, uint32_t rounds) {
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
-  std::vector<uint64_t> key{e->graph_epoch, e->flags_epoch, rounds};
+  std::vector<uint64_t> key{e->graph_epoch, e->flags_epoch, rounds, e->pull_words};
   for (uint32_t t = 0; t < nt; ++t) {
     key.push_back(tab[t].W ? groups[t].size() : ~0ull);
     key.push_back(tab[t].W);
@@ -1033,7 +1034,7 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
         const uint32_t d = q - g.start;  // level of the nodes whose block g is written this round
         if (d + 1 >= T.level_off.size()) continue;
         const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
-        const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, kPullWords / g.wn));
+        const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, e->pull_words / g.wn));
         e->pull_bytes[q] += static_cast<uint64_t>(hi - lo) * g.wn * 8;
         for (uint32_t u = lo; u < hi; u += per) {
           PullChunk c{};
@@ -1064,6 +1065,7 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
                                  e->d_node_parent.as<uint32_t>(), e->stream),
             "chunk parents");
   e->pull_key = key;
+  e->ghost_key.clear();  // multi-GPU: the chunks' shipping ranges are assigned again
   return PS_OK;
 }
 
@@ -1097,6 +1099,10 @@ int build_ghost_plan(ps_engine* e, const std::vector<TopicDev>& tab, const std::
     return e->topics[t].gcnt[(static_cast<size_t>(d) * world + a) * world + b];
   };
   e->ghost_rounds.assign(rounds + 2, ps_engine::GhostRound{});
+  struct ShipRange {
+    uint32_t round, topic, e0, e1;
+  };
+  std::vector<ShipRange> ship;
   e->pack_host.clear();
   e->pack_seg_host.clear();
   e->ghost_off_host.assign(e->n_nodes, kGhostNone);
@@ -1135,6 +1141,9 @@ int build_ghost_plan(ps_engine* e, const std::vector<TopicDev>& tab, const std::
       R.s_len[b] = region(me, b, b);
       so += R.s_len[b];
     }
+    // Records of level-0 parents (roots, seeded) are packed by k_pack this
+    // round; deeper parents' records are written by the k_pull launch of the
+    // round before, which writes those parents' rows (PullChunk e_lo/e_hi)
     R.pack0 = static_cast<uint32_t>(e->pack_host.size());
     R.seg0 = static_cast<uint32_t>(e->pack_seg_host.size());
     uint64_t word0 = 0;
@@ -1153,9 +1162,12 @@ int build_ghost_plan(ps_engine* e, const std::vector<TopicDev>& tab, const std::
         e->pack_host.push_back(pe);
       }
       const uint32_t e1 = static_cast<uint32_t>(e->pack_host.size());
-      if (e1 > e0) {
+      if (e1 == e0) continue;
+      if (d == 1) {
         e->pack_seg_host.push_back(PackSeg{e0, e1, t, W, word0});
-        word0 += static_cast<uint64_t>(e1 - e0) * W;
+        word0 += static_cast<uint64_t>(e1 - e0) * pack_units(W);
+      } else {
+        ship.push_back(ShipRange{q - 1, t, e0, e1});
       }
     }
     R.pack1 = static_cast<uint32_t>(e->pack_host.size());
@@ -1183,6 +1195,30 @@ int build_ghost_plan(ps_engine* e, const std::vector<TopicDev>& tab, const std::
     }
     e->ghost_send_max = std::max(e->ghost_send_max, so);
     e->ghost_recv_max = std::max(e->ghost_recv_max, ro);
+  }
+  // each shipping range to the chunks of round q - 1 that write its parents
+  // (entries and chunks both in node order within a topic)
+  for (PullChunk& c : e->pull_host) c.e_lo = c.e_hi = 0;
+  for (const ShipRange& sr : ship) {
+    uint32_t k = sr.e0;
+    for (uint32_t ci = e->pull_off[sr.round]; ci < e->pull_off[sr.round + 1]; ++ci) {
+      PullChunk& c = e->pull_host[ci];
+      if (c.topic != sr.topic) continue;
+      while (k < sr.e1 && e->pack_host[k].node < c.node_begin) ++k;  // (never: every parent is in a chunk)
+      c.e_lo = k;
+      while (k < sr.e1 && e->pack_host[k].node < c.node_end) ++k;
+      c.e_hi = k;
+    }
+    if (k != sr.e1) return e->fail(PS_E_STATE, "ghost records outside the round's chunks");
+  }
+  if (!e->pull_host.empty()) {
+    HIP_TRY(hipMemcpyAsync(e->d_pull.p, e->pull_host.data(), e->pull_host.size() * sizeof(PullChunk),
+                           hipMemcpyHostToDevice, e->stream),
+            "upload pull chunks");
+    if (e->gpu_graph)  // parent ranges again (the host copy holds none)
+      HIP_TRY(launch_chunk_parents(e->d_pull.as<PullChunk>(), static_cast<uint32_t>(e->pull_host.size()),
+                                   e->d_node_parent.as<uint32_t>(), e->stream),
+              "chunk parents");
   }
   HIP_TRY(e->d_pack.ensure(std::max<size_t>(e->pack_host.size(), 1) * sizeof(PackEntry)), "alloc pack entries");
   HIP_TRY(e->d_pack_seg.ensure(std::max<size_t>(e->pack_seg_host.size(), 1) * sizeof(PackSeg)), "alloc pack segments");
@@ -1933,7 +1969,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
           if (R.seg1 > R.seg0) {
             const PackSeg& last = e->pack_seg_host[R.seg1 - 1];
             HIP_TRY(launch_pack(e->d_pack.as<PackEntry>(), e->d_pack_seg.as<PackSeg>() + R.seg0, R.seg1 - R.seg0,
-                                last.word0 + static_cast<uint64_t>(last.e1 - last.e0) * last.W, a.topics, a.seen,
+                                last.unit0 + static_cast<uint64_t>(last.e1 - last.e0) * pack_units(last.W), a.topics, a.seen,
                                 a.gen, a.gen_cur, e->d_send.as<uint64_t>(), s),
                     "pack");
           }
@@ -1958,6 +1994,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
           pa.slot_mod = kPullSlots;
           pa.ghost_off = world > 1 ? e->d_ghost_off.as<uint64_t>() : nullptr;
           pa.recv = e->d_recv.as<uint64_t>();
+          pa.ship = world > 1 ? e->d_pack.as<PackEntry>() : nullptr;
+          pa.send = e->d_send.as<uint64_t>();
           // rows nobody re-reads while they can still sit in the 256 MB MALL
           // (large rounds and the last round) store non-temporally
           const bool nt = r < e->pull_bytes.size() && (e->pull_bytes[r] >= (64ull << 20) || r == planned0);

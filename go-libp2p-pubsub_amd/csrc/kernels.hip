@@ -906,6 +906,31 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
   }
 }
 
+// Multi-GPU: the chunk's nodes that are ghost parents next round ship their
+// rows now, into the send buffer's records ([reach word][W words] at row_off
+// - 1), from the rows they copied (src[]: L2-resident, just read): one
+// pass over the records, 16-B units for even W.  Replaces a separate pack
+// launch that re-read the rows from HBM.
+__device__ __forceinline__ void pull_ship(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t e_lo,
+                                          uint32_t e_hi, const uint64_t* src, uint32_t lane) {
+  const bool pairs = !(P.W & 1u);
+  const uint32_t per = pairs ? P.W >> 1 : P.W;
+  const uint32_t total = (e_hi - e_lo) * per;
+  for (uint32_t i = lane; i < total; i += 64) {
+    const uint32_t k = i / per, r = i - k * per;
+    const PackEntry E = a.ship[e_lo + k];
+    const uint64_t row = src[E.node - nb];
+    if (r == 0) a.send[E.row_off - 1] = row != 0 ? 1ull : 0ull;
+    if (row == 0) continue;
+    const uint32_t w = pairs ? 2 * r : r;
+    const uint64_t* s = reinterpret_cast<const uint64_t*>(row) + w;
+    if (pairs)
+      *reinterpret_cast<uint4*>(a.send + E.row_off + w) = *reinterpret_cast<const uint4*>(s);
+    else
+      a.send[E.row_off + w] = *s;
+  }
+}
+
 // The block's counters of one launch into partial slot `slot` (blocks share
 // a slot: slots are zeroed per window).
 __device__ __forceinline__ void pull_flush(const PullCtr& c, uint64_t* partials, uint64_t slot, uint32_t lane,
@@ -954,14 +979,17 @@ __global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __
     // is visible to the reads that follow
     pull_resolve(a, P, ch.node_begin, n1, ch.p_lo, ch.p_hi, src, genl, lane, cur, c);
     pull_stream<kRecord, kNT>(a, P, ch.node_begin, n1, src, lane, round, c);
+    if (ch.e_hi > ch.e_lo) pull_ship(a, P, ch.node_begin, ch.e_lo, ch.e_hi, src, lane);
   }
   pull_flush(c, a.partials, blockIdx.x % a.slot_mod, lane, wid);
 }
 
 // Multi-GPU level mode: the round's ghost rows.  Thread i of the flattened
-// stream copies word i: segment (one topic, constant W) by a short scan,
-// entry = offset / W.  A parent not reached this window (stale generation)
-// ships only its zero reach word; the receiver then skips its children.
+// stream copies unit i of one record -- a 16-B word pair for even W (rows
+// and records 16-B aligned), one word for odd W: segment (one topic,
+// constant W) by a short scan, entry = offset / units per row (32-bit).  A
+// parent not reached this window (stale generation) ships only its zero
+// reach word; the receiver then skips its children.
 __global__ __launch_bounds__(kBlock) void k_pack(const PackEntry* __restrict__ entries,
                                                  const PackSeg* __restrict__ segs, uint32_t n_segs,
                                                  uint64_t total, const TopicDev* __restrict__ topics,
@@ -971,17 +999,23 @@ __global__ __launch_bounds__(kBlock) void k_pack(const PackEntry* __restrict__ e
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < total;
        i += static_cast<uint64_t>(gridDim.x) * kBlock) {
     uint32_t k = 0;
-    while (k + 1 < n_segs && segs[k + 1].word0 <= i) ++k;
+    while (k + 1 < n_segs && segs[k + 1].unit0 <= i) ++k;
     const PackSeg S = segs[k];
-    const uint64_t o = i - S.word0;
-    const uint32_t e = S.e0 + static_cast<uint32_t>(o / S.W);
-    const uint32_t w = static_cast<uint32_t>(o % S.W);
+    const bool pairs = !(S.W & 1u);
+    const uint32_t per = pairs ? S.W >> 1 : S.W;  // units per row
+    const uint32_t o = static_cast<uint32_t>(i - S.unit0);
+    const uint32_t e = S.e0 + o / per;
+    const uint32_t w = (o - (e - S.e0) * per) << (pairs ? 1 : 0);
     const PackEntry E = entries[e];
     const bool reached = gen[E.node] == cur;
     if (w == 0) send[E.row_off - 1] = reached ? 1 : 0;
     if (reached) {
       const TopicDev T = topics[S.topic];
-      send[E.row_off + w] = seen[T.wbase + static_cast<uint64_t>(E.node - T.nbase) * T.W + w];
+      const uint64_t* row = seen + T.wbase + static_cast<uint64_t>(E.node - T.nbase) * T.W + w;
+      if (pairs)
+        *reinterpret_cast<uint4*>(send + E.row_off + w) = *reinterpret_cast<const uint4*>(row);
+      else
+        send[E.row_off + w] = *row;
     }
   }
 }
@@ -1301,12 +1335,12 @@ hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_ch
   return hipGetLastError();
 }
 
-hipError_t launch_pack(const PackEntry* entries, const PackSeg* segs, uint32_t n_segs, uint64_t total_words,
+hipError_t launch_pack(const PackEntry* entries, const PackSeg* segs, uint32_t n_segs, uint64_t total_units,
                        const TopicDev* topics, const uint64_t* seen, const uint8_t* gen, uint32_t gen_cur,
                        uint64_t* send, hipStream_t s) {
-  if (total_words == 0 || n_segs == 0) return hipSuccess;
-  const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(4096, (total_words + kBlock - 1) / kBlock));
-  hipLaunchKernelGGL(k_pack, dim3(grid), dim3(kBlock), 0, s, entries, segs, n_segs, total_words, topics, seen, gen,
+  if (total_units == 0 || n_segs == 0) return hipSuccess;
+  const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(4096, (total_units + kBlock - 1) / kBlock));
+  hipLaunchKernelGGL(k_pack, dim3(grid), dim3(kBlock), 0, s, entries, segs, n_segs, total_units, topics, seen, gen,
                      gen_cur, send);
   return hipGetLastError();
 }
@@ -1314,6 +1348,21 @@ hipError_t launch_pack(const PackEntry* entries, const PackSeg* segs, uint32_t n
 hipError_t launch_chunk_parents(PullChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_chunk_parents, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, chunks, n, node_parent);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(kBlock) void k_copy_regions(CopyRegions c) {
+  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x, nth = gridDim.x * kBlock;
+  for (uint32_t k = 0; k < c.n; ++k)
+    for (uint64_t i = tid; i < c.units[k]; i += nth) c.dst[k][i] = c.src[k][i];
+}
+
+hipError_t launch_copy_regions(const CopyRegions& c, hipStream_t s) {
+  uint64_t most = 0;
+  for (uint32_t k = 0; k < c.n; ++k) most = c.units[k] > most ? c.units[k] : most;
+  if (most == 0) return hipSuccess;
+  const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(2048, (most + kBlock - 1) / kBlock));
+  hipLaunchKernelGGL(k_copy_regions, dim3(grid), dim3(kBlock), 0, s, c);
   return hipGetLastError();
 }
 

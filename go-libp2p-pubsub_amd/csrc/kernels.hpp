@@ -133,11 +133,20 @@ struct PullChunk {
   uint32_t p_lo, p_hi;  // parents of [node_begin, node_end) (consecutive ids), kNone: unknown
   uint32_t W;           // row words (a start group's block width for kTopicGroups)
   uint32_t row0_lo, row0_hi;  // word offset of the row of the topic's first node (nbase)
+  // multi-GPU: PullArgs::ship entries [e_lo, e_hi) -- ghost records of the
+  // next round for nodes of this chunk, written by the wave that writes them
+  uint32_t e_lo, e_hi;
+  uint32_t pad[2];
 };
 constexpr uint32_t kPullMaxKids = 512;
 constexpr uint32_t kNoneNode = 0xFFFFFFFFu;
 constexpr uint32_t kPullWords = 1024;
 
+struct PackEntry {
+  uint32_t node;     // the parent (local node id)
+  uint32_t pad;
+  uint64_t row_off;  // row, words from the send buffer (reach word at row_off - 1)
+};
 struct PullArgs {
   const uint32_t* node_parent;  // node-space parent (kNone for roots and remote parents)
   const uint8_t* node_flags;
@@ -152,6 +161,10 @@ struct PullArgs {
   // word in recv (its reach word is the word before), or kGhostNone
   const uint64_t* ghost_off;  // null: one rank
   const uint64_t* recv;
+  // multi-GPU: the next round's ghost records of the nodes written now
+  // (PullChunk e_lo/e_hi), stored into the send buffer
+  const PackEntry* ship;
+  uint64_t* send;
   uint32_t gen_cur;
   uint32_t slot_mod;   // block b adds its counters into partial slot b % slot_mod (zeroed per window)
 };
@@ -164,17 +177,14 @@ constexpr uint64_t kGhostNone = ~0ull;
 // 16-B alignment and its reach word (parent reached this window) is the word
 // before it.  One entry per (parent, destination); the entries of one topic
 // form a segment (constant W).
-struct PackEntry {
-  uint32_t node;     // the parent (local node id)
-  uint32_t pad;
-  uint64_t row_off;  // row, words from the send buffer (reach word at row_off - 1)
-};
 __host__ __device__ inline uint32_t ghost_record_words(uint32_t W) { return W + ((W & 1u) ? 1u : 2u); }
 struct PackSeg {
   uint32_t e0, e1;  // entries
   uint32_t topic, W;
-  uint64_t word0;   // the segment's first word in the launch's flattened stream
+  uint64_t unit0;   // the segment's first unit in the launch's flattened stream (16-B pairs
+                    // for even W, words for odd W: pack_units)
 };
+__host__ __device__ inline uint32_t pack_units(uint32_t W) { return (W & 1u) ? W : W >> 1; }
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch
 
 // k_flood (flood.hip): every round of a single-start tree
@@ -261,6 +271,17 @@ struct StageCopy {
   uint32_t n;
 };
 hipError_t launch_stage_copy(const StageCopy& c, hipStream_t s);
+
+// Loopback exchange (one GPU): up to kMaxCopyRegions device regions of
+// whole 16-B units copied by one launch.
+constexpr uint32_t kMaxCopyRegions = 16;
+struct CopyRegions {
+  const uint4* src[kMaxCopyRegions];
+  uint4* dst[kMaxCopyRegions];
+  uint64_t units[kMaxCopyRegions];
+  uint32_t n;
+};
+hipError_t launch_copy_regions(const CopyRegions& c, hipStream_t s);
 // Window start: zero and stamp the roots' rows (every row of a mesh topic);
 // optionally in the same launch (WindowStart): the staged per-window copies
 // (topics_src / seeds_src then point at the staged sources), the round-0
@@ -290,7 +311,7 @@ hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_ch
                        uint32_t grid, uint32_t round, bool record, bool nt, hipStream_t s);
 
 // multi-GPU level mode: the round's ghost rows into the send buffer
-hipError_t launch_pack(const PackEntry* entries, const PackSeg* segs, uint32_t n_segs, uint64_t total_words,
+hipError_t launch_pack(const PackEntry* entries, const PackSeg* segs, uint32_t n_segs, uint64_t total_units,
                        const TopicDev* topics, const uint64_t* seen, const uint8_t* gen, uint32_t gen_cur,
                        uint64_t* send, hipStream_t s);
 // Fills PullChunk::p_lo / p_hi from the device node_parent (GPU-built graphs).
