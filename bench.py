@@ -168,9 +168,10 @@ def pmc_traffic(kernel: str, workload: str):
             d = json.load(fh)
     except (OSError, ValueError):
         return None, None
-    if d.get("kernel") != kernel or d.get("workload") != workload:
-        return None, None
-    return d.get("traffic_bytes_per_launch"), d.get("source")
+    for x in d.get("entries", []):
+        if x.get("kernel") == kernel and x.get("workload") == workload:
+            return x.get("traffic_bytes_per_launch"), x.get("source")
+    return None, None
 
 
 def kernel_split(st):
@@ -320,7 +321,8 @@ def general_path(eng, wl, deliv_expected, steps: int, warmup: int = 1, max_start
         wall = time.perf_counter() - t0
         assert tot == deliv_expected * n_steps
         per, st = instrumented(eng, step, 2)
-        roof = roofline_of(per)
+        hot = max(per, key=lambda k: (per[k][1], per[k][0]))
+        roof = roofline_of(per, *pmc_traffic(hot, f"{wl.name}-staggered"))
         roof["device_ms_per_step"] = sum(v[1] for v in per.values()) / 2
         d = st.as_dict()
         return {"value": tot / wall, "unit": "deliveries/s", "steps": n_steps, "ms_per_step": wall * 1e3 / n_steps,
@@ -355,6 +357,8 @@ def main():
     ap.add_argument("--no-check", action="store_true", help="skip delivery assertions (experiments)")
     ap.add_argument("--no-general", action="store_true",
                     help="skip the general-path leg (staggered starts, compaction mode)")
+    ap.add_argument("--general-only", action="store_true",
+                    help="run only the general-path leg and print it as the JSON line (its PMC passes)")
     ap.add_argument("--force-dist", action="store_true",
                     help="use the torch.distributed driver even with one rank (testing)")
     ap.add_argument("--partition", default="peer", choices=["peer", "subtree"],
@@ -387,6 +391,12 @@ def main():
     def step():
         eng.publish(wl.msg_topics)
         return eng.run()
+
+    if args.general_only:
+        g = general_path(eng, wl, deliv_expected, max(2, min(args.steps, 4)), warmup=max(1, args.warmup))
+        print(json.dumps({"metric": METRIC + " [general path only]", "general_path": g}), flush=True)
+        eng.close()
+        return
 
     def steps_pipelined(n):
         """n steps, each batch published and enqueued while the previous

@@ -45,7 +45,9 @@ def test_pmc_traffic_matches_kernel_and_workload():
     import json
     with open(bench.TRAFFIC_FILE) as fh:
         d = json.load(fh)
-    t, src = bench.pmc_traffic(d["kernel"], d["workload"])
-    assert t is not None and t > 0 and "FETCH_SIZE" in src
-    assert bench.pmc_traffic(d["kernel"] + "_other", d["workload"])[0] is None
-    assert bench.pmc_traffic(d["kernel"], d["workload"] + "_other")[0] is None
+    assert d["entries"]
+    for x in d["entries"]:
+        t, src = bench.pmc_traffic(x["kernel"], x["workload"])
+        assert t is not None and t > 0 and "FETCH_SIZE" in src
+        assert bench.pmc_traffic(x["kernel"] + "_other", x["workload"])[0] is None
+        assert bench.pmc_traffic(x["kernel"], x["workload"] + "_other")[0] is None

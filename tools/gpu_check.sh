@@ -30,22 +30,21 @@ cd /tmp && export TMPDIR=/tmp
 if [ "${TRACE:-1}" = 1 ]; then
   echo "[gpu_check] trace $(date +%T)"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- \
-    python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu $BARGS > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err"
-  find "$OUT/trace" -name "*kernel_stats.csv" -exec cat {} \;
+    python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu --no-general $BARGS > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_general" -o run -- \
+    python3 "$ROOT/bench.py" --steps 4 --warmup 1 --no-cpu --general-only $BARGS > "$OUT/bench_trace_general.json" 2> "$OUT/bench_trace_general.err"
 fi
 if [ "${PMC:-0}" = 1 ]; then
-  for C in FETCH_SIZE WRITE_SIZE; do
-    echo "[gpu_check] pmc $C $(date +%T)"
-    timeout -s KILL 180 rocprofv3 --pmc $C -f csv -d "$OUT/pmc_$C" -o run -- \
-      python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu $BARGS > "$OUT/pmc_$C.json" 2> "$OUT/pmc_$C.err"
+  # headline kernel (no general-path leg), then the general-path leg alone
+  for SET in main general; do
+    EXTRA="--no-general"
+    [ "$SET" = general ] && EXTRA="--general-only"
+    for C in FETCH_SIZE WRITE_SIZE; do
+      echo "[gpu_check] pmc $SET $C $(date +%T)"
+      timeout -s KILL 240 rocprofv3 --pmc $C -f csv -d "$OUT/pmc_${SET}/$C" -o run -- \
+        python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu $EXTRA $BARGS > "$OUT/pmc_${SET}_$C.json" 2> "$OUT/pmc_${SET}_$C.err"
+    done
+    python3 "$ROOT/tools/pmc_summary.py" "$OUT/pmc_${SET}" > "$OUT/pmc_summary_${SET}.json"
   done
-  python3 "$ROOT/tools/pmc_summary.py" "$OUT" > "$OUT/pmc_summary.json"
-  python3 - "$OUT/pmc_summary.json" <<'EOF'
-import json, sys
-d = json.load(open(sys.argv[1]))
-for k, v in d.items():
-    if "k_expand" in k or "k_pull" in k:
-        print(k[:60], {x: v.get(x) for x in ("hbm_read_bytes_per_dispatch_x2", "hbm_write_bytes_per_dispatch")})
-EOF
 fi
 echo "[gpu_check] done $(date +%T)"

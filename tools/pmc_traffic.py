@@ -1,14 +1,15 @@
 #!/usr/bin/env python3
-"""Writes profiles/pmc_traffic.json (bench.py's roofline.traffic) from the
-separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes of a gpu_check.sh run.
+"""Adds (or replaces) one entry of profiles/pmc_traffic.json (bench.py's
+roofline.traffic) from the separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes
+summarised by tools/pmc_summary.py.
 
-    python tools/pmc_traffic.py gpurun_out/<tag> <kernel> <workload> <round-tag>
+    python tools/pmc_traffic.py <pmc_summary.json> <kernel> <workload> <round-tag> [<source note>]
 
 HBM bytes per launch = 2 x FETCH_SIZE (gfx950: FETCH_SIZE counts half of the
 bytes of wide coalesced reads, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both
-averaged over every dispatch of the kernel's production instance in the run,
-like bench.py's algorithmic bytes per launch.  The summary of the passes is
-copied to profiles/<round-tag>/ next to it.
+averaged over every dispatch of the kernel's production instances (no hop
+record: first template argument false) in the run, like bench.py's
+algorithmic bytes per launch.  The summary is copied to profiles/<round-tag>/.
 """
 import json
 import os
@@ -16,34 +17,37 @@ import shutil
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(REPO, "profiles", "pmc_traffic.json")
 
 
 def main():
-    run_dir, kernel, workload, rtag = sys.argv[1:5]
-    summ = json.load(open(os.path.join(run_dir, "pmc_summary.json")))
-    # production instances: no hop record (first template argument false);
-    # the cache-policy variants (plain / nt stores) are one kernel to the
-    # roofline, so their traffic is averaged over all of their dispatches
-    # (k_pull: its top-levels launch k_pull_top is one of the launches too)
-    names = [k for k in summ if (f"{kernel}<false" in k or f"{kernel}_top<false" in k)
-             and "hbm_write_bytes_per_dispatch" in summ[k]]
+    summ_path, kernel, workload, rtag = sys.argv[1:5]
+    note = sys.argv[5] if len(sys.argv) > 5 else f"bench.py --workload {workload.split('-')[0]}"
+    summ = json.load(open(summ_path))
+    names = [k for k in summ if f"{kernel}<false" in k and "hbm_write_bytes_per_dispatch" in summ[k]
+             and "hbm_read_bytes_per_dispatch_x2" in summ[k]]
     if not names:
-        sys.exit(f"no {kernel}<false ...> dispatches with both counters in {run_dir}")
+        sys.exit(f"no {kernel}<false ...> dispatches with both counters in {summ_path}")
     disp = sum(summ[k]["WRITE_SIZE"]["dispatches"] for k in names)
     rd = sum(summ[k]["hbm_read_bytes_per_dispatch_x2"] * summ[k]["WRITE_SIZE"]["dispatches"] for k in names) / disp
     wr = sum(summ[k]["hbm_write_bytes_per_dispatch"] * summ[k]["WRITE_SIZE"]["dispatches"] for k in names) / disp
     os.makedirs(os.path.join(REPO, "profiles", rtag), exist_ok=True)
-    dst = os.path.join("profiles", rtag, "pmc_summary.json")
-    shutil.copy(os.path.join(run_dir, "pmc_summary.json"), os.path.join(REPO, dst))
-    out = {"kernel": kernel, "workload": workload, "instances": names,
-           "dispatches": disp,
-           "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
-           "traffic_bytes_per_launch": rd + wr,
-           "source": f"rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) of "
-                     f"bench.py --workload {workload}; read = 2 x FETCH_SIZE (gfx950); {dst}"}
-    with open(os.path.join(REPO, "profiles", "pmc_traffic.json"), "w") as fh:
-        json.dump(out, fh, indent=1)
-    print(json.dumps(out, indent=1))
+    dst = os.path.join("profiles", rtag, f"pmc_summary_{workload}.json")
+    shutil.copy(summ_path, os.path.join(REPO, dst))
+    entry = {"kernel": kernel, "workload": workload, "instances": names, "dispatches": disp,
+             "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+             "traffic_bytes_per_launch": rd + wr,
+             "source": f"rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) of {note}; "
+                       f"read = 2 x FETCH_SIZE (gfx950); {dst}"}
+    try:
+        d = json.load(open(OUT))
+    except (OSError, ValueError):
+        d = {}
+    entries = [x for x in d.get("entries", []) if (x.get("kernel"), x.get("workload")) != (kernel, workload)]
+    entries.append(entry)
+    with open(OUT, "w") as fh:
+        json.dump({"entries": entries}, fh, indent=1)
+    print(json.dumps(entry, indent=1))
 
 
 if __name__ == "__main__":
