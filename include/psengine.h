@@ -65,10 +65,11 @@ typedef struct ps_config {
 /* ps_stats.expand_mode: how the last window's rounds ran */
 #define PS_MODE_COMPACT 0u     /* k_expand over a compacted frontier (flags + scan) */
 #define PS_MODE_LEVEL_PULL 2u  /* k_pull: one launch per round, each level pulls its
-                                  parents' rows (multi-GPU windows)                */
-#define PS_MODE_FLOOD 3u       /* k_flood: every round in one persistent launch,
-                                  each level pulls its parents' rows when the
-                                  tasks writing them have published               */
+                                  parents' rows (start groups, multi-GPU windows) */
+#define PS_MODE_FLOOD 3u       /* k_flood for the leading rounds (one persistent
+                                  launch, each level pulls its parents' rows once
+                                  the tasks writing them have published), then
+                                  k_pull per round; see ps_stats.flood_rounds     */
 
 typedef struct ps_stats {
   uint64_t deliveries;         /* (peer,msg) pairs delivered by this run        */
