@@ -11,9 +11,42 @@ namespace psamd {
 SubscriptionTree::SubscriptionTree(uint32_t n_peers, uint32_t root, uint32_t width,
                                    uint32_t max_width, uint64_t seed)
     : n_(n_peers), root_(root), width_(width), max_width_(max_width), rng_(seed),
-      touched_mark_(n_peers, 0), state_(n_peers, PeerState::Out), up_(n_peers, kNone),
-      kids_(n_peers) {
-  state_[root] = PeerState::In;
+      touched_mark_(n_peers, 0), rec_(n_peers) {
+  rec_[root].state = PeerState::In;
+}
+
+void SubscriptionTree::kid_push(uint32_t p, const ChildRec& r) {
+  PeerRec& R = rec_[p];
+  if (R.spill == kNone && R.n < kInline) {
+    R.kin[R.n++] = r;
+    return;
+  }
+  if (R.spill == kNone) {  // the list outgrows the line: move it to a spill vector
+    uint32_t s;
+    if (!spill_free_.empty()) {
+      s = spill_free_.back();
+      spill_free_.pop_back();
+    } else {
+      s = static_cast<uint32_t>(spill_.size());
+      spill_.emplace_back();
+    }
+    spill_[s].assign(R.kin, R.kin + R.n);
+    R.spill = s;
+  }
+  auto& v = spill_[R.spill];
+  v.resize(R.n);
+  v.push_back(r);
+  R.n = static_cast<uint16_t>(v.size());
+}
+
+void SubscriptionTree::kid_clear(uint32_t p) {
+  PeerRec& R = rec_[p];
+  if (R.spill != kNone) {
+    spill_[R.spill].clear();
+    spill_free_.push_back(R.spill);
+    R.spill = kNone;
+  }
+  R.n = 0;
 }
 
 void SubscriptionTree::touch(uint32_t p) {
@@ -38,21 +71,37 @@ bool SubscriptionTree::reachable_memo(uint32_t p) {
       ok = true;
       break;
     }
-    if (reach_stamp_[p] == no || state_[p] != PeerState::In || up_[p] == kNone) break;
+    if (reach_stamp_[p] == no || rec_[p].state != PeerState::In || rec_[p].up == kNone) break;
     walk_.push_back(p);
-    p = up_[p];
+    p = rec_[p].up;
   }
   for (uint32_t q : walk_) reach_stamp_[q] = ok ? yes : no;
   return ok;
 }
 
-bool SubscriptionTree::below_orphan(uint32_t p) const {
+// Memoised over one pass like reachable_memo (unreached Part'ed parents of a
+// decayed tree share their upstream paths): orphan_stamp_ = 2*pass + 1 for
+// "an Orphan cuts the path", 2*pass for "it does not".
+bool SubscriptionTree::below_orphan(uint32_t p) {
+  const uint32_t no = 2 * reach_pass_, yes = no + 1;
+  if (orphan_stamp_.size() != n_) orphan_stamp_.assign(n_, 0xFFFFFFFFu);
+  walk_.clear();
+  bool cut = false;
   for (uint32_t hops = 0; hops <= n_ && p != root_ && p != kNone; ++hops) {
-    if (state_[p] == PeerState::Orphan) return true;
-    if (state_[p] != PeerState::In) return false;
-    p = up_[p];
+    if (orphan_stamp_[p] == yes || orphan_stamp_[p] == no) {
+      cut = orphan_stamp_[p] == yes;
+      break;
+    }
+    if (rec_[p].state == PeerState::Orphan) {
+      cut = true;
+      break;
+    }
+    if (rec_[p].state != PeerState::In) break;
+    walk_.push_back(p);
+    p = rec_[p].up;
   }
-  return false;
+  for (uint32_t q : walk_) orphan_stamp_[q] = cut ? yes : no;
+  return cut;
 }
 
 // SplitMix64: stands in for Go's randomised map iteration (rule Q2).
@@ -68,36 +117,36 @@ uint64_t SubscriptionTree::next_random() {
 // joinParents (241-307) at prio=false.
 int SubscriptionTree::attach(uint32_t at, uint32_t joiner, bool prio) {
   while (true) {
-    auto& list = kids_[at];
+    const uint32_t cnt = rec_[at].n;
     const size_t cap = prio ? max_width_ : width_;
-    if (list.size() < cap) {
-      list.push_back(ChildRec{joiner, kNone, 0, false});
-      up_[joiner] = at;
-      state_[joiner] = PeerState::In;
+    if (cnt < cap) {
+      kid_push(at, ChildRec{joiner, kNone, 0, 0});
+      rec_[joiner].up = at;
+      rec_[joiner].state = PeerState::In;
       touch(joiner);
       // State{Peers:[joiner], NumPeers: sub.size(=0)} upstream (137-147);
       // only a node holding a live `in` stream sends it (client.go:106).
-      const uint32_t gp = up_[at];
-      if (at != root_ && gp != kNone && state_[at] == PeerState::In) {
-        for (auto& r : kids_[gp])
-          if (r.id == at) {
-            r.redirects = 1;
-            r.last_state = joiner;
+      const uint32_t gp = rec_[at].up;
+      if (at != root_ && gp != kNone && rec_[at].state == PeerState::In) {
+        ChildRec* k = kids(gp);
+        for (uint32_t i = 0, m = rec_[gp].n; i < m; ++i)
+          if (k[i].id == at) {
+            k[i].redirects = 1;
+            k[i].last_state = joiner;
             break;
           }
       }
       return PS_OK;
     }
-    if (list.empty()) return PS_E_NOPARENT;
+    if (cnt == 0) return PS_E_NOPARENT;
+    ChildRec* list = kids(at);
     // the walk continues at one of these children: start fetching their
-    // entries while the redirect choice is made
-    for (const auto& r : list) {
-      __builtin_prefetch(&kids_[r.id]);
-      __builtin_prefetch(&state_[r.id]);
-    }
+    // lines (state, upstream, child list) while the redirect choice is made
+    for (uint32_t i = 0; i < cnt; ++i) __builtin_prefetch(&rec_[list[i].id]);
     int64_t best = 10000000000ll;
     uint32_t ties = 0;
-    for (const auto& r : list) {
+    for (uint32_t i = 0; i < cnt; ++i) {
+      const ChildRec& r = list[i];
       if (r.parted) continue;
       if (r.redirects < best) {
         best = r.redirects;
@@ -109,7 +158,8 @@ int SubscriptionTree::attach(uint32_t at, uint32_t joiner, bool prio) {
     if (ties == 0) return PS_E_NOPARENT;
     uint32_t k = ties > 1 ? static_cast<uint32_t>(next_random() % ties) : 0;
     ChildRec* pick = nullptr;
-    for (auto& r : list) {
+    for (uint32_t i = 0; i < cnt; ++i) {
+      ChildRec& r = list[i];
       if (r.parted || r.redirects != best) continue;
       if (k-- == 0) {
         pick = &r;
@@ -118,7 +168,7 @@ int SubscriptionTree::attach(uint32_t at, uint32_t joiner, bool prio) {
     }
     pick->redirects += 1;
     const uint32_t target = pick->id;
-    if (state_[target] == PeerState::Failed) return PS_E_UNREACHABLE;
+    if (rec_[target].state == PeerState::Failed) return PS_E_UNREACHABLE;
     at = target;
     prio = false;
   }
@@ -126,7 +176,7 @@ int SubscriptionTree::attach(uint32_t at, uint32_t joiner, bool prio) {
 
 int SubscriptionTree::subscribe(uint32_t peer) {
   if (peer >= n_) return PS_E_INVAL;
-  if (peer == root_ || state_[peer] != PeerState::Out) return PS_E_STATE;
+  if (peer == root_ || rec_[peer].state != PeerState::Out) return PS_E_STATE;
   return attach(root_, peer, false);
 }
 
@@ -134,40 +184,45 @@ int SubscriptionTree::subscribe(uint32_t peer) {
 // the last one `gone` reported (`rescue`) is re-joined at `at` with prio
 // (redistributeChildren, subtree.go:356-375); the rest are orphaned (Q5).
 void SubscriptionTree::depart(uint32_t at, uint32_t gone, uint32_t rescue) {
-  for (const auto& r : kids_[gone])
-    if (r.id != rescue && state_[r.id] == PeerState::In) {
-      state_[r.id] = PeerState::Orphan;
-      touch(r.id);
-    }
-  kids_[gone].clear();
+  {
+    const ChildRec* k = kids(gone);
+    for (uint32_t i = 0, m = rec_[gone].n; i < m; ++i)
+      if (k[i].id != rescue && rec_[k[i].id].state == PeerState::In) {
+        rec_[k[i].id].state = PeerState::Orphan;
+        touch(k[i].id);
+      }
+  }
+  kid_clear(gone);
   if (rescue == kNone) return;
-  if (state_[rescue] != PeerState::In || up_[rescue] != gone) return;
-  state_[rescue] = PeerState::Out;
+  if (rec_[rescue].state != PeerState::In || rec_[rescue].up != gone) return;
+  rec_[rescue].state = PeerState::Out;
   touch(rescue);
   if (attach(at, rescue, true) != PS_OK) {
-    state_[rescue] = PeerState::Orphan;
-    up_[rescue] = gone;
+    rec_[rescue].state = PeerState::Orphan;
+    rec_[rescue].up = gone;
   }
 }
 
 int SubscriptionTree::close_client(uint32_t peer) {
   if (peer >= n_) return PS_E_INVAL;
-  if (peer == root_ || state_[peer] != PeerState::In) return PS_E_STATE;
-  const uint32_t at = up_[peer];
-  state_[peer] = PeerState::Dead;
+  if (peer == root_ || rec_[peer].state != PeerState::In) return PS_E_STATE;
+  const uint32_t at = rec_[peer].up;
+  rec_[peer].state = PeerState::Dead;
   touch(peer);
   ChildRec* rec = nullptr;
-  if (at != kNone && state_[at] != PeerState::Failed)  // a Part to a closed host is lost
-    for (auto& r : kids_[at])
-      if (r.id == peer) {
-        rec = &r;
+  if (at != kNone && rec_[at].state != PeerState::Failed) {  // a Part to a closed host is lost
+    ChildRec* k = kids(at);
+    for (uint32_t i = 0, m = rec_[at].n; i < m; ++i)
+      if (k[i].id == peer) {
+        rec = &k[i];
         break;
       }
+  }
   if (rec == nullptr) {
     depart(at, peer, kNone);
     return PS_OK;
   }
-  rec->parted = true;  // handleChildMessages Part (subtree.go:62-70)
+  rec->parted = 1;  // handleChildMessages Part (subtree.go:62-70)
   needs_pass_ = true;
   parted_at_.push_back(at);
   depart(at, peer, rec->last_state);
@@ -177,25 +232,26 @@ int SubscriptionTree::close_client(uint32_t peer) {
 void SubscriptionTree::prefetch_leave(uint32_t peer, int stage) const {
   if (peer >= n_) return;
   if (stage == 0) {
-    __builtin_prefetch(&state_[peer]);
-    __builtin_prefetch(&up_[peer]);
-    __builtin_prefetch(&kids_[peer]);
+    __builtin_prefetch(&rec_[peer]);
     return;
   }
-  if (!kids_[peer].empty()) __builtin_prefetch(kids_[peer].data());
-  const uint32_t at = up_[peer];
+  const PeerRec& R = rec_[peer];
+  if (R.spill != kNone) __builtin_prefetch(spill_[R.spill].data());
+  const uint32_t at = R.up;
   if (at < n_) {
-    __builtin_prefetch(&kids_[at]);
-    __builtin_prefetch(&state_[at]);
-    if (!kids_[at].empty()) __builtin_prefetch(kids_[at].data());
+    __builtin_prefetch(&rec_[at]);
+    if (rec_[at].spill != kNone) __builtin_prefetch(spill_[rec_[at].spill].data());
   }
+  // the rescued child re-joins at `at`; the orphans' lines are written
+  const ChildRec* k = kids(peer);
+  for (uint32_t i = 0, m = R.n; i < m; ++i) __builtin_prefetch(&rec_[k[i].id]);
 }
 
 int SubscriptionTree::close_host(uint32_t peer) {
   if (peer >= n_) return PS_E_INVAL;
   if (peer == root_) return PS_E_STATE;
-  if (state_[peer] != PeerState::In && state_[peer] != PeerState::Orphan) return PS_E_STATE;
-  state_[peer] = PeerState::Failed;
+  if (rec_[peer].state != PeerState::In && rec_[peer].state != PeerState::Orphan) return PS_E_STATE;
+  rec_[peer].state = PeerState::Failed;
   touch(peer);
   pending_failures_ = true;
   needs_pass_ = true;
@@ -217,6 +273,7 @@ int SubscriptionTree::after_message(const ReachQuery* reach) {
     if (reach_stamp_.size() != n_) reach_stamp_.assign(n_, 0xFFFFFFFFu);
     if (++reach_pass_ >= 0x7FFFFFF0u) {
       std::fill(reach_stamp_.begin(), reach_stamp_.end(), 0xFFFFFFFFu);
+      std::fill(orphan_stamp_.begin(), orphan_stamp_.end(), 0xFFFFFFFFu);
       reach_pass_ = 1;
     }
     std::vector<uint8_t> reached(parted_at_.size());
@@ -236,21 +293,21 @@ int SubscriptionTree::after_message(const ReachQuery* reach) {
         if (p < n_ && !below_orphan(p)) keep.push_back(p);
         continue;
       }
-      auto& list = kids_[p];
-      size_t w = 0;
-      for (size_t k = 0; k < list.size(); ++k) {
+      ChildRec* list = kids(p);
+      uint32_t w = 0;
+      for (uint32_t k = 0, m = rec_[p].n; k < m; ++k) {
         const ChildRec r = list[k];
         if (r.parted) {
-          if (state_[r.id] == PeerState::Dead) {
-            state_[r.id] = PeerState::Out;
-            up_[r.id] = kNone;
+          if (rec_[r.id].state == PeerState::Dead) {
+            rec_[r.id].state = PeerState::Out;
+            rec_[r.id].up = kNone;
             touch(r.id);
           }
           continue;
         }
         list[w++] = r;
       }
-      list.resize(w);
+      kid_shrink(p, w);
     }
     parted_at_.swap(keep);
     needs_pass_ = !parted_at_.empty();
@@ -264,30 +321,30 @@ int SubscriptionTree::after_message(const ReachQuery* reach) {
     uint32_t p = q.front();
     q.pop_front();
     order.push_back(p);
-    for (const auto& r : kids_[p])
-      if (state_[r.id] == PeerState::In) q.push_back(r.id);
+    for (const ChildRec& r : children(p))
+      if (rec_[r.id].state == PeerState::In) q.push_back(r.id);
   }
   for (uint32_t p : order) {
-    auto& list = kids_[p];
+    ChildRec* list = kids(p);
     std::vector<ChildRec> failed;
-    size_t w = 0;
-    for (size_t i = 0; i < list.size(); ++i) {
+    uint32_t w = 0;
+    for (uint32_t i = 0, m = rec_[p].n; i < m; ++i) {
       ChildRec r = list[i];
       if (r.parted) {  // delete(sub.children, c.id), subtree.go:329-331
-        if (state_[r.id] == PeerState::Dead) {
-          state_[r.id] = PeerState::Out;
-          up_[r.id] = kNone;
+        if (rec_[r.id].state == PeerState::Dead) {
+          rec_[r.id].state = PeerState::Out;
+          rec_[r.id].up = kNone;
           touch(r.id);
         }
         continue;
       }
-      if (state_[r.id] == PeerState::Failed) {  // write error, subtree.go:333-336
+      if (rec_[r.id].state == PeerState::Failed) {  // write error, subtree.go:333-336
         failed.push_back(r);
         continue;
       }
       list[w++] = r;
     }
-    list.resize(w);
+    kid_shrink(p, w);
     for (const auto& r : failed) depart(p, r.id, r.last_state);  // 342-349
   }
   pending_failures_ = false;
@@ -295,7 +352,7 @@ int SubscriptionTree::after_message(const ReachQuery* reach) {
   // Part'ed entries under parents this message did not reach stay listed
   std::vector<uint32_t> keep;
   for (uint32_t p : parted_at_)
-    for (const auto& r : kids_[p])
+    for (const ChildRec& r : children(p))
       if (r.parted) {
         keep.push_back(p);
         needs_pass_ = true;
@@ -303,8 +360,8 @@ int SubscriptionTree::after_message(const ReachQuery* reach) {
       }
   parted_at_.swap(keep);
   for (uint32_t p = 0; p < n_ && !pending_failures_; ++p)
-    if (state_[p] == PeerState::Failed && up_[p] != kNone) {
-      for (const auto& r : kids_[up_[p]])
+    if (rec_[p].state == PeerState::Failed && rec_[p].up != kNone) {
+      for (const ChildRec& r : children(rec_[p].up))
         if (r.id == p) {
           pending_failures_ = true;
           needs_pass_ = true;
@@ -320,8 +377,8 @@ void SubscriptionTree::attached_parents(std::vector<uint32_t>& parent) const {
   while (!stack.empty()) {
     uint32_t p = stack.back();
     stack.pop_back();
-    for (const auto& r : kids_[p])
-      if (state_[r.id] == PeerState::In) {
+    for (const ChildRec& r : children(p))
+      if (rec_[r.id].state == PeerState::In) {
         parent[r.id] = p;
         stack.push_back(r.id);
       }

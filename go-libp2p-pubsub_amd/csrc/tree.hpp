@@ -20,8 +20,17 @@ enum class PeerState : uint8_t { Out = 0, In = 1, Dead = 2, Failed = 3, Orphan =
 struct ChildRec {
   uint32_t id;
   uint32_t last_state;  // `children` of the last State message (one peer)
-  int64_t redirects;    // `size`: reset to NumPeers+1 = 1 by State, ++ per redirect
-  bool parted;          // `dead`: set by a Part message
+  int32_t redirects;    // `size`: reset to NumPeers+1 = 1 by State, ++ per redirect
+  uint32_t parted;      // `dead`: set by a Part message
+};
+
+// A peer's child records, in insertion order (iteration only).
+struct ChildSpan {
+  const ChildRec* b;
+  const ChildRec* e;
+  const ChildRec* begin() const { return b; }
+  const ChildRec* end() const { return e; }
+  size_t size() const { return static_cast<size_t>(e - b); }
 };
 
 class SubscriptionTree {
@@ -37,10 +46,7 @@ class SubscriptionTree {
   // peer's own entries, stage 1 (a few peers later) its child lists and its
   // parent's list, so close_client() finds them resident.
   void prefetch_leave(uint32_t peer, int stage) const;
-  void prefetch_peer(uint32_t peer) const {  // state and upstream (in_parent)
-    __builtin_prefetch(&state_[peer]);
-    __builtin_prefetch(&up_[peer]);
-  }
+  void prefetch_peer(uint32_t peer) const { __builtin_prefetch(&rec_[peer]); }  // state, upstream, children
   int close_host(uint32_t peer);    // abrupt
   // Called once per message that floods this topic: lazy prune and repair of
   // failed writes at every node the message reached (rule Q3).  `reach`, if
@@ -52,6 +58,7 @@ class SubscriptionTree {
   bool has_pending_failures() const { return pending_failures_; }
   // a Part or a host failure happened since the last after_message()
   bool needs_message_pass() const { return needs_pass_; }
+  size_t parted_parents() const { return parted_at_.size(); }  // pending lazy prunes (diagnostics)
 
   // Attached structure: parent of every peer reachable from the root through
   // subscribed peers, kNone elsewhere.
@@ -59,12 +66,17 @@ class SubscriptionTree {
   // Upstream of every subscribed (In) peer, kNone elsewhere; reachability from
   // the root is left to the consumer (the GPU rebuild).  take_touched() hands
   // out the peers whose entry may have changed since the last call.
-  uint32_t in_parent(uint32_t p) const { return state_[p] == PeerState::In && p != root_ ? up_[p] : kNone; }
+  uint32_t in_parent(uint32_t p) const {
+    return rec_[p].state == PeerState::In && p != root_ ? rec_[p].up : kNone;
+  }
   void take_touched(std::vector<uint32_t>& out);
   // Peers reachable for the NEXT message (failed hosts cut their subtree).
   // Children lists in insertion order.
-  const std::vector<ChildRec>& children(uint32_t p) const { return kids_[p]; }
-  PeerState state(uint32_t p) const { return state_[p]; }
+  ChildSpan children(uint32_t p) const {
+    const ChildRec* k = kids(p);
+    return ChildSpan{k, k + rec_[p].n};
+  }
+  PeerState state(uint32_t p) const { return rec_[p].state; }
   uint32_t root() const { return root_; }
   uint32_t n_peers() const { return n_; }
 
@@ -76,8 +88,30 @@ class SubscriptionTree {
   // In-state path from the root?  Memoised over one pass: every peer on a
   // walked path is stamped reachable / unreachable (top levels are shared).
   bool reachable_memo(uint32_t p);
-  bool below_orphan(uint32_t p) const;  // an Orphan on the upstream path (cut for good)
+  bool below_orphan(uint32_t p);  // an Orphan on the upstream path (cut for good); memoised per pass
   void touch(uint32_t p);             // (state, upstream) of p may have changed
+
+  // One cache line per peer: upstream, state and (up to kInline) child
+  // records, so a join walk touches one line per level (and prefetches the
+  // candidate children's lines while it picks among them).  Longer lists
+  // (prio re-joins up to MaxWidth, wide trees) live in spill_.
+  static constexpr uint32_t kInline = 3;
+  struct alignas(64) PeerRec {
+    uint32_t up = kNone;  // upstream peer (the other end of `in`)
+    PeerState state = PeerState::Out;
+    uint8_t pad = 0;
+    uint16_t n = 0;          // children
+    uint32_t spill = kNone;  // index into spill_, or kNone: the records are inline
+    ChildRec kin[kInline];
+  };
+  static_assert(sizeof(PeerRec) == 64, "one cache line per peer");
+  ChildRec* kids(uint32_t p) { return rec_[p].spill == kNone ? rec_[p].kin : spill_[rec_[p].spill].data(); }
+  const ChildRec* kids(uint32_t p) const {
+    return rec_[p].spill == kNone ? rec_[p].kin : spill_[rec_[p].spill].data();
+  }
+  void kid_push(uint32_t p, const ChildRec& r);
+  void kid_clear(uint32_t p);
+  void kid_shrink(uint32_t p, uint32_t n) { rec_[p].n = static_cast<uint16_t>(n); }
 
   uint32_t n_ = 0, root_ = 0, width_ = 2, max_width_ = 5;
   uint64_t rng_ = 0;
@@ -87,11 +121,12 @@ class SubscriptionTree {
   std::vector<uint32_t> touched_;    // peers whose attachment may have changed
   std::vector<uint8_t> touched_mark_;
   std::vector<uint32_t> reach_stamp_;  // 2*pass: reachable, 2*pass+1: not (reachable_memo)
+  std::vector<uint32_t> orphan_stamp_;  // 2*pass: not cut, 2*pass+1: cut (below_orphan)
   uint32_t reach_pass_ = 0;
   std::vector<uint32_t> walk_;
-  std::vector<PeerState> state_;
-  std::vector<uint32_t> up_;  // upstream peer (the other end of `in`)
-  std::vector<std::vector<ChildRec>> kids_;
+  std::vector<PeerRec> rec_;
+  std::vector<std::vector<ChildRec>> spill_;
+  std::vector<uint32_t> spill_free_;
 };
 
 }  // namespace psamd
