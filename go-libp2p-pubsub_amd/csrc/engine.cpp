@@ -2635,6 +2635,9 @@ int run_body(ps_engine* e, ps_stats* stp, bool may_defer) {
                 "reach query");
         HIP_TRY(hipMemcpyAsync(outv.data(), dout, k, hipMemcpyDeviceToHost, e->stream), "read reach query");
         HIP_TRY(hipStreamSynchronize(e->stream), "sync");
+        if (e->host_timing)
+          std::fprintf(stderr, "[psengine] prune reach query: %u parents, done at %.3f ms\n", k,
+                       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - e->t_run0).count());
         return PS_OK;
       };
       int rc = T.tree.after_message(gpu_reach ? &q : nullptr);
@@ -2644,8 +2647,9 @@ int run_body(ps_engine* e, ps_stats* stp, bool may_defer) {
   }
   e->have_hops = record;
   if (e->host_timing)
-    std::fprintf(stderr, "[psengine] after-message prune %.3f ms\n",
-                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_am).count());
+    std::fprintf(stderr, "[psengine] after-message prune %.3f ms (started at %.3f ms)\n",
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_am).count(),
+                 std::chrono::duration<double, std::milli>(t_am - e->t_run0).count());
   st.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
   return PS_OK;
 }
