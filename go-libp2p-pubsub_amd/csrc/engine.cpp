@@ -1078,20 +1078,25 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
 // rank's pack entries (its parents to ship, with their record offsets in the
 // send buffer) and each ghost-fed node's row offset in the receive buffer
 // follow.  Cached per node space, start rounds and row widths.
-int build_ghost_plan(ps_engine* e, const std::vector<TopicDev>& tab, const std::vector<uint32_t>& tstart,
-                     uint32_t rounds) {
+int build_ghost_plan(ps_engine* e, const std::vector<TopicDev>& tab, const std::vector<uint32_t>& wglob,
+                     const std::vector<uint32_t>& tstart, uint32_t rounds) {
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
   const int32_t world = e->world, me = e->rank;
+  // Every size here is computed from message-derived widths (wglob) and the
+  // global cross counts, identically on every rank -- also on a rank that
+  // owns none of a topic's nodes (its tab entry is idle): the ranks must agree
+  // on which rounds exchange and on every region's size.
   std::vector<uint64_t> key{e->graph_epoch, rounds};
   for (uint32_t t = 0; t < nt; ++t) {
-    key.push_back(tab[t].W ? tstart[t] : ~0ull);
+    key.push_back(wglob[t] ? tstart[t] : ~0ull);
+    key.push_back(wglob[t]);
     key.push_back(tab[t].W);
   }
   if (key == e->ghost_key) return PS_OK;
   e->ghost_key.clear();
   auto level_of = [&](uint32_t q, uint32_t t) -> uint32_t {  // level written in round q, 0: none
     const TopicHost& T = e->topics[t];
-    if (!tab[t].W || !T.exists || q <= tstart[t] || T.gcnt.empty()) return 0;
+    if (!wglob[t] || !T.exists || q <= tstart[t] || T.gcnt.empty()) return 0;
     const uint32_t d = q - tstart[t];
     return d <= T.depth ? d : 0;
   };
@@ -1120,7 +1125,7 @@ int build_ghost_plan(ps_engine* e, const std::vector<TopicDev>& tab, const std::
       for (uint32_t t = 0; t < nt; ++t) {
         rec_off[static_cast<size_t>(peer) * nt + t] = words;
         const uint32_t d = level_of(q, t);
-        if (d) words += gcnt(t, d, a, b) * ghost_record_words(tab[t].W);
+        if (d) words += gcnt(t, d, a, b) * ghost_record_words(wglob[t]);
       }
       return words * 8;
     };
@@ -1151,7 +1156,7 @@ int build_ghost_plan(ps_engine* e, const std::vector<TopicDev>& tab, const std::
       const uint32_t d = level_of(q, t);
       if (!d) continue;
       const TopicHost& T = e->topics[t];
-      const uint32_t W = tab[t].W, rw = ghost_record_words(W);
+      const uint32_t W = wglob[t], rw = ghost_record_words(W);
       const uint32_t e0 = static_cast<uint32_t>(e->pack_host.size());
       for (uint32_t i = T.send_lvl[d]; i < T.send_lvl[d + 1]; ++i) {
         const uint32_t b = T.send_dst[i] >> kRemoteRankShift, k = T.send_dst[i] & kRemoteIdMask;
@@ -1184,7 +1189,7 @@ int build_ghost_plan(ps_engine* e, const std::vector<TopicDev>& tab, const std::
       const uint32_t d = level_of(q, t);
       if (!d) continue;
       const TopicHost& T = e->topics[t];
-      const uint32_t W = tab[t].W, rw = ghost_record_words(W);
+      const uint32_t W = wglob[t], rw = ghost_record_words(W);
       for (uint32_t u = T.nbase + T.level_off[d]; u < T.nbase + T.level_off[d + 1]; ++u) {
         const uint32_t g = e->ghost_ref[u];
         if (g == kNone) continue;
@@ -1492,6 +1497,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   std::vector<uint32_t> tstart(std::max<uint32_t>(nt, 1), 0);  // single-start topics
   std::vector<std::vector<StartGroup>> groups(std::max<uint32_t>(nt, 1));
   std::vector<std::vector<uint32_t>> pos(std::max<uint32_t>(nt, 1));  // window slot -> row bit
+  bool multi_any = false;  // some topic's window has several start rounds
+  std::vector<uint32_t> wglob(std::max<uint32_t>(nt, 1), 0);  // row words of every active topic, on every rank
   for (uint32_t t = 0; t < nt; ++t) {
     const TopicHost& T = e->topics[t];
     TopicDev& d = tab[t];
@@ -1512,11 +1519,17 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     if (e->run_zero_start) s_lo = s_hi = 0;
     max_start = std::max(max_start, s_hi);
     const bool one_start = s_lo == s_hi;
+    // (decided from the window's messages alone: the same on every rank,
+    // also on one that owns none of the topic's nodes)
+    multi_any |= !one_start && !T.mesh;
     // a tree topic whose window messages share one start round: every node
     // receives once, so arrival rows are its seen rows (kTopicSingleStart)
     if (one_start && !T.mesh) d.flags |= kTopicSingleStart;
     tstart[t] = msgs[win[t].idx[0]].start;
-    if (T.n_nodes == 0) continue;
+    // (the row layout depends on the window's messages only: every rank
+    // computes the same W, also one that owns none of the topic's nodes --
+    // its tab entry then stays idle, W = 0, but wglob keeps the width the
+    // cross-rank sizes are computed with)
     if (one_start || T.mesh) {
       d.W = ceil_div(win[t].n, 64);
       d.w_msgs = d.W;
@@ -1553,6 +1566,11 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         const uint32_t k = msgs[win[t].idx[li]].start - s_lo;
         P[li] = wfirst[k] * 64 + fill[k]++;
       }
+    }
+    wglob[t] = d.W;
+    if (T.n_nodes == 0) {
+      d.W = d.w_msgs = 0;
+      continue;
     }
     wtot = (wtot + 15) & ~15ull;  // topic blocks start on a 128-B line
     d.wbase = wtot;
@@ -1595,8 +1613,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // one rank, one k_pull launch per round over every group's level of that
   // round, its blocks stored group-major; PS_F_COMPACT sends every window
   // through the compaction path.
-  bool multi = false;
-  for (uint32_t t = 0; t < nt; ++t) multi |= tab[t].W && groups[t].size() > 1;
+  const bool multi = multi_any;
   const bool level =
       !(e->cfg.flags & PS_F_COMPACT) && !any_mesh && planned0 + 1 < round_cap && !(multi && world > 1);
   std::vector<GroupDev> gtab;  // start groups of the group-major topics
@@ -1696,7 +1713,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       while (flood_rounds < planned0 && e->pull_bytes[flood_rounds + 1] <= e->flood_top_bytes) ++flood_rounds;
       if (flood_rounds) rc2 = build_flood_tasks(e, tab, tstart, flood_rounds);
     }
-    if (!rc2 && world > 1) rc2 = build_ghost_plan(e, tab, tstart, planned0);
+    if (!rc2 && world > 1) rc2 = build_ghost_plan(e, tab, wglob, tstart, planned0);
     if (rc2) return rc2;
     // desc[3q..]: round q's partial slots (first, end, stride) for the reduce
     auto& desc = e->desc_host;
@@ -1738,7 +1755,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     for (uint32_t t = 0; t < nt; ++t) {
       const TopicHost& T = e->topics[t];
       if (starts_of[t].empty()) continue;
-      const uint64_t Wt = tab[t].W;
+      const uint64_t Wt = wglob[t];
       for (const auto& c : T.cross)
         for (uint32_t s0 = 0; s0 <= max_start; ++s0) {
           const uint32_t r = c.level + 1 + s0;
@@ -1964,6 +1981,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         a.a_next = arr[r & 1];
         // multi-GPU: this round's ghost parents (rows written last round, or
         // seeded roots) to the ranks owning their children, then the exchange
+        if (world > 1 && e->host_timing)
+          std::fprintf(stderr, "[psengine] rank %d round %u/%u: ghost exchange %d\n", me, r, planned0,
+                       static_cast<int>(e->ghost_rounds[r].any));
         if (world > 1 && e->ghost_rounds[r].any) {
           const auto& R = e->ghost_rounds[r];
           if (R.seg1 > R.seg0) {

@@ -3,8 +3,11 @@
 (oracle/psoracle.c), wider than the pytest suite: random trees and meshes,
 live masks, staggered or single start rounds, several topics, small windows
 (many windows per run), eager / lazy seen, pipelined runs, churn sequences
-on restated join trees, 2-4 ranks on the loopback transport, and
-per-subscriber drains.  Every case is bit-exact or the
+on restated join trees, 2-4 ranks on the loopback transport, per-subscriber
+drains, and every execution mode on the same inputs (k_flood with random
+k_flood / k_pull splits and task sizes, per-round k_pull, start groups, the
+compaction path): identical deliveries, per-round counts and seen digests
+on the production (non-recording) instance.  Every case is bit-exact or the
 script reports it (seed and case) and exits non-zero.
 
     python tools/fuzz_gpu.py [--cases 300] [--seed 0] [--max-peers 4000]
@@ -57,7 +60,10 @@ def case_topology(rng, max_peers):
     starts = rng.integers(0, 5, size=n_msgs) if staggered else None
     topics = rng.integers(0, n_topics, size=n_msgs)
     window = int(rng.choice([64, 200, 65536]))
-    flags = PE.F_NO_LAZY_SEEN if rng.random() < 0.2 else 0
+    flags = (PE.F_NO_LAZY_SEEN if rng.random() < 0.2 else 0) | (PE.F_COMPACT if rng.random() < 0.2 else 0)
+    if staggered and rng.random() < 0.5:
+        starts = rng.integers(0, 9, size=n_msgs)
+    set_modes(rng)
     record = True
     pipelined = rng.random() < 0.3
     with PE.Engine(n, n_topics, record_hops=record, msg_window=window, flags=flags) as e:
@@ -95,6 +101,67 @@ def case_topology(rng, max_peers):
                     return f"topic {t} msg {m}: peers {bad} engine {got[bad]} oracle {hops[0][bad]}"
         if st.deliveries != total:
             return f"deliveries {st.deliveries} != oracle {total}"
+    return None
+
+
+MODE_ENV = ("PSAMD_FLOOD", "PSAMD_FLOOD_TOP_BYTES", "PSAMD_FLOOD_WORDS")
+
+
+def set_modes(rng):
+    """Random execution-mode switches for the next engine (read at creation)."""
+    for k in MODE_ENV:
+        os.environ.pop(k, None)
+    if rng.random() < 0.2:
+        os.environ["PSAMD_FLOOD"] = "0"
+    if rng.random() < 0.4:
+        os.environ["PSAMD_FLOOD_TOP_BYTES"] = str(int(rng.choice([0, 256, 4096, 65536])))
+    if rng.random() < 0.3:
+        os.environ["PSAMD_FLOOD_WORDS"] = str(int(rng.choice([64, 256, 4096])))
+
+
+def case_modes(rng, max_peers):
+    """One set of trees, live mask and publishes (single or staggered
+    starts) through every mode, production instances: the same deliveries,
+    per-round deliveries and seen digest, and the oracle's deliveries."""
+    n = int(rng.integers(2, max_peers))
+    n_topics = int(rng.integers(1, 5))
+    live = (rng.random(n) > rng.choice([0.0, 0.05, 0.3])).astype(np.uint8)
+    n_msgs = int(rng.integers(1, 900))
+    starts = rng.integers(0, int(rng.integers(1, 9)), size=n_msgs) if rng.random() < 0.6 else None
+    topics = rng.integers(0, n_topics, size=n_msgs)
+    trees = []
+    for _ in range(n_topics):
+        root = int(rng.integers(0, n))
+        trees.append((root, random_tree(rng, n, root)))
+    total = 0
+    for t, (root, par) in enumerate(trees):
+        rp, cl = O.parents_to_csr(par)
+        tot, _, _ = O.disseminate(rp, cl, root, live, 1, want_hops=False)
+        total += tot * int((topics == t).sum())
+    ref = None
+    window = int(rng.choice([128, 65536]))
+    modes = [({}, 0), ({}, PE.F_COMPACT), ({"PSAMD_FLOOD": "0"}, 0),
+             ({"PSAMD_FLOOD_TOP_BYTES": str(int(rng.choice([0, 512, 1 << 30])))}, 0),
+             ({"PSAMD_FLOOD_WORDS": "64"}, 0)]
+    for env, flags in modes:
+        for k in MODE_ENV:
+            os.environ.pop(k, None)
+        os.environ.update(env)
+        with PE.Engine(n, n_topics, flags=flags, msg_window=window) as e:
+            for t, (root, par) in enumerate(trees):
+                e.set_tree(t, root, par)
+            e.set_live(live)
+            e.publish(topics, starts)
+            st = e.run()
+            key = (st.deliveries, st.duplicates, st.as_dict()["deliveries_per_round"], e.seen_digest())
+        if st.deliveries != total:
+            return f"mode {env} flags {flags}: deliveries {st.deliveries} != oracle {total}"
+        if ref is None:
+            ref = key
+        elif key != ref:
+            return f"mode {env} flags {flags}: counters or digest differ from the default mode"
+    for k in MODE_ENV:
+        os.environ.pop(k, None)
     return None
 
 
@@ -189,7 +256,7 @@ def case_dist(rng, max_peers):
         if any(x.is_alive() for x in th):
             return "rank thread hung"
         if errs:
-            return f"rank error: {errs[0]}"
+            return "rank errors: " + " | ".join(str(x) for x in errs)
         total = 0
         for t, (par, root) in enumerate(trees):
             idx = np.nonzero(topics == t)[0]
@@ -244,17 +311,21 @@ def main():
     ap.add_argument("--cases", type=int, default=300)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--max-peers", type=int, default=4000)
+    ap.add_argument("--only", type=int, nargs="*", help="run just these case numbers (reproduce a failure)")
     args = ap.parse_args()
     fails = 0
     t0 = time.time()
-    for c in range(args.cases):
+    for c in (args.only if args.only else range(args.cases)):
         rng = np.random.default_rng([args.seed, c])
-        kind = ("topology", "churn", "dist", "topology", "drain")[c % 5]
-        fn = {"topology": case_topology, "churn": case_churn, "dist": case_dist, "drain": case_drain}[kind]
+        kind = ("topology", "churn", "dist", "topology", "drain", "modes")[c % 6]
+        fn = {"topology": case_topology, "churn": case_churn, "dist": case_dist, "drain": case_drain,
+              "modes": case_modes}[kind]
         try:
             err = fn(rng, args.max_peers)
         except PE.EngineError as ex:
             err = f"engine error: {ex}"
+        for k in MODE_ENV:
+            os.environ.pop(k, None)
         if err:
             fails += 1
             print(f"FAIL case {c} ({kind}, seed {args.seed}): {err}", flush=True)
