@@ -1255,13 +1255,16 @@ int build_ghost_plan(ps_engine* e, const std::vector<TopicDev>& tab, const std::
 // into the parent range and its granules.  Per round, the tasks share
 // min(256, tasks) counter slots (slot 0 is the window's timeout word).
 // Cached per node space, rounds, start rounds and row widths.
-int build_flood_tasks(ps_engine* e, const std::vector<TopicDev>& tab, const std::vector<uint32_t>& tstart,
-                      uint32_t rounds) {
+int build_flood_tasks(ps_engine* e, const std::vector<TopicDev>& tab,
+                      const std::vector<std::vector<StartGroup>>& groups, uint32_t rounds) {
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
   std::vector<uint64_t> key{e->graph_epoch, rounds, e->flood_words};
   for (uint32_t t = 0; t < nt; ++t) {
-    key.push_back(tab[t].W ? tstart[t] : ~0ull);
+    key.push_back(tab[t].W ? groups[t].size() : ~0ull);
     key.push_back(tab[t].W);
+    key.push_back(tab[t].wbase << 1 | ((tab[t].flags & kTopicGroups) ? 1 : 0));
+    if (tab[t].W)
+      for (const StartGroup& g : groups[t]) key.push_back(static_cast<uint64_t>(g.start) << 32 | g.w0);
   }
   if (key == e->flood_key) return PS_OK;
   e->flood_key.clear();
@@ -1271,43 +1274,54 @@ int build_flood_tasks(ps_engine* e, const std::vector<TopicDev>& tab, const std:
   SG.clear();
   e->flood_slot0.assign(rounds + 2, 0);
   e->flood_nslot.assign(rounds + 2, 0);
-  std::vector<uint32_t> seg_prev(nt, kNone);  // each topic's segment of the previous round
+  // each (topic, start group)'s segment of the previous round
+  std::vector<std::vector<uint32_t>> seg_prev(nt);
+  for (uint32_t t = 0; t < nt; ++t) seg_prev[t].assign(groups[t].size(), kNone);
   uint32_t slot = 1, gran = 0;
   for (uint32_t q = 1; q <= rounds; ++q) {
     const size_t first = TK.size();
     for (uint32_t t = 0; t < nt; ++t) {
       const TopicHost& T = e->topics[t];
-      const uint32_t W = tab[t].W;
-      if (W == 0 || q < tstart[t] + 1) continue;
-      const uint32_t d = q - tstart[t];
-      if (d + 1 >= T.level_off.size()) continue;
-      const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
-      if (lo == hi) continue;
-      uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kFloodMaxNodes, e->flood_words / W));
-      const uint32_t gsz = std::min(per, kFloodGranule);
-      per -= per % gsz;  // whole granules per task
-      const uint32_t pseg = d == 1 ? kNone : seg_prev[t];  // level 1: the seeded root
-      seg_prev[t] = static_cast<uint32_t>(SG.size());
-      FloodSeg sg{};
-      sg.task0 = static_cast<uint32_t>(TK.size());
-      sg.node0 = T.nbase + lo;
-      sg.per = per;
-      sg.n_tasks = ceil_div(hi - lo, per);
-      sg.gbase = gran;
-      sg.gsz = gsz;
-      sg.pad[0] = hi - lo;  // nodes of the level
-      SG.push_back(sg);
-      gran += ceil_div(hi - lo, gsz);
-      for (uint32_t u = lo; u < hi; u += per) {
-        FloodTask k{};
-        k.nb = T.nbase + u;
-        k.ne = T.nbase + std::min(u + per, hi);
-        k.topic = t;
-        k.round = q;
-        k.g_own = sg.gbase + (u - lo) / gsz;
-        k.gsz = gsz;
-        k.pseg = pseg;
-        TK.push_back(k);
+      if (tab[t].W == 0) continue;
+      const bool gm = (tab[t].flags & kTopicGroups) != 0;
+      for (size_t gi = 0; gi < groups[t].size(); ++gi) {
+        const StartGroup& g = groups[t][gi];
+        const uint32_t W = gm ? g.wn : tab[t].W;
+        if (q < g.start + 1) continue;
+        const uint32_t d = q - g.start;
+        if (d + 1 >= T.level_off.size()) continue;
+        const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
+        if (lo == hi) continue;
+        uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kFloodMaxNodes, e->flood_words / W));
+        const uint32_t gsz = std::min(per, kFloodGranule);
+        per -= per % gsz;  // whole granules per task
+        const uint32_t pseg = d == 1 ? kNone : seg_prev[t][gi];  // level 1: the seeded root
+        const uint32_t seg = static_cast<uint32_t>(SG.size());
+        seg_prev[t][gi] = seg;
+        FloodSeg sg{};
+        sg.task0 = static_cast<uint32_t>(TK.size());
+        sg.node0 = T.nbase + lo;
+        sg.per = per;
+        sg.n_tasks = ceil_div(hi - lo, per);
+        sg.gbase = gran;
+        sg.gsz = gsz;
+        sg.nodes = hi - lo;  // nodes of the level
+        sg.W = W;
+        sg.row0 = tab[t].wbase + (gm ? static_cast<uint64_t>(tab[t].n_nodes) * g.w0 : 0);
+        SG.push_back(sg);
+        gran += ceil_div(hi - lo, gsz);
+        for (uint32_t u = lo; u < hi; u += per) {
+          FloodTask k{};
+          k.nb = T.nbase + u;
+          k.ne = T.nbase + std::min(u + per, hi);
+          k.topic = t;
+          k.round = q;
+          k.g_own = sg.gbase + (u - lo) / gsz;
+          k.gsz = gsz;
+          k.pseg = pseg;
+          k.seg = seg;
+          TK.push_back(k);
+        }
       }
     }
     const uint32_t n_round = static_cast<uint32_t>(TK.size() - first);
@@ -1702,7 +1716,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     const uint64_t blocks = (bound + 3) / 4;  // ~1 entry per wave at least
     return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(e->expand_grid, blocks)));
   };
-  const bool flood_ok = level && !multi && world == 1 && e->flood_on && !e->flood_broken &&
+  const bool flood_ok = level && world == 1 && e->flood_on && !e->flood_broken &&
                         e->flood_grid > 0 && e->n_nodes < 0x80000000u;  // k_flood marks node ids with bit 31
   uint32_t flood_rounds = 0;    // rounds 1..flood_rounds: k_flood
   std::vector<uint32_t> lgrid;  // per-round launches: grid of every round
@@ -1711,7 +1725,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     int rc2 = build_pull_chunks(e, tab, groups, planned0);
     if (!rc2 && flood_ok) {
       while (flood_rounds < planned0 && e->pull_bytes[flood_rounds + 1] <= e->flood_top_bytes) ++flood_rounds;
-      if (flood_rounds) rc2 = build_flood_tasks(e, tab, tstart, flood_rounds);
+      if (flood_rounds) rc2 = build_flood_tasks(e, tab, groups, flood_rounds);
     }
     if (!rc2 && world > 1) rc2 = build_ghost_plan(e, tab, wglob, tstart, planned0);
     if (rc2) return rc2;
@@ -1948,6 +1962,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     if (flood) {
       FloodArgs fa{};
       fa.tasks = e->d_flood_tasks.as<FloodTask>();
+      fa.segs = e->d_flood_segs.as<FloodSeg>();
       fa.node_parent = e->d_node_parent.as<uint32_t>();
       fa.node_flags = a.node_flags;
       fa.topics = a.topics;

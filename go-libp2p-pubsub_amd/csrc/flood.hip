@@ -40,7 +40,6 @@ namespace {
 
 using namespace dev;
 
-constexpr uint32_t kMergeBit = 0x80000000u;  // src[]: the node already holds rows of this window
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
@@ -188,28 +187,21 @@ __device__ __forceinline__ void flood_stream_odd(const FloodArgs& a, uint64_t* o
   }
 }
 
-// Merging path, word by word: a node that already holds messages of this
-// window (never on a tree whose window messages share one start round, kept
-// exact anyway: new = parent & ~own, the duplicates counted), or a parent
-// range too wide for 32-bit buffer offsets.  8-B agent-scope accesses (sc1).
+// Wide path, word by word: a parent range too wide for 32-bit buffer
+// offsets.  8-B agent-scope accesses (sc1).
 template <bool kRecord>
-__device__ void flood_stream_merge(const FloodArgs& a, uint64_t* out_row, uint32_t total, uint32_t W,
-                                   const uint64_t* prow, uint32_t pbase, const uint32_t* src, uint32_t lane,
-                                   uint32_t round, PullCtr& c) {
+__device__ void flood_stream_wide(const FloodArgs& a, uint64_t* out_row, uint32_t total, uint32_t W,
+                                  const uint64_t* prow, uint32_t pbase, const uint32_t* src, uint32_t lane,
+                                  uint32_t round, PullCtr& c) {
   for (uint32_t i = lane; i < total; i += 64) {
     const uint32_t kk = i / W, r = i - kk * W;
-    const uint32_t s = src[kk];
-    if (s == kNoneNode) continue;
-    const uint32_t p = s & ~kMergeBit;
+    const uint32_t p = src[kk];
+    if (p == kNoneNode) continue;
     const uint64_t m = ld_agent64(prow + static_cast<uint64_t>(p - pbase) * W + r);
-    uint64_t* o = out_row + i;
-    const uint64_t own = (s & kMergeBit) ? ld_agent64(o) : 0ull;
-    const uint64_t nm = m & ~own;
-    __hip_atomic_store(o, own | nm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    c.deliv += __popcll(nm);
-    c.dup += __popcll(m & own);
+    __hip_atomic_store(out_row + i, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    c.deliv += __popcll(m);
     c.sw += 1;
-    if constexpr (kRecord) record_word(a.hop_rec, (out_row - a.seen) + i, nm, round);
+    if constexpr (kRecord) record_word(a.hop_rec, (out_row - a.seen) + i, m, round);
   }
 }
 
@@ -263,9 +255,9 @@ __global__ __launch_bounds__(kBlock, kFloodBlocksPerCu) void k_flood(FloodArgs a
     const uint32_t me = T.nb + (in ? lane : nk - 1);
     const uint32_t p = a.node_parent[me];
     const uint32_t f = a.node_flags[me];
-    const uint32_t own = a.gen[me];  // only this wave writes this byte in this launch
     uint32_t prev = kNoneNode;
     const TopicDev D = a.topics[T.topic];
+    const FloodSeg S = a.segs[T.seg];
     // the next task's record, consumed after this one
     const FloodTask Tn = a.tasks[ti + nw < a.n_tasks ? ti + nw : ti];
     if (lane == 0 && T.nb > 0) prev = a.node_parent[T.nb - 1];
@@ -309,15 +301,15 @@ __global__ __launch_bounds__(kBlock, kFloodBlocksPerCu) void k_flood(FloodArgs a
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the row loads below the poll
     uint64_t t_b = stamp();
     pf[2] += t_b - t_a;
-    const uint32_t W = rfl(D.W), nbase = rfl(D.nbase);
-    const uint64_t wbase = static_cast<uint64_t>(rfl(static_cast<uint32_t>(D.wbase >> 32))) << 32 |
-                           rfl(static_cast<uint32_t>(D.wbase));
-    const uint64_t base = wbase - static_cast<uint64_t>(nbase) * W;
-    // resolve: the parent whose row each node receives
+    const uint32_t W = rfl(S.W), nbase = rfl(D.nbase);
+    const uint64_t row0 = static_cast<uint64_t>(rfl(static_cast<uint32_t>(S.row0 >> 32))) << 32 |
+                          rfl(static_cast<uint32_t>(S.row0));
+    const uint64_t base = row0 - static_cast<uint64_t>(nbase) * W;
+    // resolve: the parent whose row each node receives.  Every row (block)
+    // is written once per window -- a node is reached once per start group
+    // -- so it is fresh: new = row(parent) & ~0, written whole.
     const bool ok = up && (f & kNodeLive);
-    const bool fresh = own != cur;
-    if (in) src[lane] = ok ? (p | (fresh ? 0u : kMergeBit)) : kNoneNode;
-    const bool merge = __any(ok && !fresh);
+    if (in) src[lane] = ok ? p : kNoneNode;
     {
       uint32_t pv = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
       if (lane == 0) pv = T.nb > nbase ? prev : kNoneNode;
@@ -338,8 +330,8 @@ __global__ __launch_bounds__(kBlock, kFloodBlocksPerCu) void k_flood(FloodArgs a
     uint64_t* out_row = a.seen + base + static_cast<uint64_t>(T.nb) * W;
     const uint64_t* prow = a.seen + base + static_cast<uint64_t>(T.p_lo) * W;
     const uint64_t span = static_cast<uint64_t>(T.p_hi - T.p_lo + 1) * W * 8;
-    if (merge || span >= kOutOfRange) {
-      flood_stream_merge<kRecord>(a, out_row, total, W, prow, T.p_lo, src, lane, T.round, c);
+    if (span >= kOutOfRange) {  // parent range too wide for 32-bit buffer offsets
+      flood_stream_wide<kRecord>(a, out_row, total, W, prow, T.p_lo, src, lane, T.round, c);
     } else {
       const __amdgpu_buffer_rsrc_t rin = rsrc(prow, static_cast<uint32_t>(span));
       if (W & 1u)
@@ -394,7 +386,7 @@ __global__ __launch_bounds__(kBlock) void k_flood_deps(FloodTask* __restrict__ t
     const FloodSeg s = segs[t.pseg];
     // a parent outside its level could only mis-order, never index outside
     // the granules (clamped)
-    const uint32_t nodes = s.pad[0];
+    const uint32_t nodes = s.nodes;
     const uint32_t lo = t.p_lo >= s.node0 ? min(t.p_lo - s.node0, nodes - 1) : 0u;
     if (t.p_hi < t.p_lo || t.p_hi - s.node0 >= nodes) t.p_hi = s.node0 + nodes - 1;
     t.p_lo = s.node0 + lo;

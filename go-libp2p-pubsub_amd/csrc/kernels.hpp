@@ -202,16 +202,20 @@ struct FloodTask {
   uint32_t p_lo, p_hi;      // parents of the run (consecutive ids)              [k_flood_deps]
   uint32_t pg_lo, pg_hi;    // parent granules to poll; kNoneNode: parent = root [k_flood_deps]
   uint32_t pnode0, pgsz;    // parent level: first node and nodes per granule    [k_flood_deps]
-  uint32_t pseg, pad;       // host: the parent level's segment (kNoneNode: root)
+  uint32_t pseg;            // host: the parent level's segment (kNoneNode: root)
+  uint32_t seg;             // the task's own segment (row stride and base)
 };
-// One level of one topic: tasks task0 .. task0 + n_tasks - 1 of `per` nodes
-// each from node0, granules gbase .. of gsz nodes each.
+// One level of one topic (of one start group): tasks task0 .. task0 +
+// n_tasks - 1 of `per` nodes each from node0, granules gbase .. of gsz nodes
+// each; rows of W words, node u's at row0 + (u - nbase) * W.
 struct FloodSeg {
   uint32_t task0, node0, per, n_tasks;
-  uint32_t gbase, gsz, pad[2];
+  uint32_t gbase, gsz, nodes, W;
+  uint64_t row0;  // word offset of the topic's first node's row (its start group's block region)
 };
 struct FloodArgs {
   const FloodTask* tasks;
+  const FloodSeg* segs;
   const uint32_t* node_parent;
   const uint8_t* node_flags;
   const TopicDev* topics;

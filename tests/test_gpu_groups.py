@@ -42,8 +42,8 @@ def run(level, n, topics, live, msg_topics, starts, record=True):
         eng.set_live(live)
         first = eng.publish(msg_topics, starts)
         st = eng.run()
-        if level:
-            assert st.expand_mode == PE.MODE_LEVEL_PULL
+        if level:  # k_flood for the small leading rounds, k_pull after
+            assert st.expand_mode in (PE.MODE_FLOOD, PE.MODE_LEVEL_PULL)
         else:
             assert st.expand_mode == PE.MODE_COMPACT
         hops = [eng.hops(first + m) for m in range(len(msg_topics))] if record else None
@@ -53,7 +53,7 @@ def run(level, n, topics, live, msg_topics, starts, record=True):
 
 
 @pytest.mark.parametrize("seed", range(6))
-def test_groups_match_oracle_and_compaction(seed):
+def test_groups_match_oracle_and_compaction(monkeypatch, seed):
     """Several topics, start rounds 0..7 drawn per message (some topics with
     a single start), ~12 % dead peers: level mode with start groups and the
     compaction path both equal the oracle message by message, and leave the
@@ -78,7 +78,14 @@ def test_groups_match_oracle_and_compaction(seed):
         rp, cl = O.parents_to_csr(parent)
         exp[t] = O.disseminate(rp, cl, root, live, 1)[1][0]
     outs = []
-    for level in (True, False):
+    # level mode: the default k_flood / k_pull split, every round in k_flood,
+    # every round in k_pull; then the compaction path
+    for level, env in ((True, {}), (True, {"PSAMD_FLOOD_TOP_BYTES": str(1 << 40)}), (True, {"PSAMD_FLOOD": "0"}),
+                       (False, {})):
+        for k in ("PSAMD_FLOOD_TOP_BYTES", "PSAMD_FLOOD"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         st, hops, deliv, pm, digest = run(level, n, topics, live, msg_topics, starts)
         for m, t in enumerate(msg_topics):
             if not np.array_equal(hops[m], exp[int(t)]):
@@ -89,7 +96,7 @@ def test_groups_match_oracle_and_compaction(seed):
         d = st.as_dict()
         outs.append((st.deliveries, st.rounds, d["deliveries_per_round"], digest,
                      [x.tobytes() for x in deliv], pm))
-    assert outs[0] == outs[1]
+    assert all(o == outs[0] for o in outs)
     # per-round deliveries: message m reaches level d in round starts[m] + d
     per = np.zeros(64, dtype=np.int64)
     for m, t in enumerate(msg_topics):
@@ -143,7 +150,7 @@ def test_cfg3_staggered_full_size():
         sizes = WL.build_engine_topics(eng, wl)
         first = eng.publish(wl.msg_topics, starts)
         st = eng.run()
-        assert st.expand_mode == PE.MODE_LEVEL_PULL
+        assert st.expand_mode == PE.MODE_FLOOD and 0 < st.flood_rounds < st.rounds
         assert st.deliveries == wl.expected_deliveries(sizes) == 34_354_202_750
         assert st.duplicates == 0
         hist = np.zeros(80, dtype=np.int64)
