@@ -1996,9 +1996,6 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         a.a_next = arr[r & 1];
         // multi-GPU: this round's ghost parents (rows written last round, or
         // seeded roots) to the ranks owning their children, then the exchange
-        if (world > 1 && e->host_timing)
-          std::fprintf(stderr, "[psengine] rank %d round %u/%u: ghost exchange %d\n", me, r, planned0,
-                       static_cast<int>(e->ghost_rounds[r].any));
         if (world > 1 && e->ghost_rounds[r].any) {
           const auto& R = e->ghost_rounds[r];
           if (R.seg1 > R.seg0) {

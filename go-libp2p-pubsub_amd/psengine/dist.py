@@ -12,6 +12,11 @@ Scaling: "weak" (default) keeps the per-GPU work of the N=1
 workload: the same topology, N x the messages (each rank holds 1/N of every
 tree, so it moves as many row words as one GPU does at N=1); "strong" runs
 the N=1 workload unchanged.
+
+Beside the partitioned run, `message_sharded` times SURVEY.md §8e's other
+decomposition on the same ranks: every rank holds the whole topology (a
+replicated CSR) and disseminates its own share of the messages -- messages
+are independent on a churn-free batch, so no exchange is needed.
 """
 from __future__ import annotations
 
@@ -80,7 +85,20 @@ def bench_main(args, descr: dict, metric: str):
     json_fd = os.dup(1)
     os.dup2(2, 1)
     rank, world, local = env_ranks()
+    local = local % max(1, torch.cuda.device_count())  # (counting does not initialise the GPU)
     torch.cuda.set_device(local)
+    if getattr(args, "message_only", False):
+        # the message-sharded leg alone (no RCCL communicator: also runs with
+        # several ranks on one GPU, e.g. to test it on a one-GPU box)
+        dist = init("gloo")
+        ms = message_sharded(args, dist, torch.device("cuda", local), rank, world, descr, totals_dev=None)
+        if rank == 0:
+            sys.stdout.flush()
+            os.write(json_fd, (json.dumps({"metric": metric + " [message-sharded leg only]", "n_gpus": world,
+                                           "message_sharded": ms}) + "\n").encode())
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     dist = init("nccl")  # RCCL on ROCm
     dev = torch.device("cuda", local)
     part = PART_SUBTREE if getattr(args, "partition", "peer") == "subtree" else PART_PEER
@@ -171,8 +189,52 @@ def bench_main(args, descr: dict, metric: str):
             "last_step_rank0": {"rounds": st.rounds, "run_ms": st.run_ms,
                                 "expand_ms": st.expand_ms, "host_ms": st.host_ms},
         }
+    eng.close()
+    if world > 1 and not getattr(args, "no_message_leg", False):
+        ms = message_sharded(args, dist, dev, rank, world, descr)
+        if rank == 0:
+            out["message_sharded"] = ms
+    if rank == 0:
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())
-    eng.close()
     dist.barrier()
     dist.destroy_process_group()
+
+
+def message_sharded(args, dist, dev, rank: int, world: int, descr: dict, totals_dev="same") -> dict:
+    """Every rank: a one-GPU engine over the whole topology, its own batch of
+    the N=1 workload's messages (weak scaling: N x the messages in all), the
+    same pipelined steps; the job's deliveries over the slowest rank's time."""
+    import torch
+
+    wl = WL.CONFIGS[args.workload]() if args.scale == 1.0 else WL.scaled(args.workload, args.scale)
+    local = dev.index if dev.index is not None else 0
+    eng = Engine(wl.n_peers, len(wl.topics), device=local, seed=wl.seed)
+    sizes = WL.build_engine_topics(eng, wl)
+    expected = wl.expected_deliveries(sizes)
+    for _ in range(args.warmup):
+        eng.publish(wl.msg_topics)
+        st = eng.run()
+        assert args.no_check or st.deliveries == expected
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    local_deliv = 0
+    for i in range(args.steps):
+        eng.publish(wl.msg_topics)
+        eng.run_async()
+        if i:
+            local_deliv += eng.wait().deliveries
+    if args.steps:
+        local_deliv += eng.wait().deliveries
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    wall, total = job_totals(dist, elapsed, local_deliv, dev if totals_dev == "same" else totals_dev)
+    eng.close()
+    if not args.no_check:
+        assert total == expected * args.steps * world, (total, expected * args.steps * world)
+    return {"value": total / wall, "unit": "deliveries/s", "ms_per_step": wall * 1e3 / max(1, args.steps),
+            "workload": f"{wl.name}: each of {world} ranks disseminates {wl.n_msgs} messages over the whole "
+                        "topology (replicated CSR, no exchange; SURVEY.md §8e alternative)",
+            "scaling": "weak"}
