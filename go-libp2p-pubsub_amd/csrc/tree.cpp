@@ -104,6 +104,60 @@ bool SubscriptionTree::below_orphan(uint32_t p) {
   return cut;
 }
 
+void SubscriptionTree::below_orphan_many(const std::vector<uint32_t>& ps, std::vector<uint8_t>& cut) {
+  constexpr size_t kWalks = 16;
+  const uint32_t no = 2 * reach_pass_, yes = no + 1;
+  if (orphan_stamp_.size() != n_) orphan_stamp_.assign(n_, 0xFFFFFFFFu);
+  cut.assign(ps.size(), 0);
+  std::vector<uint32_t> path[kWalks];
+  for (size_t b = 0; b < ps.size(); b += kWalks) {
+    const size_t m = std::min(kWalks, ps.size() - b);
+    uint32_t cur[kWalks], hops[kWalks];
+    bool done[kWalks];
+    for (size_t j = 0; j < m; ++j) {
+      cur[j] = ps[b + j];
+      hops[j] = 0;
+      done[j] = false;
+      path[j].clear();
+      if (cur[j] < n_) {
+        __builtin_prefetch(&rec_[cur[j]]);
+        __builtin_prefetch(&orphan_stamp_[cur[j]]);
+      }
+    }
+    size_t active = m;
+    while (active) {
+      for (size_t j = 0; j < m; ++j) {
+        if (done[j]) continue;
+        const uint32_t p = cur[j];
+        int res = -1;  // -1: continue upward, 0: not cut, 1: cut
+        if (p == root_ || p == kNone || p >= n_ || hops[j] > n_) {
+          res = 0;
+        } else if (orphan_stamp_[p] == yes || orphan_stamp_[p] == no) {
+          res = orphan_stamp_[p] == yes;
+        } else if (rec_[p].state == PeerState::Orphan) {
+          res = 1;
+        } else if (rec_[p].state != PeerState::In) {
+          res = 0;
+        }
+        if (res < 0) {
+          path[j].push_back(p);
+          cur[j] = rec_[p].up;
+          ++hops[j];
+          if (cur[j] < n_) {
+            __builtin_prefetch(&rec_[cur[j]]);
+            __builtin_prefetch(&orphan_stamp_[cur[j]]);
+          }
+          continue;
+        }
+        for (uint32_t q : path[j]) orphan_stamp_[q] = res ? yes : no;
+        cut[b + j] = static_cast<uint8_t>(res);
+        done[j] = true;
+        --active;
+      }
+    }
+  }
+}
+
 // SplitMix64: stands in for Go's randomised map iteration (rule Q2).
 uint64_t SubscriptionTree::next_random() {
   uint64_t z = (rng_ += 0x9E3779B97F4A7C15ull);
@@ -265,8 +319,18 @@ int SubscriptionTree::after_message(const ReachQuery* reach) {
     // entries (subtree.go:329-331), draws nothing from the tie-break stream,
     // so the order does not matter -- visit just the parents holding one,
     // if the message reached them (an In-state path from the root).
-    std::sort(parted_at_.begin(), parted_at_.end());
-    parted_at_.erase(std::unique(parted_at_.begin(), parted_at_.end()), parted_at_.end());
+    // distinct parents (the pass is order free): marked once, marks reset
+    {
+      if (dedup_mark_.size() != n_) dedup_mark_.assign(n_, 0);
+      size_t w = 0;
+      for (uint32_t p : parted_at_)
+        if (p < n_ && !dedup_mark_[p]) {
+          dedup_mark_[p] = 1;
+          parted_at_[w++] = p;
+        }
+      parted_at_.resize(w);
+      for (uint32_t p : parted_at_) dedup_mark_[p] = 0;
+    }
     // reachability of the message's tree, before this pass mutates anything
     // (the prune below only edits child lists of reached parents and puts Dead
     // children Out: no reached peer's path changes)
@@ -284,6 +348,14 @@ int SubscriptionTree::after_message(const ReachQuery* reach) {
       for (size_t i = 0; i < parted_at_.size(); ++i)
         reached[i] = parted_at_[i] < n_ && reachable_memo(parted_at_[i]);
     }
+    // the unreached ones: cut for good (below an Orphan) or kept for a later
+    // message, decided by walks run in lockstep
+    std::vector<uint32_t> unreached;
+    for (size_t i = 0; i < parted_at_.size(); ++i)
+      if (!reached[i] && parted_at_[i] < n_) unreached.push_back(parted_at_[i]);
+    std::vector<uint8_t> cut;
+    below_orphan_many(unreached, cut);
+    size_t ui = 0;
     std::vector<uint32_t> keep;
     // scattered parents: their lines are fetched 16 ahead, their children's 8 ahead
     constexpr size_t kAhead0 = 16, kAhead1 = 8;
@@ -304,7 +376,7 @@ int SubscriptionTree::after_message(const ReachQuery* reach) {
       if (!reached[i]) {
         // pruned by a later message that reaches it -- unless an orphan cuts
         // it off for good (an Orphan never becomes In again, Q5)
-        if (p < n_ && !below_orphan(p)) keep.push_back(p);
+        if (p < n_ && !cut[ui++]) keep.push_back(p);
         continue;
       }
       ChildRec* list = kids(p);

@@ -89,6 +89,8 @@ class SubscriptionTree {
   // walked path is stamped reachable / unreachable (top levels are shared).
   bool reachable_memo(uint32_t p);
   bool below_orphan(uint32_t p);  // an Orphan on the upstream path (cut for good); memoised per pass
+  // below_orphan of many peers, kWalks walks in lockstep (their cache misses overlap)
+  void below_orphan_many(const std::vector<uint32_t>& ps, std::vector<uint8_t>& cut);
   void touch(uint32_t p);             // (state, upstream) of p may have changed
 
   // One cache line per peer: upstream, state and (up to kInline) child
@@ -120,6 +122,7 @@ class SubscriptionTree {
   std::vector<uint32_t> parted_at_;  // parents holding a Part'ed child entry
   std::vector<uint32_t> touched_;    // peers whose attachment may have changed
   std::vector<uint8_t> touched_mark_;
+  std::vector<uint8_t> dedup_mark_;  // after_message: distinct Part'ed parents
   std::vector<uint32_t> reach_stamp_;  // 2*pass: reachable, 2*pass+1: not (reachable_memo)
   std::vector<uint32_t> orphan_stamp_;  // 2*pass: not cut, 2*pass+1: cut (below_orphan)
   uint32_t reach_pass_ = 0;
