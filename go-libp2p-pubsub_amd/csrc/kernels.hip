@@ -846,40 +846,48 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
       const uint64_t* s = go ? reinterpret_cast<const uint64_t*>(row) + r : out + i;
       return PullVec{go, *reinterpret_cast<const uint4*>(s)};
     };
-    for (uint32_t i0 = 0; i0 < total; i0 += kU * 128) {
+    // the stream starts h words before the run, at a 128-B line, so every
+    // 1-KB wave store covers whole lines (lanes before the run store its
+    // first pair again, with the value its owner stores)
+    const uint32_t h = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out) & 127) >> 3;
+    for (uint32_t i0 = 0; i0 < total + h; i0 += kU * 128) {
       PullVec x[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
-        const uint32_t i = i0 + u * 128 + 2 * lane;
-        x[u] = one(i < total ? i : total - 2);
+        const int32_t i = static_cast<int32_t>(i0 + u * 128 + 2 * lane) - static_cast<int32_t>(h);
+        x[u] = one(i < 0 ? 0u : (static_cast<uint32_t>(i) < total ? static_cast<uint32_t>(i) : total - 2));
       }
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
-        const uint32_t i = i0 + u * 128 + 2 * lane;
+        const int32_t is = static_cast<int32_t>(i0 + u * 128 + 2 * lane) - static_cast<int32_t>(h);
+        const bool inr = is >= 0 && static_cast<uint32_t>(is) < total;
+        const uint32_t i = is < 0 ? 0u : (inr ? static_cast<uint32_t>(is) : total - 2);
         if constexpr (kRecord) {
-          if (x[u].go && i < total) {
+          if (x[u].go && inr) {
             *reinterpret_cast<uint4*>(out + i) = x[u].v;
             const uint64_t cw = (out - a.seen) + i;
             record_word(a.hop_rec, cw, static_cast<uint64_t>(x[u].v.y) << 32 | x[u].v.x, round);
             record_word(a.hop_rec, cw + 1, static_cast<uint64_t>(x[u].v.w) << 32 | x[u].v.z, round);
           }
         } else {
-          store_row16<kNT>(out + (i < total ? i : total - 2), x[u].v);
+          store_row16<kNT>(out + i, x[u].v);
         }
-        const bool own = x[u].go && i < total;
+        const bool own = x[u].go && inr;
         c.deliv += own ? popc4(x[u].v) : 0u;
         c.sw += own ? 2u : 0u;
       }
     }
   } else {
     // odd W: one word (8 B) per lane, the same pipeline
-    for (uint32_t i0 = 0; i0 < total; i0 += kU * 64) {
+    const uint32_t h = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out) & 127) >> 3;  // line-aligned start
+    for (uint32_t i0 = 0; i0 < total + h; i0 += kU * 64) {
       uint64_t m[kU];
       bool go[kU];
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
-        const uint32_t i = i0 + u * 64 + lane;
-        const uint32_t ic = i < total ? i : total - 1;  // past the end: the run's last word again
+        const int32_t is = static_cast<int32_t>(i0 + u * 64 + lane) - static_cast<int32_t>(h);
+        // before the run: its first word again; past the end: its last word again
+        const uint32_t ic = is < 0 ? 0u : (static_cast<uint32_t>(is) < total ? static_cast<uint32_t>(is) : total - 1);
         int32_t kk, r;
         split(ic, kk, r);
         const uint64_t row = src[kk];
@@ -889,16 +897,18 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
       }
 #pragma unroll
       for (uint32_t u = 0; u < kU; ++u) {
-        const uint32_t i = i0 + u * 64 + lane;
+        const int32_t is = static_cast<int32_t>(i0 + u * 64 + lane) - static_cast<int32_t>(h);
+        const bool inr = is >= 0 && static_cast<uint32_t>(is) < total;
+        const uint32_t i = is < 0 ? 0u : (inr ? static_cast<uint32_t>(is) : total - 1);
         if constexpr (kRecord) {
-          if (go[u] && i < total) {
+          if (go[u] && inr) {
             out[i] = m[u];
             record_word(a.hop_rec, (out - a.seen) + i, m[u], round);
           }
         } else {
-          store_row8<kNT>(out + (i < total ? i : total - 1), m[u]);
+          store_row8<kNT>(out + i, m[u]);
         }
-        const bool own = go[u] && i < total;
+        const bool own = go[u] && inr;
         c.deliv += own ? __popcll(m[u]) : 0u;
         c.sw += own ? 1u : 0u;
       }
