@@ -376,7 +376,8 @@ def main():
                     help="one blocking ps_run per step (default: pipelined ps_run_async / ps_wait, "
                          "the next batch is published and planned while the previous one's kernels run)")
     ap.add_argument("--no-message-leg", action="store_true",
-                    help="N>1: skip the message-sharded leg (replicated topology, no exchange)")
+                    help="N>1: skip the alternative decompositions (the other partition, and message "
+                         "sharding: replicated topology, no exchange)")
     ap.add_argument("--message-only", action="store_true",
                     help="N>1: only the message-sharded leg (gloo bootstrap, no RCCL; testing)")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],

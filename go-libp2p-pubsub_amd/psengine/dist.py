@@ -13,10 +13,13 @@ workload: the same topology, N x the messages (each rank holds 1/N of every
 tree, so it moves as many row words as one GPU does at N=1); "strong" runs
 the N=1 workload unchanged.
 
-Beside the partitioned run, `message_sharded` times SURVEY.md §8e's other
-decomposition on the same ranks: every rank holds the whole topology (a
-replicated CSR) and disseminates its own share of the messages -- messages
-are independent on a churn-free batch, so no exchange is needed.
+Beside the partitioned run (the JSON line's value), two legs time SURVEY.md
+§8e's other decompositions on the same ranks: the other partition
+(`subtree_partition` beside the peer-hash headline: cross edges only above
+level L, so almost no exchange) and `message_sharded`: every rank holds the
+whole topology (a replicated CSR) and disseminates its own share of the
+messages -- messages are independent on a churn-free batch, so no exchange
+is needed.
 """
 from __future__ import annotations
 
@@ -102,6 +105,33 @@ def bench_main(args, descr: dict, metric: str):
     dist = init("nccl")  # RCCL on ROCm
     dev = torch.device("cuda", local)
     part = PART_SUBTREE if getattr(args, "partition", "peer") == "subtree" else PART_PEER
+    out = partitioned(args, dist, dev, rank, world, descr, metric, part)
+    if world > 1 and not getattr(args, "no_message_leg", False):
+        # the decompositions SURVEY.md §8e allows beside the mandated peer hash,
+        # on the same ranks: level-L subtrees (cross edges only above level L)
+        # and message sharding (replicated topology, no exchange)
+        other = PART_PEER if part == PART_SUBTREE else PART_SUBTREE
+        leg = partitioned(args, dist, dev, rank, world, descr, metric, other)
+        ms = message_sharded(args, dist, dev, rank, world, descr)
+        if rank == 0:
+            keep = ("value", "unit", "ms_per_step", "roofline", "config")
+            out["peer_partition" if other == PART_PEER else "subtree_partition"] = {k: leg[k] for k in keep}
+            out["message_sharded"] = ms
+    if rank == 0:
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str, part: int):
+    """The node-partitioned run: every rank owns a hash (PART_PEER) or
+    subtree (PART_SUBTREE) share of every tree; the frontier rows that cross
+    ranks are exchanged each round over the engine's RCCL communicator.
+    Returns the bench JSON object on rank 0 (None elsewhere)."""
+    import torch
+
+    local = dev.index if dev.index is not None else 0
     wl = workload(args, world)
     scaling = getattr(args, "scaling", "weak") if world > 1 else "weak"
     uid = share_bytes(dist, unique_id, rank)
@@ -111,9 +141,10 @@ def bench_main(args, descr: dict, metric: str):
     eng.dist_init(rank, world, uid, part)
     sizes = WL.build_engine_topics(eng, wl)
     expected = wl.expected_deliveries(sizes)
+    pname = "peer" if part == PART_PEER else "subtree"
     if rank == 0:
-        print(f"[bench] {wl.name} on {world} GPUs ({'peer' if part == PART_PEER else 'subtree'} "
-              f"partition), setup {time.perf_counter() - t0:.1f}s", file=sys.stderr, flush=True)
+        print(f"[bench] {wl.name} on {world} GPUs ({pname} partition), setup {time.perf_counter() - t0:.1f}s",
+              file=sys.stderr, flush=True)
 
     def step():
         eng.publish(wl.msg_topics)
@@ -159,6 +190,7 @@ def bench_main(args, descr: dict, metric: str):
     slow_exp_ms, _ = job_totals(dist, exp_ms, 0, dev)
     if not args.no_check:
         assert total == expected * args.steps, (total, expected * args.steps)
+    out = None
     if rank == 0:
         value = total / wall
         # per GPU: the job's expand bytes over the slowest rank's expand time / N
@@ -180,8 +212,7 @@ def bench_main(args, descr: dict, metric: str):
                        "topics": len(wl.topics), "subscriptions": int(sum(sizes)),
                        "messages": wl.n_msgs, "deliveries_per_step": expected,
                        "parallelism": f"{world} GPUs, nodes hash-partitioned "
-                                      f"({'peer' if part == PART_PEER else 'subtree'}), "
-                                      "RCCL all-to-allv frontier exchange per round"},
+                                      f"({pname}), RCCL all-to-allv frontier exchange per round"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0, "traffic": None,
                          "kernel": MODE_KERNEL.get(st.expand_mode, "k_expand"),
@@ -190,15 +221,7 @@ def bench_main(args, descr: dict, metric: str):
                                 "expand_ms": st.expand_ms, "host_ms": st.host_ms},
         }
     eng.close()
-    if world > 1 and not getattr(args, "no_message_leg", False):
-        ms = message_sharded(args, dist, dev, rank, world, descr)
-        if rank == 0:
-            out["message_sharded"] = ms
-    if rank == 0:
-        sys.stdout.flush()
-        os.write(json_fd, (json.dumps(out) + "\n").encode())
-    dist.barrier()
-    dist.destroy_process_group()
+    return out
 
 
 def message_sharded(args, dist, dev, rank: int, world: int, descr: dict, totals_dev="same") -> dict:
