@@ -214,12 +214,15 @@ def case_churn(rng, max_peers):
     return None
 
 
+MAX_WORLD = 4  # --max-world
+
+
 def case_dist(rng, max_peers):
-    """world 2-4 engines on the loopback transport (one thread each), random
-    trees, live masks, single or staggered starts, either partition: the
-    union of the ranks' hops equals the oracle's."""
+    """world 2..MAX_WORLD engines on the loopback transport (one thread
+    each), random trees, live masks, single or staggered starts, either
+    partition: the union of the ranks' hops equals the oracle's."""
     import threading
-    world = int(rng.integers(2, 5))
+    world = int(rng.integers(2, MAX_WORLD + 1))
     n = int(rng.integers(world + 2, max(world + 3, max_peers // 2)))
     n_topics = int(rng.integers(1, 4))
     part = int(rng.integers(0, 2))
@@ -312,12 +315,18 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--max-peers", type=int, default=4000)
     ap.add_argument("--only", type=int, nargs="*", help="run just these case numbers (reproduce a failure)")
+    ap.add_argument("--max-world", type=int, default=4, help="most loopback ranks of a dist case")
+    ap.add_argument("--kinds", nargs="*", help="only these case kinds (topology churn dist drain modes)")
     args = ap.parse_args()
+    global MAX_WORLD
+    MAX_WORLD = args.max_world
     fails = 0
     t0 = time.time()
     for c in (args.only if args.only else range(args.cases)):
         rng = np.random.default_rng([args.seed, c])
         kind = ("topology", "churn", "dist", "topology", "drain", "modes")[c % 6]
+        if args.kinds and kind not in args.kinds:
+            continue
         fn = {"topology": case_topology, "churn": case_churn, "dist": case_dist, "drain": case_drain,
               "modes": case_modes}[kind]
         try:
