@@ -356,7 +356,9 @@ def general_path(eng, wl, deliv_expected, steps: int, warmup: int = 1, max_start
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default: 500 on one GPU -- 0.7 s of back-to-back cfg3 batches, "
+                         "long enough for a utilisation sampler to see -- and 10 for cfg5 or N > 1)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="cfg3", choices=sorted(DESCR))
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug)")
@@ -386,6 +388,9 @@ def main():
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.steps is None:
+        one = args.gpus <= 1 and world <= 1 and not args.force_dist
+        args.steps = 500 if one and args.workload != "cfg5" else 10
     if args.workload == "cfg5":
         return bench_cfg5(args)
     if args.gpus > 1 or world > 1 or args.force_dist:
