@@ -176,12 +176,28 @@ def pmc_traffic(kernel: str, workload: str):
 
 def kernel_split(st):
     """{kernel: (algorithmic bytes, device ms, launches)} of one run, by the
-    rocprofv3 names of the launches that ran its rounds: k_flood (the leading
-    rounds of a single-rank level window, one persistent launch, timed into
-    round 1), k_pull (one launch per remaining round) or k_expand
-    (compaction mode)."""
+    rocprofv3 names of the launches that ran its rounds (ps_stats.round_kernel
+    where the engine reports it): k_flood (the leading rounds of a single-rank
+    level window, one persistent launch, timed into round 1), k_pull (one
+    launch per round), k_pull_pair (two rounds per launch, timed into the
+    first) or k_expand (compaction mode)."""
     kern = PE.MODE_KERNEL.get(st.expand_mode, "k_expand")
     fr = int(getattr(st, "flood_rounds", 0))
+    kinds = list(getattr(st, "round_kernel", []))
+    n = min(int(st.rounds), PE.MAX_ROUNDS - 1)
+    if st.windows == 1 and any(kinds[1:n + 1]) and st.expand_mode != PE.MODE_COMPACT:
+        per = {}
+        for q in range(1, n + 1):
+            name = PE.ROUND_KERNEL.get(kinds[q])
+            if name is None:
+                continue
+            acc = per.setdefault(name, [0, 0.0, 0])
+            acc[0] += int(st.expand_bytes_per_round[q])
+            acc[1] += float(st.expand_ms_per_round[q])
+            first = {PE.K_FLOOD: q == 1, PE.K_PULL: int(st.expand_bytes_per_round[q]) > 0,
+                     PE.K_PAIR: True}.get(kinds[q], False)
+            acc[2] += 1 if first else 0
+        return {k: tuple(v) for k, v in per.items()}
     if st.expand_mode != PE.MODE_FLOOD or fr >= st.rounds or st.windows != 1:
         return {kern: (st.expand_bytes, st.expand_ms, st.expand_launches)}
     bf = sum(int(st.expand_bytes_per_round[q]) for q in range(1, fr + 1))

@@ -181,6 +181,16 @@ struct ps_engine {
   std::vector<PullChunk> pull_host;
   std::vector<uint32_t> pull_off;
   DevBuf d_pull;
+  // k_pull_pair: rounds q and q + 1 in one launch, one rank
+  // (PSAMD_PULL_PAIR=0: one k_pull launch per round)
+  bool pair_on = true;
+  uint32_t pair_words = kPairWords;  // LDS row stage per wave (PSAMD_PAIR_WORDS: 1024 or 512)
+  std::vector<uint64_t> pp_key;
+  std::vector<PullChunk> pp_host;
+  std::vector<uint32_t> pp_lo, pp_hi;  // round q: chunks of the pair launch starting at q
+  std::vector<uint8_t> pp_kind;        // per round of the cached plan: PS_K_*
+  std::vector<uint8_t> round_kind;     // per round of the current window: PS_K_* (empty: k_expand)
+  DevBuf d_pp;
 
   // fused node space (host mirror)
   uint32_t n_nodes = 0, n_pad = 16;
@@ -255,6 +265,7 @@ struct ps_engine {
     uint64_t* ha = nullptr;  // pinned: apply counters of a multi-GPU window
     uint32_t planned0 = 0;
     int32_t world = 1;
+    std::vector<uint8_t> kinds;  // round_kind of the window
   };
   Inflight infl[2];
   uint32_t infl_head = 0, infl_count = 0;
@@ -1069,6 +1080,142 @@ int build_pull_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
   return PS_OK;
 }
 
+// Pair launches (k_pull_pair): one launch writes rounds q
+// and q + 1, each wave a run of level-d nodes and then every child of the run
+// from the rows it holds in LDS, so round q + 1 reads no parent row from HBM.
+// Which rounds pair up is a small dynamic program over the rounds after
+// k_flood's: a pair saves round q + 1's parent-row reads (level d's internal
+// nodes x row bytes) and one launch (priced as kLaunchBytes of traffic).  A
+// round pairs only if each row it writes (and each level-1 row of a start
+// group entering at round q) fits the LDS stage.  Fills e->pp_kind (PS_K_*
+// per round); cached with the pull chunks.
+int build_pair_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
+                      const std::vector<std::vector<StartGroup>>& groups, uint32_t rounds, uint32_t first) {
+  std::vector<uint64_t> key = e->pull_key;  // (graph, flags, rounds, row widths, start groups)
+  key.push_back(first);
+  key.push_back(e->pair_on ? e->pair_words : 0);
+  if (key == e->pp_key) return PS_OK;
+  const uint32_t stage = e->pair_words;
+  constexpr double kLaunchBytes = 16e6;  // ~3 us of launch ramp and tail at ~5.5 TB/s
+  const uint32_t nt = static_cast<uint32_t>(e->topics.size());
+  auto& kind = e->pp_kind;
+  kind.assign(rounds + 2, PS_K_NONE);
+  for (uint32_t q = 1; q <= first && q <= rounds; ++q) kind[q] = PS_K_FLOOD;
+  auto width = [&](uint32_t t, const StartGroup& g) { return (tab[t].flags & kTopicGroups) ? g.wn : tab[t].W; };
+  // per round: parent-row bytes read (estimate), and whether it can pair
+  std::vector<double> rd(rounds + 2, 0.0);
+  std::vector<uint8_t> can(rounds + 2, 0);
+  for (uint32_t q = first + 1; q <= rounds; ++q) {
+    bool ok = e->pair_on && q + 1 <= rounds;
+    for (uint32_t t = 0; t < nt; ++t) {
+      const TopicHost& T = e->topics[t];
+      if (tab[t].W == 0) continue;
+      for (const StartGroup& g : groups[t]) {
+        const uint32_t W = width(t, g);
+        if (q >= g.start + 1) {
+          const uint32_t d = q - g.start;
+          if (d + 1 >= T.level_off.size()) continue;
+          const double parents = d == 1 ? 1.0 : (d - 1 < T.level_internal.size() ? T.level_internal[d - 1] : 0);
+          rd[q] += parents * W * 8.0;
+          ok = ok && W <= stage;
+        } else if (g.start == q && T.level_off.size() > 2) {
+          ok = ok && W <= stage;  // its level 1 runs in the pair launch as a plain run
+        }
+      }
+    }
+    can[q] = ok;
+  }
+  // best[q]: traffic of rounds q..rounds
+  std::vector<double> best(rounds + 3, 0.0);
+  std::vector<uint8_t> take(rounds + 2, 0);
+  auto cost = [&](uint32_t q) {
+    const double b = static_cast<double>(e->pull_bytes[q]);
+    return b + rd[q] + (b > 0 ? kLaunchBytes : 0.0);
+  };
+  for (uint32_t q = rounds; q > first; --q) {
+    best[q] = cost(q) + best[q + 1];
+    if (can[q]) {
+      const double wb = static_cast<double>(e->pull_bytes[q]) + static_cast<double>(e->pull_bytes[q + 1]);
+      const double pc = wb + rd[q] + kLaunchBytes + best[q + 2];
+      if (pc < best[q]) {
+        best[q] = pc;
+        take[q] = 1;
+      }
+    }
+  }
+  auto& C = e->pp_host;
+  C.clear();
+  e->pp_lo.assign(rounds + 2, 0);
+  e->pp_hi.assign(rounds + 2, 0);
+  const bool gpu = e->gpu_graph;
+  for (uint32_t q = first + 1; q <= rounds; ++q) {
+    if (!take[q]) {
+      kind[q] = e->pull_bytes[q] ? PS_K_PULL : PS_K_NONE;
+      continue;
+    }
+    kind[q] = PS_K_PAIR;
+    kind[q + 1] = PS_K_PAIR2;
+    e->pp_lo[q] = static_cast<uint32_t>(C.size());
+    for (uint32_t t = 0; t < nt; ++t) {
+      const TopicHost& T = e->topics[t];
+      if (tab[t].W == 0) continue;
+      const bool gm = (tab[t].flags & kTopicGroups) != 0;
+      for (const StartGroup& g : groups[t]) {
+        const uint32_t W = width(t, g);
+        uint32_t d, per;
+        bool late = false;
+        if (q >= g.start + 1) {
+          d = q - g.start;
+          if (d + 1 >= T.level_off.size()) continue;
+          const uint32_t n = T.level_off[d + 1] - T.level_off[d];
+          const uint32_t kids = d + 2 < T.level_off.size() ? T.level_off[d + 2] - T.level_off[d + 1] : 0;
+          // about 2 x pull_words row words per wave, parents and children together
+          const double f = static_cast<double>(kids) / std::max<uint32_t>(1, n);
+          per = static_cast<uint32_t>(std::max(1.0, 2.0 * e->pull_words / (W * (1.0 + f))));
+        } else if (g.start == q && T.level_off.size() > 2) {
+          d = 1;
+          late = true;
+          per = std::max<uint32_t>(1, e->pull_words / W);
+        } else {
+          continue;
+        }
+        per = std::min<uint32_t>({per, kPairPar, stage / W});
+        const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
+        const uint64_t row0 = tab[t].wbase + (gm ? static_cast<uint64_t>(tab[t].n_nodes) * g.w0 : 0);
+        for (uint32_t u = lo; u < hi; u += per) {
+          PullChunk c{};
+          c.node_begin = T.nbase + u;
+          c.node_end = T.nbase + std::min(u + per, hi);
+          c.topic = t;
+          c.p_lo = gpu ? kNone : e->node_parent[c.node_begin];
+          c.p_hi = gpu ? kNone : e->node_parent[c.node_end - 1];
+          c.W = W;
+          c.row0_lo = static_cast<uint32_t>(row0);
+          c.row0_hi = static_cast<uint32_t>(row0 >> 32);
+          c.c_lo = late ? kNoneNode : 0;  // children: filled in on the device
+          C.push_back(c);
+        }
+      }
+    }
+    e->pp_hi[q] = static_cast<uint32_t>(C.size());
+    ++q;  // round q + 1 is the pair's second round
+  }
+  HIP_TRY(e->d_pp.ensure(std::max<size_t>(C.size(), 1) * sizeof(PullChunk)), "alloc pair chunks");
+  if (!C.empty()) {
+    HIP_TRY(hipMemcpyAsync(e->d_pp.p, C.data(), C.size() * sizeof(PullChunk), hipMemcpyHostToDevice, e->stream),
+            "upload pair chunks");
+    if (gpu)
+      HIP_TRY(launch_chunk_parents(e->d_pp.as<PullChunk>(), static_cast<uint32_t>(C.size()),
+                                   e->d_node_parent.as<uint32_t>(), e->stream),
+              "pair chunk parents");
+    HIP_TRY(launch_pair_kids(e->d_pp.as<PullChunk>(), static_cast<uint32_t>(C.size()), e->d_row_ptr.as<uint32_t>(),
+                             e->d_col.as<uint32_t>(), e->stream),
+            "pair chunk children");
+  }
+  e->pp_key = key;
+  return PS_OK;
+}
+
 // Multi-GPU level mode: the per-round exchange of ghost
 // parents.  Region (a -> b, round q) holds, for the topics active in round q
 // in topic order, one record per a -> b ghost parent of that round's level:
@@ -1361,9 +1508,12 @@ int build_flood_tasks(ps_engine* e, const std::vector<TopicDev>& tab,
 // Returns false when a k_flood dependency wait timed out (its timeout word
 // is folded into row 0).
 bool accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uint32_t r, uint32_t planned0,
-                       uint32_t mode, uint32_t flood_rounds, uint32_t launches, int32_t world) {
+                       uint32_t mode, uint32_t flood_rounds, uint32_t launches, int32_t world,
+                       const std::vector<uint8_t>& kinds) {
   const bool pull = mode == PS_MODE_LEVEL_PULL || mode == PS_MODE_FLOOD;
+  std::memset(st->round_kernel, 0, sizeof(st->round_kernel));
   for (uint32_t q = 1; q <= r; ++q) {
+    const uint8_t kind = q < kinds.size() ? kinds[q] : static_cast<uint8_t>(pull ? PS_K_PULL : PS_K_EXPAND);
     const uint64_t* c = &hs[static_cast<size_t>(q) * kNumCtr];
     const uint64_t app_d = (world > 1 && q <= planned0) ? ha[static_cast<size_t>(q) * kNumCtr + kCtrDeliveries] : 0;
     const uint64_t app_u = (world > 1 && q <= planned0) ? ha[static_cast<size_t>(q) * kNumCtr + kCtrDuplicates] : 0;
@@ -1379,15 +1529,18 @@ bool accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uin
     // seen read / seen write / arrival write 8.
     uint64_t b;
     if (pull)  // pull model: per node parent id 4 + flag 1 + parent generation 1 (k_flood:
-               // + its own generation 1, the seen test), per reached node its generation
-               // write 1; parent rows read once; rows written
-      b = c[kCtrChildren] * (q <= flood_rounds ? 7 : 6) + c[kCtrMeshChildren] * 1 + c[kCtrEntryWords] * 8 +
-          c[kCtrSeenWrites] * 8;
+               // + its own generation 1, the seen test; the second round of a k_pull_pair
+               // launch: no parent generation, its parents' reach and rows are in LDS),
+               // per reached node its generation write 1; parent rows read once (from
+               // HBM: none in a pair's second round); rows written
+      b = c[kCtrChildren] * (kind == PS_K_FLOOD ? 7 : kind == PS_K_PAIR2 ? 5 : 6) + c[kCtrMeshChildren] * 1 +
+          c[kCtrEntryWords] * 8 + c[kCtrSeenWrites] * 8;
     else
       b = c[kCtrEntries] * 18 + c[kCtrEntryWords] * 8 + c[kCtrClearWords] * 8 + c[kCtrChildren] * 3 +
           c[kCtrMeshChildren] * 4 + c[kCtrSeenReads] * 8 + c[kCtrSeenWrites] * 8 + c[kCtrArrivalWrites] * 8;
     st->expand_bytes += b;
     if (q < PS_MAX_ROUNDS) {
+      st->round_kernel[q] = kind;
       st->expand_bytes_per_round[q] += b;
       st->deliveries_per_round[q] += c[kCtrDeliveries] + app_d;
       st->frontier_per_round[q] += static_cast<uint32_t>(c[kCtrEntries]);
@@ -1728,6 +1881,15 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       if (flood_rounds) rc2 = build_flood_tasks(e, tab, groups, flood_rounds);
     }
     if (!rc2 && world > 1) rc2 = build_ghost_plan(e, tab, wglob, tstart, planned0);
+    // one rank: rounds q, q + 1 in one k_pull_pair launch where it pays
+    // (round_kind; several ranks: the exchange separates every round)
+    if (!rc2 && world == 1) {
+      rc2 = build_pair_chunks(e, tab, groups, planned0, flood_rounds);
+      e->round_kind = e->pp_kind;
+    } else {
+      e->round_kind.assign(planned0 + 2, PS_K_PULL);
+      for (uint32_t q = 1; q <= flood_rounds; ++q) e->round_kind[q] = PS_K_FLOOD;
+    }
     if (rc2) return rc2;
     // desc[3q..]: round q's partial slots (first, end, stride) for the reduce
     auto& desc = e->desc_host;
@@ -1750,11 +1912,15 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     woff.assign(planned0 + 2, 0);
     woff[flood_rounds + 1] = slot;
     for (uint32_t q = flood_rounds + 1; q <= planned0; ++q) {
-      lgrid[q] = ceil_div(e->pull_off[q + 1] - e->pull_off[q], kBlock / 64);
-      woff[q + 1] = woff[q] + std::min<uint32_t>(lgrid[q], kPullSlots);
-      desc[3 * q] = woff[q];
-      desc[3 * q + 1] = woff[q + 1];
-      desc[3 * q + 2] = 1;
+      const bool pair = e->round_kind[q] == PS_K_PAIR;
+      lgrid[q] = ceil_div(pair ? e->pp_hi[q] - e->pp_lo[q] : e->pull_off[q + 1] - e->pull_off[q], kBlock / 64);
+      for (uint32_t k = q; k <= q + (pair ? 1u : 0u); ++k) {  // a pair launch: the same slots for both rounds
+        woff[k + 1] = woff[k] + std::min<uint32_t>(lgrid[q], kPullSlots);
+        desc[3 * k] = woff[k];
+        desc[3 * k + 1] = woff[k + 1];
+        desc[3 * k + 2] = 1;
+      }
+      if (pair) lgrid[++q] = 0;
     }
     n_slots = woff[planned0 + 1];
     HIP_TRY(e->d_partials.ensure(static_cast<size_t>(std::max<uint32_t>(n_slots, 1)) * kNumCtr * 8),
@@ -1954,7 +2120,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     // k_flood, or start groups: every root row is seeded up front into arr[0]
     // (and seen: k_flood reads parent rows from there), the blocks of later
     // start rounds included -- a block is read only in its own rounds
-    const bool upfront = flood || multi;
+    bool pairs = false;
+    for (uint32_t q = 1; q <= planned0; ++q) pairs |= e->round_kind[q] == PS_K_PAIR;
+    const bool upfront = flood || multi || pairs;  // (a pair launch's plain level-1 runs read roots)
     if (upfront && max_start > 0)
       HIP_TRY(launch_seed(e->d_seeds.as<SeedDev>(), seed_off[1], seed_off[max_start + 1], arr[0], a.seen, nullptr,
                           nullptr, s),
@@ -2030,10 +2198,20 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
           pa.send = e->d_send.as<uint64_t>();
           // rows nobody re-reads while they can still sit in the 256 MB MALL
           // (large rounds and the last round) store non-temporally
-          const bool nt = r < e->pull_bytes.size() && (e->pull_bytes[r] >= (64ull << 20) || r == planned0);
-          HIP_TRY(launch_pull(pa, e->d_pull.as<PullChunk>() + e->pull_off[r], e->pull_off[r + 1] - e->pull_off[r],
-                              lgrid[r], r, record, nt, s),
-                  "pull");
+          const bool pair = e->round_kind[r] == PS_K_PAIR;
+          const uint32_t rw = pair ? r + 1 : r;  // the round whose rows the next launch reads
+          const bool nt = rw < e->pull_bytes.size() && (e->pull_bytes[rw] >= (64ull << 20) || rw == planned0);
+          if (pair) {
+            pa.partials2 = partials + static_cast<size_t>(e->woff_host[r + 1]) * kNumCtr;
+            pa.all_current = (e->cfg.flags & PS_F_NO_LAZY_SEEN) ? 1u : 0u;
+            HIP_TRY(launch_pull_pair(pa, e->d_pp.as<PullChunk>() + e->pp_lo[r], e->pp_hi[r] - e->pp_lo[r], lgrid[r],
+                                     r, record, nt, e->pair_words, s),
+                    "pull pair");
+          } else {
+            HIP_TRY(launch_pull(pa, e->d_pull.as<PullChunk>() + e->pull_off[r], e->pull_off[r + 1] - e->pull_off[r],
+                                lgrid[r], r, record, nt, s),
+                    "pull");
+          }
           HIP_TRY(time_mark(false), "event");
         }
         if (!upfront) HIP_TRY(seed_round(r, a.a_next), "seed");
@@ -2048,6 +2226,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
                                  direct ? e->defer_into->hs_dev : nullptr, s),
             "reduce rounds");
   } else {
+  e->round_kind.clear();  // (accumulate_window: every round k_expand)
   HIP_TRY(seed_round(0, arr[0]), "seed");
   HIP_TRY(compact(0, 0), "compact");
   while (true) {
@@ -2126,6 +2305,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     f.launches = launches;
     f.mode = mode;
     f.flood_rounds = flood_rounds;
+    f.kinds = e->round_kind;
     e->last_topics = tab;
     for (uint32_t t = 0; t < nt; ++t) {
       e->last_cnt[t] = tab[t].W ? win[t].n : 0;
@@ -2164,7 +2344,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   }
   HIP_TRY(hipStreamSynchronize(s), "sync");
   if (mode == PS_MODE_FLOOD && e->flood_profile && e->flood_prof_waves) flood_profile_report(e);
-  if (!accumulate_window(st, hs.data(), ha.data(), r, planned0, mode, flood_rounds, launches, world)) {
+  if (!accumulate_window(st, hs.data(), ha.data(), r, planned0, mode, flood_rounds, launches, world,
+                         e->round_kind)) {
     e->flood_broken = true;
     return e->fail(PS_E_DEVICE, "k_flood: a dependency wait timed out (waves not co-resident?); "
                                 "per-round launches from now on");
@@ -2285,6 +2466,9 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_HOST_TIMING")) e->host_timing = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD")) e->flood_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_PULL_PAIR")) e->pair_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_PAIR_WORDS"))
+    e->pair_words = std::atoi(v) == static_cast<int>(kPairWords / 2) ? kPairWords / 2 : kPairWords;
   if (const char* v = std::getenv("PSAMD_FLOOD_PROFILE")) e->flood_profile = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD_WORDS"))
     e->flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
@@ -2734,7 +2918,8 @@ int ps_wait(ps_engine* e, ps_stats* out) {
     HIP_TRY(hipEventElapsedTime(&ms, f.ev0, f.ev1), "elapsed");
     f.st.run_ms += ms;
     f.deferred = false;
-    if (!accumulate_window(&f.st, f.hs, f.ha, f.r, f.planned0, f.mode, f.flood_rounds, f.launches, f.world)) {
+    if (!accumulate_window(&f.st, f.hs, f.ha, f.r, f.planned0, f.mode, f.flood_rounds, f.launches, f.world,
+                           f.kinds)) {
       e->flood_broken = true;
       return e->fail(PS_E_DEVICE, "k_flood: a dependency wait timed out (waves not co-resident?); "
                                   "per-round launches from now on");

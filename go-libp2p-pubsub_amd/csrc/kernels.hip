@@ -740,9 +740,10 @@ struct PullTopic {
 // the nodes' own metadata, so phase 1 costs one memory round trip.
 __device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t nk,
                                              uint32_t p_lo, uint32_t p_hi, uint64_t* src, uint8_t* genl,
-                                             uint32_t lane, uint32_t cur, PullCtr& c) {
+                                             uint32_t lane, uint32_t cur, PullCtr& c,
+                                             uint32_t stage_cap = kPullMaxKids) {
   uint32_t g0 = 0;
-  const bool staged = p_lo != kNoneNode && p_hi - p_lo < kPullMaxKids;
+  const bool staged = p_lo != kNoneNode && p_hi - p_lo < stage_cap;  // genl holds stage_cap + 8 bytes
   if (staged) {
     g0 = p_lo & ~3u;
     const uint32_t nd = ((p_hi + 4u) & ~3u) - g0;  // bytes, whole dwords
@@ -817,10 +818,12 @@ __device__ __forceinline__ void store_row8(uint64_t* p, uint64_t v) {
 // flight, then 8 stores, unconditional and branch-free (a skipped lane writes
 // its own row back unchanged, a lane past the run's end stores the run's last
 // pair again with the value its owner stores), so the compiler counts vmcnt
-// exactly instead of draining at branches.
-template <bool kRecord, bool kNT>
+// exactly instead of draining at branches.  kLds (k_pull_pair): every word
+// also goes to lrows[i], the run's rows in LDS for its children.
+template <bool kRecord, bool kNT, bool kLds = false>
 __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t nk,
-                                            const uint64_t* src, uint32_t lane, uint32_t round, PullCtr& c) {
+                                            const uint64_t* src, uint32_t lane, uint32_t round, PullCtr& c,
+                                            uint64_t* lrows = nullptr) {
   constexpr uint32_t kU = 8;
   const uint32_t W = P.W;
   const uint64_t base = P.base;
@@ -872,6 +875,7 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
         } else {
           store_row16<kNT>(out + i, x[u].v);
         }
+        if constexpr (kLds) *reinterpret_cast<uint4*>(lrows + i) = x[u].v;  // (i clamped: its owner's value)
         const bool own = x[u].go && inr;
         c.deliv += own ? popc4(x[u].v) : 0u;
         c.sw += own ? 2u : 0u;
@@ -908,6 +912,7 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
         } else {
           store_row8<kNT>(out + i, m[u]);
         }
+        if constexpr (kLds) lrows[i] = m[u];
         const bool own = go[u] && inr;
         c.deliv += own ? __popcll(m[u]) : 0u;
         c.sw += own ? 1u : 0u;
@@ -992,6 +997,221 @@ __global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __
     if (ch.e_hi > ch.e_lo) pull_ship(a, P, ch.node_begin, ch.e_lo, ch.e_hi, src, lane);
   }
   pull_flush(c, a.partials, blockIdx.x % a.slot_mod, lane, wid);
+}
+
+// k_pull_pair: rounds q and q + 1 in one launch (one rank).
+// A wave writes a run of level-d nodes as k_pull does (phase A: round q, the
+// parents' rows from HBM, reach decided from this window's generation
+// bytes), keeping the rows it writes in LDS, and then every child of the run
+// (phase B: round q + 1, level d + 1 -- the children of a BFS-numbered run
+// are consecutive ids): a child copies its parent's row as round q left it,
+// read from LDS instead of HBM, if the parent was reached and the child is
+// live, and stamps its generation.  No other wave writes those parents or
+// reads those children, so the launch needs no cross-wave ordering.
+//
+// Phase B, one sub-run of at most kPairKids children: resolve into ctab (the
+// LDS word offset of the parent's row, or kPairWords: a zero pair, so an
+// unreached child's row is written with zeros -- stale under its old
+// generation byte, so never read), then one line-aligned output stream with
+// the phase-A pipeline.
+// The first sub-run's parent ids and flags arrive prefetched (pf_p, pf_f:
+// loaded with phase A's metadata, one memory round trip for both).
+template <bool kRecord, bool kNT, uint32_t kWords>
+__device__ __forceinline__ void pair_kids(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t n1,
+                                          uint32_t c_lo, uint32_t c_hi, const uint64_t* reach,
+                                          const uint64_t* lrows, uint32_t* ctab, uint32_t lane, uint32_t round,
+                                          const uint32_t* pf_p, const uint32_t* pf_f, PullCtr& c) {
+  constexpr uint32_t kU = 8;
+  constexpr uint32_t kZero = kWords;
+  const uint32_t W = P.W;
+  const uint32_t cur = a.gen_cur & 0xFF;
+  const float rw = 1.0f / static_cast<float>(W);
+  auto split = [&](uint32_t i, int32_t& kk, int32_t& r) {
+    kk = static_cast<int32_t>(static_cast<float>(i) * rw);
+    r = static_cast<int32_t>(i) - kk * static_cast<int32_t>(W);
+    const int32_t lo = r < 0, hi = r >= static_cast<int32_t>(W);
+    kk += hi - lo;
+    r += (lo - hi) * static_cast<int32_t>(W);
+  };
+  for (uint32_t k0 = c_lo; k0 < c_hi; k0 += kPairKids) {
+    const uint32_t nk = min(kPairKids, c_hi - k0);
+#pragma unroll
+    for (uint32_t s = 0; s < kPairKids / 64; ++s) {
+      const uint32_t j0 = s * 64;
+      if (j0 >= nk) break;
+      const uint32_t j = j0 + lane;
+      const bool in = j < nk;
+      uint32_t p = kNoneNode, f = 0;
+      if (k0 == c_lo) {
+        p = in ? pf_p[s] : kNoneNode;
+        f = pf_f[s];
+      } else if (in) {
+        p = a.node_parent[k0 + j];
+        f = a.node_flags[k0 + j];
+      }
+      const uint32_t kp = p - nb;  // the parent's place in the run
+      const bool up = in && kp < n1 && (a.all_current || ((reach[kp >> 6] >> (kp & 63)) & 1ull));
+      const bool ok = up && (f & kNodeLive);
+      if (in) ctab[j] = ok ? kp * W : kZero;
+      if (ok) a.gen[k0 + j] = static_cast<uint8_t>(cur);
+      uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
+      if (lane == 0) prev = k0 + j0 > P.nbase ? a.node_parent[k0 + j0 - 1] : kNoneNode;
+      c.kids += in;
+      c.reached += ok;
+      c.parents += (up && p != prev) ? 1u : 0u;  // (its row is read from LDS: no parent words)
+    }
+    const uint32_t total = nk * W;
+    uint64_t* const out = a.seen + P.base + static_cast<uint64_t>(k0) * W;
+    const uint32_t h = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out) & 127) >> 3;
+    if (!(W & 1u)) {
+      for (uint32_t i0 = 0; i0 < total + h; i0 += kU * 128) {
+        uint4 x[kU];
+        bool go[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+          const int32_t is = static_cast<int32_t>(i0 + u * 128 + 2 * lane) - static_cast<int32_t>(h);
+          const uint32_t i = is < 0 ? 0u : (static_cast<uint32_t>(is) < total ? static_cast<uint32_t>(is) : total - 2);
+          int32_t kk, r;
+          split(i, kk, r);
+          const uint32_t off = ctab[kk];
+          go[u] = off != kZero;
+          x[u] = *reinterpret_cast<const uint4*>(lrows + (go[u] ? off + r : kZero));
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+          const int32_t is = static_cast<int32_t>(i0 + u * 128 + 2 * lane) - static_cast<int32_t>(h);
+          const bool inr = is >= 0 && static_cast<uint32_t>(is) < total;
+          const uint32_t i = is < 0 ? 0u : (inr ? static_cast<uint32_t>(is) : total - 2);
+          if constexpr (kRecord) {
+            if (go[u] && inr) {
+              *reinterpret_cast<uint4*>(out + i) = x[u];
+              const uint64_t cw = (out - a.seen) + i;
+              record_word(a.hop_rec, cw, static_cast<uint64_t>(x[u].y) << 32 | x[u].x, round);
+              record_word(a.hop_rec, cw + 1, static_cast<uint64_t>(x[u].w) << 32 | x[u].z, round);
+            }
+          } else {
+            store_row16<kNT>(out + i, x[u]);
+          }
+          const bool own = go[u] && inr;
+          c.deliv += own ? popc4(x[u]) : 0u;
+          c.sw += own ? 2u : 0u;
+        }
+      }
+    } else {
+      for (uint32_t i0 = 0; i0 < total + h; i0 += kU * 64) {
+        uint64_t m[kU];
+        bool go[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+          const int32_t is = static_cast<int32_t>(i0 + u * 64 + lane) - static_cast<int32_t>(h);
+          const uint32_t i = is < 0 ? 0u : (static_cast<uint32_t>(is) < total ? static_cast<uint32_t>(is) : total - 1);
+          int32_t kk, r;
+          split(i, kk, r);
+          const uint32_t off = ctab[kk];
+          go[u] = off != kZero;
+          m[u] = lrows[go[u] ? off + r : kZero];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+          const int32_t is = static_cast<int32_t>(i0 + u * 64 + lane) - static_cast<int32_t>(h);
+          const bool inr = is >= 0 && static_cast<uint32_t>(is) < total;
+          const uint32_t i = is < 0 ? 0u : (inr ? static_cast<uint32_t>(is) : total - 1);
+          if constexpr (kRecord) {
+            if (go[u] && inr) {
+              out[i] = m[u];
+              record_word(a.hop_rec, (out - a.seen) + i, m[u], round);
+            }
+          } else {
+            store_row8<kNT>(out + i, m[u]);
+          }
+          const bool own = go[u] && inr;
+          c.deliv += own ? __popcll(m[u]) : 0u;
+          c.sw += own ? 1u : 0u;
+        }
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void ctr_add(PullCtr& d, const PullCtr& s) {
+  d.deliv += s.deliv;
+  d.dup += s.dup;
+  d.sw += s.sw;
+  d.kids += s.kids;
+  d.reached += s.reached;
+  d.parents += s.parents;
+  d.pwords += s.pwords;
+}
+
+template <bool kRecord, bool kNT2, uint32_t kWords>
+__global__ __launch_bounds__(kBlock, kWords == kPairWords ? 4 : 6) void k_pull_pair(PullArgs a, const PullChunk* __restrict__ chunks,
+                                                      uint32_t n_chunks, uint32_t round) {
+  __shared__ uint64_t rows_lds[kBlock / 64][kWords + 2];  // + the zero pair
+  __shared__ uint64_t tab_lds[kBlock / 64][kPairPar];         // phase A sources, then phase B's ctab
+  __shared__ uint32_t gen_lds[kBlock / 64][kPairPar / 4 + 2];
+  __shared__ uint64_t reach_lds[kBlock / 64][kPairPar / 64];
+  static_assert(kPairKids * 4 <= kPairPar * 8, "ctab fits the source table");
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t wave = blockIdx.x * (kBlock / 64) + wid;
+  uint64_t* rows = rows_lds[wid];
+  uint64_t* src = tab_lds[wid];
+  uint64_t* reach = reach_lds[wid];
+  uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds[wid]);
+  const uint32_t cur = a.gen_cur & 0xFF;
+  PullCtr c, c2;
+  if (wave < n_chunks) {
+    const PullChunk ch = chunks[wave];
+    const TopicDev T = a.topics[ch.topic];
+    PullTopic P;
+    P.W = ch.W;
+    P.nbase = T.nbase;
+    P.base = (static_cast<uint64_t>(ch.row0_hi) << 32 | ch.row0_lo) - static_cast<uint64_t>(T.nbase) * ch.W;
+    P.root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
+    const uint32_t n1 = ch.node_end - ch.node_begin;  // <= kPairPar, n1 * W <= kWords (host plan)
+    const bool late = ch.c_lo == kNoneNode;           // a level-1 run of round q + 1
+    if (lane < 2) rows[kWords + lane] = 0;
+    // the first children's metadata, issued ahead of phase A's own
+    uint32_t pf_p[kPairKids / 64], pf_f[kPairKids / 64];
+    const uint32_t nk0 = late ? 0u : min(kPairKids, ch.c_hi - ch.c_lo);
+#pragma unroll
+    for (uint32_t s = 0; s < kPairKids / 64; ++s) {
+      const uint32_t j = s * 64 + lane;
+      pf_p[s] = j < nk0 ? a.node_parent[ch.c_lo + j] : kNoneNode;
+      pf_f[s] = j < nk0 ? a.node_flags[ch.c_lo + j] : 0u;
+    }
+    PullCtr ca;
+    pull_resolve(a, P, ch.node_begin, n1, ch.p_lo, ch.p_hi, src, genl, lane, cur, ca, kPairPar);
+    for (uint32_t j0 = 0; j0 < n1; j0 += 64) {
+      const uint64_t b = __ballot(j0 + lane < n1 && src[j0 + lane] != 0);
+      if (lane == 0) reach[j0 >> 6] = b;
+    }
+    pull_stream<kRecord, true, true>(a, P, ch.node_begin, n1, src, lane, round + (late ? 1 : 0), ca, rows);
+    if (late) {
+      ctr_add(c2, ca);
+    } else {
+      ctr_add(c, ca);
+      if (ch.c_hi > ch.c_lo)
+        pair_kids<kRecord, kNT2, kWords>(a, P, ch.node_begin, n1, ch.c_lo, ch.c_hi, reach, rows,
+                                         reinterpret_cast<uint32_t*>(src), lane, round + 1, pf_p, pf_f, c2);
+    }
+  }
+  pull_flush(c, a.partials, blockIdx.x % a.slot_mod, lane, wid);
+  __syncthreads();  // (pull_flush's block table is reused)
+  pull_flush(c2, a.partials2, blockIdx.x % a.slot_mod, lane, wid);
+}
+
+// Children ranges of the pair chunks (GPU or host node space alike).
+__global__ __launch_bounds__(kBlock) void k_pair_kids(PullChunk* __restrict__ chunks, uint32_t n,
+                                                      const uint32_t* __restrict__ row_ptr,
+                                                      const uint32_t* __restrict__ col) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  PullChunk& c = chunks[i];
+  if (c.c_lo == kNoneNode) return;
+  const uint32_t rb = row_ptr[c.node_begin], re = row_ptr[c.node_end];
+  c.c_lo = re > rb ? col[rb] : 0u;
+  c.c_hi = re > rb ? col[re - 1] + 1u : 0u;
 }
 
 // Multi-GPU level mode: the round's ghost rows.  Thread i of the flattened
@@ -1342,6 +1562,39 @@ hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_ch
     hipLaunchKernelGGL((k_pull<false, true>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
   else
     hipLaunchKernelGGL((k_pull<false, false>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
+  return hipGetLastError();
+}
+
+template <uint32_t kWords>
+void pull_pair_as(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks, uint32_t grid, uint32_t round,
+                  bool record, bool nt2, hipStream_t s) {
+  if (record)
+    hipLaunchKernelGGL((k_pull_pair<true, false, kWords>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks,
+                       round);
+  else if (nt2)
+    hipLaunchKernelGGL((k_pull_pair<false, true, kWords>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks,
+                       round);
+  else
+    hipLaunchKernelGGL((k_pull_pair<false, false, kWords>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks,
+                       round);
+}
+
+hipError_t launch_pull_pair(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks, uint32_t grid,
+                            uint32_t round, bool record, bool nt2, uint32_t words, hipStream_t s) {
+  if (n_chunks == 0 || grid == 0) return hipSuccess;
+  if (words == kPairWords)
+    pull_pair_as<kPairWords>(a, chunks, n_chunks, grid, round, record, nt2, s);
+  else if (words == kPairWords / 2)
+    pull_pair_as<kPairWords / 2>(a, chunks, n_chunks, grid, round, record, nt2, s);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_pair_kids(PullChunk* chunks, uint32_t n, const uint32_t* row_ptr, const uint32_t* col,
+                            hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pair_kids, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, chunks, n, row_ptr, col);
   return hipGetLastError();
 }
 

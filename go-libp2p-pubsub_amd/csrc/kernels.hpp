@@ -136,7 +136,10 @@ struct PullChunk {
   // multi-GPU: PullArgs::ship entries [e_lo, e_hi) -- ghost records of the
   // next round for nodes of this chunk, written by the wave that writes them
   uint32_t e_lo, e_hi;
-  uint32_t pad[2];
+  // k_pull_pair: the children of [node_begin, node_end) (consecutive ids,
+  // filled in on the device), written in round q + 1 by the same wave; c_lo =
+  // kNoneNode: a run written in round q + 1 itself (level 1 under a root)
+  uint32_t c_lo, c_hi;
 };
 constexpr uint32_t kPullMaxKids = 512;
 constexpr uint32_t kNoneNode = 0xFFFFFFFFu;
@@ -167,7 +170,18 @@ struct PullArgs {
   uint64_t* send;
   uint32_t gen_cur;
   uint32_t slot_mod;   // block b adds its counters into partial slot b % slot_mod (zeroed per window)
+  // k_pull_pair: round q + 1's partial slots; all_current: every generation
+  // byte was stamped up front (PS_F_NO_LAZY_SEEN), so every parent counts as
+  // reached, as the generation test of a separate launch would find
+  uint64_t* partials2;
+  uint32_t all_current;
 };
+// k_pull_pair: per wave, a run of at most kPairPar nodes
+// whose rows (at most kPairWords words in all) stay in LDS for its children,
+// streamed kPairKids children at a time
+constexpr uint32_t kPairWords = 1024;
+constexpr uint32_t kPairPar = 128;
+constexpr uint32_t kPairKids = 256;
 constexpr uint64_t kGhostNone = ~0ull;
 
 // Multi-GPU level mode: before round q, each rank ships the
@@ -313,6 +327,19 @@ hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, uint3
 // blocks; nt: the row stores are non-temporal (rounds nobody re-reads soon)
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
                        uint32_t grid, uint32_t round, bool record, bool nt, hipStream_t s);
+
+// Level mode, rounds q and q + 1 in one launch (one rank): a wave writes its
+// run's rows (round q, always non-temporal: the run's children are written
+// from LDS, nothing re-reads them), then the children's rows (round q + 1;
+// nt2: non-temporal too)
+// words: the LDS row stage per wave, kPairWords or kPairWords / 2 (the
+// chunks' rows must fit it)
+hipError_t launch_pull_pair(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks, uint32_t grid,
+                            uint32_t round, bool record, bool nt2, uint32_t words, hipStream_t s);
+// Fills PullChunk::c_lo / c_hi of pair chunks from the device CSR (children
+// of a BFS-numbered run are consecutive ids)
+hipError_t launch_pair_kids(PullChunk* chunks, uint32_t n, const uint32_t* row_ptr, const uint32_t* col,
+                            hipStream_t s);
 
 // multi-GPU level mode: the round's ghost rows into the send buffer
 hipError_t launch_pack(const PackEntry* entries, const PackSeg* segs, uint32_t n_segs, uint64_t total_units,

@@ -30,6 +30,10 @@ F_NO_LAZY_SEEN = 0x4
 F_COMPACT = 0x8
 MODE_COMPACT, MODE_LEVEL_PULL, MODE_FLOOD = 0, 2, 3
 # ps_stats.expand_mode -> the kernel that ran the window's rounds
+# ps_stats.round_kernel: the launch kind that wrote each round
+K_NONE, K_FLOOD, K_PULL, K_PAIR, K_PAIR2, K_EXPAND = 0, 1, 2, 3, 4, 5
+ROUND_KERNEL = {K_FLOOD: "k_flood", K_PULL: "k_pull", K_PAIR: "k_pull_pair", K_PAIR2: "k_pull_pair",
+                K_EXPAND: "k_expand"}
 MODE_KERNEL = {MODE_COMPACT: "k_expand", MODE_LEVEL_PULL: "k_pull", MODE_FLOOD: "k_flood"}
 
 # C prototypes exported by libpsengine.so: (name, restype, argtypes)
@@ -57,9 +61,11 @@ class Stats(C.Structure):
                 ("deliveries_per_round", C.c_uint64 * MAX_ROUNDS),
                 ("expand_ms_per_round", C.c_float * MAX_ROUNDS),
                 ("frontier_per_round", C.c_uint32 * MAX_ROUNDS),
-                ("expand_bytes_per_round", C.c_uint64 * MAX_ROUNDS)]
+                ("expand_bytes_per_round", C.c_uint64 * MAX_ROUNDS),
+                ("round_kernel", C.c_uint8 * MAX_ROUNDS)]
 
-    PER_ROUND = ("deliveries_per_round", "expand_ms_per_round", "frontier_per_round", "expand_bytes_per_round")
+    PER_ROUND = ("deliveries_per_round", "expand_ms_per_round", "frontier_per_round", "expand_bytes_per_round",
+                 "round_kernel")
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_ if k not in self.PER_ROUND}

@@ -91,7 +91,17 @@ typedef struct ps_stats {
   float expand_ms_per_round[PS_MAX_ROUNDS];   /* TIME flag, summed over windows  */
   uint32_t frontier_per_round[PS_MAX_ROUNDS]; /* expanded entries per round      */
   uint64_t expand_bytes_per_round[PS_MAX_ROUNDS]; /* algorithmic bytes per round */
+  uint8_t round_kernel[PS_MAX_ROUNDS]; /* PS_K_*: the launch kind that wrote each
+                                          round of the last window              */
 } ps_stats;
+
+/* ps_stats.round_kernel */
+#define PS_K_NONE 0u
+#define PS_K_FLOOD 1u   /* k_flood (its one launch is timed into round 1)      */
+#define PS_K_PULL 2u    /* k_pull, one launch for this round                   */
+#define PS_K_PAIR 3u    /* k_pull_pair: this round and the next in one launch   */
+#define PS_K_PAIR2 4u   /* k_pull_pair: the second round of the launch above    */
+#define PS_K_EXPAND 5u  /* k_expand (compaction mode)                          */
 
 typedef struct ps_engine ps_engine;
 

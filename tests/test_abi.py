@@ -49,11 +49,13 @@ def test_code_object_is_gfx950(lib):
 
 def test_struct_layouts(lib):
     assert ctypes.sizeof(PE.Config) == 40
-    assert ctypes.sizeof(PE.Stats) == 9 * 8 + 3 * 8 + 8 + PE.MAX_ROUNDS * 24
+    assert ctypes.sizeof(PE.Stats) == 9 * 8 + 3 * 8 + 8 + PE.MAX_ROUNDS * 25
     src = open(HEADER).read()
     assert f"#define PS_MAX_ROUNDS {PE.MAX_ROUNDS}" in src
     for name, val in [("PS_F_RECORD_HOPS", PE.F_RECORD_HOPS), ("PS_F_TIME_KERNELS", PE.F_TIME_KERNELS)]:
         assert re.search(rf"#define {name} 0x{val:x}u", src)
+    for name in ("NONE", "FLOOD", "PULL", "PAIR", "PAIR2", "EXPAND"):  # ps_stats.round_kernel
+        assert re.search(rf"#define PS_K_{name} {getattr(PE, 'K_' + name)}u", src)
 
 
 def test_version_and_error_paths(lib):

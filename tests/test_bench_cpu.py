@@ -39,6 +39,23 @@ def test_hybrid_window_split():
     assert set(bench.kernel_split(_st(PE.MODE_FLOOD, 9, 2, flood_rounds=12, ms=ms, by=by))) == {"k_flood"}
 
 
+def test_round_kernel_split():
+    """ps_stats.round_kernel: k_flood (rounds 1..4, timed into round 1), two
+    k_pull_pair launches (rounds 5+6, 8+9, each timed into its first round),
+    k_pull for rounds 7 and 10: per-kernel bytes, time and launch counts."""
+    ms = [0.0, 0.05, 0, 0, 0, 0.3, 0.0, 0.2, 0.5, 0.0, 0.1]
+    by = [0, 1, 1, 1, 1, 100, 200, 300, 400, 500, 600]
+    st = _st(PE.MODE_FLOOD, 5, 1, rounds=10, flood_rounds=4, ms=ms, by=by)
+    st.round_kernel = [0] + [PE.K_FLOOD] * 4 + [PE.K_PAIR, PE.K_PAIR2, PE.K_PULL, PE.K_PAIR, PE.K_PAIR2,
+                                                 PE.K_PULL] + [0] * (PE.MAX_ROUNDS - 11)
+    sp = bench.kernel_split(st)
+    assert sp["k_flood"] == (4, 0.05, 1)
+    assert sp["k_pull_pair"][0] == 100 + 200 + 400 + 500 and abs(sp["k_pull_pair"][1] - 0.8) < 1e-9
+    assert sp["k_pull_pair"][2] == 2
+    assert sp["k_pull"][0] == 900 and abs(sp["k_pull"][1] - 0.3) < 1e-9 and sp["k_pull"][2] == 2
+    assert bench.hot_kernel(st) == "k_pull_pair"
+
+
 def test_pmc_traffic_matches_kernel_and_workload():
     """The committed PMC traffic is quoted only for the kernel and workload it
     was measured on."""

@@ -57,9 +57,11 @@ def run_mode(monkeypatch, flood, n, topics, live, msg_topics, record=True, start
             assert 1 <= st.flood_rounds <= st.rounds
             if top is None:
                 assert st.flood_rounds == st.rounds and st.expand_launches == 1
-            elif st.rounds < PE.MAX_ROUNDS:
+            elif st.rounds < PE.MAX_ROUNDS:  # k_pull rounds with rows, k_pull_pair round pairs
+                k = list(st.round_kernel)
                 assert st.expand_launches == 1 + sum(
-                    1 for q in range(st.flood_rounds + 1, st.rounds + 1) if st.expand_bytes_per_round[q])
+                    1 for q in range(st.flood_rounds + 1, st.rounds + 1)
+                    if (k[q] == PE.K_PULL and st.expand_bytes_per_round[q]) or k[q] == PE.K_PAIR)
         hops = [eng.hops(first + m) for m in range(len(msg_topics))] if record else None
         digest = eng.seen_digest()
     return st, hops, digest
