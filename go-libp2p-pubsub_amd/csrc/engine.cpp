@@ -1913,7 +1913,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     woff[flood_rounds + 1] = slot;
     for (uint32_t q = flood_rounds + 1; q <= planned0; ++q) {
       const bool pair = e->round_kind[q] == PS_K_PAIR;
-      lgrid[q] = ceil_div(pair ? e->pp_hi[q] - e->pp_lo[q] : e->pull_off[q + 1] - e->pull_off[q], kBlock / 64);
+      lgrid[q] = pair ? e->pp_hi[q] - e->pp_lo[q]  // (one-wave workgroups)
+                      : ceil_div(e->pull_off[q + 1] - e->pull_off[q], kBlock / 64);
       for (uint32_t k = q; k <= q + (pair ? 1u : 0u); ++k) {  // a pair launch: the same slots for both rounds
         woff[k + 1] = woff[k] + std::min<uint32_t>(lgrid[q], kPullSlots);
         desc[3 * k] = woff[k];

@@ -1143,21 +1143,32 @@ __device__ __forceinline__ void ctr_add(PullCtr& d, const PullCtr& s) {
   d.pwords += s.pwords;
 }
 
+// One wave per workgroup: a chunk's two phases take longer when its run has
+// more children, and a wave that finished early would otherwise hold its
+// block's LDS at a block barrier until its siblings are done; each wave
+// adds its counters with its own atomics instead.
+__device__ __forceinline__ void pull_flush_wave(const PullCtr& c, uint64_t* partials, uint64_t slot, uint32_t lane) {
+  const uint64_t v7[7] = {wave_sum_u64(c.deliv),   wave_sum_u64(c.sw),      wave_sum_u64(c.kids),
+                          wave_sum_u64(c.reached), wave_sum_u64(c.parents), wave_sum_u64(c.pwords),
+                          wave_sum_u64(c.dup)};
+  if (lane < kNumCtr) {
+    const uint64_t v = pull_ctr_pick(v7, lane);
+    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(partials + slot * kNumCtr + lane),
+                     static_cast<unsigned long long>(v));
+  }
+}
+
 template <bool kRecord, bool kNT2, uint32_t kWords>
-__global__ __launch_bounds__(kBlock, kWords == kPairWords ? 4 : 6) void k_pull_pair(PullArgs a, const PullChunk* __restrict__ chunks,
-                                                      uint32_t n_chunks, uint32_t round) {
-  __shared__ uint64_t rows_lds[kBlock / 64][kWords + 2];  // + the zero pair
-  __shared__ uint64_t tab_lds[kBlock / 64][kPairPar];         // phase A sources, then phase B's ctab
-  __shared__ uint32_t gen_lds[kBlock / 64][kPairPar / 4 + 2];
-  __shared__ uint64_t reach_lds[kBlock / 64][kPairPar / 64];
+__global__ __launch_bounds__(64) void k_pull_pair(PullArgs a, const PullChunk* __restrict__ chunks,
+                                                  uint32_t n_chunks, uint32_t round) {
+  __shared__ uint64_t rows[kWords + 2];  // + the zero pair
+  __shared__ uint64_t src[kPairPar];     // phase A sources, then phase B's ctab
+  __shared__ uint32_t gen_lds[kPairPar / 4 + 2];
+  __shared__ uint64_t reach[kPairPar / 64];
   static_assert(kPairKids * 4 <= kPairPar * 8, "ctab fits the source table");
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t wave = blockIdx.x * (kBlock / 64) + wid;
-  uint64_t* rows = rows_lds[wid];
-  uint64_t* src = tab_lds[wid];
-  uint64_t* reach = reach_lds[wid];
-  uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds[wid]);
+  const uint32_t lane = threadIdx.x;
+  const uint32_t wave = blockIdx.x;
+  uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds);
   const uint32_t cur = a.gen_cur & 0xFF;
   PullCtr c, c2;
   if (wave < n_chunks) {
@@ -1196,9 +1207,8 @@ __global__ __launch_bounds__(kBlock, kWords == kPairWords ? 4 : 6) void k_pull_p
                                          reinterpret_cast<uint32_t*>(src), lane, round + 1, pf_p, pf_f, c2);
     }
   }
-  pull_flush(c, a.partials, blockIdx.x % a.slot_mod, lane, wid);
-  __syncthreads();  // (pull_flush's block table is reused)
-  pull_flush(c2, a.partials2, blockIdx.x % a.slot_mod, lane, wid);
+  pull_flush_wave(c, a.partials, blockIdx.x % a.slot_mod, lane);
+  pull_flush_wave(c2, a.partials2, blockIdx.x % a.slot_mod, lane);
 }
 
 // Children ranges of the pair chunks (GPU or host node space alike).
@@ -1556,6 +1566,12 @@ hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
                        uint32_t grid, uint32_t round, bool record, bool nt, hipStream_t s) {
   if (n_chunks == 0 || grid == 0) return hipSuccess;
+  static const size_t xlds = std::getenv("PSAMD_XLDS") ? std::atoi(std::getenv("PSAMD_XLDS")) : 0;  // EXPERIMENT
+  if (xlds && !record) {
+    if (nt) hipLaunchKernelGGL((k_pull<false, true>), dim3(grid), dim3(kBlock), xlds, s, a, chunks, n_chunks, round);
+    else hipLaunchKernelGGL((k_pull<false, false>), dim3(grid), dim3(kBlock), xlds, s, a, chunks, n_chunks, round);
+    return hipGetLastError();
+  }
   if (record)  // parity runs: one variant
     hipLaunchKernelGGL((k_pull<true, false>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
   else if (nt)
@@ -1569,14 +1585,11 @@ template <uint32_t kWords>
 void pull_pair_as(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks, uint32_t grid, uint32_t round,
                   bool record, bool nt2, hipStream_t s) {
   if (record)
-    hipLaunchKernelGGL((k_pull_pair<true, false, kWords>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks,
-                       round);
+    hipLaunchKernelGGL((k_pull_pair<true, false, kWords>), dim3(grid), dim3(64), 0, s, a, chunks, n_chunks, round);
   else if (nt2)
-    hipLaunchKernelGGL((k_pull_pair<false, true, kWords>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks,
-                       round);
+    hipLaunchKernelGGL((k_pull_pair<false, true, kWords>), dim3(grid), dim3(64), 0, s, a, chunks, n_chunks, round);
   else
-    hipLaunchKernelGGL((k_pull_pair<false, false, kWords>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks,
-                       round);
+    hipLaunchKernelGGL((k_pull_pair<false, false, kWords>), dim3(grid), dim3(64), 0, s, a, chunks, n_chunks, round);
 }
 
 hipError_t launch_pull_pair(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks, uint32_t grid,

@@ -333,7 +333,8 @@ hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_ch
 // from LDS, nothing re-reads them), then the children's rows (round q + 1;
 // nt2: non-temporal too)
 // words: the LDS row stage per wave, kPairWords or kPairWords / 2 (the
-// chunks' rows must fit it)
+// chunks' rows must fit it); one 64-thread workgroup per chunk, grid =
+// n_chunks
 hipError_t launch_pull_pair(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks, uint32_t grid,
                             uint32_t round, bool record, bool nt2, uint32_t words, hipStream_t s);
 // Fills PullChunk::c_lo / c_hi of pair chunks from the device CSR (children
