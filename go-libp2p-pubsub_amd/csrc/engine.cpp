@@ -184,7 +184,6 @@ struct ps_engine {
   // k_pull_pair: rounds q and q + 1 in one launch, one rank
   // (PSAMD_PULL_PAIR=0: one k_pull launch per round)
   bool pair_on = true;
-  uint32_t pair_words = kPairWords;  // LDS row stage per wave (PSAMD_PAIR_WORDS: 1024 or 512)
   std::vector<uint64_t> pp_key;
   std::vector<PullChunk> pp_host;
   std::vector<uint32_t> pp_lo, pp_hi;  // round q: chunks of the pair launch starting at q
@@ -1093,10 +1092,10 @@ int build_pair_chunks(ps_engine* e, const std::vector<TopicDev>& tab,
                       const std::vector<std::vector<StartGroup>>& groups, uint32_t rounds, uint32_t first) {
   std::vector<uint64_t> key = e->pull_key;  // (graph, flags, rounds, row widths, start groups)
   key.push_back(first);
-  key.push_back(e->pair_on ? e->pair_words : 0);
+  key.push_back(e->pair_on ? 1 : 0);
   if (key == e->pp_key) return PS_OK;
-  const uint32_t stage = e->pair_words;
-  constexpr double kLaunchBytes = 16e6;  // ~3 us of launch ramp and tail at ~5.5 TB/s
+  constexpr uint32_t stage = kPairWords;
+  constexpr double kLaunchBytes = 16e6;  // ~3 us of launch ramp and tail at ~5.5 TB/s (64, 200 MB: same plan on cfg3)
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
   auto& kind = e->pp_kind;
   kind.assign(rounds + 2, PS_K_NONE);
@@ -1913,10 +1912,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     woff[flood_rounds + 1] = slot;
     for (uint32_t q = flood_rounds + 1; q <= planned0; ++q) {
       const bool pair = e->round_kind[q] == PS_K_PAIR;
-      lgrid[q] = pair ? e->pp_hi[q] - e->pp_lo[q]  // (one-wave workgroups)
+      lgrid[q] = pair ? e->pp_hi[q] - e->pp_lo[q]  // (one one-wave workgroup per chunk)
                       : ceil_div(e->pull_off[q + 1] - e->pull_off[q], kBlock / 64);
       for (uint32_t k = q; k <= q + (pair ? 1u : 0u); ++k) {  // a pair launch: the same slots for both rounds
-        woff[k + 1] = woff[k] + std::min<uint32_t>(lgrid[q], kPullSlots);
+        woff[k + 1] = woff[k] + std::min<uint32_t>(lgrid[q], pair ? kPairSlots : kPullSlots);
         desc[3 * k] = woff[k];
         desc[3 * k + 1] = woff[k + 1];
         desc[3 * k + 2] = 1;
@@ -2204,9 +2203,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
           const bool nt = rw < e->pull_bytes.size() && (e->pull_bytes[rw] >= (64ull << 20) || rw == planned0);
           if (pair) {
             pa.partials2 = partials + static_cast<size_t>(e->woff_host[r + 1]) * kNumCtr;
+            pa.slot_mod = kPairSlots;
             pa.all_current = (e->cfg.flags & PS_F_NO_LAZY_SEEN) ? 1u : 0u;
             HIP_TRY(launch_pull_pair(pa, e->d_pp.as<PullChunk>() + e->pp_lo[r], e->pp_hi[r] - e->pp_lo[r], lgrid[r],
-                                     r, record, nt, e->pair_words, s),
+                                     r, record, nt, s),
                     "pull pair");
           } else {
             HIP_TRY(launch_pull(pa, e->d_pull.as<PullChunk>() + e->pull_off[r], e->pull_off[r + 1] - e->pull_off[r],
@@ -2468,8 +2468,6 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD")) e->flood_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_PAIR")) e->pair_on = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_PAIR_WORDS"))
-    e->pair_words = std::atoi(v) == static_cast<int>(kPairWords / 2) ? kPairWords / 2 : kPairWords;
   if (const char* v = std::getenv("PSAMD_FLOOD_PROFILE")) e->flood_profile = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD_WORDS"))
     e->flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));

@@ -725,6 +725,43 @@ struct PullVec {
   uint4 v;
 };
 
+// Counters of the pull kernels, two forms: PullCtr (devutil.hpp) counts per
+// lane, as k_pull's block reduction wants; WaveCtr keeps one per-lane
+// delivery sum and counts everything else wave-uniformly (ballots: scalar
+// registers), which k_pull_pair's persistent waves carry across chunks for
+// two rounds without the vector registers per-lane counters would take.
+struct WaveCtr {
+  uint32_t deliv = 0;                      // per lane
+  uint32_t kids = 0, reached = 0, parents = 0;  // wave-uniform
+  uint64_t sw = 0, pwords = 0;             // wave-uniform: words written, parent words read
+};
+// One batch of (up to 64) nodes: visited (in), reached (ok), a reached
+// parent's first child (par); W_sw row words written per reached node,
+// W_pw parent row words read per counted parent.
+__device__ __forceinline__ void ctr_nodes(PullCtr& c, bool in, bool ok, bool par, uint32_t, uint32_t W_pw) {
+  c.kids += in;
+  c.reached += ok;
+  if (par) {
+    c.parents += 1;
+    c.pwords += W_pw;
+  }
+}
+__device__ __forceinline__ void ctr_nodes(WaveCtr& c, bool in, bool ok, bool par, uint32_t W_sw, uint32_t W_pw) {
+  c.kids += __popcll(__ballot(in));
+  const uint32_t r = __popcll(__ballot(ok));
+  c.reached += r;
+  c.sw += static_cast<uint64_t>(r) * W_sw;
+  const uint32_t p = __popcll(__ballot(par));
+  c.parents += p;
+  c.pwords += static_cast<uint64_t>(p) * W_pw;
+}
+// One lane's stored unit: its delivered bits, and (PullCtr) its words.
+__device__ __forceinline__ void ctr_unit(PullCtr& c, bool own, uint32_t pop, uint32_t words) {
+  c.deliv += own ? pop : 0u;
+  c.sw += own ? words : 0u;
+}
+__device__ __forceinline__ void ctr_unit(WaveCtr& c, bool own, uint32_t pop, uint32_t) { c.deliv += own ? pop : 0u; }
+
 // Chunk constants: row of node u = base + u * W (a start group's block row
 // for kTopicGroups topics).
 struct PullTopic {
@@ -738,9 +775,10 @@ struct PullTopic {
 // parents of a run are consecutive node ids [p_lo, p_hi] (BFS numbering):
 // their generation bytes are staged into LDS by loads issued together with
 // the nodes' own metadata, so phase 1 costs one memory round trip.
+template <class Ctr>
 __device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t nk,
                                              uint32_t p_lo, uint32_t p_hi, uint64_t* src, uint8_t* genl,
-                                             uint32_t lane, uint32_t cur, PullCtr& c,
+                                             uint32_t lane, uint32_t cur, Ctr& c,
                                              uint32_t stage_cap = kPullMaxKids) {
   uint32_t g0 = 0;
   const bool staged = p_lo != kNoneNode && p_hi - p_lo < stage_cap;  // genl holds stage_cap + 8 bytes
@@ -785,12 +823,7 @@ __device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic&
     const bool ok = up && (f & kNodeLive);
     if (in) src[j] = ok ? row : 0ull;
     if (ok) a.gen[nb + j] = static_cast<uint8_t>(cur);
-    c.kids += in;
-    c.reached += ok;
-    if (up && pid != prev) {
-      c.parents += 1;
-      c.pwords += P.W;
-    }
+    ctr_nodes(c, in, ok, up && pid != prev, P.W, P.W);
   }
 }
 
@@ -820,9 +853,9 @@ __device__ __forceinline__ void store_row8(uint64_t* p, uint64_t v) {
 // pair again with the value its owner stores), so the compiler counts vmcnt
 // exactly instead of draining at branches.  kLds (k_pull_pair): every word
 // also goes to lrows[i], the run's rows in LDS for its children.
-template <bool kRecord, bool kNT, bool kLds = false>
+template <bool kRecord, bool kNT, bool kLds = false, class Ctr = PullCtr>
 __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t nk,
-                                            const uint64_t* src, uint32_t lane, uint32_t round, PullCtr& c,
+                                            const uint64_t* src, uint32_t lane, uint32_t round, Ctr& c,
                                             uint64_t* lrows = nullptr) {
   constexpr uint32_t kU = 8;
   const uint32_t W = P.W;
@@ -877,8 +910,7 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
         }
         if constexpr (kLds) *reinterpret_cast<uint4*>(lrows + i) = x[u].v;  // (i clamped: its owner's value)
         const bool own = x[u].go && inr;
-        c.deliv += own ? popc4(x[u].v) : 0u;
-        c.sw += own ? 2u : 0u;
+        ctr_unit(c, own, popc4(x[u].v), 2u);
       }
     }
   } else {
@@ -914,8 +946,7 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
         }
         if constexpr (kLds) lrows[i] = m[u];
         const bool own = go[u] && inr;
-        c.deliv += own ? __popcll(m[u]) : 0u;
-        c.sw += own ? 1u : 0u;
+        ctr_unit(c, own, __popcll(m[u]), 1u);
       }
     }
   }
@@ -1020,7 +1051,7 @@ template <bool kRecord, bool kNT, uint32_t kWords>
 __device__ __forceinline__ void pair_kids(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t n1,
                                           uint32_t c_lo, uint32_t c_hi, const uint64_t* reach,
                                           const uint64_t* lrows, uint32_t* ctab, uint32_t lane, uint32_t round,
-                                          const uint32_t* pf_p, const uint32_t* pf_f, PullCtr& c) {
+                                          const uint32_t* pf_p, const uint32_t* pf_f, WaveCtr& c) {
   constexpr uint32_t kU = 8;
   constexpr uint32_t kZero = kWords;
   const uint32_t W = P.W;
@@ -1050,15 +1081,13 @@ __device__ __forceinline__ void pair_kids(const PullArgs& a, const PullTopic& P,
         f = a.node_flags[k0 + j];
       }
       const uint32_t kp = p - nb;  // the parent's place in the run
-      const bool up = in && kp < n1 && (a.all_current || ((reach[kp >> 6] >> (kp & 63)) & 1ull));
+      const bool up = in && kp < n1 && ((a.all_current & 1u) || ((reach[kp >> 6] >> (kp & 63)) & 1ull));
       const bool ok = up && (f & kNodeLive);
       if (in) ctab[j] = ok ? kp * W : kZero;
       if (ok) a.gen[k0 + j] = static_cast<uint8_t>(cur);
       uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
       if (lane == 0) prev = k0 + j0 > P.nbase ? a.node_parent[k0 + j0 - 1] : kNoneNode;
-      c.kids += in;
-      c.reached += ok;
-      c.parents += (up && p != prev) ? 1u : 0u;  // (its row is read from LDS: no parent words)
+      ctr_nodes(c, in, ok, up && p != prev, W, 0u);  // (parent rows from LDS: no parent words read)
     }
     const uint32_t total = nk * W;
     uint64_t* const out = a.seen + P.base + static_cast<uint64_t>(k0) * W;
@@ -1093,8 +1122,7 @@ __device__ __forceinline__ void pair_kids(const PullArgs& a, const PullTopic& P,
             store_row16<kNT>(out + i, x[u]);
           }
           const bool own = go[u] && inr;
-          c.deliv += own ? popc4(x[u]) : 0u;
-          c.sw += own ? 2u : 0u;
+          ctr_unit(c, own, popc4(x[u]), 2u);
         }
       }
     } else {
@@ -1125,17 +1153,15 @@ __device__ __forceinline__ void pair_kids(const PullArgs& a, const PullTopic& P,
             store_row8<kNT>(out + i, m[u]);
           }
           const bool own = go[u] && inr;
-          c.deliv += own ? __popcll(m[u]) : 0u;
-          c.sw += own ? 1u : 0u;
+          ctr_unit(c, own, __popcll(m[u]), 1u);
         }
       }
     }
   }
 }
 
-__device__ __forceinline__ void ctr_add(PullCtr& d, const PullCtr& s) {
+__device__ __forceinline__ void ctr_add(WaveCtr& d, const WaveCtr& s) {
   d.deliv += s.deliv;
-  d.dup += s.dup;
   d.sw += s.sw;
   d.kids += s.kids;
   d.reached += s.reached;
@@ -1143,14 +1169,11 @@ __device__ __forceinline__ void ctr_add(PullCtr& d, const PullCtr& s) {
   d.pwords += s.pwords;
 }
 
-// One wave per workgroup: a chunk's two phases take longer when its run has
-// more children, and a wave that finished early would otherwise hold its
-// block's LDS at a block barrier until its siblings are done; each wave
-// adds its counters with its own atomics instead.
-__device__ __forceinline__ void pull_flush_wave(const PullCtr& c, uint64_t* partials, uint64_t slot, uint32_t lane) {
-  const uint64_t v7[7] = {wave_sum_u64(c.deliv),   wave_sum_u64(c.sw),      wave_sum_u64(c.kids),
-                          wave_sum_u64(c.reached), wave_sum_u64(c.parents), wave_sum_u64(c.pwords),
-                          wave_sum_u64(c.dup)};
+// Counters of a wave (two rounds) added with its own atomics: no block
+// reduction, so no barrier.
+__device__ __forceinline__ void pull_flush_wave(const WaveCtr& c, uint64_t* partials, uint64_t slot, uint32_t lane) {
+  // (one chunk per wave: its per-lane delivery sums total at most 2^18 bits)
+  const uint64_t v7[7] = {__reduce_add_sync(~0ull, c.deliv), c.sw, c.kids, c.reached, c.parents, c.pwords, 0ull};
   if (lane < kNumCtr) {
     const uint64_t v = pull_ctr_pick(v7, lane);
     if (v) atomicAdd(reinterpret_cast<unsigned long long*>(partials + slot * kNumCtr + lane),
@@ -1158,30 +1181,37 @@ __device__ __forceinline__ void pull_flush_wave(const PullCtr& c, uint64_t* part
   }
 }
 
-template <bool kRecord, bool kNT2, uint32_t kWords>
+// One wave per workgroup, one chunk per wave (grid = n_chunks; the loop
+// only guards a smaller grid).  A chunk's two phases take longer when its
+// run has more children: one-wave workgroups never wait for siblings (a
+// 4-wave block's barrier held its LDS behind the slowest chunk: cfg3 (18,19)
+// 583 -> 549 us).  Persistent waves looping over chunks measured slower at
+// every grid tried (resident grid 700 us, 8192 waves 588 us, one chunk per
+// wave 543 us): a wave's chunks run back to back, each paying its round
+// trips, where fresh waves overlap them.
+template <bool kRecord, bool kNT2>
 __global__ __launch_bounds__(64) void k_pull_pair(PullArgs a, const PullChunk* __restrict__ chunks,
                                                   uint32_t n_chunks, uint32_t round) {
-  __shared__ uint64_t rows[kWords + 2];  // + the zero pair
-  __shared__ uint64_t src[kPairPar];     // phase A sources, then phase B's ctab
+  __shared__ uint64_t rows[kPairWords + 2];  // + the zero pair
+  __shared__ uint64_t src[kPairPar];         // phase A sources, then phase B's ctab
   __shared__ uint32_t gen_lds[kPairPar / 4 + 2];
   __shared__ uint64_t reach[kPairPar / 64];
   static_assert(kPairKids * 4 <= kPairPar * 8, "ctab fits the source table");
   const uint32_t lane = threadIdx.x;
-  const uint32_t wave = blockIdx.x;
   uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds);
   const uint32_t cur = a.gen_cur & 0xFF;
-  PullCtr c, c2;
-  if (wave < n_chunks) {
-    const PullChunk ch = chunks[wave];
+  if (lane < 2) rows[kPairWords + lane] = 0;
+  WaveCtr c, c2;
+  for (uint32_t ci = blockIdx.x; ci < n_chunks; ci += gridDim.x) {
+    const PullChunk ch = chunks[ci];
     const TopicDev T = a.topics[ch.topic];
     PullTopic P;
     P.W = ch.W;
     P.nbase = T.nbase;
     P.base = (static_cast<uint64_t>(ch.row0_hi) << 32 | ch.row0_lo) - static_cast<uint64_t>(T.nbase) * ch.W;
     P.root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
-    const uint32_t n1 = ch.node_end - ch.node_begin;  // <= kPairPar, n1 * W <= kWords (host plan)
+    const uint32_t n1 = ch.node_end - ch.node_begin;  // <= kPairPar, n1 * W <= kPairWords (host plan)
     const bool late = ch.c_lo == kNoneNode;           // a level-1 run of round q + 1
-    if (lane < 2) rows[kWords + lane] = 0;
     // the first children's metadata, issued ahead of phase A's own
     uint32_t pf_p[kPairKids / 64], pf_f[kPairKids / 64];
     const uint32_t nk0 = late ? 0u : min(kPairKids, ch.c_hi - ch.c_lo);
@@ -1191,7 +1221,7 @@ __global__ __launch_bounds__(64) void k_pull_pair(PullArgs a, const PullChunk* _
       pf_p[s] = j < nk0 ? a.node_parent[ch.c_lo + j] : kNoneNode;
       pf_f[s] = j < nk0 ? a.node_flags[ch.c_lo + j] : 0u;
     }
-    PullCtr ca;
+    WaveCtr ca;
     pull_resolve(a, P, ch.node_begin, n1, ch.p_lo, ch.p_hi, src, genl, lane, cur, ca, kPairPar);
     for (uint32_t j0 = 0; j0 < n1; j0 += 64) {
       const uint64_t b = __ballot(j0 + lane < n1 && src[j0 + lane] != 0);
@@ -1203,8 +1233,8 @@ __global__ __launch_bounds__(64) void k_pull_pair(PullArgs a, const PullChunk* _
     } else {
       ctr_add(c, ca);
       if (ch.c_hi > ch.c_lo)
-        pair_kids<kRecord, kNT2, kWords>(a, P, ch.node_begin, n1, ch.c_lo, ch.c_hi, reach, rows,
-                                         reinterpret_cast<uint32_t*>(src), lane, round + 1, pf_p, pf_f, c2);
+        pair_kids<kRecord, kNT2, kPairWords>(a, P, ch.node_begin, n1, ch.c_lo, ch.c_hi, reach, rows,
+                                             reinterpret_cast<uint32_t*>(src), lane, round + 1, pf_p, pf_f, c2);
     }
   }
   pull_flush_wave(c, a.partials, blockIdx.x % a.slot_mod, lane);
@@ -1566,12 +1596,6 @@ hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
                        uint32_t grid, uint32_t round, bool record, bool nt, hipStream_t s) {
   if (n_chunks == 0 || grid == 0) return hipSuccess;
-  static const size_t xlds = std::getenv("PSAMD_XLDS") ? std::atoi(std::getenv("PSAMD_XLDS")) : 0;  // EXPERIMENT
-  if (xlds && !record) {
-    if (nt) hipLaunchKernelGGL((k_pull<false, true>), dim3(grid), dim3(kBlock), xlds, s, a, chunks, n_chunks, round);
-    else hipLaunchKernelGGL((k_pull<false, false>), dim3(grid), dim3(kBlock), xlds, s, a, chunks, n_chunks, round);
-    return hipGetLastError();
-  }
   if (record)  // parity runs: one variant
     hipLaunchKernelGGL((k_pull<true, false>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
   else if (nt)
@@ -1581,26 +1605,16 @@ hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_ch
   return hipGetLastError();
 }
 
-template <uint32_t kWords>
-void pull_pair_as(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks, uint32_t grid, uint32_t round,
-                  bool record, bool nt2, hipStream_t s) {
-  if (record)
-    hipLaunchKernelGGL((k_pull_pair<true, false, kWords>), dim3(grid), dim3(64), 0, s, a, chunks, n_chunks, round);
-  else if (nt2)
-    hipLaunchKernelGGL((k_pull_pair<false, true, kWords>), dim3(grid), dim3(64), 0, s, a, chunks, n_chunks, round);
-  else
-    hipLaunchKernelGGL((k_pull_pair<false, false, kWords>), dim3(grid), dim3(64), 0, s, a, chunks, n_chunks, round);
-}
-
 hipError_t launch_pull_pair(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks, uint32_t grid,
-                            uint32_t round, bool record, bool nt2, uint32_t words, hipStream_t s) {
+                            uint32_t round, bool record, bool nt2, hipStream_t s) {
   if (n_chunks == 0 || grid == 0) return hipSuccess;
-  if (words == kPairWords)
-    pull_pair_as<kPairWords>(a, chunks, n_chunks, grid, round, record, nt2, s);
-  else if (words == kPairWords / 2)
-    pull_pair_as<kPairWords / 2>(a, chunks, n_chunks, grid, round, record, nt2, s);
+  grid = grid < n_chunks ? grid : n_chunks;
+  if (record)
+    hipLaunchKernelGGL((k_pull_pair<true, false>), dim3(grid), dim3(64), 0, s, a, chunks, n_chunks, round);
+  else if (nt2)
+    hipLaunchKernelGGL((k_pull_pair<false, true>), dim3(grid), dim3(64), 0, s, a, chunks, n_chunks, round);
   else
-    return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_pull_pair<false, false>), dim3(grid), dim3(64), 0, s, a, chunks, n_chunks, round);
   return hipGetLastError();
 }
 

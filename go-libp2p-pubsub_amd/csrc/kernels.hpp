@@ -200,6 +200,9 @@ struct PackSeg {
 };
 __host__ __device__ inline uint32_t pack_units(uint32_t W) { return (W & 1u) ? W : W >> 1; }
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch
+// k_pull_pair: every wave adds its counters with atomics (no block
+// reduction) into slot wave % kPairSlots
+constexpr uint32_t kPairSlots = 4096;
 
 // k_flood (flood.hip): every round of a single-start tree
 // window in one persistent launch.  A task = the nodes [nb, ne) of one BFS
@@ -332,11 +335,10 @@ hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_ch
 // run's rows (round q, always non-temporal: the run's children are written
 // from LDS, nothing re-reads them), then the children's rows (round q + 1;
 // nt2: non-temporal too)
-// words: the LDS row stage per wave, kPairWords or kPairWords / 2 (the
-// chunks' rows must fit it); one 64-thread workgroup per chunk, grid =
-// n_chunks
+// One-wave workgroups, one chunk each (grid = n_chunks); a chunk's rows fit
+// the kPairWords LDS stage
 hipError_t launch_pull_pair(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks, uint32_t grid,
-                            uint32_t round, bool record, bool nt2, uint32_t words, hipStream_t s);
+                            uint32_t round, bool record, bool nt2, hipStream_t s);
 // Fills PullChunk::c_lo / c_hi of pair chunks from the device CSR (children
 // of a BFS-numbered run are consecutive ids)
 hipError_t launch_pair_kids(PullChunk* chunks, uint32_t n, const uint32_t* row_ptr, const uint32_t* col,
