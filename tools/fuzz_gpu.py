@@ -104,7 +104,7 @@ def case_topology(rng, max_peers):
     return None
 
 
-MODE_ENV = ("PSAMD_FLOOD", "PSAMD_FLOOD_TOP_BYTES", "PSAMD_FLOOD_WORDS")
+MODE_ENV = ("PSAMD_FLOOD", "PSAMD_FLOOD_TOP_BYTES", "PSAMD_FLOOD_WORDS", "PSAMD_PULL_PAIR")
 
 
 def set_modes(rng):
@@ -117,6 +117,8 @@ def set_modes(rng):
         os.environ["PSAMD_FLOOD_TOP_BYTES"] = str(int(rng.choice([0, 256, 4096, 65536])))
     if rng.random() < 0.3:
         os.environ["PSAMD_FLOOD_WORDS"] = str(int(rng.choice([64, 256, 4096])))
+    if rng.random() < 0.3:
+        os.environ["PSAMD_PULL_PAIR"] = "0"
 
 
 def case_modes(rng, max_peers):
@@ -141,8 +143,9 @@ def case_modes(rng, max_peers):
     ref = None
     window = int(rng.choice([128, 65536]))
     modes = [({}, 0), ({}, PE.F_COMPACT), ({"PSAMD_FLOOD": "0"}, 0),
+             ({"PSAMD_FLOOD": "0", "PSAMD_PULL_PAIR": "0"}, 0),
              ({"PSAMD_FLOOD_TOP_BYTES": str(int(rng.choice([0, 512, 1 << 30])))}, 0),
-             ({"PSAMD_FLOOD_WORDS": "64"}, 0)]
+             ({"PSAMD_FLOOD_WORDS": "64"}, 0), ({}, PE.F_NO_LAZY_SEEN)]
     for env, flags in modes:
         for k in MODE_ENV:
             os.environ.pop(k, None)
