@@ -380,6 +380,9 @@ def main():
     ap.add_argument("--scale", type=float, default=1.0, help="shrink the workload (debug)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--sustain", type=float, default=8.0,
+                    help="seconds of back-to-back pipelined steps after the timed region (one GPU; "
+                         "reported under 'sustained', not in value); 0 skips")
     ap.add_argument("--no-check", action="store_true", help="skip delivery assertions (experiments)")
     ap.add_argument("--no-general", action="store_true",
                     help="skip the general-path leg (staggered starts, compaction mode)")
@@ -497,6 +500,19 @@ def main():
                       "expand_us_per_round": [round(x * 1e3, 1) for x in
                                               st.as_dict()["expand_ms_per_round"]]},
     }
+    if args.sustain > 0:
+        # the same pipelined steps back to back for a few seconds after the
+        # timed region: sustained throughput, and device activity long enough
+        # for a utilisation sampler polling every few seconds to see
+        n_sus, deliv_sus, t0 = 0, 0, time.perf_counter()
+        while time.perf_counter() - t0 < args.sustain:
+            for st in steps_pipelined(100):
+                deliv_sus += st.deliveries
+            n_sus += 100
+        wall_sus = time.perf_counter() - t0
+        assert args.no_check or deliv_sus == deliv_expected * n_sus
+        out["sustained"] = {"value": deliv_sus / wall_sus, "unit": "deliveries/s", "steps": n_sus,
+                            "seconds": wall_sus, "ms_per_step": wall_sus * 1e3 / n_sus}
     if not args.no_general and not args.no_check:
         out["general_path"] = general_path(eng, wl, deliv_expected, max(2, min(args.steps, 4)))
     if not args.no_cpu:

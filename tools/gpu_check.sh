@@ -19,7 +19,7 @@ if [ "${TESTS:-1}" = 1 ]; then
   tail -2 "$OUT/pytest.log"
 fi
 echo "[gpu_check] bench $(date +%T)"
-timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 $BARGS > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --sustain 3 $BARGS > "$OUT/bench.json" 2> "$OUT/bench.err"
 cat "$OUT/bench.json"
 if [ -n "${AB:-}" ]; then
   echo "[gpu_check] bench A/B ($AB) $(date +%T)"
@@ -30,7 +30,7 @@ cd /tmp && export TMPDIR=/tmp
 if [ "${TRACE:-1}" = 1 ]; then
   echo "[gpu_check] trace $(date +%T)"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace" -o run -- \
-    python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu --no-general $BARGS > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err"
+    python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu --no-general --sustain 0 $BARGS > "$OUT/bench_trace.json" 2> "$OUT/bench_trace.err"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/trace_general" -o run -- \
     python3 "$ROOT/bench.py" --steps 4 --warmup 1 --no-cpu --general-only $BARGS > "$OUT/bench_trace_general.json" 2> "$OUT/bench_trace_general.err"
 fi
@@ -42,7 +42,7 @@ if [ "${PMC:-0}" = 1 ]; then
     for C in FETCH_SIZE WRITE_SIZE; do
       echo "[gpu_check] pmc $SET $C $(date +%T)"
       timeout -s KILL 240 rocprofv3 --pmc $C -f csv -d "$OUT/pmc_${SET}/$C" -o run -- \
-        python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu $EXTRA $BARGS > "$OUT/pmc_${SET}_$C.json" 2> "$OUT/pmc_${SET}_$C.err"
+        python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu --sustain 0 $EXTRA $BARGS > "$OUT/pmc_${SET}_$C.json" 2> "$OUT/pmc_${SET}_$C.err"
     done
     python3 "$ROOT/tools/pmc_summary.py" "$OUT/pmc_${SET}" > "$OUT/pmc_summary_${SET}.json"
   done
