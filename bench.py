@@ -31,6 +31,10 @@ METRIC = "deliveries/sec (peer×msg) at 1M peers, 1/2/4/8 GPU; % of HBM roofline
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "pmc_traffic.json")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PAIR_BYTES = 28.375  # SURVEY.md §8d bytes/delivery of the (peer,msg)-pair formulation
+# HBM rates this pool's MI355X reaches (context for frac; peak stays the spec)
+MEASURED_CEILINGS = {"copy_read_plus_write_GBs": [5400, 5700], "write_only_GBs": [5800, 6100],
+                     "hipMemset_GBs": [6500, 6700],
+                     "source": "tools/probe/hbm_write_probe.hip, profiles/r02/hbm_probe.txt"}
 
 DESCR = {
     "cfg2": "100k peers, 1 topic, TreeOpts{8,20}, 10k-message burst",
@@ -241,6 +245,7 @@ def roofline_of(per, traffic=None, traffic_src=None):
     f = fig(hot)
     return {"bound": "hbm", "achieved": f["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": f["frac"], "traffic": traffic, "kernel": hot, "avg_launch_us": f["avg_launch_us"],
+            "measured_ceilings": MEASURED_CEILINGS,
             "bytes_per_launch": f["bytes_per_launch"],
             "timing": "HIP events around every launch on the engine stream, "
                       "separate instrumented steps after the timed region",
