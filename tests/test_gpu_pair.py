@@ -231,3 +231,51 @@ def test_pair_rows_wider_than_stage(monkeypatch):
         outs.append(key)
     assert outs[0] == outs[1]
     assert outs[0][0] == int((exp[0] != 0xFF).sum()) * 70000 + int((exp[1] != 0xFF).sum()) * 100
+
+
+def test_pair_deep_chain_hops_past_255(monkeypatch):
+    """A chain of 600 peers through pair launches only (PSAMD_FLOOD=0): 299
+    pair launches of one node each; hops past 255 saturate at 254 as in the
+    restatement."""
+    n = 600
+    parent = np.full(n, O.NONE, dtype=np.uint32)
+    parent[1:] = np.arange(n - 1, dtype=np.uint32)
+    live = np.ones(n, dtype=np.uint8)
+    exp = oracle_hops([(0, parent)], live)[0]
+    msg_topics = np.zeros(130, dtype=np.uint32)
+    st, kinds, hops, _, key = run(monkeypatch, True, n, [(0, parent)], live, msg_topics)
+    assert st.deliveries == 130 * (n - 1)
+    assert kinds.count(PE.K_PAIR) >= 100
+    for m in (0, 64, 129):
+        assert np.array_equal(hops[m], exp)
+    _, _, _, _, key0 = run(monkeypatch, False, n, [(0, parent)], live, msg_topics)
+    assert key == key0
+
+
+def test_pair_many_windows_and_drains(monkeypatch):
+    """1,500 messages over two topics through 128-message windows (6+ windows,
+    generations advancing per window) with start groups: pair launches give the oracle's
+    hops, and each subscriber's drain (ps_read_peer_messages: its message ids
+    in arrival order) equals the per-round launches'."""
+    rng = np.random.default_rng(997)
+    n, topics, live = make_case(rng, 1500, 2500, nt_hi=2, dead=0.08)
+    msg_topics = rng.integers(0, len(topics), size=1500).astype(np.uint32)
+    starts = rng.integers(0, 4, size=1500).astype(np.uint32)
+    exp = oracle_hops(topics, live)
+    peers = [int(p) for p in rng.integers(0, n, size=12)]
+    outs = []
+    for pair in (False, True):
+        monkeypatch.setenv("PSAMD_PULL_PAIR", "1" if pair else "0")
+        monkeypatch.setenv("PSAMD_FLOOD", "0")
+        with PE.Engine(n, len(topics), record_hops=True, msg_window=128) as eng:
+            for t, (root, parent) in enumerate(topics):
+                eng.set_tree(t, root, parent)
+            eng.set_live(live)
+            first = eng.publish(msg_topics, starts)
+            st = eng.run()
+            assert st.windows >= 6  # (128 messages per topic per window)
+            for m in range(0, 1500, 37):
+                assert np.array_equal(eng.hops(first + m), exp[int(msg_topics[m])]), (pair, m)
+            drains = [eng.peer_messages(t, p).tolist() for t in range(len(topics)) for p in peers]
+            outs.append((st.deliveries, drains))
+    assert outs[0] == outs[1]
