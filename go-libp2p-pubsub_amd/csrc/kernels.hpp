@@ -201,8 +201,10 @@ struct PackSeg {
 __host__ __device__ inline uint32_t pack_units(uint32_t W) { return (W & 1u) ? W : W >> 1; }
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch
 // k_pull_pair: every wave adds its counters with atomics (no block
-// reduction) into slot wave % kPairSlots
-constexpr uint32_t kPairSlots = 4096;
+// reduction) into slot wave % kPairSlots.  (4096 slots: no faster than 256,
+// and k_reduce_rounds folds each round's slots in one block -- 26 us per
+// step -- and k_window_init zeroes them.)
+constexpr uint32_t kPairSlots = kPullSlots;
 
 // k_flood (flood.hip): every round of a single-start tree
 // window in one persistent launch.  A task = the nodes [nb, ne) of one BFS
