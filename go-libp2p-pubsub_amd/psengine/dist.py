@@ -110,13 +110,27 @@ def bench_main(args, descr: dict, metric: str):
         # the decompositions SURVEY.md §8e allows beside the mandated peer hash,
         # on the same ranks: level-L subtrees (cross edges only above level L)
         # and message sharding (replicated topology, no exchange)
+        # (a leg that fails on every rank alike -- memory, a communicator --
+        # is reported in the line instead of losing the headline run above)
         other = PART_PEER if part == PART_SUBTREE else PART_SUBTREE
-        leg = partitioned(args, dist, dev, rank, world, descr, metric, other)
-        ms = message_sharded(args, dist, dev, rank, world, descr)
-        if rank == 0:
-            keep = ("value", "unit", "ms_per_step", "roofline", "config")
-            out["peer_partition" if other == PART_PEER else "subtree_partition"] = {k: leg[k] for k in keep}
-            out["message_sharded"] = ms
+        key = "peer_partition" if other == PART_PEER else "subtree_partition"
+        try:
+            leg = partitioned(args, dist, dev, rank, world, descr, metric, other)
+            if rank == 0:
+                keep = ("value", "unit", "ms_per_step", "roofline", "config")
+                out[key] = {k: leg[k] for k in keep}
+        except Exception as exc:  # noqa: BLE001
+            print(f"[bench] rank {rank}: {key} leg failed: {exc!r}", file=sys.stderr, flush=True)
+            if rank == 0:
+                out[key] = {"error": repr(exc)}
+        try:
+            ms = message_sharded(args, dist, dev, rank, world, descr)
+            if rank == 0:
+                out["message_sharded"] = ms
+        except Exception as exc:  # noqa: BLE001
+            print(f"[bench] rank {rank}: message_sharded leg failed: {exc!r}", file=sys.stderr, flush=True)
+            if rank == 0:
+                out["message_sharded"] = {"error": repr(exc)}
     if rank == 0:
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())
