@@ -1594,12 +1594,18 @@ hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record
 }
 
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                       uint32_t grid, uint32_t round, bool record, bool nt, hipStream_t s) {
+                       uint32_t grid, uint32_t round, bool record, bool nt, bool cap, hipStream_t s) {
   if (n_chunks == 0 || grid == 0) return hipSuccess;
+  // cap: the large (nt) rounds run at most 5 blocks per CU -- 10 KB of LDS
+  // left unused per block caps residency (8 blocks: 6 % slower on cfg3's big
+  // rounds on one rank); small rounds keep full residency, they need the
+  // waves in flight
+  const size_t kBigRoundLdsPad = cap ? 10240 : 0;
   if (record)  // parity runs: one variant
     hipLaunchKernelGGL((k_pull<true, false>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
   else if (nt)
-    hipLaunchKernelGGL((k_pull<false, true>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
+    hipLaunchKernelGGL((k_pull<false, true>), dim3(grid), dim3(kBlock), kBigRoundLdsPad, s, a, chunks, n_chunks,
+                       round);
   else
     hipLaunchKernelGGL((k_pull<false, false>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
   return hipGetLastError();

@@ -179,7 +179,7 @@ struct PullArgs {
 // k_pull_pair: per wave, a run of at most kPairPar nodes
 // whose rows (at most kPairWords words in all) stay in LDS for its children,
 // streamed kPairKids children at a time
-constexpr uint32_t kPairWords = 1024;
+constexpr uint32_t kPairWords = 768;  // (1024: 17 resident waves/CU, cfg3 +3 % slower; 512: 1 parent of 330 words)
 constexpr uint32_t kPairPar = 128;
 constexpr uint32_t kPairKids = 256;
 constexpr uint64_t kGhostNone = ~0ull;
@@ -329,9 +329,10 @@ hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t*
                        uint64_t* seen, uint8_t* next_flag, uint8_t* blk_flag, hipStream_t s);
 hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid, hipStream_t s);
 // Level mode, pull direction: one wave per chunk, grid = ceil(n_chunks / 4)
-// blocks; nt: the row stores are non-temporal (rounds nobody re-reads soon)
+// blocks; nt: the row stores are non-temporal (rounds nobody re-reads soon);
+// cap: an nt round runs at most 5 blocks per CU (one rank)
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                       uint32_t grid, uint32_t round, bool record, bool nt, hipStream_t s);
+                       uint32_t grid, uint32_t round, bool record, bool nt, bool cap, hipStream_t s);
 
 // Level mode, rounds q and q + 1 in one launch (one rank): a wave writes its
 // run's rows (round q, always non-temporal: the run's children are written

@@ -214,7 +214,7 @@ def test_pair_eager_seen(monkeypatch):
 
 def test_pair_rows_wider_than_stage(monkeypatch):
     """A topic whose rows exceed the LDS stage (70,000 messages: 1,094 words
-    > 1,024) never pairs; a narrow topic beside it in the same window still
+    > 768) never pairs; a narrow topic beside it in the same window still
     gives the oracle's hops."""
     rng = np.random.default_rng(995)
     n = 600
