@@ -7,15 +7,19 @@ topology already resident in HBM.  Prints ONE JSON line (rank 0).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3]
 
-N > 1 is launched by torch.distributed.run (one process per GPU); peers are
-hash-partitioned (owner(p) = splitmix64(p) mod N) and the per-round frontier
-exchange runs over RCCL (see psengine/dist.py).
+N > 1 runs one process per GPU: under torch.distributed.run (WORLD_SIZE must
+equal --gpus), or, started without a launcher, bench.py starts that launcher
+itself as a child process (launch_plan).  Peers are hash-partitioned
+(owner(p) = splitmix64(p) mod N) and the per-round frontier exchange runs over
+RCCL (see psengine/dist.py).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -69,59 +73,110 @@ def host_threads():
     except OSError:
         pass
     return threads, {"os_cpu_count": os.cpu_count(), "affinity": aff, "omp_num_threads": omp,
-                     "model": model}
+                     "cgroup_cpus": cgroup_cpus(), "model": model}
 
 
-def cpu_baseline(eng, wl, sizes, budget_s: float = 10.0):
+def cgroup_cpus():
+    """CPUs this process's cgroup may use (cpu.max / cfs quota), or None when
+    unlimited.  On the GPU box the quota is the GPU's share of the host (~16 of
+    256): 256 OpenMP threads on it time-slice every level barrier (measured:
+    one cfg3 pass took 124 s, 2.8e8 deliveries/s)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, per = fh.read().split()[:2]
+        if q != "max":
+            return max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as fh:
+            q = int(fh.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as fh:
+            per = int(fh.read())
+        if q > 0:
+            return max(1, q // per)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(eng, wl, sizes, budget_s: float = 10.0, deliv_expected=None):
     """The CPU restatements (oracle/, ports) timed on the host's cores, on the
     same trees and the same message mix:
-      value        or_levels_bits -- the algorithm the GPU runs (messages as
+      value        or_levels_run -- the algorithm the GPU runs (messages as
                    bits, rounds level-synchronous, OpenMP over each level's
-                   nodes), the whole workload, repeated within half the budget;
+                   nodes), whole passes of the workload, on every host thread
+                   the process may run (the affinity mask,
+                   capped by the cgroup CPU quota -- not by OMP_NUM_THREADS),
+                   a third of the budget; the per-topology work (BFS numbering, rows allocated
+                   and touched) is done once before, as the GPU's timed steps
+                   exclude the node-space build;
+      share        the same on this process's CPU share (affinity capped by
+                   OMP_NUM_THREADS: 16 on the GPU box), a third of the budget;
       per_message  or_disseminate -- one BFS per message (subtree.go:319-354 +
                    client.go:100-132 literally), OpenMP over messages, on a
-                   growing sample of the messages for the other half."""
+                   growing sample of the messages for the last third.
+    Every pass's deliveries are checked against the workload's."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
 
-    threads, host = host_threads()
+    share, host = host_threads()
+    # every host thread the process may run (SURVEY.md §8d: threads = nproc),
+    # within the cgroup's CPU quota where there is one
+    every = max(1, min(host["affinity"], host["cgroup_cpus"] or host["affinity"]))
     graphs = {}
     for t in range(len(wl.topics)):
         rp, cl = O.parents_to_csr(eng.parents(t))
         graphs[t] = (rp, cl)
     live = np.ones(wl.n_peers, dtype=np.uint8)
     counts = np.bincount(wl.msg_topics, minlength=len(wl.topics))
-    # bit-sliced, level-synchronous: whole passes over the workload
-    bits_deliv, bits_s, passes = 0, 0.0, 0
-    while passes == 0 or bits_s < budget_s / 2:
-        t0 = time.perf_counter()
-        for t, k in enumerate(counts):
-            if k:
-                bits_deliv += O.levels_bits(*graphs[t], wl.topics[t].root, live, int(k), threads=threads)
-        bits_s += time.perf_counter() - t0
-        passes += 1
+    plans = {t: O.Levels(*graphs[t], wl.topics[t].root, int(k)) for t, k in enumerate(counts) if k}
+    for t, pl in plans.items():  # untimed: first touch of every row page
+        pl.run(live, threads=share)
+
+    def bits_leg(threads, budget):
+        deliv, spent, passes = 0, 0.0, 0
+        while passes == 0 or spent < budget:
+            t0 = time.perf_counter()
+            got = sum(pl.run(live, threads=threads) for pl in plans.values())
+            spent += time.perf_counter() - t0
+            passes += 1
+            if deliv_expected is not None:
+                assert got == deliv_expected, (got, deliv_expected)
+            deliv += got
+        return deliv, spent, passes
+
+    all_d, all_s, all_p = bits_leg(every, budget_s / 3)
+    sh_d, sh_s, sh_p = bits_leg(share, budget_s / 3) if share != every else (all_d, all_s, all_p)
+    for pl in plans.values():
+        pl.close()
     # per-message BFS: a growing sample, topic mix kept
     frac = 0.0005
     done_deliv, done_msgs, spent = 0, 0, 0.0
-    while spent < budget_s / 2 and frac <= 1.0:
+    while spent < budget_s / 3 and frac <= 1.0:
         per_topic = np.maximum(1, np.round(counts.astype(np.float64) * frac)).astype(int)
         per_topic[counts == 0] = 0
         t0 = time.perf_counter()
         for t, k in enumerate(per_topic):
             if k:
                 tot, _, _ = O.disseminate(*graphs[t], wl.topics[t].root, live, int(k),
-                                          want_hops=False, threads=threads)
+                                          want_hops=False, threads=share)
                 done_deliv += tot
                 done_msgs += int(k)
         spent += time.perf_counter() - t0
         frac *= 2
-    return {"value": bits_deliv / bits_s, "unit": "deliveries/s", "cores": threads, "kind": "port",
+    algo = ("oracle/psoracle.c or_levels_run, the GPU's algorithm restated (64 messages per u64, "
+            "level-synchronous rounds, OpenMP over each level's nodes; BFS numbering and row "
+            "allocation once per topic, untimed); Go reference not buildable (no go toolchain)")
+    return {"value": all_d / all_s, "unit": "deliveries/s", "cores": every, "kind": "port",
             "host": host,
-            "sample": f"{passes} whole pass(es) of the workload ({bits_deliv} deliveries, {bits_s:.1f} s on "
-                      f"{threads} host threads): oracle/psoracle.c or_levels_bits, the GPU's algorithm "
-                      "restated (64 messages per u64, level-synchronous rounds, OpenMP over each level's "
-                      "nodes); Go reference not buildable (no go toolchain)",
-            "per_message": {"value": done_deliv / spent, "unit": "deliveries/s", "cores": threads,
+            "sample": f"{all_p} whole pass(es) of the workload ({all_d} deliveries, {all_s:.1f} s on "
+                      f"{every} host threads: every CPU of the affinity mask within the cgroup quota"
+                      f" (os.cpu_count() {os.cpu_count()}, quota {host['cgroup_cpus']})): {algo}",
+            "share": {"value": sh_d / sh_s, "unit": "deliveries/s", "cores": share, "kind": "port",
+                      "sample": f"{sh_p} whole pass(es), {sh_d} deliveries, {sh_s:.1f} s on {share} threads "
+                                "(this process's CPU share: affinity capped by OMP_NUM_THREADS)"},
+            "per_message": {"value": done_deliv / spent, "unit": "deliveries/s", "cores": share,
                             "kind": "port",
                             "sample": f"{done_msgs} of the workload's messages (topic mix kept), {done_deliv} "
                                       f"deliveries, {spent:.1f} s: oracle/psoracle.c or_disseminate, one BFS "
@@ -374,6 +429,38 @@ def general_path(eng, wl, deliv_expected, steps: int, warmup: int = 1, max_start
     return out
 
 
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(args, env, argv, port=None):
+    """How this invocation gets its ranks, decided before any GPU call:
+      None          run here (one GPU, or a rank of a torchrun launch whose
+                    WORLD_SIZE equals --gpus);
+      [cmd, ...]    --gpus N > 1 without a launcher: start N ranks as a child
+                    `python -m torch.distributed.run` (rendezvous on
+                    127.0.0.1) with the same arguments; its rank 0 prints the line;
+      "message"     refuse: a launch whose rank count differs from --gpus
+                    (the line would report the wrong n_gpus), or cfg5 on N > 1.
+    So no invocation can print a line whose n_gpus differs from --gpus."""
+    ws = env.get("WORLD_SIZE")
+    if args.gpus < 1:
+        return f"--gpus {args.gpus}: need at least 1"
+    if args.workload == "cfg5" and (args.gpus > 1 or (ws is not None and int(ws) > 1)):
+        return "cfg5 (churn end to end) is a single-GPU workload: run it with --gpus 1"
+    if ws is None:
+        if args.gpus == 1:
+            return None
+        return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+                "--master-addr=127.0.0.1", f"--master-port={port or free_port()}",
+                os.path.abspath(__file__)] + list(argv)
+    if int(ws) != args.gpus:
+        return f"launched with WORLD_SIZE={ws} but --gpus {args.gpus}: they must agree"
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -411,6 +498,14 @@ def main():
                          "N=1), strong = the N=1 workload unchanged")
     args = ap.parse_args()
 
+    # --gpus N: N ranks, whoever starts us (before anything touches the GPU)
+    plan = launch_plan(args, os.environ, sys.argv[1:])
+    if plan is not None:
+        if isinstance(plan, str):
+            log(f"[bench] {plan}")
+            sys.exit(2)
+        log(f"[bench] starting {args.gpus} ranks: {' '.join(plan)}")
+        sys.exit(subprocess.run(plan).returncode)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.steps is None:
         one = args.gpus <= 1 and world <= 1 and not args.force_dist
@@ -521,7 +616,7 @@ def main():
     if not args.no_general and not args.no_check:
         out["general_path"] = general_path(eng, wl, deliv_expected, max(2, min(args.steps, 4)))
     if not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(eng, wl, sizes, args.cpu_budget)
+        out["cpu_baseline"] = cpu_baseline(eng, wl, sizes, args.cpu_budget, deliv_expected)
     print(json.dumps(out), flush=True)
     eng.close()
 

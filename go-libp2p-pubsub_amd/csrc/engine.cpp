@@ -158,6 +158,7 @@ struct ps_engine {
   uint32_t pull_words = kPullWords;    // row words per k_pull chunk (512..4096 measured: 1024 best)
   uint64_t flood_top_bytes = 16ull << 20;  // k_flood runs the leading rounds writing at most this many row bytes
   uint32_t flood_epoch = 0;   // granule tag of the last launch (granules are never reset)
+  uint32_t flood_spin_ticks = 200000000u;  // dependency-wait bound: 2 s of s_memrealtime (100 MHz); PSAMD_FLOOD_SPIN_TICKS
   std::vector<uint64_t> flood_key;
   std::vector<FloodTask> flood_tasks;
   std::vector<FloodSeg> flood_segs;
@@ -2144,7 +2145,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       if (++e->flood_epoch == 0) ++e->flood_epoch;  // granules of older launches carry older epochs
       fa.epoch = e->flood_epoch;
       fa.gen_cur = a.gen_cur;
-      fa.spin_ticks = 200000000u;  // 2 s of s_memrealtime (100 MHz)
+      fa.spin_ticks = e->flood_spin_ticks;
       const uint32_t flood_blocks = std::min<uint32_t>(e->flood_grid, ceil_div(fa.n_tasks, kBlock / 64));
       if (e->flood_profile) {
         HIP_TRY(e->d_flood_prof.ensure(static_cast<size_t>(flood_blocks) * 4 * kFloodProf * 8), "alloc flood profile");
@@ -2328,6 +2329,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   }
   HIP_TRY(hipEventSynchronize(e->ev_run1), "sync");
   const auto t_sync = std::chrono::steady_clock::now();
+  const ps_stats keep = *st;  // a k_flood timeout re-runs the window from these stats
   float ms = 0.f;
   HIP_TRY(hipEventElapsedTime(&ms, e->ev_run0, e->ev_run1), "elapsed");
   st->run_ms += ms;
@@ -2349,9 +2351,14 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   if (mode == PS_MODE_FLOOD && e->flood_profile && e->flood_prof_waves) flood_profile_report(e);
   if (!accumulate_window(st, hs.data(), ha.data(), r, planned0, mode, flood_rounds, launches, world,
                          e->round_kind)) {
+    // a k_flood dependency wait timed out (its waves were not all resident:
+    // another engine or process shares the GPU): this window's rows are
+    // incomplete.  Run the same window again with per-round launches under a
+    // fresh generation, and keep those from now on.
     e->flood_broken = true;
-    return e->fail(PS_E_DEVICE, "k_flood: a dependency wait timed out (waves not co-resident?); "
-                                "per-round launches from now on");
+    *st = keep;
+    if (e->host_timing) std::fprintf(stderr, "[psengine] k_flood timed out: window re-run per round\n");
+    return run_window(e, msgs, win, st);
   }
   if (e->host_timing) {
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
@@ -2473,6 +2480,8 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_FLOOD_PROFILE")) e->flood_profile = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD_WORDS"))
     e->flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
+  if (const char* v = std::getenv("PSAMD_FLOOD_SPIN_TICKS"))  // tests: 0 forces the timeout fallback
+    e->flood_spin_ticks = static_cast<uint32_t>(std::strtoul(v, nullptr, 0));
   if (const char* v = std::getenv("PSAMD_FLOOD_TOP_BYTES"))  // the k_flood / k_pull split (tests: ~0 = all k_flood)
     e->flood_top_bytes = std::strtoull(v, nullptr, 0);
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||

@@ -731,10 +731,18 @@ struct PullVec {
 // registers), which k_pull_pair's persistent waves carry across chunks for
 // two rounds without the vector registers per-lane counters would take.
 struct WaveCtr {
-  uint32_t deliv = 0;                      // per lane
+  uint32_t deliv = 0;                      // per lane, folded into dsum per sub-run
   uint32_t kids = 0, reached = 0, parents = 0;  // wave-uniform
   uint64_t sw = 0, pwords = 0;             // wave-uniform: words written, parent words read
+  uint64_t dsum = 0;                       // wave-uniform: folded deliveries
 };
+// The per-lane delivery count into the 64-bit wave total: after each sub-run
+// of at most kPairKids rows (<= 2^24 bits), so neither the lane counts nor
+// the sum over a wide run's children (f * W * 64 bits) wrap.
+__device__ __forceinline__ void ctr_fold(WaveCtr& c) {
+  c.dsum += __builtin_amdgcn_readfirstlane(__reduce_add_sync(~0ull, c.deliv));  // (a sub-run: < 2^32)
+  c.deliv = 0;
+}
 // One batch of (up to 64) nodes: visited (in), reached (ok), a reached
 // parent's first child (par); W_sw row words written per reached node,
 // W_pw parent row words read per counted parent.
@@ -1157,11 +1165,13 @@ __device__ __forceinline__ void pair_kids(const PullArgs& a, const PullTopic& P,
         }
       }
     }
+    ctr_fold(c);
   }
 }
 
 __device__ __forceinline__ void ctr_add(WaveCtr& d, const WaveCtr& s) {
-  d.deliv += s.deliv;
+  d.deliv += s.deliv;  // (one phase-A run: <= kPairWords * 64 bits, folded below)
+  d.dsum += s.dsum;
   d.sw += s.sw;
   d.kids += s.kids;
   d.reached += s.reached;
@@ -1172,8 +1182,8 @@ __device__ __forceinline__ void ctr_add(WaveCtr& d, const WaveCtr& s) {
 // Counters of a wave (two rounds) added with its own atomics: no block
 // reduction, so no barrier.
 __device__ __forceinline__ void pull_flush_wave(const WaveCtr& c, uint64_t* partials, uint64_t slot, uint32_t lane) {
-  // (one chunk per wave: its per-lane delivery sums total at most 2^18 bits)
-  const uint64_t v7[7] = {__reduce_add_sync(~0ull, c.deliv), c.sw, c.kids, c.reached, c.parents, c.pwords, 0ull};
+  const uint64_t v7[7] = {c.dsum + __reduce_add_sync(~0ull, c.deliv), c.sw, c.kids, c.reached, c.parents,
+                          c.pwords, 0ull};
   if (lane < kNumCtr) {
     const uint64_t v = pull_ctr_pick(v7, lane);
     if (v) atomicAdd(reinterpret_cast<unsigned long long*>(partials + slot * kNumCtr + lane),
@@ -1228,6 +1238,10 @@ __global__ __launch_bounds__(64) void k_pull_pair(PullArgs a, const PullChunk* _
       if (lane == 0) reach[j0 >> 6] = b;
     }
     pull_stream<kRecord, true, true>(a, P, ch.node_begin, n1, src, lane, round + (late ? 1 : 0), ca, rows);
+    ctr_fold(ca);
+    // src (u64 sources) and ctab (u32 offsets) share the LDS table: no memory
+    // access may move across the switch from one view to the other
+    asm volatile("" ::: "memory");
     if (late) {
       ctr_add(c2, ca);
     } else {
@@ -1236,6 +1250,7 @@ __global__ __launch_bounds__(64) void k_pull_pair(PullArgs a, const PullChunk* _
         pair_kids<kRecord, kNT2, kPairWords>(a, P, ch.node_begin, n1, ch.c_lo, ch.c_hi, reach, rows,
                                              reinterpret_cast<uint32_t*>(src), lane, round + 1, pf_p, pf_f, c2);
     }
+    asm volatile("" ::: "memory");
   }
   pull_flush_wave(c, a.partials, blockIdx.x % a.slot_mod, lane);
   pull_flush_wave(c2, a.partials2, blockIdx.x % a.slot_mod, lane);

@@ -36,7 +36,7 @@ void SubscriptionTree::kid_push(uint32_t p, const ChildRec& r) {
   auto& v = spill_[R.spill];
   v.resize(R.n);
   v.push_back(r);
-  R.n = static_cast<uint16_t>(v.size());
+  R.n = static_cast<uint32_t>(v.size());
 }
 
 void SubscriptionTree::kid_clear(uint32_t p) {

@@ -101,8 +101,8 @@ class SubscriptionTree {
   struct alignas(64) PeerRec {
     uint32_t up = kNone;  // upstream peer (the other end of `in`)
     PeerState state = PeerState::Out;
-    uint8_t pad = 0;
-    uint16_t n = 0;          // children
+    uint8_t pad[3] = {0, 0, 0};
+    uint32_t n = 0;          // children (TreeWidth / MaxWidth are unbounded: no 16-bit count)
     uint32_t spill = kNone;  // index into spill_, or kNone: the records are inline
     ChildRec kin[kInline];
   };
@@ -113,7 +113,7 @@ class SubscriptionTree {
   }
   void kid_push(uint32_t p, const ChildRec& r);
   void kid_clear(uint32_t p);
-  void kid_shrink(uint32_t p, uint32_t n) { rec_[p].n = static_cast<uint16_t>(n); }
+  void kid_shrink(uint32_t p, uint32_t n) { rec_[p].n = n; }
 
   uint32_t n_ = 0, root_ = 0, width_ = 2, max_width_ = 5;
   uint64_t rng_ = 0;

@@ -81,13 +81,17 @@ def workload(args, world: int):
 
 
 def bench_main(args, descr: dict, metric: str):
+    rank, world, local = env_ranks()
+    gpus = getattr(args, "gpus", world)
+    if world != gpus:
+        raise SystemExit(f"[bench] rank {rank}: WORLD_SIZE={world} but --gpus {gpus}; "
+                         "the line would report the wrong n_gpus")
     import torch
 
     # RCCL prints its version banner on stdout when a communicator comes up:
     # keep stdout for the one JSON line (rank 0), everything else to stderr
     json_fd = os.dup(1)
     os.dup2(2, 1)
-    rank, world, local = env_ranks()
     local = local % max(1, torch.cuda.device_count())  # (counting does not initialise the GPU)
     torch.cuda.set_device(local)
     if getattr(args, "message_only", False):

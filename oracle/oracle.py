@@ -49,6 +49,11 @@ def lib():
                                      u32p, u8p, C.POINTER(C.c_uint64), C.c_uint32, C.c_int]
         L.or_levels_bits.restype = C.c_int64
         L.or_levels_bits.argtypes = [C.c_uint32, u32p, u32p, C.c_uint32, u8p, C.c_uint32, C.c_int]
+        L.or_levels_new.restype = P
+        L.or_levels_new.argtypes = [C.c_uint32, u32p, u32p, C.c_uint32, C.c_uint32]
+        L.or_levels_run.restype = C.c_int64
+        L.or_levels_run.argtypes = [P, u8p, C.c_int]
+        L.or_levels_free.argtypes = [P]
         L.or_splitmix64.argtypes = [C.POINTER(C.c_uint64)]
         L.or_splitmix64.restype = C.c_uint64
         _lib = L
@@ -150,3 +155,32 @@ def levels_bits(row_ptr, col, root: int, live, n_msgs: int, threads: int = 1) ->
     if tot < 0:
         raise RuntimeError(f"or_levels_bits -> {tot}")
     return int(tot)
+
+
+class Levels:
+    """or_levels_new / or_levels_run: the bit-sliced restatement with the
+    per-topology work (BFS numbering, rows allocated and touched) done once,
+    so a timed pass is the level loop alone (bench.py cpu_baseline)."""
+
+    def __init__(self, row_ptr, col, root: int, n_msgs: int):
+        self._rp = np.ascontiguousarray(row_ptr, dtype=np.uint32)
+        self._cl = np.ascontiguousarray(col, dtype=np.uint32)
+        self._h = lib().or_levels_new(self._rp.shape[0] - 1, _ptr(self._rp, C.c_uint32),
+                                      _ptr(self._cl, C.c_uint32), root, n_msgs)
+        if not self._h:
+            raise RuntimeError("or_levels_new failed")
+
+    def run(self, live, threads: int = 1) -> int:
+        lv = np.ascontiguousarray(live, dtype=np.uint8)
+        tot = lib().or_levels_run(self._h, _ptr(lv, C.c_uint8), threads)
+        if tot < 0:
+            raise RuntimeError(f"or_levels_run -> {tot}")
+        return int(tot)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().or_levels_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()

@@ -422,59 +422,100 @@ int64_t or_disseminate(uint32_t n, const uint32_t* row_ptr, const uint32_t* col,
  * over the level's nodes (OpenMP): a node whose parent was reached and which
  * is live receives new = row(parent) & ~seen(node) (seen is empty: each node
  * is reached once on a tree, subtree.go:324-337 / client.go:124-130).  Rows
- * are BFS-position major.  Returns total deliveries (popcount of every new
- * word), or <0 on error. */
-int64_t or_levels_bits(uint32_t n, const uint32_t* row_ptr, const uint32_t* col, uint32_t root,
-                       const uint8_t* live, uint32_t n_msgs, int n_threads) {
-  if (root >= n) return OR_E_INVAL;
-  if (n_threads < 1) n_threads = 1;
-  if (n_msgs == 0) return 0;
-  const uint32_t W = (n_msgs + 63) / 64;
-  /* BFS numbering: order[], parent position, level starts */
-  uint32_t* order = (uint32_t*)malloc(sizeof(uint32_t) * n);
-  uint32_t* ppos = (uint32_t*)malloc(sizeof(uint32_t) * n);
+ * are BFS-position major.
+ *
+ * Split in two like the GPU engine: or_levels_new does the per-topology work
+ * (BFS numbering, row allocation, first touch of the rows) once, and
+ * or_levels_run is one pass over a batch -- what the baseline times, as the
+ * GPU's timed steps exclude the node-space build and reuse their buffers. */
+struct or_levels {
+  uint32_t n, qt, nl, W, n_msgs;
+  uint32_t *order, *ppos, *lvl;
+  uint64_t* rows;
+  uint8_t* reached;
+};
+
+void or_levels_free(or_levels* L) {
+  if (!L) return;
+  free(L->order), free(L->ppos), free(L->lvl), free(L->rows), free(L->reached);
+  free(L);
+}
+
+or_levels* or_levels_new(uint32_t n, const uint32_t* row_ptr, const uint32_t* col, uint32_t root,
+                         uint32_t n_msgs) {
+  if (root >= n || n_msgs == 0) return NULL;
+  or_levels* L = (or_levels*)calloc(1, sizeof(or_levels));
   uint32_t* pos = (uint32_t*)malloc(sizeof(uint32_t) * n);
-  uint32_t* lvl = (uint32_t*)malloc(sizeof(uint32_t) * (n + 2));
-  if (!order || !ppos || !pos || !lvl) {
-    free(order), free(ppos), free(pos), free(lvl);
-    return OR_E_NOMEM;
+  if (!L || !pos) {
+    free(L), free(pos);
+    return NULL;
   }
+  L->n = n;
+  L->n_msgs = n_msgs;
+  L->W = (n_msgs + 63) / 64;
+  L->order = (uint32_t*)malloc(sizeof(uint32_t) * n);
+  L->ppos = (uint32_t*)malloc(sizeof(uint32_t) * n);
+  L->lvl = (uint32_t*)malloc(sizeof(uint32_t) * (n + 2));
+  if (!L->order || !L->ppos || !L->lvl) {
+    free(pos);
+    or_levels_free(L);
+    return NULL;
+  }
+  /* BFS numbering: order[], parent position, level starts */
   for (uint32_t i = 0; i < n; i++) pos[i] = OR_NONE;
   uint32_t qt = 0, nl = 0;
-  order[qt] = root;
-  ppos[qt] = OR_NONE;
+  L->order[qt] = root;
+  L->ppos[qt] = OR_NONE;
   pos[root] = qt++;
-  lvl[nl++] = 0;
+  L->lvl[nl++] = 0;
   uint32_t lo = 0;
   while (lo < qt) {
     const uint32_t hi = qt;
-    lvl[nl++] = hi;
+    L->lvl[nl++] = hi;
     for (uint32_t i = lo; i < hi; i++)
-      for (uint32_t e = row_ptr[order[i]]; e < row_ptr[order[i] + 1]; e++) {
+      for (uint32_t e = row_ptr[L->order[i]]; e < row_ptr[L->order[i] + 1]; e++) {
         const uint32_t c = col[e];
         if (pos[c] != OR_NONE) continue;
         pos[c] = qt;
-        order[qt] = c;
-        ppos[qt++] = i;
+        L->order[qt] = c;
+        L->ppos[qt++] = i;
       }
     lo = hi;
   }
-  uint64_t* rows = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)qt * W);
-  uint8_t* reached = (uint8_t*)calloc(qt, 1);
-  if (!rows || !reached) {
-    free(order), free(ppos), free(pos), free(lvl), free(rows), free(reached);
-    return OR_E_NOMEM;
+  free(pos);
+  L->qt = qt;
+  L->nl = nl;
+  L->rows = (uint64_t*)calloc((size_t)qt * L->W, sizeof(uint64_t)); /* zeroed: touched once here */
+  L->reached = (uint8_t*)calloc(qt, 1);
+  if (!L->rows || !L->reached) {
+    or_levels_free(L);
+    return NULL;
   }
+  memset(L->rows, 0, sizeof(uint64_t) * (size_t)qt * L->W);
+  return L;
+}
+
+/* One pass: every message of the batch from the root down every level.
+ * Returns total deliveries (popcount of every new word). */
+int64_t or_levels_run(or_levels* L, const uint8_t* live, int n_threads) {
+  if (!L) return OR_E_INVAL;
+  if (n_threads < 1) n_threads = 1;
+  const uint32_t W = L->W;
+  uint64_t* rows = L->rows;
+  uint8_t* reached = L->reached;
+  const uint32_t* ppos = L->ppos;
+  const uint32_t* order = L->order;
   /* PublishMessage: the root holds the window's messages (not a recipient) */
   for (uint32_t w = 0; w < W; w++) rows[w] = ~0ull;
-  if (n_msgs % 64) rows[W - 1] = (1ull << (n_msgs % 64)) - 1;
+  if (L->n_msgs % 64) rows[W - 1] = (1ull << (L->n_msgs % 64)) - 1;
   reached[0] = 1;
   int64_t total = 0;
-  for (uint32_t d = 1; d + 1 < nl; d++) {
-    const int64_t a = lvl[d], b = lvl[d + 1];
+  for (uint32_t d = 1; d + 1 < L->nl; d++) {
+    const int64_t a = L->lvl[d], b = L->lvl[d + 1];
 #pragma omp parallel for num_threads(n_threads) schedule(static, 256) reduction(+ : total)
     for (int64_t u = a; u < b; u++) {
       const uint32_t p = ppos[u];
+      reached[u] = 0;
       if (!reached[p] || !live[order[u]]) continue;
       reached[u] = 1;
       const uint64_t* src = rows + (size_t)p * W;
@@ -488,6 +529,16 @@ int64_t or_levels_bits(uint32_t n, const uint32_t* row_ptr, const uint32_t* col,
       total += k;
     }
   }
-  free(order), free(ppos), free(pos), free(lvl), free(rows), free(reached);
+  return total;
+}
+
+int64_t or_levels_bits(uint32_t n, const uint32_t* row_ptr, const uint32_t* col, uint32_t root,
+                       const uint8_t* live, uint32_t n_msgs, int n_threads) {
+  if (root >= n) return OR_E_INVAL;
+  if (n_msgs == 0) return 0;
+  or_levels* L = or_levels_new(n, row_ptr, col, root, n_msgs);
+  if (!L) return OR_E_NOMEM;
+  const int64_t total = or_levels_run(L, live, n_threads);
+  or_levels_free(L);
   return total;
 }

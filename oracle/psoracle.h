@@ -88,6 +88,14 @@ int64_t or_disseminate(uint32_t n, const uint32_t* row_ptr, const uint32_t* col,
  * nodes.  Returns total deliveries, or <0 on error. */
 int64_t or_levels_bits(uint32_t n, const uint32_t* row_ptr, const uint32_t* col, uint32_t root,
                        const uint8_t* live, uint32_t n_msgs, int n_threads);
+/* The same, split like the engine: or_levels_new does the per-topology work
+ * (BFS numbering, rows allocated and touched) once; or_levels_run is one pass
+ * of a batch of n_msgs messages (what bench.py's cpu_baseline times). */
+typedef struct or_levels or_levels;
+or_levels* or_levels_new(uint32_t n, const uint32_t* row_ptr, const uint32_t* col, uint32_t root,
+                         uint32_t n_msgs);
+int64_t or_levels_run(or_levels* plan, const uint8_t* live, int n_threads);
+void or_levels_free(or_levels* plan);
 
 /* SplitMix64 (shared definition with the engine and the synthetic workload
  * generator). */

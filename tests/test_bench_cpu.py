@@ -68,3 +68,63 @@ def test_pmc_traffic_matches_kernel_and_workload():
         assert t is not None and t > 0 and "FETCH_SIZE" in src
         assert bench.pmc_traffic(x["kernel"] + "_other", x["workload"])[0] is None
         assert bench.pmc_traffic(x["kernel"], x["workload"] + "_other")[0] is None
+
+
+def _args(**kw):
+    base = dict(gpus=1, workload="cfg3")
+    base.update(kw)
+    return types.SimpleNamespace(**base)
+
+
+def test_launch_plan_one_gpu_runs_here():
+    assert bench.launch_plan(_args(), {}, []) is None
+    assert bench.launch_plan(_args(gpus=4), {"WORLD_SIZE": "4"}, []) is None
+
+
+def test_launch_plan_starts_n_ranks_without_a_launcher():
+    """--gpus N without WORLD_SIZE: a child torch.distributed.run with N
+    ranks on 127.0.0.1 and the same arguments."""
+    argv = ["--gpus", "8", "--steps", "5", "--workload", "cfg4"]
+    cmd = bench.launch_plan(_args(gpus=8, workload="cfg4"), {}, argv, port=29777)
+    assert isinstance(cmd, list)
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and "--master-port=29777" in cmd
+    i = cmd.index(bench.os.path.abspath(bench.__file__))
+    assert cmd[i + 1:] == argv
+
+
+def test_launch_plan_refuses_mismatch_and_cfg5():
+    assert isinstance(bench.launch_plan(_args(gpus=2), {"WORLD_SIZE": "4"}, []), str)
+    assert isinstance(bench.launch_plan(_args(gpus=1), {"WORLD_SIZE": "2"}, []), str)
+    assert isinstance(bench.launch_plan(_args(gpus=2, workload="cfg5"), {}, []), str)
+    assert isinstance(bench.launch_plan(_args(gpus=0), {}, []), str)
+
+
+def test_bench_mismatch_exits_nonzero():
+    """A torchrun rank whose WORLD_SIZE differs from --gpus exits non-zero
+    and prints no JSON line (checked before anything touches the GPU)."""
+    import subprocess
+    import sys
+    env = dict(bench.os.environ, WORLD_SIZE="2", RANK="0")
+    p = subprocess.run([sys.executable, bench.__file__, "--gpus", "4", "--no-cpu"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and p.stdout.strip() == ""
+    assert "must agree" in p.stderr
+
+
+def test_dist_bench_main_asserts_world():
+    from psengine import dist
+    import pytest
+    env = dict(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    old = {k: bench.os.environ.get(k) for k in env}
+    bench.os.environ.update(env)
+    try:
+        with pytest.raises(SystemExit):
+            dist.bench_main(_args(gpus=4), bench.DESCR, bench.METRIC)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                bench.os.environ.pop(k, None)
+            else:
+                bench.os.environ[k] = v

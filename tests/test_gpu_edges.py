@@ -155,3 +155,28 @@ def test_deep_chain_beyond_255_hops(staggered, n):
         for m in (0, 1, k - 1):
             assert np.array_equal(e.hops(first + m), hops[0]), m
         assert e.depth(0) == (n - 1, n)
+
+
+def test_wide_join_beyond_65535_children():
+    """TreeWidth 70,000: the root takes every joiner directly
+    (subtree.go:141-152).  The child count of a peer is a 32-bit field: a
+    16-bit one wrapped at child 65,536 and dropped the spill list.
+    The attached tree equals the oracle's restated joins, and a message reaches
+    every member in one hop; a leave of the root's last child redistributes
+    nothing (it has no children) and keeps the others."""
+    n, w = 70_002, 70_000
+    with PE.Engine(n, 1, record_hops=True, seed=3) as e:
+        e.topic_create(0, 0, w, w)
+        e.join(0, np.arange(1, n))
+        par = e.parents(0)
+        t = O.Tree(n, 0, w, w, PE.Engine.topic_seed(3, 0))
+        t.join_all(range(1, n))
+        assert np.array_equal(par, t.parents())
+        assert (par[1:w + 1] == 0).all()
+        first = e.publish(np.zeros(3))
+        st = e.run()
+        assert st.deliveries == 3 * (n - 1)
+        assert np.array_equal(e.hops(first), t.message())
+        e.leave(0, np.array([w]))
+        t.leave(w)
+        assert np.array_equal(e.parents(0), t.parents())

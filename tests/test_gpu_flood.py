@@ -306,3 +306,51 @@ def test_cfg3_topology_dead_mask_hops_record_instance():
             _, oh, _ = O.disseminate(rp, cl, wl.topics[t].root, live, 1)
             for m in rng.choice(idx, size=min(16, len(idx)), replace=False):
                 assert np.array_equal(eng.hops(first + int(m)), oh[0]), (t, int(m))
+
+
+def test_flood_timeout_reruns_window_per_round(monkeypatch):
+    """k_flood needs every wave resident; when they are not (another engine
+    shares the GPU) a dependency wait times out.  PSAMD_FLOOD_SPIN_TICKS=0
+    forces that on a 40-level tree: the same window is re-run with per-round
+    launches under a fresh generation (exact hops, counters and digest), and
+    later windows keep the per-round launches.  An asynchronous run that times
+    out reports PS_E_DEVICE from ps_wait and the next run is exact."""
+    rng = np.random.default_rng(5)
+    n = 3000
+    parent = np.full(n, O.NONE, dtype=np.uint32)
+    parent[1:] = np.maximum(0, np.arange(1, n) - 1 - rng.integers(0, 75, n - 1)).astype(np.uint32)
+    live = (rng.random(n) > 0.03).astype(np.uint8)
+    live[0] = 1
+    rp, cl = O.parents_to_csr(parent)
+    _, oh, _ = O.disseminate(rp, cl, 0, live, 1)
+    n_msgs = 130
+    monkeypatch.setenv("PSAMD_FLOOD", "1")
+    monkeypatch.setenv("PSAMD_FLOOD_TOP_BYTES", str(1 << 40))
+    monkeypatch.setenv("PSAMD_FLOOD_SPIN_TICKS", "0")
+    with PE.Engine(n, 1, record_hops=True) as eng:
+        eng.set_tree(0, 0, parent)
+        eng.set_live(live)
+        d0 = eng.depth(0)[0]
+        assert d0 >= 20
+        for rep in range(2):
+            first = eng.publish(np.zeros(n_msgs))
+            st = eng.run()
+            assert st.expand_mode == PE.MODE_LEVEL_PULL, rep  # k_flood gave up
+            assert st.windows == 1 and st.deliveries == n_msgs * int((oh[0][1:] != 0xFF).sum())
+            for m in (0, 64, n_msgs - 1):
+                assert np.array_equal(eng.hops(first + m), oh[0]), (rep, m)
+    monkeypatch.setenv("PSAMD_FLOOD_SPIN_TICKS", "0")
+    with PE.Engine(n, 1) as eng:
+        eng.set_tree(0, 0, parent)
+        eng.set_live(live)
+        eng.publish(np.zeros(n_msgs))
+        eng.run_async()
+        with pytest.raises(PE.EngineError) as ei:
+            eng.wait()
+        assert "k_flood" in str(ei.value)
+        first = eng.publish(np.zeros(n_msgs))
+        st = eng.run()
+        assert st.expand_mode == PE.MODE_LEVEL_PULL
+        assert st.deliveries == n_msgs * int((oh[0][1:] != 0xFF).sum())
+        got = eng.delivered(first + 7)
+        assert np.array_equal(got.astype(bool), oh[0] != 0xFF)

@@ -234,3 +234,11 @@ def test_levels_bits_matches_per_message_bfs(oracle_lib, seed):
     for n_msgs in (1, 63, 64, 65, 300):
         tot, _, _ = O.disseminate(rp, cl, root, live, n_msgs, want_hops=False)
         assert O.levels_bits(rp, cl, root, live, n_msgs, threads=2) == tot
+        plan = O.Levels(rp, cl, root, n_msgs)
+        live2 = live.copy()
+        live2[rng.integers(0, n, 5)] = 0
+        tot2, _, _ = O.disseminate(rp, cl, root, live2, n_msgs, want_hops=False)
+        for _ in range(2):  # repeated passes over one plan, with a changing mask
+            assert plan.run(live, threads=3) == tot
+            assert plan.run(live2, threads=1) == tot2
+        plan.close()
