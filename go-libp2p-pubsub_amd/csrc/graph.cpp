@@ -1,0 +1,789 @@
+// graph.cpp -- the node space of the engine: per topic the
+// owned tree nodes reachable from the root, numbered level by level, CSR child
+// lists, node flags; built on the host (any rank count) or rebuilt on the GPU
+// after churn (gbuild.hip, one rank).
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <tuple>
+
+#include "engine.hpp"
+#include "gbuild.hpp"
+
+namespace psamd {
+
+bool topic_ok(const ps_engine* e, uint32_t topic) { return topic < e->topics.size() && e->topics[topic].exists; }
+
+// Child lists of one topic in peer space, insertion order.
+void peer_children(const ps_engine* e, const TopicHost& T, std::vector<uint32_t>& rp, std::vector<uint32_t>& cl) {
+  const uint32_t n = e->cfg.n_peers;
+  if (T.kind == Kind::Children) {
+    rp = T.rp;
+    cl = T.cl;
+    return;
+  }
+  rp.assign(n + 1, 0);
+  if (T.kind == Kind::Parent) {
+    for (uint32_t c = 0; c < n; ++c)
+      if (T.parent[c] != kNone && c != T.root) rp[T.parent[c] + 1]++;
+    for (uint32_t i = 0; i < n; ++i) rp[i + 1] += rp[i];
+    cl.assign(rp[n], 0);
+    std::vector<uint32_t> fill(rp.begin(), rp.end() - 1);
+    for (uint32_t c = 0; c < n; ++c)
+      if (T.parent[c] != kNone && c != T.root) cl[fill[T.parent[c]]++] = c;
+    return;
+  }
+  // Kind::Join: attached children (subscribed and not failed) in map order
+  for (uint32_t p = 0; p < n; ++p) {
+    uint32_t k = 0;
+    for (const auto& r : T.tree.children(p))
+      if (T.tree.state(r.id) == PeerState::In) ++k;
+    rp[p + 1] = k;
+  }
+  for (uint32_t i = 0; i < n; ++i) rp[i + 1] += rp[i];
+  cl.assign(rp[n], 0);
+  for (uint32_t p = 0; p < n; ++p) {
+    uint32_t o = rp[p];
+    for (const auto& r : T.tree.children(p))
+      if (T.tree.state(r.id) == PeerState::In) cl[o++] = r.id;
+  }
+}
+
+// Ownership of one topic's nodes (positions in its BFS order) among `world`
+// ranks.  PS_PART_PEER: owner = splitmix64(peer) mod world.
+// PS_PART_SUBTREE: nodes at BFS level >= L belong to the owner of their
+// ancestor at level L; the level-L subtrees are dealt largest first to the
+// least-loaded rank; the levels above L stay with the root's owner.  L =
+// split_depth, or (0) the first level holding >= 64*world nodes, so only
+// edges out of level L - 1 cross ranks.
+void partition_topic(const std::vector<uint32_t>& order, const std::vector<uint32_t>& bfs_parent,
+                     const std::vector<uint32_t>& level, int32_t world, uint32_t part, uint32_t split_depth,
+                     std::vector<int32_t>& owner) {
+  const size_t n = order.size();
+  owner.assign(n, 0);
+  if (world <= 1) return;
+  auto mix = [](uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  };
+  uint32_t L = split_depth;
+  if (part == PS_PART_SUBTREE && L == 0) {
+    std::vector<uint64_t> cnt;
+    for (size_t u = 0; u < n; ++u) {
+      if (level[u] >= cnt.size()) cnt.resize(level[u] + 1, 0);
+      cnt[level[u]]++;
+    }
+    L = static_cast<uint32_t>(cnt.size() ? cnt.size() - 1 : 0);
+    for (uint32_t d = 0; d < cnt.size(); ++d)
+      if (cnt[d] >= 64ull * world) {
+        L = d;
+        break;
+      }
+  }
+  std::vector<uint32_t> anc(n, kNone);
+  const bool subtree = part == PS_PART_SUBTREE && L > 0;
+  // subtree mode: the level-L subtrees go to ranks largest first, each to the
+  // least-loaded rank (LPT), so every rank holds the same share of this
+  // topic's nodes whatever the topic's message weight (hashing the subtree
+  // roots left 14 % imbalance at 8 ranks on cfg3)
+  std::vector<uint64_t> size(subtree ? n : 0, 0);
+  const int32_t top_owner = n ? static_cast<int32_t>(mix(order[0]) % static_cast<uint64_t>(world)) : 0;
+  uint64_t n_top = 0;
+  for (size_t u = 0; u < n; ++u) {
+    if (subtree && level[u] >= L) {
+      anc[u] = level[u] == L ? static_cast<uint32_t>(u) : anc[bfs_parent[u]];
+      size[anc[u]]++;
+    } else if (subtree) {
+      owner[u] = top_owner;
+      ++n_top;
+    } else {
+      owner[u] = static_cast<int32_t>(mix(order[u]) % static_cast<uint64_t>(world));
+    }
+  }
+  if (!subtree) return;
+  std::vector<uint32_t> roots;
+  for (size_t u = 0; u < n; ++u)
+    if (level[u] == L) roots.push_back(static_cast<uint32_t>(u));
+  std::sort(roots.begin(), roots.end(), [&](uint32_t a, uint32_t b) {
+    return size[a] != size[b] ? size[a] > size[b] : order[a] < order[b];
+  });
+  std::vector<uint64_t> load(world, 0);
+  load[top_owner] = n_top;  // the dealing evens out the top levels too
+  for (uint32_t u : roots) {
+    int32_t best = 0;
+    for (int32_t q = 1; q < world; ++q)
+      if (load[q] < load[best]) best = q;
+    owner[u] = best;
+    load[best] += size[u];
+  }
+  for (size_t u = 0; u < n; ++u)
+    if (level[u] > L) owner[u] = owner[anc[u]];
+}
+
+namespace {
+
+// One topic's BFS over its child lists: global positions in BFS order, each
+// position's BFS parent and level; local[peer] = position (reset by caller).
+struct TopicBfs {
+  std::vector<uint32_t> rp, cl, order, bfs_parent, level;
+  std::vector<int32_t> owner;
+};
+
+int topic_bfs(ps_engine* e, const TopicHost& T, std::vector<uint32_t>& local, TopicBfs& B) {
+  const uint32_t n = e->cfg.n_peers;
+  peer_children(e, T, B.rp, B.cl);
+  B.order.assign(1, T.root);
+  B.bfs_parent.assign(1, kNone);
+  B.level.assign(1, 0);
+  local[T.root] = 0;
+  for (size_t qi = 0; qi < B.order.size(); ++qi) {
+    const uint32_t p = B.order[qi];
+    for (uint32_t k = B.rp[p]; k < B.rp[p + 1]; ++k) {
+      const uint32_t c = B.cl[k];
+      if (c >= n) return e->fail(PS_E_INVAL, "child id out of range");
+      if (local[c] == kNone) {
+        local[c] = static_cast<uint32_t>(B.order.size());
+        B.order.push_back(c);
+        B.bfs_parent.push_back(static_cast<uint32_t>(qi));
+        B.level.push_back(B.level[qi] + 1);
+      }
+    }
+  }
+  partition_topic(B.order, B.bfs_parent, B.level, e->world, e->partition, e->split_depth, B.owner);
+  return PS_OK;
+}
+
+}  // namespace
+
+// Builds this rank's node space.  Per topic, every rank's owned nodes are
+// numbered level by level (each rank computes every rank's numbering, so
+// remote ids and ghost record indices agree without a handshake).  Level d + 1
+// of rank r: first the nodes whose parent r owns, in (parent id, sibling)
+// order -- so the children of consecutive parents are consecutive ids, as in
+// BFS order, which is what one rank gets -- then the ghost-fed nodes, grouped
+// by the parent's owner a and ordered by record index k (a numbers its
+// parents with children on r in its own node order).  A round's nodes that
+// need no exchange are therefore one contiguous range ahead of those that
+// read records.  CSR over node ids; a child owned by another rank is
+// kRemoteBit | rank << 27 | its id at that rank.
+int build_graph(ps_engine* e) {
+  const uint32_t n = e->cfg.n_peers;
+  const int32_t world = e->world, me = e->rank;
+  e->node_peer.clear();
+  e->node_parent.clear();
+  e->node_topic.clear();
+  e->row_ptr.assign(1, 0);
+  e->col.clear();
+  e->remote_fed.clear();
+  e->ghost_ref.clear();
+  e->ship_host.clear();
+  std::vector<uint32_t> local(n, kNone);  // peer -> BFS position
+  TopicBfs B;
+  const uint32_t ntop = static_cast<uint32_t>(e->topics.size());
+  // node-space base of every topic at every rank (a remote child is addressed
+  // by its fused node id at its owner)
+  std::vector<uint64_t> base_at(static_cast<size_t>(ntop) * std::max(world, 1), 0);
+  if (world > 1) {
+    std::vector<uint64_t> run(world, 0);
+    for (uint32_t t = 0; t < ntop; ++t) {
+      for (int32_t q = 0; q < world; ++q) base_at[static_cast<size_t>(t) * world + q] = run[q];
+      TopicHost& T = e->topics[t];
+      if (!T.exists) continue;
+      int rc = topic_bfs(e, T, local, B);
+      if (rc) return rc;
+      for (size_t u = 0; u < B.order.size(); ++u) run[B.owner[u]]++;
+      for (uint32_t p : B.order) local[p] = kNone;
+    }
+  }
+  std::vector<uint32_t> loc, ghost_of, mine;
+  std::vector<std::vector<uint32_t>> cur(std::max(world, 1)), nxt_local(std::max(world, 1));
+  std::vector<std::vector<uint32_t>> nxt_ghost(static_cast<size_t>(std::max(world, 1)) * std::max(world, 1));
+  uint64_t n_total = 0;
+  for (uint32_t t = 0; t < ntop; ++t) {
+    TopicHost& T = e->topics[t];
+    T.nbase = static_cast<uint32_t>(n_total);
+    T.n_nodes = 0;
+    T.depth = 0;
+    T.mesh = false;
+    T.root_local = true;
+    T.max_deg = 0;
+    T.cross.clear();
+    T.level_internal.clear();
+    T.level_off.clear();
+    T.level_local.clear();
+    T.gcnt.clear();
+    T.send_node.clear();
+    T.send_dst.clear();
+    T.send_lvl.clear();
+    T.ship0 = static_cast<uint32_t>(e->ship_host.size());
+    if (!T.exists) continue;
+    {
+      int rc = topic_bfs(e, T, local, B);
+      if (rc) return rc;
+    }
+    const auto& rp = B.rp;
+    const auto& cl = B.cl;
+    const auto& order = B.order;
+    const auto& owner = B.owner;
+    const uint32_t N = static_cast<uint32_t>(order.size());
+    for (uint32_t p : order) T.max_deg = std::max(T.max_deg, rp[p + 1] - rp[p]);
+    T.depth = B.level.back();
+    {
+      std::vector<uint32_t> indeg(N, 0);
+      for (uint32_t u = 0; u < N; ++u)
+        for (uint32_t k = rp[order[u]]; k < rp[order[u] + 1]; ++k) indeg[local[cl[k]]]++;
+      for (uint32_t u = 0; u < N; ++u)
+        if (indeg[u] > (u == 0 ? 0u : 1u)) T.mesh = true;
+    }
+    if (T.mesh && world > 1) return e->fail(PS_E_STATE, "multi-GPU engines support tree topics only");
+    T.root_local = owner[0] == me;
+    // per-rank numbering, level by level (see above)
+    const int32_t W = std::max(world, 1);
+    loc.assign(N, 0);
+    if (world > 1) ghost_of.assign(N, kNone);
+    mine.clear();
+    std::vector<uint32_t> next_id(W, 0);
+    for (auto& v : cur) v.clear();
+    cur[owner[0]].push_back(0);
+    loc[0] = next_id[owner[0]]++;
+    T.level_off.assign(T.depth + 2, 0);
+    T.level_local.assign(T.depth + 1, 0);
+    T.gcnt.assign(world > 1 ? static_cast<size_t>(T.depth + 2) * world * world : 0, 0);
+    T.send_lvl.assign(T.depth + 3, 0);
+    if (owner[0] == me) {
+      mine.push_back(0);
+      T.level_local[0] = 1;
+    }
+    T.level_off[1] = static_cast<uint32_t>(mine.size());
+    std::vector<uint32_t> kk(W);
+    for (uint32_t d = 0; d < T.depth; ++d) {
+      for (auto& v : nxt_local) v.clear();
+      for (auto& v : nxt_ghost) v.clear();
+      uint32_t* gc = world > 1 ? &T.gcnt[static_cast<size_t>(d + 1) * world * world] : nullptr;
+      for (int32_t a = 0; a < W; ++a)
+        for (uint32_t u : cur[a]) {
+          const uint32_t p = order[u];
+          uint32_t mask = 0;
+          for (uint32_t k = rp[p]; k < rp[p + 1]; ++k) {
+            const uint32_t v = local[cl[k]];
+            if (B.bfs_parent[v] != u) continue;  // (a mesh edge into an earlier-numbered node)
+            const int32_t b = owner[v];
+            if (b == a) {
+              nxt_local[a].push_back(v);
+              continue;
+            }
+            if (!(mask >> b & 1u)) {
+              mask |= 1u << b;
+              kk[b] = gc[a * world + b]++;
+              if (kk[b] > kRemoteIdMask) return e->fail(PS_E_NOMEM, "ghost rows of one level exceed 2^27");
+              if (a == me) {
+                e->ship_host.push_back(ShipEntry{T.nbase + loc[u], static_cast<uint32_t>(b) << kRemoteRankShift | kk[b]});
+                T.send_node.push_back(T.nbase + loc[u]);
+                T.send_dst.push_back(static_cast<uint32_t>(b) << kRemoteRankShift | kk[b]);
+              }
+            }
+            ghost_of[v] = static_cast<uint32_t>(a) << kRemoteRankShift | kk[b];
+            nxt_ghost[static_cast<size_t>(b) * W + a].push_back(v);
+          }
+        }
+      T.send_lvl[d + 2] = static_cast<uint32_t>(T.send_node.size());
+      for (int32_t r = 0; r < W; ++r) {
+        auto& c = cur[r];
+        c.swap(nxt_local[r]);
+        if (r == me) T.level_local[d + 1] = static_cast<uint32_t>(c.size());
+        for (int32_t a = 0; a < W; ++a) {
+          const auto& g = nxt_ghost[static_cast<size_t>(r) * W + a];
+          c.insert(c.end(), g.begin(), g.end());
+        }
+        for (uint32_t v : c) loc[v] = next_id[r]++;
+        if (r == me) {
+          mine.insert(mine.end(), c.begin(), c.end());
+          T.level_off[d + 2] = static_cast<uint32_t>(mine.size());
+        }
+      }
+    }
+    for (uint32_t d = 1; d < T.send_lvl.size(); ++d) T.send_lvl[d] = std::max(T.send_lvl[d], T.send_lvl[d - 1]);
+    // emit the owned nodes in local-id order
+    T.level_internal.assign(T.depth + 1, 0);
+    std::map<std::tuple<uint32_t, uint32_t, uint32_t>, uint32_t> cross;
+    if (world > 1)
+      for (uint32_t u = 0; u < N; ++u)
+        for (uint32_t k = rp[order[u]]; k < rp[order[u] + 1]; ++k) {
+          const uint32_t v = local[cl[k]];
+          if (owner[v] != owner[u])
+            cross[{B.level[u], static_cast<uint32_t>(owner[u]), static_cast<uint32_t>(owner[v])}]++;
+        }
+    for (uint32_t u : mine) {
+      const uint32_t p = order[u];
+      const uint32_t deg = rp[p + 1] - rp[p];
+      const uint32_t bp = B.bfs_parent[u];
+      e->node_peer.push_back(p);
+      if (world > 1) e->ghost_ref.push_back(u ? ghost_of[u] : kNone);
+      e->node_parent.push_back(u && owner[bp] == me ? T.nbase + loc[bp] : kNone);
+      e->node_topic.push_back(static_cast<uint16_t>(t));
+      for (uint32_t k = rp[p]; k < rp[p + 1]; ++k) {
+        const uint32_t v = local[cl[k]];
+        if (owner[v] == me) {
+          e->col.push_back(T.nbase + loc[v]);
+        } else {
+          const uint64_t id = base_at[static_cast<size_t>(t) * world + owner[v]] + loc[v];
+          if (id > kRemoteIdMask) return e->fail(PS_E_NOMEM, "rank node space exceeds 2^27");
+          e->col.push_back(kRemoteBit | (static_cast<uint32_t>(owner[v]) << kRemoteRankShift) |
+                           static_cast<uint32_t>(id));
+        }
+      }
+      e->row_ptr.push_back(static_cast<uint32_t>(e->col.size()));
+      if (deg) T.level_internal[B.level[u]]++;
+      if (u && owner[bp] != me) e->remote_fed.push_back(T.nbase + loc[u]);
+      if (e->col.size() >= 0xFFFFFFF0ull) return e->fail(PS_E_NOMEM, "edge space exceeds 2^32");
+    }
+    for (const auto& kv : cross)
+      T.cross.push_back({std::get<0>(kv.first), std::get<1>(kv.first), std::get<2>(kv.first), kv.second});
+    T.n_nodes = static_cast<uint32_t>(mine.size());
+    for (uint32_t p : order) local[p] = kNone;
+    n_total += T.n_nodes;
+    if (n_total >= 0xFFFFFFF0ull) return e->fail(PS_E_NOMEM, "node space exceeds 2^32 nodes");
+  }
+  e->n_nodes = static_cast<uint32_t>(n_total);
+  e->n_pad = ((e->n_nodes + 15) / 16) * 16;
+  if (e->n_pad == 0) e->n_pad = 16;
+  return PS_OK;
+}
+
+void build_flags(ps_engine* e) {
+  e->node_flags.assign(e->n_nodes, 0);
+  for (uint32_t u = 0; u < e->n_nodes; ++u) {
+    const uint32_t p = e->node_peer[u];
+    uint8_t f = e->live[p] ? kNodeLive : 0;
+    if (e->row_ptr[u + 1] > e->row_ptr[u]) f |= kNodeInternal;
+    for (uint32_t k = e->row_ptr[u]; k < e->row_ptr[u + 1]; ++k)
+      if (e->col[k] & kRemoteBit) {
+        f |= kNodeSplit;
+        break;
+      }
+    e->node_flags[u] = f;
+  }
+  for (const auto& T : e->topics)
+    if (T.exists && T.n_nodes && T.root_local) e->node_flags[T.nbase] |= kNodeLive;  // roots forward
+}
+
+// Host copies of the node space when it was built on the GPU (record-mode
+// readback, ps_read_delivered, the push kernel's level schedule).
+int ensure_mirrors(ps_engine* e) {
+  if (e->mirrors_valid) return PS_OK;
+  const size_t nn = e->n_nodes;
+  e->node_peer.resize(nn);
+  e->node_parent.resize(nn);
+  e->node_topic.resize(nn);
+  e->node_flags.resize(nn);
+  e->row_ptr.resize(nn + 1);
+  hipStream_t s = e->stream;
+  HIP_TRY(hipMemcpyAsync(e->row_ptr.data(), e->d_row_ptr.p, (nn + 1) * 4, hipMemcpyDeviceToHost, s), "read row_ptr");
+  HIP_TRY(hipStreamSynchronize(s), "sync");
+  e->col.resize(e->row_ptr[nn]);
+  if (nn) {
+    HIP_TRY(hipMemcpyAsync(e->node_peer.data(), e->d_node_peer.p, nn * 4, hipMemcpyDeviceToHost, s), "read node_peer");
+    HIP_TRY(hipMemcpyAsync(e->node_parent.data(), e->d_node_parent.p, nn * 4, hipMemcpyDeviceToHost, s),
+            "read node_parent");
+    HIP_TRY(hipMemcpyAsync(e->node_topic.data(), e->d_node_topic.p, nn * 2, hipMemcpyDeviceToHost, s), "read node_topic");
+    HIP_TRY(hipMemcpyAsync(e->node_flags.data(), e->d_node_flags.p, nn, hipMemcpyDeviceToHost, s), "read node_flags");
+  }
+  if (!e->col.empty())
+    HIP_TRY(hipMemcpyAsync(e->col.data(), e->d_col.p, e->col.size() * 4, hipMemcpyDeviceToHost, s), "read col");
+  HIP_TRY(hipStreamSynchronize(s), "sync");
+  e->mirrors_valid = true;
+  return PS_OK;
+}
+
+namespace {
+
+bool can_gpu_build(const ps_engine* e) {
+  if (!e->gpu_build_on || e->world != 1 || e->cfg.n_peers >= (1u << kBuildPeerBits)) return false;
+  bool any = false;
+  for (const auto& T : e->topics) {
+    if (!T.exists) continue;
+    if (T.kind != Kind::Join && T.kind != Kind::Parent) return false;
+    any = true;
+  }
+  return any;
+}
+
+// GPU rebuild of the node space (gbuild.hip): ship the
+// changed upstream entries, then per topic depth (pointer jumping) -> sort
+// of (depth, parent, peer) -> node ids, parents, fan-out; one scan for the
+// CSR, flags from the live mask.  Two small readbacks: reachable counts and
+// depths (to lay out the topics), then the level tables.  *fallback: a tree
+// deeper than the sort key allows -- the caller builds on the host.
+int gpu_build_graph(ps_engine* e, bool* fallback) {
+  *fallback = false;
+  const auto tb0 = std::chrono::steady_clock::now();
+  const uint32_t n = e->cfg.n_peers;
+  const uint32_t nt = static_cast<uint32_t>(e->topics.size());
+  hipStream_t s = e->stream;
+  HIP_TRY(e->d_tpar.ensure(static_cast<size_t>(nt) * n * 4), "alloc parents");
+  // 1. parent deltas of every topic, one upload
+  auto& pairs = e->pairs_host;
+  pairs.clear();
+  e->pair_off.assign(nt + 1, 0);
+  std::vector<uint32_t> cand;
+  for (uint32_t t = 0; t < nt; ++t) {
+    TopicHost& T = e->topics[t];
+    e->pair_off[t] = pairs.size() / 2;
+    if (!T.exists) continue;
+    uint32_t* par_t = e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n;
+    bool full = false;
+    if (!T.par_dev_valid) {
+      HIP_TRY(hipMemsetAsync(par_t, 0xFF, static_cast<size_t>(n) * 4, s), "clear parents");
+      T.par_mirror.assign(n, kNone);
+      T.par_dev_valid = true;
+      full = true;
+    }
+    auto diff = [&](uint32_t p, uint32_t v) {
+      if (T.par_mirror[p] != v) {
+        T.par_mirror[p] = v;
+        pairs.push_back(p);
+        pairs.push_back(v);
+      }
+    };
+    if (T.kind == Kind::Join) {
+      T.tree.take_touched(cand);
+      if (full)
+        for (uint32_t p = 0; p < n; ++p) diff(p, T.tree.in_parent(p));
+      else
+        for (size_t i = 0; i < cand.size(); ++i) {
+          if (i + 16 < cand.size()) {  // touched peers are scattered: fetch ahead
+            T.tree.prefetch_peer(cand[i + 16]);
+            __builtin_prefetch(&T.par_mirror[cand[i + 16]]);
+          }
+          diff(cand[i], T.tree.in_parent(cand[i]));
+        }
+    } else if (T.par_full_dirty || full) {
+      for (uint32_t p = 0; p < n; ++p) diff(p, p == T.root ? kNone : T.parent[p]);
+      T.par_full_dirty = false;
+    }
+  }
+  e->pair_off[nt] = pairs.size() / 2;
+  if (!pairs.empty()) {
+    HIP_TRY(e->d_pairs.ensure(pairs.size() * 4), "alloc deltas");
+    HIP_TRY(hipMemcpyAsync(e->d_pairs.p, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, s),
+            "upload deltas");
+    for (uint32_t t = 0; t < nt; ++t)
+      HIP_TRY(launch_scatter_pairs(e->d_pairs.as<uint32_t>() + 2 * e->pair_off[t],
+                                   static_cast<uint32_t>(e->pair_off[t + 1] - e->pair_off[t]),
+                                   e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n, s),
+              "scatter deltas");
+  }
+  using clk = std::chrono::steady_clock;
+  const auto tb1 = clk::now();
+  // 2. depth keys and sort per topic
+  HIP_TRY(e->d_anc0.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
+  HIP_TRY(e->d_anc1.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
+  HIP_TRY(e->d_dep0.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
+  HIP_TRY(e->d_dep1.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
+  HIP_TRY(e->d_keys0.ensure(static_cast<size_t>(n) * 8), "alloc keys");
+  HIP_TRY(e->d_skeys.ensure(static_cast<size_t>(nt) * n * 8), "alloc sorted keys");
+  HIP_TRY(e->d_gstat.ensure(static_cast<size_t>(nt) * 4 * 4), "alloc build stats");
+  HIP_TRY(e->d_lvl.ensure(static_cast<size_t>(nt) * 512 * 4), "alloc level tables");
+  size_t cub_bytes = 0, scan_bytes = 0;
+  HIP_TRY(sort_keys(nullptr, &cub_bytes, nullptr, nullptr, n, s), "sort size");
+  HIP_TRY(e->d_cub.ensure(std::max<size_t>(cub_bytes, 16)), "alloc sort temp");
+  // [t][reach, max depth, max fan-out, unresolved]
+  uint32_t* gstat = e->d_gstat.as<uint32_t>();
+  auto& gs = e->gstat_host;
+  auto& lh = e->lvl_host;
+  // pointer jumping sized from the last build's depth (x4 headroom); a topic
+  // that grew deeper reports unresolved peers and is redone with full jumps
+  std::vector<uint32_t> jumps(nt, depth_jumps_full(n));
+  for (uint32_t t = 0; t < nt; ++t) {
+    const uint32_t d = e->topics[t].depth;
+    if (d) jumps[t] = std::min(jumps[t], depth_jumps_full(4 * d));
+  }
+  for (int pass = 0; pass < 2; ++pass) {
+    HIP_TRY(hipMemsetAsync(e->d_gstat.p, 0, static_cast<size_t>(nt) * 4 * 4, s), "clear build stats");
+    HIP_TRY(hipMemsetAsync(e->d_lvl.p, 0, static_cast<size_t>(nt) * 512 * 4, s), "clear level tables");
+    for (uint32_t t = 0; t < nt; ++t) {
+      const TopicHost& T = e->topics[t];
+      if (!T.exists) continue;
+      HIP_TRY(launch_depth_keys(e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n, n, T.root, jumps[t],
+                                e->d_anc0.as<uint32_t>(), e->d_anc1.as<uint32_t>(),
+                                e->d_dep0.as<uint32_t>(), e->d_dep1.as<uint32_t>(),
+                                e->d_keys0.as<uint64_t>(), gstat + 4 * t, s),
+              "depth");
+      size_t tb = e->d_cub.bytes;
+      HIP_TRY(sort_keys(e->d_cub.p, &tb, e->d_keys0.as<uint64_t>(),
+                        e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n, s),
+              "sort");
+      HIP_TRY(launch_level_starts(e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n,
+                                  e->d_lvl.as<uint32_t>() + 512 * t, s),
+              "level starts");
+    }
+    // (level starts of unreachable peers' keys land in slot 255: ignored)
+    gs.assign(static_cast<size_t>(nt) * 4, 0);
+    lh.assign(static_cast<size_t>(nt) * 512, 0);
+    HIP_TRY(hipMemcpyAsync(gs.data(), gstat, gs.size() * 4, hipMemcpyDeviceToHost, s), "read build stats");
+    HIP_TRY(hipMemcpyAsync(lh.data(), e->d_lvl.p, lh.size() * 4, hipMemcpyDeviceToHost, s), "read level starts");
+    HIP_TRY(hipStreamSynchronize(s), "sync");
+    bool redo = false;
+    for (uint32_t t = 0; t < nt; ++t)
+      if (e->topics[t].exists && gs[4 * t + 3]) {
+        jumps[t] = depth_jumps_full(n);
+        redo = true;
+      }
+    if (!redo) break;
+  }
+  const auto tb2 = clk::now();
+  for (uint32_t t = 0; t < nt; ++t)
+    if (e->topics[t].exists && gs[4 * t + 1] >= kBuildMaxDepth) {
+      *fallback = true;  // deeper than the key's depth field
+      return PS_OK;
+    }
+  // 3. layout: topic t's nodes at [nbase_t, nbase_t + R_t)
+  uint64_t n_total = 0;
+  e->roots_host.clear();
+  for (uint32_t t = 0; t < nt; ++t) {
+    TopicHost& T = e->topics[t];
+    T.nbase = static_cast<uint32_t>(n_total);
+    T.n_nodes = T.exists ? gs[4 * t] : 0;
+    if (T.n_nodes) e->roots_host.push_back(T.nbase);
+    n_total += T.n_nodes;
+  }
+  if (n_total >= 0xFFFFFFF0ull) return e->fail(PS_E_NOMEM, "node space exceeds 2^32 nodes");
+  const uint32_t nn = static_cast<uint32_t>(n_total);
+  e->n_nodes = nn;
+  e->n_pad = std::max<uint32_t>(16, ((nn + 15) / 16) * 16);
+  HIP_TRY(e->d_row_ptr.ensure((static_cast<size_t>(nn) + 1) * 4), "alloc row_ptr");
+  HIP_TRY(e->d_col.ensure(std::max<size_t>(nn, 1) * 4), "alloc col");
+  HIP_TRY(e->d_node_topic.ensure(std::max<size_t>(nn, 1) * 2), "alloc node_topic");
+  HIP_TRY(e->d_node_peer.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_peer");
+  HIP_TRY(e->d_node_parent.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_parent");
+  HIP_TRY(e->d_node_flags.ensure(e->n_pad + 16), "alloc node_flags");
+  HIP_TRY(e->d_deg.ensure((static_cast<size_t>(nn) + 1) * 4), "alloc fan-out");
+  HIP_TRY(e->d_first.ensure(std::max<size_t>(nn, 1) * 4), "alloc first child");
+  HIP_TRY(e->d_local.ensure(static_cast<size_t>(n) * 4), "alloc local ids");
+  HIP_TRY(hipMemsetAsync(e->d_deg.p, 0, (static_cast<size_t>(nn) + 1) * 4, s), "clear fan-out");
+  HIP_TRY(hipMemsetAsync(e->d_first.p, 0xFF, std::max<size_t>(nn, 1) * 4, s), "clear first child");
+  uint32_t* lvl = e->d_lvl.as<uint32_t>();  // [t][0..255] level start, [t][256..511] internal count
+  // BFS placement, level by level and without sorting: the keys are already
+  // grouped by level and, within a level, by parent peer with siblings in peer
+  // order; the groups go in parent node order (an exclusive scan of the
+  // parents' fan-out), each child at its sibling rank
+  HIP_TRY(e->d_cnt.ensure(static_cast<size_t>(n) * 4), "alloc fan-out by peer");
+  HIP_TRY(e->d_fidx.ensure(static_cast<size_t>(n) * 4), "alloc first child index");
+  HIP_TRY(e->d_childoff.ensure(static_cast<size_t>(n) * 4 + 4), "alloc child offsets");
+  {
+    size_t sb = 0;
+    HIP_TRY(scan_u32(nullptr, &sb, nullptr, nullptr, n, s), "scan size");
+    HIP_TRY(e->d_cub.ensure(std::max<size_t>(sb, 16)), "alloc scan temp");
+  }
+  uint32_t* cnt = e->d_cnt.as<uint32_t>();
+  uint32_t* fidx = e->d_fidx.as<uint32_t>();
+  uint32_t* childoff = e->d_childoff.as<uint32_t>();
+  for (uint32_t t = 0; t < nt; ++t) {
+    TopicHost& T = e->topics[t];
+    if (!T.n_nodes) continue;
+    const uint32_t depth = gs[4 * t + 1];
+    const uint64_t* keys = e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n;
+    const uint16_t tt = static_cast<uint16_t>(t);
+    HIP_TRY(hipMemsetAsync(cnt, 0, static_cast<size_t>(n) * 4, s), "clear fan-out by peer");
+    HIP_TRY(hipMemsetAsync(fidx, 0xFF, static_cast<size_t>(n) * 4, s), "clear first child index");
+    HIP_TRY(launch_child_stats(keys, T.n_nodes, cnt, fidx, s), "child stats");
+    // the small top levels (and their parents) go in one single-block launch
+    auto lvl_end = [&](uint32_t d) { return d == depth ? T.n_nodes : lh[512 * t + d + 1]; };
+    uint32_t d_small = 1;
+    while (d_small <= depth && lvl_end(d_small) - lh[512 * t + d_small] <= e->small_place &&
+           lh[512 * t + d_small] - lh[512 * t + d_small - 1] <= e->small_place)
+      ++d_small;
+    if (d_small > 1) {
+      HIP_TRY(launch_place_small(keys, e->d_lvl.as<uint32_t>() + 512 * t, d_small, depth, T.n_nodes, T.nbase, tt,
+                                 cnt, fidx, e->d_node_peer.as<uint32_t>(), e->d_node_topic.as<uint16_t>(),
+                                 e->d_local.as<uint32_t>(), e->d_node_parent.as<uint32_t>(),
+                                 e->d_deg.as<uint32_t>(), e->d_first.as<uint32_t>(), s),
+              "place small levels");
+    } else {
+      HIP_TRY(launch_place_root(keys, T.nbase, tt, cnt, e->d_node_peer.as<uint32_t>(),
+                                e->d_node_topic.as<uint16_t>(), e->d_local.as<uint32_t>(),
+                                e->d_node_parent.as<uint32_t>(), e->d_deg.as<uint32_t>(), s),
+              "place root");
+    }
+    for (uint32_t d = d_small; d <= depth; ++d) {
+      const uint32_t plo = lh[512 * t + d - 1];
+      const uint32_t lo = lh[512 * t + d];
+      const uint32_t hi = d == depth ? T.n_nodes : lh[512 * t + d + 1];
+      size_t tb = e->d_cub.bytes;
+      HIP_TRY(scan_u32(e->d_cub.p, &tb, e->d_deg.as<uint32_t>() + T.nbase + plo, childoff, lo - plo, s),
+              "scan fan-out");
+      HIP_TRY(launch_place_level(keys, lo, hi, T.nbase, T.nbase + plo, childoff, cnt, fidx, tt,
+                                 e->d_node_peer.as<uint32_t>(), e->d_node_topic.as<uint16_t>(),
+                                 e->d_local.as<uint32_t>(), e->d_node_parent.as<uint32_t>(),
+                                 e->d_deg.as<uint32_t>(), e->d_first.as<uint32_t>(), s),
+              "place level");
+    }
+  }
+  for (uint32_t t = 0; t < nt; ++t) {
+    const TopicHost& T = e->topics[t];
+    if (!T.n_nodes) continue;
+    HIP_TRY(launch_level_internal(e->d_deg.as<uint32_t>(), T.nbase, T.n_nodes, lvl + 512 * t, gs[4 * t + 1],
+                                  lvl + 512 * t + 256, gstat + 4 * t + 2, s),
+            "level stats");
+  }
+  // 4. CSR: row_ptr = exclusive scan of the fan-out; children consecutive
+  HIP_TRY(scan_u32(nullptr, &scan_bytes, nullptr, nullptr, nn + 1, s), "scan size");
+  HIP_TRY(e->d_cub.ensure(std::max<size_t>(scan_bytes, 16)), "alloc scan temp");
+  size_t tb = e->d_cub.bytes;
+  HIP_TRY(scan_u32(e->d_cub.p, &tb, e->d_deg.as<uint32_t>(), e->d_row_ptr.as<uint32_t>(), nn + 1, s), "scan");
+  HIP_TRY(launch_fill_col(e->d_row_ptr.as<uint32_t>(), e->d_first.as<uint32_t>(), nn, e->d_col.as<uint32_t>(), s),
+          "fill col");
+  // 5. level tables back to the host (rounds, chunks, grid bounds)
+  const auto tb3 = clk::now();
+  HIP_TRY(hipMemcpyAsync(lh.data(), lvl, lh.size() * 4, hipMemcpyDeviceToHost, s), "read level tables");
+  HIP_TRY(hipMemcpyAsync(gs.data(), gstat, gs.size() * 4, hipMemcpyDeviceToHost, s), "read build stats");
+  HIP_TRY(hipStreamSynchronize(s), "sync");
+  if (e->host_timing) {
+    auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+    std::fprintf(stderr, "[psengine] gpu build: deltas %.3f ms (%zu), depth+sort+readback %.3f ms, "
+                 "placement enqueue %.3f ms, drain %.3f ms\n", ms(tb0, tb1), pairs.size() / 2,
+                 ms(tb1, tb2), ms(tb2, tb3), ms(tb3, clk::now()));
+  }
+  for (uint32_t t = 0; t < nt; ++t) {
+    TopicHost& T = e->topics[t];
+    T.mesh = false;
+    T.root_local = true;
+    T.cross.clear();
+    T.depth = T.n_nodes ? gs[4 * t + 1] : 0;
+    T.max_deg = gs[4 * t + 2];
+    T.level_off.assign(T.depth + 2, 0);
+    T.level_internal.assign(T.depth + 1, 0);
+    T.level_local.clear();
+    T.gcnt.clear();
+    T.send_node.clear();
+    T.send_dst.clear();
+    T.send_lvl.clear();
+    if (!T.n_nodes) continue;
+    for (uint32_t d = 0; d <= T.depth; ++d) {
+      T.level_off[d] = lh[512 * t + d];
+      T.level_internal[d] = lh[512 * t + 256 + d];
+    }
+    T.level_off[T.depth + 1] = T.n_nodes;
+    T.level_local.assign(T.depth + 1, 0);
+    for (uint32_t d = 0; d <= T.depth; ++d) T.level_local[d] = T.level_off[d + 1] - T.level_off[d];
+  }
+  e->remote_fed.clear();
+  e->ghost_ref.clear();
+  e->ship_host.clear();
+  e->gpu_graph = true;
+  e->mirrors_valid = false;
+  return PS_OK;
+}
+
+}  // namespace
+
+int upload_graph(ps_engine* e) {
+  // nothing changed: no uploads, and no stream sync (a pipelined run must not
+  // wait here for the previous run's kernels)
+  if (!e->graph_dirty && !e->flags_dirty) return PS_OK;
+  if (e->graph_dirty) {
+    bool built = false;
+    if (can_gpu_build(e)) {
+      bool fallback = false;
+      int rc = gpu_build_graph(e, &fallback);
+      if (rc) return rc;
+      built = !fallback;
+    }
+    if (!built) {
+      int rc = build_graph(e);
+      if (rc) return rc;
+      e->gpu_graph = false;
+      e->mirrors_valid = true;
+      const size_t nn = e->n_nodes;
+      HIP_TRY(e->d_row_ptr.ensure((nn + 1) * 4), "alloc row_ptr");
+      HIP_TRY(e->d_col.ensure(std::max<size_t>(e->col.size(), 1) * 4), "alloc col");
+      HIP_TRY(e->d_node_topic.ensure(std::max<size_t>(nn, 1) * 2), "alloc node_topic");
+      HIP_TRY(e->d_node_peer.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_peer");
+      HIP_TRY(e->d_node_parent.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_parent");
+      // padded to n_pad: the expand kernel stages flag bytes as whole dwords
+      HIP_TRY(e->d_node_flags.ensure(e->n_pad + 16), "alloc node_flags");
+      HIP_TRY(hipMemcpyAsync(e->d_row_ptr.p, e->row_ptr.data(), (nn + 1) * 4, hipMemcpyHostToDevice, e->stream),
+              "upload row_ptr");
+      if (!e->col.empty())
+        HIP_TRY(hipMemcpyAsync(e->d_col.p, e->col.data(), e->col.size() * 4, hipMemcpyHostToDevice, e->stream),
+                "upload col");
+      if (nn) {
+        HIP_TRY(hipMemcpyAsync(e->d_node_topic.p, e->node_topic.data(), nn * 2, hipMemcpyHostToDevice, e->stream),
+                "upload node_topic");
+        HIP_TRY(hipMemcpyAsync(e->d_node_peer.p, e->node_peer.data(), nn * 4, hipMemcpyHostToDevice, e->stream),
+                "upload node_peer");
+        HIP_TRY(hipMemcpyAsync(e->d_node_parent.p, e->node_parent.data(), nn * 4, hipMemcpyHostToDevice,
+                               e->stream),
+                "upload node_parent");
+      }
+      if (e->world > 1) {  // ghost parents: the record each ghost-fed node reads, the records each parent ships
+        HIP_TRY(e->d_ghost_ref.ensure(std::max<size_t>(nn, 1) * 4), "alloc ghost refs");
+        HIP_TRY(e->d_ship.ensure(std::max<size_t>(e->ship_host.size(), 1) * sizeof(ShipEntry)), "alloc ship entries");
+        if (nn)
+          HIP_TRY(hipMemcpyAsync(e->d_ghost_ref.p, e->ghost_ref.data(), nn * 4, hipMemcpyHostToDevice, e->stream),
+                  "upload ghost refs");
+        if (!e->ship_host.empty())
+          HIP_TRY(hipMemcpyAsync(e->d_ship.p, e->ship_host.data(), e->ship_host.size() * sizeof(ShipEntry),
+                                 hipMemcpyHostToDevice, e->stream),
+                  "upload ship entries");
+      }
+    }
+    const size_t nn = e->n_nodes;
+    bool fresh = false;
+    const size_t flag_bytes = static_cast<size_t>(ceil_div(e->n_pad, kFlagsPerBlock)) * kFlagsPerBlock;
+    HIP_TRY(e->d_flags.ensure(flag_bytes, &fresh), "alloc flags");
+    HIP_TRY(hipMemsetAsync(e->d_flags.p, 0, e->d_flags.bytes, e->stream), "clear flags");
+    const size_t n_blk = ceil_div(e->n_pad, kFlagsPerBlock);
+    HIP_TRY(e->d_blk.ensure(n_blk), "alloc block flags");
+    HIP_TRY(hipMemsetAsync(e->d_blk.p, 0, e->d_blk.bytes, e->stream), "clear block flags");
+    HIP_TRY(e->d_gen.ensure(e->n_pad + 16), "alloc generations");
+    e->n_remote_fed = static_cast<uint32_t>(e->remote_fed.size());
+    HIP_TRY(e->d_remote_fed.ensure(std::max<size_t>(e->remote_fed.size(), 1) * 4), "alloc remote list");
+    if (!e->remote_fed.empty())
+      HIP_TRY(hipMemcpyAsync(e->d_remote_fed.p, e->remote_fed.data(), e->remote_fed.size() * 4,
+                             hipMemcpyHostToDevice, e->stream),
+              "upload remote list");
+    HIP_TRY(hipMemsetAsync(e->d_gen.p, 0, e->d_gen.bytes, e->stream), "clear generations");
+    e->gen_cur = 0;  // node ids changed: every row is stale
+    HIP_TRY(e->d_frontier.ensure(std::max<size_t>(nn, 1) * 4), "alloc frontier");
+    HIP_TRY(e->d_wgcount.ensure(static_cast<size_t>(ceil_div(e->n_pad, kFlagsPerBlock)) * 4),
+            "alloc wg_count");
+    e->graph_dirty = false;
+    e->flags_dirty = true;
+    e->have_window = false;  // the node space of the last window is gone
+    ++e->graph_epoch;
+  }
+  if (e->flags_dirty) {
+    ++e->flags_epoch;
+    if (e->gpu_graph) {
+      const uint32_t n = e->cfg.n_peers;
+      HIP_TRY(e->d_live.ensure(n), "alloc live mask");
+      HIP_TRY(e->d_roots.ensure(std::max<size_t>(e->roots_host.size(), 1) * 4), "alloc roots");
+      HIP_TRY(hipMemcpyAsync(e->d_live.p, e->live.data(), n, hipMemcpyHostToDevice, e->stream), "upload live");
+      if (!e->roots_host.empty())
+        HIP_TRY(hipMemcpyAsync(e->d_roots.p, e->roots_host.data(), e->roots_host.size() * 4,
+                               hipMemcpyHostToDevice, e->stream),
+                "upload roots");
+      HIP_TRY(launch_node_flags(e->d_node_peer.as<uint32_t>(), e->d_row_ptr.as<uint32_t>(),
+                                e->d_live.as<uint8_t>(), e->n_nodes, e->d_roots.as<uint32_t>(),
+                                static_cast<uint32_t>(e->roots_host.size()), e->d_node_flags.as<uint8_t>(),
+                                e->stream),
+              "node flags");
+      e->mirrors_valid = false;
+    } else {
+      build_flags(e);
+      if (e->n_nodes)
+        HIP_TRY(hipMemcpyAsync(e->d_node_flags.p, e->node_flags.data(), e->n_nodes, hipMemcpyHostToDevice,
+                               e->stream),
+                "upload node_flags");
+    }
+    e->flags_dirty = false;
+  }
+  // host mirrors may be rebuilt by the next call: finish the uploads now
+  HIP_TRY(hipStreamSynchronize(e->stream), "sync uploads");
+  return PS_OK;
+}
+
+}  // namespace psamd

@@ -786,7 +786,7 @@ struct PullTopic {
 template <class Ctr>
 __device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t nk,
                                              uint32_t p_lo, uint32_t p_hi, uint64_t* src, uint8_t* genl,
-                                             uint32_t lane, uint32_t cur, Ctr& c,
+                                             uint32_t lane, uint32_t cur, Ctr& c, uint32_t gin,
                                              uint32_t stage_cap = kPullMaxKids) {
   uint32_t g0 = 0;
   const bool staged = p_lo != kNoneNode && p_hi - p_lo < stage_cap;  // genl holds stage_cap + 8 bytes
@@ -810,12 +810,15 @@ __device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic&
     if (in && p != kNoneNode) {
       up = (staged ? genl[p - g0] : a.gen[p]) == cur;
       row = reinterpret_cast<uint64_t>((p == P.root ? a.a_cur : a.seen) + P.base + static_cast<uint64_t>(p) * P.W);
-    } else if (in && a.ghost_off) {  // parent on another rank: its row arrived this round
-      const uint64_t g = a.ghost_off[nb + j];
-      if (g != kGhostNone) {
-        up = a.recv[g - 1] != 0;
-        row = reinterpret_cast<uint64_t>(a.recv + g);
-        pid = 0x80000000u | static_cast<uint32_t>(g);
+    } else if (in && gin != kNoneNode) {  // parent on another rank: its record arrived this round
+      const uint32_t g = a.ghost_ref[nb + j];
+      if (g != kNoneNode) {
+        const GhostSeg* S = a.gsegs + gin;
+        const uint64_t* rec = a.recv + S->rbase[g >> kRemoteRankShift] +
+                              static_cast<uint64_t>(g & kRemoteIdMask) * S->rw;
+        up = rec[0] != 0;  // an unreached parent's record starts with a zero word
+        row = reinterpret_cast<uint64_t>(rec);
+        pid = 0x80000000u | g;
       }
     }
     uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(pid), 1, 64));
@@ -824,8 +827,8 @@ __device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic&
       const uint32_t q = nb + j0;
       if (q > P.nbase) {
         prev = a.node_parent[q - 1];
-        if (prev == kNoneNode && a.ghost_off && a.ghost_off[q - 1] != kGhostNone)
-          prev = 0x80000000u | static_cast<uint32_t>(a.ghost_off[q - 1]);
+        if (prev == kNoneNode && gin != kNoneNode && a.ghost_ref[q - 1] != kNoneNode)
+          prev = 0x80000000u | a.ghost_ref[q - 1];
       }
     }
     const bool ok = up && (f & kNodeLive);
@@ -961,27 +964,33 @@ __device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& 
 }
 
 // Multi-GPU: the chunk's nodes that are ghost parents next round ship their
-// rows now, into the send buffer's records ([reach word][W words] at row_off
-// - 1), from the rows they copied (src[]: L2-resident, just read): one
-// pass over the records, 16-B units for even W.  Replaces a separate pack
-// launch that re-read the rows from HBM.
+// rows now, as records in the send buffer (GhostSeg gout: record k to rank b
+// at sbase[b] + k * W), from the rows they copied (src[]: L2-resident, just
+// read): one pass over the records, 16-B units for even W.  An unreached
+// node's record gets a zero first word.  Replaces a separate pack launch that
+// re-read the rows from HBM.
 __device__ __forceinline__ void pull_ship(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t e_lo,
-                                          uint32_t e_hi, const uint64_t* src, uint32_t lane) {
+                                          uint32_t e_hi, uint32_t gout, const uint64_t* src, uint32_t lane) {
+  const GhostSeg* S = a.gsegs + gout;
   const bool pairs = !(P.W & 1u);
   const uint32_t per = pairs ? P.W >> 1 : P.W;
   const uint32_t total = (e_hi - e_lo) * per;
   for (uint32_t i = lane; i < total; i += 64) {
     const uint32_t k = i / per, r = i - k * per;
-    const PackEntry E = a.ship[e_lo + k];
+    const ShipEntry E = a.ship[e_lo + k];
     const uint64_t row = src[E.node - nb];
-    if (r == 0) a.send[E.row_off - 1] = row != 0 ? 1ull : 0ull;
-    if (row == 0) continue;
+    uint64_t* rec = a.send + S->sbase[E.dst >> kRemoteRankShift] +
+                    static_cast<uint64_t>(E.dst & kRemoteIdMask) * P.W;
+    if (row == 0) {
+      if (r == 0) rec[0] = 0;
+      continue;
+    }
     const uint32_t w = pairs ? 2 * r : r;
     const uint64_t* s = reinterpret_cast<const uint64_t*>(row) + w;
     if (pairs)
-      *reinterpret_cast<uint4*>(a.send + E.row_off + w) = *reinterpret_cast<const uint4*>(s);
+      *reinterpret_cast<uint4*>(rec + w) = *reinterpret_cast<const uint4*>(s);
     else
-      a.send[E.row_off + w] = *s;
+      rec[w] = *s;
   }
 }
 
@@ -1031,9 +1040,9 @@ __global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __
     const uint32_t n1 = ch.node_end - ch.node_begin;
     // LDS ops of a wave are processed in order: the table written in phase 1
     // is visible to the reads that follow
-    pull_resolve(a, P, ch.node_begin, n1, ch.p_lo, ch.p_hi, src, genl, lane, cur, c);
+    pull_resolve(a, P, ch.node_begin, n1, ch.p_lo, ch.p_hi, src, genl, lane, cur, c, ch.gin);
     pull_stream<kRecord, kNT>(a, P, ch.node_begin, n1, src, lane, round, c);
-    if (ch.e_hi > ch.e_lo) pull_ship(a, P, ch.node_begin, ch.e_lo, ch.e_hi, src, lane);
+    if (ch.e_hi > ch.e_lo) pull_ship(a, P, ch.node_begin, ch.e_lo, ch.e_hi, ch.gout, src, lane);
   }
   pull_flush(c, a.partials, blockIdx.x % a.slot_mod, lane, wid);
 }
@@ -1232,7 +1241,7 @@ __global__ __launch_bounds__(64) void k_pull_pair(PullArgs a, const PullChunk* _
       pf_f[s] = j < nk0 ? a.node_flags[ch.c_lo + j] : 0u;
     }
     WaveCtr ca;
-    pull_resolve(a, P, ch.node_begin, n1, ch.p_lo, ch.p_hi, src, genl, lane, cur, ca, kPairPar);
+    pull_resolve(a, P, ch.node_begin, n1, ch.p_lo, ch.p_hi, src, genl, lane, cur, ca, ch.gin, kPairPar);
     for (uint32_t j0 = 0; j0 < n1; j0 += 64) {
       const uint64_t b = __ballot(j0 + lane < n1 && src[j0 + lane] != 0);
       if (lane == 0) reach[j0 >> 6] = b;
@@ -1269,18 +1278,14 @@ __global__ __launch_bounds__(kBlock) void k_pair_kids(PullChunk* __restrict__ ch
   c.c_hi = re > rb ? col[re - 1] + 1u : 0u;
 }
 
-// Multi-GPU level mode: the round's ghost rows.  Thread i of the flattened
-// stream copies unit i of one record -- a 16-B word pair for even W (rows
-// and records 16-B aligned), one word for odd W: segment (one topic,
-// constant W) by a short scan, entry = offset / units per row (32-bit).  A
-// parent not reached this window (stale generation) ships only its zero
-// reach word; the receiver then skips its children.
-__global__ __launch_bounds__(kBlock) void k_pack(const PackEntry* __restrict__ entries,
+// Multi-GPU level mode: the topic roots' records of a round (the roots are
+// seeded, so always reached).  Thread i of the flattened stream copies unit i
+// of one record -- a 16-B word pair for even W, one word for odd W: segment
+// (one root, constant W) by a short scan, entry = offset / units per row.
+__global__ __launch_bounds__(kBlock) void k_pack(const ShipEntry* __restrict__ ship,
                                                  const PackSeg* __restrict__ segs, uint32_t n_segs,
-                                                 uint64_t total, const TopicDev* __restrict__ topics,
-                                                 const uint64_t* __restrict__ seen, const uint8_t* __restrict__ gen,
-                                                 uint32_t gen_cur, uint64_t* __restrict__ send) {
-  const uint8_t cur = static_cast<uint8_t>(gen_cur);
+                                                 uint64_t total, const GhostSeg* __restrict__ gsegs,
+                                                 const uint64_t* __restrict__ seen, uint64_t* __restrict__ send) {
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < total;
        i += static_cast<uint64_t>(gridDim.x) * kBlock) {
     uint32_t k = 0;
@@ -1291,17 +1296,14 @@ __global__ __launch_bounds__(kBlock) void k_pack(const PackEntry* __restrict__ e
     const uint32_t o = static_cast<uint32_t>(i - S.unit0);
     const uint32_t e = S.e0 + o / per;
     const uint32_t w = (o - (e - S.e0) * per) << (pairs ? 1 : 0);
-    const PackEntry E = entries[e];
-    const bool reached = gen[E.node] == cur;
-    if (w == 0) send[E.row_off - 1] = reached ? 1 : 0;
-    if (reached) {
-      const TopicDev T = topics[S.topic];
-      const uint64_t* row = seen + T.wbase + static_cast<uint64_t>(E.node - T.nbase) * T.W + w;
-      if (pairs)
-        *reinterpret_cast<uint4*>(send + E.row_off + w) = *reinterpret_cast<const uint4*>(row);
-      else
-        send[E.row_off + w] = *row;
-    }
+    const ShipEntry E = ship[e];
+    uint64_t* rec = send + gsegs[S.gseg].sbase[E.dst >> kRemoteRankShift] +
+                    static_cast<uint64_t>(E.dst & kRemoteIdMask) * S.W;
+    const uint64_t* row = seen + S.row + w;
+    if (pairs)
+      *reinterpret_cast<uint4*>(rec + w) = *reinterpret_cast<const uint4*>(row);
+    else
+      rec[w] = *row;
   }
 }
 
@@ -1646,13 +1648,11 @@ hipError_t launch_pair_kids(PullChunk* chunks, uint32_t n, const uint32_t* row_p
   return hipGetLastError();
 }
 
-hipError_t launch_pack(const PackEntry* entries, const PackSeg* segs, uint32_t n_segs, uint64_t total_units,
-                       const TopicDev* topics, const uint64_t* seen, const uint8_t* gen, uint32_t gen_cur,
-                       uint64_t* send, hipStream_t s) {
+hipError_t launch_pack(const ShipEntry* ship, const PackSeg* segs, uint32_t n_segs, uint64_t total_units,
+                       const GhostSeg* gsegs, const uint64_t* seen, uint64_t* send, hipStream_t s) {
   if (total_units == 0 || n_segs == 0) return hipSuccess;
   const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(4096, (total_units + kBlock - 1) / kBlock));
-  hipLaunchKernelGGL(k_pack, dim3(grid), dim3(kBlock), 0, s, entries, segs, n_segs, total_units, topics, seen, gen,
-                     gen_cur, send);
+  hipLaunchKernelGGL(k_pack, dim3(grid), dim3(kBlock), 0, s, ship, segs, n_segs, total_units, gsegs, seen, send);
   return hipGetLastError();
 }
 

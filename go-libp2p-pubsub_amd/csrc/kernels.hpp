@@ -120,7 +120,7 @@ struct ExpandArgs {
   uint64_t* partials;  // [n_waves][kNumCtr]
   uint16_t* hop_rec;   // [word*64 + bit] = round (kHopRecNone: none), record mode only
   uint32_t gen_cur;
-  uint8_t* send;                  // send regions of this round (multi-GPU)
+  uint8_t* send;                  // send regions of this round (multi-GPU compaction mode)
   uint64_t send_off[kMaxRanks];   // byte offset of the region for each rank
 };
 
@@ -140,16 +140,45 @@ struct PullChunk {
   // filled in on the device), written in round q + 1 by the same wave; c_lo =
   // kNoneNode: a run written in round q + 1 itself (level 1 under a root)
   uint32_t c_lo, c_hi;
+  // multi-GPU: GhostSeg of this round (a ghost-fed node reads its parent's
+  // record there) and of the next round (the records [e_lo, e_hi) ship
+  // into); kNoneNode: none
+  uint32_t gin, gout;
+  uint32_t group;  // host: the start group (index in the topic's groups) whose block the chunk writes
+  uint32_t pad;
 };
 constexpr uint32_t kPullMaxKids = 512;
 constexpr uint32_t kNoneNode = 0xFFFFFFFFu;
 constexpr uint32_t kPullWords = 1024;
 
-struct PackEntry {
-  uint32_t node;     // the parent (local node id)
-  uint32_t pad;
-  uint64_t row_off;  // row, words from the send buffer (reach word at row_off - 1)
+// Multi-GPU level mode.  Before round q each rank ships the
+// rows of its parents of the level written in round q - 1 that have children
+// on other ranks -- once per destination rank -- as records of W words (the
+// start group's block): record k of the (round, topic, group)'s a -> b block
+// is a's k-th such parent in a's node order.  No header: a reached parent's
+// block holds every message of its start group (a tree, one start round per
+// block), so its first word is non-zero; an unreached parent's record starts
+// with a zero word and its children stay unreached.
+struct ShipEntry {
+  uint32_t node;  // the parent (local node id)
+  uint32_t dst;   // destination rank << 27 | record index k
 };
+struct GhostSeg {              // one (round, topic, start group)
+  uint64_t rbase[kMaxRanks];   // recv buffer: first word of the records from rank a
+  uint64_t sbase[kMaxRanks];   // send buffer: first word of the records to rank b (the round's half)
+  uint32_t rw;                 // record words (the block width)
+  uint32_t topic;
+};
+// k_pack: a topic root's records (round s_g + 1 of each start group g), from
+// its seeded row; one segment per (round, topic, group).
+struct PackSeg {
+  uint32_t e0, e1;  // the root's ship entries
+  uint32_t gseg;    // GhostSeg of the round
+  uint32_t W;
+  uint64_t row;     // word offset of the root's row (block)
+  uint64_t unit0;   // the segment's first unit in the launch's flattened stream (pack_units)
+};
+__host__ __device__ inline uint32_t pack_units(uint32_t W) { return (W & 1u) ? W : W >> 1; }
 struct PullArgs {
   const uint32_t* node_parent;  // node-space parent (kNone for roots and remote parents)
   const uint8_t* node_flags;
@@ -159,14 +188,15 @@ struct PullArgs {
   uint8_t* gen;
   uint16_t* hop_rec;
   uint64_t* partials;  // [n_blocks][kNumCtr]
-  // multi-GPU: a node whose parent lives on another rank reads that parent's
-  // row from this round's receive buffer: ghost_off[node] = the row's first
-  // word in recv (its reach word is the word before), or kGhostNone
-  const uint64_t* ghost_off;  // null: one rank
+  // multi-GPU: a node whose parent lives on another rank (ghost_ref[node] =
+  // rank << 27 | k, kNoneNode otherwise) reads record k of that rank in this
+  // round's receive buffer (GhostSeg gin)
+  const uint32_t* ghost_ref;  // null: one rank
+  const GhostSeg* gsegs;
   const uint64_t* recv;
-  // multi-GPU: the next round's ghost records of the nodes written now
-  // (PullChunk e_lo/e_hi), stored into the send buffer
-  const PackEntry* ship;
+  // multi-GPU: the next round's records of the nodes written now
+  // (PullChunk e_lo/e_hi, GhostSeg gout), stored into the send buffer
+  const ShipEntry* ship;
   uint64_t* send;
   uint32_t gen_cur;
   uint32_t slot_mod;   // block b adds its counters into partial slot b % slot_mod (zeroed per window)
@@ -182,23 +212,6 @@ struct PullArgs {
 constexpr uint32_t kPairWords = 768;  // (1024: 17 resident waves/CU, cfg3 +3 % slower; 512: 1 parent of 330 words)
 constexpr uint32_t kPairPar = 128;
 constexpr uint32_t kPairKids = 256;
-constexpr uint64_t kGhostNone = ~0ull;
-
-// Multi-GPU level mode: before round q, each rank ships the
-// rows of its level-(q-1) parents that have children on other ranks -- once
-// per destination rank -- into that rank's region of the send buffer.  A
-// ghost record is [pad if W is even][reach word][W row words]: the row keeps
-// 16-B alignment and its reach word (parent reached this window) is the word
-// before it.  One entry per (parent, destination); the entries of one topic
-// form a segment (constant W).
-__host__ __device__ inline uint32_t ghost_record_words(uint32_t W) { return W + ((W & 1u) ? 1u : 2u); }
-struct PackSeg {
-  uint32_t e0, e1;  // entries
-  uint32_t topic, W;
-  uint64_t unit0;   // the segment's first unit in the launch's flattened stream (16-B pairs
-                    // for even W, words for odd W: pack_units)
-};
-__host__ __device__ inline uint32_t pack_units(uint32_t W) { return (W & 1u) ? W : W >> 1; }
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch
 // k_pull_pair: every wave adds its counters with atomics (no block
 // reduction) into slot wave % kPairSlots.  (4096 slots: no faster than 256,
@@ -347,10 +360,9 @@ hipError_t launch_pull_pair(const PullArgs& a, const PullChunk* chunks, uint32_t
 hipError_t launch_pair_kids(PullChunk* chunks, uint32_t n, const uint32_t* row_ptr, const uint32_t* col,
                             hipStream_t s);
 
-// multi-GPU level mode: the round's ghost rows into the send buffer
-hipError_t launch_pack(const PackEntry* entries, const PackSeg* segs, uint32_t n_segs, uint64_t total_units,
-                       const TopicDev* topics, const uint64_t* seen, const uint8_t* gen, uint32_t gen_cur,
-                       uint64_t* send, hipStream_t s);
+// multi-GPU level mode: the roots' records of the round into the send buffer
+hipError_t launch_pack(const ShipEntry* ship, const PackSeg* segs, uint32_t n_segs, uint64_t total_units,
+                       const GhostSeg* gsegs, const uint64_t* seen, uint64_t* send, hipStream_t s);
 // Fills PullChunk::p_lo / p_hi from the device node_parent (GPU-built graphs).
 hipError_t launch_chunk_parents(PullChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s);
 // k_flood (flood.hip): grid = resident blocks (<= flood_blocks_per_cu x CUs)

@@ -1,0 +1,1111 @@
+// run.cpp -- the round loop on the GPU (ps_run / ps_run_async / ps_wait):
+// plan uploads, one window's launches on the engine's stream (level mode:
+// k_flood, k_pull_pair, k_pull; N ranks: the ghost exchange on a second
+// stream beside each round's locally fed chunks; compaction mode: k_expand +
+// frontier compaction), counters and readbacks.  DESIGN.md §5-§7.
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+
+#include "engine.hpp"
+#include "gbuild.hpp"
+
+namespace psamd {
+
+namespace {
+
+int upload_pull(ps_engine* e) {
+  if (e->pull.version == e->pull_up) return PS_OK;
+  const auto& C = e->pull.chunks;
+  HIP_TRY(e->d_pull.ensure(std::max<size_t>(C.size(), 1) * sizeof(PullChunk)), "alloc pull chunks");
+  if (!C.empty()) {
+    HIP_TRY(hipMemcpyAsync(e->d_pull.p, C.data(), C.size() * sizeof(PullChunk), hipMemcpyHostToDevice, e->stream),
+            "upload pull chunks");
+    if (e->gpu_graph)  // parent ranges for the generation staging
+      HIP_TRY(launch_chunk_parents(e->d_pull.as<PullChunk>(), static_cast<uint32_t>(C.size()),
+                                   e->d_node_parent.as<uint32_t>(), e->stream),
+              "chunk parents");
+  }
+  e->pull_up = e->pull.version;
+  return PS_OK;
+}
+
+int upload_pair(ps_engine* e) {
+  if (e->pair.version == e->pair_up) return PS_OK;
+  const auto& C = e->pair.chunks;
+  HIP_TRY(e->d_pp.ensure(std::max<size_t>(C.size(), 1) * sizeof(PullChunk)), "alloc pair chunks");
+  if (!C.empty()) {
+    HIP_TRY(hipMemcpyAsync(e->d_pp.p, C.data(), C.size() * sizeof(PullChunk), hipMemcpyHostToDevice, e->stream),
+            "upload pair chunks");
+    if (e->gpu_graph)
+      HIP_TRY(launch_chunk_parents(e->d_pp.as<PullChunk>(), static_cast<uint32_t>(C.size()),
+                                   e->d_node_parent.as<uint32_t>(), e->stream),
+              "pair chunk parents");
+    HIP_TRY(launch_pair_kids(e->d_pp.as<PullChunk>(), static_cast<uint32_t>(C.size()), e->d_row_ptr.as<uint32_t>(),
+                             e->d_col.as<uint32_t>(), e->stream),
+            "pair chunk children");
+  }
+  e->pair_up = e->pair.version;
+  return PS_OK;
+}
+
+int upload_flood(ps_engine* e) {
+  if (e->flood.version == e->flood_up) return PS_OK;
+  const auto& TK = e->flood.tasks;
+  const auto& SG = e->flood.segs;
+  const size_t n = TK.size();
+  HIP_TRY(e->d_flood_tasks.ensure(std::max<size_t>(n, 1) * sizeof(FloodTask)), "alloc flood tasks");
+  HIP_TRY(e->d_flood_segs.ensure(std::max<size_t>(SG.size(), 1) * sizeof(FloodSeg)), "alloc flood segments");
+  bool fresh = false;  // granules of a fresh allocation carry no epoch yet
+  HIP_TRY(e->d_flood_gran.ensure(std::max<size_t>(e->flood.granules, 1) * 8, &fresh), "alloc flood granules");
+  if (fresh) HIP_TRY(hipMemsetAsync(e->d_flood_gran.p, 0, e->d_flood_gran.bytes, e->stream), "clear granules");
+  if (n) {
+    HIP_TRY(hipMemcpyAsync(e->d_flood_tasks.p, TK.data(), n * sizeof(FloodTask), hipMemcpyHostToDevice, e->stream),
+            "upload flood tasks");
+    HIP_TRY(hipMemcpyAsync(e->d_flood_segs.p, SG.data(), SG.size() * sizeof(FloodSeg), hipMemcpyHostToDevice,
+                           e->stream),
+            "upload flood segments");
+    HIP_TRY(launch_flood_deps(e->d_flood_tasks.as<FloodTask>(), static_cast<uint32_t>(n),
+                              e->d_flood_segs.as<FloodSeg>(), e->d_node_parent.as<uint32_t>(), e->stream),
+            "flood dependencies");
+  }
+  e->flood_up = e->flood.version;
+  return PS_OK;
+}
+
+int upload_ghost(ps_engine* e) {
+  const GhostPlan& G = e->ghost;
+  HIP_TRY(e->d_gsegs.ensure(std::max<size_t>(G.segs.size(), 1) * sizeof(GhostSeg)), "alloc ghost segments");
+  HIP_TRY(e->d_pack.ensure(std::max<size_t>(G.pack.size(), 1) * sizeof(PackSeg)), "alloc pack segments");
+  HIP_TRY(e->d_send.ensure(std::max<uint64_t>(2 * G.send_half, 16) * 8), "alloc send buffer");
+  HIP_TRY(e->d_recv.ensure(std::max<uint64_t>(G.recv_words, 16) * 8), "alloc recv buffer");
+  if (!G.segs.empty())
+    HIP_TRY(hipMemcpyAsync(e->d_gsegs.p, G.segs.data(), G.segs.size() * sizeof(GhostSeg), hipMemcpyHostToDevice,
+                           e->stream),
+            "upload ghost segments");
+  if (!G.pack.empty())
+    HIP_TRY(hipMemcpyAsync(e->d_pack.p, G.pack.data(), G.pack.size() * sizeof(PackSeg), hipMemcpyHostToDevice,
+                           e->stream),
+            "upload pack segments");
+  return PS_OK;
+}
+
+// Host -> device copies of one window through a pinned staging slot
+// (ps_engine::Staging): asynchronous for the host, stream-ordered.
+struct Upload {
+  void* dst;
+  const void* src;
+  size_t bytes;
+};
+// With `fold` set and the copy-kernel form, nothing is launched: *fold gets
+// the copies for a kernel that folds them in, and staged[i] the device-mapped
+// address of upload i's staged bytes (else its destination).
+int stage_uploads(ps_engine* e, const Upload* ups, size_t n, hipStream_t s, StageCopy* fold = nullptr,
+                  const void** staged = nullptr) {
+  if (fold) *fold = StageCopy{};
+  for (size_t i = 0; staged && i < n; ++i) staged[i] = ups[i].dst;
+  size_t need = 0;
+  for (size_t i = 0; i < n; ++i) need += (ups[i].bytes + 255) & ~size_t(255);
+  if (need == 0) return PS_OK;
+  // the slot of the asynchronous run being enqueued (its previous user was
+  // waited for before the run slot was reused); synchronous runs start with
+  // nothing in flight
+  ps_engine::Staging& g = e->stg[e->defer_into ? e->defer_into - e->infl : 0];
+  if (need > g.cap) {
+    if (g.h) HIP_TRY(hipHostFree(g.h), "free staging");
+    g.h = nullptr;
+    g.cap = 0;
+    const size_t cap = std::max<size_t>(need, 64 << 10);
+    void* h = nullptr;
+    HIP_TRY(hipHostMalloc(&h, cap, hipHostMallocMapped | hipHostMallocCoherent), "alloc staging");
+    g.h = static_cast<uint8_t*>(h);
+    g.cap = cap;
+    void* d = nullptr;
+    HIP_TRY(hipHostGetDevicePointer(&d, h, 0), "map staging");
+    g.d = static_cast<uint8_t*>(d);
+  }
+  // one copy kernel for up to kStageMax arrays of whole u32 words; blits
+  // otherwise
+  bool kernel = n <= kStageMax;
+  for (size_t i = 0; i < n; ++i) kernel = kernel && ups[i].bytes % 4 == 0;
+  StageCopy c{};
+  size_t off = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (!ups[i].bytes) continue;
+    std::memcpy(g.h + off, ups[i].src, ups[i].bytes);
+    if (kernel) {
+      if (staged && fold) staged[i] = g.d + off;
+      c.src[c.n] = reinterpret_cast<const uint32_t*>(g.d + off);
+      c.dst[c.n] = static_cast<uint32_t*>(ups[i].dst);
+      c.words[c.n++] = static_cast<uint32_t>(ups[i].bytes / 4);
+    } else {
+      HIP_TRY(hipMemcpyAsync(ups[i].dst, g.h + off, ups[i].bytes, hipMemcpyHostToDevice, s), "upload");
+    }
+    off += (ups[i].bytes + 255) & ~size_t(255);
+  }
+  if (kernel && fold)
+    *fold = c;
+  else if (kernel)
+    HIP_TRY(launch_stage_copy(c, s), "stage copy");
+  return PS_OK;
+}
+
+// Debug (PSAMD_FLOOD_PROFILE=1): where k_flood's waves spent the last launch.
+void flood_profile_report(ps_engine* e) {
+  const uint32_t nw = e->flood_prof_waves;
+  std::vector<uint64_t> p(static_cast<size_t>(nw) * kFloodProf);
+  if (hipMemcpy(p.data(), e->d_flood_prof.p, p.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+  uint64_t t0 = ~0ull, t1 = 0, smax = 0;
+  double sum[kFloodProf] = {};
+  std::vector<double> ends;
+  for (uint32_t w = 0; w < nw; ++w) {
+    const uint64_t* q = &p[static_cast<size_t>(w) * kFloodProf];
+    t0 = std::min(t0, q[0]);
+    t1 = std::max(t1, q[1]);
+    smax = std::max(smax, q[0]);
+    for (uint32_t k = 2; k < kFloodProf; ++k) sum[k] += static_cast<double>(q[k]);
+    ends.push_back(static_cast<double>(q[1]));
+  }
+  std::sort(ends.begin(), ends.end());
+  auto us = [](double ticks) { return ticks / 100.0; };  // s_memrealtime: 100 MHz
+  const double busy = sum[2] + sum[3] + sum[4] + sum[5];
+  std::fprintf(stderr,
+               "[psengine] k_flood profile: %u waves, span %.1f us, start skew %.1f us, ends p50 %.1f p90 %.1f "
+               "max %.1f us; per wave avg: wait %.1f resolve %.1f stream %.1f publish %.1f us (%.0f%%/%.0f%%/%.0f%%/"
+               "%.0f%%), %.1f tasks; waits in the last third of the rounds %.1f us\n",
+               nw, us(static_cast<double>(t1 - t0)), us(static_cast<double>(smax - t0)),
+               us(ends[ends.size() / 2] - t0), us(ends[ends.size() * 9 / 10] - t0), us(ends.back() - t0),
+               us(sum[2] / nw), us(sum[3] / nw), us(sum[4] / nw), us(sum[5] / nw), 100 * sum[2] / busy,
+               100 * sum[3] / busy, 100 * sum[4] / busy, 100 * sum[5] / busy, sum[6] / nw, us(sum[7] / nw));
+}
+
+// Propagates one window: per topic t, win[t] lists the messages (indices into
+// `msgs`) whose bits form t's block of W_t = ceil(|win[t]|/64) words.
+int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<WinSlice>& win, ps_stats* st) {
+  const auto t_g0 = std::chrono::steady_clock::now();
+  int rc = upload_graph(e);
+  if (rc) return rc;
+  const uint32_t nt = static_cast<uint32_t>(e->topics.size());
+  const int32_t world = e->world, me = e->rank;
+  const auto t_w0 = std::chrono::steady_clock::now();
+  if (e->host_timing)
+    std::fprintf(stderr, "[psengine] graph upload/build %.3f ms (%s)\n",
+                 std::chrono::duration<double, std::milli>(t_w0 - t_g0).count(), e->gpu_graph ? "gpu" : "host");
+  WindowLayout L;
+  rc = plan_window_layout(e, msgs, win, L);
+  if (rc) return rc;
+  if (L.wtot == 0 && world == 1) return PS_OK;
+  auto& tab = L.tab;
+  auto& groups = L.groups;
+  const uint64_t wtot = L.wtot;
+  const uint32_t max_start = L.max_start, planned0 = L.planned0, round_cap = L.round_cap;
+  const bool level = L.level, any_mesh = L.any_mesh, need_direct = L.need_direct;
+  const auto t_w1 = std::chrono::steady_clock::now();
+  const bool record = (e->cfg.flags & PS_F_RECORD_HOPS) != 0;
+  HIP_TRY(e->d_seen.ensure(wtot * 8), "alloc seen");
+  HIP_TRY(e->d_arr0.ensure(wtot * 8), "alloc arrivals");
+  HIP_TRY(e->d_arr1.ensure(wtot * 8), "alloc arrivals");
+  if (record) HIP_TRY(e->d_hop.ensure(wtot * 64 * 2), "alloc hop record");
+  const uint32_t n_waves = e->expand_grid * (kBlock / 64);
+  // staged + direct kernel counters side by side
+  HIP_TRY(e->d_partials.ensure(static_cast<size_t>(2) * n_waves * kNumCtr * 8), "alloc partials");
+  // per-round counter rows: the planned rounds plus slack, grown (content kept)
+  // if a mesh path outlives them
+  uint32_t stats_rows = std::min<uint32_t>(round_cap, std::max<uint32_t>(kMaxRoundsCap, L.max_depth + max_start + 32));
+  HIP_TRY(e->d_stats.ensure(static_cast<size_t>(stats_rows + 1) * kNumCtr * 8), "alloc stats");
+  HIP_TRY(e->d_apply_stats.ensure(static_cast<size_t>(stats_rows + 1) * kNumCtr * 8), "alloc apply stats");
+  HIP_TRY(e->d_topics.ensure(tab.size() * sizeof(TopicDev)), "alloc topics");
+  HIP_TRY(e->d_nfront.ensure(4), "alloc n_front");
+  HIP_TRY(e->d_groups.ensure(std::max<size_t>(L.gtab.size(), 1) * sizeof(GroupDev)), "alloc groups");
+  // word offset of virtual word w of node u's row (u relative to the topic)
+  auto phys = [&](uint32_t t, uint64_t u, uint32_t w) { return phys_word(tab[t], groups[t], u, w); };
+
+  // root injections (owned roots only), grouped by round: mask[t][round][word]
+  std::vector<std::vector<uint64_t>> inj(nt);
+  for (uint32_t t = 0; t < nt; ++t) {
+    const TopicDev& d = tab[t];
+    if (d.W == 0 || !(d.flags & kTopicRootLocal)) continue;
+    inj[t].assign(static_cast<size_t>(max_start + 1) * d.W, 0);
+    if (e->run_zero_start) {  // bits 0 .. n-1 of round 0
+      for (uint32_t w = 0; w < win[t].n / 64; ++w) inj[t][w] = ~0ull;
+      if (win[t].n % 64) inj[t][win[t].n / 64] = (1ull << (win[t].n % 64)) - 1;
+    } else {
+      for (uint32_t li = 0; li < win[t].n; ++li) {
+        const uint32_t b = L.pos[t].empty() ? li : L.pos[t][li];
+        inj[t][static_cast<size_t>(msgs[win[t].idx[li]].start) * d.W + (b >> 6)] |= 1ull << (b & 63);
+      }
+    }
+  }
+  std::vector<SeedDev> seeds;
+  std::vector<uint32_t> seed_off(max_start + 2, 0);
+  for (uint32_t r = 0; r <= max_start; ++r) {
+    for (uint32_t t = 0; t < nt; ++t) {
+      TopicDev& d = tab[t];
+      if (r == 0) d.seed_lo = static_cast<uint32_t>(seeds.size());
+      if (inj[t].empty()) continue;
+      if (d.flags & kTopicGroups) {
+        // group-major: the root's block of the group starting this round is
+        // set whole (k_window_init zeroes block 0 only)
+        for (const StartGroup& g : groups[t])
+          if (g.start == r)
+            for (uint32_t w = g.w0; w < g.w0 + g.wn; ++w)
+              seeds.push_back(SeedDev{phys(t, 0, w), inj[t][static_cast<size_t>(r) * d.W + w], d.nbase, 1});
+      } else {
+        for (uint32_t w = 0; w < d.W; ++w) {
+          const uint64_t m = inj[t][static_cast<size_t>(r) * d.W + w];
+          if (m) seeds.push_back(SeedDev{d.wbase + w, m, d.nbase, 0});  // root = node 0
+        }
+      }
+      if (r == 0) d.seed_n = static_cast<uint32_t>(seeds.size()) - d.seed_lo;
+    }
+    seed_off[r + 1] = static_cast<uint32_t>(seeds.size());
+  }
+  HIP_TRY(e->d_seeds.ensure(seeds.size() * sizeof(SeedDev)), "alloc seeds");
+  const auto t_w2 = std::chrono::steady_clock::now();
+
+  // Start rounds present per topic.  A node at BFS level d receives a
+  // message started at round s in round s + d and is expanded in round
+  // s + d + 1: that bounds each round's frontier (grid size) and, for the
+  // multi-GPU compaction exchange, each round's cross-rank traffic exactly.
+  std::vector<std::vector<uint8_t>> starts_of(nt);
+  for (uint32_t t = 0; t < nt; ++t) {
+    if (win[t].n == 0 || !e->topics[t].exists) continue;
+    starts_of[t].assign(max_start + 1, 0);
+    if (e->run_zero_start)
+      starts_of[t][0] = 1;
+    else
+      for (uint32_t li = 0; li < win[t].n; ++li) starts_of[t][msgs[win[t].idx[li]].start] = 1;
+  }
+  auto round_grid = [&](uint32_t r) -> uint32_t {
+    if (any_mesh) return e->expand_grid;
+    uint64_t bound = 0;
+    for (uint32_t t = 0; t < nt; ++t) {
+      if (tab[t].W == 0) continue;
+      const auto& li = e->topics[t].level_internal;
+      for (uint32_t s0 = 0; s0 <= max_start; ++s0) {
+        if (!starts_of[t][s0] || r < 1 + s0) continue;
+        const uint32_t d = r - 1 - s0;
+        if (d < li.size()) bound += li[d];
+      }
+    }
+    const uint64_t blocks = (bound + 3) / 4;  // ~1 entry per wave at least
+    return static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>(e->expand_grid, blocks)));
+  };
+  // Level mode: one rank runs the leading rounds whose rows are small
+  // (latency bound) as ONE persistent k_flood launch, then k_pull_pair /
+  // k_pull launches (bandwidth bound); N ranks run k_pull_pair / k_pull with
+  // the ghost exchange between rounds.  PSAMD_FLOOD=0 selects per-round
+  // launches on one rank too.
+  const bool flood_ok = level && world == 1 && e->flood_on && !e->flood_broken && e->flood_grid > 0 &&
+                        e->n_nodes < 0x80000000u;  // k_flood marks node ids with bit 31
+  uint32_t flood_rounds = 0;    // rounds 1..flood_rounds: k_flood
+  std::vector<uint32_t> lgrid;  // per-round launches: blocks of every round (L and G parts together)
+  uint32_t n_slots = 0;         // level mode: partial counter slots of the window
+  if (level) {
+    bool changed = plan_pull_chunks(e, L);
+    if (flood_ok) {
+      flood_rounds = plan_flood_rounds(e, L);
+      if (flood_rounds) plan_flood_tasks(e, L, flood_rounds);
+    }
+    bool gch = false;
+    rc = plan_ghost(e, L, &gch);
+    if (rc) return rc;
+    changed |= gch;
+    changed |= plan_pair_chunks(e, L, flood_rounds);
+    if (world > 1 && changed) annotate_chunks(e, L);
+    e->round_kind = e->pair.kind;
+    if ((rc = upload_pull(e)) || (rc = upload_pair(e))) return rc;
+    if (flood_rounds && (rc = upload_flood(e))) return rc;
+    if (world > 1 && gch && (rc = upload_ghost(e))) return rc;
+    // desc[3q..]: round q's partial slots (first, end, stride) for the reduce
+    auto& desc = e->desc_host;
+    desc.assign(3 * (planned0 + 2), 0);
+    uint32_t slot = 0;
+    if (flood_rounds) {
+      desc[0] = 0;  // row 0: k_flood's timeout word (slot 0)
+      desc[1] = 1;
+      desc[2] = 1;
+      for (uint32_t q = 1; q <= flood_rounds; ++q) {
+        desc[3 * q] = e->flood.slot0[q];
+        desc[3 * q + 1] = e->flood.slot0[q] + e->flood.nslot[q];
+        desc[3 * q + 2] = e->flood.nslot[q] ? 1 : 0;
+      }
+      slot = e->flood.slots;
+    }
+    // the launches of round q own the slots [woff[q], woff[q+1]): one per
+    // block (pull) or wave (pair), at most kPullSlots; the L and G parts of
+    // a round share them (counters are added)
+    lgrid.assign(planned0 + 1, 0);
+    auto& woff = e->woff_host;
+    woff.assign(planned0 + 2, 0);
+    woff[flood_rounds + 1] = slot;
+    for (uint32_t q = flood_rounds + 1; q <= planned0; ++q) {
+      const bool pair = e->round_kind[q] == PS_K_PAIR;
+      lgrid[q] = pair ? e->pair.hi[q] - e->pair.lo[q]  // (one one-wave workgroup per chunk)
+                      : ceil_div(e->pull.gsplit[q] - e->pull.off[q], kBlock / 64) +
+                            ceil_div(e->pull.off[q + 1] - e->pull.gsplit[q], kBlock / 64);
+      for (uint32_t k = q; k <= q + (pair ? 1u : 0u); ++k) {  // a pair launch: the same slots for both rounds
+        woff[k + 1] = woff[k] + std::min<uint32_t>(lgrid[q], pair ? kPairSlots : kPullSlots);
+        desc[3 * k] = woff[k];
+        desc[3 * k + 1] = woff[k + 1];
+        desc[3 * k + 2] = 1;
+      }
+      if (pair) lgrid[++q] = 0;
+    }
+    n_slots = woff[planned0 + 1];
+    HIP_TRY(e->d_partials.ensure(static_cast<size_t>(std::max<uint32_t>(n_slots, 1)) * kNumCtr * 8),
+            "alloc level partials");
+    HIP_TRY(e->d_woff.ensure(desc.size() * 4), "alloc reduce descriptors");
+  }
+  // compaction mode on N ranks: cross-rank capacities (items = node words)
+  // per round: cap[r][from*world+to]
+  std::vector<std::vector<uint64_t>> cap;
+  if (world > 1 && !level) {
+    uint64_t max_send = 0, max_recv = 0;
+    cap.assign(planned0 + 1, std::vector<uint64_t>(static_cast<size_t>(world) * world, 0));
+    for (uint32_t t = 0; t < nt; ++t) {
+      const TopicHost& T = e->topics[t];
+      if (starts_of[t].empty()) continue;
+      const uint64_t Wt = L.wglob[t];
+      for (const auto& c : T.cross)
+        for (uint32_t s0 = 0; s0 <= max_start; ++s0) {
+          const uint32_t r = c.level + 1 + s0;
+          if (starts_of[t][s0] && r <= planned0) cap[r][c.from * world + c.to] += c.count * Wt;
+        }
+    }
+    for (uint32_t r = 1; r <= planned0; ++r) {
+      uint64_t sb = 0, rb = 0;
+      for (int32_t q = 0; q < world; ++q) {
+        if (cap[r][me * world + q]) sb += kRegionHeader + cap[r][me * world + q] * sizeof(XItem);
+        if (cap[r][q * world + me]) rb += kRegionHeader + cap[r][q * world + me] * sizeof(XItem);
+      }
+      max_send = std::max(max_send, sb);
+      max_recv = std::max(max_recv, rb);
+    }
+    HIP_TRY(e->d_send.ensure(max_send), "alloc send regions");
+    HIP_TRY(e->d_recv.ensure(max_recv), "alloc recv regions");
+  }
+
+  const bool flood = flood_rounds > 0;
+  const uint32_t mode = flood ? PS_MODE_FLOOD : level ? PS_MODE_LEVEL_PULL : PS_MODE_COMPACT;
+  const auto t_w3 = std::chrono::steady_clock::now();
+  hipStream_t s = e->stream;
+  // the window's first kernel also copies the staged uploads, applies the
+  // round-0 seeds of tree roots and clears the pull partial slots (level
+  // mode without meshes; the eager seen clear below would erase the seeds)
+  const bool fold = level && !any_mesh && !(e->cfg.flags & PS_F_NO_LAZY_SEEN);
+  WindowStart ws{};
+  const void* staged[4] = {nullptr, nullptr, nullptr, nullptr};
+  {
+    const Upload ups[4] = {{e->d_topics.p, tab.data(), tab.size() * sizeof(TopicDev)},
+                           {e->d_seeds.p, seeds.data(), seeds.size() * sizeof(SeedDev)},
+                           {e->d_woff.p, e->desc_host.data(), level ? e->desc_host.size() * 4 : 0},
+                           {e->d_groups.p, L.gtab.data(), L.gtab.size() * sizeof(GroupDev)}};
+    const int rcu = stage_uploads(e, ups, 4, s, fold ? &ws.copy : nullptr, staged);
+    if (rcu) return rcu;
+  }
+  if (fold) {
+    if (seed_off[1] > 0) ws.seeds = static_cast<const SeedDev*>(staged[1]);
+    ws.zero = e->d_partials.as<uint64_t>();
+    ws.zero_words = static_cast<uint64_t>(n_slots) * kNumCtr;
+  }
+  const bool seeds0_done = ws.seeds != nullptr;
+  const bool partials_done = ws.zero != nullptr;
+  HIP_TRY(hipEventRecord(e->ev_run0, s), "event");
+  const auto t_first = std::chrono::steady_clock::now();
+  // new window generation: every tree row from older windows becomes stale
+  if (++e->gen_cur > 255) {
+    HIP_TRY(hipMemsetAsync(e->d_gen.p, 0, e->d_gen.bytes, s), "clear generations");
+    e->gen_cur = 1;
+  }
+  HIP_TRY(launch_window_init(static_cast<const TopicDev*>(fold ? staged[0] : e->d_topics.p), nt,
+                             e->d_seen.as<uint64_t>(), e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>(),
+                             e->d_gen.as<uint8_t>(), e->gen_cur, any_mesh, ws, s),
+          "window init");
+  if (e->n_remote_fed && !level)
+    HIP_TRY(launch_init_nodes(e->d_remote_fed.as<uint32_t>(), e->n_remote_fed, e->d_node_topic.as<uint16_t>(),
+                              e->d_topics.as<TopicDev>(), e->d_seen.as<uint64_t>(), e->d_arr0.as<uint64_t>(),
+                              e->d_arr1.as<uint64_t>(), e->d_gen.as<uint8_t>(), e->gen_cur, !level, s),
+            "init remote-fed rows");
+  if (e->cfg.flags & PS_F_NO_LAZY_SEEN) {
+    // eager variant: clear every row and mark every node current, so the
+    // expand kernel reads each child's seen word before it tests and sets it
+    HIP_TRY(hipMemsetAsync(e->d_seen.p, 0, wtot * 8, s), "clear seen");
+    HIP_TRY(hipMemsetAsync(e->d_gen.p, static_cast<int>(e->gen_cur), e->d_gen.bytes, s), "stamp generations");
+  }
+  if (record) HIP_TRY(hipMemsetAsync(e->d_hop.p, 0xFF, wtot * 64 * 2, s), "clear hop record");
+  if (world > 1)  // (level mode: stays zero; the pull kernels count every delivery)
+    HIP_TRY(hipMemsetAsync(e->d_apply_stats.p, 0, static_cast<size_t>(planned0 + 1) * kNumCtr * 8, s),
+            "clear apply stats");
+
+  ExpandArgs a{};
+  bool host_stats_written = false;  // the reduce wrote the deferred slot's pinned rows
+  a.frontier = e->d_frontier.as<uint32_t>();
+  a.n_front = e->d_nfront.as<uint32_t>();
+  a.row_ptr = e->d_row_ptr.as<uint32_t>();
+  a.col = e->d_col.as<uint32_t>();
+  a.node_topic = e->d_node_topic.as<uint16_t>();
+  a.node_flags = e->d_node_flags.as<uint8_t>();
+  a.topics = e->d_topics.as<TopicDev>();
+  a.seen = e->d_seen.as<uint64_t>();
+  a.gen = e->d_gen.as<uint8_t>();
+  a.gen_cur = e->gen_cur;
+  a.next_flag = e->d_flags.as<uint8_t>();
+  a.blk_flag = e->d_blk.as<uint8_t>();
+  a.hop_rec = record ? e->d_hop.as<uint16_t>() : nullptr;
+  a.send = e->d_send.as<uint8_t>();
+  uint64_t* const partials = e->d_partials.as<uint64_t>();
+  uint64_t* arr[2] = {e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>()};
+  uint64_t* stats = e->d_stats.as<uint64_t>();
+  const bool timed = (e->cfg.flags & PS_F_TIME_KERNELS) != 0;
+
+  auto seed_round = [&](uint32_t r, uint64_t* into) -> hipError_t {
+    if (r > max_start) return hipSuccess;
+    return launch_seed(e->d_seeds.as<SeedDev>(), seed_off[r], seed_off[r + 1], into, a.seen,
+                       level ? nullptr : a.next_flag, level ? nullptr : a.blk_flag, s);
+  };
+  auto compact = [&](uint32_t r, uint32_t waves_r) -> hipError_t {
+    hipError_t x = launch_flag_count(a.next_flag, a.blk_flag, e->n_pad, e->d_wgcount.as<uint32_t>(), partials,
+                                     waves_r, r ? stats + r * kNumCtr : nullptr, s);
+    if (x != hipSuccess) return x;
+    return launch_flag_compact(a.next_flag, a.blk_flag, e->n_pad, e->d_wgcount.as<uint32_t>(),
+                               e->d_frontier.as<uint32_t>(), e->d_nfront.as<uint32_t>(), s);
+  };
+  // compaction mode on N ranks, round r: region layout, header reset, exchange, apply
+  std::vector<uint64_t> s_off(world, 0), s_len(world, 0), r_off(world, 0), r_len(world, 0);
+  auto layout = [&](uint32_t r) -> bool {
+    if (world <= 1 || r > planned0 || cap.empty()) return false;
+    uint64_t so = 0, ro = 0;
+    bool any = false;
+    for (int32_t q = 0; q < world; ++q) {
+      const uint64_t cs = cap[r][me * world + q], cr = cap[r][q * world + me];
+      s_off[q] = so;
+      s_len[q] = cs ? kRegionHeader + cs * sizeof(XItem) : 0;
+      so += s_len[q];
+      r_off[q] = ro;
+      r_len[q] = cr ? kRegionHeader + cr * sizeof(XItem) : 0;
+      ro += r_len[q];
+      for (int32_t z = 0; z < world; ++z) any |= cap[r][q * world + z] != 0;
+    }
+    for (int32_t q = 0; q < world && q < kMaxRanks; ++q) a.send_off[q] = s_off[q];
+    return any;  // the same verdict on every rank
+  };
+
+  uint32_t planned = planned0;
+  uint32_t r = 0;
+  size_t ev_used = 0;
+  std::vector<uint32_t> ev_round;  // round of every timed launch pair
+  uint32_t launches = 0;
+  auto time_mark = [&](bool begin) -> hipError_t {
+    if (!timed) return hipSuccess;
+    if (begin) ev_round.push_back(r);
+    if (begin && ev_used + 2 > e->ev_k.size()) {
+      hipEvent_t x, y;
+      hipError_t c = hipEventCreate(&x);
+      if (c == hipSuccess) c = hipEventCreate(&y);
+      if (c != hipSuccess) return c;
+      e->ev_k.push_back(x);
+      e->ev_k.push_back(y);
+    }
+    const hipError_t c = hipEventRecord(e->ev_k[ev_used + (begin ? 0 : 1)], s);
+    if (!begin) ev_used += 2;
+    return c;
+  };
+  // compaction mode: all-to-allv of this round's send regions, then the apply kernel
+  auto xchg = [&](uint32_t rr) -> int {
+    std::string xerr;
+    hipError_t xe = e->transport->exchange(a.send, s_off, s_len, e->d_recv.as<uint8_t>(), r_off, r_len, s, &xerr);
+    if (xe != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
+    ApplyArgs ap{};
+    ap.recv = e->d_recv.as<uint8_t>();
+    ap.world = static_cast<uint32_t>(world);
+    ap.cap_pre[0] = 0;
+    for (int32_t q = 0; q < world; ++q) {
+      ap.recv_off[q] = r_off[q];
+      ap.cap_pre[q + 1] = ap.cap_pre[q] + cap[rr][q * world + me];
+    }
+    ap.node_topic = a.node_topic;
+    ap.node_flags = a.node_flags;
+    ap.topics = a.topics;
+    ap.seen = a.seen;
+    ap.a_next = a.a_next;
+    ap.next_flag = level ? nullptr : a.next_flag;
+    ap.blk_flag = level ? nullptr : a.blk_flag;
+    ap.hop_rec = a.hop_rec;
+    ap.stats = e->d_apply_stats.as<uint64_t>() + static_cast<size_t>(rr) * kNumCtr;
+    ap.gen = level ? a.gen : nullptr;
+    ap.gen_cur = a.gen_cur;
+    HIP_TRY(launch_apply(ap, rr, record, s), "apply");
+    return PS_OK;
+  };
+  if (level) {
+    // static frontier, counters reduced once per window
+    if (!partials_done)  // blocks / waves add into shared partial slots
+      HIP_TRY(hipMemsetAsync(partials, 0, static_cast<size_t>(n_slots) * kNumCtr * 8, s), "clear partials");
+    if (!seeds0_done) HIP_TRY(seed_round(0, arr[0]), "seed");
+    // k_flood, start groups or pair launches: every root row is seeded up
+    // front into arr[0] (and seen: k_flood reads parent rows from there), the
+    // blocks of later start rounds included -- a block is read only in its
+    // own rounds
+    bool pairs = false;
+    for (uint32_t q = 1; q <= planned0; ++q) pairs |= e->round_kind[q] == PS_K_PAIR;
+    const bool upfront = flood || L.multi || pairs;  // (a pair launch's plain level-1 runs read roots)
+    if (upfront && max_start > 0)
+      HIP_TRY(launch_seed(e->d_seeds.as<SeedDev>(), seed_off[1], seed_off[max_start + 1], arr[0], a.seen, nullptr,
+                          nullptr, s),
+              "seed");
+    if (flood) {
+      FloodArgs fa{};
+      fa.tasks = e->d_flood_tasks.as<FloodTask>();
+      fa.segs = e->d_flood_segs.as<FloodSeg>();
+      fa.node_parent = e->d_node_parent.as<uint32_t>();
+      fa.node_flags = a.node_flags;
+      fa.topics = a.topics;
+      fa.seen = a.seen;
+      fa.gen = a.gen;
+      fa.hop_rec = a.hop_rec;
+      fa.granules = e->d_flood_gran.as<uint64_t>();
+      fa.partials = partials;
+      fa.err = reinterpret_cast<uint32_t*>(partials);  // slot 0, reduced into row 0
+      fa.n_tasks = static_cast<uint32_t>(e->flood.tasks.size());
+      if (++e->flood_epoch == 0) ++e->flood_epoch;  // granules of older launches carry older epochs
+      fa.epoch = e->flood_epoch;
+      fa.gen_cur = a.gen_cur;
+      fa.spin_ticks = e->flood_spin_ticks;
+      const uint32_t flood_blocks = std::min<uint32_t>(e->flood_grid, ceil_div(fa.n_tasks, kBlock / 64));
+      if (e->flood_profile) {
+        HIP_TRY(e->d_flood_prof.ensure(static_cast<size_t>(flood_blocks) * 4 * kFloodProf * 8), "alloc flood profile");
+        fa.prof = e->d_flood_prof.as<uint64_t>();
+        fa.prof_split = flood_rounds * 2 / 3;
+        e->flood_prof_waves = flood_blocks * 4;
+      }
+      r = 1;  // the per-round kernel times of a timed run go to round 1
+      HIP_TRY(time_mark(true), "event");
+      ++launches;
+      HIP_TRY(launch_flood(fa, flood_blocks, record, s), "flood");
+      HIP_TRY(time_mark(false), "event");
+    }
+    PullArgs pa{};
+    pa.node_parent = e->d_node_parent.as<uint32_t>();
+    pa.node_flags = a.node_flags;
+    pa.topics = a.topics;
+    pa.seen = a.seen;
+    pa.gen = a.gen;
+    pa.hop_rec = a.hop_rec;
+    pa.gen_cur = a.gen_cur;
+    pa.ghost_ref = world > 1 ? e->d_ghost_ref.as<uint32_t>() : nullptr;
+    pa.gsegs = e->d_gsegs.as<GhostSeg>();
+    pa.recv = e->d_recv.as<uint64_t>();
+    pa.ship = world > 1 ? e->d_ship.as<ShipEntry>() : nullptr;
+    pa.send = e->d_send.as<uint64_t>();
+    pa.all_current = (e->cfg.flags & PS_F_NO_LAZY_SEEN) ? 1u : 0u;
+    for (r = flood_rounds + 1; r <= planned0; ++r) {
+      const uint8_t kind = e->round_kind[r];
+      if (kind == PS_K_PAIR2) continue;  // written by the pair launch of round r - 1
+      a.a_cur = upfront ? arr[0] : arr[(r - 1) & 1];
+      a.a_next = arr[r & 1];
+      pa.a_cur = a.a_cur;
+      // N ranks: this round's records (rows the last round wrote; the
+      // seeded roots' packed now) go to the ranks owning their children on
+      // the exchange stream, while this round's locally fed chunks run; the
+      // ghost-fed chunks wait for the exchange
+      const bool xr = world > 1 && r < e->ghost.rounds.size() && e->ghost.rounds[r].any;
+      if (xr) {
+        const GhostRound& R = e->ghost.rounds[r];
+        if (R.pack1 > R.pack0)
+          HIP_TRY(launch_pack(e->d_ship.as<ShipEntry>(), e->d_pack.as<PackSeg>() + R.pack0, R.pack1 - R.pack0,
+                              R.pack_units, e->d_gsegs.as<GhostSeg>(), a.seen, e->d_send.as<uint64_t>(), s),
+                  "pack");
+        HIP_TRY(hipEventRecord(e->ev_round, s), "event");
+        HIP_TRY(hipStreamWaitEvent(e->xstream, e->ev_round, 0), "exchange wait");
+        std::string xerr;
+        const uint8_t* sb = e->d_send.as<uint8_t>() + (r & 1) * e->ghost.send_half * 8;
+        const hipError_t xe = e->transport->exchange(sb, R.s_off, R.s_len, e->d_recv.as<uint8_t>(), R.r_off,
+                                                     R.r_len, e->xstream, &xerr);
+        if (xe != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
+        HIP_TRY(hipEventRecord(e->ev_xchg, e->xstream), "event");
+      }
+      if (!lgrid[r] && !xr) continue;
+      const bool pair = kind == PS_K_PAIR;
+      // rows nobody re-reads while they can still sit in the 256 MB MALL
+      // (large rounds and the last round) store non-temporally
+      const uint32_t rw = pair ? r + 1 : r;  // the round whose rows the next launch reads
+      const bool nt = rw < e->pull.bytes.size() && (e->pull.bytes[rw] >= (64ull << 20) || rw == planned0);
+      pa.partials = partials + static_cast<size_t>(e->woff_host[r]) * kNumCtr;
+      pa.slot_mod = pair ? kPairSlots : kPullSlots;
+      if (pair) pa.partials2 = partials + static_cast<size_t>(e->woff_host[r + 1]) * kNumCtr;
+      // the locally fed part, then (after the exchange) the ghost-fed part
+      for (int part = 0; part < 2; ++part) {
+        if (part == 1 && xr) HIP_TRY(hipStreamWaitEvent(s, e->ev_xchg, 0), "exchange join");
+        uint32_t c0, c1;
+        if (pair) {
+          c0 = part ? e->pair.gsplit[r] : e->pair.lo[r];
+          c1 = part ? e->pair.hi[r] : e->pair.gsplit[r];
+        } else {
+          c0 = part ? e->pull.gsplit[r] : e->pull.off[r];
+          c1 = part ? e->pull.off[r + 1] : e->pull.gsplit[r];
+        }
+        if (c1 <= c0) continue;
+        HIP_TRY(time_mark(true), "event");
+        ++launches;
+        if (pair) {
+          HIP_TRY(launch_pull_pair(pa, e->d_pp.as<PullChunk>() + c0, c1 - c0, c1 - c0, r, record, nt, s),
+                  "pull pair");
+        } else {
+          // one rank: big rounds at 5 blocks per CU (+6 %); N ranks keep full
+          // residency (4 loopback ranks on one GPU: 6.49 -> 7.13 ms capped)
+          HIP_TRY(launch_pull(pa, e->d_pull.as<PullChunk>() + c0, c1 - c0, ceil_div(c1 - c0, kBlock / 64), r,
+                              record, nt, world == 1, s),
+                  "pull");
+        }
+        HIP_TRY(time_mark(false), "event");
+      }
+      if (!upfront) HIP_TRY(seed_round(r, a.a_next), "seed");
+    }
+    r = planned0;
+    // a deferred window's counters go straight into its pinned rows
+    const bool direct = e->defer_last && e->defer_into && !record && !timed && r <= PS_MAX_ROUNDS &&
+                        (world == 1 || planned0 <= PS_MAX_ROUNDS);
+    host_stats_written = direct;
+    HIP_TRY(launch_reduce_rounds(partials, e->d_woff.as<uint32_t>(), planned0, stats,
+                                 direct ? e->defer_into->hs_dev : nullptr, s),
+            "reduce rounds");
+  } else {
+    e->round_kind.clear();  // (accumulate_window: every round k_expand)
+    HIP_TRY(seed_round(0, arr[0]), "seed");
+    HIP_TRY(compact(0, 0), "compact");
+    while (true) {
+      for (; r < planned && r < round_cap;) {
+        ++r;
+        a.a_cur = arr[(r - 1) & 1];
+        a.a_next = arr[r & 1];
+        const bool xr = layout(r);
+        if (xr)
+          for (int32_t q = 0; q < world; ++q)
+            if (s_len[q]) HIP_TRY(hipMemsetAsync(a.send + s_off[q], 0, kRegionHeader, s), "reset header");
+        HIP_TRY(time_mark(true), "event");
+        ++launches;
+        const uint32_t grid_r = r <= planned0 ? round_grid(r) : e->expand_grid;
+        a.partials = partials;
+        HIP_TRY(launch_expand(a, r, record, grid_r, s), "expand");
+        uint32_t waves_r = grid_r * (kBlock / 64);
+        if (need_direct) {
+          a.partials = partials + static_cast<size_t>(waves_r) * kNumCtr;
+          HIP_TRY(launch_expand_direct(a, r, record, e->expand_grid, s), "expand direct");
+          waves_r += n_waves;
+        }
+        HIP_TRY(time_mark(false), "event");
+        if (xr) {
+          const int rc3 = xchg(r);
+          if (rc3) return rc3;
+        }
+        HIP_TRY(seed_round(r, a.a_next), "seed");
+        HIP_TRY(compact(r, waves_r), "compact");
+      }
+      uint32_t left = 0;
+      HIP_TRY(hipMemcpyAsync(&left, e->d_nfront.p, 4, hipMemcpyDeviceToHost, s), "read frontier");
+      HIP_TRY(hipStreamSynchronize(s), "sync");
+      if (left == 0 || r >= round_cap) {
+        if (left) return e->fail(PS_E_STATE, "propagation did not converge");
+        break;
+      }
+      if (world > 1) return e->fail(PS_E_STATE, "multi-GPU frontier outlived the planned rounds");
+      planned = r + 8;  // live mask lengthened a mesh path beyond the BFS depth
+      if (planned + 1 > stats_rows) {  // grow the round rows, keeping the counted ones
+        const uint32_t rows = std::min<uint32_t>(round_cap, std::max(planned + 1, 2 * stats_rows));
+        DevBuf grown;
+        HIP_TRY(grown.ensure(static_cast<size_t>(rows + 1) * kNumCtr * 8), "grow stats");
+        HIP_TRY(hipMemcpyAsync(grown.p, e->d_stats.p, static_cast<size_t>(stats_rows + 1) * kNumCtr * 8,
+                               hipMemcpyDeviceToDevice, s),
+                "keep stats");
+        HIP_TRY(hipStreamSynchronize(s), "sync");
+        std::swap(grown.p, e->d_stats.p);
+        std::swap(grown.bytes, e->d_stats.bytes);
+        stats = e->d_stats.as<uint64_t>();
+        stats_rows = rows;
+      }
+    }
+  }
+  const bool defer = e->defer_last && e->defer_into && !record && !timed && r <= PS_MAX_ROUNDS &&
+                     (world == 1 || planned0 <= PS_MAX_ROUNDS);  // the pinned slots hold PS_MAX_ROUNDS + 1 rows
+  if (!defer) HIP_TRY(hipEventRecord(e->ev_run1, s), "event");
+  const auto t_enq = std::chrono::steady_clock::now();
+  auto remember = [&]() {
+    // the last window, for ps_read_delivered / ps_read_peer_messages / ps_seen_digest
+    e->last_topics = tab;
+    for (uint32_t t = 0; t < nt; ++t) {
+      e->last_cnt[t] = tab[t].W ? win[t].n : 0;
+      e->last_lo[t] = win[t].n ? e->run_rank[win[t].idx[0]] : 0;
+    }
+    e->last_pos.swap(L.pos);
+    e->last_groups.swap(L.groups);
+    e->have_window = true;
+  };
+  if (defer) {
+    // asynchronous run: the counters follow the kernels on the stream into
+    // pinned memory (level mode: written there by the reduce itself); the
+    // window's end event marks their arrival; ps_wait accumulates them
+    ps_engine::Inflight& f = *e->defer_into;
+    if (!host_stats_written)
+      HIP_TRY(hipMemcpyAsync(f.hs, stats, static_cast<size_t>(r + 1) * kNumCtr * 8, hipMemcpyDeviceToHost, s),
+              "read stats");
+    if (world > 1)
+      HIP_TRY(hipMemcpyAsync(f.ha, e->d_apply_stats.p, static_cast<size_t>(planned0 + 1) * kNumCtr * 8,
+                             hipMemcpyDeviceToHost, s),
+              "read apply stats");
+    HIP_TRY(hipEventRecord(e->ev_run1, s), "event");
+    f.deferred = true;
+    f.planned0 = planned0;
+    f.world = world;
+    f.r = r;
+    f.launches = launches;
+    f.mode = mode;
+    f.flood_rounds = flood_rounds;
+    f.kinds = e->round_kind;
+    remember();
+    if (e->host_timing) {
+      auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+      std::fprintf(stderr, "[psengine] async window: plan %.3f ms (run->window %.3f, topics %.3f, seeds %.3f, "
+                   "schedule %.3f, uploads %.3f), enqueue %.3f ms\n",
+                   ms(e->t_run0, t_first), ms(e->t_run0, t_w0), ms(t_w0, t_w1), ms(t_w1, t_w2), ms(t_w2, t_w3),
+                   ms(t_w3, t_first), ms(t_first, t_enq));
+    }
+    return PS_OK;
+  }
+  HIP_TRY(hipEventSynchronize(e->ev_run1), "sync");
+  const auto t_sync = std::chrono::steady_clock::now();
+  const ps_stats keep = *st;  // a k_flood timeout re-runs the window from these stats
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, e->ev_run0, e->ev_run1), "elapsed");
+  st->run_ms += ms;
+  for (size_t i = 0; i < ev_used; i += 2) {
+    float k = 0.f;
+    HIP_TRY(hipEventElapsedTime(&k, e->ev_k[i], e->ev_k[i + 1]), "elapsed");
+    st->expand_ms += k;
+    const size_t q = ev_round[i / 2];  // round of this launch
+    if (q < PS_MAX_ROUNDS) st->expand_ms_per_round[q] += k;
+  }
+  std::vector<uint64_t> hs(static_cast<size_t>(r + 1) * kNumCtr), ha;
+  HIP_TRY(hipMemcpyAsync(hs.data(), stats, hs.size() * 8, hipMemcpyDeviceToHost, s), "read stats");
+  if (world > 1) {
+    ha.resize(static_cast<size_t>(planned0 + 1) * kNumCtr);
+    HIP_TRY(hipMemcpyAsync(ha.data(), e->d_apply_stats.p, ha.size() * 8, hipMemcpyDeviceToHost, s),
+            "read apply stats");
+  }
+  HIP_TRY(hipStreamSynchronize(s), "sync");
+  if (mode == PS_MODE_FLOOD && e->flood_profile && e->flood_prof_waves) flood_profile_report(e);
+  if (!accumulate_window(st, hs.data(), ha.data(), r, planned0, mode, flood_rounds, launches, world,
+                         e->round_kind)) {
+    // a k_flood dependency wait timed out (its waves were not all resident:
+    // another engine or process shares the GPU): this window's rows are
+    // incomplete.  Run the same window again with per-round launches under a
+    // fresh generation, and keep those from now on.
+    e->flood_broken = true;
+    *st = keep;
+    if (e->host_timing) std::fprintf(stderr, "[psengine] k_flood timed out: window re-run per round\n");
+    return run_window(e, msgs, win, st);
+  }
+  if (e->host_timing) {
+    auto ms2 = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
+    std::fprintf(stderr, "[psengine] window: plan %.3f ms (run->window %.3f, topics %.3f, seeds %.3f, "
+                 "schedule %.3f, uploads %.3f), enqueue %.3f ms, wait %.3f ms, tail %.3f ms\n",
+                 ms2(e->t_run0, t_first), ms2(e->t_run0, t_w0), ms2(t_w0, t_w1), ms2(t_w1, t_w2), ms2(t_w2, t_w3),
+                 ms2(t_w3, t_first), ms2(t_first, t_enq), ms2(t_enq, t_sync),
+                 ms2(t_sync, std::chrono::steady_clock::now()));
+  }
+  if (record) {
+    {
+      int rcm = ensure_mirrors(e);
+      if (rcm) return rcm;
+    }
+    std::vector<uint16_t> hr(wtot * 64);
+    if (!hr.empty()) {
+      HIP_TRY(hipMemcpyAsync(hr.data(), e->d_hop.p, hr.size() * 2, hipMemcpyDeviceToHost, s), "read hops");
+      HIP_TRY(hipStreamSynchronize(s), "sync");
+    }
+    const uint32_t np = e->cfg.n_peers;
+    for (uint32_t t = 0; t < nt; ++t) {
+      const TopicDev& d = tab[t];
+      if (d.W == 0) continue;
+      for (uint32_t li = 0; li < win[t].n; ++li) {
+        const uint32_t mi = win[t].idx[li];
+        const uint32_t s0 = msgs[mi].start;
+        const uint32_t b = L.pos[t].empty() ? li : L.pos[t][li];
+        uint8_t* row = e->hops.data() + static_cast<size_t>(mi) * np;
+        for (uint32_t u = 0; u < d.n_nodes; ++u) {
+          const uint16_t v = hr[phys(t, u, b >> 6) * 64 + (b & 63)];
+          // hop = round - start round, saturated at 254 (0xFF: not delivered)
+          if (v != kHopRecNone) row[e->node_peer[d.nbase + u]] = static_cast<uint8_t>(std::min<uint32_t>(v - s0, 254u));
+        }
+      }
+    }
+  }
+  remember();
+  return PS_OK;
+}
+
+// Messages of one phase (per topic, a slice of the run's topic-sorted index
+// array), split into windows of at most msg_window messages per topic.
+int run_phase(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<WinSlice>& per, ps_stats* st) {
+  const uint32_t nt = static_cast<uint32_t>(e->topics.size());
+  const uint32_t cap = e->cfg.msg_window;
+  uint32_t n_win = 0;
+  for (const auto& v : per) n_win = std::max(n_win, (v.n + cap - 1) / cap);
+  std::vector<WinSlice> win(nt);
+  for (uint32_t k = 0; k < n_win; ++k) {
+    for (uint32_t t = 0; t < nt; ++t) {
+      const uint32_t lo = k * cap;
+      win[t].idx = per[t].idx + std::min(lo, per[t].n);
+      win[t].n = lo < per[t].n ? std::min(cap, per[t].n - lo) : 0;
+    }
+    e->defer_last = e->defer_phase && k + 1 == n_win;
+    int rc = run_window(e, msgs, win, st);
+    e->defer_last = false;
+    if (rc) return rc;
+  }
+  return PS_OK;
+}
+
+}  // namespace
+
+// Counters of one window (rows r x kNumCtr, apply rows for multi-GPU) into
+// the run's stats.  Returns false when a k_flood dependency wait timed out
+// (its timeout word is folded into row 0).
+bool accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uint32_t r, uint32_t planned0,
+                       uint32_t mode, uint32_t flood_rounds, uint32_t launches, int32_t world,
+                       const std::vector<uint8_t>& kinds) {
+  const bool pull = mode == PS_MODE_LEVEL_PULL || mode == PS_MODE_FLOOD;
+  std::memset(st->round_kernel, 0, sizeof(st->round_kernel));
+  for (uint32_t q = 1; q <= r; ++q) {
+    const uint8_t kind = q < kinds.size() ? kinds[q] : static_cast<uint8_t>(pull ? PS_K_PULL : PS_K_EXPAND);
+    const uint64_t* c = &hs[static_cast<size_t>(q) * kNumCtr];
+    const uint64_t app_d = (world > 1 && q <= planned0) ? ha[static_cast<size_t>(q) * kNumCtr + kCtrDeliveries] : 0;
+    const uint64_t app_u = (world > 1 && q <= planned0) ? ha[static_cast<size_t>(q) * kNumCtr + kCtrDuplicates] : 0;
+    st->deliveries += c[kCtrDeliveries] + app_d;
+    st->duplicates += c[kCtrDuplicates] + app_u;
+    st->frontier_entries += c[kCtrEntries];
+    st->child_visits += c[kCtrChildren];
+    st->edge_words += c[kCtrSeenWrites];
+    // algorithmic bytes of the expand kernel (DESIGN.md §5.1 byte model):
+    // per entry frontier id 4 + topic 2 + row_ptr pair 8 + first child 4;
+    // per entry word the arrival read 8 (+ 8 when cleared); per child its
+    // flag byte + generation read/write (tree) or col id 4 (mesh); per
+    // seen read / seen write / arrival write 8.
+    uint64_t b;
+    if (pull)  // pull model: per node parent id 4 + flag 1 + parent generation 1 (k_flood:
+               // + its own generation 1, the seen test; the second round of a k_pull_pair
+               // launch: no parent generation, its parents' reach and rows are in LDS),
+               // per reached node its generation write 1; parent rows read once (from
+               // HBM: none in a pair's second round); rows written
+      b = c[kCtrChildren] * (kind == PS_K_FLOOD ? 7 : kind == PS_K_PAIR2 ? 5 : 6) + c[kCtrMeshChildren] * 1 +
+          c[kCtrEntryWords] * 8 + c[kCtrSeenWrites] * 8;
+    else
+      b = c[kCtrEntries] * 18 + c[kCtrEntryWords] * 8 + c[kCtrClearWords] * 8 + c[kCtrChildren] * 3 +
+          c[kCtrMeshChildren] * 4 + c[kCtrSeenReads] * 8 + c[kCtrSeenWrites] * 8 + c[kCtrArrivalWrites] * 8;
+    st->expand_bytes += b;
+    if (q < PS_MAX_ROUNDS) {
+      st->round_kernel[q] = kind;
+      st->expand_bytes_per_round[q] += b;
+      st->deliveries_per_round[q] += c[kCtrDeliveries] + app_d;
+      st->frontier_per_round[q] += static_cast<uint32_t>(c[kCtrEntries]);
+    }
+  }
+  st->rounds += r;
+  st->expand_launches += launches;
+  st->expand_mode = mode;
+  st->flood_rounds = flood_rounds;
+  st->windows += 1;
+  return mode != PS_MODE_FLOOD || hs[kCtrDeliveries] == 0;
+}
+
+// ps_run's body.  may_defer: the last window of the final phase may leave its
+// counters on the stream (ps_run_async); *stp is completed by ps_wait then.
+int run_body(ps_engine* e, ps_stats* stp, bool may_defer) {
+  const auto t_host0 = std::chrono::steady_clock::now();
+  e->t_run0 = t_host0;
+  ps_stats& st = *stp;
+  if (hipSetDevice(e->cfg.device) != hipSuccess) return e->fail(PS_E_DEVICE, "hipSetDevice");
+  e->last_msgs.clear();
+  e->last_msgs.swap(e->pending);
+  e->run_zero_start = !e->pending_nonzero_start;
+  e->pending_nonzero_start = false;
+  const std::vector<RunMsg>& msgs = e->last_msgs;
+  const uint32_t nmsg = static_cast<uint32_t>(msgs.size());
+  e->last_first = e->next_msg - nmsg;
+  e->last_n = nmsg;
+  e->have_hops = false;
+  e->have_window = false;
+  const bool record = (e->cfg.flags & PS_F_RECORD_HOPS) != 0;
+  if (record) {
+    const uint64_t bytes = static_cast<uint64_t>(nmsg) * e->cfg.n_peers;
+    if (bytes > (8ull << 30)) return e->fail(PS_E_NOMEM, "hop record larger than 8 GiB");
+    e->hops.assign(bytes, PS_HOP_NONE);
+  }
+  const uint32_t nt = static_cast<uint32_t>(e->topics.size());
+  // one counting sort: message indices grouped by topic, publish order kept
+  auto& off = e->run_topic_off;
+  off.assign(nt + 1, 0);
+  for (uint32_t i = 0; i < nmsg; ++i) off[msgs[i].topic + 1]++;
+  for (uint32_t t = 0; t < nt; ++t) off[t + 1] += off[t];
+  e->run_sorted.resize(nmsg);
+  e->run_rank.resize(nmsg);
+  {
+    std::vector<uint32_t> fill(off.begin(), off.end() - 1);
+    for (uint32_t i = 0; i < nmsg; ++i) {
+      const uint32_t t = msgs[i].topic;
+      e->run_rank[i] = fill[t] - off[t];
+      e->run_sorted[fill[t]++] = i;
+    }
+  }
+  e->last_lo.assign(nt, 0);
+  e->last_cnt.assign(nt, 0);
+  std::vector<uint32_t> head(nt, 0);
+  auto slice = [&](uint32_t t, uint32_t from, uint32_t n) {
+    WinSlice w;
+    w.idx = e->run_sorted.data() + off[t] + from;
+    w.n = n;
+    return w;
+  };
+  // Abruptly dropped hosts: the first message through the failed edge is lost
+  // below it, then the parent repairs (subtree.go:333-351): that message runs
+  // on its own over the current tree, the rest over the repaired one.
+  while (true) {
+    std::vector<WinSlice> solo(nt);
+    bool any = false;
+    for (uint32_t t = 0; t < nt; ++t) {
+      TopicHost& T = e->topics[t];
+      const uint32_t cnt = off[t + 1] - off[t];
+      if (T.exists && T.kind == Kind::Join && T.tree.has_pending_failures() && head[t] < cnt) {
+        solo[t] = slice(t, head[t], 1);
+        head[t]++;
+        any = true;
+      }
+    }
+    if (!any) break;
+    int rc = run_phase(e, msgs, solo, &st);
+    if (rc) return rc;
+    for (uint32_t t = 0; t < nt; ++t)
+      if (solo[t].n) {
+        e->topics[t].tree.after_message();
+        e->graph_dirty = true;
+      }
+  }
+  {
+    std::vector<WinSlice> rest(nt);
+    bool any = false;
+    for (uint32_t t = 0; t < nt; ++t) {
+      const uint32_t cnt = off[t + 1] - off[t];
+      rest[t] = slice(t, head[t], cnt - head[t]);
+      any |= rest[t].n > 0;
+    }
+    if (any) {
+      e->defer_phase = may_defer && !record;
+      int rc = run_phase(e, msgs, rest, &st);
+      e->defer_phase = false;
+      if (rc) return rc;
+    }
+  }
+  // lazy prune of Part'ed children at every forwarding node (subtree.go:326-331)
+  const auto t_am = std::chrono::steady_clock::now();
+  const bool gpu_reach = e->gpu_graph && !e->graph_dirty;  // the node space the messages ran on
+  for (uint32_t t = 0; t < nt; ++t) {
+    TopicHost& T = e->topics[t];
+    if (T.exists && T.kind == Kind::Join && head[t] < off[t + 1] - off[t] && T.tree.needs_message_pass()) {
+      // on a GPU-built node space the message's reach is a lookup there (a
+      // host walk to the root per Part'ed parent costs ~0.2 us each)
+      SubscriptionTree::ReachQuery q = [e, &T](const std::vector<uint32_t>& peers, std::vector<uint8_t>& outv) -> int {
+        const uint32_t k = static_cast<uint32_t>(peers.size());
+        if (!k) return PS_OK;
+        HIP_TRY(e->d_pairs.ensure(static_cast<size_t>(k) * 4 + k + 16), "alloc reach query");
+        uint32_t* dp = e->d_pairs.as<uint32_t>();
+        uint8_t* dout = reinterpret_cast<uint8_t*>(dp + k);
+        HIP_TRY(hipMemcpyAsync(dp, peers.data(), static_cast<size_t>(k) * 4, hipMemcpyHostToDevice, e->stream),
+                "upload reach query");
+        HIP_TRY(launch_reach_query(dp, k, e->cfg.n_peers, e->d_local.as<uint32_t>(), e->d_node_peer.as<uint32_t>(),
+                                   T.nbase, T.n_nodes, dout, e->stream),
+                "reach query");
+        HIP_TRY(hipMemcpyAsync(outv.data(), dout, k, hipMemcpyDeviceToHost, e->stream), "read reach query");
+        HIP_TRY(hipStreamSynchronize(e->stream), "sync");
+        if (e->host_timing)
+          std::fprintf(stderr, "[psengine] prune reach query: %u parents, done at %.3f ms\n", k,
+                       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - e->t_run0).count());
+        return PS_OK;
+      };
+      int rc = T.tree.after_message(gpu_reach ? &q : nullptr);
+      if (rc) return rc;
+      e->graph_dirty = true;
+    }
+  }
+  e->have_hops = record;
+  if (e->host_timing)
+    std::fprintf(stderr, "[psengine] after-message prune %.3f ms (started at %.3f ms)\n",
+                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_am).count(),
+                 std::chrono::duration<double, std::milli>(t_am - e->t_run0).count());
+  st.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_host0).count();
+  return PS_OK;
+}
+
+}  // namespace psamd
+
+using namespace psamd;
+
+extern "C" {
+
+int ps_run(ps_engine* e, ps_stats* out) {
+  if (!e) return PS_E_INVAL;
+  if (e->host_only) return e->fail(PS_E_STATE, "planner probe: no device");
+  if (e->infl_count) return e->fail(PS_E_STATE, "asynchronous runs pending: ps_wait first");
+  ps_stats st{};
+  const int rc = run_body(e, &st, false);
+  if (rc) return rc;
+  if (out) *out = st;
+  return PS_OK;
+}
+
+int ps_run_async(ps_engine* e) {
+  if (!e) return PS_E_INVAL;
+  if (e->host_only) return e->fail(PS_E_STATE, "planner probe: no device");
+  if (e->infl_count >= 2) return e->fail(PS_E_STATE, "two runs in flight: ps_wait first");
+  ps_engine::Inflight& f = e->infl[(e->infl_head + e->infl_count) % 2];
+  f.st = ps_stats{};
+  f.deferred = false;
+  hipEvent_t ev0 = e->ev_run0, ev1 = e->ev_run1;
+  e->ev_run0 = f.ev0;  // this run's window events belong to its slot
+  e->ev_run1 = f.ev1;
+  e->defer_into = &f;
+  const int rc = run_body(e, &f.st, true);
+  e->ev_run0 = ev0;
+  e->ev_run1 = ev1;
+  e->defer_into = nullptr;
+  if (rc) {
+    (void)hipStreamSynchronize(e->stream);
+    return rc;
+  }
+  ++e->infl_count;
+  return PS_OK;
+}
+
+int ps_wait(ps_engine* e, ps_stats* out) {
+  if (!e) return PS_E_INVAL;
+  if (!e->infl_count) return e->fail(PS_E_NOTREADY, "no asynchronous run pending");
+  ps_engine::Inflight& f = e->infl[e->infl_head];
+  e->infl_head = (e->infl_head + 1) % 2;
+  --e->infl_count;
+  if (f.deferred) {
+    HIP_TRY(hipEventSynchronize(f.ev1), "sync");
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, f.ev0, f.ev1), "elapsed");
+    f.st.run_ms += ms;
+    f.deferred = false;
+    if (!accumulate_window(&f.st, f.hs, f.ha, f.r, f.planned0, f.mode, f.flood_rounds, f.launches, f.world,
+                           f.kinds)) {
+      e->flood_broken = true;
+      return e->fail(PS_E_DEVICE, "k_flood: a dependency wait timed out (waves not co-resident?); "
+                                  "per-round launches from now on");
+    }
+  }
+  if (out) *out = f.st;
+  return PS_OK;
+}
+
+}  // extern "C"

@@ -12,8 +12,9 @@ LIB = os.path.join(LIBDIR, "libpsengine.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["kernels.hip", "flood.hip", "gbuild.hip", "engine.cpp", "tree.cpp", "dist.cpp", "codec.cpp", "pubsub.cpp"]
-HEADERS = ["kernels.hpp", "devutil.hpp", "gbuild.hpp", "tree.hpp", "dist.hpp"]
+SOURCES = ["kernels.hip", "flood.hip", "gbuild.hip", "graph.cpp", "plan.cpp", "run.cpp", "api.cpp", "tree.cpp",
+           "dist.cpp", "codec.cpp", "pubsub.cpp"]
+HEADERS = ["kernels.hpp", "devutil.hpp", "gbuild.hpp", "tree.hpp", "dist.hpp", "engine.hpp"]
 
 
 def _stale() -> bool:
@@ -23,6 +24,7 @@ def _stale() -> bool:
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     deps.append(os.path.join(REPO, "include", "psengine.h"))
     deps.append(os.path.join(REPO, "include", "pubsub.hpp"))
+    deps.append(os.path.join(REPO, "include", "psengine_plan.h"))
     return any(os.path.getmtime(d) > t for d in deps)
 
 

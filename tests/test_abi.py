@@ -14,8 +14,11 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "psengine.h")
 
 
-def declared():
-    src = open(HEADER).read()
+PLAN_HEADER = os.path.join(REPO, "include", "psengine_plan.h")
+
+
+def declared(header=HEADER):
+    src = open(header).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(ps_[a-z_0-9]+)\s*\(", src)))
 
@@ -38,6 +41,20 @@ def test_header_symbols_exported(lib):
     assert not missing, missing
     bound = {p[0] for p in PE.PROTOTYPES}
     assert set(names) == bound, set(names) ^ bound
+
+
+def test_plan_probe_symbols_exported(lib):
+    """The host-only planner probe (include/psengine_plan.h, tests only) is
+    exported and bound by psengine.plan."""
+    from psengine import plan as PL
+
+    names = declared(PLAN_HEADER)
+    assert names == sorted(p[0] for p in PL.PROTOTYPES)
+    out = subprocess.run(["nm", "-D", "--defined-only", PE.lib_path()], capture_output=True,
+                         text=True, check=True).stdout
+    exported = set(re.findall(r" T (ps_\w+)", out))
+    assert not [n for n in names if n not in exported]
+    PL.lib()
 
 
 def test_code_object_is_gfx950(lib):

@@ -1,0 +1,165 @@
+"""GPU: BASELINE cfg2 and cfg4 at FULL size against the restatement with a
+dead mask -- the single-rank production instance, and cfg4 (16,777,216 peers)
+hash-sharded over two loopback ranks under PS_PART_PEER.
+
+A dead peer stops forwarding (subtree.go:324-337, the dead-child skip at
+:326-331), so its subtree is cut: ~2 % dead peers, including a child of the
+root and a grandchild, cut real subtrees out of the top levels.  Checked:
+
+* the exact deliveries and the per-round histogram of or_disseminate
+  (oracle/psoracle.c) times the message count -- every message of a
+  single-start burst reaches the same peers at the same hops;
+* the delivered peer sets of 16 sampled messages (ps_read_delivered, the
+  union over ranks);
+* the seen-state digest: the ranks' digests add up to the single engine's.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle as O
+import psengine as PE
+from psengine import workloads as WL
+
+pytestmark = pytest.mark.gpu
+
+
+def dead_mask(parent, root, n, frac=0.02, seed=17):
+    rng = np.random.default_rng(seed)
+    live = (rng.random(n) > frac).astype(np.uint8)
+    kids = np.nonzero(parent == root)[0]
+    live[kids[0]] = 0  # a child of the root: a whole top subtree is cut
+    grand = np.nonzero(parent == kids[-1])[0]
+    live[grand[0]] = 0
+    live[kids[-1]] = 1
+    live[root] = 1
+    return live
+
+
+def oracle_reach(parent, root, live):
+    rp, cl = O.parents_to_csr(parent)
+    tot, oh, hist = O.disseminate(rp, cl, root, live, 1, hist_len=64)
+    return tot, oh[0] != 0xFF, hist.astype(np.int64)
+
+
+def check_run(stats, n_msgs, tot, hist):
+    assert sum(s.deliveries for s in stats) == tot * n_msgs
+    assert sum(s.duplicates for s in stats) == 0
+    per = np.zeros(PE.MAX_ROUNDS, dtype=np.int64)
+    for s in stats:
+        per += np.array(list(s.deliveries_per_round), dtype=np.int64)
+    assert per[1:64].tolist() == (hist[1:64] * n_msgs).tolist()
+    assert int(per[64:].sum()) == 0
+
+
+def sampled(n_msgs, k=16, seed=5):
+    return np.random.default_rng(seed).choice(n_msgs, size=min(k, n_msgs), replace=False)
+
+
+@pytest.fixture(scope="module")
+def cfg4_tree():
+    """cfg4's tree (TreeOpts{8,20}, the restated joins of 16M - 1 peers in
+    order) and its dead mask, built once for the module."""
+    wl = WL.cfg4()
+    with PE.Engine(wl.n_peers, 1, seed=wl.seed) as eng:
+        WL.build_engine_topics(eng, wl)
+        parent = eng.parents(0)
+    live = dead_mask(parent, 0, wl.n_peers)
+    tot, reach, hist = oracle_reach(parent, 0, live)
+    assert reach.sum() < wl.n_peers - 1 - 0.02 * wl.n_peers  # subtrees were cut
+    return wl, parent, live, tot, reach, hist
+
+
+def test_cfg2_full_size_dead_mask_against_oracle():
+    """cfg2 (100k peers, TreeOpts{8,20}, 10k burst) on the production
+    instance: k_flood + k_pull_pair / k_pull at fan-out 8-20 with dead peers."""
+    wl = WL.cfg2()
+    with PE.Engine(wl.n_peers, 1, seed=wl.seed) as eng:
+        WL.build_engine_topics(eng, wl)
+        parent = eng.parents(0)
+        live = dead_mask(parent, 0, wl.n_peers)
+        tot, reach, hist = oracle_reach(parent, 0, live)
+        eng.set_live(live)
+        first = eng.publish(wl.msg_topics)
+        st = eng.run()
+        assert st.expand_mode == PE.MODE_FLOOD
+        check_run([st], wl.n_msgs, tot, hist)
+        for m in sampled(wl.n_msgs):
+            assert np.array_equal(eng.delivered(first + int(m)).astype(bool), reach), int(m)
+
+
+def test_cfg4_full_size_dead_mask_single_rank(cfg4_tree):
+    """cfg4 at full size on one rank, production instance, dead mask."""
+    wl, parent, live, tot, reach, hist = cfg4_tree
+    with PE.Engine(wl.n_peers, 1, seed=wl.seed) as eng:
+        eng.set_tree(0, 0, parent)
+        eng.set_live(live)
+        first = eng.publish(wl.msg_topics)
+        st = eng.run()
+        assert st.expand_mode == PE.MODE_FLOOD
+        assert PE.K_PAIR in list(st.round_kernel)  # the pair launches ran
+        check_run([st], wl.n_msgs, tot, hist)
+        for m in sampled(wl.n_msgs):
+            assert np.array_equal(eng.delivered(first + int(m)).astype(bool), reach), int(m)
+        cfg4_tree_digest[0] = eng.seen_digest()
+
+
+cfg4_tree_digest = [None]
+
+
+def test_cfg4_full_size_two_ranks_peer_hash(cfg4_tree):
+    """cfg4 at full size hash-sharded over 2 loopback ranks (owner(p) =
+    splitmix64(p) mod 2): every round ships ghost parent rows;
+    deliveries, histogram, sampled delivered sets (union over the ranks) and
+    the digest sum against the oracle and the single engine."""
+    wl, parent, live, tot, reach, hist = cfg4_tree
+    world = 2
+    lb = PE.Loopback(world)
+    engines = [PE.Engine(wl.n_peers, 1, seed=wl.seed) for _ in range(world)]
+    try:
+        for r, e in enumerate(engines):
+            e.dist_init_loopback(lb, r, PE.PART_PEER)
+            e.set_tree(0, 0, parent)
+            e.set_live(live)
+        firsts = [e.publish(wl.msg_topics) for e in engines]
+        stats = [None] * world
+        errs = []
+
+        def go(r):
+            try:
+                stats[r] = engines[r].run()
+            except Exception as ex:  # noqa: BLE001
+                errs.append((r, ex))
+
+        th = [threading.Thread(target=go, args=(r,)) for r in range(world)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=200)
+        assert not any(t.is_alive() for t in th), "rank thread hung"
+        assert not errs, errs
+        assert all(s.expand_mode == PE.MODE_LEVEL_PULL for s in stats)
+        check_run(stats, wl.n_msgs, tot, hist)
+        own = PE.partition_owner(parent, 0, 0, world, PE.PART_PEER)
+        assert 0.45 < float((own == 0).sum()) / float((own >= 0).sum()) < 0.55
+        for m in sampled(wl.n_msgs, seed=9):
+            got = np.zeros(wl.n_peers, dtype=bool)
+            for r, e in enumerate(engines):
+                d = e.delivered(firsts[r] + int(m)).astype(bool)
+                assert not (d & (own != r)).any()  # a rank reports its own nodes only
+                got |= d
+            assert np.array_equal(got, reach), int(m)
+        digest = sum(e.seen_digest() for e in engines) % (1 << 64)
+        if cfg4_tree_digest[0] is None:
+            with PE.Engine(wl.n_peers, 1, seed=wl.seed) as one:
+                one.set_tree(0, 0, parent)
+                one.set_live(live)
+                one.publish(wl.msg_topics)
+                one.run()
+                cfg4_tree_digest[0] = one.seen_digest()
+        assert digest == cfg4_tree_digest[0]
+    finally:
+        for e in engines:
+            e.close()
+        lb.close()

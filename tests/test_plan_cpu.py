@@ -1,0 +1,407 @@
+"""CPU tests of the engine's launch planners through the host-only probe
+(include/psengine_plan.h): the C++ planners build every rank's node space and
+window plan exactly as ps_run does, and a Python emulator replays the level
+mode from those tables alone -- chunks, round pairs, ghost records shipped by
+the chunks that write the parents, root records packed, the per-round
+all-to-allv regions, records read back by the ghost-fed nodes -- with the row
+blocks as data.  The union of the ranks' deliveries must equal the CPU
+restatement (oracle/psoracle.c), every node of every start group must be
+written exactly once, and every reached node's block must equal its root's
+(subtree.go:319-354, client.go:100-132).
+
+The 2-rank case also runs in two gloo processes, the regions exchanged with
+all_gather_object: the ghost layout tested on the CPU against a real
+process boundary."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle as O
+import psengine as PE
+from psengine import plan as PL
+
+MASK = (1 << 27) - 1
+NONE = 0xFFFFFFFF
+K_GROUPS = 8  # kTopicGroups
+
+
+def random_tree(rng, n, root, fan=None):
+    perm = rng.permutation(n)
+    perm = np.concatenate([[root], perm[perm != root]])
+    parent = np.full(n, O.NONE, dtype=np.uint32)
+    kids = np.zeros(n, dtype=np.int64)
+    for i in range(1, n):
+        while True:
+            p = perm[rng.integers(max(0, i - 40), i)] if fan else perm[rng.integers(0, i)]
+            if not fan or kids[p] < fan:
+                break
+        parent[perm[i]] = p
+        kids[p] += 1
+    return parent
+
+
+def root_block(t, gi, wn):
+    r = np.random.default_rng(1000 * t + gi)
+    b = r.integers(1, 1 << 63, size=wn, dtype=np.uint64)
+    return b  # first word non-zero, as a group's first message bit is
+
+
+class RankSim:
+    """One rank of the level mode, driven by its plan tables only."""
+
+    def __init__(self, plan: PL.Plan, live):
+        self.p = plan
+        self.info = plan.info()
+        assert self.info["level"] == 1
+        self.peer = plan.get(PL.NODES).astype(np.int64)
+        self.parent = plan.get(PL.PARENT).astype(np.int64)
+        self.gref = plan.get(PL.GHOST_REF).astype(np.int64)
+        self.kind = plan.get(PL.ROUND_KIND).astype(np.int64)
+        self.topics = [plan.topic(t) for t in range(plan.n_topics)]
+        self.lay = [plan.layout(t) for t in range(plan.n_topics)]
+        self.segs = plan.segs() if plan.world > 1 else []
+        self.shipv = plan.ship() if plan.world > 1 else np.zeros((0, 2), np.int64)
+        self.live = live
+        wtot = 0
+        for T, Ly in zip(self.topics, self.lay):
+            wtot = max(wtot, Ly["wbase"] + T["n_nodes"] * Ly["W"])
+        self.rows = np.zeros(wtot + 16, dtype=np.uint64)
+        self.reached = np.zeros(self.info["nodes"], dtype=bool)
+        self.writes = {}  # (node, group) -> times written
+        self.send = np.zeros(2 * self.info["send_half"] + 16, dtype=np.uint64)
+        self.recv = np.zeros(self.info["recv_words"] + 16, dtype=np.uint64)
+        self.node_topic = np.zeros(self.info["nodes"], dtype=np.int64)
+        self.level = np.zeros(self.info["nodes"], dtype=np.int64)
+        for t, T in enumerate(self.topics):
+            self.node_topic[T["nbase"]:T["nbase"] + T["n_nodes"]] = t
+            lo = T["level_off"]
+            for d in range(T["depth"] + 1):
+                self.level[T["nbase"] + lo[d]:T["nbase"] + lo[d + 1]] = d
+        # seeds: every owned root's blocks
+        for t, (T, Ly) in enumerate(zip(self.topics, self.lay)):
+            if T["root_local"] and T["n_nodes"] and Ly["W"]:
+                self.reached[T["nbase"]] = True
+                for gi, (_, w0, wn) in enumerate(Ly["groups"]):
+                    r0 = self.block_row0(t, gi)
+                    self.rows[r0:r0 + wn] = root_block(t, gi, wn)
+
+    def block_row0(self, t, gi):
+        Ly, T = self.lay[t], self.topics[t]
+        _, w0, wn = Ly["groups"][gi]
+        return Ly["wbase"] + (T["n_nodes"] * w0 if Ly["flags"] & K_GROUPS else 0)
+
+    def row(self, c, u):
+        nbase = self.topics[c["topic"]]["nbase"]
+        a = c["row0"] + (u - nbase) * c["W"]
+        return a, a + c["W"]
+
+    def pack(self, q):
+        for ps in self.p.pack(q):
+            seg = self.segs[ps["gseg"]]
+            for e in range(ps["e0"], ps["e1"]):
+                _, dst = self.shipv[e]
+                b, k = dst >> 27, dst & MASK
+                a = seg["sbase"][b] + k * ps["W"]
+                self.send[a:a + ps["W"]] = self.rows[ps["row"]:ps["row"] + ps["W"]]
+
+    def regions_out(self, q):
+        """{dest rank: words} of round q's send regions."""
+        x = self.p.xchg(q)
+        if not x["any"]:
+            return {}
+        half = (q & 1) * self.info["send_half"]
+        out = {}
+        for b in range(self.p.world):
+            if b != self.p.rank:
+                s0 = half + x["s_off"][b] // 8
+                out[b] = self.send[s0:s0 + x["s_len"][b] // 8].copy()
+        return out
+
+    def regions_in(self, q, got):
+        """got: {source rank: words}"""
+        x = self.p.xchg(q)
+        for a, w in got.items():
+            assert w.shape[0] * 8 == x["r_len"][a], (q, a, w.shape[0] * 8, x["r_len"][a])
+            r0 = x["r_off"][a] // 8
+            self.recv[r0:r0 + w.shape[0]] = w
+
+    def node_step(self, c, u, gin):
+        """Node u of chunk c receives its parent's block: True if reached."""
+        p = self.parent[u]
+        if p != NONE:
+            pa, pb = self.row(c, p)
+            up, src = self.reached[p], self.rows[pa:pb]
+        else:
+            g = self.gref[u]
+            assert g != NONE and gin != NONE, (u, g, gin)
+            seg = self.segs[gin]
+            assert seg["rw"] == c["W"]
+            a = seg["rbase"][g >> 27] + (g & MASK) * c["W"]
+            src = self.recv[a:a + c["W"]]
+            up = src[0] != 0
+        ok = bool(up and self.live[self.peer[u]])
+        key = (u, c["group"])
+        self.writes[key] = self.writes.get(key, 0) + 1
+        if ok:
+            ra, rb = self.row(c, u)
+            self.rows[ra:rb] = src
+        if self.reached[u]:
+            assert ok, u  # reach is the same for every start group of a tree
+        self.reached[u] |= ok
+        return ok
+
+    def ship(self, c, oks):
+        if c["gout"] == NONE:
+            assert c["e_lo"] == c["e_hi"] or self.p.world == 1
+            return
+        seg = self.segs[c["gout"]]
+        for e in range(c["e_lo"], c["e_hi"]):
+            node, dst = self.shipv[e]
+            assert c["node_begin"] <= node < c["node_end"]
+            b, k = dst >> 27, dst & MASK
+            a = seg["sbase"][b] + k * c["W"]
+            if oks[node]:
+                ra, rb = self.row(c, node)
+                self.send[a:a + c["W"]] = self.rows[ra:rb]
+            else:
+                self.send[a] = 0
+
+    def chunks_of(self, q):
+        k = self.kind[q] if q < self.kind.shape[0] else 0
+        if k == PE.K_PAIR2:
+            return None
+        return self.p.chunks(PL.PAIR if k == PE.K_PAIR else PL.PULL, q), k == PE.K_PAIR
+
+    def run_round(self, q, part):
+        """The chunks of round q: part 0 = locally fed, 1 = ghost-fed."""
+        r = self.chunks_of(q)
+        if r is None:
+            return
+        (lo, split, hi, ch), pair = r
+        sel = ch[:split - lo] if part == 0 else ch[split - lo:]
+        for c in sel:
+            oks = {}
+            nodes = range(c["node_begin"], c["node_end"])
+            if part == 0 and not pair:
+                assert all(self.parent[u] != NONE or self.gref[u] == NONE for u in nodes)
+            for u in nodes:
+                oks[u] = self.node_step(c, u, c["gin"])
+            if not pair:
+                self.ship(c, oks)
+                continue
+            assert c["gout"] == NONE and c["e_lo"] == c["e_hi"]
+            if c["c_lo"] == NONE:
+                continue  # a level-1 run of the second round: no children in this launch
+            # phase B: every child of the run, consecutive ids, from the run's rows
+            kids = np.nonzero(np.isin(self.parent, np.arange(c["node_begin"], c["node_end"])))[0]
+            if kids.shape[0]:
+                assert np.array_equal(kids, np.arange(kids[0], kids[-1] + 1)), "children not consecutive"
+            for v in kids:
+                self.node_step(c, int(v), NONE)
+
+
+def emulate(sims, q_max, exchange):
+    for q in range(1, q_max + 1):
+        for s in sims:
+            s.pack(q)
+        exchange(q)
+        for part in (0, 1):
+            for s in sims:
+                s.run_round(q, part)
+
+
+def in_process_exchange(sims):
+    def go(q):
+        outs = [s.regions_out(q) for s in sims]
+        for b, s in enumerate(sims):
+            if s.p.xchg(q)["any"]:
+                s.regions_in(q, {a: outs[a][b] for a in range(len(sims)) if a != b})
+    return go
+
+
+def check(sims, trees, roots, live, n_groups):
+    """Deliveries equal the restatement's; every node written once per group;
+    every reached block equals its root's."""
+    n = live.shape[0]
+    for t, (par, root) in enumerate(zip(trees, roots)):
+        rp, cl = O.parents_to_csr(par)
+        _, oh, _ = O.disseminate(rp, cl, root, live, 1)
+        exp = oh[0] != 0xFF
+        got = np.zeros(n, dtype=bool)
+        for s in sims:
+            T = s.topics[t]
+            Ly = s.lay[t]
+            if not T["n_nodes"] or not Ly["W"]:
+                continue
+            for u in range(T["nbase"], T["nbase"] + T["n_nodes"]):
+                if s.level[u] == 0:
+                    continue
+                for gi in range(len(Ly["groups"])):
+                    assert s.writes.get((u, gi), 0) == 1, (t, u, gi, s.writes.get((u, gi), 0))
+                if s.reached[u]:
+                    got[s.peer[u]] = True
+                    for gi, (_, w0, wn) in enumerate(Ly["groups"]):
+                        r0 = s.block_row0(t, gi) + (u - T["nbase"]) * wn
+                        assert np.array_equal(s.rows[r0:r0 + wn], root_block(t, gi, wn)), (t, u, gi)
+        assert np.array_equal(got, exp), (t, int((got != exp).sum()))
+        assert len(Ly["groups"]) == n_groups[t] or not Ly["W"]
+
+
+def build(world, partition, n=1500, n_topics=2, seed=0, fan=None):
+    rng = np.random.default_rng(seed)
+    roots = [int(x) for x in rng.choice(n, size=n_topics, replace=False)]
+    trees = [random_tree(rng, n, r, fan) for r in roots]
+    live = (rng.random(n) > 0.08).astype(np.uint8)
+    for r in roots:
+        live[r] = 1
+    return rng, trees, roots, live
+
+
+@pytest.mark.parametrize("staggered", [False, True])
+@pytest.mark.parametrize("world,partition", [(1, PE.PART_PEER), (2, PE.PART_PEER), (3, PE.PART_PEER),
+                                             (4, PE.PART_SUBTREE), (4, PE.PART_PEER)])
+def test_plans_replay_to_the_oracle(world, partition, staggered):
+    rng, trees, roots, live = build(world, partition, seed=world * 7 + partition + 3 * staggered, fan=4)
+    n_msgs = 300
+    topics = rng.integers(0, len(trees), size=n_msgs)
+    starts = rng.integers(0, 4, size=n_msgs) if staggered else None
+    plans = [PL.Plan(np.stack(trees), roots, world, r, partition) for r in range(world)]
+    for p in plans:
+        p.window(topics, starts)
+    info = [p.info() for p in plans]
+    assert len({i["rounds"] for i in info}) == 1  # every rank plans the same rounds
+    for q in range(1, info[0]["rounds"] + 1):  # ... and the same exchange rounds and region sizes
+        xs = [p.xchg(q) for p in plans]
+        assert len({x["any"] for x in xs}) == 1
+        if xs[0]["any"]:
+            for a in range(world):
+                for b in range(world):
+                    if a != b:
+                        assert xs[a]["s_len"][b] == xs[b]["r_len"][a]
+                        assert xs[a]["s_len"][b] % 128 == 0 and xs[a]["s_off"][b] % 128 == 0
+    sims = [RankSim(p, live) for p in plans]
+    emulate(sims, info[0]["rounds"], in_process_exchange(sims))
+    n_groups = [len(np.unique(starts[topics == t])) if staggered else 1 for t in range(len(trees))]
+    check(sims, trees, roots, live, n_groups)
+    if world > 1 and partition == PE.PART_SUBTREE:
+        # the subtree partition exchanges in one round per (topic, group) only
+        ex = sum(plans[0].xchg(q)["any"] for q in range(1, info[0]["rounds"] + 1))
+        assert ex <= len(trees) * max(n_groups)
+
+
+def test_local_chunks_precede_ghost_chunks():
+    """Per round, the locally fed nodes of a level come first (their chunks run
+    while the exchange is in flight); the ghost-fed ones follow, grouped by
+    source rank and ordered by record index (sequential reads of the receive
+    buffer)."""
+    _, trees, roots, live = build(4, PE.PART_PEER, n=3000, n_topics=1, seed=11, fan=6)
+    p = PL.Plan(np.stack(trees), roots, 4, 1, PE.PART_PEER)
+    p.window(np.zeros(200, dtype=np.uint32))
+    gref = p.get(PL.GHOST_REF).astype(np.int64)
+    T = p.topic(0)
+    lo, ll = T["level_off"], T["level_local"]
+    for d in range(1, T["depth"] + 1):
+        a, b = T["nbase"] + lo[d], T["nbase"] + lo[d + 1]
+        loc = T["nbase"] + lo[d] + ll[d]
+        assert (gref[a:loc] == NONE).all() and (gref[loc:b] != NONE).all()
+        g = gref[loc:b]
+        key = (g >> 27) * (1 << 27) + (g & MASK)
+        assert (np.diff(key) >= 0).all()
+    for q in range(1, p.info()["rounds"] + 1):
+        k = p.get(PL.ROUND_KIND)[q]
+        if k != PE.K_PULL:
+            continue
+        lo_c, split, hi_c, ch = p.chunks(PL.PULL, q)
+        assert all((gref[c["node_begin"]:c["node_end"]] == NONE).all() for c in ch[:split - lo_c])
+        assert all((gref[c["node_begin"]:c["node_end"]] != NONE).all() for c in ch[split - lo_c:])
+
+
+def test_multi_rank_pairs_only_without_exchange():
+    """N ranks pair rounds (k_pull_pair) only where round q + 1 and q + 2
+    exchange nothing: under the subtree partition, every round but the split
+    level's neighbourhood."""
+    _, trees, roots, live = build(2, PE.PART_SUBTREE, n=20000, n_topics=1, seed=5)
+    plans = [PL.Plan(np.stack(trees), roots, 2, r, PE.PART_SUBTREE) for r in range(2)]
+    for p in plans:
+        p.window(np.zeros(600, dtype=np.uint32))
+    for p in plans:
+        kind = p.get(PL.ROUND_KIND)
+        rounds = p.info()["rounds"]
+        anyx = [False] + [p.xchg(q)["any"] for q in range(1, rounds + 1)] + [False, False]
+        assert sum(anyx) == 1
+        assert any(k == PE.K_PAIR for k in kind)
+        for q in range(1, rounds + 1):
+            if kind[q] == PE.K_PAIR:
+                assert not anyx[q + 1] and not anyx[q + 2]
+    sims = [RankSim(p, live) for p in plans]
+    emulate(sims, plans[0].info()["rounds"], in_process_exchange(sims))
+    check(sims, trees, roots, live, [1])
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _gloo_worker(rank, world, port, staggered, out):
+    import torch.distributed as tdist
+
+    from psengine import dist as D
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist = D.init("gloo")
+    try:
+        rng, trees, roots, live = build(world, PE.PART_PEER, n=1200, n_topics=2, seed=31 + staggered, fan=5)
+        topics = rng.integers(0, 2, size=200)
+        starts = rng.integers(0, 3, size=200) if staggered else None
+        p = PL.Plan(np.stack(trees), roots, world, rank, PE.PART_PEER)
+        p.window(topics, starts)
+        sim = RankSim(p, live)
+
+        def exchange(q):
+            mine = sim.regions_out(q)
+            allr = [None] * world
+            tdist.all_gather_object(allr, mine)
+            if p.xchg(q)["any"]:
+                sim.regions_in(q, {a: allr[a][rank] for a in range(world) if a != rank})
+
+        rounds = p.info()["rounds"]
+        for q in range(1, rounds + 1):
+            sim.pack(q)
+            exchange(q)
+            for part in (0, 1):
+                sim.run_round(q, part)
+        reached = sorted((int(sim.node_topic[u]), int(sim.peer[u])) for u in np.nonzero(sim.reached)[0]
+                         if sim.level[u] != 0)
+        allr = [None] * world
+        tdist.all_gather_object(allr, (reached, [sim.writes.get(k, 0) for k in sorted(sim.writes)]))
+        if rank == 0:
+            out[staggered] = allr
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("staggered", [0, 1])
+def test_gloo_world2_replays_the_plans(staggered):
+    import torch.multiprocessing as mp
+
+    world = 2
+    manager = mp.Manager()
+    out = manager.dict()
+    mp.spawn(_gloo_worker, args=(world, _free_port(), staggered, out), nprocs=world, join=True)
+    rng, trees, roots, live = build(world, PE.PART_PEER, n=1200, n_topics=2, seed=31 + staggered, fan=5)
+    got = set()
+    for reached, writes in out[staggered]:
+        got |= {tuple(x) for x in reached}
+        assert all(w == 1 for w in writes)
+    exp = set()
+    for t, (par, root) in enumerate(zip(trees, roots)):
+        rp, cl = O.parents_to_csr(par)
+        _, oh, _ = O.disseminate(rp, cl, root, live, 1)
+        exp |= {(t, int(x)) for x in np.nonzero(oh[0] != 0xFF)[0]}
+    assert got == exp
