@@ -625,7 +625,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         if (xe != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
         HIP_TRY(hipEventRecord(e->ev_xchg, e->xstream), "event");
       }
-      if (!lgrid[r] && !xr) continue;
+      if (!lgrid[r] && !xr) {
+        if (!upfront) HIP_TRY(seed_round(r, a.a_next), "seed");  // (messages starting this round)
+        continue;
+      }
       const bool pair = kind == PS_K_PAIR;
       // rows nobody re-reads while they can still sit in the 256 MB MALL
       // (large rounds and the last round) store non-temporally
