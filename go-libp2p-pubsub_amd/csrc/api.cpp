@@ -102,6 +102,7 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_FLOOD")) e->flood_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_PAIR")) e->pair_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD_PROFILE")) e->flood_profile = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_XCHG_OVERLAP")) e->xchg_overlap = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD_WORDS"))
     e->flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
   if (const char* v = std::getenv("PSAMD_FLOOD_SPIN_TICKS"))  // tests: 0 forces the timeout fallback

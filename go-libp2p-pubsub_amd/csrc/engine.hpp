@@ -197,6 +197,7 @@ struct ps_engine {
   hipStream_t xstream = nullptr;  // multi-GPU: the exchange, beside the round's local chunks
   hipEvent_t ev_run0 = nullptr, ev_run1 = nullptr;
   hipEvent_t ev_round = nullptr, ev_xchg = nullptr;  // multi-GPU: round boundary, exchange done
+  bool xchg_overlap = true;  // PSAMD_XCHG_OVERLAP=0: the exchange on the main stream, one launch per round after it
   std::vector<hipEvent_t> ev_k;  // pairs around expand launches
   uint32_t n_cus = 256, expand_grid = 2048;
   bool host_only = false;        // a planner probe (psengine_plan.h): no device

@@ -701,624 +701,6 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
   }
 }
 
-// ------------------------------------------------------------------ pull ---
-// Level mode, pull direction, one launch per round (multi-GPU windows, whose
-// rounds are separated by the frontier exchange; PSAMD_FLOOD=0 on one GPU).
-// In a single-start tree window a node of BFS level d receives, in round
-// s + d, exactly its parent's row -- if the parent was reached this window
-// (generation current) and the node is live -- and it is fresh (it has seen
-// nothing this window), so the seen test-and-set is new = row(parent) & ~0
-// and the whole row is written.  A wave owns a contiguous run of next-level
-// nodes, whose rows form one contiguous output stream:
-//   phase 1  resolves each node's source into a wave-private LDS table: its
-//            parent if the parent is in the frontier (generation current) and
-//            the node is live, else none; the node's generation is stamped;
-//   phase 2  streams the run's rows in order with 16-B stores (8-B for odd
-//            W), each lane's load taken from its node's parent row (siblings
-//            read the same parent row: L2 hits).  Loads are unconditional (a
-//            skipped node reads its own row) so the unrolled body keeps
-//            several in flight.
-// Counters: deliveries, seen writes, nodes visited, nodes reached, parents
-// expanded (a reached parent counts at its first child) and their row words.
-struct PullVec {
-  bool go;
-  uint4 v;
-};
-
-// Counters of the pull kernels, two forms: PullCtr (devutil.hpp) counts per
-// lane, as k_pull's block reduction wants; WaveCtr keeps one per-lane
-// delivery sum and counts everything else wave-uniformly (ballots: scalar
-// registers), which k_pull_pair's persistent waves carry across chunks for
-// two rounds without the vector registers per-lane counters would take.
-struct WaveCtr {
-  uint32_t deliv = 0;                      // per lane, folded into dsum per sub-run
-  uint32_t kids = 0, reached = 0, parents = 0;  // wave-uniform
-  uint64_t sw = 0, pwords = 0;             // wave-uniform: words written, parent words read
-  uint64_t dsum = 0;                       // wave-uniform: folded deliveries
-};
-// The per-lane delivery count into the 64-bit wave total: after each sub-run
-// of at most kPairKids rows (<= 2^24 bits), so neither the lane counts nor
-// the sum over a wide run's children (f * W * 64 bits) wrap.
-__device__ __forceinline__ void ctr_fold(WaveCtr& c) {
-  c.dsum += __builtin_amdgcn_readfirstlane(__reduce_add_sync(~0ull, c.deliv));  // (a sub-run: < 2^32)
-  c.deliv = 0;
-}
-// One batch of (up to 64) nodes: visited (in), reached (ok), a reached
-// parent's first child (par); W_sw row words written per reached node,
-// W_pw parent row words read per counted parent.
-__device__ __forceinline__ void ctr_nodes(PullCtr& c, bool in, bool ok, bool par, uint32_t, uint32_t W_pw) {
-  c.kids += in;
-  c.reached += ok;
-  if (par) {
-    c.parents += 1;
-    c.pwords += W_pw;
-  }
-}
-__device__ __forceinline__ void ctr_nodes(WaveCtr& c, bool in, bool ok, bool par, uint32_t W_sw, uint32_t W_pw) {
-  c.kids += __popcll(__ballot(in));
-  const uint32_t r = __popcll(__ballot(ok));
-  c.reached += r;
-  c.sw += static_cast<uint64_t>(r) * W_sw;
-  const uint32_t p = __popcll(__ballot(par));
-  c.parents += p;
-  c.pwords += static_cast<uint64_t>(p) * W_pw;
-}
-// One lane's stored unit: its delivered bits, and (PullCtr) its words.
-__device__ __forceinline__ void ctr_unit(PullCtr& c, bool own, uint32_t pop, uint32_t words) {
-  c.deliv += own ? pop : 0u;
-  c.sw += own ? words : 0u;
-}
-__device__ __forceinline__ void ctr_unit(WaveCtr& c, bool own, uint32_t pop, uint32_t) { c.deliv += own ? pop : 0u; }
-
-// Chunk constants: row of node u = base + u * W (a start group's block row
-// for kTopicGroups topics).
-struct PullTopic {
-  uint64_t base;
-  uint32_t W, nbase, root;
-};
-
-// Phase 1 for the nodes [nb, nb + nk) of one level: src[j] = the address of
-// the row node nb + j copies (its parent's row: the root's arrival row, a
-// seen row, or -- multi-GPU -- a ghost row in the receive buffer), or 0.  The
-// parents of a run are consecutive node ids [p_lo, p_hi] (BFS numbering):
-// their generation bytes are staged into LDS by loads issued together with
-// the nodes' own metadata, so phase 1 costs one memory round trip.
-template <class Ctr>
-__device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t nk,
-                                             uint32_t p_lo, uint32_t p_hi, uint64_t* src, uint8_t* genl,
-                                             uint32_t lane, uint32_t cur, Ctr& c, uint32_t gin,
-                                             uint32_t stage_cap = kPullMaxKids) {
-  uint32_t g0 = 0;
-  const bool staged = p_lo != kNoneNode && p_hi - p_lo < stage_cap;  // genl holds stage_cap + 8 bytes
-  if (staged) {
-    g0 = p_lo & ~3u;
-    const uint32_t nd = ((p_hi + 4u) & ~3u) - g0;  // bytes, whole dwords
-    const uint32_t* gsrc = reinterpret_cast<const uint32_t*>(a.gen + g0);
-    for (uint32_t d = lane; 4 * d < nd; d += 64) reinterpret_cast<uint32_t*>(genl)[d] = gsrc[d];
-  }
-  for (uint32_t j0 = 0; j0 < nk; j0 += 64) {
-    const uint32_t j = j0 + lane;
-    const bool in = j < nk;
-    uint32_t p = kNoneNode, f = 0;
-    if (in) {
-      p = a.node_parent[nb + j];
-      f = a.node_flags[nb + j];
-    }
-    bool up = false;  // the parent was reached this window
-    uint64_t row = 0;
-    uint32_t pid = p;  // the parent's identity for the once-per-parent count
-    if (in && p != kNoneNode) {
-      up = (staged ? genl[p - g0] : a.gen[p]) == cur;
-      row = reinterpret_cast<uint64_t>((p == P.root ? a.a_cur : a.seen) + P.base + static_cast<uint64_t>(p) * P.W);
-    } else if (in && gin != kNoneNode) {  // parent on another rank: its record arrived this round
-      const uint32_t g = a.ghost_ref[nb + j];
-      if (g != kNoneNode) {
-        const GhostSeg* S = a.gsegs + gin;
-        const uint64_t* rec = a.recv + S->rbase[g >> kRemoteRankShift] +
-                              static_cast<uint64_t>(g & kRemoteIdMask) * S->rw;
-        up = rec[0] != 0;  // an unreached parent's record starts with a zero word
-        row = reinterpret_cast<uint64_t>(rec);
-        pid = 0x80000000u | g;
-      }
-    }
-    uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(pid), 1, 64));
-    if (lane == 0) {
-      prev = kNoneNode;
-      const uint32_t q = nb + j0;
-      if (q > P.nbase) {
-        prev = a.node_parent[q - 1];
-        if (prev == kNoneNode && gin != kNoneNode && a.ghost_ref[q - 1] != kNoneNode)
-          prev = 0x80000000u | a.ghost_ref[q - 1];
-      }
-    }
-    const bool ok = up && (f & kNodeLive);
-    if (in) src[j] = ok ? row : 0ull;
-    if (ok) a.gen[nb + j] = static_cast<uint8_t>(cur);
-    ctr_nodes(c, in, ok, up && pid != prev, P.W, P.W);
-  }
-}
-
-// row store of the pull stream: plain, or non-temporal (`nt`: rows nobody
-// re-reads soon)
-template <bool kNT>
-__device__ __forceinline__ void store_row16(uint64_t* p, const uint4& v) {
-  if constexpr (kNT) {
-    u32x4 x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, reinterpret_cast<u32x4*>(p));
-  } else {
-    *reinterpret_cast<uint4*>(p) = v;
-  }
-}
-template <bool kNT>
-__device__ __forceinline__ void store_row8(uint64_t* p, uint64_t v) {
-  if constexpr (kNT)
-    __builtin_nontemporal_store(v, p);
-  else
-    *p = v;
-}
-
-// Phase 2: the rows of nodes [nb, nb + nk) as one output stream, each lane's
-// load from the row its node copies (src[], kNoneNode = skip).  8 loads in
-// flight, then 8 stores, unconditional and branch-free (a skipped lane writes
-// its own row back unchanged, a lane past the run's end stores the run's last
-// pair again with the value its owner stores), so the compiler counts vmcnt
-// exactly instead of draining at branches.  kLds (k_pull_pair): every word
-// also goes to lrows[i], the run's rows in LDS for its children.
-template <bool kRecord, bool kNT, bool kLds = false, class Ctr = PullCtr>
-__device__ __forceinline__ void pull_stream(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t nk,
-                                            const uint64_t* src, uint32_t lane, uint32_t round, Ctr& c,
-                                            uint64_t* lrows = nullptr) {
-  constexpr uint32_t kU = 8;
-  const uint32_t W = P.W;
-  const uint64_t base = P.base;
-  const uint32_t total = nk * W;
-  uint64_t* const out = a.seen + base + static_cast<uint64_t>(nb) * W;
-  const float rw = 1.0f / static_cast<float>(W);
-  // row kk = i / W and word r of the run, branch-free (float estimate off by
-  // at most one; i < 2^24)
-  auto split = [&](uint32_t i, int32_t& kk, int32_t& r) {
-    kk = static_cast<int32_t>(static_cast<float>(i) * rw);
-    r = static_cast<int32_t>(i) - kk * static_cast<int32_t>(W);
-    const int32_t lo = r < 0, hi = r >= static_cast<int32_t>(W);
-    kk += hi - lo;
-    r += (lo - hi) * static_cast<int32_t>(W);
-  };
-  if (!(W & 1u)) {
-    // even W: every row 16-B aligned, a 2-word pair never straddles rows
-    auto one = [&](uint32_t i) {
-      int32_t kk, r;
-      split(i, kk, r);
-      const uint64_t row = src[kk];
-      const bool go = row != 0;
-      const uint64_t* s = go ? reinterpret_cast<const uint64_t*>(row) + r : out + i;
-      return PullVec{go, *reinterpret_cast<const uint4*>(s)};
-    };
-    // the stream starts h words before the run, at a 128-B line, so every
-    // 1-KB wave store covers whole lines (lanes before the run store its
-    // first pair again, with the value its owner stores)
-    const uint32_t h = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out) & 127) >> 3;
-    for (uint32_t i0 = 0; i0 < total + h; i0 += kU * 128) {
-      PullVec x[kU];
-#pragma unroll
-      for (uint32_t u = 0; u < kU; ++u) {
-        const int32_t i = static_cast<int32_t>(i0 + u * 128 + 2 * lane) - static_cast<int32_t>(h);
-        x[u] = one(i < 0 ? 0u : (static_cast<uint32_t>(i) < total ? static_cast<uint32_t>(i) : total - 2));
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < kU; ++u) {
-        const int32_t is = static_cast<int32_t>(i0 + u * 128 + 2 * lane) - static_cast<int32_t>(h);
-        const bool inr = is >= 0 && static_cast<uint32_t>(is) < total;
-        const uint32_t i = is < 0 ? 0u : (inr ? static_cast<uint32_t>(is) : total - 2);
-        if constexpr (kRecord) {
-          if (x[u].go && inr) {
-            *reinterpret_cast<uint4*>(out + i) = x[u].v;
-            const uint64_t cw = (out - a.seen) + i;
-            record_word(a.hop_rec, cw, static_cast<uint64_t>(x[u].v.y) << 32 | x[u].v.x, round);
-            record_word(a.hop_rec, cw + 1, static_cast<uint64_t>(x[u].v.w) << 32 | x[u].v.z, round);
-          }
-        } else {
-          store_row16<kNT>(out + i, x[u].v);
-        }
-        if constexpr (kLds) *reinterpret_cast<uint4*>(lrows + i) = x[u].v;  // (i clamped: its owner's value)
-        const bool own = x[u].go && inr;
-        ctr_unit(c, own, popc4(x[u].v), 2u);
-      }
-    }
-  } else {
-    // odd W: one word (8 B) per lane, the same pipeline
-    const uint32_t h = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out) & 127) >> 3;  // line-aligned start
-    for (uint32_t i0 = 0; i0 < total + h; i0 += kU * 64) {
-      uint64_t m[kU];
-      bool go[kU];
-#pragma unroll
-      for (uint32_t u = 0; u < kU; ++u) {
-        const int32_t is = static_cast<int32_t>(i0 + u * 64 + lane) - static_cast<int32_t>(h);
-        // before the run: its first word again; past the end: its last word again
-        const uint32_t ic = is < 0 ? 0u : (static_cast<uint32_t>(is) < total ? static_cast<uint32_t>(is) : total - 1);
-        int32_t kk, r;
-        split(ic, kk, r);
-        const uint64_t row = src[kk];
-        go[u] = row != 0;
-        const uint64_t* s = go[u] ? reinterpret_cast<const uint64_t*>(row) + r : out + ic;
-        m[u] = *s;
-      }
-#pragma unroll
-      for (uint32_t u = 0; u < kU; ++u) {
-        const int32_t is = static_cast<int32_t>(i0 + u * 64 + lane) - static_cast<int32_t>(h);
-        const bool inr = is >= 0 && static_cast<uint32_t>(is) < total;
-        const uint32_t i = is < 0 ? 0u : (inr ? static_cast<uint32_t>(is) : total - 1);
-        if constexpr (kRecord) {
-          if (go[u] && inr) {
-            out[i] = m[u];
-            record_word(a.hop_rec, (out - a.seen) + i, m[u], round);
-          }
-        } else {
-          store_row8<kNT>(out + i, m[u]);
-        }
-        if constexpr (kLds) lrows[i] = m[u];
-        const bool own = go[u] && inr;
-        ctr_unit(c, own, __popcll(m[u]), 1u);
-      }
-    }
-  }
-}
-
-// Multi-GPU: the chunk's nodes that are ghost parents next round ship their
-// rows now, as records in the send buffer (GhostSeg gout: record k to rank b
-// at sbase[b] + k * W), from the rows they copied (src[]: L2-resident, just
-// read): one pass over the records, 16-B units for even W.  An unreached
-// node's record gets a zero first word.  Replaces a separate pack launch that
-// re-read the rows from HBM.
-__device__ __forceinline__ void pull_ship(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t e_lo,
-                                          uint32_t e_hi, uint32_t gout, const uint64_t* src, uint32_t lane) {
-  const GhostSeg* S = a.gsegs + gout;
-  const bool pairs = !(P.W & 1u);
-  const uint32_t per = pairs ? P.W >> 1 : P.W;
-  const uint32_t total = (e_hi - e_lo) * per;
-  for (uint32_t i = lane; i < total; i += 64) {
-    const uint32_t k = i / per, r = i - k * per;
-    const ShipEntry E = a.ship[e_lo + k];
-    const uint64_t row = src[E.node - nb];
-    uint64_t* rec = a.send + S->sbase[E.dst >> kRemoteRankShift] +
-                    static_cast<uint64_t>(E.dst & kRemoteIdMask) * P.W;
-    if (row == 0) {
-      if (r == 0) rec[0] = 0;
-      continue;
-    }
-    const uint32_t w = pairs ? 2 * r : r;
-    const uint64_t* s = reinterpret_cast<const uint64_t*>(row) + w;
-    if (pairs)
-      *reinterpret_cast<uint4*>(rec + w) = *reinterpret_cast<const uint4*>(s);
-    else
-      rec[w] = *s;
-  }
-}
-
-// The block's counters of one launch into partial slot `slot` (blocks share
-// a slot: slots are zeroed per window).
-__device__ __forceinline__ void pull_flush(const PullCtr& c, uint64_t* partials, uint64_t slot, uint32_t lane,
-                                           uint32_t wid) {
-  __shared__ uint64_t red[kBlock / 64][7];
-  const uint64_t v7[7] = {wave_sum_u64(c.deliv),   wave_sum_u64(c.sw),      wave_sum_u64(c.kids),
-                          wave_sum_u64(c.reached), wave_sum_u64(c.parents), wave_sum_u64(c.pwords),
-                          wave_sum_u64(c.dup)};
-  if (lane == 0)
-#pragma unroll
-    for (int q = 0; q < 7; ++q) red[wid][q] = v7[q];
-  __syncthreads();
-  if (threadIdx.x < kNumCtr) {
-    uint64_t t[7] = {0, 0, 0, 0, 0, 0, 0};
-    for (int w = 0; w < kBlock / 64; ++w)
-#pragma unroll
-      for (int q = 0; q < 7; ++q) t[q] += red[w][q];
-    const uint64_t v = pull_ctr_pick(t, threadIdx.x);
-    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(partials + slot * kNumCtr + threadIdx.x),
-                     static_cast<unsigned long long>(v));
-  }
-}
-
-template <bool kRecord, bool kNT>
-__global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __restrict__ chunks,
-                                                 uint32_t n_chunks, uint32_t round) {
-  __shared__ uint64_t src_lds[kBlock / 64][kPullMaxKids];
-  __shared__ uint32_t gen_lds[kBlock / 64][kPullMaxKids / 4 + 2];
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t wave = blockIdx.x * (kBlock / 64) + wid;
-  uint64_t* src = src_lds[wid];
-  uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds[wid]);
-  const uint32_t cur = a.gen_cur & 0xFF;
-  PullCtr c;
-  if (wave < n_chunks) {  // one chunk per wave
-    const PullChunk ch = chunks[wave];
-    const TopicDev T = a.topics[ch.topic];
-    PullTopic P;
-    P.W = ch.W;
-    P.nbase = T.nbase;
-    P.base = (static_cast<uint64_t>(ch.row0_hi) << 32 | ch.row0_lo) - static_cast<uint64_t>(T.nbase) * ch.W;
-    P.root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
-    const uint32_t n1 = ch.node_end - ch.node_begin;
-    // LDS ops of a wave are processed in order: the table written in phase 1
-    // is visible to the reads that follow
-    pull_resolve(a, P, ch.node_begin, n1, ch.p_lo, ch.p_hi, src, genl, lane, cur, c, ch.gin);
-    pull_stream<kRecord, kNT>(a, P, ch.node_begin, n1, src, lane, round, c);
-    if (ch.e_hi > ch.e_lo) pull_ship(a, P, ch.node_begin, ch.e_lo, ch.e_hi, ch.gout, src, lane);
-  }
-  pull_flush(c, a.partials, blockIdx.x % a.slot_mod, lane, wid);
-}
-
-// k_pull_pair: rounds q and q + 1 in one launch (one rank).
-// A wave writes a run of level-d nodes as k_pull does (phase A: round q, the
-// parents' rows from HBM, reach decided from this window's generation
-// bytes), keeping the rows it writes in LDS, and then every child of the run
-// (phase B: round q + 1, level d + 1 -- the children of a BFS-numbered run
-// are consecutive ids): a child copies its parent's row as round q left it,
-// read from LDS instead of HBM, if the parent was reached and the child is
-// live, and stamps its generation.  No other wave writes those parents or
-// reads those children, so the launch needs no cross-wave ordering.
-//
-// Phase B, one sub-run of at most kPairKids children: resolve into ctab (the
-// LDS word offset of the parent's row, or kPairWords: a zero pair, so an
-// unreached child's row is written with zeros -- stale under its old
-// generation byte, so never read), then one line-aligned output stream with
-// the phase-A pipeline.
-// The first sub-run's parent ids and flags arrive prefetched (pf_p, pf_f:
-// loaded with phase A's metadata, one memory round trip for both).
-template <bool kRecord, bool kNT, uint32_t kWords>
-__device__ __forceinline__ void pair_kids(const PullArgs& a, const PullTopic& P, uint32_t nb, uint32_t n1,
-                                          uint32_t c_lo, uint32_t c_hi, const uint64_t* reach,
-                                          const uint64_t* lrows, uint32_t* ctab, uint32_t lane, uint32_t round,
-                                          const uint32_t* pf_p, const uint32_t* pf_f, WaveCtr& c) {
-  constexpr uint32_t kU = 8;
-  constexpr uint32_t kZero = kWords;
-  const uint32_t W = P.W;
-  const uint32_t cur = a.gen_cur & 0xFF;
-  const float rw = 1.0f / static_cast<float>(W);
-  auto split = [&](uint32_t i, int32_t& kk, int32_t& r) {
-    kk = static_cast<int32_t>(static_cast<float>(i) * rw);
-    r = static_cast<int32_t>(i) - kk * static_cast<int32_t>(W);
-    const int32_t lo = r < 0, hi = r >= static_cast<int32_t>(W);
-    kk += hi - lo;
-    r += (lo - hi) * static_cast<int32_t>(W);
-  };
-  for (uint32_t k0 = c_lo; k0 < c_hi; k0 += kPairKids) {
-    const uint32_t nk = min(kPairKids, c_hi - k0);
-#pragma unroll
-    for (uint32_t s = 0; s < kPairKids / 64; ++s) {
-      const uint32_t j0 = s * 64;
-      if (j0 >= nk) break;
-      const uint32_t j = j0 + lane;
-      const bool in = j < nk;
-      uint32_t p = kNoneNode, f = 0;
-      if (k0 == c_lo) {
-        p = in ? pf_p[s] : kNoneNode;
-        f = pf_f[s];
-      } else if (in) {
-        p = a.node_parent[k0 + j];
-        f = a.node_flags[k0 + j];
-      }
-      const uint32_t kp = p - nb;  // the parent's place in the run
-      const bool up = in && kp < n1 && ((a.all_current & 1u) || ((reach[kp >> 6] >> (kp & 63)) & 1ull));
-      const bool ok = up && (f & kNodeLive);
-      if (in) ctab[j] = ok ? kp * W : kZero;
-      if (ok) a.gen[k0 + j] = static_cast<uint8_t>(cur);
-      uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
-      if (lane == 0) prev = k0 + j0 > P.nbase ? a.node_parent[k0 + j0 - 1] : kNoneNode;
-      ctr_nodes(c, in, ok, up && p != prev, W, 0u);  // (parent rows from LDS: no parent words read)
-    }
-    const uint32_t total = nk * W;
-    uint64_t* const out = a.seen + P.base + static_cast<uint64_t>(k0) * W;
-    const uint32_t h = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out) & 127) >> 3;
-    if (!(W & 1u)) {
-      for (uint32_t i0 = 0; i0 < total + h; i0 += kU * 128) {
-        uint4 x[kU];
-        bool go[kU];
-#pragma unroll
-        for (uint32_t u = 0; u < kU; ++u) {
-          const int32_t is = static_cast<int32_t>(i0 + u * 128 + 2 * lane) - static_cast<int32_t>(h);
-          const uint32_t i = is < 0 ? 0u : (static_cast<uint32_t>(is) < total ? static_cast<uint32_t>(is) : total - 2);
-          int32_t kk, r;
-          split(i, kk, r);
-          const uint32_t off = ctab[kk];
-          go[u] = off != kZero;
-          x[u] = *reinterpret_cast<const uint4*>(lrows + (go[u] ? off + r : kZero));
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kU; ++u) {
-          const int32_t is = static_cast<int32_t>(i0 + u * 128 + 2 * lane) - static_cast<int32_t>(h);
-          const bool inr = is >= 0 && static_cast<uint32_t>(is) < total;
-          const uint32_t i = is < 0 ? 0u : (inr ? static_cast<uint32_t>(is) : total - 2);
-          if constexpr (kRecord) {
-            if (go[u] && inr) {
-              *reinterpret_cast<uint4*>(out + i) = x[u];
-              const uint64_t cw = (out - a.seen) + i;
-              record_word(a.hop_rec, cw, static_cast<uint64_t>(x[u].y) << 32 | x[u].x, round);
-              record_word(a.hop_rec, cw + 1, static_cast<uint64_t>(x[u].w) << 32 | x[u].z, round);
-            }
-          } else {
-            store_row16<kNT>(out + i, x[u]);
-          }
-          const bool own = go[u] && inr;
-          ctr_unit(c, own, popc4(x[u]), 2u);
-        }
-      }
-    } else {
-      for (uint32_t i0 = 0; i0 < total + h; i0 += kU * 64) {
-        uint64_t m[kU];
-        bool go[kU];
-#pragma unroll
-        for (uint32_t u = 0; u < kU; ++u) {
-          const int32_t is = static_cast<int32_t>(i0 + u * 64 + lane) - static_cast<int32_t>(h);
-          const uint32_t i = is < 0 ? 0u : (static_cast<uint32_t>(is) < total ? static_cast<uint32_t>(is) : total - 1);
-          int32_t kk, r;
-          split(i, kk, r);
-          const uint32_t off = ctab[kk];
-          go[u] = off != kZero;
-          m[u] = lrows[go[u] ? off + r : kZero];
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kU; ++u) {
-          const int32_t is = static_cast<int32_t>(i0 + u * 64 + lane) - static_cast<int32_t>(h);
-          const bool inr = is >= 0 && static_cast<uint32_t>(is) < total;
-          const uint32_t i = is < 0 ? 0u : (inr ? static_cast<uint32_t>(is) : total - 1);
-          if constexpr (kRecord) {
-            if (go[u] && inr) {
-              out[i] = m[u];
-              record_word(a.hop_rec, (out - a.seen) + i, m[u], round);
-            }
-          } else {
-            store_row8<kNT>(out + i, m[u]);
-          }
-          const bool own = go[u] && inr;
-          ctr_unit(c, own, __popcll(m[u]), 1u);
-        }
-      }
-    }
-    ctr_fold(c);
-  }
-}
-
-__device__ __forceinline__ void ctr_add(WaveCtr& d, const WaveCtr& s) {
-  d.deliv += s.deliv;  // (one phase-A run: <= kPairWords * 64 bits, folded below)
-  d.dsum += s.dsum;
-  d.sw += s.sw;
-  d.kids += s.kids;
-  d.reached += s.reached;
-  d.parents += s.parents;
-  d.pwords += s.pwords;
-}
-
-// Counters of a wave (two rounds) added with its own atomics: no block
-// reduction, so no barrier.
-__device__ __forceinline__ void pull_flush_wave(const WaveCtr& c, uint64_t* partials, uint64_t slot, uint32_t lane) {
-  const uint64_t v7[7] = {c.dsum + __reduce_add_sync(~0ull, c.deliv), c.sw, c.kids, c.reached, c.parents,
-                          c.pwords, 0ull};
-  if (lane < kNumCtr) {
-    const uint64_t v = pull_ctr_pick(v7, lane);
-    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(partials + slot * kNumCtr + lane),
-                     static_cast<unsigned long long>(v));
-  }
-}
-
-// One wave per workgroup, one chunk per wave (grid = n_chunks; the loop
-// only guards a smaller grid).  A chunk's two phases take longer when its
-// run has more children: one-wave workgroups never wait for siblings (a
-// 4-wave block's barrier held its LDS behind the slowest chunk: cfg3 (18,19)
-// 583 -> 549 us).  Persistent waves looping over chunks measured slower at
-// every grid tried (resident grid 700 us, 8192 waves 588 us, one chunk per
-// wave 543 us): a wave's chunks run back to back, each paying its round
-// trips, where fresh waves overlap them.
-template <bool kRecord, bool kNT2>
-__global__ __launch_bounds__(64) void k_pull_pair(PullArgs a, const PullChunk* __restrict__ chunks,
-                                                  uint32_t n_chunks, uint32_t round) {
-  __shared__ uint64_t rows[kPairWords + 2];  // + the zero pair
-  __shared__ uint64_t src[kPairPar];         // phase A sources, then phase B's ctab
-  __shared__ uint32_t gen_lds[kPairPar / 4 + 2];
-  __shared__ uint64_t reach[kPairPar / 64];
-  static_assert(kPairKids * 4 <= kPairPar * 8, "ctab fits the source table");
-  const uint32_t lane = threadIdx.x;
-  uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds);
-  const uint32_t cur = a.gen_cur & 0xFF;
-  if (lane < 2) rows[kPairWords + lane] = 0;
-  WaveCtr c, c2;
-  for (uint32_t ci = blockIdx.x; ci < n_chunks; ci += gridDim.x) {
-    const PullChunk ch = chunks[ci];
-    const TopicDev T = a.topics[ch.topic];
-    PullTopic P;
-    P.W = ch.W;
-    P.nbase = T.nbase;
-    P.base = (static_cast<uint64_t>(ch.row0_hi) << 32 | ch.row0_lo) - static_cast<uint64_t>(T.nbase) * ch.W;
-    P.root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
-    const uint32_t n1 = ch.node_end - ch.node_begin;  // <= kPairPar, n1 * W <= kPairWords (host plan)
-    const bool late = ch.c_lo == kNoneNode;           // a level-1 run of round q + 1
-    // the first children's metadata, issued ahead of phase A's own
-    uint32_t pf_p[kPairKids / 64], pf_f[kPairKids / 64];
-    const uint32_t nk0 = late ? 0u : min(kPairKids, ch.c_hi - ch.c_lo);
-#pragma unroll
-    for (uint32_t s = 0; s < kPairKids / 64; ++s) {
-      const uint32_t j = s * 64 + lane;
-      pf_p[s] = j < nk0 ? a.node_parent[ch.c_lo + j] : kNoneNode;
-      pf_f[s] = j < nk0 ? a.node_flags[ch.c_lo + j] : 0u;
-    }
-    WaveCtr ca;
-    pull_resolve(a, P, ch.node_begin, n1, ch.p_lo, ch.p_hi, src, genl, lane, cur, ca, ch.gin, kPairPar);
-    for (uint32_t j0 = 0; j0 < n1; j0 += 64) {
-      const uint64_t b = __ballot(j0 + lane < n1 && src[j0 + lane] != 0);
-      if (lane == 0) reach[j0 >> 6] = b;
-    }
-    pull_stream<kRecord, true, true>(a, P, ch.node_begin, n1, src, lane, round + (late ? 1 : 0), ca, rows);
-    ctr_fold(ca);
-    // src (u64 sources) and ctab (u32 offsets) share the LDS table: no memory
-    // access may move across the switch from one view to the other
-    asm volatile("" ::: "memory");
-    if (late) {
-      ctr_add(c2, ca);
-    } else {
-      ctr_add(c, ca);
-      if (ch.c_hi > ch.c_lo)
-        pair_kids<kRecord, kNT2, kPairWords>(a, P, ch.node_begin, n1, ch.c_lo, ch.c_hi, reach, rows,
-                                             reinterpret_cast<uint32_t*>(src), lane, round + 1, pf_p, pf_f, c2);
-    }
-    asm volatile("" ::: "memory");
-  }
-  pull_flush_wave(c, a.partials, blockIdx.x % a.slot_mod, lane);
-  pull_flush_wave(c2, a.partials2, blockIdx.x % a.slot_mod, lane);
-}
-
-// Children ranges of the pair chunks (GPU or host node space alike).
-__global__ __launch_bounds__(kBlock) void k_pair_kids(PullChunk* __restrict__ chunks, uint32_t n,
-                                                      const uint32_t* __restrict__ row_ptr,
-                                                      const uint32_t* __restrict__ col) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  PullChunk& c = chunks[i];
-  if (c.c_lo == kNoneNode) return;
-  const uint32_t rb = row_ptr[c.node_begin], re = row_ptr[c.node_end];
-  c.c_lo = re > rb ? col[rb] : 0u;
-  c.c_hi = re > rb ? col[re - 1] + 1u : 0u;
-}
-
-// Multi-GPU level mode: the topic roots' records of a round (the roots are
-// seeded, so always reached).  Thread i of the flattened stream copies unit i
-// of one record -- a 16-B word pair for even W, one word for odd W: segment
-// (one root, constant W) by a short scan, entry = offset / units per row.
-__global__ __launch_bounds__(kBlock) void k_pack(const ShipEntry* __restrict__ ship,
-                                                 const PackSeg* __restrict__ segs, uint32_t n_segs,
-                                                 uint64_t total, const GhostSeg* __restrict__ gsegs,
-                                                 const uint64_t* __restrict__ seen, uint64_t* __restrict__ send) {
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < total;
-       i += static_cast<uint64_t>(gridDim.x) * kBlock) {
-    uint32_t k = 0;
-    while (k + 1 < n_segs && segs[k + 1].unit0 <= i) ++k;
-    const PackSeg S = segs[k];
-    const bool pairs = !(S.W & 1u);
-    const uint32_t per = pairs ? S.W >> 1 : S.W;  // units per row
-    const uint32_t o = static_cast<uint32_t>(i - S.unit0);
-    const uint32_t e = S.e0 + o / per;
-    const uint32_t w = (o - (e - S.e0) * per) << (pairs ? 1 : 0);
-    const ShipEntry E = ship[e];
-    uint64_t* rec = send + gsegs[S.gseg].sbase[E.dst >> kRemoteRankShift] +
-                    static_cast<uint64_t>(E.dst & kRemoteIdMask) * S.W;
-    const uint64_t* row = seen + S.row + w;
-    if (pairs)
-      *reinterpret_cast<uint4*>(rec + w) = *reinterpret_cast<const uint4*>(row);
-    else
-      rec[w] = *row;
-  }
-}
-
-// GPU-built node spaces have no host mirror of node_parent: the chunks'
-// parent ranges (k_pull's generation staging) are filled in on the device.
-__global__ __launch_bounds__(kBlock) void k_chunk_parents(PullChunk* __restrict__ chunks, uint32_t n,
-                                                          const uint32_t* __restrict__ node_parent) {
-  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  PullChunk& c = chunks[i];
-  if (c.node_end <= c.node_begin) return;
-  c.p_lo = node_parent[c.node_begin];
-  c.p_hi = node_parent[c.node_end - 1];
-}
-
 __global__ __launch_bounds__(kBlock) void k_stage_copy(StageCopy c) {
   const uint32_t tid = blockIdx.x * kBlock + threadIdx.x, nth = gridDim.x * kBlock;
   for (uint32_t k = 0; k < c.n; ++k)
@@ -1607,58 +989,6 @@ hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record
     hipLaunchKernelGGL((k_expand<true, true>), dim3(grid), dim3(kBlock), 0, s, a, round);
   else
     hipLaunchKernelGGL((k_expand<false, true>), dim3(grid), dim3(kBlock), 0, s, a, round);
-  return hipGetLastError();
-}
-
-hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                       uint32_t grid, uint32_t round, bool record, bool nt, bool cap, hipStream_t s) {
-  if (n_chunks == 0 || grid == 0) return hipSuccess;
-  // cap: the large (nt) rounds run at most 5 blocks per CU -- 10 KB of LDS
-  // left unused per block caps residency (8 blocks: 6 % slower on cfg3's big
-  // rounds on one rank); small rounds keep full residency, they need the
-  // waves in flight
-  const size_t kBigRoundLdsPad = cap ? 10240 : 0;
-  if (record)  // parity runs: one variant
-    hipLaunchKernelGGL((k_pull<true, false>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
-  else if (nt)
-    hipLaunchKernelGGL((k_pull<false, true>), dim3(grid), dim3(kBlock), kBigRoundLdsPad, s, a, chunks, n_chunks,
-                       round);
-  else
-    hipLaunchKernelGGL((k_pull<false, false>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
-  return hipGetLastError();
-}
-
-hipError_t launch_pull_pair(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks, uint32_t grid,
-                            uint32_t round, bool record, bool nt2, hipStream_t s) {
-  if (n_chunks == 0 || grid == 0) return hipSuccess;
-  grid = grid < n_chunks ? grid : n_chunks;
-  if (record)
-    hipLaunchKernelGGL((k_pull_pair<true, false>), dim3(grid), dim3(64), 0, s, a, chunks, n_chunks, round);
-  else if (nt2)
-    hipLaunchKernelGGL((k_pull_pair<false, true>), dim3(grid), dim3(64), 0, s, a, chunks, n_chunks, round);
-  else
-    hipLaunchKernelGGL((k_pull_pair<false, false>), dim3(grid), dim3(64), 0, s, a, chunks, n_chunks, round);
-  return hipGetLastError();
-}
-
-hipError_t launch_pair_kids(PullChunk* chunks, uint32_t n, const uint32_t* row_ptr, const uint32_t* col,
-                            hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_pair_kids, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, chunks, n, row_ptr, col);
-  return hipGetLastError();
-}
-
-hipError_t launch_pack(const ShipEntry* ship, const PackSeg* segs, uint32_t n_segs, uint64_t total_units,
-                       const GhostSeg* gsegs, const uint64_t* seen, uint64_t* send, hipStream_t s) {
-  if (total_units == 0 || n_segs == 0) return hipSuccess;
-  const uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>(4096, (total_units + kBlock - 1) / kBlock));
-  hipLaunchKernelGGL(k_pack, dim3(grid), dim3(kBlock), 0, s, ship, segs, n_segs, total_units, gsegs, seen, send);
-  return hipGetLastError();
-}
-
-hipError_t launch_chunk_parents(PullChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_chunk_parents, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, chunks, n, node_parent);
   return hipGetLastError();
 }
 

@@ -610,20 +610,23 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       // the exchange stream, while this round's locally fed chunks run; the
       // ghost-fed chunks wait for the exchange
       const bool xr = world > 1 && r < e->ghost.rounds.size() && e->ghost.rounds[r].any;
+      hipStream_t xs = e->xchg_overlap ? e->xstream : s;
       if (xr) {
         const GhostRound& R = e->ghost.rounds[r];
         if (R.pack1 > R.pack0)
           HIP_TRY(launch_pack(e->d_ship.as<ShipEntry>(), e->d_pack.as<PackSeg>() + R.pack0, R.pack1 - R.pack0,
                               R.pack_units, e->d_gsegs.as<GhostSeg>(), a.seen, e->d_send.as<uint64_t>(), s),
                   "pack");
-        HIP_TRY(hipEventRecord(e->ev_round, s), "event");
-        HIP_TRY(hipStreamWaitEvent(e->xstream, e->ev_round, 0), "exchange wait");
+        if (xs != s) {
+          HIP_TRY(hipEventRecord(e->ev_round, s), "event");
+          HIP_TRY(hipStreamWaitEvent(xs, e->ev_round, 0), "exchange wait");
+        }
         std::string xerr;
         const uint8_t* sb = e->d_send.as<uint8_t>() + (r & 1) * e->ghost.send_half * 8;
         const hipError_t xe = e->transport->exchange(sb, R.s_off, R.s_len, e->d_recv.as<uint8_t>(), R.r_off,
-                                                     R.r_len, e->xstream, &xerr);
+                                                     R.r_len, xs, &xerr);
         if (xe != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
-        HIP_TRY(hipEventRecord(e->ev_xchg, e->xstream), "event");
+        if (xs != s) HIP_TRY(hipEventRecord(e->ev_xchg, xs), "event");
       }
       if (!lgrid[r] && !xr) {
         if (!upfront) HIP_TRY(seed_round(r, a.a_next), "seed");  // (messages starting this round)
@@ -637,15 +640,17 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       pa.partials = partials + static_cast<size_t>(e->woff_host[r]) * kNumCtr;
       pa.slot_mod = pair ? kPairSlots : kPullSlots;
       if (pair) pa.partials2 = partials + static_cast<size_t>(e->woff_host[r + 1]) * kNumCtr;
-      // the locally fed part, then (after the exchange) the ghost-fed part
-      for (int part = 0; part < 2; ++part) {
-        if (part == 1 && xr) HIP_TRY(hipStreamWaitEvent(s, e->ev_xchg, 0), "exchange join");
+      // the locally fed part, then (after the exchange) the ghost-fed part;
+      // without the overlap (PSAMD_XCHG_OVERLAP=0) one launch after the exchange
+      const bool split = xs != s;
+      for (int part = split ? 0 : 1; part < 2; ++part) {
+        if (part == 1 && xr && split) HIP_TRY(hipStreamWaitEvent(s, e->ev_xchg, 0), "exchange join");
         uint32_t c0, c1;
         if (pair) {
-          c0 = part ? e->pair.gsplit[r] : e->pair.lo[r];
+          c0 = part ? (split ? e->pair.gsplit[r] : e->pair.lo[r]) : e->pair.lo[r];
           c1 = part ? e->pair.hi[r] : e->pair.gsplit[r];
         } else {
-          c0 = part ? e->pull.gsplit[r] : e->pull.off[r];
+          c0 = part ? (split ? e->pull.gsplit[r] : e->pull.off[r]) : e->pull.off[r];
           c1 = part ? e->pull.off[r + 1] : e->pull.gsplit[r];
         }
         if (c1 <= c0) continue;

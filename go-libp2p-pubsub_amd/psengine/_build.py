@@ -12,7 +12,7 @@ LIB = os.path.join(LIBDIR, "libpsengine.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-SOURCES = ["kernels.hip", "flood.hip", "gbuild.hip", "graph.cpp", "plan.cpp", "run.cpp", "api.cpp", "tree.cpp",
+SOURCES = ["kernels.hip", "pull.hip", "flood.hip", "gbuild.hip", "graph.cpp", "plan.cpp", "run.cpp", "api.cpp", "tree.cpp",
            "dist.cpp", "codec.cpp", "pubsub.cpp"]
 HEADERS = ["kernels.hpp", "devutil.hpp", "gbuild.hpp", "tree.hpp", "dist.hpp", "engine.hpp"]
 
@@ -29,12 +29,31 @@ def _stale() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
+    """Each source to an object in parallel (the kernels are launched from
+    their own translation unit, so no relocatable device code), then one
+    link into lib/libpsengine.so."""
     if not force and not _stale():
         return LIB
+    from concurrent.futures import ThreadPoolExecutor
+
     os.makedirs(LIBDIR, exist_ok=True)
-    cmd = [HIPCC, "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           "-I" + os.path.join(REPO, "include"), "-I" + CSRC]
-    cmd += [os.path.join(CSRC, f) for f in SOURCES]
+    objdir = os.path.join(LIBDIR, "obj")
+    os.makedirs(objdir, exist_ok=True)
+    flags = ["-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-Wall",
+             "-I" + os.path.join(REPO, "include"), "-I" + CSRC]
+
+    def compile_one(f):
+        obj = os.path.join(objdir, f + ".o")
+        cmd = [HIPCC] + flags + ["-c", os.path.join(CSRC, f), "-o", obj]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+        return obj
+
+    jobs = max(1, min(len(SOURCES), int(os.environ.get("MAX_JOBS", "0") or 0) or (os.cpu_count() or 4), 16))
+    with ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, SOURCES))
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-fPIC", "-shared"] + objs
     cmd += ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib", "-o", LIB + ".tmp"]
     if verbose:
         print(" ".join(cmd))

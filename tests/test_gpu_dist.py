@@ -61,9 +61,10 @@ def merged_hops(engines, msg):
 @pytest.mark.parametrize("world,partition", [(2, PE.PART_SUBTREE), (3, PE.PART_PEER),
                                              (4, PE.PART_SUBTREE), (4, PE.PART_PEER)])
 def test_sharded_trees_match_oracle(world, partition, staggered):
-    """Staggered starts run the compaction path; a single start round runs
-    level mode (pull kernel + split-parent send + apply stamping reached
-    remote-fed nodes), with dead peers cutting subtrees across ranks."""
+    """Level mode on N ranks, single start round and staggered starts (start
+    groups: one word block per start round, each group's ghost records
+    exchanged in its own rounds), with dead peers cutting subtrees across
+    ranks; never the compaction path."""
     rng = np.random.default_rng(world * 10 + partition + 100 * staggered)
     n, n_topics = 2500, 3
     lb, engines = make_ranks(world, n, n_topics, partition)
@@ -77,6 +78,7 @@ def test_sharded_trees_match_oracle(world, partition, staggered):
         e.set_live(live)
     firsts = [e.publish(topics, starts) for e in engines]
     stats = run_ranks(engines)
+    assert all(st.expand_mode == PE.MODE_LEVEL_PULL for st in stats), [st.expand_mode for st in stats]
     total = 0
     for t in range(n_topics):
         root = int(np.nonzero(trees[t] == O.NONE)[0][0])
@@ -242,3 +244,34 @@ def test_cfg4_shaped_peer_partition(world):
     for e in engines:
         e.close()
     lb.close()
+
+
+@pytest.mark.parametrize("world,partition", [(2, PE.PART_PEER), (4, PE.PART_PEER), (3, PE.PART_SUBTREE)])
+def test_sharded_modes_agree(world, partition):
+    """The same staggered batch on N ranks through level mode (start groups,
+    the exchange beside the local chunks) and through the compaction path
+    (PS_F_COMPACT): identical per-rank hops, deliveries and digests."""
+    rng = np.random.default_rng(77 + world)
+    n, n_topics = 4000, 2
+    trees = [random_tree(rng, n, int(rng.integers(0, n))) for _ in range(n_topics)]
+    live = (rng.random(n) > 0.05).astype(np.uint8)
+    topics = rng.integers(0, n_topics, size=400)
+    starts = rng.integers(0, 6, size=400)
+    out = {}
+    for flags in (0, PE.F_COMPACT):
+        lb, engines = make_ranks(world, n, n_topics, partition, flags=flags)
+        for e in engines:
+            for t in range(n_topics):
+                e.set_tree(t, int(np.nonzero(trees[t] == O.NONE)[0][0]), trees[t])
+            e.set_live(live)
+        firsts = [e.publish(topics, starts) for e in engines]
+        stats = run_ranks(engines)
+        assert all(st.expand_mode == (PE.MODE_COMPACT if flags else PE.MODE_LEVEL_PULL) for st in stats)
+        out[flags] = ([merged_hops(engines, firsts[0] + m) for m in (0, 1, 199, 399)],
+                      sum(st.deliveries for st in stats), sum(e.seen_digest() for e in engines) % (1 << 64))
+        for e in engines:
+            e.close()
+        lb.close()
+    a, b = out[0], out[PE.F_COMPACT]
+    assert all(np.array_equal(x, y) for x, y in zip(a[0], b[0]))
+    assert a[1:] == b[1:]

@@ -26,10 +26,14 @@ ap.add_argument("--workload", default="cfg4")
 ap.add_argument("--scale", type=float, default=0.25)
 ap.add_argument("--partition", default="peer", choices=["peer", "subtree"])
 ap.add_argument("--steps", type=int, default=5)
+ap.add_argument("--staggered", action="store_true",
+                help="start rounds uniform over 0..7 (paced publishing: start groups), both legs")
 args = ap.parse_args()
 part = PE.PART_PEER if args.partition == "peer" else PE.PART_SUBTREE
 wl = WL.CONFIGS[args.workload]() if args.scale == 1.0 else WL.scaled(args.workload, args.scale)
 base_msgs = wl.msg_topics.copy()
+base_starts = ((WL.stream(wl.seed ^ 0x57A6, np.arange(base_msgs.shape[0])) % np.uint64(8)).astype(np.uint32)
+               if args.staggered else None)
 
 # the single-rank step on the same topology and per-rank message count
 t0 = time.perf_counter()
@@ -39,7 +43,7 @@ print(f"[loopback] {wl.name} x{args.scale}: {wl.n_peers} peers, setup {time.perf
 exp1 = wl.expected_deliveries(sizes)
 one_ms = []
 for step in range(args.steps + 1):
-    one.publish(base_msgs)
+    one.publish(base_msgs, base_starts)
     t0 = time.perf_counter()
     st = one.run()
     one_ms.append((time.perf_counter() - t0) * 1e3)
@@ -49,6 +53,7 @@ one.close()
 single = float(np.median(one_ms[1:]))
 
 msgs = np.tile(base_msgs, args.world)
+starts = None if base_starts is None else np.tile(base_starts, args.world)
 lb = PE.Loopback(args.world)
 engs = []
 t0 = time.perf_counter()
@@ -66,7 +71,7 @@ for step in range(args.steps + 1):
 
     def go(r):
         try:
-            engs[r].publish(msgs)
+            engs[r].publish(msgs, starts)
             stats[r] = engs[r].run()
         except Exception as ex:  # noqa: BLE001
             errs.append((r, ex))
