@@ -254,7 +254,7 @@ def kernel_split(st):
             acc[0] += int(st.expand_bytes_per_round[q])
             acc[1] += float(st.expand_ms_per_round[q])
             first = {PE.K_FLOOD: q == 1, PE.K_PULL: int(st.expand_bytes_per_round[q]) > 0,
-                     PE.K_PAIR: True}.get(kinds[q], False)
+                     PE.K_PAIR: True, PE.K_CHAIN: True}.get(kinds[q], False)
             acc[2] += 1 if first else 0
         return {k: tuple(v) for k, v in per.items()}
     if st.expand_mode != PE.MODE_FLOOD or fr >= st.rounds or st.windows != 1:

@@ -103,6 +103,10 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   if (const char* v = std::getenv("PSAMD_PULL_PAIR")) e->pair_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD_PROFILE")) e->flood_profile = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_XCHG_OVERLAP")) e->xchg_overlap = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_REVERSE")) e->alt_reverse = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_CHAIN"))  // rounds per launch at most: 1 (k_pull only), 2 (pairs), 3, 4
+    e->chain_max = static_cast<uint32_t>(std::max(1, std::min(static_cast<int>(kChainLevels), std::atoi(v))));
+  if (const char* v = std::getenv("PSAMD_NT_BYTES")) e->nt_bytes = std::strtoull(v, nullptr, 0);
   if (const char* v = std::getenv("PSAMD_FLOOD_WORDS"))
     e->flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
   if (const char* v = std::getenv("PSAMD_FLOOD_SPIN_TICKS"))  // tests: 0 forces the timeout fallback
@@ -745,6 +749,21 @@ int ps_plan_get(ps_engine* e, uint32_t what, uint32_t index, uint64_t* out, size
       for (uint32_t k = G.rounds[index].pack0; k < G.rounds[index].pack1; ++k) {
         const PackSeg& p = G.pack[k];
         v.insert(v.end(), {p.e0, p.e1, p.gseg, p.W, p.row, p.unit0});
+      }
+      break;
+    }
+    case PS_PLAN_CHAIN: {
+      const PairPlan& P = e->pair;
+      if (index >= P.len.size() || P.len[index] < 3) {
+        v = {0};
+        break;
+      }
+      v = {P.len[index]};
+      for (uint32_t k = P.lo[index]; k < P.hi[index]; ++k) {
+        const ChainChunk& c = P.chain[k];
+        v.insert(v.end(), {c.node_begin, c.node_end, c.topic, c.W, static_cast<uint64_t>(c.row0_hi) << 32 | c.row0_lo,
+                           c.w0, c.S, c.levels, c.r0, c.win, c.group});
+        for (uint32_t f = 0; f <= kChainLevels; ++f) v.push_back(c.first[f]);
       }
       break;
     }

@@ -158,8 +158,10 @@ struct PullPlan {
 struct PairPlan {
   std::vector<uint64_t> key;
   uint64_t version = 0;
-  std::vector<PullChunk> chunks;
-  std::vector<uint32_t> lo, hi, gsplit;  // round q: chunks of the pair launch starting at q
+  std::vector<PullChunk> chunks;         // pair launches
+  std::vector<ChainChunk> chain;         // chain launches
+  std::vector<uint32_t> lo, hi, gsplit;  // round q: chunks (pair) or chain chunks of the launch starting at q
+  std::vector<uint32_t> len;             // round q: rounds of the launch starting at q (0: none)
   std::vector<uint8_t> kind;             // per round: PS_K_*
 };
 struct FloodPlan {
@@ -246,6 +248,10 @@ struct ps_engine {
   // k_pull_pair: rounds q and q + 1 in one launch
   // (PSAMD_PULL_PAIR=0: one k_pull launch per round)
   bool pair_on = true;
+  uint32_t chain_max = psamd::kChainLevels;  // rounds per launch at most (PSAMD_CHAIN: 2 = pairs only)
+  psamd::DevBuf d_chain;
+  bool alt_reverse = false;       // PSAMD_REVERSE=1: consecutive launches run their chunks in opposite orders
+  uint64_t nt_bytes = 64ull << 20;  // rows of rounds writing at least this much store non-temporally (PSAMD_NT_BYTES)
   psamd::PairPlan pair;
   psamd::DevBuf d_pp;
   uint64_t pair_up = ~0ull;

@@ -205,6 +205,13 @@ struct PullArgs {
   // reached, as the generation test of a separate launch would find
   uint64_t* partials2;
   uint32_t all_current;
+  // the launch takes its chunks last to first: it reads first the parent
+  // rows the previous launch (which ran the other way) wrote last
+  uint32_t reverse;
+  // k_pull_chain: the CSR offsets (a run's children are consecutive ids) and
+  // the partial slots of each round of the launch
+  const uint32_t* row_ptr;
+  uint64_t* partials_r[4];
 };
 // k_pull_pair: per wave, a run of at most kPairPar nodes
 // whose rows (at most kPairWords words in all) stay in LDS for its children,
@@ -212,6 +219,36 @@ struct PullArgs {
 constexpr uint32_t kPairWords = 768;  // (1024: 17 resident waves/CU, cfg3 +3 % slower; 512: 1 parent of 330 words)
 constexpr uint32_t kPairPar = 128;
 constexpr uint32_t kPairKids = 256;
+// k_pull_chain: up to kChainLevels rounds in one launch.  A
+// wave owns a run of level-d nodes and a column slice [w0, w0 + S) of their
+// rows (S = W: whole rows); it writes the run (round q, parents' rows from
+// HBM), then every descendant of the run level by level, each copying its
+// parent's slice from the LDS stage the wave wrote one level above -- only
+// the run's parents are read from HBM.  Staged levels are processed in
+// windows of `win` nodes, depth first, so any fan-out fits the stage.
+constexpr uint32_t kChainLevels = 4;
+constexpr uint32_t kChainWords = 1024;  // LDS stage words per wave (the run + one window per inner level)
+constexpr uint32_t kChainKids = 128;    // nodes resolved per sub-run (a window is at most this)
+constexpr uint32_t kChainPar = 128;     // nodes of a run at most
+struct ChainChunk {
+  uint32_t node_begin, node_end;  // the run (level d)
+  uint32_t topic;
+  uint32_t p_lo, p_hi;            // parents of the run (consecutive ids), kNone: unknown
+  uint32_t W;                     // row stride, words
+  uint32_t row0_lo, row0_hi;      // row of the topic's first node (its start group's block)
+  uint16_t w0, S;                 // the column slice of every row
+  uint8_t levels;                 // levels written: d .. d + levels - 1 (rounds r0 + k of the launch)
+  uint8_t r0;                     // the run's round within the launch (a start group entering late: > 0)
+  uint16_t win;                   // nodes per window of an inner staged level
+  // first node of levels d .. d + levels: a run [x0, x1) of level d + k has
+  // the children [row_ptr[x0] - row_ptr[first[k]] + first[k + 1], ...x1...)
+  uint32_t first[kChainLevels + 1];
+  uint32_t group;                 // host: the start group
+};
+hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32_t n_chunks, uint32_t round,
+                             bool record, bool nt, hipStream_t s);
+// ChainChunk::p_lo / p_hi from the device node_parent (GPU-built graphs)
+hipError_t launch_chain_parents(ChainChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s);
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch
 // k_pull_pair: every wave adds its counters with atomics (no block
 // reduction) into slot wave % kPairSlots.  (4096 slots: no faster than 256,

@@ -214,18 +214,19 @@ bool plan_pull_chunks(ps_engine* e, const WindowLayout& L) {
   return true;
 }
 
-// Pair launches (k_pull_pair): one launch writes rounds q
-// and q + 1, each wave a run of level-d nodes and then every child of the run
-// from the rows it holds in LDS, so round q + 1 reads no parent row from HBM.
-// Which rounds pair up is a small dynamic program over the rounds after
-// k_flood's: a pair saves round q + 1's parent-row reads (level d's internal
-// nodes x row bytes) and one launch (priced as kLaunchBytes of traffic).  A
-// round pairs only if each row it writes (and each level-1 row of a start
-// group entering at round q) fits the LDS stage -- and, on N ranks, if
-// neither round q + 1 nor round q + 2 exchanges records (every child of the
-// run is local and nothing written in round q + 1 ships).  Fills pair.kind
-// (PS_K_* per round); cached with the pull chunks and the ghost plan's
-// exchange rounds.
+// Multi-round launches: k_pull_pair writes rounds
+// q and q + 1, k_pull_chain rounds q .. q + L - 1 (L = 3, 4) -- each wave a
+// run of level-d nodes and then every descendant of the run from the rows it
+// holds in LDS, so only round q reads parent rows from HBM.  Which rounds go
+// together is a small dynamic program over the rounds after k_flood's: a
+// launch costs its rows, round q's parent-row reads (level d - 1's internal
+// nodes x row bytes) and kLaunchBytes of launch ramp and tail.  A pair needs
+// each row of round q (and each level-1 row of a start group entering at q)
+// to fit the kPairWords stage; a chain slices wide rows into columns instead.
+// On N ranks a launch spans only rounds whose successors exchange nothing
+// (every child is local and nothing written inside ships), and a chain also
+// needs round q itself exchange-free.  Fills pair.kind (PS_K_* per round);
+// cached with the pull chunks and the ghost plan's exchange rounds.
 bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   const uint32_t rounds = L.planned0;
   const auto& tab = L.tab;
@@ -233,6 +234,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   std::vector<uint64_t> key = e->pull.key;  // (graph, flags, rounds, row widths, start groups)
   key.push_back(first);
   key.push_back(e->pair_on ? 1 : 0);
+  key.push_back(e->chain_max);
   for (size_t q = 0; q < xchg.size(); ++q) key.push_back(xchg[q].any);
   PairPlan& PP = e->pair;
   if (key == PP.key) return false;
@@ -240,15 +242,16 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   constexpr uint32_t stage = kPairWords;
   constexpr double kLaunchBytes = 16e6;  // ~3 us of launch ramp and tail at ~5.5 TB/s (64, 200 MB: same plan on cfg3)
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
+  const uint32_t max_len = e->pair_on ? std::max<uint32_t>(1, std::min<uint32_t>(e->chain_max, kChainLevels)) : 1;
   auto& kind = PP.kind;
   kind.assign(rounds + 2, PS_K_NONE);
   for (uint32_t q = 1; q <= first && q <= rounds; ++q) kind[q] = PS_K_FLOOD;
   auto exch = [&](uint32_t q) { return q < xchg.size() && xchg[q].any; };
-  // per round: parent-row bytes read (estimate), and whether it can pair
+  // per round: parent-row bytes read (estimate), and whether a pair fits
   std::vector<double> rd(rounds + 2, 0.0);
-  std::vector<uint8_t> can(rounds + 2, 0);
+  std::vector<uint8_t> can2(rounds + 2, 0);
   for (uint32_t q = first + 1; q <= rounds; ++q) {
-    bool ok = e->pair_on && q + 1 <= rounds && !exch(q + 1) && !exch(q + 2);
+    bool ok = max_len >= 2 && q + 1 <= rounds && !exch(q + 1) && !exch(q + 2);
     for (uint32_t t = 0; t < nt; ++t) {
       const TopicHost& T = e->topics[t];
       if (tab[t].W == 0) continue;
@@ -265,36 +268,108 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
         }
       }
     }
-    can[q] = ok;
+    can2[q] = ok;
   }
-  // best[q]: traffic of rounds q..rounds
-  std::vector<double> best(rounds + 3, 0.0);
-  std::vector<uint8_t> take(rounds + 2, 0);
-  auto cost = [&](uint32_t q) {
-    const double b = static_cast<double>(e->pull.bytes[q]);
-    return b + rd[q] + (b > 0 ? kLaunchBytes : 0.0);
+  auto can = [&](uint32_t q, uint32_t len) {
+    if (len == 1) return true;
+    if (len == 2) return static_cast<bool>(can2[q]);
+    if (len > max_len || q + len - 1 > rounds || exch(q)) return false;
+    for (uint32_t k = 1; k <= len; ++k)
+      if (exch(q + k)) return false;
+    return true;
   };
+  // best[q]: traffic of rounds q..rounds; take[q]: rounds of the launch starting at q
+  std::vector<double> best(rounds + 6, 0.0);
+  std::vector<uint8_t> take(rounds + 2, 1);
   for (uint32_t q = rounds; q > first; --q) {
-    best[q] = cost(q) + best[q + 1];
-    if (can[q]) {
-      const double wb = static_cast<double>(e->pull.bytes[q]) + static_cast<double>(e->pull.bytes[q + 1]);
-      const double pc = wb + rd[q] + kLaunchBytes + best[q + 2];
-      if (pc < best[q]) {
-        best[q] = pc;
-        take[q] = 1;
+    best[q] = 1e300;
+    double wb = 0;
+    for (uint32_t len = 1; len <= std::min<uint32_t>(4, rounds - q + 1); ++len) {
+      wb += static_cast<double>(e->pull.bytes[q + len - 1]);
+      if (!can(q, len)) continue;
+      const double c = wb + rd[q] + (wb > 0 ? kLaunchBytes : 0.0) + best[q + len];
+      if (c < best[q]) {
+        best[q] = c;
+        take[q] = static_cast<uint8_t>(len);
       }
     }
   }
   auto& C = PP.chunks;
   C.clear();
+  PP.chain.clear();
   PP.lo.assign(rounds + 2, 0);
   PP.hi.assign(rounds + 2, 0);
   PP.gsplit.assign(rounds + 2, 0);
+  PP.len.assign(rounds + 2, 0);
   const bool gpu = e->gpu_graph;
   std::vector<PullChunk> ghost;
   for (uint32_t q = first + 1; q <= rounds; ++q) {
-    if (!take[q]) {
+    const uint32_t len = take[q];
+    if (len == 1) {
       kind[q] = e->pull.bytes[q] ? PS_K_PULL : PS_K_NONE;
+      continue;
+    }
+    PP.len[q] = len;
+    if (len >= 3) {
+      kind[q] = PS_K_CHAIN;
+      for (uint32_t k = 1; k < len; ++k) kind[q + k] = PS_K_CHAIN2;
+      PP.lo[q] = static_cast<uint32_t>(PP.chain.size());
+      for (uint32_t t = 0; t < nt; ++t) {
+        const TopicHost& T = e->topics[t];
+        if (tab[t].W == 0) continue;
+        for (uint32_t gi = 0; gi < L.groups[t].size(); ++gi) {
+          const StartGroup& g = L.groups[t][gi];
+          const uint32_t W = block_w(tab[t], g);
+          // the group's level written in round q (r0 = 0), or its level 1 when
+          // it enters inside the launch (round q + r0)
+          uint32_t d, r0;
+          if (q >= g.start + 1) {
+            d = q - g.start;
+            r0 = 0;
+          } else if (g.start + 1 < q + len) {
+            d = 1;
+            r0 = g.start + 1 - q;
+          } else {
+            continue;
+          }
+          if (d > T.depth || d + 1 >= T.level_off.size()) continue;
+          const uint32_t levels = std::min(len - r0, T.depth - d + 1);
+          // column slices: the run and one window per inner level of at least
+          // kMinNodes nodes each fit the kChainWords stage
+          constexpr uint32_t kMinNodes = 4;
+          const uint32_t staged = std::max<uint32_t>(1, levels - 1);  // levels held in LDS at once
+          uint32_t S = W;
+          if (W * kMinNodes * staged > kChainWords) S = std::max<uint32_t>(2, (kChainWords / (kMinNodes * staged)) & ~1u);
+          const uint32_t budget = kChainWords / S;  // nodes the stage holds
+          const uint32_t n0 = std::max<uint32_t>(1, std::min<uint32_t>(kChainPar, levels > 2 ? budget / staged : budget));
+          const uint32_t win = levels > 2 ? std::max<uint32_t>(1, std::min<uint32_t>(kChainKids, budget / staged)) : 0;
+          const uint64_t row0 = block_row0(tab[t], g);
+          const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
+          for (uint32_t u = lo; u < hi; u += n0)
+            for (uint32_t w0 = 0; w0 < W; w0 += S) {
+              ChainChunk c{};
+              c.node_begin = T.nbase + u;
+              c.node_end = T.nbase + std::min(u + n0, hi);
+              c.topic = t;
+              c.p_lo = gpu ? kNone : e->node_parent[c.node_begin];
+              c.p_hi = gpu ? kNone : e->node_parent[c.node_end - 1];
+              c.W = W;
+              c.row0_lo = static_cast<uint32_t>(row0);
+              c.row0_hi = static_cast<uint32_t>(row0 >> 32);
+              c.w0 = static_cast<uint16_t>(w0);
+              c.S = static_cast<uint16_t>(std::min(S, W - w0));
+              c.levels = static_cast<uint8_t>(levels);
+              c.r0 = static_cast<uint8_t>(r0);
+              c.win = static_cast<uint16_t>(win);
+              for (uint32_t k = 0; k <= levels && k <= kChainLevels; ++k) c.first[k] = T.nbase + T.level_off[d + k];
+              c.group = gi;
+              PP.chain.push_back(c);
+            }
+        }
+      }
+      PP.hi[q] = static_cast<uint32_t>(PP.chain.size());
+      PP.gsplit[q] = PP.hi[q];
+      q += len - 1;
       continue;
     }
     kind[q] = PS_K_PAIR;
@@ -652,7 +727,7 @@ void annotate_chunks(ps_engine* e, const WindowLayout& L) {
   for (uint32_t q = 1; q <= rounds && q + 1 < P.off.size(); ++q) annotate(P.chunks, P.off[q], P.off[q + 1], q, true);
   PairPlan& PP = e->pair;
   for (uint32_t q = 1; q < PP.lo.size(); ++q)
-    if (PP.hi[q] > PP.lo[q]) annotate(PP.chunks, PP.lo[q], PP.hi[q], q, false);
+    if (PP.len[q] == 2 && PP.hi[q] > PP.lo[q]) annotate(PP.chunks, PP.lo[q], PP.hi[q], q, false);
   ++P.version;
   ++PP.version;
 }

@@ -341,8 +341,8 @@ __global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __
   uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds[wid]);
   const uint32_t cur = a.gen_cur & 0xFF;
   PullCtr c;
-  if (wave < n_chunks) {  // one chunk per wave
-    const PullChunk ch = chunks[wave];
+  if (wave < n_chunks) {  // one chunk per wave (reverse: the last chunk first)
+    const PullChunk ch = chunks[a.reverse ? n_chunks - 1 - wave : wave];
     const TopicDev T = a.topics[ch.topic];
     PullTopic P;
     P.W = ch.W;
@@ -534,7 +534,7 @@ __global__ __launch_bounds__(64) void k_pull_pair(PullArgs a, const PullChunk* _
   if (lane < 2) rows[kPairWords + lane] = 0;
   WaveCtr c, c2;
   for (uint32_t ci = blockIdx.x; ci < n_chunks; ci += gridDim.x) {
-    const PullChunk ch = chunks[ci];
+    const PullChunk ch = chunks[a.reverse ? n_chunks - 1 - ci : ci];
     const TopicDev T = a.topics[ch.topic];
     PullTopic P;
     P.W = ch.W;
@@ -631,6 +631,308 @@ __global__ __launch_bounds__(kBlock) void k_chunk_parents(PullChunk* __restrict_
   c.p_hi = node_parent[c.node_end - 1];
 }
 
+// ------------------------------------------------------------- pull chain ---
+// k_pull_chain: kChainLevels rounds at most per launch.  A
+// wave owns a run of level-d nodes and a column slice [w0, w0 + S) of their
+// rows.  Level 0 (round q): the run resolves its parents from this window's
+// generation bytes (as k_pull) and streams the slices of their rows from HBM
+// into its own rows and the LDS stage.  Level k >= 1 (round q + k): the
+// children of the level above's current window -- consecutive ids, found
+// from row_ptr -- copy their parent's slice from the stage iff the parent was
+// reached (an LDS reach bit) and they are live; an inner level is staged in
+// windows of `win` nodes, each window's children handled before the next
+// window (depth first), so the stage holds the run plus one window per inner
+// level whatever the fan-out.  An unreached node's slice is written with
+// zeros (stale under its old generation byte, never read).  Slices are
+// independent (a row is copied word for word), so the waves of one run's
+// slices agree on every reach decision; only the slice-0 wave stamps
+// generations and counts nodes.
+struct ChainStep {
+  uint64_t base;   // row of node u = base + u * W (+ w0)
+  uint32_t W, w0, S, nbase;
+  bool slice0;
+};
+
+// The element split of a slice stream: element i of a run of nodes with S
+// words each -> (node kk, word r), branch-free (float estimate off by at most
+// one; i < 2^24).
+__device__ __forceinline__ void chain_split(uint32_t i, float rs, uint32_t S, int32_t& kk, int32_t& r) {
+  kk = static_cast<int32_t>(static_cast<float>(i) * rs);
+  r = static_cast<int32_t>(i) - kk * static_cast<int32_t>(S);
+  const int32_t lo = r < 0, hi = r >= static_cast<int32_t>(S);
+  kk += hi - lo;
+  r += (lo - hi) * static_cast<int32_t>(S);
+}
+
+// Streams nk nodes' slices [y0, y0 + nk): element (kk, r) = source slot
+// tab[kk] (LDS offset into `stage`, kZero: zeros) + r -- or, level 0, the
+// parent row address src64[kk] (0: rewrite the node's own words) -- into the
+// node's row in HBM and, when dst != kNone, the stage at dst + kk * S + r.
+// 16-B units (even S) or words; lanes past the end repeat the last unit.
+template <bool kRecord, bool kNT, bool kFromHbm>
+__device__ __forceinline__ void chain_stream(const PullArgs& a, const ChainStep& C, uint32_t y0, uint32_t nk,
+                                             const uint32_t* tab, const uint64_t* src64, uint64_t* stage,
+                                             uint32_t dst, uint32_t lane, uint32_t round, WaveCtr& c) {
+  constexpr uint32_t kU = 8;
+  constexpr uint32_t kZero = kChainWords;
+  const uint32_t S = C.S, W = C.W;
+  const uint32_t total = nk * S;
+  if (total == 0) return;
+  uint64_t* const out = a.seen + C.base + static_cast<uint64_t>(y0) * W + C.w0;
+  const float rs = 1.0f / static_cast<float>(S);
+  if (!(S & 1u)) {
+    for (uint32_t i0 = 0; i0 < total; i0 += kU * 128) {
+      uint4 x[kU];
+      bool go[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t is = i0 + u * 128 + 2 * lane;
+        const uint32_t i = is < total ? is : total - 2;
+        int32_t kk, r;
+        chain_split(i, rs, S, kk, r);
+        const uint64_t* q;
+        if constexpr (kFromHbm) {
+          const uint64_t row = src64[kk];
+          go[u] = row != 0;
+          q = go[u] ? reinterpret_cast<const uint64_t*>(row) + C.w0 + r : out + static_cast<uint64_t>(kk) * W + r;
+        } else {
+          const uint32_t off = tab[kk];
+          go[u] = off != kZero;
+          q = stage + (go[u] ? off + r : kZero);
+        }
+        x[u] = *reinterpret_cast<const uint4*>(q);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t is = i0 + u * 128 + 2 * lane;
+        const bool inr = is < total;
+        const uint32_t i = inr ? is : total - 2;
+        int32_t kk, r;
+        chain_split(i, rs, S, kk, r);
+        uint64_t* o = out + static_cast<uint64_t>(kk) * W + r;
+        if constexpr (kRecord) {
+          if (go[u] && inr) {
+            *reinterpret_cast<uint4*>(o) = x[u];
+            const uint64_t cw = o - a.seen;
+            record_word(a.hop_rec, cw, static_cast<uint64_t>(x[u].y) << 32 | x[u].x, round);
+            record_word(a.hop_rec, cw + 1, static_cast<uint64_t>(x[u].w) << 32 | x[u].z, round);
+          } else if (!kFromHbm && inr) {
+            *reinterpret_cast<uint4*>(o) = x[u];  // (zeros of an unreached node)
+          }
+        } else {
+          store_row16<kNT>(o, x[u]);
+        }
+        if (dst != kNoneNode) *reinterpret_cast<uint4*>(stage + dst + kk * S + r) = x[u];
+        ctr_unit(c, go[u] && inr, popc4(x[u]), 2u);
+      }
+    }
+  } else {
+    for (uint32_t i0 = 0; i0 < total; i0 += kU * 64) {
+      uint64_t m[kU];
+      bool go[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t is = i0 + u * 64 + lane;
+        const uint32_t i = is < total ? is : total - 1;
+        int32_t kk, r;
+        chain_split(i, rs, S, kk, r);
+        const uint64_t* q;
+        if constexpr (kFromHbm) {
+          const uint64_t row = src64[kk];
+          go[u] = row != 0;
+          q = go[u] ? reinterpret_cast<const uint64_t*>(row) + C.w0 + r : out + static_cast<uint64_t>(kk) * W + r;
+        } else {
+          const uint32_t off = tab[kk];
+          go[u] = off != kZero;
+          q = stage + (go[u] ? off + r : kZero);
+        }
+        m[u] = *q;
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t is = i0 + u * 64 + lane;
+        const bool inr = is < total;
+        const uint32_t i = inr ? is : total - 1;
+        int32_t kk, r;
+        chain_split(i, rs, S, kk, r);
+        uint64_t* o = out + static_cast<uint64_t>(kk) * W + r;
+        if constexpr (kRecord) {
+          if (go[u] && inr) {
+            *o = m[u];
+            record_word(a.hop_rec, o - a.seen, m[u], round);
+          } else if (!kFromHbm && inr) {
+            *o = m[u];
+          }
+        } else {
+          store_row8<kNT>(o, m[u]);
+        }
+        if (dst != kNoneNode) stage[dst + kk * S + r] = m[u];
+        ctr_unit(c, go[u] && inr, static_cast<uint32_t>(__popcll(m[u])), 1u);
+      }
+    }
+  }
+}
+
+// One sub-run of an inner level: the nodes [y0, y0 + nk) (<= kChainKids),
+// children of the window [x0, ...) staged at src_base: resolve each node's
+// parent slot into tab (kZero: unreached or dead), stamp generations
+// (slice 0), reach bits of the sub-run into reach_out (when staged).
+__device__ __forceinline__ void chain_resolve(const PullArgs& a, const ChainStep& C, uint32_t x0,
+                                              const uint64_t* reach_in, uint32_t src_base, uint32_t y0, uint32_t nk,
+                                              uint32_t* tab, uint64_t* reach_out, uint32_t lane, uint32_t cur,
+                                              WaveCtr& c) {
+  constexpr uint32_t kZero = kChainWords;
+  for (uint32_t j0 = 0; j0 < nk; j0 += 64) {
+    const uint32_t j = j0 + lane;
+    const bool in = j < nk;
+    uint32_t p = kNoneNode, f = 0;
+    if (in) {
+      p = a.node_parent[y0 + j];
+      f = a.node_flags[y0 + j];
+    }
+    const uint32_t kp = p - x0;  // the parent's place in its window
+    const bool up = in && ((a.all_current & 1u) || ((reach_in[kp >> 6] >> (kp & 63)) & 1ull));
+    const bool ok = up && (f & kNodeLive);
+    if (in) tab[j] = ok ? src_base + kp * C.S : kZero;
+    if (ok && C.slice0) a.gen[y0 + j] = static_cast<uint8_t>(cur);
+    const uint64_t b = __ballot(ok);
+    if (reach_out && lane == 0) reach_out[j0 >> 6] = b;
+    uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
+    if (lane == 0) prev = y0 + j0 > C.nbase ? a.node_parent[y0 + j0 - 1] : kNoneNode;
+    // nodes and parents counted once per run (slice 0); words per slice (the
+    // parents' slices come from LDS: no parent words read)
+    ctr_nodes(c, in && C.slice0, ok && C.slice0, up && p != prev && C.slice0, C.S, 0u);
+    if (!C.slice0) c.sw += static_cast<uint64_t>(__popcll(b)) * C.S;
+  }
+}
+
+// children of the consecutive nodes [x0, x1) of level k (k < levels): a
+// consecutive range of level k + 1
+__device__ __forceinline__ void chain_kids(const PullArgs& a, const ChainChunk& ch, uint32_t k, uint32_t rp_base,
+                                           uint32_t x0, uint32_t x1, uint32_t& c0, uint32_t& c1) {
+  c0 = a.row_ptr[x0] - rp_base + ch.first[k + 1];
+  c1 = a.row_ptr[x1] - rp_base + ch.first[k + 1];
+}
+
+__device__ __forceinline__ void chain_flush(WaveCtr& c, uint64_t* partials, uint64_t slot, uint32_t lane) {
+  ctr_fold(c);
+  const uint64_t v7[7] = {c.dsum, c.sw, c.kids, c.reached, c.parents, c.pwords, 0ull};
+  if (partials && lane < kNumCtr) {
+    const uint64_t v = pull_ctr_pick(v7, lane);
+    if (v) atomicAdd(reinterpret_cast<unsigned long long*>(partials + slot * kNumCtr + lane),
+                     static_cast<unsigned long long>(v));
+  }
+  c = WaveCtr{};
+}
+
+__global__ __launch_bounds__(kBlock) void k_chain_parents(ChainChunk* __restrict__ chunks, uint32_t n,
+                                                          const uint32_t* __restrict__ node_parent) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  ChainChunk& c = chunks[i];
+  c.p_lo = node_parent[c.node_begin];
+  c.p_hi = node_parent[c.node_end - 1];
+}
+
+template <bool kRecord, bool kNT>
+__global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk* __restrict__ chunks,
+                                                   uint32_t n_chunks, uint32_t round) {
+  __shared__ uint64_t stage[kChainWords + 2];       // the run, then one window per inner level; + a zero pair
+  __shared__ uint64_t src[kChainPar];               // level 0: the parents' row addresses
+  __shared__ uint32_t tab[kChainKids];              // an inner sub-run's stage offsets
+  __shared__ uint32_t gen_lds[kChainPar / 4 + 2];
+  __shared__ uint64_t reach[kChainLevels - 1][kChainKids / 64];  // reach bits: the run, each inner window
+  const uint32_t lane = threadIdx.x;
+  uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds);
+  const uint32_t cur = a.gen_cur & 0xFF;
+  if (lane < 2) stage[kChainWords + lane] = 0;
+  const uint32_t ci = blockIdx.x;
+  if (ci >= n_chunks) return;
+  const ChainChunk ch = chunks[a.reverse ? n_chunks - 1 - ci : ci];
+  const TopicDev T = a.topics[ch.topic];
+  ChainStep C;
+  C.W = ch.W;
+  C.w0 = ch.w0;
+  C.S = ch.S;
+  C.nbase = T.nbase;
+  C.base = (static_cast<uint64_t>(ch.row0_hi) << 32 | ch.row0_lo) - static_cast<uint64_t>(T.nbase) * ch.W;
+  C.slice0 = ch.w0 == 0;
+  const uint32_t levels = ch.levels;
+  const uint32_t n0 = ch.node_end - ch.node_begin;  // <= kChainPar (host plan)
+  const uint32_t win = ch.win;
+  const uint32_t base1 = n0 * C.S, base2 = base1 + win * C.S;  // inner windows' stage offsets
+  uint64_t* const slot_ptr[kChainLevels] = {a.partials_r[0], a.partials_r[1], a.partials_r[2], a.partials_r[3]};
+  const uint64_t slot = blockIdx.x % a.slot_mod;
+  WaveCtr c;
+  // level 0: the run, parents' slices from HBM
+  {
+    PullTopic P;
+    P.W = ch.W;
+    P.nbase = T.nbase;
+    P.base = C.base;
+    P.root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
+    PullCtr pc;
+    pull_resolve(a, P, ch.node_begin, n0, ch.p_lo, ch.p_hi, src, genl, lane, cur, pc, kNoneNode, kChainPar);
+    // (pull_resolve stamps generations and counts whole rows: slice 0 keeps
+    // its node counts, every slice its own words)
+    const uint32_t nodes = __reduce_add_sync(~0ull, pc.kids), hit = __reduce_add_sync(~0ull, pc.reached);
+    const uint32_t par = __reduce_add_sync(~0ull, pc.parents);
+    if (C.slice0) {
+      c.kids += __builtin_amdgcn_readfirstlane(nodes);
+      c.reached += __builtin_amdgcn_readfirstlane(hit);
+      c.parents += __builtin_amdgcn_readfirstlane(par);
+    }
+    c.sw += static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(hit)) * C.S;
+    c.pwords += static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(par)) * C.S;
+    for (uint32_t j0 = 0; j0 < n0; j0 += 64) {
+      const uint64_t b = __ballot(j0 + lane < n0 && src[j0 + lane] != 0);
+      if (lane == 0) reach[0][j0 >> 6] = b;
+    }
+    chain_stream<kRecord, kNT, true>(a, C, ch.node_begin, n0, nullptr, src, stage, levels > 1 ? 0u : kNoneNode, lane,
+                                     round + ch.r0, c);
+    chain_flush(c, slot_ptr[ch.r0], slot, lane);
+  }
+  if (levels < 2) return;
+  asm volatile("" ::: "memory");
+  const uint32_t rp1 = a.row_ptr[ch.first[0]];
+  uint32_t c1_0, c1_1;
+  chain_kids(a, ch, 0, rp1, ch.node_begin, ch.node_end, c1_0, c1_1);
+  const uint32_t step1 = levels > 2 ? win : kChainKids;
+  WaveCtr c1, c2, c3;
+  const uint32_t rp2 = levels > 2 ? a.row_ptr[ch.first[1]] : 0u;
+  const uint32_t rp3 = levels > 3 ? a.row_ptr[ch.first[2]] : 0u;
+  for (uint32_t y0 = c1_0; y0 < c1_1; y0 += step1) {
+    const uint32_t ny = min(step1, c1_1 - y0);
+    chain_resolve(a, C, ch.node_begin, reach[0], 0u, y0, ny, tab, levels > 2 ? reach[1] : nullptr, lane, cur, c1);
+    chain_stream<kRecord, kNT, false>(a, C, y0, ny, tab, nullptr, stage, levels > 2 ? base1 : kNoneNode, lane,
+                                      round + ch.r0 + 1, c1);
+    ctr_fold(c1);
+    if (levels < 3) continue;
+    uint32_t c2_0, c2_1;
+    chain_kids(a, ch, 1, rp2, y0, y0 + ny, c2_0, c2_1);
+    const uint32_t step2 = levels > 3 ? win : kChainKids;
+    for (uint32_t z0 = c2_0; z0 < c2_1; z0 += step2) {
+      const uint32_t nz = min(step2, c2_1 - z0);
+      chain_resolve(a, C, y0, reach[1], base1, z0, nz, tab, levels > 3 ? reach[2] : nullptr, lane, cur, c2);
+      chain_stream<kRecord, kNT, false>(a, C, z0, nz, tab, nullptr, stage, levels > 3 ? base2 : kNoneNode, lane,
+                                        round + ch.r0 + 2, c2);
+      ctr_fold(c2);
+      if (levels < 4) continue;
+      uint32_t c3_0, c3_1;
+      chain_kids(a, ch, 2, rp3, z0, z0 + nz, c3_0, c3_1);
+      for (uint32_t u0 = c3_0; u0 < c3_1; u0 += kChainKids) {
+        const uint32_t nu = min(kChainKids, c3_1 - u0);
+        chain_resolve(a, C, z0, reach[2], base2, u0, nu, tab, nullptr, lane, cur, c3);
+        chain_stream<kRecord, kNT, false>(a, C, u0, nu, tab, nullptr, stage, kNoneNode, lane, round + ch.r0 + 3, c3);
+        ctr_fold(c3);
+      }
+    }
+  }
+  chain_flush(c1, slot_ptr[ch.r0 + 1], slot, lane);
+  if (levels > 2) chain_flush(c2, slot_ptr[ch.r0 + 2], slot, lane);
+  if (levels > 3) chain_flush(c3, slot_ptr[ch.r0 + 3], slot, lane);
+}
+
 }  // namespace
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
                        uint32_t grid, uint32_t round, bool record, bool nt, bool cap, hipStream_t s) {
@@ -681,6 +983,25 @@ hipError_t launch_pack(const ShipEntry* ship, const PackSeg* segs, uint32_t n_se
 hipError_t launch_chunk_parents(PullChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_chunk_parents, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, chunks, n, node_parent);
+  return hipGetLastError();
+}
+
+
+hipError_t launch_chain_parents(ChainChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_chain_parents, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, chunks, n, node_parent);
+  return hipGetLastError();
+}
+
+hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32_t n_chunks, uint32_t round,
+                             bool record, bool nt, hipStream_t s) {
+  if (n_chunks == 0) return hipSuccess;
+  if (record)
+    hipLaunchKernelGGL((k_pull_chain<true, false>), dim3(n_chunks), dim3(64), 0, s, a, chunks, n_chunks, round);
+  else if (nt)
+    hipLaunchKernelGGL((k_pull_chain<false, true>), dim3(n_chunks), dim3(64), 0, s, a, chunks, n_chunks, round);
+  else
+    hipLaunchKernelGGL((k_pull_chain<false, false>), dim3(n_chunks), dim3(64), 0, s, a, chunks, n_chunks, round);
   return hipGetLastError();
 }
 

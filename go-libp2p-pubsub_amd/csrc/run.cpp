@@ -45,6 +45,16 @@ int upload_pair(ps_engine* e) {
                              e->d_col.as<uint32_t>(), e->stream),
             "pair chunk children");
   }
+  const auto& K = e->pair.chain;
+  HIP_TRY(e->d_chain.ensure(std::max<size_t>(K.size(), 1) * sizeof(ChainChunk)), "alloc chain chunks");
+  if (!K.empty()) {
+    HIP_TRY(hipMemcpyAsync(e->d_chain.p, K.data(), K.size() * sizeof(ChainChunk), hipMemcpyHostToDevice, e->stream),
+            "upload chain chunks");
+    if (e->gpu_graph)
+      HIP_TRY(launch_chain_parents(e->d_chain.as<ChainChunk>(), static_cast<uint32_t>(K.size()),
+                                   e->d_node_parent.as<uint32_t>(), e->stream),
+              "chain chunk parents");
+  }
   e->pair_up = e->pair.version;
   return PS_OK;
 }
@@ -340,17 +350,20 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     woff.assign(planned0 + 2, 0);
     woff[flood_rounds + 1] = slot;
     for (uint32_t q = flood_rounds + 1; q <= planned0; ++q) {
-      const bool pair = e->round_kind[q] == PS_K_PAIR;
-      lgrid[q] = pair ? e->pair.hi[q] - e->pair.lo[q]  // (one one-wave workgroup per chunk)
-                      : ceil_div(e->pull.gsplit[q] - e->pull.off[q], kBlock / 64) +
-                            ceil_div(e->pull.off[q + 1] - e->pull.gsplit[q], kBlock / 64);
-      for (uint32_t k = q; k <= q + (pair ? 1u : 0u); ++k) {  // a pair launch: the same slots for both rounds
-        woff[k + 1] = woff[k] + std::min<uint32_t>(lgrid[q], pair ? kPairSlots : kPullSlots);
+      const uint8_t kq = e->round_kind[q];
+      const bool multi_round = kq == PS_K_PAIR || kq == PS_K_CHAIN;
+      const uint32_t len = multi_round ? e->pair.len[q] : 1u;
+      lgrid[q] = multi_round ? e->pair.hi[q] - e->pair.lo[q]  // (one one-wave workgroup per chunk)
+                             : ceil_div(e->pull.gsplit[q] - e->pull.off[q], kBlock / 64) +
+                                   ceil_div(e->pull.off[q + 1] - e->pull.gsplit[q], kBlock / 64);
+      for (uint32_t k = q; k < q + len; ++k) {  // a multi-round launch: one slot range per round
+        woff[k + 1] = woff[k] + std::min<uint32_t>(lgrid[q], multi_round ? kPairSlots : kPullSlots);
         desc[3 * k] = woff[k];
         desc[3 * k + 1] = woff[k + 1];
         desc[3 * k + 2] = 1;
       }
-      if (pair) lgrid[++q] = 0;
+      for (uint32_t k = 1; k < len; ++k) lgrid[q + k] = 0;
+      q += len - 1;
     }
     n_slots = woff[planned0 + 1];
     HIP_TRY(e->d_partials.ensure(static_cast<size_t>(std::max<uint32_t>(n_slots, 1)) * kNumCtr * 8),
@@ -548,7 +561,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     // blocks of later start rounds included -- a block is read only in its
     // own rounds
     bool pairs = false;
-    for (uint32_t q = 1; q <= planned0; ++q) pairs |= e->round_kind[q] == PS_K_PAIR;
+    for (uint32_t q = 1; q <= planned0; ++q) pairs |= e->round_kind[q] == PS_K_PAIR || e->round_kind[q] == PS_K_CHAIN;
     const bool upfront = flood || L.multi || pairs;  // (a pair launch's plain level-1 runs read roots)
     if (upfront && max_start > 0)
       HIP_TRY(launch_seed(e->d_seeds.as<SeedDev>(), seed_off[1], seed_off[max_start + 1], arr[0], a.seen, nullptr,
@@ -599,9 +612,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     pa.ship = world > 1 ? e->d_ship.as<ShipEntry>() : nullptr;
     pa.send = e->d_send.as<uint64_t>();
     pa.all_current = (e->cfg.flags & PS_F_NO_LAZY_SEEN) ? 1u : 0u;
+    uint32_t dir = 1;  // the first launch after k_flood runs forward
     for (r = flood_rounds + 1; r <= planned0; ++r) {
       const uint8_t kind = e->round_kind[r];
-      if (kind == PS_K_PAIR2) continue;  // written by the pair launch of round r - 1
+      if (kind == PS_K_PAIR2 || kind == PS_K_CHAIN2) continue;  // written by the launch of an earlier round
       a.a_cur = upfront ? arr[0] : arr[(r - 1) & 1];
       a.a_next = arr[r & 1];
       pa.a_cur = a.a_cur;
@@ -633,10 +647,31 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         continue;
       }
       const bool pair = kind == PS_K_PAIR;
+      if (kind == PS_K_CHAIN) {  // rounds r .. r + len - 1 in one launch (one rank, or no exchange inside)
+        const uint32_t len = e->pair.len[r];
+        const uint32_t last = r + len - 1;
+        const bool ntc = last == planned0 || (last < e->pull.bytes.size() && e->pull.bytes[last] >= e->nt_bytes);
+        pa.slot_mod = kPairSlots;
+        pa.row_ptr = e->d_row_ptr.as<uint32_t>();
+        for (uint32_t k = 0; k < kChainLevels; ++k)
+          pa.partials_r[k] = k < len ? partials + static_cast<size_t>(e->woff_host[r + k]) * kNumCtr : nullptr;
+        pa.reverse = 0;
+        HIP_TRY(time_mark(true), "event");
+        ++launches;
+        HIP_TRY(launch_pull_chain(pa, e->d_chain.as<ChainChunk>() + e->pair.lo[r], e->pair.hi[r] - e->pair.lo[r], r,
+                                  record, ntc, s),
+                "pull chain");
+        HIP_TRY(time_mark(false), "event");
+        if (xr) HIP_TRY(hipStreamWaitEvent(s, e->ev_xchg, 0), "exchange join");  // (never: chains skip exchange rounds)
+        continue;
+      }
       // rows nobody re-reads while they can still sit in the 256 MB MALL
       // (large rounds and the last round) store non-temporally
       const uint32_t rw = pair ? r + 1 : r;  // the round whose rows the next launch reads
-      const bool nt = rw < e->pull.bytes.size() && (e->pull.bytes[rw] >= (64ull << 20) || rw == planned0);
+      const bool nt = rw < e->pull.bytes.size() && (e->pull.bytes[rw] >= e->nt_bytes || rw == planned0);
+      // alternate directions: each launch starts with the parents the one
+      // before it wrote last (PSAMD_REVERSE=0: always forward)
+      pa.reverse = e->alt_reverse ? (dir ^= 1u) : 0u;
       pa.partials = partials + static_cast<size_t>(e->woff_host[r]) * kNumCtr;
       pa.slot_mod = pair ? kPairSlots : kPullSlots;
       if (pair) pa.partials2 = partials + static_cast<size_t>(e->woff_host[r + 1]) * kNumCtr;
@@ -905,7 +940,8 @@ bool accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uin
                // launch: no parent generation, its parents' reach and rows are in LDS),
                // per reached node its generation write 1; parent rows read once (from
                // HBM: none in a pair's second round); rows written
-      b = c[kCtrChildren] * (kind == PS_K_FLOOD ? 7 : kind == PS_K_PAIR2 ? 5 : 6) + c[kCtrMeshChildren] * 1 +
+      b = c[kCtrChildren] * (kind == PS_K_FLOOD ? 7 : (kind == PS_K_PAIR2 || kind == PS_K_CHAIN2) ? 5 : 6) +
+          c[kCtrMeshChildren] * 1 +
           c[kCtrEntryWords] * 8 + c[kCtrSeenWrites] * 8;
     else
       b = c[kCtrEntries] * 18 + c[kCtrEntryWords] * 8 + c[kCtrClearWords] * 8 + c[kCtrChildren] * 3 +

@@ -31,9 +31,9 @@ F_COMPACT = 0x8
 MODE_COMPACT, MODE_LEVEL_PULL, MODE_FLOOD = 0, 2, 3
 # ps_stats.expand_mode -> the kernel that ran the window's rounds
 # ps_stats.round_kernel: the launch kind that wrote each round
-K_NONE, K_FLOOD, K_PULL, K_PAIR, K_PAIR2, K_EXPAND = 0, 1, 2, 3, 4, 5
+K_NONE, K_FLOOD, K_PULL, K_PAIR, K_PAIR2, K_EXPAND, K_CHAIN, K_CHAIN2 = 0, 1, 2, 3, 4, 5, 6, 7
 ROUND_KERNEL = {K_FLOOD: "k_flood", K_PULL: "k_pull", K_PAIR: "k_pull_pair", K_PAIR2: "k_pull_pair",
-                K_EXPAND: "k_expand"}
+                K_EXPAND: "k_expand", K_CHAIN: "k_pull_chain", K_CHAIN2: "k_pull_chain"}
 MODE_KERNEL = {MODE_COMPACT: "k_expand", MODE_LEVEL_PULL: "k_pull", MODE_FLOOD: "k_flood"}
 
 # C prototypes exported by libpsengine.so: (name, restype, argtypes)

@@ -9,7 +9,8 @@ import numpy as np
 
 from . import DistConfig, EngineError, PART_PEER, _P, _p, _u32arr, load
 
-INFO, NODES, PARENT, GHOST_REF, TOPIC, LAYOUT, ROUND_KIND, PULL, PAIR, XCHG, SEGS, SHIP, PACK = range(13)
+INFO, NODES, PARENT, GHOST_REF, TOPIC, LAYOUT, ROUND_KIND, PULL, PAIR, XCHG, SEGS, SHIP, PACK, CHAIN = range(14)
+CHAIN_FIELDS = ("node_begin", "node_end", "topic", "W", "row0", "w0", "S", "levels", "r0", "win", "group")
 CHUNK_FIELDS = ("node_begin", "node_end", "topic", "W", "row0", "e_lo", "e_hi", "gin", "gout", "group",
                 "p_lo", "p_hi", "c_lo")
 PROTOTYPES = [
@@ -123,3 +124,17 @@ class Plan:
     def pack(self, q: int):
         v = self.get(PACK, q).reshape(-1, 6).astype(np.int64)
         return [dict(zip(("e0", "e1", "gseg", "W", "row", "unit0"), (int(x) for x in r))) for r in v]
+
+    def chain(self, q: int):
+        """(rounds, [chunk dicts]) of the chain launch starting at round q (rounds 0: none)."""
+        v = self.get(CHAIN, q)
+        n = int(v[0])
+        if n == 0:
+            return 0, []
+        body = v[1:].reshape(-1, len(CHAIN_FIELDS) + 5)
+        out = []
+        for row in body:
+            c = dict(zip(CHAIN_FIELDS, (int(x) for x in row[:len(CHAIN_FIELDS)])))
+            c["first"] = [int(x) for x in row[len(CHAIN_FIELDS):]]
+            out.append(c)
+        return n, out

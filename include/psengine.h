@@ -102,6 +102,8 @@ typedef struct ps_stats {
 #define PS_K_PAIR 3u    /* k_pull_pair: this round and the next in one launch   */
 #define PS_K_PAIR2 4u   /* k_pull_pair: the second round of the launch above    */
 #define PS_K_EXPAND 5u  /* k_expand (compaction mode)                          */
+#define PS_K_CHAIN 6u   /* k_pull_chain: this round and the next 2-3 in one launch */
+#define PS_K_CHAIN2 7u  /* k_pull_chain: a later round of the launch above      */
 
 typedef struct ps_engine ps_engine;
 

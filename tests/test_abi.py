@@ -71,7 +71,7 @@ def test_struct_layouts(lib):
     assert f"#define PS_MAX_ROUNDS {PE.MAX_ROUNDS}" in src
     for name, val in [("PS_F_RECORD_HOPS", PE.F_RECORD_HOPS), ("PS_F_TIME_KERNELS", PE.F_TIME_KERNELS)]:
         assert re.search(rf"#define {name} 0x{val:x}u", src)
-    for name in ("NONE", "FLOOD", "PULL", "PAIR", "PAIR2", "EXPAND"):  # ps_stats.round_kernel
+    for name in ("NONE", "FLOOD", "PULL", "PAIR", "PAIR2", "EXPAND", "CHAIN", "CHAIN2"):  # ps_stats.round_kernel
         assert re.search(rf"#define PS_K_{name} {getattr(PE, 'K_' + name)}u", src)
 
 

@@ -51,6 +51,7 @@ def oracle_hops(topics, live):
 def run(monkeypatch, pair, n, topics, live, msg_topics, starts=None, record=True, flood=False, flags=0,
         msg_window=65536):
     monkeypatch.setenv("PSAMD_PULL_PAIR", "1" if pair else "0")
+    monkeypatch.setenv("PSAMD_CHAIN", "2")  # pairs only (k_pull_chain: test_gpu_chain.py)
     monkeypatch.setenv("PSAMD_FLOOD", "1" if flood else "0")
     monkeypatch.delenv("PSAMD_FLOOD_TOP_BYTES", raising=False)
     with PE.Engine(n, len(topics), record_hops=record, flags=flags, msg_window=msg_window) as eng:
@@ -130,6 +131,7 @@ def test_pair_after_flood(monkeypatch, seed):
     top = sum(int((parent == root).sum()) * (-(-int((msg_topics == t).sum()) // 64)) * 8
               for t, (root, parent) in enumerate(topics))
     monkeypatch.setenv("PSAMD_FLOOD_TOP_BYTES", str(top))
+    monkeypatch.setenv("PSAMD_CHAIN", "2")
     outs = []
     for pair in (False, True):
         monkeypatch.setenv("PSAMD_PULL_PAIR", "1" if pair else "0")
@@ -263,6 +265,7 @@ def test_pair_many_windows_and_drains(monkeypatch):
     starts = rng.integers(0, 4, size=1500).astype(np.uint32)
     exp = oracle_hops(topics, live)
     peers = [int(p) for p in rng.integers(0, n, size=12)]
+    monkeypatch.setenv("PSAMD_CHAIN", "2")
     outs = []
     for pair in (False, True):
         monkeypatch.setenv("PSAMD_PULL_PAIR", "1" if pair else "0")

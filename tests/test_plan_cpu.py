@@ -127,30 +127,60 @@ class RankSim:
             r0 = x["r_off"][a] // 8
             self.recv[r0:r0 + w.shape[0]] = w
 
-    def node_step(self, c, u, gin):
-        """Node u of chunk c receives its parent's block: True if reached."""
+    def node_step(self, c, u, gin, cols=None):
+        """Node u of chunk c receives its parent's block (columns cols =
+        (w0, S) of it, chains; default the whole block): True if reached."""
+        w0, S = cols if cols else (0, c["W"])
         p = self.parent[u]
         if p != NONE:
-            pa, pb = self.row(c, p)
-            up, src = self.reached[p], self.rows[pa:pb]
+            pa, _ = self.row(c, p)
+            up, src = self.reached[p], self.rows[pa + w0:pa + w0 + S]
         else:
             g = self.gref[u]
             assert g != NONE and gin != NONE, (u, g, gin)
             seg = self.segs[gin]
             assert seg["rw"] == c["W"]
             a = seg["rbase"][g >> 27] + (g & MASK) * c["W"]
-            src = self.recv[a:a + c["W"]]
-            up = src[0] != 0
+            src = self.recv[a + w0:a + w0 + S]
+            up = self.recv[a] != 0
         ok = bool(up and self.live[self.peer[u]])
-        key = (u, c["group"])
-        self.writes[key] = self.writes.get(key, 0) + 1
+        self.writes.setdefault((u, c["group"]), []).append((w0, S))
         if ok:
-            ra, rb = self.row(c, u)
-            self.rows[ra:rb] = src
+            ra, _ = self.row(c, u)
+            self.rows[ra + w0:ra + w0 + S] = src
         if self.reached[u]:
-            assert ok, u  # reach is the same for every start group of a tree
+            assert ok, u  # reach is the same for every start group (and column slice) of a tree
         self.reached[u] |= ok
         return ok
+
+    def run_chain(self, q):
+        """A k_pull_chain launch: per chunk its run (level d, round q + r0),
+        then each level's children of the level above, column slice [w0, w0 + S)."""
+        n, chunks = self.p.chain(q)
+        assert n >= 3
+        for c in chunks:
+            c["W"] = c["W"]
+            L, S, win = c["levels"], c["S"], c["win"]
+            n0 = c["node_end"] - c["node_begin"]
+            assert 1 <= L <= 4 and c["r0"] + L <= n and n0 <= 128 and win <= 128
+            assert S % 2 == 0 or S == c["W"]
+            assert n0 * S + max(0, L - 2) * win * S <= 1024, (n0, S, L, win)  # the LDS stage
+            assert c["first"][0] == self.topics[c["topic"]]["nbase"] + self.topics[c["topic"]]["level_off"][
+                self.level[c["node_begin"]]]
+            win_nodes = list(range(c["node_begin"], c["node_end"]))
+            for u in win_nodes:
+                self.node_step(c, u, NONE, (c["w0"], S))
+            for k in range(1, L):
+                kids = np.nonzero(np.isin(self.parent, np.asarray(win_nodes)))[0]
+                if kids.shape[0]:
+                    assert np.array_equal(kids, np.arange(kids[0], kids[-1] + 1)), "children not consecutive"
+                    assert c["first"][k] <= kids[0] and kids[-1] < c["first"][k + 1]
+                    # the kernel's range from row_ptr: the kids of the nodes of level k - 1 before this window
+                    before = np.isin(self.parent, np.arange(c["first"][k - 1], win_nodes[0])).sum()
+                    assert kids[0] == c["first"][k] + before
+                for v in kids:
+                    self.node_step(c, int(v), NONE, (c["w0"], S))
+                win_nodes = [int(v) for v in kids]
 
     def ship(self, c, oks):
         if c["gout"] == NONE:
@@ -170,12 +200,17 @@ class RankSim:
 
     def chunks_of(self, q):
         k = self.kind[q] if q < self.kind.shape[0] else 0
-        if k == PE.K_PAIR2:
+        if k in (PE.K_PAIR2, PE.K_CHAIN2):
             return None
         return self.p.chunks(PL.PAIR if k == PE.K_PAIR else PL.PULL, q), k == PE.K_PAIR
 
     def run_round(self, q, part):
         """The chunks of round q: part 0 = locally fed, 1 = ghost-fed."""
+        k = self.kind[q] if q < self.kind.shape[0] else 0
+        if k == PE.K_CHAIN:
+            if part == 0:
+                self.run_chain(q)
+            return
         r = self.chunks_of(q)
         if r is None:
             return
@@ -238,8 +273,13 @@ def check(sims, trees, roots, live, n_groups):
             for u in range(T["nbase"], T["nbase"] + T["n_nodes"]):
                 if s.level[u] == 0:
                     continue
-                for gi in range(len(Ly["groups"])):
-                    assert s.writes.get((u, gi), 0) == 1, (t, u, gi, s.writes.get((u, gi), 0))
+                for gi, (_, _, wn) in enumerate(Ly["groups"]):
+                    cols = sorted(s.writes.get((u, gi), []))  # the column slices written: tile [0, W) once
+                    pos = 0
+                    for w0, S in cols:
+                        assert w0 == pos, (t, u, gi, cols)
+                        pos += S
+                    assert pos == (wn if Ly["flags"] & K_GROUPS else Ly["W"]), (t, u, gi, cols)
                 if s.reached[u]:
                     got[s.peer[u]] = True
                     for gi, (_, w0, wn) in enumerate(Ly["groups"]):
@@ -379,7 +419,7 @@ def _gloo_worker(rank, world, port, staggered, out):
         reached = sorted((int(sim.node_topic[u]), int(sim.peer[u])) for u in np.nonzero(sim.reached)[0]
                          if sim.level[u] != 0)
         allr = [None] * world
-        tdist.all_gather_object(allr, (reached, [sim.writes.get(k, 0) for k in sorted(sim.writes)]))
+        tdist.all_gather_object(allr, (reached, [len(sim.writes[k]) for k in sorted(sim.writes)]))
         if rank == 0:
             out[staggered] = allr
     finally:
