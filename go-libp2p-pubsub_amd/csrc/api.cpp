@@ -62,6 +62,27 @@ extern "C" {
 
 const char* ps_version(void) { return "psengine-mi355x 0.3 (gfx950)"; }
 
+// Switches read at creation: debug timing, and the modes the parity tests
+// cover (the planner probe reads the same ones).
+static void read_switches(ps_engine* e) {
+  if (const char* v = std::getenv("PSAMD_HOST_TIMING")) e->host_timing = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_FLOOD")) e->flood_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_PULL_PAIR")) e->pair_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_FLOOD_PROFILE")) e->flood_profile = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_XCHG_OVERLAP")) e->xchg_overlap = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_REVERSE")) e->alt_reverse = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_CHAIN"))  // rounds per launch at most: 1 (k_pull only), 2 (pairs), 3, 4
+    e->chain_max = static_cast<uint32_t>(std::max(1, std::min(static_cast<int>(kChainLevels), std::atoi(v))));
+  if (const char* v = std::getenv("PSAMD_NT_BYTES")) e->nt_bytes = std::strtoull(v, nullptr, 0);
+  if (const char* v = std::getenv("PSAMD_FLOOD_WORDS"))
+    e->flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
+  if (const char* v = std::getenv("PSAMD_FLOOD_SPIN_TICKS"))  // tests: 0 forces the timeout fallback
+    e->flood_spin_ticks = static_cast<uint32_t>(std::strtoul(v, nullptr, 0));
+  if (const char* v = std::getenv("PSAMD_FLOOD_TOP_BYTES"))  // the k_flood / k_pull split (tests: ~0 = all k_flood)
+    e->flood_top_bytes = std::strtoull(v, nullptr, 0);
+}
+
 int ps_create(const ps_config* cfg, ps_engine** out) {
   if (!cfg || !out) return PS_E_INVAL;
   *out = nullptr;
@@ -96,23 +117,7 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
     if (flood_blocks_per_cu(&bpc) == hipSuccess && bpc > 0)
       e->flood_grid = e->n_cus * std::min<uint32_t>(static_cast<uint32_t>(bpc), kFloodBlocksPerCu);
   }
-  // switches: debug timing, and the modes the parity tests cover
-  if (const char* v = std::getenv("PSAMD_HOST_TIMING")) e->host_timing = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_FLOOD")) e->flood_on = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_PULL_PAIR")) e->pair_on = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_FLOOD_PROFILE")) e->flood_profile = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_XCHG_OVERLAP")) e->xchg_overlap = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_REVERSE")) e->alt_reverse = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_CHAIN"))  // rounds per launch at most: 1 (k_pull only), 2 (pairs), 3, 4
-    e->chain_max = static_cast<uint32_t>(std::max(1, std::min(static_cast<int>(kChainLevels), std::atoi(v))));
-  if (const char* v = std::getenv("PSAMD_NT_BYTES")) e->nt_bytes = std::strtoull(v, nullptr, 0);
-  if (const char* v = std::getenv("PSAMD_FLOOD_WORDS"))
-    e->flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
-  if (const char* v = std::getenv("PSAMD_FLOOD_SPIN_TICKS"))  // tests: 0 forces the timeout fallback
-    e->flood_spin_ticks = static_cast<uint32_t>(std::strtoul(v, nullptr, 0));
-  if (const char* v = std::getenv("PSAMD_FLOOD_TOP_BYTES"))  // the k_flood / k_pull split (tests: ~0 = all k_flood)
-    e->flood_top_bytes = std::strtoull(v, nullptr, 0);
+  read_switches(e);
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess) {
     delete e;
@@ -589,6 +594,7 @@ int ps_plan_create(uint32_t n_peers, uint32_t n_topics, const uint32_t* roots, c
   e->cfg.msg_window = kDefaultWindow;
   e->topics.resize(n_topics);
   e->live.assign(n_peers, 1);
+  read_switches(e);
   e->gpu_build_on = false;
   for (uint32_t t = 0; t < n_topics; ++t) {
     int rc = ps_topic_set_tree(e, t, roots[t], parents + static_cast<size_t>(t) * n_peers);

@@ -248,7 +248,9 @@ struct ps_engine {
   // k_pull_pair: rounds q and q + 1 in one launch
   // (PSAMD_PULL_PAIR=0: one k_pull launch per round)
   bool pair_on = true;
-  uint32_t chain_max = psamd::kChainLevels;  // rounds per launch at most (PSAMD_CHAIN: 2 = pairs only)
+  // rounds per launch at most (PSAMD_CHAIN, 1..4): 2 = pairs, the default --
+  // chains (3, 4) measured slower on cfg2/3/4
+  uint32_t chain_max = 2;
   psamd::DevBuf d_chain;
   bool alt_reverse = false;       // PSAMD_REVERSE=1: consecutive launches run their chunks in opposite orders
   uint64_t nt_bytes = 64ull << 20;  // rows of rounds writing at least this much store non-temporally (PSAMD_NT_BYTES)

@@ -299,10 +299,17 @@ def build(world, partition, n=1500, n_topics=2, seed=0, fan=None):
     return rng, trees, roots, live
 
 
+@pytest.mark.parametrize("chain", [2, 4])
 @pytest.mark.parametrize("staggered", [False, True])
 @pytest.mark.parametrize("world,partition", [(1, PE.PART_PEER), (2, PE.PART_PEER), (3, PE.PART_PEER),
                                              (4, PE.PART_SUBTREE), (4, PE.PART_PEER)])
-def test_plans_replay_to_the_oracle(world, partition, staggered):
+def test_plans_replay_to_the_oracle(monkeypatch, world, partition, staggered, chain):
+    """PSAMD_CHAIN (read at engine creation): 2 = round pairs (the default),
+    4 = chains of up to four rounds where nothing is exchanged inside (and
+    no k_flood launch for the leading rounds, so the chains start at round 1)."""
+    monkeypatch.setenv("PSAMD_CHAIN", str(chain))
+    if chain > 2:
+        monkeypatch.setenv("PSAMD_FLOOD", "0")
     rng, trees, roots, live = build(world, partition, seed=world * 7 + partition + 3 * staggered, fan=4)
     n_msgs = 300
     topics = rng.integers(0, len(trees), size=n_msgs)
@@ -325,6 +332,11 @@ def test_plans_replay_to_the_oracle(world, partition, staggered):
     emulate(sims, info[0]["rounds"], in_process_exchange(sims))
     n_groups = [len(np.unique(starts[topics == t])) if staggered else 1 for t in range(len(trees))]
     check(sims, trees, roots, live, n_groups)
+    kinds = set(int(k) for p in plans for k in p.get(PL.ROUND_KIND))
+    if chain == 2:
+        assert PE.K_CHAIN not in kinds
+    elif world == 1 or partition == PE.PART_SUBTREE:
+        assert PE.K_CHAIN in kinds, kinds
     if world > 1 and partition == PE.PART_SUBTREE:
         # the subtree partition exchanges in one round per (topic, group) only
         ex = sum(plans[0].xchg(q)["any"] for q in range(1, info[0]["rounds"] + 1))
