@@ -70,11 +70,11 @@ static void read_switches(ps_engine* e) {
   if (const char* v = std::getenv("PSAMD_FLOOD")) e->flood_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_PAIR")) e->pair_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD_PROFILE")) e->flood_profile = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_XCHG_OVERLAP")) e->xchg_overlap = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_REVERSE")) e->alt_reverse = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_XCHG_OVERLAP")) e->xchg_overlap_env = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_CHAIN"))  // rounds per launch at most: 1 (k_pull only), 2 (pairs), 3, 4
     e->chain_max = static_cast<uint32_t>(std::max(1, std::min(static_cast<int>(kChainLevels), std::atoi(v))));
-  if (const char* v = std::getenv("PSAMD_NT_BYTES")) e->nt_bytes = std::strtoull(v, nullptr, 0);
+  if (const char* v = std::getenv("PSAMD_CHAIN_WORDS"))  // row words a chain wave writes (planner target)
+    e->chain_words = static_cast<uint32_t>(std::min(1 << 20, std::max(256, std::atoi(v))));
   if (const char* v = std::getenv("PSAMD_FLOOD_WORDS"))
     e->flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
   if (const char* v = std::getenv("PSAMD_FLOOD_SPIN_TICKS"))  // tests: 0 forces the timeout fallback
@@ -169,6 +169,7 @@ void ps_destroy(ps_engine* e) {
   }
   for (auto& g : e->stg)
     if (g.h) (void)hipHostFree(g.h);
+  if (e->pairs_pinned) (void)hipHostFree(e->pairs_pinned);
   e->transport.reset();  // (a communicator before its streams)
   if (e->xstream) (void)hipStreamDestroy(e->xstream);
   if (e->stream) (void)hipStreamDestroy(e->stream);
@@ -513,6 +514,7 @@ int ps_dist_init(ps_engine* e, const ps_dist_config* dc, const uint8_t id[PS_UNI
   std::string err;
   e->transport = make_rccl_transport(dc->rank, dc->world, id, &err);
   if (!e->transport) return e->fail(PS_E_DEVICE, err);
+  e->xchg_overlap = e->xchg_overlap_env != 0;
   return PS_OK;
 }
 
@@ -541,6 +543,7 @@ int ps_dist_init_loopback(ps_engine* e, const ps_dist_config* dc, ps_loopback* l
   if ((rc = dist_streams(e))) return rc;
   e->transport = make_loopback_transport(lb->g, dc->rank, e->cfg.device);
   if (!e->transport) return e->fail(PS_E_INVAL, "loopback group size != world");
+  e->xchg_overlap = e->xchg_overlap_env < 0 ? false : e->xchg_overlap_env != 0;
   return PS_OK;
 }
 
@@ -768,7 +771,7 @@ int ps_plan_get(ps_engine* e, uint32_t what, uint32_t index, uint64_t* out, size
       for (uint32_t k = P.lo[index]; k < P.hi[index]; ++k) {
         const ChainChunk& c = P.chain[k];
         v.insert(v.end(), {c.node_begin, c.node_end, c.topic, c.W, static_cast<uint64_t>(c.row0_hi) << 32 | c.row0_lo,
-                           c.w0, c.S, c.levels, c.r0, c.win, c.group});
+                           c.w0, c.S, c.levels, c.r0, c.group});
         for (uint32_t f = 0; f <= kChainLevels; ++f) v.push_back(c.first[f]);
       }
       break;

@@ -161,6 +161,7 @@ struct PairPlan {
   std::vector<PullChunk> chunks;         // pair launches
   std::vector<ChainChunk> chain;         // chain launches
   std::vector<uint32_t> lo, hi, gsplit;  // round q: chunks (pair) or chain chunks of the launch starting at q
+                                         // (chains: whole rows [lo, gsplit), column slices [gsplit, hi))
   std::vector<uint32_t> len;             // round q: rounds of the launch starting at q (0: none)
   std::vector<uint8_t> kind;             // per round: PS_K_*
 };
@@ -199,7 +200,12 @@ struct ps_engine {
   hipStream_t xstream = nullptr;  // multi-GPU: the exchange, beside the round's local chunks
   hipEvent_t ev_run0 = nullptr, ev_run1 = nullptr;
   hipEvent_t ev_round = nullptr, ev_xchg = nullptr;  // multi-GPU: round boundary, exchange done
-  bool xchg_overlap = true;  // PSAMD_XCHG_OVERLAP=0: the exchange on the main stream, one launch per round after it
+  // the exchange on its own stream beside the round's locally fed chunks:
+  // RCCL yes; the loopback transport (a copy kernel on the same GPU) no --
+  // there it only contends with the chunks (4 loopback ranks, cfg4: 7.06 vs
+  // 6.32 ms/step, profiles/r03/loopback); PSAMD_XCHG_OVERLAP=0/1 forces it
+  int xchg_overlap_env = -1;
+  bool xchg_overlap = true;
   std::vector<hipEvent_t> ev_k;  // pairs around expand launches
   uint32_t n_cus = 256, expand_grid = 2048;
   bool host_only = false;        // a planner probe (psengine_plan.h): no device
@@ -212,8 +218,10 @@ struct ps_engine {
   bool gpu_graph = false;     // the current node space was built on the GPU
   bool mirrors_valid = true;  // host copies of node_peer / flags / CSR are current
   std::vector<uint32_t> pairs_host, gstat_host, lvl_host, roots_host;
+  uint32_t* pairs_pinned = nullptr;  // pinned staging of the parent deltas
+  size_t pairs_pinned_cap = 0;       // (u32 words)
   std::vector<size_t> pair_off;
-  psamd::DevBuf d_tpar, d_anc0, d_anc1, d_dep0, d_dep1, d_keys0, d_skeys, d_local, d_deg, d_first, d_lvl,
+  psamd::DevBuf d_tpar, d_orph, d_anc0, d_anc1, d_dep0, d_dep1, d_keys0, d_skeys, d_local, d_deg, d_first, d_lvl,
       d_gstat, d_cub, d_pairs, d_live, d_roots, d_cnt, d_fidx, d_childoff;
   std::chrono::steady_clock::time_point t_run0;
   // k_flood: a single-rank level window's leading rounds in
@@ -248,12 +256,16 @@ struct ps_engine {
   // k_pull_pair: rounds q and q + 1 in one launch
   // (PSAMD_PULL_PAIR=0: one k_pull launch per round)
   bool pair_on = true;
-  // rounds per launch at most (PSAMD_CHAIN, 1..4): 2 = pairs, the default --
-  // chains (3, 4) measured slower on cfg2/3/4
+  // rounds per launch at most (PSAMD_CHAIN, 1..kChainLevels): 2 = pairs
   uint32_t chain_max = 2;
   psamd::DevBuf d_chain;
-  bool alt_reverse = false;       // PSAMD_REVERSE=1: consecutive launches run their chunks in opposite orders
-  uint64_t nt_bytes = 64ull << 20;  // rows of rounds writing at least this much store non-temporally (PSAMD_NT_BYTES)
+  uint32_t chain_words = 8192;    // row words per chain wave, the planner's target (PSAMD_CHAIN_WORDS)
+  std::vector<uint64_t> chain_fail_key;  // a pair plan whose chain ranges overflowed kChainCap: no chains
+  psamd::DevBuf d_chain_ovf;
+  // rows of rounds writing at least this much store non-temporally (the MALL
+  // cannot hold them for the next launch: reversing launch order and cached
+  // stores measured 0-50 % slower, profiles/r03/ab_mall_reverse.txt)
+  static constexpr uint64_t kNtBytes = 64ull << 20;
   psamd::PairPlan pair;
   psamd::DevBuf d_pp;
   uint64_t pair_up = ~0ull;

@@ -21,9 +21,12 @@ constexpr uint32_t kStatBlocks = 1024;  // grid of the reducing kernels
 uint32_t blocks(uint64_t n) { return static_cast<uint32_t>(std::max<uint64_t>(1, (n + kB - 1) / kB)); }
 
 __global__ __launch_bounds__(kB) void k_scatter_pairs(const uint32_t* __restrict__ pairs, uint32_t n,
-                                                      uint32_t* __restrict__ par) {
+                                                      uint32_t* __restrict__ par, uint8_t* __restrict__ orph) {
   const uint32_t i = blockIdx.x * kB + threadIdx.x;
-  if (i < n) par[pairs[2 * i]] = pairs[2 * i + 1];
+  if (i >= n) return;
+  const uint32_t p = pairs[2 * i], v = pairs[2 * i + 1];
+  par[p] = v >= kOrphanCode ? kNoneP : v;
+  orph[p] = v == kOrphanCode;
 }
 
 // anc = upstream (root: itself), dep = 1 (root: 0)
@@ -311,10 +314,14 @@ __global__ __launch_bounds__(kSmallB) void k_place_small(
 
 // out[i] = 1 iff peers[i] holds a node of the topic placed at [nbase, nbase +
 // n_nodes) by the last build (local[] may hold stale ids: node_peer confirms)
+// (the upward walk of an unreached peer: at most the depth of its cut
+// subtree, <= n_peers hops; the build bounds attached depths by 255)
 __global__ __launch_bounds__(kB) void k_reach_query(const uint32_t* __restrict__ peers, uint32_t n,
                                                     uint32_t n_peers, const uint32_t* __restrict__ local,
                                                     const uint32_t* __restrict__ node_peer, uint32_t nbase,
-                                                    uint32_t n_nodes, uint8_t* __restrict__ out) {
+                                                    uint32_t n_nodes, const uint32_t* __restrict__ par,
+                                                    const uint8_t* __restrict__ orph, uint32_t root,
+                                                    uint8_t* __restrict__ out) {
   const uint32_t i = blockIdx.x * kB + threadIdx.x;
   if (i >= n) return;
   const uint32_t p = peers[i];
@@ -322,6 +329,17 @@ __global__ __launch_bounds__(kB) void k_reach_query(const uint32_t* __restrict__
   if (p < n_peers) {
     const uint32_t u = local[p];
     r = u >= nbase && u - nbase < n_nodes && node_peer[u] == p;
+    if (!r) {  // below_orphan (tree.cpp): the first peer without an upstream
+      uint32_t q = p;
+      for (uint32_t h = 0; h < n_peers && q != root; ++h) {
+        const uint32_t up = par[q];
+        if (up >= n_peers) {
+          r = orph[q] ? 2 : 0;
+          break;
+        }
+        q = up;
+      }
+    }
   }
   out[i] = r;
 }
@@ -329,11 +347,11 @@ __global__ __launch_bounds__(kB) void k_reach_query(const uint32_t* __restrict__
 }  // namespace
 
 hipError_t launch_reach_query(const uint32_t* peers, uint32_t n, uint32_t n_peers, const uint32_t* local,
-                              const uint32_t* node_peer, uint32_t nbase, uint32_t n_nodes, uint8_t* out,
-                              hipStream_t s) {
+                              const uint32_t* node_peer, uint32_t nbase, uint32_t n_nodes, const uint32_t* par,
+                              const uint8_t* orph, uint32_t root, uint8_t* out, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_reach_query, dim3(blocks(n)), dim3(kB), 0, s, peers, n, n_peers, local, node_peer,
-                     nbase, n_nodes, out);
+                     nbase, n_nodes, par, orph, root, out);
   return hipGetLastError();
 }
 
@@ -389,9 +407,9 @@ hipError_t launch_level_internal(const uint32_t* deg, uint32_t nbase, uint32_t R
   return hipGetLastError();
 }
 
-hipError_t launch_scatter_pairs(const uint32_t* pairs, uint32_t n, uint32_t* par, hipStream_t s) {
+hipError_t launch_scatter_pairs(const uint32_t* pairs, uint32_t n, uint32_t* par, uint8_t* orph, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_scatter_pairs, dim3(blocks(n)), dim3(kB), 0, s, pairs, n, par);
+  hipLaunchKernelGGL(k_scatter_pairs, dim3(blocks(n)), dim3(kB), 0, s, pairs, n, par, orph);
   return hipGetLastError();
 }
 

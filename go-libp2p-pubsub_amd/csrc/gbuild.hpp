@@ -19,8 +19,11 @@ constexpr uint32_t kBuildMaxDepth = 255;  // depth bits of the sort key
 constexpr uint32_t kBuildPeerBits = 28;   // peer / parent bits of the sort key
 constexpr uint32_t kBuildSmallLevel = 8192;  // levels placed by the one-block kernel
 
-// (peer, value) pairs scattered into a parent array
-hipError_t launch_scatter_pairs(const uint32_t* pairs, uint32_t n, uint32_t* par, hipStream_t s);
+// Pair value of an Orphan peer (not subscribed: no upstream; its subtree is
+// cut for good, rule Q5): par[p] = kNone, orph[p] = 1.
+constexpr uint32_t kOrphanCode = 0xFFFFFFFEu;
+// (peer, value) pairs scattered into a parent array and its orphan bytes
+hipError_t launch_scatter_pairs(const uint32_t* pairs, uint32_t n, uint32_t* par, uint8_t* orph, hipStream_t s);
 
 // Depth of every peer (pointer jumping, `jumps` steps: depths up to 2^jumps
 // resolve): keys[p] = depth << 56 | parent << 28 | p for peers reachable from
@@ -69,11 +72,13 @@ hipError_t launch_place_level(const uint64_t* keys, uint32_t lo, uint32_t hi, ui
                               const uint32_t* childoff, const uint32_t* cnt, const uint32_t* firstidx,
                               uint16_t topic, uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
                               uint32_t* node_parent, uint32_t* deg, uint32_t* first, hipStream_t s);
-// out[i] = 1 iff peer peers[i] holds a node of the topic at [nbase, nbase +
-// n_nodes) in the last GPU build (the message's reach, for the lazy prune)
+// The lazy prune's questions about peers[i] (tree.hpp ReachQuery), from the
+// last GPU build: out[i] = 1 if the peer holds a node of the topic at [nbase,
+// nbase + n_nodes) (the message reached it), else 2 if its upstream path
+// (par, from the peer itself) ends at an Orphan (cut for good), else 0.
 hipError_t launch_reach_query(const uint32_t* peers, uint32_t n, uint32_t n_peers, const uint32_t* local,
-                              const uint32_t* node_peer, uint32_t nbase, uint32_t n_nodes, uint8_t* out,
-                              hipStream_t s);
+                              const uint32_t* node_peer, uint32_t nbase, uint32_t n_nodes, const uint32_t* par,
+                              const uint8_t* orph, uint32_t root, uint8_t* out, hipStream_t s);
 // col[row_ptr[u] + j] = first[u] + j
 hipError_t launch_fill_col(const uint32_t* row_ptr, const uint32_t* first, uint32_t n_nodes,
                            uint32_t* col, hipStream_t s);

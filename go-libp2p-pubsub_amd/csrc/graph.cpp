@@ -423,6 +423,8 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
   hipStream_t s = e->stream;
   HIP_TRY(e->d_tpar.ensure(static_cast<size_t>(nt) * n * 4), "alloc parents");
+  HIP_TRY(e->d_orph.ensure(static_cast<size_t>(nt) * n), "alloc orphan bytes");
+  static_assert(SubscriptionTree::kOrphanUp == kOrphanCode, "one orphan code");
   // 1. parent deltas of every topic, one upload
   auto& pairs = e->pairs_host;
   pairs.clear();
@@ -434,8 +436,10 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
     if (!T.exists) continue;
     uint32_t* par_t = e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n;
     bool full = false;
+    uint8_t* orph_t = e->d_orph.as<uint8_t>() + static_cast<size_t>(t) * n;
     if (!T.par_dev_valid) {
       HIP_TRY(hipMemsetAsync(par_t, 0xFF, static_cast<size_t>(n) * 4, s), "clear parents");
+      HIP_TRY(hipMemsetAsync(orph_t, 0, n, s), "clear orphan bytes");
       T.par_mirror.assign(n, kNone);
       T.par_dev_valid = true;
       full = true;
@@ -450,14 +454,14 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
     if (T.kind == Kind::Join) {
       T.tree.take_touched(cand);
       if (full)
-        for (uint32_t p = 0; p < n; ++p) diff(p, T.tree.in_parent(p));
+        for (uint32_t p = 0; p < n; ++p) diff(p, T.tree.upstream_code(p));
       else
         for (size_t i = 0; i < cand.size(); ++i) {
           if (i + 16 < cand.size()) {  // touched peers are scattered: fetch ahead
             T.tree.prefetch_peer(cand[i + 16]);
             __builtin_prefetch(&T.par_mirror[cand[i + 16]]);
           }
-          diff(cand[i], T.tree.in_parent(cand[i]));
+          diff(cand[i], T.tree.upstream_code(cand[i]));
         }
     } else if (T.par_full_dirty || full) {
       for (uint32_t p = 0; p < n; ++p) diff(p, p == T.root ? kNone : T.parent[p]);
@@ -467,12 +471,26 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   e->pair_off[nt] = pairs.size() / 2;
   if (!pairs.empty()) {
     HIP_TRY(e->d_pairs.ensure(pairs.size() * 4), "alloc deltas");
-    HIP_TRY(hipMemcpyAsync(e->d_pairs.p, pairs.data(), pairs.size() * 4, hipMemcpyHostToDevice, s),
+    // through pinned memory: an asynchronous DMA (a pageable source is staged
+    // by the runtime, synchronously); the build syncs before the next reuse
+    if (e->pairs_pinned_cap < pairs.size()) {
+      if (e->pairs_pinned) HIP_TRY(hipHostFree(e->pairs_pinned), "free pinned deltas");
+      e->pairs_pinned = nullptr;
+      e->pairs_pinned_cap = 0;
+      const size_t cap = std::max<size_t>(pairs.size() + pairs.size() / 2, 1 << 16);
+      void* h = nullptr;
+      HIP_TRY(hipHostMalloc(&h, cap * 4, hipHostMallocDefault), "alloc pinned deltas");
+      e->pairs_pinned = static_cast<uint32_t*>(h);
+      e->pairs_pinned_cap = cap;
+    }
+    std::memcpy(e->pairs_pinned, pairs.data(), pairs.size() * 4);
+    HIP_TRY(hipMemcpyAsync(e->d_pairs.p, e->pairs_pinned, pairs.size() * 4, hipMemcpyHostToDevice, s),
             "upload deltas");
     for (uint32_t t = 0; t < nt; ++t)
       HIP_TRY(launch_scatter_pairs(e->d_pairs.as<uint32_t>() + 2 * e->pair_off[t],
                                    static_cast<uint32_t>(e->pair_off[t + 1] - e->pair_off[t]),
-                                   e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n, s),
+                                   e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n,
+                                   e->d_orph.as<uint8_t>() + static_cast<size_t>(t) * n, s),
               "scatter deltas");
   }
   using clk = std::chrono::steady_clock;

@@ -205,13 +205,10 @@ struct PullArgs {
   // reached, as the generation test of a separate launch would find
   uint64_t* partials2;
   uint32_t all_current;
-  // the launch takes its chunks last to first: it reads first the parent
-  // rows the previous launch (which ran the other way) wrote last
-  uint32_t reverse;
   // k_pull_chain: the CSR offsets (a run's children are consecutive ids) and
   // the partial slots of each round of the launch
   const uint32_t* row_ptr;
-  uint64_t* partials_r[4];
+  uint64_t* partials_r[6];  // (kChainLevels)
 };
 // k_pull_pair: per wave, a run of at most kPairPar nodes
 // whose rows (at most kPairWords words in all) stay in LDS for its children,
@@ -221,15 +218,24 @@ constexpr uint32_t kPairPar = 128;
 constexpr uint32_t kPairKids = 256;
 // k_pull_chain: up to kChainLevels rounds in one launch.  A
 // wave owns a run of level-d nodes and a column slice [w0, w0 + S) of their
-// rows (S = W: whole rows); it writes the run (round q, parents' rows from
-// HBM), then every descendant of the run level by level, each copying its
-// parent's slice from the LDS stage the wave wrote one level above -- only
-// the run's parents are read from HBM.  Staged levels are processed in
-// windows of `win` nodes, depth first, so any fan-out fits the stage.
-constexpr uint32_t kChainLevels = 4;
-constexpr uint32_t kChainWords = 1024;  // LDS stage words per wave (the run + one window per inner level)
-constexpr uint32_t kChainKids = 128;    // nodes resolved per sub-run (a window is at most this)
-constexpr uint32_t kChainPar = 128;     // nodes of a run at most
+// rows (S = W: whole rows, the usual case; slices only for rows wider than
+// the stage).  It writes the run (round q, the parents' rows from HBM) and
+// keeps those rows in its LDS stage; then, level by level, every descendant
+// of the run (round q + k: the level-(d + k) nodes of the subtree, one
+// contiguous id range per level).  In a single-start window a reached node's
+// row is its parent's row as round q + k - 1 wrote it, and that row is a
+// stage row: a node's entry in the level table is the stage slot of the row
+// its parent holds (kChainNone: unreached), so no level below the run reads
+// a row from HBM.  Level ranges are at most kChainCap nodes (the host sizes
+// the runs; k_chain_ranges fills and checks the ranges on the device).
+constexpr uint32_t kChainLevels = 6;
+static_assert(sizeof(PullArgs::partials_r) / sizeof(uint64_t*) == kChainLevels, "a slot row per chain level");
+constexpr uint32_t kChainWords = 768;  // LDS stage words per wave: the run's rows (slices)
+constexpr uint32_t kChainKids = 256;   // nodes resolved per sub-run of a level
+constexpr uint32_t kChainPar = 128;    // nodes of a run at most (stage slots < kChainZero)
+constexpr uint32_t kChainCap = 1024;   // nodes of one level of a chunk at most (LDS level tables)
+constexpr uint8_t kChainNone = 0xFF;   // level table: unreached
+constexpr uint8_t kChainZero = 0xFE;   // level table: reached with a zero row (PS_F_NO_LAZY_SEEN only)
 struct ChainChunk {
   uint32_t node_begin, node_end;  // the run (level d)
   uint32_t topic;
@@ -239,14 +245,20 @@ struct ChainChunk {
   uint16_t w0, S;                 // the column slice of every row
   uint8_t levels;                 // levels written: d .. d + levels - 1 (rounds r0 + k of the launch)
   uint8_t r0;                     // the run's round within the launch (a start group entering late: > 0)
-  uint16_t win;                   // nodes per window of an inner staged level
+  uint16_t group;                 // host: the start group
   // first node of levels d .. d + levels: a run [x0, x1) of level d + k has
   // the children [row_ptr[x0] - row_ptr[first[k]] + first[k + 1], ...x1...)
   uint32_t first[kChainLevels + 1];
-  uint32_t group;                 // host: the start group
+  // level k >= 1 of the chunk: the descendants [lo[k], hi[k]) (k_chain_ranges)
+  uint32_t lo[kChainLevels], hi[kChainLevels];
 };
+// ChainChunk::lo / hi from the device CSR; *overflow is set non-zero when a
+// level range exceeds kChainCap (the plan is then not used)
+hipError_t launch_chain_ranges(ChainChunk* chunks, uint32_t n, const uint32_t* row_ptr, uint32_t* overflow,
+                               hipStream_t s);
+// slices: chunks of rows wider than the stage (column slices; their own launch)
 hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32_t n_chunks, uint32_t round,
-                             bool record, bool nt, hipStream_t s);
+                             bool record, bool nt, bool slices, hipStream_t s);
 // ChainChunk::p_lo / p_hi from the device node_parent (GPU-built graphs)
 hipError_t launch_chain_parents(ChainChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s);
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch

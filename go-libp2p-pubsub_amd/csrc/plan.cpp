@@ -215,14 +215,15 @@ bool plan_pull_chunks(ps_engine* e, const WindowLayout& L) {
 }
 
 // Multi-round launches: k_pull_pair writes rounds
-// q and q + 1, k_pull_chain rounds q .. q + L - 1 (L = 3, 4) -- each wave a
-// run of level-d nodes and then every descendant of the run from the rows it
-// holds in LDS, so only round q reads parent rows from HBM.  Which rounds go
+// q and q + 1, k_pull_chain rounds q .. q + L - 1 (L = 3 .. kChainLevels) --
+// each wave a run of level-d nodes and then every descendant of the run from
+// the rows it holds in LDS, so only round q reads parent rows from HBM.  Which rounds go
 // together is a small dynamic program over the rounds after k_flood's: a
 // launch costs its rows, round q's parent-row reads (level d - 1's internal
 // nodes x row bytes) and kLaunchBytes of launch ramp and tail.  A pair needs
 // each row of round q (and each level-1 row of a start group entering at q)
-// to fit the kPairWords stage; a chain slices wide rows into columns instead.
+// to fit the kPairWords stage; a chain slices wide rows into columns instead
+// and sizes its runs by the levels' growth (chain_size).
 // On N ranks a launch spans only rounds whose successors exchange nothing
 // (every child is local and nothing written inside ships), and a chain also
 // needs round q itself exchange-free.  Fills pair.kind (PS_K_* per round);
@@ -235,6 +236,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   key.push_back(first);
   key.push_back(e->pair_on ? 1 : 0);
   key.push_back(e->chain_max);
+  key.push_back(e->chain_words);
   for (size_t q = 0; q < xchg.size(); ++q) key.push_back(xchg[q].any);
   PairPlan& PP = e->pair;
   if (key == PP.key) return false;
@@ -270,13 +272,71 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
     }
     can2[q] = ok;
   }
+  // A chain of `levels` levels from level d of (topic t, block of W words):
+  // its runs, column slice and per-level growth.  Runs are sized so that the
+  // stage holds their rows (slices of kChainWords words for wider rows), the
+  // expected widest level range is half of kChainCap (k_chain_ranges checks
+  // the real ranges), and a wave writes about chain_words row words.
+  struct ChainSize {
+    uint32_t R = 0, S = 0;  // R = 0: no chain of this length
+  };
+  auto chain_size = [&](const TopicHost& T, uint32_t d, uint32_t levels, uint32_t W) {
+    ChainSize z;
+    const double n0 = static_cast<double>(T.level_off[d + 1] - T.level_off[d]);
+    if (n0 == 0) {  // no node of the level on this rank: nothing to cut
+      z.R = 1;
+      z.S = std::max<uint32_t>(1, std::min(W, kChainWords));
+      return z;
+    }
+    double gmax = 1.0, gsum = 1.0;
+    for (uint32_t k = 1; k < levels && d + k + 1 < T.level_off.size(); ++k) {
+      const double g = static_cast<double>(T.level_off[d + k + 1] - T.level_off[d + k]) / n0;
+      gmax = std::max(gmax, g);
+      gsum += g;
+    }
+    if (gmax > kChainCap / 2) return z;  // even one node's subtree is expected too wide
+    z.S = W <= kChainWords ? W : kChainWords;
+    const double r = std::min({static_cast<double>(kChainPar), static_cast<double>(kChainWords / z.S),
+                               std::floor(kChainCap / 2 / gmax),
+                               std::floor(static_cast<double>(e->chain_words) / (z.S * gsum))});
+    z.R = static_cast<uint32_t>(std::max(1.0, r));
+    return z;
+  };
+  // the (topic, group)s a launch of rounds q .. q + len - 1 writes: level d
+  // from round q + r0 for `levels` levels
+  auto chain_parts = [&](uint32_t q, uint32_t len, auto&& fn) {
+    for (uint32_t t = 0; t < nt; ++t) {
+      const TopicHost& T = e->topics[t];
+      if (tab[t].W == 0) continue;
+      for (uint32_t gi = 0; gi < L.groups[t].size(); ++gi) {
+        const StartGroup& g = L.groups[t][gi];
+        uint32_t d, r0;
+        if (q >= g.start + 1) {
+          d = q - g.start;
+          r0 = 0;
+        } else if (g.start + 1 < q + len) {
+          d = 1;
+          r0 = g.start + 1 - q;
+        } else {
+          continue;
+        }
+        if (d > T.depth || d + 1 >= T.level_off.size()) continue;
+        fn(t, gi, d, r0, std::min(len - r0, T.depth - d + 1));
+      }
+    }
+  };
+  const bool chains_ok = key != e->chain_fail_key;  // (ranges overflowed under this plan once)
   auto can = [&](uint32_t q, uint32_t len) {
     if (len == 1) return true;
     if (len == 2) return static_cast<bool>(can2[q]);
-    if (len > max_len || q + len - 1 > rounds || exch(q)) return false;
+    if (!chains_ok || len > max_len || q + len - 1 > rounds || exch(q)) return false;
     for (uint32_t k = 1; k <= len; ++k)
       if (exch(q + k)) return false;
-    return true;
+    bool ok = true;
+    chain_parts(q, len, [&](uint32_t t, uint32_t gi, uint32_t d, uint32_t, uint32_t levels) {
+      ok = ok && chain_size(e->topics[t], d, levels, block_w(tab[t], L.groups[t][gi])).R > 0;
+    });
+    return ok;
   };
   // best[q]: traffic of rounds q..rounds; take[q]: rounds of the launch starting at q
   std::vector<double> best(rounds + 6, 0.0);
@@ -284,7 +344,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   for (uint32_t q = rounds; q > first; --q) {
     best[q] = 1e300;
     double wb = 0;
-    for (uint32_t len = 1; len <= std::min<uint32_t>(4, rounds - q + 1); ++len) {
+    for (uint32_t len = 1; len <= std::min<uint32_t>(kChainLevels, rounds - q + 1); ++len) {
       wb += static_cast<double>(e->pull.bytes[q + len - 1]);
       if (!can(q, len)) continue;
       const double c = wb + rd[q] + (wb > 0 ? kLaunchBytes : 0.0) + best[q + len];
@@ -314,61 +374,38 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
       kind[q] = PS_K_CHAIN;
       for (uint32_t k = 1; k < len; ++k) kind[q + k] = PS_K_CHAIN2;
       PP.lo[q] = static_cast<uint32_t>(PP.chain.size());
-      for (uint32_t t = 0; t < nt; ++t) {
+      std::vector<ChainChunk> sliced;  // rows wider than the stage: after the whole-row chunks
+      chain_parts(q, len, [&](uint32_t t, uint32_t gi, uint32_t d, uint32_t r0, uint32_t levels) {
         const TopicHost& T = e->topics[t];
-        if (tab[t].W == 0) continue;
-        for (uint32_t gi = 0; gi < L.groups[t].size(); ++gi) {
-          const StartGroup& g = L.groups[t][gi];
-          const uint32_t W = block_w(tab[t], g);
-          // the group's level written in round q (r0 = 0), or its level 1 when
-          // it enters inside the launch (round q + r0)
-          uint32_t d, r0;
-          if (q >= g.start + 1) {
-            d = q - g.start;
-            r0 = 0;
-          } else if (g.start + 1 < q + len) {
-            d = 1;
-            r0 = g.start + 1 - q;
-          } else {
-            continue;
+        const StartGroup& g = L.groups[t][gi];
+        const uint32_t W = block_w(tab[t], g);
+        const ChainSize z = chain_size(T, d, levels, W);
+        const uint64_t row0 = block_row0(tab[t], g);
+        const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
+        for (uint32_t u = lo; u < hi; u += z.R)
+          for (uint32_t w0 = 0; w0 < W; w0 += z.S) {
+            ChainChunk c{};
+            c.node_begin = T.nbase + u;
+            c.node_end = T.nbase + std::min(u + z.R, hi);
+            c.topic = t;
+            c.p_lo = gpu ? kNone : e->node_parent[c.node_begin];
+            c.p_hi = gpu ? kNone : e->node_parent[c.node_end - 1];
+            c.W = W;
+            c.row0_lo = static_cast<uint32_t>(row0);
+            c.row0_hi = static_cast<uint32_t>(row0 >> 32);
+            c.w0 = static_cast<uint16_t>(w0);
+            c.S = static_cast<uint16_t>(std::min(z.S, W - w0));
+            c.levels = static_cast<uint8_t>(levels);
+            c.r0 = static_cast<uint8_t>(r0);
+            c.group = static_cast<uint16_t>(gi);
+            for (uint32_t k = 0; k <= levels && k <= kChainLevels; ++k)
+              c.first[k] = T.nbase + (d + k < T.level_off.size() ? T.level_off[d + k] : T.n_nodes);
+            (z.S < W ? sliced : PP.chain).push_back(c);
           }
-          if (d > T.depth || d + 1 >= T.level_off.size()) continue;
-          const uint32_t levels = std::min(len - r0, T.depth - d + 1);
-          // column slices: the run and one window per inner level of at least
-          // kMinNodes nodes each fit the kChainWords stage
-          constexpr uint32_t kMinNodes = 4;
-          const uint32_t staged = std::max<uint32_t>(1, levels - 1);  // levels held in LDS at once
-          uint32_t S = W;
-          if (W * kMinNodes * staged > kChainWords) S = std::max<uint32_t>(2, (kChainWords / (kMinNodes * staged)) & ~1u);
-          const uint32_t budget = kChainWords / S;  // nodes the stage holds
-          const uint32_t n0 = std::max<uint32_t>(1, std::min<uint32_t>(kChainPar, levels > 2 ? budget / staged : budget));
-          const uint32_t win = levels > 2 ? std::max<uint32_t>(1, std::min<uint32_t>(kChainKids, budget / staged)) : 0;
-          const uint64_t row0 = block_row0(tab[t], g);
-          const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
-          for (uint32_t u = lo; u < hi; u += n0)
-            for (uint32_t w0 = 0; w0 < W; w0 += S) {
-              ChainChunk c{};
-              c.node_begin = T.nbase + u;
-              c.node_end = T.nbase + std::min(u + n0, hi);
-              c.topic = t;
-              c.p_lo = gpu ? kNone : e->node_parent[c.node_begin];
-              c.p_hi = gpu ? kNone : e->node_parent[c.node_end - 1];
-              c.W = W;
-              c.row0_lo = static_cast<uint32_t>(row0);
-              c.row0_hi = static_cast<uint32_t>(row0 >> 32);
-              c.w0 = static_cast<uint16_t>(w0);
-              c.S = static_cast<uint16_t>(std::min(S, W - w0));
-              c.levels = static_cast<uint8_t>(levels);
-              c.r0 = static_cast<uint8_t>(r0);
-              c.win = static_cast<uint16_t>(win);
-              for (uint32_t k = 0; k <= levels && k <= kChainLevels; ++k) c.first[k] = T.nbase + T.level_off[d + k];
-              c.group = gi;
-              PP.chain.push_back(c);
-            }
-        }
-      }
+      });
+      PP.gsplit[q] = static_cast<uint32_t>(PP.chain.size());
+      PP.chain.insert(PP.chain.end(), sliced.begin(), sliced.end());
       PP.hi[q] = static_cast<uint32_t>(PP.chain.size());
-      PP.gsplit[q] = PP.hi[q];
       q += len - 1;
       continue;
     }

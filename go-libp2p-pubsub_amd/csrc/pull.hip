@@ -341,8 +341,8 @@ __global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __
   uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds[wid]);
   const uint32_t cur = a.gen_cur & 0xFF;
   PullCtr c;
-  if (wave < n_chunks) {  // one chunk per wave (reverse: the last chunk first)
-    const PullChunk ch = chunks[a.reverse ? n_chunks - 1 - wave : wave];
+  if (wave < n_chunks) {  // one chunk per wave
+    const PullChunk ch = chunks[wave];
     const TopicDev T = a.topics[ch.topic];
     PullTopic P;
     P.W = ch.W;
@@ -534,7 +534,7 @@ __global__ __launch_bounds__(64) void k_pull_pair(PullArgs a, const PullChunk* _
   if (lane < 2) rows[kPairWords + lane] = 0;
   WaveCtr c, c2;
   for (uint32_t ci = blockIdx.x; ci < n_chunks; ci += gridDim.x) {
-    const PullChunk ch = chunks[a.reverse ? n_chunks - 1 - ci : ci];
+    const PullChunk ch = chunks[ci];
     const TopicDev T = a.topics[ch.topic];
     PullTopic P;
     P.W = ch.W;
@@ -632,21 +632,23 @@ __global__ __launch_bounds__(kBlock) void k_chunk_parents(PullChunk* __restrict_
 }
 
 // ------------------------------------------------------------- pull chain ---
-// k_pull_chain: kChainLevels rounds at most per launch.  A
-// wave owns a run of level-d nodes and a column slice [w0, w0 + S) of their
-// rows.  Level 0 (round q): the run resolves its parents from this window's
-// generation bytes (as k_pull) and streams the slices of their rows from HBM
-// into its own rows and the LDS stage.  Level k >= 1 (round q + k): the
-// children of the level above's current window -- consecutive ids, found
-// from row_ptr -- copy their parent's slice from the stage iff the parent was
-// reached (an LDS reach bit) and they are live; an inner level is staged in
-// windows of `win` nodes, each window's children handled before the next
-// window (depth first), so the stage holds the run plus one window per inner
-// level whatever the fan-out.  An unreached node's slice is written with
-// zeros (stale under its old generation byte, never read).  Slices are
-// independent (a row is copied word for word), so the waves of one run's
-// slices agree on every reach decision; only the slice-0 wave stamps
-// generations and counts nodes.
+// k_pull_chain: rounds q .. q + L - 1 in one launch (one
+// rank, or rounds that exchange nothing).  A wave owns a run of level-d nodes
+// and a column slice [w0, w0 + S) of their rows (S = W unless the rows are
+// wider than the stage).  Level 0 (round q + r0): the run resolves its
+// parents from this window's generation bytes, as k_pull does, and streams
+// their rows from HBM into its own rows and the LDS stage.  Level k >= 1
+// (round q + r0 + k): the run's descendants of that level, the contiguous
+// ids [lo[k], hi[k]) (k_chain_ranges), in sub-runs of kChainKids: a node
+// copies its parent's row as the level above wrote it -- if the parent was
+// reached and the node is live -- and the level above wrote the row of its
+// stage slot, so each node's entry in the level table is that slot
+// (kChainNone: unreached).  No level below the run reads a row from HBM, and
+// every level's rows form one contiguous output stream (S = W).  An
+// unreached node's row is written with zeros (stale under its old generation
+// byte, never read).  Slices are independent (a row is copied word for
+// word), so the waves of one run's slices agree on every reach decision;
+// only the slice-0 wave stamps generations and counts nodes.
 struct ChainStep {
   uint64_t base;   // row of node u = base + u * W (+ w0)
   uint32_t W, w0, S, nbase;
@@ -664,11 +666,12 @@ __device__ __forceinline__ void chain_split(uint32_t i, float rs, uint32_t S, in
   r += (lo - hi) * static_cast<int32_t>(S);
 }
 
-// Streams nk nodes' slices [y0, y0 + nk): element (kk, r) = source slot
-// tab[kk] (LDS offset into `stage`, kZero: zeros) + r -- or, level 0, the
-// parent row address src64[kk] (0: rewrite the node's own words) -- into the
-// node's row in HBM and, when dst != kNone, the stage at dst + kk * S + r.
-// 16-B units (even S) or words; lanes past the end repeat the last unit.
+// Column slices (S < W): streams nk nodes' slices [y0, y0 + nk): element
+// (kk, r) = source slot tab[kk] (LDS offset into `stage`, kChainWords: zeros)
+// + r -- or, level 0, the parent row address src64[kk] (0: rewrite the
+// node's own words) -- into the node's row in HBM and, when dst !=
+// kNoneNode, the stage at dst + kk * S + r.  16-B units (even S) or words;
+// lanes past the end repeat the last unit.
 template <bool kRecord, bool kNT, bool kFromHbm>
 __device__ __forceinline__ void chain_stream(const PullArgs& a, const ChainStep& C, uint32_t y0, uint32_t nk,
                                              const uint32_t* tab, const uint64_t* src64, uint64_t* stage,
@@ -773,45 +776,146 @@ __device__ __forceinline__ void chain_stream(const PullArgs& a, const ChainStep&
   }
 }
 
-// One sub-run of an inner level: the nodes [y0, y0 + nk) (<= kChainKids),
-// children of the window [x0, ...) staged at src_base: resolve each node's
-// parent slot into tab (kZero: unreached or dead), stamp generations
-// (slice 0), reach bits of the sub-run into reach_out (when staged).
-__device__ __forceinline__ void chain_resolve(const PullArgs& a, const ChainStep& C, uint32_t x0,
-                                              const uint64_t* reach_in, uint32_t src_base, uint32_t y0, uint32_t nk,
-                                              uint32_t* tab, uint64_t* reach_out, uint32_t lane, uint32_t cur,
-                                              WaveCtr& c) {
-  constexpr uint32_t kZero = kChainWords;
-  for (uint32_t j0 = 0; j0 < nk; j0 += 64) {
-    const uint32_t j = j0 + lane;
-    const bool in = j < nk;
-    uint32_t p = kNoneNode, f = 0;
-    if (in) {
-      p = a.node_parent[y0 + j];
-      f = a.node_flags[y0 + j];
+// Whole rows (S = W): the nodes [y0, y0 + nk) as one line-aligned output
+// stream from the stage (ctab[kk]: the stage offset of node kk's source row,
+// kZero: the zero pair), k_pull's 8-in-flight pipeline with LDS sources.
+template <bool kRecord, bool kNT, uint32_t kZero>
+__device__ __forceinline__ void stage_stream(const PullArgs& a, uint64_t* out, uint32_t nk, uint32_t W,
+                                             const uint32_t* ctab, const uint64_t* lrows, uint32_t lane,
+                                             uint32_t round, WaveCtr& c) {
+  constexpr uint32_t kU = 8;
+  const float rw = 1.0f / static_cast<float>(W);
+  auto split = [&](uint32_t i, int32_t& kk, int32_t& r) {
+    kk = static_cast<int32_t>(static_cast<float>(i) * rw);
+    r = static_cast<int32_t>(i) - kk * static_cast<int32_t>(W);
+    const int32_t lo = r < 0, hi = r >= static_cast<int32_t>(W);
+    kk += hi - lo;
+    r += (lo - hi) * static_cast<int32_t>(W);
+  };
+  const uint32_t total = nk * W;
+  const uint32_t h = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(out) & 127) >> 3;
+  if (!(W & 1u)) {
+    for (uint32_t i0 = 0; i0 < total + h; i0 += kU * 128) {
+      uint4 x[kU];
+      bool go[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const int32_t is = static_cast<int32_t>(i0 + u * 128 + 2 * lane) - static_cast<int32_t>(h);
+        const uint32_t i = is < 0 ? 0u : (static_cast<uint32_t>(is) < total ? static_cast<uint32_t>(is) : total - 2);
+        int32_t kk, r;
+        split(i, kk, r);
+        const uint32_t off = ctab[kk];
+        go[u] = off != kZero;
+        x[u] = *reinterpret_cast<const uint4*>(lrows + (go[u] ? off + r : kZero));
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const int32_t is = static_cast<int32_t>(i0 + u * 128 + 2 * lane) - static_cast<int32_t>(h);
+        const bool inr = is >= 0 && static_cast<uint32_t>(is) < total;
+        const uint32_t i = is < 0 ? 0u : (inr ? static_cast<uint32_t>(is) : total - 2);
+        if constexpr (kRecord) {
+          if (go[u] && inr) {
+            *reinterpret_cast<uint4*>(out + i) = x[u];
+            const uint64_t cw = (out - a.seen) + i;
+            record_word(a.hop_rec, cw, static_cast<uint64_t>(x[u].y) << 32 | x[u].x, round);
+            record_word(a.hop_rec, cw + 1, static_cast<uint64_t>(x[u].w) << 32 | x[u].z, round);
+          } else if (inr) {
+            *reinterpret_cast<uint4*>(out + i) = x[u];  // (zeros of an unreached node)
+          }
+        } else {
+          store_row16<kNT>(out + i, x[u]);
+        }
+        ctr_unit(c, go[u] && inr, popc4(x[u]), 2u);
+      }
     }
-    const uint32_t kp = p - x0;  // the parent's place in its window
-    const bool up = in && ((a.all_current & 1u) || ((reach_in[kp >> 6] >> (kp & 63)) & 1ull));
-    const bool ok = up && (f & kNodeLive);
-    if (in) tab[j] = ok ? src_base + kp * C.S : kZero;
-    if (ok && C.slice0) a.gen[y0 + j] = static_cast<uint8_t>(cur);
-    const uint64_t b = __ballot(ok);
-    if (reach_out && lane == 0) reach_out[j0 >> 6] = b;
-    uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
-    if (lane == 0) prev = y0 + j0 > C.nbase ? a.node_parent[y0 + j0 - 1] : kNoneNode;
-    // nodes and parents counted once per run (slice 0); words per slice (the
-    // parents' slices come from LDS: no parent words read)
-    ctr_nodes(c, in && C.slice0, ok && C.slice0, up && p != prev && C.slice0, C.S, 0u);
-    if (!C.slice0) c.sw += static_cast<uint64_t>(__popcll(b)) * C.S;
+  } else {
+    for (uint32_t i0 = 0; i0 < total + h; i0 += kU * 64) {
+      uint64_t m[kU];
+      bool go[kU];
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const int32_t is = static_cast<int32_t>(i0 + u * 64 + lane) - static_cast<int32_t>(h);
+        const uint32_t i = is < 0 ? 0u : (static_cast<uint32_t>(is) < total ? static_cast<uint32_t>(is) : total - 1);
+        int32_t kk, r;
+        split(i, kk, r);
+        const uint32_t off = ctab[kk];
+        go[u] = off != kZero;
+        m[u] = lrows[go[u] ? off + r : kZero];
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < kU; ++u) {
+        const int32_t is = static_cast<int32_t>(i0 + u * 64 + lane) - static_cast<int32_t>(h);
+        const bool inr = is >= 0 && static_cast<uint32_t>(is) < total;
+        const uint32_t i = is < 0 ? 0u : (inr ? static_cast<uint32_t>(is) : total - 1);
+        if constexpr (kRecord) {
+          if (go[u] && inr) {
+            out[i] = m[u];
+            record_word(a.hop_rec, (out - a.seen) + i, m[u], round);
+          } else if (inr) {
+            out[i] = m[u];
+          }
+        } else {
+          store_row8<kNT>(out + i, m[u]);
+        }
+        ctr_unit(c, go[u] && inr, static_cast<uint32_t>(__popcll(m[u])), 1u);
+      }
+    }
   }
 }
 
-// children of the consecutive nodes [x0, x1) of level k (k < levels): a
-// consecutive range of level k + 1
-__device__ __forceinline__ void chain_kids(const PullArgs& a, const ChainChunk& ch, uint32_t k, uint32_t rp_base,
-                                           uint32_t x0, uint32_t x1, uint32_t& c0, uint32_t& c1) {
-  c0 = a.row_ptr[x0] - rp_base + ch.first[k + 1];
-  c1 = a.row_ptr[x1] - rp_base + ch.first[k + 1];
+// One sub-run of level k: the nodes [y0, y0 + nk) (<= kChainKids), whose
+// parents lie in the level above, [x0, ...) with level table `up_tab`.  Each
+// node's stage offset into ctab (kChainWords: zeros) and its own table entry
+// into `tab` (indexed from the level's first node, y0 - lo); generations
+// stamped and nodes counted by the slice-0 wave.  pf_p / pf_f: the sub-run's
+// parent ids and flags when prefetched (null: loaded here).
+__device__ __forceinline__ void chain_resolve(const PullArgs& a, const ChainStep& C, uint32_t x0,
+                                              const uint8_t* up_tab, uint32_t y0, uint32_t nk, uint32_t* ctab,
+                                              uint8_t* tab, uint32_t lane, uint32_t cur, const uint32_t* pf_p,
+                                              const uint32_t* pf_f, WaveCtr& c) {
+  constexpr uint32_t kZero = kChainWords;
+#pragma unroll
+  for (uint32_t s = 0; s < kChainKids / 64; ++s) {
+    const uint32_t j0 = s * 64;
+    if (j0 >= nk) break;
+    const uint32_t j = j0 + lane;
+    const bool in = j < nk;
+    uint32_t p = kNoneNode, f = 0;
+    if (pf_p) {
+      p = in ? pf_p[s] : kNoneNode;
+      f = pf_f[s];
+    } else if (in) {
+      p = a.node_parent[y0 + j];
+      f = a.node_flags[y0 + j];
+    }
+    const uint8_t src = in ? up_tab[p - x0] : kChainNone;  // the parent's stage slot
+    const bool up = in && ((a.all_current & 1u) || src != kChainNone);
+    const bool ok = up && (f & kNodeLive);
+    if (in) {
+      ctab[j] = (ok && src < kChainZero) ? static_cast<uint32_t>(src) * C.S : kZero;
+      tab[j] = ok ? (src < kChainZero ? src : kChainZero) : kChainNone;
+    }
+    if (ok && C.slice0) a.gen[y0 + j] = static_cast<uint8_t>(cur);
+    uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
+    if (lane == 0) prev = y0 + j0 > C.nbase ? a.node_parent[y0 + j0 - 1] : kNoneNode;
+    // nodes and parents counted once per run (slice 0); words per slice (the
+    // parents' rows come from LDS: no parent words read)
+    ctr_nodes(c, in && C.slice0, ok && C.slice0, up && p != prev && C.slice0, C.S, 0u);
+    if (!C.slice0) c.sw += static_cast<uint64_t>(__popcll(__ballot(ok))) * C.S;
+  }
+}
+
+// The partial slots of round r0 + k of a chain launch (a switch: no dynamic
+// index into the kernel arguments).
+__device__ __forceinline__ uint64_t* chain_slots(const PullArgs& a, uint32_t i) {
+  switch (i) {
+    case 0: return a.partials_r[0];
+    case 1: return a.partials_r[1];
+    case 2: return a.partials_r[2];
+    case 3: return a.partials_r[3];
+    case 4: return a.partials_r[4];
+    default: return a.partials_r[5];
+  }
 }
 
 __device__ __forceinline__ void chain_flush(WaveCtr& c, uint64_t* partials, uint64_t slot, uint32_t lane) {
@@ -834,103 +938,137 @@ __global__ __launch_bounds__(kBlock) void k_chain_parents(ChainChunk* __restrict
   c.p_hi = node_parent[c.node_end - 1];
 }
 
-template <bool kRecord, bool kNT>
+// The descendant ranges of every chain chunk: in BFS order the children of
+// the level-(d + k) nodes [x0, x1) are the level-(d + k + 1) nodes
+// first[k + 1] + [row_ptr[x0], row_ptr[x1]) - row_ptr[first[k]].  A range
+// wider than kChainCap (the LDS level tables) flags the plan as unusable.
+__global__ __launch_bounds__(kBlock) void k_chain_ranges(ChainChunk* __restrict__ chunks, uint32_t n,
+                                                         const uint32_t* __restrict__ row_ptr,
+                                                         uint32_t* __restrict__ overflow) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  ChainChunk& c = chunks[i];
+  uint32_t x0 = c.node_begin, x1 = c.node_end;
+  bool over = false;
+  c.lo[0] = x0;
+  c.hi[0] = x1;
+  for (uint32_t k = 1; k < c.levels && k < kChainLevels; ++k) {
+    const uint32_t base = row_ptr[c.first[k - 1]];
+    const uint32_t y0 = c.first[k] + (row_ptr[x0] - base), y1 = c.first[k] + (row_ptr[x1] - base);
+    c.lo[k] = y0;
+    c.hi[k] = y1;
+    over |= y1 - y0 > kChainCap;
+    x0 = y0;
+    x1 = y1;
+  }
+  if (over) atomicOr(overflow, 1u);
+}
+
+// kSlices: the launch's chunks of rows wider than the stage (column slices,
+// a separate launch: the whole-row path keeps its registers)
+template <bool kRecord, bool kNT, bool kSlices>
 __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk* __restrict__ chunks,
                                                    uint32_t n_chunks, uint32_t round) {
-  __shared__ uint64_t stage[kChainWords + 2];       // the run, then one window per inner level; + a zero pair
-  __shared__ uint64_t src[kChainPar];               // level 0: the parents' row addresses
-  __shared__ uint32_t tab[kChainKids];              // an inner sub-run's stage offsets
+  __shared__ uint64_t stage[kChainWords + 2];  // the run's rows (slices); + the zero pair
+  __shared__ uint64_t src[kChainPar];          // level 0: the parents' row addresses; then ctab
+  static_assert(kChainKids * 4 <= kChainPar * 8, "ctab fits the source table");
+  uint32_t* const ctab = reinterpret_cast<uint32_t*>(src);  // a sub-run's stage offsets (levels >= 1)
   __shared__ uint32_t gen_lds[kChainPar / 4 + 2];
-  __shared__ uint64_t reach[kChainLevels - 1][kChainKids / 64];  // reach bits: the run, each inner window
+  __shared__ uint8_t tabs[2][kChainCap];       // level tables: this level's and the one above
   const uint32_t lane = threadIdx.x;
   uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds);
   const uint32_t cur = a.gen_cur & 0xFF;
   if (lane < 2) stage[kChainWords + lane] = 0;
   const uint32_t ci = blockIdx.x;
   if (ci >= n_chunks) return;
-  const ChainChunk ch = chunks[a.reverse ? n_chunks - 1 - ci : ci];
-  const TopicDev T = a.topics[ch.topic];
+  // the chunk's scalars (its level ranges are read per level, not held)
+  const ChainChunk* const cp = chunks + ci;
+  const uint32_t node_begin = cp->node_begin, node_end = cp->node_end, topic = cp->topic;
+  const uint32_t p_lo = cp->p_lo, p_hi = cp->p_hi, r0 = cp->r0, levels = cp->levels;
+  const TopicDev T = a.topics[topic];
   ChainStep C;
-  C.W = ch.W;
-  C.w0 = ch.w0;
-  C.S = ch.S;
+  C.W = cp->W;
+  C.w0 = kSlices ? cp->w0 : 0u;
+  C.S = kSlices ? cp->S : C.W;
   C.nbase = T.nbase;
-  C.base = (static_cast<uint64_t>(ch.row0_hi) << 32 | ch.row0_lo) - static_cast<uint64_t>(T.nbase) * ch.W;
-  C.slice0 = ch.w0 == 0;
-  const uint32_t levels = ch.levels;
-  const uint32_t n0 = ch.node_end - ch.node_begin;  // <= kChainPar (host plan)
-  const uint32_t win = ch.win;
-  const uint32_t base1 = n0 * C.S, base2 = base1 + win * C.S;  // inner windows' stage offsets
-  uint64_t* const slot_ptr[kChainLevels] = {a.partials_r[0], a.partials_r[1], a.partials_r[2], a.partials_r[3]};
+  C.base = (static_cast<uint64_t>(cp->row0_hi) << 32 | cp->row0_lo) - static_cast<uint64_t>(T.nbase) * C.W;
+  C.slice0 = C.w0 == 0;
+  const uint32_t n0 = node_end - node_begin;  // <= kChainPar, n0 * S <= kChainWords (host plan)
   const uint64_t slot = blockIdx.x % a.slot_mod;
-  WaveCtr c;
-  // level 0: the run, parents' slices from HBM
+  // level 1's first sub-run: parent ids and flags issued with level 0's metadata
+  uint32_t pf_p[kChainKids / 64], pf_f[kChainKids / 64];
+  const uint32_t lo1 = cp->lo[1];
+  const uint32_t nk1 = levels > 1 ? min(kChainKids, cp->hi[1] - lo1) : 0u;
+#pragma unroll
+  for (uint32_t s = 0; s < kChainKids / 64; ++s) {
+    const uint32_t j = s * 64 + lane;
+    pf_p[s] = j < nk1 ? a.node_parent[lo1 + j] : kNoneNode;
+    pf_f[s] = j < nk1 ? a.node_flags[lo1 + j] : 0u;
+  }
+  // level 0: the run, parents' rows (slices) from HBM
   {
     PullTopic P;
-    P.W = ch.W;
+    P.W = C.W;
     P.nbase = T.nbase;
     P.base = C.base;
     P.root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
-    PullCtr pc;
-    pull_resolve(a, P, ch.node_begin, n0, ch.p_lo, ch.p_hi, src, genl, lane, cur, pc, kNoneNode, kChainPar);
-    // (pull_resolve stamps generations and counts whole rows: slice 0 keeps
-    // its node counts, every slice its own words)
-    const uint32_t nodes = __reduce_add_sync(~0ull, pc.kids), hit = __reduce_add_sync(~0ull, pc.reached);
-    const uint32_t par = __reduce_add_sync(~0ull, pc.parents);
-    if (C.slice0) {
-      c.kids += __builtin_amdgcn_readfirstlane(nodes);
-      c.reached += __builtin_amdgcn_readfirstlane(hit);
-      c.parents += __builtin_amdgcn_readfirstlane(par);
-    }
-    c.sw += static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(hit)) * C.S;
-    c.pwords += static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(par)) * C.S;
-    for (uint32_t j0 = 0; j0 < n0; j0 += 64) {
-      const uint64_t b = __ballot(j0 + lane < n0 && src[j0 + lane] != 0);
-      if (lane == 0) reach[0][j0 >> 6] = b;
-    }
-    chain_stream<kRecord, kNT, true>(a, C, ch.node_begin, n0, nullptr, src, stage, levels > 1 ? 0u : kNoneNode, lane,
-                                     round + ch.r0, c);
-    chain_flush(c, slot_ptr[ch.r0], slot, lane);
-  }
-  if (levels < 2) return;
-  asm volatile("" ::: "memory");
-  const uint32_t rp1 = a.row_ptr[ch.first[0]];
-  uint32_t c1_0, c1_1;
-  chain_kids(a, ch, 0, rp1, ch.node_begin, ch.node_end, c1_0, c1_1);
-  const uint32_t step1 = levels > 2 ? win : kChainKids;
-  WaveCtr c1, c2, c3;
-  const uint32_t rp2 = levels > 2 ? a.row_ptr[ch.first[1]] : 0u;
-  const uint32_t rp3 = levels > 3 ? a.row_ptr[ch.first[2]] : 0u;
-  for (uint32_t y0 = c1_0; y0 < c1_1; y0 += step1) {
-    const uint32_t ny = min(step1, c1_1 - y0);
-    chain_resolve(a, C, ch.node_begin, reach[0], 0u, y0, ny, tab, levels > 2 ? reach[1] : nullptr, lane, cur, c1);
-    chain_stream<kRecord, kNT, false>(a, C, y0, ny, tab, nullptr, stage, levels > 2 ? base1 : kNoneNode, lane,
-                                      round + ch.r0 + 1, c1);
-    ctr_fold(c1);
-    if (levels < 3) continue;
-    uint32_t c2_0, c2_1;
-    chain_kids(a, ch, 1, rp2, y0, y0 + ny, c2_0, c2_1);
-    const uint32_t step2 = levels > 3 ? win : kChainKids;
-    for (uint32_t z0 = c2_0; z0 < c2_1; z0 += step2) {
-      const uint32_t nz = min(step2, c2_1 - z0);
-      chain_resolve(a, C, y0, reach[1], base1, z0, nz, tab, levels > 3 ? reach[2] : nullptr, lane, cur, c2);
-      chain_stream<kRecord, kNT, false>(a, C, z0, nz, tab, nullptr, stage, levels > 3 ? base2 : kNoneNode, lane,
-                                        round + ch.r0 + 2, c2);
-      ctr_fold(c2);
-      if (levels < 4) continue;
-      uint32_t c3_0, c3_1;
-      chain_kids(a, ch, 2, rp3, z0, z0 + nz, c3_0, c3_1);
-      for (uint32_t u0 = c3_0; u0 < c3_1; u0 += kChainKids) {
-        const uint32_t nu = min(kChainKids, c3_1 - u0);
-        chain_resolve(a, C, z0, reach[2], base2, u0, nu, tab, nullptr, lane, cur, c3);
-        chain_stream<kRecord, kNT, false>(a, C, u0, nu, tab, nullptr, stage, kNoneNode, lane, round + ch.r0 + 3, c3);
-        ctr_fold(c3);
+    WaveCtr c;
+    if constexpr (!kSlices) {
+      pull_resolve(a, P, node_begin, n0, p_lo, p_hi, src, genl, lane, cur, c, kNoneNode, kChainPar);
+      pull_stream<kRecord, true, true>(a, P, node_begin, n0, src, lane, round + r0, c, stage);
+    } else {
+      // (pull_resolve stamps generations and counts whole rows: slice 0 keeps
+      // its node counts, every slice its own words)
+      PullCtr pc;
+      pull_resolve(a, P, node_begin, n0, p_lo, p_hi, src, genl, lane, cur, pc, kNoneNode, kChainPar);
+      const uint32_t nodes = __reduce_add_sync(~0ull, pc.kids), hit = __reduce_add_sync(~0ull, pc.reached);
+      const uint32_t par = __reduce_add_sync(~0ull, pc.parents);
+      if (C.slice0) {
+        c.kids += __builtin_amdgcn_readfirstlane(nodes);
+        c.reached += __builtin_amdgcn_readfirstlane(hit);
+        c.parents += __builtin_amdgcn_readfirstlane(par);
       }
+      c.sw += static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(hit)) * C.S;
+      c.pwords += static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(par)) * C.S;
+      chain_stream<kRecord, true, true>(a, C, node_begin, n0, nullptr, src, stage, 0u, lane, round + r0, c);
     }
+    // the run's level table: a node's own stage slot if reached.  (Eager
+    // seen, PS_F_NO_LAZY_SEEN: an unreached node's slot holds its own row,
+    // zeros, so every node keeps its slot, as the generation test of a
+    // separate launch would find every generation current.)
+    for (uint32_t j = lane; j < n0; j += 64)
+      tabs[0][j] = (src[j] != 0 || (a.all_current & 1u)) ? static_cast<uint8_t>(j) : kChainNone;
+    chain_flush(c, chain_slots(a, r0), slot, lane);
   }
-  chain_flush(c1, slot_ptr[ch.r0 + 1], slot, lane);
-  if (levels > 2) chain_flush(c2, slot_ptr[ch.r0 + 2], slot, lane);
-  if (levels > 3) chain_flush(c3, slot_ptr[ch.r0 + 3], slot, lane);
+  // src (level 0's sources) is dead from here and its LDS becomes ctab: no
+  // memory access may move across the switch from one view to the other
+  asm volatile("" ::: "memory");
+  uint32_t x0 = node_begin;
+  for (uint32_t k = 1; k < levels; ++k) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(cp->lo[k]), hi = __builtin_amdgcn_readfirstlane(cp->hi[k]);
+    const uint8_t* up_tab = tabs[(k - 1) & 1];
+    uint8_t* tab = tabs[k & 1];
+    const bool ntk = kNT || k + 1 < levels;  // (only the launch's last level may be re-read soon)
+    WaveCtr c;
+    for (uint32_t y0 = lo; y0 < hi; y0 += kChainKids) {
+      const uint32_t nk = min(kChainKids, hi - y0);
+      chain_resolve(a, C, x0, up_tab, y0, nk, ctab, tab + (y0 - lo), lane, cur,
+                    k == 1 && y0 == lo ? pf_p : nullptr, pf_f, c);
+      if constexpr (!kSlices) {
+        uint64_t* out = a.seen + C.base + static_cast<uint64_t>(y0) * C.W;
+        if (ntk)
+          stage_stream<kRecord, true, kChainWords>(a, out, nk, C.W, ctab, stage, lane, round + r0 + k, c);
+        else
+          stage_stream<kRecord, false, kChainWords>(a, out, nk, C.W, ctab, stage, lane, round + r0 + k, c);
+      } else {
+        chain_stream<kRecord, true, false>(a, C, y0, nk, ctab, nullptr, stage, kNoneNode, lane, round + r0 + k, c);
+      }
+      ctr_fold(c);
+    }
+    chain_flush(c, chain_slots(a, r0 + k), slot, lane);
+    x0 = lo;
+    asm volatile("" ::: "memory");
+  }
 }
 
 }  // namespace
@@ -993,15 +1131,29 @@ hipError_t launch_chain_parents(ChainChunk* chunks, uint32_t n, const uint32_t* 
   return hipGetLastError();
 }
 
+hipError_t launch_chain_ranges(ChainChunk* chunks, uint32_t n, const uint32_t* row_ptr, uint32_t* overflow,
+                               hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_chain_ranges, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, chunks, n, row_ptr, overflow);
+  return hipGetLastError();
+}
+
 hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32_t n_chunks, uint32_t round,
-                             bool record, bool nt, hipStream_t s) {
+                             bool record, bool nt, bool slices, hipStream_t s) {
   if (n_chunks == 0) return hipSuccess;
-  if (record)
-    hipLaunchKernelGGL((k_pull_chain<true, false>), dim3(n_chunks), dim3(64), 0, s, a, chunks, n_chunks, round);
-  else if (nt)
-    hipLaunchKernelGGL((k_pull_chain<false, true>), dim3(n_chunks), dim3(64), 0, s, a, chunks, n_chunks, round);
-  else
-    hipLaunchKernelGGL((k_pull_chain<false, false>), dim3(n_chunks), dim3(64), 0, s, a, chunks, n_chunks, round);
+  const dim3 g(n_chunks), b(64);
+  if (slices) {
+    if (record)
+      hipLaunchKernelGGL((k_pull_chain<true, false, true>), g, b, 0, s, a, chunks, n_chunks, round);
+    else
+      hipLaunchKernelGGL((k_pull_chain<false, true, true>), g, b, 0, s, a, chunks, n_chunks, round);
+  } else if (record) {
+    hipLaunchKernelGGL((k_pull_chain<true, false, false>), g, b, 0, s, a, chunks, n_chunks, round);
+  } else if (nt) {
+    hipLaunchKernelGGL((k_pull_chain<false, true, false>), g, b, 0, s, a, chunks, n_chunks, round);
+  } else {
+    hipLaunchKernelGGL((k_pull_chain<false, false, false>), g, b, 0, s, a, chunks, n_chunks, round);
+  }
   return hipGetLastError();
 }
 

@@ -30,7 +30,10 @@ int upload_pull(ps_engine* e) {
   return PS_OK;
 }
 
-int upload_pair(ps_engine* e) {
+// *overflow: some chain chunk's level range exceeded kChainCap (checked once
+// per plan, with one readback): the caller replans without chains.
+int upload_pair(ps_engine* e, bool* overflow) {
+  *overflow = false;
   if (e->pair.version == e->pair_up) return PS_OK;
   const auto& C = e->pair.chunks;
   HIP_TRY(e->d_pp.ensure(std::max<size_t>(C.size(), 1) * sizeof(PullChunk)), "alloc pair chunks");
@@ -54,6 +57,18 @@ int upload_pair(ps_engine* e) {
       HIP_TRY(launch_chain_parents(e->d_chain.as<ChainChunk>(), static_cast<uint32_t>(K.size()),
                                    e->d_node_parent.as<uint32_t>(), e->stream),
               "chain chunk parents");
+    HIP_TRY(e->d_chain_ovf.ensure(4), "alloc chain overflow word");
+    HIP_TRY(hipMemsetAsync(e->d_chain_ovf.p, 0, 4, e->stream), "clear chain overflow word");
+    HIP_TRY(launch_chain_ranges(e->d_chain.as<ChainChunk>(), static_cast<uint32_t>(K.size()),
+                                e->d_row_ptr.as<uint32_t>(), e->d_chain_ovf.as<uint32_t>(), e->stream),
+            "chain ranges");
+    uint32_t ovf = 0;
+    HIP_TRY(hipMemcpyAsync(&ovf, e->d_chain_ovf.p, 4, hipMemcpyDeviceToHost, e->stream), "read chain overflow");
+    HIP_TRY(hipStreamSynchronize(e->stream), "sync");
+    if (ovf) {
+      *overflow = true;
+      return PS_OK;
+    }
   }
   e->pair_up = e->pair.version;
   return PS_OK;
@@ -323,8 +338,16 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     changed |= gch;
     changed |= plan_pair_chunks(e, L, flood_rounds);
     if (world > 1 && changed) annotate_chunks(e, L);
+    bool chain_overflow = false;
+    if ((rc = upload_pull(e)) || (rc = upload_pair(e, &chain_overflow))) return rc;
+    if (chain_overflow) {  // a subtree wider than the level tables: this plan runs without chains
+      e->chain_fail_key = e->pair.key;
+      e->pair.key.clear();
+      plan_pair_chunks(e, L, flood_rounds);
+      if (world > 1) annotate_chunks(e, L);
+      if ((rc = upload_pair(e, &chain_overflow))) return rc;
+    }
     e->round_kind = e->pair.kind;
-    if ((rc = upload_pull(e)) || (rc = upload_pair(e))) return rc;
     if (flood_rounds && (rc = upload_flood(e))) return rc;
     if (world > 1 && gch && (rc = upload_ghost(e))) return rc;
     // desc[3q..]: round q's partial slots (first, end, stride) for the reduce
@@ -612,7 +635,6 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     pa.ship = world > 1 ? e->d_ship.as<ShipEntry>() : nullptr;
     pa.send = e->d_send.as<uint64_t>();
     pa.all_current = (e->cfg.flags & PS_F_NO_LAZY_SEEN) ? 1u : 0u;
-    uint32_t dir = 1;  // the first launch after k_flood runs forward
     for (r = flood_rounds + 1; r <= planned0; ++r) {
       const uint8_t kind = e->round_kind[r];
       if (kind == PS_K_PAIR2 || kind == PS_K_CHAIN2) continue;  // written by the launch of an earlier round
@@ -650,17 +672,19 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       if (kind == PS_K_CHAIN) {  // rounds r .. r + len - 1 in one launch (one rank, or no exchange inside)
         const uint32_t len = e->pair.len[r];
         const uint32_t last = r + len - 1;
-        const bool ntc = last == planned0 || (last < e->pull.bytes.size() && e->pull.bytes[last] >= e->nt_bytes);
+        const bool ntc = last == planned0 || (last < e->pull.bytes.size() && e->pull.bytes[last] >= ps_engine::kNtBytes);
         pa.slot_mod = kPairSlots;
         pa.row_ptr = e->d_row_ptr.as<uint32_t>();
         for (uint32_t k = 0; k < kChainLevels; ++k)
           pa.partials_r[k] = k < len ? partials + static_cast<size_t>(e->woff_host[r + k]) * kNumCtr : nullptr;
-        pa.reverse = 0;
         HIP_TRY(time_mark(true), "event");
         ++launches;
-        HIP_TRY(launch_pull_chain(pa, e->d_chain.as<ChainChunk>() + e->pair.lo[r], e->pair.hi[r] - e->pair.lo[r], r,
-                                  record, ntc, s),
+        HIP_TRY(launch_pull_chain(pa, e->d_chain.as<ChainChunk>() + e->pair.lo[r], e->pair.gsplit[r] - e->pair.lo[r],
+                                  r, record, ntc, false, s),
                 "pull chain");
+        HIP_TRY(launch_pull_chain(pa, e->d_chain.as<ChainChunk>() + e->pair.gsplit[r],
+                                  e->pair.hi[r] - e->pair.gsplit[r], r, record, ntc, true, s),
+                "pull chain (column slices)");
         HIP_TRY(time_mark(false), "event");
         if (xr) HIP_TRY(hipStreamWaitEvent(s, e->ev_xchg, 0), "exchange join");  // (never: chains skip exchange rounds)
         continue;
@@ -668,10 +692,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       // rows nobody re-reads while they can still sit in the 256 MB MALL
       // (large rounds and the last round) store non-temporally
       const uint32_t rw = pair ? r + 1 : r;  // the round whose rows the next launch reads
-      const bool nt = rw < e->pull.bytes.size() && (e->pull.bytes[rw] >= e->nt_bytes || rw == planned0);
-      // alternate directions: each launch starts with the parents the one
-      // before it wrote last (PSAMD_REVERSE=0: always forward)
-      pa.reverse = e->alt_reverse ? (dir ^= 1u) : 0u;
+      const bool nt = rw < e->pull.bytes.size() && (e->pull.bytes[rw] >= ps_engine::kNtBytes || rw == planned0);
       pa.partials = partials + static_cast<size_t>(e->woff_host[r]) * kNumCtr;
       pa.slot_mod = pair ? kPairSlots : kPullSlots;
       if (pair) pa.partials2 = partials + static_cast<size_t>(e->woff_host[r + 1]) * kNumCtr;
@@ -1065,8 +1086,10 @@ int run_body(ps_engine* e, ps_stats* stp, bool may_defer) {
         uint8_t* dout = reinterpret_cast<uint8_t*>(dp + k);
         HIP_TRY(hipMemcpyAsync(dp, peers.data(), static_cast<size_t>(k) * 4, hipMemcpyHostToDevice, e->stream),
                 "upload reach query");
+        const size_t toff = static_cast<size_t>(&T - e->topics.data()) * e->cfg.n_peers;
         HIP_TRY(launch_reach_query(dp, k, e->cfg.n_peers, e->d_local.as<uint32_t>(), e->d_node_peer.as<uint32_t>(),
-                                   T.nbase, T.n_nodes, dout, e->stream),
+                                   T.nbase, T.n_nodes, e->d_tpar.as<uint32_t>() + toff, e->d_orph.as<uint8_t>() + toff,
+                                   T.tree.root(), dout, e->stream),
                 "reach query");
         HIP_TRY(hipMemcpyAsync(outv.data(), dout, k, hipMemcpyDeviceToHost, e->stream), "read reach query");
         HIP_TRY(hipStreamSynchronize(e->stream), "sync");

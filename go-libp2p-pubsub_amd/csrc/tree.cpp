@@ -341,20 +341,23 @@ int SubscriptionTree::after_message(const ReachQuery* reach) {
       reach_pass_ = 1;
     }
     std::vector<uint8_t> reached(parted_at_.size());
+    std::vector<uint8_t> cut;  // per unreached entry, in order
     if (reach) {
       int rc = (*reach)(parted_at_, reached);
       if (rc) return rc;
+      for (size_t i = 0; i < parted_at_.size(); ++i)
+        if (reached[i] != 1 && parted_at_[i] < n_) cut.push_back(reached[i] == 2);
+      for (auto& x : reached) x = x == 1;
     } else {
       for (size_t i = 0; i < parted_at_.size(); ++i)
         reached[i] = parted_at_[i] < n_ && reachable_memo(parted_at_[i]);
+      // the unreached ones: cut for good (below an Orphan) or kept for a
+      // later message, decided by walks run in lockstep
+      std::vector<uint32_t> unreached;
+      for (size_t i = 0; i < parted_at_.size(); ++i)
+        if (!reached[i] && parted_at_[i] < n_) unreached.push_back(parted_at_[i]);
+      below_orphan_many(unreached, cut);
     }
-    // the unreached ones: cut for good (below an Orphan) or kept for a later
-    // message, decided by walks run in lockstep
-    std::vector<uint32_t> unreached;
-    for (size_t i = 0; i < parted_at_.size(); ++i)
-      if (!reached[i] && parted_at_[i] < n_) unreached.push_back(parted_at_[i]);
-    std::vector<uint8_t> cut;
-    below_orphan_many(unreached, cut);
     size_t ui = 0;
     std::vector<uint32_t> keep;
     // scattered parents: their lines are fetched 16 ahead, their children's 8 ahead

@@ -50,9 +50,10 @@ class SubscriptionTree {
   int close_host(uint32_t peer);    // abrupt
   // Called once per message that floods this topic: lazy prune and repair of
   // failed writes at every node the message reached (rule Q3).  `reach`, if
-  // given, answers "did the message reach peer p" for a batch of peers (the
-  // engine asks the node space the message ran on); otherwise the tree walks
-  // up from each peer.
+  // given, answers for a batch of peers: 1 = the message reached the peer,
+  // 2 = it did not and an Orphan cuts the peer's upstream path for good, 0 =
+  // neither (the engine asks the node space the message ran on); otherwise
+  // the tree walks up from each peer.
   using ReachQuery = std::function<int(const std::vector<uint32_t>& peers, std::vector<uint8_t>& out)>;
   int after_message(const ReachQuery* reach = nullptr);
   bool has_pending_failures() const { return pending_failures_; }
@@ -68,6 +69,12 @@ class SubscriptionTree {
   // out the peers whose entry may have changed since the last call.
   uint32_t in_parent(uint32_t p) const {
     return rec_[p].state == PeerState::In && p != root_ ? rec_[p].up : kNone;
+  }
+  // in_parent, or kOrphanUp for an Orphan (its subtree is cut for good): what
+  // the GPU rebuild ships, so the lazy prune's orphan walks run there too
+  static constexpr uint32_t kOrphanUp = 0xFFFFFFFEu;
+  uint32_t upstream_code(uint32_t p) const {
+    return rec_[p].state == PeerState::Orphan ? kOrphanUp : in_parent(p);
   }
   void take_touched(std::vector<uint32_t>& out);
   // Peers reachable for the NEXT message (failed hosts cut their subtree).

@@ -10,7 +10,8 @@ import numpy as np
 from . import DistConfig, EngineError, PART_PEER, _P, _p, _u32arr, load
 
 INFO, NODES, PARENT, GHOST_REF, TOPIC, LAYOUT, ROUND_KIND, PULL, PAIR, XCHG, SEGS, SHIP, PACK, CHAIN = range(14)
-CHAIN_FIELDS = ("node_begin", "node_end", "topic", "W", "row0", "w0", "S", "levels", "r0", "win", "group")
+CHAIN_FIELDS = ("node_begin", "node_end", "topic", "W", "row0", "w0", "S", "levels", "r0", "group")
+CHAIN_LEVELS = 6  # kChainLevels
 CHUNK_FIELDS = ("node_begin", "node_end", "topic", "W", "row0", "e_lo", "e_hi", "gin", "gout", "group",
                 "p_lo", "p_hi", "c_lo")
 PROTOTYPES = [
@@ -131,7 +132,7 @@ class Plan:
         n = int(v[0])
         if n == 0:
             return 0, []
-        body = v[1:].reshape(-1, len(CHAIN_FIELDS) + 5)
+        body = v[1:].reshape(-1, len(CHAIN_FIELDS) + CHAIN_LEVELS + 1)
         out = []
         for row in body:
             c = dict(zip(CHAIN_FIELDS, (int(x) for x in row[:len(CHAIN_FIELDS)])))

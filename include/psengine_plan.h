@@ -46,8 +46,8 @@ int ps_plan_window(ps_engine* e, const uint32_t* topic_of_msg, const uint32_t* s
 #define PS_PLAN_SEGS 10       /* per segment: topic, rw, rbase[world], sbase[world] */
 #define PS_PLAN_SHIP 11       /* per ship entry: node, dst (rank << 27 | record index) */
 #define PS_PLAN_PACK 12       /* index = round: per root segment e0, e1, gseg, W, row, unit0 */
-#define PS_PLAN_CHAIN 13      /* index = round: rounds of the launch, then per chunk 16 values: node_begin,
-                                 node_end, topic, W, row0, w0, S, levels, r0, win, group, first[0..4] */
+#define PS_PLAN_CHAIN 13      /* index = round: rounds of the launch, then per chunk 17 values: node_begin,
+                                 node_end, topic, W, row0, w0, S, levels, r0, group, first[0..6] */
 int ps_plan_get(ps_engine* e, uint32_t what, uint32_t index, uint64_t* out, size_t cap, size_t* n_out);
 
 #ifdef __cplusplus

@@ -1,10 +1,10 @@
-"""k_pull_chain -- rounds q .. q + L - 1 (L = 3, 4) of a level window in one
-launch: each wave writes a run of level-d nodes (its parents' rows from HBM)
-and then every descendant of the run level by level, each copying its
-parent's column slice from the LDS stage the wave wrote one level above
- -- against the restatement (oracle/psoracle.c) and against
-one k_pull launch per round (PSAMD_CHAIN=1) and pair launches
-(PSAMD_CHAIN=2); PSAMD_CHAIN is read at engine creation.
+"""k_pull_chain -- rounds q .. q + L - 1 (L = 3 .. 6) of a level window in
+one launch: each wave writes a run of level-d nodes (its parents' rows from
+HBM, kept in its LDS stage) and then every descendant of the run level by
+level, each node copying the stage row its parent holds --
+against the restatement (oracle/psoracle.c) and against one k_pull launch per
+round (PSAMD_CHAIN=1) and pair launches (PSAMD_CHAIN=2); PSAMD_CHAIN is read
+at engine creation.
 
 Round q delivers to BFS level q - s of each topic: a node receives its
 parent's row of round q - 1 if the parent was reached this window and the
@@ -13,8 +13,8 @@ at :326-331; client.processMessages, client.go:100-132).  Every schedule must
 give the oracle's (peer, message, hop) exactly and the same per-round
 counters and final seen state: recording and production instances, single
 starts and start groups (a group entering inside a chain starts its own run
-there), lazy and eager seen, rows wider than a slice, fan-outs that overflow
-a window.
+there), lazy and eager seen, rows wider than the stage (column slices), and
+subtrees wider than the level tables (the plan falls back to pairs).
 """
 import numpy as np
 import pytest
@@ -47,7 +47,7 @@ def run(monkeypatch, chain, n, topics, live, msg_topics, starts=None, record=Tru
     return st, kinds, hops, deliv, key
 
 
-def sweep(monkeypatch, n, topics, live, msg_topics, starts=None, chains=(1, 2, 3, 4), records=(True, False),
+def sweep(monkeypatch, n, topics, live, msg_topics, starts=None, chains=(1, 2, 3, 4, 6), records=(True, False),
           expect_chain=True, **kw):
     exp = oracle_hops(topics, live)
     ref = None
@@ -79,11 +79,12 @@ def test_chain_parity(monkeypatch, seed):
     assert key[0] == sum(int((exp[t] != 0xFF).sum()) * int((msg_topics == t).sum()) for t in exp)
 
 
-@pytest.mark.parametrize("n_msgs", [6000, 21000])
+@pytest.mark.parametrize("n_msgs", [21000, 52000])
 def test_chain_column_slices(monkeypatch, n_msgs):
-    """Rows wider than a slice (94 and 330 words: the hot topic of cfg3): each
-    run is written by one wave per column slice; the slices tile every row
-    exactly, and only the slice-0 wave counts nodes."""
+    """Whole rows of 330 words (the hot topic of cfg3), and rows of 814 words,
+    wider than the 768-word stage: each run is then written by one wave per
+    column slice; the slices tile every row exactly, and only the slice-0
+    wave counts nodes."""
     rng = np.random.default_rng(1950 + n_msgs)
     n = 3000
     topics = [(0, random_tree(rng, n, 0, 3)), (7, random_tree(rng, n, 7, 5))]
@@ -91,10 +92,10 @@ def test_chain_column_slices(monkeypatch, n_msgs):
     live[0] = live[7] = 1
     msg_topics = np.concatenate([np.zeros(n_msgs, dtype=np.uint32), np.ones(150, dtype=np.uint32)])
     rng.shuffle(msg_topics)
-    sweep(monkeypatch, n, topics, live, msg_topics, records=(False,), msg_window=1 << 15)
+    sweep(monkeypatch, n, topics, live, msg_topics, records=(False,), chains=(1, 2, 4, 6), msg_window=1 << 16)
     # hops of a sample through a recording run
     exp = oracle_hops(topics, live)
-    st, kinds, hops, _, _ = run(monkeypatch, 4, n, topics, live, msg_topics[:5000], msg_window=1 << 15)
+    st, kinds, hops, _, _ = run(monkeypatch, 4, n, topics, live, msg_topics[:5000], msg_window=1 << 16)
     assert PE.K_CHAIN in kinds
     check_hops(hops, exp, msg_topics[:5000], "chain=4 record")
 
@@ -111,8 +112,8 @@ def test_chain_start_groups(monkeypatch, seed):
 
 
 def test_chain_fanout_heavy(monkeypatch):
-    """Fan-out up to 24: a run's descendants overflow the inner windows, which
-    are processed one after the other (depth first)."""
+    """Fan-out up to 24: runs of one node, or no chain where even one node's
+    subtree is expected wider than the level tables."""
     rng = np.random.default_rng(1991)
     n = 30000
     topics = [(5, random_tree(rng, n, 5, 24)), (11, random_tree(rng, n, 11, 12))]
@@ -120,7 +121,28 @@ def test_chain_fanout_heavy(monkeypatch):
     for r, _ in topics:
         live[r] = 1
     msg_topics = np.array([0] * 40 + [1] * 70 + [0] * 3000, dtype=np.uint32)  # W = 48 and W = 2
-    sweep(monkeypatch, n, topics, live, msg_topics, chains=(1, 4))
+    sweep(monkeypatch, n, topics, live, msg_topics, chains=(1, 3, 4), expect_chain=False)
+
+
+def test_chain_range_overflow_falls_back(monkeypatch):
+    """A broom: level 2 of 200 nodes, one of which has 2,000 children and the
+    others one each (the planner's average growth sizes a chain of rounds 2-4
+    into runs of ~46 nodes, so the run holding the heavy node overflows a
+    1,024-node level table): k_chain_ranges flags the plan and the window runs
+    on pairs, with the same results."""
+    n = 4000
+    parent = np.full(n, O.NONE, dtype=np.uint32)
+    parent[1:3] = 0                          # level 1: peers 1, 2
+    parent[3:203] = np.repeat([1, 2], 100)   # level 2: 200 peers
+    parent[203:2203] = 57                    # level 3: 2,000 children of peer 57 ...
+    parent[2203:2402] = [x for x in range(3, 203) if x != 57]  # ... and one of every other
+    parent[2402:] = np.arange(2402, n) - 2000  # level 4: one child each for 1,598 of them
+    live = np.ones(n, dtype=np.uint8)
+    live[5] = 0
+    msg_topics = np.zeros(500, dtype=np.uint32)
+    sweep(monkeypatch, n, [(0, parent)], live, msg_topics, chains=(1, 2, 4), expect_chain=False)
+    st, kinds, _, _, _ = run(monkeypatch, 4, n, [(0, parent)], live, msg_topics, record=False)
+    assert PE.K_CHAIN not in kinds and PE.K_PAIR in kinds, kinds
 
 
 def test_chain_eager_seen(monkeypatch):
@@ -129,7 +151,7 @@ def test_chain_eager_seen(monkeypatch):
     rng = np.random.default_rng(1993)
     n, topics, live = make_case(rng, 1000, 3000, nt_hi=2, dead=0.2)
     msg_topics = rng.integers(0, len(topics), size=300).astype(np.uint32)
-    sweep(monkeypatch, n, topics, live, msg_topics, chains=(1, 4), records=(True,), flags=PE.F_NO_LAZY_SEEN)
+    sweep(monkeypatch, n, topics, live, msg_topics, chains=(1, 4, 6), records=(True,), flags=PE.F_NO_LAZY_SEEN)
 
 
 @pytest.mark.parametrize("seed", range(2))
@@ -143,14 +165,14 @@ def test_chain_after_flood(monkeypatch, seed):
 
 
 def test_chain_deep_path_hops_past_255(monkeypatch):
-    """A 600-deep chain of peers: 4-round launches only (PSAMD_FLOOD=0); hops
+    """A 600-deep chain of peers: 4- and 6-round launches only (PSAMD_FLOOD=0); hops
     past 255 saturate at 254 as in the restatement."""
     n = 600
     parent = np.full(n, O.NONE, dtype=np.uint32)
     parent[1:] = np.arange(n - 1, dtype=np.uint32)
     live = np.ones(n, dtype=np.uint8)
     msg_topics = np.zeros(130, dtype=np.uint32)
-    sweep(monkeypatch, n, [(0, parent)], live, msg_topics, chains=(1, 4))
+    sweep(monkeypatch, n, [(0, parent)], live, msg_topics, chains=(1, 4, 6))
 
 
 def test_chain_many_windows_and_drains(monkeypatch):
@@ -162,7 +184,7 @@ def test_chain_many_windows_and_drains(monkeypatch):
     starts = rng.integers(0, 4, size=1500).astype(np.uint32)
     peers = [int(p) for p in rng.integers(0, n, size=12)]
     outs = []
-    for chain in (1, 4):
+    for chain in (1, 4, 6):
         monkeypatch.setenv("PSAMD_CHAIN", str(chain))
         monkeypatch.setenv("PSAMD_FLOOD", "0")
         with PE.Engine(n, len(topics), record_hops=True, msg_window=128) as eng:
@@ -174,4 +196,4 @@ def test_chain_many_windows_and_drains(monkeypatch):
             assert st.windows >= 6
             drains = [eng.peer_messages(t, p).tolist() for t in range(len(topics)) for p in peers]
             outs.append((st.deliveries, drains))
-    assert outs[0] == outs[1]
+    assert outs[0] == outs[1] == outs[2]

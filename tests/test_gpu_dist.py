@@ -57,14 +57,18 @@ def merged_hops(engines, msg):
     return h.min(axis=0)  # every peer is owned by exactly one rank per topic
 
 
+@pytest.mark.parametrize("overlap", ["0", "1"])
 @pytest.mark.parametrize("staggered", [True, False])
 @pytest.mark.parametrize("world,partition", [(2, PE.PART_SUBTREE), (3, PE.PART_PEER),
                                              (4, PE.PART_SUBTREE), (4, PE.PART_PEER)])
-def test_sharded_trees_match_oracle(world, partition, staggered):
+def test_sharded_trees_match_oracle(monkeypatch, world, partition, staggered, overlap):
     """Level mode on N ranks, single start round and staggered starts (start
     groups: one word block per start round, each group's ghost records
     exchanged in its own rounds), with dead peers cutting subtrees across
-    ranks; never the compaction path."""
+    ranks; never the compaction path.  overlap=1: the
+    exchange on its own stream beside the round's locally fed chunks, as RCCL
+    runs it (the loopback default is one stream)."""
+    monkeypatch.setenv("PSAMD_XCHG_OVERLAP", overlap)
     rng = np.random.default_rng(world * 10 + partition + 100 * staggered)
     n, n_topics = 2500, 3
     lb, engines = make_ranks(world, n, n_topics, partition)

@@ -159,12 +159,11 @@ class RankSim:
         n, chunks = self.p.chain(q)
         assert n >= 3
         for c in chunks:
-            c["W"] = c["W"]
-            L, S, win = c["levels"], c["S"], c["win"]
+            L, S = c["levels"], c["S"]
             n0 = c["node_end"] - c["node_begin"]
-            assert 1 <= L <= 4 and c["r0"] + L <= n and n0 <= 128 and win <= 128
+            assert 1 <= L <= PL.CHAIN_LEVELS and c["r0"] + L <= n and 1 <= n0 <= 128
             assert S % 2 == 0 or S == c["W"]
-            assert n0 * S + max(0, L - 2) * win * S <= 1024, (n0, S, L, win)  # the LDS stage
+            assert n0 * S <= 768, (n0, S, L)  # the LDS stage holds the run's rows (slices)
             assert c["first"][0] == self.topics[c["topic"]]["nbase"] + self.topics[c["topic"]]["level_off"][
                 self.level[c["node_begin"]]]
             win_nodes = list(range(c["node_begin"], c["node_end"]))
@@ -299,7 +298,7 @@ def build(world, partition, n=1500, n_topics=2, seed=0, fan=None):
     return rng, trees, roots, live
 
 
-@pytest.mark.parametrize("chain", [2, 4])
+@pytest.mark.parametrize("chain", [2, 4, 6])
 @pytest.mark.parametrize("staggered", [False, True])
 @pytest.mark.parametrize("world,partition", [(1, PE.PART_PEER), (2, PE.PART_PEER), (3, PE.PART_PEER),
                                              (4, PE.PART_SUBTREE), (4, PE.PART_PEER)])

@@ -57,12 +57,26 @@ int main(int argc, char** argv) {
     for (uint32_t p : join[b]) T.subscribe(p);
     const auto d0 = clk::now();
     const size_t pend = T.parted_parents();
-    // the engine answers reach from the GPU node space; here from a BFS,
-    // outside the timed part
+    // the engine answers reach (and cut-for-good) from the GPU node space;
+    // here from a BFS and upward walks, outside the timed part
     std::vector<uint32_t> par;
     T.attached_parents(par);
+    double tq = 0;
     SubscriptionTree::ReachQuery q = [&](const std::vector<uint32_t>& peers, std::vector<uint8_t>& out) {
-      for (size_t i = 0; i < peers.size(); ++i) out[i] = peers[i] == root || par[peers[i]] != kNone;
+      const auto q0 = clk::now();
+      for (size_t i = 0; i < peers.size(); ++i) {
+        const uint32_t p = peers[i];
+        out[i] = p == root || par[p] != kNone;
+        for (uint32_t x = p; !out[i] && x != root;) {
+          const uint32_t up = T.upstream_code(x);
+          if (up >= n) {
+            out[i] = up == SubscriptionTree::kOrphanUp ? 2 : 0;
+            break;
+          }
+          x = up;
+        }
+      }
+      tq += ms(q0, clk::now());
       return 0;
     };
     const auto d = clk::now();
@@ -72,7 +86,7 @@ int main(int argc, char** argv) {
     auto e = clk::now();
     tl += ms(a, c);
     tj += ms(c, d0);
-    tp += ms(d, e);
+    tp += ms(d, e) - tq;
   }
   std::printf("per batch: leave %.3f ms  join %.3f ms  prune (reach given) %.3f ms  (%u batches, %zu/%zu ops)\n",
               tl / batches, tj / batches, tp / batches, batches, leave[0].size(), join[0].size());
