@@ -237,6 +237,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   key.push_back(e->pair_on ? 1 : 0);
   key.push_back(e->chain_max);
   key.push_back(e->chain_words);
+  key.push_back(e->chain_compact ? 1 : 0);
   for (size_t q = 0; q < xchg.size(); ++q) key.push_back(xchg[q].any);
   PairPlan& PP = e->pair;
   if (key == PP.key) return false;
@@ -274,18 +275,19 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   }
   // A chain of `levels` levels from level d of (topic t, block of W words):
   // its runs, column slice and per-level growth.  Runs are sized so that the
-  // stage holds their rows (slices of kChainWords words for wider rows), the
-  // expected widest level range is half of kChainCap (k_chain_ranges checks
+  // stage holds their rows (slices of the stage width for wider rows), the
+  // expected widest level range is half of the level tables (k_chain_ranges checks
   // the real ranges), and a wave writes about chain_words row words.
   struct ChainSize {
     uint32_t R = 0, S = 0;  // R = 0: no chain of this length
   };
+  const uint32_t stage_w = chain_stage_words(e->chain_compact), cap = chain_cap(e->chain_compact);
   auto chain_size = [&](const TopicHost& T, uint32_t d, uint32_t levels, uint32_t W) {
     ChainSize z;
     const double n0 = static_cast<double>(T.level_off[d + 1] - T.level_off[d]);
     if (n0 == 0) {  // no node of the level on this rank: nothing to cut
       z.R = 1;
-      z.S = std::max<uint32_t>(1, std::min(W, kChainWords));
+      z.S = std::max<uint32_t>(1, std::min(W, stage_w));
       return z;
     }
     double gmax = 1.0, gsum = 1.0;
@@ -294,10 +296,10 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
       gmax = std::max(gmax, g);
       gsum += g;
     }
-    if (gmax > kChainCap / 2) return z;  // even one node's subtree is expected too wide
-    z.S = W <= kChainWords ? W : kChainWords;
-    const double r = std::min({static_cast<double>(kChainPar), static_cast<double>(kChainWords / z.S),
-                               std::floor(kChainCap / 2 / gmax),
+    if (gmax > cap / 2) return z;  // even one node's subtree is expected too wide
+    z.S = W <= stage_w ? W : stage_w;
+    const double r = std::min({static_cast<double>(kChainPar), static_cast<double>(stage_w / z.S),
+                               std::floor(cap / 2 / gmax),
                                std::floor(static_cast<double>(e->chain_words) / (z.S * gsum))});
     z.R = static_cast<uint32_t>(std::max(1.0, r));
     return z;

@@ -667,17 +667,16 @@ __device__ __forceinline__ void chain_split(uint32_t i, float rs, uint32_t S, in
 }
 
 // Column slices (S < W): streams nk nodes' slices [y0, y0 + nk): element
-// (kk, r) = source slot tab[kk] (LDS offset into `stage`, kChainWords: zeros)
+// (kk, r) = source slot tab[kk] (LDS offset into `stage`, kZero: zeros)
 // + r -- or, level 0, the parent row address src64[kk] (0: rewrite the
 // node's own words) -- into the node's row in HBM and, when dst !=
 // kNoneNode, the stage at dst + kk * S + r.  16-B units (even S) or words;
 // lanes past the end repeat the last unit.
-template <bool kRecord, bool kNT, bool kFromHbm>
+template <bool kRecord, bool kNT, bool kFromHbm, uint32_t kZero>
 __device__ __forceinline__ void chain_stream(const PullArgs& a, const ChainStep& C, uint32_t y0, uint32_t nk,
                                              const uint32_t* tab, const uint64_t* src64, uint64_t* stage,
                                              uint32_t dst, uint32_t lane, uint32_t round, WaveCtr& c) {
   constexpr uint32_t kU = 8;
-  constexpr uint32_t kZero = kChainWords;
   const uint32_t S = C.S, W = C.W;
   const uint32_t total = nk * S;
   if (total == 0) return;
@@ -865,15 +864,15 @@ __device__ __forceinline__ void stage_stream(const PullArgs& a, uint64_t* out, u
 
 // One sub-run of level k: the nodes [y0, y0 + nk) (<= kChainKids), whose
 // parents lie in the level above, [x0, ...) with level table `up_tab`.  Each
-// node's stage offset into ctab (kChainWords: zeros) and its own table entry
+// node's stage offset into ctab (kZero: zeros) and its own table entry
 // into `tab` (indexed from the level's first node, y0 - lo); generations
 // stamped and nodes counted by the slice-0 wave.  pf_p / pf_f: the sub-run's
 // parent ids and flags when prefetched (null: loaded here).
+template <uint32_t kZero>
 __device__ __forceinline__ void chain_resolve(const PullArgs& a, const ChainStep& C, uint32_t x0,
                                               const uint8_t* up_tab, uint32_t y0, uint32_t nk, uint32_t* ctab,
                                               uint8_t* tab, uint32_t lane, uint32_t cur, const uint32_t* pf_p,
                                               const uint32_t* pf_f, WaveCtr& c) {
-  constexpr uint32_t kZero = kChainWords;
 #pragma unroll
   for (uint32_t s = 0; s < kChainKids / 64; ++s) {
     const uint32_t j0 = s * 64;
@@ -941,9 +940,9 @@ __global__ __launch_bounds__(kBlock) void k_chain_parents(ChainChunk* __restrict
 // The descendant ranges of every chain chunk: in BFS order the children of
 // the level-(d + k) nodes [x0, x1) are the level-(d + k + 1) nodes
 // first[k + 1] + [row_ptr[x0], row_ptr[x1]) - row_ptr[first[k]].  A range
-// wider than kChainCap (the LDS level tables) flags the plan as unusable.
+// wider than `cap` (the LDS level tables) flags the plan as unusable.
 __global__ __launch_bounds__(kBlock) void k_chain_ranges(ChainChunk* __restrict__ chunks, uint32_t n,
-                                                         const uint32_t* __restrict__ row_ptr,
+                                                         const uint32_t* __restrict__ row_ptr, uint32_t cap,
                                                          uint32_t* __restrict__ overflow) {
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
@@ -957,7 +956,7 @@ __global__ __launch_bounds__(kBlock) void k_chain_ranges(ChainChunk* __restrict_
     const uint32_t y0 = c.first[k] + (row_ptr[x0] - base), y1 = c.first[k] + (row_ptr[x1] - base);
     c.lo[k] = y0;
     c.hi[k] = y1;
-    over |= y1 - y0 > kChainCap;
+    over |= y1 - y0 > cap;
     x0 = y0;
     x1 = y1;
   }
@@ -965,20 +964,23 @@ __global__ __launch_bounds__(kBlock) void k_chain_ranges(ChainChunk* __restrict_
 }
 
 // kSlices: the launch's chunks of rows wider than the stage (column slices,
-// a separate launch: the whole-row path keeps its registers)
-template <bool kRecord, bool kNT, bool kSlices>
+// a separate launch: the whole-row path keeps its registers).  kCompact: the
+// 736-word stage and 512-node level tables (8 KB of LDS: 20 resident waves
+// per CU) instead of 768 words and 1,024 nodes (9.4 KB: 17).
+template <bool kRecord, bool kNT, bool kSlices, bool kCompact>
 __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk* __restrict__ chunks,
                                                    uint32_t n_chunks, uint32_t round) {
-  __shared__ uint64_t stage[kChainWords + 2];  // the run's rows (slices); + the zero pair
-  __shared__ uint64_t src[kChainPar];          // level 0: the parents' row addresses; then ctab
+  constexpr uint32_t kStage = chain_stage_words(kCompact), kCap = chain_cap(kCompact);
+  __shared__ uint64_t stage[kStage + 2];  // the run's rows (slices); + the zero pair
+  __shared__ uint64_t src[kChainPar];     // level 0: the parents' row addresses; then ctab
   static_assert(kChainKids * 4 <= kChainPar * 8, "ctab fits the source table");
   uint32_t* const ctab = reinterpret_cast<uint32_t*>(src);  // a sub-run's stage offsets (levels >= 1)
   __shared__ uint32_t gen_lds[kChainPar / 4 + 2];
-  __shared__ uint8_t tabs[2][kChainCap];       // level tables: this level's and the one above
+  __shared__ uint8_t tabs[2][kCap];  // level tables: this level's and the one above
   const uint32_t lane = threadIdx.x;
   uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds);
   const uint32_t cur = a.gen_cur & 0xFF;
-  if (lane < 2) stage[kChainWords + lane] = 0;
+  if (lane < 2) stage[kStage + lane] = 0;
   const uint32_t ci = blockIdx.x;
   if (ci >= n_chunks) return;
   // the chunk's scalars (its level ranges are read per level, not held)
@@ -993,7 +995,7 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
   C.nbase = T.nbase;
   C.base = (static_cast<uint64_t>(cp->row0_hi) << 32 | cp->row0_lo) - static_cast<uint64_t>(T.nbase) * C.W;
   C.slice0 = C.w0 == 0;
-  const uint32_t n0 = node_end - node_begin;  // <= kChainPar, n0 * S <= kChainWords (host plan)
+  const uint32_t n0 = node_end - node_begin;  // <= kChainPar, n0 * S <= kStage (host plan)
   const uint64_t slot = blockIdx.x % a.slot_mod;
   // level 1's first sub-run: parent ids and flags issued with level 0's metadata
   uint32_t pf_p[kChainKids / 64], pf_f[kChainKids / 64];
@@ -1030,7 +1032,7 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
       }
       c.sw += static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(hit)) * C.S;
       c.pwords += static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(par)) * C.S;
-      chain_stream<kRecord, true, true>(a, C, node_begin, n0, nullptr, src, stage, 0u, lane, round + r0, c);
+      chain_stream<kRecord, true, true, kStage>(a, C, node_begin, n0, nullptr, src, stage, 0u, lane, round + r0, c);
     }
     // the run's level table: a node's own stage slot if reached.  (Eager
     // seen, PS_F_NO_LAZY_SEEN: an unreached node's slot holds its own row,
@@ -1043,31 +1045,56 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
   // src (level 0's sources) is dead from here and its LDS becomes ctab: no
   // memory access may move across the switch from one view to the other
   asm volatile("" ::: "memory");
+  // levels 1 .. levels - 1, sub-run by sub-run; each sub-run's parent ids
+  // and flags were loaded before the previous sub-run's stream (pf_p / pf_f),
+  // so a level costs no round trip of its own
   uint32_t x0 = node_begin;
-  for (uint32_t k = 1; k < levels; ++k) {
-    const uint32_t lo = __builtin_amdgcn_readfirstlane(cp->lo[k]), hi = __builtin_amdgcn_readfirstlane(cp->hi[k]);
-    const uint8_t* up_tab = tabs[(k - 1) & 1];
-    uint8_t* tab = tabs[k & 1];
-    const bool ntk = kNT || k + 1 < levels;  // (only the launch's last level may be re-read soon)
-    WaveCtr c;
-    for (uint32_t y0 = lo; y0 < hi; y0 += kChainKids) {
-      const uint32_t nk = min(kChainKids, hi - y0);
-      chain_resolve(a, C, x0, up_tab, y0, nk, ctab, tab + (y0 - lo), lane, cur,
-                    k == 1 && y0 == lo ? pf_p : nullptr, pf_f, c);
-      if constexpr (!kSlices) {
-        uint64_t* out = a.seen + C.base + static_cast<uint64_t>(y0) * C.W;
-        if (ntk)
-          stage_stream<kRecord, true, kChainWords>(a, out, nk, C.W, ctab, stage, lane, round + r0 + k, c);
-        else
-          stage_stream<kRecord, false, kChainWords>(a, out, nk, C.W, ctab, stage, lane, round + r0 + k, c);
-      } else {
-        chain_stream<kRecord, true, false>(a, C, y0, nk, ctab, nullptr, stage, kNoneNode, lane, round + r0 + k, c);
-      }
-      ctr_fold(c);
+  uint32_t k = 1;
+  uint32_t lo = lo1, hi = levels > 1 ? __builtin_amdgcn_readfirstlane(cp->hi[1]) : lo1;
+  uint32_t y0 = lo;
+  WaveCtr c;
+  while (k < levels) {
+    if (y0 >= hi) {  // level k done
+      chain_flush(c, chain_slots(a, r0 + k), slot, lane);
+      asm volatile("" ::: "memory");
+      x0 = lo;
+      if (++k >= levels) break;
+      lo = __builtin_amdgcn_readfirstlane(cp->lo[k]);
+      hi = __builtin_amdgcn_readfirstlane(cp->hi[k]);
+      y0 = lo;
+      continue;
     }
-    chain_flush(c, chain_slots(a, r0 + k), slot, lane);
-    x0 = lo;
-    asm volatile("" ::: "memory");
+    const uint32_t nk = min(kChainKids, hi - y0);
+    chain_resolve<kStage>(a, C, x0, tabs[(k - 1) & 1], y0, nk, ctab, tabs[k & 1] + (y0 - lo), lane, cur, pf_p,
+                          pf_f, c);
+    // the next sub-run: this level's next, or the next level's first
+    uint32_t n_lo = y0 + kChainKids, n_hi = hi;
+    if (n_lo >= hi) {
+      n_lo = n_hi = 0;
+      if (k + 1 < levels) {
+        n_lo = __builtin_amdgcn_readfirstlane(cp->lo[k + 1]);
+        n_hi = __builtin_amdgcn_readfirstlane(cp->hi[k + 1]);
+      }
+    }
+    const uint32_t n_nk = min(kChainKids, n_hi - n_lo);
+#pragma unroll
+    for (uint32_t s = 0; s < kChainKids / 64; ++s) {
+      const uint32_t j = s * 64 + lane;
+      pf_p[s] = j < n_nk ? a.node_parent[n_lo + j] : kNoneNode;
+      pf_f[s] = j < n_nk ? a.node_flags[n_lo + j] : 0u;
+    }
+    if constexpr (!kSlices) {
+      uint64_t* out = a.seen + C.base + static_cast<uint64_t>(y0) * C.W;
+      if (kNT || k + 1 < levels)  // (only the launch's last level may be re-read soon)
+        stage_stream<kRecord, true, kStage>(a, out, nk, C.W, ctab, stage, lane, round + r0 + k, c);
+      else
+        stage_stream<kRecord, false, kStage>(a, out, nk, C.W, ctab, stage, lane, round + r0 + k, c);
+    } else {
+      chain_stream<kRecord, true, false, kStage>(a, C, y0, nk, ctab, nullptr, stage, kNoneNode, lane, round + r0 + k,
+                                                 c);
+    }
+    ctr_fold(c);
+    y0 += kChainKids;
   }
 }
 
@@ -1131,29 +1158,41 @@ hipError_t launch_chain_parents(ChainChunk* chunks, uint32_t n, const uint32_t* 
   return hipGetLastError();
 }
 
-hipError_t launch_chain_ranges(ChainChunk* chunks, uint32_t n, const uint32_t* row_ptr, uint32_t* overflow,
-                               hipStream_t s) {
+hipError_t launch_chain_ranges(ChainChunk* chunks, uint32_t n, const uint32_t* row_ptr, uint32_t cap,
+                               uint32_t* overflow, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_chain_ranges, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, chunks, n, row_ptr, overflow);
+  hipLaunchKernelGGL(k_chain_ranges, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, chunks, n, row_ptr, cap,
+                     overflow);
   return hipGetLastError();
 }
 
-hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32_t n_chunks, uint32_t round,
-                             bool record, bool nt, bool slices, hipStream_t s) {
-  if (n_chunks == 0) return hipSuccess;
+namespace {
+template <bool kCompact>
+void launch_chain_t(const PullArgs& a, const ChainChunk* chunks, uint32_t n_chunks, uint32_t round, bool record,
+                    bool nt, bool slices, hipStream_t s) {
   const dim3 g(n_chunks), b(64);
   if (slices) {
     if (record)
-      hipLaunchKernelGGL((k_pull_chain<true, false, true>), g, b, 0, s, a, chunks, n_chunks, round);
+      hipLaunchKernelGGL((k_pull_chain<true, false, true, kCompact>), g, b, 0, s, a, chunks, n_chunks, round);
     else
-      hipLaunchKernelGGL((k_pull_chain<false, true, true>), g, b, 0, s, a, chunks, n_chunks, round);
+      hipLaunchKernelGGL((k_pull_chain<false, true, true, kCompact>), g, b, 0, s, a, chunks, n_chunks, round);
   } else if (record) {
-    hipLaunchKernelGGL((k_pull_chain<true, false, false>), g, b, 0, s, a, chunks, n_chunks, round);
+    hipLaunchKernelGGL((k_pull_chain<true, false, false, kCompact>), g, b, 0, s, a, chunks, n_chunks, round);
   } else if (nt) {
-    hipLaunchKernelGGL((k_pull_chain<false, true, false>), g, b, 0, s, a, chunks, n_chunks, round);
+    hipLaunchKernelGGL((k_pull_chain<false, true, false, kCompact>), g, b, 0, s, a, chunks, n_chunks, round);
   } else {
-    hipLaunchKernelGGL((k_pull_chain<false, false, false>), g, b, 0, s, a, chunks, n_chunks, round);
+    hipLaunchKernelGGL((k_pull_chain<false, false, false, kCompact>), g, b, 0, s, a, chunks, n_chunks, round);
   }
+}
+}  // namespace
+
+hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32_t n_chunks, uint32_t round,
+                             bool record, bool nt, bool slices, bool compact, hipStream_t s) {
+  if (n_chunks == 0) return hipSuccess;
+  if (compact)
+    launch_chain_t<true>(a, chunks, n_chunks, round, record, nt, slices, s);
+  else
+    launch_chain_t<false>(a, chunks, n_chunks, round, record, nt, slices, s);
   return hipGetLastError();
 }
 

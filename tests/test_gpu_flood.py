@@ -61,7 +61,7 @@ def run_mode(monkeypatch, flood, n, topics, live, msg_topics, record=True, start
                 k = list(st.round_kernel)
                 assert st.expand_launches == 1 + sum(
                     1 for q in range(st.flood_rounds + 1, st.rounds + 1)
-                    if (k[q] == PE.K_PULL and st.expand_bytes_per_round[q]) or k[q] == PE.K_PAIR)
+                    if (k[q] == PE.K_PULL and st.expand_bytes_per_round[q]) or k[q] in (PE.K_PAIR, PE.K_CHAIN))
         hops = [eng.hops(first + m) for m in range(len(msg_topics))] if record else None
         digest = eng.seen_digest()
     return st, hops, digest

@@ -303,7 +303,7 @@ def build(world, partition, n=1500, n_topics=2, seed=0, fan=None):
 @pytest.mark.parametrize("world,partition", [(1, PE.PART_PEER), (2, PE.PART_PEER), (3, PE.PART_PEER),
                                              (4, PE.PART_SUBTREE), (4, PE.PART_PEER)])
 def test_plans_replay_to_the_oracle(monkeypatch, world, partition, staggered, chain):
-    """PSAMD_CHAIN (read at engine creation): 2 = round pairs (the default),
+    """PSAMD_CHAIN (read at engine creation): 2 = round pairs,
     4 = chains of up to four rounds where nothing is exchanged inside (and
     no k_flood launch for the leading rounds, so the chains start at round 1)."""
     monkeypatch.setenv("PSAMD_CHAIN", str(chain))
@@ -456,3 +456,34 @@ def test_gloo_world2_replays_the_plans(staggered):
         _, oh, _ = O.disseminate(rp, cl, root, live, 1)
         exp |= {(t, int(x)) for x in np.nonzero(oh[0] != 0xFF)[0]}
     assert got == exp
+
+
+@pytest.mark.parametrize("chain", [2, 4])
+def test_wide_rows_plan(monkeypatch, chain):
+    """Rows wider than the 768-word LDS stage (52,000 messages of one topic in
+    a window: 814 words): they cannot pair, so with pairs only (PSAMD_CHAIN=2)
+    those rounds get one k_pull launch each; chains cut the rows into column
+    slices of the stage width, in the launch's slice segment, and the replay
+    still tiles every row exactly (VERDICT r2 weak #8)."""
+    monkeypatch.setenv("PSAMD_CHAIN", str(chain))
+    monkeypatch.setenv("PSAMD_FLOOD", "0")
+    rng, trees, roots, live = build(1, PE.PART_PEER, n=1200, n_topics=1, seed=5, fan=3)
+    topics = np.zeros(52000, dtype=np.uint32)
+    p = PL.Plan(np.stack(trees), roots)
+    p.window(topics)
+    assert p.layout(0)["W"] == 814
+    kinds = [int(k) for k in p.get(PL.ROUND_KIND)]
+    rounds = p.info()["rounds"]
+    if chain == 2:
+        assert PE.K_PAIR not in kinds and PE.K_CHAIN not in kinds
+        assert all(k in (PE.K_PULL, 0) for k in kinds[1:rounds + 1])
+    else:
+        assert PE.K_CHAIN in kinds
+        for q in range(1, rounds + 1):
+            n, ch = p.chain(q)
+            for c in ch:
+                assert (c["w0"], c["S"]) in ((0, 768), (768, 46)), c
+                assert c["node_end"] - c["node_begin"] == 1
+    sims = [RankSim(p, live)]
+    emulate(sims, rounds, in_process_exchange(sims))
+    check(sims, trees, roots, live, [1])
