@@ -429,7 +429,7 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   auto& pairs = e->pairs_host;
   pairs.clear();
   e->pair_off.assign(nt + 1, 0);
-  std::vector<uint32_t> cand;
+  std::vector<uint32_t> cand, codes;
   for (uint32_t t = 0; t < nt; ++t) {
     TopicHost& T = e->topics[t];
     e->pair_off[t] = pairs.size() / 2;
@@ -440,7 +440,7 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
     if (!T.par_dev_valid) {
       HIP_TRY(hipMemsetAsync(par_t, 0xFF, static_cast<size_t>(n) * 4, s), "clear parents");
       HIP_TRY(hipMemsetAsync(orph_t, 0, n, s), "clear orphan bytes");
-      T.par_mirror.assign(n, kNone);
+      if (T.kind != Kind::Join) T.par_mirror.assign(n, kNone);  // (joined trees ship their touched codes)
       T.par_dev_valid = true;
       full = true;
     }
@@ -452,17 +452,24 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
       }
     };
     if (T.kind == Kind::Join) {
-      T.tree.take_touched(cand);
-      if (full)
-        for (uint32_t p = 0; p < n; ++p) diff(p, T.tree.upstream_code(p));
-      else
-        for (size_t i = 0; i < cand.size(); ++i) {
-          if (i + 16 < cand.size()) {  // touched peers are scattered: fetch ahead
-            T.tree.prefetch_peer(cand[i + 16]);
-            __builtin_prefetch(&T.par_mirror[cand[i + 16]]);
+      // the tree recorded each touched peer's upstream code when it changed:
+      // ship them as they are (a peer touched without a net change costs one
+      // idempotent pair, not a visit of its scattered line here)
+      T.tree.take_touched(cand, codes);
+      if (full) {
+        for (uint32_t p = 0; p < n; ++p) {
+          const uint32_t v = T.tree.upstream_code(p);
+          if (v != kNone) {
+            pairs.push_back(p);
+            pairs.push_back(v);
           }
-          diff(cand[i], T.tree.upstream_code(cand[i]));
         }
+      } else {
+        for (size_t i = 0; i < cand.size(); ++i) {
+          pairs.push_back(cand[i]);
+          pairs.push_back(codes[i]);
+        }
+      }
     } else if (T.par_full_dirty || full) {
       for (uint32_t p = 0; p < n; ++p) diff(p, p == T.root ? kNone : T.parent[p]);
       T.par_full_dirty = false;

@@ -11,7 +11,7 @@ namespace psamd {
 SubscriptionTree::SubscriptionTree(uint32_t n_peers, uint32_t root, uint32_t width,
                                    uint32_t max_width, uint64_t seed)
     : n_(n_peers), root_(root), width_(width), max_width_(max_width), rng_(seed),
-      touched_mark_(n_peers, 0), rec_(n_peers) {
+      touched_at_(n_peers, 0), rec_(n_peers) {
   rec_[root].state = PeerState::In;
 }
 
@@ -49,17 +49,31 @@ void SubscriptionTree::kid_clear(uint32_t p) {
   R.n = 0;
 }
 
+// Called after every change of p's state or upstream: records p's upstream
+// code while its line is hot (take_touched hands the codes out without
+// visiting the peers again).
 void SubscriptionTree::touch(uint32_t p) {
-  if (!touched_mark_[p]) {
-    touched_mark_[p] = 1;
-    touched_.push_back(p);
+  const uint32_t code = upstream_code(p);
+  if (touched_at_[p]) {
+    touched_code_[touched_at_[p] - 1] = code;
+    return;
   }
+  touched_.push_back(p);
+  touched_code_.push_back(code);
+  touched_at_[p] = static_cast<uint32_t>(touched_.size());
 }
 
 void SubscriptionTree::take_touched(std::vector<uint32_t>& out) {
-  out.swap(touched_);
+  std::vector<uint32_t> codes;
+  take_touched(out, codes);
+}
+
+void SubscriptionTree::take_touched(std::vector<uint32_t>& peers, std::vector<uint32_t>& codes) {
+  peers.swap(touched_);
+  codes.swap(touched_code_);
   touched_.clear();
-  for (uint32_t p : out) touched_mark_[p] = 0;
+  touched_code_.clear();
+  for (uint32_t p : peers) touched_at_[p] = 0;
 }
 
 bool SubscriptionTree::reachable_memo(uint32_t p) {
@@ -254,6 +268,7 @@ void SubscriptionTree::depart(uint32_t at, uint32_t gone, uint32_t rescue) {
   if (attach(at, rescue, true) != PS_OK) {
     rec_[rescue].state = PeerState::Orphan;
     rec_[rescue].up = gone;
+    touch(rescue);
   }
 }
 

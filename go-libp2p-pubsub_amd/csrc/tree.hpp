@@ -66,7 +66,8 @@ class SubscriptionTree {
   void attached_parents(std::vector<uint32_t>& parent) const;
   // Upstream of every subscribed (In) peer, kNone elsewhere; reachability from
   // the root is left to the consumer (the GPU rebuild).  take_touched() hands
-  // out the peers whose entry may have changed since the last call.
+  // out the peers whose entry may have changed since the last call (and their
+  // upstream codes, recorded when they changed).
   uint32_t in_parent(uint32_t p) const {
     return rec_[p].state == PeerState::In && p != root_ ? rec_[p].up : kNone;
   }
@@ -77,6 +78,7 @@ class SubscriptionTree {
     return rec_[p].state == PeerState::Orphan ? kOrphanUp : in_parent(p);
   }
   void take_touched(std::vector<uint32_t>& out);
+  void take_touched(std::vector<uint32_t>& peers, std::vector<uint32_t>& codes);
   // Peers reachable for the NEXT message (failed hosts cut their subtree).
   // Children lists in insertion order.
   ChildSpan children(uint32_t p) const {
@@ -127,8 +129,9 @@ class SubscriptionTree {
   bool pending_failures_ = false;
   bool needs_pass_ = false;
   std::vector<uint32_t> parted_at_;  // parents holding a Part'ed child entry
-  std::vector<uint32_t> touched_;    // peers whose attachment may have changed
-  std::vector<uint8_t> touched_mark_;
+  std::vector<uint32_t> touched_;       // peers whose attachment may have changed
+  std::vector<uint32_t> touched_code_;  // ... and their upstream_code() after the last change
+  std::vector<uint32_t> touched_at_;    // per peer: its index in touched_ + 1 (0: not listed)
   std::vector<uint8_t> dedup_mark_;  // after_message: distinct Part'ed parents
   std::vector<uint32_t> reach_stamp_;  // 2*pass: reachable, 2*pass+1: not (reachable_memo)
   std::vector<uint32_t> orphan_stamp_;  // 2*pass: not cut, 2*pass+1: cut (below_orphan)
