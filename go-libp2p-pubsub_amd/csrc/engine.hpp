@@ -260,7 +260,6 @@ struct ps_engine {
   uint32_t chain_max = 4;
   psamd::DevBuf d_chain;
   uint32_t chain_words = 8192;    // row words per chain wave, the planner's target (PSAMD_CHAIN_WORDS)
-  bool chain_compact = false;     // PSAMD_CHAIN_COMPACT=1: 736-word stage, 512-node level tables (more waves)
   std::vector<uint64_t> chain_fail_key;  // a pair plan whose chain ranges overflowed the level tables: no chains
   psamd::DevBuf d_chain_ovf;
   // rows of rounds writing at least this much store non-temporally (the MALL

@@ -226,16 +226,14 @@ constexpr uint32_t kPairKids = 256;
 // row is its parent's row as round q + k - 1 wrote it, and that row is a
 // stage row: a node's entry in the level table is the stage slot of the row
 // its parent holds (kChainNone: unreached), so no level below the run reads
-// a row from HBM.  Level ranges are at most chain_cap() nodes (the host sizes
+// a row from HBM.  Level ranges are at most kChainCap nodes (the host sizes
 // the runs; k_chain_ranges fills and checks the ranges on the device).
 constexpr uint32_t kChainLevels = 6;
 static_assert(sizeof(PullArgs::partials_r) / sizeof(uint64_t*) == kChainLevels, "a slot row per chain level");
 constexpr uint32_t kChainKids = 256;   // nodes resolved per sub-run of a level
 constexpr uint32_t kChainPar = 128;    // nodes of a run at most (stage slots < kChainZero)
-// LDS stage words per wave (the run's rows, slices) and nodes of one level of
-// a chunk at most (the LDS level tables): 768 / 1,024, or compact 736 / 512
-__host__ __device__ constexpr uint32_t chain_stage_words(bool compact) { return compact ? 736u : 768u; }
-__host__ __device__ constexpr uint32_t chain_cap(bool compact) { return compact ? 512u : 1024u; }
+constexpr uint32_t kChainWords = 768;  // LDS stage words per wave: the run's rows (slices)
+constexpr uint32_t kChainCap = 1024;   // nodes of one level of a chunk at most (the LDS level tables)
 constexpr uint8_t kChainNone = 0xFF;   // level table: unreached
 constexpr uint8_t kChainZero = 0xFE;   // level table: reached with a zero row (PS_F_NO_LAZY_SEEN only)
 struct ChainChunk {
@@ -258,10 +256,9 @@ struct ChainChunk {
 // level range exceeds cap (the plan is then not used)
 hipError_t launch_chain_ranges(ChainChunk* chunks, uint32_t n, const uint32_t* row_ptr, uint32_t cap,
                                uint32_t* overflow, hipStream_t s);
-// slices: chunks of rows wider than the stage (column slices; their own
-// launch); compact: the 736-word stage / 512-node tables (chain_stage_words)
+// slices: chunks of rows wider than the stage (column slices; their own launch)
 hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32_t n_chunks, uint32_t round,
-                             bool record, bool nt, bool slices, bool compact, hipStream_t s);
+                             bool record, bool nt, bool slices, hipStream_t s);
 // ChainChunk::p_lo / p_hi from the device node_parent (GPU-built graphs)
 hipError_t launch_chain_parents(ChainChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s);
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch

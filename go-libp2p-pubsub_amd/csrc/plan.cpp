@@ -237,7 +237,6 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   key.push_back(e->pair_on ? 1 : 0);
   key.push_back(e->chain_max);
   key.push_back(e->chain_words);
-  key.push_back(e->chain_compact ? 1 : 0);
   for (size_t q = 0; q < xchg.size(); ++q) key.push_back(xchg[q].any);
   PairPlan& PP = e->pair;
   if (key == PP.key) return false;
@@ -281,7 +280,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   struct ChainSize {
     uint32_t R = 0, S = 0;  // R = 0: no chain of this length
   };
-  const uint32_t stage_w = chain_stage_words(e->chain_compact), cap = chain_cap(e->chain_compact);
+  constexpr uint32_t stage_w = kChainWords, cap = kChainCap;
   auto chain_size = [&](const TopicHost& T, uint32_t d, uint32_t levels, uint32_t W) {
     ChainSize z;
     const double n0 = static_cast<double>(T.level_off[d + 1] - T.level_off[d]);

@@ -964,13 +964,14 @@ __global__ __launch_bounds__(kBlock) void k_chain_ranges(ChainChunk* __restrict_
 }
 
 // kSlices: the launch's chunks of rows wider than the stage (column slices,
-// a separate launch: the whole-row path keeps its registers).  kCompact: the
-// 736-word stage and 512-node level tables (8 KB of LDS: 20 resident waves
-// per CU) instead of 768 words and 1,024 nodes (9.4 KB: 17).
-template <bool kRecord, bool kNT, bool kSlices, bool kCompact>
+// a separate launch: the whole-row path keeps its registers).  LDS 9.4 KB per
+// one-wave workgroup: 17 resident waves per CU.  (A 736-word stage with
+// 512-node tables, 8 KB and 20 waves, measured no faster: cfg3 1.029 vs 1.021
+// ms/step, profiles/r03/ab_chain_v2.txt.)
+template <bool kRecord, bool kNT, bool kSlices>
 __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk* __restrict__ chunks,
                                                    uint32_t n_chunks, uint32_t round) {
-  constexpr uint32_t kStage = chain_stage_words(kCompact), kCap = chain_cap(kCompact);
+  constexpr uint32_t kStage = kChainWords, kCap = kChainCap;
   __shared__ uint64_t stage[kStage + 2];  // the run's rows (slices); + the zero pair
   __shared__ uint64_t src[kChainPar];     // level 0: the parents' row addresses; then ctab
   static_assert(kChainKids * 4 <= kChainPar * 8, "ctab fits the source table");
@@ -1166,33 +1167,22 @@ hipError_t launch_chain_ranges(ChainChunk* chunks, uint32_t n, const uint32_t* r
   return hipGetLastError();
 }
 
-namespace {
-template <bool kCompact>
-void launch_chain_t(const PullArgs& a, const ChainChunk* chunks, uint32_t n_chunks, uint32_t round, bool record,
-                    bool nt, bool slices, hipStream_t s) {
+hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32_t n_chunks, uint32_t round,
+                             bool record, bool nt, bool slices, hipStream_t s) {
+  if (n_chunks == 0) return hipSuccess;
   const dim3 g(n_chunks), b(64);
   if (slices) {
     if (record)
-      hipLaunchKernelGGL((k_pull_chain<true, false, true, kCompact>), g, b, 0, s, a, chunks, n_chunks, round);
+      hipLaunchKernelGGL((k_pull_chain<true, false, true>), g, b, 0, s, a, chunks, n_chunks, round);
     else
-      hipLaunchKernelGGL((k_pull_chain<false, true, true, kCompact>), g, b, 0, s, a, chunks, n_chunks, round);
+      hipLaunchKernelGGL((k_pull_chain<false, true, true>), g, b, 0, s, a, chunks, n_chunks, round);
   } else if (record) {
-    hipLaunchKernelGGL((k_pull_chain<true, false, false, kCompact>), g, b, 0, s, a, chunks, n_chunks, round);
+    hipLaunchKernelGGL((k_pull_chain<true, false, false>), g, b, 0, s, a, chunks, n_chunks, round);
   } else if (nt) {
-    hipLaunchKernelGGL((k_pull_chain<false, true, false, kCompact>), g, b, 0, s, a, chunks, n_chunks, round);
+    hipLaunchKernelGGL((k_pull_chain<false, true, false>), g, b, 0, s, a, chunks, n_chunks, round);
   } else {
-    hipLaunchKernelGGL((k_pull_chain<false, false, false, kCompact>), g, b, 0, s, a, chunks, n_chunks, round);
+    hipLaunchKernelGGL((k_pull_chain<false, false, false>), g, b, 0, s, a, chunks, n_chunks, round);
   }
-}
-}  // namespace
-
-hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32_t n_chunks, uint32_t round,
-                             bool record, bool nt, bool slices, bool compact, hipStream_t s) {
-  if (n_chunks == 0) return hipSuccess;
-  if (compact)
-    launch_chain_t<true>(a, chunks, n_chunks, round, record, nt, slices, s);
-  else
-    launch_chain_t<false>(a, chunks, n_chunks, round, record, nt, slices, s);
   return hipGetLastError();
 }
 

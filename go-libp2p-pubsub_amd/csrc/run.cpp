@@ -60,7 +60,7 @@ int upload_pair(ps_engine* e, bool* overflow) {
     HIP_TRY(e->d_chain_ovf.ensure(4), "alloc chain overflow word");
     HIP_TRY(hipMemsetAsync(e->d_chain_ovf.p, 0, 4, e->stream), "clear chain overflow word");
     HIP_TRY(launch_chain_ranges(e->d_chain.as<ChainChunk>(), static_cast<uint32_t>(K.size()),
-                                e->d_row_ptr.as<uint32_t>(), chain_cap(e->chain_compact),
+                                e->d_row_ptr.as<uint32_t>(), kChainCap,
                                 e->d_chain_ovf.as<uint32_t>(), e->stream),
             "chain ranges");
     uint32_t ovf = 0;
@@ -681,10 +681,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         HIP_TRY(time_mark(true), "event");
         ++launches;
         HIP_TRY(launch_pull_chain(pa, e->d_chain.as<ChainChunk>() + e->pair.lo[r], e->pair.gsplit[r] - e->pair.lo[r],
-                                  r, record, ntc, false, e->chain_compact, s),
+                                  r, record, ntc, false, s),
                 "pull chain");
         HIP_TRY(launch_pull_chain(pa, e->d_chain.as<ChainChunk>() + e->pair.gsplit[r],
-                                  e->pair.hi[r] - e->pair.gsplit[r], r, record, ntc, true, e->chain_compact, s),
+                                  e->pair.hi[r] - e->pair.gsplit[r], r, record, ntc, true, s),
                 "pull chain (column slices)");
         HIP_TRY(time_mark(false), "event");
         if (xr) HIP_TRY(hipStreamWaitEvent(s, e->ev_xchg, 0), "exchange join");  // (never: chains skip exchange rounds)

@@ -22,4 +22,6 @@ for W in cfg3 cfg4; do
     env $E timeout -k 10 200 $B --workload $W > $O/${W}_$V.json 2> $O/${W}_$V.err
   done
 done
+echo "[ab_chain2] cfg5 $(date +%T)"
+PSAMD_HOST_TIMING=1 timeout -k 10 300 python -u bench.py --workload cfg5 --steps 10 --warmup 3 --no-cpu > $O/cfg5.json 2> $O/cfg5.err
 echo "[ab_chain2] done $(date +%T)"
