@@ -231,7 +231,9 @@ struct ps_engine {
   uint32_t flood_grid = 0;    // resident blocks (0: k_flood unavailable)
   uint32_t flood_words = psamd::kFloodWords;  // row words per task (PSAMD_FLOOD_WORDS)
   uint32_t pull_words = psamd::kPullWords;    // row words per k_pull chunk (512..4096 measured: 1024 best)
-  uint64_t flood_top_bytes = 16ull << 20;  // k_flood runs the leading rounds writing at most this many row bytes
+  // k_flood runs the leading rounds writing at most this many row bytes (with
+  // chains after it: 4 MB; 16 MB was best before them, profiles/r03/ab_flood_top.txt)
+  uint64_t flood_top_bytes = 4ull << 20;
   uint32_t flood_epoch = 0;   // granule tag of the last launch (granules are never reset)
   uint32_t flood_spin_ticks = 200000000u;  // dependency-wait bound: 2 s of s_memrealtime (100 MHz); PSAMD_FLOOD_SPIN_TICKS
   psamd::FloodPlan flood;
