@@ -5,8 +5,8 @@ live masks, staggered or single start rounds, several topics, small windows
 (many windows per run), eager / lazy seen, pipelined runs, churn sequences
 on restated join trees, 2-4 ranks on the loopback transport, per-subscriber
 drains, and every execution mode on the same inputs (k_flood with random
-k_flood / k_pull splits and task sizes, per-round k_pull, start groups, the
-compaction path): identical deliveries, per-round counts and seen digests
+k_flood / k_pull splits and task sizes, per-round k_pull, pairs, chains of
+3-6 rounds with random run sizes, start groups, the compaction path): identical deliveries, per-round counts and seen digests
 on the production (non-recording) instance.  Every case is bit-exact or the
 script reports it (seed and case) and exits non-zero.
 
@@ -104,7 +104,8 @@ def case_topology(rng, max_peers):
     return None
 
 
-MODE_ENV = ("PSAMD_FLOOD", "PSAMD_FLOOD_TOP_BYTES", "PSAMD_FLOOD_WORDS", "PSAMD_PULL_PAIR")
+MODE_ENV = ("PSAMD_FLOOD", "PSAMD_FLOOD_TOP_BYTES", "PSAMD_FLOOD_WORDS", "PSAMD_PULL_PAIR", "PSAMD_CHAIN",
+            "PSAMD_CHAIN_WORDS")
 
 
 def set_modes(rng):
@@ -119,6 +120,10 @@ def set_modes(rng):
         os.environ["PSAMD_FLOOD_WORDS"] = str(int(rng.choice([64, 256, 4096])))
     if rng.random() < 0.3:
         os.environ["PSAMD_PULL_PAIR"] = "0"
+    if rng.random() < 0.5:  # launches of at most 2 (pairs) .. 6 rounds (chains)
+        os.environ["PSAMD_CHAIN"] = str(int(rng.integers(2, 7)))
+    if rng.random() < 0.3:  # chain runs sized for fewer / more row words per wave
+        os.environ["PSAMD_CHAIN_WORDS"] = str(int(rng.choice([256, 1024, 32768])))
 
 
 def case_modes(rng, max_peers):
@@ -144,6 +149,9 @@ def case_modes(rng, max_peers):
     window = int(rng.choice([128, 65536]))
     modes = [({}, 0), ({}, PE.F_COMPACT), ({"PSAMD_FLOOD": "0"}, 0),
              ({"PSAMD_FLOOD": "0", "PSAMD_PULL_PAIR": "0"}, 0),
+             ({"PSAMD_FLOOD": "0", "PSAMD_CHAIN": "2"}, 0),
+             ({"PSAMD_FLOOD": "0", "PSAMD_CHAIN": str(int(rng.integers(3, 7))),
+               "PSAMD_CHAIN_WORDS": str(int(rng.choice([256, 8192])))}, 0),
              ({"PSAMD_FLOOD_TOP_BYTES": str(int(rng.choice([0, 512, 1 << 30])))}, 0),
              ({"PSAMD_FLOOD_WORDS": "64"}, 0), ({}, PE.F_NO_LAZY_SEEN)]
     for env, flags in modes:

@@ -10,6 +10,10 @@ tail -n 1 $O/pytest.log
 echo "[r03c] driver command $(date +%T)"
 timeout -k 10 400 python -u bench.py > $O/bench_driver_cmd.json 2> $O/bench_driver_cmd.err
 timeout -k 10 300 python -u bench.py --workload cfg2 --steps 200 --warmup 5 --sustain 0 > $O/bench_cfg2.json 2> $O/bench_cfg2.err
+for L in 5 6; do
+  PSAMD_CHAIN=$L timeout -k 10 200 python -u bench.py --steps 200 --warmup 5 --no-cpu --no-general --sustain 0 > $O/cfg3_chain$L.json 2> $O/cfg3_chain$L.err
+done
+timeout -k 10 200 python -u bench.py --steps 200 --warmup 5 --no-cpu --no-general --sustain 0 > $O/cfg3_chain4.json 2> $O/cfg3_chain4.err
 echo "[r03c] cfg5 trace $(date +%T)"
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$GRAFT_REPO_ROOT/$O/trace_cfg5" -o run -- \
