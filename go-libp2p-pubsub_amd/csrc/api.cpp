@@ -663,7 +663,9 @@ int ps_plan_window(ps_engine* e, const uint32_t* topic_of_msg, const uint32_t* s
   bool gch = false;
   rc = plan_ghost(e, L, &gch);
   if (rc) return rc;
-  plan_pair_chunks(e, L, 0);
+  // the k_flood split a one-rank run would take (its rounds replay as pulls)
+  const uint32_t first = e->world == 1 && e->flood_on ? plan_flood_rounds(e, L) : 0;
+  plan_pair_chunks(e, L, first);
   if (e->world > 1) annotate_chunks(e, L);
   e->round_kind = e->pair.kind;
   return PS_OK;
