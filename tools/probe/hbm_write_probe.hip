@@ -88,6 +88,33 @@ __global__ __launch_bounds__(64) void k_fill_wave(u32x4* __restrict__ out, size_
   }
 }
 
+// One-shot waves writing kKB contiguous KB each (1-KB stores, 8 in flight),
+// optionally reading one unit per kMix units first (the chain kernels' mix:
+// ~1 byte read per 8 written).
+template <int kKB, int kMix, bool kNT>
+__global__ __launch_bounds__(64) void k_fill_piece(const u32x4* __restrict__ in, u32x4* __restrict__ out, size_t n,
+                                                   unsigned v) {
+  const size_t base = static_cast<size_t>(blockIdx.x) * (kKB * 64);  // units of 16 B
+  u32x4 acc = {v, v, v, v};
+  for (int b = 0; b < kKB; b += 8) {
+    u32x4 x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const size_t i = base + static_cast<size_t>(b + u) * 64 + threadIdx.x;
+      x[u] = acc;
+      if (kMix && ((b + u) % kMix) == 0 && i < n) x[u] = in[i];
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const size_t i = base + static_cast<size_t>(b + u) * 64 + threadIdx.x;
+      if (i < n) {
+        if constexpr (kNT) __builtin_nontemporal_store(x[u], out + i);
+        else out[i] = x[u];
+      }
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   const size_t bytes = (argc > 1 ? std::atoll(argv[1]) : 2048) << 20;
   const size_t n = bytes / 16;
@@ -139,6 +166,22 @@ int main(int argc, char** argv) {
     const float p1n = timeit([&] { hipLaunchKernelGGL((k_fill_wave<1, true>), dim3(grid), dim3(64), 0, 0, a, n, 5u); });
     std::printf("one-shot 8-KB waves (%u): 1-KB stores %.2f / nt %.2f TB/s; 64-B lanes %.2f / nt %.2f TB/s\n", grid,
                 bytes / p0 / 1e9, bytes / p0n / 1e9, bytes / p1 / 1e9, bytes / p1n / 1e9);
+  }
+  {
+    auto piece = [&](auto kern, int kb) {
+      const unsigned grid = static_cast<unsigned>((n + kb * 64 - 1) / (kb * 64));
+      return timeit([&] { hipLaunchKernelGGL(kern, dim3(grid), dim3(64), 0, 0, b, a, n, 9u); });
+    };
+    std::printf("one-shot waves, contiguous piece per wave, nt / default stores (TB/s of writes):\n");
+    std::printf("  8 KB   %.2f / %.2f\n", bytes / piece(k_fill_piece<8, 0, true>, 8) / 1e9,
+                bytes / piece(k_fill_piece<8, 0, false>, 8) / 1e9);
+    std::printf("  32 KB  %.2f / %.2f\n", bytes / piece(k_fill_piece<32, 0, true>, 32) / 1e9,
+                bytes / piece(k_fill_piece<32, 0, false>, 32) / 1e9);
+    std::printf("  128 KB %.2f / %.2f\n", bytes / piece(k_fill_piece<128, 0, true>, 128) / 1e9,
+                bytes / piece(k_fill_piece<128, 0, false>, 128) / 1e9);
+    const float m8 = piece(k_fill_piece<32, 8, true>, 32);
+    std::printf("  32 KB, 1 of 8 units read first (nt): %.2f TB/s written + %.2f read\n", bytes / m8 / 1e9,
+                bytes / 8 / m8 / 1e9);
   }
   const float ms = timeit([&] { CK(hipMemsetAsync(a, 3, bytes, 0)); });
   std::printf("hipMemsetAsync: %.2f TB/s\n", bytes / ms / 1e9);
