@@ -1,20 +1,11 @@
 #!/bin/bash
-# A/B of the general-path leg (staggered cfg3) under env lists, alternating.
-# usage: tools/ab_general.sh OUTDIR REPEATS "ENV1" "ENV2" ...
-set -o pipefail
-out=$1; reps=$2; shift 2
-mkdir -p "$out"
-for rep in $(seq 1 "$reps"); do
-  i=0
-  for envs in "$@"; do
-    i=$((i + 1))
-    env $envs timeout -k 10 200 python -u bench.py --general-only --steps 8 --warmup 2 --no-cpu \
-        > "$out/g${i}_$rep.json" 2> "$out/g${i}_$rep.err" || { echo "variant $i failed: $envs" >> "$out/summary.txt"; exit 1; }
-    python3 -c "
-import json
-g=json.loads(open('$out/g${i}_$rep.json').read().strip().splitlines()[-1])['general_path']
-print(f\"[$envs] ms/step {g['ms_per_step']:.3f} device ms/step {g['roofline']['device_ms_per_step']:.3f} compaction {g['compaction']['ms_per_step']:.2f}\")
-" >> "$out/summary.txt"
-  done
+# General path (start rounds 0..7) by the longest launch (PSAMD_CHAIN 2/4/6).
+set -euo pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${1:-abgen}
+mkdir -p $O
+for L in 2 4 6; do
+  echo "[ab_general] chain $L $(date +%T)"
+  PSAMD_CHAIN=$L timeout -k 10 300 python -u bench.py --general-only --steps 20 --warmup 3 --no-cpu > $O/general_chain$L.json 2> $O/general_chain$L.err
 done
-cat "$out/summary.txt"
+echo "[ab_general] done $(date +%T)"
