@@ -258,8 +258,11 @@ struct ps_engine {
   // k_pull_pair: rounds q and q + 1 in one launch
   // (PSAMD_PULL_PAIR=0: one k_pull launch per round)
   bool pair_on = true;
-  // rounds per launch at most (PSAMD_CHAIN, 1..kChainLevels): 2 = pairs
-  uint32_t chain_max = 4;
+  // rounds per launch at most (PSAMD_CHAIN, 1..kChainLevels, both kinds of
+  // window): 2 = pairs.  Defaults by measurement (profiles/r03/ab_chain_v2.txt):
+  // 4 for single-start windows (cfg3 burst 1.016 vs 1.033 ms at 6), 6 for
+  // windows with start groups (paced cfg3 1.363 vs 1.443 ms at 4)
+  uint32_t chain_max = 4, chain_max_groups = 6;
   psamd::DevBuf d_chain;
   uint32_t chain_words = 8192;    // row words per chain wave, the planner's target (PSAMD_CHAIN_WORDS)
   std::vector<uint64_t> chain_fail_key;  // a pair plan whose chain ranges overflowed the level tables: no chains

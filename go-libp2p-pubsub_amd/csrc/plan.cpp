@@ -236,6 +236,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   key.push_back(first);
   key.push_back(e->pair_on ? 1 : 0);
   key.push_back(e->chain_max);
+  key.push_back(e->chain_max_groups);
   key.push_back(e->chain_words);
   for (size_t q = 0; q < xchg.size(); ++q) key.push_back(xchg[q].any);
   PairPlan& PP = e->pair;
@@ -244,7 +245,8 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   constexpr uint32_t stage = kPairWords;
   constexpr double kLaunchBytes = 16e6;  // ~3 us of launch ramp and tail at ~5.5 TB/s (64, 200 MB: same plan on cfg3)
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
-  const uint32_t max_len = e->pair_on ? std::max<uint32_t>(1, std::min<uint32_t>(e->chain_max, kChainLevels)) : 1;
+  const uint32_t chain_max = L.multi ? e->chain_max_groups : e->chain_max;
+  const uint32_t max_len = e->pair_on ? std::max<uint32_t>(1, std::min<uint32_t>(chain_max, kChainLevels)) : 1;
   auto& kind = PP.kind;
   kind.assign(rounds + 2, PS_K_NONE);
   for (uint32_t q = 1; q <= first && q <= rounds; ++q) kind[q] = PS_K_FLOOD;
