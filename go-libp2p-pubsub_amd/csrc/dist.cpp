@@ -86,6 +86,8 @@ struct LoopbackGroup {
     hipEvent_t sent = nullptr;        // send regions complete (stream order)
     hipEvent_t read[2] = {nullptr, nullptr};  // this rank finished copying from the others:
                                               // exchange k records read[k & 1]
+    hipEvent_t used[2] = {nullptr, nullptr};  // zero copy: this rank's launches that read the
+                                              // others' regions are done (consumed call k: used[k & 1])
   };
   std::vector<Slot> slot;
 
@@ -130,12 +132,17 @@ class LoopbackTransport final : public Transport {
     (void)hipSetDevice(device_);
     (void)hipEventCreateWithFlags(&sent_, hipEventDisableTiming);
     for (auto& r : read_) (void)hipEventCreateWithFlags(&r, hipEventDisableTiming);
-    g_->slot[rank_].read[0] = read_[0];
-    g_->slot[rank_].read[1] = read_[1];
+    for (auto& r : used_) (void)hipEventCreateWithFlags(&r, hipEventDisableTiming);
+    for (int k = 0; k < 2; ++k) {
+      g_->slot[rank_].read[k] = read_[k];
+      g_->slot[rank_].used[k] = used_[k];
+    }
   }
   ~LoopbackTransport() override {
     if (sent_) (void)hipEventDestroy(sent_);
     for (auto& r : read_)
+      if (r) (void)hipEventDestroy(r);
+    for (auto& r : used_)
       if (r) (void)hipEventDestroy(r);
   }
   int rank() const override { return rank_; }
@@ -189,6 +196,48 @@ class LoopbackTransport final : public Transport {
     return hipSuccess;
   }
 
+  // Zero copy (level mode): the ranks share one process and one device, so a
+  // receiving launch reads the sender's region where it lies -- no copy
+  // launch, no receive buffer.  Two barriers as in exchange(): `sent` is
+  // re-recorded only after every rank has enqueued its waits on it.
+  bool zero_copy() const override { return true; }
+  hipError_t exchange_zc(const uint8_t* send, const std::vector<uint64_t>& send_off,
+                         std::vector<const uint8_t*>& peer, hipStream_t s, std::string* err) override {
+    hipError_t e = hipEventRecord(sent_, s);
+    if (e != hipSuccess) return fail(e, err);
+    auto& me = g_->slot[rank_];
+    me.send = send;
+    me.send_off = &send_off;
+    me.sent = sent_;
+    if (!g_->barrier()) return timeout(err);  // every rank published regions + `sent`
+    peer.assign(g_->world, nullptr);
+    for (int src = 0; src < g_->world; ++src) {
+      if (src == rank_) continue;
+      const auto& o = g_->slot[src];
+      if ((e = hipStreamWaitEvent(s, o.sent, 0)) != hipSuccess) return fail(e, err);
+      peer[src] = o.send + (*o.send_off)[rank_];
+    }
+    if (!g_->barrier()) return timeout(err);  // every rank enqueued its waits on `sent`
+    return hipSuccess;
+  }
+  // After the launches that read the others' regions: nobody's region is
+  // rewritten (the next round's records) before every reader is done.  The
+  // `used` events alternate, so one is re-recorded two calls later, after
+  // the next call's barrier, which every rank reaches once it has enqueued
+  // its waits on it.
+  hipError_t consumed(hipStream_t s, std::string* err) override {
+    const int par = uparity_;
+    uparity_ ^= 1;
+    hipError_t e = hipEventRecord(used_[par], s);
+    if (e != hipSuccess) return fail(e, err);
+    if (!g_->barrier()) return timeout(err);
+    for (int q = 0; q < g_->world; ++q) {
+      if (q == rank_) continue;
+      if ((e = hipStreamWaitEvent(s, g_->slot[q].used[par], 0)) != hipSuccess) return fail(e, err);
+    }
+    return hipSuccess;
+  }
+
  private:
   static hipError_t timeout(std::string* err) {
     if (err) *err = "loopback exchange: a rank did not arrive (group broken)";
@@ -200,8 +249,8 @@ class LoopbackTransport final : public Transport {
   }
   LoopbackGroup* g_;
   int rank_, device_;
-  hipEvent_t sent_ = nullptr, read_[2] = {nullptr, nullptr};
-  int parity_ = 0;
+  hipEvent_t sent_ = nullptr, read_[2] = {nullptr, nullptr}, used_[2] = {nullptr, nullptr};
+  int parity_ = 0, uparity_ = 0;
 };
 
 }  // namespace

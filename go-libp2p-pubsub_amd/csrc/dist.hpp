@@ -7,8 +7,9 @@
 //   RcclTransport      ncclSend / ncclRecv pairs in one group (all-to-allv over
 //                      xGMI), the production transport.
 //   LoopbackTransport  `world` engines of one process (threads) copy each
-//                      other's regions device-to-device; lets the real kernels
-//                      and routing be tested on a single GPU.
+//                      other's regions device-to-device (compaction mode) or,
+//                      in level mode, read them in place (zero-copy); lets the
+//                      real kernels and routing be tested on a single GPU.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -32,6 +33,24 @@ class Transport {
                               const std::vector<uint64_t>& recv_len, hipStream_t s,
                               std::string* err) = 0;
   virtual const char* name() const = 0;
+  // Zero-copy exchange (level mode; only transports whose ranks share one
+  // address space): publish this round's send regions and get, per source
+  // rank a, the address of a's region for this rank (peer[a]); the caller's
+  // launches read the records there, then call consumed() on the same stream
+  // once they are enqueued -- a's region may be rewritten only after every
+  // reader's consumed() point.
+  virtual bool zero_copy() const { return false; }
+  virtual hipError_t exchange_zc(const uint8_t* send, const std::vector<uint64_t>& send_off,
+                                 std::vector<const uint8_t*>& peer, hipStream_t s, std::string* err) {
+    (void)send, (void)send_off, (void)peer, (void)s;
+    if (err) *err = "zero-copy exchange not supported by this transport";
+    return hipErrorNotSupported;
+  }
+  virtual hipError_t consumed(hipStream_t s, std::string* err) {
+    (void)s;
+    if (err) *err = "zero-copy exchange not supported by this transport";
+    return hipErrorNotSupported;
+  }
 };
 
 std::unique_ptr<Transport> make_rccl_transport(int rank, int world, const uint8_t id[128],

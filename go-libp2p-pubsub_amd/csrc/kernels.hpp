@@ -198,6 +198,11 @@ struct PullArgs {
   // (PullChunk e_lo/e_hi, GhostSeg gout), stored into the send buffer
   const ShipEntry* ship;
   uint64_t* send;
+  // per source rank a: the base its records are addressed from (record k of
+  // (round, topic, group) block at rsrc[a] + GhostSeg::rbase[a] + k * rw):
+  // the receive buffer for every rank, or -- the zero-copy loopback -- rank
+  // a's own send region, offset so that the same rbase applies
+  const uint64_t* rsrc[kMaxRanks];
   uint32_t gen_cur;
   uint32_t slot_mod;   // block b adds its counters into partial slot b % slot_mod (zeroed per window)
   // k_pull_pair: round q + 1's partial slots; all_current: every generation

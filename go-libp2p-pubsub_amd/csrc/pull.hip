@@ -89,6 +89,15 @@ struct PullTopic {
   uint32_t W, nbase, root;
 };
 
+// The record base of source rank r (a per-lane value: a select chain over the
+// kernel arguments, not an indexed copy of them in scratch)
+__device__ __forceinline__ const uint64_t* rank_base(const PullArgs& a, uint32_t r) {
+  const uint64_t* b = a.rsrc[0];
+#pragma unroll
+  for (uint32_t k = 1; k < kMaxRanks; ++k) b = r == k ? a.rsrc[k] : b;
+  return b;
+}
+
 // Phase 1 for the nodes [nb, nb + nk) of one level: src[j] = the address of
 // the row node nb + j copies (its parent's row: the root's arrival row, a
 // seen row, or -- multi-GPU -- a ghost row in the receive buffer), or 0.  The
@@ -126,7 +135,8 @@ __device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic&
       const uint32_t g = a.ghost_ref[nb + j];
       if (g != kNoneNode) {
         const GhostSeg* S = a.gsegs + gin;
-        const uint64_t* rec = a.recv + S->rbase[g >> kRemoteRankShift] +
+        const uint32_t src_rank = g >> kRemoteRankShift;
+        const uint64_t* rec = rank_base(a, src_rank) + S->rbase[src_rank] +
                               static_cast<uint64_t>(g & kRemoteIdMask) * S->rw;
         up = rec[0] != 0;  // an unreached parent's record starts with a zero word
         row = reinterpret_cast<uint64_t>(rec);

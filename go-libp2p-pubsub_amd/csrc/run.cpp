@@ -633,6 +633,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     pa.ghost_ref = world > 1 ? e->d_ghost_ref.as<uint32_t>() : nullptr;
     pa.gsegs = e->d_gsegs.as<GhostSeg>();
     pa.recv = e->d_recv.as<uint64_t>();
+    for (int32_t q = 0; q < kMaxRanks; ++q) pa.rsrc[q] = pa.recv;
+    const bool zero_copy = world > 1 && e->transport->zero_copy();
+    std::vector<const uint8_t*> peer_region;
     pa.ship = world > 1 ? e->d_ship.as<ShipEntry>() : nullptr;
     pa.send = e->d_send.as<uint64_t>();
     pa.all_current = (e->cfg.flags & PS_F_NO_LAZY_SEEN) ? 1u : 0u;
@@ -660,9 +663,20 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         }
         std::string xerr;
         const uint8_t* sb = e->d_send.as<uint8_t>() + (r & 1) * e->ghost.send_half * 8;
-        const hipError_t xe = e->transport->exchange(sb, R.s_off, R.s_len, e->d_recv.as<uint8_t>(), R.r_off,
-                                                     R.r_len, xs, &xerr);
-        if (xe != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
+        if (zero_copy) {
+          // the ghost-fed nodes read each source's region in place: rsrc[a] is
+          // offset so that the receive-side record bases (rbase) apply
+          const hipError_t xe = e->transport->exchange_zc(sb, R.s_off, peer_region, xs, &xerr);
+          if (xe != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
+          for (int32_t q = 0; q < world && q < kMaxRanks; ++q)
+            if (q != me && peer_region[q])
+              pa.rsrc[q] = reinterpret_cast<const uint64_t*>(reinterpret_cast<uintptr_t>(peer_region[q]) -
+                                                             R.r_off[q]);
+        } else {
+          const hipError_t xe = e->transport->exchange(sb, R.s_off, R.s_len, e->d_recv.as<uint8_t>(), R.r_off,
+                                                       R.r_len, xs, &xerr);
+          if (xe != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
+        }
         if (xs != s) HIP_TRY(hipEventRecord(e->ev_xchg, xs), "event");
       }
       if (!lgrid[r] && !xr) {
@@ -724,6 +738,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
                   "pull");
         }
         HIP_TRY(time_mark(false), "event");
+      }
+      if (xr && zero_copy) {  // the sources' regions of this round may be rewritten once every rank is here
+        std::string xerr;
+        if (e->transport->consumed(s, &xerr) != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
       }
       if (!upfront) HIP_TRY(seed_round(r, a.a_next), "seed");
     }
