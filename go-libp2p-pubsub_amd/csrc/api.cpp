@@ -74,6 +74,8 @@ static void read_switches(ps_engine* e) {
   if (const char* v = std::getenv("PSAMD_CHAIN"))  // rounds per launch at most: 1 (k_pull only), 2 (pairs), 3, 4
     e->chain_max = e->chain_max_groups =
         static_cast<uint32_t>(std::max(1, std::min(static_cast<int>(kChainLevels), std::atoi(v))));
+  if (const char* v = std::getenv("PSAMD_PAD_WORDS")) e->pad_words = static_cast<uint32_t>(std::max(2, std::atoi(v)));
+  if (const char* v = std::getenv("PSAMD_LAUNCH_BYTES")) e->launch_bytes = std::max(0.0, std::atof(v));
   if (const char* v = std::getenv("PSAMD_CHAIN_WORDS"))  // row words a chain wave writes (planner target)
     e->chain_words = static_cast<uint32_t>(std::min(1 << 20, std::max(256, std::atoi(v))));
   if (const char* v = std::getenv("PSAMD_FLOOD_WORDS"))

@@ -264,6 +264,8 @@ struct ps_engine {
   // windows with start groups (paced cfg3 1.363 vs 1.443 ms at 4)
   uint32_t chain_max = 4, chain_max_groups = 6;
   psamd::DevBuf d_chain;
+  uint32_t pad_words = 16;        // rows of at least this many words padded to even (PSAMD_PAD_WORDS)
+  double launch_bytes = 16e6;     // planner: a launch's ramp and tail as row bytes (PSAMD_LAUNCH_BYTES)
   uint32_t chain_words = 8192;    // row words per chain wave, the planner's target (PSAMD_CHAIN_WORDS)
   std::vector<uint64_t> chain_fail_key;  // a pair plan whose chain ranges overflowed the level tables: no chains
   psamd::DevBuf d_chain_ovf;

@@ -940,7 +940,9 @@ hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_
                               uint64_t* a0, uint64_t* a1, uint8_t* gen, uint32_t gen_cur,
                               bool any_mesh, const WindowStart& ws, hipStream_t s) {
   if (n_topics == 0) return hipSuccess;
-  const dim3 grid(any_mesh ? 64 : 1, n_topics);
+  // tree topics need block x = 0 only; the other blocks share the staged
+  // copies and the partial-slot clear (>= 256 blocks in all)
+  const dim3 grid(any_mesh ? 64 : std::max<uint32_t>(1, (256 + n_topics - 1) / n_topics), n_topics);
   hipLaunchKernelGGL(k_window_init, grid, dim3(kBlock), 0, s, topics, seen, a0, a1, gen, gen_cur, ws);
   return hipGetLastError();
 }

@@ -69,9 +69,12 @@ int plan_window_layout(ps_engine* e, const std::vector<RunMsg>& msgs, const std:
     if (one_start || T.mesh) {
       d.W = ceil_div(win[t].n, 64);
       d.w_msgs = d.W;
-      // rows of >= 64 words are padded to an even length so that every row
-      // starts 16-B aligned (the kernels store them as dwordx4)
-      if (d.W >= 64) d.W += d.W & 1u;
+      // rows of >= pad_words (16) words are padded to an even length so that
+      // every row starts 16-B aligned (the kernels store them as dwordx4):
+      // <= 1/16 more bytes against half the store instructions (cfg3 1.015
+      // -> 1.003 ms/step, the 4-rank cfg4 loopback's 63-word rows 2.49x ->
+      // 2.32x; profiles/r03/ab_pad.txt)
+      if (d.W >= e->pad_words) d.W += d.W & 1u;
       L.groups[t].push_back(StartGroup{s_lo, 0, d.W});
     } else {
       // Start groups (a tree's messages entering at different rounds): the
@@ -238,12 +241,13 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   key.push_back(e->chain_max);
   key.push_back(e->chain_max_groups);
   key.push_back(e->chain_words);
+  key.push_back(static_cast<uint64_t>(e->launch_bytes));
   for (size_t q = 0; q < xchg.size(); ++q) key.push_back(xchg[q].any);
   PairPlan& PP = e->pair;
   if (key == PP.key) return false;
   PP.key = key;
   constexpr uint32_t stage = kPairWords;
-  constexpr double kLaunchBytes = 16e6;  // ~3 us of launch ramp and tail at ~5.5 TB/s (64, 200 MB: same plan on cfg3)
+  const double kLaunchBytes = e->launch_bytes;  // ~3 us of launch ramp and tail at ~5.5 TB/s
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
   const uint32_t chain_max = L.multi ? e->chain_max_groups : e->chain_max;
   const uint32_t max_len = e->pair_on ? std::max<uint32_t>(1, std::min<uint32_t>(chain_max, kChainLevels)) : 1;

@@ -297,22 +297,65 @@ __device__ __forceinline__ void pull_ship(const PullArgs& a, const PullTopic& P,
   const bool pairs = !(P.W & 1u);
   const uint32_t per = pairs ? P.W >> 1 : P.W;
   const uint32_t total = (e_hi - e_lo) * per;
-  for (uint32_t i = lane; i < total; i += 64) {
-    const uint32_t k = i / per, r = i - k * per;
-    const ShipEntry E = a.ship[e_lo + k];
-    const uint64_t row = src[E.node - nb];
-    uint64_t* rec = a.send + S->sbase[E.dst >> kRemoteRankShift] +
-                    static_cast<uint64_t>(E.dst & kRemoteIdMask) * P.W;
-    if (row == 0) {
-      if (r == 0) rec[0] = 0;
-      continue;
+  const float rp = 1.0f / static_cast<float>(per);
+  // unit i -> (entry k, unit r of its record), branch-free (float estimate
+  // off by at most one; i < 2^24), instead of an integer division per unit
+  auto split = [&](uint32_t i, uint32_t& k, uint32_t& r) {
+    int32_t kk = static_cast<int32_t>(static_cast<float>(i) * rp);
+    int32_t rr = static_cast<int32_t>(i) - kk * static_cast<int32_t>(per);
+    const int32_t lo = rr < 0, hi = rr >= static_cast<int32_t>(per);
+    kk += hi - lo;
+    rr += (lo - hi) * static_cast<int32_t>(per);
+    k = static_cast<uint32_t>(kk);
+    r = static_cast<uint32_t>(rr);
+  };
+  // kU units in flight per lane: the entry, source and row loads of all of
+  // them before their stores (one dependent chain per unit, overlapped)
+  constexpr uint32_t kU = 4;
+  for (uint32_t i0 = lane; i0 < total; i0 += 64 * kU) {
+    uint4 v[kU];
+    uint64_t* dst[kU];
+    bool live[kU], head[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      const uint32_t i = i0 + 64 * u;
+      live[u] = false;
+      head[u] = false;
+      dst[u] = nullptr;
+      v[u] = uint4{0, 0, 0, 0};
+      if (i < total) {
+        uint32_t k, r;
+        split(i, k, r);
+        const ShipEntry E = a.ship[e_lo + k];
+        const uint64_t row = src[E.node - nb];
+        const uint32_t w = pairs ? 2 * r : r;
+        dst[u] = a.send + S->sbase[E.dst >> kRemoteRankShift] + static_cast<uint64_t>(E.dst & kRemoteIdMask) * P.W + w;
+        head[u] = r == 0;
+        live[u] = row != 0;
+        if (live[u]) {
+          const uint64_t* s = reinterpret_cast<const uint64_t*>(row) + w;
+          if (pairs) {
+            v[u] = *reinterpret_cast<const uint4*>(s);
+          } else {
+            const uint64_t x = *s;
+            v[u].x = static_cast<uint32_t>(x);
+            v[u].y = static_cast<uint32_t>(x >> 32);
+          }
+        }
+      }
     }
-    const uint32_t w = pairs ? 2 * r : r;
-    const uint64_t* s = reinterpret_cast<const uint64_t*>(row) + w;
-    if (pairs)
-      *reinterpret_cast<uint4*>(rec + w) = *reinterpret_cast<const uint4*>(s);
-    else
-      rec[w] = *s;
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+      if (!dst[u]) continue;
+      if (!live[u]) {  // an unreached parent's record: a zero first word
+        if (head[u]) dst[u][0] = 0;
+        continue;
+      }
+      if (pairs)
+        *reinterpret_cast<uint4*>(dst[u]) = v[u];
+      else
+        dst[u][0] = static_cast<uint64_t>(v[u].y) << 32 | v[u].x;
+    }
   }
 }
 

@@ -2,7 +2,7 @@
 # Zero-copy loopback exchange: multi-rank parity, then the 4-rank loopback benches and a trace.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r03zc
+O=gpurun_out/${ZC_OUT:-r03zc}
 mkdir -p $O
 echo "[zc] tests $(date +%T)"
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_dist.py tests/test_gpu_fullsize.py > $O/tests.log 2>&1
