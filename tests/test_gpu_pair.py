@@ -127,8 +127,12 @@ def test_pair_after_flood(monkeypatch, seed):
     n, topics, live = make_case(rng, 20000, 40000, nt_hi=3, fan_lo=2, fan_hi=4, dead=0.03)
     msg_topics = rng.integers(0, len(topics), size=int(rng.integers(300, 3000))).astype(np.uint32)
     exp = oracle_hops(topics, live)
-    # k_flood for the rounds writing no more row bytes than round 1
-    top = sum(int((parent == root).sum()) * (-(-int((msg_topics == t).sum()) // 64)) * 8
+    # k_flood for the rounds writing no more row bytes than round 1 (rows of
+    # 16+ words padded to an even length, plan.cpp window_layout)
+    def width(k):
+        w = -(-k // 64)
+        return w + (w & 1) if w >= 16 else w
+    top = sum(int((parent == root).sum()) * width(int((msg_topics == t).sum())) * 8
               for t, (root, parent) in enumerate(topics))
     monkeypatch.setenv("PSAMD_FLOOD_TOP_BYTES", str(top))
     monkeypatch.setenv("PSAMD_CHAIN", "2")
