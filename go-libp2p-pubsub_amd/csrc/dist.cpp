@@ -86,8 +86,8 @@ struct LoopbackGroup {
     hipEvent_t sent = nullptr;        // send regions complete (stream order)
     hipEvent_t read[2] = {nullptr, nullptr};  // this rank finished copying from the others:
                                               // exchange k records read[k & 1]
-    hipEvent_t used[2] = {nullptr, nullptr};  // zero copy: this rank's launches that read the
-                                              // others' regions are done (consumed call k: used[k & 1])
+    hipEvent_t used[kSendBufs] = {};  // zero copy: this rank's launches that read the others'
+                                      // regions of round r are done (used[r % kSendBufs])
   };
   std::vector<Slot> slot;
 
@@ -132,11 +132,9 @@ class LoopbackTransport final : public Transport {
     (void)hipSetDevice(device_);
     (void)hipEventCreateWithFlags(&sent_, hipEventDisableTiming);
     for (auto& r : read_) (void)hipEventCreateWithFlags(&r, hipEventDisableTiming);
-    for (auto& r : used_) (void)hipEventCreateWithFlags(&r, hipEventDisableTiming);
-    for (int k = 0; k < 2; ++k) {
-      g_->slot[rank_].read[k] = read_[k];
-      g_->slot[rank_].used[k] = used_[k];
-    }
+    for (auto& r : used_) (void)hipEventCreateWithFlags(&r, hipEventDisableTiming);  // (never recorded: no-op waits)
+    for (int k = 0; k < 2; ++k) g_->slot[rank_].read[k] = read_[k];
+    for (uint32_t k = 0; k < kSendBufs; ++k) g_->slot[rank_].used[k] = used_[k];
   }
   ~LoopbackTransport() override {
     if (sent_) (void)hipEventDestroy(sent_);
@@ -220,20 +218,24 @@ class LoopbackTransport final : public Transport {
     if (!g_->barrier()) return timeout(err);  // every rank enqueued its waits on `sent`
     return hipSuccess;
   }
-  // After the launches that read the others' regions: nobody's region is
-  // rewritten (the next round's records) before every reader is done.  The
-  // `used` events alternate, so one is re-recorded two calls later, after
-  // the next call's barrier, which every rank reaches once it has enqueued
-  // its waits on it.
-  hipError_t consumed(hipStream_t s, std::string* err) override {
-    const int par = uparity_;
-    uparity_ ^= 1;
-    hipError_t e = hipEventRecord(used_[par], s);
+  // After the launches that read the others' regions of round r: used[r %
+  // kSendBufs] marks them done.  The writers wait for it in reuse(r), before
+  // their launches of round r + kSendBufs - 1 rewrite those regions -- one
+  // round later than a wait here, so a round's readers and the next round's
+  // writers overlap.  An event is re-recorded kSendBufs rounds later, after
+  // that round's exchange barrier, which every rank reaches only once it has
+  // enqueued its reuse wait on it.
+  hipError_t consumed(hipStream_t s, uint32_t round, std::string* err) override {
+    hipError_t e = hipEventRecord(used_[round % kSendBufs], s);
     if (e != hipSuccess) return fail(e, err);
-    if (!g_->barrier()) return timeout(err);
+    if (!g_->barrier()) return timeout(err);  // every rank recorded its `used`
+    return hipSuccess;
+  }
+  hipError_t reuse(hipStream_t s, uint32_t round, std::string* err) override {
     for (int q = 0; q < g_->world; ++q) {
       if (q == rank_) continue;
-      if ((e = hipStreamWaitEvent(s, g_->slot[q].used[par], 0)) != hipSuccess) return fail(e, err);
+      const hipError_t e = hipStreamWaitEvent(s, g_->slot[q].used[round % kSendBufs], 0);
+      if (e != hipSuccess) return fail(e, err);
     }
     return hipSuccess;
   }
@@ -249,8 +251,8 @@ class LoopbackTransport final : public Transport {
   }
   LoopbackGroup* g_;
   int rank_, device_;
-  hipEvent_t sent_ = nullptr, read_[2] = {nullptr, nullptr}, used_[2] = {nullptr, nullptr};
-  int parity_ = 0, uparity_ = 0;
+  hipEvent_t sent_ = nullptr, read_[2] = {nullptr, nullptr}, used_[kSendBufs] = {};
+  int parity_ = 0;
 };
 
 }  // namespace

@@ -19,6 +19,13 @@
 #include <vector>
 
 namespace psamd {
+// Level mode's send buffer: one part per round, cycling (round r ships into
+// part r % kSendBufs), so that a round's readers and the writers of the
+// round after it need not wait for each other (zero copy: reuse()).
+constexpr uint32_t kSendBufs = 3;
+}  // namespace psamd
+
+namespace psamd {
 
 class Transport {
  public:
@@ -36,9 +43,10 @@ class Transport {
   // Zero-copy exchange (level mode; only transports whose ranks share one
   // address space): publish this round's send regions and get, per source
   // rank a, the address of a's region for this rank (peer[a]); the caller's
-  // launches read the records there, then call consumed() on the same stream
-  // once they are enqueued -- a's region may be rewritten only after every
-  // reader's consumed() point.
+  // launches read the records there, then call consumed(round) on the same
+  // stream once they are enqueued; before a's launches rewrite that region
+  // (kSendBufs rounds later) a calls reuse(round), which orders its stream
+  // after every reader's consumed(round) point.
   virtual bool zero_copy() const { return false; }
   virtual hipError_t exchange_zc(const uint8_t* send, const std::vector<uint64_t>& send_off,
                                  std::vector<const uint8_t*>& peer, hipStream_t s, std::string* err) {
@@ -46,8 +54,13 @@ class Transport {
     if (err) *err = "zero-copy exchange not supported by this transport";
     return hipErrorNotSupported;
   }
-  virtual hipError_t consumed(hipStream_t s, std::string* err) {
-    (void)s;
+  virtual hipError_t consumed(hipStream_t s, uint32_t round, std::string* err) {
+    (void)s, (void)round;
+    if (err) *err = "zero-copy exchange not supported by this transport";
+    return hipErrorNotSupported;
+  }
+  virtual hipError_t reuse(hipStream_t s, uint32_t round, std::string* err) {
+    (void)s, (void)round;
     if (err) *err = "zero-copy exchange not supported by this transport";
     return hipErrorNotSupported;
   }

@@ -187,7 +187,7 @@ struct GhostPlan {
   std::vector<GhostSeg> segs;     // per (round, topic, start group): record bases
   std::vector<std::vector<std::vector<uint32_t>>> seg_of;  // [round][topic][group] -> segs index (kNoneNode: none)
   std::vector<PackSeg> pack;      // roots' records (level-1 rounds)
-  uint64_t send_half = 0;         // words per half of the double-buffered send buffer
+  uint64_t send_half = 0;         // words per part of the send buffer (kSendBufs parts, by round)
   uint64_t recv_words = 0;
 };
 

@@ -723,7 +723,7 @@ int plan_ghost(ps_engine* e, const WindowLayout& L, bool* changed) {
   // written while round q's are in flight)
   for (size_t si = 0; si < G.segs.size(); ++si)
     for (int32_t b = 0; b < world; ++b)
-      if (b != me) G.segs[si].sbase[b] += (seg_round[si] & 1) * G.send_half;
+      if (b != me) G.segs[si].sbase[b] += (seg_round[si] % kSendBufs) * G.send_half;
   return PS_OK;
 }
 

@@ -103,7 +103,7 @@ int upload_ghost(ps_engine* e) {
   const GhostPlan& G = e->ghost;
   HIP_TRY(e->d_gsegs.ensure(std::max<size_t>(G.segs.size(), 1) * sizeof(GhostSeg)), "alloc ghost segments");
   HIP_TRY(e->d_pack.ensure(std::max<size_t>(G.pack.size(), 1) * sizeof(PackSeg)), "alloc pack segments");
-  HIP_TRY(e->d_send.ensure(std::max<uint64_t>(2 * G.send_half, 16) * 8), "alloc send buffer");
+  HIP_TRY(e->d_send.ensure(std::max<uint64_t>(kSendBufs * G.send_half, 16) * 8), "alloc send buffer");
   HIP_TRY(e->d_recv.ensure(std::max<uint64_t>(G.recv_words, 16) * 8), "alloc recv buffer");
   if (!G.segs.empty())
     HIP_TRY(hipMemcpyAsync(e->d_gsegs.p, G.segs.data(), G.segs.size() * sizeof(GhostSeg), hipMemcpyHostToDevice,
@@ -639,7 +639,18 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     pa.ship = world > 1 ? e->d_ship.as<ShipEntry>() : nullptr;
     pa.send = e->d_send.as<uint64_t>();
     pa.all_current = (e->cfg.flags & PS_F_NO_LAZY_SEEN) ? 1u : 0u;
+    // zero copy: the launches of round r ship into send part (r + 1) %
+    // kSendBufs, which the readers of round r + 1 - kSendBufs may still hold
+    auto reuse = [&](uint32_t q) -> int {
+      if (!zero_copy || q < 1 || q >= e->ghost.rounds.size() || !e->ghost.rounds[q].any) return PS_OK;
+      std::string xerr;
+      if (e->transport->reuse(s, q, &xerr) != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
+      return PS_OK;
+    };
+    static_assert(kSendBufs == 3, "reuse() below waits kSendBufs - 1 rounds back");
     for (r = flood_rounds + 1; r <= planned0; ++r) {
+      if (r >= 3)
+        if (const int rc = reuse(r - 2)) return rc;
       const uint8_t kind = e->round_kind[r];
       if (kind == PS_K_PAIR2 || kind == PS_K_CHAIN2) continue;  // written by the launch of an earlier round
       a.a_cur = upfront ? arr[0] : arr[(r - 1) & 1];
@@ -662,7 +673,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
           HIP_TRY(hipStreamWaitEvent(xs, e->ev_round, 0), "exchange wait");
         }
         std::string xerr;
-        const uint8_t* sb = e->d_send.as<uint8_t>() + (r & 1) * e->ghost.send_half * 8;
+        const uint8_t* sb = e->d_send.as<uint8_t>() + (r % kSendBufs) * e->ghost.send_half * 8;
         if (zero_copy) {
           // the ghost-fed nodes read each source's region in place: rsrc[a] is
           // offset so that the receive-side record bases (rbase) apply
@@ -739,12 +750,16 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         }
         HIP_TRY(time_mark(false), "event");
       }
-      if (xr && zero_copy) {  // the sources' regions of this round may be rewritten once every rank is here
+      if (xr && zero_copy) {  // the sources' regions of round r: read once the launches above end
         std::string xerr;
-        if (e->transport->consumed(s, &xerr) != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
+        if (e->transport->consumed(s, r, &xerr) != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
       }
       if (!upfront) HIP_TRY(seed_round(r, a.a_next), "seed");
     }
+    // the window's last two exchange rounds: before the next window writes
+    if (planned0 >= 2)
+      if (const int rc = reuse(planned0 - 1)) return rc;
+    if (const int rc = reuse(planned0)) return rc;
     r = planned0;
     // a deferred window's counters go straight into its pinned rows
     const bool direct = e->defer_last && e->defer_into && !record && !timed && r <= PS_MAX_ROUNDS &&

@@ -70,7 +70,7 @@ class RankSim:
         self.rows = np.zeros(wtot + 16, dtype=np.uint64)
         self.reached = np.zeros(self.info["nodes"], dtype=bool)
         self.writes = {}  # (node, group) -> times written
-        self.send = np.zeros(2 * self.info["send_half"] + 16, dtype=np.uint64)
+        self.send = np.zeros(3 * self.info["send_half"] + 16, dtype=np.uint64)  # kSendBufs parts
         self.recv = np.zeros(self.info["recv_words"] + 16, dtype=np.uint64)
         self.node_topic = np.zeros(self.info["nodes"], dtype=np.int64)
         self.level = np.zeros(self.info["nodes"], dtype=np.int64)
@@ -111,7 +111,7 @@ class RankSim:
         x = self.p.xchg(q)
         if not x["any"]:
             return {}
-        half = (q & 1) * self.info["send_half"]
+        half = (q % 3) * self.info["send_half"]
         out = {}
         for b in range(self.p.world):
             if b != self.p.rank:
