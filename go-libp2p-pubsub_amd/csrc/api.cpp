@@ -74,6 +74,7 @@ static void read_switches(ps_engine* e) {
   if (const char* v = std::getenv("PSAMD_CHAIN"))  // rounds per launch at most: 1 (k_pull only), 2 (pairs), 3, 4
     e->chain_max = e->chain_max_groups =
         static_cast<uint32_t>(std::max(1, std::min(static_cast<int>(kChainLevels), std::atoi(v))));
+  if (const char* v = std::getenv("PSAMD_OVERLAP")) e->overlap_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PAD_WORDS")) e->pad_words = static_cast<uint32_t>(std::max(2, std::atoi(v)));
   if (const char* v = std::getenv("PSAMD_LAUNCH_BYTES")) e->launch_bytes = std::max(0.0, std::atof(v));
   if (const char* v = std::getenv("PSAMD_CHAIN_WORDS"))  // row words a chain wave writes (planner target)
@@ -122,7 +123,11 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   }
   read_switches(e);
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess) {
+      hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_gate[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_gate[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_pre, hipEventDisableTiming) != hipSuccess) {
     delete e;
     return PS_E_DEVICE;
   }
@@ -162,8 +167,9 @@ void ps_destroy(ps_engine* e) {
   (void)hipSetDevice(e->cfg.device);
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->xstream) (void)hipStreamSynchronize(e->xstream);
+  if (e->pstream) (void)hipStreamSynchronize(e->pstream);
   for (auto ev : e->ev_k) (void)hipEventDestroy(ev);
-  for (hipEvent_t ev : {e->ev_run0, e->ev_run1, e->ev_round, e->ev_xchg})
+  for (hipEvent_t ev : {e->ev_run0, e->ev_run1, e->ev_round, e->ev_xchg, e->ev_gate[0], e->ev_gate[1], e->ev_pre})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& f : e->infl) {
     if (f.ev0) (void)hipEventDestroy(f.ev0);
@@ -175,6 +181,7 @@ void ps_destroy(ps_engine* e) {
   if (e->pairs_pinned) (void)hipHostFree(e->pairs_pinned);
   e->transport.reset();  // (a communicator before its streams)
   if (e->xstream) (void)hipStreamDestroy(e->xstream);
+  if (e->pstream) (void)hipStreamDestroy(e->pstream);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -490,12 +497,20 @@ int ps_read_peer_messages(ps_engine* e, uint32_t topic, uint32_t peer, uint32_t*
   return PS_OK;
 }
 
+int ps_overlapped_windows(ps_engine* e, uint64_t* count_out) {
+  if (!e || !count_out) return PS_E_INVAL;
+  *count_out = e->overlapped;
+  return PS_OK;
+}
+
 int ps_seen_digest(ps_engine* e, uint64_t* digest_out) {
   if (!e || !digest_out) return PS_E_INVAL;
   if (!e->have_window) return e->fail(PS_E_NOTREADY, "no completed run");
   HIP_TRY(hipMemsetAsync(e->d_digest.p, 0, 8, e->stream), "clear digest");
   HIP_TRY(launch_digest(e->d_seen.as<uint64_t>(), e->d_gen.as<uint8_t>(), e->gen_cur, e->d_node_peer.as<uint32_t>(),
-                        e->d_node_topic.as<uint16_t>(), e->d_topics.as<TopicDev>(), e->d_groups.as<GroupDev>(),
+                        e->d_node_topic.as<uint16_t>(),
+                        (e->last_slot ? e->d_topics1 : e->d_topics).as<TopicDev>(),
+                        (e->last_slot ? e->d_groups1 : e->d_groups).as<GroupDev>(),
                         e->n_nodes, e->d_digest.as<uint64_t>(), e->stream),
           "digest");
   HIP_TRY(hipMemcpyAsync(digest_out, e->d_digest.p, 8, hipMemcpyDeviceToHost, e->stream), "read digest");

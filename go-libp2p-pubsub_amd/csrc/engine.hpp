@@ -364,6 +364,27 @@ struct ps_engine {
   bool defer_last = false;   // ... and this window is that last window
   Inflight* defer_into = nullptr;
 
+  // Cross-window overlap.  A deep single-rank window (at
+  // least overlap_min_rounds rounds, one start round) plans no k_flood; its
+  // leading launches -- a few % of its bytes, rounds 1..P, latency bound --
+  // form the prefix.  Its gate is the launch that starts at round P + 1 (the
+  // last one reading a level <= P).  A pipelined window whose predecessor
+  // (other slot) is in flight with the same plan runs its window init and
+  // prefix on pstream once that predecessor's gate is done, beside the
+  // predecessor's remaining launches: they touch only levels > P + 1, and the
+  // per-window tables (topics, seeds, reduce descriptors, partial slots) are
+  // per slot.  PSAMD_OVERLAP=0: off.
+  bool overlap_on = true;
+  uint32_t overlap_min_rounds = 12;
+  hipStream_t pstream = nullptr;
+  hipEvent_t ev_gate[2] = {nullptr, nullptr}, ev_pre = nullptr;
+  bool gate_valid = false;
+  uint32_t gate_slot = 0;
+  std::vector<uint64_t> gate_key;  // plan versions, node-space epochs and P of the gate's window
+  uint64_t overlapped = 0;         // windows whose prefix ran beside their predecessor (stats)
+  uint32_t last_slot = 0;          // the slot of the last enqueued window's tables
+  psamd::DevBuf d_topics1, d_woff1, d_groups1, d_partials1, d_seeds1;  // slot 1's tables
+
   int fail(int code, const std::string& m) {
     err = m;
     return code;

@@ -209,8 +209,18 @@ void flood_profile_report(ps_engine* e) {
 // `msgs`) whose bits form t's block of W_t = ceil(|win[t]|/64) words.
 int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<WinSlice>& win, ps_stats* st) {
   const auto t_g0 = std::chrono::steady_clock::now();
+  const uint64_t epochs0 = e->graph_epoch ^ (e->flags_epoch << 32);
   int rc = upload_graph(e);
   if (rc) return rc;
+  // the per-window device tables of this run's slot: a pipelined window's
+  // leading launches may run beside the previous window's last ones (the
+  // other slot), see `overlap` below
+  const uint32_t slot = e->defer_into ? static_cast<uint32_t>(e->defer_into - e->infl) : 0u;
+  DevBuf& d_topics = slot ? e->d_topics1 : e->d_topics;
+  DevBuf& d_woff = slot ? e->d_woff1 : e->d_woff;
+  DevBuf& d_groups = slot ? e->d_groups1 : e->d_groups;
+  DevBuf& d_partials = slot ? e->d_partials1 : e->d_partials;
+  DevBuf& d_seeds = slot ? e->d_seeds1 : e->d_seeds;
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
   const int32_t world = e->world, me = e->rank;
   const auto t_w0 = std::chrono::steady_clock::now();
@@ -234,15 +244,15 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   if (record) HIP_TRY(e->d_hop.ensure(wtot * 64 * 2), "alloc hop record");
   const uint32_t n_waves = e->expand_grid * (kBlock / 64);
   // staged + direct kernel counters side by side
-  HIP_TRY(e->d_partials.ensure(static_cast<size_t>(2) * n_waves * kNumCtr * 8), "alloc partials");
+  HIP_TRY(d_partials.ensure(static_cast<size_t>(2) * n_waves * kNumCtr * 8), "alloc partials");
   // per-round counter rows: the planned rounds plus slack, grown (content kept)
   // if a mesh path outlives them
   uint32_t stats_rows = std::min<uint32_t>(round_cap, std::max<uint32_t>(kMaxRoundsCap, L.max_depth + max_start + 32));
   HIP_TRY(e->d_stats.ensure(static_cast<size_t>(stats_rows + 1) * kNumCtr * 8), "alloc stats");
   HIP_TRY(e->d_apply_stats.ensure(static_cast<size_t>(stats_rows + 1) * kNumCtr * 8), "alloc apply stats");
-  HIP_TRY(e->d_topics.ensure(tab.size() * sizeof(TopicDev)), "alloc topics");
+  HIP_TRY(d_topics.ensure(tab.size() * sizeof(TopicDev)), "alloc topics");
   HIP_TRY(e->d_nfront.ensure(4), "alloc n_front");
-  HIP_TRY(e->d_groups.ensure(std::max<size_t>(L.gtab.size(), 1) * sizeof(GroupDev)), "alloc groups");
+  HIP_TRY(d_groups.ensure(std::max<size_t>(L.gtab.size(), 1) * sizeof(GroupDev)), "alloc groups");
   // word offset of virtual word w of node u's row (u relative to the topic)
   auto phys = [&](uint32_t t, uint64_t u, uint32_t w) { return phys_word(tab[t], groups[t], u, w); };
 
@@ -286,7 +296,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     }
     seed_off[r + 1] = static_cast<uint32_t>(seeds.size());
   }
-  HIP_TRY(e->d_seeds.ensure(seeds.size() * sizeof(SeedDev)), "alloc seeds");
+  HIP_TRY(d_seeds.ensure(seeds.size() * sizeof(SeedDev)), "alloc seeds");
   const auto t_w2 = std::chrono::steady_clock::now();
 
   // Start rounds present per topic.  A node at BFS level d receives a
@@ -322,11 +332,16 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // k_pull launches (bandwidth bound); N ranks run k_pull_pair / k_pull with
   // the ghost exchange between rounds.  PSAMD_FLOOD=0 selects per-round
   // launches on one rank too.
-  const bool flood_ok = level && world == 1 && e->flood_on && !e->flood_broken && e->flood_grid > 0 &&
+  // deep single-start windows: per-round launches from round 1 (their first
+  // few form the prefix that may overlap the previous window)
+  const bool deep = e->overlap_on && level && world == 1 && !any_mesh && !record && !L.multi &&
+                    planned0 >= e->overlap_min_rounds;
+  const bool flood_ok = !deep && level && world == 1 && e->flood_on && !e->flood_broken && e->flood_grid > 0 &&
                         e->n_nodes < 0x80000000u;  // k_flood marks node ids with bit 31
   uint32_t flood_rounds = 0;    // rounds 1..flood_rounds: k_flood
   std::vector<uint32_t> lgrid;  // per-round launches: blocks of every round (L and G parts together)
   uint32_t n_slots = 0;         // level mode: partial counter slots of the window
+  bool fresh = false;           // level mode: no plan upload this window
   if (level) {
     bool changed = plan_pull_chunks(e, L);
     if (flood_ok) {
@@ -340,6 +355,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     changed |= plan_pair_chunks(e, L, flood_rounds);
     if (world > 1 && changed) annotate_chunks(e, L);
     bool chain_overflow = false;
+    // (nothing re-uploaded: the plan the previous window ran, a condition of the overlap)
+    fresh = e->pull.version == e->pull_up && e->pair.version == e->pair_up;
     if ((rc = upload_pull(e)) || (rc = upload_pair(e, &chain_overflow))) return rc;
     if (chain_overflow) {  // a subtree wider than the level tables: this plan runs without chains
       e->chain_fail_key = e->pair.key;
@@ -390,9 +407,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       q += len - 1;
     }
     n_slots = woff[planned0 + 1];
-    HIP_TRY(e->d_partials.ensure(static_cast<size_t>(std::max<uint32_t>(n_slots, 1)) * kNumCtr * 8),
+    fresh = fresh && !chain_overflow;
+    HIP_TRY(d_partials.ensure(static_cast<size_t>(std::max<uint32_t>(n_slots, 1)) * kNumCtr * 8),
             "alloc level partials");
-    HIP_TRY(e->d_woff.ensure(desc.size() * 4), "alloc reduce descriptors");
+    HIP_TRY(d_woff.ensure(desc.size() * 4), "alloc reduce descriptors");
   }
   // compaction mode on N ranks: cross-rank capacities (items = node words)
   // per round: cap[r][from*world+to]
@@ -427,6 +445,42 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   const uint32_t mode = flood ? PS_MODE_FLOOD : level ? PS_MODE_LEVEL_PULL : PS_MODE_COMPACT;
   const auto t_w3 = std::chrono::steady_clock::now();
   hipStream_t s = e->stream;
+  // the prefix (deep windows): leading launches of at most 1/64 of the
+  // window's row bytes, rounds 1..pre_P, followed by a launch starting at
+  // round pre_P + 1 (the gate) and at least one more
+  uint32_t pre_P = 0;
+  if (deep && flood_rounds == 0) {
+    uint64_t total = 0;
+    for (uint32_t q = 1; q <= planned0 && q < e->pull.bytes.size(); ++q) total += e->pull.bytes[q];
+    std::vector<std::pair<uint32_t, uint32_t>> ls;  // launches: (first round, last round)
+    for (uint32_t q = 1; q <= planned0; ++q) {
+      const uint8_t k = e->round_kind[q];
+      if (k != PS_K_PULL && k != PS_K_PAIR && k != PS_K_CHAIN) continue;
+      const uint32_t len = k == PS_K_PULL ? 1u : e->pair.len[q];
+      ls.emplace_back(q, q + len - 1);
+    }
+    uint64_t acc = 0;
+    for (size_t i = 0; i + 2 < ls.size(); ++i) {
+      uint64_t b = 0;
+      for (uint32_t q = ls[i].first; q <= ls[i].second && q < e->pull.bytes.size(); ++q) b += e->pull.bytes[q];
+      if (acc + b > total / 64 || ls[i + 1].first != ls[i].second + 1) break;
+      acc += b;
+      pre_P = ls[i].second;
+    }
+  }
+  std::vector<uint64_t> gkey;
+  if (pre_P)
+    gkey = {e->pull.version, e->pair.version, e->graph_epoch, e->flags_epoch, pre_P, wtot, planned0};
+  const bool overlap = pre_P && fresh && e->defer_into && e->gate_valid && e->gate_slot != slot &&
+                       e->gate_key == gkey && epochs0 == (e->graph_epoch ^ (e->flags_epoch << 32)) &&
+                       e->gen_cur + 1 <= 255 && level && !any_mesh &&
+                       !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS));
+  e->gate_valid = false;  // (this window records its own gate below)
+  if (overlap) {
+    HIP_TRY(hipStreamWaitEvent(e->pstream, e->ev_gate[e->gate_slot], 0), "wait for the previous gate");
+    s = e->pstream;
+    ++e->overlapped;
+  }
   // the window's first kernel also copies the staged uploads, applies the
   // round-0 seeds of tree roots and clears the pull partial slots (level
   // mode without meshes; the eager seen clear below would erase the seeds)
@@ -434,16 +488,16 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   WindowStart ws{};
   const void* staged[4] = {nullptr, nullptr, nullptr, nullptr};
   {
-    const Upload ups[4] = {{e->d_topics.p, tab.data(), tab.size() * sizeof(TopicDev)},
-                           {e->d_seeds.p, seeds.data(), seeds.size() * sizeof(SeedDev)},
-                           {e->d_woff.p, e->desc_host.data(), level ? e->desc_host.size() * 4 : 0},
-                           {e->d_groups.p, L.gtab.data(), L.gtab.size() * sizeof(GroupDev)}};
+    const Upload ups[4] = {{d_topics.p, tab.data(), tab.size() * sizeof(TopicDev)},
+                           {d_seeds.p, seeds.data(), seeds.size() * sizeof(SeedDev)},
+                           {d_woff.p, e->desc_host.data(), level ? e->desc_host.size() * 4 : 0},
+                           {d_groups.p, L.gtab.data(), L.gtab.size() * sizeof(GroupDev)}};
     const int rcu = stage_uploads(e, ups, 4, s, fold ? &ws.copy : nullptr, staged);
     if (rcu) return rcu;
   }
   if (fold) {
     if (seed_off[1] > 0) ws.seeds = static_cast<const SeedDev*>(staged[1]);
-    ws.zero = e->d_partials.as<uint64_t>();
+    ws.zero = d_partials.as<uint64_t>();
     ws.zero_words = static_cast<uint64_t>(n_slots) * kNumCtr;
   }
   const bool seeds0_done = ws.seeds != nullptr;
@@ -455,13 +509,13 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     HIP_TRY(hipMemsetAsync(e->d_gen.p, 0, e->d_gen.bytes, s), "clear generations");
     e->gen_cur = 1;
   }
-  HIP_TRY(launch_window_init(static_cast<const TopicDev*>(fold ? staged[0] : e->d_topics.p), nt,
+  HIP_TRY(launch_window_init(static_cast<const TopicDev*>(fold ? staged[0] : d_topics.p), nt,
                              e->d_seen.as<uint64_t>(), e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>(),
                              e->d_gen.as<uint8_t>(), e->gen_cur, any_mesh, ws, s),
           "window init");
   if (e->n_remote_fed && !level)
     HIP_TRY(launch_init_nodes(e->d_remote_fed.as<uint32_t>(), e->n_remote_fed, e->d_node_topic.as<uint16_t>(),
-                              e->d_topics.as<TopicDev>(), e->d_seen.as<uint64_t>(), e->d_arr0.as<uint64_t>(),
+                              d_topics.as<TopicDev>(), e->d_seen.as<uint64_t>(), e->d_arr0.as<uint64_t>(),
                               e->d_arr1.as<uint64_t>(), e->d_gen.as<uint8_t>(), e->gen_cur, !level, s),
             "init remote-fed rows");
   if (e->cfg.flags & PS_F_NO_LAZY_SEEN) {
@@ -483,7 +537,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   a.col = e->d_col.as<uint32_t>();
   a.node_topic = e->d_node_topic.as<uint16_t>();
   a.node_flags = e->d_node_flags.as<uint8_t>();
-  a.topics = e->d_topics.as<TopicDev>();
+  a.topics = d_topics.as<TopicDev>();
   a.seen = e->d_seen.as<uint64_t>();
   a.gen = e->d_gen.as<uint8_t>();
   a.gen_cur = e->gen_cur;
@@ -491,14 +545,14 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   a.blk_flag = e->d_blk.as<uint8_t>();
   a.hop_rec = record ? e->d_hop.as<uint16_t>() : nullptr;
   a.send = e->d_send.as<uint8_t>();
-  uint64_t* const partials = e->d_partials.as<uint64_t>();
+  uint64_t* const partials = d_partials.as<uint64_t>();
   uint64_t* arr[2] = {e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>()};
   uint64_t* stats = e->d_stats.as<uint64_t>();
   const bool timed = (e->cfg.flags & PS_F_TIME_KERNELS) != 0;
 
   auto seed_round = [&](uint32_t r, uint64_t* into) -> hipError_t {
     if (r > max_start) return hipSuccess;
-    return launch_seed(e->d_seeds.as<SeedDev>(), seed_off[r], seed_off[r + 1], into, a.seen,
+    return launch_seed(d_seeds.as<SeedDev>(), seed_off[r], seed_off[r + 1], into, a.seen,
                        level ? nullptr : a.next_flag, level ? nullptr : a.blk_flag, s);
   };
   auto compact = [&](uint32_t r, uint32_t waves_r) -> hipError_t {
@@ -588,7 +642,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     for (uint32_t q = 1; q <= planned0; ++q) pairs |= e->round_kind[q] == PS_K_PAIR || e->round_kind[q] == PS_K_CHAIN;
     const bool upfront = flood || L.multi || pairs;  // (a pair launch's plain level-1 runs read roots)
     if (upfront && max_start > 0)
-      HIP_TRY(launch_seed(e->d_seeds.as<SeedDev>(), seed_off[1], seed_off[max_start + 1], arr[0], a.seen, nullptr,
+      HIP_TRY(launch_seed(d_seeds.as<SeedDev>(), seed_off[1], seed_off[max_start + 1], arr[0], a.seen, nullptr,
                           nullptr, s),
               "seed");
     if (flood) {
@@ -648,7 +702,20 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       return PS_OK;
     };
     static_assert(kSendBufs == 3, "reuse() below waits kSendBufs - 1 rounds back");
+    bool gate_done = false;
     for (r = flood_rounds + 1; r <= planned0; ++r) {
+      if (s != e->stream && r > pre_P) {  // the prefix is enqueued: the rest follows it on the main stream
+        HIP_TRY(hipEventRecord(e->ev_pre, s), "event");
+        s = e->stream;
+        HIP_TRY(hipStreamWaitEvent(s, e->ev_pre, 0), "prefix join");
+      }
+      if (pre_P && !gate_done && r > pre_P + 1) {  // the gate launch is enqueued
+        HIP_TRY(hipEventRecord(e->ev_gate[slot], e->stream), "event");
+        e->gate_valid = true;
+        e->gate_slot = slot;
+        e->gate_key = gkey;
+        gate_done = true;
+      }
       if (r >= 3)
         if (const int rc = reuse(r - 2)) return rc;
       const uint8_t kind = e->round_kind[r];
@@ -756,6 +823,11 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       }
       if (!upfront) HIP_TRY(seed_round(r, a.a_next), "seed");
     }
+    if (s != e->stream) {  // (a prefix never ends a window; kept safe)
+      HIP_TRY(hipEventRecord(e->ev_pre, s), "event");
+      s = e->stream;
+      HIP_TRY(hipStreamWaitEvent(s, e->ev_pre, 0), "prefix join");
+    }
     // the window's last two exchange rounds: before the next window writes
     if (planned0 >= 2)
       if (const int rc = reuse(planned0 - 1)) return rc;
@@ -765,7 +837,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     const bool direct = e->defer_last && e->defer_into && !record && !timed && r <= PS_MAX_ROUNDS &&
                         (world == 1 || planned0 <= PS_MAX_ROUNDS);
     host_stats_written = direct;
-    HIP_TRY(launch_reduce_rounds(partials, e->d_woff.as<uint32_t>(), planned0, stats,
+    HIP_TRY(launch_reduce_rounds(partials, d_woff.as<uint32_t>(), planned0, stats,
                                  direct ? e->defer_into->hs_dev : nullptr, s),
             "reduce rounds");
   } else {
@@ -838,6 +910,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     e->last_pos.swap(L.pos);
     e->last_groups.swap(L.groups);
     e->have_window = true;
+    e->last_slot = slot;
   };
   if (defer) {
     // asynchronous run: the counters follow the kernels on the stream into
@@ -864,9 +937,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     if (e->host_timing) {
       auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
       std::fprintf(stderr, "[psengine] async window: plan %.3f ms (run->window %.3f, topics %.3f, seeds %.3f, "
-                   "schedule %.3f, uploads %.3f), enqueue %.3f ms\n",
+                   "schedule %.3f, uploads %.3f), enqueue %.3f ms, prefix P %u%s\n",
                    ms(e->t_run0, t_first), ms(e->t_run0, t_w0), ms(t_w0, t_w1), ms(t_w1, t_w2), ms(t_w2, t_w3),
-                   ms(t_w3, t_first), ms(t_first, t_enq));
+                   ms(t_w3, t_first), ms(t_first, t_enq), pre_P, overlap ? " (beside the previous window)" : "");
     }
     return PS_OK;
   }

@@ -123,6 +123,7 @@ PROTOTYPES = [
     ("ps_read_delivered", C.c_int, [_P, _u32, _u8p]),
     ("ps_read_peer_messages", C.c_int, [_P, _u32, _u32, _u32p, C.c_size_t, C.POINTER(C.c_size_t)]),
     ("ps_seen_digest", C.c_int, [_P, _u64p]),
+    ("ps_overlapped_windows", C.c_int, [_P, _u64p]),
     ("ps_msg_encode", C.c_int, [C.POINTER(MessageC), C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     ("ps_msg_decode", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(MessageBuf), C.POINTER(C.c_size_t)]),
     ("ps_dist_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
@@ -331,6 +332,12 @@ class Engine:
     def seen_digest(self) -> int:
         d = C.c_uint64()
         self._check(self._L.ps_seen_digest(self._h, C.byref(d)))
+        return d.value
+
+    def overlapped_windows(self) -> int:
+        """Pipelined windows whose prefix ran beside the previous window."""
+        d = C.c_uint64()
+        self._check(self._L.ps_overlapped_windows(self._h, C.byref(d)))
         return d.value
 
     # multi-GPU

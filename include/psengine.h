@@ -197,6 +197,11 @@ int ps_read_peer_messages(ps_engine* e, uint32_t topic, uint32_t peer, uint32_t*
  * multi-GPU engine sums its owned nodes (the ranks' digests add up). */
 int ps_seen_digest(ps_engine* e, uint64_t* digest_out);
 
+/* Pipelined windows (ps_run_async) whose leading launches ran beside the
+ * previous window's last launches (no reference
+ * counterpart: a scheduling diagnostic). */
+int ps_overlapped_windows(ps_engine* e, uint64_t* count_out);
+
 /* ---- multi-GPU: one engine (process) per GPU --------------------------------
  * Every rank creates the same topics and memberships and publishes the same
  * messages; each owns a hash partition of every topic's tree nodes and ps_run

@@ -110,3 +110,40 @@ def test_async_with_hop_record_and_churn():
             exp = ot.message()
             assert np.array_equal(e.hops(first), exp), step
             assert st.deliveries == 20 * int((exp != 0xFF).sum())
+
+
+@pytest.mark.parametrize("dead", [0.0, 0.03])
+def test_overlapped_windows_equal_blocking(dead):
+    """Deep windows pipelined with the same plan: each window's leading
+    launches run beside the previous window's last ones.
+    Every run's counters and the final rows equal blocking runs, and the
+    overlap did happen."""
+    wl = WL.cfg3(200_000, 16, 5000)
+    rng = np.random.default_rng(11)
+    live = (rng.random(wl.n_peers) >= dead).astype(np.uint8)
+    live[:16] = 1  # roots
+    batch = wl.msg_topics
+    out = []
+    for pipelined in (False, True):
+        e = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed)
+        WL.build_engine_topics(e, wl)
+        e.set_live(live)
+        res = []
+        if pipelined:
+            for i in range(8):
+                e.publish(batch)
+                e.run_async()
+                if i:
+                    res.append(stats_key(e.wait()))
+            res.append(stats_key(e.wait()))
+            assert e.overlapped_windows() >= 5
+        else:
+            for i in range(8):
+                e.publish(batch)
+                res.append(stats_key(e.run()))
+            assert e.overlapped_windows() == 0
+            assert res[-1][2] >= 12  # a deep window (rounds)
+        out.append((res, e.seen_digest()))
+        e.close()
+    assert out[0][0] == out[1][0]
+    assert out[0][1] == out[1][1]

@@ -41,6 +41,8 @@ def run_mode(monkeypatch, flood, n, topics, live, msg_topics, record=True, start
     rounds writing at most that many row bytes, k_pull the rest (default:
     32 MB, every round of these small trees)."""
     monkeypatch.setenv("PSAMD_FLOOD", "1" if flood else "0")
+    # (deep windows plan no k_flood while the cross-window overlap is on)
+    monkeypatch.setenv("PSAMD_OVERLAP", "0" if flood else "1")
     for var, val in (("PSAMD_FLOOD_WORDS", words), ("PSAMD_FLOOD_TOP_BYTES", top)):
         if val is None:
             monkeypatch.delenv(var, raising=False)
@@ -206,6 +208,7 @@ def test_flood_follows_live_changes(monkeypatch):
     """Kill and revive top-level peers between runs of one engine: every run
     decides reachability from its own window's generation stamps."""
     monkeypatch.setenv("PSAMD_FLOOD", "1")
+    monkeypatch.setenv("PSAMD_OVERLAP", "0")  # (deep windows plan no k_flood otherwise)
     rng = np.random.default_rng(9)
     n = 3000
     parent = random_tree(rng, n, 0, fan=3)
@@ -262,7 +265,8 @@ def test_cfg3_full_size_dead_mask_against_oracle():
         eng.set_live(live)
         first = eng.publish(wl.msg_topics)
         st = eng.run()
-        assert st.expand_mode == PE.MODE_FLOOD
+        # the default deep-window plan: chains from round 1, no k_flood
+        assert st.expand_mode == PE.MODE_LEVEL_PULL and PE.K_CHAIN in set(st.round_kernel)
         cnt = np.bincount(wl.msg_topics, minlength=len(wl.topics))
         exp_total, exp_hist, reach = 0, np.zeros(64, dtype=np.int64), {}
         for t, ts in enumerate(wl.topics):
@@ -325,6 +329,7 @@ def test_flood_timeout_reruns_window_per_round(monkeypatch):
     _, oh, _ = O.disseminate(rp, cl, 0, live, 1)
     n_msgs = 130
     monkeypatch.setenv("PSAMD_FLOOD", "1")
+    monkeypatch.setenv("PSAMD_OVERLAP", "0")  # (deep windows plan no k_flood otherwise)
     monkeypatch.setenv("PSAMD_FLOOD_TOP_BYTES", str(1 << 40))
     monkeypatch.setenv("PSAMD_FLOOD_SPIN_TICKS", "0")
     with PE.Engine(n, 1, record_hops=True) as eng:

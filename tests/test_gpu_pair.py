@@ -136,6 +136,7 @@ def test_pair_after_flood(monkeypatch, seed):
               for t, (root, parent) in enumerate(topics))
     monkeypatch.setenv("PSAMD_FLOOD_TOP_BYTES", str(top))
     monkeypatch.setenv("PSAMD_CHAIN", "2")
+    monkeypatch.setenv("PSAMD_OVERLAP", "0")  # (deep windows plan no k_flood otherwise)
     outs = []
     for pair in (False, True):
         monkeypatch.setenv("PSAMD_PULL_PAIR", "1" if pair else "0")

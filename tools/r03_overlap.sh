@@ -1,0 +1,23 @@
+#!/bin/bash
+# Cross-window overlap: async tests, full GPU suite, cfg3 bench with and without, per-launch timing.
+set -euo pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${1:-r03ovl}
+mkdir -p $O
+echo "[ovl] async tests $(date +%T)"
+timeout -k 10 300 python -u -m pytest tests/test_gpu_async.py -x -v --timeout 200 --timeout-method thread > $O/pytest_async.log 2>&1
+tail -n 1 $O/pytest_async.log
+B="python -u bench.py --steps 300 --warmup 5 --no-cpu --no-general --sustain 0"
+for rep in 1 2; do
+  for OV in 1 0; do
+    echo "[ovl] cfg3 overlap=$OV $rep $(date +%T)"
+    PSAMD_OVERLAP=$OV timeout -k 10 200 $B --workload cfg3 > $O/cfg3_ov${OV}_$rep.json 2> $O/cfg3_ov${OV}_$rep.err
+  done
+done
+for W in cfg2 cfg4; do
+  timeout -k 10 200 $B --workload $W > $O/${W}.json 2> $O/${W}.err
+done
+echo "[ovl] suite $(date +%T)"
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+tail -n 1 $O/pytest_gpu.log
+echo "[ovl] done $(date +%T)"
