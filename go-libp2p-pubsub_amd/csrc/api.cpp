@@ -75,6 +75,7 @@ static void read_switches(ps_engine* e) {
     e->chain_max = e->chain_max_groups =
         static_cast<uint32_t>(std::max(1, std::min(static_cast<int>(kChainLevels), std::atoi(v))));
   if (const char* v = std::getenv("PSAMD_OVERLAP")) e->overlap_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_OVERLAP_BYTES")) e->overlap_min_bytes = std::strtoull(v, nullptr, 10);
   if (const char* v = std::getenv("PSAMD_PAD_WORDS")) e->pad_words = static_cast<uint32_t>(std::max(2, std::atoi(v)));
   if (const char* v = std::getenv("PSAMD_LAUNCH_BYTES")) e->launch_bytes = std::max(0.0, std::atof(v));
   if (const char* v = std::getenv("PSAMD_CHAIN_WORDS"))  // row words a chain wave writes (planner target)
@@ -124,6 +125,8 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   read_switches(e);
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&e->rstream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&e->ev_end, hipEventDisableTiming) != hipSuccess ||
       hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_gate[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&e->ev_gate[1], hipEventDisableTiming) != hipSuccess ||
@@ -168,8 +171,9 @@ void ps_destroy(ps_engine* e) {
   if (e->stream) (void)hipStreamSynchronize(e->stream);
   if (e->xstream) (void)hipStreamSynchronize(e->xstream);
   if (e->pstream) (void)hipStreamSynchronize(e->pstream);
+  if (e->rstream) (void)hipStreamSynchronize(e->rstream);
   for (auto ev : e->ev_k) (void)hipEventDestroy(ev);
-  for (hipEvent_t ev : {e->ev_run0, e->ev_run1, e->ev_round, e->ev_xchg, e->ev_gate[0], e->ev_gate[1], e->ev_pre})
+  for (hipEvent_t ev : {e->ev_run0, e->ev_run1, e->ev_round, e->ev_xchg, e->ev_gate[0], e->ev_gate[1], e->ev_pre, e->ev_end})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& f : e->infl) {
     if (f.ev0) (void)hipEventDestroy(f.ev0);
@@ -182,6 +186,7 @@ void ps_destroy(ps_engine* e) {
   e->transport.reset();  // (a communicator before its streams)
   if (e->xstream) (void)hipStreamDestroy(e->xstream);
   if (e->pstream) (void)hipStreamDestroy(e->pstream);
+  if (e->rstream) (void)hipStreamDestroy(e->rstream);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }

@@ -376,8 +376,10 @@ struct ps_engine {
   // per slot.  PSAMD_OVERLAP=0: off.
   bool overlap_on = true;
   uint32_t overlap_min_rounds = 12;
+  uint64_t overlap_min_bytes = 512ull << 20;  // row bytes of the window at least (PSAMD_OVERLAP_BYTES)
   hipStream_t pstream = nullptr;
-  hipEvent_t ev_gate[2] = {nullptr, nullptr}, ev_pre = nullptr;
+  hipStream_t rstream = nullptr;  // a pipelined window's counter reduce, beside the next window
+  hipEvent_t ev_gate[2] = {nullptr, nullptr}, ev_pre = nullptr, ev_end = nullptr;
   bool gate_valid = false;
   uint32_t gate_slot = 0;
   std::vector<uint64_t> gate_key;  // plan versions, node-space epochs and P of the gate's window

@@ -825,7 +825,7 @@ __global__ __launch_bounds__(kBlock) void k_reduce_rounds(const uint64_t* __rest
   if (threadIdx.x < kNumCtr) {
     uint64_t t = 0;
     for (uint32_t k = threadIdx.x; k < kAct; k += kNumCtr) t += red[k];
-    round_stats[static_cast<uint64_t>(q) * kNumCtr + threadIdx.x] = t;
+    if (round_stats) round_stats[static_cast<uint64_t>(q) * kNumCtr + threadIdx.x] = t;
     if (host_stats) {  // fine-grained pinned host rows: visible to the host once the kernel ends
       __hip_atomic_store(host_stats + static_cast<uint64_t>(q) * kNumCtr + threadIdx.x, t, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);

@@ -356,7 +356,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     if (world > 1 && changed) annotate_chunks(e, L);
     bool chain_overflow = false;
     // (nothing re-uploaded: the plan the previous window ran, a condition of the overlap)
-    fresh = e->pull.version == e->pull_up && e->pair.version == e->pair_up;
+    fresh = e->pull.version == e->pull_up && e->pair.version == e->pair_up &&
+            (!flood_rounds || e->flood.version == e->flood_up);
     if ((rc = upload_pull(e)) || (rc = upload_pair(e, &chain_overflow))) return rc;
     if (chain_overflow) {  // a subtree wider than the level tables: this plan runs without chains
       e->chain_fail_key = e->pair.key;
@@ -449,9 +450,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // window's row bytes, rounds 1..pre_P, followed by a launch starting at
   // round pre_P + 1 (the gate) and at least one more
   uint32_t pre_P = 0;
-  if (deep && flood_rounds == 0) {
-    uint64_t total = 0;
+  uint64_t total = 0;  // the window's row bytes
+  if (level)
     for (uint32_t q = 1; q <= planned0 && q < e->pull.bytes.size(); ++q) total += e->pull.bytes[q];
+  if (deep && flood_rounds == 0) {
     std::vector<std::pair<uint32_t, uint32_t>> ls;  // launches: (first round, last round)
     for (uint32_t q = 1; q <= planned0; ++q) {
       const uint8_t k = e->round_kind[q];
@@ -468,10 +470,18 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       pre_P = ls[i].second;
     }
   }
+  // every single-rank tree window may overlap its window init (pre_P = 0:
+  // the gate is the predecessor's first launch, the last one reading the
+  // root rows the init rewrites); deep windows also their leading launches
+  // (windows of under 512 MB: the stream hand-offs cost more than the init
+  // they hide -- cfg2 0.066 -> 0.068-0.073 ms/step, cfg4 0.4536 -> 0.4502)
+  const bool pcap = e->overlap_on && level && world == 1 && !any_mesh && !record && !L.multi &&
+                    !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS)) && total >= e->overlap_min_bytes;
   std::vector<uint64_t> gkey;
-  if (pre_P)
-    gkey = {e->pull.version, e->pair.version, e->graph_epoch, e->flags_epoch, pre_P, wtot, planned0};
-  const bool overlap = pre_P && fresh && e->defer_into && e->gate_valid && e->gate_slot != slot &&
+  if (pcap)
+    gkey = {e->pull.version, e->pair.version, e->flood.version, e->graph_epoch, e->flags_epoch, pre_P,
+            flood_rounds, wtot, planned0};
+  const bool overlap = pcap && fresh && e->defer_into && e->gate_valid && e->gate_slot != slot &&
                        e->gate_key == gkey && epochs0 == (e->graph_epoch ^ (e->flags_epoch << 32)) &&
                        e->gen_cur + 1 <= 255 && level && !any_mesh &&
                        !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS));
@@ -531,6 +541,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
 
   ExpandArgs a{};
   bool host_stats_written = false;  // the reduce wrote the deferred slot's pinned rows
+  bool reduce_side = false;         // ... on e->rstream (the window's end event goes there)
   a.frontier = e->d_frontier.as<uint32_t>();
   a.n_front = e->d_nfront.as<uint32_t>();
   a.row_ptr = e->d_row_ptr.as<uint32_t>();
@@ -646,6 +657,11 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
                           nullptr, s),
               "seed");
     if (flood) {
+      if (s != e->stream) {  // (pre_P = 0) the window init is enqueued: k_flood follows it on the main stream
+        HIP_TRY(hipEventRecord(e->ev_pre, s), "event");
+        s = e->stream;
+        HIP_TRY(hipStreamWaitEvent(s, e->ev_pre, 0), "prefix join");
+      }
       FloodArgs fa{};
       fa.tasks = e->d_flood_tasks.as<FloodTask>();
       fa.segs = e->d_flood_segs.as<FloodSeg>();
@@ -709,7 +725,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         s = e->stream;
         HIP_TRY(hipStreamWaitEvent(s, e->ev_pre, 0), "prefix join");
       }
-      if (pre_P && !gate_done && r > pre_P + 1) {  // the gate launch is enqueued
+      if (pcap && !gate_done && r > pre_P + 1) {  // the gate launch is enqueued
         HIP_TRY(hipEventRecord(e->ev_gate[slot], e->stream), "event");
         e->gate_valid = true;
         e->gate_slot = slot;
@@ -837,8 +853,19 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     const bool direct = e->defer_last && e->defer_into && !record && !timed && r <= PS_MAX_ROUNDS &&
                         (world == 1 || planned0 <= PS_MAX_ROUNDS);
     host_stats_written = direct;
-    HIP_TRY(launch_reduce_rounds(partials, d_woff.as<uint32_t>(), planned0, stats,
-                                 direct ? e->defer_into->hs_dev : nullptr, s),
+    // a pipelined window's reduce runs on its own stream, beside the next
+    // window's first launches (its partial slots and descriptors are this
+    // slot's; ps_wait waits for it through the window's end event)
+    hipStream_t rs = s;
+    if (direct && pcap) {
+      HIP_TRY(hipEventRecord(e->ev_end, s), "event");
+      HIP_TRY(hipStreamWaitEvent(e->rstream, e->ev_end, 0), "reduce wait");
+      rs = e->rstream;
+    }
+    reduce_side = rs != s;
+    // (beside other windows it writes only the slot's pinned rows, not the shared device rows)
+    HIP_TRY(launch_reduce_rounds(partials, d_woff.as<uint32_t>(), planned0, reduce_side ? nullptr : stats,
+                                 direct ? e->defer_into->hs_dev : nullptr, rs),
             "reduce rounds");
   } else {
     e->round_kind.clear();  // (accumulate_window: every round k_expand)
@@ -924,7 +951,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       HIP_TRY(hipMemcpyAsync(f.ha, e->d_apply_stats.p, static_cast<size_t>(planned0 + 1) * kNumCtr * 8,
                              hipMemcpyDeviceToHost, s),
               "read apply stats");
-    HIP_TRY(hipEventRecord(e->ev_run1, s), "event");
+    HIP_TRY(hipEventRecord(e->ev_run1, reduce_side ? e->rstream : s), "event");
     f.deferred = true;
     f.planned0 = planned0;
     f.world = world;

@@ -112,16 +112,19 @@ def test_async_with_hop_record_and_churn():
             assert st.deliveries == 20 * int((exp != 0xFF).sum())
 
 
-@pytest.mark.parametrize("dead", [0.0, 0.03])
-def test_overlapped_windows_equal_blocking(dead):
+@pytest.mark.parametrize("dead,full", [(0.0, False), (0.03, False), (0.02, True)])
+def test_overlapped_windows_equal_blocking(monkeypatch, dead, full):
     """Deep windows pipelined with the same plan: each window's leading
     launches run beside the previous window's last ones.
     Every run's counters and the final rows equal blocking runs, and the
-    overlap did happen."""
-    wl = WL.cfg3(200_000, 16, 5000)
+    overlap did happen.  Small cases lower the window-size floor of the
+    overlap; the full-size cfg3 case keeps the default."""
+    if not full:
+        monkeypatch.setenv("PSAMD_OVERLAP_BYTES", "0")
+    wl = WL.cfg3() if full else WL.cfg3(200_000, 16, 5000)
     rng = np.random.default_rng(11)
     live = (rng.random(wl.n_peers) >= dead).astype(np.uint8)
-    live[:16] = 1  # roots
+    live[[ts.root for ts in wl.topics]] = 1
     batch = wl.msg_topics
     out = []
     for pipelined in (False, True):
