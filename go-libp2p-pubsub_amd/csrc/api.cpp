@@ -124,13 +124,7 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   }
   read_switches(e);
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&e->rstream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&e->ev_end, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess ||
-      hipEventCreateWithFlags(&e->ev_gate[0], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&e->ev_gate[1], hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&e->ev_pre, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess) {
     delete e;
     return PS_E_DEVICE;
   }

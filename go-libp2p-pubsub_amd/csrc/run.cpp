@@ -477,6 +477,12 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // they hide -- cfg2 0.066 -> 0.068-0.073 ms/step, cfg4 0.4536 -> 0.4502)
   const bool pcap = e->overlap_on && level && world == 1 && !any_mesh && !record && !L.multi &&
                     !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS)) && total >= e->overlap_min_bytes;
+  if (pcap && !e->pstream) {  // (created on first use: multi-rank engines never need them)
+    HIP_TRY(hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking), "prefix stream");
+    HIP_TRY(hipStreamCreateWithFlags(&e->rstream, hipStreamNonBlocking), "reduce stream");
+    for (hipEvent_t* ev : {&e->ev_gate[0], &e->ev_gate[1], &e->ev_pre, &e->ev_end})
+      HIP_TRY(hipEventCreateWithFlags(ev, hipEventDisableTiming), "overlap events");
+  }
   std::vector<uint64_t> gkey;
   if (pcap)
     gkey = {e->pull.version, e->pair.version, e->flood.version, e->graph_epoch, e->flags_epoch, pre_P,
