@@ -77,6 +77,7 @@ static void read_switches(ps_engine* e) {
   if (const char* v = std::getenv("PSAMD_OVERLAP")) e->overlap_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_OVERLAP_BYTES")) e->overlap_min_bytes = std::strtoull(v, nullptr, 10);
   if (const char* v = std::getenv("PSAMD_PAD_WORDS")) e->pad_words = static_cast<uint32_t>(std::max(2, std::atoi(v)));
+  if (const char* v = std::getenv("PSAMD_CHAIN_TAIL")) e->chain_tail = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_LAUNCH_BYTES")) e->launch_bytes = std::max(0.0, std::atof(v));
   if (const char* v = std::getenv("PSAMD_CHAIN_WORDS"))  // row words a chain wave writes (planner target)
     e->chain_words = static_cast<uint32_t>(std::min(1 << 20, std::max(256, std::atoi(v))));
@@ -681,7 +682,7 @@ int ps_plan_window(ps_engine* e, const uint32_t* topic_of_msg, const uint32_t* s
   rc = plan_ghost(e, L, &gch);
   if (rc) return rc;
   // the k_flood split a one-rank run would take (its rounds replay as pulls)
-  const uint32_t first = e->world == 1 && e->flood_on ? plan_flood_rounds(e, L) : 0;
+  const uint32_t first = e->world == 1 && e->flood_on && !deep_window(e, L) ? plan_flood_rounds(e, L) : 0;
   plan_pair_chunks(e, L, first);
   if (e->world > 1) annotate_chunks(e, L);
   e->round_kind = e->pair.kind;

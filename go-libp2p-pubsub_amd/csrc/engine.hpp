@@ -265,6 +265,7 @@ struct ps_engine {
   uint32_t chain_max = 4, chain_max_groups = 6;
   psamd::DevBuf d_chain;
   uint32_t pad_words = 16;        // rows of at least this many words padded to even (PSAMD_PAD_WORDS)
+  bool chain_tail = true;         // a chain ending at the last round may be one round longer (PSAMD_CHAIN_TAIL)
   double launch_bytes = 16e6;     // planner: a launch's ramp and tail as row bytes (PSAMD_LAUNCH_BYTES)
   uint32_t chain_words = 8192;    // row words per chain wave, the planner's target (PSAMD_CHAIN_WORDS)
   std::vector<uint64_t> chain_fail_key;  // a pair plan whose chain ranges overflowed the level tables: no chains
@@ -425,6 +426,8 @@ bool plan_flood_tasks(ps_engine* e, const WindowLayout& L, uint32_t rounds);
 int plan_ghost(ps_engine* e, const WindowLayout& L, bool* changed);
 void annotate_chunks(ps_engine* e, const WindowLayout& L);
 uint32_t plan_flood_rounds(const ps_engine* e, const WindowLayout& L);
+// A deep single-start window: chains from round 1, no k_flood.
+bool deep_window(const ps_engine* e, const WindowLayout& L);
 
 // run.cpp
 int run_body(ps_engine* e, ps_stats* st, bool may_defer);

@@ -242,6 +242,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   key.push_back(e->chain_max_groups);
   key.push_back(e->chain_words);
   key.push_back(static_cast<uint64_t>(e->launch_bytes));
+  key.push_back(e->chain_tail ? 1 : 0);
   for (size_t q = 0; q < xchg.size(); ++q) key.push_back(xchg[q].any);
   PairPlan& PP = e->pair;
   if (key == PP.key) return false;
@@ -333,10 +334,17 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
     }
   };
   const bool chains_ok = key != e->chain_fail_key;  // (ranges overflowed under this plan once)
+  // the window's last round with rows: a chain ending there may take one
+  // round more than chain_max (the last level is the leaves' partial level;
+  // it saves the tail round's own launch)
+  uint32_t last_r = 0;
+  for (uint32_t q = 1; q <= rounds && q < e->pull.bytes.size(); ++q)
+    if (e->pull.bytes[q]) last_r = q;
   auto can = [&](uint32_t q, uint32_t len) {
     if (len == 1) return true;
     if (len == 2) return static_cast<bool>(can2[q]);
-    if (!chains_ok || len > max_len || q + len - 1 > rounds || exch(q)) return false;
+    const bool tail = e->chain_tail && len == max_len + 1 && q + len - 1 == last_r && max_len >= 3;
+    if (!chains_ok || (len > max_len && !tail) || len > kChainLevels || q + len - 1 > rounds || exch(q)) return false;
     for (uint32_t k = 1; k <= len; ++k)
       if (exch(q + k)) return false;
     bool ok = true;
@@ -352,6 +360,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
     best[q] = 1e300;
     double wb = 0;
     for (uint32_t len = 1; len <= std::min<uint32_t>(kChainLevels, rounds - q + 1); ++len) {
+      if (len > max_len + 1) break;
       wb += static_cast<double>(e->pull.bytes[q + len - 1]);
       if (!can(q, len)) continue;
       const double c = wb + rd[q] + (wb > 0 ? kLaunchBytes : 0.0) + best[q + len];
@@ -479,6 +488,11 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
 // k_flood (one rank) runs the leading rounds that each write at most
 // flood_top_bytes of rows: latency bound, one launch each would cost more
 // than their bytes.
+bool deep_window(const ps_engine* e, const WindowLayout& L) {
+  return e->overlap_on && L.level && e->world == 1 && !L.any_mesh && !(e->cfg.flags & PS_F_RECORD_HOPS) &&
+         !L.multi && L.planned0 >= e->overlap_min_rounds;
+}
+
 uint32_t plan_flood_rounds(const ps_engine* e, const WindowLayout& L) {
   uint32_t r = 0;
   while (r < L.planned0 && e->pull.bytes[r + 1] <= e->flood_top_bytes) ++r;

@@ -334,8 +334,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // launches on one rank too.
   // deep single-start windows: per-round launches from round 1 (their first
   // few form the prefix that may overlap the previous window)
-  const bool deep = e->overlap_on && level && world == 1 && !any_mesh && !record && !L.multi &&
-                    planned0 >= e->overlap_min_rounds;
+  const bool deep = deep_window(e, L);
   const bool flood_ok = !deep && level && world == 1 && e->flood_on && !e->flood_broken && e->flood_grid > 0 &&
                         e->n_nodes < 0x80000000u;  // k_flood marks node ids with bit 31
   uint32_t flood_rounds = 0;    // rounds 1..flood_rounds: k_flood
