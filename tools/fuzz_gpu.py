@@ -105,7 +105,7 @@ def case_topology(rng, max_peers):
 
 
 MODE_ENV = ("PSAMD_FLOOD", "PSAMD_FLOOD_TOP_BYTES", "PSAMD_FLOOD_WORDS", "PSAMD_PULL_PAIR", "PSAMD_CHAIN",
-            "PSAMD_CHAIN_WORDS")
+            "PSAMD_CHAIN_WORDS", "PSAMD_OVERLAP_BYTES", "PSAMD_OVERLAP_ROUNDS")
 
 
 def set_modes(rng):
@@ -320,6 +320,59 @@ def case_drain(rng, max_peers):
     return None
 
 
+def case_pipeline(rng, max_peers):
+    """Pipelined runs of one batch with the cross-window overlap forced on
+    small windows (PSAMD_OVERLAP_BYTES=0, random depth floor, random launch
+    modes): every run's deliveries equal the oracle's, the last run's
+    delivered sets of sampled messages equal the oracle's reach, and the rows'
+    digest equals a blocking engine's on the same inputs."""
+    n = int(rng.integers(64, max_peers))
+    n_topics = int(rng.integers(1, 4))
+    live = (rng.random(n) > rng.choice([0.0, 0.05, 0.2])).astype(np.uint8)
+    n_msgs = int(rng.integers(1, 600))
+    topics = rng.integers(0, n_topics, size=n_msgs)
+    roots = [int(rng.integers(0, n)) for _ in range(n_topics)]
+    pars = [random_tree(rng, n, r) for r in roots]
+    runs = int(rng.integers(3, 7))
+    set_modes(rng)
+    os.environ["PSAMD_OVERLAP_BYTES"] = "0"
+    os.environ["PSAMD_OVERLAP_ROUNDS"] = str(int(rng.choice([2, 4, 8, 12])))
+    exp_total, reach = 0, []
+    for t in range(n_topics):
+        rp, cl = O.parents_to_csr(pars[t])
+        tot, hops, _ = O.disseminate(rp, cl, roots[t], live, 1)
+        exp_total += tot * int((topics == t).sum())
+        reach.append(hops[0] != 0xFF)
+    digests = []
+    for pipelined in (True, False):
+        with PE.Engine(n, n_topics) as e:
+            for t in range(n_topics):
+                e.set_tree(t, roots[t], pars[t])
+            e.set_live(live)
+            sts = []
+            for i in range(runs):
+                first = e.publish(topics)
+                if pipelined:
+                    e.run_async()
+                    if i:
+                        sts.append(e.wait())
+                else:
+                    sts.append(e.run())
+            if pipelined:
+                sts.append(e.wait())
+            for i, st in enumerate(sts):
+                if st.deliveries != exp_total:
+                    return f"pipelined={pipelined} run {i}: deliveries {st.deliveries} != oracle {exp_total}"
+            for m in rng.choice(n_msgs, size=min(n_msgs, 12), replace=False):
+                got = e.delivered(first + int(m)).astype(bool)
+                if not np.array_equal(got, reach[int(topics[m])]):
+                    return f"pipelined={pipelined} msg {m}: delivered set differs from the oracle"
+            digests.append(e.seen_digest())
+    if digests[0] != digests[1]:
+        return f"digest pipelined {digests[0]:#x} != blocking {digests[1]:#x}"
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", type=int, default=300)
@@ -327,7 +380,7 @@ def main():
     ap.add_argument("--max-peers", type=int, default=4000)
     ap.add_argument("--only", type=int, nargs="*", help="run just these case numbers (reproduce a failure)")
     ap.add_argument("--max-world", type=int, default=4, help="most loopback ranks of a dist case")
-    ap.add_argument("--kinds", nargs="*", help="only these case kinds (topology churn dist drain modes)")
+    ap.add_argument("--kinds", nargs="*", help="only these case kinds (topology churn dist drain modes pipeline)")
     args = ap.parse_args()
     global MAX_WORLD
     MAX_WORLD = args.max_world
@@ -335,11 +388,11 @@ def main():
     t0 = time.time()
     for c in (args.only if args.only else range(args.cases)):
         rng = np.random.default_rng([args.seed, c])
-        kind = ("topology", "churn", "dist", "topology", "drain", "modes")[c % 6]
+        kind = ("topology", "churn", "dist", "topology", "drain", "modes", "pipeline")[c % 7]
         if args.kinds and kind not in args.kinds:
             continue
         fn = {"topology": case_topology, "churn": case_churn, "dist": case_dist, "drain": case_drain,
-              "modes": case_modes}[kind]
+              "modes": case_modes, "pipeline": case_pipeline}[kind]
         try:
             err = fn(rng, args.max_peers)
         except PE.EngineError as ex:
