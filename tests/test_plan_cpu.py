@@ -487,3 +487,34 @@ def test_wide_rows_plan(monkeypatch, chain):
     sims = [RankSim(p, live)]
     emulate(sims, rounds, in_process_exchange(sims))
     check(sims, trees, roots, live, [1])
+
+
+@pytest.mark.parametrize("overlap", [0, 1])
+def test_deep_window_plan(monkeypatch, overlap):
+    """A deep single-start window (>= 12 rounds) plans chains from round 1 and
+    no k_flood while the cross-window overlap is on; the
+    chain that ends at the last round may take one round more than chain_max
+    (PSAMD_CHAIN_TAIL).  With the overlap off, k_flood takes the leading
+    rounds again.  Either plan replays to the oracle."""
+    monkeypatch.setenv("PSAMD_OVERLAP", str(overlap))
+    rng = np.random.default_rng(17)
+    n = 6000
+    parent = np.full(n, NONE, dtype=np.uint32)
+    parent[1:] = (np.arange(1, n) - 1) // 2  # a complete binary tree: 13 levels
+    live = (rng.random(n) > 0.05).astype(np.uint8)
+    live[0] = 1
+    p = PL.Plan(parent[None, :], [0])
+    p.window(np.zeros(3000, dtype=np.uint32))
+    kinds = [int(k) for k in p.get(PL.ROUND_KIND)]
+    rounds = p.info()["rounds"]
+    last = max(q for q in range(1, rounds + 1) if kinds[q] != 0)
+    if overlap:
+        assert PE.K_FLOOD not in kinds and kinds[1] == PE.K_CHAIN, kinds
+        starts = [q for q in range(1, rounds + 1) if kinds[q] == PE.K_CHAIN]
+        n_last, _ = p.chain(starts[-1])
+        assert starts[-1] + n_last - 1 == last and n_last == 5, (kinds, n_last)  # chain_max 4, + 1 at the tail
+    else:
+        assert kinds[1] == PE.K_FLOOD, kinds
+    sims = [RankSim(p, live)]
+    emulate(sims, rounds, in_process_exchange(sims))
+    check(sims, [parent], [0], live, [1])
