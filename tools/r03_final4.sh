@@ -5,6 +5,9 @@ set -euo pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${1:-r03i}
 mkdir -p $O
+echo "[final4] smoke $(date +%T)"
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+tail -n 2 $O/smoke.log
 echo "[final4] driver command $(date +%T)"
 timeout -k 10 400 python -u bench.py > $O/bench_driver_cmd.json 2> $O/bench_driver_cmd.err
 for W in cfg4 cfg2; do
