@@ -75,6 +75,8 @@ static void read_switches(ps_engine* e) {
     e->chain_max = e->chain_max_groups =
         static_cast<uint32_t>(std::max(1, std::min(static_cast<int>(kChainLevels), std::atoi(v))));
   if (const char* v = std::getenv("PSAMD_OVERLAP")) e->overlap_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_OVERLAP_ROUNDS"))  // tests: the depth floor of a deep window
+    e->overlap_min_rounds = static_cast<uint32_t>(std::max(2, std::atoi(v)));
   if (const char* v = std::getenv("PSAMD_OVERLAP_BYTES")) e->overlap_min_bytes = std::strtoull(v, nullptr, 10);
   if (const char* v = std::getenv("PSAMD_PAD_WORDS")) e->pad_words = static_cast<uint32_t>(std::max(2, std::atoi(v)));
   if (const char* v = std::getenv("PSAMD_CHAIN_TAIL")) e->chain_tail = std::atoi(v) != 0;
