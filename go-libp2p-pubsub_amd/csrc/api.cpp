@@ -32,6 +32,7 @@ int dist_common(ps_engine* e, const ps_dist_config* dc) {
   if (dc->world < 1 || dc->world > kMaxRanks || dc->rank < 0 || dc->rank >= dc->world)
     return e->fail(PS_E_INVAL, "rank/world out of range (world <= 16)");
   if (dc->partition != PS_PART_PEER && dc->partition != PS_PART_SUBTREE) return e->fail(PS_E_INVAL, "unknown partition");
+  if (dc->flags & ~PS_DIST_F_COPY) return e->fail(PS_E_INVAL, "unknown dist flag");
   if (!e->pending.empty()) return e->fail(PS_E_STATE, "messages pending");
   e->rank = dc->rank;
   e->world = dc->world;
@@ -54,6 +55,67 @@ int dist_streams(ps_engine* e) {
 
 }  // namespace
 
+namespace {
+
+ps_plan_opts current_opts(const ps_engine* e) {
+  ps_plan_opts o{};
+  o.flood_top_bytes = e->flood_top_bytes;
+  o.overlap_min_bytes = e->overlap_min_bytes;
+  o.launch_bytes = static_cast<uint64_t>(e->launch_bytes);
+  o.flood = e->flood_on ? 1 : 0;
+  o.chain_max = e->chain_max;
+  o.chain_max_groups = e->chain_max_groups;
+  o.chain_tail = e->chain_tail ? 1 : 0;
+  o.chain_words = e->chain_words;
+  o.flood_words = e->flood_words;
+  o.pad_words = e->pad_words;
+  o.overlap = e->overlap_on ? 1 : 0;
+  o.overlap_min_rounds = e->overlap_min_rounds;
+  o.xchg_overlap = e->xchg_overlap_env;
+  o.gpu_build = e->gpu_build_on ? 1 : 0;
+  o.flood_spin_ticks = e->flood_spin_ticks;
+  return o;
+}
+
+const char* check_opts(const ps_plan_opts& o) {
+  if (o.chain_max < 1 || o.chain_max > kChainLevels || o.chain_max_groups < 1 || o.chain_max_groups > kChainLevels)
+    return "chain_max / chain_max_groups out of 1..6";
+  if (o.chain_words < 256 || o.chain_words > (1u << 20)) return "chain_words out of 256..2^20";
+  if (o.flood_words < 64 || o.flood_words > (1u << 16)) return "flood_words out of 64..65536";
+  if (o.pad_words < 2) return "pad_words < 2";
+  if (o.overlap_min_rounds < 2) return "overlap_min_rounds < 2";
+  if (o.xchg_overlap < -1 || o.xchg_overlap > 1) return "xchg_overlap not -1, 0 or 1";
+  if (o.flood > 1 || o.chain_tail > 1 || o.overlap > 1 || o.gpu_build > 1) return "switch not 0 or 1";
+  return nullptr;
+}
+
+// the exchange stream of a multi-rank engine: forced by the options, or
+// (auto) on whenever the transport copies the records
+void refresh_xchg_overlap(ps_engine* e) {
+  if (e->transport) e->xchg_overlap = e->xchg_overlap_env < 0 ? !e->transport->zero_copy() : e->xchg_overlap_env != 0;
+}
+
+void apply_opts(ps_engine* e, const ps_plan_opts& o) {
+  e->flood_top_bytes = o.flood_top_bytes;
+  e->overlap_min_bytes = o.overlap_min_bytes;
+  e->launch_bytes = static_cast<double>(o.launch_bytes);
+  e->flood_on = o.flood != 0;
+  e->chain_max = o.chain_max;
+  e->chain_max_groups = o.chain_max_groups;
+  e->chain_tail = o.chain_tail != 0;
+  e->chain_words = o.chain_words;
+  e->flood_words = o.flood_words;
+  e->pad_words = o.pad_words;
+  e->overlap_on = o.overlap != 0;
+  e->overlap_min_rounds = o.overlap_min_rounds;
+  e->xchg_overlap_env = o.xchg_overlap;
+  e->gpu_build_on = o.gpu_build != 0;
+  e->flood_spin_ticks = o.flood_spin_ticks;
+  refresh_xchg_overlap(e);
+}
+
+}  // namespace
+
 struct ps_loopback {
   psamd::LoopbackGroup* g;
 };
@@ -62,39 +124,75 @@ extern "C" {
 
 const char* ps_version(void) { return "psengine-mi355x 0.3 (gfx950)"; }
 
-// Switches read at creation: debug timing, and the modes the parity tests
-// cover (the planner probe reads the same ones).
+// Debug switches read at creation (host phase times, per-wave profiles: they
+// change no plan).  The plan options come from ps_set_plan_opts; only A/B
+// tools that also set PSAMD_AB=1 may override them from the environment.
 static void read_switches(ps_engine* e) {
   if (const char* v = std::getenv("PSAMD_HOST_TIMING")) e->host_timing = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_GPU_BUILD")) e->gpu_build_on = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_FLOOD")) e->flood_on = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_PULL_PAIR")) e->pair_on = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD_PROFILE")) e->flood_profile = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_XCHG_OVERLAP")) e->xchg_overlap_env = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_CHAIN"))  // rounds per launch at most: 1 (k_pull only), 2 (pairs), 3, 4
-    e->chain_max = e->chain_max_groups =
+  if (const char* v = std::getenv("PSAMD_CHAIN_PROFILE")) e->chain_prof_path = v;
+  const char* ab = std::getenv("PSAMD_AB");
+  if (!ab || std::atoi(ab) == 0) return;
+  ps_plan_opts o = current_opts(e);
+  if (const char* v = std::getenv("PSAMD_GPU_BUILD")) o.gpu_build = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_FLOOD")) o.flood = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_PULL_PAIR"))  // 0: one k_pull launch per round
+    if (std::atoi(v) == 0) o.chain_max = o.chain_max_groups = 1;
+  if (const char* v = std::getenv("PSAMD_XCHG_OVERLAP")) o.xchg_overlap = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_CHAIN"))  // rounds per launch at most: 1 (k_pull only), 2 (pairs), 3..6
+    o.chain_max = o.chain_max_groups =
         static_cast<uint32_t>(std::max(1, std::min(static_cast<int>(kChainLevels), std::atoi(v))));
-  if (const char* v = std::getenv("PSAMD_OVERLAP")) e->overlap_on = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_OVERLAP_ROUNDS"))  // tests: the depth floor of a deep window
-    e->overlap_min_rounds = static_cast<uint32_t>(std::max(2, std::atoi(v)));
-  if (const char* v = std::getenv("PSAMD_OVERLAP_BYTES")) e->overlap_min_bytes = std::strtoull(v, nullptr, 10);
-  if (const char* v = std::getenv("PSAMD_PAD_WORDS")) e->pad_words = static_cast<uint32_t>(std::max(2, std::atoi(v)));
-  if (const char* v = std::getenv("PSAMD_CHAIN_TAIL")) e->chain_tail = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_LAUNCH_BYTES")) e->launch_bytes = std::max(0.0, std::atof(v));
-  if (const char* v = std::getenv("PSAMD_CHAIN_WORDS"))  // row words a chain wave writes (planner target)
-    e->chain_words = static_cast<uint32_t>(std::min(1 << 20, std::max(256, std::atoi(v))));
+  if (const char* v = std::getenv("PSAMD_OVERLAP")) o.overlap = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_OVERLAP_ROUNDS"))
+    o.overlap_min_rounds = static_cast<uint32_t>(std::max(2, std::atoi(v)));
+  if (const char* v = std::getenv("PSAMD_OVERLAP_BYTES")) o.overlap_min_bytes = std::strtoull(v, nullptr, 10);
+  if (const char* v = std::getenv("PSAMD_PAD_WORDS")) o.pad_words = static_cast<uint32_t>(std::max(2, std::atoi(v)));
+  if (const char* v = std::getenv("PSAMD_CHAIN_TAIL")) o.chain_tail = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_LAUNCH_BYTES")) o.launch_bytes = static_cast<uint64_t>(std::max(0.0, std::atof(v)));
+  if (const char* v = std::getenv("PSAMD_CHAIN_WORDS"))
+    o.chain_words = static_cast<uint32_t>(std::min(1 << 20, std::max(256, std::atoi(v))));
   if (const char* v = std::getenv("PSAMD_FLOOD_WORDS"))
-    e->flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
-  if (const char* v = std::getenv("PSAMD_FLOOD_SPIN_TICKS"))  // tests: 0 forces the timeout fallback
-    e->flood_spin_ticks = static_cast<uint32_t>(std::strtoul(v, nullptr, 0));
-  if (const char* v = std::getenv("PSAMD_FLOOD_TOP_BYTES"))  // the k_flood / k_pull split (tests: ~0 = all k_flood)
-    e->flood_top_bytes = std::strtoull(v, nullptr, 0);
+    o.flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
+  if (const char* v = std::getenv("PSAMD_FLOOD_SPIN_TICKS")) o.flood_spin_ticks = static_cast<uint32_t>(std::strtoul(v, nullptr, 0));
+  if (const char* v = std::getenv("PSAMD_FLOOD_TOP_BYTES")) o.flood_top_bytes = std::strtoull(v, nullptr, 0);
+  if (!check_opts(o)) apply_opts(e, o);
+}
+
+int ps_plan_opts_default(ps_plan_opts* out) {
+  if (!out) return PS_E_INVAL;
+  const ps_engine fresh;  // (the member initialisers are the defaults)
+  *out = current_opts(&fresh);
+  return PS_OK;
+}
+
+int ps_get_plan_opts(const ps_engine* e, ps_plan_opts* out) {
+  if (!e || !out) return PS_E_INVAL;
+  *out = current_opts(e);
+  return PS_OK;
+}
+
+int ps_set_plan_opts(ps_engine* e, const ps_plan_opts* o) {
+  if (!e || !o) return PS_E_INVAL;
+  if (const char* why = check_opts(*o)) return e->fail(PS_E_INVAL, why);
+  if (e->infl_count) return e->fail(PS_E_STATE, "asynchronous runs pending: ps_wait first");
+  const ps_plan_opts old = current_opts(e);
+  apply_opts(e, *o);
+  // a changed node-space build or row padding re-plans everything; the plan
+  // keys cover the rest (chain lengths, words, tail, launch price, k_flood split)
+  if (old.gpu_build != o->gpu_build || old.pad_words != o->pad_words) e->graph_dirty = true;
+  e->pull.key.clear();
+  e->pair.key.clear();
+  e->flood.key.clear();
+  e->chain_fail_key.clear();
+  e->gate_valid = false;
+  return PS_OK;
 }
 
 int ps_create(const ps_config* cfg, ps_engine** out) {
   if (!cfg || !out) return PS_E_INVAL;
   *out = nullptr;
   if (cfg->n_peers == 0 || cfg->n_topics == 0 || cfg->n_topics > 65535) return PS_E_INVAL;
+  if (cfg->msg_window > kMaxWindow) return PS_E_INVAL;  // (rows of at most 2^24 words)
   auto* e = new (std::nothrow) ps_engine();
   if (!e) return PS_E_NOMEM;
   e->cfg = *cfg;
@@ -534,7 +632,7 @@ int ps_dist_init(ps_engine* e, const ps_dist_config* dc, const uint8_t id[PS_UNI
   std::string err;
   e->transport = make_rccl_transport(dc->rank, dc->world, id, &err);
   if (!e->transport) return e->fail(PS_E_DEVICE, err);
-  e->xchg_overlap = e->xchg_overlap_env != 0;
+  refresh_xchg_overlap(e);
   return PS_OK;
 }
 
@@ -561,9 +659,9 @@ int ps_dist_init_loopback(ps_engine* e, const ps_dist_config* dc, ps_loopback* l
   if (rc) return rc;
   if (dc->world == 1) return PS_OK;
   if ((rc = dist_streams(e))) return rc;
-  e->transport = make_loopback_transport(lb->g, dc->rank, e->cfg.device);
+  e->transport = make_loopback_transport(lb->g, dc->rank, e->cfg.device, (dc->flags & PS_DIST_F_COPY) != 0);
   if (!e->transport) return e->fail(PS_E_INVAL, "loopback group size != world");
-  e->xchg_overlap = e->xchg_overlap_env < 0 ? false : e->xchg_overlap_env != 0;
+  refresh_xchg_overlap(e);
   return PS_OK;
 }
 
@@ -648,6 +746,12 @@ int ps_plan_create(uint32_t n_peers, uint32_t n_topics, const uint32_t* roots, c
 
 void ps_plan_destroy(ps_engine* e) {
   if (e && e->host_only) delete e;
+}
+
+int ps_plan_set_msg_window(ps_engine* e, uint32_t msg_window) {
+  if (!e || !e->host_only || msg_window == 0 || msg_window > kMaxWindow) return PS_E_INVAL;
+  e->cfg.msg_window = ((msg_window + 63) / 64) * 64;
+  return PS_OK;
 }
 
 int ps_plan_window(ps_engine* e, const uint32_t* topic_of_msg, const uint32_t* start_round, size_t n_msgs,

@@ -128,7 +128,8 @@ namespace {
 
 class LoopbackTransport final : public Transport {
  public:
-  LoopbackTransport(LoopbackGroup* g, int rank, int device) : g_(g), rank_(rank), device_(device) {
+  LoopbackTransport(LoopbackGroup* g, int rank, int device, bool copy)
+      : g_(g), rank_(rank), device_(device), copy_(copy) {
     (void)hipSetDevice(device_);
     (void)hipEventCreateWithFlags(&sent_, hipEventDisableTiming);
     for (auto& r : read_) (void)hipEventCreateWithFlags(&r, hipEventDisableTiming);
@@ -197,8 +198,10 @@ class LoopbackTransport final : public Transport {
   // Zero copy (level mode): the ranks share one process and one device, so a
   // receiving launch reads the sender's region where it lies -- no copy
   // launch, no receive buffer.  Two barriers as in exchange(): `sent` is
-  // re-recorded only after every rank has enqueued its waits on it.
-  bool zero_copy() const override { return true; }
+  // re-recorded only after every rank has enqueued its waits on it.  With
+  // PS_DIST_F_COPY (copy_) level mode takes exchange() instead, the RCCL
+  // transport's data path: the records land in the receive buffer.
+  bool zero_copy() const override { return !copy_; }
   hipError_t exchange_zc(const uint8_t* send, const std::vector<uint64_t>& send_off,
                          std::vector<const uint8_t*>& peer, hipStream_t s, std::string* err) override {
     hipError_t e = hipEventRecord(sent_, s);
@@ -251,15 +254,16 @@ class LoopbackTransport final : public Transport {
   }
   LoopbackGroup* g_;
   int rank_, device_;
+  bool copy_;
   hipEvent_t sent_ = nullptr, read_[2] = {nullptr, nullptr}, used_[kSendBufs] = {};
   int parity_ = 0;
 };
 
 }  // namespace
 
-std::unique_ptr<Transport> make_loopback_transport(LoopbackGroup* g, int rank, int device) {
+std::unique_ptr<Transport> make_loopback_transport(LoopbackGroup* g, int rank, int device, bool copy) {
   if (!g || rank < 0 || rank >= g->world) return nullptr;
-  return std::make_unique<LoopbackTransport>(g, rank, device);
+  return std::make_unique<LoopbackTransport>(g, rank, device, copy);
 }
 
 }  // namespace psamd

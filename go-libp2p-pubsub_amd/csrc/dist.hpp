@@ -7,9 +7,10 @@
 //   RcclTransport      ncclSend / ncclRecv pairs in one group (all-to-allv over
 //                      xGMI), the production transport.
 //   LoopbackTransport  `world` engines of one process (threads) copy each
-//                      other's regions device-to-device (compaction mode) or,
-//                      in level mode, read them in place (zero-copy); lets the
-//                      real kernels and routing be tested on a single GPU.
+//                      other's regions device-to-device (compaction mode;
+//                      level mode with PS_DIST_F_COPY) or, in level mode, read
+//                      them in place (zero-copy); lets the real kernels and
+//                      routing be tested on a single GPU.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -73,6 +74,8 @@ int rccl_unique_id(uint8_t id_out[128]);
 struct LoopbackGroup;
 LoopbackGroup* loopback_create(int world);
 void loopback_destroy(LoopbackGroup* g);
-std::unique_ptr<Transport> make_loopback_transport(LoopbackGroup* g, int rank, int device);
+// copy: level mode copies the records into the receive buffer (the RCCL data
+// path) instead of reading them in place (zero copy)
+std::unique_ptr<Transport> make_loopback_transport(LoopbackGroup* g, int rank, int device, bool copy);
 
 }  // namespace psamd

@@ -27,6 +27,7 @@ namespace psamd {
 constexpr uint32_t kMaxRoundsCap = 4096;  // round buffers' minimum size (deeper windows grow them)
 constexpr uint32_t kMaxStartRound = 200;
 constexpr uint32_t kDefaultWindow = 65536;
+constexpr uint32_t kMaxWindow = 1u << 30;  // messages per topic per window at most (ps_config.msg_window)
 
 inline uint32_t ceil_div(uint64_t a, uint64_t b) { return static_cast<uint32_t>((a + b - 1) / b); }
 
@@ -200,10 +201,11 @@ struct ps_engine {
   hipStream_t xstream = nullptr;  // multi-GPU: the exchange, beside the round's local chunks
   hipEvent_t ev_run0 = nullptr, ev_run1 = nullptr;
   hipEvent_t ev_round = nullptr, ev_xchg = nullptr;  // multi-GPU: round boundary, exchange done
-  // the exchange on its own stream beside the round's locally fed chunks:
-  // RCCL yes; the loopback transport (a copy kernel on the same GPU) no --
-  // there it only contends with the chunks (4 loopback ranks, cfg4: 7.06 vs
-  // 6.32 ms/step, profiles/r03/loopback); PSAMD_XCHG_OVERLAP=0/1 forces it
+  // the exchange on its own stream beside the round's locally fed chunks
+  // (ps_plan_opts.xchg_overlap, -1 = auto): a transport that copies the
+  // records (RCCL; the loopback with PS_DIST_F_COPY) yes; the zero-copy
+  // loopback no -- there it only contends for the same GPU (4 loopback
+  // ranks, cfg4: 7.06 vs 6.32 ms/step, profiles/r03/loopback)
   int xchg_overlap_env = -1;
   bool xchg_overlap = true;
   std::vector<hipEvent_t> ev_k;  // pairs around expand launches
@@ -242,6 +244,10 @@ struct ps_engine {
   bool flood_profile = false;  // PSAMD_FLOOD_PROFILE=1: per-wave phase times of k_flood to stderr (sync runs)
   psamd::DevBuf d_flood_prof;
   uint32_t flood_prof_waves = 0;
+  // PSAMD_CHAIN_PROFILE=<file>: per-wave start / end / words of every
+  // k_pull_chain launch of blocking windows, appended to <file> (debug)
+  std::string chain_prof_path;
+  psamd::DevBuf d_chain_prof;
 
   std::vector<psamd::TopicHost> topics;
   std::vector<uint8_t> live;
@@ -255,11 +261,9 @@ struct ps_engine {
   psamd::PullPlan pull;
   psamd::DevBuf d_pull;
   uint64_t pull_up = ~0ull;  // plan version of the chunks on the device
-  // k_pull_pair: rounds q and q + 1 in one launch
-  // (PSAMD_PULL_PAIR=0: one k_pull launch per round)
-  bool pair_on = true;
-  // rounds per launch at most (PSAMD_CHAIN, 1..kChainLevels, both kinds of
-  // window): 2 = pairs.  Defaults by measurement (profiles/r03/ab_chain_v2.txt):
+  // rounds per launch at most (ps_plan_opts.chain_max, 1..kChainLevels): 1 =
+  // one k_pull per round, 2 = pairs (k_pull_pair), 3..6 chains.
+  // Defaults by measurement (profiles/r03/ab_chain_v2.txt):
   // 4 for single-start windows (cfg3 burst 1.016 vs 1.033 ms at 6), 6 for
   // windows with start groups (paced cfg3 1.363 vs 1.443 ms at 4)
   uint32_t chain_max = 4, chain_max_groups = 6;

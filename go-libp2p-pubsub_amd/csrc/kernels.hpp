@@ -214,7 +214,11 @@ struct PullArgs {
   // the partial slots of each round of the launch
   const uint32_t* row_ptr;
   uint64_t* partials_r[6];  // (kChainLevels)
+  // debug (PSAMD_CHAIN_PROFILE): per chunk kChainProf words -- s_memrealtime
+  // at the wave's start and end, row words written, HW_ID and XCC_ID; null: off
+  uint64_t* prof;
 };
+constexpr uint32_t kChainProf = 4;
 // k_pull_pair: per wave, a run of at most kPairPar nodes
 // whose rows (at most kPairWords words in all) stay in LDS for its children,
 // streamed kPairKids children at a time
@@ -247,7 +251,7 @@ struct ChainChunk {
   uint32_t p_lo, p_hi;            // parents of the run (consecutive ids), kNone: unknown
   uint32_t W;                     // row stride, words
   uint32_t row0_lo, row0_hi;      // row of the topic's first node (its start group's block)
-  uint16_t w0, S;                 // the column slice of every row
+  uint32_t w0, S;                 // the column slice of every row (rows reach 2^24 words)
   uint8_t levels;                 // levels written: d .. d + levels - 1 (rounds r0 + k of the launch)
   uint8_t r0;                     // the run's round within the launch (a start group entering late: > 0)
   uint16_t group;                 // host: the start group

@@ -237,7 +237,6 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   const auto& xchg = e->ghost.rounds;
   std::vector<uint64_t> key = e->pull.key;  // (graph, flags, rounds, row widths, start groups)
   key.push_back(first);
-  key.push_back(e->pair_on ? 1 : 0);
   key.push_back(e->chain_max);
   key.push_back(e->chain_max_groups);
   key.push_back(e->chain_words);
@@ -251,7 +250,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   const double kLaunchBytes = e->launch_bytes;  // ~3 us of launch ramp and tail at ~5.5 TB/s
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
   const uint32_t chain_max = L.multi ? e->chain_max_groups : e->chain_max;
-  const uint32_t max_len = e->pair_on ? std::max<uint32_t>(1, std::min<uint32_t>(chain_max, kChainLevels)) : 1;
+  const uint32_t max_len = std::max<uint32_t>(1, std::min<uint32_t>(chain_max, kChainLevels));
   auto& kind = PP.kind;
   kind.assign(rounds + 2, PS_K_NONE);
   for (uint32_t q = 1; q <= first && q <= rounds; ++q) kind[q] = PS_K_FLOOD;
@@ -409,8 +408,8 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
             c.W = W;
             c.row0_lo = static_cast<uint32_t>(row0);
             c.row0_hi = static_cast<uint32_t>(row0 >> 32);
-            c.w0 = static_cast<uint16_t>(w0);
-            c.S = static_cast<uint16_t>(std::min(z.S, W - w0));
+            c.w0 = w0;
+            c.S = std::min(z.S, W - w0);
             c.levels = static_cast<uint8_t>(levels);
             c.r0 = static_cast<uint8_t>(r0);
             c.group = static_cast<uint16_t>(gi);
@@ -488,9 +487,16 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
 // k_flood (one rank) runs the leading rounds that each write at most
 // flood_top_bytes of rows: latency bound, one launch each would cost more
 // than their bytes.
+// (Windows under overlap_min_bytes never overlap -- run.cpp's byte floor --
+// so they keep k_flood: a small deep tree has nothing to gain from chains.)
 bool deep_window(const ps_engine* e, const WindowLayout& L) {
-  return e->overlap_on && L.level && e->world == 1 && !L.any_mesh && !(e->cfg.flags & PS_F_RECORD_HOPS) &&
-         !L.multi && L.planned0 >= e->overlap_min_rounds;
+  if (!(e->overlap_on && L.level && e->world == 1 && !L.any_mesh && !(e->cfg.flags & PS_F_RECORD_HOPS) &&
+        !L.multi && L.planned0 >= e->overlap_min_rounds))
+    return false;
+  uint64_t rows = 0;  // the window's row bytes, as run.cpp's floor counts them
+  for (uint32_t t = 0; t < L.tab.size(); ++t)
+    rows += static_cast<uint64_t>(L.tab[t].n_nodes) * L.tab[t].W * 8;
+  return rows >= e->overlap_min_bytes;
 }
 
 uint32_t plan_flood_rounds(const ps_engine* e, const WindowLayout& L) {

@@ -1037,6 +1037,9 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
   if (lane < 2) stage[kStage + lane] = 0;
   const uint32_t ci = blockIdx.x;
   if (ci >= n_chunks) return;
+  // debug profile (PSAMD_CHAIN_PROFILE): the wave's start, end and words
+  const uint64_t t_start = a.prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
+  uint64_t words_out = 0;
   // the chunk's scalars (its level ranges are read per level, not held)
   const ChainChunk* const cp = chunks + ci;
   const uint32_t node_begin = cp->node_begin, node_end = cp->node_end, topic = cp->topic;
@@ -1094,6 +1097,7 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
     // separate launch would find every generation current.)
     for (uint32_t j = lane; j < n0; j += 64)
       tabs[0][j] = (src[j] != 0 || (a.all_current & 1u)) ? static_cast<uint8_t>(j) : kChainNone;
+    words_out += c.sw;
     chain_flush(c, chain_slots(a, r0), slot, lane);
   }
   // src (level 0's sources) is dead from here and its LDS becomes ctab: no
@@ -1109,6 +1113,7 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
   WaveCtr c;
   while (k < levels) {
     if (y0 >= hi) {  // level k done
+      words_out += c.sw;
       chain_flush(c, chain_slots(a, r0 + k), slot, lane);
       asm volatile("" ::: "memory");
       x0 = lo;
@@ -1149,6 +1154,15 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
     }
     ctr_fold(c);
     y0 += kChainKids;
+  }
+  if (a.prof) {
+    // (HW_ID: wave, SIMD, CU, SE bits; XCC_ID[3:0], hwreg 20 on gfx950)
+    const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
+    const uint64_t v = lane == 0 ? t_start : lane == 1 ? t_end : lane == 2 ? words_out
+                                                                            : (static_cast<uint64_t>(xcc) << 32 | hw);
+    if (lane < kChainProf) a.prof[static_cast<uint64_t>(ci) * kChainProf + lane] = v;
   }
 }
 

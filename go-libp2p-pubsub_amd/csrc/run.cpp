@@ -205,6 +205,33 @@ void flood_profile_report(ps_engine* e) {
                100 * sum[3] / busy, 100 * sum[4] / busy, 100 * sum[5] / busy, sum[6] / nw, us(sum[7] / nw));
 }
 
+// Debug (PSAMD_CHAIN_PROFILE=<file>): appends the last blocking window's
+// k_pull_chain wave records to <file> (tools/chain_profile.py reads them):
+// u64 magic, u64 launches, per launch (round, rounds, lo, gsplit, hi), u64
+// chunks, then per chunk kChainProf profile words and (topic, W, S, run
+// nodes << 8 | levels).
+void chain_profile_dump(ps_engine* e, uint32_t planned0) {
+  const auto& K = e->pair.chain;
+  std::vector<uint64_t> p(K.size() * kChainProf);
+  if (p.empty() || hipMemcpy(p.data(), e->d_chain_prof.p, p.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) return;
+  std::vector<uint64_t> out{0x50524F4643484149ull, 0};
+  for (uint32_t q = 1; q <= planned0 && q < e->round_kind.size(); ++q)
+    if (e->round_kind[q] == PS_K_CHAIN) {
+      out.insert(out.end(), {q, e->pair.len[q], e->pair.lo[q], e->pair.gsplit[q], e->pair.hi[q]});
+      ++out[1];
+    }
+  out.push_back(K.size());
+  for (size_t i = 0; i < K.size(); ++i) {
+    out.insert(out.end(), p.begin() + i * kChainProf, p.begin() + (i + 1) * kChainProf);
+    out.insert(out.end(), {K[i].topic, K[i].W, K[i].S,
+                           static_cast<uint64_t>(K[i].node_end - K[i].node_begin) << 8 | K[i].levels});
+  }
+  if (FILE* f = std::fopen(e->chain_prof_path.c_str(), "ab")) {
+    std::fwrite(out.data(), 8, out.size(), f);
+    std::fclose(f);
+  }
+}
+
 // Propagates one window: per topic t, win[t] lists the messages (indices into
 // `msgs`) whose bits form t's block of W_t = ceil(|win[t]|/64) words.
 int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<WinSlice>& win, ps_stats* st) {
@@ -491,6 +518,14 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
                        e->gen_cur + 1 <= 255 && level && !any_mesh &&
                        !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS));
   e->gate_valid = false;  // (this window records its own gate below)
+  // the window's effective plan (ps_stats diagnostics)
+  st->prefix_rounds = pcap ? pre_P : 0;
+  st->overlapped += overlap ? 1 : 0;
+  st->xchg_path = PS_XCHG_NONE;
+  st->plan_max_rounds = 1;
+  if (level)
+    for (uint32_t q = flood_rounds + 1; q <= planned0 && q < e->pair.len.size(); ++q)
+      st->plan_max_rounds = std::max(st->plan_max_rounds, e->pair.len[q]);
   if (overlap) {
     HIP_TRY(hipStreamWaitEvent(e->pstream, e->ev_gate[e->gate_slot], 0), "wait for the previous gate");
     s = e->pstream;
@@ -545,6 +580,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
             "clear apply stats");
 
   ExpandArgs a{};
+  bool cprof = false;               // debug: chain launches profiled (PSAMD_CHAIN_PROFILE)
   bool host_stats_written = false;  // the reduce wrote the deferred slot's pinned rows
   bool reduce_side = false;         // ... on e->rstream (the window's end event goes there)
   a.frontier = e->d_frontier.as<uint32_t>();
@@ -623,6 +659,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     std::string xerr;
     hipError_t xe = e->transport->exchange(a.send, s_off, s_len, e->d_recv.as<uint8_t>(), r_off, r_len, s, &xerr);
     if (xe != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
+    st->xchg_path = PS_XCHG_COPY;
+    st->xchg_rounds += 1;
+    for (const uint64_t n : r_len) st->xchg_bytes += n;
     ApplyArgs ap{};
     ap.recv = e->d_recv.as<uint8_t>();
     ap.world = static_cast<uint32_t>(world);
@@ -714,6 +753,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     pa.ship = world > 1 ? e->d_ship.as<ShipEntry>() : nullptr;
     pa.send = e->d_send.as<uint64_t>();
     pa.all_current = (e->cfg.flags & PS_F_NO_LAZY_SEEN) ? 1u : 0u;
+    // debug: the chain launches' per-wave profile (blocking windows only)
+    cprof = !e->chain_prof_path.empty() && !(e->defer_last && e->defer_into) && !e->pair.chain.empty();
+    if (cprof) HIP_TRY(e->d_chain_prof.ensure(e->pair.chain.size() * kChainProf * 8), "alloc chain profile");
     // zero copy: the launches of round r ship into send part (r + 1) %
     // kSendBufs, which the readers of round r + 1 - kSendBufs may still hold
     auto reuse = [&](uint32_t q) -> int {
@@ -761,6 +803,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
           HIP_TRY(hipStreamWaitEvent(xs, e->ev_round, 0), "exchange wait");
         }
         std::string xerr;
+        st->xchg_path = zero_copy ? PS_XCHG_ZERO_COPY : PS_XCHG_COPY;
+        st->xchg_rounds += 1;
+        for (const uint64_t n : R.r_len) st->xchg_bytes += n;
         const uint8_t* sb = e->d_send.as<uint8_t>() + (r % kSendBufs) * e->ghost.send_half * 8;
         if (zero_copy) {
           // the ghost-fed nodes read each source's region in place: rsrc[a] is
@@ -793,12 +838,16 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
           pa.partials_r[k] = k < len ? partials + static_cast<size_t>(e->woff_host[r + k]) * kNumCtr : nullptr;
         HIP_TRY(time_mark(true), "event");
         ++launches;
+        uint64_t* const prof = cprof ? e->d_chain_prof.as<uint64_t>() : nullptr;
+        pa.prof = prof ? prof + static_cast<size_t>(e->pair.lo[r]) * kChainProf : nullptr;
         HIP_TRY(launch_pull_chain(pa, e->d_chain.as<ChainChunk>() + e->pair.lo[r], e->pair.gsplit[r] - e->pair.lo[r],
                                   r, record, ntc, false, s),
                 "pull chain");
+        pa.prof = prof ? prof + static_cast<size_t>(e->pair.gsplit[r]) * kChainProf : nullptr;
         HIP_TRY(launch_pull_chain(pa, e->d_chain.as<ChainChunk>() + e->pair.gsplit[r],
                                   e->pair.hi[r] - e->pair.gsplit[r], r, record, ntc, true, s),
                 "pull chain (column slices)");
+        pa.prof = nullptr;
         HIP_TRY(time_mark(false), "event");
         if (xr) HIP_TRY(hipStreamWaitEvent(s, e->ev_xchg, 0), "exchange join");  // (never: chains skip exchange rounds)
         continue;
@@ -997,6 +1046,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   }
   HIP_TRY(hipStreamSynchronize(s), "sync");
   if (mode == PS_MODE_FLOOD && e->flood_profile && e->flood_prof_waves) flood_profile_report(e);
+  if (cprof) chain_profile_dump(e, planned0);
   if (!accumulate_window(st, hs.data(), ha.data(), r, planned0, mode, flood_rounds, launches, world,
                          e->round_kind)) {
     // a k_flood dependency wait timed out (its waves were not all resident:
@@ -1284,7 +1334,13 @@ int ps_run_async(ps_engine* e) {
   e->ev_run1 = ev1;
   e->defer_into = nullptr;
   if (rc) {
+    // a failed window may have left its init and prefix on pstream or a
+    // reduce on rstream: drain every stream, and let no later window start
+    // beside a gate this one recorded
     (void)hipStreamSynchronize(e->stream);
+    for (hipStream_t x : {e->pstream, e->rstream, e->xstream})
+      if (x) (void)hipStreamSynchronize(x);
+    e->gate_valid = false;
     return rc;
   }
   ++e->infl_count;

@@ -62,7 +62,10 @@ class Stats(C.Structure):
                 ("expand_ms_per_round", C.c_float * MAX_ROUNDS),
                 ("frontier_per_round", C.c_uint32 * MAX_ROUNDS),
                 ("expand_bytes_per_round", C.c_uint64 * MAX_ROUNDS),
-                ("round_kernel", C.c_uint8 * MAX_ROUNDS)]
+                ("round_kernel", C.c_uint8 * MAX_ROUNDS),
+                ("plan_max_rounds", C.c_uint32), ("prefix_rounds", C.c_uint32),
+                ("overlapped", C.c_uint32), ("xchg_path", C.c_uint32),
+                ("xchg_rounds", C.c_uint64), ("xchg_bytes", C.c_uint64)]
 
     PER_ROUND = ("deliveries_per_round", "expand_ms_per_round", "frontier_per_round", "expand_bytes_per_round",
                  "round_kernel")
@@ -80,7 +83,24 @@ class Stats(C.Structure):
 
 class DistConfig(C.Structure):
     _fields_ = [("rank", C.c_int32), ("world", C.c_int32), ("partition", C.c_uint32),
-                ("split_depth", C.c_uint32)]
+                ("split_depth", C.c_uint32), ("flags", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+DIST_F_COPY = 0x1  # loopback: copy the records into the receive buffer (the RCCL data path)
+XCHG_NONE, XCHG_ZERO_COPY, XCHG_COPY = 0, 1, 2  # ps_stats.xchg_path
+
+
+class PlanOpts(C.Structure):
+    """ps_plan_opts (include/psengine.h): the launch-plan knobs."""
+    _fields_ = [("flood_top_bytes", C.c_uint64), ("overlap_min_bytes", C.c_uint64),
+                ("launch_bytes", C.c_uint64), ("flood", C.c_uint32), ("chain_max", C.c_uint32),
+                ("chain_max_groups", C.c_uint32), ("chain_tail", C.c_uint32), ("chain_words", C.c_uint32),
+                ("flood_words", C.c_uint32), ("pad_words", C.c_uint32), ("overlap", C.c_uint32),
+                ("overlap_min_rounds", C.c_uint32), ("xchg_overlap", C.c_int32), ("gpu_build", C.c_uint32),
+                ("flood_spin_ticks", C.c_uint32)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class MessageC(C.Structure):
@@ -114,6 +134,9 @@ PROTOTYPES = [
     ("ps_topic_depth", C.c_int, [_P, _u32, _u32p, _u32p]),
     ("ps_set_live", C.c_int, [_P, _u8p]),
     ("ps_set_flags", C.c_int, [_P, _u32]),
+    ("ps_plan_opts_default", C.c_int, [C.POINTER(PlanOpts)]),
+    ("ps_get_plan_opts", C.c_int, [_P, C.POINTER(PlanOpts)]),
+    ("ps_set_plan_opts", C.c_int, [_P, C.POINTER(PlanOpts)]),
     ("ps_publish", C.c_int, [_P, _u32p, C.c_size_t, _u32p]),
     ("ps_publish_at", C.c_int, [_P, _u32p, _u32p, C.c_size_t, _u32p]),
     ("ps_run", C.c_int, [_P, C.POINTER(Stats)]),
@@ -179,7 +202,8 @@ class Engine:
     def __init__(self, n_peers: int, n_topics: int = 1, tree_width: int = 2,
                  tree_max_width: int = 5, msg_window: int = 65536, device: int = 0,
                  record_hops: bool = False, time_kernels: bool = False, seed: int = 1,
-                 flags: int = 0):
+                 flags: int = 0, plan: dict | None = None):
+        """plan: launch-plan options to set right away (ps_set_plan_opts)."""
         L = load()
         self.n_peers = n_peers
         self.n_topics = n_topics
@@ -193,6 +217,8 @@ class Engine:
             raise EngineError(rc, "ps_create failed (is a GPU visible?)")
         self._h = h
         self._L = L
+        if plan:
+            self.set_plan(**plan)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -269,6 +295,24 @@ class Engine:
         """Replaces the PS_F_* flags for the next runs (ps_set_flags)."""
         self._check(self._L.ps_set_flags(self._h, flags))
         self.flags = flags
+
+    def plan_opts(self) -> dict:
+        """The effective launch-plan options (ps_get_plan_opts)."""
+        o = PlanOpts()
+        self._check(self._L.ps_get_plan_opts(self._h, C.byref(o)))
+        return o.as_dict()
+
+    def set_plan(self, **kw) -> dict:
+        """Changes launch-plan options by name (ps_set_plan_opts), e.g.
+        set_plan(flood=0, chain_max=2); returns the effective options."""
+        o = PlanOpts()
+        self._check(self._L.ps_get_plan_opts(self._h, C.byref(o)))
+        for k, v in kw.items():
+            if k not in dict(PlanOpts._fields_):
+                raise KeyError(f"no plan option {k!r}")
+            setattr(o, k, int(v))
+        self._check(self._L.ps_set_plan_opts(self._h, C.byref(o)))
+        return self.plan_opts()
 
     def set_time_kernels(self, on: bool):
         self.set_flags((self.flags & ~F_TIME_KERNELS) | (F_TIME_KERNELS if on else 0))
@@ -349,8 +393,10 @@ class Engine:
         self._check(self._L.ps_dist_init(self._h, C.byref(dc), uid))
 
     def dist_init_loopback(self, group: "Loopback", rank: int, partition: int = PART_PEER,
-                           split_depth: int = 0):
-        dc = DistConfig(rank, group.world, partition, split_depth)
+                           split_depth: int = 0, copy: bool = False):
+        """copy: the records go through the receive buffer (PS_DIST_F_COPY), the
+        RCCL transport's data path, instead of being read in place."""
+        dc = DistConfig(rank, group.world, partition, split_depth, DIST_F_COPY if copy else 0, 0)
         self._check(self._L.ps_dist_init_loopback(self._h, C.byref(dc), group._h))
 
 
@@ -394,6 +440,15 @@ def partition_owner(parent, root: int, topic: int, world: int, partition: int = 
     if rc != PS_OK:
         raise EngineError(rc, "ps_partition_owner")
     return out
+
+
+def default_plan_opts() -> dict:
+    """ps_plan_opts_default: the options every engine starts from."""
+    o = PlanOpts()
+    rc = load().ps_plan_opts_default(C.byref(o))
+    if rc != PS_OK:
+        raise EngineError(rc, "ps_plan_opts_default")
+    return o.as_dict()
 
 
 def version() -> str:

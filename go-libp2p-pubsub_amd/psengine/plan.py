@@ -7,7 +7,7 @@ import ctypes as C
 
 import numpy as np
 
-from . import DistConfig, EngineError, PART_PEER, _P, _p, _u32arr, load
+from . import DistConfig, EngineError, PART_PEER, PlanOpts, _P, _p, _u32arr, load
 
 INFO, NODES, PARENT, GHOST_REF, TOPIC, LAYOUT, ROUND_KIND, PULL, PAIR, XCHG, SEGS, SHIP, PACK, CHAIN = range(14)
 CHAIN_FIELDS = ("node_begin", "node_end", "topic", "W", "row0", "w0", "S", "levels", "r0", "group")
@@ -18,6 +18,7 @@ PROTOTYPES = [
     ("ps_plan_create", C.c_int, [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                  C.POINTER(DistConfig), C.POINTER(_P)]),
     ("ps_plan_destroy", None, [_P]),
+    ("ps_plan_set_msg_window", C.c_int, [_P, C.c_uint32]),
     ("ps_plan_window", C.c_int, [_P, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_size_t, C.c_uint32]),
     ("ps_plan_get", C.c_int, [_P, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64), C.c_size_t,
                               C.POINTER(C.c_size_t)]),
@@ -42,7 +43,7 @@ class Plan:
     absent) rooted at `roots`."""
 
     def __init__(self, parents, roots, world: int = 1, rank: int = 0, partition: int = PART_PEER,
-                 split_depth: int = 0):
+                 split_depth: int = 0, plan: dict | None = None):
         par = np.ascontiguousarray(np.asarray(parents, dtype=np.uint32).reshape(len(roots), -1))
         self.n_topics, self.n_peers = par.shape
         rt = _u32arr(roots)
@@ -54,6 +55,8 @@ class Plan:
             raise EngineError(rc, "ps_plan_create")
         self._h = h
         self.world, self.rank = world, rank
+        if plan:
+            self.set_plan(**plan)
 
     def close(self):
         if getattr(self, "_h", None):
@@ -62,6 +65,26 @@ class Plan:
 
     def __del__(self):
         self.close()
+
+    def set_plan(self, **kw) -> dict:
+        """Launch-plan options by name (ps_set_plan_opts on the probe)."""
+        L = lib()
+        o = PlanOpts()
+        L.ps_get_plan_opts(self._h, C.byref(o))
+        for k, v in kw.items():
+            if k not in dict(PlanOpts._fields_):
+                raise KeyError(f"no plan option {k!r}")
+            setattr(o, k, int(v))
+        rc = L.ps_set_plan_opts(self._h, C.byref(o))
+        if rc != 0:
+            raise EngineError(rc, "ps_set_plan_opts")
+        L.ps_get_plan_opts(self._h, C.byref(o))
+        return o.as_dict()
+
+    def set_msg_window(self, n: int):
+        rc = lib().ps_plan_set_msg_window(self._h, n)
+        if rc != 0:
+            raise EngineError(rc, "ps_plan_set_msg_window")
 
     def window(self, topics, starts=None, flags: int = 0):
         t = _u32arr(topics)

@@ -55,7 +55,8 @@ typedef struct ps_config {
   uint32_t n_topics;       /* topic slots [0, n_topics)                        */
   uint32_t tree_width;     /* DefaultTreeWidth  (pubsub.go:16), 0 -> 2         */
   uint32_t tree_max_width; /* DefaultTreeMaxWidth (pubsub.go:17), 0 -> 5       */
-  uint32_t msg_window;     /* max messages per topic per window, 0 -> 65536    */
+  uint32_t msg_window;     /* max messages per topic per window, 0 -> 65536,
+                              at most 2^30 (PS_E_INVAL above)                  */
   int32_t device;          /* HIP device ordinal                               */
   uint32_t flags;          /* PS_F_*                                           */
   uint32_t reserved;
@@ -93,7 +94,24 @@ typedef struct ps_stats {
   uint64_t expand_bytes_per_round[PS_MAX_ROUNDS]; /* algorithmic bytes per round */
   uint8_t round_kernel[PS_MAX_ROUNDS]; /* PS_K_*: the launch kind that wrote each
                                           round of the last window              */
+  /* the effective plan of the last window (scheduling diagnostics) */
+  uint32_t plan_max_rounds;    /* rounds of its longest launch (1: k_pull, 2: pair,
+                                  3..7: chain; k_flood counts as 1)            */
+  uint32_t prefix_rounds;      /* leading rounds that may run beside the previous
+                                  window (0: none)             */
+  uint32_t overlapped;         /* windows of this run whose prefix ran beside
+                                  their predecessor                             */
+  uint32_t xchg_path;          /* N ranks: PS_XCHG_* of the last window         */
+  uint64_t xchg_rounds;        /* N ranks: rounds of this run that exchanged     */
+  uint64_t xchg_bytes;         /* N ranks: ghost-record bytes this rank received */
 } ps_stats;
+
+/* ps_stats.xchg_path: how a multi-rank level window's ghost records moved */
+#define PS_XCHG_NONE 0u       /* one rank, or nothing exchanged                */
+#define PS_XCHG_ZERO_COPY 1u  /* read in place from the sender's send region
+                                 (loopback ranks sharing one process and GPU)  */
+#define PS_XCHG_COPY 2u       /* copied into this rank's receive buffer (RCCL
+                                 send/recv; the loopback with PS_DIST_F_COPY)  */
 
 /* ps_stats.round_kernel */
 #define PS_K_NONE 0u
@@ -149,6 +167,42 @@ int ps_topic_depth(ps_engine* e, uint32_t topic, uint32_t* depth_out, uint32_t* 
 /* Replace the engine's PS_F_* flags (e.g. PS_F_TIME_KERNELS for an
  * instrumented run between untimed ones); applies to the next ps_run. */
 int ps_set_flags(ps_engine* e, uint32_t flags);
+
+/* ---- launch-plan options ----------------------------------
+ * The schedule knobs whose defaults were chosen by measurement (the A/B
+ * records under profiles/).  ps_create starts from the defaults; a caller
+ * pins or changes them only through ps_set_plan_opts -- the environment does
+ * not touch them, except for A/B tools that set PSAMD_AB=1 (then the PSAMD_*
+ * variables are read at ps_create).  Plans are rebuilt on the next run. */
+typedef struct ps_plan_opts {
+  uint64_t flood_top_bytes;    /* k_flood runs the leading rounds that each write at
+                                  most this many row bytes (4 MiB)              */
+  uint64_t overlap_min_bytes;  /* windows of fewer row bytes never overlap (512 MiB) */
+  uint64_t launch_bytes;       /* planner: a launch's ramp and tail, as row bytes (16e6) */
+  uint32_t flood;              /* 1: k_flood for a one-rank window's leading rounds (1) */
+  uint32_t chain_max;          /* rounds per launch at most, single-start windows:
+                                  1 = one k_pull per round, 2 = pairs, 3..6 chains (4) */
+  uint32_t chain_max_groups;   /* the same for windows with start groups (6)     */
+  uint32_t chain_tail;         /* 1: a chain ending at the last round may take one
+                                  round more (1)                                */
+  uint32_t chain_words;        /* row words a chain wave writes, planner target (8192) */
+  uint32_t flood_words;        /* row words per k_flood task (2048)              */
+  uint32_t pad_words;          /* rows of at least this many words padded to even (16) */
+  uint32_t overlap;            /* 1: pipelined deep windows overlap their leading
+                                  launches with the previous window (1)          */
+  uint32_t overlap_min_rounds; /* ... windows of at least this many rounds (12) */
+  int32_t xchg_overlap;        /* N ranks: exchange on its own stream beside the
+                                  locally fed chunks: -1 auto (RCCL yes, loopback
+                                  no), 0, 1 (-1)                                */
+  uint32_t gpu_build;          /* 1: rebuild a one-rank node space on the GPU (1) */
+  uint32_t flood_spin_ticks;   /* k_flood dependency-wait bound, 100-MHz ticks (2e8) */
+} ps_plan_opts;
+
+int ps_plan_opts_default(ps_plan_opts* out);
+/* effective options of an engine (the defaults, or what ps_set_plan_opts set) */
+int ps_get_plan_opts(const ps_engine* e, ps_plan_opts* out);
+/* PS_E_INVAL on an out-of-range value; PS_E_STATE with runs in flight */
+int ps_set_plan_opts(ps_engine* e, const ps_plan_opts* opts);
 
 /* Subscribed-and-live mask over peers (1 = receives and forwards).  A peer
  * whose client stopped reading (client.go:103-131) is 0. Default: all 1. */
@@ -224,7 +278,14 @@ typedef struct ps_dist_config {
   int32_t world;        /* <= 16 */
   uint32_t partition;   /* PS_PART_*                                    */
   uint32_t split_depth; /* PS_PART_SUBTREE: split level, 0 = automatic */
+  uint32_t flags;       /* PS_DIST_F_*                                  */
+  uint32_t reserved;
 } ps_dist_config;
+/* ps_dist_config.flags: the loopback transport copies every round's ghost
+ * records into the receiver's buffer, the data path of the RCCL transport
+ * (send parts, receive buffer, exchange stream), instead of reading them in
+ * place (tests run the RCCL-shaped path on one GPU with it; RCCL: ignored) */
+#define PS_DIST_F_COPY 0x1u
 
 /* rank 0 creates the RCCL id; the caller ships it to every rank */
 int ps_dist_unique_id(uint8_t id_out[PS_UNIQUE_ID_BYTES]);

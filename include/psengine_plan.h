@@ -22,6 +22,8 @@ extern "C" {
 int ps_plan_create(uint32_t n_peers, uint32_t n_topics, const uint32_t* roots, const uint32_t* parents,
                    const ps_dist_config* dc, ps_engine** out);
 void ps_plan_destroy(ps_engine* e);
+/* ps_config.msg_window of the probe (default 65536; PS_E_INVAL above 2^30) */
+int ps_plan_set_msg_window(ps_engine* e, uint32_t msg_window);
 /* Plans the first window of a batch (topic and start round per message; a
  * null start_round = all round 0), as ps_run would; flags: PS_F_* */
 int ps_plan_window(ps_engine* e, const uint32_t* topic_of_msg, const uint32_t* start_round, size_t n_msgs,

@@ -66,7 +66,7 @@ def test_code_object_is_gfx950(lib):
 
 def test_struct_layouts(lib):
     assert ctypes.sizeof(PE.Config) == 40
-    assert ctypes.sizeof(PE.Stats) == 9 * 8 + 3 * 8 + 8 + PE.MAX_ROUNDS * 25
+    assert ctypes.sizeof(PE.Stats) == 9 * 8 + 3 * 8 + 8 + PE.MAX_ROUNDS * 25 + 16 + 16
     src = open(HEADER).read()
     assert f"#define PS_MAX_ROUNDS {PE.MAX_ROUNDS}" in src
     for name, val in [("PS_F_RECORD_HOPS", PE.F_RECORD_HOPS), ("PS_F_TIME_KERNELS", PE.F_TIME_KERNELS)]:
@@ -92,3 +92,29 @@ def test_no_cpu_fallback_without_gpu(lib):
     with pytest.raises(PE.EngineError) as ei:
         PE.Engine(8)
     assert ei.value.code == -6
+
+
+def test_struct_offsets_match_c(tmp_path):
+    """Every field of the ctypes mirrors sits where the C compiler puts it
+    (gcc on include/psengine.h)."""
+    structs = {"ps_config": PE.Config, "ps_stats": PE.Stats, "ps_dist_config": PE.DistConfig,
+               "ps_plan_opts": PE.PlanOpts, "ps_message": PE.MessageC, "ps_message_buf": PE.MessageBuf}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "psengine.h"', "int main(void) {"]
+    for cname, cls in structs.items():
+        lines.append(f'  printf("{cname} sizeof %zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            cf = "type" if f == "type" else f
+            lines.append(f'  printf("{cname} {f} %zu\\n", offsetof({cname}, {cf}));')
+    lines.append("  return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = {}
+    for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        s, f, v = line.split()
+        got[(s, f)] = int(v)
+    for cname, cls in structs.items():
+        assert got[(cname, "sizeof")] == ctypes.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert got[(cname, f)] == getattr(cls, f).offset, (cname, f)

@@ -112,29 +112,46 @@ def test_async_with_hop_record_and_churn():
             assert st.deliveries == 20 * int((exp != 0xFF).sum())
 
 
+def vary_counts(msg_topics, i):
+    """Window i's batch: each topic loses up to (n_t - 1) % 64 of its last
+    messages, so its row width ceil(n_t / 64) -- and the plan -- stays, while
+    its last row word differs from window to window."""
+    keep = np.ones(msg_topics.shape[0], dtype=bool)
+    for t in np.unique(msg_topics):
+        idx = np.nonzero(msg_topics == t)[0]
+        drop = (i * 7 + int(t)) % ((idx.shape[0] - 1) % 64 + 1)
+        if drop:
+            keep[idx[-drop:]] = False
+    return msg_topics[keep]
+
+
 @pytest.mark.parametrize("dead,full", [(0.0, False), (0.03, False), (0.02, True)])
 def test_overlapped_windows_equal_blocking(monkeypatch, dead, full):
     """Deep windows pipelined with the same plan: each window's leading
     launches run beside the previous window's last ones.
     Every run's counters and the final rows equal blocking runs, and the
     overlap did happen.  Small cases lower the window-size floor of the
-    overlap; the full-size cfg3 case keeps the default."""
-    if not full:
-        monkeypatch.setenv("PSAMD_OVERLAP_BYTES", "0")
+    overlap; the full-size cfg3 case keeps the default.  Consecutive windows
+    carry different message counts per topic (the same row widths, so the
+    same plan and the overlap still applies), so their rows differ in every
+    topic's last word: a launch reading rows its successor had already
+    rewritten would change its own window's counters."""
     wl = WL.cfg3() if full else WL.cfg3(200_000, 16, 5000)
     rng = np.random.default_rng(11)
     live = (rng.random(wl.n_peers) >= dead).astype(np.uint8)
     live[[ts.root for ts in wl.topics]] = 1
-    batch = wl.msg_topics
+    batches = [vary_counts(wl.msg_topics, i) for i in range(8)]
+    assert len({b.shape[0] for b in batches}) > 4
+    plan = {} if full else {"overlap_min_bytes": 0}
     out = []
     for pipelined in (False, True):
-        e = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed)
+        e = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed, plan=plan)
         WL.build_engine_topics(e, wl)
         e.set_live(live)
         res = []
         if pipelined:
             for i in range(8):
-                e.publish(batch)
+                e.publish(batches[i])
                 e.run_async()
                 if i:
                     res.append(stats_key(e.wait()))
@@ -142,7 +159,7 @@ def test_overlapped_windows_equal_blocking(monkeypatch, dead, full):
             assert e.overlapped_windows() >= 5
         else:
             for i in range(8):
-                e.publish(batch)
+                e.publish(batches[i])
                 res.append(stats_key(e.run()))
             assert e.overlapped_windows() == 0
             assert res[-1][2] >= 12  # a deep window (rounds)

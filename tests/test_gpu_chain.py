@@ -3,8 +3,7 @@ one launch: each wave writes a run of level-d nodes (its parents' rows from
 HBM, kept in its LDS stage) and then every descendant of the run level by
 level, each node copying the stage row its parent holds --
 against the restatement (oracle/psoracle.c) and against one k_pull launch per
-round (PSAMD_CHAIN=1) and pair launches (PSAMD_CHAIN=2); PSAMD_CHAIN is read
-at engine creation.
+round (ps_plan_opts.chain_max = 1) and pair launches (chain_max = 2).
 
 Round q delivers to BFS level q - s of each topic: a node receives its
 parent's row of round q - 1 if the parent was reached this window and the
@@ -28,11 +27,8 @@ pytestmark = pytest.mark.gpu
 
 def run(monkeypatch, chain, n, topics, live, msg_topics, starts=None, record=True, flood=False, flags=0,
         msg_window=65536):
-    monkeypatch.setenv("PSAMD_PULL_PAIR", "1")
-    monkeypatch.setenv("PSAMD_CHAIN", str(chain))
-    monkeypatch.setenv("PSAMD_FLOOD", "1" if flood else "0")
-    monkeypatch.delenv("PSAMD_FLOOD_TOP_BYTES", raising=False)
-    with PE.Engine(n, len(topics), record_hops=record, flags=flags, msg_window=msg_window) as eng:
+    opts = {"chain_max": chain, "chain_max_groups": chain, "flood": int(flood)}
+    with PE.Engine(n, len(topics), record_hops=record, flags=flags, msg_window=msg_window, plan=opts) as eng:
         for t, (root, parent) in enumerate(topics):
             eng.set_tree(t, root, parent)
         eng.set_live(live)
@@ -93,11 +89,14 @@ def test_chain_column_slices(monkeypatch, n_msgs):
     msg_topics = np.concatenate([np.zeros(n_msgs, dtype=np.uint32), np.ones(150, dtype=np.uint32)])
     rng.shuffle(msg_topics)
     sweep(monkeypatch, n, topics, live, msg_topics, records=(False,), chains=(1, 2, 4, 6), msg_window=1 << 16)
-    # hops of a sample through a recording run
+    # hops of every message through a recording run of the same rows: at
+    # 52,000 messages the hot rows (814 words) are column-sliced, so the
+    # recording slice variant (k_pull_chain<record, slices>) is checked too
+    # 
     exp = oracle_hops(topics, live)
-    st, kinds, hops, _, _ = run(monkeypatch, 4, n, topics, live, msg_topics[:5000], msg_window=1 << 16)
+    st, kinds, hops, _, _ = run(monkeypatch, 4, n, topics, live, msg_topics, msg_window=1 << 16)
     assert PE.K_CHAIN in kinds
-    check_hops(hops, exp, msg_topics[:5000], "chain=4 record")
+    check_hops(hops, exp, msg_topics, "chain=4 record")
 
 
 @pytest.mark.parametrize("seed", range(4))
@@ -165,7 +164,7 @@ def test_chain_after_flood(monkeypatch, seed):
 
 
 def test_chain_deep_path_hops_past_255(monkeypatch):
-    """A 600-deep chain of peers: 4- and 6-round launches only (PSAMD_FLOOD=0); hops
+    """A 600-deep chain of peers: 4- and 6-round launches only (flood 0); hops
     past 255 saturate at 254 as in the restatement."""
     n = 600
     parent = np.full(n, O.NONE, dtype=np.uint32)
@@ -185,9 +184,8 @@ def test_chain_many_windows_and_drains(monkeypatch):
     peers = [int(p) for p in rng.integers(0, n, size=12)]
     outs = []
     for chain in (1, 4, 6):
-        monkeypatch.setenv("PSAMD_CHAIN", str(chain))
-        monkeypatch.setenv("PSAMD_FLOOD", "0")
-        with PE.Engine(n, len(topics), record_hops=True, msg_window=128) as eng:
+        opts = {"chain_max": chain, "chain_max_groups": chain, "flood": 0}
+        with PE.Engine(n, len(topics), record_hops=True, msg_window=128, plan=opts) as eng:
             for t, (root, parent) in enumerate(topics):
                 eng.set_tree(t, root, parent)
             eng.set_live(live)

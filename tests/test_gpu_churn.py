@@ -21,15 +21,7 @@ pytestmark = pytest.mark.gpu
 
 def make_engine(n, gpu_build, n_topics=1, **kw):
     """An engine whose node space is rebuilt on the GPU (default) or host."""
-    old = os.environ.get("PSAMD_GPU_BUILD")
-    os.environ["PSAMD_GPU_BUILD"] = "1" if gpu_build else "0"
-    try:
-        return PE.Engine(n, n_topics, **kw)
-    finally:
-        if old is None:
-            del os.environ["PSAMD_GPU_BUILD"]
-        else:
-            os.environ["PSAMD_GPU_BUILD"] = old
+    return PE.Engine(n, n_topics, plan={"gpu_build": int(gpu_build)}, **kw)
 
 
 @pytest.mark.parametrize("gpu_build", [True, False])

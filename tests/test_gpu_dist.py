@@ -44,12 +44,21 @@ def run_ranks(engines):
     return stats
 
 
-def make_ranks(world, n, n_topics, partition, split_depth=0, **kw):
+def make_ranks(world, n, n_topics, partition, split_depth=0, copy=False, **kw):
+    """copy: the RCCL-shaped data path (PS_DIST_F_COPY: records through the
+    receive buffer) instead of the zero-copy loopback reads."""
     lb = PE.Loopback(world)
     engines = [PE.Engine(n, n_topics, record_hops=True, **kw) for _ in range(world)]
     for r, e in enumerate(engines):
-        e.dist_init_loopback(lb, r, partition, split_depth)
+        e.dist_init_loopback(lb, r, partition, split_depth, copy=copy)
     return lb, engines
+
+
+def check_path(stats, copy):
+    """Which transport path ran (ps_stats.xchg_path), on every rank."""
+    want = PE.XCHG_COPY if copy else PE.XCHG_ZERO_COPY
+    assert all(st.xchg_rounds > 0 for st in stats), [st.xchg_rounds for st in stats]
+    assert all(st.xchg_path == want for st in stats), [st.xchg_path for st in stats]
 
 
 def merged_hops(engines, msg):
@@ -57,21 +66,24 @@ def merged_hops(engines, msg):
     return h.min(axis=0)  # every peer is owned by exactly one rank per topic
 
 
-@pytest.mark.parametrize("overlap", ["0", "1"])
+@pytest.mark.parametrize("copy", [False, True])
+@pytest.mark.parametrize("overlap", [0, 1])
 @pytest.mark.parametrize("staggered", [True, False])
 @pytest.mark.parametrize("world,partition", [(2, PE.PART_SUBTREE), (3, PE.PART_PEER),
                                              (4, PE.PART_SUBTREE), (4, PE.PART_PEER)])
-def test_sharded_trees_match_oracle(monkeypatch, world, partition, staggered, overlap):
+def test_sharded_trees_match_oracle(world, partition, staggered, overlap, copy):
     """Level mode on N ranks, single start round and staggered starts (start
     groups: one word block per start round, each group's ghost records
     exchanged in its own rounds), with dead peers cutting subtrees across
     ranks; never the compaction path.  overlap=1: the
     exchange on its own stream beside the round's locally fed chunks, as RCCL
-    runs it (the loopback default is one stream)."""
-    monkeypatch.setenv("PSAMD_XCHG_OVERLAP", overlap)
+    runs it (the zero-copy loopback default is one stream).  copy: the records
+    go through each receiver's buffer (PS_DIST_F_COPY) -- the RCCL transport's
+    data path: send parts, receive buffer, exchange stream (VERDICT r3 item 1;
+    subtree.go:333, client.go:103-131)."""
     rng = np.random.default_rng(world * 10 + partition + 100 * staggered)
     n, n_topics = 2500, 3
-    lb, engines = make_ranks(world, n, n_topics, partition)
+    lb, engines = make_ranks(world, n, n_topics, partition, copy=copy, plan={"xchg_overlap": overlap})
     trees = [random_tree(rng, n, int(rng.integers(0, n))) for _ in range(n_topics)]
     live = (rng.random(n) > 0.08).astype(np.uint8)
     topics = rng.integers(0, n_topics, size=150)
@@ -83,6 +95,7 @@ def test_sharded_trees_match_oracle(monkeypatch, world, partition, staggered, ov
     firsts = [e.publish(topics, starts) for e in engines]
     stats = run_ranks(engines)
     assert all(st.expand_mode == PE.MODE_LEVEL_PULL for st in stats), [st.expand_mode for st in stats]
+    check_path(stats, copy)
     total = 0
     for t in range(n_topics):
         root = int(np.nonzero(trees[t] == O.NONE)[0][0])
@@ -212,8 +225,9 @@ def test_sharded_churn_batches():
     lb.close()
 
 
+@pytest.mark.parametrize("copy", [False, True])
 @pytest.mark.parametrize("world", [2, 4])
-def test_cfg4_shaped_peer_partition(world):
+def test_cfg4_shaped_peer_partition(world, copy):
     """cfg4-shaped trees (TreeOpts{8,20} by the restated joins, scaled to
     200k peers) under the peer hash (the default partition),
     with ~3 % dead peers: every round ships ghost parents over the loopback
@@ -233,12 +247,13 @@ def test_cfg4_shaped_peer_partition(world):
     lb = PE.Loopback(world)
     engines = [PE.Engine(wl.n_peers, 1, seed=wl.seed, record_hops=True) for _ in range(world)]
     for r, e in enumerate(engines):
-        e.dist_init_loopback(lb, r)  # PART_PEER by default
+        e.dist_init_loopback(lb, r, copy=copy)  # PART_PEER by default
         WL.build_engine_topics(e, wl)
         e.set_live(live)
     firsts = [e.publish(wl.msg_topics) for e in engines]
     stats = run_ranks(engines)
     assert all(s.expand_mode == PE.MODE_LEVEL_PULL for s in stats)
+    check_path(stats, copy)
     assert sum(s.deliveries for s in stats) == st1.deliveries
     assert sum(e.seen_digest() for e in engines) % (1 << 64) == d1
     rp, cl = O.parents_to_csr(par)

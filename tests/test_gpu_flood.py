@@ -5,8 +5,8 @@ Round q delivers to BFS level q - s_t of each topic: a node receives its
 parent's row of round q - 1 if the parent was reached this window and the
 node is live (subtree.forwardMessage, subtree.go:319-354, the dead-child skip
 at :326-331; client.processMessages, client.go:100-132).  k_flood orders the
-rounds by per-task dependencies inside one launch; PSAMD_FLOOD=0 (read at
-engine creation) runs one k_pull launch per round instead.  Both must give
+rounds by per-task dependencies inside one launch; ps_plan_opts.flood = 0
+runs one k_pull launch per round instead.  Both must give
 the oracle's (peer, message, hop) exactly, the same per-round counters, and
 the same final seen state -- recording and production instances alike.
 """
@@ -37,18 +37,16 @@ def random_tree(rng, n, root, fan):
 
 
 def run_mode(monkeypatch, flood, n, topics, live, msg_topics, record=True, starts=None, words=None, top=None):
-    """One window; `top` (PSAMD_FLOOD_TOP_BYTES): k_flood runs the leading
-    rounds writing at most that many row bytes, k_pull the rest (default:
-    32 MB, every round of these small trees)."""
-    monkeypatch.setenv("PSAMD_FLOOD", "1" if flood else "0")
+    """One window; `top` (ps_plan_opts.flood_top_bytes): k_flood runs the
+    leading rounds writing at most that many row bytes, k_pull the rest
+    (default: 4 MB, every round of these small trees)."""
     # (deep windows plan no k_flood while the cross-window overlap is on)
-    monkeypatch.setenv("PSAMD_OVERLAP", "0" if flood else "1")
-    for var, val in (("PSAMD_FLOOD_WORDS", words), ("PSAMD_FLOOD_TOP_BYTES", top)):
-        if val is None:
-            monkeypatch.delenv(var, raising=False)
-        else:
-            monkeypatch.setenv(var, str(val))
-    with PE.Engine(n, len(topics), record_hops=record) as eng:
+    opts = {"flood": int(flood), "overlap": 0 if flood else 1}
+    if top is not None:
+        opts["flood_top_bytes"] = top
+    if words is not None:
+        opts["flood_words"] = words
+    with PE.Engine(n, len(topics), record_hops=record, plan=opts) as eng:
         for t, (root, parent) in enumerate(topics):
             eng.set_tree(t, root, parent)
         eng.set_live(live)
@@ -207,8 +205,6 @@ def test_flood_deep_chain(monkeypatch):
 def test_flood_follows_live_changes(monkeypatch):
     """Kill and revive top-level peers between runs of one engine: every run
     decides reachability from its own window's generation stamps."""
-    monkeypatch.setenv("PSAMD_FLOOD", "1")
-    monkeypatch.setenv("PSAMD_OVERLAP", "0")  # (deep windows plan no k_flood otherwise)
     rng = np.random.default_rng(9)
     n = 3000
     parent = random_tree(rng, n, 0, fan=3)
@@ -216,7 +212,7 @@ def test_flood_follows_live_changes(monkeypatch):
     live = np.ones(n, dtype=np.uint8)
     kids = np.nonzero(parent == 0)[0]
     grand = np.nonzero(np.isin(parent, kids))[0]
-    with PE.Engine(n, 1, record_hops=True) as eng:
+    with PE.Engine(n, 1, record_hops=True, plan={"flood": 1, "overlap": 0}) as eng:
         eng.set_tree(0, 0, parent)
         for step, change in enumerate([None, kids[:1], grand[:3], None, "revive"]):
             if isinstance(change, str):
@@ -314,7 +310,7 @@ def test_cfg3_topology_dead_mask_hops_record_instance():
 
 def test_flood_timeout_reruns_window_per_round(monkeypatch):
     """k_flood needs every wave resident; when they are not (another engine
-    shares the GPU) a dependency wait times out.  PSAMD_FLOOD_SPIN_TICKS=0
+    shares the GPU) a dependency wait times out.  flood_spin_ticks = 0
     forces that on a 40-level tree: the same window is re-run with per-round
     launches under a fresh generation (exact hops, counters and digest), and
     later windows keep the per-round launches.  An asynchronous run that times
@@ -328,11 +324,8 @@ def test_flood_timeout_reruns_window_per_round(monkeypatch):
     rp, cl = O.parents_to_csr(parent)
     _, oh, _ = O.disseminate(rp, cl, 0, live, 1)
     n_msgs = 130
-    monkeypatch.setenv("PSAMD_FLOOD", "1")
-    monkeypatch.setenv("PSAMD_OVERLAP", "0")  # (deep windows plan no k_flood otherwise)
-    monkeypatch.setenv("PSAMD_FLOOD_TOP_BYTES", str(1 << 40))
-    monkeypatch.setenv("PSAMD_FLOOD_SPIN_TICKS", "0")
-    with PE.Engine(n, 1, record_hops=True) as eng:
+    opts = {"flood": 1, "overlap": 0, "flood_top_bytes": 1 << 40, "flood_spin_ticks": 0}
+    with PE.Engine(n, 1, record_hops=True, plan=opts) as eng:
         eng.set_tree(0, 0, parent)
         eng.set_live(live)
         d0 = eng.depth(0)[0]
@@ -344,8 +337,7 @@ def test_flood_timeout_reruns_window_per_round(monkeypatch):
             assert st.windows == 1 and st.deliveries == n_msgs * int((oh[0][1:] != 0xFF).sum())
             for m in (0, 64, n_msgs - 1):
                 assert np.array_equal(eng.hops(first + m), oh[0]), (rep, m)
-    monkeypatch.setenv("PSAMD_FLOOD_SPIN_TICKS", "0")
-    with PE.Engine(n, 1) as eng:
+    with PE.Engine(n, 1, plan={"flood_spin_ticks": 0}) as eng:
         eng.set_tree(0, 0, parent)
         eng.set_live(live)
         eng.publish(np.zeros(n_msgs))

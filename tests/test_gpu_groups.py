@@ -35,8 +35,8 @@ def random_tree(rng, n, root, fan):
     return parent
 
 
-def run(level, n, topics, live, msg_topics, starts, record=True):
-    with PE.Engine(n, len(topics), record_hops=record, flags=0 if level else PE.F_COMPACT) as eng:
+def run(level, n, topics, live, msg_topics, starts, record=True, plan=None):
+    with PE.Engine(n, len(topics), record_hops=record, flags=0 if level else PE.F_COMPACT, plan=plan) as eng:
         for t, (root, parent) in enumerate(topics):
             eng.set_tree(t, root, parent)
         eng.set_live(live)
@@ -80,13 +80,8 @@ def test_groups_match_oracle_and_compaction(monkeypatch, seed):
     outs = []
     # level mode: the default k_flood / k_pull split, every round in k_flood,
     # every round in k_pull; then the compaction path
-    for level, env in ((True, {}), (True, {"PSAMD_FLOOD_TOP_BYTES": str(1 << 40)}), (True, {"PSAMD_FLOOD": "0"}),
-                       (False, {})):
-        for k in ("PSAMD_FLOOD_TOP_BYTES", "PSAMD_FLOOD"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in env.items():
-            monkeypatch.setenv(k, v)
-        st, hops, deliv, pm, digest = run(level, n, topics, live, msg_topics, starts)
+    for level, opts in ((True, {}), (True, {"flood_top_bytes": 1 << 40}), (True, {"flood": 0}), (False, {})):
+        st, hops, deliv, pm, digest = run(level, n, topics, live, msg_topics, starts, plan=opts)
         for m, t in enumerate(msg_topics):
             if not np.array_equal(hops[m], exp[int(t)]):
                 bad = np.nonzero(hops[m] != exp[int(t)])[0][:8]

@@ -2,7 +2,7 @@
 wave writing a run of level-d nodes and then all their children from the
 rows it holds in LDS -- against the restatement
 (oracle/psoracle.c) and against one k_pull launch per round
-(PSAMD_PULL_PAIR=0, read at engine creation).
+(ps_plan_opts.chain_max = 1).
 
 Round q delivers to BFS level q - s of each topic: a node receives its
 parent's row of round q - 1 if the parent was reached this window and the
@@ -50,11 +50,9 @@ def oracle_hops(topics, live):
 
 def run(monkeypatch, pair, n, topics, live, msg_topics, starts=None, record=True, flood=False, flags=0,
         msg_window=65536):
-    monkeypatch.setenv("PSAMD_PULL_PAIR", "1" if pair else "0")
-    monkeypatch.setenv("PSAMD_CHAIN", "2")  # pairs only (k_pull_chain: test_gpu_chain.py)
-    monkeypatch.setenv("PSAMD_FLOOD", "1" if flood else "0")
-    monkeypatch.delenv("PSAMD_FLOOD_TOP_BYTES", raising=False)
-    with PE.Engine(n, len(topics), record_hops=record, flags=flags, msg_window=msg_window) as eng:
+    # pairs only (chain_max 2; k_pull_chain: test_gpu_chain.py), or one k_pull per round
+    opts = {"chain_max": 2 if pair else 1, "chain_max_groups": 2 if pair else 1, "flood": int(flood)}
+    with PE.Engine(n, len(topics), record_hops=record, flags=flags, msg_window=msg_window, plan=opts) as eng:
         for t, (root, parent) in enumerate(topics):
             eng.set_tree(t, root, parent)
         eng.set_live(live)
@@ -134,13 +132,12 @@ def test_pair_after_flood(monkeypatch, seed):
         return w + (w & 1) if w >= 16 else w
     top = sum(int((parent == root).sum()) * width(int((msg_topics == t).sum())) * 8
               for t, (root, parent) in enumerate(topics))
-    monkeypatch.setenv("PSAMD_FLOOD_TOP_BYTES", str(top))
-    monkeypatch.setenv("PSAMD_CHAIN", "2")
-    monkeypatch.setenv("PSAMD_OVERLAP", "0")  # (deep windows plan no k_flood otherwise)
     outs = []
     for pair in (False, True):
-        monkeypatch.setenv("PSAMD_PULL_PAIR", "1" if pair else "0")
-        with PE.Engine(n, len(topics), record_hops=True) as eng:
+        # (overlap 0: deep windows plan no k_flood otherwise)
+        opts = {"flood_top_bytes": top, "chain_max": 2 if pair else 1, "chain_max_groups": 2 if pair else 1,
+                "overlap": 0}
+        with PE.Engine(n, len(topics), record_hops=True, plan=opts) as eng:
             for t, (root, parent) in enumerate(topics):
                 eng.set_tree(t, root, parent)
             eng.set_live(live)
@@ -270,12 +267,10 @@ def test_pair_many_windows_and_drains(monkeypatch):
     starts = rng.integers(0, 4, size=1500).astype(np.uint32)
     exp = oracle_hops(topics, live)
     peers = [int(p) for p in rng.integers(0, n, size=12)]
-    monkeypatch.setenv("PSAMD_CHAIN", "2")
     outs = []
     for pair in (False, True):
-        monkeypatch.setenv("PSAMD_PULL_PAIR", "1" if pair else "0")
-        monkeypatch.setenv("PSAMD_FLOOD", "0")
-        with PE.Engine(n, len(topics), record_hops=True, msg_window=128) as eng:
+        opts = {"chain_max": 2 if pair else 1, "chain_max_groups": 2 if pair else 1, "flood": 0}
+        with PE.Engine(n, len(topics), record_hops=True, msg_window=128, plan=opts) as eng:
             for t, (root, parent) in enumerate(topics):
                 eng.set_tree(t, root, parent)
             eng.set_live(live)

@@ -302,18 +302,18 @@ def build(world, partition, n=1500, n_topics=2, seed=0, fan=None):
 @pytest.mark.parametrize("staggered", [False, True])
 @pytest.mark.parametrize("world,partition", [(1, PE.PART_PEER), (2, PE.PART_PEER), (3, PE.PART_PEER),
                                              (4, PE.PART_SUBTREE), (4, PE.PART_PEER)])
-def test_plans_replay_to_the_oracle(monkeypatch, world, partition, staggered, chain):
-    """PSAMD_CHAIN (read at engine creation): 2 = round pairs,
-    4 = chains of up to four rounds where nothing is exchanged inside (and
-    no k_flood launch for the leading rounds, so the chains start at round 1)."""
-    monkeypatch.setenv("PSAMD_CHAIN", str(chain))
+def test_plans_replay_to_the_oracle(world, partition, staggered, chain):
+    """ps_plan_opts.chain_max: 2 = round pairs, 4 = chains of up to four
+    rounds where nothing is exchanged inside (and no k_flood launch for the
+    leading rounds, so the chains start at round 1)."""
+    opts = {"chain_max": chain, "chain_max_groups": chain}
     if chain > 2:
-        monkeypatch.setenv("PSAMD_FLOOD", "0")
+        opts["flood"] = 0
     rng, trees, roots, live = build(world, partition, seed=world * 7 + partition + 3 * staggered, fan=4)
     n_msgs = 300
     topics = rng.integers(0, len(trees), size=n_msgs)
     starts = rng.integers(0, 4, size=n_msgs) if staggered else None
-    plans = [PL.Plan(np.stack(trees), roots, world, r, partition) for r in range(world)]
+    plans = [PL.Plan(np.stack(trees), roots, world, r, partition, plan=opts) for r in range(world)]
     for p in plans:
         p.window(topics, starts)
     info = [p.info() for p in plans]
@@ -459,17 +459,15 @@ def test_gloo_world2_replays_the_plans(staggered):
 
 
 @pytest.mark.parametrize("chain", [2, 4])
-def test_wide_rows_plan(monkeypatch, chain):
+def test_wide_rows_plan(chain):
     """Rows wider than the 768-word LDS stage (52,000 messages of one topic in
-    a window: 814 words): they cannot pair, so with pairs only (PSAMD_CHAIN=2)
+    a window: 814 words): they cannot pair, so with pairs only (chain_max 2)
     those rounds get one k_pull launch each; chains cut the rows into column
     slices of the stage width, in the launch's slice segment, and the replay
     still tiles every row exactly (VERDICT r2 weak #8)."""
-    monkeypatch.setenv("PSAMD_CHAIN", str(chain))
-    monkeypatch.setenv("PSAMD_FLOOD", "0")
     rng, trees, roots, live = build(1, PE.PART_PEER, n=1200, n_topics=1, seed=5, fan=3)
     topics = np.zeros(52000, dtype=np.uint32)
-    p = PL.Plan(np.stack(trees), roots)
+    p = PL.Plan(np.stack(trees), roots, plan={"chain_max": chain, "chain_max_groups": chain, "flood": 0})
     p.window(topics)
     assert p.layout(0)["W"] == 814
     kinds = [int(k) for k in p.get(PL.ROUND_KIND)]
@@ -490,20 +488,20 @@ def test_wide_rows_plan(monkeypatch, chain):
 
 
 @pytest.mark.parametrize("overlap", [0, 1])
-def test_deep_window_plan(monkeypatch, overlap):
+def test_deep_window_plan(overlap):
     """A deep single-start window (>= 12 rounds) plans chains from round 1 and
-    no k_flood while the cross-window overlap is on; the
-    chain that ends at the last round may take one round more than chain_max
-    (PSAMD_CHAIN_TAIL).  With the overlap off, k_flood takes the leading
+    no k_flood while the cross-window overlap is on (this
+    window's 2.3 MB of rows pass the byte floor only with it lowered to 0);
+    the chain that ends at the last round may take one round more than
+    chain_max (chain_tail).  With the overlap off, k_flood takes the leading
     rounds again.  Either plan replays to the oracle."""
-    monkeypatch.setenv("PSAMD_OVERLAP", str(overlap))
     rng = np.random.default_rng(17)
     n = 6000
     parent = np.full(n, NONE, dtype=np.uint32)
     parent[1:] = (np.arange(1, n) - 1) // 2  # a complete binary tree: 13 levels
     live = (rng.random(n) > 0.05).astype(np.uint8)
     live[0] = 1
-    p = PL.Plan(parent[None, :], [0])
+    p = PL.Plan(parent[None, :], [0], plan={"overlap": overlap, "overlap_min_bytes": 0})
     p.window(np.zeros(3000, dtype=np.uint32))
     kinds = [int(k) for k in p.get(PL.ROUND_KIND)]
     rounds = p.info()["rounds"]
@@ -518,3 +516,72 @@ def test_deep_window_plan(monkeypatch, overlap):
     sims = [RankSim(p, live)]
     emulate(sims, rounds, in_process_exchange(sims))
     check(sims, [parent], [0], live, [1])
+
+
+def test_small_deep_window_keeps_flood():
+    """A deep window below the overlap byte floor (512 MB of rows by default)
+    can never overlap its predecessor, so it keeps the latency-optimal k_flood
+    for its leading rounds instead of the deep-window chains."""
+    n = 6000
+    parent = np.full(n, NONE, dtype=np.uint32)
+    parent[1:] = (np.arange(1, n) - 1) // 2  # 13 levels
+    p = PL.Plan(parent[None, :], [0])
+    assert p.set_plan()["overlap"] == 1  # (the default)
+    p.window(np.zeros(3000, dtype=np.uint32))
+    kinds = [int(k) for k in p.get(PL.ROUND_KIND)]
+    assert kinds[1] == PE.K_FLOOD, kinds
+
+
+def test_wide_rows_past_u16_columns():
+    """Rows wider than 65,535 words (msg_window above 4.19M messages): the
+    chain chunks' column offsets w0 are 32-bit (a u16 w0 wrapped
+    and the slices rewrote the wrong columns).  Every slice of a 66,600-word
+    row keeps its true offset and the slices tile the row exactly."""
+    n = 40
+    parent = np.full(n, NONE, dtype=np.uint32)
+    parent[1:] = (np.arange(1, n) - 1) // 3
+    p = PL.Plan(parent[None, :], [0], plan={"flood": 0, "chain_max": 4})
+    p.set_msg_window(66600 * 64)
+    p.window(np.zeros(66600 * 64 - 10, dtype=np.uint32))
+    W = p.layout(0)["W"]
+    assert W == 66600, W
+    kinds = [int(k) for k in p.get(PL.ROUND_KIND)]
+    assert PE.K_CHAIN in kinds, kinds
+    for q in range(1, p.info()["rounds"] + 1):
+        n_r, ch = p.chain(q)
+        by_run = {}
+        for c in ch:
+            by_run.setdefault(c["node_begin"], []).append((c["w0"], c["S"]))
+        for cols in by_run.values():
+            cols.sort()
+            assert cols[0][0] == 0 and cols[-1][0] > 65535, cols[-3:]
+            for (a, sa), (b, _) in zip(cols, cols[1:]):
+                assert a + sa == b
+            assert cols[-1][0] + cols[-1][1] == W
+
+
+def test_plan_opts_defaults_pinned():
+    """The production plan is pinned by ps_plan_opts defaults, not by the
+    environment: a stray PSAMD_* variable changes nothing unless the A/B
+    switch PSAMD_AB=1 is set too."""
+    d = PE.default_plan_opts()
+    assert d == {"flood_top_bytes": 4 << 20, "overlap_min_bytes": 512 << 20, "launch_bytes": 16_000_000,
+                 "flood": 1, "chain_max": 4, "chain_max_groups": 6, "chain_tail": 1, "chain_words": 8192,
+                 "flood_words": 2048, "pad_words": 16, "overlap": 1, "overlap_min_rounds": 12,
+                 "xchg_overlap": -1, "gpu_build": 1, "flood_spin_ticks": 200_000_000}, d
+    parent = np.full(64, NONE, dtype=np.uint32)
+    parent[1:] = (np.arange(1, 64) - 1) // 2
+    env = dict(os.environ)
+    try:
+        os.environ["PSAMD_CHAIN"] = "2"
+        os.environ["PSAMD_FLOOD"] = "0"
+        os.environ.pop("PSAMD_AB", None)
+        assert PL.Plan(parent[None, :], [0]).set_plan() == {**d, "gpu_build": 0}  # ignored (a probe builds on the host)
+        os.environ["PSAMD_AB"] = "1"
+        ab = PL.Plan(parent[None, :], [0]).set_plan()
+        assert ab["chain_max"] == 2 and ab["flood"] == 0  # the A/B tools' override
+    finally:
+        os.environ.clear()
+        os.environ.update(env)
+    with pytest.raises(PE.EngineError):
+        PL.Plan(parent[None, :], [0]).set_plan(chain_max=7)

@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # Chain parity tests, then the chain-length A/B (PSAMD_CHAIN = 2 pairs, 3, 4, 6) on cfg3 / cfg4 / cfg2.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"

@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # Full GPU suite on the chain default, then chain tuning A/B: compact LDS (20 waves/CU)
 # and the per-wave row-word target, on cfg3 / cfg4.
 set -euo pipefail

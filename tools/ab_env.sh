@@ -1,3 +1,4 @@
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # A/B of engine environment switches on the cfg3 bench (no tests):
 #   VARIANTS="A=1,B=2 C=3" bash tools/ab_env.sh <tag> [bench args]
 set -euo pipefail

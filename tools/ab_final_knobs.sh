@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # Last knob sweep on the final tree: chain length, chain run size, deep-window floor for cfg4.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"

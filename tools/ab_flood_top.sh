@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # The k_flood / multi-round-launch split (PSAMD_FLOOD_TOP_BYTES) with chains, cfg2 / cfg3 / cfg4.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"

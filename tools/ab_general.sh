@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # General path (start rounds 0..7) by the longest launch (PSAMD_CHAIN 2/4/6).
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"

@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # The planner's launch cost (PSAMD_LAUNCH_BYTES: a launch's ramp and tail as row bytes):
 # cfg3 plans 3+4+4+1 rounds at 16 MB, 4+4+4 at 128 MB.
 set -euo pipefail

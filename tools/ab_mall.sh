@@ -1,3 +1,4 @@
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # A/B: alternating chunk direction (PSAMD_REVERSE) x phase-B store policy (PSAMD_NT_BYTES) on cfg3 / cfg4
 set -e
 cd $GRAFT_REPO_ROOT

@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # Chains from round 1 instead of k_flood for the leading rounds (PSAMD_FLOOD=0), smaller top splits.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"

@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # Row padding to an even word count from PSAMD_PAD_WORDS words (16-B stores): cfg3 and the
 # 4-rank loopback (63-word rows), then the per-launch sweep.
 set -euo pipefail

@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # A chain ending at the window's last round may take one round more (PSAMD_CHAIN_TAIL): cfg3 A/B, chain tests.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"

@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # Bench A/B over environment settings (one bench run each, no CPU leg).
 #   tools/env_sweep.sh <tag> "<VAR=val[,VAR2=val2]> ..." [bench args]
 set -euo pipefail

@@ -24,6 +24,10 @@ sys.path.insert(0, os.path.join(REPO, "go-libp2p-pubsub_amd"))
 sys.path.insert(0, os.path.join(REPO, "oracle"))
 
 import oracle as O  # noqa: E402
+
+# the fuzzer draws plan options through the environment (read at ps_create
+# only with the A/B switch on)
+os.environ["PSAMD_AB"] = "1"
 import psengine as PE  # noqa: E402
 
 

@@ -1,3 +1,4 @@
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # k_pull_pair A/B: parity tests under both LDS stage sizes, then the cfg3
 # bench with pairs (1024- and 512-word stages) and without
 set -euo pipefail

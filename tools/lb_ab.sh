@@ -1,3 +1,4 @@
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # A/B of the multi-rank exchange overlap on the 4-rank cfg4 loopback (peer hash)
 set -e
 cd $GRAFT_REPO_ROOT

@@ -1,3 +1,4 @@
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 set -e
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/lb

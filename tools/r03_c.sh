@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # Flood split at 4 MB: GPU suite, driver bench command, cfg2; cfg5 kernel trace.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"

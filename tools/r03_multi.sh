@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # Round-3 GPU session: the 4-rank loopback exchange (overlap on/off, both
 # partitions, staggered), its kernel trace, cfg5 host timing, and the MALL
 # A/B (chunk direction x phase-B store policy).  Every GPU step under its own

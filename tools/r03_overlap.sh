@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # Cross-window overlap: async tests, full GPU suite, cfg3 bench with and without, per-launch timing.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"

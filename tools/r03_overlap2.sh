@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # Window-init overlap for every pipelined tree window + reduce on its own stream: tests and benches.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"

@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # Zero-copy loopback exchange: multi-rank parity, then the 4-rank loopback benches and a trace.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"

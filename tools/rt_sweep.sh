@@ -1,4 +1,5 @@
 #!/bin/bash
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 # Per-launch device times (tools/round_timing.py) under planner switches.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"

@@ -1,3 +1,4 @@
+export PSAMD_AB=1  # plan options from the environment (A/B tools only)
 set -euo pipefail
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/xlds; mkdir -p $O
