@@ -125,6 +125,14 @@ __device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic&
       p = a.node_parent[nb + j];
       f = a.node_flags[nb + j];
     }
+    // lane 0: the previous node's parent (and ghost reference), issued with
+    // the group's own loads -- not a second round trip after them
+    const uint32_t q = nb + j0;
+    uint32_t pm = kNoneNode, gm = kNoneNode;
+    if (lane == 0 && q > P.nbase) {
+      pm = a.node_parent[q - 1];
+      if (gin != kNoneNode) gm = a.ghost_ref[q - 1];
+    }
     bool up = false;  // the parent was reached this window
     uint64_t row = 0;
     uint32_t pid = p;  // the parent's identity for the once-per-parent count
@@ -144,15 +152,7 @@ __device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic&
       }
     }
     uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(pid), 1, 64));
-    if (lane == 0) {
-      prev = kNoneNode;
-      const uint32_t q = nb + j0;
-      if (q > P.nbase) {
-        prev = a.node_parent[q - 1];
-        if (prev == kNoneNode && gin != kNoneNode && a.ghost_ref[q - 1] != kNoneNode)
-          prev = 0x80000000u | a.ghost_ref[q - 1];
-      }
-    }
+    if (lane == 0) prev = pm != kNoneNode ? pm : gm != kNoneNode ? 0x80000000u | gm : kNoneNode;
     const bool ok = up && (f & kNodeLive);
     if (in) src[j] = ok ? row : 0ull;
     if (ok) a.gen[nb + j] = static_cast<uint8_t>(cur);
@@ -915,46 +915,151 @@ __device__ __forceinline__ void stage_stream(const PullArgs& a, uint64_t* out, u
   }
 }
 
-// One sub-run of level k: the nodes [y0, y0 + nk) (<= kChainKids), whose
-// parents lie in the level above, [x0, ...) with level table `up_tab`.  Each
-// node's stage offset into ctab (kZero: zeros) and its own table entry
-// into `tab` (indexed from the level's first node, y0 - lo); generations
-// stamped and nodes counted by the slice-0 wave.  pf_p / pf_f: the sub-run's
-// parent ids and flags when prefetched (null: loaded here).
-template <uint32_t kZero>
-__device__ __forceinline__ void chain_resolve(const PullArgs& a, const ChainStep& C, uint32_t x0,
-                                              const uint8_t* up_tab, uint32_t y0, uint32_t nk, uint32_t* ctab,
-                                              uint8_t* tab, uint32_t lane, uint32_t cur, const uint32_t* pf_p,
-                                              const uint32_t* pf_f, WaveCtr& c) {
-#pragma unroll
-  for (uint32_t s = 0; s < kChainKids / 64; ++s) {
-    const uint32_t j0 = s * 64;
-    if (j0 >= nk) break;
-    const uint32_t j = j0 + lane;
-    const bool in = j < nk;
-    uint32_t p = kNoneNode, f = 0;
-    if (pf_p) {
-      p = in ? pf_p[s] : kNoneNode;
-      f = pf_f[s];
-    } else if (in) {
-      p = a.node_parent[y0 + j];
-      f = a.node_flags[y0 + j];
-    }
-    const uint8_t src = in ? up_tab[p - x0] : kChainNone;  // the parent's stage slot
-    const bool up = in && ((a.all_current & 1u) || src != kChainNone);
-    const bool ok = up && (f & kNodeLive);
-    if (in) {
-      ctab[j] = (ok && src < kChainZero) ? static_cast<uint32_t>(src) * C.S : kZero;
-      tab[j] = ok ? (src < kChainZero ? src : kChainZero) : kChainNone;
-    }
-    if (ok && C.slice0) a.gen[y0 + j] = static_cast<uint8_t>(cur);
-    uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(p), 1, 64));
-    if (lane == 0) prev = y0 + j0 > C.nbase ? a.node_parent[y0 + j0 - 1] : kNoneNode;
-    // nodes and parents counted once per run (slice 0); words per slice (the
-    // parents' rows come from LDS: no parent words read)
-    ctr_nodes(c, in && C.slice0, ok && C.slice0, up && p != prev && C.slice0, C.S, 0u);
-    if (!C.slice0) c.sw += static_cast<uint64_t>(__popcll(__ballot(ok))) * C.S;
+// Levels 1 .. levels - 1 of a chain chunk, as metadata preloaded into
+// registers: per node its parent's index in the level above (relative to that
+// level's first node, < kChainCap) and its live flag, in 16 bits, two nodes
+// per register -- kMetaSlots slots of 64 nodes per batch, the levels one
+// after the other, each from a slot boundary.  The first batch is issued at
+// the wave's start, beside level 0's loads, so the level loop issues no
+// global load at all: gfx950 counts loads and stores on one in-order counter
+// (vmcnt), and a load issued behind a level's row stores could be consumed
+// only once those stores had drained -- which the previous form (each
+// sub-run's ids loaded before the sub-run above streamed, and a per-group
+// load of the previous node's parent for the counters) paid at every level
+// (profiles/r04/chain_prof_*: 5 us fixed + 4.9 us per 8-KB row-kword per wave).
+constexpr uint32_t kMetaSlots = 16;      // 64-node slots per batch: 1,024 nodes
+constexpr int kWaitVmcnt0 = 0x0F70;      // s_waitcnt vmcnt(0) expcnt(7) lgkmcnt(15) (gfx9 encoding)
+constexpr uint32_t kMetaNone = 0xFFFFu;  // no node at the lane's position
+constexpr uint32_t kMetaLive = 0x4000u;  // the node is live (below: the parent's index)
+struct ChainMeta {
+  uint32_t w[kMetaSlots / 2];  // slot i in half i & 1 of w[i / 2]
+  uint32_t g0;                 // the batch's first global slot
+};
+
+// Walks the metadata slots (64 nodes of levels >= 1, each level from a slot
+// boundary) level by level: the level k of slot g, its first slot kb, its
+// slot count ns, its node range [lo, hi) and the first node plo of the level
+// above.  Wave-uniform; no loop per slot, so the callers' slot loops unroll.
+// (A level with no node ends the walk: every deeper level is empty too.)
+struct MetaCursor {
+  uint32_t k, kb, ns, lo, hi, plo;
+  __device__ __forceinline__ void enter(const ChainChunk* cp, uint32_t levels) {
+    if (k >= levels) return;
+    plo = lo;
+    lo = __builtin_amdgcn_readfirstlane(cp->lo[k]);
+    hi = __builtin_amdgcn_readfirstlane(cp->hi[k]);
+    ns = (hi - lo + 63) >> 6;
+    if (ns == 0) k = levels;
   }
+  // the cursor at slot g0
+  __device__ __forceinline__ void start(const ChainChunk* cp, uint32_t levels, uint32_t g0) {
+    k = 1;
+    kb = 0;
+    lo = __builtin_amdgcn_readfirstlane(cp->lo[0]);
+    enter(cp, levels);
+    while (k < levels && g0 >= kb + ns) {
+      kb += ns;
+      ++k;
+      enter(cp, levels);
+    }
+  }
+  // the cursor at slot g (g = the previous slot + 1)
+  __device__ __forceinline__ void step(const ChainChunk* cp, uint32_t levels, uint32_t g) {
+    if (k < levels && g >= kb + ns) {
+      kb += ns;
+      ++k;
+      enter(cp, levels);
+    }
+  }
+};
+
+// Issues the batch of slots g0 .. g0 + kMetaSlots - 1: raw parent ids and
+// flag dwords into p / f (unconsumed, so nothing waits here).
+__device__ __forceinline__ void chain_meta_issue(const PullArgs& a, const ChainChunk* cp, uint32_t levels,
+                                                 uint32_t g0, uint32_t lane, uint32_t (&p)[kMetaSlots],
+                                                 uint32_t (&f)[kMetaSlots]) {
+  MetaCursor m;
+  m.start(cp, levels, g0);
+#pragma unroll
+  for (uint32_t i = 0; i < kMetaSlots; ++i) {
+    if (i) m.step(cp, levels, g0 + i);
+    if (m.k >= levels) break;  // (past the chunk's last level: no loads)
+    const uint32_t y = m.lo + (g0 + i - m.kb) * 64 + lane;
+    const uint32_t ys = y < m.hi ? y : 0u;  // (clamped: node 0 exists)
+    p[i] = a.node_parent[ys];
+    // the flag byte's aligned dword (a byte load's zero extension would
+    // consume it here; node_flags is padded past n_pad)
+    f[i] = reinterpret_cast<const uint32_t*>(a.node_flags)[ys >> 2];
+  }
+}
+
+// Packs the issued batch (the first use of p / f: the loads' wait).
+__device__ __forceinline__ void chain_meta_pack(const ChainChunk* cp, uint32_t levels, uint32_t g0, uint32_t lane,
+                                                const uint32_t (&p)[kMetaSlots], const uint32_t (&f)[kMetaSlots],
+                                                ChainMeta& M) {
+  M.g0 = g0;
+  MetaCursor m;
+  m.start(cp, levels, g0);
+#pragma unroll
+  for (uint32_t i = 0; i < kMetaSlots; ++i) {
+    if (i) m.step(cp, levels, g0 + i);
+    if (m.k >= levels) break;  // (the slots past it are never picked)
+    const uint32_t y = m.lo + (g0 + i - m.kb) * 64 + lane;
+    const uint32_t e = y < m.hi
+                           ? (p[i] - m.plo) | (((f[i] >> (8 * (y & 3))) & kNodeLive) ? kMetaLive : 0u)
+                           : kMetaNone;
+    if (i & 1)
+      M.w[i / 2] |= e << 16;
+    else
+      M.w[i / 2] = e;
+  }
+  // every batch load has landed (slots past the chunk's last level are never
+  // consumed): without this the waitcnt pass keeps them pending across the
+  // level loop and drains the row stores at its head
+  __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
+}
+
+// The lane's entry of batch slot i (wave-uniform i < kMetaSlots): a select
+// chain over the registers (no dynamic register index).
+__device__ __forceinline__ uint32_t chain_meta_pick(const ChainMeta& M, uint32_t i) {
+  uint32_t w = M.w[0];
+#pragma unroll
+  for (uint32_t r = 1; r < kMetaSlots / 2; ++r) {
+    uint32_t t = M.w[r];
+    asm volatile("" : "+v"(t));  // (a register value: keeps the chain from becoming an indexed scratch load)
+    w = (i >> 1) == r ? t : w;
+  }
+  return (i & 1) ? w >> 16 : w & 0xFFFFu;
+}
+
+// One group of 64 nodes of level k (entry e per lane; j = the lane's index
+// in the sub-run, y its node): the node's stage offset into ctab (kZero:
+// zeros) and its own level-table entry into tab; generation stamped and nodes
+// counted by the slice-0 wave.  carry: the parent index of the group's last
+// node, for the next group's first (a parent counts once, at its first
+// child; kNoneNode at a level's start: no parent spans two chunks).
+template <uint32_t kZero>
+__device__ __forceinline__ void chain_group(const PullArgs& a, const ChainStep& C, uint32_t e, const uint8_t* up_tab,
+                                            uint32_t y, uint32_t j, uint32_t* ctab, uint8_t* tab, uint32_t cur,
+                                            uint32_t lane, uint32_t& carry, WaveCtr& c) {
+  const bool in = e != kMetaNone;
+  const uint32_t rel = e & (kMetaLive - 1);
+  const uint8_t src = in ? up_tab[rel] : kChainNone;  // the parent's stage slot
+  const bool up = in && ((a.all_current & 1u) || src != kChainNone);
+  const bool ok = up && (e & kMetaLive);
+  if (in) {
+    ctab[j] = (ok && src < kChainZero) ? static_cast<uint32_t>(src) * C.S : kZero;
+    tab[j] = ok ? (src < kChainZero ? src : kChainZero) : kChainNone;
+  }
+  if (ok && C.slice0) a.gen[y] = static_cast<uint8_t>(cur);
+  const uint32_t mine = in ? rel : kNoneNode;
+  uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(mine), 1, 64));
+  if (lane == 0) prev = carry;
+  carry = __builtin_amdgcn_readlane(mine, 63);
+  // nodes and parents counted once per run (slice 0); words per slice (the
+  // parents' rows come from LDS: no parent words read)
+  ctr_nodes(c, in && C.slice0, ok && C.slice0, up && rel != prev && C.slice0, C.S, 0u);
+  if (!C.slice0) c.sw += static_cast<uint64_t>(__popcll(__ballot(ok))) * C.S;
 }
 
 // The partial slots of round r0 + k of a chain launch (a switch: no dynamic
@@ -1054,18 +1159,13 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
   C.slice0 = C.w0 == 0;
   const uint32_t n0 = node_end - node_begin;  // <= kChainPar, n0 * S <= kStage (host plan)
   const uint64_t slot = blockIdx.x % a.slot_mod;
-  // level 1's first sub-run: parent ids and flags issued with level 0's metadata
-  uint32_t pf_p[kChainKids / 64], pf_f[kChainKids / 64];
-  const uint32_t lo1 = cp->lo[1];
-  const uint32_t nk1 = levels > 1 ? min(kChainKids, cp->hi[1] - lo1) : 0u;
-#pragma unroll
-  for (uint32_t s = 0; s < kChainKids / 64; ++s) {
-    const uint32_t j = s * 64 + lane;
-    pf_p[s] = j < nk1 ? a.node_parent[lo1 + j] : kNoneNode;
-    pf_f[s] = j < nk1 ? a.node_flags[lo1 + j] : 0u;
-  }
-  // level 0: the run, parents' rows (slices) from HBM
+  // levels 1 ..: the first metadata batch, issued before level 0's loads
+  // (one round trip for both); packed once level 0's sources are resolved
+  ChainMeta M;
   {
+    uint32_t mp[kMetaSlots], mf[kMetaSlots];
+    if (levels > 1) chain_meta_issue(a, cp, levels, 0u, lane, mp, mf);
+    // level 0: the run, parents' rows (slices) from HBM
     PullTopic P;
     P.W = C.W;
     P.nbase = T.nbase;
@@ -1074,12 +1174,14 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
     WaveCtr c;
     if constexpr (!kSlices) {
       pull_resolve(a, P, node_begin, n0, p_lo, p_hi, src, genl, lane, cur, c, kNoneNode, kChainPar);
+      if (levels > 1) chain_meta_pack(cp, levels, 0u, lane, mp, mf, M);
       pull_stream<kRecord, true, true>(a, P, node_begin, n0, src, lane, round + r0, c, stage);
     } else {
       // (pull_resolve stamps generations and counts whole rows: slice 0 keeps
       // its node counts, every slice its own words)
       PullCtr pc;
       pull_resolve(a, P, node_begin, n0, p_lo, p_hi, src, genl, lane, cur, pc, kNoneNode, kChainPar);
+      if (levels > 1) chain_meta_pack(cp, levels, 0u, lane, mp, mf, M);
       const uint32_t nodes = __reduce_add_sync(~0ull, pc.kids), hit = __reduce_add_sync(~0ull, pc.reached);
       const uint32_t par = __reduce_add_sync(~0ull, pc.parents);
       if (C.slice0) {
@@ -1103,57 +1205,47 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
   // src (level 0's sources) is dead from here and its LDS becomes ctab: no
   // memory access may move across the switch from one view to the other
   asm volatile("" ::: "memory");
-  // levels 1 .. levels - 1, sub-run by sub-run; each sub-run's parent ids
-  // and flags were loaded before the previous sub-run's stream (pf_p / pf_f),
-  // so a level costs no round trip of its own
-  uint32_t x0 = node_begin;
-  uint32_t k = 1;
-  uint32_t lo = lo1, hi = levels > 1 ? __builtin_amdgcn_readfirstlane(cp->hi[1]) : lo1;
-  uint32_t y0 = lo;
-  WaveCtr c;
-  while (k < levels) {
-    if (y0 >= hi) {  // level k done
-      words_out += c.sw;
-      chain_flush(c, chain_slots(a, r0 + k), slot, lane);
-      asm volatile("" ::: "memory");
-      x0 = lo;
-      if (++k >= levels) break;
-      lo = __builtin_amdgcn_readfirstlane(cp->lo[k]);
-      hi = __builtin_amdgcn_readfirstlane(cp->hi[k]);
-      y0 = lo;
-      continue;
-    }
-    const uint32_t nk = min(kChainKids, hi - y0);
-    chain_resolve<kStage>(a, C, x0, tabs[(k - 1) & 1], y0, nk, ctab, tabs[k & 1] + (y0 - lo), lane, cur, pf_p,
-                          pf_f, c);
-    // the next sub-run: this level's next, or the next level's first
-    uint32_t n_lo = y0 + kChainKids, n_hi = hi;
-    if (n_lo >= hi) {
-      n_lo = n_hi = 0;
-      if (k + 1 < levels) {
-        n_lo = __builtin_amdgcn_readfirstlane(cp->lo[k + 1]);
-        n_hi = __builtin_amdgcn_readfirstlane(cp->hi[k + 1]);
+  // levels 1 .. levels - 1, sub-run by sub-run (<= kChainKids nodes): every
+  // node's parent and flag come from the preloaded batch, so no level waits
+  // for the stores above it; a batch is reloaded only when a chunk's levels
+  // hold more than kMetaSlots slots (a wait, rare: runs are sized for less)
+  uint32_t g = 0;  // the global metadata slot of the next node group
+  for (uint32_t k = 1; k < levels; ++k) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane(cp->lo[k]), hi = __builtin_amdgcn_readfirstlane(cp->hi[k]);
+    const uint8_t* const up_tab = tabs[(k - 1) & 1];
+    uint32_t carry = kNoneNode;
+    WaveCtr c;
+    for (uint32_t y0 = lo; y0 < hi; y0 += kChainKids) {
+      const uint32_t nk = min(kChainKids, hi - y0);
+      const uint32_t ng = (nk + 63) >> 6;
+      if (g + ng > M.g0 + kMetaSlots) {
+        uint32_t mp[kMetaSlots], mf[kMetaSlots];
+        chain_meta_issue(a, cp, levels, g, lane, mp, mf);
+        chain_meta_pack(cp, levels, g, lane, mp, mf, M);
       }
-    }
-    const uint32_t n_nk = min(kChainKids, n_hi - n_lo);
+      uint8_t* const tab = tabs[k & 1] + (y0 - lo);
 #pragma unroll
-    for (uint32_t s = 0; s < kChainKids / 64; ++s) {
-      const uint32_t j = s * 64 + lane;
-      pf_p[s] = j < n_nk ? a.node_parent[n_lo + j] : kNoneNode;
-      pf_f[s] = j < n_nk ? a.node_flags[n_lo + j] : 0u;
+      for (uint32_t s = 0; s < kChainKids / 64; ++s) {
+        if (s >= ng) break;
+        chain_group<kStage>(a, C, chain_meta_pick(M, g + s - M.g0), up_tab, y0 + s * 64 + lane, s * 64 + lane, ctab,
+                            tab, cur, lane, carry, c);
+      }
+      g += ng;
+      if constexpr (!kSlices) {
+        uint64_t* out = a.seen + C.base + static_cast<uint64_t>(y0) * C.W;
+        if (kNT || k + 1 < levels)  // (only the launch's last level may be re-read soon)
+          stage_stream<kRecord, true, kStage>(a, out, nk, C.W, ctab, stage, lane, round + r0 + k, c);
+        else
+          stage_stream<kRecord, false, kStage>(a, out, nk, C.W, ctab, stage, lane, round + r0 + k, c);
+      } else {
+        chain_stream<kRecord, true, false, kStage>(a, C, y0, nk, ctab, nullptr, stage, kNoneNode, lane,
+                                                   round + r0 + k, c);
+      }
+      ctr_fold(c);
     }
-    if constexpr (!kSlices) {
-      uint64_t* out = a.seen + C.base + static_cast<uint64_t>(y0) * C.W;
-      if (kNT || k + 1 < levels)  // (only the launch's last level may be re-read soon)
-        stage_stream<kRecord, true, kStage>(a, out, nk, C.W, ctab, stage, lane, round + r0 + k, c);
-      else
-        stage_stream<kRecord, false, kStage>(a, out, nk, C.W, ctab, stage, lane, round + r0 + k, c);
-    } else {
-      chain_stream<kRecord, true, false, kStage>(a, C, y0, nk, ctab, nullptr, stage, kNoneNode, lane, round + r0 + k,
-                                                 c);
-    }
-    ctr_fold(c);
-    y0 += kChainKids;
+    words_out += c.sw;
+    chain_flush(c, chain_slots(a, r0 + k), slot, lane);
+    asm volatile("" ::: "memory");
   }
   if (a.prof) {
     // (HW_ID: wave, SIMD, CU, SE bits; XCC_ID[3:0], hwreg 20 on gfx950)

@@ -505,8 +505,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
                     !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS)) && total >= e->overlap_min_bytes;
   if (pcap && !e->pstream) {  // (created on first use: multi-rank engines never need them)
     HIP_TRY(hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking), "prefix stream");
-    HIP_TRY(hipStreamCreateWithFlags(&e->rstream, hipStreamNonBlocking), "reduce stream");
-    for (hipEvent_t* ev : {&e->ev_gate[0], &e->ev_gate[1], &e->ev_pre, &e->ev_end})
+    for (hipEvent_t* ev : {&e->ev_gate[0], &e->ev_gate[1], &e->ev_pre})
       HIP_TRY(hipEventCreateWithFlags(ev, hipEventDisableTiming), "overlap events");
   }
   std::vector<uint64_t> gkey;
@@ -911,7 +910,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     // window's first launches (its partial slots and descriptors are this
     // slot's; ps_wait waits for it through the window's end event)
     hipStream_t rs = s;
-    if (direct && pcap) {
+    if (direct && world == 1) {  // (every pipelined one-rank window: the next one's launches never wait for it)
+      if (!e->rstream) HIP_TRY(hipStreamCreateWithFlags(&e->rstream, hipStreamNonBlocking), "reduce stream");
+      if (!e->ev_end) HIP_TRY(hipEventCreateWithFlags(&e->ev_end, hipEventDisableTiming), "reduce event");
       HIP_TRY(hipEventRecord(e->ev_end, s), "event");
       HIP_TRY(hipStreamWaitEvent(e->rstream, e->ev_end, 0), "reduce wait");
       rs = e->rstream;

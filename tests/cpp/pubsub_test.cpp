@@ -5,6 +5,7 @@
 // subscriber receives exactly the published bytes, in order.
 //
 //   tests/cpp/bin/pubsub_test [test-name ...]      (exit 0 = all passed)
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -200,6 +201,109 @@ void TestWireCodec() {
   REQUIRE(pos == stream.size() && readMessage(stream, &pos, &r3), "EOF after two values");
 }
 
+// INTEGRATION.md's cgo shim, call for call, through the C ABI: publish in
+// batches, a run (ps_run) and a delivery to every subscriber
+// (ps_read_peer_messages) whenever a topic's pending messages reach the
+// window, and a final flush.  140,000 messages of one topic (more than two
+// 65,536-message windows): every subscriber yields every message exactly
+// once, in publish order (client.go:26-28,124-128).  Then the same burst as
+// ONE run: ps_read_peer_messages holds only the last window -- the loss the
+// shim's window flush avoids.
+struct Shim {
+  static constexpr uint32_t kWindow = 65536;
+  ps_engine* e = nullptr;
+  std::vector<size_t> pending;  // topic -> messages since the last run
+  struct Sub {
+    uint32_t topic, peer;
+    std::vector<uint32_t> got;  // payload indices, in channel order
+  };
+  std::vector<Sub> subs;
+  std::vector<uint32_t> payload;  // msg id - base -> payload index
+  uint32_t base = 0;
+
+  explicit Shim(uint32_t n_peers) {
+    ps_config cfg{};
+    cfg.n_peers = n_peers;
+    cfg.n_topics = 1;
+    cfg.tree_width = DefaultTreeWidth;
+    cfg.tree_max_width = DefaultTreeMaxWidth;
+    cfg.msg_window = kWindow;
+    REQUIRE(ps_create(&cfg, &e) == PS_OK, "ps_create");
+    pending.assign(1, 0);
+  }
+  ~Shim() { ps_destroy(e); }
+  void flush() {
+    if (pending[0] == 0) return;
+    ps_stats st{};
+    REQUIRE(ps_run(e, &st) == PS_OK, "ps_run: %s", ps_last_error(e));
+    pending.assign(1, 0);
+    std::vector<uint32_t> ids(1024);
+    for (Sub& s : subs) {
+      size_t n = 0;
+      int rc = ps_read_peer_messages(e, s.topic, s.peer, ids.data(), ids.size(), &n);
+      if (rc == PS_E_RANGE && n > ids.size()) {
+        ids.resize(n);
+        rc = ps_read_peer_messages(e, s.topic, s.peer, ids.data(), ids.size(), &n);
+      }
+      REQUIRE(rc == PS_OK, "ps_read_peer_messages: %s", ps_last_error(e));
+      for (size_t k = 0; k < n; ++k) s.got.push_back(payload[ids[k] - base]);
+    }
+  }
+  void publish(uint32_t topic, uint32_t first_payload, size_t count) {
+    while (count) {
+      const size_t k = std::min(count, kWindow - pending[topic]);
+      std::vector<uint32_t> topics(k, topic);
+      uint32_t first = 0;
+      REQUIRE(ps_publish(e, topics.data(), k, &first) == PS_OK, "ps_publish");
+      if (payload.empty()) base = first;
+      for (size_t i = 0; i < k; ++i) {
+        if (first + i - base >= payload.size()) payload.resize(first + i - base + 1);
+        payload[first + i - base] = first_payload + static_cast<uint32_t>(i);
+      }
+      first_payload += static_cast<uint32_t>(k);
+      pending[topic] += k;
+      count -= k;
+      if (pending[topic] == kWindow) flush();
+    }
+  }
+};
+
+void TestShimWindowFlush() {
+  constexpr uint32_t kPeers = 48, kMsgs = 140000, kBatch = 1000;
+  {
+    Shim g(kPeers);
+    REQUIRE(ps_topic_create(g.e, 0, 0, 0, 0) == PS_OK, "ps_topic_create");
+    for (uint32_t p = 1; p < kPeers; ++p) {
+      int32_t st = 0;
+      REQUIRE(ps_topic_join(g.e, 0, &p, 1, &st) == PS_OK && st == PS_OK, "join %u", p);
+      g.subs.push_back(Shim::Sub{0, p, {}});
+    }
+    for (uint32_t i = 0; i < kMsgs; i += kBatch) g.publish(0, i, kBatch);
+    g.flush();
+    for (const auto& s : g.subs) {
+      REQUIRE(s.got.size() == kMsgs, "peer %u yielded %zu of %u messages", s.peer, s.got.size(), kMsgs);
+      for (uint32_t i = 0; i < kMsgs; ++i) REQUIRE(s.got[i] == i, "peer %u: message %u out of order", s.peer, i);
+    }
+  }
+  {  // one unflushed run of the same burst: only its last window is readable
+    Shim g(kPeers);
+    REQUIRE(ps_topic_create(g.e, 0, 0, 0, 0) == PS_OK, "ps_topic_create");
+    for (uint32_t p = 1; p < kPeers; ++p) {
+      int32_t st = 0;
+      ps_topic_join(g.e, 0, &p, 1, &st);
+    }
+    std::vector<uint32_t> topics(kMsgs, 0);
+    uint32_t first = 0;
+    REQUIRE(ps_publish(g.e, topics.data(), kMsgs, &first) == PS_OK, "ps_publish");
+    ps_stats st{};
+    REQUIRE(ps_run(g.e, &st) == PS_OK && st.windows == 3, "ps_run");
+    std::vector<uint32_t> ids(kMsgs);
+    size_t n = 0;
+    REQUIRE(ps_read_peer_messages(g.e, 0, 7, ids.data(), ids.size(), &n) == PS_OK, "read");
+    REQUIRE(n == kMsgs - 2 * Shim::kWindow && ids[0] == first + 2 * Shim::kWindow, "last window only: %zu", n);
+  }
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -212,6 +316,7 @@ int main(int argc, char** argv) {
       {"TestPaced1000", TestPaced1000},
       {"TestBurstOrder", TestBurstOrder},
       {"TestTwoTopics", TestTwoTopics},
+      {"TestShimWindowFlush", TestShimWindowFlush},
   };
   int failed = 0, ran = 0;
   for (const auto& t : tests) {

@@ -1,6 +1,7 @@
 """GPU: the reference's own tests (pubsub_test.go: TestBasicPubsub,
 TestNodesDropping, TestLowerNodesDropping, TestNodesDroppingGracefully) plus
-a paced 1000-message run, a burst, two topics and the wire codec, written
+a paced 1000-message run, a burst, two topics, the wire codec and
+INTEGRATION.md's cgo shim sequence over more than two message windows, written
 against the C++ mirror of the reference API (include/pubsub.hpp) and run as
 one native binary (tests/cpp/pubsub_test.cpp) whose floods go through
 libpsengine.so on the GPU.  Same skip sets and assertions as the reference.
@@ -14,7 +15,7 @@ from psengine import _build
 pytestmark = pytest.mark.gpu
 
 TESTS = ["TestWireCodec", "TestBasicPubsub", "TestNodesDropping", "TestLowerNodesDropping",
-         "TestNodesDroppingGracefully", "TestPaced1000", "TestBurstOrder", "TestTwoTopics"]
+         "TestNodesDroppingGracefully", "TestPaced1000", "TestBurstOrder", "TestTwoTopics", "TestShimWindowFlush"]
 
 
 @pytest.fixture(scope="module")

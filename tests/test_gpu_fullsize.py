@@ -1,6 +1,8 @@
 """GPU: BASELINE cfg2 and cfg4 at FULL size against the restatement with a
 dead mask -- the single-rank production instance, and cfg4 (16,777,216 peers)
-hash-sharded over two loopback ranks under PS_PART_PEER.
+hash-sharded over 2, 4 and 8 loopback ranks under PS_PART_PEER, the north
+star's 8-way split included, through the
+zero-copy exchange and the RCCL-shaped copy path (PS_DIST_F_COPY).
 
 A dead peer stops forwarding (subtree.go:324-337, the dead-child skip at
 :326-331), so its subtree is cut: ~2 % dead peers, including a child of the
@@ -108,18 +110,21 @@ def test_cfg4_full_size_dead_mask_single_rank(cfg4_tree):
 cfg4_tree_digest = [None]
 
 
-def test_cfg4_full_size_two_ranks_peer_hash(cfg4_tree):
-    """cfg4 at full size hash-sharded over 2 loopback ranks (owner(p) =
-    splitmix64(p) mod 2, SURVEY.md §8e): every round ships ghost parent rows;
-    deliveries, histogram, sampled delivered sets (union over the ranks) and
-    the digest sum against the oracle and the single engine."""
+@pytest.mark.parametrize("world,copy", [(2, False), (2, True), (4, False), (4, True), (8, False), (8, True)])
+def test_cfg4_full_size_ranks_peer_hash(cfg4_tree, world, copy):
+    """cfg4 at full size hash-sharded over `world` loopback ranks (owner(p) =
+    splitmix64(p) mod world; 8 = the north star's split):
+    every round ships ghost parent rows -- read in place, or (copy) through
+    each receiver's buffer as RCCL moves them; deliveries, the per-round
+    histogram, 16 sampled delivered sets (the union over the ranks) and the
+    digest sum against the oracle and the single engine
+    (subtree.go:324-337)."""
     wl, parent, live, tot, reach, hist = cfg4_tree
-    world = 2
     lb = PE.Loopback(world)
     engines = [PE.Engine(wl.n_peers, 1, seed=wl.seed) for _ in range(world)]
     try:
         for r, e in enumerate(engines):
-            e.dist_init_loopback(lb, r, PE.PART_PEER)
+            e.dist_init_loopback(lb, r, PE.PART_PEER, copy=copy)
             e.set_tree(0, 0, parent)
             e.set_live(live)
         firsts = [e.publish(wl.msg_topics) for e in engines]
@@ -136,13 +141,16 @@ def test_cfg4_full_size_two_ranks_peer_hash(cfg4_tree):
         for t in th:
             t.start()
         for t in th:
-            t.join(timeout=200)
+            t.join(timeout=300)
         assert not any(t.is_alive() for t in th), "rank thread hung"
         assert not errs, errs
         assert all(s.expand_mode == PE.MODE_LEVEL_PULL for s in stats)
+        want = PE.XCHG_COPY if copy else PE.XCHG_ZERO_COPY
+        assert all(s.xchg_path == want and s.xchg_rounds > 0 for s in stats), [s.xchg_path for s in stats]
         check_run(stats, wl.n_msgs, tot, hist)
         own = PE.partition_owner(parent, 0, 0, world, PE.PART_PEER)
-        assert 0.45 < float((own == 0).sum()) / float((own >= 0).sum()) < 0.55
+        for r in range(world):
+            assert 0.9 / world < float((own == r).sum()) / float((own >= 0).sum()) < 1.1 / world
         for m in sampled(wl.n_msgs, seed=9):
             got = np.zeros(wl.n_peers, dtype=bool)
             for r, e in enumerate(engines):

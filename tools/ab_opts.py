@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""A/B of launch-plan options (ps_set_plan_opts) on one engine.
+
+    python tools/ab_opts.py --workload cfg2 --variants '[{}, {"overlap_min_bytes": 0}]' [--reps 6 --steps 200]
+
+Variants alternate (A B A B ...) on the same engine and topology; each rep
+runs `steps` pipelined steps (ps_run_async / ps_wait, as bench.py times them)
+and checks the deliveries.  Prints one JSON line: per variant the ms/step of
+every rep, the median, and the effective plan of its last window."""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "go-libp2p-pubsub_amd"))
+
+import psengine as PE  # noqa: E402
+from psengine import workloads as WL  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="cfg3")
+    ap.add_argument("--variants", default='[{}]')
+    ap.add_argument("--reps", type=int, default=6)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--sync", action="store_true")
+    args = ap.parse_args()
+    variants = json.loads(args.variants)
+    wl = WL.CONFIGS[args.workload]()
+    eng = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed)
+    sizes = WL.build_engine_topics(eng, wl)
+    expect = wl.expected_deliveries(sizes)
+    base = eng.plan_opts()
+    res = [[] for _ in variants]
+    last = [None] * len(variants)
+    for rep in range(args.reps):
+        for i, v in enumerate(variants):
+            eng.set_plan(**{**base, **v})
+            for _ in range(3):  # warm: plans rebuilt, uploads done
+                eng.publish(wl.msg_topics)
+                assert eng.run().deliveries == expect
+            t0 = time.perf_counter()
+            tot = 0
+            if args.sync:
+                for _ in range(args.steps):
+                    eng.publish(wl.msg_topics)
+                    st = eng.run()
+                    tot += st.deliveries
+            else:
+                for k in range(args.steps):
+                    eng.publish(wl.msg_topics)
+                    eng.run_async()
+                    if k:
+                        tot += eng.wait().deliveries
+                st = eng.wait()
+                tot += st.deliveries
+            wall = time.perf_counter() - t0
+            assert tot == expect * args.steps, (tot, expect)
+            res[i].append(wall * 1e3 / args.steps)
+            last[i] = {"plan_max_rounds": st.plan_max_rounds, "prefix_rounds": st.prefix_rounds,
+                       "flood_rounds": st.flood_rounds, "rounds": st.rounds, "overlapped": st.overlapped}
+        print(f"[ab] rep {rep}: " + "  ".join(f"{r[-1]:.4f}" for r in res), file=sys.stderr, flush=True)
+    out = {"workload": args.workload, "steps": args.steps, "sync": args.sync,
+           "variants": [{"opts": v, "ms_per_step": [round(x, 4) for x in r], "median": round(statistics.median(r), 4),
+                         "last_window": l} for v, r, l in zip(variants, res, last)]}
+    print(json.dumps(out))
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
