@@ -556,6 +556,7 @@ def main():
     t0 = time.perf_counter()
     sts = steps(args.steps)
     wall = time.perf_counter() - t0
+    overlapped_timed = sum(int(st.overlapped) for st in sts)
     tot_deliv = sum(st.deliveries for st in sts)
     assert args.no_check or tot_deliv == deliv_expected * args.steps
     value = tot_deliv / wall
@@ -590,6 +591,12 @@ def main():
         "pair_model": {"bytes_per_delivery": PAIR_BYTES, "equiv_GBs_not_achievable": pair_gbs,
                        "note": "model-equivalent rate of the 28.375 B/delivery pair formulation; "
                                "this engine moves 64 messages per 8-B word (roofline.bytes_per_launch)"},
+        # the plan the timed steps ran: the engine's plan options (ps_get_plan_opts:
+        # the measured defaults; the environment cannot change them) and the
+        # effective plan of the last window
+        "plan": {"opts": eng.plan_opts(), "max_rounds_per_launch": st.plan_max_rounds,
+                 "prefix_rounds": st.prefix_rounds, "flood_rounds": st.flood_rounds,
+                 "overlapped_windows_timed": overlapped_timed},
         "last_step": {"rounds": st.rounds, "windows": st.windows, "flood_rounds": st.flood_rounds,
                       "run_ms": st.run_ms,
                       "expand_ms": st.expand_ms, "host_ms": st.host_ms,

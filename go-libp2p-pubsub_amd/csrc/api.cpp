@@ -74,6 +74,8 @@ ps_plan_opts current_opts(const ps_engine* e) {
   o.xchg_overlap = e->xchg_overlap_env;
   o.gpu_build = e->gpu_build_on ? 1 : 0;
   o.flood_spin_ticks = e->flood_spin_ticks;
+  o.chain_nt = e->chain_nt ? 1 : 0;
+  o.chain_waves = e->chain_waves;
   return o;
 }
 
@@ -85,7 +87,8 @@ const char* check_opts(const ps_plan_opts& o) {
   if (o.pad_words < 2) return "pad_words < 2";
   if (o.overlap_min_rounds < 2) return "overlap_min_rounds < 2";
   if (o.xchg_overlap < -1 || o.xchg_overlap > 1) return "xchg_overlap not -1, 0 or 1";
-  if (o.flood > 1 || o.chain_tail > 1 || o.overlap > 1 || o.gpu_build > 1) return "switch not 0 or 1";
+  if (o.flood > 1 || o.chain_tail > 1 || o.overlap > 1 || o.gpu_build > 1 || o.chain_nt > 1 || o.chain_waves > 16)
+    return "switch not 0 or 1";
   return nullptr;
 }
 
@@ -111,6 +114,8 @@ void apply_opts(ps_engine* e, const ps_plan_opts& o) {
   e->xchg_overlap_env = o.xchg_overlap;
   e->gpu_build_on = o.gpu_build != 0;
   e->flood_spin_ticks = o.flood_spin_ticks;
+  e->chain_nt = o.chain_nt != 0;
+  e->chain_waves = o.chain_waves;
   refresh_xchg_overlap(e);
 }
 
@@ -155,6 +160,8 @@ static void read_switches(ps_engine* e) {
     o.flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
   if (const char* v = std::getenv("PSAMD_FLOOD_SPIN_TICKS")) o.flood_spin_ticks = static_cast<uint32_t>(std::strtoul(v, nullptr, 0));
   if (const char* v = std::getenv("PSAMD_FLOOD_TOP_BYTES")) o.flood_top_bytes = std::strtoull(v, nullptr, 0);
+  if (const char* v = std::getenv("PSAMD_CHAIN_WAVES"))
+    o.chain_waves = static_cast<uint32_t>(std::max(0, std::min(16, std::atoi(v))));
   if (!check_opts(o)) apply_opts(e, o);
 }
 

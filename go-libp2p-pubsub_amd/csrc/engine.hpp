@@ -272,6 +272,8 @@ struct ps_engine {
   bool chain_tail = true;         // a chain ending at the last round may be one round longer (PSAMD_CHAIN_TAIL)
   double launch_bytes = 16e6;     // planner: a launch's ramp and tail as row bytes (PSAMD_LAUNCH_BYTES)
   uint32_t chain_words = 8192;    // row words per chain wave, the planner's target (PSAMD_CHAIN_WORDS)
+  uint32_t chain_waves = 12;      // chain launches: resident waves per CU at most (ps_plan_opts)
+  bool chain_nt = true;           // chain launches: level 0 and the inner levels stored non-temporally
   std::vector<uint64_t> chain_fail_key;  // a pair plan whose chain ranges overflowed the level tables: no chains
   psamd::DevBuf d_chain_ovf;
   // rows of rounds writing at least this much store non-temporally (the MALL

@@ -215,7 +215,7 @@ struct PullArgs {
   const uint32_t* row_ptr;
   uint64_t* partials_r[6];  // (kChainLevels)
   // debug (PSAMD_CHAIN_PROFILE): per chunk kChainProf words -- s_memrealtime
-  // at the wave's start and end, row words written, HW_ID and XCC_ID; null: off
+  // at the chunk's start and end, row words written, HW_ID and XCC_ID; null: off
   uint64_t* prof;
 };
 constexpr uint32_t kChainProf = 4;
@@ -260,14 +260,22 @@ struct ChainChunk {
   uint32_t first[kChainLevels + 1];
   // level k >= 1 of the chunk: the descendants [lo[k], hi[k]) (k_chain_ranges)
   uint32_t lo[kChainLevels], hi[kChainLevels];
+  // the topic's first node, and its root node if this rank owns it (the
+  // root's row is the seeded arrival row), else kNoneNode: node-space
+  // properties, so the kernel needs no topic-table read before its loads
+  uint32_t nbase, root;
 };
+static_assert(sizeof(ChainChunk) == 128, "two chunk descriptors per 256-B line");
 // ChainChunk::lo / hi from the device CSR; *overflow is set non-zero when a
 // level range exceeds cap (the plan is then not used)
 hipError_t launch_chain_ranges(ChainChunk* chunks, uint32_t n, const uint32_t* row_ptr, uint32_t cap,
                                uint32_t* overflow, hipStream_t s);
 // slices: chunks of rows wider than the stage (column slices; their own launch)
+// inner_nt: level 0 and the inner levels store non-temporally (false: plain, A/B)
+// waves_per_cu: resident chain waves per CU at most (an LDS pad; 0: no cap)
 hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32_t n_chunks, uint32_t round,
-                             bool record, bool nt, bool slices, hipStream_t s);
+                             bool record, bool nt, bool slices, bool inner_nt, uint32_t waves_per_cu,
+                             hipStream_t s);
 // ChainChunk::p_lo / p_hi from the device node_parent (GPU-built graphs)
 hipError_t launch_chain_parents(ChainChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s);
 constexpr uint32_t kPullSlots = 256;  // partial slots per round of a pull launch

@@ -413,6 +413,8 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
             c.levels = static_cast<uint8_t>(levels);
             c.r0 = static_cast<uint8_t>(r0);
             c.group = static_cast<uint16_t>(gi);
+            c.nbase = T.nbase;
+            c.root = T.root_local ? T.nbase : kNoneNode;
             for (uint32_t k = 0; k <= levels && k <= kChainLevels; ++k)
               c.first[k] = T.nbase + (d + k < T.level_off.size() ? T.level_off[d + k] : T.n_nodes);
             (z.S < W ? sliced : PP.chain).push_back(c);

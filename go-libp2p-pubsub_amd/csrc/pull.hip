@@ -4,6 +4,7 @@
 // Reference: subtree.forwardMessage (subtree.go:319-354) and
 // client.processMessages (client.go:100-132).
 #include <algorithm>
+#include <cstddef>
 
 #include "devutil.hpp"
 #include "kernels.hpp"
@@ -13,6 +14,13 @@ namespace psamd {
 namespace {
 
 using namespace dev;
+
+// LDS-DMA: lane i copies N bytes from its own global address into
+// lds_base + i * N (lds_base wave-uniform); no VGPR destination, counted on
+// vmcnt like a load.
+#define PSAMD_DMA(g, lds_base, N)                                                        \
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(g), \
+                                   (__attribute__((address_space(3))) void*)(lds_base), N, 0, 0)
 // ------------------------------------------------------------------ pull ---
 // Level mode, pull direction, one launch per round (multi-GPU windows, whose
 // rounds are separated by the frontier exchange; PSAMD_FLOOD=0 on one GPU).
@@ -936,11 +944,12 @@ struct ChainMeta {
   uint32_t g0;                 // the batch's first global slot
 };
 
-// Walks the metadata slots (64 nodes of levels >= 1, each level from a slot
-// boundary) level by level: the level k of slot g, its first slot kb, its
-// slot count ns, its node range [lo, hi) and the first node plo of the level
-// above.  Wave-uniform; no loop per slot, so the callers' slot loops unroll.
-// (A level with no node ends the walk: every deeper level is empty too.)
+// Walks the metadata slots (64 nodes of a chunk's levels 0 .., each level
+// from a slot boundary) level by level: the level k of slot g, its first slot
+// kb, its slot count ns, its node range [lo, hi) and the first node plo of the
+// level above (level 0: the run's first parent).  Wave-uniform; no loop per
+// slot, so the callers' slot loops unroll.  (A level with no node ends the
+// walk: every deeper level is empty too.)
 struct MetaCursor {
   uint32_t k, kb, ns, lo, hi, plo;
   __device__ __forceinline__ void enter(const ChainChunk* cp, uint32_t levels) {
@@ -951,11 +960,11 @@ struct MetaCursor {
     ns = (hi - lo + 63) >> 6;
     if (ns == 0) k = levels;
   }
-  // the cursor at slot g0
-  __device__ __forceinline__ void start(const ChainChunk* cp, uint32_t levels, uint32_t g0) {
-    k = 1;
+  // the cursor at slot g0 (p_lo: the run's first parent)
+  __device__ __forceinline__ void start(const ChainChunk* cp, uint32_t levels, uint32_t g0, uint32_t p_lo) {
+    k = 0;
     kb = 0;
-    lo = __builtin_amdgcn_readfirstlane(cp->lo[0]);
+    lo = p_lo;
     enter(cp, levels);
     while (k < levels && g0 >= kb + ns) {
       kb += ns;
@@ -976,10 +985,10 @@ struct MetaCursor {
 // Issues the batch of slots g0 .. g0 + kMetaSlots - 1: raw parent ids and
 // flag dwords into p / f (unconsumed, so nothing waits here).
 __device__ __forceinline__ void chain_meta_issue(const PullArgs& a, const ChainChunk* cp, uint32_t levels,
-                                                 uint32_t g0, uint32_t lane, uint32_t (&p)[kMetaSlots],
-                                                 uint32_t (&f)[kMetaSlots]) {
+                                                 uint32_t p_lo, uint32_t g0, uint32_t lane,
+                                                 uint32_t (&p)[kMetaSlots], uint32_t (&f)[kMetaSlots]) {
   MetaCursor m;
-  m.start(cp, levels, g0);
+  m.start(cp, levels, g0, p_lo);
 #pragma unroll
   for (uint32_t i = 0; i < kMetaSlots; ++i) {
     if (i) m.step(cp, levels, g0 + i);
@@ -994,12 +1003,12 @@ __device__ __forceinline__ void chain_meta_issue(const PullArgs& a, const ChainC
 }
 
 // Packs the issued batch (the first use of p / f: the loads' wait).
-__device__ __forceinline__ void chain_meta_pack(const ChainChunk* cp, uint32_t levels, uint32_t g0, uint32_t lane,
-                                                const uint32_t (&p)[kMetaSlots], const uint32_t (&f)[kMetaSlots],
-                                                ChainMeta& M) {
+__device__ __forceinline__ void chain_meta_pack(const ChainChunk* cp, uint32_t levels, uint32_t p_lo, uint32_t g0,
+                                                uint32_t lane, const uint32_t (&p)[kMetaSlots],
+                                                const uint32_t (&f)[kMetaSlots], ChainMeta& M) {
   M.g0 = g0;
   MetaCursor m;
-  m.start(cp, levels, g0);
+  m.start(cp, levels, g0, p_lo);
 #pragma unroll
   for (uint32_t i = 0; i < kMetaSlots; ++i) {
     if (i) m.step(cp, levels, g0 + i);
@@ -1037,11 +1046,12 @@ __device__ __forceinline__ uint32_t chain_meta_pick(const ChainMeta& M, uint32_t
 // zeros) and its own level-table entry into tab; generation stamped and nodes
 // counted by the slice-0 wave.  carry: the parent index of the group's last
 // node, for the next group's first (a parent counts once, at its first
-// child; kNoneNode at a level's start: no parent spans two chunks).
+// child).  pw: parent-row words read per counted parent (level 0: the
+// parents' rows came from HBM; deeper levels: none, they are stage rows).
 template <uint32_t kZero>
 __device__ __forceinline__ void chain_group(const PullArgs& a, const ChainStep& C, uint32_t e, const uint8_t* up_tab,
                                             uint32_t y, uint32_t j, uint32_t* ctab, uint8_t* tab, uint32_t cur,
-                                            uint32_t lane, uint32_t& carry, WaveCtr& c) {
+                                            uint32_t lane, uint32_t pw, uint32_t& carry, WaveCtr& c) {
   const bool in = e != kMetaNone;
   const uint32_t rel = e & (kMetaLive - 1);
   const uint8_t src = in ? up_tab[rel] : kChainNone;  // the parent's stage slot
@@ -1056,10 +1066,13 @@ __device__ __forceinline__ void chain_group(const PullArgs& a, const ChainStep& 
   uint32_t prev = static_cast<uint32_t>(__shfl_up(static_cast<int>(mine), 1, 64));
   if (lane == 0) prev = carry;
   carry = __builtin_amdgcn_readlane(mine, 63);
-  // nodes and parents counted once per run (slice 0); words per slice (the
-  // parents' rows come from LDS: no parent words read)
-  ctr_nodes(c, in && C.slice0, ok && C.slice0, up && rel != prev && C.slice0, C.S, 0u);
-  if (!C.slice0) c.sw += static_cast<uint64_t>(__popcll(__ballot(ok))) * C.S;
+  // nodes and parents counted once per run (slice 0); words per slice
+  const bool first = up && rel != prev;
+  ctr_nodes(c, in && C.slice0, ok && C.slice0, first && C.slice0, C.S, pw);
+  if (!C.slice0) {
+    c.sw += static_cast<uint64_t>(__popcll(__ballot(ok))) * C.S;
+    c.pwords += static_cast<uint64_t>(__popcll(__ballot(first))) * pw;
+  }
 }
 
 // The partial slots of round r0 + k of a chain launch (a switch: no dynamic
@@ -1121,125 +1134,194 @@ __global__ __launch_bounds__(kBlock) void k_chain_ranges(ChainChunk* __restrict_
   if (over) atomicOr(overflow, 1u);
 }
 
-// kSlices: the launch's chunks of rows wider than the stage (column slices,
-// a separate launch: the whole-row path keeps its registers).  LDS 9.4 KB per
-// one-wave workgroup: 17 resident waves per CU.  (A 736-word stage with
-// 512-node tables, 8 KB and 20 waves, measured no faster: cfg3 1.029 vs 1.021
-// ms/step, profiles/r03/ab_chain_v2.txt.)
+// Level 0 of a chain chunk whose parent span is wider than the stage (the
+// run's parents are consecutive ids, but childless ones between them count
+// in the span): the run resolves its parents as k_pull does and streams their
+// rows from HBM into its own rows and the stage at its own slots (run nodes *
+// S <= kStage, host plan); the run's level table holds each reached node's
+// own slot.  (Eager seen, PS_F_NO_LAZY_SEEN: an unreached node's slot holds
+// its own row, zeros, so every node keeps its slot.)  src: kChainPar row
+// addresses (the ctab LDS, dead until level 1).
 template <bool kRecord, bool kNT, bool kSlices>
+__device__ __forceinline__ void chain_level0_direct(const PullArgs& a, const ChainStep& C, const ChainChunk* cp,
+                                                 uint32_t p_lo, uint32_t p_hi, uint64_t* src, uint8_t* genl,
+                                                 uint64_t* stage, uint8_t* tab0, uint32_t lane, uint32_t cur,
+                                                 uint32_t round, uint64_t slot, uint64_t* partials,
+                                                 uint64_t& words_out) {
+  constexpr uint32_t kStage = kChainWords;
+  const uint32_t node_begin = cp->node_begin, n0 = cp->node_end - node_begin;
+  PullTopic P;
+  P.W = C.W;
+  P.nbase = C.nbase;
+  P.base = C.base;
+  P.root = cp->root;
+  WaveCtr c;
+  if constexpr (!kSlices) {
+    pull_resolve(a, P, node_begin, n0, p_lo, p_hi, src, genl, lane, cur, c, kNoneNode, kChainPar);
+    pull_stream<kRecord, kNT, true>(a, P, node_begin, n0, src, lane, round, c, stage);
+  } else {
+    // (pull_resolve stamps generations and counts whole rows: slice 0 keeps
+    // its node counts, every slice its own words)
+    PullCtr pc;
+    pull_resolve(a, P, node_begin, n0, p_lo, p_hi, src, genl, lane, cur, pc, kNoneNode, kChainPar);
+    const uint32_t nodes = __reduce_add_sync(~0ull, pc.kids), hit = __reduce_add_sync(~0ull, pc.reached);
+    const uint32_t par = __reduce_add_sync(~0ull, pc.parents);
+    if (C.slice0) {
+      c.kids += __builtin_amdgcn_readfirstlane(nodes);
+      c.reached += __builtin_amdgcn_readfirstlane(hit);
+      c.parents += __builtin_amdgcn_readfirstlane(par);
+    }
+    c.sw += static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(hit)) * C.S;
+    c.pwords += static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(par)) * C.S;
+    chain_stream<kRecord, kNT, true, kStage>(a, C, node_begin, n0, nullptr, src, stage, 0u, lane, round, c);
+  }
+  for (uint32_t j = lane; j < n0; j += 64)
+    tab0[j] = (src[j] != 0 || (a.all_current & 1u)) ? static_cast<uint8_t>(j) : kChainNone;
+  words_out += c.sw;
+  chain_flush(c, partials, slot, lane);
+}
+
+// kSlices: the launch's chunks of rows wider than the stage (column slices,
+// a separate launch: the whole-row path keeps its registers).  kInNT: every
+// level but the launch's last stores non-temporally (the default;
+// ps_plan_opts.chain_nt = 0: plain stores, A/B); kNT: the last level too.
+//
+// One round trip before the first store: a run's parents are consecutive
+// ids, so their rows (slices) are one block, copied into the stage by
+// LDS-DMA beside the metadata batch (the run and its descendants) and the
+// parents' generation bytes.  In a single-start window a reached node's row
+// is its parent's row, so level 0 is written from the stage like every level
+// below it: the parents' table (level -1) holds each reached parent's stage
+// slot.  (The previous form read the topic table, then the run's metadata,
+// then the parent rows: three dependent round trips per wave, 15 % of a
+// bulk-launch wave's life, profiles/r04/chain_prof_*.)
+template <bool kRecord, bool kNT, bool kSlices, bool kInNT = true, uint32_t kSimdWaves = 0>
 __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk* __restrict__ chunks,
                                                    uint32_t n_chunks, uint32_t round) {
+  // kSimdWaves (3 or 2): a register the kernel never uses, declared clobbered,
+  // sizes its VGPR allocation so that exactly that many waves fit per SIMD --
+  // a residency cap spread evenly over the CU's 4 SIMDs (an LDS cap leaves
+  // the placement to the dispatcher: 12 waves per CU 0.920 ms/step on cfg3,
+  // 3 per SIMD 0.90, profiles/r04/ab_chain_waves.txt)
+  if constexpr (kSimdWaves == 3) asm volatile("" ::: "v140");
+  if constexpr (kSimdWaves == 2) asm volatile("" ::: "v180");
   constexpr uint32_t kStage = kChainWords, kCap = kChainCap;
-  __shared__ uint64_t stage[kStage + 2];  // the run's rows (slices); + the zero pair
-  __shared__ uint64_t src[kChainPar];     // level 0: the parents' row addresses; then ctab
-  static_assert(kChainKids * 4 <= kChainPar * 8, "ctab fits the source table");
-  uint32_t* const ctab = reinterpret_cast<uint32_t*>(src);  // a sub-run's stage offsets (levels >= 1)
-  __shared__ uint32_t gen_lds[kChainPar / 4 + 2];
-  __shared__ uint8_t tabs[2][kCap];  // level tables: this level's and the one above
+  __shared__ __attribute__((aligned(16))) uint64_t stage[kStage + 2];  // the parents' rows (slices); + the zero pair
+  __shared__ __attribute__((aligned(16))) uint32_t ctab[kChainKids];   // a sub-run's stage offsets
+  static_assert(kChainKids * 4 >= kChainPar * 8, "ctab holds the direct level 0's row addresses");
+  __shared__ uint32_t gen_lds[kChainPar / 4 + 2];                      // the parents' generation bytes
+  __shared__ uint8_t tabs[2][kCap];  // level tables: this level's and the one above (level -1: the parents)
   const uint32_t lane = threadIdx.x;
-  uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds);
   const uint32_t cur = a.gen_cur & 0xFF;
-  if (lane < 2) stage[kStage + lane] = 0;
   const uint32_t ci = blockIdx.x;
   if (ci >= n_chunks) return;
   // debug profile (PSAMD_CHAIN_PROFILE): the wave's start, end and words
   const uint64_t t_start = a.prof ? __builtin_amdgcn_s_memrealtime() : 0ull;
   uint64_t words_out = 0;
-  // the chunk's scalars (its level ranges are read per level, not held)
   const ChainChunk* const cp = chunks + ci;
-  const uint32_t node_begin = cp->node_begin, node_end = cp->node_end, topic = cp->topic;
-  const uint32_t p_lo = cp->p_lo, p_hi = cp->p_hi, r0 = cp->r0, levels = cp->levels;
-  const TopicDev T = a.topics[topic];
+  // (levels and r0 through their dword: a sub-dword field read becomes a
+  // vector load, one more round trip before the first store)
+  static_assert(offsetof(ChainChunk, levels) == 40 && offsetof(ChainChunk, r0) == 41, "ChainChunk layout");
+  const uint32_t lr = reinterpret_cast<const uint32_t*>(cp)[10];
+  const uint32_t p_lo = cp->p_lo, p_hi = cp->p_hi, levels = lr & 0xFFu, r0 = (lr >> 8) & 0xFFu;
   ChainStep C;
   C.W = cp->W;
   C.w0 = kSlices ? cp->w0 : 0u;
   C.S = kSlices ? cp->S : C.W;
-  C.nbase = T.nbase;
-  C.base = (static_cast<uint64_t>(cp->row0_hi) << 32 | cp->row0_lo) - static_cast<uint64_t>(T.nbase) * C.W;
+  C.nbase = cp->nbase;
+  C.base = (static_cast<uint64_t>(cp->row0_hi) << 32 | cp->row0_lo) - static_cast<uint64_t>(C.nbase) * C.W;
   C.slice0 = C.w0 == 0;
-  const uint32_t n0 = node_end - node_begin;  // <= kChainPar, n0 * S <= kStage (host plan)
   const uint64_t slot = blockIdx.x % a.slot_mod;
-  // levels 1 ..: the first metadata batch, issued before level 0's loads
-  // (one round trip for both); packed once level 0's sources are resolved
+  // the parents [p_lo, p_hi]: their rows (slices) and generation bytes.  The
+  // span holds every parent id between the run's first and last, childless
+  // ones too, so it may exceed the run (the host sizes runs, not spans): a
+  // span wider than the stage takes the direct path (level 0 from HBM, after
+  // the metadata: one round trip more)
+  const uint32_t n_par = p_hi - p_lo + 1;
+  const bool direct = n_par > kChainPar || n_par * C.S > kStage;
+  const uint32_t words = n_par * C.S;
+  const uint64_t* prow = (p_lo == cp->root ? a.a_cur : a.seen) + C.base + static_cast<uint64_t>(p_lo) * C.W + C.w0;
+  const uint32_t g0 = p_lo & ~3u;
+  const uint32_t n_gd = (((p_hi + 4u) & ~3u) - g0) >> 2;  // the parents' generation dwords (<= kChainPar / 4 + 1)
+  // the previous node's parent: a parent whose children straddle two runs counts once
+  const uint32_t pm = cp->node_begin > C.nbase ? a.node_parent[cp->node_begin - 1] : kNoneNode;
   ChainMeta M;
   {
     uint32_t mp[kMetaSlots], mf[kMetaSlots];
-    if (levels > 1) chain_meta_issue(a, cp, levels, 0u, lane, mp, mf);
-    // level 0: the run, parents' rows (slices) from HBM
-    PullTopic P;
-    P.W = C.W;
-    P.nbase = T.nbase;
-    P.base = C.base;
-    P.root = (T.flags & kTopicRootLocal) ? T.nbase : kNoneNode;
-    WaveCtr c;
-    if constexpr (!kSlices) {
-      pull_resolve(a, P, node_begin, n0, p_lo, p_hi, src, genl, lane, cur, c, kNoneNode, kChainPar);
-      if (levels > 1) chain_meta_pack(cp, levels, 0u, lane, mp, mf, M);
-      pull_stream<kRecord, true, true>(a, P, node_begin, n0, src, lane, round + r0, c, stage);
-    } else {
-      // (pull_resolve stamps generations and counts whole rows: slice 0 keeps
-      // its node counts, every slice its own words)
-      PullCtr pc;
-      pull_resolve(a, P, node_begin, n0, p_lo, p_hi, src, genl, lane, cur, pc, kNoneNode, kChainPar);
-      if (levels > 1) chain_meta_pack(cp, levels, 0u, lane, mp, mf, M);
-      const uint32_t nodes = __reduce_add_sync(~0ull, pc.kids), hit = __reduce_add_sync(~0ull, pc.reached);
-      const uint32_t par = __reduce_add_sync(~0ull, pc.parents);
-      if (C.slice0) {
-        c.kids += __builtin_amdgcn_readfirstlane(nodes);
-        c.reached += __builtin_amdgcn_readfirstlane(hit);
-        c.parents += __builtin_amdgcn_readfirstlane(par);
+    chain_meta_issue(a, cp, levels, p_lo, 0u, lane, mp, mf);
+    if (!direct) {
+      if (lane < n_gd) PSAMD_DMA(reinterpret_cast<const uint32_t*>(a.gen + g0) + lane, gen_lds, 4);
+      if (!(C.W & 1u)) {
+        // 16-B units (even rows and slices start 16-B aligned), 1 KB per instruction
+        const uint32_t units = words >> 1;
+        const float rs = 1.0f / static_cast<float>(C.S);
+        for (uint32_t u0 = 0; u0 < units; u0 += 64) {
+          const uint32_t u = min(u0 + lane, units - 1);  // (lanes past the end repeat the last unit)
+          int32_t kk, r;
+          chain_split(2 * u, rs, C.S, kk, r);  // (word 2u: S is even, a unit never straddles two rows)
+          PSAMD_DMA(prow + static_cast<uint64_t>(kk) * C.W + r, stage + 2 * u0, 16);
+        }
+      } else {
+        // odd rows (whole rows only: slices are even): contiguous, dwords
+        const uint32_t* pw32 = reinterpret_cast<const uint32_t*>(prow);
+        for (uint32_t d0 = 0; d0 < 2 * words; d0 += 64)
+          PSAMD_DMA(pw32 + min(d0 + lane, 2 * words - 1), reinterpret_cast<uint32_t*>(stage) + d0, 4);
       }
-      c.sw += static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(hit)) * C.S;
-      c.pwords += static_cast<uint64_t>(__builtin_amdgcn_readfirstlane(par)) * C.S;
-      chain_stream<kRecord, true, true, kStage>(a, C, node_begin, n0, nullptr, src, stage, 0u, lane, round + r0, c);
     }
-    // the run's level table: a node's own stage slot if reached.  (Eager
-    // seen, PS_F_NO_LAZY_SEEN: an unreached node's slot holds its own row,
-    // zeros, so every node keeps its slot, as the generation test of a
-    // separate launch would find every generation current.)
-    for (uint32_t j = lane; j < n0; j += 64)
-      tabs[0][j] = (src[j] != 0 || (a.all_current & 1u)) ? static_cast<uint8_t>(j) : kChainNone;
-    words_out += c.sw;
-    chain_flush(c, chain_slots(a, r0), slot, lane);
+    chain_meta_pack(cp, levels, p_lo, 0u, lane, mp, mf, M);  // (waits for every load above)
   }
-  // src (level 0's sources) is dead from here and its LDS becomes ctab: no
-  // memory access may move across the switch from one view to the other
-  asm volatile("" ::: "memory");
-  // levels 1 .. levels - 1, sub-run by sub-run (<= kChainKids nodes): every
-  // node's parent and flag come from the preloaded batch, so no level waits
-  // for the stores above it; a batch is reloaded only when a chunk's levels
-  // hold more than kMetaSlots slots (a wait, rare: runs are sized for less)
-  uint32_t g = 0;  // the global metadata slot of the next node group
-  for (uint32_t k = 1; k < levels; ++k) {
+  if (lane < 2) stage[kStage + lane] = 0;
+  uint32_t g = 0;   // the global metadata slot of the next node group
+  uint32_t k0 = 0;  // the first level of the loop below
+  if (!direct) {
+    // the parents' table: a reached parent's stage slot (eager seen,
+    // PS_F_NO_LAZY_SEEN: every generation counts as current)
+    const uint8_t* genl = reinterpret_cast<const uint8_t*>(gen_lds);
+    for (uint32_t i = lane; i < n_par; i += 64)
+      tabs[1][i] = (genl[p_lo + i - g0] == cur || (a.all_current & 1u)) ? static_cast<uint8_t>(i) : kChainNone;
+  } else {
+    chain_level0_direct<kRecord, kInNT, kSlices>(a, C, cp, p_lo, p_hi, reinterpret_cast<uint64_t*>(ctab),
+                                                 reinterpret_cast<uint8_t*>(gen_lds), stage, tabs[0], lane, cur,
+                                                 round + r0, slot, chain_slots(a, r0), words_out);
+    g = (cp->node_end - cp->node_begin + 63) >> 6;  // (the batch's level-0 slots)
+    k0 = 1;
+    asm volatile("" ::: "memory");  // (level 0's sources become ctab)
+  }
+  // levels k0 .. levels - 1, sub-run by sub-run (<= kChainKids nodes): every
+  // node's parent and flag come from the preloaded batch and every source
+  // row from the stage, so no level waits for the stores above it; a batch
+  // is reloaded only when a chunk's levels hold more than kMetaSlots slots (a
+  // wait, rare: runs are sized for less)
+  for (uint32_t k = k0; k < levels; ++k) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane(cp->lo[k]), hi = __builtin_amdgcn_readfirstlane(cp->hi[k]);
     const uint8_t* const up_tab = tabs[(k - 1) & 1];
-    uint32_t carry = kNoneNode;
+    uint32_t carry = k == 0 && pm == p_lo ? 0u : kNoneNode;
     WaveCtr c;
     for (uint32_t y0 = lo; y0 < hi; y0 += kChainKids) {
       const uint32_t nk = min(kChainKids, hi - y0);
       const uint32_t ng = (nk + 63) >> 6;
       if (g + ng > M.g0 + kMetaSlots) {
         uint32_t mp[kMetaSlots], mf[kMetaSlots];
-        chain_meta_issue(a, cp, levels, g, lane, mp, mf);
-        chain_meta_pack(cp, levels, g, lane, mp, mf, M);
+        chain_meta_issue(a, cp, levels, p_lo, g, lane, mp, mf);
+        chain_meta_pack(cp, levels, p_lo, g, lane, mp, mf, M);
       }
       uint8_t* const tab = tabs[k & 1] + (y0 - lo);
 #pragma unroll
       for (uint32_t s = 0; s < kChainKids / 64; ++s) {
         if (s >= ng) break;
         chain_group<kStage>(a, C, chain_meta_pick(M, g + s - M.g0), up_tab, y0 + s * 64 + lane, s * 64 + lane, ctab,
-                            tab, cur, lane, carry, c);
+                            tab, cur, lane, k == 0 ? C.S : 0u, carry, c);
       }
       g += ng;
       if constexpr (!kSlices) {
         uint64_t* out = a.seen + C.base + static_cast<uint64_t>(y0) * C.W;
-        if (kNT || k + 1 < levels)  // (only the launch's last level may be re-read soon)
-          stage_stream<kRecord, true, kStage>(a, out, nk, C.W, ctab, stage, lane, round + r0 + k, c);
+        if (k + 1 < levels)  // (only the launch's last level may be re-read soon)
+          stage_stream<kRecord, kInNT, kStage>(a, out, nk, C.W, ctab, stage, lane, round + r0 + k, c);
         else
-          stage_stream<kRecord, false, kStage>(a, out, nk, C.W, ctab, stage, lane, round + r0 + k, c);
+          stage_stream<kRecord, kNT, kStage>(a, out, nk, C.W, ctab, stage, lane, round + r0 + k, c);
       } else {
-        chain_stream<kRecord, true, false, kStage>(a, C, y0, nk, ctab, nullptr, stage, kNoneNode, lane,
-                                                   round + r0 + k, c);
+        chain_stream<kRecord, kInNT, false, kStage>(a, C, y0, nk, ctab, nullptr, stage, kNoneNode, lane,
+                                                    round + r0 + k, c);
       }
       ctr_fold(c);
     }
@@ -1252,8 +1334,11 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
     const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
     const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
     const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);
-    const uint64_t v = lane == 0 ? t_start : lane == 1 ? t_end : lane == 2 ? words_out
-                                                                            : (static_cast<uint64_t>(xcc) << 32 | hw);
+    // (bit 40: level 0 took the direct path)
+    const uint64_t v = lane == 0   ? t_start
+                       : lane == 1 ? t_end
+                       : lane == 2 ? words_out
+                                   : (static_cast<uint64_t>(direct) << 40 | static_cast<uint64_t>(xcc) << 32 | hw);
     if (lane < kChainProf) a.prof[static_cast<uint64_t>(ci) * kChainProf + lane] = v;
   }
 }
@@ -1326,22 +1411,72 @@ hipError_t launch_chain_ranges(ChainChunk* chunks, uint32_t n, const uint32_t* r
   return hipGetLastError();
 }
 
+namespace {
+// Dynamic LDS that caps a launch of a one-wave kernel at `waves` resident
+// workgroups per CU (160 KB of LDS per CU, allocated in 512-B granules): the
+// static LDS plus the pad stays above 160 KB / (waves + 1).  0: no cap.
+template <class K>
+size_t lds_cap_pad(K kernel, uint32_t waves) {
+  if (waves == 0) return 0;
+  hipFuncAttributes fa{};
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kernel)) != hipSuccess) return 0;
+  const size_t per = (160u * 1024u) / waves - 512u;
+  return per > fa.sharedSizeBytes ? per - fa.sharedSizeBytes : 0;
+}
+}  // namespace
+
 hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32_t n_chunks, uint32_t round,
-                             bool record, bool nt, bool slices, hipStream_t s) {
+                             bool record, bool nt, bool slices, bool inner_nt, uint32_t waves_per_cu,
+                             hipStream_t s) {
   if (n_chunks == 0) return hipSuccess;
+  // (every variant has the same static LDS: one pad for all)
+  static const size_t pads[17] = {
+      0,  lds_cap_pad(k_pull_chain<false, true, false>, 1), lds_cap_pad(k_pull_chain<false, true, false>, 2),
+      lds_cap_pad(k_pull_chain<false, true, false>, 3),  lds_cap_pad(k_pull_chain<false, true, false>, 4),
+      lds_cap_pad(k_pull_chain<false, true, false>, 5),  lds_cap_pad(k_pull_chain<false, true, false>, 6),
+      lds_cap_pad(k_pull_chain<false, true, false>, 7),  lds_cap_pad(k_pull_chain<false, true, false>, 8),
+      lds_cap_pad(k_pull_chain<false, true, false>, 9),  lds_cap_pad(k_pull_chain<false, true, false>, 10),
+      lds_cap_pad(k_pull_chain<false, true, false>, 11), lds_cap_pad(k_pull_chain<false, true, false>, 12),
+      lds_cap_pad(k_pull_chain<false, true, false>, 13), lds_cap_pad(k_pull_chain<false, true, false>, 14),
+      lds_cap_pad(k_pull_chain<false, true, false>, 15), lds_cap_pad(k_pull_chain<false, true, false>, 16)};
+  // 12 and 8 per CU: 3 and 2 per SIMD through the register allocation
+  // (whole rows, production variants); other caps through an LDS pad
+  const uint32_t simd = waves_per_cu == 12 ? 3u : waves_per_cu == 8 ? 2u : 0u;
+  const size_t pad = simd ? 0 : pads[std::min<uint32_t>(waves_per_cu, 16)];
   const dim3 g(n_chunks), b(64);
+#define PSAMD_CHAIN(...) hipLaunchKernelGGL((k_pull_chain<__VA_ARGS__>), g, b, pad, s, a, chunks, n_chunks, round)
   if (slices) {
     if (record)
-      hipLaunchKernelGGL((k_pull_chain<true, false, true>), g, b, 0, s, a, chunks, n_chunks, round);
+      PSAMD_CHAIN(true, false, true);
+    else if (simd == 3)
+      PSAMD_CHAIN(false, true, true, true, 3);
+    else if (simd == 2)
+      PSAMD_CHAIN(false, true, true, true, 2);
     else
-      hipLaunchKernelGGL((k_pull_chain<false, true, true>), g, b, 0, s, a, chunks, n_chunks, round);
+      PSAMD_CHAIN(false, true, true);
   } else if (record) {
-    hipLaunchKernelGGL((k_pull_chain<true, false, false>), g, b, 0, s, a, chunks, n_chunks, round);
+    PSAMD_CHAIN(true, false, false);
+  } else if (!inner_nt) {  // (A/B: plain stores for level 0 and the inner levels)
+    if (nt)
+      PSAMD_CHAIN(false, true, false, false);
+    else
+      PSAMD_CHAIN(false, false, false, false);
+  } else if (simd == 3) {
+    if (nt)
+      PSAMD_CHAIN(false, true, false, true, 3);
+    else
+      PSAMD_CHAIN(false, false, false, true, 3);
+  } else if (simd == 2) {
+    if (nt)
+      PSAMD_CHAIN(false, true, false, true, 2);
+    else
+      PSAMD_CHAIN(false, false, false, true, 2);
   } else if (nt) {
-    hipLaunchKernelGGL((k_pull_chain<false, true, false>), g, b, 0, s, a, chunks, n_chunks, round);
+    PSAMD_CHAIN(false, true, false);
   } else {
-    hipLaunchKernelGGL((k_pull_chain<false, false, false>), g, b, 0, s, a, chunks, n_chunks, round);
+    PSAMD_CHAIN(false, false, false);
   }
+#undef PSAMD_CHAIN
   return hipGetLastError();
 }
 

@@ -840,11 +840,12 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         uint64_t* const prof = cprof ? e->d_chain_prof.as<uint64_t>() : nullptr;
         pa.prof = prof ? prof + static_cast<size_t>(e->pair.lo[r]) * kChainProf : nullptr;
         HIP_TRY(launch_pull_chain(pa, e->d_chain.as<ChainChunk>() + e->pair.lo[r], e->pair.gsplit[r] - e->pair.lo[r],
-                                  r, record, ntc, false, s),
+                                  r, record, ntc, false, e->chain_nt, e->chain_waves, s),
                 "pull chain");
         pa.prof = prof ? prof + static_cast<size_t>(e->pair.gsplit[r]) * kChainProf : nullptr;
         HIP_TRY(launch_pull_chain(pa, e->d_chain.as<ChainChunk>() + e->pair.gsplit[r],
-                                  e->pair.hi[r] - e->pair.gsplit[r], r, record, ntc, true, s),
+                                  e->pair.hi[r] - e->pair.gsplit[r], r, record, ntc, true, e->chain_nt,
+                                  e->chain_waves, s),
                 "pull chain (column slices)");
         pa.prof = nullptr;
         HIP_TRY(time_mark(false), "event");

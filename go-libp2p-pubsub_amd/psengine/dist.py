@@ -236,7 +236,11 @@ def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str
                          "kernel": MODE_KERNEL.get(st.expand_mode, "k_expand"),
                          "note": "per-GPU: job expand bytes / slowest rank's expand time / N"},
             "last_step_rank0": {"rounds": st.rounds, "run_ms": st.run_ms,
-                                "expand_ms": st.expand_ms, "host_ms": st.host_ms},
+                                "expand_ms": st.expand_ms, "host_ms": st.host_ms,
+                                "xchg_path": {0: "none", 1: "zero-copy", 2: "copy"}.get(int(st.xchg_path)),
+                                "xchg_rounds": st.xchg_rounds, "xchg_bytes_received": st.xchg_bytes,
+                                "max_rounds_per_launch": st.plan_max_rounds},
+            "plan_opts": eng.plan_opts(),
         }
     eng.close()
     return out

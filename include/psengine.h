@@ -196,6 +196,10 @@ typedef struct ps_plan_opts {
                                   no), 0, 1 (-1)                                */
   uint32_t gpu_build;          /* 1: rebuild a one-rank node space on the GPU (1) */
   uint32_t flood_spin_ticks;   /* k_flood dependency-wait bound, 100-MHz ticks (2e8) */
+  uint32_t chain_nt;           /* 1: chain launches store level 0 and their inner
+                                  levels non-temporally, 0: plain stores (1)    */
+  uint32_t chain_waves;        /* chain launches: resident waves per CU at most,
+                                  1..16 (an LDS pad), 0: as many as fit (12)    */
 } ps_plan_opts;
 
 int ps_plan_opts_default(ps_plan_opts* out);

@@ -26,8 +26,8 @@ pytestmark = pytest.mark.gpu
 
 
 def run(monkeypatch, chain, n, topics, live, msg_topics, starts=None, record=True, flood=False, flags=0,
-        msg_window=65536):
-    opts = {"chain_max": chain, "chain_max_groups": chain, "flood": int(flood)}
+        msg_window=65536, waves=12):
+    opts = {"chain_max": chain, "chain_max_groups": chain, "flood": int(flood), "chain_waves": waves}
     with PE.Engine(n, len(topics), record_hops=record, flags=flags, msg_window=msg_window, plan=opts) as eng:
         for t, (root, parent) in enumerate(topics):
             eng.set_tree(t, root, parent)
@@ -60,6 +60,12 @@ def sweep(monkeypatch, n, topics, live, msg_topics, starts=None, chains=(1, 2, 3
             cur = (key, [x.tolist() for x in deliv])
             ref = ref or cur
             assert cur == ref, (chain, record)
+            if chain >= 3 and not record:
+                # no residency cap (ps_plan_opts.chain_waves = 0): the same
+                # rows, counters and digest
+                _, _, _, deliv0, key0 = run(monkeypatch, chain, n, topics, live, msg_topics, starts, record=False,
+                                            waves=0, **kw)
+                assert (key0, [x.tolist() for x in deliv0]) == ref, (chain, "no residency cap")
     return ref
 
 

@@ -46,6 +46,7 @@ def parse(path: str):
 def launch_report(rnd, ln, ch):
     t0, t1, words = ch[:, 0].astype(np.int64), ch[:, 1].astype(np.int64), ch[:, 2].astype(np.float64)
     xcc = (ch[:, 3] >> np.uint64(32)).astype(np.int64) & 0xF
+    direct = ((ch[:, 3] >> np.uint64(40)) & np.uint64(1)).astype(bool)
     base = t0.min()
     s, e = (t0 - base) * TICK_US, (t1 - base) * TICK_US
     span = float(e.max())
@@ -78,6 +79,8 @@ def launch_report(rnd, ln, ch):
         "words_p10_p50_p90_max": [int(np.percentile(words, q)) for q in (10, 50, 90, 100)],
         "fit_dur_us": {"fixed": round(float(coef[0]), 2), "per_kword": round(float(coef[1]) * 1e3, 3)},
         "per_xcc": per_xcc,
+        "direct_level0": {"waves": int(direct.sum()), "words": int(words[direct].sum()),
+                          "dur_us_p50": round(float(np.median(dur[direct])), 1) if direct.any() else None},
     }
 
 
