@@ -48,8 +48,8 @@ int dist_streams(ps_engine* e) {
   if (e->xstream) return PS_OK;
   HIP_TRY(hipSetDevice(e->cfg.device), "hipSetDevice");
   HIP_TRY(hipStreamCreateWithFlags(&e->xstream, hipStreamNonBlocking), "exchange stream");
-  HIP_TRY(hipEventCreateWithFlags(&e->ev_round, hipEventDisableTiming), "round event");
-  HIP_TRY(hipEventCreateWithFlags(&e->ev_xchg, hipEventDisableTiming), "exchange event");
+  HIP_TRY(hipEventCreateWithFlags(&e->ev_round, kStreamEvent), "round event");
+  HIP_TRY(hipEventCreateWithFlags(&e->ev_xchg, kStreamEvent), "exchange event");
   return PS_OK;
 }
 
@@ -76,6 +76,7 @@ ps_plan_opts current_opts(const ps_engine* e) {
   o.flood_spin_ticks = e->flood_spin_ticks;
   o.chain_nt = e->chain_nt ? 1 : 0;
   o.chain_waves = e->chain_waves;
+  o.flood_min_rounds = e->flood_min_rounds;
   return o;
 }
 
@@ -87,7 +88,8 @@ const char* check_opts(const ps_plan_opts& o) {
   if (o.pad_words < 2) return "pad_words < 2";
   if (o.overlap_min_rounds < 2) return "overlap_min_rounds < 2";
   if (o.xchg_overlap < -1 || o.xchg_overlap > 1) return "xchg_overlap not -1, 0 or 1";
-  if (o.flood > 1 || o.chain_tail > 1 || o.overlap > 1 || o.gpu_build > 1 || o.chain_nt > 1 || o.chain_waves > 16)
+  if (o.flood > 1 || o.chain_tail > 1 || o.overlap > 1 || o.gpu_build > 1 || o.chain_nt > 1 || o.chain_waves > 16 ||
+      o.flood_min_rounds < 1 || o.reserved != 0)
     return "switch not 0 or 1";
   return nullptr;
 }
@@ -116,6 +118,7 @@ void apply_opts(ps_engine* e, const ps_plan_opts& o) {
   e->flood_spin_ticks = o.flood_spin_ticks;
   e->chain_nt = o.chain_nt != 0;
   e->chain_waves = o.chain_waves;
+  e->flood_min_rounds = o.flood_min_rounds;
   refresh_xchg_overlap(e);
 }
 
@@ -160,6 +163,9 @@ static void read_switches(ps_engine* e) {
     o.flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
   if (const char* v = std::getenv("PSAMD_FLOOD_SPIN_TICKS")) o.flood_spin_ticks = static_cast<uint32_t>(std::strtoul(v, nullptr, 0));
   if (const char* v = std::getenv("PSAMD_FLOOD_TOP_BYTES")) o.flood_top_bytes = std::strtoull(v, nullptr, 0);
+  if (const char* v = std::getenv("PSAMD_REDUCE_FORK_BYTES")) e->reduce_fork_bytes = std::strtoull(v, nullptr, 10);
+  if (const char* v = std::getenv("PSAMD_FLOOD_MIN_ROUNDS"))
+    o.flood_min_rounds = static_cast<uint32_t>(std::max(1, std::atoi(v)));
   if (const char* v = std::getenv("PSAMD_CHAIN_WAVES"))
     o.chain_waves = static_cast<uint32_t>(std::max(0, std::min(16, std::atoi(v))));
   if (!check_opts(o)) apply_opts(e, o);
@@ -232,13 +238,13 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   }
   read_switches(e);
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreate(&e->ev_run0) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess) {
+      hipEventCreateWithFlags(&e->ev_run0, kStartEvent) != hipSuccess || hipEventCreate(&e->ev_run1) != hipSuccess) {
     delete e;
     return PS_E_DEVICE;
   }
   for (auto& f : e->infl) {
     void* h = nullptr;
-    if (hipEventCreate(&f.ev0) != hipSuccess || hipEventCreate(&f.ev1) != hipSuccess ||
+    if (hipEventCreateWithFlags(&f.ev0, kStartEvent) != hipSuccess || hipEventCreate(&f.ev1) != hipSuccess ||
         hipHostMalloc(&h, 2 * (PS_MAX_ROUNDS + 1) * kNumCtr * 8, hipHostMallocMapped | hipHostMallocCoherent) !=
             hipSuccess) {
       ps_destroy(e);

@@ -131,9 +131,9 @@ class LoopbackTransport final : public Transport {
   LoopbackTransport(LoopbackGroup* g, int rank, int device, bool copy)
       : g_(g), rank_(rank), device_(device), copy_(copy) {
     (void)hipSetDevice(device_);
-    (void)hipEventCreateWithFlags(&sent_, hipEventDisableTiming);
-    for (auto& r : read_) (void)hipEventCreateWithFlags(&r, hipEventDisableTiming);
-    for (auto& r : used_) (void)hipEventCreateWithFlags(&r, hipEventDisableTiming);  // (never recorded: no-op waits)
+    (void)hipEventCreateWithFlags(&sent_, kStreamEvent);
+    for (auto& r : read_) (void)hipEventCreateWithFlags(&r, kStreamEvent);
+    for (auto& r : used_) (void)hipEventCreateWithFlags(&r, kStreamEvent);  // (never recorded: no-op waits)
     for (int k = 0; k < 2; ++k) g_->slot[rank_].read[k] = read_[k];
     for (uint32_t k = 0; k < kSendBufs; ++k) g_->slot[rank_].used[k] = used_[k];
   }

@@ -24,6 +24,15 @@ namespace psamd {
 // part r % kSendBufs), so that a round's readers and the writers of the
 // round after it need not wait for each other (zero copy: reuse()).
 constexpr uint32_t kSendBufs = 3;
+// Events that only order streams of this device (cross-stream waits, the
+// prefix/gate/reduce hand-offs, the loopback exchange): a device-scope
+// release.  The default system-scope fence writes back and invalidates the
+// caches at every record -- ~10 us on the recording queue after a launch that
+// wrote rows (cfg2: the gap between a window's chain and the next window).
+constexpr unsigned kStreamEvent = hipEventDisableTiming | hipEventReleaseToDevice;
+// A window's start mark: timing only (its end event keeps the system fence:
+// the host reads the window's counters from pinned memory after it).
+constexpr unsigned kStartEvent = hipEventReleaseToDevice;
 }  // namespace psamd
 
 namespace psamd {

@@ -236,6 +236,7 @@ struct ps_engine {
   // k_flood runs the leading rounds writing at most this many row bytes (with
   // chains after it: 4 MB; 16 MB was best before them, profiles/r03/ab_flood_top.txt)
   uint64_t flood_top_bytes = 4ull << 20;
+  uint32_t flood_min_rounds = 4;  // k_flood only for at least this many leading rounds (ps_plan_opts)
   uint32_t flood_epoch = 0;   // granule tag of the last launch (granules are never reset)
   uint32_t flood_spin_ticks = 200000000u;  // dependency-wait bound: 2 s of s_memrealtime (100 MHz); PSAMD_FLOOD_SPIN_TICKS
   psamd::FloodPlan flood;
@@ -384,6 +385,7 @@ struct ps_engine {
   bool overlap_on = true;
   uint32_t overlap_min_rounds = 12;
   uint64_t overlap_min_bytes = 512ull << 20;  // row bytes of the window at least (PSAMD_OVERLAP_BYTES)
+  uint64_t reduce_fork_bytes = 0;              // (A/B) windows of fewer row bytes reduce on their own stream
   hipStream_t pstream = nullptr;
   hipStream_t rstream = nullptr;  // a pipelined window's counter reduce, beside the next window
   hipEvent_t ev_gate[2] = {nullptr, nullptr}, ev_pre = nullptr, ev_end = nullptr;

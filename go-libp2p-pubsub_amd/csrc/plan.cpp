@@ -501,10 +501,14 @@ bool deep_window(const ps_engine* e, const WindowLayout& L) {
   return rows >= e->overlap_min_bytes;
 }
 
+// (Fewer than flood_min_rounds leading rounds cost less as a chain launch:
+// k_flood's dependency hand-offs are a few us per round -- cfg2, 3 rounds:
+// 0.066 ms/step with k_flood, 0.058 without; cfg4, 5 rounds: 0.447 with,
+// 0.457 without; profiles/r04/ab/NOTES.md.)
 uint32_t plan_flood_rounds(const ps_engine* e, const WindowLayout& L) {
   uint32_t r = 0;
   while (r < L.planned0 && e->pull.bytes[r + 1] <= e->flood_top_bytes) ++r;
-  return r;
+  return r >= e->flood_min_rounds ? r : 0;
 }
 
 // One persistent launch (k_flood, flood.hip): every level of every active

@@ -506,7 +506,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   if (pcap && !e->pstream) {  // (created on first use: multi-rank engines never need them)
     HIP_TRY(hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking), "prefix stream");
     for (hipEvent_t* ev : {&e->ev_gate[0], &e->ev_gate[1], &e->ev_pre})
-      HIP_TRY(hipEventCreateWithFlags(ev, hipEventDisableTiming), "overlap events");
+      HIP_TRY(hipEventCreateWithFlags(ev, kStreamEvent), "overlap events");
   }
   std::vector<uint64_t> gkey;
   if (pcap)
@@ -911,9 +911,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     // window's first launches (its partial slots and descriptors are this
     // slot's; ps_wait waits for it through the window's end event)
     hipStream_t rs = s;
-    if (direct && world == 1) {  // (every pipelined one-rank window: the next one's launches never wait for it)
+    if (direct && world == 1 && total >= e->reduce_fork_bytes) {  // (the next window's launches never wait for it)
       if (!e->rstream) HIP_TRY(hipStreamCreateWithFlags(&e->rstream, hipStreamNonBlocking), "reduce stream");
-      if (!e->ev_end) HIP_TRY(hipEventCreateWithFlags(&e->ev_end, hipEventDisableTiming), "reduce event");
+      if (!e->ev_end) HIP_TRY(hipEventCreateWithFlags(&e->ev_end, kStreamEvent), "reduce event");
       HIP_TRY(hipEventRecord(e->ev_end, s), "event");
       HIP_TRY(hipStreamWaitEvent(e->rstream, e->ev_end, 0), "reduce wait");
       rs = e->rstream;

@@ -97,7 +97,8 @@ class PlanOpts(C.Structure):
                 ("chain_max_groups", C.c_uint32), ("chain_tail", C.c_uint32), ("chain_words", C.c_uint32),
                 ("flood_words", C.c_uint32), ("pad_words", C.c_uint32), ("overlap", C.c_uint32),
                 ("overlap_min_rounds", C.c_uint32), ("xchg_overlap", C.c_int32), ("gpu_build", C.c_uint32),
-                ("flood_spin_ticks", C.c_uint32), ("chain_nt", C.c_uint32), ("chain_waves", C.c_uint32)]
+                ("flood_spin_ticks", C.c_uint32), ("chain_nt", C.c_uint32), ("chain_waves", C.c_uint32),
+                ("flood_min_rounds", C.c_uint32), ("reserved", C.c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

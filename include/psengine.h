@@ -200,6 +200,9 @@ typedef struct ps_plan_opts {
                                   levels non-temporally, 0: plain stores (1)    */
   uint32_t chain_waves;        /* chain launches: resident waves per CU at most,
                                   1..16 (an LDS pad), 0: as many as fit (12)    */
+  uint32_t flood_min_rounds;   /* k_flood only when it would run at least this many
+                                  leading rounds; fewer go to chain launches (4) */
+  uint32_t reserved;
 } ps_plan_opts;
 
 int ps_plan_opts_default(ps_plan_opts* out);

@@ -41,7 +41,7 @@ def run_mode(monkeypatch, flood, n, topics, live, msg_topics, record=True, start
     leading rounds writing at most that many row bytes, k_pull the rest
     (default: 4 MB, every round of these small trees)."""
     # (deep windows plan no k_flood while the cross-window overlap is on)
-    opts = {"flood": int(flood), "overlap": 0 if flood else 1}
+    opts = {"flood": int(flood), "overlap": 0 if flood else 1, "flood_min_rounds": 1}
     if top is not None:
         opts["flood_top_bytes"] = top
     if words is not None:
@@ -212,7 +212,7 @@ def test_flood_follows_live_changes(monkeypatch):
     live = np.ones(n, dtype=np.uint8)
     kids = np.nonzero(parent == 0)[0]
     grand = np.nonzero(np.isin(parent, kids))[0]
-    with PE.Engine(n, 1, record_hops=True, plan={"flood": 1, "overlap": 0}) as eng:
+    with PE.Engine(n, 1, record_hops=True, plan={"flood": 1, "overlap": 0, "flood_min_rounds": 1}) as eng:
         eng.set_tree(0, 0, parent)
         for step, change in enumerate([None, kids[:1], grand[:3], None, "revive"]):
             if isinstance(change, str):

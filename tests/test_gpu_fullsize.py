@@ -75,7 +75,8 @@ def cfg4_tree():
 
 def test_cfg2_full_size_dead_mask_against_oracle():
     """cfg2 (100k peers, TreeOpts{8,20}, 10k burst) on the production
-    instance: k_flood + k_pull_pair / k_pull at fan-out 8-20 with dead peers."""
+    instance: chain launches from round 1 (3 leading rounds are below
+    ps_plan_opts.flood_min_rounds) at fan-out 8-20 with dead peers."""
     wl = WL.cfg2()
     with PE.Engine(wl.n_peers, 1, seed=wl.seed) as eng:
         WL.build_engine_topics(eng, wl)
@@ -85,7 +86,7 @@ def test_cfg2_full_size_dead_mask_against_oracle():
         eng.set_live(live)
         first = eng.publish(wl.msg_topics)
         st = eng.run()
-        assert st.expand_mode == PE.MODE_FLOOD
+        assert st.expand_mode == PE.MODE_LEVEL_PULL and PE.K_CHAIN in set(st.round_kernel)
         check_run([st], wl.n_msgs, tot, hist)
         for m in sampled(wl.n_msgs):
             assert np.array_equal(eng.delivered(first + int(m)).astype(bool), reach), int(m)

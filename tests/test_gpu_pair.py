@@ -136,7 +136,7 @@ def test_pair_after_flood(monkeypatch, seed):
     for pair in (False, True):
         # (overlap 0: deep windows plan no k_flood otherwise)
         opts = {"flood_top_bytes": top, "chain_max": 2 if pair else 1, "chain_max_groups": 2 if pair else 1,
-                "overlap": 0}
+                "overlap": 0, "flood_min_rounds": 1}
         with PE.Engine(n, len(topics), record_hops=True, plan=opts) as eng:
             for t, (root, parent) in enumerate(topics):
                 eng.set_tree(t, root, parent)

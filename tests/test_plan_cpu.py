@@ -569,7 +569,7 @@ def test_plan_opts_defaults_pinned():
                  "flood": 1, "chain_max": 4, "chain_max_groups": 6, "chain_tail": 1, "chain_words": 8192,
                  "flood_words": 2048, "pad_words": 16, "overlap": 1, "overlap_min_rounds": 12,
                  "xchg_overlap": -1, "gpu_build": 1, "flood_spin_ticks": 200_000_000, "chain_nt": 1,
-                 "chain_waves": 12}, d
+                 "chain_waves": 12, "flood_min_rounds": 4, "reserved": 0}, d
     parent = np.full(64, NONE, dtype=np.uint32)
     parent[1:] = (np.arange(1, 64) - 1) // 2
     env = dict(os.environ)
