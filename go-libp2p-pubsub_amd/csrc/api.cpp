@@ -163,6 +163,8 @@ static void read_switches(ps_engine* e) {
     o.flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
   if (const char* v = std::getenv("PSAMD_FLOOD_SPIN_TICKS")) o.flood_spin_ticks = static_cast<uint32_t>(std::strtoul(v, nullptr, 0));
   if (const char* v = std::getenv("PSAMD_FLOOD_TOP_BYTES")) o.flood_top_bytes = std::strtoull(v, nullptr, 0);
+  if (const char* v = std::getenv("PSAMD_LB_PLACE")) e->lb_place = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_PULL_CAP_N")) e->pull_cap_n = static_cast<uint32_t>(std::atoi(v));
   if (const char* v = std::getenv("PSAMD_REDUCE_FORK_BYTES")) e->reduce_fork_bytes = std::strtoull(v, nullptr, 10);
   if (const char* v = std::getenv("PSAMD_FLOOD_MIN_ROUNDS"))
     o.flood_min_rounds = static_cast<uint32_t>(std::max(1, std::atoi(v)));
@@ -333,7 +335,12 @@ int ps_topic_join(ps_engine* e, uint32_t topic, const uint32_t* peers, size_t n,
   TopicHost* T = join_topic(e, topic);
   if (!T) return PS_E_STATE;
   int first = PS_OK;
+  // a joiner's own line is written when it attaches, at the end of a walk
+  // of ~17 dependent hops: fetched a few joins ahead (tools/probe/tree_bench)
+  constexpr size_t kAhead = 8;
+  for (size_t i = 0; i < std::min(n, kAhead); ++i) T->tree.prefetch_join(peers[i]);
   for (size_t i = 0; i < n; ++i) {
+    if (i + kAhead < n) T->tree.prefetch_join(peers[i + kAhead]);
     int rc = T->tree.subscribe(peers[i]);
     if (status_out) status_out[i] = rc;
     if (rc && !first) {

@@ -1,6 +1,8 @@
 // dist.cpp -- RCCL and in-process loopback frontier-exchange transports.
 #include "dist.hpp"
 
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 #include <rccl/rccl.h>
@@ -116,6 +118,15 @@ struct LoopbackGroup {
     return true;
   }
 };
+
+unsigned stream_event_flags() {
+  static const unsigned f = [] {
+    const char* v = std::getenv("PSAMD_SYSTEM_EVENTS");
+    return (v && std::atoi(v) != 0) ? static_cast<unsigned>(hipEventDisableTiming)
+                                     : static_cast<unsigned>(hipEventDisableTiming | hipEventReleaseToDevice);
+  }();
+  return f;
+}
 
 LoopbackGroup* loopback_create(int world) {
   if (world < 1) return nullptr;

@@ -29,7 +29,9 @@ constexpr uint32_t kSendBufs = 3;
 // release.  The default system-scope fence writes back and invalidates the
 // caches at every record -- ~10 us on the recording queue after a launch that
 // wrote rows (cfg2: the gap between a window's chain and the next window).
-constexpr unsigned kStreamEvent = hipEventDisableTiming | hipEventReleaseToDevice;
+// (A/B: PSAMD_SYSTEM_EVENTS=1 restores the system-scope default)
+unsigned stream_event_flags();
+#define kStreamEvent (::psamd::stream_event_flags())
 // A window's start mark: timing only (its end event keeps the system fence:
 // the host reads the window's counters from pinned memory after it).
 constexpr unsigned kStartEvent = hipEventReleaseToDevice;

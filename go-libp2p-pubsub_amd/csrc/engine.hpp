@@ -213,6 +213,7 @@ struct ps_engine {
   bool host_only = false;        // a planner probe (psengine_plan.h): no device
   psamd::WindowLayout probe;     // the probe's last planned window
   bool host_timing = false;      // PSAMD_HOST_TIMING=1: host phase times to stderr
+  bool lb_place = true;           // levels placed by one look-back launch each (A/B: PSAMD_LB_PLACE=0)
   uint32_t small_place = 512;    // top levels up to this many nodes placed by one block
   // GPU rebuild of the node space: on by default for one
   // rank and tree topics (PSAMD_GPU_BUILD=0: host build)
@@ -224,7 +225,7 @@ struct ps_engine {
   size_t pairs_pinned_cap = 0;       // (u32 words)
   std::vector<size_t> pair_off;
   psamd::DevBuf d_tpar, d_orph, d_anc0, d_anc1, d_dep0, d_dep1, d_keys0, d_skeys, d_local, d_deg, d_first, d_lvl,
-      d_gstat, d_cub, d_pairs, d_live, d_roots, d_cnt, d_fidx, d_childoff;
+      d_gstat, d_cub, d_pairs, d_live, d_roots, d_cnt, d_fidx, d_childoff, d_lbstat;
   std::chrono::steady_clock::time_point t_run0;
   // k_flood: a single-rank level window's leading rounds in
   // one persistent launch; PSAMD_FLOOD=0 runs per-round launches instead
@@ -385,7 +386,8 @@ struct ps_engine {
   bool overlap_on = true;
   uint32_t overlap_min_rounds = 12;
   uint64_t overlap_min_bytes = 512ull << 20;  // row bytes of the window at least (PSAMD_OVERLAP_BYTES)
-  uint64_t reduce_fork_bytes = 0;              // (A/B) windows of fewer row bytes reduce on their own stream
+  uint64_t reduce_fork_bytes = 0;
+  uint32_t pull_cap_n = 0;                     // (A/B) N ranks: k_pull nt blocks per CU at most (0: no cap)              // (A/B) windows of fewer row bytes reduce on their own stream
   hipStream_t pstream = nullptr;
   hipStream_t rstream = nullptr;  // a pipelined window's counter reduce, beside the next window
   hipEvent_t ev_gate[2] = {nullptr, nullptr}, ev_pre = nullptr, ev_end = nullptr;

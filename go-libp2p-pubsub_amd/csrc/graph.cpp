@@ -512,7 +512,8 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   HIP_TRY(e->d_gstat.ensure(static_cast<size_t>(nt) * 4 * 4), "alloc build stats");
   HIP_TRY(e->d_lvl.ensure(static_cast<size_t>(nt) * 512 * 4), "alloc level tables");
   size_t cub_bytes = 0, scan_bytes = 0;
-  HIP_TRY(sort_keys(nullptr, &cub_bytes, nullptr, nullptr, n, s), "sort size");
+  const BuildKey kf = build_key(n);
+  HIP_TRY(sort_keys(nullptr, &cub_bytes, nullptr, nullptr, n, kf, s), "sort size");
   HIP_TRY(e->d_cub.ensure(std::max<size_t>(cub_bytes, 16)), "alloc sort temp");
   // [t][reach, max depth, max fan-out, unresolved]
   uint32_t* gstat = e->d_gstat.as<uint32_t>();
@@ -534,14 +535,14 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
       HIP_TRY(launch_depth_keys(e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n, n, T.root, jumps[t],
                                 e->d_anc0.as<uint32_t>(), e->d_anc1.as<uint32_t>(),
                                 e->d_dep0.as<uint32_t>(), e->d_dep1.as<uint32_t>(),
-                                e->d_keys0.as<uint64_t>(), gstat + 4 * t, s),
+                                e->d_keys0.as<uint64_t>(), gstat + 4 * t, kf, s),
               "depth");
       size_t tb = e->d_cub.bytes;
       HIP_TRY(sort_keys(e->d_cub.p, &tb, e->d_keys0.as<uint64_t>(),
-                        e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n, s),
+                        e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n, kf, s),
               "sort");
       HIP_TRY(launch_level_starts(e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n,
-                                  e->d_lvl.as<uint32_t>() + 512 * t, s),
+                                  e->d_lvl.as<uint32_t>() + 512 * t, kf, s),
               "level starts");
     }
     // (level starts of unreachable peers' keys land in slot 255: ignored)
@@ -613,7 +614,7 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
     const uint16_t tt = static_cast<uint16_t>(t);
     HIP_TRY(hipMemsetAsync(cnt, 0, static_cast<size_t>(n) * 4, s), "clear fan-out by peer");
     HIP_TRY(hipMemsetAsync(fidx, 0xFF, static_cast<size_t>(n) * 4, s), "clear first child index");
-    HIP_TRY(launch_child_stats(keys, T.n_nodes, cnt, fidx, s), "child stats");
+    HIP_TRY(launch_child_stats(keys, T.n_nodes, cnt, fidx, kf, s), "child stats");
     // the small top levels (and their parents) go in one single-block launch
     auto lvl_end = [&](uint32_t d) { return d == depth ? T.n_nodes : lh[512 * t + d + 1]; };
     uint32_t d_small = 1;
@@ -624,17 +625,36 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
       HIP_TRY(launch_place_small(keys, e->d_lvl.as<uint32_t>() + 512 * t, d_small, depth, T.n_nodes, T.nbase, tt,
                                  cnt, fidx, e->d_node_peer.as<uint32_t>(), e->d_node_topic.as<uint16_t>(),
                                  e->d_local.as<uint32_t>(), e->d_node_parent.as<uint32_t>(),
-                                 e->d_deg.as<uint32_t>(), e->d_first.as<uint32_t>(), s),
+                                 e->d_deg.as<uint32_t>(), e->d_first.as<uint32_t>(), kf, s),
               "place small levels");
     } else {
       HIP_TRY(launch_place_root(keys, T.nbase, tt, cnt, e->d_node_peer.as<uint32_t>(),
                                 e->d_node_topic.as<uint16_t>(), e->d_local.as<uint32_t>(),
-                                e->d_node_parent.as<uint32_t>(), e->d_deg.as<uint32_t>(), s),
+                                e->d_node_parent.as<uint32_t>(), e->d_deg.as<uint32_t>(), kf, s),
               "place root");
     }
+    // the levels below: one look-back launch each (their tiles' status
+    // words zeroed once per topic)
+    size_t tiles = 0;
+    for (uint32_t d = d_small; d <= depth; ++d) tiles += lb_tiles(lh[512 * t + d] - lh[512 * t + d - 1]);
+    if (tiles) {
+      HIP_TRY(e->d_lbstat.ensure(tiles * 8), "alloc look-back status");
+      HIP_TRY(hipMemsetAsync(e->d_lbstat.p, 0, tiles * 8, s), "clear look-back status");
+    }
+    uint64_t* lbst = e->d_lbstat.as<uint64_t>();
     for (uint32_t d = d_small; d <= depth; ++d) {
       const uint32_t plo = lh[512 * t + d - 1];
       const uint32_t lo = lh[512 * t + d];
+      if (e->lb_place) {
+        HIP_TRY(launch_place_level_lb(keys, lo - plo, T.nbase + plo, T.nbase + lo, cnt, fidx, tt,
+                                      e->d_node_peer.as<uint32_t>(), e->d_node_topic.as<uint16_t>(),
+                                      e->d_local.as<uint32_t>(), e->d_node_parent.as<uint32_t>(),
+                                      e->d_deg.as<uint32_t>(), e->d_first.as<uint32_t>(), lbst, gstat + 4 * t + 3, kf,
+                                      s),
+                "place level");
+        lbst += lb_tiles(lo - plo);
+        continue;
+      }
       const uint32_t hi = d == depth ? T.n_nodes : lh[512 * t + d + 1];
       size_t tb = e->d_cub.bytes;
       HIP_TRY(scan_u32(e->d_cub.p, &tb, e->d_deg.as<uint32_t>() + T.nbase + plo, childoff, lo - plo, s),
@@ -642,7 +662,7 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
       HIP_TRY(launch_place_level(keys, lo, hi, T.nbase, T.nbase + plo, childoff, cnt, fidx, tt,
                                  e->d_node_peer.as<uint32_t>(), e->d_node_topic.as<uint16_t>(),
                                  e->d_local.as<uint32_t>(), e->d_node_parent.as<uint32_t>(),
-                                 e->d_deg.as<uint32_t>(), e->d_first.as<uint32_t>(), s),
+                                 e->d_deg.as<uint32_t>(), e->d_first.as<uint32_t>(), kf, s),
               "place level");
     }
   }
@@ -665,6 +685,11 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   HIP_TRY(hipMemcpyAsync(lh.data(), lvl, lh.size() * 4, hipMemcpyDeviceToHost, s), "read level tables");
   HIP_TRY(hipMemcpyAsync(gs.data(), gstat, gs.size() * 4, hipMemcpyDeviceToHost, s), "read build stats");
   HIP_TRY(hipStreamSynchronize(s), "sync");
+  for (uint32_t t = 0; t < nt; ++t)
+    if (e->topics[t].n_nodes && gs[4 * t + 3]) {  // a stalled placement look-back: build on the host
+      *fallback = true;
+      return PS_OK;
+    }
   if (e->host_timing) {
     auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
     std::fprintf(stderr, "[psengine] gpu build: deltas %.3f ms (%zu), depth+sort+readback %.3f ms, "

@@ -1344,14 +1344,31 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
 }
 
 }  // namespace
+
+namespace {
+// Dynamic LDS that caps a launch at `waves` resident
+// workgroups per CU (160 KB of LDS per CU, allocated in 512-B granules): the
+// static LDS plus the pad stays above 160 KB / (waves + 1).  0: no cap.
+template <class K>
+size_t lds_cap_pad(K kernel, uint32_t waves) {
+  if (waves == 0) return 0;
+  hipFuncAttributes fa{};
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kernel)) != hipSuccess) return 0;
+  const size_t per = (160u * 1024u) / waves - 512u;
+  return per > fa.sharedSizeBytes ? per - fa.sharedSizeBytes : 0;
+}
+}  // namespace
+
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                       uint32_t grid, uint32_t round, bool record, bool nt, bool cap, hipStream_t s) {
+                       uint32_t grid, uint32_t round, bool record, bool nt, bool cap, uint32_t cap_blocks,
+                       hipStream_t s) {
   if (n_chunks == 0 || grid == 0) return hipSuccess;
   // cap: the large (nt) rounds run at most 5 blocks per CU -- 10 KB of LDS
   // left unused per block caps residency (8 blocks: 6 % slower on cfg3's big
   // rounds on one rank); small rounds keep full residency, they need the
   // waves in flight
-  const size_t kBigRoundLdsPad = cap ? 10240 : 0;
+  // (cap_blocks, N ranks: an A/B cap of blocks per CU, PSAMD_PULL_CAP_N)
+  const size_t kBigRoundLdsPad = cap ? 10240 : cap_blocks ? lds_cap_pad(k_pull<false, true>, cap_blocks) : 0;
   if (record)  // parity runs: one variant
     hipLaunchKernelGGL((k_pull<true, false>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
   else if (nt)
@@ -1411,19 +1428,6 @@ hipError_t launch_chain_ranges(ChainChunk* chunks, uint32_t n, const uint32_t* r
   return hipGetLastError();
 }
 
-namespace {
-// Dynamic LDS that caps a launch of a one-wave kernel at `waves` resident
-// workgroups per CU (160 KB of LDS per CU, allocated in 512-B granules): the
-// static LDS plus the pad stays above 160 KB / (waves + 1).  0: no cap.
-template <class K>
-size_t lds_cap_pad(K kernel, uint32_t waves) {
-  if (waves == 0) return 0;
-  hipFuncAttributes fa{};
-  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kernel)) != hipSuccess) return 0;
-  const size_t per = (160u * 1024u) / waves - 512u;
-  return per > fa.sharedSizeBytes ? per - fa.sharedSizeBytes : 0;
-}
-}  // namespace
 
 hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32_t n_chunks, uint32_t round,
                              bool record, bool nt, bool slices, bool inner_nt, uint32_t waves_per_cu,

@@ -47,6 +47,12 @@ class SubscriptionTree {
   // parent's list, so close_client() finds them resident.
   void prefetch_leave(uint32_t peer, int stage) const;
   void prefetch_peer(uint32_t peer) const { __builtin_prefetch(&rec_[peer]); }  // state, upstream, children
+  // a joiner's own line and touched-list slot (written when it attaches)
+  void prefetch_join(uint32_t peer) const {
+    if (peer >= n_) return;
+    __builtin_prefetch(&rec_[peer], 1);
+    __builtin_prefetch(&touched_at_[peer], 1);
+  }
   int close_host(uint32_t peer);    // abrupt
   // Called once per message that floods this topic: lazy prune and repair of
   // failed writes at every node the message reached (rule Q3).  `reach`, if

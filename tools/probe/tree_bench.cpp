@@ -8,6 +8,7 @@
 //       tools/probe/tree_bench.cpp go-libp2p-pubsub_amd/csrc/tree.cpp -o /tmp/tree_bench
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstdio>
 #include <random>
 #include <vector>
@@ -49,8 +50,11 @@ int main(int argc, char** argv) {
       member[p] = 0;
     }
     auto bb = clk::now();
-    for (uint32_t p : join)
-      if (T.subscribe(p) == 0) member[p] = 1;
+    const bool pf = std::getenv("TB_PREFETCH") != nullptr;
+    for (size_t i = 0; i < join.size(); ++i) {
+      if (pf && i + 8 < join.size()) T.prefetch_join(join[i + 8]);
+      if (T.subscribe(join[i]) == 0) member[join[i]] = 1;
+    }
     auto c = clk::now();
     T.after_message(nullptr);
     T.take_touched(touched);
