@@ -163,6 +163,8 @@ static void read_switches(ps_engine* e) {
     o.flood_words = static_cast<uint32_t>(std::min(1 << 16, std::max(64, std::atoi(v))));
   if (const char* v = std::getenv("PSAMD_FLOOD_SPIN_TICKS")) o.flood_spin_ticks = static_cast<uint32_t>(std::strtoul(v, nullptr, 0));
   if (const char* v = std::getenv("PSAMD_FLOOD_TOP_BYTES")) o.flood_top_bytes = std::strtoull(v, nullptr, 0);
+  if (const char* v = std::getenv("PSAMD_UPLOAD_REUSE")) e->upload_reuse = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_SIG_WINDOWS")) e->sig_windows = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_LB_PLACE")) e->lb_place = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_CAP_N")) e->pull_cap_n = static_cast<uint32_t>(std::atoi(v));
   if (const char* v = std::getenv("PSAMD_REDUCE_FORK_BYTES")) e->reduce_fork_bytes = std::strtoull(v, nullptr, 10);
@@ -247,7 +249,7 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
   for (auto& f : e->infl) {
     void* h = nullptr;
     if (hipEventCreateWithFlags(&f.ev0, kStartEvent) != hipSuccess || hipEventCreate(&f.ev1) != hipSuccess ||
-        hipHostMalloc(&h, 2 * (PS_MAX_ROUNDS + 1) * kNumCtr * 8, hipHostMallocMapped | hipHostMallocCoherent) !=
+        hipHostMalloc(&h, 2 * (PS_MAX_ROUNDS + 1) * kNumCtr * 8 + 64, hipHostMallocMapped | hipHostMallocCoherent) !=
             hipSuccess) {
       ps_destroy(e);
       return PS_E_DEVICE;
@@ -260,6 +262,9 @@ int ps_create(const ps_config* cfg, ps_engine** out) {
     }
     f.hs_dev = static_cast<uint64_t*>(hd);
     f.ha = f.hs + (PS_MAX_ROUNDS + 1) * kNumCtr;
+    f.sig = f.hs + 2 * (PS_MAX_ROUNDS + 1) * kNumCtr;
+    f.sig_dev = f.hs_dev + 2 * (PS_MAX_ROUNDS + 1) * kNumCtr;
+    f.sig[0] = 0;
   }
   e->topics.resize(cfg->n_topics);
   e->live.assign(cfg->n_peers, 1);

@@ -34,6 +34,7 @@ inline uint32_t ceil_div(uint64_t a, uint64_t b) { return static_cast<uint32_t>(
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  uint64_t gen = 0;  // allocations made (a shadow of the contents is valid for one)
   DevBuf() = default;
   DevBuf(const DevBuf&) = delete;
   DevBuf& operator=(const DevBuf&) = delete;
@@ -55,6 +56,7 @@ struct DevBuf {
       return e;
     }
     bytes = n;
+    ++gen;
     if (fresh) *fresh = true;
     return hipSuccess;
   }
@@ -213,7 +215,18 @@ struct ps_engine {
   bool host_only = false;        // a planner probe (psengine_plan.h): no device
   psamd::WindowLayout probe;     // the probe's last planned window
   bool host_timing = false;      // PSAMD_HOST_TIMING=1: host phase times to stderr
-  bool lb_place = true;           // levels placed by one look-back launch each (A/B: PSAMD_LB_PLACE=0)
+  bool lb_place = true;
+  bool sig_windows = true;
+  // per-window uploads (topic table, seeds, descriptors) kept on the device:
+  // the bytes last staged into each buffer, skipped when a window repeats them
+  struct UploadShadow {
+    uint64_t gen = 0;
+    std::vector<uint8_t> data;
+  };
+  std::map<const psamd::DevBuf*, UploadShadow> upload_shadow;
+  bool upload_reuse = true;  // (A/B: PSAMD_UPLOAD_REUSE=0)
+  bool defer_into_signalled = false;  // the window being enqueued raises its flag in its reduce        // pipelined one-rank windows end with a pinned flag, not an event (A/B: PSAMD_SIG_WINDOWS=0)
+  uint64_t sig_seq = 0;           // levels placed by one look-back launch each (A/B: PSAMD_LB_PLACE=0)
   uint32_t small_place = 512;    // top levels up to this many nodes placed by one block
   // GPU rebuild of the node space: on by default for one
   // rank and tree topics (PSAMD_GPU_BUILD=0: host build)
@@ -225,7 +238,7 @@ struct ps_engine {
   size_t pairs_pinned_cap = 0;       // (u32 words)
   std::vector<size_t> pair_off;
   psamd::DevBuf d_tpar, d_orph, d_anc0, d_anc1, d_dep0, d_dep1, d_keys0, d_skeys, d_local, d_deg, d_first, d_lvl,
-      d_gstat, d_cub, d_pairs, d_live, d_roots, d_cnt, d_fidx, d_childoff, d_lbstat;
+      d_gstat, d_cub, d_pairs, d_live, d_roots, d_cnt, d_fidx, d_childoff, d_lbstat, d_sigctr;
   std::chrono::steady_clock::time_point t_run0;
   // k_flood: a single-rank level window's leading rounds in
   // one persistent launch; PSAMD_FLOOD=0 runs per-round launches instead
@@ -349,6 +362,12 @@ struct ps_engine {
     uint64_t* hs = nullptr;      // pinned: (PS_MAX_ROUNDS + 1) x kNumCtr counters
     uint64_t* hs_dev = nullptr;  // hs, device-mapped (k_reduce_rounds writes it)
     uint64_t* ha = nullptr;      // pinned: apply counters of a multi-GPU window
+    // signalled windows (no end event): sig[0] = the window's sequence number
+    // once done, sig[1] / sig[2] = its start / end s_memrealtime stamps
+    uint64_t* sig = nullptr;
+    uint64_t* sig_dev = nullptr;
+    uint64_t seq = 0;
+    bool signalled = false;
     uint32_t planned0 = 0;
     int32_t world = 1;
     std::vector<uint8_t> kinds;  // round_kind of the window

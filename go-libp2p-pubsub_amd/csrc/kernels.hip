@@ -85,6 +85,7 @@ __global__ __launch_bounds__(kBlock) void k_window_init(const TopicDev* __restri
   for (uint64_t i = static_cast<uint64_t>(bid) * kBlock + threadIdx.x; i < ws.zero_words;
        i += static_cast<uint64_t>(nb) * kBlock)
     ws.zero[i] = 0;
+  if (ws.t0 && bid == 0 && threadIdx.x == 0) *ws.t0 = __builtin_amdgcn_s_memrealtime();
   const TopicDev T = topics[blockIdx.y];
   if (T.W == 0 || T.n_nodes == 0) return;
   const bool mesh = (T.flags & kTopicMesh) != 0;
@@ -799,7 +800,8 @@ __device__ __forceinline__ void block_reduce_ctrs(const uint64_t* __restrict__ p
 __global__ __launch_bounds__(kBlock) void k_reduce_rounds(const uint64_t* __restrict__ partials,
                                                           const uint32_t* __restrict__ desc,
                                                           uint64_t* __restrict__ round_stats,
-                                                          uint64_t* __restrict__ host_stats) {
+                                                          uint64_t* __restrict__ host_stats,
+                                                          WindowSignal sig) {
   constexpr uint32_t kAct = (kBlock / kNumCtr) * kNumCtr;
   __shared__ uint64_t red[kBlock];
   const uint32_t q = blockIdx.x;
@@ -829,7 +831,19 @@ __global__ __launch_bounds__(kBlock) void k_reduce_rounds(const uint64_t* __rest
     if (host_stats) {  // fine-grained pinned host rows: visible to the host once the kernel ends
       __hip_atomic_store(host_stats + static_cast<uint64_t>(q) * kNumCtr + threadIdx.x, t, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
+      if (!sig.flag) __threadfence_system();  // (a signalled window fences once, below)
+    }
+  }
+  // a signalled window: the last block to finish stamps the end and raises
+  // the flag (after every block's rows; the counter re-zeroes itself)
+  if (sig.flag) __syncthreads();  // (the block's row stores precede its fence)
+  if (sig.flag && threadIdx.x == 0) {
+    __threadfence_system();
+    if (atomicAdd(sig.ctr, 1u) == gridDim.x - 1) {
+      sig.flag[2] = __builtin_amdgcn_s_memrealtime();
       __threadfence_system();
+      __hip_atomic_store(sig.flag, sig.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      atomicExch(sig.ctr, 0u);
     }
   }
 }
@@ -936,6 +950,20 @@ __global__ __launch_bounds__(kBlock) void k_digest(const uint64_t* __restrict__ 
 
 }  // namespace
 
+namespace {
+__global__ void k_window_done(uint64_t* sig, uint64_t seq) {
+  if (threadIdx.x) return;
+  sig[2] = __builtin_amdgcn_s_memrealtime();
+  __threadfence_system();
+  __hip_atomic_store(sig, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+}  // namespace
+
+hipError_t launch_window_done(uint64_t* sig, uint64_t seq, hipStream_t s) {
+  hipLaunchKernelGGL(k_window_done, dim3(1), dim3(64), 0, s, sig, seq);
+  return hipGetLastError();
+}
+
 hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_t* seen,
                               uint64_t* a0, uint64_t* a1, uint8_t* gen, uint32_t gen_cur,
                               bool any_mesh, const WindowStart& ws, hipStream_t s) {
@@ -1020,10 +1048,10 @@ hipError_t launch_stage_copy(const StageCopy& c, hipStream_t s) {
 }
 
 hipError_t launch_reduce_rounds(const uint64_t* partials, const uint32_t* desc, uint32_t n_rounds,
-                                uint64_t* round_stats, uint64_t* host_stats, hipStream_t s) {
-  if (n_rounds == 0) return hipSuccess;
+                                uint64_t* round_stats, uint64_t* host_stats, const WindowSignal& sig, hipStream_t s) {
+  if (n_rounds == 0) return sig.flag ? launch_window_done(sig.flag, sig.seq, s) : hipSuccess;
   hipLaunchKernelGGL(k_reduce_rounds, dim3(n_rounds + 1), dim3(kBlock), 0, s, partials, desc, round_stats,
-                     host_stats);
+                     host_stats, sig);
   return hipGetLastError();
 }
 

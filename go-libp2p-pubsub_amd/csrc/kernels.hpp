@@ -394,6 +394,19 @@ struct WindowStart {
   const SeedDev* seeds = nullptr;  // apply round-0 seeds (tree topics only)
   uint64_t* zero = nullptr;        // words to clear
   uint64_t zero_words = 0;
+  uint64_t* t0 = nullptr;          // (signalled windows) the start stamp, s_memrealtime into pinned memory
+};
+// A signalled window's end, after its reduce on the same stream: the end
+// stamp into sig[2], then seq into sig[0] (pinned; system-scope release) --
+// ps_wait polls it instead of waiting on an event, whose record costs the
+// queue ~10 us between windows (profiles/r04/cfg2)
+hipError_t launch_window_done(uint64_t* sig, uint64_t seq, hipStream_t s);
+// ... or raised by the reduce's last block (no launch of its own): ctr a
+// zeroed device word (left zero again)
+struct WindowSignal {
+  uint64_t* flag = nullptr;
+  uint32_t* ctr = nullptr;
+  uint64_t seq = 0;
 };
 hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_t* seen,
                               uint64_t* a0, uint64_t* a1, uint8_t* gen, uint32_t gen_cur,
@@ -444,7 +457,7 @@ hipError_t flood_blocks_per_cu(int* out);
 // host_stats (nullable): device-mapped pinned rows that receive the same
 // counters, so an asynchronous run needs no readback copy
 hipError_t launch_reduce_rounds(const uint64_t* partials, const uint32_t* desc, uint32_t n_rounds,
-                                uint64_t* round_stats, uint64_t* host_stats, hipStream_t s);
+                                uint64_t* round_stats, uint64_t* host_stats, const WindowSignal& sig, hipStream_t s);
 // second instance: entries the staged kernel leaves (mesh, split, wide rows,
 // fan-out > 64); writes the same counters to partials + n_waves*kNumCtr
 hipError_t launch_expand_direct(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid,

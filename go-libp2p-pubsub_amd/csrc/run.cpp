@@ -4,8 +4,10 @@
 // stream beside each round's locally fed chunks; compaction mode: k_expand +
 // frontier compaction), counters and readbacks.  DESIGN.md §5-§7.
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
+#include <thread>
 
 #include "engine.hpp"
 #include "gbuild.hpp"
@@ -122,6 +124,7 @@ struct Upload {
   void* dst;
   const void* src;
   size_t bytes;
+  const DevBuf* buf;  // dst's buffer (its upload shadow), nullable
 };
 // With `fold` set and the copy-kernel form, nothing is launched: *fold gets
 // the copies for a kernel that folds them in, and staged[i] the device-mapped
@@ -130,8 +133,24 @@ int stage_uploads(ps_engine* e, const Upload* ups, size_t n, hipStream_t s, Stag
                   const void** staged = nullptr) {
   if (fold) *fold = StageCopy{};
   for (size_t i = 0; staged && i < n; ++i) staged[i] = ups[i].dst;
+  // bytes a buffer already holds (the same slot's last upload, same
+  // allocation) are not staged again: the window reads them where they lie
+  // (device memory) instead of over PCIe
+  bool keep[8] = {};
+  for (size_t i = 0; i < n && i < 8; ++i) {
+    const Upload& u = ups[i];
+    if (!u.buf || !u.bytes || !e->upload_reuse) continue;
+    auto& sh = e->upload_shadow[u.buf];
+    if (sh.gen == u.buf->gen && sh.data.size() == u.bytes && std::memcmp(sh.data.data(), u.src, u.bytes) == 0) {
+      keep[i] = true;
+      continue;
+    }
+    sh.gen = u.buf->gen;
+    sh.data.assign(static_cast<const uint8_t*>(u.src), static_cast<const uint8_t*>(u.src) + u.bytes);
+  }
   size_t need = 0;
-  for (size_t i = 0; i < n; ++i) need += (ups[i].bytes + 255) & ~size_t(255);
+  for (size_t i = 0; i < n; ++i)
+    if (!(i < 8 && keep[i])) need += (ups[i].bytes + 255) & ~size_t(255);
   if (need == 0) return PS_OK;
   // the slot of the asynchronous run being enqueued (its previous user was
   // waited for before the run slot was reused); synchronous runs start with
@@ -157,7 +176,7 @@ int stage_uploads(ps_engine* e, const Upload* ups, size_t n, hipStream_t s, Stag
   StageCopy c{};
   size_t off = 0;
   for (size_t i = 0; i < n; ++i) {
-    if (!ups[i].bytes) continue;
+    if (!ups[i].bytes || (i < 8 && keep[i])) continue;
     std::memcpy(g.h + off, ups[i].src, ups[i].bytes);
     if (kernel) {
       if (staged && fold) staged[i] = g.d + off;
@@ -537,10 +556,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   WindowStart ws{};
   const void* staged[4] = {nullptr, nullptr, nullptr, nullptr};
   {
-    const Upload ups[4] = {{d_topics.p, tab.data(), tab.size() * sizeof(TopicDev)},
-                           {d_seeds.p, seeds.data(), seeds.size() * sizeof(SeedDev)},
-                           {d_woff.p, e->desc_host.data(), level ? e->desc_host.size() * 4 : 0},
-                           {d_groups.p, L.gtab.data(), L.gtab.size() * sizeof(GroupDev)}};
+    const Upload ups[4] = {{d_topics.p, tab.data(), tab.size() * sizeof(TopicDev), &d_topics},
+                           {d_seeds.p, seeds.data(), seeds.size() * sizeof(SeedDev), &d_seeds},
+                           {d_woff.p, e->desc_host.data(), level ? e->desc_host.size() * 4 : 0, &d_woff},
+                           {d_groups.p, L.gtab.data(), L.gtab.size() * sizeof(GroupDev), &d_groups}};
     const int rcu = stage_uploads(e, ups, 4, s, fold ? &ws.copy : nullptr, staged);
     if (rcu) return rcu;
   }
@@ -551,7 +570,16 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   }
   const bool seeds0_done = ws.seeds != nullptr;
   const bool partials_done = ws.zero != nullptr;
-  HIP_TRY(hipEventRecord(e->ev_run0, s), "event");
+  // a pipelined one-rank window on the main stream alone ends with a pinned
+  // flag and timestamps instead of events (ps_wait polls the flag): no event
+  // record between consecutive windows
+  const bool sigwin = e->sig_windows && e->defer_last && e->defer_into && level && world == 1 && !record &&
+                      !(e->cfg.flags & PS_F_TIME_KERNELS) && !pcap && planned0 <= PS_MAX_ROUNDS;
+  e->defer_into_signalled = false;
+  if (sigwin)
+    ws.t0 = e->defer_into->sig_dev + 1;
+  else
+    HIP_TRY(hipEventRecord(e->ev_run0, s), "event");
   const auto t_first = std::chrono::steady_clock::now();
   // new window generation: every tree row from older windows becomes stale
   if (++e->gen_cur > 255) {
@@ -911,7 +939,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     // window's first launches (its partial slots and descriptors are this
     // slot's; ps_wait waits for it through the window's end event)
     hipStream_t rs = s;
-    if (direct && world == 1 && total >= e->reduce_fork_bytes) {  // (the next window's launches never wait for it)
+    if (direct && world == 1 && !sigwin && total >= e->reduce_fork_bytes) {  // (the next window's launches never wait for it)
       if (!e->rstream) HIP_TRY(hipStreamCreateWithFlags(&e->rstream, hipStreamNonBlocking), "reduce stream");
       if (!e->ev_end) HIP_TRY(hipEventCreateWithFlags(&e->ev_end, kStreamEvent), "reduce event");
       HIP_TRY(hipEventRecord(e->ev_end, s), "event");
@@ -919,10 +947,23 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       rs = e->rstream;
     }
     reduce_side = rs != s;
+    // a signalled window: the reduce's last block raises its flag
+    WindowSignal wsig{};
+    if (sigwin && direct && !reduce_side && s == e->stream) {
+      if (!e->d_sigctr.p) {
+        HIP_TRY(e->d_sigctr.ensure(64), "alloc window counter");
+        HIP_TRY(hipMemsetAsync(e->d_sigctr.p, 0, 64, s), "clear window counter");
+      }
+      wsig.flag = e->defer_into->sig_dev;
+      wsig.ctr = e->d_sigctr.as<uint32_t>();
+      wsig.seq = ++e->sig_seq;
+      e->defer_into->seq = wsig.seq;
+    }
     // (beside other windows it writes only the slot's pinned rows, not the shared device rows)
     HIP_TRY(launch_reduce_rounds(partials, d_woff.as<uint32_t>(), planned0, reduce_side ? nullptr : stats,
-                                 direct ? e->defer_into->hs_dev : nullptr, rs),
+                                 direct ? e->defer_into->hs_dev : nullptr, wsig, rs),
             "reduce rounds");
+    e->defer_into_signalled = wsig.flag != nullptr;
   } else {
     e->round_kind.clear();  // (accumulate_window: every round k_expand)
     HIP_TRY(seed_round(0, arr[0]), "seed");
@@ -1007,7 +1048,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       HIP_TRY(hipMemcpyAsync(f.ha, e->d_apply_stats.p, static_cast<size_t>(planned0 + 1) * kNumCtr * 8,
                              hipMemcpyDeviceToHost, s),
               "read apply stats");
-    HIP_TRY(hipEventRecord(e->ev_run1, reduce_side ? e->rstream : s), "event");
+    f.signalled = e->defer_into_signalled;  // (its flag rises with the reduce)
+    if (!f.signalled) HIP_TRY(hipEventRecord(e->ev_run1, reduce_side ? e->rstream : s), "event");
     f.deferred = true;
     f.planned0 = planned0;
     f.world = world;
@@ -1315,7 +1357,10 @@ int ps_run(ps_engine* e, ps_stats* out) {
   if (e->infl_count) return e->fail(PS_E_STATE, "asynchronous runs pending: ps_wait first");
   ps_stats st{};
   const int rc = run_body(e, &st, false);
-  if (rc) return rc;
+  if (rc) {
+    e->upload_shadow.clear();  // (a failed window's staged copies may not have run)
+    return rc;
+  }
   if (out) *out = st;
   return PS_OK;
 }
@@ -1343,6 +1388,7 @@ int ps_run_async(ps_engine* e) {
     for (hipStream_t x : {e->pstream, e->rstream, e->xstream})
       if (x) (void)hipStreamSynchronize(x);
     e->gate_valid = false;
+    e->upload_shadow.clear();  // (a failed window's staged copies may not have run)
     return rc;
   }
   ++e->infl_count;
@@ -1355,11 +1401,28 @@ int ps_wait(ps_engine* e, ps_stats* out) {
   ps_engine::Inflight& f = e->infl[e->infl_head];
   e->infl_head = (e->infl_head + 1) % 2;
   --e->infl_count;
-  if (f.deferred) {
+  if (f.deferred && f.signalled) {
+    // poll the window's flag (pinned, written after its reduce); a stream
+    // that has drained or failed without it is an error, not a hang
+    const volatile uint64_t* flag = f.sig;
+    for (uint64_t spin = 0; *flag != f.seq; ++spin) {
+      if ((spin & 1023) == 1023) {
+        const hipError_t q = hipStreamQuery(e->stream);
+        if (q != hipSuccess && q != hipErrorNotReady) return e->fail(PS_E_DEVICE, "window: stream failed");
+        if (q == hipSuccess && *flag != f.seq) return e->fail(PS_E_DEVICE, "window: completion flag missing");
+        std::this_thread::yield();
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const volatile uint64_t* t = f.sig;
+    f.st.run_ms += static_cast<double>(t[2] - t[1]) * 1e-5;  // (s_memrealtime: 100 MHz)
+  } else if (f.deferred) {
     HIP_TRY(hipEventSynchronize(f.ev1), "sync");
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, f.ev0, f.ev1), "elapsed");
     f.st.run_ms += ms;
+  }
+  if (f.deferred) {
     f.deferred = false;
     if (!accumulate_window(&f.st, f.hs, f.ha, f.r, f.planned0, f.mode, f.flood_rounds, f.launches, f.world,
                            f.kinds)) {

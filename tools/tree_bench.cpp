@@ -3,6 +3,7 @@
 // leave cost without a GPU.
 //   g++ -O3 -std=c++17 -Iinclude -Igo-libp2p-pubsub_amd/csrc tools/tree_bench.cpp \
 //       go-libp2p-pubsub_amd/csrc/tree.cpp -o /tmp/tree_bench && /tmp/tree_bench plan.bin
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <vector>
@@ -54,7 +55,13 @@ int main(int argc, char** argv) {
       T.close_client(L[i]);
     }
     auto c = clk::now();
-    for (uint32_t p : join[b]) T.subscribe(p);
+    // (as ps_topic_join: each joiner's own line fetched a few joins ahead)
+    const auto& J = join[b];
+    for (size_t i = 0; i < std::min(J.size(), size_t(8)); ++i) T.prefetch_join(J[i]);
+    for (size_t i = 0; i < J.size(); ++i) {
+      if (i + 8 < J.size()) T.prefetch_join(J[i + 8]);
+      T.subscribe(J[i]);
+    }
     const auto d0 = clk::now();
     const size_t pend = T.parted_parents();
     // the engine answers reach (and cut-for-good) from the GPU node space;
