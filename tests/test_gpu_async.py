@@ -167,3 +167,49 @@ def test_overlapped_windows_equal_blocking(monkeypatch, dead, full):
         e.close()
     assert out[0][0] == out[1][0]
     assert out[0][1] == out[1][1]
+
+
+@pytest.mark.parametrize("reuse", [1, 0])
+def test_signalled_windows_equal_blocking(monkeypatch, reuse):
+    """Small pipelined windows (under the overlap floor, one rank) end with
+    a pinned completion flag raised by the reduce instead of an event, and
+    reuse the device copies of uploads that repeat.  Runs
+    whose batches alternate between repeating and changing (same plan, new
+    seeds; a new plan) give the blocking runs' counters and final rows, and
+    the flag's timestamps a positive run time.  reuse=0 stages every upload."""
+    monkeypatch.setenv("PSAMD_AB", "1")
+    monkeypatch.setenv("PSAMD_UPLOAD_REUSE", str(reuse))
+    wl = WL.cfg3(60_000, 8, 4000)
+    rng = np.random.default_rng(5)
+    live = (rng.random(wl.n_peers) >= 0.03).astype(np.uint8)
+    live[[ts.root for ts in wl.topics]] = 1
+    base = wl.msg_topics
+    batches = [base, base, vary_counts(base, 1), vary_counts(base, 1), base[: base.shape[0] // 2], base,
+               vary_counts(base, 3), base]
+    out = []
+    for pipelined in (False, True):
+        e = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed)
+        WL.build_engine_topics(e, wl)
+        e.set_live(live)
+        res, ms = [], []
+        if pipelined:
+            for i, b in enumerate(batches):
+                e.publish(b)
+                e.run_async()
+                if i:
+                    st = e.wait()
+                    res.append(stats_key(st))
+                    ms.append(st.run_ms)
+            st = e.wait()
+            res.append(stats_key(st))
+            ms.append(st.run_ms)
+            assert all(m > 0 for m in ms), ms
+            assert e.overlapped_windows() == 0
+        else:
+            for b in batches:
+                e.publish(b)
+                res.append(stats_key(e.run()))
+        out.append((res, e.seen_digest()))
+        e.close()
+    assert out[0][0] == out[1][0]
+    assert out[0][1] == out[1][1]
