@@ -74,7 +74,7 @@ int plan_window_layout(ps_engine* e, const std::vector<RunMsg>& msgs, const std:
       // <= 1/16 more bytes against half the store instructions (cfg3 1.015
       // -> 1.003 ms/step, the 4-rank cfg4 loopback's 63-word rows 2.49x ->
       // 2.32x; profiles/r03/ab_pad.txt)
-      if (d.W >= e->pad_words) d.W += d.W & 1u;
+      if (d.W >= e->pad_words) d.W = (d.W + e->pad_align - 1) / e->pad_align * e->pad_align;
       L.groups[t].push_back(StartGroup{s_lo, 0, d.W});
     } else {
       // Start groups (a tree's messages entering at different rounds): the
@@ -242,6 +242,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   key.push_back(e->chain_words);
   key.push_back(static_cast<uint64_t>(e->launch_bytes));
   key.push_back(e->chain_tail ? 1 : 0);
+  key.push_back(e->chain_slice_small ? 1 : 0);
   for (size_t q = 0; q < xchg.size(); ++q) key.push_back(xchg[q].any);
   PairPlan& PP = e->pair;
   if (key == PP.key) return false;
@@ -287,6 +288,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
     uint32_t R = 0, S = 0;  // R = 0: no chain of this length
   };
   constexpr uint32_t stage_w = kChainWords, cap = kChainCap;
+  constexpr double kSliceChunks = 16384;  // slicing for parallelism: at most this many slice chunks per level
   auto chain_size = [&](const TopicHost& T, uint32_t d, uint32_t levels, uint32_t W) {
     ChainSize z;
     const double n0 = static_cast<double>(T.level_off[d + 1] - T.level_off[d]);
@@ -307,6 +309,22 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
                                std::floor(cap / 2 / gmax),
                                std::floor(static_cast<double>(e->chain_words) / (z.S * gsum))});
     z.R = static_cast<uint32_t>(std::max(1.0, r));
+    // A one-node run whose subtree alone is many times chain_words, on a
+    // level of few nodes, would leave the launch a few hundred long waves
+    // (cfg2: 512 waves of 31k words on 256 CUs, 29 us): its rows are cut into
+    // column slices of about chain_words / subtree nodes words instead (even,
+    // >= kMinSlice), one wave per slice -- the same split as rows wider than
+    // the stage.
+    // (Only rows of whole 128-B lines: a slice boundary inside a line would
+    // have two waves write parts of one line -- cfg2's 158-word rows cut at
+    // 40 words: 0.053 -> 0.081 ms/step.)
+    if (e->chain_slice_small && z.R == 1 && z.S == W && W % 16 == 0 && z.S * gsum > 2.0 * e->chain_words &&
+        n0 * (z.S * gsum / e->chain_words) <= kSliceChunks) {
+      constexpr uint32_t kMinSlice = 32;
+      uint32_t s = static_cast<uint32_t>(std::ceil(e->chain_words / gsum));
+      s = std::max(kMinSlice, (s + 15u) & ~15u);
+      if (s < z.S) z.S = s;
+    }
     return z;
   };
   // the (topic, group)s a launch of rounds q .. q + len - 1 writes: level d
