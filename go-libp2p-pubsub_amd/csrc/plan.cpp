@@ -309,12 +309,12 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
                                std::floor(cap / 2 / gmax),
                                std::floor(static_cast<double>(e->chain_words) / (z.S * gsum))});
     z.R = static_cast<uint32_t>(std::max(1.0, r));
-    // A one-node run whose subtree alone is many times chain_words, on a
-    // level of few nodes, would leave the launch a few hundred long waves
-    // (cfg2: 512 waves of 31k words on 256 CUs, 29 us): its rows are cut into
-    // column slices of about chain_words / subtree nodes words instead (even,
-    // >= kMinSlice), one wave per slice -- the same split as rows wider than
-    // the stage.
+    // (A/B, off by default) A one-node run whose subtree alone is many times
+    // chain_words, on a level of few nodes, leaves the launch a few hundred
+    // long waves (cfg2: 512 waves of 31k words on 256 CUs, 29 us); cutting its
+    // rows into column slices of about chain_words / subtree nodes words, one
+    // wave per slice, measured no faster: cfg2 0.0536 either way with 16-word
+    // aligned rows, cfg3 0.908 vs 0.898, cfg4 flat (profiles/r04/ab/NOTES.md).
     // (Only rows of whole 128-B lines: a slice boundary inside a line would
     // have two waves write parts of one line -- cfg2's 158-word rows cut at
     // 40 words: 0.053 -> 0.081 ms/step.)
