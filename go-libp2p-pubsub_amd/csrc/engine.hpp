@@ -217,6 +217,7 @@ struct ps_engine {
   bool host_timing = false;      // PSAMD_HOST_TIMING=1: host phase times to stderr
   bool lb_place = true;
   bool chain_slice_small = false;  // (A/B: PSAMD_CHAIN_SLICE_SMALL=1) one-node chain runs of huge subtrees cut into slices
+  bool chain2 = false;            // (A/B: PSAMD_CHAIN2=1) two-round launches as chains (v3, one round trip), not pairs
   uint32_t pad_align = 2;         // (A/B: PSAMD_PAD_ALIGN) rows of >= pad_words words padded to a multiple of this  // one-node chain runs of huge subtrees cut into slices (A/B: PSAMD_CHAIN_SLICE_SMALL=0)
   bool sig_windows = true;
   // per-window uploads (topic table, seeds, descriptors) kept on the device:

@@ -243,6 +243,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   key.push_back(static_cast<uint64_t>(e->launch_bytes));
   key.push_back(e->chain_tail ? 1 : 0);
   key.push_back(e->chain_slice_small ? 1 : 0);
+  key.push_back(e->chain2 ? 1 : 0);
   for (size_t q = 0; q < xchg.size(); ++q) key.push_back(xchg[q].any);
   PairPlan& PP = e->pair;
   if (key == PP.key) return false;
@@ -357,9 +358,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   uint32_t last_r = 0;
   for (uint32_t q = 1; q <= rounds && q < e->pull.bytes.size(); ++q)
     if (e->pull.bytes[q]) last_r = q;
-  auto can = [&](uint32_t q, uint32_t len) {
-    if (len == 1) return true;
-    if (len == 2) return static_cast<bool>(can2[q]);
+  auto can_chain = [&](uint32_t q, uint32_t len) {
     const bool tail = e->chain_tail && len == max_len + 1 && q + len - 1 == last_r && max_len >= 3;
     if (!chains_ok || (len > max_len && !tail) || len > kChainLevels || q + len - 1 > rounds || exch(q)) return false;
     for (uint32_t k = 1; k <= len; ++k)
@@ -369,6 +368,13 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
       ok = ok && chain_size(e->topics[t], d, levels, block_w(tab[t], L.groups[t][gi])).R > 0;
     });
     return ok;
+  };
+  // two rounds: a pair, or (chain2, A/B) a two-level chain where one is possible
+  auto chain_two = [&](uint32_t q) { return e->chain2 && q + 1 <= rounds && can_chain(q, 2); };
+  auto can = [&](uint32_t q, uint32_t len) {
+    if (len == 1) return true;
+    if (len == 2) return chain_two(q) || static_cast<bool>(can2[q]);
+    return can_chain(q, len);
   };
   // best[q]: traffic of rounds q..rounds; take[q]: rounds of the launch starting at q
   std::vector<double> best(rounds + 6, 0.0);
@@ -403,7 +409,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
       continue;
     }
     PP.len[q] = len;
-    if (len >= 3) {
+    if (len >= 3 || (len == 2 && chain_two(q))) {
       kind[q] = PS_K_CHAIN;
       for (uint32_t k = 1; k < len; ++k) kind[q + k] = PS_K_CHAIN2;
       PP.lo[q] = static_cast<uint32_t>(PP.chain.size());
