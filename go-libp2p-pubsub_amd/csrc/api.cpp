@@ -165,6 +165,7 @@ static void read_switches(ps_engine* e) {
   if (const char* v = std::getenv("PSAMD_FLOOD_TOP_BYTES")) o.flood_top_bytes = std::strtoull(v, nullptr, 0);
   if (const char* v = std::getenv("PSAMD_UPLOAD_REUSE")) e->upload_reuse = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_SIG_WINDOWS")) e->sig_windows = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_FUSE_REDUCE")) e->fuse_reduce = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_CHAIN2")) e->chain2 = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PAD_ALIGN")) e->pad_align = std::max(2, std::min(64, std::atoi(v))) & ~1;
   if (const char* v = std::getenv("PSAMD_CHAIN_SLICE_SMALL")) e->chain_slice_small = std::atoi(v) != 0;
@@ -487,19 +488,37 @@ int ps_set_live(ps_engine* e, const uint8_t* live) {
 int ps_publish_at(ps_engine* e, const uint32_t* topic_of_msg, const uint32_t* start_round, size_t n,
                   uint32_t* first) {
   if (!e || (n && !topic_of_msg)) return PS_E_INVAL;
-  for (size_t i = 0; i < n; ++i) {
-    if (!topic_ok(e, topic_of_msg[i])) return e->fail(PS_E_STATE, "publish to a closed topic");
-    if (start_round && start_round[i] > kMaxStartRound) return e->fail(PS_E_RANGE, "start round too large");
-  }
   if (static_cast<uint64_t>(e->next_msg) + n >= 0xFFFFFFF0ull) return e->fail(PS_E_RANGE, "message id space exhausted");
-  if (first) *first = e->next_msg;
+  // one pass: validate and append (a failure takes the batch back out); a
+  // topic is looked up only where it changes along the batch
   const size_t old = e->pending.size();
   e->pending.resize(old + n);
   RunMsg* out = e->pending.data() + old;
+  const uint32_t t0 = old ? e->pending_topic0 : (n ? topic_of_msg[0] : 0u);
+  bool mixed = old ? e->pending_mixed : false, nonzero = false;
+  uint32_t last = 0xFFFFFFFFu;
   for (size_t i = 0; i < n; ++i) {
-    out[i] = RunMsg{topic_of_msg[i], start_round ? start_round[i] : 0u};
-    e->pending_nonzero_start |= out[i].start != 0;
+    const uint32_t t = topic_of_msg[i];
+    if (t != last) {
+      if (!topic_ok(e, t)) {
+        e->pending.resize(old);
+        return e->fail(PS_E_STATE, "publish to a closed topic");
+      }
+      last = t;
+      mixed |= t != t0;
+    }
+    const uint32_t s0 = start_round ? start_round[i] : 0u;
+    if (s0 > kMaxStartRound) {
+      e->pending.resize(old);
+      return e->fail(PS_E_RANGE, "start round too large");
+    }
+    nonzero |= s0 != 0;
+    out[i] = RunMsg(t, s0);
   }
+  e->pending_topic0 = t0;
+  e->pending_mixed = mixed;
+  e->pending_nonzero_start |= nonzero;
+  if (first) *first = e->next_msg;
   e->next_msg += static_cast<uint32_t>(n);
   return PS_OK;
 }

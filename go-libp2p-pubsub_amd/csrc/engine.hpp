@@ -109,6 +109,8 @@ struct TopicHost {
 struct RunMsg {
   uint32_t topic;
   uint32_t start;
+  RunMsg() {}  // (left unset: ps_publish writes every element it appends)
+  RunMsg(uint32_t t, uint32_t s) : topic(t), start(s) {}
 };
 
 // Messages of one topic in one window: a slice of the run's topic-sorted
@@ -215,11 +217,11 @@ struct ps_engine {
   bool host_only = false;        // a planner probe (psengine_plan.h): no device
   psamd::WindowLayout probe;     // the probe's last planned window
   bool host_timing = false;      // PSAMD_HOST_TIMING=1: host phase times to stderr
-  bool lb_place = true;
+  bool lb_place = true;           // levels placed by one look-back launch each (A/B: PSAMD_LB_PLACE=0)
   bool chain_slice_small = false;  // (A/B: PSAMD_CHAIN_SLICE_SMALL=1) one-node chain runs of huge subtrees cut into slices
   bool chain2 = false;            // (A/B: PSAMD_CHAIN2=1) two-round launches as chains (v3, one round trip), not pairs
-  uint32_t pad_align = 2;         // (A/B: PSAMD_PAD_ALIGN) rows of >= pad_words words padded to a multiple of this  // one-node chain runs of huge subtrees cut into slices (A/B: PSAMD_CHAIN_SLICE_SMALL=0)
-  bool sig_windows = true;
+  uint32_t pad_align = 2;         // (A/B: PSAMD_PAD_ALIGN) rows of >= pad_words words padded to a multiple of this
+  bool sig_windows = true;        // pipelined one-rank windows end with a pinned flag, not an event (A/B: PSAMD_SIG_WINDOWS=0)
   // per-window uploads (topic table, seeds, descriptors) kept on the device:
   // the bytes last staged into each buffer, skipped when a window repeats them
   struct UploadShadow {
@@ -228,8 +230,17 @@ struct ps_engine {
   };
   std::map<const psamd::DevBuf*, UploadShadow> upload_shadow;
   bool upload_reuse = true;  // (A/B: PSAMD_UPLOAD_REUSE=0)
-  bool defer_into_signalled = false;  // the window being enqueued raises its flag in its reduce        // pipelined one-rank windows end with a pinned flag, not an event (A/B: PSAMD_SIG_WINDOWS=0)
-  uint64_t sig_seq = 0;           // levels placed by one look-back launch each (A/B: PSAMD_LB_PLACE=0)
+  bool defer_into_signalled = false;  // the window being enqueued raises its flag in its reduce
+  uint64_t sig_seq = 0;
+  // a signalled window's reduce, held back to run in the next window's first
+  // launch (k_window_turn) -- or alone, from ps_wait, if none comes first
+  // (A/B: PSAMD_FUSE_REDUCE=0)
+  bool fuse_reduce = true;
+  struct PendingReduce {
+    bool valid = false;
+    const void* owner = nullptr;  // the Inflight slot whose flag it raises
+    psamd::ReduceArgs args{};
+  } pend_reduce;
   uint32_t small_place = 512;    // top levels up to this many nodes placed by one block
   // GPU rebuild of the node space: on by default for one
   // rank and tree topics (PSAMD_GPU_BUILD=0: host build)
@@ -332,6 +343,9 @@ struct ps_engine {
   // publishes not yet run
   std::vector<psamd::RunMsg> pending;
   bool pending_nonzero_start = false;  // some pending message starts after round 0
+  bool pending_mixed = false;          // pending messages name more than one topic
+  uint32_t pending_topic0 = 0;         // ... the topic of the first one
+  uint32_t run_iota_n = 0;             // run_sorted / run_rank hold 0 .. n-1 (one-topic runs)
   bool run_zero_start = true;          // every message of the current run starts in round 0
   uint32_t next_msg = 0;
 

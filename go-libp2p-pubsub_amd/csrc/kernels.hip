@@ -69,16 +69,16 @@ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
 // the root is node 0 of its topic) and stamp its generation; mesh topics get
 // all their rows zeroed (they do not use generations).  Grid: x = chunk, y =
 // topic.
-__global__ __launch_bounds__(kBlock) void k_window_init(const TopicDev* __restrict__ topics,
-                                                        uint64_t* __restrict__ seen,
-                                                        uint64_t* __restrict__ a0,
-                                                        uint64_t* __restrict__ a1,
-                                                        uint8_t* __restrict__ gen,
-                                                        uint32_t gen_cur, WindowStart ws) {
+// (block (bx, by) of a gx x gy grid: k_window_init's own, or the init part
+// of k_window_turn)
+__device__ __forceinline__ void window_init_block(const TopicDev* __restrict__ topics, uint64_t* __restrict__ seen,
+                                                  uint64_t* __restrict__ a0, uint64_t* __restrict__ a1,
+                                                  uint8_t* __restrict__ gen, uint32_t gen_cur, const WindowStart& ws,
+                                                  uint32_t bx, uint32_t by, uint32_t gx, uint32_t gy) {
   // folded-in work (one launch instead of three): the staged copies and the
   // partial-slot clear, grid-stride over every block
-  const uint32_t nb = gridDim.x * gridDim.y;
-  const uint32_t bid = blockIdx.y * gridDim.x + blockIdx.x;
+  const uint32_t nb = gx * gy;
+  const uint32_t bid = by * gx + bx;
   for (uint32_t k = 0; k < ws.copy.n; ++k)
     for (uint32_t i = bid * kBlock + threadIdx.x; i < ws.copy.words[k]; i += nb * kBlock)
       ws.copy.dst[k][i] = ws.copy.src[k][i];
@@ -86,18 +86,18 @@ __global__ __launch_bounds__(kBlock) void k_window_init(const TopicDev* __restri
        i += static_cast<uint64_t>(nb) * kBlock)
     ws.zero[i] = 0;
   if (ws.t0 && bid == 0 && threadIdx.x == 0) *ws.t0 = __builtin_amdgcn_s_memrealtime();
-  const TopicDev T = topics[blockIdx.y];
+  const TopicDev T = topics[by];
   if (T.W == 0 || T.n_nodes == 0) return;
   const bool mesh = (T.flags & kTopicMesh) != 0;
   const uint64_t n_words = mesh ? static_cast<uint64_t>(T.n_nodes) * T.W : T.root_words;
-  if (!mesh && (blockIdx.x != 0 || !(T.flags & kTopicRootLocal))) return;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n_words;
-       i += static_cast<uint64_t>(gridDim.x) * kBlock) {
+  if (!mesh && (bx != 0 || !(T.flags & kTopicRootLocal))) return;
+  for (uint64_t i = static_cast<uint64_t>(bx) * kBlock + threadIdx.x; i < n_words;
+       i += static_cast<uint64_t>(gx) * kBlock) {
     seen[T.wbase + i] = 0;
     a0[T.wbase + i] = 0;
     a1[T.wbase + i] = 0;
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0 && (T.flags & kTopicRootLocal))
+  if (bx == 0 && threadIdx.x == 0 && (T.flags & kTopicRootLocal))
     gen[T.nbase] = static_cast<uint8_t>(gen_cur);
   if (ws.seeds && !mesh) {
     // Topic.PublishMessage (pubsub.go:111-120), round 0: this block zeroed
@@ -109,6 +109,15 @@ __global__ __launch_bounds__(kBlock) void k_window_init(const TopicDev* __restri
       seen[sd.woff] = sd.assign ? sd.mask : seen[sd.woff] | sd.mask;
     }
   }
+}
+
+__global__ __launch_bounds__(kBlock) void k_window_init(const TopicDev* __restrict__ topics,
+                                                        uint64_t* __restrict__ seen,
+                                                        uint64_t* __restrict__ a0,
+                                                        uint64_t* __restrict__ a1,
+                                                        uint8_t* __restrict__ gen,
+                                                        uint32_t gen_cur, WindowStart ws) {
+  window_init_block(topics, seen, a0, a1, gen, gen_cur, ws, blockIdx.x, blockIdx.y, gridDim.x, gridDim.y);
 }
 
 // Nodes fed by a parent on another rank: rows zeroed, so the apply kernel can
@@ -797,14 +806,14 @@ __device__ __forceinline__ void block_reduce_ctrs(const uint64_t* __restrict__ p
 // one coalesced stream of counters (kAct threads, each on one counter index)
 // and writes the round's statistics row.  Pull launches share at most
 // kPullSlots slots per round between their blocks, so the streams are short.
-__global__ __launch_bounds__(kBlock) void k_reduce_rounds(const uint64_t* __restrict__ partials,
-                                                          const uint32_t* __restrict__ desc,
-                                                          uint64_t* __restrict__ round_stats,
-                                                          uint64_t* __restrict__ host_stats,
-                                                          WindowSignal sig) {
+// (block q of nq: k_reduce_rounds' own, or the reduce part of k_window_turn)
+__device__ __forceinline__ void reduce_rounds_block(const uint64_t* __restrict__ partials,
+                                                    const uint32_t* __restrict__ desc,
+                                                    uint64_t* __restrict__ round_stats,
+                                                    uint64_t* __restrict__ host_stats, const WindowSignal& sig,
+                                                    uint32_t q, uint32_t nq) {
   constexpr uint32_t kAct = (kBlock / kNumCtr) * kNumCtr;
   __shared__ uint64_t red[kBlock];
-  const uint32_t q = blockIdx.x;
   const uint32_t first = desc[3 * q], end = desc[3 * q + 1], stride = desc[3 * q + 2];
   uint64_t acc = 0;
   if (stride && threadIdx.x < kAct) {
@@ -839,12 +848,35 @@ __global__ __launch_bounds__(kBlock) void k_reduce_rounds(const uint64_t* __rest
   if (sig.flag) __syncthreads();  // (the block's row stores precede its fence)
   if (sig.flag && threadIdx.x == 0) {
     __threadfence_system();
-    if (atomicAdd(sig.ctr, 1u) == gridDim.x - 1) {
+    if (atomicAdd(sig.ctr, 1u) == nq - 1) {
       sig.flag[2] = __builtin_amdgcn_s_memrealtime();
       __threadfence_system();
       __hip_atomic_store(sig.flag, sig.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
       atomicExch(sig.ctr, 0u);
     }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_reduce_rounds(const uint64_t* __restrict__ partials,
+                                                          const uint32_t* __restrict__ desc,
+                                                          uint64_t* __restrict__ round_stats,
+                                                          uint64_t* __restrict__ host_stats,
+                                                          WindowSignal sig) {
+  reduce_rounds_block(partials, desc, round_stats, host_stats, sig, blockIdx.x, gridDim.x);
+}
+
+// The previous window's reduce (blocks 0 .. n_rounds) beside this window's
+// init (the blocks after them, as the gx x gy grid of k_window_init).
+__global__ __launch_bounds__(kBlock) void k_window_turn(ReduceArgs rd, const TopicDev* __restrict__ topics,
+                                                        uint64_t* __restrict__ seen, uint64_t* __restrict__ a0,
+                                                        uint64_t* __restrict__ a1, uint8_t* __restrict__ gen,
+                                                        uint32_t gen_cur, WindowStart ws, uint32_t gx, uint32_t gy) {
+  const uint32_t nq = rd.n_rounds + 1;
+  if (blockIdx.x < nq) {
+    reduce_rounds_block(rd.partials, rd.desc, rd.round_stats, rd.host_stats, rd.sig, blockIdx.x, nq);
+  } else {
+    const uint32_t b = blockIdx.x - nq;
+    window_init_block(topics, seen, a0, a1, gen, gen_cur, ws, b % gx, b / gx, gx, gy);
   }
 }
 
@@ -964,14 +996,29 @@ hipError_t launch_window_done(uint64_t* sig, uint64_t seq, hipStream_t s) {
   return hipGetLastError();
 }
 
+// tree topics need block x = 0 only; the other blocks share the staged
+// copies and the partial-slot clear (>= 256 blocks in all)
+static uint32_t window_init_gx(uint32_t n_topics, bool any_mesh) {
+  return any_mesh ? 64u : std::max<uint32_t>(1, (256 + n_topics - 1) / n_topics);
+}
+
 hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_t* seen,
                               uint64_t* a0, uint64_t* a1, uint8_t* gen, uint32_t gen_cur,
                               bool any_mesh, const WindowStart& ws, hipStream_t s) {
   if (n_topics == 0) return hipSuccess;
-  // tree topics need block x = 0 only; the other blocks share the staged
-  // copies and the partial-slot clear (>= 256 blocks in all)
-  const dim3 grid(any_mesh ? 64 : std::max<uint32_t>(1, (256 + n_topics - 1) / n_topics), n_topics);
+  const dim3 grid(window_init_gx(n_topics, any_mesh), n_topics);
   hipLaunchKernelGGL(k_window_init, grid, dim3(kBlock), 0, s, topics, seen, a0, a1, gen, gen_cur, ws);
+  return hipGetLastError();
+}
+
+hipError_t launch_window_turn(const ReduceArgs& rd, const TopicDev* topics, uint32_t n_topics, uint64_t* seen,
+                              uint64_t* a0, uint64_t* a1, uint8_t* gen, uint32_t gen_cur, bool any_mesh,
+                              const WindowStart& ws, hipStream_t s) {
+  if (rd.n_rounds == 0 || n_topics == 0) return hipErrorInvalidValue;  // (the caller launches them apart)
+  const uint32_t gx = window_init_gx(n_topics, any_mesh);
+  const uint32_t grid = rd.n_rounds + 1 + gx * n_topics;
+  hipLaunchKernelGGL(k_window_turn, dim3(grid), dim3(kBlock), 0, s, rd, topics, seen, a0, a1, gen, gen_cur, ws, gx,
+                     n_topics);
   return hipGetLastError();
 }
 

@@ -411,6 +411,22 @@ struct WindowSignal {
 hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_t* seen,
                               uint64_t* a0, uint64_t* a1, uint8_t* gen, uint32_t gen_cur,
                               bool any_mesh, const WindowStart& ws, hipStream_t s);
+// A signalled window's reduce held back until the next window starts: the
+// two run as one launch (the reduce's blocks first, then the init's), one
+// kernel boundary less per pipelined window.  The two touch
+// disjoint memory: the reduce reads its own slot's partials and descriptors,
+// the init writes the other slot's.
+struct ReduceArgs {
+  const uint64_t* partials = nullptr;
+  const uint32_t* desc = nullptr;
+  uint32_t n_rounds = 0;  // > 0
+  uint64_t* round_stats = nullptr;
+  uint64_t* host_stats = nullptr;
+  WindowSignal sig{};
+};
+hipError_t launch_window_turn(const ReduceArgs& rd, const TopicDev* topics, uint32_t n_topics, uint64_t* seen,
+                              uint64_t* a0, uint64_t* a1, uint8_t* gen, uint32_t gen_cur, bool any_mesh,
+                              const WindowStart& ws, hipStream_t s);
 // stamp: mark the nodes' generation current (compaction mode)
 hipError_t launch_init_nodes(const uint32_t* nodes, uint32_t n, const uint16_t* node_topic,
                              const TopicDev* topics, uint64_t* seen, uint64_t* a0, uint64_t* a1,

@@ -129,6 +129,21 @@ struct Upload {
 // With `fold` set and the copy-kernel form, nothing is launched: *fold gets
 // the copies for a kernel that folds them in, and staged[i] the device-mapped
 // address of upload i's staged bytes (else its destination).
+}  // namespace
+
+// A held-back reduce launched on its own (ps_wait came first, or the next
+// window cannot take it into its first launch).
+int flush_reduce(ps_engine* e) {
+  if (!e->pend_reduce.valid) return PS_OK;
+  e->pend_reduce.valid = false;
+  const ReduceArgs& r = e->pend_reduce.args;
+  HIP_TRY(launch_reduce_rounds(r.partials, r.desc, r.n_rounds, r.round_stats, r.host_stats, r.sig, e->stream),
+          "reduce rounds");
+  return PS_OK;
+}
+
+namespace {
+
 int stage_uploads(ps_engine* e, const Upload* ups, size_t n, hipStream_t s, StageCopy* fold = nullptr,
                   const void** staged = nullptr) {
   if (fold) *fold = StageCopy{};
@@ -586,10 +601,25 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     HIP_TRY(hipMemsetAsync(e->d_gen.p, 0, e->d_gen.bytes, s), "clear generations");
     e->gen_cur = 1;
   }
-  HIP_TRY(launch_window_init(static_cast<const TopicDev*>(fold ? staged[0] : d_topics.p), nt,
-                             e->d_seen.as<uint64_t>(), e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>(),
-                             e->d_gen.as<uint8_t>(), e->gen_cur, any_mesh, ws, s),
-          "window init");
+  // the previous window's held-back reduce: in this launch when both run on
+  // the main stream, else on its own first
+  const bool turn = e->pend_reduce.valid && fold && s == e->stream && nt > 0;
+  if (e->pend_reduce.valid && !turn) {
+    const int rcf = flush_reduce(e);
+    if (rcf) return rcf;
+  }
+  if (turn) {
+    e->pend_reduce.valid = false;
+    HIP_TRY(launch_window_turn(e->pend_reduce.args, static_cast<const TopicDev*>(staged[0]), nt,
+                               e->d_seen.as<uint64_t>(), e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>(),
+                               e->d_gen.as<uint8_t>(), e->gen_cur, any_mesh, ws, s),
+            "reduce + window init");
+  } else {
+    HIP_TRY(launch_window_init(static_cast<const TopicDev*>(fold ? staged[0] : d_topics.p), nt,
+                               e->d_seen.as<uint64_t>(), e->d_arr0.as<uint64_t>(), e->d_arr1.as<uint64_t>(),
+                               e->d_gen.as<uint8_t>(), e->gen_cur, any_mesh, ws, s),
+            "window init");
+  }
   if (e->n_remote_fed && !level)
     HIP_TRY(launch_init_nodes(e->d_remote_fed.as<uint32_t>(), e->n_remote_fed, e->d_node_topic.as<uint16_t>(),
                               d_topics.as<TopicDev>(), e->d_seen.as<uint64_t>(), e->d_arr0.as<uint64_t>(),
@@ -960,9 +990,18 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       e->defer_into->seq = wsig.seq;
     }
     // (beside other windows it writes only the slot's pinned rows, not the shared device rows)
-    HIP_TRY(launch_reduce_rounds(partials, d_woff.as<uint32_t>(), planned0, reduce_side ? nullptr : stats,
-                                 direct ? e->defer_into->hs_dev : nullptr, wsig, rs),
-            "reduce rounds");
+    if (wsig.flag && e->fuse_reduce && planned0 > 0) {
+      // held back for the next window's first launch (k_window_turn); only
+      // this slot's buffers and the pinned rows: the shared device stats rows
+      // may be reallocated by then, and nobody reads a deferred window's
+      e->pend_reduce.valid = true;
+      e->pend_reduce.owner = e->defer_into;
+      e->pend_reduce.args = ReduceArgs{partials, d_woff.as<uint32_t>(), planned0, nullptr, e->defer_into->hs_dev, wsig};
+    } else {
+      HIP_TRY(launch_reduce_rounds(partials, d_woff.as<uint32_t>(), planned0, reduce_side ? nullptr : stats,
+                                   direct ? e->defer_into->hs_dev : nullptr, wsig, rs),
+              "reduce rounds");
+    }
     e->defer_into_signalled = wsig.flag != nullptr;
   } else {
     e->round_kind.clear();  // (accumulate_window: every round k_expand)
@@ -1241,13 +1280,23 @@ int run_body(ps_engine* e, ps_stats* stp, bool may_defer) {
   }
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
   // one counting sort: message indices grouped by topic, publish order kept
+  // (a batch of one topic: the identity, kept from the last such run)
   auto& off = e->run_topic_off;
   off.assign(nt + 1, 0);
-  for (uint32_t i = 0; i < nmsg; ++i) off[msgs[i].topic + 1]++;
-  for (uint32_t t = 0; t < nt; ++t) off[t + 1] += off[t];
-  e->run_sorted.resize(nmsg);
-  e->run_rank.resize(nmsg);
-  {
+  if (nmsg && !e->pending_mixed) {
+    for (uint32_t t = e->pending_topic0 + 1; t <= nt; ++t) off[t] = nmsg;
+    if (e->run_iota_n != nmsg) {
+      e->run_sorted.resize(nmsg);
+      e->run_rank.resize(nmsg);
+      for (uint32_t i = 0; i < nmsg; ++i) e->run_sorted[i] = e->run_rank[i] = i;
+      e->run_iota_n = nmsg;
+    }
+  } else {
+    e->run_iota_n = 0;
+    for (uint32_t i = 0; i < nmsg; ++i) off[msgs[i].topic + 1]++;
+    for (uint32_t t = 0; t < nt; ++t) off[t + 1] += off[t];
+    e->run_sorted.resize(nmsg);
+    e->run_rank.resize(nmsg);
     std::vector<uint32_t> fill(off.begin(), off.end() - 1);
     for (uint32_t i = 0; i < nmsg; ++i) {
       const uint32_t t = msgs[i].topic;
@@ -1255,6 +1304,7 @@ int run_body(ps_engine* e, ps_stats* stp, bool may_defer) {
       e->run_sorted[fill[t]++] = i;
     }
   }
+  e->pending_mixed = false;
   e->last_lo.assign(nt, 0);
   e->last_cnt.assign(nt, 0);
   std::vector<uint32_t> head(nt, 0);
@@ -1389,6 +1439,7 @@ int ps_run_async(ps_engine* e) {
       if (x) (void)hipStreamSynchronize(x);
     e->gate_valid = false;
     e->upload_shadow.clear();  // (a failed window's staged copies may not have run)
+    if (e->pend_reduce.owner == &f) e->pend_reduce.valid = false;  // (its window failed: nobody waits for it)
     return rc;
   }
   ++e->infl_count;
@@ -1401,6 +1452,10 @@ int ps_wait(ps_engine* e, ps_stats* out) {
   ps_engine::Inflight& f = e->infl[e->infl_head];
   e->infl_head = (e->infl_head + 1) % 2;
   --e->infl_count;
+  if (e->pend_reduce.valid && e->pend_reduce.owner == &f) {
+    const int rc = flush_reduce(e);
+    if (rc) return rc;
+  }
   if (f.deferred && f.signalled) {
     // poll the window's flag (pinned, written after its reduce); a stream
     // that has drained or failed without it is an error, not a hang

@@ -200,6 +200,9 @@ def _p(a, t):
 class Engine:
     """One engine = one GPU's worth of topics (NewTopicManager, pubsub.go:26-31)."""
 
+    _pub_arr = None  # the last uint32 array published and its ctypes pointer
+    _pub_ptr = None
+
     def __init__(self, n_peers: int, n_topics: int = 1, tree_width: int = 2,
                  tree_max_width: int = 5, msg_window: int = 65536, device: int = 0,
                  record_hops: bool = False, time_kernels: bool = False, seed: int = 1,
@@ -325,14 +328,22 @@ class Engine:
 
     # hot path
     def publish(self, topics, start_rounds=None) -> int:
-        t = _u32arr(topics)
+        # (the same uint32 array again, the usual batch loop: its pointer is
+        # reused -- ndarray.ctypes costs microseconds per call)
+        if topics is self._pub_arr:
+            t, tp = topics, self._pub_ptr
+        else:
+            t = _u32arr(topics)
+            tp = _p(t, C.c_uint32)
+            if t is topics:
+                self._pub_arr, self._pub_ptr = t, tp
         first = C.c_uint32()
         if start_rounds is None:
-            self._check(self._L.ps_publish(self._h, _p(t, C.c_uint32), t.shape[0], C.byref(first)))
+            self._check(self._L.ps_publish(self._h, tp, t.shape[0], C.byref(first)))
         else:
             s = _u32arr(start_rounds)
             assert s.shape == t.shape
-            self._check(self._L.ps_publish_at(self._h, _p(t, C.c_uint32), _p(s, C.c_uint32),
+            self._check(self._L.ps_publish_at(self._h, tp, _p(s, C.c_uint32),
                                               t.shape[0], C.byref(first)))
         return first.value
 
