@@ -213,3 +213,66 @@ def test_signalled_windows_equal_blocking(monkeypatch, reuse):
         e.close()
     assert out[0][0] == out[1][0]
     assert out[0][1] == out[1][1]
+
+
+@pytest.mark.parametrize("fuse", [1, 0])
+def test_held_back_reduce_orderings(monkeypatch, fuse):
+    """A signalled window's reduce waits for the next window's first launch
+    (k_window_turn) or for ps_wait.  Every order of the
+    entry points -- wait right away, two in flight, a live-mask change and a
+    readback between them, one-topic batches (no sort) beside mixed ones,
+    batches published in several calls -- gives the blocking runs' counters
+    and rows.  fuse=0: the reduce launches with its own window."""
+    monkeypatch.setenv("PSAMD_AB", "1")
+    monkeypatch.setenv("PSAMD_FUSE_REDUCE", str(fuse))
+    wl = WL.cfg3(40_000, 6, 3000)
+    rng = np.random.default_rng(17)
+    live0 = np.ones(wl.n_peers, dtype=np.uint8)
+    live1 = (rng.random(wl.n_peers) >= 0.05).astype(np.uint8)
+    live1[[ts.root for ts in wl.topics]] = 1
+    base = wl.msg_topics
+    one = np.full(700, 2, dtype=np.uint32)        # one topic: identity order, no sort
+    one_b = np.full(300, 4, dtype=np.uint32)
+    # (op, arg): publish / publish2 (two calls) / async / wait / live / read
+    script = [("publish", base), ("async", None), ("wait", None),
+              ("publish", one), ("async", None), ("publish", base), ("async", None), ("wait", None), ("wait", None),
+              ("publish", one), ("async", None), ("live", live1), ("publish2", (one, one_b)), ("async", None),
+              ("wait", None), ("read", None), ("wait", None),
+              ("publish", base[:1000]), ("async", None), ("publish", one), ("async", None), ("wait", None),
+              ("live", live0), ("publish", one), ("async", None), ("wait", None), ("wait", None)]
+    out = []
+    for pipelined in (False, True):
+        e = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed)
+        WL.build_engine_topics(e, wl)
+        res, reads = [], []
+        first = 0
+        for op, arg in script:
+            if op == "publish":
+                first = e.publish(arg)
+            elif op == "publish2":
+                first = e.publish(arg[0])
+                e.publish(arg[1])
+            elif op == "live":
+                e.set_live(arg)
+            elif op == "async":
+                if pipelined:
+                    e.run_async()
+                else:
+                    res.append(stats_key(e.run()))
+            elif op == "wait":
+                if pipelined:
+                    res.append(stats_key(e.wait()))
+            elif op == "read":
+                reads.append(e.delivered(first).tobytes())
+        out.append((res, reads, e.seen_digest()))
+        e.close()
+    assert out[0][0] == out[1][0]
+    assert out[0][1] == out[1][1]
+    assert out[0][2] == out[1][2]
+    # the batch published in two one-topic calls ran as one mixed batch (run 5
+    # of the script): the same as publishing it in one call
+    with PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed) as e:
+        WL.build_engine_topics(e, wl)
+        e.set_live(live1)
+        e.publish(np.concatenate([one, one_b]))
+        assert stats_key(e.run()) == out[0][0][4]
