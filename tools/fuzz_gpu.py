@@ -325,11 +325,13 @@ def case_drain(rng, max_peers):
 
 
 def case_pipeline(rng, max_peers):
-    """Pipelined runs of one batch with the cross-window overlap forced on
-    small windows (PSAMD_OVERLAP_BYTES=0, random depth floor, random launch
-    modes): every run's deliveries equal the oracle's, the last run's
-    delivered sets of sampled messages equal the oracle's reach, and the rows'
-    digest equals a blocking engine's on the same inputs."""
+    """Pipelined runs with the cross-window overlap forced on small windows
+    (PSAMD_OVERLAP_BYTES=0, random depth floor, random launch modes) or off
+    (signalled windows, the reduce held back into the next window's first
+    launch or not: PSAMD_FUSE_REDUCE), each run a random prefix of the batch
+    published in one or two calls: every run's deliveries equal the oracle's,
+    the last run's delivered sets of sampled messages equal the oracle's
+    reach, and the rows' digest equals a blocking engine's on the same inputs."""
     n = int(rng.integers(64, max_peers))
     n_topics = int(rng.integers(1, 4))
     live = (rng.random(n) > rng.choice([0.0, 0.05, 0.2])).astype(np.uint8)
@@ -339,14 +341,17 @@ def case_pipeline(rng, max_peers):
     pars = [random_tree(rng, n, r) for r in roots]
     runs = int(rng.integers(3, 7))
     set_modes(rng)
-    os.environ["PSAMD_OVERLAP_BYTES"] = "0"
+    os.environ["PSAMD_OVERLAP_BYTES"] = str(rng.choice([0, 4_000_000_000]))
     os.environ["PSAMD_OVERLAP_ROUNDS"] = str(int(rng.choice([2, 4, 8, 12])))
-    exp_total, reach = 0, []
+    os.environ["PSAMD_FUSE_REDUCE"] = str(int(rng.integers(0, 2)))
+    per_topic, reach = [], []
     for t in range(n_topics):
         rp, cl = O.parents_to_csr(pars[t])
         tot, hops, _ = O.disseminate(rp, cl, roots[t], live, 1)
-        exp_total += tot * int((topics == t).sum())
+        per_topic.append(tot)
         reach.append(hops[0] != 0xFF)
+    cuts = [int(rng.integers(1, n_msgs + 1)) for _ in range(runs)]
+    splits = [int(rng.integers(0, c + 1)) for c in cuts]
     digests = []
     for pipelined in (True, False):
         with PE.Engine(n, n_topics) as e:
@@ -355,7 +360,10 @@ def case_pipeline(rng, max_peers):
             e.set_live(live)
             sts = []
             for i in range(runs):
-                first = e.publish(topics)
+                b = topics[: cuts[i]]
+                first = e.publish(b[: splits[i]]) if splits[i] else None
+                f2 = e.publish(b[splits[i]:]) if splits[i] < cuts[i] else None
+                first = f2 if first is None else first
                 if pipelined:
                     e.run_async()
                     if i:
@@ -365,9 +373,11 @@ def case_pipeline(rng, max_peers):
             if pipelined:
                 sts.append(e.wait())
             for i, st in enumerate(sts):
-                if st.deliveries != exp_total:
-                    return f"pipelined={pipelined} run {i}: deliveries {st.deliveries} != oracle {exp_total}"
-            for m in rng.choice(n_msgs, size=min(n_msgs, 12), replace=False):
+                exp = sum(per_topic[int(t)] for t in topics[: cuts[i]])
+                if st.deliveries != exp:
+                    return f"pipelined={pipelined} run {i}: deliveries {st.deliveries} != oracle {exp}"
+            last = cuts[-1]
+            for m in rng.choice(last, size=min(last, 12), replace=False):
                 got = e.delivered(first + int(m)).astype(bool)
                 if not np.array_equal(got, reach[int(topics[m])]):
                     return f"pipelined={pipelined} msg {m}: delivered set differs from the oracle"
