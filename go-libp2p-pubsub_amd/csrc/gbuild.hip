@@ -551,8 +551,9 @@ hipError_t launch_depth_keys(const uint32_t* par, uint32_t n, uint32_t root, uin
 }
 
 hipError_t sort_keys(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
-                     BuildKey kf, hipStream_t s) {
-  return hipcub::DeviceRadixSort::SortKeys(temp, *temp_bytes, in, out, n, 0, static_cast<int>(kf.sort_bits()), s);
+                     BuildKey kf, bool peer_bits, hipStream_t s) {
+  return hipcub::DeviceRadixSort::SortKeys(temp, *temp_bytes, in, out, n, peer_bits ? 0 : static_cast<int>(kf.b),
+                                           static_cast<int>(kf.sort_bits()), s);
 }
 
 hipError_t scan_u32(void* temp, size_t* temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n,

@@ -60,9 +60,13 @@ inline uint32_t depth_jumps_full(uint32_t n) {
   return j + 1;
 }
 
-// hipcub radix sort of n keys (in -> out); temp queried when temp == nullptr
+// hipcub radix sort of n keys (in -> out); temp queried when temp == nullptr.
+// peer_bits = false: only the (depth, parent) bits are sorted -- the radix
+// sort is stable and the keys come in peer order (keys[p] is peer p's), so
+// siblings still end up in peer order, with b fewer key bits to pass over
+// (cfg5: 28 of 48 bits); true: every bit (A/B: PSAMD_SORT_PEER_BITS=1)
 hipError_t sort_keys(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
-                     BuildKey kf, hipStream_t s);
+                     BuildKey kf, bool peer_bits, hipStream_t s);
 // exclusive scan of n u32 (in -> out)
 hipError_t scan_u32(void* temp, size_t* temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n,
                     hipStream_t s);
