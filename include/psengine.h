@@ -82,7 +82,11 @@ typedef struct ps_stats {
   uint64_t windows;            /* propagation windows                            */
   uint64_t rounds;             /* synchronous rounds launched                    */
   uint64_t expand_launches;    /* expand kernel launches                         */
-  double run_ms;               /* device time of the whole run (HIP events)      */
+  double run_ms;               /* device time of the whole run (HIP events; a
+                                  pipelined one-rank window: its start and
+                                  reduce-end device stamps -- a reduce held back
+                                  into the next window's first launch, or to
+                                  ps_wait, ends there)                          */
   double expand_ms;            /* summed expand-kernel device time (TIME flag)   */
   double host_ms;              /* wall time of the ps_run call                   */
   uint32_t expand_mode;        /* hot kernel of the last window: PS_MODE_*       */
