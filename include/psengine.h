@@ -237,7 +237,9 @@ int ps_run(ps_engine* e, ps_stats* out);
  * in flight), so the caller can publish and enqueue the next batch; ps_wait
  * completes the oldest run in flight and returns its stats.  Reads
  * (ps_read_*, ps_seen_digest) and membership changes stay stream-ordered
- * behind the runs in flight; ps_run refuses while any is pending. */
+ * behind the runs in flight; ps_run refuses while any is pending.  (A one-rank
+ * run's counter reduce may be held back to ride in the next ps_run_async's
+ * first launch; ps_wait launches it itself when no run came first.) */
 int ps_run_async(ps_engine* e);
 int ps_wait(ps_engine* e, ps_stats* out);
 
