@@ -167,6 +167,7 @@ static void read_switches(ps_engine* e) {
   if (const char* v = std::getenv("PSAMD_SIG_WINDOWS")) e->sig_windows = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FUSE_REDUCE")) e->fuse_reduce = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_SORT_PEER_BITS")) e->sort_peer_bits = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_OVERLAP_SHALLOW")) e->overlap_shallow = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_CHAIN2")) e->chain2 = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PAD_ALIGN")) e->pad_align = std::max(2, std::min(64, std::atoi(v))) & ~1;
   if (const char* v = std::getenv("PSAMD_CHAIN_SLICE_SMALL")) e->chain_slice_small = std::atoi(v) != 0;

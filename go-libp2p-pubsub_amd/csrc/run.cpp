@@ -535,8 +535,12 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // root rows the init rewrites); deep windows also their leading launches
   // (windows of under 512 MB: the stream hand-offs cost more than the init
   // they hide -- cfg2 0.066 -> 0.068-0.073 ms/step, cfg4 0.4536 -> 0.4502)
+  // (a shallow window -- k_flood leading rounds, nothing but its init to hide
+  // -- ends signalled instead: its events cost more than the init, cfg4
+  // 0.4472-0.4479 -> 0.4421-0.4425 ms/step, profiles/r04/ab/shallow_signalled.log)
   const bool pcap = e->overlap_on && level && world == 1 && !any_mesh && !record && !L.multi &&
-                    !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS)) && total >= e->overlap_min_bytes;
+                    !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS)) && total >= e->overlap_min_bytes &&
+                    (deep || e->overlap_shallow);
   if (pcap && !e->pstream) {  // (created on first use: multi-rank engines never need them)
     HIP_TRY(hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking), "prefix stream");
     for (hipEvent_t* ev : {&e->ev_gate[0], &e->ev_gate[1], &e->ev_pre})
