@@ -442,7 +442,7 @@ hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, uint3
 // (N ranks, 0: no cap)
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
                        uint32_t grid, uint32_t round, bool record, bool nt, bool cap, uint32_t cap_blocks,
-                       hipStream_t s);
+                       uint32_t simd_waves, hipStream_t s);
 
 // Level mode, rounds q and q + 1 in one launch (one rank): a wave writes its
 // run's rows (round q, always non-temporal: the run's children are written

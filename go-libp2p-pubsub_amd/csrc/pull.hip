@@ -390,9 +390,14 @@ __device__ __forceinline__ void pull_flush(const PullCtr& c, uint64_t* partials,
   }
 }
 
-template <bool kRecord, bool kNT>
+template <bool kRecord, bool kNT, uint32_t kSimdWaves = 0>
 __global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __restrict__ chunks,
                                                  uint32_t n_chunks, uint32_t round) {
+  // (A/B, PSAMD_PULL_SIMD: a clobbered register sizes the VGPR allocation so
+  // that at most kSimdWaves waves fit per SIMD, as k_pull_chain does)
+  if constexpr (kSimdWaves == 4) asm volatile("" ::: "v100");
+  if constexpr (kSimdWaves == 5) asm volatile("" ::: "v90");
+  if constexpr (kSimdWaves == 6) asm volatile("" ::: "v76");
   __shared__ uint64_t src_lds[kBlock / 64][kPullMaxKids];
   __shared__ uint32_t gen_lds[kBlock / 64][kPullMaxKids / 4 + 2];
   const uint32_t lane = threadIdx.x & 63;
@@ -1361,8 +1366,17 @@ size_t lds_cap_pad(K kernel, uint32_t waves) {
 
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
                        uint32_t grid, uint32_t round, bool record, bool nt, bool cap, uint32_t cap_blocks,
-                       hipStream_t s) {
+                       uint32_t simd_waves, hipStream_t s) {
   if (n_chunks == 0 || grid == 0) return hipSuccess;
+  if (nt && !record && simd_waves >= 4 && simd_waves <= 6) {  // (A/B: waves per SIMD by register allocation)
+    if (simd_waves == 4)
+      hipLaunchKernelGGL((k_pull<false, true, 4>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
+    else if (simd_waves == 5)
+      hipLaunchKernelGGL((k_pull<false, true, 5>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
+    else
+      hipLaunchKernelGGL((k_pull<false, true, 6>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
+    return hipGetLastError();
+  }
   // cap: the large (nt) rounds run at most 5 blocks per CU -- 10 KB of LDS
   // left unused per block caps residency (8 blocks: 6 % slower on cfg3's big
   // rounds on one rank); small rounds keep full residency, they need the

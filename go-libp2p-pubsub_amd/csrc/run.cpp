@@ -944,7 +944,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
           // one rank: big rounds at 5 blocks per CU (+6 %); N ranks keep full
           // residency (4 loopback ranks on one GPU: 6.49 -> 7.13 ms capped)
           HIP_TRY(launch_pull(pa, e->d_pull.as<PullChunk>() + c0, c1 - c0, ceil_div(c1 - c0, kBlock / 64), r,
-                              record, nt, world == 1, e->pull_cap_n, s),
+                              record, nt, world == 1 && !e->pull_simd, e->pull_cap_n, e->pull_simd, s),
                   "pull");
         }
         HIP_TRY(time_mark(false), "event");
