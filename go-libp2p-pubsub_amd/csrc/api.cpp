@@ -168,6 +168,7 @@ static void read_switches(ps_engine* e) {
   if (const char* v = std::getenv("PSAMD_FUSE_REDUCE")) e->fuse_reduce = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_SORT_PEER_BITS")) e->sort_peer_bits = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PULL_SIMD")) e->pull_simd = static_cast<uint32_t>(std::atoi(v));
+  if (const char* v = std::getenv("PSAMD_CHAIN_LPT")) e->chain_lpt = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_OVERLAP_SHALLOW")) e->overlap_shallow = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_CHAIN2")) e->chain2 = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_PAD_ALIGN")) e->pad_align = std::max(2, std::min(64, std::atoi(v))) & ~1;

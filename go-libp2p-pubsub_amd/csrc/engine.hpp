@@ -242,6 +242,7 @@ struct ps_engine {
     psamd::ReduceArgs args{};
   } pend_reduce;
   bool overlap_shallow = false;  // (A/B: PSAMD_OVERLAP_SHALLOW=1) windows under overlap_min_rounds overlap their init too
+  bool chain_lpt = false;        // (A/B: PSAMD_CHAIN_LPT=1) a chain launch's whole-row chunks heaviest first
   uint32_t pull_simd = 0;        // (A/B: PSAMD_PULL_SIMD=4..6) big k_pull rounds at that many waves per SIMD
   bool sort_peer_bits = false;   // (A/B: PSAMD_SORT_PEER_BITS=1) the rebuild sorts the peer bits too
   uint32_t small_place = 512;    // top levels up to this many nodes placed by one block

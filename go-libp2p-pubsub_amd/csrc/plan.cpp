@@ -244,6 +244,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   key.push_back(e->chain_tail ? 1 : 0);
   key.push_back(e->chain_slice_small ? 1 : 0);
   key.push_back(e->chain2 ? 1 : 0);
+  key.push_back(e->chain_lpt ? 1 : 0);
   for (size_t q = 0; q < xchg.size(); ++q) key.push_back(xchg[q].any);
   PairPlan& PP = e->pair;
   if (key == PP.key) return false;
@@ -414,11 +415,17 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
       for (uint32_t k = 1; k < len; ++k) kind[q + k] = PS_K_CHAIN2;
       PP.lo[q] = static_cast<uint32_t>(PP.chain.size());
       std::vector<ChainChunk> sliced;  // rows wider than the stage: after the whole-row chunks
+      std::vector<double> weight;      // (A/B chain_lpt) expected words of each whole-row chunk
       chain_parts(q, len, [&](uint32_t t, uint32_t gi, uint32_t d, uint32_t r0, uint32_t levels) {
         const TopicHost& T = e->topics[t];
         const StartGroup& g = L.groups[t][gi];
         const uint32_t W = block_w(tab[t], g);
         const ChainSize z = chain_size(T, d, levels, W);
+        double gsum = 1.0;  // expected nodes per level-d node over the chunk's levels
+        if (e->chain_lpt && T.level_off[d + 1] > T.level_off[d])
+          for (uint32_t k = 1; k < levels && d + k + 1 < T.level_off.size(); ++k)
+            gsum += static_cast<double>(T.level_off[d + k + 1] - T.level_off[d + k]) /
+                    static_cast<double>(T.level_off[d + 1] - T.level_off[d]);
         const uint64_t row0 = block_row0(tab[t], g);
         const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
         for (uint32_t u = lo; u < hi; u += z.R)
@@ -442,8 +449,17 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
             for (uint32_t k = 0; k <= levels && k <= kChainLevels; ++k)
               c.first[k] = T.nbase + (d + k < T.level_off.size() ? T.level_off[d + k] : T.n_nodes);
             (z.S < W ? sliced : PP.chain).push_back(c);
+            if (e->chain_lpt && z.S >= W) weight.push_back((c.node_end - c.node_begin) * gsum * c.S);
           }
       });
+      if (e->chain_lpt && weight.size() == PP.chain.size() - PP.lo[q]) {
+        // the heaviest chunks first: the launch's tail is left to the light ones
+        std::vector<uint32_t> ord(weight.size());
+        for (uint32_t i = 0; i < ord.size(); ++i) ord[i] = i;
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return weight[x] > weight[y]; });
+        std::vector<ChainChunk> tmp(PP.chain.begin() + PP.lo[q], PP.chain.end());
+        for (uint32_t i = 0; i < ord.size(); ++i) PP.chain[PP.lo[q] + i] = tmp[ord[i]];
+      }
       PP.gsplit[q] = static_cast<uint32_t>(PP.chain.size());
       PP.chain.insert(PP.chain.end(), sliced.begin(), sliced.end());
       PP.hi[q] = static_cast<uint32_t>(PP.chain.size());
