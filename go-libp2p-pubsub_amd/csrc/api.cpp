@@ -128,9 +128,33 @@ struct ps_loopback {
   psamd::LoopbackGroup* g;
 };
 
+namespace {
+thread_local std::string g_abi_error;  // ps_abi_check's last mismatch (ps_last_error(NULL))
+}  // namespace
+
 extern "C" {
 
-const char* ps_version(void) { return "psengine-mi355x 0.3 (gfx950)"; }
+const char* ps_version(void) { return "psengine-mi355x 0.5 (gfx950, abi 5)"; }
+
+uint32_t ps_abi_version(void) { return PS_ABI_VERSION; }
+
+int ps_abi_check(uint32_t abi_version, size_t config_size, size_t stats_size, size_t plan_opts_size,
+                 size_t dist_config_size) {
+  char buf[256];
+  if (abi_version != PS_ABI_VERSION)
+    std::snprintf(buf, sizeof buf, "ABI version %u, the library is %u", abi_version, PS_ABI_VERSION);
+  else if (config_size != sizeof(ps_config) || stats_size != sizeof(ps_stats) ||
+           plan_opts_size != sizeof(ps_plan_opts) || dist_config_size != sizeof(ps_dist_config))
+    std::snprintf(buf, sizeof buf,
+                  "struct sizes (config %zu, stats %zu, plan_opts %zu, dist_config %zu) differ from the library's "
+                  "(%zu, %zu, %zu, %zu)",
+                  config_size, stats_size, plan_opts_size, dist_config_size, sizeof(ps_config), sizeof(ps_stats),
+                  sizeof(ps_plan_opts), sizeof(ps_dist_config));
+  else
+    return PS_OK;
+  g_abi_error = buf;
+  return PS_E_INVAL;
+}
 
 // Debug switches read at creation (host phase times, per-wave profiles: they
 // change no plan).  The plan options come from ps_set_plan_opts; only A/B
@@ -166,16 +190,7 @@ static void read_switches(ps_engine* e) {
   if (const char* v = std::getenv("PSAMD_UPLOAD_REUSE")) e->upload_reuse = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_SIG_WINDOWS")) e->sig_windows = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FUSE_REDUCE")) e->fuse_reduce = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_SORT_PEER_BITS")) e->sort_peer_bits = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_PULL_SIMD")) e->pull_simd = static_cast<uint32_t>(std::atoi(v));
-  if (const char* v = std::getenv("PSAMD_CHAIN_LPT")) e->chain_lpt = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_OVERLAP_SHALLOW")) e->overlap_shallow = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_CHAIN2")) e->chain2 = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_PAD_ALIGN")) e->pad_align = std::max(2, std::min(64, std::atoi(v))) & ~1;
-  if (const char* v = std::getenv("PSAMD_CHAIN_SLICE_SMALL")) e->chain_slice_small = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_LB_PLACE")) e->lb_place = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_PULL_CAP_N")) e->pull_cap_n = static_cast<uint32_t>(std::atoi(v));
-  if (const char* v = std::getenv("PSAMD_REDUCE_FORK_BYTES")) e->reduce_fork_bytes = std::strtoull(v, nullptr, 10);
   if (const char* v = std::getenv("PSAMD_FLOOD_MIN_ROUNDS"))
     o.flood_min_rounds = static_cast<uint32_t>(std::max(1, std::atoi(v)));
   if (const char* v = std::getenv("PSAMD_CHAIN_WAVES"))
@@ -314,7 +329,9 @@ void ps_destroy(ps_engine* e) {
   delete e;
 }
 
-const char* ps_last_error(const ps_engine* e) { return e ? e->err.c_str() : "null engine"; }
+const char* ps_last_error(const ps_engine* e) {
+  return e ? e->err.c_str() : g_abi_error.empty() ? "null engine" : g_abi_error.c_str();
+}
 
 int ps_topic_create(ps_engine* e, uint32_t topic, uint32_t root, uint32_t w, uint32_t mw) {
   if (!e) return PS_E_INVAL;

@@ -218,9 +218,6 @@ struct ps_engine {
   psamd::WindowLayout probe;     // the probe's last planned window
   bool host_timing = false;      // PSAMD_HOST_TIMING=1: host phase times to stderr
   bool lb_place = true;           // levels placed by one look-back launch each (A/B: PSAMD_LB_PLACE=0)
-  bool chain_slice_small = false;  // (A/B: PSAMD_CHAIN_SLICE_SMALL=1) one-node chain runs of huge subtrees cut into slices
-  bool chain2 = false;            // (A/B: PSAMD_CHAIN2=1) two-round launches as chains (v3, one round trip), not pairs
-  uint32_t pad_align = 2;         // (A/B: PSAMD_PAD_ALIGN) rows of >= pad_words words padded to a multiple of this
   bool sig_windows = true;        // pipelined one-rank windows end with a pinned flag, not an event (A/B: PSAMD_SIG_WINDOWS=0)
   // per-window uploads (topic table, seeds, descriptors) kept on the device:
   // the bytes last staged into each buffer, skipped when a window repeats them
@@ -241,10 +238,6 @@ struct ps_engine {
     const void* owner = nullptr;  // the Inflight slot whose flag it raises
     psamd::ReduceArgs args{};
   } pend_reduce;
-  bool overlap_shallow = false;  // (A/B: PSAMD_OVERLAP_SHALLOW=1) windows under overlap_min_rounds overlap their init too
-  bool chain_lpt = false;        // (A/B: PSAMD_CHAIN_LPT=1) a chain launch's whole-row chunks heaviest first
-  uint32_t pull_simd = 0;        // (A/B: PSAMD_PULL_SIMD=4..6) big k_pull rounds at that many waves per SIMD
-  bool sort_peer_bits = false;   // (A/B: PSAMD_SORT_PEER_BITS=1) the rebuild sorts the peer bits too
   uint32_t small_place = 512;    // top levels up to this many nodes placed by one block
   // GPU rebuild of the node space: on by default for one
   // rank and tree topics (PSAMD_GPU_BUILD=0: host build)
@@ -426,8 +419,6 @@ struct ps_engine {
   bool overlap_on = true;
   uint32_t overlap_min_rounds = 12;
   uint64_t overlap_min_bytes = 512ull << 20;  // row bytes of the window at least (PSAMD_OVERLAP_BYTES)
-  uint64_t reduce_fork_bytes = 0;
-  uint32_t pull_cap_n = 0;                     // (A/B) N ranks: k_pull nt blocks per CU at most (0: no cap)              // (A/B) windows of fewer row bytes reduce on their own stream
   hipStream_t pstream = nullptr;
   hipStream_t rstream = nullptr;  // a pipelined window's counter reduce, beside the next window
   hipEvent_t ev_gate[2] = {nullptr, nullptr}, ev_pre = nullptr, ev_end = nullptr;

@@ -513,7 +513,7 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   HIP_TRY(e->d_lvl.ensure(static_cast<size_t>(nt) * 512 * 4), "alloc level tables");
   size_t cub_bytes = 0, scan_bytes = 0;
   const BuildKey kf = build_key(n);
-  HIP_TRY(sort_keys(nullptr, &cub_bytes, nullptr, nullptr, n, kf, e->sort_peer_bits, s), "sort size");
+  HIP_TRY(sort_keys(nullptr, &cub_bytes, nullptr, nullptr, n, kf, false, s), "sort size");
   HIP_TRY(e->d_cub.ensure(std::max<size_t>(cub_bytes, 16)), "alloc sort temp");
   // [t][reach, max depth, max fan-out, unresolved]
   uint32_t* gstat = e->d_gstat.as<uint32_t>();
@@ -539,7 +539,7 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
               "depth");
       size_t tb = e->d_cub.bytes;
       HIP_TRY(sort_keys(e->d_cub.p, &tb, e->d_keys0.as<uint64_t>(),
-                        e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n, kf, e->sort_peer_bits, s),
+                        e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n, kf, false, s),
               "sort");
       HIP_TRY(launch_level_starts(e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n,
                                   e->d_lvl.as<uint32_t>() + 512 * t, kf, s),

@@ -438,11 +438,10 @@ hipError_t launch_seed(const SeedDev* seeds, uint32_t lo, uint32_t hi, uint64_t*
 hipError_t launch_expand(const ExpandArgs& a, uint32_t round, bool record, uint32_t grid, hipStream_t s);
 // Level mode, pull direction: one wave per chunk, grid = ceil(n_chunks / 4)
 // blocks; nt: the row stores are non-temporal (rounds nobody re-reads soon);
-// cap: an nt round runs at most 5 blocks per CU (one rank); else cap_blocks
-// (N ranks, 0: no cap)
+// cap: an nt round runs at most 5 blocks per CU (one rank; N ranks keep full
+// residency)
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                       uint32_t grid, uint32_t round, bool record, bool nt, bool cap, uint32_t cap_blocks,
-                       uint32_t simd_waves, hipStream_t s);
+                       uint32_t grid, uint32_t round, bool record, bool nt, bool cap, hipStream_t s);
 
 // Level mode, rounds q and q + 1 in one launch (one rank): a wave writes its
 // run's rows (round q, always non-temporal: the run's children are written

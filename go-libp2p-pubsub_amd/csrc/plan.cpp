@@ -74,7 +74,8 @@ int plan_window_layout(ps_engine* e, const std::vector<RunMsg>& msgs, const std:
       // <= 1/16 more bytes against half the store instructions (cfg3 1.015
       // -> 1.003 ms/step, the 4-rank cfg4 loopback's 63-word rows 2.49x ->
       // 2.32x; profiles/r03/ab_pad.txt)
-      if (d.W >= e->pad_words) d.W = (d.W + e->pad_align - 1) / e->pad_align * e->pad_align;
+      // (16-word alignment measured no faster: profiles/r04/ab/NOTES.md)
+      if (d.W >= e->pad_words) d.W = (d.W + 1) & ~1u;
       L.groups[t].push_back(StartGroup{s_lo, 0, d.W});
     } else {
       // Start groups (a tree's messages entering at different rounds): the
@@ -242,9 +243,6 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   key.push_back(e->chain_words);
   key.push_back(static_cast<uint64_t>(e->launch_bytes));
   key.push_back(e->chain_tail ? 1 : 0);
-  key.push_back(e->chain_slice_small ? 1 : 0);
-  key.push_back(e->chain2 ? 1 : 0);
-  key.push_back(e->chain_lpt ? 1 : 0);
   for (size_t q = 0; q < xchg.size(); ++q) key.push_back(xchg[q].any);
   PairPlan& PP = e->pair;
   if (key == PP.key) return false;
@@ -290,7 +288,6 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
     uint32_t R = 0, S = 0;  // R = 0: no chain of this length
   };
   constexpr uint32_t stage_w = kChainWords, cap = kChainCap;
-  constexpr double kSliceChunks = 16384;  // slicing for parallelism: at most this many slice chunks per level
   auto chain_size = [&](const TopicHost& T, uint32_t d, uint32_t levels, uint32_t W) {
     ChainSize z;
     const double n0 = static_cast<double>(T.level_off[d + 1] - T.level_off[d]);
@@ -311,22 +308,10 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
                                std::floor(cap / 2 / gmax),
                                std::floor(static_cast<double>(e->chain_words) / (z.S * gsum))});
     z.R = static_cast<uint32_t>(std::max(1.0, r));
-    // (A/B, off by default) A one-node run whose subtree alone is many times
-    // chain_words, on a level of few nodes, leaves the launch a few hundred
-    // long waves (cfg2: 512 waves of 31k words on 256 CUs, 29 us); cutting its
-    // rows into column slices of about chain_words / subtree nodes words, one
-    // wave per slice, measured no faster: cfg2 0.0536 either way with 16-word
-    // aligned rows, cfg3 0.908 vs 0.898, cfg4 flat (profiles/r04/ab/NOTES.md).
-    // (Only rows of whole 128-B lines: a slice boundary inside a line would
-    // have two waves write parts of one line -- cfg2's 158-word rows cut at
-    // 40 words: 0.053 -> 0.081 ms/step.)
-    if (e->chain_slice_small && z.R == 1 && z.S == W && W % 16 == 0 && z.S * gsum > 2.0 * e->chain_words &&
-        n0 * (z.S * gsum / e->chain_words) <= kSliceChunks) {
-      constexpr uint32_t kMinSlice = 32;
-      uint32_t s = static_cast<uint32_t>(std::ceil(e->chain_words / gsum));
-      s = std::max(kMinSlice, (s + 15u) & ~15u);
-      if (s < z.S) z.S = s;
-    }
+    // (Rejected in round 4, profiles/r04/ab/NOTES.md: one-node runs of huge
+    // subtrees cut into column slices for parallelism -- cfg2 0.0536 either
+    // way, cfg3 0.908 vs 0.898 -- and two-round launches as two-level chains
+    // instead of pairs.)
     return z;
   };
   // the (topic, group)s a launch of rounds q .. q + len - 1 writes: level d
@@ -370,11 +355,9 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
     });
     return ok;
   };
-  // two rounds: a pair, or (chain2, A/B) a two-level chain where one is possible
-  auto chain_two = [&](uint32_t q) { return e->chain2 && q + 1 <= rounds && can_chain(q, 2); };
   auto can = [&](uint32_t q, uint32_t len) {
     if (len == 1) return true;
-    if (len == 2) return chain_two(q) || static_cast<bool>(can2[q]);
+    if (len == 2) return static_cast<bool>(can2[q]);
     return can_chain(q, len);
   };
   // best[q]: traffic of rounds q..rounds; take[q]: rounds of the launch starting at q
@@ -410,22 +393,16 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
       continue;
     }
     PP.len[q] = len;
-    if (len >= 3 || (len == 2 && chain_two(q))) {
+    if (len >= 3) {
       kind[q] = PS_K_CHAIN;
       for (uint32_t k = 1; k < len; ++k) kind[q + k] = PS_K_CHAIN2;
       PP.lo[q] = static_cast<uint32_t>(PP.chain.size());
       std::vector<ChainChunk> sliced;  // rows wider than the stage: after the whole-row chunks
-      std::vector<double> weight;      // (A/B chain_lpt) expected words of each whole-row chunk
       chain_parts(q, len, [&](uint32_t t, uint32_t gi, uint32_t d, uint32_t r0, uint32_t levels) {
         const TopicHost& T = e->topics[t];
         const StartGroup& g = L.groups[t][gi];
         const uint32_t W = block_w(tab[t], g);
         const ChainSize z = chain_size(T, d, levels, W);
-        double gsum = 1.0;  // expected nodes per level-d node over the chunk's levels
-        if (e->chain_lpt && T.level_off[d + 1] > T.level_off[d])
-          for (uint32_t k = 1; k < levels && d + k + 1 < T.level_off.size(); ++k)
-            gsum += static_cast<double>(T.level_off[d + k + 1] - T.level_off[d + k]) /
-                    static_cast<double>(T.level_off[d + 1] - T.level_off[d]);
         const uint64_t row0 = block_row0(tab[t], g);
         const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
         for (uint32_t u = lo; u < hi; u += z.R)
@@ -449,17 +426,9 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
             for (uint32_t k = 0; k <= levels && k <= kChainLevels; ++k)
               c.first[k] = T.nbase + (d + k < T.level_off.size() ? T.level_off[d + k] : T.n_nodes);
             (z.S < W ? sliced : PP.chain).push_back(c);
-            if (e->chain_lpt && z.S >= W) weight.push_back((c.node_end - c.node_begin) * gsum * c.S);
           }
       });
-      if (e->chain_lpt && weight.size() == PP.chain.size() - PP.lo[q]) {
-        // the heaviest chunks first: the launch's tail is left to the light ones
-        std::vector<uint32_t> ord(weight.size());
-        for (uint32_t i = 0; i < ord.size(); ++i) ord[i] = i;
-        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return weight[x] > weight[y]; });
-        std::vector<ChainChunk> tmp(PP.chain.begin() + PP.lo[q], PP.chain.end());
-        for (uint32_t i = 0; i < ord.size(); ++i) PP.chain[PP.lo[q] + i] = tmp[ord[i]];
-      }
+      // (heaviest chunks first measured no difference: profiles/r04/ab/chain_lpt.log)
       PP.gsplit[q] = static_cast<uint32_t>(PP.chain.size());
       PP.chain.insert(PP.chain.end(), sliced.begin(), sliced.end());
       PP.hi[q] = static_cast<uint32_t>(PP.chain.size());

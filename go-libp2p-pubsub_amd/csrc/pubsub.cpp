@@ -71,6 +71,11 @@ Network::Network(uint32_t n_hosts, uint32_t max_topics, int device) : max_topics
   cfg.msg_window = window_;
   cfg.device = device;
   cfg.seed = 1;
+  if (PS_ABI_CHECK() != PS_OK) {
+    e_ = nullptr;
+    status_ = Error{PS_E_INVAL, ps_last_error(nullptr)};
+    return;
+  }
   const int rc = ps_create(&cfg, &e_);
   if (rc != PS_OK) {
     e_ = nullptr;

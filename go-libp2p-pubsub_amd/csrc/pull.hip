@@ -390,14 +390,11 @@ __device__ __forceinline__ void pull_flush(const PullCtr& c, uint64_t* partials,
   }
 }
 
-template <bool kRecord, bool kNT, uint32_t kSimdWaves = 0>
+// (Capping the big rounds' residency through the register allocation, as
+// k_pull_chain does, measured no gain: profiles/r04/ab/pull_simd.log.)
+template <bool kRecord, bool kNT>
 __global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __restrict__ chunks,
                                                  uint32_t n_chunks, uint32_t round) {
-  // (A/B, PSAMD_PULL_SIMD: a clobbered register sizes the VGPR allocation so
-  // that at most kSimdWaves waves fit per SIMD, as k_pull_chain does)
-  if constexpr (kSimdWaves == 4) asm volatile("" ::: "v100");
-  if constexpr (kSimdWaves == 5) asm volatile("" ::: "v90");
-  if constexpr (kSimdWaves == 6) asm volatile("" ::: "v76");
   __shared__ uint64_t src_lds[kBlock / 64][kPullMaxKids];
   __shared__ uint32_t gen_lds[kBlock / 64][kPullMaxKids / 4 + 2];
   const uint32_t lane = threadIdx.x & 63;
@@ -1009,7 +1006,7 @@ __device__ __forceinline__ void chain_meta_issue(const PullArgs& a, const ChainC
 
 // Packs the issued batch (the first use of p / f: the loads' wait).
 __device__ __forceinline__ void chain_meta_pack(const ChainChunk* cp, uint32_t levels, uint32_t p_lo, uint32_t g0,
-                                                uint32_t lane, const uint32_t (&p)[kMetaSlots],
+                                                bool direct, uint32_t lane, const uint32_t (&p)[kMetaSlots],
                                                 const uint32_t (&f)[kMetaSlots], ChainMeta& M) {
   M.g0 = g0;
   MetaCursor m;
@@ -1019,8 +1016,12 @@ __device__ __forceinline__ void chain_meta_pack(const ChainChunk* cp, uint32_t l
     if (i) m.step(cp, levels, g0 + i);
     if (m.k >= levels) break;  // (the slots past it are never picked)
     const uint32_t y = m.lo + (g0 + i - m.kb) * 64 + lane;
-    const uint32_t e = y < m.hi
-                           ? (p[i] - m.plo) | (((f[i] >> (8 * (y & 3))) & kNodeLive) ? kMetaLive : 0u)
+    // (a level-0 entry of the direct path -- parents spanning more than the
+    // stage, possibly > 65,535 ids -- is never picked: kMetaNone, so that it
+    // cannot spill into the next slot's half; deeper levels' parent indices
+    // are < kChainCap, checked by k_chain_ranges)
+    const uint32_t e = (y < m.hi && (m.k > 0 || !direct))
+                           ? ((p[i] - m.plo) & (kMetaLive - 1)) | (((f[i] >> (8 * (y & 3))) & kNodeLive) ? kMetaLive : 0u)
                            : kMetaNone;
     if (i & 1)
       M.w[i / 2] |= e << 16;
@@ -1203,13 +1204,12 @@ __device__ __forceinline__ void chain_level0_direct(const PullArgs& a, const Cha
 template <bool kRecord, bool kNT, bool kSlices, bool kInNT = true, uint32_t kSimdWaves = 0>
 __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk* __restrict__ chunks,
                                                    uint32_t n_chunks, uint32_t round) {
-  // kSimdWaves (3 or 2): a register the kernel never uses, declared clobbered,
+  // kSimdWaves (3): a register the kernel never uses, declared clobbered,
   // sizes its VGPR allocation so that exactly that many waves fit per SIMD --
   // a residency cap spread evenly over the CU's 4 SIMDs (an LDS cap leaves
   // the placement to the dispatcher: 12 waves per CU 0.920 ms/step on cfg3,
   // 3 per SIMD 0.90, profiles/r04/ab_chain_waves.txt)
   if constexpr (kSimdWaves == 3) asm volatile("" ::: "v140");
-  if constexpr (kSimdWaves == 2) asm volatile("" ::: "v180");
   constexpr uint32_t kStage = kChainWords, kCap = kChainCap;
   __shared__ __attribute__((aligned(16))) uint64_t stage[kStage + 2];  // the parents' rows (slices); + the zero pair
   __shared__ __attribute__((aligned(16))) uint32_t ctab[kChainKids];   // a sub-run's stage offsets
@@ -1273,7 +1273,7 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
           PSAMD_DMA(pw32 + min(d0 + lane, 2 * words - 1), reinterpret_cast<uint32_t*>(stage) + d0, 4);
       }
     }
-    chain_meta_pack(cp, levels, p_lo, 0u, lane, mp, mf, M);  // (waits for every load above)
+    chain_meta_pack(cp, levels, p_lo, 0u, direct, lane, mp, mf, M);  // (waits for every load above)
   }
   if (lane < 2) stage[kStage + lane] = 0;
   uint32_t g = 0;   // the global metadata slot of the next node group
@@ -1308,7 +1308,7 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
       if (g + ng > M.g0 + kMetaSlots) {
         uint32_t mp[kMetaSlots], mf[kMetaSlots];
         chain_meta_issue(a, cp, levels, p_lo, g, lane, mp, mf);
-        chain_meta_pack(cp, levels, p_lo, g, lane, mp, mf, M);
+        chain_meta_pack(cp, levels, p_lo, g, direct, lane, mp, mf, M);
       }
       uint8_t* const tab = tabs[k & 1] + (y0 - lo);
 #pragma unroll
@@ -1365,24 +1365,13 @@ size_t lds_cap_pad(K kernel, uint32_t waves) {
 }  // namespace
 
 hipError_t launch_pull(const PullArgs& a, const PullChunk* chunks, uint32_t n_chunks,
-                       uint32_t grid, uint32_t round, bool record, bool nt, bool cap, uint32_t cap_blocks,
-                       uint32_t simd_waves, hipStream_t s) {
+                       uint32_t grid, uint32_t round, bool record, bool nt, bool cap, hipStream_t s) {
   if (n_chunks == 0 || grid == 0) return hipSuccess;
-  if (nt && !record && simd_waves >= 4 && simd_waves <= 6) {  // (A/B: waves per SIMD by register allocation)
-    if (simd_waves == 4)
-      hipLaunchKernelGGL((k_pull<false, true, 4>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
-    else if (simd_waves == 5)
-      hipLaunchKernelGGL((k_pull<false, true, 5>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
-    else
-      hipLaunchKernelGGL((k_pull<false, true, 6>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
-    return hipGetLastError();
-  }
   // cap: the large (nt) rounds run at most 5 blocks per CU -- 10 KB of LDS
   // left unused per block caps residency (8 blocks: 6 % slower on cfg3's big
   // rounds on one rank); small rounds keep full residency, they need the
   // waves in flight
-  // (cap_blocks, N ranks: an A/B cap of blocks per CU, PSAMD_PULL_CAP_N)
-  const size_t kBigRoundLdsPad = cap ? 10240 : cap_blocks ? lds_cap_pad(k_pull<false, true>, cap_blocks) : 0;
+  const size_t kBigRoundLdsPad = cap ? 10240 : 0;
   if (record)  // parity runs: one variant
     hipLaunchKernelGGL((k_pull<true, false>), dim3(grid), dim3(kBlock), 0, s, a, chunks, n_chunks, round);
   else if (nt)
@@ -1457,9 +1446,9 @@ hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32
       lds_cap_pad(k_pull_chain<false, true, false>, 11), lds_cap_pad(k_pull_chain<false, true, false>, 12),
       lds_cap_pad(k_pull_chain<false, true, false>, 13), lds_cap_pad(k_pull_chain<false, true, false>, 14),
       lds_cap_pad(k_pull_chain<false, true, false>, 15), lds_cap_pad(k_pull_chain<false, true, false>, 16)};
-  // 12 and 8 per CU: 3 and 2 per SIMD through the register allocation
-  // (whole rows, production variants); other caps through an LDS pad
-  const uint32_t simd = waves_per_cu == 12 ? 3u : waves_per_cu == 8 ? 2u : 0u;
+  // 12 per CU: 3 per SIMD through the register allocation (the production
+  // variants); other caps through an LDS pad
+  const uint32_t simd = waves_per_cu == 12 ? 3u : 0u;
   const size_t pad = simd ? 0 : pads[std::min<uint32_t>(waves_per_cu, 16)];
   const dim3 g(n_chunks), b(64);
 #define PSAMD_CHAIN(...) hipLaunchKernelGGL((k_pull_chain<__VA_ARGS__>), g, b, pad, s, a, chunks, n_chunks, round)
@@ -1468,8 +1457,6 @@ hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32
       PSAMD_CHAIN(true, false, true);
     else if (simd == 3)
       PSAMD_CHAIN(false, true, true, true, 3);
-    else if (simd == 2)
-      PSAMD_CHAIN(false, true, true, true, 2);
     else
       PSAMD_CHAIN(false, true, true);
   } else if (record) {
@@ -1484,11 +1471,6 @@ hipError_t launch_pull_chain(const PullArgs& a, const ChainChunk* chunks, uint32
       PSAMD_CHAIN(false, true, false, true, 3);
     else
       PSAMD_CHAIN(false, false, false, true, 3);
-  } else if (simd == 2) {
-    if (nt)
-      PSAMD_CHAIN(false, true, false, true, 2);
-    else
-      PSAMD_CHAIN(false, false, false, true, 2);
   } else if (nt) {
     PSAMD_CHAIN(false, true, false);
   } else {

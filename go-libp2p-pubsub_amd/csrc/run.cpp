@@ -4,6 +4,8 @@
 // stream beside each round's locally fed chunks; compaction mode: k_expand +
 // frontier compaction), counters and readbacks.  DESIGN.md §5-§7.
 #include <algorithm>
+#include <chrono>
+#include <immintrin.h>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -539,8 +541,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // -- ends signalled instead: its events cost more than the init, cfg4
   // 0.4472-0.4479 -> 0.4421-0.4425 ms/step, profiles/r04/ab/shallow_signalled.log)
   const bool pcap = e->overlap_on && level && world == 1 && !any_mesh && !record && !L.multi &&
-                    !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS)) && total >= e->overlap_min_bytes &&
-                    (deep || e->overlap_shallow);
+                    !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS)) && total >= e->overlap_min_bytes && deep;
   if (pcap && !e->pstream) {  // (created on first use: multi-rank engines never need them)
     HIP_TRY(hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking), "prefix stream");
     for (hipEvent_t* ev : {&e->ev_gate[0], &e->ev_gate[1], &e->ev_pre})
@@ -944,7 +945,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
           // one rank: big rounds at 5 blocks per CU (+6 %); N ranks keep full
           // residency (4 loopback ranks on one GPU: 6.49 -> 7.13 ms capped)
           HIP_TRY(launch_pull(pa, e->d_pull.as<PullChunk>() + c0, c1 - c0, ceil_div(c1 - c0, kBlock / 64), r,
-                              record, nt, world == 1 && !e->pull_simd, e->pull_cap_n, e->pull_simd, s),
+                              record, nt, world == 1, s),
                   "pull");
         }
         HIP_TRY(time_mark(false), "event");
@@ -973,7 +974,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     // window's first launches (its partial slots and descriptors are this
     // slot's; ps_wait waits for it through the window's end event)
     hipStream_t rs = s;
-    if (direct && world == 1 && !sigwin && total >= e->reduce_fork_bytes) {  // (the next window's launches never wait for it)
+    if (direct && world == 1 && !sigwin) {  // (the next window's launches never wait for it)
       if (!e->rstream) HIP_TRY(hipStreamCreateWithFlags(&e->rstream, hipStreamNonBlocking), "reduce stream");
       if (!e->ev_end) HIP_TRY(hipEventCreateWithFlags(&e->ev_end, kStreamEvent), "reduce event");
       HIP_TRY(hipEventRecord(e->ev_end, s), "event");
@@ -1464,12 +1465,23 @@ int ps_wait(ps_engine* e, ps_stats* out) {
     // poll the window's flag (pinned, written after its reduce); a stream
     // that has drained or failed without it is an error, not a hang
     const volatile uint64_t* flag = f.sig;
+    // Back-off: pause-spin for the first ~50 us (a cfg2 window
+    // is ~50 us: a sleep's timer slack would cost a step), then yield the
+    // core between polls, and past 2 ms sleep 20 us per poll -- a caller
+    // publishing the next batch from another thread is not starved
+    const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t spin = 0; *flag != f.seq; ++spin) {
-      if ((spin & 1023) == 1023) {
+      _mm_pause();
+      if ((spin & 255) == 255) {
         const hipError_t q = hipStreamQuery(e->stream);
         if (q != hipSuccess && q != hipErrorNotReady) return e->fail(PS_E_DEVICE, "window: stream failed");
         if (q == hipSuccess && *flag != f.seq) return e->fail(PS_E_DEVICE, "window: completion flag missing");
-        std::this_thread::yield();
+        const auto us =
+            std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+        if (us > 2000)
+          std::this_thread::sleep_for(std::chrono::microseconds(20));
+        else if (us > 50)
+          std::this_thread::yield();
       }
     }
     std::atomic_thread_fence(std::memory_order_acquire);

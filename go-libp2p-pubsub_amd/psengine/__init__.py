@@ -119,8 +119,12 @@ class MessageBuf(C.Structure):
                 ("tree_width", C.c_int64), ("tree_max_width", C.c_int64), ("num_peers", C.c_int64)]
 
 
+ABI_VERSION = 5  # PS_ABI_VERSION of include/psengine.h this binding mirrors
+
 PROTOTYPES = [
     ("ps_version", C.c_char_p, []),
+    ("ps_abi_version", C.c_uint32, []),
+    ("ps_abi_check", C.c_int, [C.c_uint32, C.c_size_t, C.c_size_t, C.c_size_t, C.c_size_t]),
     ("ps_create", C.c_int, [C.POINTER(Config), C.POINTER(_P)]),
     ("ps_destroy", None, [_P]),
     ("ps_last_error", C.c_char_p, [_P]),
@@ -179,6 +183,11 @@ def load(build_if_missing: bool = False):
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        # the structs this module declares must match the library's layouts
+        rc = L.ps_abi_check(ABI_VERSION, C.sizeof(Config), C.sizeof(Stats), C.sizeof(PlanOpts),
+                            C.sizeof(DistConfig))
+        if rc != 0:
+            raise RuntimeError(f"libpsengine ABI mismatch: {L.ps_last_error(None).decode()}")
         _lib = L
     return _lib
 

@@ -135,6 +135,20 @@ void ps_destroy(ps_engine* e);
 const char* ps_last_error(const ps_engine* e);
 const char* ps_version(void);
 
+/* ABI guard.  The public structs' layouts are versioned by PS_ABI_VERSION
+ * (5: ps_stats gained the plan diagnostics and xchg fields, ps_dist_config
+ * its flags word -- a caller built against an older header would read or
+ * write past its own structs).  A binding calls ps_abi_check once, with the
+ * sizes it was compiled with (PS_ABI_CHECK() in C/C++); PS_E_INVAL on any
+ * mismatch, with ps_last_error(NULL) naming it. */
+#define PS_ABI_VERSION 5u
+uint32_t ps_abi_version(void);
+int ps_abi_check(uint32_t abi_version, size_t config_size, size_t stats_size,
+                 size_t plan_opts_size, size_t dist_config_size);
+#define PS_ABI_CHECK()                                                        \
+  ps_abi_check(PS_ABI_VERSION, sizeof(ps_config), sizeof(ps_stats),           \
+               sizeof(struct ps_plan_opts), sizeof(struct ps_dist_config))
+
 /* ---- topics: TopicManager.NewTopic + TreeOpts (pubsub.go:49-97),
  *      Topic.Close (pubsub.go:99-103).  width 0 -> engine default.            */
 int ps_topic_create(ps_engine* e, uint32_t topic, uint32_t root,

@@ -84,6 +84,66 @@ def test_version_and_error_paths(lib):
     assert lib.ps_create(ctypes.byref(cfg), ctypes.byref(h)) == -1  # n_peers == 0
 
 
+def test_abi_check(lib):
+    """ps_abi_check accepts the sizes this binding was built with and refuses
+    a caller compiled against another layout (ps_stats grew 32 B,
+    ps_dist_config 8 B, without a version bump)."""
+    assert lib.ps_abi_version() == PE.ABI_VERSION == 5
+    sizes = (ctypes.sizeof(PE.Config), ctypes.sizeof(PE.Stats), ctypes.sizeof(PE.PlanOpts),
+             ctypes.sizeof(PE.DistConfig))
+    assert lib.ps_abi_check(PE.ABI_VERSION, *sizes) == 0
+    assert lib.ps_abi_check(3, *sizes) == -1
+    assert b"ABI version 3" in lib.ps_last_error(None)
+    old = (sizes[0], sizes[1] - 32, sizes[2], sizes[3] - 8)  # the round-3 layouts
+    assert lib.ps_abi_check(PE.ABI_VERSION, *old) == -1
+    assert b"struct sizes" in lib.ps_last_error(None)
+    assert b"abi 5" in lib.ps_version()
+
+
+def _kernel_regs(tmp_path):
+    """{kernel symbol: (vgpr_count, agpr_count)} from the gfx950 code
+    objects' AMDGPU metadata notes (llvm-objdump --offloading extracts them
+    next to its input, so it runs on a copy)."""
+    import shutil
+
+    so = tmp_path / "libpsengine.so"
+    shutil.copy(PE.lib_path(), so)
+    llvm = "/opt/rocm/lib/llvm/bin"
+    subprocess.run([f"{llvm}/llvm-objdump", "--offloading", str(so)], capture_output=True, check=True,
+                   cwd=tmp_path)
+    regs = {}
+    for co in sorted(tmp_path.glob("*gfx950*")):
+        notes = subprocess.run([f"{llvm}/llvm-readelf", "--notes", str(co)], capture_output=True, text=True,
+                               check=True).stdout
+        for blk in notes.split("  - .agpr_count:")[1:]:
+            name = re.search(r"\.name:\s+(\S+)", blk).group(1)
+            vg = int(re.search(r"\.vgpr_count:\s+(\d+)", blk).group(1))
+            regs[name] = (vg, int(blk.split("\n")[0].strip()))
+    return regs
+
+
+def test_chain_residency_vgprs(lib, tmp_path):
+    """The production k_pull_chain variants (kSimdWaves = 3) must allocate
+    registers for exactly 3 waves per SIMD (512 VGPRs per lane, allocated
+    in granules of 8, AGPRs from the same file): the round-4 residency gain
+    (0.951 -> 0.902 ms/step on cfg3) rests on a clobbered
+    v140, which a compiler change could silently undo.  The uncapped
+    variants must fit more than 3, or the cap would be doing nothing."""
+    regs = _kernel_regs(tmp_path)
+
+    def waves(v):
+        return 512 // ((v[0] + v[1] + 7) // 8 * 8)
+
+    capped = {k: v for k, v in regs.items() if "k_pull_chain" in k and k.endswith("Lj3EEEvNS_8PullArgsEPKNS_10ChainChunkEjj")}
+    free = {k: v for k, v in regs.items() if "k_pull_chain" in k and "Lj0EEEv" in k}
+    assert len(capped) >= 3, sorted(regs)
+    for k, v in capped.items():
+        assert waves(v) == 3, (k, v)
+    assert free
+    for k, v in free.items():
+        assert waves(v) > 3, (k, v)
+
+
 def test_no_cpu_fallback_without_gpu(lib):
     """On a machine without a GPU the engine refuses to start (PS_E_DEVICE):
     there is no silent CPU path."""

@@ -201,3 +201,29 @@ def test_chain_many_windows_and_drains(monkeypatch):
             drains = [eng.peer_messages(t, p).tolist() for t in range(len(topics)) for p in peers]
             outs.append((st.deliveries, drains))
     assert outs[0] == outs[1] == outs[2]
+
+
+def test_chain_direct_level0_wide_parent_span(monkeypatch):
+    """a chain run of <= 64 nodes whose parents span more
+    than 65,535 ids, with a level below it.  Level 2 holds 140,000 nodes and
+    only its first and last have children (2 each), so the chain of rounds
+    3-5 has one run of 4 nodes whose parents' span takes the direct level-0
+    path; its level-0 metadata slot shares a register with level 1's.  The
+    relative parent index (139,999) must not spill into level 1's half: the
+    second level-3 node is dead, and a spilled bit would hand its children
+    the live fourth node's row.  (Rounds 1-2 pair: the level-1 -> 2 growth of
+    700 is wider than a chain's level tables.)"""
+    from test_plan_cpu import wide_span_tree
+
+    parent, _, _, l3 = wide_span_tree()
+    l4 = l3 + 4
+    n = parent.shape[0]
+    live = np.ones(n, dtype=np.uint8)
+    live[l3 + 1] = 0
+    msg_topics = np.zeros(100, dtype=np.uint32)
+    sweep(monkeypatch, n, [(0, parent)], live, msg_topics, chains=(1, 3, 4))
+    for record in (True, False):
+        st, kinds, hops, _, _ = run(monkeypatch, 4, n, [(0, parent)], live, msg_topics, record=record)
+        assert kinds[1] == PE.K_PAIR and kinds[3] == PE.K_CHAIN, kinds
+    exp = oracle_hops([(0, parent)], live)[0]
+    assert exp[l4 + 2] == exp[l4 + 3] == 0xFF and exp[l4 + 6] == 4

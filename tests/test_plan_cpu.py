@@ -586,3 +586,35 @@ def test_plan_opts_defaults_pinned():
         os.environ.update(env)
     with pytest.raises(PE.EngineError):
         PL.Plan(parent[None, :], [0]).set_plan(chain_max=7)
+
+
+def wide_span_tree():
+    """Level 1: 200 nodes; level 2: 700 children each (140,000 nodes), of
+    which only the first and the last have children (2 each); levels 4 and 5
+    double.  Peer ids are BFS numbers.  Returns (parent, first level-2 id,
+    last level-2 id, first level-3 id)."""
+    parent = [NONE] + [0] * 200 + list(np.repeat(np.arange(1, 201), 700))
+    l2_first, l2_last = 201, 140200
+    parent += [l2_first, l2_first, l2_last, l2_last]
+    l3 = 140201
+    parent += [l3 + j // 2 for j in range(8)]
+    parent += [l3 + 4 + j // 2 for j in range(16)]
+    return np.array(parent, dtype=np.uint32), l2_first, l2_last, l3
+
+
+def test_chain_run_with_wide_parent_span_plan():
+    """The plan behind test_gpu_chain.py::test_chain_direct_level0_wide_parent_span
+    (ADVICE r4): rounds 1-2 pair (level 2 grows 700x, wider than a chain's
+    level tables), rounds 3-5 chain, and that chain's one run of level-3
+    nodes has parents 139,999 ids apart -- the direct level-0 path whose
+    metadata slot must not spill into level 1's."""
+    parent, l2_first, l2_last, l3 = wide_span_tree()
+    p = PL.Plan(parent[None, :], [0], plan={"flood": 0, "chain_max": 4})
+    p.window(np.zeros(100, dtype=np.uint32))
+    kinds = [int(k) for k in p.get(PL.ROUND_KIND)]
+    assert kinds[1] == PE.K_PAIR and kinds[3] == PE.K_CHAIN, kinds
+    n_r, ch = p.chain(3)
+    assert n_r == 3 and len(ch) == 1, (n_r, ch)
+    c = ch[0]
+    assert (c["node_begin"], c["node_end"]) == (l3, l3 + 4)
+    assert parent[c["node_end"] - 1] - parent[c["node_begin"]] == l2_last - l2_first > 65535

@@ -1,9 +1,9 @@
 #!/bin/bash
-# Round-4 evidence: GPU suite, driver bench command with CPU baseline, kernel
+# Round-end evidence: GPU suite, driver bench command with CPU baseline, kernel
 # traces + PMC passes (gpu_check), cfg2/cfg4/cfg5 lines, 4-rank loopback.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"
-TAG=${1:-r04final}
+TAG=${1:-final}
 O=gpurun_out/$TAG
 mkdir -p $O
 echo "[final] smoke $(date +%T)"
