@@ -372,7 +372,7 @@ def bench_cfg5(args):
     eng.close()
 
 
-def general_path(eng, wl, deliv_expected, steps: int, warmup: int = 1, max_start: int = 7):
+def general_path(eng, wl, deliv_expected, steps: int, warmup: int = 1, max_start: int = 7, compact_steps: int = 2):
     """The general path: the same workload published with staggered start
     rounds, uniform over 0..max_start -- paced publishing as the reference's
     tests do it (pubsub_test.go:101-131).  Level mode runs each topic's
@@ -410,18 +410,19 @@ def general_path(eng, wl, deliv_expected, steps: int, warmup: int = 1, max_start
         roof["device_ms_per_step"] = sum(v[1] for v in per.values()) / 2
         d = st.as_dict()
         return {"value": tot / wall, "unit": "deliveries/s", "steps": n_steps, "ms_per_step": wall * 1e3 / n_steps,
-                "rounds": st.rounds, "roofline": roof,
+                "rounds": st.rounds, "level_aligned": int(st.level_aligned), "roofline": roof,
                 "expand_us_per_round": [round(x * 1e3, 1) for x in d["expand_ms_per_round"]],
                 "mbytes_per_round": [round(x / 1e6, 1) for x in d["expand_bytes_per_round"]]}
 
     flags = eng.flags
     out = leg((PE.MODE_FLOOD, PE.MODE_LEVEL_PULL), steps)
     out["workload"] = (f"{wl.name} with start rounds uniform over 0..{max_start} (paced publishing): "
-                       "start groups: k_flood for the small leading rounds, then one k_pull launch per round")
+                       "start groups, level-aligned (launch round q writes BFS level q of every group; "
+                       "each group's deliveries counted in round start + q)")
     out["deliveries_per_step"] = deliv_expected
     eng.set_flags(flags | PE.F_COMPACT)
     try:
-        comp = leg((PE.MODE_COMPACT,), max(1, steps // 2))
+        comp = leg((PE.MODE_COMPACT,), compact_steps)
     finally:
         eng.set_flags(flags)
     comp["workload"] = "the same steps through the compaction path (PS_F_COMPACT): k_expand + frontier compaction"
@@ -530,7 +531,7 @@ def main():
         return eng.run()
 
     if args.general_only:
-        g = general_path(eng, wl, deliv_expected, max(2, min(args.steps, 4)), warmup=max(1, args.warmup))
+        g = general_path(eng, wl, deliv_expected, max(2, min(args.steps, 100)), warmup=max(1, args.warmup))
         print(json.dumps({"metric": METRIC + " [general path only]", "general_path": g}), flush=True)
         eng.close()
         return
@@ -621,7 +622,7 @@ def main():
         out["sustained"] = {"value": deliv_sus / wall_sus, "unit": "deliveries/s", "steps": n_sus,
                             "seconds": wall_sus, "ms_per_step": wall_sus * 1e3 / n_sus}
     if not args.no_general and not args.no_check:
-        out["general_path"] = general_path(eng, wl, deliv_expected, max(2, min(args.steps, 4)))
+        out["general_path"] = general_path(eng, wl, deliv_expected, max(20, min(args.steps, 100)))
     if not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(eng, wl, sizes, args.cpu_budget, deliv_expected)
     print(json.dumps(out), flush=True)

@@ -77,6 +77,7 @@ ps_plan_opts current_opts(const ps_engine* e) {
   o.chain_nt = e->chain_nt ? 1 : 0;
   o.chain_waves = e->chain_waves;
   o.flood_min_rounds = e->flood_min_rounds;
+  o.align_groups = e->align_groups ? 1 : 0;
   return o;
 }
 
@@ -89,7 +90,7 @@ const char* check_opts(const ps_plan_opts& o) {
   if (o.overlap_min_rounds < 2) return "overlap_min_rounds < 2";
   if (o.xchg_overlap < -1 || o.xchg_overlap > 1) return "xchg_overlap not -1, 0 or 1";
   if (o.flood > 1 || o.chain_tail > 1 || o.overlap > 1 || o.gpu_build > 1 || o.chain_nt > 1 || o.chain_waves > 16 ||
-      o.flood_min_rounds < 1 || o.reserved != 0)
+      o.flood_min_rounds < 1 || o.align_groups > 1)
     return "switch not 0 or 1";
   return nullptr;
 }
@@ -119,6 +120,7 @@ void apply_opts(ps_engine* e, const ps_plan_opts& o) {
   e->chain_nt = o.chain_nt != 0;
   e->chain_waves = o.chain_waves;
   e->flood_min_rounds = o.flood_min_rounds;
+  e->align_groups = o.align_groups != 0;
   refresh_xchg_overlap(e);
 }
 
@@ -873,14 +875,14 @@ int ps_plan_get(ps_engine* e, uint32_t what, uint32_t index, uint64_t* out, size
                        static_cast<uint64_t>(c.row0_hi) << 32 | c.row0_lo, static_cast<uint64_t>(c.e_lo),
                        static_cast<uint64_t>(c.e_hi), static_cast<uint64_t>(c.gin), static_cast<uint64_t>(c.gout),
                        static_cast<uint64_t>(c.group), static_cast<uint64_t>(c.p_lo), static_cast<uint64_t>(c.p_hi),
-                       static_cast<uint64_t>(c.c_lo)})
+                       static_cast<uint64_t>(c.c_lo), static_cast<uint64_t>(c.soff)})
       v.push_back(x);
   };
   switch (what) {
     case PS_PLAN_INFO:
       v = {L ? L->planned0 : 0u, e->n_nodes, e->pull.chunks.size(), e->pair.chunks.size(),
            static_cast<uint64_t>(e->world), static_cast<uint64_t>(e->rank), e->ghost.send_half, e->ghost.recv_words,
-           e->ghost.segs.size(), L && L->level ? 1u : 0u, e->ship_host.size()};
+           e->ghost.segs.size(), L && L->level ? 1u : 0u, e->ship_host.size(), L && L->aligned ? L->srows : 0u};
       break;
     case PS_PLAN_NODES:
       v.assign(e->node_peer.begin(), e->node_peer.end());
@@ -904,7 +906,8 @@ int ps_plan_get(ps_engine* e, uint32_t what, uint32_t index, uint64_t* out, size
       if (!L || index >= e->topics.size()) return e->fail(PS_E_RANGE, "topic");
       const TopicDev& d = L->tab[index];
       v = {d.W, d.wbase, d.flags, L->groups[index].size()};
-      for (const StartGroup& g : L->groups[index]) v.insert(v.end(), {g.start, g.w0, g.wn});
+      // (the true start round: a level-aligned window plans from start 0, soff = the start)
+      for (const StartGroup& g : L->groups[index]) v.insert(v.end(), {g.start + g.soff, g.w0, g.wn});
       break;
     }
     case PS_PLAN_ROUND_KIND:

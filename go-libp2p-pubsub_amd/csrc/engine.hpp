@@ -24,7 +24,11 @@
 
 namespace psamd {
 
-constexpr uint32_t kMaxRoundsCap = 4096;  // round buffers' minimum size (deeper windows grow them)
+constexpr uint32_t kMaxRoundsCap = 4096;
+// counter rows of a level-aligned window at most (launch rounds x start
+// rounds): a run slot's pinned block holds 2 x (PS_MAX_ROUNDS + 1) rows
+// (the second half, the multi-rank apply rows, is free on one rank)
+constexpr uint32_t kAlignedRowsMax = 2 * (PS_MAX_ROUNDS + 1);  // round buffers' minimum size (deeper windows grow them)
 constexpr uint32_t kMaxStartRound = 200;
 constexpr uint32_t kDefaultWindow = 65536;
 constexpr uint32_t kMaxWindow = 1u << 30;  // messages per topic per window at most (ps_config.msg_window)
@@ -124,8 +128,14 @@ struct WinSlice {
 // every row: a tree node at level d receives the block in round start + d.
 // A topic whose window messages share one start round has one group, the
 // whole row.
+// soff: a level-aligned window (WindowLayout::aligned) plans every group as
+// if it started in round 0 (start = 0) -- launch round q writes level q of
+// every group -- and soff is the group's true start round, added to the
+// launch round wherever a round is observable (counter rows, hop records).
+// Otherwise soff = 0 and start is the true start round.
 struct StartGroup {
   uint32_t start, w0, wn;
+  uint32_t soff = 0;
 };
 
 // Word offset of virtual word w of row u (relative to the topic's first
@@ -146,6 +156,13 @@ struct WindowLayout {
   uint32_t planned0 = 0;                   // rounds of the window: max depth + latest start + 1
   uint32_t round_cap = 0;
   bool multi = false;                      // some tree window has several start rounds
+  // level-aligned start groups (one rank, ps_plan_opts.align_groups): the
+  // planners see every group start in round 0 (planned0 = max depth + 1
+  // launch rounds); counters go to srows rows per launch round (row q *
+  // srows + soff: true round q + soff), true_rounds = planned0 + srows - 1
+  bool aligned = false;
+  uint32_t srows = 1;
+  uint32_t true_rounds = 0;
   bool any_mesh = false, need_direct = false;
   bool level = false;                      // level mode (else the compaction path)
 };
@@ -262,6 +279,7 @@ struct ps_engine {
   // chains after it: 4 MB; 16 MB was best before them, profiles/r03/ab_flood_top.txt)
   uint64_t flood_top_bytes = 4ull << 20;
   uint32_t flood_min_rounds = 4;  // k_flood only for at least this many leading rounds (ps_plan_opts)
+  bool align_groups = true;       // one-rank start-group windows run level-aligned (ps_plan_opts)
   uint32_t flood_epoch = 0;   // granule tag of the last launch (granules are never reset)
   uint32_t flood_spin_ticks = 200000000u;  // dependency-wait bound: 2 s of s_memrealtime (100 MHz); PSAMD_FLOOD_SPIN_TICKS
   psamd::FloodPlan flood;
@@ -383,6 +401,7 @@ struct ps_engine {
     uint64_t seq = 0;
     bool signalled = false;
     uint32_t planned0 = 0;
+    uint32_t srows = 1;          // counter rows per launch round (level-aligned start groups)
     int32_t world = 1;
     std::vector<uint8_t> kinds;  // round_kind of the window
   };
@@ -473,7 +492,7 @@ bool deep_window(const ps_engine* e, const WindowLayout& L);
 // run.cpp
 int run_body(ps_engine* e, ps_stats* st, bool may_defer);
 bool accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uint32_t r, uint32_t planned0,
-                       uint32_t mode, uint32_t flood_rounds, uint32_t launches, int32_t world,
+                       uint32_t srows, uint32_t mode, uint32_t flood_rounds, uint32_t launches, int32_t world,
                        const std::vector<uint8_t>& kinds);
 
 }  // namespace psamd

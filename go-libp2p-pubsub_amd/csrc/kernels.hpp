@@ -145,7 +145,10 @@ struct PullChunk {
   // into); kNoneNode: none
   uint32_t gin, gout;
   uint32_t group;  // host: the start group (index in the topic's groups) whose block the chunk writes
-  uint32_t pad;
+  // level-aligned windows (PullArgs::srow != 0): the group's start round --
+  // its counters go to row soff of the launch round, its hops are recorded
+  // as round + soff; 0 otherwise
+  uint32_t soff;
 };
 constexpr uint32_t kPullMaxKids = 512;
 constexpr uint32_t kNoneNode = 0xFFFFFFFFu;
@@ -214,6 +217,10 @@ struct PullArgs {
   // the partial slots of each round of the launch
   const uint32_t* row_ptr;
   uint64_t* partials_r[6];  // (kChainLevels)
+  // level-aligned start groups: counter words between the rows of two start
+  // offsets of one launch round (partials + soff * srow); 0: rows by round
+  // (a chain chunk's r0 + k), per-block counter reduce in k_pull
+  uint32_t srow;
   // debug (PSAMD_CHAIN_PROFILE): per chunk kChainProf words -- s_memrealtime
   // at the chunk's start and end, row words written, HW_ID and XCC_ID; null: off
   uint64_t* prof;
@@ -253,7 +260,8 @@ struct ChainChunk {
   uint32_t row0_lo, row0_hi;      // row of the topic's first node (its start group's block)
   uint32_t w0, S;                 // the column slice of every row (rows reach 2^24 words)
   uint8_t levels;                 // levels written: d .. d + levels - 1 (rounds r0 + k of the launch)
-  uint8_t r0;                     // the run's round within the launch (a start group entering late: > 0)
+  uint8_t r0;                     // the run's round within the launch (a start group entering late: > 0);
+                                  // level-aligned windows (PullArgs::srow): the group's start round
   uint16_t group;                 // host: the start group
   // first node of levels d .. d + levels: a run [x0, x1) of level d + k has
   // the children [row_ptr[x0] - row_ptr[first[k]] + first[k + 1], ...x1...)

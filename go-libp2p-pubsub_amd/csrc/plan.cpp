@@ -136,6 +136,33 @@ int plan_window_layout(ps_engine* e, const std::vector<RunMsg>& msgs, const std:
     d.root_words = L.groups[t][0].wn;
     for (const StartGroup& g : L.groups[t]) L.gtab.push_back(GroupDev{g.w0, g.wn});
   }
+  L.true_rounds = L.planned0;
+  // Level-aligned start groups (one rank).  In a tree window the groups are
+  // independent: group g's block at level d depends only on its block at
+  // level d - 1, whatever round that ran in -- the tree and the live mask do
+  // not change inside a window, so a message published in round s reaches
+  // the same peers at the same hops as one published in round 0, only s
+  // rounds later (client.go:100-132: hop = depth).  So every group runs on
+  // the burst's schedule: launch round q writes level q of every group (the
+  // planners see start 0), and the true round q + soff appears only where it
+  // is observable: each group's counters go to its own row of the launch
+  // round, its hop records carry q + soff.  max_start rounds fewer, and the
+  // deep-window machinery (chains from round 1, the cross-window overlap)
+  // applies to paced publishing as to a burst.  The reduce rows (launch
+  // rounds x start rounds) must fit the pinned rows of a run slot.
+  const uint32_t srows = L.max_start + 1;
+  if (L.multi && L.level && !L.any_mesh && e->world == 1 && e->align_groups && srows <= 255 &&
+      static_cast<uint64_t>(L.max_depth + 2) * srows <= kAlignedRowsMax) {
+    L.aligned = true;
+    L.srows = srows;
+    for (uint32_t t = 0; t < nt; ++t)
+      for (StartGroup& g : L.groups[t]) {
+        g.soff = g.start;
+        g.start = 0;
+      }
+    L.max_start = 0;
+    L.planned0 = L.max_depth + 1;
+  }
   return PS_OK;
 }
 
@@ -159,7 +186,8 @@ bool plan_pull_chunks(ps_engine* e, const WindowLayout& L) {
     key.push_back(tab[t].W);
     key.push_back(tab[t].wbase << 1 | ((tab[t].flags & kTopicGroups) ? 1 : 0));
     if (tab[t].W)
-      for (const StartGroup& g : L.groups[t]) key.push_back(static_cast<uint64_t>(g.start) << 32 | g.w0);
+      for (const StartGroup& g : L.groups[t])
+        key.insert(key.end(), {static_cast<uint64_t>(g.start) << 32 | g.w0, g.soff});
   }
   PullPlan& P = e->pull;
   if (key == P.key) return false;
@@ -173,7 +201,7 @@ bool plan_pull_chunks(ps_engine* e, const WindowLayout& L) {
   P.bytes.assign(rounds + 2, 0);
   std::vector<PullChunk> ghost;
   auto cut = [&](std::vector<PullChunk>& out, uint32_t t, uint32_t gi, uint32_t u0, uint32_t u1, uint32_t per,
-                 uint32_t W, uint64_t row0) {
+                 uint32_t W, uint64_t row0, uint32_t soff) {
     const TopicHost& T = e->topics[t];
     for (uint32_t u = u0; u < u1; u += per) {
       PullChunk c{};
@@ -187,6 +215,7 @@ bool plan_pull_chunks(ps_engine* e, const WindowLayout& L) {
       c.row0_hi = static_cast<uint32_t>(row0 >> 32);
       c.gin = c.gout = kNoneNode;
       c.group = gi;
+      c.soff = soff;
       out.push_back(c);
     }
   };
@@ -206,8 +235,8 @@ bool plan_pull_chunks(ps_engine* e, const WindowLayout& L) {
         const uint32_t W = block_w(tab[t], g);
         const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, e->pull_words / W));
         P.bytes[q] += static_cast<uint64_t>(hi - lo) * W * 8;
-        cut(P.chunks, t, gi, lo, lo + nl, per, W, block_row0(tab[t], g));
-        cut(ghost, t, gi, lo + nl, hi, per, W, block_row0(tab[t], g));
+        cut(P.chunks, t, gi, lo, lo + nl, per, W, block_row0(tab[t], g), g.soff);
+        cut(ghost, t, gi, lo + nl, hi, per, W, block_row0(tab[t], g), g.soff);
       }
     }
     P.gsplit[q] = static_cast<uint32_t>(P.chunks.size());
@@ -250,7 +279,8 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   constexpr uint32_t stage = kPairWords;
   const double kLaunchBytes = e->launch_bytes;  // ~3 us of launch ramp and tail at ~5.5 TB/s
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
-  const uint32_t chain_max = L.multi ? e->chain_max_groups : e->chain_max;
+  // (level-aligned start groups run the burst's schedule: chain_max)
+  const uint32_t chain_max = (L.multi && !L.aligned) ? e->chain_max_groups : e->chain_max;
   const uint32_t max_len = std::max<uint32_t>(1, std::min<uint32_t>(chain_max, kChainLevels));
   auto& kind = PP.kind;
   kind.assign(rounds + 2, PS_K_NONE);
@@ -419,7 +449,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
             c.w0 = w0;
             c.S = std::min(z.S, W - w0);
             c.levels = static_cast<uint8_t>(levels);
-            c.r0 = static_cast<uint8_t>(r0);
+            c.r0 = static_cast<uint8_t>(L.aligned ? g.soff : r0);  // (aligned: r0 = 0, the group's start)
             c.group = static_cast<uint16_t>(gi);
             c.nbase = T.nbase;
             c.root = T.root_local ? T.nbase : kNoneNode;
@@ -481,6 +511,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
             c.c_lo = late ? kNoneNode : 0;  // children: filled in on the device
             c.gin = c.gout = kNoneNode;
             c.group = gi;
+            c.soff = g.soff;
             (part ? ghost : C).push_back(c);
           }
         }
@@ -502,7 +533,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
 // so they keep k_flood: a small deep tree has nothing to gain from chains.)
 bool deep_window(const ps_engine* e, const WindowLayout& L) {
   if (!(e->overlap_on && L.level && e->world == 1 && !L.any_mesh && !(e->cfg.flags & PS_F_RECORD_HOPS) &&
-        !L.multi && L.planned0 >= e->overlap_min_rounds))
+        (!L.multi || L.aligned) && L.planned0 >= e->overlap_min_rounds))
     return false;
   uint64_t rows = 0;  // the window's row bytes, as run.cpp's floor counts them
   for (uint32_t t = 0; t < L.tab.size(); ++t)
@@ -538,7 +569,8 @@ bool plan_flood_tasks(ps_engine* e, const WindowLayout& L, uint32_t rounds) {
     key.push_back(tab[t].W);
     key.push_back(tab[t].wbase << 1 | ((tab[t].flags & kTopicGroups) ? 1 : 0));
     if (tab[t].W)
-      for (const StartGroup& g : L.groups[t]) key.push_back(static_cast<uint64_t>(g.start) << 32 | g.w0);
+      for (const StartGroup& g : L.groups[t])
+        key.insert(key.end(), {static_cast<uint64_t>(g.start) << 32 | g.w0, g.soff});
   }
   FloodPlan& F = e->flood;
   if (key == F.key) return false;
@@ -547,8 +579,10 @@ bool plan_flood_tasks(ps_engine* e, const WindowLayout& L, uint32_t rounds) {
   auto& SG = F.segs;
   TK.clear();
   SG.clear();
-  F.slot0.assign(rounds + 2, 0);
-  F.nslot.assign(rounds + 2, 0);
+  // counter rows: per round, or (level-aligned) per round and start group
+  const uint32_t srows = L.srows;
+  F.slot0.assign(static_cast<size_t>(rounds + 2) * srows, 0);
+  F.nslot.assign(static_cast<size_t>(rounds + 2) * srows, 0);
   // each (topic, start group)'s segment of the previous round
   std::vector<std::vector<uint32_t>> seg_prev(nt);
   for (uint32_t t = 0; t < nt; ++t) seg_prev[t].assign(L.groups[t].size(), kNone);
@@ -589,7 +623,8 @@ bool plan_flood_tasks(ps_engine* e, const WindowLayout& L, uint32_t rounds) {
           k.nb = T.nbase + u;
           k.ne = T.nbase + std::min(u + per, hi);
           k.topic = t;
-          k.round = q;
+          k.round = q + g.soff;
+          k.slot0 = g.soff;  // (the row, until the slots are assigned below)
           k.g_own = sg.gbase + (u - lo) / gsz;
           k.gsz = gsz;
           k.pseg = pseg;
@@ -598,16 +633,22 @@ bool plan_flood_tasks(ps_engine* e, const WindowLayout& L, uint32_t rounds) {
         }
       }
     }
-    const uint32_t n_round = static_cast<uint32_t>(TK.size() - first);
-    if (!n_round) continue;
-    const uint32_t ns = std::min<uint32_t>(kPullSlots, n_round);
-    F.slot0[q] = slot;
-    F.nslot[q] = ns;
-    for (size_t i = first; i < TK.size(); ++i) {
-      TK[i].slot0 = slot;
-      TK[i].nslot = ns;
+    if (TK.size() == first) continue;
+    for (uint32_t so = 0; so < srows; ++so) {  // the round's row of each start offset
+      uint32_t n_row = 0;
+      for (size_t i = first; i < TK.size(); ++i) n_row += TK[i].slot0 == so;
+      if (!n_row) continue;
+      const uint32_t ns = std::min<uint32_t>(kPullSlots, n_row);
+      const size_t v = static_cast<size_t>(q) * srows + so;
+      F.slot0[v] = slot;
+      F.nslot[v] = ns;
+      slot += ns;
     }
-    slot += ns;
+    for (size_t i = first; i < TK.size(); ++i) {
+      const size_t v = static_cast<size_t>(q) * srows + TK[i].slot0;
+      TK[i].slot0 = F.slot0[v];
+      TK[i].nslot = F.nslot[v];
+    }
   }
   F.slots = slot;
   F.granules = gran;

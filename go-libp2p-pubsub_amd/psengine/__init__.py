@@ -65,7 +65,8 @@ class Stats(C.Structure):
                 ("round_kernel", C.c_uint8 * MAX_ROUNDS),
                 ("plan_max_rounds", C.c_uint32), ("prefix_rounds", C.c_uint32),
                 ("overlapped", C.c_uint32), ("xchg_path", C.c_uint32),
-                ("xchg_rounds", C.c_uint64), ("xchg_bytes", C.c_uint64)]
+                ("xchg_rounds", C.c_uint64), ("xchg_bytes", C.c_uint64),
+                ("level_aligned", C.c_uint32), ("reserved2", C.c_uint32)]
 
     PER_ROUND = ("deliveries_per_round", "expand_ms_per_round", "frontier_per_round", "expand_bytes_per_round",
                  "round_kernel")
@@ -98,7 +99,7 @@ class PlanOpts(C.Structure):
                 ("flood_words", C.c_uint32), ("pad_words", C.c_uint32), ("overlap", C.c_uint32),
                 ("overlap_min_rounds", C.c_uint32), ("xchg_overlap", C.c_int32), ("gpu_build", C.c_uint32),
                 ("flood_spin_ticks", C.c_uint32), ("chain_nt", C.c_uint32), ("chain_waves", C.c_uint32),
-                ("flood_min_rounds", C.c_uint32), ("reserved", C.c_uint32)]
+                ("flood_min_rounds", C.c_uint32), ("align_groups", C.c_uint32)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -13,7 +13,7 @@ INFO, NODES, PARENT, GHOST_REF, TOPIC, LAYOUT, ROUND_KIND, PULL, PAIR, XCHG, SEG
 CHAIN_FIELDS = ("node_begin", "node_end", "topic", "W", "row0", "w0", "S", "levels", "r0", "group")
 CHAIN_LEVELS = 6  # kChainLevels
 CHUNK_FIELDS = ("node_begin", "node_end", "topic", "W", "row0", "e_lo", "e_hi", "gin", "gout", "group",
-                "p_lo", "p_hi", "c_lo")
+                "p_lo", "p_hi", "c_lo", "soff")
 PROTOTYPES = [
     ("ps_plan_create", C.c_int, [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                  C.POINTER(DistConfig), C.POINTER(_P)]),
@@ -107,7 +107,7 @@ class Plan:
     def info(self) -> dict:
         v = self.get(INFO)
         keys = ("rounds", "nodes", "pull_chunks", "pair_chunks", "world", "rank", "send_half", "recv_words",
-                "segs", "level", "ship")
+                "segs", "level", "ship", "aligned_rows")
         return {k: int(x) for k, x in zip(keys, v)}
 
     def chunks(self, what: int, q: int):

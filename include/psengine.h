@@ -108,6 +108,13 @@ typedef struct ps_stats {
   uint32_t xchg_path;          /* N ranks: PS_XCHG_* of the last window         */
   uint64_t xchg_rounds;        /* N ranks: rounds of this run that exchanged     */
   uint64_t xchg_bytes;         /* N ranks: ghost-record bytes this rank received */
+  uint32_t level_aligned;      /* the last window ran level-aligned start groups
+                                  (ps_plan_opts.align_groups): round_kernel,
+                                  expand_bytes_per_round and expand_ms_per_round
+                                  are indexed by launch round = BFS level;
+                                  deliveries_per_round / frontier_per_round stay
+                                  by round (start + level)                      */
+  uint32_t reserved2;
 } ps_stats;
 
 /* ps_stats.xchg_path: how a multi-rank level window's ghost records moved */
@@ -220,7 +227,12 @@ typedef struct ps_plan_opts {
                                   1..16 (an LDS pad), 0: as many as fit (12)    */
   uint32_t flood_min_rounds;   /* k_flood only when it would run at least this many
                                   leading rounds; fewer go to chain launches (4) */
-  uint32_t reserved;
+  uint32_t align_groups;       /* 1: a one-rank window with start groups (paced
+                                  publishing) runs level-aligned -- launch round q
+                                  writes BFS level q of every start group, each
+                                  group's deliveries counted and recorded in its
+                                  own round (start + level) -- instead of one
+                                  launch schedule over start + depth rounds (1) */
 } ps_plan_opts;
 
 int ps_plan_opts_default(ps_plan_opts* out);

@@ -169,6 +169,69 @@ def test_overlapped_windows_equal_blocking(monkeypatch, dead, full):
     assert out[0][1] == out[1][1]
 
 
+def vary_group_counts(msg_topics, starts, i):
+    """Window i's staggered batch: each (topic, start round) group loses up
+    to (n - 1) % 128 of its last messages, so every group block's even word
+    width -- and the plan -- stays, while its last word differs per window."""
+    keep = np.ones(msg_topics.shape[0], dtype=bool)
+    for t in np.unique(msg_topics):
+        for s0 in np.unique(starts):
+            idx = np.nonzero((msg_topics == t) & (starts == s0))[0]
+            if idx.shape[0] == 0:
+                continue
+            drop = (i * 7 + int(t) + 3 * int(s0)) % ((idx.shape[0] - 1) % 128 + 1)
+            if drop:
+                keep[idx[-drop:]] = False
+    return msg_topics[keep], starts[keep]
+
+
+@pytest.mark.parametrize("dead,full", [(0.03, False), (0.02, True)])
+def test_overlapped_staggered_windows_equal_blocking(monkeypatch, dead, full):
+    """Paced publishing (start rounds 0..7), pipelined: level-aligned start
+    groups make a deep window whose leading launches run beside the previous
+    window's last ones.  Eight windows with different
+    counts per (topic, start) group -- the same group widths, so the same
+    plan and the overlap applies -- equal blocking runs counter for counter
+    and in the final rows, and the blocking round-by-round schedule
+    (align_groups 0) too; the overlap did happen."""
+    wl = WL.cfg3() if full else WL.cfg3(200_000, 16, 5000)
+    rng = np.random.default_rng(12)
+    live = (rng.random(wl.n_peers) >= dead).astype(np.uint8)
+    live[[ts.root for ts in wl.topics]] = 1
+    starts = (WL.stream(wl.seed ^ 0x57A6, np.arange(wl.n_msgs)) % np.uint64(8)).astype(np.uint32)
+    batches = [vary_group_counts(wl.msg_topics, starts, i) for i in range(8)]
+    assert len({b[0].shape[0] for b in batches}) > 4
+    base = {} if full else {"overlap_min_bytes": 0}
+    out = []
+    for pipelined, align in ((False, 1), (True, 1), (False, 0)):
+        e = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed, plan={**base, "align_groups": align})
+        WL.build_engine_topics(e, wl)
+        e.set_live(live)
+        res = []
+        if pipelined:
+            for i in range(8):
+                e.publish(*batches[i])
+                e.run_async()
+                if i:
+                    res.append(stats_key(e.wait()))
+            res.append(stats_key(e.wait()))
+        else:
+            for i in range(8):
+                e.publish(*batches[i])
+                st = e.run()
+                assert bool(st.level_aligned) == bool(align)
+                res.append(stats_key(st))
+            assert e.overlapped_windows() == 0
+        out.append((res, e.seen_digest()))
+        if pipelined:
+            assert e.overlapped_windows() >= 5
+        e.close()
+    assert out[0][1] == out[1][1] == out[2][1]
+    assert out[0][0] == out[1][0]
+    # (expand_bytes, key index 4, differ by schedule: compare the rest)
+    assert [k[:4] + k[5:] for k in out[0][0]] == [k[:4] + k[5:] for k in out[2][0]]
+
+
 @pytest.mark.parametrize("reuse", [1, 0])
 def test_signalled_windows_equal_blocking(monkeypatch, reuse):
     """Small pipelined windows (under the overlap floor, one rank) end with

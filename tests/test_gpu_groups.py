@@ -79,8 +79,12 @@ def test_groups_match_oracle_and_compaction(monkeypatch, seed):
         exp[t] = O.disseminate(rp, cl, root, live, 1)[1][0]
     outs = []
     # level mode: the default k_flood / k_pull split, every round in k_flood,
-    # every round in k_pull; then the compaction path
-    for level, opts in ((True, {}), (True, {"flood_top_bytes": 1 << 40}), (True, {"flood": 0}), (False, {})):
+    # every round in k_pull -- level-aligned (the default, one launch
+    # schedule over the BFS levels of every start group) and round by round
+    # (align_groups 0); then the compaction path
+    for level, opts in ((True, {}), (True, {"flood_top_bytes": 1 << 40}), (True, {"flood": 0}),
+                        (True, {"align_groups": 0}), (True, {"align_groups": 0, "flood": 0}),
+                        (True, {"chain_max": 1}), (True, {"chain_max": 2}), (False, {})):
         st, hops, deliv, pm, digest = run(level, n, topics, live, msg_topics, starts, plan=opts)
         for m, t in enumerate(msg_topics):
             if not np.array_equal(hops[m], exp[int(t)]):
@@ -119,8 +123,9 @@ def test_groups_production_instance_and_windows():
     rp, cl = O.parents_to_csr(parent)
     exp = O.disseminate(rp, cl, root, live, 1)[1][0]
     outs = []
-    for level in (True, False):
-        with PE.Engine(n, 1, msg_window=200, flags=0 if level else PE.F_COMPACT) as eng:
+    for level, align in ((True, 1), (True, 0), (False, 1)):
+        with PE.Engine(n, 1, msg_window=200, flags=0 if level else PE.F_COMPACT,
+                       plan={"align_groups": align}) as eng:
             eng.set_tree(0, root, parent)
             eng.set_live(live)
             first = eng.publish(msg_topics, starts)
@@ -129,7 +134,7 @@ def test_groups_production_instance_and_windows():
             for m in (len(starts) - 1, len(starts) - 2, len(starts) - 50):  # the last window's
                 assert np.array_equal(eng.delivered(first + m), ((exp != 0xFF) & (exp > 0)).astype(np.uint8))
             outs.append((st.deliveries, st.as_dict()["deliveries_per_round"], eng.seen_digest()))
-    assert outs[0] == outs[1]
+    assert outs[0] == outs[1] == outs[2]
     assert outs[0][0] == len(starts) * int(((exp != 0xFF) & (exp > 0)).sum())
 
 
@@ -138,14 +143,26 @@ def test_cfg3_staggered_full_size():
     bench's general-path workload): level mode with start groups delivers
     exactly what the single-start window delivers, the per-round histogram
     is the single-start one shifted per group, and 16 sampled messages per
-    topic class (hot 0, mid 8, cold 63) are delivered to exactly the tree."""
+    topic class (hot 0, mid 8, cold 63) are delivered to exactly the tree.
+    Level-aligned (the default: a deep window, chains from round 1, 21
+    launch rounds for 28 rounds) and round by round (align_groups 0: k_flood
+    for the leading rounds) leave the same counters and seen digest."""
     wl = WL.cfg3()
     starts = (WL.stream(wl.seed ^ 0x57A6, np.arange(wl.n_msgs)) % np.uint64(8)).astype(np.uint32)
+    with PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed, plan={"align_groups": 0}) as eng:
+        WL.build_engine_topics(eng, wl)
+        eng.publish(wl.msg_topics, starts)
+        st0 = eng.run()
+        assert st0.expand_mode == PE.MODE_FLOOD and 0 < st0.flood_rounds < st0.rounds and not st0.level_aligned
+        ref = (st0.deliveries, st0.rounds, st0.as_dict()["deliveries_per_round"], eng.seen_digest())
     with PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed) as eng:
         sizes = WL.build_engine_topics(eng, wl)
         first = eng.publish(wl.msg_topics, starts)
         st = eng.run()
-        assert st.expand_mode == PE.MODE_FLOOD and 0 < st.flood_rounds < st.rounds
+        assert st.level_aligned and st.expand_mode == PE.MODE_LEVEL_PULL, (st.level_aligned, st.expand_mode)
+        kinds = list(st.round_kernel)
+        assert kinds[1] == PE.K_CHAIN and PE.K_FLOOD not in kinds, kinds[:30]
+        assert (st.deliveries, st.rounds, st.as_dict()["deliveries_per_round"], eng.seen_digest()) == ref
         assert st.deliveries == wl.expected_deliveries(sizes) == 34_354_202_750
         assert st.duplicates == 0
         hist = np.zeros(80, dtype=np.int64)

@@ -161,7 +161,12 @@ class RankSim:
         for c in chunks:
             L, S = c["levels"], c["S"]
             n0 = c["node_end"] - c["node_begin"]
-            assert 1 <= L <= PL.CHAIN_LEVELS and c["r0"] + L <= n and 1 <= n0 <= 128
+            if self.info["aligned_rows"]:  # level-aligned start groups: r0 = the group's start round
+                assert 1 <= L <= n and c["r0"] < self.info["aligned_rows"] and 1 <= n0 <= 128
+                lay = self.lay[c["topic"]]
+                assert c["r0"] == lay["groups"][c["group"]][0]
+            else:
+                assert 1 <= L <= PL.CHAIN_LEVELS and c["r0"] + L <= n and 1 <= n0 <= 128
             assert S % 2 == 0 or S == c["W"]
             assert n0 * S <= 768, (n0, S, L)  # the LDS stage holds the run's rows (slices)
             assert c["first"][0] == self.topics[c["topic"]]["nbase"] + self.topics[c["topic"]]["level_off"][
@@ -518,6 +523,49 @@ def test_deep_window_plan(overlap):
     check(sims, [parent], [0], live, [1])
 
 
+@pytest.mark.parametrize("align", [0, 1])
+def test_aligned_start_groups_plan(align):
+    """Paced publishing on one rank (start rounds 0..7): with align_groups the
+    window plans like the burst -- launch round q writes BFS level q of every
+    start group, rounds = depth + 1, chains from round 1 as a deep window --
+    and every chunk carries its group's start round (soff, a chain chunk's
+    r0) for its counter row and hop records; without it, one schedule over
+    start + depth rounds.  Both replay to the oracle, every group's block
+    written once per node."""
+    rng = np.random.default_rng(23)
+    n = 6000
+    parent = np.full(n, NONE, dtype=np.uint32)
+    parent[1:] = (np.arange(1, n) - 1) // 2  # 13 levels
+    live = (rng.random(n) > 0.05).astype(np.uint8)
+    live[0] = 1
+    p = PL.Plan(parent[None, :], [0], plan={"align_groups": align, "overlap_min_bytes": 0})
+    msgs = np.zeros(3000, dtype=np.uint32)
+    starts = (np.arange(3000) % 8).astype(np.uint32)
+    p.window(msgs, starts)
+    info = p.info()
+    groups = p.layout(0)["groups"]
+    assert [g[0] for g in groups] == list(range(8))
+    kinds = [int(k) for k in p.get(PL.ROUND_KIND)]
+    if align:
+        assert info["aligned_rows"] == 8 and info["rounds"] == 13, info
+        assert PE.K_FLOOD not in kinds and kinds[1] == PE.K_CHAIN, kinds
+        seen = set()
+        for q in range(1, info["rounds"] + 1):
+            if kinds[q] == PE.K_CHAIN:
+                for c in p.chain(q)[1]:
+                    assert c["r0"] == groups[c["group"]][0]
+                    seen.add(c["r0"])
+            elif kinds[q] in (PE.K_PULL, PE.K_PAIR):
+                for c in p.chunks(PL.PAIR if kinds[q] == PE.K_PAIR else PL.PULL, q)[3]:
+                    assert c["soff"] == groups[c["group"]][0]
+        assert seen == set(range(8))
+    else:
+        assert info["aligned_rows"] == 0 and info["rounds"] == 13 + 7, info
+    sims = [RankSim(p, live)]
+    emulate(sims, info["rounds"], in_process_exchange(sims))
+    check(sims, [parent], [0], live, [8])
+
+
 def test_small_deep_window_keeps_flood():
     """A deep window below the overlap byte floor (512 MB of rows by default)
     can never overlap its predecessor, so it keeps the latency-optimal k_flood
@@ -569,7 +617,7 @@ def test_plan_opts_defaults_pinned():
                  "flood": 1, "chain_max": 4, "chain_max_groups": 6, "chain_tail": 1, "chain_words": 8192,
                  "flood_words": 2048, "pad_words": 16, "overlap": 1, "overlap_min_rounds": 12,
                  "xchg_overlap": -1, "gpu_build": 1, "flood_spin_ticks": 200_000_000, "chain_nt": 1,
-                 "chain_waves": 12, "flood_min_rounds": 4, "reserved": 0}, d
+                 "chain_waves": 12, "flood_min_rounds": 4, "align_groups": 1}, d
     parent = np.full(64, NONE, dtype=np.uint32)
     parent[1:] = (np.arange(1, 64) - 1) // 2
     env = dict(os.environ)

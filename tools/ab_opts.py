@@ -30,12 +30,19 @@ def main():
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--sync", action="store_true")
+    ap.add_argument("--staggered", type=int, default=0,
+                    help="start rounds uniform over 0..N (bench.py's general path: paced publishing)")
     args = ap.parse_args()
     variants = json.loads(args.variants)
     wl = WL.CONFIGS[args.workload]()
     eng = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed)
     sizes = WL.build_engine_topics(eng, wl)
     expect = wl.expected_deliveries(sizes)
+    starts = None
+    if args.staggered:
+        import numpy as np
+
+        starts = (WL.stream(wl.seed ^ 0x57A6, np.arange(wl.n_msgs)) % np.uint64(args.staggered + 1)).astype(np.uint32)
     base = eng.plan_opts()
     res = [[] for _ in variants]
     last = [None] * len(variants)
@@ -43,18 +50,18 @@ def main():
         for i, v in enumerate(variants):
             eng.set_plan(**{**base, **v})
             for _ in range(3):  # warm: plans rebuilt, uploads done
-                eng.publish(wl.msg_topics)
+                eng.publish(wl.msg_topics, starts)
                 assert eng.run().deliveries == expect
             t0 = time.perf_counter()
             tot = 0
             if args.sync:
                 for _ in range(args.steps):
-                    eng.publish(wl.msg_topics)
+                    eng.publish(wl.msg_topics, starts)
                     st = eng.run()
                     tot += st.deliveries
             else:
                 for k in range(args.steps):
-                    eng.publish(wl.msg_topics)
+                    eng.publish(wl.msg_topics, starts)
                     eng.run_async()
                     if k:
                         tot += eng.wait().deliveries

@@ -24,12 +24,16 @@ def main():
     ap.add_argument("--workload", default="cfg2")
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--staggered", type=int, default=0, help="start rounds uniform over 0..N (paced publishing)")
     args = ap.parse_args()
     wl = WL.CONFIGS[args.workload]()
     eng = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed)
     WL.build_engine_topics(eng, wl)
+    starts = None
+    if args.staggered:
+        starts = (WL.stream(wl.seed ^ 0x57A6, np.arange(wl.n_msgs)) % np.uint64(args.staggered + 1)).astype(np.uint32)
     for _ in range(5):
-        eng.publish(wl.msg_topics)
+        eng.publish(wl.msg_topics, starts)
         eng.run()
     for rep in range(args.reps):
         tp = tr = tw = 0
@@ -37,7 +41,7 @@ def main():
         t0 = time.perf_counter_ns()
         for i in range(args.steps):
             a = time.perf_counter_ns()
-            eng.publish(wl.msg_topics)
+            eng.publish(wl.msg_topics, starts)
             b = time.perf_counter_ns()
             eng.run_async()
             c = time.perf_counter_ns()
