@@ -875,14 +875,14 @@ int ps_plan_get(ps_engine* e, uint32_t what, uint32_t index, uint64_t* out, size
                        static_cast<uint64_t>(c.row0_hi) << 32 | c.row0_lo, static_cast<uint64_t>(c.e_lo),
                        static_cast<uint64_t>(c.e_hi), static_cast<uint64_t>(c.gin), static_cast<uint64_t>(c.gout),
                        static_cast<uint64_t>(c.group), static_cast<uint64_t>(c.p_lo), static_cast<uint64_t>(c.p_hi),
-                       static_cast<uint64_t>(c.c_lo), static_cast<uint64_t>(c.soff)})
+                       static_cast<uint64_t>(c.c_lo)})
       v.push_back(x);
   };
   switch (what) {
     case PS_PLAN_INFO:
       v = {L ? L->planned0 : 0u, e->n_nodes, e->pull.chunks.size(), e->pair.chunks.size(),
            static_cast<uint64_t>(e->world), static_cast<uint64_t>(e->rank), e->ghost.send_half, e->ghost.recv_words,
-           e->ghost.segs.size(), L && L->level ? 1u : 0u, e->ship_host.size(), L && L->aligned ? L->srows : 0u};
+           e->ghost.segs.size(), L && L->level ? 1u : 0u, e->ship_host.size(), L && L->aligned ? 1u : 0u};
       break;
     case PS_PLAN_NODES:
       v.assign(e->node_peer.begin(), e->node_peer.end());
@@ -906,8 +906,12 @@ int ps_plan_get(ps_engine* e, uint32_t what, uint32_t index, uint64_t* out, size
       if (!L || index >= e->topics.size()) return e->fail(PS_E_RANGE, "topic");
       const TopicDev& d = L->tab[index];
       v = {d.W, d.wbase, d.flags, L->groups[index].size()};
-      // (the true start round: a level-aligned window plans from start 0, soff = the start)
-      for (const StartGroup& g : L->groups[index]) v.insert(v.end(), {g.start + g.soff, g.w0, g.wn});
+      for (const StartGroup& g : L->groups[index]) v.insert(v.end(), {g.start, g.w0, g.wn});
+      // level-aligned: the start groups over the packed row (start, first bit, messages)
+      const auto& AG = L->split.groups;
+      const size_t na = L->aligned && index < AG.size() ? AG[index].size() : 0;
+      v.push_back(na);
+      for (size_t i = 0; i < na; ++i) v.insert(v.end(), {AG[index][i].start, AG[index][i].b0, AG[index][i].n});
       break;
     }
     case PS_PLAN_ROUND_KIND:

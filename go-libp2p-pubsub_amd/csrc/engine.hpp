@@ -24,11 +24,11 @@
 
 namespace psamd {
 
-constexpr uint32_t kMaxRoundsCap = 4096;
-// counter rows of a level-aligned window at most (launch rounds x start
-// rounds): a run slot's pinned block holds 2 x (PS_MAX_ROUNDS + 1) rows
-// (the second half, the multi-rank apply rows, is free on one rank)
-constexpr uint32_t kAlignedRowsMax = 2 * (PS_MAX_ROUNDS + 1);  // round buffers' minimum size (deeper windows grow them)
+constexpr uint32_t kMaxRoundsCap = 4096;  // round buffers' minimum size (deeper windows grow them)
+// counter rows of a level-aligned window at most (its rounds and its reach
+// rows): a run slot's pinned block holds 2 x (PS_MAX_ROUNDS + 1) rows (the
+// second half, the multi-rank apply rows, is free on one rank)
+constexpr uint32_t kAlignedRowsMax = 2 * (PS_MAX_ROUNDS + 1);
 constexpr uint32_t kMaxStartRound = 200;
 constexpr uint32_t kDefaultWindow = 65536;
 constexpr uint32_t kMaxWindow = 1u << 30;  // messages per topic per window at most (ps_config.msg_window)
@@ -128,14 +128,25 @@ struct WinSlice {
 // every row: a tree node at level d receives the block in round start + d.
 // A topic whose window messages share one start round has one group, the
 // whole row.
-// soff: a level-aligned window (WindowLayout::aligned) plans every group as
-// if it started in round 0 (start = 0) -- launch round q writes level q of
-// every group -- and soff is the group's true start round, added to the
-// launch round wherever a round is observable (counter rows, hop records).
-// Otherwise soff = 0 and start is the true start round.
 struct StartGroup {
   uint32_t start, w0, wn;
-  uint32_t soff = 0;
+};
+
+// A level-aligned window (WindowLayout::aligned): the messages of one topic
+// that start in one round, and their row bits [b0, b0 + n) (rows are packed
+// node-major, bits sorted by start round).
+struct AlignedGroup {
+  uint32_t start, b0, n;
+};
+// The per-round split of a level-aligned window: reached and frontier
+// counts per (topic, BFS level), from k_level_reach.  seg_lo[t]: topic t's
+// first segment (levels 0 .. depth_t), kNone: inactive.
+struct AlignedSplit {
+  std::vector<uint32_t> seg_lo, seg_n;
+  std::vector<std::vector<AlignedGroup>> groups;
+  uint32_t n_segs = 0;
+  uint32_t row0 = 0;  // the counter row of segment pair 0 (after the window's rounds)
+  bool eager = false;
 };
 
 // Word offset of virtual word w of row u (relative to the topic's first
@@ -156,13 +167,14 @@ struct WindowLayout {
   uint32_t planned0 = 0;                   // rounds of the window: max depth + latest start + 1
   uint32_t round_cap = 0;
   bool multi = false;                      // some tree window has several start rounds
-  // level-aligned start groups (one rank, ps_plan_opts.align_groups): the
-  // planners see every group start in round 0 (planned0 = max depth + 1
-  // launch rounds); counters go to srows rows per launch round (row q *
-  // srows + soff: true round q + soff), true_rounds = planned0 + srows - 1
+  // level-aligned start groups (one rank, ps_plan_opts.align_groups): every
+  // topic's row is one node-major block with its messages' bits sorted by
+  // start round (AlignedSplit::groups); the planners see one start (round
+  // 0: planned0 = max depth + 1 launch rounds); true_rounds = planned0 +
+  // the latest start round
   bool aligned = false;
-  uint32_t srows = 1;
   uint32_t true_rounds = 0;
+  AlignedSplit split;
   bool any_mesh = false, need_direct = false;
   bool level = false;                      // level mode (else the compaction path)
 };
@@ -301,6 +313,12 @@ struct ps_engine {
   // level mode, per-round counter slots and their reduce descriptors
   std::vector<uint32_t> woff_host, desc_host;
   psamd::DevBuf d_woff;
+  // level-aligned windows: the (topic, level) pieces of k_level_reach, cached
+  // per node space and active topic set
+  psamd::DevBuf d_reach;
+  std::vector<psamd::ReachPiece> reach_host;
+  std::vector<uint64_t> reach_key;
+  uint32_t n_reach = 0;
   // level mode, pull direction: per-round chunks of next-level nodes
   psamd::PullPlan pull;
   psamd::DevBuf d_pull;
@@ -401,7 +419,8 @@ struct ps_engine {
     uint64_t seq = 0;
     bool signalled = false;
     uint32_t planned0 = 0;
-    uint32_t srows = 1;          // counter rows per launch round (level-aligned start groups)
+    uint32_t true_rounds = 0;   // level-aligned windows: rounds by start round (else planned0)
+    psamd::AlignedSplit split;  // level-aligned windows: the per-round split
     int32_t world = 1;
     std::vector<uint8_t> kinds;  // round_kind of the window
   };
@@ -492,7 +511,12 @@ bool deep_window(const ps_engine* e, const WindowLayout& L);
 // run.cpp
 int run_body(ps_engine* e, ps_stats* st, bool may_defer);
 bool accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uint32_t r, uint32_t planned0,
-                       uint32_t srows, uint32_t mode, uint32_t flood_rounds, uint32_t launches, int32_t world,
-                       const std::vector<uint8_t>& kinds);
+                       uint32_t mode, uint32_t flood_rounds, uint32_t launches, int32_t world,
+                       const std::vector<uint8_t>& kinds, bool by_round = true);
+// A level-aligned window's per-round deliveries and frontier entries from
+// its reach rows (hs rows split.row0 ..): false when they disagree with the
+// kernels' per-level counters (rows 1 .. r)
+bool split_aligned_window(ps_stats* st, const uint64_t* hs, uint32_t r, uint32_t true_rounds,
+                          const AlignedSplit& sp);
 
 }  // namespace psamd

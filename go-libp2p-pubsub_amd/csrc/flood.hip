@@ -227,7 +227,7 @@ __global__ __launch_bounds__(kBlock, kFloodBlocksPerCu) void k_flood(FloodArgs a
   uint32_t* src = src_lds[wid];
   const uint32_t cur = a.gen_cur & 0xFF;
   PullCtr c;
-  uint32_t slot = kNoneNode, slot0 = kNoneNode;
+  uint32_t slot = kNoneNode, round = 0;
   uint64_t pf[kFloodProf] = {0, 0, 0, 0, 0, 0, 0, 0};  // debug profile (a.prof)
   auto stamp = [&]() -> uint64_t { return a.prof ? __builtin_amdgcn_s_memrealtime() : 0; };
   uint64_t t_a = stamp();
@@ -242,9 +242,9 @@ __global__ __launch_bounds__(kBlock, kFloodBlocksPerCu) void k_flood(FloodArgs a
   uint64_t pend_val = 0;
   uint32_t pend_at = kNoneNode;
   for (uint32_t ti = wave; ti < a.n_tasks; ti += nw) {
-    if (T.slot0 != slot0) {  // a new counter row: the round's (level-aligned windows: the round and start group's)
+    if (T.round != round) {  // tasks come level by level: a wave's rounds only grow
       if (slot != kNoneNode) flood_flush(a, c, slot, lane);
-      slot0 = T.slot0;
+      round = T.round;
       slot = T.slot0 + wave % T.nslot;
     }
     const uint32_t nk = T.ne - T.nb;

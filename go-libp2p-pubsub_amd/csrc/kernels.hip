@@ -1094,6 +1094,53 @@ hipError_t launch_stage_copy(const StageCopy& c, hipStream_t s) {
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(kBlock) void k_level_reach(const ReachPiece* __restrict__ pieces,
+                                                        const uint8_t* __restrict__ gen, uint32_t gen_cur,
+                                                        const uint8_t* __restrict__ node_flags,
+                                                        const TopicDev* __restrict__ topics,
+                                                        const uint64_t* __restrict__ seen, uint32_t eager,
+                                                        unsigned long long* __restrict__ out) {
+  __shared__ uint32_t red[2][kBlock / 64];
+  const ReachPiece P = pieces[blockIdx.x];
+  const TopicDev T = topics[P.topic];
+  const uint32_t cur = gen_cur & 0xFF;
+  uint32_t r = 0, f = 0;
+  for (uint32_t u = P.lo + threadIdx.x; u < P.hi; u += kBlock) {
+    bool reached;
+    if (u == T.nbase)
+      reached = true;  // the root: seeded
+    else if (eager)
+      reached = seen[T.wbase + static_cast<uint64_t>(u - T.nbase) * T.W] != 0;
+    else
+      reached = gen[u] == cur;
+    const bool internal = (node_flags[u] & kNodeInternal) != 0;
+    r += reached ? 1u : 0u;
+    f += (internal && (reached || eager)) ? 1u : 0u;
+  }
+  r = __reduce_add_sync(~0ull, r);
+  f = __reduce_add_sync(~0ull, f);
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wid] = r;
+    red[1][wid] = f;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    uint32_t t = 0;
+    for (uint32_t w = 0; w < kBlock / 64; ++w) t += red[threadIdx.x][w];
+    if (t) atomicAdd(out + 2 * P.seg + threadIdx.x, static_cast<unsigned long long>(t));
+  }
+}
+
+hipError_t launch_level_reach(const ReachPiece* pieces, uint32_t n, const uint8_t* gen, uint32_t gen_cur,
+                              const uint8_t* node_flags, const TopicDev* topics, const uint64_t* seen, bool eager,
+                              uint64_t* out, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_level_reach, dim3(n), dim3(kBlock), 0, s, pieces, gen, gen_cur, node_flags, topics, seen,
+                     eager ? 1u : 0u, reinterpret_cast<unsigned long long*>(out));
+  return hipGetLastError();
+}
+
 hipError_t launch_reduce_rounds(const uint64_t* partials, const uint32_t* desc, uint32_t n_rounds,
                                 uint64_t* round_stats, uint64_t* host_stats, const WindowSignal& sig, hipStream_t s) {
   if (n_rounds == 0) return sig.flag ? launch_window_done(sig.flag, sig.seq, s) : hipSuccess;

@@ -145,10 +145,7 @@ struct PullChunk {
   // into); kNoneNode: none
   uint32_t gin, gout;
   uint32_t group;  // host: the start group (index in the topic's groups) whose block the chunk writes
-  // level-aligned windows (PullArgs::srow != 0): the group's start round --
-  // its counters go to row soff of the launch round, its hops are recorded
-  // as round + soff; 0 otherwise
-  uint32_t soff;
+  uint32_t pad;
 };
 constexpr uint32_t kPullMaxKids = 512;
 constexpr uint32_t kNoneNode = 0xFFFFFFFFu;
@@ -217,10 +214,6 @@ struct PullArgs {
   // the partial slots of each round of the launch
   const uint32_t* row_ptr;
   uint64_t* partials_r[6];  // (kChainLevels)
-  // level-aligned start groups: counter words between the rows of two start
-  // offsets of one launch round (partials + soff * srow); 0: rows by round
-  // (a chain chunk's r0 + k), per-block counter reduce in k_pull
-  uint32_t srow;
   // debug (PSAMD_CHAIN_PROFILE): per chunk kChainProf words -- s_memrealtime
   // at the chunk's start and end, row words written, HW_ID and XCC_ID; null: off
   uint64_t* prof;
@@ -260,8 +253,7 @@ struct ChainChunk {
   uint32_t row0_lo, row0_hi;      // row of the topic's first node (its start group's block)
   uint32_t w0, S;                 // the column slice of every row (rows reach 2^24 words)
   uint8_t levels;                 // levels written: d .. d + levels - 1 (rounds r0 + k of the launch)
-  uint8_t r0;                     // the run's round within the launch (a start group entering late: > 0);
-                                  // level-aligned windows (PullArgs::srow): the group's start round
+  uint8_t r0;                     // the run's round within the launch (a start group entering late: > 0)
   uint16_t group;                 // host: the start group
   // first node of levels d .. d + levels: a run [x0, x1) of level d + k has
   // the children [row_ptr[x0] - row_ptr[first[k]] + first[k + 1], ...x1...)
@@ -424,6 +416,21 @@ hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_
 // kernel boundary less per pipelined window.  The two touch
 // disjoint memory: the reduce reads its own slot's partials and descriptors,
 // the init writes the other slot's.
+// A level-aligned window's per-(topic, level) reach counts:
+// the nodes [lo, hi) of segment seg (one BFS level of one topic; a level is
+// cut into pieces of at most kReachPiece nodes).  out[2 * seg] += reached
+// nodes, out[2 * seg + 1] += frontier nodes (reached and internal; eager
+// seen: internal, as the level kernels count their parents then).  Reached:
+// the generation byte is this window's (eager seen: the row's first word is
+// non-zero -- its first message's bit); a topic root always.
+struct ReachPiece {
+  uint32_t seg, lo, hi, topic;
+};
+constexpr uint32_t kReachPiece = 16384;
+hipError_t launch_level_reach(const ReachPiece* pieces, uint32_t n, const uint8_t* gen, uint32_t gen_cur,
+                              const uint8_t* node_flags, const TopicDev* topics, const uint64_t* seen, bool eager,
+                              uint64_t* out, hipStream_t s);
+
 struct ReduceArgs {
   const uint64_t* partials = nullptr;
   const uint32_t* desc = nullptr;

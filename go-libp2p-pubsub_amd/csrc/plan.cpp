@@ -43,6 +43,37 @@ int plan_window_layout(ps_engine* e, const std::vector<RunMsg>& msgs, const std:
   L.tstart.assign(std::max<uint32_t>(nt, 1), 0);
   L.wglob.assign(std::max<uint32_t>(nt, 1), 0);
   L.need_direct = e->world > 1;
+  // Level-aligned start groups (one rank, ps_plan_opts.align_groups).  In a
+  // tree window, messages published in different rounds are independent:
+  // the tree and the live mask do not change inside a window, so a message
+  // published in round s reaches the same peers at the same hops as one
+  // published in round 0, s rounds later (hop = depth, client.go:100-132).
+  // Its topic's row is then the burst's row -- node-major, one bit per
+  // message, the bits sorted by start round -- and the window runs the
+  // burst's schedule over the BFS levels (every start taken as round 0).
+  // Only the observable rounds differ: round s + d delivers level d of the
+  // messages starting in s.  The per-round counters are split after the
+  // window from each (topic, level)'s reached and frontier nodes
+  // (k_level_reach, checked against the kernels' per-level counters).  The
+  // reach rows ride in the window's counter reduce and must fit a run
+  // slot's pinned rows.
+  bool align = false;
+  if (e->world == 1 && e->align_groups && !e->run_zero_start && !(e->cfg.flags & PS_F_COMPACT)) {
+    bool multi = false, mesh = false;
+    uint64_t segs = 0;
+    uint32_t depth = 0;
+    for (uint32_t t = 0; t < nt; ++t) {
+      const TopicHost& T = e->topics[t];
+      if (!T.exists || win[t].n == 0) continue;
+      mesh |= T.mesh;
+      const uint32_t s0 = msgs[win[t].idx[0]].start;
+      for (uint32_t li = 1; li < win[t].n && !multi; ++li) multi |= msgs[win[t].idx[li]].start != s0;
+      segs += T.depth + 1;
+      depth = std::max(depth, T.depth);
+    }
+    align = multi && !mesh && depth + 2 + ceil_div(2 * segs, static_cast<uint64_t>(kNumCtr)) <= kAlignedRowsMax;
+  }
+  uint32_t true_max_start = 0;
   for (uint32_t t = 0; t < nt; ++t) {
     const TopicHost& T = e->topics[t];
     TopicDev& d = L.tab[t];
@@ -59,6 +90,24 @@ int plan_window_layout(ps_engine* e, const std::vector<RunMsg>& msgs, const std:
         s_hi = std::max(s_hi, s0);
       }
     if (e->run_zero_start) s_lo = s_hi = 0;
+    true_max_start = std::max(true_max_start, s_hi);
+    if (align) {
+      // the topic's start groups over its packed row: bits by (start, window order)
+      auto& G = L.split.groups;
+      G.resize(nt);
+      std::vector<uint32_t> cnt(s_hi - s_lo + 2, 0);
+      for (uint32_t li = 0; li < win[t].n; ++li) cnt[msgs[win[t].idx[li]].start - s_lo + 1]++;
+      for (uint32_t k = 0; k <= s_hi - s_lo; ++k) {
+        if (cnt[k + 1]) G[t].push_back(AlignedGroup{s_lo + k, cnt[k], cnt[k + 1]});
+        cnt[k + 1] += cnt[k];
+      }
+      if (s_lo != s_hi) {
+        auto& P = L.pos[t];
+        P.resize(win[t].n);
+        for (uint32_t li = 0; li < win[t].n; ++li) P[li] = cnt[msgs[win[t].idx[li]].start - s_lo]++;
+      }
+      s_lo = s_hi = 0;  // (planned as one start, round 0)
+    }
     L.max_start = std::max(L.max_start, s_hi);
     const bool one_start = s_lo == s_hi;
     L.multi |= !one_start && !T.mesh;
@@ -137,31 +186,23 @@ int plan_window_layout(ps_engine* e, const std::vector<RunMsg>& msgs, const std:
     for (const StartGroup& g : L.groups[t]) L.gtab.push_back(GroupDev{g.w0, g.wn});
   }
   L.true_rounds = L.planned0;
-  // Level-aligned start groups (one rank).  In a tree window the groups are
-  // independent: group g's block at level d depends only on its block at
-  // level d - 1, whatever round that ran in -- the tree and the live mask do
-  // not change inside a window, so a message published in round s reaches
-  // the same peers at the same hops as one published in round 0, only s
-  // rounds later (client.go:100-132: hop = depth).  So every group runs on
-  // the burst's schedule: launch round q writes level q of every group (the
-  // planners see start 0), and the true round q + soff appears only where it
-  // is observable: each group's counters go to its own row of the launch
-  // round, its hop records carry q + soff.  max_start rounds fewer, and the
-  // deep-window machinery (chains from round 1, the cross-window overlap)
-  // applies to paced publishing as to a burst.  The reduce rows (launch
-  // rounds x start rounds) must fit the pinned rows of a run slot.
-  const uint32_t srows = L.max_start + 1;
-  if (L.multi && L.level && !L.any_mesh && e->world == 1 && e->align_groups && srows <= 255 &&
-      static_cast<uint64_t>(L.max_depth + 2) * srows <= kAlignedRowsMax) {
+  if (align && !L.level) return e->fail(PS_E_STATE, "aligned window outside level mode");  // (unreachable)
+  if (align) {
+    AlignedSplit& sp = L.split;
     L.aligned = true;
-    L.srows = srows;
-    for (uint32_t t = 0; t < nt; ++t)
-      for (StartGroup& g : L.groups[t]) {
-        g.soff = g.start;
-        g.start = 0;
-      }
-    L.max_start = 0;
-    L.planned0 = L.max_depth + 1;
+    L.true_rounds = L.planned0 + true_max_start;
+    sp.seg_lo.assign(nt, kNone);
+    sp.seg_n.assign(nt, 0);
+    for (uint32_t t = 0; t < nt; ++t) {
+      if (!L.tab[t].W) continue;
+      sp.seg_lo[t] = sp.n_segs;
+      sp.seg_n[t] = e->topics[t].depth + 1;  // levels 0 .. depth
+      sp.n_segs += sp.seg_n[t];
+    }
+    sp.row0 = L.planned0 + 1;
+    sp.eager = (e->cfg.flags & PS_F_NO_LAZY_SEEN) != 0;
+  } else {
+    L.split = AlignedSplit{};
   }
   return PS_OK;
 }
@@ -186,8 +227,7 @@ bool plan_pull_chunks(ps_engine* e, const WindowLayout& L) {
     key.push_back(tab[t].W);
     key.push_back(tab[t].wbase << 1 | ((tab[t].flags & kTopicGroups) ? 1 : 0));
     if (tab[t].W)
-      for (const StartGroup& g : L.groups[t])
-        key.insert(key.end(), {static_cast<uint64_t>(g.start) << 32 | g.w0, g.soff});
+      for (const StartGroup& g : L.groups[t]) key.push_back(static_cast<uint64_t>(g.start) << 32 | g.w0);
   }
   PullPlan& P = e->pull;
   if (key == P.key) return false;
@@ -201,7 +241,7 @@ bool plan_pull_chunks(ps_engine* e, const WindowLayout& L) {
   P.bytes.assign(rounds + 2, 0);
   std::vector<PullChunk> ghost;
   auto cut = [&](std::vector<PullChunk>& out, uint32_t t, uint32_t gi, uint32_t u0, uint32_t u1, uint32_t per,
-                 uint32_t W, uint64_t row0, uint32_t soff) {
+                 uint32_t W, uint64_t row0) {
     const TopicHost& T = e->topics[t];
     for (uint32_t u = u0; u < u1; u += per) {
       PullChunk c{};
@@ -215,7 +255,6 @@ bool plan_pull_chunks(ps_engine* e, const WindowLayout& L) {
       c.row0_hi = static_cast<uint32_t>(row0 >> 32);
       c.gin = c.gout = kNoneNode;
       c.group = gi;
-      c.soff = soff;
       out.push_back(c);
     }
   };
@@ -235,8 +274,8 @@ bool plan_pull_chunks(ps_engine* e, const WindowLayout& L) {
         const uint32_t W = block_w(tab[t], g);
         const uint32_t per = std::max<uint32_t>(1, std::min<uint32_t>(kPullMaxKids, e->pull_words / W));
         P.bytes[q] += static_cast<uint64_t>(hi - lo) * W * 8;
-        cut(P.chunks, t, gi, lo, lo + nl, per, W, block_row0(tab[t], g), g.soff);
-        cut(ghost, t, gi, lo + nl, hi, per, W, block_row0(tab[t], g), g.soff);
+        cut(P.chunks, t, gi, lo, lo + nl, per, W, block_row0(tab[t], g));
+        cut(ghost, t, gi, lo + nl, hi, per, W, block_row0(tab[t], g));
       }
     }
     P.gsplit[q] = static_cast<uint32_t>(P.chunks.size());
@@ -279,8 +318,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   constexpr uint32_t stage = kPairWords;
   const double kLaunchBytes = e->launch_bytes;  // ~3 us of launch ramp and tail at ~5.5 TB/s
   const uint32_t nt = static_cast<uint32_t>(e->topics.size());
-  // (level-aligned start groups run the burst's schedule: chain_max)
-  const uint32_t chain_max = (L.multi && !L.aligned) ? e->chain_max_groups : e->chain_max;
+  const uint32_t chain_max = L.multi ? e->chain_max_groups : e->chain_max;
   const uint32_t max_len = std::max<uint32_t>(1, std::min<uint32_t>(chain_max, kChainLevels));
   auto& kind = PP.kind;
   kind.assign(rounds + 2, PS_K_NONE);
@@ -449,7 +487,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
             c.w0 = w0;
             c.S = std::min(z.S, W - w0);
             c.levels = static_cast<uint8_t>(levels);
-            c.r0 = static_cast<uint8_t>(L.aligned ? g.soff : r0);  // (aligned: r0 = 0, the group's start)
+            c.r0 = static_cast<uint8_t>(r0);
             c.group = static_cast<uint16_t>(gi);
             c.nbase = T.nbase;
             c.root = T.root_local ? T.nbase : kNoneNode;
@@ -511,7 +549,6 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
             c.c_lo = late ? kNoneNode : 0;  // children: filled in on the device
             c.gin = c.gout = kNoneNode;
             c.group = gi;
-            c.soff = g.soff;
             (part ? ghost : C).push_back(c);
           }
         }
@@ -533,7 +570,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
 // so they keep k_flood: a small deep tree has nothing to gain from chains.)
 bool deep_window(const ps_engine* e, const WindowLayout& L) {
   if (!(e->overlap_on && L.level && e->world == 1 && !L.any_mesh && !(e->cfg.flags & PS_F_RECORD_HOPS) &&
-        (!L.multi || L.aligned) && L.planned0 >= e->overlap_min_rounds))
+        !L.multi && L.planned0 >= e->overlap_min_rounds))
     return false;
   uint64_t rows = 0;  // the window's row bytes, as run.cpp's floor counts them
   for (uint32_t t = 0; t < L.tab.size(); ++t)
@@ -569,8 +606,7 @@ bool plan_flood_tasks(ps_engine* e, const WindowLayout& L, uint32_t rounds) {
     key.push_back(tab[t].W);
     key.push_back(tab[t].wbase << 1 | ((tab[t].flags & kTopicGroups) ? 1 : 0));
     if (tab[t].W)
-      for (const StartGroup& g : L.groups[t])
-        key.insert(key.end(), {static_cast<uint64_t>(g.start) << 32 | g.w0, g.soff});
+      for (const StartGroup& g : L.groups[t]) key.push_back(static_cast<uint64_t>(g.start) << 32 | g.w0);
   }
   FloodPlan& F = e->flood;
   if (key == F.key) return false;
@@ -579,10 +615,8 @@ bool plan_flood_tasks(ps_engine* e, const WindowLayout& L, uint32_t rounds) {
   auto& SG = F.segs;
   TK.clear();
   SG.clear();
-  // counter rows: per round, or (level-aligned) per round and start group
-  const uint32_t srows = L.srows;
-  F.slot0.assign(static_cast<size_t>(rounds + 2) * srows, 0);
-  F.nslot.assign(static_cast<size_t>(rounds + 2) * srows, 0);
+  F.slot0.assign(rounds + 2, 0);
+  F.nslot.assign(rounds + 2, 0);
   // each (topic, start group)'s segment of the previous round
   std::vector<std::vector<uint32_t>> seg_prev(nt);
   for (uint32_t t = 0; t < nt; ++t) seg_prev[t].assign(L.groups[t].size(), kNone);
@@ -623,8 +657,7 @@ bool plan_flood_tasks(ps_engine* e, const WindowLayout& L, uint32_t rounds) {
           k.nb = T.nbase + u;
           k.ne = T.nbase + std::min(u + per, hi);
           k.topic = t;
-          k.round = q + g.soff;
-          k.slot0 = g.soff;  // (the row, until the slots are assigned below)
+          k.round = q;
           k.g_own = sg.gbase + (u - lo) / gsz;
           k.gsz = gsz;
           k.pseg = pseg;
@@ -633,22 +666,16 @@ bool plan_flood_tasks(ps_engine* e, const WindowLayout& L, uint32_t rounds) {
         }
       }
     }
-    if (TK.size() == first) continue;
-    for (uint32_t so = 0; so < srows; ++so) {  // the round's row of each start offset
-      uint32_t n_row = 0;
-      for (size_t i = first; i < TK.size(); ++i) n_row += TK[i].slot0 == so;
-      if (!n_row) continue;
-      const uint32_t ns = std::min<uint32_t>(kPullSlots, n_row);
-      const size_t v = static_cast<size_t>(q) * srows + so;
-      F.slot0[v] = slot;
-      F.nslot[v] = ns;
-      slot += ns;
-    }
+    const uint32_t n_round = static_cast<uint32_t>(TK.size() - first);
+    if (!n_round) continue;
+    const uint32_t ns = std::min<uint32_t>(kPullSlots, n_round);
+    F.slot0[q] = slot;
+    F.nslot[q] = ns;
     for (size_t i = first; i < TK.size(); ++i) {
-      const size_t v = static_cast<size_t>(q) * srows + TK[i].slot0;
-      TK[i].slot0 = F.slot0[v];
-      TK[i].nslot = F.nslot[v];
+      TK[i].slot0 = slot;
+      TK[i].nslot = ns;
     }
+    slot += ns;
   }
   F.slots = slot;
   F.granules = gran;

@@ -390,19 +390,6 @@ __device__ __forceinline__ void pull_flush(const PullCtr& c, uint64_t* partials,
   }
 }
 
-// A level-aligned window's k_pull (PullArgs::srow): each wave adds its own
-// chunk's counters into its start group's row (the chunks of one block may
-// belong to different groups); no block barrier.
-__device__ __forceinline__ void pull_flush_own(const PullCtr& c, uint64_t* partials, uint64_t slot, uint32_t lane) {
-  const uint64_t v7[7] = {wave_sum_u64(c.deliv),   wave_sum_u64(c.sw),      wave_sum_u64(c.kids),
-                          wave_sum_u64(c.reached), wave_sum_u64(c.parents), wave_sum_u64(c.pwords),
-                          wave_sum_u64(c.dup)};
-  const uint64_t v = lane < kNumCtr ? pull_ctr_pick(v7, lane) : 0;
-  if (v)
-    atomicAdd(reinterpret_cast<unsigned long long*>(partials + slot * kNumCtr + lane),
-              static_cast<unsigned long long>(v));
-}
-
 // (Capping the big rounds' residency through the register allocation, as
 // k_pull_chain does, measured no gain: profiles/r04/ab/pull_simd.log.)
 template <bool kRecord, bool kNT>
@@ -417,10 +404,8 @@ __global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __
   uint8_t* genl = reinterpret_cast<uint8_t*>(gen_lds[wid]);
   const uint32_t cur = a.gen_cur & 0xFF;
   PullCtr c;
-  uint32_t soff = 0;
   if (wave < n_chunks) {  // one chunk per wave
     const PullChunk ch = chunks[wave];
-    soff = ch.soff;
     const TopicDev T = a.topics[ch.topic];
     PullTopic P;
     P.W = ch.W;
@@ -431,15 +416,10 @@ __global__ __launch_bounds__(kBlock) void k_pull(PullArgs a, const PullChunk* __
     // LDS ops of a wave are processed in order: the table written in phase 1
     // is visible to the reads that follow
     pull_resolve(a, P, ch.node_begin, n1, ch.p_lo, ch.p_hi, src, genl, lane, cur, c, ch.gin);
-    pull_stream<kRecord, kNT>(a, P, ch.node_begin, n1, src, lane, round + ch.soff, c);
+    pull_stream<kRecord, kNT>(a, P, ch.node_begin, n1, src, lane, round, c);
     if (ch.e_hi > ch.e_lo) pull_ship(a, P, ch.node_begin, ch.e_lo, ch.e_hi, ch.gout, src, lane);
   }
-  if (a.srow) {  // (wave-uniform)
-    if (wave < n_chunks)
-      pull_flush_own(c, a.partials + static_cast<uint64_t>(soff) * a.srow, blockIdx.x % a.slot_mod, lane);
-  } else {
-    pull_flush(c, a.partials, blockIdx.x % a.slot_mod, lane, wid);
-  }
+  pull_flush(c, a.partials, blockIdx.x % a.slot_mod, lane, wid);
 }
 
 // k_pull_pair: rounds q and q + 1 in one launch (one rank).
@@ -641,8 +621,7 @@ __global__ __launch_bounds__(64) void k_pull_pair(PullArgs a, const PullChunk* _
       const uint64_t b = __ballot(j0 + lane < n1 && src[j0 + lane] != 0);
       if (lane == 0) reach[j0 >> 6] = b;
     }
-    pull_stream<kRecord, true, true>(a, P, ch.node_begin, n1, src, lane, round + ch.soff + (late ? 1 : 0), ca,
-                                     rows);
+    pull_stream<kRecord, true, true>(a, P, ch.node_begin, n1, src, lane, round + (late ? 1 : 0), ca, rows);
     ctr_fold(ca);
     // src (u64 sources) and ctab (u32 offsets) share the LDS table: no memory
     // access may move across the switch from one view to the other
@@ -653,22 +632,12 @@ __global__ __launch_bounds__(64) void k_pull_pair(PullArgs a, const PullChunk* _
       ctr_add(c, ca);
       if (ch.c_hi > ch.c_lo)
         pair_kids<kRecord, kNT2, kPairWords>(a, P, ch.node_begin, n1, ch.c_lo, ch.c_hi, reach, rows,
-                                             reinterpret_cast<uint32_t*>(src), lane, round + ch.soff + 1, pf_p, pf_f,
-                                             c2);
+                                             reinterpret_cast<uint32_t*>(src), lane, round + 1, pf_p, pf_f, c2);
     }
     asm volatile("" ::: "memory");
-    if (a.srow) {  // level-aligned: each chunk into its start group's rows
-      const uint64_t o = static_cast<uint64_t>(ch.soff) * a.srow;
-      pull_flush_wave(c, a.partials + o, blockIdx.x % a.slot_mod, lane);
-      pull_flush_wave(c2, a.partials2 + o, blockIdx.x % a.slot_mod, lane);
-      c = WaveCtr{};
-      c2 = WaveCtr{};
-    }
   }
-  if (!a.srow) {
-    pull_flush_wave(c, a.partials, blockIdx.x % a.slot_mod, lane);
-    pull_flush_wave(c2, a.partials2, blockIdx.x % a.slot_mod, lane);
-  }
+  pull_flush_wave(c, a.partials, blockIdx.x % a.slot_mod, lane);
+  pull_flush_wave(c2, a.partials2, blockIdx.x % a.slot_mod, lane);
 }
 
 // Children ranges of the pair chunks (GPU or host node space alike).
@@ -1125,13 +1094,6 @@ __device__ __forceinline__ uint64_t* chain_slots(const PullArgs& a, uint32_t i) 
   }
 }
 
-// Round r0 + k's slot row of a chain launch; level-aligned (srow): level
-// k's row block, row r0 (the chunk's start group) of it.
-__device__ __forceinline__ uint64_t* chain_row(const PullArgs& a, uint32_t r0, uint32_t k) {
-  if (a.srow) return chain_slots(a, k) + static_cast<uint64_t>(r0) * a.srow;
-  return chain_slots(a, r0 + k);
-}
-
 __device__ __forceinline__ void chain_flush(WaveCtr& c, uint64_t* partials, uint64_t slot, uint32_t lane) {
   ctr_fold(c);
   const uint64_t v7[7] = {c.dsum, c.sw, c.kids, c.reached, c.parents, c.pwords, 0ull};
@@ -1325,7 +1287,7 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
   } else {
     chain_level0_direct<kRecord, kInNT, kSlices>(a, C, cp, p_lo, p_hi, reinterpret_cast<uint64_t*>(ctab),
                                                  reinterpret_cast<uint8_t*>(gen_lds), stage, tabs[0], lane, cur,
-                                                 round + r0, slot, chain_row(a, r0, 0), words_out);
+                                                 round + r0, slot, chain_slots(a, r0), words_out);
     g = (cp->node_end - cp->node_begin + 63) >> 6;  // (the batch's level-0 slots)
     k0 = 1;
     asm volatile("" ::: "memory");  // (level 0's sources become ctab)
@@ -1369,7 +1331,7 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
       ctr_fold(c);
     }
     words_out += c.sw;
-    chain_flush(c, chain_row(a, r0, k), slot, lane);
+    chain_flush(c, chain_slots(a, r0 + k), slot, lane);
     asm volatile("" ::: "memory");
   }
   if (a.prof) {

@@ -298,7 +298,6 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   auto& groups = L.groups;
   const uint64_t wtot = L.wtot;
   const uint32_t max_start = L.max_start, planned0 = L.planned0, round_cap = L.round_cap;
-  const uint32_t sr = L.srows;  // counter rows per round (level-aligned start groups: one per start round)
   const bool level = L.level, any_mesh = L.any_mesh, need_direct = L.need_direct;
   const auto t_w1 = std::chrono::steady_clock::now();
   const bool record = (e->cfg.flags & PS_F_RECORD_HOPS) != 0;
@@ -332,7 +331,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     } else {
       for (uint32_t li = 0; li < win[t].n; ++li) {
         const uint32_t b = L.pos[t].empty() ? li : L.pos[t][li];
-        // (level-aligned: every group's root block is seeded before launch round 1)
+        // (level-aligned: every message is seeded before launch round 1)
         const uint32_t r0 = L.aligned ? 0u : msgs[win[t].idx[li]].start;
         inj[t][static_cast<size_t>(r0) * d.W + (b >> 6)] |= 1ull << (b & 63);
       }
@@ -406,6 +405,34 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   uint32_t flood_rounds = 0;    // rounds 1..flood_rounds: k_flood
   std::vector<uint32_t> lgrid;  // per-round launches: blocks of every round (L and G parts together)
   uint32_t n_slots = 0;         // level mode: partial counter slots of the window
+  // level-aligned windows: counter rows of the reach counts after the rounds'
+  const uint32_t reach_rows =
+      L.aligned ? static_cast<uint32_t>(ceil_div(2ull * L.split.n_segs, static_cast<uint64_t>(kNumCtr))) : 0u;
+  uint32_t reach_slot0 = 0;
+  if (L.aligned) {
+    // the (topic, level) pieces, cached per node space and active topic set
+    std::vector<uint64_t> key{e->graph_epoch};
+    for (uint32_t t = 0; t < nt; ++t) key.push_back(L.split.seg_lo[t]);
+    if (key != e->reach_key) {
+      std::vector<ReachPiece>& pc = e->reach_host;
+      pc.clear();
+      for (uint32_t t = 0; t < nt; ++t) {
+        if (L.split.seg_lo[t] == kNone) continue;
+        const TopicHost& T = e->topics[t];
+        for (uint32_t dl = 0; dl < L.split.seg_n[t]; ++dl)
+          for (uint32_t u = T.level_off[dl]; u < T.level_off[dl + 1]; u += kReachPiece)
+            pc.push_back(ReachPiece{L.split.seg_lo[t] + dl, T.nbase + u,
+                                    T.nbase + std::min<uint32_t>(u + kReachPiece, T.level_off[dl + 1]), t});
+      }
+      HIP_TRY(e->d_reach.ensure(std::max<size_t>(pc.size(), 1) * sizeof(ReachPiece)), "alloc reach pieces");
+      if (!pc.empty())
+        HIP_TRY(hipMemcpyAsync(e->d_reach.p, pc.data(), pc.size() * sizeof(ReachPiece), hipMemcpyHostToDevice,
+                               e->stream),
+                "upload reach pieces");
+      e->n_reach = static_cast<uint32_t>(pc.size());
+      e->reach_key = key;
+    }
+  }
   bool fresh = false;           // level mode: no plan upload this window
   if (level) {
     bool changed = plan_pull_chunks(e, L);
@@ -434,32 +461,28 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     e->round_kind = e->pair.kind;
     if (flood_rounds && (rc = upload_flood(e))) return rc;
     if (world > 1 && gch && (rc = upload_ghost(e))) return rc;
-    // desc[3v..]: counter row v's partial slots (first, end, stride) for the
-    // reduce; row v = round q (level-aligned: v = q * srows + soff, launch
-    // round q of the groups starting in round soff)
+    // desc[3q..]: round q's partial slots (first, end, stride) for the reduce
     auto& desc = e->desc_host;
-    desc.assign(3 * ((planned0 + 2) * sr), 0);
+    desc.assign(3 * (planned0 + 2 + reach_rows), 0);
     uint32_t slot = 0;
     if (flood_rounds) {
       desc[0] = 0;  // row 0: k_flood's timeout word (slot 0)
       desc[1] = 1;
       desc[2] = 1;
-      for (uint32_t v = sr; v < (flood_rounds + 1) * sr; ++v) {
-        desc[3 * v] = e->flood.slot0[v];
-        desc[3 * v + 1] = e->flood.slot0[v] + e->flood.nslot[v];
-        desc[3 * v + 2] = e->flood.nslot[v] ? 1 : 0;
+      for (uint32_t q = 1; q <= flood_rounds; ++q) {
+        desc[3 * q] = e->flood.slot0[q];
+        desc[3 * q + 1] = e->flood.slot0[q] + e->flood.nslot[q];
+        desc[3 * q + 2] = e->flood.nslot[q] ? 1 : 0;
       }
       slot = e->flood.slots;
     }
     // the launches of round q own the slots [woff[q], woff[q+1]): one per
     // block (pull) or wave (pair), at most kPullSlots; the L and G parts of
-    // a round share them (counters are added).  Level-aligned: the same
-    // number of slots for each start group, rows q * srows .. q * srows +
-    // srows - 1 (PullArgs::srow apart)
+    // a round share them (counters are added)
     lgrid.assign(planned0 + 1, 0);
     auto& woff = e->woff_host;
-    woff.assign((planned0 + 2) * sr, 0);
-    woff[(flood_rounds + 1) * sr] = slot;
+    woff.assign(planned0 + 2, 0);
+    woff[flood_rounds + 1] = slot;
     for (uint32_t q = flood_rounds + 1; q <= planned0; ++q) {
       const uint8_t kq = e->round_kind[q];
       const bool multi_round = kq == PS_K_PAIR || kq == PS_K_CHAIN;
@@ -467,18 +490,25 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       lgrid[q] = multi_round ? e->pair.hi[q] - e->pair.lo[q]  // (one one-wave workgroup per chunk)
                              : ceil_div(e->pull.gsplit[q] - e->pull.off[q], kBlock / 64) +
                                    ceil_div(e->pull.off[q + 1] - e->pull.gsplit[q], kBlock / 64);
-      for (uint32_t k = q; k < q + len; ++k)  // a multi-round launch: one slot range per round (and start)
-        for (uint32_t so = 0; so < sr; ++so) {
-          const uint32_t v = k * sr + so;
-          woff[v + 1] = woff[v] + std::min<uint32_t>(lgrid[q], multi_round ? kPairSlots : kPullSlots);
-          desc[3 * v] = woff[v];
-          desc[3 * v + 1] = woff[v + 1];
-          desc[3 * v + 2] = 1;
-        }
+      for (uint32_t k = q; k < q + len; ++k) {  // a multi-round launch: one slot range per round
+        woff[k + 1] = woff[k] + std::min<uint32_t>(lgrid[q], multi_round ? kPairSlots : kPullSlots);
+        desc[3 * k] = woff[k];
+        desc[3 * k + 1] = woff[k + 1];
+        desc[3 * k + 2] = 1;
+      }
       for (uint32_t k = 1; k < len; ++k) lgrid[q + k] = 0;
       q += len - 1;
     }
-    n_slots = woff[(planned0 + 1) * sr];
+    n_slots = woff[planned0 + 1];
+    // level-aligned: the reach counts (2 per (topic, level) segment, kNumCtr
+    // per slot) as pseudo-slots after the rounds', one reduce row each
+    reach_slot0 = n_slots;
+    for (uint32_t j = 0; j < reach_rows; ++j) {
+      desc[3 * (planned0 + 1 + j)] = n_slots + j;
+      desc[3 * (planned0 + 1 + j) + 1] = n_slots + j + 1;
+      desc[3 * (planned0 + 1 + j) + 2] = 1;
+    }
+    n_slots += reach_rows;
     fresh = fresh && !chain_overflow;
     HIP_TRY(d_partials.ensure(static_cast<size_t>(std::max<uint32_t>(n_slots, 1)) * kNumCtr * 8),
             "alloc level partials");
@@ -549,7 +579,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // (a shallow window -- k_flood leading rounds, nothing but its init to hide
   // -- ends signalled instead: its events cost more than the init, cfg4
   // 0.4472-0.4479 -> 0.4421-0.4425 ms/step, profiles/r04/ab/shallow_signalled.log)
-  const bool pcap = e->overlap_on && level && world == 1 && !any_mesh && !record && (!L.multi || L.aligned) &&
+  const bool pcap = e->overlap_on && level && world == 1 && !any_mesh && !record && !L.multi &&
                     !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS)) && total >= e->overlap_min_bytes && deep;
   if (pcap && !e->pstream) {  // (created on first use: multi-rank engines never need them)
     HIP_TRY(hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking), "prefix stream");
@@ -906,8 +936,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         pa.slot_mod = kPairSlots;
         pa.row_ptr = e->d_row_ptr.as<uint32_t>();
         for (uint32_t k = 0; k < kChainLevels; ++k)
-          pa.partials_r[k] = k < len ? partials + static_cast<size_t>(e->woff_host[(r + k) * sr]) * kNumCtr : nullptr;
-        pa.srow = L.aligned ? (e->woff_host[r * sr + 1] - e->woff_host[r * sr]) * kNumCtr : 0u;
+          pa.partials_r[k] = k < len ? partials + static_cast<size_t>(e->woff_host[r + k]) * kNumCtr : nullptr;
         HIP_TRY(time_mark(true), "event");
         ++launches;
         uint64_t* const prof = cprof ? e->d_chain_prof.as<uint64_t>() : nullptr;
@@ -929,10 +958,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       // (large rounds and the last round) store non-temporally
       const uint32_t rw = pair ? r + 1 : r;  // the round whose rows the next launch reads
       const bool nt = rw < e->pull.bytes.size() && (e->pull.bytes[rw] >= ps_engine::kNtBytes || rw == planned0);
-      pa.partials = partials + static_cast<size_t>(e->woff_host[r * sr]) * kNumCtr;
+      pa.partials = partials + static_cast<size_t>(e->woff_host[r]) * kNumCtr;
       pa.slot_mod = pair ? kPairSlots : kPullSlots;
-      if (pair) pa.partials2 = partials + static_cast<size_t>(e->woff_host[(r + 1) * sr]) * kNumCtr;
-      pa.srow = L.aligned ? (e->woff_host[r * sr + 1] - e->woff_host[r * sr]) * kNumCtr : 0u;
+      if (pair) pa.partials2 = partials + static_cast<size_t>(e->woff_host[r + 1]) * kNumCtr;
       // the locally fed part, then (after the exchange) the ghost-fed part;
       // without the overlap (PSAMD_XCHG_OVERLAP=0) one launch after the exchange
       const bool split = xs != s;
@@ -977,6 +1005,12 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       if (const int rc = reuse(planned0 - 1)) return rc;
     if (const int rc = reuse(planned0)) return rc;
     r = planned0;
+    // level-aligned: each (topic, level)'s reached and frontier nodes, for
+    // the per-round split (into the pseudo-slots after the rounds')
+    if (L.aligned && e->n_reach)
+      HIP_TRY(launch_level_reach(e->d_reach.as<ReachPiece>(), e->n_reach, a.gen, a.gen_cur, a.node_flags, a.topics,
+                                 a.seen, L.split.eager, partials + static_cast<size_t>(reach_slot0) * kNumCtr, s),
+              "level reach");
     // a deferred window's counters go straight into its pinned rows
     const bool direct = e->defer_last && e->defer_into && !record && !timed && r <= PS_MAX_ROUNDS &&
                         (world == 1 || planned0 <= PS_MAX_ROUNDS);
@@ -1012,10 +1046,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       // may be reallocated by then, and nobody reads a deferred window's
       e->pend_reduce.valid = true;
       e->pend_reduce.owner = e->defer_into;
-      e->pend_reduce.args = ReduceArgs{partials, d_woff.as<uint32_t>(), (planned0 + 1) * sr - 1, nullptr,
-                                       e->defer_into->hs_dev, wsig};
+      e->pend_reduce.args =
+          ReduceArgs{partials, d_woff.as<uint32_t>(), planned0 + reach_rows, nullptr, e->defer_into->hs_dev, wsig};
     } else {
-      HIP_TRY(launch_reduce_rounds(partials, d_woff.as<uint32_t>(), (planned0 + 1) * sr - 1, reduce_side ? nullptr : stats,
+      HIP_TRY(launch_reduce_rounds(partials, d_woff.as<uint32_t>(), planned0 + reach_rows, reduce_side ? nullptr : stats,
                                    direct ? e->defer_into->hs_dev : nullptr, wsig, rs),
               "reduce rounds");
     }
@@ -1098,7 +1132,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     // window's end event marks their arrival; ps_wait accumulates them
     ps_engine::Inflight& f = *e->defer_into;
     if (!host_stats_written)
-      HIP_TRY(hipMemcpyAsync(f.hs, stats, static_cast<size_t>(r + 1) * sr * kNumCtr * 8, hipMemcpyDeviceToHost, s),
+      HIP_TRY(hipMemcpyAsync(f.hs, stats, static_cast<size_t>(r + 1 + reach_rows) * kNumCtr * 8,
+                             hipMemcpyDeviceToHost, s),
               "read stats");
     if (world > 1)
       HIP_TRY(hipMemcpyAsync(f.ha, e->d_apply_stats.p, static_cast<size_t>(planned0 + 1) * kNumCtr * 8,
@@ -1108,7 +1143,11 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     if (!f.signalled) HIP_TRY(hipEventRecord(e->ev_run1, reduce_side ? e->rstream : s), "event");
     f.deferred = true;
     f.planned0 = planned0;
-    f.srows = sr;
+    f.true_rounds = L.aligned ? L.true_rounds : 0u;
+    if (L.aligned)
+      f.split = L.split;
+    else
+      f.split.n_segs = 0;
     f.world = world;
     f.r = r;
     f.launches = launches;
@@ -1138,7 +1177,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     const size_t q = ev_round[i / 2];  // round of this launch
     if (q < PS_MAX_ROUNDS) st->expand_ms_per_round[q] += k;
   }
-  std::vector<uint64_t> hs(static_cast<size_t>(r + 1) * sr * kNumCtr), ha;
+  std::vector<uint64_t> hs(static_cast<size_t>(r + 1 + reach_rows) * kNumCtr), ha;
   HIP_TRY(hipMemcpyAsync(hs.data(), stats, hs.size() * 8, hipMemcpyDeviceToHost, s), "read stats");
   if (world > 1) {
     ha.resize(static_cast<size_t>(planned0 + 1) * kNumCtr);
@@ -1148,8 +1187,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   HIP_TRY(hipStreamSynchronize(s), "sync");
   if (mode == PS_MODE_FLOOD && e->flood_profile && e->flood_prof_waves) flood_profile_report(e);
   if (cprof) chain_profile_dump(e, planned0);
-  if (!accumulate_window(st, hs.data(), ha.data(), r, planned0, sr, mode, flood_rounds, launches, world,
-                         e->round_kind)) {
+  if (L.aligned && !split_aligned_window(st, hs.data(), r, L.true_rounds, L.split))
+    return e->fail(PS_E_DEVICE, "level-aligned window: reach counts disagree with the per-level counters");
+  if (!accumulate_window(st, hs.data(), ha.data(), r, planned0, mode, flood_rounds, launches, world,
+                         e->round_kind, !L.aligned)) {
     // a k_flood dependency wait timed out (its waves were not all resident:
     // another engine or process shares the GPU): this window's rows are
     // incomplete.  Run the same window again with per-round launches under a
@@ -1183,7 +1224,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       if (d.W == 0) continue;
       for (uint32_t li = 0; li < win[t].n; ++li) {
         const uint32_t mi = win[t].idx[li];
-        const uint32_t s0 = msgs[mi].start;
+        const uint32_t s0 = L.aligned ? 0u : msgs[mi].start;  // (level-aligned: the record holds the level)
         const uint32_t b = L.pos[t].empty() ? li : L.pos[t][li];
         uint8_t* row = e->hops.data() + static_cast<size_t>(mi) * np;
         for (uint32_t u = 0; u < d.n_nodes; ++u) {
@@ -1226,17 +1267,13 @@ int run_phase(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<W
 // the run's stats.  Returns false when a k_flood dependency wait timed out
 // (its timeout word is folded into row 0).
 bool accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uint32_t r, uint32_t planned0,
-                       uint32_t srows, uint32_t mode, uint32_t flood_rounds, uint32_t launches, int32_t world,
-                       const std::vector<uint8_t>& kinds) {
+                       uint32_t mode, uint32_t flood_rounds, uint32_t launches, int32_t world,
+                       const std::vector<uint8_t>& kinds, bool by_round) {
   const bool pull = mode == PS_MODE_LEVEL_PULL || mode == PS_MODE_FLOOD;
   std::memset(st->round_kernel, 0, sizeof(st->round_kernel));
-  // row v = launch round q = v / srows of the groups starting in round
-  // v % srows (level-aligned windows; else srows = 1, v = q): its deliveries
-  // belong to round q + v % srows, its launch to round q
-  for (uint32_t v = srows; v < (r + 1) * srows; ++v) {
-    const uint32_t q = v / srows, rt = q + v % srows;
+  for (uint32_t q = 1; q <= r; ++q) {
     const uint8_t kind = q < kinds.size() ? kinds[q] : static_cast<uint8_t>(pull ? PS_K_PULL : PS_K_EXPAND);
-    const uint64_t* c = &hs[static_cast<size_t>(v) * kNumCtr];
+    const uint64_t* c = &hs[static_cast<size_t>(q) * kNumCtr];
     const uint64_t app_d = (world > 1 && q <= planned0) ? ha[static_cast<size_t>(q) * kNumCtr + kCtrDeliveries] : 0;
     const uint64_t app_u = (world > 1 && q <= planned0) ? ha[static_cast<size_t>(q) * kNumCtr + kCtrDuplicates] : 0;
     st->deliveries += c[kCtrDeliveries] + app_d;
@@ -1265,19 +1302,58 @@ bool accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uin
     if (q < PS_MAX_ROUNDS) {
       st->round_kernel[q] = kind;
       st->expand_bytes_per_round[q] += b;
-    }
-    if (rt < PS_MAX_ROUNDS) {
-      st->deliveries_per_round[rt] += c[kCtrDeliveries] + app_d;
-      st->frontier_per_round[rt] += static_cast<uint32_t>(c[kCtrEntries]);
+      if (by_round) {  // (level-aligned windows: split_aligned_window)
+        st->deliveries_per_round[q] += c[kCtrDeliveries] + app_d;
+        st->frontier_per_round[q] += static_cast<uint32_t>(c[kCtrEntries]);
+      }
     }
   }
-  st->rounds += r + srows - 1;
-  st->level_aligned = srows > 1 ? 1u : 0u;
+  st->rounds += by_round ? r : 0;
+  st->level_aligned = by_round ? 0u : 1u;
   st->expand_launches += launches;
   st->expand_mode = mode;
   st->flood_rounds = flood_rounds;
   st->windows += 1;
   return mode != PS_MODE_FLOOD || hs[kCtrDeliveries] == 0;
+}
+
+// A level-aligned window: row d (1 .. r) holds the
+// kernels' counters of BFS level d over every topic; the reach rows after
+// them, per (topic, level) segment, the reached nodes and the frontier
+// nodes.  Level d of topic t delivers each message of group g (start s_g,
+// n_g messages) to every reached node in round s_g + d -- the reached node
+// holds its root's row, every message of the topic -- and expands the
+// frontier nodes of level d - 1 in that round.  Both are checked, level by
+// level, against the kernels' own popcounts and parent counts first.
+bool split_aligned_window(ps_stats* st, const uint64_t* hs, uint32_t r, uint32_t true_rounds,
+                          const AlignedSplit& sp) {
+  const uint64_t* reach = hs + static_cast<size_t>(r + 1) * kNumCtr;  // 2 per segment
+  const uint32_t nt = static_cast<uint32_t>(sp.seg_lo.size());
+  std::vector<uint64_t> deliv(r + 1, 0), front(r + 1, 0);
+  for (uint32_t t = 0; t < nt; ++t) {
+    if (sp.seg_lo[t] == kNone) continue;
+    uint64_t n_msgs = 0;
+    for (const AlignedGroup& g : sp.groups[t]) n_msgs += g.n;
+    for (uint32_t d = 1; d < sp.seg_n[t] && d <= r; ++d) {
+      const uint64_t reached = reach[2 * (sp.seg_lo[t] + d)], fr = reach[2 * (sp.seg_lo[t] + d - 1) + 1];
+      deliv[d] += reached * n_msgs;
+      front[d] += fr;
+      for (const AlignedGroup& g : sp.groups[t]) {
+        const uint32_t rt = g.start + d;
+        if (rt < PS_MAX_ROUNDS) {
+          st->deliveries_per_round[rt] += reached * g.n;
+          st->frontier_per_round[rt] += static_cast<uint32_t>(fr);
+        }
+      }
+    }
+  }
+  bool ok = true;
+  for (uint32_t d = 1; d <= r; ++d) {
+    const uint64_t* c = &hs[static_cast<size_t>(d) * kNumCtr];
+    ok = ok && c[kCtrDeliveries] == deliv[d] && c[kCtrEntries] == front[d];
+  }
+  st->rounds += true_rounds;
+  return ok;
 }
 
 // ps_run's body.  may_defer: the last window of the final phase may leave its
@@ -1515,8 +1591,11 @@ int ps_wait(ps_engine* e, ps_stats* out) {
   }
   if (f.deferred) {
     f.deferred = false;
-    if (!accumulate_window(&f.st, f.hs, f.ha, f.r, f.planned0, f.srows, f.mode, f.flood_rounds, f.launches, f.world,
-                           f.kinds)) {
+    const bool aligned = f.split.n_segs > 0;
+    if (aligned && !split_aligned_window(&f.st, f.hs, f.r, f.true_rounds, f.split))
+      return e->fail(PS_E_DEVICE, "level-aligned window: reach counts disagree with the per-level counters");
+    if (!accumulate_window(&f.st, f.hs, f.ha, f.r, f.planned0, f.mode, f.flood_rounds, f.launches, f.world,
+                           f.kinds, !aligned)) {
       e->flood_broken = true;
       return e->fail(PS_E_DEVICE, "k_flood: a dependency wait timed out (waves not co-resident?); "
                                   "per-round launches from now on");

@@ -13,7 +13,7 @@ INFO, NODES, PARENT, GHOST_REF, TOPIC, LAYOUT, ROUND_KIND, PULL, PAIR, XCHG, SEG
 CHAIN_FIELDS = ("node_begin", "node_end", "topic", "W", "row0", "w0", "S", "levels", "r0", "group")
 CHAIN_LEVELS = 6  # kChainLevels
 CHUNK_FIELDS = ("node_begin", "node_end", "topic", "W", "row0", "e_lo", "e_hi", "gin", "gout", "group",
-                "p_lo", "p_hi", "c_lo", "soff")
+                "p_lo", "p_hi", "c_lo")
 PROTOTYPES = [
     ("ps_plan_create", C.c_int, [C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
                                  C.POINTER(DistConfig), C.POINTER(_P)]),
@@ -107,7 +107,7 @@ class Plan:
     def info(self) -> dict:
         v = self.get(INFO)
         keys = ("rounds", "nodes", "pull_chunks", "pair_chunks", "world", "rank", "send_half", "recv_words",
-                "segs", "level", "ship", "aligned_rows")
+                "segs", "level", "ship", "aligned")
         return {k: int(x) for k, x in zip(keys, v)}
 
     def chunks(self, what: int, q: int):
@@ -127,8 +127,11 @@ class Plan:
     def layout(self, t: int) -> dict:
         v = self.get(LAYOUT, t)
         ng = int(v[3])
+        na = int(v[4 + 3 * ng])
+        a0 = 5 + 3 * ng
         return {"W": int(v[0]), "wbase": int(v[1]), "flags": int(v[2]),
-                "groups": [tuple(int(x) for x in v[4 + 3 * i:7 + 3 * i]) for i in range(ng)]}
+                "groups": [tuple(int(x) for x in v[4 + 3 * i:7 + 3 * i]) for i in range(ng)],
+                "aligned_groups": [tuple(int(x) for x in v[a0 + 3 * i:a0 + 3 + 3 * i]) for i in range(na)]}
 
     def xchg(self, q: int) -> dict:
         v = self.get(XCHG, q)

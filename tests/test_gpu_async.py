@@ -170,18 +170,16 @@ def test_overlapped_windows_equal_blocking(monkeypatch, dead, full):
 
 
 def vary_group_counts(msg_topics, starts, i):
-    """Window i's staggered batch: each (topic, start round) group loses up
-    to (n - 1) % 128 of its last messages, so every group block's even word
-    width -- and the plan -- stays, while its last word differs per window."""
+    """Window i's staggered batch: each topic loses up to (n_t - 1) % 64 of
+    its last messages (of whatever start rounds), so its packed row width
+    ceil(n_t / 64) -- and the plan -- stays, while its start groups' sizes
+    and its last row word change from window to window."""
     keep = np.ones(msg_topics.shape[0], dtype=bool)
     for t in np.unique(msg_topics):
-        for s0 in np.unique(starts):
-            idx = np.nonzero((msg_topics == t) & (starts == s0))[0]
-            if idx.shape[0] == 0:
-                continue
-            drop = (i * 7 + int(t) + 3 * int(s0)) % ((idx.shape[0] - 1) % 128 + 1)
-            if drop:
-                keep[idx[-drop:]] = False
+        idx = np.nonzero(msg_topics == t)[0]
+        drop = (i * 7 + int(t)) % ((idx.shape[0] - 1) % 64 + 1)
+        if drop:
+            keep[idx[-drop:]] = False
     return msg_topics[keep], starts[keep]
 
 
@@ -190,8 +188,8 @@ def test_overlapped_staggered_windows_equal_blocking(monkeypatch, dead, full):
     """Paced publishing (start rounds 0..7), pipelined: level-aligned start
     groups make a deep window whose leading launches run beside the previous
     window's last ones.  Eight windows with different
-    counts per (topic, start) group -- the same group widths, so the same
-    plan and the overlap applies -- equal blocking runs counter for counter
+    counts per (topic, start) group -- the same packed row widths, so the
+    same plan and the overlap applies -- equal blocking runs counter for counter
     and in the final rows, and the blocking round-by-round schedule
     (align_groups 0) too; the overlap did happen."""
     wl = WL.cfg3() if full else WL.cfg3(200_000, 16, 5000)

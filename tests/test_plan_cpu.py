@@ -161,12 +161,7 @@ class RankSim:
         for c in chunks:
             L, S = c["levels"], c["S"]
             n0 = c["node_end"] - c["node_begin"]
-            if self.info["aligned_rows"]:  # level-aligned start groups: r0 = the group's start round
-                assert 1 <= L <= n and c["r0"] < self.info["aligned_rows"] and 1 <= n0 <= 128
-                lay = self.lay[c["topic"]]
-                assert c["r0"] == lay["groups"][c["group"]][0]
-            else:
-                assert 1 <= L <= PL.CHAIN_LEVELS and c["r0"] + L <= n and 1 <= n0 <= 128
+            assert 1 <= L <= PL.CHAIN_LEVELS and c["r0"] + L <= n and 1 <= n0 <= 128
             assert S % 2 == 0 or S == c["W"]
             assert n0 * S <= 768, (n0, S, L)  # the LDS stage holds the run's rows (slices)
             assert c["first"][0] == self.topics[c["topic"]]["nbase"] + self.topics[c["topic"]]["level_off"][
@@ -290,7 +285,10 @@ def check(sims, trees, roots, live, n_groups):
                         r0 = s.block_row0(t, gi) + (u - T["nbase"]) * wn
                         assert np.array_equal(s.rows[r0:r0 + wn], root_block(t, gi, wn)), (t, u, gi)
         assert np.array_equal(got, exp), (t, int((got != exp).sum()))
-        assert len(Ly["groups"]) == n_groups[t] or not Ly["W"]
+        if sims[0].info["aligned"]:  # level-aligned: one packed block, the start groups over its bits
+            assert len(Ly["groups"]) == 1 and (len(Ly["aligned_groups"]) == n_groups[t] or not Ly["W"])
+        else:
+            assert len(Ly["groups"]) == n_groups[t] or not Ly["W"]
 
 
 def build(world, partition, n=1500, n_topics=2, seed=0, fan=None):
@@ -526,12 +524,12 @@ def test_deep_window_plan(overlap):
 @pytest.mark.parametrize("align", [0, 1])
 def test_aligned_start_groups_plan(align):
     """Paced publishing on one rank (start rounds 0..7): with align_groups the
-    window plans like the burst -- launch round q writes BFS level q of every
-    start group, rounds = depth + 1, chains from round 1 as a deep window --
-    and every chunk carries its group's start round (soff, a chain chunk's
-    r0) for its counter row and hop records; without it, one schedule over
-    start + depth rounds.  Both replay to the oracle, every group's block
-    written once per node."""
+    window plans exactly like the burst -- one packed node-major row per
+    topic, its bits sorted by start round, launch round q writing BFS level
+    q, chains from round 1 as a deep window -- and the start groups are bit
+    ranges of that row (start, first bit, messages); without it, one
+    group-major block per start round over start + depth rounds.  Both
+    replay to the oracle."""
     rng = np.random.default_rng(23)
     n = 6000
     parent = np.full(n, NONE, dtype=np.uint32)
@@ -543,24 +541,18 @@ def test_aligned_start_groups_plan(align):
     starts = (np.arange(3000) % 8).astype(np.uint32)
     p.window(msgs, starts)
     info = p.info()
-    groups = p.layout(0)["groups"]
-    assert [g[0] for g in groups] == list(range(8))
+    lay = p.layout(0)
     kinds = [int(k) for k in p.get(PL.ROUND_KIND)]
+    burst = PL.Plan(parent[None, :], [0], plan={"overlap_min_bytes": 0})
+    burst.window(msgs)
     if align:
-        assert info["aligned_rows"] == 8 and info["rounds"] == 13, info
-        assert PE.K_FLOOD not in kinds and kinds[1] == PE.K_CHAIN, kinds
-        seen = set()
-        for q in range(1, info["rounds"] + 1):
-            if kinds[q] == PE.K_CHAIN:
-                for c in p.chain(q)[1]:
-                    assert c["r0"] == groups[c["group"]][0]
-                    seen.add(c["r0"])
-            elif kinds[q] in (PE.K_PULL, PE.K_PAIR):
-                for c in p.chunks(PL.PAIR if kinds[q] == PE.K_PAIR else PL.PULL, q)[3]:
-                    assert c["soff"] == groups[c["group"]][0]
-        assert seen == set(range(8))
+        assert info["aligned"] == 1 and info["rounds"] == 13, info
+        assert lay["W"] == 48 and lay["groups"] == [(0, 0, 48)], lay  # ceil(3000 / 64) = 47, padded even
+        assert lay["aligned_groups"] == [(s0, 375 * s0, 375) for s0 in range(8)], lay["aligned_groups"]
+        assert kinds == [int(k) for k in burst.get(PL.ROUND_KIND)] and kinds[1] == PE.K_CHAIN, kinds
     else:
-        assert info["aligned_rows"] == 0 and info["rounds"] == 13 + 7, info
+        assert info["aligned"] == 0 and info["rounds"] == 13 + 7, info
+        assert [g[0] for g in lay["groups"]] == list(range(8)) and not lay["aligned_groups"]
     sims = [RankSim(p, live)]
     emulate(sims, info["rounds"], in_process_exchange(sims))
     check(sims, [parent], [0], live, [8])
