@@ -192,7 +192,6 @@ static void read_switches(ps_engine* e) {
   if (const char* v = std::getenv("PSAMD_UPLOAD_REUSE")) e->upload_reuse = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_SIG_WINDOWS")) e->sig_windows = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FUSE_REDUCE")) e->fuse_reduce = std::atoi(v) != 0;
-  if (const char* v = std::getenv("PSAMD_LB_PLACE")) e->lb_place = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD_MIN_ROUNDS"))
     o.flood_min_rounds = static_cast<uint32_t>(std::max(1, std::atoi(v)));
   if (const char* v = std::getenv("PSAMD_CHAIN_WAVES"))

@@ -84,6 +84,7 @@ struct TopicHost {
   bool mesh = false;
   bool root_local = true;                // this rank owns the root
   uint32_t max_deg = 0;
+  uint32_t top_levels = 1;  // GPU build: levels 1 .. top_levels - 1 fit the one-block top kernel
   std::vector<uint32_t> level_internal;  // BFS level -> owned nodes with children
   std::vector<uint32_t> level_off;       // BFS level -> first owned node (topic-relative)
   // multi-GPU: the owned nodes of level d are [level_off[d], level_off[d] +
@@ -246,7 +247,6 @@ struct ps_engine {
   bool host_only = false;        // a planner probe (psengine_plan.h): no device
   psamd::WindowLayout probe;     // the probe's last planned window
   bool host_timing = false;      // PSAMD_HOST_TIMING=1: host phase times to stderr
-  bool lb_place = true;           // levels placed by one look-back launch each (A/B: PSAMD_LB_PLACE=0)
   bool sig_windows = true;        // pipelined one-rank windows end with a pinned flag, not an event (A/B: PSAMD_SIG_WINDOWS=0)
   // per-window uploads (topic table, seeds, descriptors) kept on the device:
   // the bytes last staged into each buffer, skipped when a window repeats them
@@ -267,7 +267,6 @@ struct ps_engine {
     const void* owner = nullptr;  // the Inflight slot whose flag it raises
     psamd::ReduceArgs args{};
   } pend_reduce;
-  uint32_t small_place = 512;    // top levels up to this many nodes placed by one block
   // GPU rebuild of the node space: on by default for one
   // rank and tree topics (PSAMD_GPU_BUILD=0: host build)
   bool gpu_build_on = true;
@@ -277,8 +276,8 @@ struct ps_engine {
   uint32_t* pairs_pinned = nullptr;  // pinned staging of the parent deltas
   size_t pairs_pinned_cap = 0;       // (u32 words)
   std::vector<size_t> pair_off;
-  psamd::DevBuf d_tpar, d_orph, d_anc0, d_anc1, d_dep0, d_dep1, d_keys0, d_skeys, d_local, d_deg, d_first, d_lvl,
-      d_gstat, d_cub, d_pairs, d_live, d_roots, d_cnt, d_fidx, d_childoff, d_lbstat, d_sigctr;
+  psamd::DevBuf d_tpar, d_orph, d_local, d_first, d_lvl,
+      d_gstat, d_cub, d_pairs, d_live, d_roots, d_cnt, d_fidx, d_childoff, d_lbstat, d_sigctr, d_kids, d_big, d_tb;
   std::chrono::steady_clock::time_point t_run0;
   // k_flood: a single-rank level window's leading rounds in
   // one persistent launch; PSAMD_FLOOD=0 runs per-round launches instead

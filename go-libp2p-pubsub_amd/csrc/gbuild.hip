@@ -1,6 +1,6 @@
 // gbuild.hip -- gfx950 kernels of the GPU node-space rebuild (gbuild.hpp).
 // Integer work over peer-indexed arrays: coalesced, HBM/latency-bound; the
-// sort and the scan are hipcub's (rocPRIM) device primitives.
+// one scan over the peers (the child lists' offsets) is hipcub's.
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -15,7 +15,6 @@ namespace {
 constexpr uint32_t kB = 256;
 constexpr uint32_t kNoneP = 0xFFFFFFFFu;
 
-constexpr uint32_t kStatBlocks = 1024;  // grid of the reducing kernels
 
 uint32_t blocks(uint64_t n) { return static_cast<uint32_t>(std::max<uint64_t>(1, (n + kB - 1) / kB)); }
 
@@ -26,95 +25,6 @@ __global__ __launch_bounds__(kB) void k_scatter_pairs(const uint32_t* __restrict
   const uint32_t p = pairs[2 * i], v = pairs[2 * i + 1];
   par[p] = v >= kOrphanCode ? kNoneP : v;
   orph[p] = v == kOrphanCode;
-}
-
-// anc = upstream (root: itself), dep = 1 (root: 0)
-__global__ __launch_bounds__(kB) void k_depth_init(const uint32_t* __restrict__ par, uint32_t n,
-                                                   uint32_t root, uint32_t* __restrict__ anc,
-                                                   uint32_t* __restrict__ dep) {
-  const uint32_t p = blockIdx.x * kB + threadIdx.x;
-  if (p >= n) return;
-  anc[p] = p == root ? root : par[p];
-  dep[p] = p == root ? 0u : 1u;
-}
-
-// One pointer-jumping step: dep += dep[anc], anc = anc[anc]; the root is a
-// fixed point, kNone (not subscribed / cut) absorbs.
-__global__ __launch_bounds__(kB) void k_depth_jump(const uint32_t* __restrict__ ai,
-                                                   const uint32_t* __restrict__ di,
-                                                   uint32_t* __restrict__ ao, uint32_t* __restrict__ dout,
-                                                   uint32_t n, uint32_t root) {
-  const uint32_t p = blockIdx.x * kB + threadIdx.x;
-  if (p >= n) return;
-  const uint32_t a = ai[p];
-  if (a == kNoneP || a == root) {
-    ao[p] = a;
-    dout[p] = di[p];
-    return;
-  }
-  ao[p] = ai[a];
-  dout[p] = di[p] + di[a];
-}
-
-// Block-wide max / sum through LDS: one global atomic per block (thousands of
-// same-address atomics, one per wave, serialise in one L2 channel).
-template <bool kMax>
-__device__ uint32_t block_reduce(uint32_t v, uint32_t* lds) {
-#pragma unroll
-  for (int s = 32; s >= 1; s >>= 1) {
-    const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), s, 64));
-    v = kMax ? max(v, o) : v + o;
-  }
-  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
-  __syncthreads();
-  v = lds[0];
-  for (uint32_t w = 1; w < kB / 64; ++w) v = kMax ? max(v, lds[w]) : v + lds[w];
-  __syncthreads();
-  return v;
-}
-
-// Keys of the reachable peers (grid-stride): kf.make(depth, parent, peer),
-// ~0 otherwise.  gstat[0] += reachable, gstat[1] = max depth,
-// gstat[3] += peers whose ancestor is neither the root nor cut (the jump
-// steps did not cover their depth: the caller repeats with more steps).
-__global__ __launch_bounds__(kB) void k_depth_keys(const uint32_t* __restrict__ anc,
-                                                   const uint32_t* __restrict__ dep,
-                                                   const uint32_t* __restrict__ par, uint32_t n,
-                                                   uint32_t root, uint64_t* __restrict__ keys,
-                                                   uint32_t* __restrict__ gstat, BuildKey kf) {
-  __shared__ uint32_t lds[kB / 64];
-  uint32_t cnt = 0, far = 0, m = 0;
-  for (uint32_t p = blockIdx.x * kB + threadIdx.x; p < n; p += gridDim.x * kB) {
-    const uint32_t a = anc[p];
-    uint64_t k = ~0ull;
-    if (a == root) {
-      const uint32_t d = dep[p];
-      const uint32_t pp = p == root ? 0u : par[p];
-      k = kf.make(min(d, kBuildMaxDepth), pp, p);
-      ++cnt;
-      m = max(m, d);
-    } else if (a != kNoneP) {
-      ++far;
-    }
-    keys[p] = k;
-  }
-  cnt = block_reduce<false>(cnt, lds);
-  m = block_reduce<true>(m, lds);
-  far = block_reduce<false>(far, lds);
-  if (threadIdx.x == 0) {
-    if (cnt) atomicAdd(gstat + 0, cnt);
-    if (m) atomicMax(gstat + 1, m);
-    if (far) atomicAdd(gstat + 3, far);
-  }
-}
-
-__global__ __launch_bounds__(kB) void k_fill_col(const uint32_t* __restrict__ row_ptr,
-                                                 const uint32_t* __restrict__ first, uint32_t n_nodes,
-                                                 uint32_t* __restrict__ col) {
-  const uint32_t u = blockIdx.x * kB + threadIdx.x;
-  if (u >= n_nodes) return;
-  const uint32_t b = row_ptr[u], e = row_ptr[u + 1];
-  for (uint32_t k = b; k < e; ++k) col[k] = first[u] + (k - b);
 }
 
 __global__ __launch_bounds__(kB) void k_node_flags(const uint32_t* __restrict__ node_peer,
@@ -132,295 +42,6 @@ __global__ __launch_bounds__(kB) void k_root_flags(const uint32_t* __restrict__ 
                                                    uint8_t* __restrict__ flags) {
   const uint32_t i = blockIdx.x * kB + threadIdx.x;
   if (i < n) flags[roots[i]] |= kNodeLive;  // roots forward (they are not recipients)
-}
-
-// Level starts of a topic's (depth, parent, peer)-sorted keys (first R valid).
-__global__ __launch_bounds__(kB) void k_level_starts(const uint64_t* __restrict__ keys, uint32_t R,
-                                                     uint32_t* __restrict__ lvl_start, BuildKey kf) {
-  const uint32_t u = blockIdx.x * kB + threadIdx.x;
-  if (u >= R) return;
-  const uint32_t d = kf.depth(keys[u]);
-  if (u == 0 || kf.depth(keys[u - 1]) != d) lvl_start[d] = u;
-}
-
-// Internal nodes per level and the largest fan-out of a topic placed at
-// [nbase, nbase + R) with level starts lvl_start[0..depth] (topic-relative):
-// a per-block LDS histogram over the levels, flushed with one atomic per
-// non-empty bin (a tree has a few dozen levels: per-node global atomics on
-// them serialise).
-__global__ __launch_bounds__(kB) void k_level_internal(const uint32_t* __restrict__ deg, uint32_t nbase,
-                                                       uint32_t R, const uint32_t* __restrict__ lvl_start,
-                                                       uint32_t depth, uint32_t* __restrict__ lvl_internal,
-                                                       uint32_t* __restrict__ max_deg) {
-  __shared__ uint32_t hist[kBuildMaxDepth + 1];
-  __shared__ uint32_t starts[kBuildMaxDepth + 2];
-  __shared__ uint32_t lds[kB / 64];
-  for (uint32_t d = threadIdx.x; d <= kBuildMaxDepth; d += kB) hist[d] = 0;
-  for (uint32_t d = threadIdx.x; d <= depth; d += kB) starts[d] = lvl_start[d];
-  __syncthreads();
-  uint32_t m = 0;
-  for (uint32_t u = blockIdx.x * kB + threadIdx.x; u < R; u += gridDim.x * kB) {
-    const uint32_t dg = deg[nbase + u];
-    if (!dg) continue;
-    m = max(m, dg);
-    uint32_t lo = 0, hi = depth;  // last level whose start <= u
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1) / 2;
-      if (starts[mid] <= u)
-        lo = mid;
-      else
-        hi = mid - 1;
-    }
-    atomicAdd(hist + lo, 1u);
-  }
-  m = block_reduce<true>(m, lds);  // includes the barrier after the histogram
-  for (uint32_t d = threadIdx.x; d <= depth; d += kB)
-    if (hist[d]) atomicAdd(lvl_internal + d, hist[d]);
-  if (threadIdx.x == 0 && m) atomicMax(max_deg, m);
-}
-
-// Fan-out and first child of every parent peer in one topic's (depth, parent,
-// peer)-sorted keys (first R valid; keys[0] is the root): cnt[parent] += 1,
-// firstidx[parent] = min index.  Siblings are contiguous and sorted by peer.
-__global__ __launch_bounds__(kB) void k_child_stats(const uint64_t* __restrict__ keys, uint32_t R,
-                                                    uint32_t* __restrict__ cnt,
-                                                    uint32_t* __restrict__ firstidx, BuildKey kf) {
-  const uint32_t i = blockIdx.x * kB + threadIdx.x;
-  if (i == 0 || i >= R) return;
-  const uint32_t pp = kf.parent(keys[i]);
-  atomicAdd(cnt + pp, 1u);
-  atomicMin(firstidx + pp, i);
-}
-
-__global__ void k_place_root(const uint64_t* __restrict__ keys, uint32_t nbase, uint16_t topic,
-                             const uint32_t* __restrict__ cnt, uint32_t* __restrict__ node_peer,
-                             uint16_t* __restrict__ node_topic, uint32_t* __restrict__ local,
-                             uint32_t* __restrict__ node_parent, uint32_t* __restrict__ deg, BuildKey kf) {
-  if (threadIdx.x) return;
-  const uint32_t peer = kf.peer(keys[0]);
-  node_peer[nbase] = peer;
-  node_topic[nbase] = topic;
-  local[peer] = nbase;
-  node_parent[nbase] = kNoneP;
-  deg[nbase] = cnt[peer];
-}
-
-// BFS placement of level d (keys [lo, hi), nodes nbase + [lo, hi)) without a
-// sort: the children of parent node u form one group at nbase + lo +
-// childoff[u - prev0] (exclusive scan of the parents' fan-out, in parent node
-// order), each child at its rank among its siblings (index - first index).
-__global__ __launch_bounds__(kB) void k_place_level(
-    const uint64_t* __restrict__ keys, uint32_t lo, uint32_t hi, uint32_t nbase, uint32_t prev0,
-    const uint32_t* __restrict__ childoff, const uint32_t* __restrict__ cnt,
-    const uint32_t* __restrict__ firstidx, uint16_t topic, uint32_t* __restrict__ node_peer,
-    uint16_t* __restrict__ node_topic, uint32_t* __restrict__ local, uint32_t* __restrict__ node_parent,
-    uint32_t* __restrict__ deg, uint32_t* __restrict__ first, BuildKey kf) {
-  const uint32_t i = lo + blockIdx.x * kB + threadIdx.x;
-  if (i >= hi) return;
-  const uint64_t k = keys[i];
-  const uint32_t peer = kf.peer(k);
-  const uint32_t pp = kf.parent(k);
-  const uint32_t pu = local[pp];
-  const uint32_t f = firstidx[pp];
-  const uint32_t node = nbase + lo + childoff[pu - prev0] + (i - f);
-  node_peer[node] = peer;
-  node_topic[node] = topic;
-  local[peer] = node;
-  node_parent[node] = pu;
-  deg[node] = cnt[peer];
-  if (i == f) first[pu] = node;
-}
-
-// BFS placement of level d in ONE launch, parent-centric: tile b (one
-// block) owns the parent nodes pbase + [256 b, 256 b + 256) of level d - 1,
-// scans their fan-out in the block and takes its prefix from the tiles before
-// it by a decoupled look-back (status[b]: kLbAgg | the tile's sum once known,
-// kLbIncl | the inclusive prefix once its own prefix is; tiles start in
-// order, so a tile only ever waits on tiles already running).  The children
-// of the tile's parents are then one contiguous range: child k of the tile's
-// flattened child list is node cbase + prefix + k, its parent the tile's
-// parent whose inclusive sum first exceeds k, its peer the key at
-// firstidx[parent peer] + its sibling rank.  (The previous form: a device scan
-// of the parents' fan-out -- two launches -- then a child-parallel placement;
-// three launches per level.)  A look-back that spins past kLbSpin polls
-// flags the build as failed (*err), and the caller builds on the host.
-constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbFlags = 3ull << 62;
-constexpr uint32_t kLbSpin = 1u << 24;
-
-__global__ __launch_bounds__(kB) void k_place_level_lb(
-    const uint64_t* __restrict__ keys, uint32_t np, uint32_t pbase, uint32_t cbase,
-    const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ firstidx, uint16_t topic,
-    uint32_t* __restrict__ node_peer, uint16_t* __restrict__ node_topic, uint32_t* __restrict__ local,
-    uint32_t* __restrict__ node_parent, uint32_t* __restrict__ deg, uint32_t* __restrict__ first,
-    uint64_t* __restrict__ status, uint32_t* __restrict__ err, BuildKey kf) {
-  __shared__ uint32_t incl_s[kB];
-  __shared__ uint32_t peer_s[kB];
-  __shared__ uint32_t wsum[kB / 64];
-  __shared__ uint32_t prefix_s;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const uint32_t tile = blockIdx.x;
-  const uint32_t j0 = tile * kB + tid;
-  const uint32_t u = pbase + j0;
-  const bool valid = j0 < np;
-  const uint32_t dg = valid ? deg[u] : 0u;
-  peer_s[tid] = valid ? node_peer[u] : 0u;
-  // block inclusive scan of the fan-out
-  uint32_t inc = dg;
-#pragma unroll
-  for (int sh = 1; sh < 64; sh <<= 1) {
-    const uint32_t o = static_cast<uint32_t>(__shfl_up(static_cast<int>(inc), sh, 64));
-    if (lane >= static_cast<uint32_t>(sh)) inc += o;
-  }
-  if (lane == 63) wsum[w] = inc;
-  __syncthreads();
-  uint32_t base = 0, agg = 0;
-#pragma unroll
-  for (uint32_t q = 0; q < kB / 64; ++q) {
-    base += q < w ? wsum[q] : 0u;
-    agg += wsum[q];
-  }
-  incl_s[tid] = base + inc;
-  if (w == 0) {
-    // the look-back, one wave: 64 predecessors per step (lane i reads tile
-    // j - i), summed up to the nearest inclusive one
-    uint32_t prefix = 0;
-    if (tile == 0) {
-      if (lane == 0) __hip_atomic_store(status, kLbIncl | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      if (lane == 0) __hip_atomic_store(status + tile, kLbAgg | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      uint32_t spins = 0;
-      int32_t j = static_cast<int32_t>(tile) - 1;
-      for (;;) {
-        const int32_t idx = j - static_cast<int32_t>(lane);
-        const uint64_t v = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)
-                                    : kLbIncl;  // (before tile 0: an inclusive zero)
-        if (__any((v & kLbFlags) == 0)) {  // a predecessor has not published yet
-          if (++spins > kLbSpin) {
-            if (lane == 0) atomicOr(err, 1u);
-            break;
-          }
-          continue;
-        }
-        const uint64_t incl_mask = __ballot((v & kLbFlags) == kLbIncl);
-        const uint32_t stop = incl_mask ? static_cast<uint32_t>(__builtin_ctzll(incl_mask)) : 63u;
-        uint32_t part = lane <= stop ? static_cast<uint32_t>(v) : 0u;
-#pragma unroll
-        for (int sh = 32; sh >= 1; sh >>= 1) part += static_cast<uint32_t>(__shfl_xor(static_cast<int>(part), sh, 64));
-        prefix += part;
-        if (incl_mask) break;
-        j -= 64;
-      }
-      if (lane == 0)
-        __hip_atomic_store(status + tile, kLbIncl | (prefix + agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (lane == 0) prefix_s = prefix;
-  }
-  __syncthreads();
-  const uint32_t prefix = prefix_s;
-  // the tile's children, flattened: child k's parent is the first q with
-  // incl_s[q] > k (binary search over the tile's 256 parents)
-  for (uint32_t k = tid; k < agg; k += kB) {
-    uint32_t lo = 0, hi = kB - 1;
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (incl_s[mid] > k)
-        hi = mid;
-      else
-        lo = mid + 1;
-    }
-    const uint32_t q = lo;
-    const uint32_t rank = k - (q ? incl_s[q - 1] : 0u);  // (k minus the parent's exclusive sum)
-    const uint32_t pu = pbase + tile * kB + q;
-    const uint32_t pp = peer_s[q];
-    const uint32_t peer = kf.peer(keys[firstidx[pp] + rank]);
-    const uint32_t node = cbase + prefix + k;
-    node_peer[node] = peer;
-    node_topic[node] = topic;
-    local[peer] = node;
-    node_parent[node] = pu;
-    deg[node] = cnt[peer];
-    if (rank == 0) first[pu] = node;
-  }
-}
-
-// The small top levels of one topic in ONE block (one launch for what would be
-// 3 launches per level): root, then each level 1 .. d_end - 1 (at most
-// kBuildSmallLevel nodes and parents) with the parents' fan-out scanned in
-// LDS.  Nodes placed by other waves of the block are read back through L1-
-// bypassing loads after the barrier.
-constexpr uint32_t kSmallB = 1024;
-constexpr uint32_t kSmallPer = kBuildSmallLevel / kSmallB;
-
-__device__ __forceinline__ uint32_t load_agent(const uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__global__ __launch_bounds__(kSmallB) void k_place_small(
-    const uint64_t* __restrict__ keys, const uint32_t* __restrict__ lvl, uint32_t d_end, uint32_t depth, uint32_t n_nodes,
-    uint32_t nbase, uint16_t topic, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ firstidx,
-    uint32_t* __restrict__ node_peer, uint16_t* __restrict__ node_topic, uint32_t* local,
-    uint32_t* __restrict__ node_parent, uint32_t* deg, uint32_t* __restrict__ first, BuildKey kf) {
-  __shared__ uint32_t off[kBuildSmallLevel];
-  __shared__ uint32_t wsum[kSmallB / 64];
-  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (tid == 0) {
-    const uint32_t peer = kf.peer(keys[0]);
-    node_peer[nbase] = peer;
-    node_topic[nbase] = topic;
-    local[peer] = nbase;
-    node_parent[nbase] = kNoneP;
-    deg[nbase] = cnt[peer];
-  }
-  __threadfence_block();
-  __syncthreads();
-  for (uint32_t d = 1; d < d_end; ++d) {
-    const uint32_t plo = lvl[d - 1], lo = lvl[d];
-    const uint32_t hi = d == depth ? n_nodes : lvl[d + 1];
-    const uint32_t np = lo - plo;
-    // exclusive scan of the parents' fan-out: kSmallPer per thread, then waves
-    uint32_t v[kSmallPer];
-    uint32_t run = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kSmallPer; ++k) {
-      const uint32_t j = tid * kSmallPer + k;
-      v[k] = j < np ? load_agent(deg + nbase + plo + j) : 0u;
-      run += v[k];
-    }
-    uint32_t incl = run;
-#pragma unroll
-    for (int sh = 1; sh < 64; sh <<= 1) {
-      const uint32_t o = static_cast<uint32_t>(__shfl_up(static_cast<int>(incl), sh, 64));
-      if (lane >= static_cast<uint32_t>(sh)) incl += o;
-    }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    uint32_t base = 0;
-    for (uint32_t q = 0; q < w; ++q) base += wsum[q];
-    uint32_t acc = base + incl - run;
-#pragma unroll
-    for (uint32_t k = 0; k < kSmallPer; ++k) {
-      const uint32_t j = tid * kSmallPer + k;
-      if (j < np) off[j] = acc;
-      acc += v[k];
-    }
-    __syncthreads();
-    for (uint32_t i = lo + tid; i < hi; i += kSmallB) {
-      const uint64_t kk = keys[i];
-      const uint32_t peer = kf.peer(kk);
-      const uint32_t pp = kf.parent(kk);
-      const uint32_t pu = load_agent(local + pp);
-      const uint32_t f = firstidx[pp];
-      const uint32_t node = nbase + lo + off[pu - nbase - plo] + (i - f);
-      node_peer[node] = peer;
-      node_topic[node] = topic;
-      local[peer] = node;
-      node_parent[node] = pu;
-      deg[node] = cnt[peer];
-      if (i == f) first[pu] = node;
-    }
-    __threadfence_block();
-    __syncthreads();
-  }
 }
 
 // out[i] = 1 iff peers[i] holds a node of the topic placed at [nbase, nbase +
@@ -455,7 +76,380 @@ __global__ __launch_bounds__(kB) void k_reach_query(const uint32_t* __restrict__
   out[i] = r;
 }
 
+// ---- by-parent CSR BFS rebuild -----------
+
+// cnt[v] += 1 for every peer p whose upstream v is a peer (histogram of the
+// parent array)
+__global__ __launch_bounds__(kB) void k_kid_count(const uint32_t* __restrict__ par, uint32_t n,
+                                                  uint32_t* __restrict__ cnt) {
+  const uint32_t p = blockIdx.x * kB + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t v = par[p];
+  if (v < n) atomicAdd(cnt + v, 1u);
+}
+
+// kids[koff[v] + i] = the i-th arriving child of v (order fixed below)
+__global__ __launch_bounds__(kB) void k_kid_scatter(const uint32_t* __restrict__ par, uint32_t n,
+                                                    const uint32_t* __restrict__ koff, uint32_t* __restrict__ fill,
+                                                    uint32_t* __restrict__ kids) {
+  const uint32_t p = blockIdx.x * kB + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t v = par[p];
+  if (v < n) kids[koff[v] + atomicAdd(fill + v, 1u)] = p;
+}
+
+// Siblings in peer order (a deterministic BFS numbering): a parent's list of
+// at most kKidSmall children sorted by its own thread; longer lists are
+// queued for k_kid_sort_big.
+constexpr uint32_t kKidSmall = 32;
+constexpr uint32_t kKidBig = 4096;  // the LDS sort's capacity (longer lists keep their arrival order)
+__global__ __launch_bounds__(kB) void k_kid_sort(const uint32_t* __restrict__ koff, const uint32_t* __restrict__ cnt,
+                                                 uint32_t n, uint32_t* __restrict__ kids, uint32_t* __restrict__ big,
+                                                 uint32_t* __restrict__ n_big) {
+  const uint32_t v = blockIdx.x * kB + threadIdx.x;
+  if (v >= n) return;
+  const uint32_t c = cnt[v];
+  if (c < 2) return;
+  if (c > kKidSmall) {
+    big[atomicAdd(n_big, 1u)] = v;
+    return;
+  }
+  uint32_t* k = kids + koff[v];
+  for (uint32_t i = 1; i < c; ++i) {
+    const uint32_t x = k[i];
+    uint32_t j = i;
+    for (; j > 0 && k[j - 1] > x; --j) k[j] = k[j - 1];
+    k[j] = x;
+  }
+}
+
+// One block per queued long list (grid-stride): a bitonic sort in LDS
+__global__ __launch_bounds__(kB) void k_kid_sort_big(const uint32_t* __restrict__ koff,
+                                                     const uint32_t* __restrict__ cnt, uint32_t* __restrict__ kids,
+                                                     const uint32_t* __restrict__ big,
+                                                     const uint32_t* __restrict__ n_big) {
+  __shared__ uint32_t x[kKidBig];
+  const uint32_t nb = *n_big;
+  for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+    const uint32_t v = big[b];
+    const uint32_t c = cnt[v];
+    if (c > kKidBig) continue;
+    uint32_t* k = kids + koff[v];
+    uint32_t m = 1;
+    while (m < c) m <<= 1;
+    for (uint32_t i = threadIdx.x; i < m; i += kB) x[i] = i < c ? k[i] : 0xFFFFFFFFu;
+    __syncthreads();
+    for (uint32_t size = 2; size <= m; size <<= 1)
+      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+        for (uint32_t i = threadIdx.x; i < m; i += kB) {
+          const uint32_t j = i ^ stride;
+          if (j > i) {
+            const bool up = (i & size) == 0;
+            const uint32_t a = x[i], bb = x[j];
+            if ((a > bb) == up) {
+              x[i] = bb;
+              x[j] = a;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    for (uint32_t i = threadIdx.x; i < c; i += kB) k[i] = x[i];
+    __syncthreads();
+  }
+}
+
+// The placement of a child node c (topic-relative index cr >= 1, level d)
+// of parent node pu: node arrays, the peer -> node map, its flags (live;
+// internal when the peer has children) and its CSR column (edge cr - 1 of
+// the topic: BFS numbering makes col the identity shifted by one).
+__device__ __forceinline__ bool place_child(const PlaceArgs& P, uint32_t nbase, uint32_t ebase, uint32_t cr,
+                                            uint32_t pu, uint32_t peer) {
+  const uint32_t c = nbase + cr;
+  P.node_peer[c] = peer;
+  P.node_topic[c] = P.topic;
+  P.local[peer] = c;
+  P.node_parent[c] = pu;
+  P.col[ebase + cr - 1] = c;
+  const bool internal = P.cnt[peer] != 0;
+  P.flags[c] = (P.live[peer] ? kNodeLive : 0) | (internal ? kNodeInternal : 0);
+  return internal;
+}
+
+// A parent node's CSR row and first child (topic-relative child start cs)
+__device__ __forceinline__ void place_row(const PlaceArgs& P, uint32_t nbase, uint32_t ebase, uint32_t u,
+                                          uint32_t cs) {
+  P.row_ptr[u] = ebase + cs - 1;
+  P.first[u] = nbase + cs;
+}
+
+// The end of a level pass: the next level's start, the topic's node and edge
+// end (the next active topic's bases, and the CSR's closing entry)
+__device__ __forceinline__ void place_close(const PlaceArgs& P, uint32_t nbase, uint32_t ebase, uint32_t d,
+                                            uint32_t next_lo) {
+  P.lvl[d + 1] = next_lo;
+  P.tb[2 * P.a + 2] = nbase + next_lo;
+  P.tb[2 * P.a + 3] = ebase + next_lo - 1;
+  P.row_ptr[nbase + next_lo] = ebase + next_lo - 1;
+  if (next_lo > P.lvl[d]) P.gst[kGstDepth] = d;
+  __threadfence();
+  P.gst[kGstDone] = d;
+}
+
+// The root and the small top levels of one topic in ONE block: each level d
+// = 1 .. d_limit - 1 whose parents number at most kBuildSmallLevel, from the
+// parents' fan-out scanned in LDS, children flattened in parent order (a
+// binary search finds each child's parent).  Stops at the first larger level
+// (the look-back launches take over) or when the tree ends.
+constexpr uint32_t kSmallB = 1024;
+constexpr uint32_t kSmallPer = kBuildSmallLevel / kSmallB;
+
+__device__ __forceinline__ uint32_t load_agent(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kSmallB) void k_place_top(PlaceArgs P, uint32_t d_limit) {
+  __shared__ uint32_t off[kBuildSmallLevel + 1];
+  __shared__ uint32_t wsum[kSmallB / 64];
+  __shared__ uint32_t red[kSmallB / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t nbase = P.tb[2 * P.a], ebase = P.tb[2 * P.a + 1];
+  if (tid == 0) {
+    const uint32_t r = P.root;
+    P.node_peer[nbase] = r;
+    P.node_topic[nbase] = P.topic;
+    P.local[r] = nbase;
+    P.node_parent[nbase] = kNoneP;
+    const bool internal = P.cnt[r] != 0;
+    P.flags[nbase] = kNodeLive | (internal ? kNodeInternal : 0);  // roots forward (they are not recipients)
+    P.lvl[0] = 0;
+    P.lvl[1] = 1;
+    P.lvl[256] = internal ? 1u : 0u;
+    P.gst[kGstDepth] = 0;
+    P.gst[kGstMaxDeg] = P.cnt[r];
+    P.gst[kGstDone] = 0;
+    P.tb[2 * P.a + 2] = nbase + 1;
+    P.tb[2 * P.a + 3] = ebase;
+    P.row_ptr[nbase + 1] = ebase;
+  }
+  __threadfence_block();
+  __syncthreads();
+  uint32_t plo = 0, lo = 1, mdeg = 0;
+  for (uint32_t d = 1; d < d_limit; ++d) {
+    const uint32_t np = lo - plo;
+    if (np == 0 || np > kBuildSmallLevel) break;
+    // exclusive scan of the parents' fan-out: kSmallPer per thread, then waves
+    uint32_t v[kSmallPer];
+    uint32_t run = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPer; ++k) {
+      const uint32_t j = tid * kSmallPer + k;
+      v[k] = j < np ? P.cnt[load_agent(P.node_peer + nbase + plo + j)] : 0u;
+      run += v[k];
+    }
+    uint32_t incl = run;
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) {
+      const uint32_t o = static_cast<uint32_t>(__shfl_up(static_cast<int>(incl), sh, 64));
+      if (lane >= static_cast<uint32_t>(sh)) incl += o;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t base = 0, total = 0;
+    for (uint32_t q = 0; q < kSmallB / 64; ++q) {
+      base += q < w ? wsum[q] : 0u;
+      total += wsum[q];
+    }
+    uint32_t acc = base + incl - run;
+#pragma unroll
+    for (uint32_t k = 0; k < kSmallPer; ++k) {
+      const uint32_t j = tid * kSmallPer + k;
+      if (j < np) {
+        off[j] = acc;  // exclusive
+        place_row(P, nbase, ebase, nbase + plo + j, lo + acc);
+        mdeg = max(mdeg, v[k]);
+      }
+      acc += v[k];
+    }
+    if (tid == 0) off[np] = total;
+    __syncthreads();
+    uint32_t n_int = 0;
+    for (uint32_t k = tid; k < total; k += kSmallB) {
+      uint32_t a = 0, b = np - 1;  // the last parent whose exclusive offset <= k
+      while (a < b) {
+        const uint32_t mid = (a + b + 1) >> 1;
+        if (off[mid] <= k)
+          a = mid;
+        else
+          b = mid - 1;
+      }
+      const uint32_t pp = load_agent(P.node_peer + nbase + plo + a);
+      const uint32_t peer = P.kids[P.koff[pp] + (k - off[a])];
+      n_int += place_child(P, nbase, ebase, lo + k, nbase + plo + a, peer) ? 1u : 0u;
+    }
+    n_int = __reduce_add_sync(~0ull, n_int);
+    if (lane == 0) red[w] = n_int;
+    __threadfence_block();
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t t = 0;
+      for (uint32_t q = 0; q < kSmallB / 64; ++q) t += red[q];
+      P.lvl[256 + d] = t;
+      place_close(P, nbase, ebase, d, lo + total);
+    }
+    __syncthreads();
+    plo = lo;
+    lo += total;
+  }
+  mdeg = __reduce_max_sync(~0ull, mdeg);
+  if (lane == 0 && mdeg) atomicMax(P.gst + kGstMaxDeg, mdeg);
+}
+
+// Level d (the children of level d - 1's nodes) in ONE launch, parent-centric
+// (tile b = one block owns the parents 256 b .. 256 b + 255 of the level,
+// scans their fan-out and takes its prefix from the tiles before it by a
+// decoupled look-back -- status[b], zeroed per launch -- so the children of
+// the tile's parents are one contiguous node range).  The level's size comes
+// from the level table the previous launch closed; the grid is the host's
+// estimate: a level with more tiles than blocks flags kBuildErrGrid and the
+// build is redone with full grids.  A level the top kernel already placed is
+// skipped; a launch whose parent level is not placed flags kBuildErrOrder.
+constexpr uint64_t kLbAgg = 1ull << 62, kLbIncl = 2ull << 62, kLbFlags = 3ull << 62;
+constexpr uint32_t kLbSpin = 1u << 24;
+
+__global__ __launch_bounds__(kB) void k_place_lb(PlaceArgs P, uint32_t d, uint64_t* __restrict__ status) {
+  __shared__ uint32_t incl_s[kB];
+  __shared__ uint32_t peer_s[kB];
+  __shared__ uint32_t wsum[kB / 64];
+  __shared__ uint32_t prefix_s;
+  const uint32_t done = P.gst[kGstDone];
+  if (done >= d) return;  // (placed by the top kernel)
+  if (done + 1 != d) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(P.err, kBuildErrOrder);
+    return;
+  }
+  const uint32_t plo = P.lvl[d - 1], lo = P.lvl[d], np = lo - plo;
+  const uint32_t nbase = P.tb[2 * P.a], ebase = P.tb[2 * P.a + 1];
+  if (np == 0) {  // the tree ended above: close the level
+    if (blockIdx.x == 0 && threadIdx.x == 0) place_close(P, nbase, ebase, d, lo);
+    return;
+  }
+  const uint32_t ntiles = lb_tiles(np);
+  if (ntiles > gridDim.x) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(P.err, kBuildErrGrid);
+    return;
+  }
+  const uint32_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint32_t j0 = tile * kB + tid;
+  const uint32_t u = nbase + plo + j0;
+  const bool valid = j0 < np;
+  const uint32_t pp = valid ? P.node_peer[u] : 0u;
+  const uint32_t dg = valid ? P.cnt[pp] : 0u;
+  peer_s[tid] = pp;
+  uint32_t inc = dg;
+#pragma unroll
+  for (int sh = 1; sh < 64; sh <<= 1) {
+    const uint32_t o = static_cast<uint32_t>(__shfl_up(static_cast<int>(inc), sh, 64));
+    if (lane >= static_cast<uint32_t>(sh)) inc += o;
+  }
+  if (lane == 63) wsum[w] = inc;
+  __syncthreads();
+  uint32_t base = 0, agg = 0;
+#pragma unroll
+  for (uint32_t q = 0; q < kB / 64; ++q) {
+    base += q < w ? wsum[q] : 0u;
+    agg += wsum[q];
+  }
+  incl_s[tid] = base + inc;
+  if (w == 0) {
+    uint32_t prefix = 0;
+    if (tile == 0) {
+      if (lane == 0) __hip_atomic_store(status, kLbIncl | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      if (lane == 0) __hip_atomic_store(status + tile, kLbAgg | agg, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      uint32_t spins = 0;
+      int32_t j = static_cast<int32_t>(tile) - 1;
+      for (;;) {
+        const int32_t idx = j - static_cast<int32_t>(lane);
+        const uint64_t v = idx >= 0 ? __hip_atomic_load(status + idx, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)
+                                    : kLbIncl;
+        if (__any((v & kLbFlags) == 0)) {
+          if (++spins > kLbSpin) {
+            if (lane == 0) atomicOr(P.err, kBuildErrStall);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        const uint64_t incl_mask = __ballot((v & kLbFlags) == kLbIncl);
+        const uint32_t stop = incl_mask ? static_cast<uint32_t>(__builtin_ctzll(incl_mask)) : 63u;
+        uint32_t part = lane <= stop ? static_cast<uint32_t>(v) : 0u;
+#pragma unroll
+        for (int sh = 32; sh >= 1; sh >>= 1) part += static_cast<uint32_t>(__shfl_xor(static_cast<int>(part), sh, 64));
+        prefix += part;
+        if (incl_mask) break;
+        j -= 64;
+      }
+      if (lane == 0)
+        __hip_atomic_store(status + tile, kLbIncl | (prefix + agg), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) prefix_s = prefix;
+  }
+  __syncthreads();
+  const uint32_t prefix = prefix_s;
+  if (valid) place_row(P, nbase, ebase, u, lo + prefix + incl_s[tid] - dg);
+  uint32_t n_int = 0;
+  for (uint32_t k = tid; k < agg; k += kB) {
+    uint32_t a = 0, b = kB - 1;  // the first parent whose inclusive sum exceeds k
+    while (a < b) {
+      const uint32_t mid = (a + b) >> 1;
+      if (incl_s[mid] > k)
+        b = mid;
+      else
+        a = mid + 1;
+    }
+    const uint32_t rank = k - (a ? incl_s[a - 1] : 0u);
+    const uint32_t peer = P.kids[P.koff[peer_s[a]] + rank];
+    n_int += place_child(P, nbase, ebase, lo + prefix + k, nbase + plo + tile * kB + a, peer) ? 1u : 0u;
+  }
+  n_int = __reduce_add_sync(~0ull, n_int);
+  uint32_t mdeg = __reduce_max_sync(~0ull, dg);
+  if (lane == 0) {
+    if (n_int) atomicAdd(P.lvl + 256 + d, n_int);
+    if (mdeg) atomicMax(P.gst + kGstMaxDeg, mdeg);
+  }
+  if (tile == ntiles - 1 && tid == 0) place_close(P, nbase, ebase, d, lo + prefix + agg);
+}
+
 }  // namespace
+
+
+hipError_t build_kids(const uint32_t* par, uint32_t n, uint32_t* cnt, uint32_t* koff, uint32_t* fill, uint32_t* kids,
+                      uint32_t* big, uint32_t* n_big, void* temp, size_t temp_bytes, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(cnt, 0, (static_cast<size_t>(n) + 1) * 4, s);
+  if (e == hipSuccess) e = hipMemsetAsync(fill, 0, static_cast<size_t>(n) * 4, s);
+  if (e == hipSuccess) e = hipMemsetAsync(n_big, 0, 4, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_kid_count, dim3(blocks(n)), dim3(kB), 0, s, par, n, cnt);
+  e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, cnt, koff, n + 1, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_kid_scatter, dim3(blocks(n)), dim3(kB), 0, s, par, n, koff, fill, kids);
+  hipLaunchKernelGGL(k_kid_sort, dim3(blocks(n)), dim3(kB), 0, s, koff, cnt, n, kids, big, n_big);
+  hipLaunchKernelGGL(k_kid_sort_big, dim3(64), dim3(kB), 0, s, koff, cnt, kids, big, n_big);
+  return hipGetLastError();
+}
+
+hipError_t launch_place_top(const PlaceArgs& P, uint32_t d_limit, hipStream_t s) {
+  hipLaunchKernelGGL(k_place_top, dim3(1), dim3(kSmallB), 0, s, P, d_limit);
+  return hipGetLastError();
+}
+
+hipError_t launch_place_lb(const PlaceArgs& P, uint32_t d, uint32_t grid, uint64_t* status, hipStream_t s) {
+  hipLaunchKernelGGL(k_place_lb, dim3(std::max<uint32_t>(grid, 1)), dim3(kB), 0, s, P, d, status);
+  return hipGetLastError();
+}
 
 hipError_t launch_reach_query(const uint32_t* peers, uint32_t n, uint32_t n_peers, const uint32_t* local,
                               const uint32_t* node_peer, uint32_t nbase, uint32_t n_nodes, const uint32_t* par,
@@ -466,106 +460,15 @@ hipError_t launch_reach_query(const uint32_t* peers, uint32_t n, uint32_t n_peer
   return hipGetLastError();
 }
 
-hipError_t launch_child_stats(const uint64_t* keys, uint32_t R, uint32_t* cnt, uint32_t* firstidx,
-                              BuildKey kf, hipStream_t s) {
-  if (R < 2) return hipSuccess;
-  hipLaunchKernelGGL(k_child_stats, dim3(blocks(R)), dim3(kB), 0, s, keys, R, cnt, firstidx, kf);
-  return hipGetLastError();
-}
-
-hipError_t launch_place_root(const uint64_t* keys, uint32_t nbase, uint16_t topic, const uint32_t* cnt,
-                             uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
-                             uint32_t* node_parent, uint32_t* deg, BuildKey kf, hipStream_t s) {
-  hipLaunchKernelGGL(k_place_root, dim3(1), dim3(64), 0, s, keys, nbase, topic, cnt, node_peer, node_topic,
-                     local, node_parent, deg, kf);
-  return hipGetLastError();
-}
-
-hipError_t launch_place_small(const uint64_t* keys, const uint32_t* lvl, uint32_t d_end, uint32_t depth, uint32_t n_nodes,
-                              uint32_t nbase, uint16_t topic, const uint32_t* cnt, const uint32_t* firstidx,
-                              uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
-                              uint32_t* node_parent, uint32_t* deg, uint32_t* first, BuildKey kf, hipStream_t s) {
-  if (d_end > depth + 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_place_small, dim3(1), dim3(kSmallB), 0, s, keys, lvl, d_end, depth, n_nodes, nbase, topic, cnt,
-                     firstidx, node_peer, node_topic, local, node_parent, deg, first, kf);
-  return hipGetLastError();
-}
-
-hipError_t launch_place_level(const uint64_t* keys, uint32_t lo, uint32_t hi, uint32_t nbase, uint32_t prev0,
-                              const uint32_t* childoff, const uint32_t* cnt, const uint32_t* firstidx,
-                              uint16_t topic, uint32_t* node_peer, uint16_t* node_topic, uint32_t* local,
-                              uint32_t* node_parent, uint32_t* deg, uint32_t* first, BuildKey kf, hipStream_t s) {
-  if (hi <= lo) return hipSuccess;
-  hipLaunchKernelGGL(k_place_level, dim3(blocks(hi - lo)), dim3(kB), 0, s, keys, lo, hi, nbase, prev0,
-                     childoff, cnt, firstidx, topic, node_peer, node_topic, local, node_parent, deg, first, kf);
-  return hipGetLastError();
-}
-
-hipError_t launch_place_level_lb(const uint64_t* keys, uint32_t np, uint32_t pbase, uint32_t cbase,
-                                 const uint32_t* cnt, const uint32_t* firstidx, uint16_t topic, uint32_t* node_peer,
-                                 uint16_t* node_topic, uint32_t* local, uint32_t* node_parent, uint32_t* deg,
-                                 uint32_t* first, uint64_t* status, uint32_t* err, BuildKey kf, hipStream_t s) {
-  if (np == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_place_level_lb, dim3(lb_tiles(np)), dim3(kB), 0, s, keys, np, pbase, cbase, cnt, firstidx,
-                     topic, node_peer, node_topic, local, node_parent, deg, first, status, err, kf);
-  return hipGetLastError();
-}
-
-hipError_t launch_level_starts(const uint64_t* keys, uint32_t R, uint32_t* lvl_start, BuildKey kf, hipStream_t s) {
-  if (R == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_level_starts, dim3(blocks(R)), dim3(kB), 0, s, keys, R, lvl_start, kf);
-  return hipGetLastError();
-}
-
-hipError_t launch_level_internal(const uint32_t* deg, uint32_t nbase, uint32_t R,
-                                 const uint32_t* lvl_start, uint32_t depth, uint32_t* lvl_internal,
-                                 uint32_t* max_deg, hipStream_t s) {
-  if (R == 0) return hipSuccess;
-  if (depth > kBuildMaxDepth) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_level_internal, dim3(std::min(blocks(R), kStatBlocks)), dim3(kB), 0, s, deg, nbase,
-                     R, lvl_start, depth,
-                     lvl_internal, max_deg);
-  return hipGetLastError();
-}
-
 hipError_t launch_scatter_pairs(const uint32_t* pairs, uint32_t n, uint32_t* par, uint8_t* orph, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_scatter_pairs, dim3(blocks(n)), dim3(kB), 0, s, pairs, n, par, orph);
   return hipGetLastError();
 }
 
-hipError_t launch_depth_keys(const uint32_t* par, uint32_t n, uint32_t root, uint32_t jumps,
-                             uint32_t* anc0, uint32_t* anc1, uint32_t* dep0, uint32_t* dep1,
-                             uint64_t* keys, uint32_t* gstat, BuildKey kf, hipStream_t s) {
-  hipLaunchKernelGGL(k_depth_init, dim3(blocks(n)), dim3(kB), 0, s, par, n, root, anc0, dep0);
-  // after j jumps every peer's ancestor is 2^j levels up (or the root / cut)
-  uint32_t *ai = anc0, *ao = anc1, *di = dep0, *dout = dep1;
-  for (uint32_t j = 0; j < jumps; ++j) {
-    hipLaunchKernelGGL(k_depth_jump, dim3(blocks(n)), dim3(kB), 0, s, ai, di, ao, dout, n, root);
-    std::swap(ai, ao);
-    std::swap(di, dout);
-  }
-  hipLaunchKernelGGL(k_depth_keys, dim3(std::min(blocks(n), kStatBlocks)), dim3(kB), 0, s, ai, di, par, n,
-                     root, keys, gstat, kf);
-  return hipGetLastError();
-}
-
-hipError_t sort_keys(void* temp, size_t* temp_bytes, const uint64_t* in, uint64_t* out, uint32_t n,
-                     BuildKey kf, bool peer_bits, hipStream_t s) {
-  return hipcub::DeviceRadixSort::SortKeys(temp, *temp_bytes, in, out, n, peer_bits ? 0 : static_cast<int>(kf.b),
-                                           static_cast<int>(kf.sort_bits()), s);
-}
-
 hipError_t scan_u32(void* temp, size_t* temp_bytes, const uint32_t* in, uint32_t* out, uint32_t n,
                     hipStream_t s) {
   return hipcub::DeviceScan::ExclusiveSum(temp, *temp_bytes, in, out, n, s);
-}
-
-hipError_t launch_fill_col(const uint32_t* row_ptr, const uint32_t* first, uint32_t n_nodes,
-                           uint32_t* col, hipStream_t s) {
-  if (n_nodes == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_fill_col, dim3(blocks(n_nodes)), dim3(kB), 0, s, row_ptr, first, n_nodes, col);
-  return hipGetLastError();
 }
 
 hipError_t launch_node_flags(const uint32_t* node_peer, const uint32_t* row_ptr,

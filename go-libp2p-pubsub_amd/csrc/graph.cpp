@@ -502,207 +502,181 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   }
   using clk = std::chrono::steady_clock;
   const auto tb1 = clk::now();
-  // 2. depth keys and sort per topic
-  HIP_TRY(e->d_anc0.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
-  HIP_TRY(e->d_anc1.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
-  HIP_TRY(e->d_dep0.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
-  HIP_TRY(e->d_dep1.ensure(static_cast<size_t>(n) * 4), "alloc scratch");
-  HIP_TRY(e->d_keys0.ensure(static_cast<size_t>(n) * 8), "alloc keys");
-  HIP_TRY(e->d_skeys.ensure(static_cast<size_t>(nt) * n * 8), "alloc sorted keys");
-  HIP_TRY(e->d_gstat.ensure(static_cast<size_t>(nt) * 4 * 4), "alloc build stats");
+  // 2. node capacity: every peer of every existing topic (the reachable
+  //    counts are known only once placed); the node arrays are written in place
+  std::vector<uint32_t> act;  // existing topics in node-space order
+  for (uint32_t t = 0; t < nt; ++t)
+    if (e->topics[t].exists) act.push_back(t);
+  const uint32_t na = static_cast<uint32_t>(act.size());
+  const uint64_t cap = static_cast<uint64_t>(na) * n + 16;
+  if (cap >= 0xFFFFFFF0ull) {  // (every peer of every topic as a node: the host build sizes exactly)
+    *fallback = true;
+    return PS_OK;
+  }
+  HIP_TRY(e->d_row_ptr.ensure((cap + 1) * 4), "alloc row_ptr");
+  HIP_TRY(e->d_col.ensure(cap * 4), "alloc col");
+  HIP_TRY(e->d_node_topic.ensure(cap * 2), "alloc node_topic");
+  HIP_TRY(e->d_node_peer.ensure(cap * 4), "alloc node_peer");
+  HIP_TRY(e->d_node_parent.ensure(cap * 4), "alloc node_parent");
+  HIP_TRY(e->d_node_flags.ensure(((cap + 15) / 16) * 16 + 16), "alloc node_flags");
+  HIP_TRY(e->d_first.ensure(cap * 4), "alloc first child");
+  HIP_TRY(e->d_local.ensure(static_cast<size_t>(n) * 4), "alloc local ids");
+  HIP_TRY(e->d_live.ensure(n), "alloc live mask");
+  HIP_TRY(hipMemcpyAsync(e->d_live.p, e->live.data(), n, hipMemcpyHostToDevice, s), "upload live");
+  // the peer-space CSR scratch (one topic at a time)
+  HIP_TRY(e->d_cnt.ensure((static_cast<size_t>(n) + 1) * 4), "alloc fan-out by peer");
+  HIP_TRY(e->d_childoff.ensure((static_cast<size_t>(n) + 1) * 4), "alloc child offsets");
+  HIP_TRY(e->d_fidx.ensure(static_cast<size_t>(n) * 4), "alloc scatter fill");
+  HIP_TRY(e->d_kids.ensure(static_cast<size_t>(n) * 4 + 4), "alloc children");
+  HIP_TRY(e->d_big.ensure(static_cast<size_t>(n) * 4 + 4), "alloc long child lists");
+  size_t scan_bytes = 0;
+  HIP_TRY(scan_u32(nullptr, &scan_bytes, nullptr, nullptr, n + 1, s), "scan size");
+  HIP_TRY(e->d_cub.ensure(std::max<size_t>(scan_bytes, 16)), "alloc scan temp");
+  HIP_TRY(e->d_gstat.ensure(static_cast<size_t>(nt) * kGstWords * 4 + 16), "alloc build stats");
   HIP_TRY(e->d_lvl.ensure(static_cast<size_t>(nt) * 512 * 4), "alloc level tables");
-  size_t cub_bytes = 0, scan_bytes = 0;
-  const BuildKey kf = build_key(n);
-  HIP_TRY(sort_keys(nullptr, &cub_bytes, nullptr, nullptr, n, kf, false, s), "sort size");
-  HIP_TRY(e->d_cub.ensure(std::max<size_t>(cub_bytes, 16)), "alloc sort temp");
-  // [t][reach, max depth, max fan-out, unresolved]
+  HIP_TRY(e->d_tb.ensure((2 * static_cast<size_t>(na) + 2) * 4), "alloc topic bases");
   uint32_t* gstat = e->d_gstat.as<uint32_t>();
+  uint32_t* err = gstat + static_cast<size_t>(nt) * kGstWords;
   auto& gs = e->gstat_host;
   auto& lh = e->lvl_host;
-  // pointer jumping sized from the last build's depth (x4 headroom); a topic
-  // that grew deeper reports unresolved peers and is redone with full jumps
-  std::vector<uint32_t> jumps(nt, depth_jumps_full(n));
-  for (uint32_t t = 0; t < nt; ++t) {
-    const uint32_t d = e->topics[t].depth;
-    if (d) jumps[t] = std::min(jumps[t], depth_jumps_full(4 * d));
-  }
-  for (int pass = 0; pass < 2; ++pass) {
-    HIP_TRY(hipMemsetAsync(e->d_gstat.p, 0, static_cast<size_t>(nt) * 4 * 4, s), "clear build stats");
-    HIP_TRY(hipMemsetAsync(e->d_lvl.p, 0, static_cast<size_t>(nt) * 512 * 4, s), "clear level tables");
-    for (uint32_t t = 0; t < nt; ++t) {
-      const TopicHost& T = e->topics[t];
-      if (!T.exists) continue;
-      HIP_TRY(launch_depth_keys(e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n, n, T.root, jumps[t],
-                                e->d_anc0.as<uint32_t>(), e->d_anc1.as<uint32_t>(),
-                                e->d_dep0.as<uint32_t>(), e->d_dep1.as<uint32_t>(),
-                                e->d_keys0.as<uint64_t>(), gstat + 4 * t, kf, s),
-              "depth");
-      size_t tb = e->d_cub.bytes;
-      HIP_TRY(sort_keys(e->d_cub.p, &tb, e->d_keys0.as<uint64_t>(),
-                        e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n, kf, false, s),
-              "sort");
-      HIP_TRY(launch_level_starts(e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n, n,
-                                  e->d_lvl.as<uint32_t>() + 512 * t, kf, s),
-              "level starts");
-    }
-    // (level starts of unreachable peers' keys land in slot 255: ignored)
-    gs.assign(static_cast<size_t>(nt) * 4, 0);
-    lh.assign(static_cast<size_t>(nt) * 512, 0);
-    HIP_TRY(hipMemcpyAsync(gs.data(), gstat, gs.size() * 4, hipMemcpyDeviceToHost, s), "read build stats");
-    HIP_TRY(hipMemcpyAsync(lh.data(), e->d_lvl.p, lh.size() * 4, hipMemcpyDeviceToHost, s), "read level starts");
-    HIP_TRY(hipStreamSynchronize(s), "sync");
-    bool redo = false;
-    for (uint32_t t = 0; t < nt; ++t)
-      if (e->topics[t].exists && gs[4 * t + 3]) {
-        jumps[t] = depth_jumps_full(n);
-        redo = true;
-      }
-    if (!redo) break;
-  }
-  const auto tb2 = clk::now();
-  for (uint32_t t = 0; t < nt; ++t)
-    if (e->topics[t].exists && gs[4 * t + 1] >= kBuildMaxDepth) {
-      *fallback = true;  // deeper than the key's depth field
-      return PS_OK;
-    }
-  // 3. layout: topic t's nodes at [nbase_t, nbase_t + R_t)
-  uint64_t n_total = 0;
-  e->roots_host.clear();
-  for (uint32_t t = 0; t < nt; ++t) {
-    TopicHost& T = e->topics[t];
-    T.nbase = static_cast<uint32_t>(n_total);
-    T.n_nodes = T.exists ? gs[4 * t] : 0;
-    if (T.n_nodes) e->roots_host.push_back(T.nbase);
-    n_total += T.n_nodes;
-  }
-  if (n_total >= 0xFFFFFFF0ull) return e->fail(PS_E_NOMEM, "node space exceeds 2^32 nodes");
-  const uint32_t nn = static_cast<uint32_t>(n_total);
-  e->n_nodes = nn;
-  e->n_pad = std::max<uint32_t>(16, ((nn + 15) / 16) * 16);
-  HIP_TRY(e->d_row_ptr.ensure((static_cast<size_t>(nn) + 1) * 4), "alloc row_ptr");
-  HIP_TRY(e->d_col.ensure(std::max<size_t>(nn, 1) * 4), "alloc col");
-  HIP_TRY(e->d_node_topic.ensure(std::max<size_t>(nn, 1) * 2), "alloc node_topic");
-  HIP_TRY(e->d_node_peer.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_peer");
-  HIP_TRY(e->d_node_parent.ensure(std::max<size_t>(nn, 1) * 4), "alloc node_parent");
-  HIP_TRY(e->d_node_flags.ensure(e->n_pad + 16), "alloc node_flags");
-  HIP_TRY(e->d_deg.ensure((static_cast<size_t>(nn) + 1) * 4), "alloc fan-out");
-  HIP_TRY(e->d_first.ensure(std::max<size_t>(nn, 1) * 4), "alloc first child");
-  HIP_TRY(e->d_local.ensure(static_cast<size_t>(n) * 4), "alloc local ids");
-  HIP_TRY(hipMemsetAsync(e->d_deg.p, 0, (static_cast<size_t>(nn) + 1) * 4, s), "clear fan-out");
-  HIP_TRY(hipMemsetAsync(e->d_first.p, 0xFF, std::max<size_t>(nn, 1) * 4, s), "clear first child");
-  uint32_t* lvl = e->d_lvl.as<uint32_t>();  // [t][0..255] level start, [t][256..511] internal count
-  // BFS placement, level by level and without sorting: the keys are already
-  // grouped by level and, within a level, by parent peer with siblings in peer
-  // order; the groups go in parent node order (an exclusive scan of the
-  // parents' fan-out), each child at its sibling rank
-  HIP_TRY(e->d_cnt.ensure(static_cast<size_t>(n) * 4), "alloc fan-out by peer");
-  HIP_TRY(e->d_fidx.ensure(static_cast<size_t>(n) * 4), "alloc first child index");
-  HIP_TRY(e->d_childoff.ensure(static_cast<size_t>(n) * 4 + 4), "alloc child offsets");
-  {
-    size_t sb = 0;
-    HIP_TRY(scan_u32(nullptr, &sb, nullptr, nullptr, n, s), "scan size");
-    HIP_TRY(e->d_cub.ensure(std::max<size_t>(sb, 16)), "alloc scan temp");
-  }
-  uint32_t* cnt = e->d_cnt.as<uint32_t>();
-  uint32_t* fidx = e->d_fidx.as<uint32_t>();
-  uint32_t* childoff = e->d_childoff.as<uint32_t>();
-  for (uint32_t t = 0; t < nt; ++t) {
-    TopicHost& T = e->topics[t];
-    if (!T.n_nodes) continue;
-    const uint32_t depth = gs[4 * t + 1];
-    const uint64_t* keys = e->d_skeys.as<uint64_t>() + static_cast<size_t>(t) * n;
-    const uint16_t tt = static_cast<uint16_t>(t);
-    HIP_TRY(hipMemsetAsync(cnt, 0, static_cast<size_t>(n) * 4, s), "clear fan-out by peer");
-    HIP_TRY(hipMemsetAsync(fidx, 0xFF, static_cast<size_t>(n) * 4, s), "clear first child index");
-    HIP_TRY(launch_child_stats(keys, T.n_nodes, cnt, fidx, kf, s), "child stats");
-    // the small top levels (and their parents) go in one single-block launch
-    auto lvl_end = [&](uint32_t d) { return d == depth ? T.n_nodes : lh[512 * t + d + 1]; };
-    uint32_t d_small = 1;
-    while (d_small <= depth && lvl_end(d_small) - lh[512 * t + d_small] <= e->small_place &&
-           lh[512 * t + d_small] - lh[512 * t + d_small - 1] <= e->small_place)
-      ++d_small;
-    if (d_small > 1) {
-      HIP_TRY(launch_place_small(keys, e->d_lvl.as<uint32_t>() + 512 * t, d_small, depth, T.n_nodes, T.nbase, tt,
-                                 cnt, fidx, e->d_node_peer.as<uint32_t>(), e->d_node_topic.as<uint16_t>(),
-                                 e->d_local.as<uint32_t>(), e->d_node_parent.as<uint32_t>(),
-                                 e->d_deg.as<uint32_t>(), e->d_first.as<uint32_t>(), kf, s),
-              "place small levels");
-    } else {
-      HIP_TRY(launch_place_root(keys, T.nbase, tt, cnt, e->d_node_peer.as<uint32_t>(),
-                                e->d_node_topic.as<uint16_t>(), e->d_local.as<uint32_t>(),
-                                e->d_node_parent.as<uint32_t>(), e->d_deg.as<uint32_t>(), kf, s),
-              "place root");
-    }
-    // the levels below: one look-back launch each (their tiles' status
-    // words zeroed once per topic)
-    size_t tiles = 0;
-    for (uint32_t d = d_small; d <= depth; ++d) tiles += lb_tiles(lh[512 * t + d] - lh[512 * t + d - 1]);
-    if (tiles) {
-      HIP_TRY(e->d_lbstat.ensure(tiles * 8), "alloc look-back status");
-      HIP_TRY(hipMemsetAsync(e->d_lbstat.p, 0, tiles * 8, s), "clear look-back status");
-    }
-    uint64_t* lbst = e->d_lbstat.as<uint64_t>();
-    for (uint32_t d = d_small; d <= depth; ++d) {
-      const uint32_t plo = lh[512 * t + d - 1];
-      const uint32_t lo = lh[512 * t + d];
-      if (e->lb_place) {
-        HIP_TRY(launch_place_level_lb(keys, lo - plo, T.nbase + plo, T.nbase + lo, cnt, fidx, tt,
-                                      e->d_node_peer.as<uint32_t>(), e->d_node_topic.as<uint16_t>(),
-                                      e->d_local.as<uint32_t>(), e->d_node_parent.as<uint32_t>(),
-                                      e->d_deg.as<uint32_t>(), e->d_first.as<uint32_t>(), lbst, gstat + 4 * t + 3, kf,
-                                      s),
-                "place level");
-        lbst += lb_tiles(lo - plo);
-        continue;
-      }
-      const uint32_t hi = d == depth ? T.n_nodes : lh[512 * t + d + 1];
-      size_t tb = e->d_cub.bytes;
-      HIP_TRY(scan_u32(e->d_cub.p, &tb, e->d_deg.as<uint32_t>() + T.nbase + plo, childoff, lo - plo, s),
-              "scan fan-out");
-      HIP_TRY(launch_place_level(keys, lo, hi, T.nbase, T.nbase + plo, childoff, cnt, fidx, tt,
-                                 e->d_node_peer.as<uint32_t>(), e->d_node_topic.as<uint16_t>(),
-                                 e->d_local.as<uint32_t>(), e->d_node_parent.as<uint32_t>(),
-                                 e->d_deg.as<uint32_t>(), e->d_first.as<uint32_t>(), kf, s),
-              "place level");
-    }
-  }
-  for (uint32_t t = 0; t < nt; ++t) {
+  std::vector<uint32_t> tb(2 * na + 2, 0);
+  // per topic: the levels the look-back launches take (from the top kernel's
+  // last reach to 2 past the last depth: the pass past the deepest level
+  // closes its leaves' CSR rows) and each launch's grid, from the last build's
+  // level sizes (a level that outgrew its grid is redone with full grids)
+  const uint32_t full = lb_tiles(n);
+  std::vector<uint32_t> d_from(nt, 1), d_to(nt, 0);
+  for (uint32_t t : act) {
     const TopicHost& T = e->topics[t];
-    if (!T.n_nodes) continue;
-    HIP_TRY(launch_level_internal(e->d_deg.as<uint32_t>(), T.nbase, T.n_nodes, lvl + 512 * t, gs[4 * t + 1],
-                                  lvl + 512 * t + 256, gstat + 4 * t + 2, s),
-            "level stats");
+    if (T.level_off.size() >= 2 && T.depth) {
+      d_from[t] = std::max<uint32_t>(1, T.top_levels);
+      d_to[t] = std::min<uint32_t>(kBuildMaxDepth - 1, T.depth + 2);
+    } else {
+      d_to[t] = 24;
+    }
   }
-  // 4. CSR: row_ptr = exclusive scan of the fan-out; children consecutive
-  HIP_TRY(scan_u32(nullptr, &scan_bytes, nullptr, nullptr, nn + 1, s), "scan size");
-  HIP_TRY(e->d_cub.ensure(std::max<size_t>(scan_bytes, 16)), "alloc scan temp");
-  size_t tb = e->d_cub.bytes;
-  HIP_TRY(scan_u32(e->d_cub.p, &tb, e->d_deg.as<uint32_t>(), e->d_row_ptr.as<uint32_t>(), nn + 1, s), "scan");
-  HIP_TRY(launch_fill_col(e->d_row_ptr.as<uint32_t>(), e->d_first.as<uint32_t>(), nn, e->d_col.as<uint32_t>(), s),
-          "fill col");
-  // 5. level tables back to the host (rounds, chunks, grid bounds)
-  const auto tb3 = clk::now();
-  HIP_TRY(hipMemcpyAsync(lh.data(), lvl, lh.size() * 4, hipMemcpyDeviceToHost, s), "read level tables");
-  HIP_TRY(hipMemcpyAsync(gs.data(), gstat, gs.size() * 4, hipMemcpyDeviceToHost, s), "read build stats");
-  HIP_TRY(hipStreamSynchronize(s), "sync");
-  for (uint32_t t = 0; t < nt; ++t)
-    if (e->topics[t].n_nodes && gs[4 * t + 3]) {  // a stalled placement look-back: build on the host
+  bool full_grids = false;
+  const auto tb2 = clk::now();
+  for (int attempt = 0;; ++attempt) {
+    if (attempt >= 8) {
       *fallback = true;
       return PS_OK;
     }
+    HIP_TRY(hipMemsetAsync(e->d_gstat.p, 0, e->d_gstat.bytes, s), "clear build stats");
+    HIP_TRY(hipMemsetAsync(e->d_lvl.p, 0, e->d_lvl.bytes, s), "clear level tables");
+    HIP_TRY(hipMemsetAsync(e->d_tb.p, 0, e->d_tb.bytes, s), "clear topic bases");
+    // look-back status words: one region per level launch
+    size_t st_words = 0;
+    std::vector<std::vector<uint32_t>> grids(nt);
+    for (uint32_t t : act) {
+      const TopicHost& T = e->topics[t];
+      for (uint32_t d = d_from[t]; d <= d_to[t]; ++d) {
+        uint32_t g = full;
+        if (!full_grids && d < T.level_off.size() && d >= 1 && T.level_off.size() >= 2) {
+          const uint64_t np = T.level_off[d] - T.level_off[d - 1];
+          g = std::min<uint32_t>(full, lb_tiles(static_cast<uint32_t>(std::min<uint64_t>(np + np / 4 + 2048, n))));
+        }
+        grids[t].push_back(g);
+        st_words += g;
+      }
+    }
+    HIP_TRY(e->d_lbstat.ensure(std::max<size_t>(st_words, 1) * 8), "alloc look-back status");
+    HIP_TRY(hipMemsetAsync(e->d_lbstat.p, 0, std::max<size_t>(st_words, 1) * 8, s), "clear look-back status");
+    uint64_t* lbst = e->d_lbstat.as<uint64_t>();
+    for (uint32_t ai = 0; ai < na; ++ai) {
+      const uint32_t t = act[ai];
+      const TopicHost& T = e->topics[t];
+      HIP_TRY(build_kids(e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n, n, e->d_cnt.as<uint32_t>(),
+                         e->d_childoff.as<uint32_t>(), e->d_fidx.as<uint32_t>(), e->d_kids.as<uint32_t>(),
+                         e->d_big.as<uint32_t>(), e->d_big.as<uint32_t>() + n, e->d_cub.p, e->d_cub.bytes, s),
+              "child lists");
+      PlaceArgs P{};
+      P.kids = e->d_kids.as<uint32_t>();
+      P.koff = e->d_childoff.as<uint32_t>();
+      P.cnt = e->d_cnt.as<uint32_t>();
+      P.live = e->d_live.as<uint8_t>();
+      P.node_peer = e->d_node_peer.as<uint32_t>();
+      P.node_topic = e->d_node_topic.as<uint16_t>();
+      P.local = e->d_local.as<uint32_t>();
+      P.node_parent = e->d_node_parent.as<uint32_t>();
+      P.row_ptr = e->d_row_ptr.as<uint32_t>();
+      P.col = e->d_col.as<uint32_t>();
+      P.first = e->d_first.as<uint32_t>();
+      P.flags = e->d_node_flags.as<uint8_t>();
+      P.lvl = e->d_lvl.as<uint32_t>() + 512 * static_cast<size_t>(t);
+      P.gst = gstat + static_cast<size_t>(t) * kGstWords;
+      P.tb = e->d_tb.as<uint32_t>();
+      P.err = err;
+      P.a = ai;
+      P.root = T.root;
+      P.topic = static_cast<uint16_t>(t);
+      HIP_TRY(launch_place_top(P, d_from[t] > 1 ? d_from[t] : kBuildMaxDepth, s), "place top levels");
+      for (uint32_t i = 0, d = d_from[t]; d <= d_to[t]; ++d, ++i) {
+        HIP_TRY(launch_place_lb(P, d, grids[t][i], lbst, s), "place level");
+        lbst += grids[t][i];
+      }
+    }
+    gs.assign(static_cast<size_t>(nt) * kGstWords + 4, 0);
+    lh.assign(static_cast<size_t>(nt) * 512, 0);
+    HIP_TRY(hipMemcpyAsync(gs.data(), gstat, gs.size() * 4, hipMemcpyDeviceToHost, s), "read build stats");
+    HIP_TRY(hipMemcpyAsync(lh.data(), e->d_lvl.p, lh.size() * 4, hipMemcpyDeviceToHost, s), "read level tables");
+    HIP_TRY(hipMemcpyAsync(tb.data(), e->d_tb.p, tb.size() * 4, hipMemcpyDeviceToHost, s), "read topic bases");
+    HIP_TRY(hipStreamSynchronize(s), "sync");
+    const uint32_t ev = gs[static_cast<size_t>(nt) * kGstWords];
+    if (ev & kBuildErrStall) {
+      *fallback = true;  // a stalled look-back: build on the host
+      return PS_OK;
+    }
+    bool redo = false;
+    if (ev & kBuildErrGrid) {
+      full_grids = true;
+      redo = true;
+    }
+    if (ev & kBuildErrOrder) {  // a top level outgrew the top kernel: every level by look-back launches
+      for (uint32_t t : act) d_from[t] = 1;
+      redo = true;
+    }
+    for (uint32_t t : act) {  // a tree deeper than the launches: more levels
+      const uint32_t done = gs[static_cast<size_t>(t) * kGstWords + kGstDone];
+      if (lh[512 * t + done + 1] != lh[512 * t + done] || done < d_to[t]) {
+        if (d_to[t] >= kBuildMaxDepth - 1 && lh[512 * t + done + 1] != lh[512 * t + done]) {
+          *fallback = true;  // deeper than the level tables
+          return PS_OK;
+        }
+        if (!(ev & (kBuildErrGrid | kBuildErrOrder)) && done >= d_to[t]) {
+          d_to[t] = std::min<uint32_t>(kBuildMaxDepth - 1, 2 * d_to[t] + 8);
+          redo = true;
+        }
+      }
+    }
+    if (!redo) break;
+  }
+  const auto tb3 = clk::now();
+  // 3. layout: topic t's nodes at [nbase_t, nbase_t + R_t) (the device's bases)
+  e->roots_host.clear();
+  for (uint32_t t = 0; t < nt; ++t) e->topics[t].n_nodes = 0;
+  for (uint32_t ai = 0; ai < na; ++ai) {
+    TopicHost& T = e->topics[act[ai]];
+    T.nbase = tb[2 * ai];
+    T.n_nodes = tb[2 * ai + 2] - tb[2 * ai];
+    e->roots_host.push_back(T.nbase);
+  }
+  const uint32_t nn = na ? tb[2 * na] : 0u;
+  e->n_nodes = nn;
+  e->n_pad = std::max<uint32_t>(16, ((nn + 15) / 16) * 16);
   if (e->host_timing) {
     auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
-    std::fprintf(stderr, "[psengine] gpu build: deltas %.3f ms (%zu), depth+sort+readback %.3f ms, "
-                 "placement enqueue %.3f ms, drain %.3f ms\n", ms(tb0, tb1), pairs.size() / 2,
-                 ms(tb1, tb2), ms(tb2, tb3), ms(tb3, clk::now()));
+    std::fprintf(stderr, "[psengine] gpu build: deltas %.3f ms (%zu), scratch %.3f ms, child lists + placement "
+                 "+ readback %.3f ms\n", ms(tb0, tb1), pairs.size() / 2, ms(tb1, tb2), ms(tb2, tb3));
   }
   for (uint32_t t = 0; t < nt; ++t) {
     TopicHost& T = e->topics[t];
     T.mesh = false;
     T.root_local = true;
     T.cross.clear();
-    T.depth = T.n_nodes ? gs[4 * t + 1] : 0;
-    T.max_deg = gs[4 * t + 2];
+    const uint32_t* g = gs.data() + static_cast<size_t>(t) * kGstWords;
+    T.depth = T.n_nodes ? g[kGstDepth] : 0;
+    T.max_deg = g[kGstMaxDeg];
     T.level_off.assign(T.depth + 2, 0);
     T.level_internal.assign(T.depth + 1, 0);
     T.level_local.clear();
@@ -710,12 +684,16 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
     T.send_node.clear();
     T.send_dst.clear();
     T.send_lvl.clear();
+    T.top_levels = 1;
     if (!T.n_nodes) continue;
     for (uint32_t d = 0; d <= T.depth; ++d) {
       T.level_off[d] = lh[512 * t + d];
       T.level_internal[d] = lh[512 * t + 256 + d];
     }
     T.level_off[T.depth + 1] = T.n_nodes;
+    // the levels the top kernel places (parents of at most kBuildSmallLevel)
+    while (T.top_levels <= T.depth && T.level_off[T.top_levels] - T.level_off[T.top_levels - 1] <= kBuildSmallLevel)
+      ++T.top_levels;
     T.level_local.assign(T.depth + 1, 0);
     for (uint32_t d = 0; d <= T.depth; ++d) T.level_local[d] = T.level_off[d + 1] - T.level_off[d];
   }
