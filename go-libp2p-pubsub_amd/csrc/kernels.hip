@@ -972,6 +972,22 @@ __global__ __launch_bounds__(kBlock) void k_digest(const uint64_t* __restrict__ 
       continue;
     }
     const uint64_t row = T.wbase + static_cast<uint64_t>(u - T.nbase) * T.W;
+    if (T.flags & kTopicPacked) {  // group g's virtual word r: its bits b0 + 64 r .. of the packed row
+      for (uint32_t g = 0; g < T.group_n; ++g) {
+        const GroupDev G = groups[T.group_lo + g];
+        for (uint32_t r = 0; r < G.wn; ++r) {
+          uint64_t x = 0;
+          if (valid && 64 * r < G.n) {
+            const uint32_t b = G.b0 + 64 * r, take = min(64u, G.n - 64 * r);
+            const uint64_t lo = seen[row + (b >> 6)] >> (b & 63);
+            const uint64_t hi = (b & 63) && (b >> 6) + 1 < T.W ? seen[row + (b >> 6) + 1] << (64 - (b & 63)) : 0ull;
+            x = (lo | hi) & (take == 64 ? ~0ull : (1ull << take) - 1);
+          }
+          acc += mix64((key0 | (G.w0 + r)) ^ mix64(x));
+        }
+      }
+      continue;
+    }
     for (uint32_t w = 0; w < T.w_msgs; ++w)
       acc += mix64((key0 | w) ^ mix64(valid ? seen[row + w] : 0ull));
   }

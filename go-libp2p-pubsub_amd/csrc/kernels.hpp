@@ -48,9 +48,17 @@ enum : uint32_t {
   // -- stored group-major: block g of node u at wbase + n_nodes * w0 +
   // (u - nbase) * wn, so a round's rows are contiguous per group.
   kTopicGroups = 8,
+  // A level-aligned window's topic with several start rounds (one rank): one
+  // node-major row, message bits sorted by start round; GroupDev [group_lo,
+  // + group_n) hold each start group's bits [b0, b0 + n) of the row and the
+  // virtual words [w0, w0 + wn) the group-major layout would give it, so the
+  // digest reads both layouts alike.  Kernels other than the digest see a
+  // single-start topic.
+  kTopicPacked = 16,
 };
 struct GroupDev {
   uint32_t w0, wn;
+  uint32_t b0, n;  // kTopicPacked: the group's bits of the packed row
 };
 constexpr uint32_t kEntrySplit = 0x100;  // per-entry flag bit next to TopicDev.flags
 

@@ -183,7 +183,7 @@ int plan_window_layout(ps_engine* e, const std::vector<RunMsg>& msgs, const std:
     d.group_lo = static_cast<uint32_t>(L.gtab.size());
     d.group_n = static_cast<uint32_t>(L.groups[t].size());
     d.root_words = L.groups[t][0].wn;
-    for (const StartGroup& g : L.groups[t]) L.gtab.push_back(GroupDev{g.w0, g.wn});
+    for (const StartGroup& g : L.groups[t]) L.gtab.push_back(GroupDev{g.w0, g.wn, 0, 0});
   }
   L.true_rounds = L.planned0;
   if (align && !L.level) return e->fail(PS_E_STATE, "aligned window outside level mode");  // (unreachable)
@@ -195,6 +195,18 @@ int plan_window_layout(ps_engine* e, const std::vector<RunMsg>& msgs, const std:
     sp.seg_n.assign(nt, 0);
     for (uint32_t t = 0; t < nt; ++t) {
       if (!L.tab[t].W) continue;
+      TopicDev& d = L.tab[t];
+      if (sp.groups[t].size() > 1) {  // the digest's virtual group-major words
+        d.flags |= kTopicPacked;
+        d.group_lo = static_cast<uint32_t>(L.gtab.size());
+        d.group_n = static_cast<uint32_t>(sp.groups[t].size());
+        uint32_t w0 = 0;
+        for (const AlignedGroup& g : sp.groups[t]) {
+          const uint32_t wn = (ceil_div(g.n, 64) + 1) & ~1u;
+          L.gtab.push_back(GroupDev{w0, wn, g.b0, g.n});
+          w0 += wn;
+        }
+      }
       sp.seg_lo[t] = sp.n_segs;
       sp.seg_n[t] = e->topics[t].depth + 1;  // levels 0 .. depth
       sp.n_segs += sp.seg_n[t];
