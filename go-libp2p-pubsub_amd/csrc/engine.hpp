@@ -516,6 +516,6 @@ bool accumulate_window(ps_stats* st, const uint64_t* hs, const uint64_t* ha, uin
 // its reach rows (hs rows split.row0 ..): false when they disagree with the
 // kernels' per-level counters (rows 1 .. r)
 bool split_aligned_window(ps_stats* st, const uint64_t* hs, uint32_t r, uint32_t true_rounds,
-                          const AlignedSplit& sp);
+                          const AlignedSplit& sp, std::string* why = nullptr);
 
 }  // namespace psamd

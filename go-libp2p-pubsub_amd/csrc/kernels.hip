@@ -91,8 +91,11 @@ __device__ __forceinline__ void window_init_block(const TopicDev* __restrict__ t
   const bool mesh = (T.flags & kTopicMesh) != 0;
   const uint64_t n_words = mesh ? static_cast<uint64_t>(T.n_nodes) * T.W : T.root_words;
   if (!mesh && (bx != 0 || !(T.flags & kTopicRootLocal))) return;
-  for (uint64_t i = static_cast<uint64_t>(bx) * kBlock + threadIdx.x; i < n_words;
-       i += static_cast<uint64_t>(gx) * kBlock) {
+  // (a tree root's row: block 0 alone, every word -- striding by the grid's
+  // gx blocks left words 256 .. of rows wider than 256 words stale: a window
+  // with fewer messages than the one before kept the old ones' bits there)
+  const uint64_t step = static_cast<uint64_t>(mesh ? gx : 1u) * kBlock;
+  for (uint64_t i = static_cast<uint64_t>(bx) * kBlock + threadIdx.x; i < n_words; i += step) {
     seen[T.wbase + i] = 0;
     a0[T.wbase + i] = 0;
     a1[T.wbase + i] = 0;

@@ -112,6 +112,22 @@ def test_async_with_hop_record_and_churn():
             assert st.deliveries == 20 * int((exp != 0xFF).sum())
 
 
+def reached_per_topic(e, wl, live):
+    """Peers each topic's messages reach on the engine's trees under `live`
+    (the restatement's BFS, one message per topic)."""
+    out = []
+    for t, ts in enumerate(wl.topics):
+        rp, cl = O.parents_to_csr(e.parents(t))
+        tot, _, _ = O.disseminate(rp, cl, ts.root, live, 1, want_hops=False)
+        out.append(int(tot))
+    return np.array(out, dtype=np.int64)
+
+
+def expected_deliveries(msg_topics, reach):
+    """Every message reaches its topic's reached peers (trees: no duplicates)."""
+    return int((np.bincount(msg_topics, minlength=reach.shape[0]).astype(np.int64) * reach).sum())
+
+
 def vary_counts(msg_topics, i):
     """Window i's batch: each topic loses up to (n_t - 1) % 64 of its last
     messages, so its row width ceil(n_t / 64) -- and the plan -- stays, while
@@ -158,9 +174,14 @@ def test_overlapped_windows_equal_blocking(monkeypatch, dead, full):
             res.append(stats_key(e.wait()))
             assert e.overlapped_windows() >= 5
         else:
+            reach = reached_per_topic(e, wl, live)
             for i in range(8):
                 e.publish(batches[i])
                 res.append(stats_key(e.run()))
+                # exact: a window with fewer messages than the one before must
+                # not keep the old ones' bits in its root rows (rows wider
+                # than 256 words: cfg3's hot topic)
+                assert res[-1][0] == expected_deliveries(batches[i], reach), i
             assert e.overlapped_windows() == 0
             assert res[-1][2] >= 12  # a deep window (rounds)
         out.append((res, e.seen_digest()))
@@ -214,10 +235,12 @@ def test_overlapped_staggered_windows_equal_blocking(monkeypatch, dead, full):
                     res.append(stats_key(e.wait()))
             res.append(stats_key(e.wait()))
         else:
+            reach = reached_per_topic(e, wl, live)
             for i in range(8):
                 e.publish(*batches[i])
                 st = e.run()
                 assert bool(st.level_aligned) == bool(align)
+                assert st.deliveries == expected_deliveries(batches[i][0], reach), i
                 res.append(stats_key(st))
             assert e.overlapped_windows() == 0
         out.append((res, e.seen_digest()))
