@@ -317,7 +317,7 @@ struct ps_engine {
   psamd::DevBuf d_reach;
   std::vector<psamd::ReachPiece> reach_host;
   std::vector<uint64_t> reach_key;
-  uint32_t n_reach = 0;
+  uint32_t n_reach = 0, reach_a = 0;  // pieces; those of levels <= the prefix P (first)
   // level mode, pull direction: per-round chunks of next-level nodes
   psamd::PullPlan pull;
   psamd::DevBuf d_pull;

@@ -410,29 +410,6 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   const uint32_t reach_rows =
       L.aligned ? static_cast<uint32_t>(ceil_div(2ull * L.split.n_segs, static_cast<uint64_t>(kNumCtr))) : 0u;
   uint32_t reach_slot0 = 0;
-  if (L.aligned) {
-    // the (topic, level) pieces, cached per node space and active topic set
-    std::vector<uint64_t> key{e->graph_epoch};
-    for (uint32_t t = 0; t < nt; ++t) key.push_back(L.split.seg_lo[t]);
-    if (key != e->reach_key) {
-      std::vector<ReachPiece>& pc = e->reach_host;
-      pc.clear();
-      for (uint32_t t = 0; t < nt; ++t) {
-        if (L.split.seg_lo[t] == kNone) continue;
-        const TopicHost& T = e->topics[t];
-        for (uint32_t dl = 0; dl < L.split.seg_n[t]; ++dl)
-          for (uint32_t u = T.level_off[dl]; u < T.level_off[dl + 1]; u += kReachPiece)
-            pc.push_back(ReachPiece{L.split.seg_lo[t] + dl, T.nbase + u,
-                                    T.nbase + std::min<uint32_t>(u + kReachPiece, T.level_off[dl + 1]), t});
-      }
-      HIP_TRY(e->d_reach.ensure(std::max<size_t>(pc.size(), 1) * sizeof(ReachPiece)), "alloc reach pieces");
-      if (!pc.empty())
-        HIP_TRY(hipMemcpyAsync(e->d_reach.p, pc.data(), pc.size() * sizeof(ReachPiece), hipMemcpyHostToDevice,
-                               e->stream),
-                "upload reach pieces");
-      e->n_reach = static_cast<uint32_t>(pc.size());
-      e->reach_key = key;
-    }
   }
   bool fresh = false;           // level mode: no plan upload this window
   if (level) {
@@ -571,6 +548,40 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       acc += b;
       pre_P = ls[i].second;
     }
+  }
+  // level-aligned: the (topic, level) pieces of k_level_reach, levels <= P
+  // first (they are counted before the gate launch: a pipelined successor's
+  // prefix may restamp those levels' generation bytes beside this window's
+  // remaining launches), cached per node space, active topic set and P
+  uint32_t reach_a = 0;  // pieces of levels <= pre_P
+  if (L.aligned) {
+    std::vector<uint64_t> key{e->graph_epoch, pre_P};
+    for (uint32_t t = 0; t < nt; ++t) key.push_back(L.split.seg_lo[t]);
+    if (key != e->reach_key) {
+      std::vector<ReachPiece>& pc = e->reach_host;
+      pc.clear();
+      for (int part = 0; part < 2; ++part) {
+        for (uint32_t t = 0; t < nt; ++t) {
+          if (L.split.seg_lo[t] == kNone) continue;
+          const TopicHost& T = e->topics[t];
+          for (uint32_t dl = 0; dl < L.split.seg_n[t]; ++dl) {
+            if ((dl <= pre_P) != (part == 0)) continue;
+            for (uint32_t u = T.level_off[dl]; u < T.level_off[dl + 1]; u += kReachPiece)
+              pc.push_back(ReachPiece{L.split.seg_lo[t] + dl, T.nbase + u,
+                                      T.nbase + std::min<uint32_t>(u + kReachPiece, T.level_off[dl + 1]), t});
+          }
+        }
+        if (part == 0) e->reach_a = static_cast<uint32_t>(pc.size());
+      }
+      HIP_TRY(e->d_reach.ensure(std::max<size_t>(pc.size(), 1) * sizeof(ReachPiece)), "alloc reach pieces");
+      if (!pc.empty())
+        HIP_TRY(hipMemcpyAsync(e->d_reach.p, pc.data(), pc.size() * sizeof(ReachPiece), hipMemcpyHostToDevice,
+                               e->stream),
+                "upload reach pieces");
+      e->n_reach = static_cast<uint32_t>(pc.size());
+      e->reach_key = key;
+    }
+    reach_a = e->reach_a;
   }
   // every single-rank tree window may overlap its window init (pre_P = 0:
   // the gate is the predecessor's first launch, the last one reading the
@@ -868,11 +879,18 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     };
     static_assert(kSendBufs == 3, "reuse() below waits kSendBufs - 1 rounds back");
     bool gate_done = false;
+    bool reach_a_done = false;
     for (r = flood_rounds + 1; r <= planned0; ++r) {
       if (s != e->stream && r > pre_P) {  // the prefix is enqueued: the rest follows it on the main stream
         HIP_TRY(hipEventRecord(e->ev_pre, s), "event");
         s = e->stream;
         HIP_TRY(hipStreamWaitEvent(s, e->ev_pre, 0), "prefix join");
+      }
+      if (L.aligned && r == pre_P + 1 && reach_a && !reach_a_done) {  // levels <= P counted before the gate
+        HIP_TRY(launch_level_reach(e->d_reach.as<ReachPiece>(), reach_a, a.gen, a.gen_cur, a.node_flags, a.topics,
+                                   a.seen, L.split.eager, partials + static_cast<size_t>(reach_slot0) * kNumCtr, s),
+                "level reach (prefix levels)");
+        reach_a_done = true;
       }
       if (pcap && !gate_done && r > pre_P + 1) {  // the gate launch is enqueued
         HIP_TRY(hipEventRecord(e->ev_gate[slot], e->stream), "event");
@@ -1008,10 +1026,13 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     r = planned0;
     // level-aligned: each (topic, level)'s reached and frontier nodes, for
     // the per-round split (into the pseudo-slots after the rounds')
-    if (L.aligned && e->n_reach)
-      HIP_TRY(launch_level_reach(e->d_reach.as<ReachPiece>(), e->n_reach, a.gen, a.gen_cur, a.node_flags, a.topics,
-                                 a.seen, L.split.eager, partials + static_cast<size_t>(reach_slot0) * kNumCtr, s),
+    if (L.aligned && e->n_reach) {
+      const uint32_t from = reach_a_done ? reach_a : 0u;
+      HIP_TRY(launch_level_reach(e->d_reach.as<ReachPiece>() + from, e->n_reach - from, a.gen, a.gen_cur,
+                                 a.node_flags, a.topics, a.seen, L.split.eager,
+                                 partials + static_cast<size_t>(reach_slot0) * kNumCtr, s),
               "level reach");
+    }
     // a deferred window's counters go straight into its pinned rows
     const bool direct = e->defer_last && e->defer_into && !record && !timed && r <= PS_MAX_ROUNDS &&
                         (world == 1 || planned0 <= PS_MAX_ROUNDS);
