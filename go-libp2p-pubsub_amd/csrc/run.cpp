@@ -410,7 +410,6 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   const uint32_t reach_rows =
       L.aligned ? static_cast<uint32_t>(ceil_div(2ull * L.split.n_segs, static_cast<uint64_t>(kNumCtr))) : 0u;
   uint32_t reach_slot0 = 0;
-  }
   bool fresh = false;           // level mode: no plan upload this window
   if (level) {
     bool changed = plan_pull_chunks(e, L);
