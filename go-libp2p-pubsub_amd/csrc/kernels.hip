@@ -1134,7 +1134,7 @@ __global__ __launch_bounds__(kBlock) void k_level_reach(const ReachPiece* __rest
       reached = gen[u] == cur;
     const bool internal = (node_flags[u] & kNodeInternal) != 0;
     r += reached ? 1u : 0u;
-    f += (internal && (reached || eager)) ? 1u : 0u;
+    f += (internal && reached) ? 1u : 0u;
   }
   r = __reduce_add_sync(~0ull, r);
   f = __reduce_add_sync(~0ull, f);

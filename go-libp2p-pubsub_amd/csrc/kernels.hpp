@@ -427,8 +427,7 @@ hipError_t launch_window_init(const TopicDev* topics, uint32_t n_topics, uint64_
 // A level-aligned window's per-(topic, level) reach counts:
 // the nodes [lo, hi) of segment seg (one BFS level of one topic; a level is
 // cut into pieces of at most kReachPiece nodes).  out[2 * seg] += reached
-// nodes, out[2 * seg + 1] += frontier nodes (reached and internal; eager
-// seen: internal, as the level kernels count their parents then).  Reached:
+// nodes, out[2 * seg + 1] += frontier nodes (reached and internal).  Reached:
 // the generation byte is this window's (eager seen: the row's first word is
 // non-zero -- its first message's bit); a topic root always.
 struct ReachPiece {

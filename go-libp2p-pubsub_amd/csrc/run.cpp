@@ -1391,7 +1391,10 @@ bool split_aligned_window(ps_stats* st, const uint64_t* hs, uint32_t r, uint32_t
   bool ok = true;
   for (uint32_t d = 1; d <= r; ++d) {
     const uint64_t* c = &hs[static_cast<size_t>(d) * kNumCtr];
-    if (c[kCtrDeliveries] != deliv[d] || c[kCtrEntries] != front[d]) {
+    // (eager seen, PS_F_NO_LAZY_SEEN: every generation is stamped up front and
+    // the level kernels count parents by their own reach tests -- k_flood's
+    // granules, the pull kernels' stamps -- so only the deliveries compare)
+    if (c[kCtrDeliveries] != deliv[d] || (!sp.eager && c[kCtrEntries] != front[d])) {
       if (ok && why)
         *why = "level " + std::to_string(d) + ": deliveries " + std::to_string(c[kCtrDeliveries]) + " vs " +
                std::to_string(deliv[d]) + ", frontier " + std::to_string(c[kCtrEntries]) + " vs " +
