@@ -311,6 +311,7 @@ void ps_destroy(ps_engine* e) {
   if (e->xstream) (void)hipStreamSynchronize(e->xstream);
   if (e->pstream) (void)hipStreamSynchronize(e->pstream);
   if (e->rstream) (void)hipStreamSynchronize(e->rstream);
+  if (e->qstream) (void)hipStreamSynchronize(e->qstream);
   for (auto ev : e->ev_k) (void)hipEventDestroy(ev);
   for (hipEvent_t ev : {e->ev_run0, e->ev_run1, e->ev_round, e->ev_xchg, e->ev_gate[0], e->ev_gate[1], e->ev_pre, e->ev_end})
     if (ev) (void)hipEventDestroy(ev);
@@ -326,6 +327,7 @@ void ps_destroy(ps_engine* e) {
   if (e->xstream) (void)hipStreamDestroy(e->xstream);
   if (e->pstream) (void)hipStreamDestroy(e->pstream);
   if (e->rstream) (void)hipStreamDestroy(e->rstream);
+  if (e->qstream) (void)hipStreamDestroy(e->qstream);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }

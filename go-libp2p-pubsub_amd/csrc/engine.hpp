@@ -277,7 +277,7 @@ struct ps_engine {
   size_t pairs_pinned_cap = 0;       // (u32 words)
   std::vector<size_t> pair_off;
   psamd::DevBuf d_tpar, d_orph, d_local, d_first, d_lvl,
-      d_gstat, d_cub, d_pairs, d_live, d_roots, d_cnt, d_fidx, d_childoff, d_lbstat, d_sigctr, d_kids, d_big, d_tb;
+      d_gstat, d_cub, d_pairs, d_live, d_roots, d_cnt, d_fidx, d_childoff, d_lbstat, d_sigctr, d_kids, d_big, d_tb, d_ndeg, d_nkat, d_query;
   std::chrono::steady_clock::time_point t_run0;
   // k_flood: a single-rank level window's leading rounds in
   // one persistent launch; PSAMD_FLOOD=0 runs per-round launches instead
@@ -458,6 +458,10 @@ struct ps_engine {
   uint64_t overlap_min_bytes = 512ull << 20;  // row bytes of the window at least (PSAMD_OVERLAP_BYTES)
   hipStream_t pstream = nullptr;
   hipStream_t rstream = nullptr;  // a pipelined window's counter reduce, beside the next window
+  // the lazy prune's reach queries: they read the node space of the window
+  // just enqueued (its build is complete), not its rows, so they run beside
+  // the window's kernels instead of behind them
+  hipStream_t qstream = nullptr;
   hipEvent_t ev_gate[2] = {nullptr, nullptr}, ev_pre = nullptr, ev_end = nullptr;
   bool gate_valid = false;
   uint32_t gate_slot = 0;

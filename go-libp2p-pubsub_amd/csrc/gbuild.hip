@@ -171,9 +171,11 @@ __device__ __forceinline__ bool place_child(const PlaceArgs& P, uint32_t nbase, 
   P.local[peer] = c;
   P.node_parent[c] = pu;
   P.col[ebase + cr - 1] = c;
-  const bool internal = P.cnt[peer] != 0;
-  P.flags[c] = (P.live[peer] ? kNodeLive : 0) | (internal ? kNodeInternal : 0);
-  return internal;
+  const uint32_t dg = P.cnt[peer];
+  P.ndeg[c] = dg;
+  P.nkat[c] = P.koff[peer];
+  P.flags[c] = (P.live[peer] ? kNodeLive : 0) | (dg ? kNodeInternal : 0);
+  return dg != 0;
 }
 
 // A parent node's CSR row and first child (topic-relative child start cs)
@@ -197,19 +199,19 @@ __device__ __forceinline__ void place_close(const PlaceArgs& P, uint32_t nbase, 
 }
 
 // The root and the small top levels of one topic in ONE block: each level d
-// = 1 .. d_limit - 1 whose parents number at most kBuildSmallLevel, from the
+// = 1 .. d_limit - 1 whose parents number at most kBuildTopLevel, from the
 // parents' fan-out scanned in LDS, children flattened in parent order (a
 // binary search finds each child's parent).  Stops at the first larger level
 // (the look-back launches take over) or when the tree ends.
-constexpr uint32_t kSmallB = 1024;
-constexpr uint32_t kSmallPer = kBuildSmallLevel / kSmallB;
+constexpr uint32_t kSmallB = kBuildTopLevel;
+constexpr uint32_t kSmallPer = 1;  // parents per thread
 
 __device__ __forceinline__ uint32_t load_agent(const uint32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(kSmallB) void k_place_top(PlaceArgs P, uint32_t d_limit) {
-  __shared__ uint32_t off[kBuildSmallLevel + 1];
+  __shared__ uint32_t off[kBuildTopLevel + 1];
   __shared__ uint32_t wsum[kSmallB / 64];
   __shared__ uint32_t red[kSmallB / 64];
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -221,6 +223,8 @@ __global__ __launch_bounds__(kSmallB) void k_place_top(PlaceArgs P, uint32_t d_l
     P.local[r] = nbase;
     P.node_parent[nbase] = kNoneP;
     const bool internal = P.cnt[r] != 0;
+    P.ndeg[nbase] = P.cnt[r];
+    P.nkat[nbase] = P.koff[r];
     P.flags[nbase] = kNodeLive | (internal ? kNodeInternal : 0);  // roots forward (they are not recipients)
     P.lvl[0] = 0;
     P.lvl[1] = 1;
@@ -237,14 +241,14 @@ __global__ __launch_bounds__(kSmallB) void k_place_top(PlaceArgs P, uint32_t d_l
   uint32_t plo = 0, lo = 1, mdeg = 0;
   for (uint32_t d = 1; d < d_limit; ++d) {
     const uint32_t np = lo - plo;
-    if (np == 0 || np > kBuildSmallLevel) break;
+    if (np == 0 || np > kBuildTopLevel) break;
     // exclusive scan of the parents' fan-out: kSmallPer per thread, then waves
     uint32_t v[kSmallPer];
     uint32_t run = 0;
 #pragma unroll
     for (uint32_t k = 0; k < kSmallPer; ++k) {
       const uint32_t j = tid * kSmallPer + k;
-      v[k] = j < np ? P.cnt[load_agent(P.node_peer + nbase + plo + j)] : 0u;
+      v[k] = j < np ? load_agent(P.ndeg + nbase + plo + j) : 0u;
       run += v[k];
     }
     uint32_t incl = run;
@@ -283,8 +287,7 @@ __global__ __launch_bounds__(kSmallB) void k_place_top(PlaceArgs P, uint32_t d_l
         else
           b = mid - 1;
       }
-      const uint32_t pp = load_agent(P.node_peer + nbase + plo + a);
-      const uint32_t peer = P.kids[P.koff[pp] + (k - off[a])];
+      const uint32_t peer = P.kids[load_agent(P.nkat + nbase + plo + a) + (k - off[a])];
       n_int += place_child(P, nbase, ebase, lo + k, nbase + plo + a, peer) ? 1u : 0u;
     }
     n_int = __reduce_add_sync(~0ull, n_int);
@@ -345,9 +348,8 @@ __global__ __launch_bounds__(kB) void k_place_lb(PlaceArgs P, uint32_t d, uint64
   const uint32_t j0 = tile * kB + tid;
   const uint32_t u = nbase + plo + j0;
   const bool valid = j0 < np;
-  const uint32_t pp = valid ? P.node_peer[u] : 0u;
-  const uint32_t dg = valid ? P.cnt[pp] : 0u;
-  peer_s[tid] = pp;
+  const uint32_t dg = valid ? P.ndeg[u] : 0u;
+  peer_s[tid] = valid ? P.nkat[u] : 0u;  // (the parent's first child in kids)
   uint32_t inc = dg;
 #pragma unroll
   for (int sh = 1; sh < 64; sh <<= 1) {
@@ -411,7 +413,7 @@ __global__ __launch_bounds__(kB) void k_place_lb(PlaceArgs P, uint32_t d, uint64
         a = mid + 1;
     }
     const uint32_t rank = k - (a ? incl_s[a - 1] : 0u);
-    const uint32_t peer = P.kids[P.koff[peer_s[a]] + rank];
+    const uint32_t peer = P.kids[peer_s[a] + rank];
     n_int += place_child(P, nbase, ebase, lo + prefix + k, nbase + plo + tile * kB + a, peer) ? 1u : 0u;
   }
   n_int = __reduce_add_sync(~0ull, n_int);

@@ -17,7 +17,11 @@ namespace psamd {
 
 constexpr uint32_t kBuildMaxDepth = 255;  // levels of the level tables
 constexpr uint32_t kBuildPeerBits = 28;   // peer ids below 2^28 (the GPU build's bound)
-constexpr uint32_t kBuildSmallLevel = 8192;  // levels placed by the one-block kernel
+constexpr uint32_t kBuildSmallLevel = 8192;  // the one-block kernel's LDS scan capacity
+// levels whose parents number at most this many are placed by the one-block
+// kernel (its levels are latency chains: 512 was the best cut of 0 / 512 /
+// 2048 / 8192 in round 4, and 8192 cost 0.24 ms per cfg5 rebuild here)
+constexpr uint32_t kBuildTopLevel = 512;
 
 // Pair value of an Orphan peer (not subscribed: no upstream; its subtree is
 // cut for good, rule Q5): par[p] = kNone, orph[p] = 1.
@@ -57,6 +61,11 @@ struct PlaceArgs {
   uint32_t* col;
   uint32_t* first;
   uint8_t* flags;
+  // node space, written with each placed node for the next level's pass
+  // (coalesced there, instead of a dependent random read of the peer's):
+  // its fan-out and the index of its first child in kids
+  uint32_t* ndeg;
+  uint32_t* nkat;
   uint32_t* lvl;  // this topic's table: [d] level start (topic-relative), [256 + d] internal nodes
   uint32_t* gst;  // this topic's stat words
   uint32_t* tb;   // [2 a] node base, [2 a + 1] edge base of active topic a (a + 1's written at the end)

@@ -520,6 +520,8 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   HIP_TRY(e->d_node_parent.ensure(cap * 4), "alloc node_parent");
   HIP_TRY(e->d_node_flags.ensure(((cap + 15) / 16) * 16 + 16), "alloc node_flags");
   HIP_TRY(e->d_first.ensure(cap * 4), "alloc first child");
+  HIP_TRY(e->d_ndeg.ensure(cap * 4), "alloc node fan-out");
+  HIP_TRY(e->d_nkat.ensure(cap * 4), "alloc node child index");
   HIP_TRY(e->d_local.ensure(static_cast<size_t>(n) * 4), "alloc local ids");
   HIP_TRY(e->d_live.ensure(n), "alloc live mask");
   HIP_TRY(hipMemcpyAsync(e->d_live.p, e->live.data(), n, hipMemcpyHostToDevice, s), "upload live");
@@ -603,6 +605,8 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
       P.col = e->d_col.as<uint32_t>();
       P.first = e->d_first.as<uint32_t>();
       P.flags = e->d_node_flags.as<uint8_t>();
+      P.ndeg = e->d_ndeg.as<uint32_t>();
+      P.nkat = e->d_nkat.as<uint32_t>();
       P.lvl = e->d_lvl.as<uint32_t>() + 512 * static_cast<size_t>(t);
       P.gst = gstat + static_cast<size_t>(t) * kGstWords;
       P.tb = e->d_tb.as<uint32_t>();
@@ -691,8 +695,8 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
       T.level_internal[d] = lh[512 * t + 256 + d];
     }
     T.level_off[T.depth + 1] = T.n_nodes;
-    // the levels the top kernel places (parents of at most kBuildSmallLevel)
-    while (T.top_levels <= T.depth && T.level_off[T.top_levels] - T.level_off[T.top_levels - 1] <= kBuildSmallLevel)
+    // the levels the top kernel places (parents of at most kBuildTopLevel)
+    while (T.top_levels <= T.depth && T.level_off[T.top_levels] - T.level_off[T.top_levels - 1] <= kBuildTopLevel)
       ++T.top_levels;
     T.level_local.assign(T.depth + 1, 0);
     for (uint32_t d = 0; d <= T.depth; ++d) T.level_local[d] = T.level_off[d + 1] - T.level_off[d];

@@ -1515,18 +1515,22 @@ int run_body(ps_engine* e, ps_stats* stp, bool may_defer) {
       SubscriptionTree::ReachQuery q = [e, &T](const std::vector<uint32_t>& peers, std::vector<uint8_t>& outv) -> int {
         const uint32_t k = static_cast<uint32_t>(peers.size());
         if (!k) return PS_OK;
-        HIP_TRY(e->d_pairs.ensure(static_cast<size_t>(k) * 4 + k + 16), "alloc reach query");
-        uint32_t* dp = e->d_pairs.as<uint32_t>();
+        // (its own stream: the GPU build ended with a stream sync, so the node
+        // space it reads is complete; the window's kernels need not finish)
+        if (!e->qstream) HIP_TRY(hipStreamCreateWithFlags(&e->qstream, hipStreamNonBlocking), "query stream");
+        hipStream_t qs = e->qstream;
+        HIP_TRY(e->d_query.ensure(static_cast<size_t>(k) * 4 + k + 16), "alloc reach query");
+        uint32_t* dp = e->d_query.as<uint32_t>();
         uint8_t* dout = reinterpret_cast<uint8_t*>(dp + k);
-        HIP_TRY(hipMemcpyAsync(dp, peers.data(), static_cast<size_t>(k) * 4, hipMemcpyHostToDevice, e->stream),
+        HIP_TRY(hipMemcpyAsync(dp, peers.data(), static_cast<size_t>(k) * 4, hipMemcpyHostToDevice, qs),
                 "upload reach query");
         const size_t toff = static_cast<size_t>(&T - e->topics.data()) * e->cfg.n_peers;
         HIP_TRY(launch_reach_query(dp, k, e->cfg.n_peers, e->d_local.as<uint32_t>(), e->d_node_peer.as<uint32_t>(),
                                    T.nbase, T.n_nodes, e->d_tpar.as<uint32_t>() + toff, e->d_orph.as<uint8_t>() + toff,
-                                   T.tree.root(), dout, e->stream),
+                                   T.tree.root(), dout, qs),
                 "reach query");
-        HIP_TRY(hipMemcpyAsync(outv.data(), dout, k, hipMemcpyDeviceToHost, e->stream), "read reach query");
-        HIP_TRY(hipStreamSynchronize(e->stream), "sync");
+        HIP_TRY(hipMemcpyAsync(outv.data(), dout, k, hipMemcpyDeviceToHost, qs), "read reach query");
+        HIP_TRY(hipStreamSynchronize(qs), "sync");
         if (e->host_timing)
           std::fprintf(stderr, "[psengine] prune reach query: %u parents, done at %.3f ms\n", k,
                        std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - e->t_run0).count());
