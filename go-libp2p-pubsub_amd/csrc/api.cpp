@@ -506,6 +506,7 @@ int ps_set_live(ps_engine* e, const uint8_t* live) {
   if (!e || !live) return PS_E_INVAL;
   for (uint32_t p = 0; p < e->cfg.n_peers; ++p) e->live[p] = live[p] ? 1 : 0;
   e->flags_dirty = true;
+  e->live_dev_valid = false;
   return PS_OK;
 }
 

@@ -272,12 +272,14 @@ struct ps_engine {
   bool gpu_build_on = true;
   bool gpu_graph = false;     // the current node space was built on the GPU
   bool mirrors_valid = true;  // host copies of node_peer / flags / CSR are current
-  std::vector<uint32_t> pairs_host, gstat_host, lvl_host, roots_host;
+  std::vector<uint32_t> pairs_host, gstat_host, roots_host;
+  bool live_dev_valid = false;  // d_live holds `live` (uploaded again only after ps_set_live)
+  bool flags_built = false;     // the last GPU build wrote the node flags (no flags pass needed)
   uint32_t* pairs_pinned = nullptr;  // pinned staging of the parent deltas
   size_t pairs_pinned_cap = 0;       // (u32 words)
   std::vector<size_t> pair_off;
-  psamd::DevBuf d_tpar, d_orph, d_local, d_first, d_lvl,
-      d_gstat, d_cub, d_pairs, d_live, d_roots, d_cnt, d_fidx, d_childoff, d_lbstat, d_sigctr, d_kids, d_big, d_tb, d_ndeg, d_nkat, d_query;
+  psamd::DevBuf d_tpar, d_orph, d_local, d_first,
+      d_gstat, d_cub, d_pairs, d_live, d_roots, d_cnt, d_fidx, d_childoff, d_lbstat, d_sigctr, d_kids, d_big, d_ndeg, d_nkat, d_query;
   std::chrono::steady_clock::time_point t_run0;
   // k_flood: a single-rank level window's leading rounds in
   // one persistent launch; PSAMD_FLOOD=0 runs per-round launches instead

@@ -78,6 +78,13 @@ __global__ __launch_bounds__(kB) void k_reach_query(const uint32_t* __restrict__
 
 // ---- by-parent CSR BFS rebuild -----------
 
+__global__ __launch_bounds__(kB) void k_clear(ClearRegions r) {
+  for (uint32_t k = 0; k < r.n; ++k)
+    for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kB + threadIdx.x; i < r.words[k];
+         i += static_cast<uint64_t>(gridDim.x) * kB)
+      r.p[k][i] = 0;
+}
+
 // cnt[v] += 1 for every peer p whose upstream v is a peer (histogram of the
 // parent array)
 __global__ __launch_bounds__(kB) void k_kid_count(const uint32_t* __restrict__ par, uint32_t n,
@@ -428,14 +435,16 @@ __global__ __launch_bounds__(kB) void k_place_lb(PlaceArgs P, uint32_t d, uint64
 }  // namespace
 
 
+hipError_t launch_clear(const ClearRegions& r, hipStream_t s) {
+  if (r.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_clear, dim3(1024), dim3(kB), 0, s, r);
+  return hipGetLastError();
+}
+
 hipError_t build_kids(const uint32_t* par, uint32_t n, uint32_t* cnt, uint32_t* koff, uint32_t* fill, uint32_t* kids,
                       uint32_t* big, uint32_t* n_big, void* temp, size_t temp_bytes, hipStream_t s) {
-  hipError_t e = hipMemsetAsync(cnt, 0, (static_cast<size_t>(n) + 1) * 4, s);
-  if (e == hipSuccess) e = hipMemsetAsync(fill, 0, static_cast<size_t>(n) * 4, s);
-  if (e == hipSuccess) e = hipMemsetAsync(n_big, 0, 4, s);
-  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_kid_count, dim3(blocks(n)), dim3(kB), 0, s, par, n, cnt);
-  e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, cnt, koff, n + 1, s);
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, cnt, koff, n + 1, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_kid_scatter, dim3(blocks(n)), dim3(kB), 0, s, par, n, koff, fill, kids);
   hipLaunchKernelGGL(k_kid_sort, dim3(blocks(n)), dim3(kB), 0, s, koff, cnt, n, kids, big, n_big);

@@ -73,8 +73,18 @@ struct PlaceArgs {
   uint32_t a, root;
   uint16_t topic;
 };
+// Zeroes up to 8 regions of u32 words in one launch (the build's scratch and
+// stat block: one launch instead of a fill per buffer)
+struct ClearRegions {
+  uint32_t* p[8];
+  uint64_t words[8];
+  uint32_t n;
+};
+hipError_t launch_clear(const ClearRegions& r, hipStream_t s);
+
 // peer-space CSR of one topic's parent array (temp: the scan's, queried with
 // scan_u32 over n + 1 entries; cnt has n + 1 entries)
+// (cnt, fill and *n_big zeroed by the caller)
 hipError_t build_kids(const uint32_t* par, uint32_t n, uint32_t* cnt, uint32_t* koff, uint32_t* fill, uint32_t* kids,
                       uint32_t* big, uint32_t* n_big, void* temp, size_t temp_bytes, hipStream_t s);
 // the root and the top levels of at most kBuildSmallLevel parents each, levels < d_limit

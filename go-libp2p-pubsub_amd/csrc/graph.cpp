@@ -523,8 +523,11 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   HIP_TRY(e->d_ndeg.ensure(cap * 4), "alloc node fan-out");
   HIP_TRY(e->d_nkat.ensure(cap * 4), "alloc node child index");
   HIP_TRY(e->d_local.ensure(static_cast<size_t>(n) * 4), "alloc local ids");
-  HIP_TRY(e->d_live.ensure(n), "alloc live mask");
-  HIP_TRY(hipMemcpyAsync(e->d_live.p, e->live.data(), n, hipMemcpyHostToDevice, s), "upload live");
+  {
+    bool fresh = false;
+    HIP_TRY(e->d_live.ensure(n, &fresh), "alloc live mask");
+    if (fresh) e->live_dev_valid = false;
+  }
   // the peer-space CSR scratch (one topic at a time)
   HIP_TRY(e->d_cnt.ensure((static_cast<size_t>(n) + 1) * 4), "alloc fan-out by peer");
   HIP_TRY(e->d_childoff.ensure((static_cast<size_t>(n) + 1) * 4), "alloc child offsets");
@@ -534,14 +537,22 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   size_t scan_bytes = 0;
   HIP_TRY(scan_u32(nullptr, &scan_bytes, nullptr, nullptr, n + 1, s), "scan size");
   HIP_TRY(e->d_cub.ensure(std::max<size_t>(scan_bytes, 16)), "alloc scan temp");
-  HIP_TRY(e->d_gstat.ensure(static_cast<size_t>(nt) * kGstWords * 4 + 16), "alloc build stats");
-  HIP_TRY(e->d_lvl.ensure(static_cast<size_t>(nt) * 512 * 4), "alloc level tables");
-  HIP_TRY(e->d_tb.ensure((2 * static_cast<size_t>(na) + 2) * 4), "alloc topic bases");
+  // one block, one clear and one readback: per-topic stat words, the error
+  // word, per-topic level tables, the active topics' bases
+  const size_t o_err = static_cast<size_t>(nt) * kGstWords, o_lvl = (o_err + 4 + 3) & ~size_t(3),
+               o_tb = o_lvl + static_cast<size_t>(nt) * 512, blk_words = o_tb + 2 * static_cast<size_t>(na) + 2;
+  HIP_TRY(e->d_gstat.ensure(blk_words * 4), "alloc build stats");
   uint32_t* gstat = e->d_gstat.as<uint32_t>();
-  uint32_t* err = gstat + static_cast<size_t>(nt) * kGstWords;
-  auto& gs = e->gstat_host;
-  auto& lh = e->lvl_host;
-  std::vector<uint32_t> tb(2 * na + 2, 0);
+  uint32_t* err = gstat + o_err;
+  auto& blk = e->gstat_host;
+  blk.assign(blk_words, 0);
+  const uint32_t* gs = blk.data();
+  const uint32_t* lh = blk.data() + o_lvl;
+  const uint32_t* tb = blk.data() + o_tb;
+  if (!e->live_dev_valid) {
+    HIP_TRY(hipMemcpyAsync(e->d_live.p, e->live.data(), n, hipMemcpyHostToDevice, s), "upload live");
+    e->live_dev_valid = true;
+  }
   // per topic: the levels the look-back launches take (from the top kernel's
   // last reach to 2 past the last depth: the pass past the deepest level
   // closes its leaves' CSR rows) and each launch's grid, from the last build's
@@ -564,9 +575,6 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
       *fallback = true;
       return PS_OK;
     }
-    HIP_TRY(hipMemsetAsync(e->d_gstat.p, 0, e->d_gstat.bytes, s), "clear build stats");
-    HIP_TRY(hipMemsetAsync(e->d_lvl.p, 0, e->d_lvl.bytes, s), "clear level tables");
-    HIP_TRY(hipMemsetAsync(e->d_tb.p, 0, e->d_tb.bytes, s), "clear topic bases");
     // look-back status words: one region per level launch
     size_t st_words = 0;
     std::vector<std::vector<uint32_t>> grids(nt);
@@ -583,11 +591,30 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
       }
     }
     HIP_TRY(e->d_lbstat.ensure(std::max<size_t>(st_words, 1) * 8), "alloc look-back status");
-    HIP_TRY(hipMemsetAsync(e->d_lbstat.p, 0, std::max<size_t>(st_words, 1) * 8, s), "clear look-back status");
+    {
+      ClearRegions cr{};
+      cr.p[0] = gstat;
+      cr.words[0] = blk_words;
+      cr.p[1] = e->d_lbstat.as<uint32_t>();
+      cr.words[1] = 2 * std::max<size_t>(st_words, 1);
+      cr.n = 2;
+      HIP_TRY(launch_clear(cr, s), "clear build block");
+    }
     uint64_t* lbst = e->d_lbstat.as<uint64_t>();
     for (uint32_t ai = 0; ai < na; ++ai) {
       const uint32_t t = act[ai];
       const TopicHost& T = e->topics[t];
+      {
+        ClearRegions cr{};
+        cr.p[0] = e->d_cnt.as<uint32_t>();
+        cr.words[0] = static_cast<uint64_t>(n) + 1;
+        cr.p[1] = e->d_fidx.as<uint32_t>();
+        cr.words[1] = n;
+        cr.p[2] = e->d_big.as<uint32_t>() + n;
+        cr.words[2] = 1;
+        cr.n = 3;
+        HIP_TRY(launch_clear(cr, s), "clear child-list scratch");
+      }
       HIP_TRY(build_kids(e->d_tpar.as<uint32_t>() + static_cast<size_t>(t) * n, n, e->d_cnt.as<uint32_t>(),
                          e->d_childoff.as<uint32_t>(), e->d_fidx.as<uint32_t>(), e->d_kids.as<uint32_t>(),
                          e->d_big.as<uint32_t>(), e->d_big.as<uint32_t>() + n, e->d_cub.p, e->d_cub.bytes, s),
@@ -607,9 +634,9 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
       P.flags = e->d_node_flags.as<uint8_t>();
       P.ndeg = e->d_ndeg.as<uint32_t>();
       P.nkat = e->d_nkat.as<uint32_t>();
-      P.lvl = e->d_lvl.as<uint32_t>() + 512 * static_cast<size_t>(t);
+      P.lvl = gstat + o_lvl + 512 * static_cast<size_t>(t);
       P.gst = gstat + static_cast<size_t>(t) * kGstWords;
-      P.tb = e->d_tb.as<uint32_t>();
+      P.tb = gstat + o_tb;
       P.err = err;
       P.a = ai;
       P.root = T.root;
@@ -620,13 +647,9 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
         lbst += grids[t][i];
       }
     }
-    gs.assign(static_cast<size_t>(nt) * kGstWords + 4, 0);
-    lh.assign(static_cast<size_t>(nt) * 512, 0);
-    HIP_TRY(hipMemcpyAsync(gs.data(), gstat, gs.size() * 4, hipMemcpyDeviceToHost, s), "read build stats");
-    HIP_TRY(hipMemcpyAsync(lh.data(), e->d_lvl.p, lh.size() * 4, hipMemcpyDeviceToHost, s), "read level tables");
-    HIP_TRY(hipMemcpyAsync(tb.data(), e->d_tb.p, tb.size() * 4, hipMemcpyDeviceToHost, s), "read topic bases");
+    HIP_TRY(hipMemcpyAsync(blk.data(), gstat, blk_words * 4, hipMemcpyDeviceToHost, s), "read build block");
     HIP_TRY(hipStreamSynchronize(s), "sync");
-    const uint32_t ev = gs[static_cast<size_t>(nt) * kGstWords];
+    const uint32_t ev = gs[o_err];
     if (ev & kBuildErrStall) {
       *fallback = true;  // a stalled look-back: build on the host
       return PS_OK;
@@ -678,7 +701,7 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
     T.mesh = false;
     T.root_local = true;
     T.cross.clear();
-    const uint32_t* g = gs.data() + static_cast<size_t>(t) * kGstWords;
+    const uint32_t* g = gs + static_cast<size_t>(t) * kGstWords;
     T.depth = T.n_nodes ? g[kGstDepth] : 0;
     T.max_deg = g[kGstMaxDeg];
     T.level_off.assign(T.depth + 2, 0);
@@ -706,6 +729,7 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
   e->ship_host.clear();
   e->gpu_graph = true;
   e->mirrors_valid = false;
+  e->flags_built = true;  // (node flags from the current live mask: the flags pass can skip them)
   return PS_OK;
 }
 
@@ -791,18 +815,26 @@ int upload_graph(ps_engine* e) {
     ++e->flags_epoch;
     if (e->gpu_graph) {
       const uint32_t n = e->cfg.n_peers;
-      HIP_TRY(e->d_live.ensure(n), "alloc live mask");
+      bool fresh = false;
+      HIP_TRY(e->d_live.ensure(n, &fresh), "alloc live mask");
       HIP_TRY(e->d_roots.ensure(std::max<size_t>(e->roots_host.size(), 1) * 4), "alloc roots");
-      HIP_TRY(hipMemcpyAsync(e->d_live.p, e->live.data(), n, hipMemcpyHostToDevice, e->stream), "upload live");
-      if (!e->roots_host.empty())
-        HIP_TRY(hipMemcpyAsync(e->d_roots.p, e->roots_host.data(), e->roots_host.size() * 4,
-                               hipMemcpyHostToDevice, e->stream),
-                "upload roots");
-      HIP_TRY(launch_node_flags(e->d_node_peer.as<uint32_t>(), e->d_row_ptr.as<uint32_t>(),
-                                e->d_live.as<uint8_t>(), e->n_nodes, e->d_roots.as<uint32_t>(),
-                                static_cast<uint32_t>(e->roots_host.size()), e->d_node_flags.as<uint8_t>(),
-                                e->stream),
-              "node flags");
+      if (fresh || !e->live_dev_valid) {
+        HIP_TRY(hipMemcpyAsync(e->d_live.p, e->live.data(), n, hipMemcpyHostToDevice, e->stream), "upload live");
+        e->live_dev_valid = true;
+      }
+      // (the GPU build wrote every node's flags from this live mask itself)
+      if (!e->flags_built) {
+        if (!e->roots_host.empty())
+          HIP_TRY(hipMemcpyAsync(e->d_roots.p, e->roots_host.data(), e->roots_host.size() * 4,
+                                 hipMemcpyHostToDevice, e->stream),
+                  "upload roots");
+        HIP_TRY(launch_node_flags(e->d_node_peer.as<uint32_t>(), e->d_row_ptr.as<uint32_t>(),
+                                  e->d_live.as<uint8_t>(), e->n_nodes, e->d_roots.as<uint32_t>(),
+                                  static_cast<uint32_t>(e->roots_host.size()), e->d_node_flags.as<uint8_t>(),
+                                  e->stream),
+                "node flags");
+      }
+      e->flags_built = false;
       e->mirrors_valid = false;
     } else {
       build_flags(e);
