@@ -55,6 +55,39 @@ def test_cfg5_scaled_batches_match_oracle(gpu_build):
     eng.close()
 
 
+def test_cfg5_pipelined_churn_matches_oracle():
+    """bench.py's cfg5 loop: batch b's leaves and joins run on the host while
+    batch b - 1's propagation is still in flight (ps_run_async / ps_wait, no
+    hop record so the windows defer); every batch's deliveries equal the
+    oracle's reach on the tree of that batch, and the trees stay the oracle's."""
+    wl = WL.cfg5(20_000, batches=8, per_batch=70)
+    plan = WL.churn_plan(wl, 8)
+    eng = make_engine(wl.n_peers, True, seed=wl.seed)
+    ot = O.Tree(wl.n_peers, 0, 2, 5, PE.Engine.topic_seed(wl.seed, 0))
+    WL.build_engine_topics(eng, wl)
+    ot.join_all(wl.topics[0].join_order)
+    want, got = [], []
+    for b, (leave, join) in enumerate(plan):
+        for p in leave:
+            ot.leave(int(p))
+        try:
+            eng.leave(0, leave)
+        except PE.EngineError:
+            pass
+        st = eng.join(0, join, check=False)
+        for p, s in zip(join, st):
+            assert ot.join(int(p)) == s, (b, p)
+        eng.publish(np.zeros(wl.n_msgs))
+        eng.run_async()
+        want.append(wl.n_msgs * int((ot.message() != 0xFF).sum()))
+        if b:
+            got.append(eng.wait().deliveries)
+        assert np.array_equal(eng.parents(0), ot.parents()), b
+    got.append(eng.wait().deliveries)
+    assert got == want
+    eng.close()
+
+
 def test_gpu_and_host_builds_agree_under_drops():
     """Joins, leaves and abrupt drops (failed-write repairs in BFS order)
     interleaved with publishes: GPU rebuild == host build, message by message
