@@ -167,6 +167,9 @@ static void read_switches(ps_engine* e) {
   if (const char* v = std::getenv("PSAMD_CHAIN_PROFILE")) e->chain_prof_path = v;
   const char* ab = std::getenv("PSAMD_AB");
   if (!ab || std::atoi(ab) == 0) return;
+  if (const char* v = std::getenv("PSAMD_TWIN")) e->twin_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_CHAIN_WORDS_LEAD"))
+    e->chain_words_lead = static_cast<uint32_t>(std::min(1 << 20, std::max(0, std::atoi(v))));
   ps_plan_opts o = current_opts(e);
   if (const char* v = std::getenv("PSAMD_GPU_BUILD")) o.gpu_build = std::atoi(v) != 0;
   if (const char* v = std::getenv("PSAMD_FLOOD")) o.flood = std::atoi(v) != 0;
@@ -312,8 +315,10 @@ void ps_destroy(ps_engine* e) {
   if (e->pstream) (void)hipStreamSynchronize(e->pstream);
   if (e->rstream) (void)hipStreamSynchronize(e->rstream);
   if (e->qstream) (void)hipStreamSynchronize(e->qstream);
+  if (e->tstream) (void)hipStreamSynchronize(e->tstream);
   for (auto ev : e->ev_k) (void)hipEventDestroy(ev);
-  for (hipEvent_t ev : {e->ev_run0, e->ev_run1, e->ev_round, e->ev_xchg, e->ev_gate[0], e->ev_gate[1], e->ev_pre, e->ev_end})
+  for (hipEvent_t ev : {e->ev_run0, e->ev_run1, e->ev_round, e->ev_xchg, e->ev_gate[0], e->ev_gate[1], e->ev_pre, e->ev_end,
+                      e->ev_tend, e->ev_e2t})
     if (ev) (void)hipEventDestroy(ev);
   for (auto& f : e->infl) {
     if (f.ev0) (void)hipEventDestroy(f.ev0);
@@ -328,6 +333,7 @@ void ps_destroy(ps_engine* e) {
   if (e->pstream) (void)hipStreamDestroy(e->pstream);
   if (e->rstream) (void)hipStreamDestroy(e->rstream);
   if (e->qstream) (void)hipStreamDestroy(e->qstream);
+  if (e->tstream) (void)hipStreamDestroy(e->tstream);
   if (e->stream) (void)hipStreamDestroy(e->stream);
   delete e;
 }
@@ -564,6 +570,7 @@ int ps_read_hops(ps_engine* e, uint32_t msg, uint8_t* hop_per_peer) {
 int ps_read_delivered(ps_engine* e, uint32_t msg, uint8_t* out) {
   if (!e || !out) return PS_E_INVAL;
   if (!e->have_window) return e->fail(PS_E_NOTREADY, "no completed run");
+  if (const int rj = twin_join(e)) return rj;  // (the last window may have run on tstream)
   if (msg < e->last_first || msg >= e->last_first + e->last_n) return e->fail(PS_E_RANGE, "message not in the last run");
   const uint32_t i = msg - e->last_first;
   const uint32_t t = e->last_msgs[i].topic;
@@ -613,6 +620,7 @@ int ps_read_peer_messages(ps_engine* e, uint32_t topic, uint32_t peer, uint32_t*
   if (!e || !n_out || (cap && !msg_out)) return PS_E_INVAL;
   *n_out = 0;
   if (!e->have_window) return e->fail(PS_E_NOTREADY, "no completed run");
+  if (const int rj = twin_join(e)) return rj;
   if (topic >= e->topics.size() || peer >= e->cfg.n_peers) return e->fail(PS_E_RANGE, "topic or peer out of range");
   const TopicDev& d = e->last_topics[topic];
   if (!d.W || !e->last_cnt[topic]) return PS_OK;
@@ -678,6 +686,7 @@ int ps_overlapped_windows(ps_engine* e, uint64_t* count_out) {
 int ps_seen_digest(ps_engine* e, uint64_t* digest_out) {
   if (!e || !digest_out) return PS_E_INVAL;
   if (!e->have_window) return e->fail(PS_E_NOTREADY, "no completed run");
+  if (const int rj = twin_join(e)) return rj;
   HIP_TRY(hipMemsetAsync(e->d_digest.p, 0, 8, e->stream), "clear digest");
   HIP_TRY(launch_digest(e->d_seen.as<uint64_t>(), e->d_gen.as<uint8_t>(), e->gen_cur, e->d_node_peer.as<uint32_t>(),
                         e->d_node_topic.as<uint16_t>(),

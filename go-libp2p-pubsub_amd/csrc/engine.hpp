@@ -15,6 +15,7 @@
 #include <map>
 #include <memory>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "dist.hpp"
@@ -63,6 +64,11 @@ struct DevBuf {
     ++gen;
     if (fresh) *fresh = true;
     return hipSuccess;
+  }
+  void swap(DevBuf& o) {
+    std::swap(p, o.p);
+    std::swap(bytes, o.bytes);
+    std::swap(gen, o.gen);
   }
   template <class T>
   T* as() const {
@@ -334,7 +340,8 @@ struct ps_engine {
   uint32_t pad_words = 16;        // rows of at least this many words padded to even (PSAMD_PAD_WORDS)
   bool chain_tail = true;         // a chain ending at the last round may be one round longer (PSAMD_CHAIN_TAIL)
   double launch_bytes = 16e6;     // planner: a launch's ramp and tail as row bytes (PSAMD_LAUNCH_BYTES)
-  uint32_t chain_words = 8192;    // row words per chain wave, the planner's target (PSAMD_CHAIN_WORDS)
+  uint32_t chain_words = 4096;    // row words per chain wave, the planner's target (8192 until r05: cfg4 0.444 -> 0.404, cfg3 -0.5..1 %, profiles/r05/ab/)
+  uint32_t chain_words_lead = 0;  // A/B only (PSAMD_CHAIN_WORDS_LEAD): the same for all but the last launch
   uint32_t chain_waves = 12;      // chain launches: resident waves per CU at most (ps_plan_opts)
   bool chain_nt = true;           // chain launches: level 0 and the inner levels stored non-temporally
   std::vector<uint64_t> chain_fail_key;  // a pair plan whose chain ranges overflowed the level tables: no chains
@@ -424,6 +431,7 @@ struct ps_engine {
     psamd::AlignedSplit split;  // level-aligned windows: the per-round split
     int32_t world = 1;
     std::vector<uint8_t> kinds;  // round_kind of the window
+    hipStream_t stream = nullptr;  // the stream the window's kernels ran on
   };
   Inflight infl[2];
   uint32_t infl_head = 0, infl_count = 0;
@@ -472,6 +480,32 @@ struct ps_engine {
   uint32_t last_slot = 0;          // the slot of the last enqueued window's tables
   psamd::DevBuf d_topics1, d_woff1, d_groups1, d_partials1, d_seeds1;  // slot 1's tables
 
+  // Twin windows.  A pipelined one-rank level window whose
+  // plan is already on the device runs ENTIRELY beside its predecessor: on
+  // the other of two streams (stream / tstream), into the other of two row
+  // sets (seen + arrivals + generation bytes, swapped so that d_seen & co.
+  // always name the last window's), with its own slot's tables and signal
+  // counter.  Nothing the two share is written by either (node space, plan
+  // tables, reach pieces are read-only; uploads make a window a non-twin).
+  // Work on `stream` that changes shared state first waits for tstream's
+  // last window (twin_join); a twin window on tstream first waits for work
+  // `stream` did since tstream last followed it (e_seq).  PSAMD_TWIN=0: off.
+  bool twin_on = true;
+  hipStream_t tstream = nullptr;
+  hipEvent_t ev_tend = nullptr, ev_e2t = nullptr;
+  bool t_pending = false;            // tstream ran a window `stream` has not waited for
+  uint64_t e_seq = 1, t_seq = 0;     // shared-state work on `stream` / the last that tstream followed
+  hipStream_t last_win_stream = nullptr;
+  psamd::DevBuf d_seen_b, d_arr0_b, d_arr1_b, d_gen_b;  // the other row set
+  uint32_t gen_cur_b = 0;
+  void swap_row_sets() {
+    d_seen.swap(d_seen_b);
+    d_arr0.swap(d_arr0_b);
+    d_arr1.swap(d_arr1_b);
+    d_gen.swap(d_gen_b);
+    std::swap(gen_cur, gen_cur_b);
+  }
+
   int fail(int code, const std::string& m) {
     err = m;
     return code;
@@ -500,6 +534,9 @@ int build_graph(ps_engine* e);  // host node space (any rank count); no device c
 void build_flags(ps_engine* e);
 int ensure_mirrors(ps_engine* e);
 int upload_graph(ps_engine* e);
+// run.cpp: the engine stream waits for tstream's last twin window (a no-op
+// when none is pending); every change of shared device state goes after it
+int twin_join(ps_engine* e);
 
 // plan.cpp (host only: no device calls)
 int plan_window_layout(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<WinSlice>& win,

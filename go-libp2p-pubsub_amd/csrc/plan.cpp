@@ -321,6 +321,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   key.push_back(e->chain_max);
   key.push_back(e->chain_max_groups);
   key.push_back(e->chain_words);
+  key.push_back(e->chain_words_lead);
   key.push_back(static_cast<uint64_t>(e->launch_bytes));
   key.push_back(e->chain_tail ? 1 : 0);
   for (size_t q = 0; q < xchg.size(); ++q) key.push_back(xchg[q].any);
@@ -368,7 +369,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
     uint32_t R = 0, S = 0;  // R = 0: no chain of this length
   };
   constexpr uint32_t stage_w = kChainWords, cap = kChainCap;
-  auto chain_size = [&](const TopicHost& T, uint32_t d, uint32_t levels, uint32_t W) {
+  auto chain_size = [&](const TopicHost& T, uint32_t d, uint32_t levels, uint32_t W, uint32_t words) {
     ChainSize z;
     const double n0 = static_cast<double>(T.level_off[d + 1] - T.level_off[d]);
     if (n0 == 0) {  // no node of the level on this rank: nothing to cut
@@ -386,7 +387,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
     z.S = W <= stage_w ? W : stage_w;
     const double r = std::min({static_cast<double>(kChainPar), static_cast<double>(stage_w / z.S),
                                std::floor(cap / 2 / gmax),
-                               std::floor(static_cast<double>(e->chain_words) / (z.S * gsum))});
+                               std::floor(static_cast<double>(words) / (z.S * gsum))});
     z.R = static_cast<uint32_t>(std::max(1.0, r));
     // (Rejected in round 4, profiles/r04/ab/NOTES.md: one-node runs of huge
     // subtrees cut into column slices for parallelism -- cfg2 0.0536 either
@@ -424,6 +425,10 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
   uint32_t last_r = 0;
   for (uint32_t q = 1; q <= rounds && q < e->pull.bytes.size(); ++q)
     if (e->pull.bytes[q]) last_r = q;
+  // (A/B: the launches before the window's last one sized by chain_words_lead)
+  auto words_of = [&](uint32_t q, uint32_t len) {
+    return e->chain_words_lead && q + len - 1 < last_r ? e->chain_words_lead : e->chain_words;
+  };
   auto can_chain = [&](uint32_t q, uint32_t len) {
     const bool tail = e->chain_tail && len == max_len + 1 && q + len - 1 == last_r && max_len >= 3;
     if (!chains_ok || (len > max_len && !tail) || len > kChainLevels || q + len - 1 > rounds || exch(q)) return false;
@@ -431,7 +436,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
       if (exch(q + k)) return false;
     bool ok = true;
     chain_parts(q, len, [&](uint32_t t, uint32_t gi, uint32_t d, uint32_t, uint32_t levels) {
-      ok = ok && chain_size(e->topics[t], d, levels, block_w(tab[t], L.groups[t][gi])).R > 0;
+      ok = ok && chain_size(e->topics[t], d, levels, block_w(tab[t], L.groups[t][gi]), words_of(q, len)).R > 0;
     });
     return ok;
   };
@@ -482,7 +487,7 @@ bool plan_pair_chunks(ps_engine* e, const WindowLayout& L, uint32_t first) {
         const TopicHost& T = e->topics[t];
         const StartGroup& g = L.groups[t][gi];
         const uint32_t W = block_w(tab[t], g);
-        const ChainSize z = chain_size(T, d, levels, W);
+        const ChainSize z = chain_size(T, d, levels, W, words_of(q, len));
         const uint64_t row0 = block_row0(tab[t], g);
         const uint32_t lo = T.level_off[d], hi = T.level_off[d + 1];
         for (uint32_t u = lo; u < hi; u += z.R)

@@ -145,6 +145,13 @@ int flush_reduce(ps_engine* e) {
   return PS_OK;
 }
 
+int twin_join(ps_engine* e) {
+  if (!e->t_pending) return PS_OK;
+  HIP_TRY(hipStreamWaitEvent(e->stream, e->ev_tend, 0), "twin join");
+  e->t_pending = false;
+  return PS_OK;
+}
+
 namespace {
 
 int stage_uploads(ps_engine* e, const Upload* ups, size_t n, hipStream_t s, StageCopy* fold = nullptr,
@@ -274,6 +281,11 @@ void chain_profile_dump(ps_engine* e, uint32_t planned0) {
 int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<WinSlice>& win, ps_stats* st) {
   const auto t_g0 = std::chrono::steady_clock::now();
   const uint64_t epochs0 = e->graph_epoch ^ (e->flags_epoch << 32);
+  if (e->graph_dirty || e->flags_dirty) {  // (the node space a twin window on tstream may still read)
+    const int rj = twin_join(e);
+    if (rj) return rj;
+    ++e->e_seq;
+  }
   int rc = upload_graph(e);
   if (rc) return rc;
   // the per-window device tables of this run's slot: a pipelined window's
@@ -427,6 +439,10 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     // (nothing re-uploaded: the plan the previous window ran, a condition of the overlap)
     fresh = e->pull.version == e->pull_up && e->pair.version == e->pair_up &&
             (!flood_rounds || e->flood.version == e->flood_up);
+    if (!fresh || (world > 1 && gch)) {  // (plan tables a twin window on tstream may still read)
+      if ((rc = twin_join(e))) return rc;
+      ++e->e_seq;
+    }
     if ((rc = upload_pull(e)) || (rc = upload_pair(e, &chain_overflow))) return rc;
     if (chain_overflow) {  // a subtree wider than the level tables: this plan runs without chains
       e->chain_fail_key = e->pair.key;
@@ -553,10 +569,14 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // prefix may restamp those levels' generation bytes beside this window's
   // remaining launches), cached per node space, active topic set and P
   uint32_t reach_a = 0;  // pieces of levels <= pre_P
+  bool reach_up = false;  // the pieces were uploaded for this window
   if (L.aligned) {
     std::vector<uint64_t> key{e->graph_epoch, pre_P};
     for (uint32_t t = 0; t < nt; ++t) key.push_back(L.split.seg_lo[t]);
     if (key != e->reach_key) {
+      if ((rc = twin_join(e))) return rc;
+      ++e->e_seq;
+      reach_up = true;
       std::vector<ReachPiece>& pc = e->reach_host;
       pc.clear();
       for (int part = 0; part < 2; ++part) {
@@ -590,8 +610,49 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   // (a shallow window -- k_flood leading rounds, nothing but its init to hide
   // -- ends signalled instead: its events cost more than the init, cfg4
   // 0.4472-0.4479 -> 0.4421-0.4425 ms/step, profiles/r04/ab/shallow_signalled.log)
-  const bool pcap = e->overlap_on && level && world == 1 && !any_mesh && !record && !L.multi &&
+  // a twin window (engine.hpp): its plan is on the device already, it ends
+  // signalled, and nothing of it needs the stream order of `stream`.  Only
+  // windows under overlap_min_bytes: a small window is latency bound and its
+  // twin fills the chip (cfg2 0.0486 -> 0.0358 ms/step); two bandwidth-bound
+  // windows side by side only share HBM and the MALL (paced cfg3 1.058 vs
+  // 1.015, cfg4 0.4437 vs 0.4432 ms/step: profiles/r05/ab/twin_*.json) --
+  // those keep the prefix overlap
+  const bool twin = e->twin_on && e->sig_windows && level && world == 1 && !any_mesh && !record &&
+                    !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS)) && flood_rounds == 0 &&
+                    e->defer_last && e->defer_into && planned0 <= PS_MAX_ROUNDS && fresh && !reach_up &&
+                    e->chain_prof_path.empty() && total < e->overlap_min_bytes;
+  const bool pcap = !twin && e->overlap_on && level && world == 1 && !any_mesh && !record && !L.multi &&
                     !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS)) && total >= e->overlap_min_bytes && deep;
+  if (!twin) {
+    if ((rc = twin_join(e))) return rc;  // (it reuses the last window's row set)
+    ++e->e_seq;
+  } else {
+    if (e->pend_reduce.valid && (rc = flush_reduce(e))) return rc;
+    ++e->overlapped;  // (ps_overlapped_windows: it may run beside its predecessor)
+    // the stream the last window did not run on, and the row set it did not write
+    if (!e->tstream) {
+      HIP_TRY(hipStreamCreateWithFlags(&e->tstream, hipStreamNonBlocking), "twin stream");
+      HIP_TRY(hipEventCreateWithFlags(&e->ev_tend, kStreamEvent), "twin events");
+      HIP_TRY(hipEventCreateWithFlags(&e->ev_e2t, kStreamEvent), "twin events");
+    }
+    s = e->last_win_stream == e->stream ? e->tstream : e->stream;
+    if (s == e->tstream && e->t_seq != e->e_seq) {  // shared state `stream` changed since tstream last followed it
+      HIP_TRY(hipEventRecord(e->ev_e2t, e->stream), "event");
+      HIP_TRY(hipStreamWaitEvent(s, e->ev_e2t, 0), "twin wait");
+      e->t_seq = e->e_seq;
+    }
+    const size_t gen_bytes = e->d_gen.bytes;
+    e->swap_row_sets();
+    HIP_TRY(e->d_seen.ensure(wtot * 8), "alloc seen");
+    HIP_TRY(e->d_arr0.ensure(wtot * 8), "alloc arrivals");
+    HIP_TRY(e->d_arr1.ensure(wtot * 8), "alloc arrivals");
+    bool gfresh = false;
+    HIP_TRY(e->d_gen.ensure(gen_bytes, &gfresh), "alloc generations");
+    if (gfresh) {
+      HIP_TRY(hipMemsetAsync(e->d_gen.p, 0, e->d_gen.bytes, s), "clear generations");
+      e->gen_cur = 0;
+    }
+  }
   if (pcap && !e->pstream) {  // (created on first use: multi-rank engines never need them)
     HIP_TRY(hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking), "prefix stream");
     for (hipEvent_t* ev : {&e->ev_gate[0], &e->ev_gate[1], &e->ev_pre})
@@ -608,7 +669,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   e->gate_valid = false;  // (this window records its own gate below)
   // the window's effective plan (ps_stats diagnostics)
   st->prefix_rounds = pcap ? pre_P : 0;
-  st->overlapped += overlap ? 1 : 0;
+  st->overlapped += (overlap || twin) ? 1 : 0;
   st->xchg_path = PS_XCHG_NONE;
   st->plan_max_rounds = 1;
   if (level)
@@ -880,7 +941,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     bool gate_done = false;
     bool reach_a_done = false;
     for (r = flood_rounds + 1; r <= planned0; ++r) {
-      if (s != e->stream && r > pre_P) {  // the prefix is enqueued: the rest follows it on the main stream
+      if (!twin && s != e->stream && r > pre_P) {  // the prefix is enqueued: the rest follows it on the main stream
         HIP_TRY(hipEventRecord(e->ev_pre, s), "event");
         s = e->stream;
         HIP_TRY(hipStreamWaitEvent(s, e->ev_pre, 0), "prefix join");
@@ -1013,7 +1074,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       }
       if (!upfront) HIP_TRY(seed_round(r, a.a_next), "seed");
     }
-    if (s != e->stream) {  // (a prefix never ends a window; kept safe)
+    if (!twin && s != e->stream) {  // (a prefix never ends a window; kept safe)
       HIP_TRY(hipEventRecord(e->ev_pre, s), "event");
       s = e->stream;
       HIP_TRY(hipStreamWaitEvent(s, e->ev_pre, 0), "prefix join");
@@ -1050,18 +1111,19 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     reduce_side = rs != s;
     // a signalled window: the reduce's last block raises its flag
     WindowSignal wsig{};
-    if (sigwin && direct && !reduce_side && s == e->stream) {
-      if (!e->d_sigctr.p) {
-        HIP_TRY(e->d_sigctr.ensure(64), "alloc window counter");
-        HIP_TRY(hipMemsetAsync(e->d_sigctr.p, 0, 64, s), "clear window counter");
+    if (sigwin && direct && !reduce_side && (s == e->stream || twin)) {
+      if (!e->d_sigctr.p) {  // (one counter per slot, a line apart: twin windows reduce side by side)
+        HIP_TRY(e->d_sigctr.ensure(256), "alloc window counter");
+        HIP_TRY(hipMemsetAsync(e->d_sigctr.p, 0, 256, s), "clear window counter");
+        if (s != e->stream) HIP_TRY(hipStreamSynchronize(s), "sync");  // (before `stream`'s windows use it)
       }
       wsig.flag = e->defer_into->sig_dev;
-      wsig.ctr = e->d_sigctr.as<uint32_t>();
+      wsig.ctr = e->d_sigctr.as<uint32_t>() + 32 * slot;
       wsig.seq = ++e->sig_seq;
       e->defer_into->seq = wsig.seq;
     }
     // (beside other windows it writes only the slot's pinned rows, not the shared device rows)
-    if (wsig.flag && e->fuse_reduce && planned0 > 0) {
+    if (wsig.flag && e->fuse_reduce && planned0 > 0 && !twin) {
       // held back for the next window's first launch (k_window_turn); only
       // this slot's buffers and the pinned rows: the shared device stats rows
       // may be reallocated by then, and nobody reads a deferred window's
@@ -1070,11 +1132,17 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       e->pend_reduce.args =
           ReduceArgs{partials, d_woff.as<uint32_t>(), planned0 + reach_rows, nullptr, e->defer_into->hs_dev, wsig};
     } else {
-      HIP_TRY(launch_reduce_rounds(partials, d_woff.as<uint32_t>(), planned0 + reach_rows, reduce_side ? nullptr : stats,
+      // (twin windows reduce side by side: neither writes the shared device rows)
+      HIP_TRY(launch_reduce_rounds(partials, d_woff.as<uint32_t>(), planned0 + reach_rows,
+                                   (reduce_side || twin) ? nullptr : stats,
                                    direct ? e->defer_into->hs_dev : nullptr, wsig, rs),
               "reduce rounds");
     }
     e->defer_into_signalled = wsig.flag != nullptr;
+    if (twin && s == e->tstream) {  // (for twin_join)
+      HIP_TRY(hipEventRecord(e->ev_tend, s), "event");
+      e->t_pending = true;
+    }
   } else {
     e->round_kind.clear();  // (accumulate_window: every round k_expand)
     HIP_TRY(seed_round(0, arr[0]), "seed");
@@ -1133,6 +1201,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   }
   const bool defer = e->defer_last && e->defer_into && !record && !timed && r <= PS_MAX_ROUNDS &&
                      (world == 1 || planned0 <= PS_MAX_ROUNDS);  // the pinned slots hold PS_MAX_ROUNDS + 1 rows
+  e->last_win_stream = s;
   if (!defer) HIP_TRY(hipEventRecord(e->ev_run1, s), "event");
   const auto t_enq = std::chrono::steady_clock::now();
   auto remember = [&]() {
@@ -1175,6 +1244,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     f.mode = mode;
     f.flood_rounds = flood_rounds;
     f.kinds = e->round_kind;
+    f.stream = s;
     remember();
     if (e->host_timing) {
       auto ms = [](auto x, auto y) { return std::chrono::duration<double, std::milli>(y - x).count(); };
@@ -1577,6 +1647,7 @@ int ps_run_async(ps_engine* e) {
   ps_engine::Inflight& f = e->infl[(e->infl_head + e->infl_count) % 2];
   f.st = ps_stats{};
   f.deferred = false;
+  f.stream = nullptr;
   hipEvent_t ev0 = e->ev_run0, ev1 = e->ev_run1;
   e->ev_run0 = f.ev0;  // this run's window events belong to its slot
   e->ev_run1 = f.ev1;
@@ -1590,8 +1661,9 @@ int ps_run_async(ps_engine* e) {
     // reduce on rstream: drain every stream, and let no later window start
     // beside a gate this one recorded
     (void)hipStreamSynchronize(e->stream);
-    for (hipStream_t x : {e->pstream, e->rstream, e->xstream})
+    for (hipStream_t x : {e->pstream, e->rstream, e->xstream, e->tstream})
       if (x) (void)hipStreamSynchronize(x);
+    e->t_pending = false;
     e->gate_valid = false;
     e->upload_shadow.clear();  // (a failed window's staged copies may not have run)
     if (e->pend_reduce.owner == &f) e->pend_reduce.valid = false;  // (its window failed: nobody waits for it)
@@ -1623,7 +1695,7 @@ int ps_wait(ps_engine* e, ps_stats* out) {
     for (uint64_t spin = 0; *flag != f.seq; ++spin) {
       _mm_pause();
       if ((spin & 255) == 255) {
-        const hipError_t q = hipStreamQuery(e->stream);
+        const hipError_t q = hipStreamQuery(f.stream ? f.stream : e->stream);
         if (q != hipSuccess && q != hipErrorNotReady) return e->fail(PS_E_DEVICE, "window: stream failed");
         if (q == hipSuccess && *flag != f.seq) return e->fail(PS_E_DEVICE, "window: completion flag missing");
         const auto us =

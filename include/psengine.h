@@ -210,7 +210,7 @@ typedef struct ps_plan_opts {
   uint32_t chain_max_groups;   /* the same for windows with start groups (6)     */
   uint32_t chain_tail;         /* 1: a chain ending at the last round may take one
                                   round more (1)                                */
-  uint32_t chain_words;        /* row words a chain wave writes, planner target (8192) */
+  uint32_t chain_words;        /* row words a chain wave writes, planner target (4096) */
   uint32_t flood_words;        /* row words per k_flood task (2048)              */
   uint32_t pad_words;          /* rows of at least this many words padded to even (16) */
   uint32_t overlap;            /* 1: pipelined deep windows overlap their leading

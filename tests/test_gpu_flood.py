@@ -283,20 +283,31 @@ def test_cfg3_full_size_dead_mask_against_oracle():
                 assert np.array_equal(got.astype(bool), reach[t]), (t, int(m))
 
 
-def test_cfg3_topology_dead_mask_hops_record_instance():
+@pytest.mark.parametrize("chain", [False, True])
+def test_cfg3_topology_dead_mask_hops_record_instance(chain):
     """The cfg3 topology (1M peers, 64 topics) with the same dead mask, a
     1,200-message Zipf burst in recording mode: (peer, message, hop) of 16
-    sampled messages per topic class equal or_disseminate's."""
+    sampled messages per topic class equal or_disseminate's.  chain: the
+    plan pinned to the production kernel -- flood = 0,
+    k_pull_chain launches from round 1 (the recording variant of the
+    headline's kernel at full topology size)."""
     wl = WL.cfg3()
     msgs = wl.msg_topics[:1200]
-    with PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed, record_hops=True) as eng:
+    plan = {"flood": 0} if chain else {}
+    with PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed, record_hops=True, plan=plan) as eng:
         WL.build_engine_topics(eng, wl)
         parents = [eng.parents(t) for t in range(len(wl.topics))]
         live = _cfg3_dead_mask(wl, parents)
         eng.set_live(live)
         first = eng.publish(msgs)
         st = eng.run()
-        assert st.expand_mode == PE.MODE_FLOOD
+        if chain:
+            kinds = list(st.round_kernel)
+            assert st.expand_mode == PE.MODE_LEVEL_PULL and PE.K_FLOOD not in kinds
+            assert kinds[1] == PE.K_CHAIN, kinds[:st.rounds + 1]  # chains from round 1
+            assert sum(k == PE.K_CHAIN for k in kinds) >= 2  # more than one chain launch
+        else:
+            assert st.expand_mode == PE.MODE_FLOOD
         rng = np.random.default_rng(6)
         for t in (0, 8, 63):
             idx = np.nonzero(msgs == t)[0]

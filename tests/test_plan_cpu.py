@@ -606,7 +606,7 @@ def test_plan_opts_defaults_pinned():
     switch PSAMD_AB=1 is set too."""
     d = PE.default_plan_opts()
     assert d == {"flood_top_bytes": 4 << 20, "overlap_min_bytes": 512 << 20, "launch_bytes": 16_000_000,
-                 "flood": 1, "chain_max": 4, "chain_max_groups": 6, "chain_tail": 1, "chain_words": 8192,
+                 "flood": 1, "chain_max": 4, "chain_max_groups": 6, "chain_tail": 1, "chain_words": 4096,
                  "flood_words": 2048, "pad_words": 16, "overlap": 1, "overlap_min_rounds": 12,
                  "xchg_overlap": -1, "gpu_build": 1, "flood_spin_ticks": 200_000_000, "chain_nt": 1,
                  "chain_waves": 12, "flood_min_rounds": 4, "align_groups": 1}, d

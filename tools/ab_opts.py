@@ -35,8 +35,29 @@ def main():
     args = ap.parse_args()
     variants = json.loads(args.variants)
     wl = WL.CONFIGS[args.workload]()
-    eng = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed)
-    sizes = WL.build_engine_topics(eng, wl)
+    # a variant's "env" (engine switches read at creation, PSAMD_AB=1 set
+    # for it) gets an engine of its own; the others share one
+    engines = {}
+
+    def engine_for(v):
+        env = v.get("env", {})
+        k = json.dumps(env, sort_keys=True)
+        if k not in engines:
+            old = {n: os.environ.get(n) for n in env}
+            os.environ.update({n: str(x) for n, x in env.items()})
+            if env:
+                os.environ["PSAMD_AB"] = "1"
+            e = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed)
+            for n, x in old.items():
+                if x is None:
+                    os.environ.pop(n, None)
+                else:
+                    os.environ[n] = x
+            os.environ.pop("PSAMD_AB", None)
+            engines[k] = (e, WL.build_engine_topics(e, wl))
+        return engines[k]
+
+    eng, sizes = engine_for({})
     expect = wl.expected_deliveries(sizes)
     starts = None
     if args.staggered:
@@ -48,7 +69,8 @@ def main():
     last = [None] * len(variants)
     for rep in range(args.reps):
         for i, v in enumerate(variants):
-            eng.set_plan(**{**base, **v})
+            eng, _ = engine_for(v)
+            eng.set_plan(**{**base, **{k: x for k, x in v.items() if k != "env"}})
             for _ in range(3):  # warm: plans rebuilt, uploads done
                 eng.publish(wl.msg_topics, starts)
                 assert eng.run().deliveries == expect
@@ -77,7 +99,8 @@ def main():
            "variants": [{"opts": v, "ms_per_step": [round(x, 4) for x in r], "median": round(statistics.median(r), 4),
                          "last_window": l} for v, r, l in zip(variants, res, last)]}
     print(json.dumps(out))
-    eng.close()
+    for e, _ in engines.values():
+        e.close()
 
 
 if __name__ == "__main__":
