@@ -287,6 +287,17 @@ struct ps_engine {
   psamd::DevBuf d_tpar, d_orph, d_local, d_first,
       d_gstat, d_cub, d_pairs, d_live, d_roots, d_cnt, d_fidx, d_childoff, d_lbstat, d_sigctr, d_kids, d_big, d_ndeg, d_nkat, d_query;
   std::chrono::steady_clock::time_point t_run0;
+  // the lazy prune's reach queries, enqueued with the GPU rebuild that
+  // precedes the run's last phase (its result comes back with the build's
+  // readback, no round trip of its own); the prune uses a result whose peers
+  // match its question, else asks the GPU itself
+  struct EarlyQuery {
+    uint32_t topic = 0;
+    std::vector<uint32_t> peers;
+    std::vector<uint8_t> out;
+    bool launched = false, ready = false;
+  };
+  std::vector<EarlyQuery> early_q;
   // k_flood: a single-rank level window's leading rounds in
   // one persistent launch; PSAMD_FLOOD=0 runs per-round launches instead
   bool flood_on = true;

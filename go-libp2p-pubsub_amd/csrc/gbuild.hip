@@ -49,9 +49,7 @@ __global__ __launch_bounds__(kB) void k_root_flags(const uint32_t* __restrict__ 
 // (the upward walk of an unreached peer: at most the depth of its cut
 // subtree, <= n_peers hops; the build bounds attached depths by 255)
 __global__ __launch_bounds__(kB) void k_reach_query(const uint32_t* __restrict__ peers, uint32_t n,
-                                                    uint32_t n_peers, const uint32_t* __restrict__ local,
-                                                    const uint32_t* __restrict__ node_peer, uint32_t nbase,
-                                                    uint32_t n_nodes, const uint32_t* __restrict__ par,
+                                                    uint32_t n_peers, const uint32_t* __restrict__ par,
                                                     const uint8_t* __restrict__ orph, uint32_t root,
                                                     uint8_t* __restrict__ out) {
   const uint32_t i = blockIdx.x * kB + threadIdx.x;
@@ -59,18 +57,18 @@ __global__ __launch_bounds__(kB) void k_reach_query(const uint32_t* __restrict__
   const uint32_t p = peers[i];
   uint8_t r = 0;
   if (p < n_peers) {
-    const uint32_t u = local[p];
-    r = u >= nbase && u - nbase < n_nodes && node_peer[u] == p;
-    if (!r) {  // below_orphan (tree.cpp): the first peer without an upstream
-      uint32_t q = p;
-      for (uint32_t h = 0; h < n_peers && q != root; ++h) {
-        const uint32_t up = par[q];
-        if (up >= n_peers) {
-          r = orph[q] ? 2 : 0;
-          break;
-        }
-        q = up;
+    // up the topic's upstream array: the root (the peer holds a node of the
+    // node space: the message reached it), or the first peer without an
+    // upstream (below_orphan, tree.cpp: 2 if it is an Orphan)
+    uint32_t q = p;
+    r = 1;
+    for (uint32_t h = 0; h < n_peers && q != root; ++h) {
+      const uint32_t up = par[q];
+      if (up >= n_peers) {
+        r = orph[q] ? 2 : 0;
+        break;
       }
+      q = up;
     }
   }
   out[i] = r;
@@ -462,12 +460,10 @@ hipError_t launch_place_lb(const PlaceArgs& P, uint32_t d, uint32_t grid, uint64
   return hipGetLastError();
 }
 
-hipError_t launch_reach_query(const uint32_t* peers, uint32_t n, uint32_t n_peers, const uint32_t* local,
-                              const uint32_t* node_peer, uint32_t nbase, uint32_t n_nodes, const uint32_t* par,
+hipError_t launch_reach_query(const uint32_t* peers, uint32_t n, uint32_t n_peers, const uint32_t* par,
                               const uint8_t* orph, uint32_t root, uint8_t* out, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_reach_query, dim3(blocks(n)), dim3(kB), 0, s, peers, n, n_peers, local, node_peer,
-                     nbase, n_nodes, par, orph, root, out);
+  hipLaunchKernelGGL(k_reach_query, dim3(blocks(n)), dim3(kB), 0, s, peers, n, n_peers, par, orph, root, out);
   return hipGetLastError();
 }
 

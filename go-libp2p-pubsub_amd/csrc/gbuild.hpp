@@ -92,12 +92,13 @@ hipError_t launch_place_top(const PlaceArgs& P, uint32_t d_limit, hipStream_t s)
 // level d (grid: the host's estimate of the parent level's tiles; status: grid zeroed words)
 hipError_t launch_place_lb(const PlaceArgs& P, uint32_t d, uint32_t grid, uint64_t* status, hipStream_t s);
 
-// The lazy prune's questions about peers[i] (tree.hpp ReachQuery), from the
-// last GPU build: out[i] = 1 if the peer holds a node of the topic at [nbase,
-// nbase + n_nodes) (the message reached it), else 2 if its upstream path
-// (par, from the peer itself) ends at an Orphan (cut for good), else 0.
-hipError_t launch_reach_query(const uint32_t* peers, uint32_t n, uint32_t n_peers, const uint32_t* local,
-                              const uint32_t* node_peer, uint32_t nbase, uint32_t n_nodes, const uint32_t* par,
+// The lazy prune's questions about peers[i] (tree.hpp ReachQuery), over the
+// topic's upstream array as the GPU build took it (par, orph: peer space):
+// out[i] = 1 if the peer's upstream path reaches the root (it holds a node of
+// the node space: the message reached it), else 2 if the path ends at an
+// Orphan (cut for good), else 0.  (Not the peer -> node map: a peer of several
+// topics maps to its node of the last topic placed.)
+hipError_t launch_reach_query(const uint32_t* peers, uint32_t n, uint32_t n_peers, const uint32_t* par,
                               const uint8_t* orph, uint32_t root, uint8_t* out, hipStream_t s);
 // node flags from the live mask (per peer) and the fan-out; roots[] forced live
 hipError_t launch_node_flags(const uint32_t* node_peer, const uint32_t* row_ptr,

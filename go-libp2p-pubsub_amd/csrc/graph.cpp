@@ -647,6 +647,30 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
         lbst += grids[t][i];
       }
     }
+    // the lazy prune's reach queries over this node space (run.cpp): their
+    // answers come back with the build block, one sync for both
+    {
+      size_t qw = 0;
+      for (const auto& q : e->early_q) qw += q.peers.size() + (q.peers.size() + 3) / 4 + 4;
+      if (qw) HIP_TRY(e->d_query.ensure(qw * 4), "alloc reach query");
+      uint32_t* qp = e->d_query.as<uint32_t>();
+      for (auto& q : e->early_q) {
+        q.launched = q.ready = false;
+        const uint32_t k = static_cast<uint32_t>(q.peers.size());
+        if (!k || std::find(act.begin(), act.end(), q.topic) == act.end()) continue;
+        uint8_t* dout = reinterpret_cast<uint8_t*>(qp + k);
+        HIP_TRY(hipMemcpyAsync(qp, q.peers.data(), static_cast<size_t>(k) * 4, hipMemcpyHostToDevice, s),
+                "upload reach query");
+        const TopicHost& T = e->topics[q.topic];
+        HIP_TRY(launch_reach_query(qp, k, n, e->d_tpar.as<uint32_t>() + static_cast<size_t>(q.topic) * n,
+                                   e->d_orph.as<uint8_t>() + static_cast<size_t>(q.topic) * n, T.root, dout, s),
+                "reach query");
+        q.out.resize(k);
+        HIP_TRY(hipMemcpyAsync(q.out.data(), dout, k, hipMemcpyDeviceToHost, s), "read reach query");
+        q.launched = true;
+        qp += k + (k + 3) / 4 + 4;
+      }
+    }
     HIP_TRY(hipMemcpyAsync(blk.data(), gstat, blk_words * 4, hipMemcpyDeviceToHost, s), "read build block");
     HIP_TRY(hipStreamSynchronize(s), "sync");
     const uint32_t ev = gs[o_err];
@@ -678,6 +702,7 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
     }
     if (!redo) break;
   }
+  for (auto& q : e->early_q) q.ready = q.launched;
   const auto tb3 = clk::now();
   // 3. layout: topic t's nodes at [nbase_t, nbase_t + R_t) (the device's bases)
   e->roots_host.clear();

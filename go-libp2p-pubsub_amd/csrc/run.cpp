@@ -547,6 +547,12 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   uint64_t total = 0;  // the window's row bytes
   if (level)
     for (uint32_t q = 1; q <= planned0 && q < e->pull.bytes.size(); ++q) total += e->pull.bytes[q];
+  // deep windows of at least overlap_min_bytes alternate between the two row
+  // sets (engine.hpp, twin windows): a window's prefix then writes no row its
+  // predecessor's last launch still reads, so the prefix may hold every
+  // launch but the last (the gate: recorded before that launch)
+  const bool alt_plan = e->twin_on && level && world == 1 && deep && flood_rounds == 0 &&
+                        total >= e->overlap_min_bytes;
   if (deep && flood_rounds == 0) {
     std::vector<std::pair<uint32_t, uint32_t>> ls;  // launches: (first round, last round)
     for (uint32_t q = 1; q <= planned0; ++q) {
@@ -562,6 +568,13 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       if (acc + b > total / 64 || ls[i + 1].first != ls[i].second + 1) break;
       acc += b;
       pre_P = ls[i].second;
+    }
+    // alternating row sets (below): every launch but the last is the prefix
+    // -- nothing the predecessor's last launch reads is written by it
+    if (alt_plan && ls.size() >= 2) {
+      bool contiguous = true;
+      for (size_t i = 0; i + 1 < ls.size(); ++i) contiguous = contiguous && ls[i + 1].first == ls[i].second + 1;
+      if (contiguous) pre_P = ls[ls.size() - 2].second;
     }
   }
   // level-aligned: the (topic, level) pieces of k_level_reach, levels <= P
@@ -623,6 +636,23 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
                     e->chain_prof_path.empty() && total < e->overlap_min_bytes;
   const bool pcap = !twin && e->overlap_on && level && world == 1 && !any_mesh && !record && !L.multi &&
                     !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS)) && total >= e->overlap_min_bytes && deep;
+  // this window into the row set the last one did not write (cleared on s
+  // when newly allocated)
+  auto switch_sets = [&](bool* fresh_gen = nullptr) -> int {
+    const size_t gen_bytes = e->d_gen.bytes;
+    e->swap_row_sets();
+    HIP_TRY(e->d_seen.ensure(wtot * 8), "alloc seen");
+    HIP_TRY(e->d_arr0.ensure(wtot * 8), "alloc arrivals");
+    HIP_TRY(e->d_arr1.ensure(wtot * 8), "alloc arrivals");
+    bool gfresh = false;
+    HIP_TRY(e->d_gen.ensure(gen_bytes, &gfresh), "alloc generations");
+    if (gfresh) {
+      HIP_TRY(hipMemsetAsync(e->d_gen.p, 0, e->d_gen.bytes, s), "clear generations");
+      e->gen_cur = 0;
+    }
+    if (fresh_gen) *fresh_gen = gfresh;
+    return PS_OK;
+  };
   if (!twin) {
     if ((rc = twin_join(e))) return rc;  // (it reuses the last window's row set)
     ++e->e_seq;
@@ -641,18 +671,11 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       HIP_TRY(hipStreamWaitEvent(s, e->ev_e2t, 0), "twin wait");
       e->t_seq = e->e_seq;
     }
-    const size_t gen_bytes = e->d_gen.bytes;
-    e->swap_row_sets();
-    HIP_TRY(e->d_seen.ensure(wtot * 8), "alloc seen");
-    HIP_TRY(e->d_arr0.ensure(wtot * 8), "alloc arrivals");
-    HIP_TRY(e->d_arr1.ensure(wtot * 8), "alloc arrivals");
-    bool gfresh = false;
-    HIP_TRY(e->d_gen.ensure(gen_bytes, &gfresh), "alloc generations");
-    if (gfresh) {
-      HIP_TRY(hipMemsetAsync(e->d_gen.p, 0, e->d_gen.bytes, s), "clear generations");
-      e->gen_cur = 0;
-    }
+    if ((rc = switch_sets())) return rc;
   }
+  const bool alt_sets = pcap && alt_plan;
+  bool sets_fresh = false;  // (the other set's generation bytes were just cleared on `stream`)
+  if (alt_sets && (rc = switch_sets(&sets_fresh))) return rc;
   if (pcap && !e->pstream) {  // (created on first use: multi-rank engines never need them)
     HIP_TRY(hipStreamCreateWithFlags(&e->pstream, hipStreamNonBlocking), "prefix stream");
     for (hipEvent_t* ev : {&e->ev_gate[0], &e->ev_gate[1], &e->ev_pre})
@@ -662,7 +685,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   if (pcap)
     gkey = {e->pull.version, e->pair.version, e->flood.version, e->graph_epoch, e->flags_epoch, pre_P,
             flood_rounds, wtot, planned0};
-  const bool overlap = pcap && fresh && e->defer_into && e->gate_valid && e->gate_slot != slot &&
+  const bool overlap = pcap && fresh && !sets_fresh && e->defer_into && e->gate_valid && e->gate_slot != slot &&
                        e->gate_key == gkey && epochs0 == (e->graph_epoch ^ (e->flags_epoch << 32)) &&
                        e->gen_cur + 1 <= 255 && level && !any_mesh &&
                        !(e->cfg.flags & (PS_F_NO_LAZY_SEEN | PS_F_TIME_KERNELS));
@@ -952,7 +975,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
                 "level reach (prefix levels)");
         reach_a_done = true;
       }
-      if (pcap && !gate_done && r > pre_P + 1) {  // the gate launch is enqueued
+      // the gate launch is enqueued (alternating sets: the gate is recorded
+      // before the window's last launch)
+      if (pcap && !gate_done && r > (alt_sets ? pre_P : pre_P + 1)) {
         HIP_TRY(hipEventRecord(e->ev_gate[slot], e->stream), "event");
         e->gate_valid = true;
         e->gate_slot = slot;
@@ -1567,6 +1592,17 @@ int run_body(ps_engine* e, ps_stats* stp, bool may_defer) {
       rest[t] = slice(t, head[t], cnt - head[t]);
       any |= rest[t].n > 0;
     }
+    // the prune's questions, asked with this phase's rebuild (graph.cpp)
+    e->early_q.clear();
+    if (any && e->graph_dirty && e->gpu_build_on)
+      for (uint32_t t = 0; t < nt; ++t) {
+        TopicHost& T = e->topics[t];
+        if (!(T.exists && T.kind == Kind::Join && rest[t].n && T.tree.parts_only_pass())) continue;
+        ps_engine::EarlyQuery q;
+        q.topic = t;
+        q.peers = T.tree.part_parents();
+        if (!q.peers.empty()) e->early_q.push_back(std::move(q));
+      }
     if (any) {
       e->defer_phase = may_defer && !record;
       int rc = run_phase(e, msgs, rest, &st);
@@ -1585,6 +1621,13 @@ int run_body(ps_engine* e, ps_stats* stp, bool may_defer) {
       SubscriptionTree::ReachQuery q = [e, &T](const std::vector<uint32_t>& peers, std::vector<uint8_t>& outv) -> int {
         const uint32_t k = static_cast<uint32_t>(peers.size());
         if (!k) return PS_OK;
+        for (const ps_engine::EarlyQuery& eq : e->early_q)  // answered with the rebuild
+          if (eq.ready && eq.topic == static_cast<uint32_t>(&T - e->topics.data()) && eq.peers.size() == k &&
+              std::equal(peers.begin(), peers.end(), eq.peers.begin())) {
+            outv = eq.out;
+            if (e->host_timing) std::fprintf(stderr, "[psengine] prune reach query: %u parents, from the rebuild\n", k);
+            return PS_OK;
+          }
         // (its own stream: the GPU build ended with a stream sync, so the node
         // space it reads is complete; the window's kernels need not finish)
         if (!e->qstream) HIP_TRY(hipStreamCreateWithFlags(&e->qstream, hipStreamNonBlocking), "query stream");
@@ -1595,9 +1638,8 @@ int run_body(ps_engine* e, ps_stats* stp, bool may_defer) {
         HIP_TRY(hipMemcpyAsync(dp, peers.data(), static_cast<size_t>(k) * 4, hipMemcpyHostToDevice, qs),
                 "upload reach query");
         const size_t toff = static_cast<size_t>(&T - e->topics.data()) * e->cfg.n_peers;
-        HIP_TRY(launch_reach_query(dp, k, e->cfg.n_peers, e->d_local.as<uint32_t>(), e->d_node_peer.as<uint32_t>(),
-                                   T.nbase, T.n_nodes, e->d_tpar.as<uint32_t>() + toff, e->d_orph.as<uint8_t>() + toff,
-                                   T.tree.root(), dout, qs),
+        HIP_TRY(launch_reach_query(dp, k, e->cfg.n_peers, e->d_tpar.as<uint32_t>() + toff,
+                                   e->d_orph.as<uint8_t>() + toff, T.tree.root(), dout, qs),
                 "reach query");
         HIP_TRY(hipMemcpyAsync(outv.data(), dout, k, hipMemcpyDeviceToHost, qs), "read reach query");
         HIP_TRY(hipStreamSynchronize(qs), "sync");
@@ -1611,6 +1653,7 @@ int run_body(ps_engine* e, ps_stats* stp, bool may_defer) {
       e->graph_dirty = true;
     }
   }
+  e->early_q.clear();
   e->have_hops = record;
   if (e->host_timing)
     std::fprintf(stderr, "[psengine] after-message prune %.3f ms (started at %.3f ms)\n",

@@ -327,6 +327,20 @@ int SubscriptionTree::close_host(uint32_t peer) {
   return PS_OK;
 }
 
+const std::vector<uint32_t>& SubscriptionTree::part_parents() {
+  // distinct parents (the pass is order free): marked once, marks reset
+  if (dedup_mark_.size() != n_) dedup_mark_.assign(n_, 0);
+  size_t w = 0;
+  for (uint32_t p : parted_at_)
+    if (p < n_ && !dedup_mark_[p]) {
+      dedup_mark_[p] = 1;
+      parted_at_[w++] = p;
+    }
+  parted_at_.resize(w);
+  for (uint32_t p : parted_at_) dedup_mark_[p] = 0;
+  return parted_at_;
+}
+
 int SubscriptionTree::after_message(const ReachQuery* reach) {
   if (!needs_pass_) return PS_OK;
   if (!pending_failures_) {
@@ -334,18 +348,7 @@ int SubscriptionTree::after_message(const ReachQuery* reach) {
     // entries (subtree.go:329-331), draws nothing from the tie-break stream,
     // so the order does not matter -- visit just the parents holding one,
     // if the message reached them (an In-state path from the root).
-    // distinct parents (the pass is order free): marked once, marks reset
-    {
-      if (dedup_mark_.size() != n_) dedup_mark_.assign(n_, 0);
-      size_t w = 0;
-      for (uint32_t p : parted_at_)
-        if (p < n_ && !dedup_mark_[p]) {
-          dedup_mark_[p] = 1;
-          parted_at_[w++] = p;
-        }
-      parted_at_.resize(w);
-      for (uint32_t p : parted_at_) dedup_mark_[p] = 0;
-    }
+    part_parents();
     // reachability of the message's tree, before this pass mutates anything
     // (the prune below only edits child lists of reached parents and puts Dead
     // children Out: no reached peer's path changes)

@@ -62,6 +62,11 @@ class SubscriptionTree {
   // the tree walks up from each peer.
   using ReachQuery = std::function<int(const std::vector<uint32_t>& peers, std::vector<uint8_t>& out)>;
   int after_message(const ReachQuery* reach = nullptr);
+  // a Parts-only message pass is pending: its distinct Part'ed parents (the
+  // peers after_message will ask `reach` about, deduplicated in place), so
+  // that the engine can ask the GPU before the message runs
+  bool parts_only_pass() const { return needs_pass_ && !pending_failures_; }
+  const std::vector<uint32_t>& part_parents();
   bool has_pending_failures() const { return pending_failures_; }
   // a Part or a host failure happened since the last after_message()
   bool needs_message_pass() const { return needs_pass_; }

@@ -153,6 +153,50 @@ def test_gpu_build_multi_topic_and_live_mask():
     assert out[0] == out[1]
 
 
+def test_gpu_build_prune_queries_shared_peers():
+    """Three Join topics over the same peers, Parts in every topic, then
+    joins: the lazy prune asks the GPU which Part'ed parents each topic's
+    message reached (asked with the rebuild, gbuild.hip k_reach_query), and
+    a peer of several topics must be judged in each topic's own tree -- the
+    GPU-built engine's trees and deliveries equal the host-built engine's
+    (whose prune walks the host trees) after every batch."""
+    rng = np.random.default_rng(23)
+    n = 5000
+    engs = [make_engine(n, g, n_topics=3, seed=12) for g in (True, False)]
+    members = []
+    for t in range(3):
+        m = np.sort(rng.choice(np.arange(1, n), size=3500, replace=False))
+        members.append(set(int(x) for x in m))
+        for e in engs:
+            e.topic_create(t, 0, 2, 5)
+            e.join(t, m)
+    for step in range(8):
+        for t in range(3):
+            cur = sorted(members[t])
+            leave = rng.choice(cur, size=60, replace=False)
+            for e in engs:
+                try:
+                    e.leave(t, leave)
+                except PE.EngineError:
+                    pass
+            members[t] -= {int(x) for x in leave}
+        msgs = np.repeat(np.arange(3, dtype=np.uint32), 40)
+        sts = []
+        for e in engs:
+            e.publish(msgs)
+            sts.append(e.run_async() or e.wait())
+        assert sts[0].deliveries == sts[1].deliveries, step
+        for t in range(3):
+            outs = [p for p in range(1, n) if p not in members[t]]
+            join = rng.choice(outs, size=50, replace=False)
+            res = [e.join(t, join, check=False) for e in engs]
+            assert np.array_equal(res[0], res[1]), (step, t)
+            members[t] |= {int(p) for p, s in zip(join, res[0]) if s == 0}
+            assert np.array_equal(engs[0].parents(t), engs[1].parents(t)), (step, t)
+    for e in engs:
+        e.close()
+
+
 def test_cfg5_full_size_batches_match_oracle():
     """BASELINE cfg5 at its stated size: 1M peers, 90 % members joined by the
     restated protocol, then batches of 1 % graceful leaves (Part + repair,
