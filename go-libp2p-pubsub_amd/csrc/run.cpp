@@ -1303,11 +1303,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   HIP_TRY(hipStreamSynchronize(s), "sync");
   if (mode == PS_MODE_FLOOD && e->flood_profile && e->flood_prof_waves) flood_profile_report(e);
   if (cprof) chain_profile_dump(e, planned0);
-  if (std::string why; L.aligned && !split_aligned_window(st, hs.data(), r, L.true_rounds, L.split, &why)) {
-    if (!std::getenv("PSAMD_SPLIT_WARN"))  // (debug: report and go on)
-      return e->fail(PS_E_DEVICE, "level-aligned window: reach counts disagree with the per-level counters (" + why + ")");
-    std::fprintf(stderr, "[psengine] split mismatch: %s\n", why.c_str());
-  }
+  if (std::string why; L.aligned && !split_aligned_window(st, hs.data(), r, L.true_rounds, L.split, &why))
+    return e->fail(PS_E_DEVICE, "level-aligned window: reach counts disagree with the per-level counters (" + why + ")");
   if (!accumulate_window(st, hs.data(), ha.data(), r, planned0, mode, flood_rounds, launches, world,
                          e->round_kind, !L.aligned)) {
     // a k_flood dependency wait timed out (its waves were not all resident:
@@ -1326,23 +1323,6 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
                  ms2(e->t_run0, t_first), ms2(e->t_run0, t_w0), ms2(t_w0, t_w1), ms2(t_w1, t_w2), ms2(t_w2, t_w3),
                  ms2(t_w3, t_first), ms2(t_first, t_enq), ms2(t_enq, t_sync),
                  ms2(t_sync, std::chrono::steady_clock::now()));
-  }
-  if (std::getenv("PSAMD_CHECK_ROOTS")) {  // (debug) every root row holds exactly its window's messages
-    for (uint32_t t = 0; t < nt; ++t) {
-      const TopicDev& d = tab[t];
-      if (!d.W || !(d.flags & kTopicRootLocal)) continue;
-      std::vector<uint64_t> rr(d.W), sr(d.W);
-      HIP_TRY(hipMemcpy(rr.data(), e->d_arr0.as<uint64_t>() + d.wbase, d.W * 8, hipMemcpyDeviceToHost), "dbg");
-      HIP_TRY(hipMemcpy(sr.data(), e->d_seen.as<uint64_t>() + d.wbase + d.W, d.W * 8, hipMemcpyDeviceToHost), "dbg");
-      uint64_t pa = 0, ps = 0;
-      for (uint32_t w = 0; w < d.W; ++w) {
-        pa += __builtin_popcountll(rr[w]);
-        ps += __builtin_popcountll(sr[w]);
-      }
-      if (pa != win[t].n || ps != win[t].n)
-        std::fprintf(stderr, "[psengine] topic %u: root row %llu bits, node 1 row %llu bits, %u messages (W %u)\n", t,
-                     static_cast<unsigned long long>(pa), static_cast<unsigned long long>(ps), win[t].n, d.W);
-    }
   }
   if (record) {
     {
