@@ -32,7 +32,10 @@ int dist_common(ps_engine* e, const ps_dist_config* dc) {
   if (dc->world < 1 || dc->world > kMaxRanks || dc->rank < 0 || dc->rank >= dc->world)
     return e->fail(PS_E_INVAL, "rank/world out of range (world <= 16)");
   if (dc->partition != PS_PART_PEER && dc->partition != PS_PART_SUBTREE) return e->fail(PS_E_INVAL, "unknown partition");
-  if (dc->flags & ~PS_DIST_F_COPY) return e->fail(PS_E_INVAL, "unknown dist flag");
+  if (dc->flags & ~(PS_DIST_F_COPY | PS_DIST_F_INPLACE)) return e->fail(PS_E_INVAL, "unknown dist flag");
+  if ((dc->flags & PS_DIST_F_COPY) && (dc->flags & PS_DIST_F_INPLACE))
+    return e->fail(PS_E_INVAL, "PS_DIST_F_INPLACE reads rows in place: not with PS_DIST_F_COPY");
+  e->inplace = dc->world > 1 && (dc->flags & PS_DIST_F_INPLACE) != 0;
   if (!e->pending.empty()) return e->fail(PS_E_STATE, "messages pending");
   e->rank = dc->rank;
   e->world = dc->world;
@@ -706,6 +709,8 @@ int ps_dist_unique_id(uint8_t id_out[PS_UNIQUE_ID_BYTES]) {
 
 int ps_dist_init(ps_engine* e, const ps_dist_config* dc, const uint8_t id[PS_UNIQUE_ID_BYTES]) {
   if (!id) return PS_E_INVAL;
+  if (dc && (dc->flags & PS_DIST_F_INPLACE))  // (separate processes: no shared row sets)
+    return e->fail(PS_E_INVAL, "PS_DIST_F_INPLACE needs ranks that share one address space (the loopback)");
   int rc = dist_common(e, dc);
   if (rc) return rc;
   if (dc->world == 1) return PS_OK;
@@ -740,7 +745,8 @@ int ps_dist_init_loopback(ps_engine* e, const ps_dist_config* dc, ps_loopback* l
   if (rc) return rc;
   if (dc->world == 1) return PS_OK;
   if ((rc = dist_streams(e))) return rc;
-  e->transport = make_loopback_transport(lb->g, dc->rank, e->cfg.device, (dc->flags & PS_DIST_F_COPY) != 0);
+  e->transport = make_loopback_transport(lb->g, dc->rank, e->cfg.device, (dc->flags & PS_DIST_F_COPY) != 0,
+                                         (dc->flags & PS_DIST_F_INPLACE) != 0);
   if (!e->transport) return e->fail(PS_E_INVAL, "loopback group size != world");
   refresh_xchg_overlap(e);
   return PS_OK;

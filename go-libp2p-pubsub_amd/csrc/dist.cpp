@@ -90,6 +90,7 @@ struct LoopbackGroup {
                                               // exchange k records read[k & 1]
     hipEvent_t used[kSendBufs] = {};  // zero copy: this rank's launches that read the others'
                                       // regions of round r are done (used[r % kSendBufs])
+    const Transport::Share* share = nullptr;  // in-place rows: published by share()
   };
   std::vector<Slot> slot;
 
@@ -139,8 +140,8 @@ namespace {
 
 class LoopbackTransport final : public Transport {
  public:
-  LoopbackTransport(LoopbackGroup* g, int rank, int device, bool copy)
-      : g_(g), rank_(rank), device_(device), copy_(copy) {
+  LoopbackTransport(LoopbackGroup* g, int rank, int device, bool copy, bool in_place)
+      : g_(g), rank_(rank), device_(device), copy_(copy), in_place_(in_place) {
     (void)hipSetDevice(device_);
     (void)hipEventCreateWithFlags(&sent_, kStreamEvent);
     for (auto& r : read_) (void)hipEventCreateWithFlags(&r, kStreamEvent);
@@ -213,6 +214,15 @@ class LoopbackTransport final : public Transport {
   // PS_DIST_F_COPY (copy_) level mode takes exchange() instead, the RCCL
   // transport's data path: the records land in the receive buffer.
   bool zero_copy() const override { return !copy_; }
+  bool in_place() const override { return in_place_; }
+  hipError_t share(const Share& mine, std::vector<Share>& all, std::string* err) override {
+    g_->slot[rank_].share = &mine;
+    if (!g_->barrier()) return timeout(err);  // every rank published
+    all.assign(g_->world, Share{});
+    for (int q = 0; q < g_->world; ++q) all[q] = *g_->slot[q].share;
+    if (!g_->barrier()) return timeout(err);  // every rank copied (`mine` may go)
+    return hipSuccess;
+  }
   hipError_t exchange_zc(const uint8_t* send, const std::vector<uint64_t>& send_off,
                          std::vector<const uint8_t*>& peer, hipStream_t s, std::string* err) override {
     hipError_t e = hipEventRecord(sent_, s);
@@ -265,16 +275,17 @@ class LoopbackTransport final : public Transport {
   }
   LoopbackGroup* g_;
   int rank_, device_;
-  bool copy_;
+  bool copy_, in_place_;
   hipEvent_t sent_ = nullptr, read_[2] = {nullptr, nullptr}, used_[kSendBufs] = {};
   int parity_ = 0;
 };
 
 }  // namespace
 
-std::unique_ptr<Transport> make_loopback_transport(LoopbackGroup* g, int rank, int device, bool copy) {
+std::unique_ptr<Transport> make_loopback_transport(LoopbackGroup* g, int rank, int device, bool copy,
+                                                  bool in_place) {
   if (!g || rank < 0 || rank >= g->world) return nullptr;
-  return std::make_unique<LoopbackTransport>(g, rank, device, copy);
+  return std::make_unique<LoopbackTransport>(g, rank, device, copy, in_place);
 }
 
 }  // namespace psamd

@@ -76,6 +76,22 @@ class Transport {
     if (err) *err = "zero-copy exchange not supported by this transport";
     return hipErrorNotSupported;
   }
+  // In-place rows (PS_DIST_F_INPLACE; ranks sharing one address space): a
+  // receiver reads a ghost parent's row where its owner wrote it.  share()
+  // swaps every rank's row-set addresses and per-topic layout (host data,
+  // all ranks call it together, at each change of the ghost plan).
+  struct Share {
+    const void* seen = nullptr;
+    const void* gen = nullptr;
+    uint32_t gen_cur = 0;
+    std::vector<uint64_t> topics;  // per topic: wbase, n_nodes, nbase, flags
+  };
+  virtual bool in_place() const { return false; }
+  virtual hipError_t share(const Share& mine, std::vector<Share>& all, std::string* err) {
+    (void)mine, (void)all;
+    if (err) *err = "in-place rows not supported by this transport";
+    return hipErrorNotSupported;
+  }
 };
 
 std::unique_ptr<Transport> make_rccl_transport(int rank, int world, const uint8_t id[128],
@@ -87,6 +103,7 @@ LoopbackGroup* loopback_create(int world);
 void loopback_destroy(LoopbackGroup* g);
 // copy: level mode copies the records into the receive buffer (the RCCL data
 // path) instead of reading them in place (zero copy)
-std::unique_ptr<Transport> make_loopback_transport(LoopbackGroup* g, int rank, int device, bool copy);
+std::unique_ptr<Transport> make_loopback_transport(LoopbackGroup* g, int rank, int device, bool copy,
+                                                  bool in_place = false);
 
 }  // namespace psamd

@@ -221,6 +221,7 @@ struct GhostRound {
   uint32_t pack0 = 0, pack1 = 0;                     // the round's root segments (k_pack)
   uint64_t pack_units = 0;                           // their units (k_pack's stream)
   bool any = false;                                  // some rank ships rows this round (same on every rank)
+  uint64_t rec_bytes = 0;                            // record bytes this rank receives (in place: roots' only)
 };
 struct GhostPlan {
   std::vector<uint64_t> key;
@@ -389,6 +390,10 @@ struct ps_engine {
 
   // multi-GPU: this engine owns a hash-partitioned share of every topic
   int32_t rank = 0, world = 1;
+  bool inplace = false;  // PS_DIST_F_INPLACE: kSegInPlace segments, RankRows of every rank
+  psamd::DevBuf d_rrows;
+  std::vector<psamd::RankRows> rrows_host;
+  bool rrows_dirty = false;
   uint32_t partition = PS_PART_PEER, split_depth = 0;
   std::unique_ptr<psamd::Transport> transport;
 

@@ -274,17 +274,22 @@ int build_graph(ps_engine* e) {
               nxt_local[a].push_back(v);
               continue;
             }
+            // PS_DIST_F_INPLACE: below the root a ghost parent is addressed by
+            // its topic-relative id at its owner (its row is read there); the
+            // roots' rows still ship as records (their seeded row)
+            const bool in_place = e->inplace && d >= 1;
             if (!(mask >> b & 1u)) {
               mask |= 1u << b;
               kk[b] = gc[a * world + b]++;
               if (kk[b] > kRemoteIdMask) return e->fail(PS_E_NOMEM, "ghost rows of one level exceed 2^27");
-              if (a == me) {
+              if (a == me && !in_place) {
                 e->ship_host.push_back(ShipEntry{T.nbase + loc[u], static_cast<uint32_t>(b) << kRemoteRankShift | kk[b]});
                 T.send_node.push_back(T.nbase + loc[u]);
                 T.send_dst.push_back(static_cast<uint32_t>(b) << kRemoteRankShift | kk[b]);
               }
             }
-            ghost_of[v] = static_cast<uint32_t>(a) << kRemoteRankShift | kk[b];
+            if (in_place && loc[u] > kRemoteIdMask) return e->fail(PS_E_NOMEM, "a rank's topic exceeds 2^27 nodes");
+            ghost_of[v] = static_cast<uint32_t>(a) << kRemoteRankShift | (in_place ? loc[u] : kk[b]);
             nxt_ghost[static_cast<size_t>(b) * W + a].push_back(v);
           }
         }

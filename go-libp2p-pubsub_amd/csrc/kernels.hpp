@@ -173,9 +173,21 @@ struct ShipEntry {
 };
 struct GhostSeg {              // one (round, topic, start group)
   uint64_t rbase[kMaxRanks];   // recv buffer: first word of the records from rank a
+                               // (kSegInPlace: the block's first row in rank a's seen rows)
   uint64_t sbase[kMaxRanks];   // send buffer: first word of the records to rank b (the round's half)
   uint32_t rw;                 // record words (the block width)
   uint32_t topic;
+  uint32_t flags;              // kSegInPlace
+  uint32_t gbase[kMaxRanks];   // kSegInPlace: the topic's first node at rank a (its generation bytes)
+};
+// PS_DIST_F_INPLACE: a ghost-fed node of this segment reads its parent's row
+// where the owner wrote it (RankRows of the owner, the parent's topic-relative
+// id there in ghost_ref), reached iff the owner stamped its generation byte
+// this window -- no record is written or shipped
+constexpr uint32_t kSegInPlace = 1u;
+struct RankRows {
+  const uint64_t* seen;
+  const uint8_t* gen;
 };
 // k_pack: a topic root's records (round s_g + 1 of each start group g), from
 // its seeded row; one segment per (round, topic, group).
@@ -211,6 +223,7 @@ struct PullArgs {
   // the receive buffer for every rank, or -- the zero-copy loopback -- rank
   // a's own send region, offset so that the same rbase applies
   const uint64_t* rsrc[kMaxRanks];
+  const RankRows* rrows;  // PS_DIST_F_INPLACE: every rank's row set (kSegInPlace segments)
   uint32_t gen_cur;
   uint32_t slot_mod;   // block b adds its counters into partial slot b % slot_mod (zeroed per window)
   // k_pull_pair: round q + 1's partial slots; all_current: every generation

@@ -750,6 +750,10 @@ int plan_ghost(ps_engine* e, const WindowLayout& L, bool* changed) {
   G.rounds.assign(rounds + 2, GhostRound{});
   G.seg_of.assign(rounds + 2, {});
   std::vector<uint32_t> seg_round;  // round of every segment
+  struct SegAt {
+    uint32_t t, gi, d;
+  };
+  std::vector<SegAt> seg_at;  // (topic, group, level) of every segment
   for (uint32_t q = 1; q <= rounds; ++q) {
     GhostRound& R = G.rounds[q];
     R.s_off.assign(world, 0);
@@ -821,6 +825,11 @@ int plan_ghost(ps_engine* e, const WindowLayout& L, bool* changed) {
       so_q[x.t][x.gi] = si;
       G.segs.push_back(S);
       seg_round.push_back(q);
+      seg_at.push_back(SegAt{x.t, x.gi, x.d});
+      const bool in_place = e->inplace && x.d >= 2;  // (level-1 nodes: the root's records)
+      if (!in_place)
+        for (int32_t a = 0; a < world; ++a)
+          if (a != me) R.rec_bytes += gcnt(x.t, x.d, a, me) * x.rw * 8;
       // level-1 records come from the seeded root: packed by k_pack
       const TopicHost& T = e->topics[x.t];
       if (x.d == 1 && T.root_local && T.send_lvl.size() > 2 && T.send_lvl[2] > T.send_lvl[1]) {
@@ -839,6 +848,45 @@ int plan_ghost(ps_engine* e, const WindowLayout& L, bool* changed) {
     R.pack_units = units;
   }
   G.send_half = std::max<uint64_t>(16, pad16(G.send_half));
+  // PS_DIST_F_INPLACE: the owners' row sets and layouts (every rank plans
+  // the same ghost key, so all of them reach this exchange together)
+  if (e->inplace && e->transport && !G.segs.empty()) {
+    Transport::Share mine;
+    mine.seen = e->d_seen.p;
+    mine.gen = e->d_gen.p;
+    mine.gen_cur = e->gen_cur;
+    for (uint32_t t = 0; t < nt; ++t) {
+      const TopicDev& d = L.tab[t];
+      mine.topics.insert(mine.topics.end(), {d.wbase, d.n_nodes, d.nbase, d.flags});
+    }
+    std::vector<Transport::Share> all;
+    std::string xerr;
+    if (e->transport->share(mine, all, &xerr) != hipSuccess) return e->fail(PS_E_DEVICE, xerr);
+    e->rrows_host.assign(kMaxRanks, RankRows{nullptr, nullptr});
+    for (int32_t a = 0; a < world; ++a) {
+      if (all[a].gen_cur != e->gen_cur || all[a].topics.size() != mine.topics.size())
+        return e->fail(PS_E_STATE, "in-place rows: the ranks' windows differ");
+      e->rrows_host[a] = RankRows{static_cast<const uint64_t*>(all[a].seen), static_cast<const uint8_t*>(all[a].gen)};
+    }
+    e->rrows_dirty = true;
+    for (size_t si = 0; si < G.segs.size(); ++si) {
+      const SegAt& x = seg_at[si];
+      if (x.d < 2) continue;
+      GhostSeg& S = G.segs[si];
+      S.flags |= kSegInPlace;
+      const StartGroup& g = L.groups[x.t][x.gi];
+      for (int32_t a = 0; a < world; ++a) {
+        if (a == me) continue;
+        const uint64_t* o = &all[a].topics[4 * static_cast<size_t>(x.t)];  // the owner's topic block
+        TopicDev od{};
+        od.wbase = o[0];
+        od.n_nodes = static_cast<uint32_t>(o[1]);
+        od.flags = static_cast<uint32_t>(o[3]);
+        S.rbase[a] = block_row0(od, g);
+        S.gbase[a] = static_cast<uint32_t>(o[2]);
+      }
+    }
+  }
   // each round's records go to its half of the send buffer (round q + 1's are
   // written while round q's are in flight)
   for (size_t si = 0; si < G.segs.size(); ++si)

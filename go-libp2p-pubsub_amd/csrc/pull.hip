@@ -151,11 +151,18 @@ __device__ __forceinline__ void pull_resolve(const PullArgs& a, const PullTopic&
       const uint32_t g = a.ghost_ref[nb + j];
       if (g != kNoneNode) {
         const GhostSeg* S = a.gsegs + gin;
-        const uint32_t src_rank = g >> kRemoteRankShift;
-        const uint64_t* rec = rank_base(a, src_rank) + S->rbase[src_rank] +
-                              static_cast<uint64_t>(g & kRemoteIdMask) * S->rw;
-        up = rec[0] != 0;  // an unreached parent's record starts with a zero word
-        row = reinterpret_cast<uint64_t>(rec);
+        const uint32_t src_rank = g >> kRemoteRankShift, k = g & kRemoteIdMask;
+        if (S->flags & kSegInPlace) {
+          // the parent's own row at its owner (k: its topic-relative id
+          // there), reached iff the owner stamped it this window
+          const RankRows R = a.rrows[src_rank];
+          row = reinterpret_cast<uint64_t>(R.seen + S->rbase[src_rank] + static_cast<uint64_t>(k) * S->rw);
+          up = R.gen[S->gbase[src_rank] + k] == cur;
+        } else {
+          const uint64_t* rec = rank_base(a, src_rank) + S->rbase[src_rank] + static_cast<uint64_t>(k) * S->rw;
+          up = rec[0] != 0;  // an unreached parent's record starts with a zero word
+          row = reinterpret_cast<uint64_t>(rec);
+        }
         pid = 0x80000000u | g;
       }
     }

@@ -942,6 +942,14 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     pa.gen_cur = a.gen_cur;
     pa.ghost_ref = world > 1 ? e->d_ghost_ref.as<uint32_t>() : nullptr;
     pa.gsegs = e->d_gsegs.as<GhostSeg>();
+    if (e->inplace && e->rrows_dirty) {  // (the owners' row sets, from the ghost plan's exchange)
+      HIP_TRY(e->d_rrows.ensure(kMaxRanks * sizeof(RankRows)), "alloc rank rows");
+      HIP_TRY(hipMemcpyAsync(e->d_rrows.p, e->rrows_host.data(), kMaxRanks * sizeof(RankRows), hipMemcpyHostToDevice,
+                             e->stream),
+              "upload rank rows");
+      e->rrows_dirty = false;
+    }
+    pa.rrows = e->inplace ? e->d_rrows.as<RankRows>() : nullptr;
     pa.recv = e->d_recv.as<uint64_t>();
     for (int32_t q = 0; q < kMaxRanks; ++q) pa.rsrc[q] = pa.recv;
     const bool zero_copy = world > 1 && e->transport->zero_copy();
@@ -1008,9 +1016,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
           HIP_TRY(hipStreamWaitEvent(xs, e->ev_round, 0), "exchange wait");
         }
         std::string xerr;
-        st->xchg_path = zero_copy ? PS_XCHG_ZERO_COPY : PS_XCHG_COPY;
+        st->xchg_path = e->inplace ? PS_XCHG_IN_PLACE : zero_copy ? PS_XCHG_ZERO_COPY : PS_XCHG_COPY;
         st->xchg_rounds += 1;
-        for (const uint64_t n : R.r_len) st->xchg_bytes += n;
+        st->xchg_bytes += R.rec_bytes;
         const uint8_t* sb = e->d_send.as<uint8_t>() + (r % kSendBufs) * e->ghost.send_half * 8;
         if (zero_copy) {
           // the ghost-fed nodes read each source's region in place: rsrc[a] is

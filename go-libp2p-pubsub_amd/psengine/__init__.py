@@ -88,7 +88,8 @@ class DistConfig(C.Structure):
 
 
 DIST_F_COPY = 0x1  # loopback: copy the records into the receive buffer (the RCCL data path)
-XCHG_NONE, XCHG_ZERO_COPY, XCHG_COPY = 0, 1, 2  # ps_stats.xchg_path
+DIST_F_INPLACE = 0x2  # loopback: ghost-fed nodes read the owner's rows in place (no records)
+XCHG_NONE, XCHG_ZERO_COPY, XCHG_COPY, XCHG_IN_PLACE = 0, 1, 2, 3  # ps_stats.xchg_path
 
 
 class PlanOpts(C.Structure):
@@ -415,10 +416,13 @@ class Engine:
         self._check(self._L.ps_dist_init(self._h, C.byref(dc), uid))
 
     def dist_init_loopback(self, group: "Loopback", rank: int, partition: int = PART_PEER,
-                           split_depth: int = 0, copy: bool = False):
+                           split_depth: int = 0, copy: bool = False, inplace: bool = False):
         """copy: the records go through the receive buffer (PS_DIST_F_COPY), the
-        RCCL transport's data path, instead of being read in place."""
-        dc = DistConfig(rank, group.world, partition, split_depth, DIST_F_COPY if copy else 0, 0)
+        RCCL transport's data path, instead of being read in place.  inplace:
+        no records below the roots -- ghost-fed nodes read their parents' rows
+        in the owner's row set (PS_DIST_F_INPLACE)."""
+        flags = (DIST_F_COPY if copy else 0) | (DIST_F_INPLACE if inplace else 0)
+        dc = DistConfig(rank, group.world, partition, split_depth, flags, 0)
         self._check(self._L.ps_dist_init_loopback(self._h, C.byref(dc), group._h))
 
 

@@ -123,6 +123,9 @@ typedef struct ps_stats {
                                  (loopback ranks sharing one process and GPU)  */
 #define PS_XCHG_COPY 2u       /* copied into this rank's receive buffer (RCCL
                                  send/recv; the loopback with PS_DIST_F_COPY)  */
+#define PS_XCHG_IN_PLACE 3u   /* ghost parents' rows read where their owner
+                                 wrote them (PS_DIST_F_INPLACE); only the topic
+                                 roots' rows still move as records            */
 
 /* ps_stats.round_kernel */
 #define PS_K_NONE 0u
@@ -325,6 +328,12 @@ typedef struct ps_dist_config {
  * (send parts, receive buffer, exchange stream), instead of reading them in
  * place (tests run the RCCL-shaped path on one GPU with it; RCCL: ignored) */
 #define PS_DIST_F_COPY 0x1u
+/* ps_dist_config.flags: ghost-fed nodes read their remote parents' rows in
+ * the owner's own row set (no packed records, no shipping; the loopback
+ * transport's ranks share one process and device -- across GPUs of a node
+ * this is what xGMI peer mappings would serve).  Not with PS_DIST_F_COPY;
+ * RCCL: refused. */
+#define PS_DIST_F_INPLACE 0x2u
 
 /* rank 0 creates the RCCL id; the caller ships it to every rank */
 int ps_dist_unique_id(uint8_t id_out[PS_UNIQUE_ID_BYTES]);

@@ -45,18 +45,20 @@ def run_ranks(engines):
 
 
 def make_ranks(world, n, n_topics, partition, split_depth=0, copy=False, **kw):
-    """copy: the RCCL-shaped data path (PS_DIST_F_COPY: records through the
-    receive buffer) instead of the zero-copy loopback reads."""
+    """copy=True: the RCCL-shaped data path (PS_DIST_F_COPY: records through
+    the receive buffer) instead of the zero-copy loopback reads; "inplace":
+    no records below the roots, ghost-fed nodes read the owner's rows
+    (PS_DIST_F_INPLACE)."""
     lb = PE.Loopback(world)
     engines = [PE.Engine(n, n_topics, record_hops=True, **kw) for _ in range(world)]
     for r, e in enumerate(engines):
-        e.dist_init_loopback(lb, r, partition, split_depth, copy=copy)
+        e.dist_init_loopback(lb, r, partition, split_depth, copy=copy is True, inplace=copy == "inplace")
     return lb, engines
 
 
 def check_path(stats, copy):
     """Which transport path ran (ps_stats.xchg_path), on every rank."""
-    want = PE.XCHG_COPY if copy else PE.XCHG_ZERO_COPY
+    want = PE.XCHG_COPY if copy is True else PE.XCHG_IN_PLACE if copy == "inplace" else PE.XCHG_ZERO_COPY
     assert all(st.xchg_rounds > 0 for st in stats), [st.xchg_rounds for st in stats]
     assert all(st.xchg_path == want for st in stats), [st.xchg_path for st in stats]
 
@@ -66,7 +68,7 @@ def merged_hops(engines, msg):
     return h.min(axis=0)  # every peer is owned by exactly one rank per topic
 
 
-@pytest.mark.parametrize("copy", [False, True])
+@pytest.mark.parametrize("copy", [False, True, "inplace"])
 @pytest.mark.parametrize("overlap", [0, 1])
 @pytest.mark.parametrize("staggered", [True, False])
 @pytest.mark.parametrize("world,partition", [(2, PE.PART_SUBTREE), (3, PE.PART_PEER),
@@ -225,7 +227,7 @@ def test_sharded_churn_batches():
     lb.close()
 
 
-@pytest.mark.parametrize("copy", [False, True])
+@pytest.mark.parametrize("copy", [False, True, "inplace"])
 @pytest.mark.parametrize("world", [2, 4])
 def test_cfg4_shaped_peer_partition(world, copy):
     """cfg4-shaped trees (TreeOpts{8,20} by the restated joins, scaled to
@@ -247,7 +249,7 @@ def test_cfg4_shaped_peer_partition(world, copy):
     lb = PE.Loopback(world)
     engines = [PE.Engine(wl.n_peers, 1, seed=wl.seed, record_hops=True) for _ in range(world)]
     for r, e in enumerate(engines):
-        e.dist_init_loopback(lb, r, copy=copy)  # PART_PEER by default
+        e.dist_init_loopback(lb, r, copy=copy is True, inplace=copy == "inplace")  # PART_PEER by default
         WL.build_engine_topics(e, wl)
         e.set_live(live)
     firsts = [e.publish(wl.msg_topics) for e in engines]

@@ -111,7 +111,8 @@ def test_cfg4_full_size_dead_mask_single_rank(cfg4_tree):
 cfg4_tree_digest = [None]
 
 
-@pytest.mark.parametrize("world,copy", [(2, False), (2, True), (4, False), (4, True), (8, False), (8, True)])
+@pytest.mark.parametrize("world,copy", [(2, False), (2, True), (2, "inplace"), (4, False), (4, True), (4, "inplace"),
+                                        (8, False), (8, True), (8, "inplace")])
 def test_cfg4_full_size_ranks_peer_hash(cfg4_tree, world, copy):
     """cfg4 at full size hash-sharded over `world` loopback ranks (owner(p) =
     splitmix64(p) mod world; 8 = the north star's split):
@@ -125,7 +126,7 @@ def test_cfg4_full_size_ranks_peer_hash(cfg4_tree, world, copy):
     engines = [PE.Engine(wl.n_peers, 1, seed=wl.seed) for _ in range(world)]
     try:
         for r, e in enumerate(engines):
-            e.dist_init_loopback(lb, r, PE.PART_PEER, copy=copy)
+            e.dist_init_loopback(lb, r, PE.PART_PEER, copy=copy is True, inplace=copy == "inplace")
             e.set_tree(0, 0, parent)
             e.set_live(live)
         firsts = [e.publish(wl.msg_topics) for e in engines]
@@ -146,7 +147,7 @@ def test_cfg4_full_size_ranks_peer_hash(cfg4_tree, world, copy):
         assert not any(t.is_alive() for t in th), "rank thread hung"
         assert not errs, errs
         assert all(s.expand_mode == PE.MODE_LEVEL_PULL for s in stats)
-        want = PE.XCHG_COPY if copy else PE.XCHG_ZERO_COPY
+        want = PE.XCHG_COPY if copy is True else PE.XCHG_IN_PLACE if copy == "inplace" else PE.XCHG_ZERO_COPY
         assert all(s.xchg_path == want and s.xchg_rounds > 0 for s in stats), [s.xchg_path for s in stats]
         check_run(stats, wl.n_msgs, tot, hist)
         own = PE.partition_owner(parent, 0, 0, world, PE.PART_PEER)

@@ -26,6 +26,9 @@ ap.add_argument("--workload", default="cfg4")
 ap.add_argument("--scale", type=float, default=0.25)
 ap.add_argument("--partition", default="peer", choices=["peer", "subtree"])
 ap.add_argument("--steps", type=int, default=5)
+ap.add_argument("--mode", default="zc", choices=["zc", "copy", "inplace"],
+                help="zero-copy records (default), records copied (PS_DIST_F_COPY), or rows read in place "
+                     "(PS_DIST_F_INPLACE)")
 ap.add_argument("--staggered", action="store_true",
                 help="start rounds uniform over 0..7 (paced publishing: start groups), both legs")
 args = ap.parse_args()
@@ -59,10 +62,10 @@ engs = []
 t0 = time.perf_counter()
 for r in range(args.world):
     e = PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed, msg_window=1 << 20)
-    e.dist_init_loopback(lb, r, part)
+    e.dist_init_loopback(lb, r, part, copy=args.mode == "copy", inplace=args.mode == "inplace")
     WL.build_engine_topics(e, wl)
     engs.append(e)
-print(f"[loopback] {args.world} ranks ({args.partition} partition) setup {time.perf_counter() - t0:.1f}s", flush=True)
+print(f"[loopback] {args.world} ranks ({args.partition} partition, {args.mode}) setup {time.perf_counter() - t0:.1f}s", flush=True)
 expected = exp1 * args.world
 times = []
 for step in range(args.steps + 1):
