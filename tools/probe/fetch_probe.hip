@@ -60,6 +60,18 @@ __global__ __launch_bounds__(256) void k_read_lds4(const unsigned* __restrict__ 
   if (acc == 0x12345678u) out[blockIdx.x] = acc;
 }
 
+// scattered 8-byte loads, one per `stride` bytes (a line each): what a
+// request for a partly used line is tallied as
+__global__ __launch_bounds__(256) void k_gather8(const uint64_t* __restrict__ in, size_t n, size_t stride_words,
+                                                 unsigned* __restrict__ out) {
+  unsigned acc = 0;
+  for (size_t i = static_cast<size_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += static_cast<size_t>(gridDim.x) * 256) {
+    const uint64_t v = in[i * stride_words];
+    acc ^= static_cast<unsigned>(v);
+  }
+  if (acc == 0x12345678u) out[blockIdx.x] = acc;
+}
+
 int main() {
   const size_t bytes = 2ull << 30;
   void* in = nullptr;
@@ -74,9 +86,14 @@ int main() {
     hipLaunchKernelGGL(k_read<unsigned>, dim3(grid), dim3(256), 0, 0, static_cast<const unsigned*>(in), bytes / 4, out);
     hipLaunchKernelGGL(k_read<uint8_t>, dim3(grid), dim3(256), 0, 0, static_cast<const uint8_t*>(in), bytes, out);
     hipLaunchKernelGGL(k_read_lds4, dim3(grid), dim3(256), 0, 0, static_cast<const unsigned*>(in), bytes / 4, out);
+    // one 8-B word per 64 B, per 128 B and per 256 B (2 GiB / stride loads)
+    for (size_t st : {8, 16, 32})
+      hipLaunchKernelGGL(k_gather8, dim3(grid), dim3(256), 0, 0, static_cast<const uint64_t*>(in), bytes / (st * 8), st,
+                         out);
   }
   CK(hipDeviceSynchronize());
-  std::printf("fetch_probe: %zu bytes read per kernel (16/8/4/1-byte loads, 4-byte LDS-DMA), 2 reps\n", bytes);
+  std::printf("fetch_probe: %zu bytes read per kernel (16/8/4/1-byte loads, 4-byte LDS-DMA; then one 8-B load "
+              "per 64/128/256 B), 2 reps\n", bytes);
   CK(hipFree(in));
   CK(hipFree(out));
   return 0;
