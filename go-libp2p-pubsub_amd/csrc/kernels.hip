@@ -1124,17 +1124,32 @@ __global__ __launch_bounds__(kBlock) void k_level_reach(const ReachPiece* __rest
   const TopicDev T = topics[P.topic];
   const uint32_t cur = gen_cur & 0xFF;
   uint32_t r = 0, f = 0;
-  for (uint32_t u = P.lo + threadIdx.x; u < P.hi; u += kBlock) {
-    bool reached;
-    if (u == T.nbase)
-      reached = true;  // the root: seeded
-    else if (eager)
-      reached = seen[T.wbase + static_cast<uint64_t>(u - T.nbase) * T.W] != 0;
-    else
-      reached = gen[u] == cur;
-    const bool internal = (node_flags[u] & kNodeInternal) != 0;
-    r += reached ? 1u : 0u;
-    f += (internal && reached) ? 1u : 0u;
+  if (eager) {
+    for (uint32_t u = P.lo + threadIdx.x; u < P.hi; u += kBlock) {
+      const bool reached = u == T.nbase || seen[T.wbase + static_cast<uint64_t>(u - T.nbase) * T.W] != 0;
+      const bool internal = (node_flags[u] & kNodeInternal) != 0;
+      r += reached ? 1u : 0u;
+      f += (internal && reached) ? 1u : 0u;
+    }
+  } else {
+    // 16 nodes per lane and load: the generation and flag bytes as dwordx4
+    // (16-B aligned units over the piece, bytes outside it masked off; both
+    // arrays are padded past n_pad)
+    const uint32_t b0 = P.lo & ~15u;
+    for (uint32_t b = b0 + 16 * threadIdx.x; b < P.hi; b += 16 * kBlock) {
+      const uint4 g = *reinterpret_cast<const uint4*>(gen + b);
+      const uint4 fl = *reinterpret_cast<const uint4*>(node_flags + b);
+      const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, fw[4] = {fl.x, fl.y, fl.z, fl.w};
+#pragma unroll
+      for (uint32_t k = 0; k < 16; ++k) {
+        const uint32_t u = b + k;
+        const bool in = u >= P.lo && u < P.hi;
+        const bool reached = in && (u == T.nbase || ((gw[k >> 2] >> (8 * (k & 3))) & 0xFFu) == cur);
+        const bool internal = ((fw[k >> 2] >> (8 * (k & 3))) & kNodeInternal) != 0;
+        r += reached ? 1u : 0u;
+        f += (internal && reached) ? 1u : 0u;
+      }
+    }
   }
   r = __reduce_add_sync(~0ull, r);
   f = __reduce_add_sync(~0ull, f);

@@ -977,7 +977,9 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         s = e->stream;
         HIP_TRY(hipStreamWaitEvent(s, e->ev_pre, 0), "prefix join");
       }
-      if (L.aligned && r == pre_P + 1 && reach_a && !reach_a_done) {  // levels <= P counted before the gate
+      // levels <= P counted before the gate (alternating row sets: no successor
+      // restamps them, the whole pass runs beside the next window, below)
+      if (L.aligned && !alt_sets && r == pre_P + 1 && reach_a && !reach_a_done) {
         HIP_TRY(launch_level_reach(e->d_reach.as<ReachPiece>(), reach_a, a.gen, a.gen_cur, a.node_flags, a.topics,
                                    a.seen, L.split.eager, partials + static_cast<size_t>(reach_slot0) * kNumCtr, s),
                 "level reach (prefix levels)");
@@ -1117,15 +1119,6 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       if (const int rc = reuse(planned0 - 1)) return rc;
     if (const int rc = reuse(planned0)) return rc;
     r = planned0;
-    // level-aligned: each (topic, level)'s reached and frontier nodes, for
-    // the per-round split (into the pseudo-slots after the rounds')
-    if (L.aligned && e->n_reach) {
-      const uint32_t from = reach_a_done ? reach_a : 0u;
-      HIP_TRY(launch_level_reach(e->d_reach.as<ReachPiece>() + from, e->n_reach - from, a.gen, a.gen_cur,
-                                 a.node_flags, a.topics, a.seen, L.split.eager,
-                                 partials + static_cast<size_t>(reach_slot0) * kNumCtr, s),
-              "level reach");
-    }
     // a deferred window's counters go straight into its pinned rows
     const bool direct = e->defer_last && e->defer_into && !record && !timed && r <= PS_MAX_ROUNDS &&
                         (world == 1 || planned0 <= PS_MAX_ROUNDS);
@@ -1142,6 +1135,18 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
       rs = e->rstream;
     }
     reduce_side = rs != s;
+    // level-aligned: each (topic, level)'s reached and frontier nodes, for
+    // the per-round split (into the pseudo-slots after the rounds'); with
+    // alternating row sets on the reduce's stream, beside the next window
+    // (its generation bytes are the other set's)
+    if (L.aligned && e->n_reach) {
+      const uint32_t from = reach_a_done ? reach_a : 0u;
+      HIP_TRY(launch_level_reach(e->d_reach.as<ReachPiece>() + from, e->n_reach - from, a.gen, a.gen_cur,
+                                 a.node_flags, a.topics, a.seen, L.split.eager,
+                                 partials + static_cast<size_t>(reach_slot0) * kNumCtr,
+                                 alt_sets && reduce_side ? rs : s),
+              "level reach");
+    }
     // a signalled window: the reduce's last block raises its flag
     WindowSignal wsig{};
     if (sigwin && direct && !reduce_side && (s == e->stream || twin)) {
