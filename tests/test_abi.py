@@ -178,3 +178,16 @@ def test_struct_offsets_match_c(tmp_path):
         assert got[(cname, "sizeof")] == ctypes.sizeof(cls), cname
         for f, _ in cls._fields_:
             assert got[(cname, f)] == getattr(cls, f).offset, (cname, f)
+
+
+def test_header_constants_match_python():
+    """The PS_* values the Python binding mirrors equal the header's (the
+    in-place exchange flag and path of round 5 included)."""
+    import re
+    hdr = open(os.path.join(REPO, "include", "psengine.h")).read()
+    vals = {m.group(1): int(m.group(2), 0) for m in re.finditer(r"#define (PS_\w+) (0x[0-9a-fA-F]+|\d+)u?", hdr)}
+    pairs = {"PS_DIST_F_COPY": PE.DIST_F_COPY, "PS_DIST_F_INPLACE": PE.DIST_F_INPLACE,
+             "PS_XCHG_NONE": PE.XCHG_NONE, "PS_XCHG_ZERO_COPY": PE.XCHG_ZERO_COPY, "PS_XCHG_COPY": PE.XCHG_COPY,
+             "PS_XCHG_IN_PLACE": PE.XCHG_IN_PLACE, "PS_K_CHAIN": PE.K_CHAIN, "PS_K_FLOOD": PE.K_FLOOD}
+    for name, py in pairs.items():
+        assert vals[name] == py, name
