@@ -347,7 +347,13 @@ __global__ __launch_bounds__(kB) void k_place_lb(PlaceArgs P, uint32_t d, uint64
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(P.err, kBuildErrGrid);
     return;
   }
-  const uint32_t tile = blockIdx.x;
+  // the tile from a ticket (status[-1], zeroed with the status words): a
+  // tile only ever waits on tiles whose blocks already run, whatever order
+  // the dispatcher starts blocks in
+  __shared__ uint32_t tile_s;
+  if (threadIdx.x == 0) tile_s = atomicAdd(reinterpret_cast<unsigned int*>(status - 1), 1u);
+  __syncthreads();
+  const uint32_t tile = tile_s;
   if (tile >= ntiles) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint32_t j0 = tile * kB + tid;

@@ -592,7 +592,7 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
           g = std::min<uint32_t>(full, lb_tiles(static_cast<uint32_t>(std::min<uint64_t>(np + np / 4 + 2048, n))));
         }
         grids[t].push_back(g);
-        st_words += g;
+        st_words += g + 1;  // (+ the launch's tile ticket, first)
       }
     }
     HIP_TRY(e->d_lbstat.ensure(std::max<size_t>(st_words, 1) * 8), "alloc look-back status");
@@ -648,8 +648,8 @@ int gpu_build_graph(ps_engine* e, bool* fallback) {
       P.topic = static_cast<uint16_t>(t);
       HIP_TRY(launch_place_top(P, d_from[t] > 1 ? d_from[t] : kBuildMaxDepth, s), "place top levels");
       for (uint32_t i = 0, d = d_from[t]; d <= d_to[t]; ++d, ++i) {
-        HIP_TRY(launch_place_lb(P, d, grids[t][i], lbst, s), "place level");
-        lbst += grids[t][i];
+        HIP_TRY(launch_place_lb(P, d, grids[t][i], lbst + 1, s), "place level");
+        lbst += grids[t][i] + 1;
       }
     }
     // the lazy prune's reach queries over this node space (run.cpp): their
