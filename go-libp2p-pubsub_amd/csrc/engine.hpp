@@ -358,6 +358,7 @@ struct ps_engine {
   bool chain_nt = true;           // chain launches: level 0 and the inner levels stored non-temporally
   std::vector<uint64_t> chain_fail_key;  // a pair plan whose chain ranges overflowed the level tables: no chains
   psamd::DevBuf d_chain_ovf;
+  psamd::DevBuf d_chain_meta, d_chain_cnt, d_chain_scan;  // the chunks' node entries (k_chain_meta)
   // rows of rounds writing at least this much store non-temporally (the MALL
   // cannot hold them for the next launch: reversing launch order and cached
   // stores measured 0-50 % slower, profiles/r03/ab_mall_reverse.txt)

@@ -201,6 +201,10 @@ struct PackSeg {
 __host__ __device__ inline uint32_t pack_units(uint32_t W) { return (W & 1u) ? W : W >> 1; }
 struct PullArgs {
   const uint32_t* node_parent;  // node-space parent (kNone for roots and remote parents)
+  // k_pull_chain: every chain chunk's node entries (16 bits: parent index
+  // relative to the level above, live bit), levels in order, from
+  // ChainChunk::first[kChainLevels] (k_chain_meta, once per plan)
+  const uint32_t* chain_meta;
   const uint8_t* node_flags;
   const TopicDev* topics;
   const uint64_t* a_cur;  // arrivals of round-1 (topic roots' seeded rows)
@@ -291,6 +295,16 @@ static_assert(sizeof(ChainChunk) == 128, "two chunk descriptors per 256-B line")
 // level range exceeds cap (the plan is then not used)
 hipError_t launch_chain_ranges(ChainChunk* chunks, uint32_t n, const uint32_t* row_ptr, uint32_t cap,
                                uint32_t* overflow, hipStream_t s);
+// The chunks' node entries (PullArgs::chain_meta) after their ranges: per
+// chunk its node count (counts[i]), an exclusive scan into
+// ChainChunk::first[kChainLevels] (the device copy's; first[] past the
+// chain's levels is unused there), the entries from node_parent and the live
+// flags.  *entries: the buffer's size in entries, read back by the caller
+// with the ranges' overflow word (`tail`: counts[n] after the scan).
+hipError_t launch_chain_meta(ChainChunk* chunks, uint32_t n, const uint32_t* node_parent, const uint8_t* node_flags,
+                             uint32_t* counts, void* scan_temp, size_t scan_bytes, uint32_t* meta, bool fill,
+                             hipStream_t s);
+size_t chain_meta_scan_bytes(uint32_t n);
 // slices: chunks of rows wider than the stage (column slices; their own launch)
 // inner_nt: level 0 and the inner levels store non-temporally (false: plain, A/B)
 // waves_per_cu: resident chain waves per CU at most (an LDS pad; 0: no cap)

@@ -6,6 +6,8 @@
 #include <algorithm>
 #include <cstddef>
 
+#include <hipcub/hipcub.hpp>
+
 #include "devutil.hpp"
 #include "kernels.hpp"
 
@@ -961,9 +963,11 @@ struct ChainMeta {
 // walk: every deeper level is empty too.)
 struct MetaCursor {
   uint32_t k, kb, ns, lo, hi, plo;
+  uint32_t mb;  // the level's first entry in the chunk's chain_meta entries
   __device__ __forceinline__ void enter(const ChainChunk* cp, uint32_t levels) {
     if (k >= levels) return;
     plo = lo;
+    mb += hi - lo;  // (the level above's entries; level 0: none, hi = lo = p_lo)
     lo = __builtin_amdgcn_readfirstlane(cp->lo[k]);
     hi = __builtin_amdgcn_readfirstlane(cp->hi[k]);
     ns = (hi - lo + 63) >> 6;
@@ -973,7 +977,8 @@ struct MetaCursor {
   __device__ __forceinline__ void start(const ChainChunk* cp, uint32_t levels, uint32_t g0, uint32_t p_lo) {
     k = 0;
     kb = 0;
-    lo = p_lo;
+    mb = 0;
+    lo = hi = p_lo;
     enter(cp, levels);
     while (k < levels && g0 >= kb + ns) {
       kb += ns;
@@ -991,11 +996,14 @@ struct MetaCursor {
   }
 };
 
-// Issues the batch of slots g0 .. g0 + kMetaSlots - 1: raw parent ids and
-// flag dwords into p / f (unconsumed, so nothing waits here).
+// Issues the batch of slots g0 .. g0 + kMetaSlots - 1: the nodes' entries,
+// contiguous per chunk in level order (k_chain_meta), 2 B per lane -- one
+// 128-B line per slot -- into q (unconsumed, so nothing waits here).
+// (Before round 5: each node's parent id and flag dword, two scattered
+// lines per slot: ~1 KB of line-granular reads per wave.)
 __device__ __forceinline__ void chain_meta_issue(const PullArgs& a, const ChainChunk* cp, uint32_t levels,
-                                                 uint32_t p_lo, uint32_t g0, uint32_t lane,
-                                                 uint32_t (&p)[kMetaSlots], uint32_t (&f)[kMetaSlots]) {
+                                                 uint32_t p_lo, uint32_t g0, uint32_t lane, uint32_t moff,
+                                                 uint32_t (&q)[kMetaSlots]) {
   MetaCursor m;
   m.start(cp, levels, g0, p_lo);
 #pragma unroll
@@ -1003,18 +1011,14 @@ __device__ __forceinline__ void chain_meta_issue(const PullArgs& a, const ChainC
     if (i) m.step(cp, levels, g0 + i);
     if (m.k >= levels) break;  // (past the chunk's last level: no loads)
     const uint32_t y = m.lo + (g0 + i - m.kb) * 64 + lane;
-    const uint32_t ys = y < m.hi ? y : 0u;  // (clamped: node 0 exists)
-    p[i] = a.node_parent[ys];
-    // the flag byte's aligned dword (a byte load's zero extension would
-    // consume it here; node_flags is padded past n_pad)
-    f[i] = reinterpret_cast<const uint32_t*>(a.node_flags)[ys >> 2];
+    const uint32_t yi = moff + (y < m.hi ? m.mb + (y - m.lo) : 0u);  // (clamped: the chunk's first entry)
+    q[i] = a.chain_meta[yi];
   }
 }
 
-// Packs the issued batch (the first use of p / f: the loads' wait).
+// Packs the issued batch (the first use of q: the loads' wait).
 __device__ __forceinline__ void chain_meta_pack(const ChainChunk* cp, uint32_t levels, uint32_t p_lo, uint32_t g0,
-                                                bool direct, uint32_t lane, const uint32_t (&p)[kMetaSlots],
-                                                const uint32_t (&f)[kMetaSlots], ChainMeta& M) {
+                                                uint32_t lane, const uint32_t (&q)[kMetaSlots], ChainMeta& M) {
   M.g0 = g0;
   MetaCursor m;
   m.start(cp, levels, g0, p_lo);
@@ -1023,13 +1027,8 @@ __device__ __forceinline__ void chain_meta_pack(const ChainChunk* cp, uint32_t l
     if (i) m.step(cp, levels, g0 + i);
     if (m.k >= levels) break;  // (the slots past it are never picked)
     const uint32_t y = m.lo + (g0 + i - m.kb) * 64 + lane;
-    // (a level-0 entry of the direct path -- parents spanning more than the
-    // stage, possibly > 65,535 ids -- is never picked: kMetaNone, so that it
-    // cannot spill into the next slot's half; deeper levels' parent indices
-    // are < kChainCap, checked by k_chain_ranges)
-    const uint32_t e = (y < m.hi && (m.k > 0 || !direct))
-                           ? ((p[i] - m.plo) & (kMetaLive - 1)) | (((f[i] >> (8 * (y & 3))) & kNodeLive) ? kMetaLive : 0u)
-                           : kMetaNone;
+    // (the direct path's level-0 entries are kMetaNone already: k_chain_meta)
+    const uint32_t e = y < m.hi ? (q[i] & 0xFFFFu) : kMetaNone;
     if (i & 1)
       M.w[i / 2] |= e << 16;
     else
@@ -1258,9 +1257,10 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
   // the previous node's parent: a parent whose children straddle two runs counts once
   const uint32_t pm = cp->node_begin > C.nbase ? a.node_parent[cp->node_begin - 1] : kNoneNode;
   ChainMeta M;
+  const uint32_t moff = cp->first[kChainLevels];  // (device copy: the chunk's first chain_meta entry)
   {
-    uint32_t mp[kMetaSlots], mf[kMetaSlots];
-    chain_meta_issue(a, cp, levels, p_lo, 0u, lane, mp, mf);
+    uint32_t mq[kMetaSlots];
+    chain_meta_issue(a, cp, levels, p_lo, 0u, lane, moff, mq);
     if (!direct) {
       if (lane < n_gd) PSAMD_DMA(reinterpret_cast<const uint32_t*>(a.gen + g0) + lane, gen_lds, 4);
       if (!(C.W & 1u)) {
@@ -1280,7 +1280,7 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
           PSAMD_DMA(pw32 + min(d0 + lane, 2 * words - 1), reinterpret_cast<uint32_t*>(stage) + d0, 4);
       }
     }
-    chain_meta_pack(cp, levels, p_lo, 0u, direct, lane, mp, mf, M);  // (waits for every load above)
+    chain_meta_pack(cp, levels, p_lo, 0u, lane, mq, M);  // (waits for every load above)
   }
   if (lane < 2) stage[kStage + lane] = 0;
   uint32_t g = 0;   // the global metadata slot of the next node group
@@ -1313,9 +1313,9 @@ __global__ __launch_bounds__(64) void k_pull_chain(PullArgs a, const ChainChunk*
       const uint32_t nk = min(kChainKids, hi - y0);
       const uint32_t ng = (nk + 63) >> 6;
       if (g + ng > M.g0 + kMetaSlots) {
-        uint32_t mp[kMetaSlots], mf[kMetaSlots];
-        chain_meta_issue(a, cp, levels, p_lo, g, lane, mp, mf);
-        chain_meta_pack(cp, levels, p_lo, g, direct, lane, mp, mf, M);
+        uint32_t mq[kMetaSlots];
+        chain_meta_issue(a, cp, levels, p_lo, g, lane, moff, mq);
+        chain_meta_pack(cp, levels, p_lo, g, lane, mq, M);
       }
       uint8_t* const tab = tabs[k & 1] + (y0 - lo);
 #pragma unroll
@@ -1427,6 +1427,76 @@ hipError_t launch_chunk_parents(PullChunk* chunks, uint32_t n, const uint32_t* n
 hipError_t launch_chain_parents(ChainChunk* chunks, uint32_t n, const uint32_t* node_parent, hipStream_t s) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(k_chain_parents, dim3((n + kBlock - 1) / kBlock), dim3(kBlock), 0, s, chunks, n, node_parent);
+  return hipGetLastError();
+}
+
+namespace {
+// per chunk: its nodes over the chain's levels (the ranges k_chain_ranges set)
+__global__ __launch_bounds__(kBlock) void k_chain_meta_count(const ChainChunk* __restrict__ chunks, uint32_t n,
+                                                             uint32_t* __restrict__ counts) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i > n) return;
+  uint32_t c = 0;
+  if (i < n) {
+    const ChainChunk& ch = chunks[i];
+    const uint32_t levels = ch.levels;
+    for (uint32_t k = 0; k < levels && k < kChainLevels; ++k) c += ch.hi[k] - ch.lo[k];
+  }
+  counts[i] = c;  // (counts[n] = 0: the scan's total lands at offs[n])
+}
+
+// one wave per chunk: entry = parent index relative to the level above (level
+// 0: to the run's first parent) | live bit, as chain_meta_pack packed them
+// from node_parent / node_flags in the kernel; kMetaNone for level 0 of a run
+// that takes the direct path (its entries are never picked)
+__global__ __launch_bounds__(kBlock) void k_chain_meta_fill(ChainChunk* __restrict__ chunks, uint32_t n,
+                                                            const uint32_t* __restrict__ offs,
+                                                            const uint32_t* __restrict__ node_parent,
+                                                            const uint8_t* __restrict__ node_flags,
+                                                            uint32_t* __restrict__ meta) {
+  const uint32_t ci = (blockIdx.x * kBlock + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (ci >= n) return;
+  ChainChunk& ch = chunks[ci];
+  const uint32_t off = offs[ci];
+  const uint32_t levels = ch.levels, p_lo = ch.p_lo, p_hi = ch.p_hi, S = ch.S;
+  const uint32_t n_par = p_hi - p_lo + 1;
+  const bool direct = n_par > kChainPar || n_par * S > kChainWords;
+  uint32_t base = 0, plo = p_lo;
+  for (uint32_t k = 0; k < levels && k < kChainLevels; ++k) {
+    const uint32_t lo = ch.lo[k], hi = ch.hi[k];
+    for (uint32_t y = lo + lane; y < hi; y += 64) {
+      uint32_t e = kMetaNone;
+      if (k > 0 || !direct)
+        e = ((node_parent[y] - plo) & (kMetaLive - 1)) | ((node_flags[y] & kNodeLive) ? kMetaLive : 0u);
+      meta[off + base + (y - lo)] = e;
+    }
+    base += hi - lo;
+    plo = lo;
+  }
+  if (lane == 0) ch.first[kChainLevels] = off;
+}
+}  // namespace
+
+size_t chain_meta_scan_bytes(uint32_t n) {
+  size_t b = 0;
+  (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, static_cast<const uint32_t*>(nullptr),
+                                         static_cast<uint32_t*>(nullptr), n + 1);
+  return b;
+}
+
+hipError_t launch_chain_meta(ChainChunk* chunks, uint32_t n, const uint32_t* node_parent, const uint8_t* node_flags,
+                             uint32_t* counts, void* scan_temp, size_t scan_bytes, uint32_t* meta, bool fill,
+                             hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  uint32_t* offs = counts + n + 1;
+  if (!fill) {
+    hipLaunchKernelGGL(k_chain_meta_count, dim3((n + kBlock) / kBlock), dim3(kBlock), 0, s, chunks, n, counts);
+    hipError_t e = hipcub::DeviceScan::ExclusiveSum(scan_temp, scan_bytes, counts, offs, n + 1, s);
+    if (e != hipSuccess) return e;
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(k_chain_meta_fill, dim3((static_cast<uint64_t>(n) * 64 + kBlock - 1) / kBlock), dim3(kBlock),
+                     0, s, chunks, n, offs, node_parent, node_flags, meta);
   return hipGetLastError();
 }
 

@@ -64,17 +64,33 @@ int upload_pair(ps_engine* e, bool* overflow) {
               "chain chunk parents");
     HIP_TRY(e->d_chain_ovf.ensure(4), "alloc chain overflow word");
     HIP_TRY(hipMemsetAsync(e->d_chain_ovf.p, 0, 4, e->stream), "clear chain overflow word");
-    HIP_TRY(launch_chain_ranges(e->d_chain.as<ChainChunk>(), static_cast<uint32_t>(K.size()),
-                                e->d_row_ptr.as<uint32_t>(), kChainCap,
+    const uint32_t nk = static_cast<uint32_t>(K.size());
+    HIP_TRY(launch_chain_ranges(e->d_chain.as<ChainChunk>(), nk, e->d_row_ptr.as<uint32_t>(), kChainCap,
                                 e->d_chain_ovf.as<uint32_t>(), e->stream),
             "chain ranges");
-    uint32_t ovf = 0;
-    HIP_TRY(hipMemcpyAsync(&ovf, e->d_chain_ovf.p, 4, hipMemcpyDeviceToHost, e->stream), "read chain overflow");
+    // the chunks' node entries: counts and their scan now, the entries once
+    // the total is back (one readback with the overflow word)
+    const size_t scan_bytes = chain_meta_scan_bytes(nk);
+    HIP_TRY(e->d_chain_scan.ensure(std::max<size_t>(scan_bytes, 16)), "alloc chain scan");
+    HIP_TRY(e->d_chain_cnt.ensure((2 * static_cast<size_t>(nk) + 2) * 4), "alloc chain counts");
+    HIP_TRY(launch_chain_meta(e->d_chain.as<ChainChunk>(), nk, nullptr, nullptr, e->d_chain_cnt.as<uint32_t>(),
+                              e->d_chain_scan.p, e->d_chain_scan.bytes, nullptr, false, e->stream),
+            "chain entry counts");
+    uint32_t back[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(&back[0], e->d_chain_ovf.p, 4, hipMemcpyDeviceToHost, e->stream), "read chain overflow");
+    HIP_TRY(hipMemcpyAsync(&back[1], e->d_chain_cnt.as<uint32_t>() + nk + 1 + nk, 4, hipMemcpyDeviceToHost,
+                           e->stream),
+            "read chain entries");
     HIP_TRY(hipStreamSynchronize(e->stream), "sync");
-    if (ovf) {
+    if (back[0]) {
       *overflow = true;
       return PS_OK;
     }
+    HIP_TRY(e->d_chain_meta.ensure(std::max<size_t>(back[1], 1) * 4), "alloc chain entries");
+    HIP_TRY(launch_chain_meta(e->d_chain.as<ChainChunk>(), nk, e->d_node_parent.as<uint32_t>(),
+                              e->d_node_flags.as<uint8_t>(), e->d_chain_cnt.as<uint32_t>(), nullptr, 0,
+                              e->d_chain_meta.as<uint32_t>(), true, e->stream),
+            "chain entries");
   }
   e->pair_up = e->pair.version;
   return PS_OK;
@@ -942,6 +958,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     pa.gen_cur = a.gen_cur;
     pa.ghost_ref = world > 1 ? e->d_ghost_ref.as<uint32_t>() : nullptr;
     pa.gsegs = e->d_gsegs.as<GhostSeg>();
+    pa.chain_meta = e->d_chain_meta.as<uint32_t>();
     if (e->inplace && e->rrows_dirty) {  // (the owners' row sets, from the ghost plan's exchange)
       HIP_TRY(e->d_rrows.ensure(kMaxRanks * sizeof(RankRows)), "alloc rank rows");
       HIP_TRY(hipMemcpyAsync(e->d_rrows.p, e->rrows_host.data(), kMaxRanks * sizeof(RankRows), hipMemcpyHostToDevice,

@@ -180,7 +180,7 @@ def load(build_if_missing: bool = False):
                 raise FileNotFoundError(
                     f"{_build.LIB} missing: run __graft_entry__.build() (no CPU fallback exists)")
             _build.build()
-        L = C.CDLL(_build.LIB)
+        L = C.CDLL(os.environ.get("PSENGINE_LIB_AB") or _build.LIB)  # (A/B tools: another build of the library)
         for name, res, args in PROTOTYPES:
             f = getattr(L, name)
             f.restype = res
