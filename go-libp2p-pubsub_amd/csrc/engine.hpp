@@ -376,6 +376,7 @@ struct ps_engine {
   std::vector<uint8_t> node_flags;
 
   psamd::DevBuf d_row_ptr, d_col, d_node_topic, d_node_flags, d_node_peer, d_node_parent;
+  psamd::DevBuf d_ext0, d_ext1;  // compaction mode, one rank: arrival extents (ExpandArgs::ext_cur)
   psamd::DevBuf d_seen, d_arr0, d_arr1, d_hop, d_flags, d_blk, d_gen, d_frontier, d_nfront, d_wgcount,
       d_partials, d_stats, d_topics, d_seeds, d_digest, d_groups;
   uint32_t gen_cur = 0;  // window generation stamped into d_gen (1..255)

@@ -9,6 +9,10 @@
 // A frontier node p forwards arrival[p] to every child c:
 //   new = arrival[p] & ~seen[c]   (drop already-seen message ids)
 // restricted to live (subscribed) children; seen[c] |= new; arrival'[c] = new.
+// Mesh children test-and-set with atomics; a tree child's test is settled
+// without a load (deliver_tree), and on one rank a tree row of 64..704 words
+// moves only its arrival extent -- the one start-group block a node receives
+// per round (ExpandArgs::ext_cur).
 // Reference: subtree.forwardMessage (subtree.go:319-354) and
 // client.processMessages (client.go:100-132).  Design: DESIGN.md §5.
 #include <algorithm>
@@ -234,6 +238,36 @@ __device__ __forceinline__ uint64_t deliver_word(const ExpandArgs& a, bool mesh,
   return nm;
 }
 
+// A tree child whose row is current: stored, not tested.  A tree node has
+// one parent, which forwards each start group's block once, and the blocks
+// are word-disjoint (plan_window_layout), so every word that carries bits now
+// is still zero in the child's seen row -- its first visit wrote the whole
+// row, later visits only their own block's words.  (Meshes keep the atomic
+// test-and-set, expand_direct; level mode relies on the same property.)
+template <bool kRecord>
+__device__ __forceinline__ uint64_t deliver_tree(const ExpandArgs& a, bool internal, uint64_t cw, uint64_t m,
+                                                 uint32_t round, ExpandCtr& k) {
+  if (m) {
+    a.seen[cw] = m;
+    k.sw += 1;
+  }
+  if (internal) {
+    a.a_next[cw] = m;
+    k.aw += 1;
+  }
+  k.deliv += __popcll(m);
+  if constexpr (kRecord) {
+    uint16_t* h = a.hop_rec + cw * 64;
+    uint64_t b = m;
+    while (b) {
+      const int q = __ffsll(static_cast<long long>(b)) - 1;
+      h[q] = hop_round(round);
+      b &= b - 1;
+    }
+  }
+  return m;
+}
+
 // A child whose row is stale (nothing seen this window): every arriving bit is
 // new, the whole row is written, no load -- so no vmcnt wait in the burst.
 template <bool kRecord>
@@ -312,6 +346,22 @@ struct EntryCtr {
   uint32_t ent = 0, ent_words = 0, kids = 0, mesh_kids = 0, clear = 0;
 };
 
+// Arrival extents (ExpandArgs::ext_cur / ext_next) apply to rows of a
+// multi-start tree topic of 64..kStageWords words: a node at depth d receives
+// only start group r - d in round r, one block of its row, so its parent
+// writes (and it later reads) only that block's words.  Producer and
+// consumer decide by the topic alone, so they always agree.
+__device__ __forceinline__ bool ext_rows(const ExpandArgs& a, uint32_t W, uint32_t tflags) {
+  return a.ext_cur != nullptr && W >= 64 && W <= kStageWords && !(tflags & (kTopicSingleStart | kTopicMesh));
+}
+constexpr uint32_t ext_whole(uint32_t W) { return W << 16; }
+// the extent a consumer uses: ext_cur[p], or the whole row if that is not a
+// sub-range of it (a guard: the stage is sized by it)
+__device__ __forceinline__ uint32_t ext_of(const ExpandArgs& a, uint32_t p, uint32_t W) {
+  const uint32_t x = a.ext_cur[p];
+  return (x >> 16) <= W && (x & 0xFFFFu) <= (x >> 16) ? x : ext_whole(W);
+}
+
 // Direct path: one entry with its loads inline (mesh topics, rows wider than
 // the stage, fan-out above 64).
 template <bool kRecord>
@@ -328,6 +378,10 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
   const uint64_t* src = (single && !is_root) ? a.seen : a.a_cur;
   const uint64_t pw = wbase + static_cast<uint64_t>(p - nbase) * W;
   const uint64_t cbase = wbase - static_cast<uint64_t>(nbase) * W;
+  // arrival extent: words outside [xlo, xhi) of p's row are stale (read as 0)
+  const bool ext = ext_rows(a, W, tflags);
+  const uint32_t xe = ext && !is_root ? ext_of(a, p, W) : ext_whole(W);
+  const uint32_t xlo = xe & 0xFFFFu, xhi = xe >> 16;
   ec.ent += 1;
   ec.ent_words += W;
   ec.kids += deg;
@@ -367,7 +421,7 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
       for (uint32_t wb = 0; wb < W; wb += 64) {
         const uint32_t w = wb + lane;
         const bool active = w < W;
-        const uint64_t m = active ? src[pw + w] : 0ull;
+        const uint64_t m = active && w >= xlo && w < xhi ? src[pw + w] : 0ull;
         for (uint32_t jj = 0; jj < cd; ++jj) {
           const uint32_t f = rl(fj, jj);
           if (!(f & kNodeLive)) continue;
@@ -378,7 +432,10 @@ __device__ void expand_direct(const ExpandArgs& a, uint32_t p, uint32_t rs, uint
           if (active)
             nm = deliver_word<kRecord>(a, mesh, stale, internal && !single,
                                        cbase + static_cast<uint64_t>(c) * W + w, m, round, k);
-          if (internal && __ballot(nm != 0) && lane == 0) mark_next(a, c);
+          if (internal && __ballot(nm != 0) && lane == 0) {
+            mark_next(a, c);
+            if (ext) a.ext_next[c] = xe;
+          }
         }
       }
     } else {
@@ -466,7 +523,7 @@ __device__ void expand_wide(const ExpandArgs& a, WaveStage& ws, uint32_t p, uint
           const uint32_t w = wb + lane;
           if (w < len) {
             const uint64_t nm =
-                deliver_word<kRecord>(a, false, false, store, crow + w, ws.words[w], round, k);
+                deliver_tree<kRecord>(a, store, crow + w, ws.words[w], round, k);
             any |= nm != 0;
           }
         }
@@ -510,9 +567,18 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
   ExpandCtr k;
   EntryCtr ec;
 
-  for (uint64_t e0 = wave; e0 < n; e0 += 64ull * n_waves) {
+  // v: the wave's slot in the sweep, numbered XCD-major (blocks are dealt
+  // to the 8 XCDs round-robin; the blocks of one XCD take consecutive
+  // slots): neighbouring entries -- their metadata, flag and generation
+  // lines -- meet in one L2 (k_expand read traffic 1.42x -> 1.18x of its
+  // algorithmic reads at equal speed, profiles/r05/expand/NOTES.md)
+  const uint32_t v = __builtin_amdgcn_readfirstlane(
+      (gridDim.x & 7u) ? wave
+                       : ((blockIdx.x & 7u) * (gridDim.x >> 3) + (blockIdx.x >> 3)) * (kBlock / 64) +
+                             (threadIdx.x >> 6));
+  for (uint64_t e0 = v; e0 < n; e0 += 64ull * n_waves) {
     const uint64_t el = e0 + static_cast<uint64_t>(lane) * n_waves;
-    uint32_t bp = 0, brs = 0, bdeg = 0, bc0 = 0, bW = 0, bnb = 0, bfl = 0, bwl = 0, bwh = 0;
+    uint32_t bp = 0, brs = 0, bdeg = 0, bc0 = 0, bW = 0, bnb = 0, bfl = 0, bwl = 0, bwh = 0, bex = 0;
     if (el < n) {
       bp = a.frontier[el];
       const uint32_t t = a.node_topic[bp];
@@ -525,6 +591,9 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
       bwl = static_cast<uint32_t>(T.wbase);
       bwh = static_cast<uint32_t>(T.wbase >> 32);
       if (bdeg && T.W) bc0 = a.col[brs];
+      // the staged words [lo, hi) of the entry's row (lo | hi << 16)
+      bex = ext_rows(a, T.W, T.flags) && !(bp == T.nbase && (T.flags & kTopicRootLocal)) ? ext_of(a, bp, T.W)
+                                                                                          : ext_whole(T.W);
     }
     const uint32_t nb = static_cast<uint32_t>(__popcll(__ballot(el < n)));
     uint32_t q = 0;
@@ -556,11 +625,12 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
       uint32_t nq = 0, sw = 0, sd = 0;
       while (q + nq < nb) {
         const uint32_t Wn = rl(bW, q + nq), dn = rl(bdeg, q + nq), fn = rl(bfl, q + nq);
-        const uint32_t cn = rl(bc0, q + nq);
+        const uint32_t cn = rl(bc0, q + nq), xn = rl(bex, q + nq);
+        const uint32_t Ln = (xn >> 16) - (xn & 0xFFFFu);  // staged words
         const uint32_t bn = 4u * (((cn + dn + 3u) >> 2) - (cn >> 2));
         if ((fn & (kTopicMesh | kEntrySplit)) || Wn > kStageWords || dn > 64) break;
-        if (sw + Wn + (Wn & 1u) > kStageWords || sd + bn > kStageBytes) break;
-        sw += Wn + (Wn & 1u);
+        if (sw + Ln + (Ln & 1u) > kStageWords || sd + bn > kStageBytes) break;
+        sw += Ln + (Ln & 1u);
         sd += bn;
         ++nq;
       }
@@ -574,18 +644,20 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
           const uint64_t wbase = (static_cast<uint64_t>(rl(bwh, i)) << 32) | rl(bwl, i);
           const uint32_t fl = rl(bfl, i);
           const bool from_seen = (fl & kTopicSingleStart) && !(p == nbase && (fl & kTopicRootLocal));
+          // the row's words [lo, lo + L): its arrival extent (even bounds) or all of it
+          const uint32_t xe = rl(bex, i), lo = xe & 0xFFFFu, L = (xe >> 16) - lo;
           const uint32_t* row = reinterpret_cast<const uint32_t*>(
-              (from_seen ? a.seen : a.a_cur) + wbase + static_cast<uint64_t>(p - nbase) * W);
+              (from_seen ? a.seen : a.a_cur) + wbase + static_cast<uint64_t>(p - nbase) * W + lo);
           uint32_t* dst = reinterpret_cast<uint32_t*>(ws.words + off);
           if ((W & 1u) == 0) {
             // even W: the row and its stage slot are 16-B aligned (topic
             // blocks start on 128-B lines, slots keep even offsets): one
             // dwordx4 DMA per lane, 1 KiB per wave instruction
-            for (uint32_t d = 0; d < 2 * W; d += 256)
-              if (d + 4 * lane < 2 * W) PSAMD_LDS_DMA(row + d + 4 * lane, dst + d, 16);
+            for (uint32_t d = 0; d < 2 * L; d += 256)
+              if (d + 4 * lane < 2 * L) PSAMD_LDS_DMA(row + d + 4 * lane, dst + d, 16);
           } else {
-            for (uint32_t d = 0; d < 2 * W; d += 64)
-              if (d + lane < 2 * W) PSAMD_LDS_DMA(row + d + lane, dst + d, 4);
+            for (uint32_t d = 0; d < 2 * L; d += 64)
+              if (d + lane < 2 * L) PSAMD_LDS_DMA(row + d + lane, dst + d, 4);
           }
           const uint32_t nd = ((c0 + deg + 3u) >> 2) - (c0 >> 2);
           if (lane < nd) {
@@ -594,7 +666,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
             PSAMD_LDS_DMA(reinterpret_cast<const uint32_t*>(a.gen) + (c0 >> 2) + lane,
                           ws.gens + doff, 4);
           }
-          off += W + (W & 1u);  // keep every staged row 16-B aligned
+          off += L + (L & 1u);  // keep every staged row 16-B aligned
           doff += 4u * nd;
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -612,10 +684,34 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
           const uint32_t fo = doff + (c0 & 3u);  // byte of child 0
           // single-start topics keep no arrival rows (see kTopicSingleStart)
           const bool keep = !(rl(bfl, i) & kTopicSingleStart);
+          const uint32_t xe = rl(bex, i), lo = xe & 0xFFFFu, hi = xe >> 16;  // staged words
           ec.ent += 1;
-          ec.ent_words += W;
+          ec.ent_words += hi - lo;
           ec.kids += deg;
           if (W >= 64) {
+            // extent rows: the children's rows change only in [tlo, thi), the
+            // staged words' nonzero range (even bounds); their arrival rows
+            // are written there alone and it becomes their extent
+            const bool ext = ext_rows(a, W, rl(bfl, i));
+            uint32_t tlo = lo, thi = hi;
+            if (ext) {
+              tlo = hi;
+              thi = lo;
+              for (uint32_t wb = lo; wb < hi; wb += 64) {
+                const uint32_t w = wb + lane;
+                const uint64_t nz = __ballot(w < hi && ws.words[off + w - lo] != 0);
+                if (nz) {
+                  tlo = min(tlo, wb + static_cast<uint32_t>(__ffsll(static_cast<long long>(nz))) - 1u);
+                  thi = wb + 64u - static_cast<uint32_t>(__clzll(static_cast<long long>(nz)));
+                }
+              }
+              if (tlo >= thi) {
+                tlo = thi = lo;
+              } else {
+                tlo &= ~1u;
+                thi = (thi + 1u) & ~1u;
+              }
+            }
             for (uint32_t jj = 0; jj < deg; ++jj) {
               const uint32_t f = ws.flags[fo + jj];
               if (!(f & kNodeLive)) continue;
@@ -626,27 +722,32 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
               const uint64_t row = cbase + static_cast<uint64_t>(c) * W;
               bool any = false;
               if (stale) {
-                // W even, row and stage offset even: two words per lane,
-                // 1 KiB per store instruction
+                // the whole seen row (zeros outside the staged words); W
+                // even, row and stage offset even: two words per lane, 1 KiB
+                // per store instruction
                 for (uint32_t wb = 0; wb < W; wb += 128) {
                   const uint32_t w = wb + 2 * lane;
                   if (w < W) {
-                    const uint4 v = *reinterpret_cast<const uint4*>(ws.words + off + w);
-                    deliver_fresh2<kRecord>(a, store, row + w, v, round, k);
+                    const bool in = w >= tlo && w < thi;
+                    const uint4 v = in ? *reinterpret_cast<const uint4*>(ws.words + off + w - lo)
+                                       : make_uint4(0u, 0u, 0u, 0u);
+                    deliver_fresh2<kRecord>(a, store && (in || !ext), row + w, v, round, k);
                     any |= (v.x | v.y | v.z | v.w) != 0;
                   }
                 }
               } else {
-                for (uint32_t wb = 0; wb < W; wb += 64) {
+                for (uint32_t wb = tlo; wb < thi; wb += 64) {
                   const uint32_t w = wb + lane;
-                  if (w < W) {
-                    const uint64_t nm = deliver_word<kRecord>(a, false, false, store, row + w,
-                                                              ws.words[off + w], round, k);
+                  if (w < thi) {
+                    const uint64_t nm = deliver_tree<kRecord>(a, store, row + w, ws.words[off + w - lo], round, k);
                     any |= nm != 0;
                   }
                 }
               }
-              if (internal && __ballot(any) && lane == 0) mark_next(a, c);
+              if (internal && __ballot(any) && lane == 0) {
+                mark_next(a, c);
+                if (ext) a.ext_next[c] = tlo | thi << 16;
+              }
             }
           } else {
             const uint32_t sh = pow2_shift(W);
@@ -671,8 +772,12 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
                   nm = m;
                 }
               } else if (live) {
-                nm = deliver_word<kRecord>(a, false, stale, keep && (f & kNodeInternal), cw, m,
-                                           round, k);
+                if (stale) {
+                  deliver_fresh<kRecord>(a, keep && (f & kNodeInternal), cw, m, round, k);
+                  nm = m;
+                } else {
+                  nm = deliver_tree<kRecord>(a, keep && (f & kNodeInternal), cw, m, round, k);
+                }
               }
               const uint64_t bal = __ballot(nm != 0);
               if (live && w == 0 && (f & kNodeInternal) && (bal & gmask)) mark_next(a, c);
@@ -686,7 +791,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
             for (uint32_t w = lane; w < W; w += 64) a.a_cur[pw + w] = 0;
             ec.clear += W;
           }
-          off += W + (W & 1u);
+          off += (hi - lo) + ((hi - lo) & 1u);  // (as phase A)
           doff += 4u * nd;
         }
       }

@@ -122,6 +122,12 @@ struct ExpandArgs {
   uint64_t* a_cur;   // arrivals of the current frontier
   uint64_t* a_next;  // arrivals for the next frontier
   uint64_t* seen;    // per-node delivered bitset (the dedup record)
+  // arrival extents (one rank; nullptr: whole rows): per node the word range
+  // [lo, hi) of its arrival row written this round (lo | hi << 16), kept for
+  // multi-start tree topics of 64..kStageWords words; the row outside it is
+  // stale and never read
+  uint32_t* ext_cur;
+  uint32_t* ext_next;
   uint8_t* gen;      // per-node window generation of its seen row (tree topics)
   uint8_t* next_flag;
   uint8_t* blk_flag;  // one byte per kFlagsPerBlock nodes: some flag set

@@ -1200,6 +1200,13 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
     }
   } else {
     e->round_kind.clear();  // (accumulate_window: every round k_expand)
+    uint32_t* ext[2] = {nullptr, nullptr};
+    if (world == 1) {  // (ghost-fed rows arrive whole: N ranks keep whole rows)
+      HIP_TRY(e->d_ext0.ensure(static_cast<size_t>(e->n_pad) * 4), "alloc extents");
+      HIP_TRY(e->d_ext1.ensure(static_cast<size_t>(e->n_pad) * 4), "alloc extents");
+      ext[0] = e->d_ext0.as<uint32_t>();
+      ext[1] = e->d_ext1.as<uint32_t>();
+    }
     HIP_TRY(seed_round(0, arr[0]), "seed");
     HIP_TRY(compact(0, 0), "compact");
     while (true) {
@@ -1207,6 +1214,8 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
         ++r;
         a.a_cur = arr[(r - 1) & 1];
         a.a_next = arr[r & 1];
+        a.ext_cur = ext[(r - 1) & 1];
+        a.ext_next = ext[r & 1];
         const bool xr = layout(r);
         if (xr)
           for (int32_t q = 0; q < world; ++q)

@@ -184,3 +184,77 @@ def test_cfg3_staggered_full_size():
             ids = np.nonzero(wl.msg_topics == t)[0]
             for m in ids[np.linspace(0, len(ids) - 1, 16).astype(int)]:
                 assert np.array_equal(eng.delivered(first + int(m)), members[t]), (t, m)
+        # the compaction path (bench.py's general_path.compaction: arrival
+        # extents for the 64..704-word rows of topics 0..6) on the same engine
+        eng.set_flags(eng.flags | PE.F_COMPACT)
+        first = eng.publish(wl.msg_topics, starts)
+        st = eng.run()
+        assert st.expand_mode == PE.MODE_COMPACT
+        assert (st.deliveries, st.rounds, st.as_dict()["deliveries_per_round"], eng.seen_digest()) == ref
+        for t in (0, 8):
+            m = int(np.nonzero(wl.msg_topics == t)[0][-1])
+            assert np.array_equal(eng.delivered(first + m), members[t]), (t, m)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_compaction_extents_match_level(seed):
+    """Compaction-path arrival extents (ExpandArgs::ext_cur): staggered tree
+    topics whose rows are 64..704 words (each node receives one start group's
+    block per round, so only that block of its arrival row is written and
+    read), beside a narrow staggered topic, a single-start topic, a node with
+    more than 64 children (the direct path consumes and produces extents) and
+    dead peers; two windows per run.  Hops equal the oracle (recording
+    instance) and the production instance leaves the same counters and seen
+    digest as level mode."""
+    rng = np.random.default_rng(900 + seed)
+    n = int(rng.integers(1500, 3000))
+    topics = []
+    for t in range(3):
+        root = int(rng.integers(0, n))
+        parent = random_tree(rng, n, root, fan=int(rng.integers(2, 6)))
+        if t == 0:  # a hub: > 64 children (deg > 64 entries take the direct path)
+            hub = int(parent[int(rng.integers(0, n))])
+            hub = hub if hub != O.NONE else root
+            anc, x = set(), hub
+            while x != O.NONE:
+                anc.add(int(x))
+                x = parent[x]
+            movable = [v for v in rng.permutation(n) if int(v) not in anc][:90]
+            parent[movable] = hub
+        topics.append((root, parent))
+    live = (rng.random(n) > 0.1).astype(np.uint8)
+    for root, _ in topics:
+        live[root] = 1
+    # topic 0: 9000 messages over starts 0..7 (windows of 8000 messages: 8
+    # groups of 12 or 8 words, W = 96 / 64); topic 1: 480 (W = 8 / 16);
+    # topic 2: 4500 at one start
+    msg_topics = np.concatenate([np.zeros(9000, np.uint32), np.ones(480, np.uint32),
+                                 np.full(4500, 2, np.uint32)])
+    starts = np.concatenate([rng.integers(0, 8, size=9480), np.full(4500, 2)]).astype(np.uint32)
+    order = rng.permutation(len(msg_topics))
+    msg_topics, starts = msg_topics[order], starts[order]
+    exp = {}
+    for t, (root, parent) in enumerate(topics):
+        rp, cl = O.parents_to_csr(parent)
+        exp[t] = O.disseminate(rp, cl, root, live, 1)[1][0]
+    outs = []
+    for level, record in ((True, False), (False, False), (False, True)):
+        with PE.Engine(n, 3, record_hops=record, msg_window=8000, flags=0 if level else PE.F_COMPACT) as eng:
+            for t, (root, parent) in enumerate(topics):
+                eng.set_tree(t, root, parent)
+            eng.set_live(live)
+            first = eng.publish(msg_topics, starts)
+            st = eng.run()
+            assert st.windows >= 2 and st.duplicates == 0
+            assert (st.expand_mode == PE.MODE_COMPACT) == (not level)
+            if record:
+                for m in list(rng.choice(len(msg_topics), 120, replace=False)) + [len(msg_topics) - 1]:
+                    want = exp[int(msg_topics[m])]
+                    got = eng.hops(first + int(m))
+                    if not np.array_equal(got, want):
+                        bad = np.nonzero(got != want)[0][:8]
+                        raise AssertionError(f"msg {m} topic {msg_topics[m]} start {starts[m]}: peers {bad} "
+                                             f"got {got[bad]} want {want[bad]}")
+            outs.append((st.deliveries, st.as_dict()["deliveries_per_round"], eng.seen_digest()))
+    assert outs[0] == outs[1] == outs[2]
+    assert outs[0][0] == sum(int(((exp[int(t)] != 0xFF) & (exp[int(t)] > 0)).sum()) for t in msg_topics)

@@ -32,7 +32,8 @@ def main():
     rd = sum(summ[k]["hbm_read_bytes_per_dispatch_x2"] * summ[k]["WRITE_SIZE"]["dispatches"] for k in names) / disp
     wr = sum(summ[k]["hbm_write_bytes_per_dispatch"] * summ[k]["WRITE_SIZE"]["dispatches"] for k in names) / disp
     os.makedirs(os.path.join(REPO, "profiles", rtag), exist_ok=True)
-    dst = os.path.join("profiles", rtag, f"pmc_summary_{workload}.json")
+    # (one file per kernel and workload: two kernels of one workload may come from different runs)
+    dst = os.path.join("profiles", rtag, f"pmc_summary_{workload}_{kernel}.json")
     shutil.copy(summ_path, os.path.join(REPO, dst))
     entry = {"kernel": kernel, "workload": workload, "instances": names, "dispatches": disp,
              "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
