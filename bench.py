@@ -365,8 +365,14 @@ def bench_cfg5(args):
     tot += st.deliveries
     run_gpu += st.run_ms
     wall = time.perf_counter() - t0
-    per, st = instrumented(
-        eng, lambda it=iter(range(args.warmup + args.steps, args.warmup + args.steps + 3)): step(next(it))[0], 3)
+    gpu_ms = []  # device span of the blocking instrumented batches (init start .. reduce end)
+
+    def blocking(it=iter(range(args.warmup + args.steps, args.warmup + args.steps + 3))):
+        st_b = step(next(it))[0]
+        gpu_ms.append(st_b.run_ms)
+        return st_b
+
+    per, st = instrumented(eng, blocking, 3)
     out = {
         "metric": METRIC + " [cfg5 end to end]",
         "value": tot / wall,
@@ -381,10 +387,15 @@ def bench_cfg5(args):
                                   "join_host": join_s * 1e3 / args.steps,
                                   "ps_run_async_host": run_host / args.steps,
                                   "ps_wait": wait_s * 1e3 / args.steps,
-                                  "ps_run_gpu": run_gpu / args.steps,
+                                  "ps_run_gpu": sum(gpu_ms) / len(gpu_ms),
+                                  "window_span_pipelined": run_gpu / args.steps,
                                   "note": "ps_run_async_host = rebuild + plan + launch + lazy prune of the batch "
                                           "(host wall inside the call); its propagation overlaps the next "
-                                          "batch's churn"},
+                                          "batch's churn. ps_run_gpu = the window's device span (init start .. "
+                                          "reduce end) in the blocking instrumented batches; "
+                                          "window_span_pipelined = the same stamps in the timed pipelined "
+                                          "batches, where a window's counter reduce rides in the next batch's "
+                                          "first launch (after that batch's host churn)"},
         "roofline": roofline_of(per),
         "last_step": {"deliveries": st.deliveries, "rounds": st.rounds, "host_ms": st.host_ms,
                       "run_ms": st.run_ms},
@@ -449,6 +460,8 @@ def general_path(eng, wl, deliv_expected, steps: int, warmup: int = 1, max_start
     finally:
         eng.set_flags(flags)
     comp["workload"] = "the same steps through the compaction path (PS_F_COMPACT): k_expand + frontier compaction"
+    comp["note"] = ("k_expand moves only arrival extents (one start-group block per node and round) and is "
+                    "scalar-issue bound, not HBM-bound: SQ counters and A/B records in profiles/r05/expand/NOTES.md")
     out["compaction"] = comp
     return out
 
