@@ -554,7 +554,8 @@ __device__ void expand_wide(const ExpandArgs& a, WaveStage& ws, uint32_t p, uint
 // are left to the second instance); kDirect = true: the direct path only.
 // Separate instances keep the hot staged kernel's register budget small.
 template <bool kRecord, bool kDirect>
-__global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void k_expand(ExpandArgs a,
+                                                                                            uint32_t round) {
   __shared__ WaveStage stage_lds[kDirect ? 1 : kBlock / 64];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave =
@@ -579,6 +580,10 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
   for (uint64_t e0 = v; e0 < n; e0 += 64ull * n_waves) {
     const uint64_t el = e0 + static_cast<uint64_t>(lane) * n_waves;
     uint32_t bp = 0, brs = 0, bdeg = 0, bc0 = 0, bW = 0, bnb = 0, bfl = 0, bwl = 0, bwh = 0, bex = 0;
+    // per lane, so the staged phases broadcast them instead of recomputing
+    // them in scalar registers: the staged row's address, the children's
+    // row base, the flag dwords
+    uint32_t brl = 0, brh = 0, bcl = 0, bch = 0, bnd = 0, bst = 0;
     if (el < n) {
       bp = a.frontier[el];
       const uint32_t t = a.node_topic[bp];
@@ -594,6 +599,20 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
       // the staged words [lo, hi) of the entry's row (lo | hi << 16)
       bex = ext_rows(a, T.W, T.flags) && !(bp == T.nbase && (T.flags & kTopicRootLocal)) ? ext_of(a, bp, T.W)
                                                                                           : ext_whole(T.W);
+      const bool from_seen = (T.flags & kTopicSingleStart) && !(bp == T.nbase && (T.flags & kTopicRootLocal));
+      const uint64_t rp = reinterpret_cast<uint64_t>((from_seen ? a.seen : a.a_cur) + T.wbase +
+                                                     static_cast<uint64_t>(bp - T.nbase) * T.W + (bex & 0xFFFFu));
+      brl = static_cast<uint32_t>(rp);
+      brh = static_cast<uint32_t>(rp >> 32);
+      // the children's rows: child c0's row, the others follow at stride W
+      const uint64_t cb = T.wbase + static_cast<uint64_t>(bc0 - T.nbase) * T.W;
+      bcl = static_cast<uint32_t>(cb);
+      bch = static_cast<uint32_t>(cb >> 32);
+      bnd = ((bc0 + bdeg + 3u) >> 2) - (bc0 >> 2);
+      // stage needs (staged words, even | flag dwords << 16), or ~0: not staged
+      const uint32_t Ls = (bex >> 16) - (bex & 0xFFFFu);
+      bst = ((bfl & (kTopicMesh | kEntrySplit)) || T.W > kStageWords || bdeg > 64) ? ~0u
+                                                                                  : (Ls + (Ls & 1u)) | (4u * bnd) << 16;
     }
     const uint32_t nb = static_cast<uint32_t>(__popcll(__ballot(el < n)));
     uint32_t q = 0;
@@ -624,13 +643,11 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
       // (sub-dword LDS-DMA does not pack lanes byte by byte)
       uint32_t nq = 0, sw = 0, sd = 0;
       while (q + nq < nb) {
-        const uint32_t Wn = rl(bW, q + nq), dn = rl(bdeg, q + nq), fn = rl(bfl, q + nq);
-        const uint32_t cn = rl(bc0, q + nq), xn = rl(bex, q + nq);
-        const uint32_t Ln = (xn >> 16) - (xn & 0xFFFFu);  // staged words
-        const uint32_t bn = 4u * (((cn + dn + 3u) >> 2) - (cn >> 2));
-        if ((fn & (kTopicMesh | kEntrySplit)) || Wn > kStageWords || dn > 64) break;
-        if (sw + Ln + (Ln & 1u) > kStageWords || sd + bn > kStageBytes) break;
-        sw += Ln + (Ln & 1u);
+        const uint32_t sn = rl(bst, q + nq);
+        if (sn == ~0u) break;
+        const uint32_t Ln = sn & 0xFFFFu, bn = sn >> 16;  // staged words (even), flag bytes
+        if (sw + Ln > kStageWords || sd + bn > kStageBytes) break;
+        sw += Ln;
         sd += bn;
         ++nq;
       }
@@ -638,16 +655,13 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
       {
         uint32_t off = 0, doff = 0;
         for (uint32_t i = q; i < q + nq; ++i) {
-          const uint32_t W = rl(bW, i), deg = rl(bdeg, i);
+          const uint32_t W = rl(bW, i);
           if (W == 0) continue;
-          const uint32_t p = rl(bp, i), nbase = rl(bnb, i), c0 = rl(bc0, i);
-          const uint64_t wbase = (static_cast<uint64_t>(rl(bwh, i)) << 32) | rl(bwl, i);
-          const uint32_t fl = rl(bfl, i);
-          const bool from_seen = (fl & kTopicSingleStart) && !(p == nbase && (fl & kTopicRootLocal));
+          const uint32_t c0 = rl(bc0, i);
           // the row's words [lo, lo + L): its arrival extent (even bounds) or all of it
           const uint32_t xe = rl(bex, i), lo = xe & 0xFFFFu, L = (xe >> 16) - lo;
-          const uint32_t* row = reinterpret_cast<const uint32_t*>(
-              (from_seen ? a.seen : a.a_cur) + wbase + static_cast<uint64_t>(p - nbase) * W + lo);
+          const uint32_t* row =
+              reinterpret_cast<const uint32_t*>((static_cast<uint64_t>(rl(brh, i)) << 32) | rl(brl, i));
           uint32_t* dst = reinterpret_cast<uint32_t*>(ws.words + off);
           if ((W & 1u) == 0) {
             // even W: the row and its stage slot are 16-B aligned (topic
@@ -659,7 +673,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
             for (uint32_t d = 0; d < 2 * L; d += 64)
               if (d + lane < 2 * L) PSAMD_LDS_DMA(row + d + lane, dst + d, 4);
           }
-          const uint32_t nd = ((c0 + deg + 3u) >> 2) - (c0 >> 2);
+          const uint32_t nd = rl(bnd, i);
           if (lane < nd) {
             PSAMD_LDS_DMA(reinterpret_cast<const uint32_t*>(a.node_flags) + (c0 >> 2) + lane,
                           ws.flags + doff, 4);
@@ -677,10 +691,9 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
         for (uint32_t i = q; i < q + nq; ++i) {
           const uint32_t W = rl(bW, i), deg = rl(bdeg, i);
           if (W == 0) continue;
-          const uint32_t p = rl(bp, i), nbase = rl(bnb, i), c0 = rl(bc0, i);
-          const uint64_t wbase = (static_cast<uint64_t>(rl(bwh, i)) << 32) | rl(bwl, i);
-          const uint64_t cbase = wbase - static_cast<uint64_t>(nbase) * W;
-          const uint32_t nd = ((c0 + deg + 3u) >> 2) - (c0 >> 2);
+          const uint32_t c0 = rl(bc0, i);
+          const uint64_t crow0 = (static_cast<uint64_t>(rl(bch, i)) << 32) | rl(bcl, i);  // child c0's row
+          const uint32_t nd = rl(bnd, i);
           const uint32_t fo = doff + (c0 & 3u);  // byte of child 0
           // single-start topics keep no arrival rows (see kTopicSingleStart)
           const bool keep = !(rl(bfl, i) & kTopicSingleStart);
@@ -719,7 +732,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
               const bool internal = (f & kNodeInternal) != 0;
               const bool store = internal && keep;
               const uint32_t c = c0 + jj;
-              const uint64_t row = cbase + static_cast<uint64_t>(c) * W;
+              const uint64_t row = crow0 + static_cast<uint64_t>(jj) * W;
               bool any = false;
               if (stale) {
                 // the whole seen row (zeros outside the staged words); W
@@ -764,7 +777,7 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
               const bool live = valid && (f & kNodeLive);
               const bool stale = ws.gens[fo + jj] != cur;
               const uint32_t c = c0 + jj;
-              const uint64_t cw = cbase + static_cast<uint64_t>(c) * W + w;
+              const uint64_t cw = crow0 + static_cast<uint64_t>(jj) * W + w;
               uint64_t nm = 0;
               if (__ballot(live && !stale) == 0) {  // burst: every live child fresh
                 if (live) {
@@ -786,8 +799,8 @@ __global__ __launch_bounds__(kBlock) void k_expand(ExpandArgs a, uint32_t round)
           // live children hold current rows now
           if (lane < deg && (ws.flags[fo + lane] & kNodeLive))
             a.gen[c0 + lane] = static_cast<uint8_t>(cur);
-          if (p == nbase && (rl(bfl, i) & kTopicRootLocal)) {  // seeded with |=: consume-and-clear
-            const uint64_t pw = wbase + static_cast<uint64_t>(p - nbase) * W;
+          if (rl(bp, i) == rl(bnb, i) && (rl(bfl, i) & kTopicRootLocal)) {  // seeded with |=: consume-and-clear
+            const uint64_t pw = (static_cast<uint64_t>(rl(bwh, i)) << 32) | rl(bwl, i);  // (the root: node nbase)
             for (uint32_t w = lane; w < W; w += 64) a.a_cur[pw + w] = 0;
             ec.clear += W;
           }
