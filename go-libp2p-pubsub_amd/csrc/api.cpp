@@ -35,14 +35,25 @@ int dist_common(ps_engine* e, const ps_dist_config* dc) {
   if (dc->flags & ~(PS_DIST_F_COPY | PS_DIST_F_INPLACE)) return e->fail(PS_E_INVAL, "unknown dist flag");
   if ((dc->flags & PS_DIST_F_COPY) && (dc->flags & PS_DIST_F_INPLACE))
     return e->fail(PS_E_INVAL, "PS_DIST_F_INPLACE reads rows in place: not with PS_DIST_F_COPY");
-  e->inplace = dc->world > 1 && (dc->flags & PS_DIST_F_INPLACE) != 0;
   if (!e->pending.empty()) return e->fail(PS_E_STATE, "messages pending");
+  // (every check above passed: the mode changes together with rank and world)
+  e->inplace = dc->world > 1 && (dc->flags & PS_DIST_F_INPLACE) != 0;
   e->rank = dc->rank;
   e->world = dc->world;
   e->partition = dc->partition;
   e->split_depth = dc->split_depth;
   e->graph_dirty = true;
   return PS_OK;
+}
+
+// a transport that failed to come up leaves the engine on one rank
+int dist_undo(ps_engine* e, int code, const std::string& why) {
+  e->transport.reset();
+  e->rank = 0;
+  e->world = 1;
+  e->inplace = false;
+  e->graph_dirty = true;
+  return e->fail(code, why);
 }
 
 // N ranks: the exchange stream and the round events (the exchange of round q
@@ -708,16 +719,35 @@ int ps_dist_unique_id(uint8_t id_out[PS_UNIQUE_ID_BYTES]) {
 }
 
 int ps_dist_init(ps_engine* e, const ps_dist_config* dc, const uint8_t id[PS_UNIQUE_ID_BYTES]) {
-  if (!id) return PS_E_INVAL;
-  if (dc && (dc->flags & PS_DIST_F_INPLACE))  // (separate processes: no shared row sets)
-    return e->fail(PS_E_INVAL, "PS_DIST_F_INPLACE needs ranks that share one address space (the loopback)");
+  if (!e || !dc || !id) return PS_E_INVAL;
+  if (dc->flags & PS_DIST_F_INPLACE)  // (RCCL moves records; mapped row sets are ps_dist_init_ipc's)
+    return e->fail(PS_E_INVAL, "PS_DIST_F_INPLACE needs mapped row sets: ps_dist_init_ipc or the loopback");
   int rc = dist_common(e, dc);
   if (rc) return rc;
   if (dc->world == 1) return PS_OK;
   if ((rc = dist_streams(e))) return rc;
   std::string err;
   e->transport = make_rccl_transport(dc->rank, dc->world, id, &err);
-  if (!e->transport) return e->fail(PS_E_DEVICE, err);
+  if (!e->transport) return dist_undo(e, PS_E_DEVICE, err);
+  refresh_xchg_overlap(e);
+  return PS_OK;
+}
+
+int ps_dist_ipc_id(uint8_t id_out[PS_UNIQUE_ID_BYTES]) {
+  if (!id_out) return PS_E_INVAL;
+  return ipc_group_id(id_out) == 0 ? PS_OK : PS_E_DEVICE;
+}
+
+int ps_dist_init_ipc(ps_engine* e, const ps_dist_config* dc, const uint8_t id[PS_UNIQUE_ID_BYTES]) {
+  if (!e || !dc || !id) return PS_E_INVAL;
+  int rc = dist_common(e, dc);
+  if (rc) return rc;
+  if (dc->world == 1) return PS_OK;
+  if ((rc = dist_streams(e))) return rc;
+  std::string err;
+  e->transport = make_ipc_transport(dc->rank, dc->world, e->cfg.device, id, e->cfg.n_topics,
+                                    (dc->flags & PS_DIST_F_COPY) != 0, (dc->flags & PS_DIST_F_INPLACE) != 0, &err);
+  if (!e->transport) return dist_undo(e, PS_E_DEVICE, err);
   refresh_xchg_overlap(e);
   return PS_OK;
 }
@@ -740,14 +770,14 @@ void ps_loopback_destroy(ps_loopback* lb) {
 }
 
 int ps_dist_init_loopback(ps_engine* e, const ps_dist_config* dc, ps_loopback* lb) {
-  if (!lb) return PS_E_INVAL;
+  if (!e || !dc || !lb) return PS_E_INVAL;
   int rc = dist_common(e, dc);
   if (rc) return rc;
   if (dc->world == 1) return PS_OK;
   if ((rc = dist_streams(e))) return rc;
   e->transport = make_loopback_transport(lb->g, dc->rank, e->cfg.device, (dc->flags & PS_DIST_F_COPY) != 0,
                                          (dc->flags & PS_DIST_F_INPLACE) != 0);
-  if (!e->transport) return e->fail(PS_E_INVAL, "loopback group size != world");
+  if (!e->transport) return dist_undo(e, PS_E_INVAL, "loopback group size != world");
   refresh_xchg_overlap(e);
   return PS_OK;
 }

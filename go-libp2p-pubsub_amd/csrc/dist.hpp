@@ -11,6 +11,9 @@
 //                      level mode with PS_DIST_F_COPY) or, in level mode, read
 //                      them in place (zero-copy); lets the real kernels and
 //                      routing be tested on a single GPU.
+//   IpcTransport       one process per rank (several may share a GPU): the
+//                      loopback's three data paths over IPC-mapped device
+//                      memory, ordered by device flags instead of events.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -97,6 +100,23 @@ class Transport {
 std::unique_ptr<Transport> make_rccl_transport(int rank, int world, const uint8_t id[128],
                                                std::string* err);
 int rccl_unique_id(uint8_t id_out[128]);
+
+// Process-shared transport: one process per rank on one node (several may
+// share a GPU).  Host-side rendezvous in a POSIX shared-memory segment named
+// by `id` (ipc_group_id on one rank, shipped by the caller like the RCCL id);
+// device buffers mapped across processes with hipIpcGetMemHandle /
+// hipIpcOpenMemHandle; stream order between ranks by monotonic device flags
+// (launch_flag_set / launch_flag_wait) in IPC-mapped memory.  Modes as the
+// loopback's: copy (exchange into the receive buffer), zero copy (read the
+// sender's region in place), in-place rows.
+int ipc_group_id(uint8_t id_out[128]);
+std::unique_ptr<Transport> make_ipc_transport(int rank, int world, int device, const uint8_t id[128],
+                                             uint32_t n_topics, bool copy, bool in_place, std::string* err);
+// Every device free bumps this epoch: an IPC export of an address range is
+// reused only while no range was freed since (a freed range's address may
+// come back as another allocation).
+void note_device_free();
+uint64_t device_free_epoch();
 
 struct LoopbackGroup;
 LoopbackGroup* loopback_create(int world);

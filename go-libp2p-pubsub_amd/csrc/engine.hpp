@@ -45,7 +45,10 @@ struct DevBuf {
   DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() { release(); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      (void)hipFree(p);
+      psamd::note_device_free();  // (IPC exports of a freed range are stale)
+    }
     p = nullptr;
     bytes = 0;
   }

@@ -1221,6 +1221,43 @@ hipError_t launch_copy_regions(const CopyRegions& c, hipStream_t s) {
   return hipGetLastError();
 }
 
+// One lane: the flag store.  The launches before it on the stream ended with
+// their release (rows and records written back past the XCDs' L2s); the
+// store itself is a vector atomic at system scope.
+__global__ void k_flag_set(uint64_t* flag, uint64_t value) {
+  if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Lane q polls rank q's flag; the wave leaves when every lane is satisfied or
+// the clock runs out (every wave reaches the exit: a dead peer cannot hang
+// the GPU, it fails the window through *err).
+__global__ void k_flag_wait(FlagWait w, uint32_t* err, uint64_t timeout_ticks) {
+  const uint32_t q = threadIdx.x;
+  const uint64_t* f = q < static_cast<uint32_t>(kMaxRanks) ? w.flag[q] : nullptr;
+  const uint64_t want = f ? w.value[q] : 0;
+  bool done = f == nullptr;
+  const uint64_t t0 = wall_clock64();
+  for (;;) {
+    if (!done) done = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= want;
+    if (__all(done)) break;
+    if (wall_clock64() - t0 > timeout_ticks) {
+      if (!done) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+hipError_t launch_flag_set(uint64_t* flag, uint64_t value, hipStream_t s) {
+  hipLaunchKernelGGL(k_flag_set, dim3(1), dim3(64), 0, s, flag, value);
+  return hipGetLastError();
+}
+
+hipError_t launch_flag_wait(const FlagWait& w, uint32_t* err, uint64_t timeout_ticks, hipStream_t s) {
+  hipLaunchKernelGGL(k_flag_wait, dim3(1), dim3(64), 0, s, w, err, timeout_ticks);
+  return hipGetLastError();
+}
+
 hipError_t launch_stage_copy(const StageCopy& c, hipStream_t s) {
   uint32_t most = 0;
   for (uint32_t k = 0; k < c.n; ++k) most = c.words[k] > most ? c.words[k] : most;

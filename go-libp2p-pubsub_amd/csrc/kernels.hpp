@@ -425,6 +425,18 @@ struct CopyRegions {
   uint32_t n;
 };
 hipError_t launch_copy_regions(const CopyRegions& c, hipStream_t s);
+// Process-shared exchange (dist.cpp IpcTransport): stream-ordered device
+// flags in IPC-mapped memory.  launch_flag_set stores `value` into `flag`
+// (system-scope release, after every launch before it on the stream);
+// launch_flag_wait holds the stream until every non-null flag[q] >= value[q]
+// (system-scope acquire polls) or `timeout_ticks` of the 100 MHz clock pass,
+// then ORs 1 into *err (pinned host memory) and lets the stream go on.
+struct FlagWait {
+  const uint64_t* flag[kMaxRanks];
+  uint64_t value[kMaxRanks];
+};
+hipError_t launch_flag_set(uint64_t* flag, uint64_t value, hipStream_t s);
+hipError_t launch_flag_wait(const FlagWait& w, uint32_t* err, uint64_t timeout_ticks, hipStream_t s);
 // Window start: zero and stamp the roots' rows (every row of a mesh topic);
 // optionally in the same launch (WindowStart): the staged per-window copies
 // (topics_src / seeds_src then point at the staged sources), the round-0

@@ -5,7 +5,6 @@
 // frontier compaction), counters and readbacks.  DESIGN.md §5-§7.
 #include <algorithm>
 #include <chrono>
-#include <immintrin.h>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -14,6 +13,16 @@
 
 #include "engine.hpp"
 #include "gbuild.hpp"
+
+namespace {
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#else
+  std::this_thread::yield();
+#endif
+}
+}  // namespace
 
 namespace psamd {
 
@@ -1755,7 +1764,7 @@ int ps_wait(ps_engine* e, ps_stats* out) {
     // publishing the next batch from another thread is not starved
     const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t spin = 0; *flag != f.seq; ++spin) {
-      _mm_pause();
+      cpu_relax();
       if ((spin & 255) == 255) {
         const hipError_t q = hipStreamQuery(f.stream ? f.stream : e->stream);
         if (q != hipSuccess && q != hipErrorNotReady) return e->fail(PS_E_DEVICE, "window: stream failed");

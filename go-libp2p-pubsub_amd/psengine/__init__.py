@@ -158,6 +158,8 @@ PROTOTYPES = [
     ("ps_msg_decode", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(MessageBuf), C.POINTER(C.c_size_t)]),
     ("ps_dist_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("ps_dist_init", C.c_int, [_P, C.POINTER(DistConfig), C.POINTER(C.c_uint8)]),
+    ("ps_dist_ipc_id", C.c_int, [C.POINTER(C.c_uint8)]),
+    ("ps_dist_init_ipc", C.c_int, [_P, C.POINTER(DistConfig), C.POINTER(C.c_uint8)]),
     ("ps_loopback_create", C.c_int, [C.c_int32, C.POINTER(_P)]),
     ("ps_loopback_destroy", None, [_P]),
     ("ps_dist_init_loopback", C.c_int, [_P, C.POINTER(DistConfig), _P]),
@@ -180,7 +182,9 @@ def load(build_if_missing: bool = False):
                 raise FileNotFoundError(
                     f"{_build.LIB} missing: run __graft_entry__.build() (no CPU fallback exists)")
             _build.build()
-        L = C.CDLL(os.environ.get("PSENGINE_LIB_AB") or _build.LIB)  # (A/B tools: another build of the library)
+        # (A/B tools: another build of the library, only under PSAMD_AB=1)
+        ab = os.environ.get("PSENGINE_LIB_AB") if os.environ.get("PSAMD_AB") == "1" else None
+        L = C.CDLL(ab or _build.LIB)
         for name, res, args in PROTOTYPES:
             f = getattr(L, name)
             f.restype = res
@@ -415,6 +419,17 @@ class Engine:
         uid = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         self._check(self._L.ps_dist_init(self._h, C.byref(dc), uid))
 
+    def dist_init_ipc(self, rank: int, world: int, group_id: bytes, partition: int = PART_PEER,
+                      split_depth: int = 0, copy: bool = False, inplace: bool = False):
+        """Process-shared sharding (ps_dist_init_ipc): one process per rank on
+        one node, device memory mapped across processes (several ranks may
+        share a GPU); group_id from ipc_group_id() on one rank.  copy / inplace
+        as for dist_init_loopback."""
+        flags = (DIST_F_COPY if copy else 0) | (DIST_F_INPLACE if inplace else 0)
+        dc = DistConfig(rank, world, partition, split_depth, flags, 0)
+        gid = (C.c_uint8 * 128).from_buffer_copy(group_id)
+        self._check(self._L.ps_dist_init_ipc(self._h, C.byref(dc), gid))
+
     def dist_init_loopback(self, group: "Loopback", rank: int, partition: int = PART_PEER,
                            split_depth: int = 0, copy: bool = False, inplace: bool = False):
         """copy: the records go through the receive buffer (PS_DIST_F_COPY), the
@@ -431,6 +446,15 @@ def unique_id() -> bytes:
     rc = load().ps_dist_unique_id(buf)
     if rc != PS_OK:
         raise EngineError(rc, "ps_dist_unique_id")
+    return bytes(buf)
+
+
+def ipc_group_id() -> bytes:
+    """A fresh group id for ps_dist_init_ipc (host only; ship it to every rank)."""
+    buf = (C.c_uint8 * 128)()
+    rc = load().ps_dist_ipc_id(buf)
+    if rc != PS_OK:
+        raise EngineError(rc, "ps_dist_ipc_id")
     return bytes(buf)
 
 

@@ -329,15 +329,31 @@ typedef struct ps_dist_config {
  * place (tests run the RCCL-shaped path on one GPU with it; RCCL: ignored) */
 #define PS_DIST_F_COPY 0x1u
 /* ps_dist_config.flags: ghost-fed nodes read their remote parents' rows in
- * the owner's own row set (no packed records, no shipping; the loopback
- * transport's ranks share one process and device -- across GPUs of a node
- * this is what xGMI peer mappings would serve).  Not with PS_DIST_F_COPY;
+ * the owner's own row set (no packed records, no shipping): the loopback's
+ * ranks share one process; ps_dist_init_ipc's map each other's row sets
+ * (across the GPUs of a node, xGMI peer reads).  Not with PS_DIST_F_COPY;
  * RCCL: refused. */
 #define PS_DIST_F_INPLACE 0x2u
 
 /* rank 0 creates the RCCL id; the caller ships it to every rank */
 int ps_dist_unique_id(uint8_t id_out[PS_UNIQUE_ID_BYTES]);
 int ps_dist_init(ps_engine* e, const ps_dist_config* dc, const uint8_t id[PS_UNIQUE_ID_BYTES]);
+/* process-shared transport: one process per rank on one node -- their GPUs
+ * map each other's memory (hipIpcGetMemHandle / hipIpcOpenMemHandle; several
+ * ranks may share one GPU, which RCCL refuses).  Rank 0 calls ps_dist_ipc_id
+ * (host only: a fresh POSIX shared-memory name) and the caller ships the id
+ * to every rank, as with the RCCL id; ps_dist_init_ipc then meets the other
+ * ranks there (host barriers in shared memory, 120 s timeout) and maps their
+ * device flag blocks.  Each round is ordered by monotonic device flags in
+ * IPC-mapped memory (a one-wave set kernel and a one-wave poll kernel with a
+ * 120 s timeout, after which the next call fails with PS_E_DEVICE): no host
+ * synchronisation with the GPU.  flags: PS_DIST_F_COPY copies the records
+ * into the receive buffer (the RCCL data path), PS_DIST_F_INPLACE reads the
+ * ghost parents' rows in their owner's row set, neither reads each sender's
+ * records in place.  Replaces the cross-host child write subtree.go:333 and
+ * the per-hop read client.go:104 for ranks that share a node. */
+int ps_dist_ipc_id(uint8_t id_out[PS_UNIQUE_ID_BYTES]);
+int ps_dist_init_ipc(ps_engine* e, const ps_dist_config* dc, const uint8_t id[PS_UNIQUE_ID_BYTES]);
 /* in-process transport: `world` engines of one process (one thread each)
  * exchange through device copies -- runs the multi-GPU path on one GPU */
 typedef struct ps_loopback ps_loopback;

@@ -21,3 +21,12 @@ def oracle_lib():
     import oracle
     oracle.build()
     return oracle
+
+
+@pytest.fixture(scope="session")
+def cfg4_full():
+    """cfg4's full-size tree, dead mask and oracle reach (fullsize_common.Cfg4Tree),
+    built once per session for the full-size and process-per-rank tests."""
+    from fullsize_common import Cfg4Tree
+
+    return Cfg4Tree()

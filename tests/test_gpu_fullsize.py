@@ -20,57 +20,16 @@ import threading
 import numpy as np
 import pytest
 
-import oracle as O
 import psengine as PE
+from fullsize_common import check_run, dead_mask, oracle_reach, sampled
 from psengine import workloads as WL
 
 pytestmark = pytest.mark.gpu
 
 
-def dead_mask(parent, root, n, frac=0.02, seed=17):
-    rng = np.random.default_rng(seed)
-    live = (rng.random(n) > frac).astype(np.uint8)
-    kids = np.nonzero(parent == root)[0]
-    live[kids[0]] = 0  # a child of the root: a whole top subtree is cut
-    grand = np.nonzero(parent == kids[-1])[0]
-    live[grand[0]] = 0
-    live[kids[-1]] = 1
-    live[root] = 1
-    return live
-
-
-def oracle_reach(parent, root, live):
-    rp, cl = O.parents_to_csr(parent)
-    tot, oh, hist = O.disseminate(rp, cl, root, live, 1, hist_len=64)
-    return tot, oh[0] != 0xFF, hist.astype(np.int64)
-
-
-def check_run(stats, n_msgs, tot, hist):
-    assert sum(s.deliveries for s in stats) == tot * n_msgs
-    assert sum(s.duplicates for s in stats) == 0
-    per = np.zeros(PE.MAX_ROUNDS, dtype=np.int64)
-    for s in stats:
-        per += np.array(list(s.deliveries_per_round), dtype=np.int64)
-    assert per[1:64].tolist() == (hist[1:64] * n_msgs).tolist()
-    assert int(per[64:].sum()) == 0
-
-
-def sampled(n_msgs, k=16, seed=5):
-    return np.random.default_rng(seed).choice(n_msgs, size=min(k, n_msgs), replace=False)
-
-
 @pytest.fixture(scope="module")
-def cfg4_tree():
-    """cfg4's tree (TreeOpts{8,20}, the restated joins of 16M - 1 peers in
-    order) and its dead mask, built once for the module."""
-    wl = WL.cfg4()
-    with PE.Engine(wl.n_peers, 1, seed=wl.seed) as eng:
-        WL.build_engine_topics(eng, wl)
-        parent = eng.parents(0)
-    live = dead_mask(parent, 0, wl.n_peers)
-    tot, reach, hist = oracle_reach(parent, 0, live)
-    assert reach.sum() < wl.n_peers - 1 - 0.02 * wl.n_peers  # subtrees were cut
-    return wl, parent, live, tot, reach, hist
+def cfg4_tree(cfg4_full):
+    return cfg4_full.astuple()
 
 
 def test_cfg2_full_size_dead_mask_against_oracle():
@@ -92,7 +51,7 @@ def test_cfg2_full_size_dead_mask_against_oracle():
             assert np.array_equal(eng.delivered(first + int(m)).astype(bool), reach), int(m)
 
 
-def test_cfg4_full_size_dead_mask_single_rank(cfg4_tree):
+def test_cfg4_full_size_dead_mask_single_rank(cfg4_tree, cfg4_full):
     """cfg4 at full size on one rank, production instance, dead mask."""
     wl, parent, live, tot, reach, hist = cfg4_tree
     with PE.Engine(wl.n_peers, 1, seed=wl.seed) as eng:
@@ -105,15 +64,12 @@ def test_cfg4_full_size_dead_mask_single_rank(cfg4_tree):
         check_run([st], wl.n_msgs, tot, hist)
         for m in sampled(wl.n_msgs):
             assert np.array_equal(eng.delivered(first + int(m)).astype(bool), reach), int(m)
-        cfg4_tree_digest[0] = eng.seen_digest()
-
-
-cfg4_tree_digest = [None]
+        assert eng.seen_digest() == cfg4_full.digest()
 
 
 @pytest.mark.parametrize("world,copy", [(2, False), (2, True), (2, "inplace"), (4, False), (4, True), (4, "inplace"),
                                         (8, False), (8, True), (8, "inplace")])
-def test_cfg4_full_size_ranks_peer_hash(cfg4_tree, world, copy):
+def test_cfg4_full_size_ranks_peer_hash(cfg4_tree, cfg4_full, world, copy):
     """cfg4 at full size hash-sharded over `world` loopback ranks (owner(p) =
     splitmix64(p) mod world; 8 = the north star's split):
     every round ships ghost parent rows -- read in place, or (copy) through
@@ -161,14 +117,7 @@ def test_cfg4_full_size_ranks_peer_hash(cfg4_tree, world, copy):
                 got |= d
             assert np.array_equal(got, reach), int(m)
         digest = sum(e.seen_digest() for e in engines) % (1 << 64)
-        if cfg4_tree_digest[0] is None:
-            with PE.Engine(wl.n_peers, 1, seed=wl.seed) as one:
-                one.set_tree(0, 0, parent)
-                one.set_live(live)
-                one.publish(wl.msg_topics)
-                one.run()
-                cfg4_tree_digest[0] = one.seen_digest()
-        assert digest == cfg4_tree_digest[0]
+        assert digest == cfg4_full.digest()
     finally:
         for e in engines:
             e.close()
