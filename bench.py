@@ -530,6 +530,13 @@ def main():
                          "sharding: replicated topology, no exchange)")
     ap.add_argument("--message-only", action="store_true",
                     help="N>1: only the message-sharded leg (gloo bootstrap, no RCCL; testing)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "rccl", "ipc"],
+                    help="N>1: the frontier exchange -- rccl (value's transport, a GPU per rank), ipc (one "
+                         "process per rank, buffers mapped across processes; ranks may share a GPU); auto = "
+                         "rccl when every rank has its own GPU, else ipc")
+    ap.add_argument("--ipc-mode", default="inplace", choices=["inplace", "zc", "copy"],
+                    help="--transport ipc: owners' rows read in place (no records), senders' records read in "
+                         "place, or records copied into the receive buffer")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="N>1: weak = N x the messages on the same topology (per-GPU work of "
                          "N=1), strong = the N=1 workload unchanged")

@@ -8,12 +8,14 @@
 
 #include <rccl/rccl.h>
 
+#include <dirent.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <unistd.h>
 
 #include <atomic>
 #include <cerrno>
+#include <cstdarg>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -321,7 +323,7 @@ namespace {
 constexpr uint64_t kIpcMagic = 0x70736970632d3036ull;
 // device flag words (u64 index into a rank's flag block, one 128-B line each)
 constexpr uint32_t kFlagSent = 0, kFlagRead = 16, kFlagUsed = 32, kFlagWords = 48;
-constexpr uint64_t kFlagTimeoutTicks = 120ull * 100000000ull;  // 120 s of the 100 MHz clock
+constexpr uint64_t kFlagTimeoutTicks = 30ull * 100000000ull;  // 30 s of the 100 MHz clock
 constexpr int kBarrierSeconds = 120;
 enum IpcKind { kSend = 0, kSeen = 1, kGen = 2, kKinds = 3 };
 
@@ -361,7 +363,12 @@ struct IpcShm {
 class IpcTransport final : public Transport {
  public:
   IpcTransport(int rank, int world, int device, bool copy, bool in_place)
-      : rank_(rank), world_(world), device_(device), copy_(copy), in_place_(in_place) {}
+      : rank_(rank), world_(world), device_(device), copy_(copy), in_place_(in_place) {
+    const char* t = std::getenv("PSAMD_IPC_TRACE");  // (debug: every call and barrier on stderr)
+    trace_ = t && std::atoi(t) != 0;
+    const char* b = std::getenv("PSAMD_IPC_BARRIER_S");
+    barrier_s_ = b && std::atoi(b) > 0 ? std::atoi(b) : kBarrierSeconds;
+  }
 
   ~IpcTransport() override {
     (void)hipSetDevice(device_);
@@ -408,7 +415,7 @@ class IpcTransport final : public Transport {
     me.world = world_;
     me.topic_words = topic_words_;
     if ((e = hipIpcGetMemHandle(&me.flags, flags_)) != hipSuccess) return fail(e, err);
-    if (!barrier()) return timeout(err);
+    if (!barrier("open")) return timeout(err);
     for (int q = 0; q < world_; ++q) {
       const IpcSlot& o = shm_->slot[q];
       if (o.world != world_ || o.topic_words != topic_words_)
@@ -426,7 +433,7 @@ class IpcTransport final : public Transport {
       opened_.push_back(p);
       peer_flags_[q] = static_cast<uint64_t*>(p);
     }
-    if (!barrier()) return timeout(err);  // every rank mapped every flag block
+    if (!barrier("mapped")) return timeout(err);  // every rank mapped every flag block
     if (rank_ == 0) shm_unlink(name);
     return true;
   }
@@ -488,11 +495,13 @@ class IpcTransport final : public Transport {
   hipError_t consumed(hipStream_t s, uint32_t round, std::string* err) override {
     const uint64_t n = ++used_;
     used_at_[round % kSendBufs] = n;
+    if (trace_) log("consumed round %u -> used %llu", round, static_cast<unsigned long long>(n));
     const hipError_t e = launch_flag_set(flags_ + kFlagUsed, n, s);
     return e == hipSuccess ? hipSuccess : fail(e, err);
   }
   hipError_t reuse(hipStream_t s, uint32_t round, std::string* err) override {
     if (const hipError_t e = check(err)) return e;
+    if (trace_) log("reuse round %u waits used %llu", round, static_cast<unsigned long long>(used_at_[round % kSendBufs]));
     return wait_all(kFlagUsed, used_at_[round % kSendBufs], s, err);
   }
 
@@ -508,8 +517,14 @@ class IpcTransport final : public Transport {
     me.gen_cur = mine.gen_cur;
     me.n_words = static_cast<uint32_t>(mine.topics.size());
     std::memcpy(topic_block(rank_), mine.topics.data(), mine.topics.size() * 8);
-    if (!barrier()) return timeout(err);  // every rank published
+    if (!barrier("share")) return timeout(err);  // every rank published
     all.assign(world_, Share{});
+    static const bool serial = [] {
+      const char* v = std::getenv("PSAMD_IPC_SERIAL_OPEN");
+      return v && std::atoi(v) != 0;
+    }();
+    for (int turn = 0; serial && turn < rank_; ++turn)
+      if (!barrier("turn", turn)) return timeout(err);
     for (int q = 0; q < world_; ++q) {
       const IpcSlot& o = shm_->slot[q];
       Share& a = all[q];
@@ -526,7 +541,9 @@ class IpcTransport final : public Transport {
       if ((e = import(q, kGen, o.gen, &b, err)) != hipSuccess) return e;
       a.gen = b;
     }
-    if (!barrier()) return timeout(err);  // every rank copied the slots (they may change)
+    for (int turn = rank_; serial && turn < world_; ++turn)
+      if (!barrier("turn", turn)) return timeout(err);
+    if (!barrier("shared")) return timeout(err);  // every rank copied the slots (they may change)
     return hipSuccess;
   }
 
@@ -563,6 +580,7 @@ class IpcTransport final : public Transport {
       c.epoch = device_free_epoch();
       c.ex.h = h;
       c.ex.ver = ++exports_;
+      if (trace_) log("export kind %d base %p size %zu ver %llu", kind, base, size, static_cast<unsigned long long>(c.ex.ver));
     }
     *out = c.ex;
     out->off = static_cast<uint64_t>(u - c.base);
@@ -573,7 +591,40 @@ class IpcTransport final : public Transport {
     Import& im = imports_[q][kind];
     if (im.ver != ex.ver) {
       void* p = nullptr;
+      if (trace_) log("open rank %d kind %d ver %llu", q, kind, static_cast<unsigned long long>(ex.ver));
+      std::atomic<bool> done{false};
+      std::thread dog;
+      if (trace_)  // (debug: where every thread of this process waits, if the open stalls)
+        dog = std::thread([&] {
+          for (int i = 0; i < 800 && !done.load(); ++i) std::this_thread::sleep_for(std::chrono::milliseconds(10));
+          if (done.load()) return;
+          for (int round = 0; round < 3 && !done.load(); ++round) {
+            DIR* d = opendir("/proc/self/task");
+            for (dirent* de = d ? readdir(d) : nullptr; de; de = readdir(d)) {
+              if (de->d_name[0] == '.') continue;
+              auto slurp = [&](const char* f) {
+                std::string path = std::string("/proc/self/task/") + de->d_name + "/" + f, out;
+                if (FILE* fp = std::fopen(path.c_str(), "r")) {
+                  char b[256];
+                  const size_t k = std::fread(b, 1, sizeof b - 1, fp);
+                  b[k] = 0;
+                  std::fclose(fp);
+                  out = b;
+                  while (!out.empty() && (out.back() == '\n' || out.back() == ' ')) out.pop_back();
+                }
+                return out;
+              };
+              log("stall: task %s %s wchan=%s syscall=%s", de->d_name, slurp("comm").c_str(), slurp("wchan").c_str(),
+                  slurp("syscall").substr(0, 24).c_str());
+            }
+            if (d) closedir(d);
+            std::this_thread::sleep_for(std::chrono::seconds(4));
+          }
+        });
       const hipError_t e = hipIpcOpenMemHandle(&p, ex.h, hipIpcMemLazyEnablePeerAccess);
+      done.store(true);
+      if (dog.joinable()) dog.join();
+      if (trace_) log("opened rank %d kind %d -> %p (%s)", q, kind, p, hipGetErrorString(e));
       if (e != hipSuccess) {
         if (err) *err = std::string("ipc transport: hipIpcOpenMemHandle of rank ") + std::to_string(q) + ": " +
                         hipGetErrorString(e);
@@ -598,7 +649,7 @@ class IpcTransport final : public Transport {
     for (int q = 0; q < kMaxRanks; ++q) pub.off[q] = q < static_cast<int>(send_off.size()) ? send_off[q] : 0;
     pub.seq = seq;
     if ((e = launch_flag_set(flags_ + kFlagSent, seq, s)) != hipSuccess) return fail(e, err);
-    if (!barrier()) return timeout(err);
+    if (!barrier("exchange", seq)) return timeout(err);
     return hipSuccess;
   }
 
@@ -633,11 +684,22 @@ class IpcTransport final : public Transport {
   // next call: the windows enqueued since may have read stale rows
   hipError_t check(std::string* err) {
     if (__atomic_load_n(err_, __ATOMIC_ACQUIRE) == 0) return hipSuccess;
-    if (err) *err = "ipc transport: a peer's device flag did not arrive within 120 s (rank died or plans diverged)";
+    if (err) *err = "ipc transport: a peer's device flag did not arrive within 30 s (rank died or plans diverged)";
     return hipErrorLaunchTimeOut;
   }
 
-  bool barrier() {
+  void log(const char* fmt, ...) __attribute__((format(printf, 2, 3))) {
+    char buf[256];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    const double t = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    std::fprintf(stderr, "[ipc %d/%d %.6f] %s\n", rank_, world_, t, buf);
+  }
+
+  bool barrier(const char* what, uint64_t seq = 0) {
+    if (trace_) log("barrier %s %llu", what, static_cast<unsigned long long>(seq));
     const uint32_t gen = shm_->generation.load(std::memory_order_acquire);
     if (shm_->broken.load(std::memory_order_acquire)) return false;
     if (shm_->arrived.fetch_add(1, std::memory_order_acq_rel) + 1 == static_cast<uint32_t>(world_)) {
@@ -654,7 +716,8 @@ class IpcTransport final : public Transport {
         continue;
       }
       std::this_thread::sleep_for(std::chrono::microseconds(20));
-      if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(kBarrierSeconds)) {
+      if ((spin & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(barrier_s_)) {
+        log("barrier %s %llu: timed out after %d s", what, static_cast<unsigned long long>(seq), barrier_s_);
         shm_->broken.store(1, std::memory_order_release);
         return false;
       }
@@ -662,7 +725,7 @@ class IpcTransport final : public Transport {
   }
 
   static hipError_t timeout(std::string* err) {
-    if (err) *err = "ipc transport: a rank did not arrive within 120 s (group broken)";
+    if (err) *err = "ipc transport: a rank did not arrive in time (group broken)";
     return hipErrorUnknown;
   }
   static hipError_t fail(hipError_t e, std::string* err) {
@@ -694,6 +757,8 @@ class IpcTransport final : public Transport {
   Import imports_[kMaxRanks][kKinds];
   std::vector<void*> opened_;
   std::vector<Pending> pending_;
+  bool trace_ = false;
+  int barrier_s_ = kBarrierSeconds;
 };
 
 }  // namespace

@@ -1240,7 +1240,11 @@ __global__ void k_flag_wait(FlagWait w, uint32_t* err, uint64_t timeout_ticks) {
   for (;;) {
     if (!done) done = __hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= want;
     if (__all(done)) break;
-    if (wall_clock64() - t0 > timeout_ticks) {
+    const uint64_t waited = wall_clock64() - t0;
+    // past 1 ms, an earlier wait that timed out ends this one too (the
+    // window fails once, instead of one timeout per round)
+    if (waited > timeout_ticks ||
+        (waited > 100000u && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0)) {
       if (!done) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       break;
     }

@@ -28,7 +28,7 @@ import os
 import sys
 import time
 
-from . import MODE_KERNEL, PART_PEER, PART_SUBTREE, Engine, unique_id
+from . import MODE_KERNEL, PART_PEER, PART_SUBTREE, Engine, ipc_group_id, load, unique_id
 from . import workloads as WL
 
 
@@ -86,6 +86,12 @@ def bench_main(args, descr: dict, metric: str):
     if world != gpus:
         raise SystemExit(f"[bench] rank {rank}: WORLD_SIZE={world} but --gpus {gpus}; "
                          "the line would report the wrong n_gpus")
+    # The engine's HIP/HSA/RCCL runtime (/opt/rocm, which libpsengine.so is
+    # built against) is bound before torch loads its bundled copies of the
+    # same sonames, so both run on it.  With torch first, the engine ran on
+    # torch's ROCm 7.0 runtime, whose hipIpcOpenMemHandle of a >= 2 GiB
+    # allocation spins forever (profiles/r06/ipc/NOTES.md).
+    load()
     import torch
 
     # RCCL prints its version banner on stdout when a communicator comes up:
@@ -106,11 +112,44 @@ def bench_main(args, descr: dict, metric: str):
         dist.barrier()
         dist.destroy_process_group()
         return
-    dist = init("nccl")  # RCCL on ROCm
+    # the exchange transport: RCCL (value's transport) when every
+    # rank has a GPU of its own; ranks that share GPUs (this pool's one-GPU
+    # boxes) take the IPC transport -- RCCL refuses two ranks on one device
+    shared = world > max(1, torch.cuda.device_count())
+    transport = getattr(args, "transport", "auto")
+    if transport == "auto":
+        transport = "ipc" if shared else "rccl"
+    if transport == "rccl" and shared:
+        raise SystemExit(f"[bench] {world} ranks on {torch.cuda.device_count()} GPU(s): RCCL refuses two ranks "
+                         "on one device; use --transport ipc")
+    dist = init("gloo" if transport == "ipc" else "nccl")  # (nccl = RCCL on ROCm)
     dev = torch.device("cuda", local)
+    tdev = None if transport == "ipc" else dev  # (gloo reduces host tensors)
     part = PART_SUBTREE if getattr(args, "partition", "peer") == "subtree" else PART_PEER
-    out = partitioned(args, dist, dev, rank, world, descr, metric, part)
-    if world > 1 and not getattr(args, "no_message_leg", False):
+    ipc_mode = getattr(args, "ipc_mode", "inplace")
+    out = partitioned(args, dist, dev, rank, world, descr, metric, part, transport, ipc_mode, tdev)
+    if shared and world > 1:
+        # N ranks sharing one GPU against one rank doing the same N x messages
+        # alone: the cost of the partition and its exchange on one device
+        one = one_rank_reference(args, dev, world) if rank == 0 else None
+        if rank == 0:
+            out["shared_gpu"] = {"ranks_per_gpu": world, "one_rank_ms_per_step": one,
+                                 "ratio_vs_one_rank": out["ms_per_step"] / one,
+                                 "note": f"{world} processes on one GPU, each owning 1/{world} of every tree, "
+                                         f"against one engine disseminating the same {world} x messages alone"}
+        dist.barrier()
+    if world > 1 and not shared and transport == "rccl" and not getattr(args, "no_message_leg", False):
+        # the same partition with the owners' rows read in place over xGMI peer
+        # mappings (IPC transport, PS_DIST_F_INPLACE): no records shipped
+        try:
+            leg = partitioned(args, dist, dev, rank, world, descr, metric, part, "ipc", "inplace", dev)
+            if rank == 0:
+                out["ipc_in_place"] = {k: leg[k] for k in ("value", "unit", "ms_per_step", "roofline", "config")}
+        except Exception as exc:  # noqa: BLE001
+            print(f"[bench] rank {rank}: ipc_in_place leg failed: {exc!r}", file=sys.stderr, flush=True)
+            if rank == 0:
+                out["ipc_in_place"] = {"error": repr(exc)}
+    if world > 1 and not shared and not getattr(args, "no_message_leg", False):
         # the decompositions SURVEY.md §8e allows beside the mandated peer hash,
         # on the same ranks: level-L subtrees (cross edges only above level L)
         # and message sharding (replicated topology, no exchange)
@@ -119,7 +158,7 @@ def bench_main(args, descr: dict, metric: str):
         other = PART_PEER if part == PART_SUBTREE else PART_SUBTREE
         key = "peer_partition" if other == PART_PEER else "subtree_partition"
         try:
-            leg = partitioned(args, dist, dev, rank, world, descr, metric, other)
+            leg = partitioned(args, dist, dev, rank, world, descr, metric, other, transport, ipc_mode, tdev)
             if rank == 0:
                 keep = ("value", "unit", "ms_per_step", "roofline", "config")
                 out[key] = {k: leg[k] for k in keep}
@@ -128,7 +167,7 @@ def bench_main(args, descr: dict, metric: str):
             if rank == 0:
                 out[key] = {"error": repr(exc)}
         try:
-            ms = message_sharded(args, dist, dev, rank, world, descr)
+            ms = message_sharded(args, dist, dev, rank, world, descr, totals_dev=tdev)
             if rank == 0:
                 out["message_sharded"] = ms
         except Exception as exc:  # noqa: BLE001
@@ -142,21 +181,29 @@ def bench_main(args, descr: dict, metric: str):
     dist.destroy_process_group()
 
 
-def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str, part: int):
+def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str, part: int,
+                transport: str = "rccl", ipc_mode: str = "inplace", tdev="same"):
     """The node-partitioned run: every rank owns a hash (PART_PEER) or
     subtree (PART_SUBTREE) share of every tree; the frontier rows that cross
-    ranks are exchanged each round over the engine's RCCL communicator.
-    Returns the bench JSON object on rank 0 (None elsewhere)."""
+    ranks are exchanged each round over the engine's RCCL communicator, or
+    (transport "ipc", one process per rank on one node) read through IPC
+    mappings of the other ranks' buffers: the owners' rows in place
+    (ipc_mode "inplace"), the senders' records in place ("zc") or copied
+    ("copy").  Returns the bench JSON object on rank 0 (None elsewhere)."""
     import torch
 
+    tdev = dev if tdev == "same" else tdev
     local = dev.index if dev.index is not None else 0
     wl = workload(args, world)
     scaling = getattr(args, "scaling", "weak") if world > 1 else "weak"
-    uid = share_bytes(dist, unique_id, rank)
+    uid = share_bytes(dist, ipc_group_id if transport == "ipc" else unique_id, rank)
     t0 = time.perf_counter()
     # one window per topic (pull kernels take rows of any width)
     eng = Engine(wl.n_peers, len(wl.topics), device=local, seed=wl.seed, msg_window=1 << 20)
-    eng.dist_init(rank, world, uid, part)
+    if transport == "ipc":
+        eng.dist_init_ipc(rank, world, uid, part, copy=ipc_mode == "copy", inplace=ipc_mode == "inplace")
+    else:
+        eng.dist_init(rank, world, uid, part)
     sizes = WL.build_engine_topics(eng, wl)
     expected = wl.expected_deliveries(sizes)
     pname = "peer" if part == PART_PEER else "subtree"
@@ -170,7 +217,7 @@ def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str
 
     for _ in range(args.warmup):
         st = step()
-    _, warm = job_totals(dist, 0.0, st.deliveries if args.warmup else 0, dev)
+    _, warm = job_totals(dist, 0.0, st.deliveries if args.warmup else 0, tdev)
     if args.warmup and not args.no_check:
         assert warm == expected, (warm, expected)
     dist.barrier()
@@ -194,7 +241,7 @@ def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str
     torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
-    wall, total = job_totals(dist, elapsed, local_deliv, dev)
+    wall, total = job_totals(dist, elapsed, local_deliv, tdev)
     # roofline pass: HIP events around every hot-kernel launch (untimed above)
     eng.set_time_kernels(True)
     bytes_, exp_ms, launches = 0, 0.0, 0
@@ -204,8 +251,8 @@ def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str
         exp_ms += st.expand_ms
         launches += st.expand_launches
     eng.set_time_kernels(False)
-    _, tot_bytes = job_totals(dist, 0.0, bytes_, dev)
-    slow_exp_ms, _ = job_totals(dist, exp_ms, 0, dev)
+    _, tot_bytes = job_totals(dist, 0.0, bytes_, tdev)
+    slow_exp_ms, _ = job_totals(dist, exp_ms, 0, tdev)
     if not args.no_check:
         assert total == expected * args.steps, (total, expected * args.steps)
     out = None
@@ -229,8 +276,11 @@ def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str
             "config": {"workload": f"{wl.name}: {descr[wl.name]}", "peers": wl.n_peers,
                        "topics": len(wl.topics), "subscriptions": int(sum(sizes)),
                        "messages": wl.n_msgs, "deliveries_per_step": expected,
-                       "parallelism": f"{world} GPUs, nodes hash-partitioned "
-                                      f"({pname}), RCCL all-to-allv frontier exchange per round"},
+                       "parallelism": f"{world} ranks, nodes partitioned ({pname}), " + (
+                           "RCCL all-to-allv frontier exchange per round" if transport == "rccl" else
+                           f"IPC transport ({ipc_mode}: "
+                           + {"inplace": "owners' rows read in place", "zc": "senders' records read in place",
+                              "copy": "records copied"}[ipc_mode] + "), device-flag ordered rounds")},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": 8000.0, "unit": "GB/s",
                          "frac": achieved / 8000.0, "traffic": None,
                          "kernel": MODE_KERNEL.get(st.expand_mode, "k_expand"),
@@ -244,6 +294,35 @@ def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str
         }
     eng.close()
     return out
+
+
+def one_rank_reference(args, dev, world: int) -> float:
+    """ms per step of one engine (no partition) disseminating the weak-scaled
+    workload's world x messages alone, pipelined like the partitioned run."""
+    import torch
+
+    wl = workload(args, world)
+    local = dev.index if dev.index is not None else 0
+    eng = Engine(wl.n_peers, len(wl.topics), device=local, seed=wl.seed, msg_window=1 << 20)
+    try:
+        sizes = WL.build_engine_topics(eng, wl)
+        expected = wl.expected_deliveries(sizes)
+        for _ in range(max(1, args.warmup)):
+            eng.publish(wl.msg_topics)
+            assert args.no_check or eng.run().deliveries == expected
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            eng.publish(wl.msg_topics)
+            eng.run_async()
+            if i:
+                eng.wait()
+        if args.steps:
+            eng.wait()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) * 1e3 / max(1, args.steps)
+    finally:
+        eng.close()
 
 
 def message_sharded(args, dist, dev, rank: int, world: int, descr: dict, totals_dev="same") -> dict:

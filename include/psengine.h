@@ -346,7 +346,7 @@ int ps_dist_init(ps_engine* e, const ps_dist_config* dc, const uint8_t id[PS_UNI
  * ranks there (host barriers in shared memory, 120 s timeout) and maps their
  * device flag blocks.  Each round is ordered by monotonic device flags in
  * IPC-mapped memory (a one-wave set kernel and a one-wave poll kernel with a
- * 120 s timeout, after which the next call fails with PS_E_DEVICE): no host
+ * 30 s timeout, after which the next call fails with PS_E_DEVICE): no host
  * synchronisation with the GPU.  flags: PS_DIST_F_COPY copies the records
  * into the receive buffer (the RCCL data path), PS_DIST_F_INPLACE reads the
  * ghost parents' rows in their owner's row set, neither reads each sender's

@@ -42,6 +42,24 @@ def sampled(n_msgs, k=16, seed=5):
     return np.random.default_rng(seed).choice(n_msgs, size=min(k, n_msgs), replace=False)
 
 
+def cfg3_dead_mask(wl, parents, frac=0.02, seed=17):
+    """~2 % dead peers, plus two dead peers in the top levels of every topic
+    (a child of the root and a grandchild), roots live."""
+    rng = np.random.default_rng(seed)
+    live = (rng.random(wl.n_peers) > frac).astype(np.uint8)
+    for t, ts in enumerate(wl.topics):
+        par = parents[t]
+        kids = np.nonzero(par == ts.root)[0]
+        if len(kids):
+            live[kids[0]] = 0
+            grand = np.nonzero(par == kids[-1])[0]
+            if len(grand):
+                live[grand[0]] = 0
+    for ts in wl.topics:
+        live[ts.root] = 1
+    return live
+
+
 class Cfg4Tree:
     """cfg4's tree (the restated joins of 16M - 1 peers in order), its dead
     mask and the oracle's reach; the single engine's seen digest on demand."""

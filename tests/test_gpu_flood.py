@@ -15,6 +15,7 @@ import pytest
 
 import oracle as O
 import psengine as PE
+from fullsize_common import cfg3_dead_mask as _cfg3_dead_mask
 from psengine import workloads as WL
 
 pytestmark = pytest.mark.gpu
@@ -227,24 +228,6 @@ def test_flood_follows_live_changes(monkeypatch):
             assert st.deliveries == total * 70, step
             for m in (0, 69):
                 assert np.array_equal(eng.hops(first + m), oh[0]), (step, m)
-
-
-def _cfg3_dead_mask(wl, parents, frac=0.02, seed=17):
-    """~2 % dead peers, plus two dead peers in the top levels of every topic
-    (a child of the root and a grandchild), roots live."""
-    rng = np.random.default_rng(seed)
-    live = (rng.random(wl.n_peers) > frac).astype(np.uint8)
-    for t, ts in enumerate(wl.topics):
-        par = parents[t]
-        kids = np.nonzero(par == ts.root)[0]
-        if len(kids):
-            live[kids[0]] = 0
-            grand = np.nonzero(par == kids[-1])[0]
-            if len(grand):
-                live[grand[0]] = 0
-    for ts in wl.topics:
-        live[ts.root] = 1
-    return live
 
 
 def test_cfg3_full_size_dead_mask_against_oracle():

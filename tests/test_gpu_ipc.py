@@ -153,3 +153,25 @@ def test_cfg4_full_size_processes_peer_hash(tmp_path, cfg4_full, world, mode):
             u |= d
         assert np.array_equal(u, reach), int(samples[k])
     assert sum(int(g["digest"]) for g in got) % (1 << 64) == cfg4_full.digest()
+
+
+def test_bench_two_processes_on_one_gpu():
+    """`bench.py --gpus 2` on this pool's one-GPU boxes: two ranks (one process
+    each, torch.distributed.run) share the GPU over the IPC transport; the
+    line reports the job's deliveries (asserted inside against the expected
+    total) and the ratio to one rank doing the same messages alone."""
+    import json
+
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("every rank has a GPU of its own: bench.py takes RCCL")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--workload", "cfg4", "--scale", "0.05",
+           "--steps", "3", "--warmup", "1", "--no-cpu"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=150, cwd=repo)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["value"] > 0
+    assert "IPC transport" in line["config"]["parallelism"]
+    assert line["shared_gpu"]["ranks_per_gpu"] == 2 and line["shared_gpu"]["ratio_vs_one_rank"] > 0
