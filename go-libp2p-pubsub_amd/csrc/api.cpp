@@ -733,6 +733,14 @@ int ps_dist_init(ps_engine* e, const ps_dist_config* dc, const uint8_t id[PS_UNI
   return PS_OK;
 }
 
+int ps_device_count(int32_t* out) {
+  if (!out) return PS_E_INVAL;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *out = n;
+  return PS_OK;
+}
+
 int ps_dist_ipc_id(uint8_t id_out[PS_UNIQUE_ID_BYTES]) {
   if (!id_out) return PS_E_INVAL;
   return ipc_group_id(id_out) == 0 ? PS_OK : PS_E_DEVICE;

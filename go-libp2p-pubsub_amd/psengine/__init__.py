@@ -158,6 +158,7 @@ PROTOTYPES = [
     ("ps_msg_decode", C.c_int, [C.c_char_p, C.c_size_t, C.POINTER(MessageBuf), C.POINTER(C.c_size_t)]),
     ("ps_dist_unique_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("ps_dist_init", C.c_int, [_P, C.POINTER(DistConfig), C.POINTER(C.c_uint8)]),
+    ("ps_device_count", C.c_int, [_i32p]),
     ("ps_dist_ipc_id", C.c_int, [C.POINTER(C.c_uint8)]),
     ("ps_dist_init_ipc", C.c_int, [_P, C.POINTER(DistConfig), C.POINTER(C.c_uint8)]),
     ("ps_loopback_create", C.c_int, [C.c_int32, C.POINTER(_P)]),
@@ -447,6 +448,13 @@ def unique_id() -> bytes:
     if rc != PS_OK:
         raise EngineError(rc, "ps_dist_unique_id")
     return bytes(buf)
+
+
+def device_count() -> int:
+    """GPUs visible to this process, through the engine's own HIP runtime."""
+    n = C.c_int32()
+    load().ps_device_count(C.byref(n))
+    return int(n.value)
 
 
 def ipc_group_id() -> bytes:

@@ -1,6 +1,10 @@
-"""Multi-GPU driver for bench.py: one process per GPU, torch.distributed for
-bootstrap, barriers and the max-over-ranks clock; the frontier exchange itself
-runs inside the engine over its own RCCL communicator (ps_dist_init).
+"""Multi-GPU driver for bench.py: one process per GPU, torch.distributed (gloo,
+host tensors) for bootstrap, barriers and the max-over-ranks clock; the
+frontier exchange itself runs inside the engine -- over its own RCCL
+communicator (ps_dist_init) when every rank has a GPU, or over the IPC
+transport (ps_dist_init_ipc) when ranks share GPUs.  torch.cuda is never used:
+the engine's calls block until their windows are done, and only the engine's
+HIP runtime (/opt/rocm) initialises the GPU.
 
 Every rank builds the same topics (the restated joins are deterministic) and
 publishes the same messages; each owns a hash partition of every topic's tree
@@ -28,7 +32,7 @@ import os
 import sys
 import time
 
-from . import MODE_KERNEL, PART_PEER, PART_SUBTREE, Engine, ipc_group_id, load, unique_id
+from . import MODE_KERNEL, PART_PEER, PART_SUBTREE, Engine, device_count, ipc_group_id, load, unique_id
 from . import workloads as WL
 
 
@@ -60,11 +64,12 @@ def share_bytes(dist, make, rank: int) -> bytes:
 
 
 def job_totals(dist, elapsed_s: float, local_count: int, device=None):
-    """(max elapsed over ranks, sum of counts over ranks)."""
+    """(max elapsed over ranks, sum of counts over ranks), over gloo."""
     import torch
 
-    t = torch.tensor([elapsed_s], dtype=torch.float64, device=device)
-    c = torch.tensor([float(local_count)], dtype=torch.float64, device=device)
+    del device  # (host tensors)
+    t = torch.tensor([elapsed_s], dtype=torch.float64)
+    c = torch.tensor([float(local_count)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dist.all_reduce(c, op=dist.ReduceOp.SUM)
     return float(t.item()), int(round(c.item()))
@@ -87,24 +92,22 @@ def bench_main(args, descr: dict, metric: str):
         raise SystemExit(f"[bench] rank {rank}: WORLD_SIZE={world} but --gpus {gpus}; "
                          "the line would report the wrong n_gpus")
     # The engine's HIP/HSA/RCCL runtime (/opt/rocm, which libpsengine.so is
-    # built against) is bound before torch loads its bundled copies of the
-    # same sonames, so both run on it.  With torch first, the engine ran on
-    # torch's ROCm 7.0 runtime, whose hipIpcOpenMemHandle of a >= 2 GiB
-    # allocation spins forever (profiles/r06/ipc/NOTES.md).
+    # built against) is bound before torch loads its bundled ROCm 7.0 copies,
+    # and torch.cuda is never touched, so only the engine's runtime initialises
+    # the GPU.  (With torch imported first the engine bound torch's copies,
+    # whose hipIpcOpenMemHandle of a >= 2 GiB allocation spins forever;
+    # initialising both copies fails ps_create: profiles/r06/ipc/NOTES.md.)
     load()
-    import torch
-
+    ndev = max(1, device_count())
     # RCCL prints its version banner on stdout when a communicator comes up:
     # keep stdout for the one JSON line (rank 0), everything else to stderr
     json_fd = os.dup(1)
     os.dup2(2, 1)
-    local = local % max(1, torch.cuda.device_count())  # (counting does not initialise the GPU)
-    torch.cuda.set_device(local)
+    local = local % ndev
+    dist = init("gloo")
     if getattr(args, "message_only", False):
-        # the message-sharded leg alone (no RCCL communicator: also runs with
-        # several ranks on one GPU, e.g. to test it on a one-GPU box)
-        dist = init("gloo")
-        ms = message_sharded(args, dist, torch.device("cuda", local), rank, world, descr, totals_dev=None)
+        # the message-sharded leg alone (no exchange)
+        ms = message_sharded(args, dist, local, rank, world, descr)
         if rank == 0:
             sys.stdout.flush()
             os.write(json_fd, (json.dumps({"metric": metric + " [message-sharded leg only]", "n_gpus": world,
@@ -115,16 +118,15 @@ def bench_main(args, descr: dict, metric: str):
     # the exchange transport: RCCL (value's transport) when every
     # rank has a GPU of its own; ranks that share GPUs (this pool's one-GPU
     # boxes) take the IPC transport -- RCCL refuses two ranks on one device
-    shared = world > max(1, torch.cuda.device_count())
+    shared = world > ndev
     transport = getattr(args, "transport", "auto")
     if transport == "auto":
         transport = "ipc" if shared else "rccl"
     if transport == "rccl" and shared:
-        raise SystemExit(f"[bench] {world} ranks on {torch.cuda.device_count()} GPU(s): RCCL refuses two ranks "
+        raise SystemExit(f"[bench] {world} ranks on {ndev} GPU(s): RCCL refuses two ranks "
                          "on one device; use --transport ipc")
-    dist = init("gloo" if transport == "ipc" else "nccl")  # (nccl = RCCL on ROCm)
-    dev = torch.device("cuda", local)
-    tdev = None if transport == "ipc" else dev  # (gloo reduces host tensors)
+    dev = local
+    tdev = None
     part = PART_SUBTREE if getattr(args, "partition", "peer") == "subtree" else PART_PEER
     ipc_mode = getattr(args, "ipc_mode", "inplace")
     out = partitioned(args, dist, dev, rank, world, descr, metric, part, transport, ipc_mode, tdev)
@@ -142,7 +144,7 @@ def bench_main(args, descr: dict, metric: str):
         # the same partition with the owners' rows read in place over xGMI peer
         # mappings (IPC transport, PS_DIST_F_INPLACE): no records shipped
         try:
-            leg = partitioned(args, dist, dev, rank, world, descr, metric, part, "ipc", "inplace", dev)
+            leg = partitioned(args, dist, dev, rank, world, descr, metric, part, "ipc", "inplace", tdev)
             if rank == 0:
                 out["ipc_in_place"] = {k: leg[k] for k in ("value", "unit", "ms_per_step", "roofline", "config")}
         except Exception as exc:  # noqa: BLE001
@@ -182,7 +184,7 @@ def bench_main(args, descr: dict, metric: str):
 
 
 def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str, part: int,
-                transport: str = "rccl", ipc_mode: str = "inplace", tdev="same"):
+                transport: str = "rccl", ipc_mode: str = "inplace", tdev=None):
     """The node-partitioned run: every rank owns a hash (PART_PEER) or
     subtree (PART_SUBTREE) share of every tree; the frontier rows that cross
     ranks are exchanged each round over the engine's RCCL communicator, or
@@ -190,10 +192,7 @@ def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str
     mappings of the other ranks' buffers: the owners' rows in place
     (ipc_mode "inplace"), the senders' records in place ("zc") or copied
     ("copy").  Returns the bench JSON object on rank 0 (None elsewhere)."""
-    import torch
-
-    tdev = dev if tdev == "same" else tdev
-    local = dev.index if dev.index is not None else 0
+    local = int(dev)
     wl = workload(args, world)
     scaling = getattr(args, "scaling", "weak") if world > 1 else "weak"
     uid = share_bytes(dist, ipc_group_id if transport == "ipc" else unique_id, rank)
@@ -221,7 +220,6 @@ def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str
     if args.warmup and not args.no_check:
         assert warm == expected, (warm, expected)
     dist.barrier()
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
     local_deliv = 0
     if getattr(args, "sync", False):
@@ -238,7 +236,6 @@ def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str
                 local_deliv += eng.wait().deliveries
         if args.steps:
             local_deliv += eng.wait().deliveries
-    torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
     wall, total = job_totals(dist, elapsed, local_deliv, tdev)
@@ -287,7 +284,7 @@ def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str
                          "note": "per-GPU: job expand bytes / slowest rank's expand time / N"},
             "last_step_rank0": {"rounds": st.rounds, "run_ms": st.run_ms,
                                 "expand_ms": st.expand_ms, "host_ms": st.host_ms,
-                                "xchg_path": {0: "none", 1: "zero-copy", 2: "copy"}.get(int(st.xchg_path)),
+                                "xchg_path": {0: "none", 1: "zero-copy", 2: "copy", 3: "in-place"}.get(int(st.xchg_path)),
                                 "xchg_rounds": st.xchg_rounds, "xchg_bytes_received": st.xchg_bytes,
                                 "max_rounds_per_launch": st.plan_max_rounds},
             "plan_opts": eng.plan_opts(),
@@ -299,10 +296,8 @@ def partitioned(args, dist, dev, rank: int, world: int, descr: dict, metric: str
 def one_rank_reference(args, dev, world: int) -> float:
     """ms per step of one engine (no partition) disseminating the weak-scaled
     workload's world x messages alone, pipelined like the partitioned run."""
-    import torch
-
     wl = workload(args, world)
-    local = dev.index if dev.index is not None else 0
+    local = int(dev)
     eng = Engine(wl.n_peers, len(wl.topics), device=local, seed=wl.seed, msg_window=1 << 20)
     try:
         sizes = WL.build_engine_topics(eng, wl)
@@ -310,7 +305,6 @@ def one_rank_reference(args, dev, world: int) -> float:
         for _ in range(max(1, args.warmup)):
             eng.publish(wl.msg_topics)
             assert args.no_check or eng.run().deliveries == expected
-        torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(args.steps):
             eng.publish(wl.msg_topics)
@@ -319,20 +313,17 @@ def one_rank_reference(args, dev, world: int) -> float:
                 eng.wait()
         if args.steps:
             eng.wait()
-        torch.cuda.synchronize()
         return (time.perf_counter() - t0) * 1e3 / max(1, args.steps)
     finally:
         eng.close()
 
 
-def message_sharded(args, dist, dev, rank: int, world: int, descr: dict, totals_dev="same") -> dict:
+def message_sharded(args, dist, dev, rank: int, world: int, descr: dict, totals_dev=None) -> dict:
     """Every rank: a one-GPU engine over the whole topology, its own batch of
     the N=1 workload's messages (weak scaling: N x the messages in all), the
     same pipelined steps; the job's deliveries over the slowest rank's time."""
-    import torch
-
     wl = WL.CONFIGS[args.workload]() if args.scale == 1.0 else WL.scaled(args.workload, args.scale)
-    local = dev.index if dev.index is not None else 0
+    local = int(dev)
     eng = Engine(wl.n_peers, len(wl.topics), device=local, seed=wl.seed)
     sizes = WL.build_engine_topics(eng, wl)
     expected = wl.expected_deliveries(sizes)
@@ -341,7 +332,6 @@ def message_sharded(args, dist, dev, rank: int, world: int, descr: dict, totals_
         st = eng.run()
         assert args.no_check or st.deliveries == expected
     dist.barrier()
-    torch.cuda.synchronize()
     t0 = time.perf_counter()
     local_deliv = 0
     for i in range(args.steps):
@@ -351,10 +341,9 @@ def message_sharded(args, dist, dev, rank: int, world: int, descr: dict, totals_
             local_deliv += eng.wait().deliveries
     if args.steps:
         local_deliv += eng.wait().deliveries
-    torch.cuda.synchronize()
     dist.barrier()
     elapsed = time.perf_counter() - t0
-    wall, total = job_totals(dist, elapsed, local_deliv, dev if totals_dev == "same" else totals_dev)
+    wall, total = job_totals(dist, elapsed, local_deliv, totals_dev)
     eng.close()
     if not args.no_check:
         assert total == expected * args.steps * world, (total, expected * args.steps * world)

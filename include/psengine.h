@@ -335,6 +335,9 @@ typedef struct ps_dist_config {
  * RCCL: refused. */
 #define PS_DIST_F_INPLACE 0x2u
 
+/* GPUs visible to this process (0 without one); a launcher decides from it
+ * whether every rank gets a GPU of its own (RCCL) or ranks share (IPC) */
+int ps_device_count(int32_t* out);
 /* rank 0 creates the RCCL id; the caller ships it to every rank */
 int ps_dist_unique_id(uint8_t id_out[PS_UNIQUE_ID_BYTES]);
 int ps_dist_init(ps_engine* e, const ps_dist_config* dc, const uint8_t id[PS_UNIQUE_ID_BYTES]);

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--partition", default="peer", choices=["peer", "subtree"])
     ap.add_argument("--staggered", action="store_true")
     args = ap.parse_args()
+    PE.load()  # (the engine's /opt/rocm runtime before torch's bundled copies: psengine/dist.py)
     import torch.distributed as dist
 
     dist.init_process_group("gloo")  # bootstrap only: the exchange is RCCL inside the engine
