@@ -24,7 +24,9 @@ def main():
     summ_path, kernel, workload, rtag = sys.argv[1:5]
     note = sys.argv[5] if len(sys.argv) > 5 else f"bench.py --workload {workload.split('-')[0]}"
     summ = json.load(open(summ_path))
-    names = [k for k in summ if f"{kernel}<false" in k and "hbm_write_bytes_per_dispatch" in summ[k]
+    # (full names: the production instances; names truncated by rocprofv3 -T:
+    # the kernel itself -- a bench run launches no recording instance)
+    names = [k for k in summ if (f"{kernel}<false" in k or k == kernel) and "hbm_write_bytes_per_dispatch" in summ[k]
              and "hbm_read_bytes_per_dispatch_x2" in summ[k]]
     if not names:
         sys.exit(f"no {kernel}<false ...> dispatches with both counters in {summ_path}")
