@@ -37,15 +37,6 @@ constexpr uint32_t kMaxWindow = 1u << 30;  // messages per topic per window at m
 
 inline uint32_t ceil_div(uint64_t a, uint64_t b) { return static_cast<uint32_t>((a + b - 1) / b); }
 
-// (A/B, PSAMD_ALLOC_ROUND=1: large allocations rounded up to 2 MiB)
-inline bool alloc_round() {
-  static const bool on = [] {
-    const char* v = std::getenv("PSAMD_ALLOC_ROUND");
-    return v && std::atoi(v) != 0;
-  }();
-  return on;
-}
-
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -68,7 +59,6 @@ struct DevBuf {
     if (n == 0) n = 16;
     if (n <= bytes) return hipSuccess;
     release();
-    if (n >= (64u << 20) && alloc_round()) n = (n + (2u << 20) - 1) & ~static_cast<size_t>((2u << 20) - 1);
     hipError_t e = hipMalloc(&p, n);
     if (e != hipSuccess) {
       p = nullptr;
