@@ -182,6 +182,7 @@ static void read_switches(ps_engine* e) {
   const char* ab = std::getenv("PSAMD_AB");
   if (!ab || std::atoi(ab) == 0) return;
   if (const char* v = std::getenv("PSAMD_TWIN")) e->twin_on = std::atoi(v) != 0;
+  if (const char* v = std::getenv("PSAMD_NARROW")) e->expand_opts = std::atoi(v) == 0 ? kExpandNoNarrow : 0u;
   if (const char* v = std::getenv("PSAMD_CHAIN_WORDS_LEAD"))
     e->chain_words_lead = static_cast<uint32_t>(std::min(1 << 20, std::max(0, std::atoi(v))));
   ps_plan_opts o = current_opts(e);

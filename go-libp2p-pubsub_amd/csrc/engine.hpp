@@ -358,6 +358,7 @@ struct ps_engine {
   double launch_bytes = 16e6;     // planner: a launch's ramp and tail as row bytes (PSAMD_LAUNCH_BYTES)
   uint32_t chain_words = 4096;    // row words per chain wave, the planner's target (8192 until r05: cfg4 0.444 -> 0.404, cfg3 -0.5..1 %, profiles/r05/ab/)
   uint32_t chain_words_lead = 0;  // A/B only (PSAMD_CHAIN_WORDS_LEAD): the same for all but the last launch
+  uint32_t expand_opts = 0;       // ExpandArgs::opts (A/B only: PSAMD_NARROW=0 -> kExpandNoNarrow)
   uint32_t chain_waves = 12;      // chain launches: resident waves per CU at most (ps_plan_opts)
   bool chain_nt = true;           // chain launches: level 0 and the inner levels stored non-temporally
   std::vector<uint64_t> chain_fail_key;  // a pair plan whose chain ranges overflowed the level tables: no chains

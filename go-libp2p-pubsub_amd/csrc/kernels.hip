@@ -540,6 +540,119 @@ __device__ void expand_wide(const ExpandArgs& a, WaveStage& ws, uint32_t p, uint
   }
 }
 
+// Narrow tree entries (rows under kNarrowWords words, at most 64 children, not
+// a topic root): the batch's (child, word) pairs as one flattened index space,
+// 64 per pass, instead of one entry at a time under scalar control.  Item x
+// of entry i (lanes in batch order, items_i = deg_i * W_i, exclusive prefix
+// pre_i) is child j = (x - pre_i) / W_i, word w = (x - pre_i) % W_i; a lane
+// finds its entry by a binary search of the prefix ends over the wave
+// (__shfl), loads the parent's arrival word and the child's flag and
+// generation bytes, and stores as deliver_fresh / deliver_tree do --
+// consecutive lanes write consecutive words of one child row.  The children's
+// generation bytes are stamped, and mark_next raised, in a second flattened
+// pass over the (entry, child) pairs, after every word pass (a child's row may
+// straddle passes, and every pass must see its pre-window generation).
+// (Each narrow entry otherwise cost ~224 scalar instructions of readlane
+// broadcasts, address arithmetic and per-child loops: profiles/r05/expand/.)
+constexpr uint32_t kNarrowWords = 64;
+
+__device__ __forceinline__ bool narrow_on(const ExpandArgs& a) { return (a.opts & kExpandNoNarrow) == 0; }
+
+// Of the wave's 64 nondecreasing `end` values, the first lane whose end
+// exceeds x (x < the last end).
+__device__ __forceinline__ uint32_t owner_of(uint32_t end, uint32_t x) {
+  uint32_t lo = 0;
+#pragma unroll
+  for (uint32_t step = 32; step; step >>= 1) {
+    const uint32_t e = static_cast<uint32_t>(__shfl(static_cast<int>(end), static_cast<int>(lo + step - 1), 64));
+    lo += e <= x ? step : 0u;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ void expand_narrow(const ExpandArgs& a, WaveStage& ws, bool narrow, uint32_t W,
+                                              uint32_t deg, uint32_t c0, uint64_t src, uint64_t crow, bool keep,
+                                              uint32_t lane, uint32_t cur, ExpandCtr& k, EntryCtr& ec) {
+  const uint64_t nmask = __ballot(narrow);
+  if (!nmask) return;
+  const uint32_t items = narrow ? deg * W : 0u;
+  const uint32_t end = wave_incl_scan(items);
+  const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(end), 63));
+  const uint32_t pre = end - items;
+  // entry fields the item lanes fetch from their owner lane
+  const uint32_t wk = W | (keep ? 0x80000000u : 0u);
+  const uint32_t sl = static_cast<uint32_t>(src), sh = static_cast<uint32_t>(src >> 32);
+  const uint32_t cl = static_cast<uint32_t>(crow), ch = static_cast<uint32_t>(crow >> 32);
+  uint8_t* const any = ws.flags;  // per entry: some word of its row is nonzero
+  if (narrow) any[lane] = 0;
+  for (uint32_t b = 0; b < total; b += 64) {
+    const uint32_t x = b + lane;
+    const bool valid = x < total;
+    const uint32_t o = owner_of(end, valid ? x : total - 1);
+    const uint32_t ow = static_cast<uint32_t>(__shfl(static_cast<int>(wk), static_cast<int>(o), 64));
+    const uint32_t Wo = ow & 0x7FFFFFFFu;
+    const uint32_t r = x - static_cast<uint32_t>(__shfl(static_cast<int>(pre), static_cast<int>(o), 64));
+    // j = r / Wo, w = r % Wo (float estimate, off by at most one; r < 2^24)
+    int32_t j = static_cast<int32_t>(static_cast<float>(r) * (1.0f / static_cast<float>(Wo)));
+    int32_t w = static_cast<int32_t>(r) - j * static_cast<int32_t>(Wo);
+    const int32_t lo = w < 0, hi = w >= static_cast<int32_t>(Wo);
+    j += hi - lo;
+    w += (lo - hi) * static_cast<int32_t>(Wo);
+    const uint32_t c = static_cast<uint32_t>(__shfl(static_cast<int>(c0), static_cast<int>(o), 64)) + j;
+    const uint64_t* s = reinterpret_cast<const uint64_t*>(
+        (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(sh), static_cast<int>(o), 64))) << 32) |
+        static_cast<uint32_t>(__shfl(static_cast<int>(sl), static_cast<int>(o), 64)));
+    const uint64_t cw =
+        ((static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(ch), static_cast<int>(o), 64))) << 32) |
+         static_cast<uint32_t>(__shfl(static_cast<int>(cl), static_cast<int>(o), 64))) +
+        static_cast<uint64_t>(j) * Wo + w;
+    uint64_t m = 0;
+    uint32_t f = 0, g = 0;
+    if (valid) {
+      m = s[w];
+      f = a.node_flags[c];
+      g = a.gen[c];
+    }
+    const bool live = valid && (f & kNodeLive);
+    if (live) {
+      const bool stale = g != cur;
+      if (stale || m) {
+        a.seen[cw] = m;
+        k.sw += 1;
+      }
+      if ((f & kNodeInternal) && (ow >> 31)) {
+        a.a_next[cw] = m;
+        k.aw += 1;
+      }
+      k.deliv += __popcll(m);
+    }
+    if (valid && j == 0 && m) any[o] = 1;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // the (entry, child) pairs: generation stamps and the next frontier
+  const uint32_t kids = narrow ? deg : 0u;
+  const uint32_t kend = wave_incl_scan(kids);
+  const uint32_t ktotal = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(kend), 63));
+  const uint32_t kpre = kend - kids;
+  for (uint32_t b = 0; b < ktotal; b += 64) {
+    const uint32_t x = b + lane;
+    const bool valid = x < ktotal;  // (every lane takes part in the shuffles)
+    const uint32_t o = owner_of(kend, valid ? x : ktotal - 1);
+    const uint32_t c = static_cast<uint32_t>(__shfl(static_cast<int>(c0), static_cast<int>(o), 64)) + x -
+                       static_cast<uint32_t>(__shfl(static_cast<int>(kpre), static_cast<int>(o), 64));
+    const uint32_t f = valid ? a.node_flags[c] : 0u;
+    if (f & kNodeLive) {
+      a.gen[c] = static_cast<uint8_t>(cur);
+      if ((f & kNodeInternal) && any[o]) mark_next(a, c);
+    }
+  }
+  ec.ent += static_cast<uint32_t>(__popcll(nmask));
+  ec.ent_words += static_cast<uint32_t>(wave_sum_u64(narrow ? W : 0u));
+  ec.kids += ktotal;
+}
+
 // Frontier entries are dealt to waves round-robin (entry e -> wave e mod
 // n_waves).  A wave loads the metadata of its next 64 entries into lane
 // registers (frontier id, row range, first child, topic fields) and
@@ -615,6 +728,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
                                                                                   : (Ls + (Ls & 1u)) | (4u * bnd) << 16;
     }
     const uint32_t nb = static_cast<uint32_t>(__popcll(__ballot(el < n)));
+    if constexpr (!kRecord && !kDirect) {
+      if (narrow_on(a)) {
+        const bool narrow = el < n && bW > 0 && bW < kNarrowWords && bst != ~0u &&
+                            !(bp == bnb && (bfl & kTopicRootLocal));
+        expand_narrow(a, ws, narrow, bW, bdeg, bc0, (static_cast<uint64_t>(brh) << 32) | brl,
+                      (static_cast<uint64_t>(bch) << 32) | bcl, !(bfl & kTopicSingleStart), lane, cur, k, ec);
+        if (narrow) bW = 0;  // (the entry loop below skips it)
+      }
+    }
     uint32_t q = 0;
     while (q < nb) {
       const uint32_t W0 = rl(bW, q), d0 = rl(bdeg, q), f0 = rl(bfl, q);

@@ -136,7 +136,9 @@ struct ExpandArgs {
   uint32_t gen_cur;
   uint8_t* send;                  // send regions of this round (multi-GPU compaction mode)
   uint64_t send_off[kMaxRanks];   // byte offset of the region for each rank
+  uint32_t opts;                  // kExpand* switches (A/B)
 };
+constexpr uint32_t kExpandNoNarrow = 1;  // narrow entries one at a time (the entry loop), not flattened
 
 // Level mode, pull direction: one wave copies the parents' rows into the
 // rows of a contiguous run of next-level nodes [node_begin, node_end) of one

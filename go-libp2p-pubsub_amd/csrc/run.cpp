@@ -805,6 +805,7 @@ int run_window(ps_engine* e, const std::vector<RunMsg>& msgs, const std::vector<
   bool host_stats_written = false;  // the reduce wrote the deferred slot's pinned rows
   bool reduce_side = false;         // ... on e->rstream (the window's end event goes there)
   a.frontier = e->d_frontier.as<uint32_t>();
+  a.opts = e->expand_opts;
   a.n_front = e->d_nfront.as<uint32_t>();
   a.row_ptr = e->d_row_ptr.as<uint32_t>();
   a.col = e->d_col.as<uint32_t>();
