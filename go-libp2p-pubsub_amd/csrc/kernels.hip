@@ -540,23 +540,37 @@ __device__ void expand_wide(const ExpandArgs& a, WaveStage& ws, uint32_t p, uint
   }
 }
 
-// Narrow tree entries (rows under kNarrowWords words, at most 64 children, not
-// a topic root): the batch's (child, word) pairs as one flattened index space,
-// 64 per pass, instead of one entry at a time under scalar control.  Item x
-// of entry i (lanes in batch order, items_i = deg_i * W_i, exclusive prefix
-// pre_i) is child j = (x - pre_i) / W_i, word w = (x - pre_i) % W_i; a lane
-// finds its entry by a binary search of the prefix ends over the wave
-// (__shfl), loads the parent's arrival word and the child's flag and
-// generation bytes, and stores as deliver_fresh / deliver_tree do --
-// consecutive lanes write consecutive words of one child row.  The children's
-// generation bytes are stamped, and mark_next raised, in a second flattened
-// pass over the (entry, child) pairs, after every word pass (a child's row may
-// straddle passes, and every pass must see its pre-window generation).
-// (Each narrow entry otherwise cost ~224 scalar instructions of readlane
-// broadcasts, address arithmetic and per-child loops: profiles/r05/expand/.)
-constexpr uint32_t kNarrowWords = 64;
+// Short tree entries: staged, not a topic root, and forwarding fewer than
+// kFlatWords words -- a row under 64 words, or the arrival extent of a 64..704
+// word row (one start-group block).  A 64-entry batch of them is one flattened
+// index space instead of one entry at a time under scalar control (each cost
+// ~224 scalar instructions of readlane broadcasts, address arithmetic and
+// per-child loops: profiles/r05/expand/):
+//   K1  (entry, child) pairs: the children's flag and generation bytes into
+//       LDS slots (at most kFlatKids per batch; a batch with more flattens a
+//       prefix of its entries and leaves the rest to the entry loop);
+//   W   (entry, child, word) triples: item x of entry i is child j, word
+//       lo_i + w with (j, w) = divmod(x - pre_i, L_i), pre_i a wave prefix of
+//       deg_i * L_i; a lane finds its entry by a 6-step binary search of the
+//       prefix ends (__shfl), loads the parent's word and stores as
+//       deliver_fresh / deliver_tree do -- consecutive lanes write consecutive
+//       words of one child row;
+//   F   a stale child of an extent row: its seen row outside the extent is
+//       zeroed (the lazy initialisation), one child at a time, 1 KiB per store;
+//   K2  (entry, child) pairs: generation stamps, mark_next and the child's
+//       extent, after every word pass (a child's row may straddle passes, and
+//       every pass must see its pre-window generation).
+// A non-root tree entry's staged extent is already the nonzero range of its
+// words (its parent computed it from the same words, which a tree child
+// receives unchanged), so the extent is forwarded as it is.
+constexpr uint32_t kFlatWords = 64;
+constexpr uint32_t kFlatKids = kStageBytes;  // child slots: ws.flags / ws.gens
+#ifndef PSAMD_FLAT_UNROLL
+#define PSAMD_FLAT_UNROLL 2
+#endif
+constexpr uint32_t kFlatUnroll = PSAMD_FLAT_UNROLL;  // (A/B builds: tools/build_variant.sh -DPSAMD_FLAT_UNROLL=n)
 
-__device__ __forceinline__ bool narrow_on(const ExpandArgs& a) { return (a.opts & kExpandNoNarrow) == 0; }
+__device__ __forceinline__ bool flat_on(const ExpandArgs& a) { return (a.opts & kExpandNoNarrow) == 0; }
 
 // Of the wave's 64 nondecreasing `end` values, the first lane whose end
 // exceeds x (x < the last end).
@@ -570,87 +584,184 @@ __device__ __forceinline__ uint32_t owner_of(uint32_t end, uint32_t x) {
   return lo;
 }
 
-__device__ __forceinline__ void expand_narrow(const ExpandArgs& a, WaveStage& ws, bool narrow, uint32_t W,
-                                              uint32_t deg, uint32_t c0, uint64_t src, uint64_t crow, bool keep,
-                                              uint32_t lane, uint32_t cur, ExpandCtr& k, EntryCtr& ec) {
-  const uint64_t nmask = __ballot(narrow);
-  if (!nmask) return;
-  const uint32_t items = narrow ? deg * W : 0u;
+__device__ __forceinline__ uint32_t shfl_u32(uint32_t v, uint32_t lane) {
+  return static_cast<uint32_t>(__shfl(static_cast<int>(v), static_cast<int>(lane), 64));
+}
+
+// One flat entry's fields, read by its items' lanes from LDS (kept there,
+// not in registers for shuffles: the hot kernel's 80 VGPRs also hold the
+// batch for the entry loop).
+struct __attribute__((aligned(16))) FlatEnt {
+  uint32_t pre;       // first W-pass item
+  uint32_t lk;        // range words L | keep << 31
+  uint32_t sl, sh;    // the staged words' address
+  uint32_t cl, ch;    // child 0's first range word (seen / arrival word index)
+  uint32_t W;         // row words
+  uint32_t kpre;      // first child slot
+  uint32_t c0;        // first child
+  uint32_t xe;        // extent rows: lo | hi << 16 (the children's arrival extent); 0 otherwise
+  uint32_t pad[2];
+};
+static_assert(sizeof(FlatEnt) == 48, "FlatEnt: three 16-B LDS reads");
+constexpr uint32_t kFlatEntOff = 16;  // FlatEnt table in ws.words, after the `any` bytes
+static_assert((kFlatEntOff + 64 * sizeof(FlatEnt) / 8) <= kStageWords, "FlatEnt table fits the stage");
+
+// flat: this lane's entry takes the flat path; xe = its staged words (lo | hi
+// << 16); ext: its children get arrival extents.  Returns whether the entry
+// was handled (false: left to the entry loop, the child slots ran out).
+__device__ __forceinline__ bool expand_flat(const ExpandArgs& a, WaveStage& ws, bool flat, uint32_t W, uint32_t xe,
+                                            bool ext, uint32_t deg, uint32_t c0, uint64_t src, uint64_t crow,
+                                            bool keep, uint32_t lane, uint32_t cur, ExpandCtr& k, EntryCtr& ec) {
+  if (!__ballot(flat)) return false;
+  // the child slots: a prefix of the flat entries whose children fit
+  {
+    const uint32_t kd = flat ? deg : 0u;
+    const uint32_t kin = wave_incl_scan(kd);
+    flat = flat && kin <= kFlatKids;
+  }
+  const uint64_t fmask = __ballot(flat);
+  if (!fmask) return false;
+  uint8_t* const fl = ws.flags;  // per child slot: node flag byte
+  uint8_t* const gn = ws.gens;   // ... generation byte (before this round's stamps)
+  uint8_t* const any = reinterpret_cast<uint8_t*>(ws.words);  // per entry lane: a word of its range is nonzero
+  FlatEnt* const fe = reinterpret_cast<FlatEnt*>(ws.words + kFlatEntOff);
+  const uint32_t lo = xe & 0xFFFFu, L = flat ? (xe >> 16) - lo : 0u;
+  const uint32_t kids = flat ? deg : 0u;
+  const uint32_t kend = wave_incl_scan(kids);
+  const uint32_t ktotal = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(kend), 63));
+  const uint32_t items = L * kids;
   const uint32_t end = wave_incl_scan(items);
   const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(end), 63));
-  const uint32_t pre = end - items;
-  // entry fields the item lanes fetch from their owner lane
-  const uint32_t wk = W | (keep ? 0x80000000u : 0u);
-  const uint32_t sl = static_cast<uint32_t>(src), sh = static_cast<uint32_t>(src >> 32);
-  const uint32_t cl = static_cast<uint32_t>(crow), ch = static_cast<uint32_t>(crow >> 32);
-  uint8_t* const any = ws.flags;  // per entry: some word of its row is nonzero
-  if (narrow) any[lane] = 0;
-  for (uint32_t b = 0; b < total; b += 64) {
-    const uint32_t x = b + lane;
-    const bool valid = x < total;
-    const uint32_t o = owner_of(end, valid ? x : total - 1);
-    const uint32_t ow = static_cast<uint32_t>(__shfl(static_cast<int>(wk), static_cast<int>(o), 64));
-    const uint32_t Wo = ow & 0x7FFFFFFFu;
-    const uint32_t r = x - static_cast<uint32_t>(__shfl(static_cast<int>(pre), static_cast<int>(o), 64));
-    // j = r / Wo, w = r % Wo (float estimate, off by at most one; r < 2^24)
-    int32_t j = static_cast<int32_t>(static_cast<float>(r) * (1.0f / static_cast<float>(Wo)));
-    int32_t w = static_cast<int32_t>(r) - j * static_cast<int32_t>(Wo);
-    const int32_t lo = w < 0, hi = w >= static_cast<int32_t>(Wo);
-    j += hi - lo;
-    w += (lo - hi) * static_cast<int32_t>(Wo);
-    const uint32_t c = static_cast<uint32_t>(__shfl(static_cast<int>(c0), static_cast<int>(o), 64)) + j;
-    const uint64_t* s = reinterpret_cast<const uint64_t*>(
-        (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(sh), static_cast<int>(o), 64))) << 32) |
-        static_cast<uint32_t>(__shfl(static_cast<int>(sl), static_cast<int>(o), 64)));
-    const uint64_t cw =
-        ((static_cast<uint64_t>(static_cast<uint32_t>(__shfl(static_cast<int>(ch), static_cast<int>(o), 64))) << 32) |
-         static_cast<uint32_t>(__shfl(static_cast<int>(cl), static_cast<int>(o), 64))) +
-        static_cast<uint64_t>(j) * Wo + w;
-    uint64_t m = 0;
-    uint32_t f = 0, g = 0;
-    if (valid) {
-      m = s[w];
-      f = a.node_flags[c];
-      g = a.gen[c];
-    }
-    const bool live = valid && (f & kNodeLive);
-    if (live) {
-      const bool stale = g != cur;
-      if (stale || m) {
-        a.seen[cw] = m;
-        k.sw += 1;
-      }
-      if ((f & kNodeInternal) && (ow >> 31)) {
-        a.a_next[cw] = m;
-        k.aw += 1;
-      }
-      k.deliv += __popcll(m);
-    }
-    if (valid && j == 0 && m) any[o] = 1;
+  {
+    FlatEnt e;
+    e.pre = end - items;
+    e.lk = L | (keep ? 0x80000000u : 0u);
+    e.sl = static_cast<uint32_t>(src);
+    e.sh = static_cast<uint32_t>(src >> 32);
+    const uint64_t crow_lo = crow + lo;  // child 0's first word of the range
+    e.cl = static_cast<uint32_t>(crow_lo);
+    e.ch = static_cast<uint32_t>(crow_lo >> 32);
+    e.W = W;
+    e.kpre = kend - kids;
+    e.c0 = c0;
+    e.xe = ext ? xe : 0u;
+    e.pad[0] = e.pad[1] = 0;
+    fe[lane] = e;
+    any[lane] = 0;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // the (entry, child) pairs: generation stamps and the next frontier
-  const uint32_t kids = narrow ? deg : 0u;
-  const uint32_t kend = wave_incl_scan(kids);
-  const uint32_t ktotal = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(kend), 63));
-  const uint32_t kpre = kend - kids;
+  // K1: the children's bytes
   for (uint32_t b = 0; b < ktotal; b += 64) {
     const uint32_t x = b + lane;
-    const bool valid = x < ktotal;  // (every lane takes part in the shuffles)
+    const bool valid = x < ktotal;  // (every lane takes part in the search's shuffles)
     const uint32_t o = owner_of(kend, valid ? x : ktotal - 1);
-    const uint32_t c = static_cast<uint32_t>(__shfl(static_cast<int>(c0), static_cast<int>(o), 64)) + x -
-                       static_cast<uint32_t>(__shfl(static_cast<int>(kpre), static_cast<int>(o), 64));
-    const uint32_t f = valid ? a.node_flags[c] : 0u;
-    if (f & kNodeLive) {
-      a.gen[c] = static_cast<uint8_t>(cur);
-      if ((f & kNodeInternal) && any[o]) mark_next(a, c);
+    if (valid) {
+      const uint32_t c = fe[o].c0 + x - fe[o].kpre;
+      fl[x] = a.node_flags[c];
+      gn[x] = a.gen[c];
     }
   }
-  ec.ent += static_cast<uint32_t>(__popcll(nmask));
-  ec.ent_words += static_cast<uint32_t>(wave_sum_u64(narrow ? W : 0u));
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // W: the words of the ranges, kFlatUnroll passes per step -- every pass's
+  // loads are issued before any pass's stores, so the parent words'
+  // load-to-use latency is paid once per step
+  for (uint32_t b = 0; b < total; b += 64 * kFlatUnroll) {
+    uint64_t m[kFlatUnroll], cw[kFlatUnroll];
+    uint32_t info[kFlatUnroll];  // flag | gen << 8 | keep << 16 | child 0 << 17 | owner << 24
+#pragma unroll
+    for (uint32_t u = 0; u < kFlatUnroll; ++u) {
+      const uint32_t x = b + u * 64 + lane;
+      const bool valid = x < total;
+      const uint32_t o = owner_of(end, valid ? x : total - 1);
+      m[u] = 0;
+      info[u] = 0;
+      cw[u] = 0;
+      if (valid) {
+        const FlatEnt& e = fe[o];
+        const uint32_t Lo = e.lk & 0x7FFFFFFFu;
+        const uint32_t r = x - e.pre;
+        // j = r / Lo, w = r % Lo (float estimate, off by at most one; r < 2^24)
+        int32_t j = static_cast<int32_t>(static_cast<float>(r) * (1.0f / static_cast<float>(Lo)));
+        int32_t w = static_cast<int32_t>(r) - j * static_cast<int32_t>(Lo);
+        const int32_t under = w < 0, over = w >= static_cast<int32_t>(Lo);
+        j += over - under;
+        w += (under - over) * static_cast<int32_t>(Lo);
+        const uint32_t slot = e.kpre + j;
+        const uint64_t* sp = reinterpret_cast<const uint64_t*>((static_cast<uint64_t>(e.sh) << 32) | e.sl);
+        cw[u] = ((static_cast<uint64_t>(e.ch) << 32) | e.cl) + static_cast<uint64_t>(j) * e.W + w;
+        m[u] = sp[w];
+        info[u] = fl[slot] | static_cast<uint32_t>(gn[slot]) << 8 | (e.lk >> 31) << 16 | (j == 0 ? 1u : 0u) << 17 |
+                  o << 24;
+      }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kFlatUnroll; ++u) {
+      const uint32_t f = info[u];
+      if (f & kNodeLive) {  // (valid items only: info is 0 elsewhere)
+        if (((f >> 8) & 0xFFu) != cur || m[u]) {
+          a.seen[cw[u]] = m[u];
+          k.sw += 1;
+        }
+        if ((f & kNodeInternal) && (f & (1u << 16))) {
+          a.a_next[cw[u]] = m[u];
+          k.aw += 1;
+        }
+        k.deliv += __popcll(m[u]);
+      }
+      if ((f & (1u << 17)) && m[u]) any[f >> 24] = 1;
+    }
+  }
+  // F: stale children of extent rows -- zeros outside the range
+  for (uint32_t b = 0; b < ktotal; b += 64) {
+    const uint32_t x = b + lane;
+    const bool valid = x < ktotal;
+    const uint32_t o = owner_of(kend, valid ? x : ktotal - 1);
+    const bool fill = valid && fe[o].xe != 0 && (fl[x] & kNodeLive) && gn[x] != cur;
+    uint64_t todo = __ballot(fill);
+    while (todo) {
+      const uint32_t v = static_cast<uint32_t>(__ffsll(static_cast<long long>(todo))) - 1u;
+      todo &= todo - 1;
+      const uint32_t ov = shfl_u32(o, v), xv = b + v;
+      const FlatEnt& e = fe[ov];
+      const uint32_t Wv = e.W, lov = e.xe & 0xFFFFu, hiv = e.xe >> 16;
+      const uint64_t row =
+          ((static_cast<uint64_t>(e.ch) << 32) | e.cl) - lov + static_cast<uint64_t>(xv - e.kpre) * Wv;
+      for (uint32_t wb = 0; wb < Wv; wb += 128) {
+        const uint32_t w = wb + 2 * lane;  // (W, lo and hi even; rows 16-B aligned)
+        if (w < Wv && (w < lov || w >= hiv)) {
+          *reinterpret_cast<uint4*>(a.seen + row + w) = make_uint4(0u, 0u, 0u, 0u);
+          k.sw += 2;
+        }
+      }
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // K2: generation stamps, the next frontier and its extents
+  for (uint32_t b = 0; b < ktotal; b += 64) {
+    const uint32_t x = b + lane;
+    const bool valid = x < ktotal;
+    const uint32_t o = owner_of(kend, valid ? x : ktotal - 1);
+    const uint32_t f = valid ? fl[x] : 0u;
+    if (f & kNodeLive) {
+      const FlatEnt& e = fe[o];
+      const uint32_t c = e.c0 + x - e.kpre;
+      a.gen[c] = static_cast<uint8_t>(cur);
+      if ((f & kNodeInternal) && any[o]) {
+        mark_next(a, c);
+        if (e.xe) a.ext_next[c] = e.xe;
+      }
+    }
+  }
+  ec.ent += static_cast<uint32_t>(__popcll(fmask));
+  ec.ent_words += static_cast<uint32_t>(wave_sum_u64(L));
   ec.kids += ktotal;
+  return flat;
 }
 
 // Frontier entries are dealt to waves round-robin (entry e -> wave e mod
@@ -712,30 +823,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) voi
       // the staged words [lo, hi) of the entry's row (lo | hi << 16)
       bex = ext_rows(a, T.W, T.flags) && !(bp == T.nbase && (T.flags & kTopicRootLocal)) ? ext_of(a, bp, T.W)
                                                                                           : ext_whole(T.W);
-      const bool from_seen = (T.flags & kTopicSingleStart) && !(bp == T.nbase && (T.flags & kTopicRootLocal));
-      const uint64_t rp = reinterpret_cast<uint64_t>((from_seen ? a.seen : a.a_cur) + T.wbase +
-                                                     static_cast<uint64_t>(bp - T.nbase) * T.W + (bex & 0xFFFFu));
+    }
+    const uint32_t nb = static_cast<uint32_t>(__popcll(__ballot(el < n)));
+    const bool is_root = bp == bnb && (bfl & kTopicRootLocal);
+    const bool staged = el < n && bW > 0 && !(bfl & (kTopicMesh | kEntrySplit)) && bW <= kStageWords && bdeg <= 64;
+    if constexpr (!kRecord && !kDirect) {
+      if (flat_on(a)) {
+        // (before the entry loop's per-lane values are computed: fewer live registers)
+        const bool short_row = staged && !is_root && (bex >> 16) - (bex & 0xFFFFu) < kFlatWords;
+        const uint64_t wbase = (static_cast<uint64_t>(bwh) << 32) | bwl;
+        const uint64_t src = reinterpret_cast<uint64_t>(((bfl & kTopicSingleStart) ? a.seen : a.a_cur) + wbase +
+                                                        static_cast<uint64_t>(bp - bnb) * bW + (bex & 0xFFFFu));
+        const uint64_t crow = wbase + static_cast<uint64_t>(bc0 - bnb) * bW;
+        if (expand_flat(a, ws, short_row, bW, bex, short_row && ext_rows(a, bW, bfl), bdeg, bc0, src, crow,
+                        !(bfl & kTopicSingleStart), lane, cur, k, ec))
+          bW = 0;  // (the entry loop below skips it)
+      }
+    }
+    if (el < n && bW) {
+      // per lane, so the staged phases broadcast them instead of recomputing
+      // them in scalar registers: the staged row's address, the children's
+      // row base, the flag dwords
+      const uint64_t wbase = (static_cast<uint64_t>(bwh) << 32) | bwl;
+      const bool from_seen = (bfl & kTopicSingleStart) && !is_root;
+      const uint64_t rp = reinterpret_cast<uint64_t>((from_seen ? a.seen : a.a_cur) + wbase +
+                                                     static_cast<uint64_t>(bp - bnb) * bW + (bex & 0xFFFFu));
       brl = static_cast<uint32_t>(rp);
       brh = static_cast<uint32_t>(rp >> 32);
       // the children's rows: child c0's row, the others follow at stride W
-      const uint64_t cb = T.wbase + static_cast<uint64_t>(bc0 - T.nbase) * T.W;
+      const uint64_t cb = wbase + static_cast<uint64_t>(bc0 - bnb) * bW;
       bcl = static_cast<uint32_t>(cb);
       bch = static_cast<uint32_t>(cb >> 32);
       bnd = ((bc0 + bdeg + 3u) >> 2) - (bc0 >> 2);
       // stage needs (staged words, even | flag dwords << 16), or ~0: not staged
       const uint32_t Ls = (bex >> 16) - (bex & 0xFFFFu);
-      bst = ((bfl & (kTopicMesh | kEntrySplit)) || T.W > kStageWords || bdeg > 64) ? ~0u
-                                                                                  : (Ls + (Ls & 1u)) | (4u * bnd) << 16;
-    }
-    const uint32_t nb = static_cast<uint32_t>(__popcll(__ballot(el < n)));
-    if constexpr (!kRecord && !kDirect) {
-      if (narrow_on(a)) {
-        const bool narrow = el < n && bW > 0 && bW < kNarrowWords && bst != ~0u &&
-                            !(bp == bnb && (bfl & kTopicRootLocal));
-        expand_narrow(a, ws, narrow, bW, bdeg, bc0, (static_cast<uint64_t>(brh) << 32) | brl,
-                      (static_cast<uint64_t>(bch) << 32) | bcl, !(bfl & kTopicSingleStart), lane, cur, k, ec);
-        if (narrow) bW = 0;  // (the entry loop below skips it)
-      }
+      bst = staged ? (Ls + (Ls & 1u)) | (4u * bnd) << 16 : ~0u;
     }
     uint32_t q = 0;
     while (q < nb) {
