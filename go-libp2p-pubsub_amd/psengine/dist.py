@@ -85,6 +85,22 @@ def workload(args, world: int):
     return wl
 
 
+def pick_transport(requested: str, world: int, ndev: int) -> str:
+    """The exchange transport of a `world`-rank run on `ndev` visible GPUs:
+    RCCL (value's transport) when every rank has a GPU of its
+    own; ranks that share GPUs (this pool's one-GPU boxes) take the IPC
+    transport -- RCCL refuses two ranks on one device."""
+    shared = world > max(1, ndev)
+    if requested == "auto":
+        return "ipc" if shared else "rccl"
+    if requested == "rccl" and shared:
+        raise SystemExit(f"[bench] {world} ranks on {ndev} GPU(s): RCCL refuses two ranks "
+                         "on one device; use --transport ipc")
+    if requested not in ("rccl", "ipc"):
+        raise SystemExit(f"[bench] unknown transport {requested!r}")
+    return requested
+
+
 def bench_main(args, descr: dict, metric: str):
     rank, world, local = env_ranks()
     gpus = getattr(args, "gpus", world)
@@ -115,16 +131,8 @@ def bench_main(args, descr: dict, metric: str):
         dist.barrier()
         dist.destroy_process_group()
         return
-    # the exchange transport: RCCL (value's transport) when every
-    # rank has a GPU of its own; ranks that share GPUs (this pool's one-GPU
-    # boxes) take the IPC transport -- RCCL refuses two ranks on one device
     shared = world > ndev
-    transport = getattr(args, "transport", "auto")
-    if transport == "auto":
-        transport = "ipc" if shared else "rccl"
-    if transport == "rccl" and shared:
-        raise SystemExit(f"[bench] {world} ranks on {ndev} GPU(s): RCCL refuses two ranks "
-                         "on one device; use --transport ipc")
+    transport = pick_transport(getattr(args, "transport", "auto"), world, ndev)
     dev = local
     tdev = None
     part = PART_SUBTREE if getattr(args, "partition", "peer") == "subtree" else PART_PEER
