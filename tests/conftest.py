@@ -30,3 +30,20 @@ def cfg4_full():
     from fullsize_common import Cfg4Tree
 
     return Cfg4Tree()
+
+
+@pytest.fixture(scope="session")
+def cfg3_cut():
+    """BASELINE cfg3's trees (the restated joins), the cut-tree dead mask and
+    or_disseminate's per-topic expectations (fullsize_common.Expect), built
+    once per session for the paced and process-per-rank tests."""
+    import psengine as PE
+    from fullsize_common import Expect, cfg3_dead_mask
+    from psengine import workloads as WL
+
+    wl = WL.cfg3()
+    with PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed) as eng:
+        WL.build_engine_topics(eng, wl)
+        parents = [eng.parents(t) for t in range(len(wl.topics))]
+    live = cfg3_dead_mask(wl, parents)
+    return wl, parents, live, Expect(wl, parents, live)

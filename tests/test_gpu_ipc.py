@@ -30,7 +30,7 @@ import numpy as np
 import pytest
 
 import psengine as PE
-from fullsize_common import check_run, sampled
+from fullsize_common import CLASSES, check_run, paced_starts, sampled
 
 pytestmark = pytest.mark.gpu
 WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "ipc_worker.py")
@@ -162,9 +162,7 @@ def test_bench_two_processes_on_one_gpu():
     total) and the ratio to one rank doing the same messages alone."""
     import json
 
-    import torch
-
-    if torch.cuda.device_count() >= 2:
+    if PE.device_count() >= 2:
         pytest.skip("every rank has a GPU of its own: bench.py takes RCCL")
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--workload", "cfg4", "--scale", "0.05",
@@ -175,3 +173,30 @@ def test_bench_two_processes_on_one_gpu():
     assert line["n_gpus"] == 2 and line["value"] > 0
     assert "IPC transport" in line["config"]["parallelism"]
     assert line["shared_gpu"]["ranks_per_gpu"] == 2 and line["shared_gpu"]["ratio_vs_one_rank"] > 0
+
+
+def test_cfg3_paced_processes_cut_tree(tmp_path, cfg3_cut):
+    """BASELINE cfg3 at full size (1M peers, 64 Zipf topics, 100k messages
+    over start rounds 0..7) on a cut tree, two processes under the peer hash,
+    owners' rows read in place: the summed deliveries and per-round histogram
+    equal or_disseminate's shifted per start group, and 8 sampled delivered
+    sets per topic class (the union over the ranks) equal the oracle's reach."""
+    wl, parents, live, exp = cfg3_cut
+    starts = paced_starts(wl)
+    samples = np.concatenate([np.random.default_rng(7 + t).choice(np.nonzero(wl.msg_topics == t)[0], 8,
+                                                                   replace=False) for t in CLASSES])
+    got = run_ranks(str(tmp_path), 2, "inplace", PE.PART_PEER, wl.n_peers, [ts.root for ts in wl.topics],
+                    np.stack(parents), live, wl.msg_topics, starts=starts, samples=samples, seed=wl.seed,
+                    timeout=170)
+    assert sum(int(g["deliveries"]) for g in got) == exp.deliveries(wl.msg_topics)
+    assert sum(int(g["duplicates"]) for g in got) == 0
+    per = sum(g["per_round"].astype(np.int64) for g in got)
+    want = exp.per_round(wl.msg_topics, starts, max(96, per.shape[0]))
+    assert per[1:].tolist() == want[1:per.shape[0]].tolist()
+    assert all(int(g["xchg_path"]) == PE.XCHG_IN_PLACE for g in got)
+    for k, m in enumerate(samples):
+        t = int(wl.msg_topics[m])
+        u = np.zeros(wl.n_peers, dtype=bool)
+        for g in got:
+            u |= np.unpackbits(g["delivered"][k])[: wl.n_peers].astype(bool)
+        assert np.array_equal(u, exp.reach(t)), (t, int(m))

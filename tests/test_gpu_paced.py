@@ -24,59 +24,11 @@ never hears the message), and is checked against the restatement
 import numpy as np
 import pytest
 
-import oracle as O
 import psengine as PE
-from fullsize_common import cfg3_dead_mask
+from fullsize_common import CLASSES, paced_starts
 from psengine import workloads as WL
 
 pytestmark = pytest.mark.gpu
-CLASSES = (0, 8, 63)
-
-
-def paced_starts(wl):
-    return (WL.stream(wl.seed ^ 0x57A6, np.arange(wl.n_msgs)) % np.uint64(8)).astype(np.uint32)
-
-
-class Expect:
-    """or_disseminate per topic on the cut trees: reached-peer counts, hop
-    histograms and, for the sampled classes, the hops themselves."""
-
-    def __init__(self, wl, parents, live):
-        self.tot = np.zeros(len(wl.topics), dtype=np.int64)
-        self.hist = np.zeros((len(wl.topics), 64), dtype=np.int64)
-        self.hops = {}
-        for t, ts in enumerate(wl.topics):
-            rp, cl = O.parents_to_csr(parents[t])
-            tot, oh, h = O.disseminate(rp, cl, ts.root, live, 1, want_hops=t in CLASSES, hist_len=64)
-            self.tot[t] = tot
-            self.hist[t] = h.astype(np.int64)
-            if t in CLASSES:
-                self.hops[t] = oh[0].copy()
-
-    def deliveries(self, msg_topics):
-        return int((np.bincount(msg_topics, minlength=self.tot.shape[0]).astype(np.int64) * self.tot).sum())
-
-    def per_round(self, msg_topics, starts, n=96):
-        """Message m reaches BFS level d in round starts[m] + d."""
-        per = np.zeros(n, dtype=np.int64)
-        for s0 in np.unique(starts):
-            sel = starts == s0
-            cnt = np.bincount(msg_topics[sel], minlength=self.tot.shape[0]).astype(np.int64)
-            per[int(s0):int(s0) + 64] += cnt @ self.hist
-        return per
-
-    def reach(self, t):
-        return (self.hops[t] != 0xFF) & (self.hops[t] > 0)
-
-
-@pytest.fixture(scope="module")
-def cfg3_cut():
-    wl = WL.cfg3()
-    with PE.Engine(wl.n_peers, len(wl.topics), seed=wl.seed) as eng:
-        WL.build_engine_topics(eng, wl)
-        parents = [eng.parents(t) for t in range(len(wl.topics))]
-    live = cfg3_dead_mask(wl, parents)
-    return wl, parents, live, Expect(wl, parents, live)
 
 
 def engine_on(wl, parents, live, **kw):
