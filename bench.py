@@ -534,6 +534,9 @@ def main():
                     help="N>1: the frontier exchange -- rccl (value's transport, a GPU per rank), ipc (one "
                          "process per rank, buffers mapped across processes; ranks may share a GPU); auto = "
                          "rccl when every rank has its own GPU, else ipc")
+    ap.add_argument("--ipc-leg", action="store_true",
+                    help="N>1 on separate GPUs: also time the peer partition over the IPC transport, owners' rows "
+                         "read in place over xGMI peer mappings (the `ipc_in_place` leg)")
     ap.add_argument("--ipc-mode", default="inplace", choices=["inplace", "zc", "copy"],
                     help="--transport ipc: owners' rows read in place (no records), senders' records read in "
                          "place, or records copied into the receive buffer")

@@ -148,9 +148,10 @@ def bench_main(args, descr: dict, metric: str):
                                  "note": f"{world} processes on one GPU, each owning 1/{world} of every tree, "
                                          f"against one engine disseminating the same {world} x messages alone"}
         dist.barrier()
-    if world > 1 and not shared and transport == "rccl" and not getattr(args, "no_message_leg", False):
+    if world > 1 and not shared and transport == "rccl" and getattr(args, "ipc_leg", False):
         # the same partition with the owners' rows read in place over xGMI peer
         # mappings (IPC transport, PS_DIST_F_INPLACE): no records shipped
+        # (opt-in: never run across separate GPUs on this pool's one-GPU boxes)
         try:
             leg = partitioned(args, dist, dev, rank, world, descr, metric, part, "ipc", "inplace", tdev)
             if rank == 0:
