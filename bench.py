@@ -460,8 +460,10 @@ def general_path(eng, wl, deliv_expected, steps: int, warmup: int = 1, max_start
     finally:
         eng.set_flags(flags)
     comp["workload"] = "the same steps through the compaction path (PS_F_COMPACT): k_expand + frontier compaction"
-    comp["note"] = ("k_expand moves only arrival extents (one start-group block per node and round) and is "
-                    "scalar-issue bound, not HBM-bound: SQ counters and A/B records in profiles/r05/expand/NOTES.md")
+    comp["note"] = ("k_expand moves only arrival extents (one start-group block per node and round); short "
+                    "entries go through flattened (child, word) passes (round 6: ~39 SALU per entry, was 224), "
+                    "and what bounds it is each batch's chain of dependent metadata loads, not HBM: SQ counters "
+                    "and A/B records in profiles/r06/expand/NOTES.md")
     out["compaction"] = comp
     return out
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-end evidence: smoke, the driver's bench command (with the CPU
 # baseline), the GPU suite + kernel traces + PMC passes (gpu_check), the
-# cfg2/cfg4/cfg5 lines and the 4-rank loopback (records and in place).
+# cfg2/cfg4/cfg5 lines and cfg4 on 2 / 4 processes sharing the GPU (IPC transport).
 # Every GPU step has its own time limit; set -e stops at the first failure.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -20,9 +20,9 @@ for W in cfg4 cfg2; do
 done
 echo "[final] cfg5 $(date +%T)"
 timeout -k 10 300 python -u bench.py --workload cfg5 > $O/bench_cfg5.json 2> $O/bench_cfg5.err
-for M in zc inplace; do
-  echo "[final] loopback $M $(date +%T)"
-  timeout -k 10 300 python -u tools/loopback_bench.py --world 4 --scale 1.0 --steps 8 --workload cfg4 --partition peer --mode $M > $O/lb_cfg4_peer4_$M.log 2>&1
-  tail -n 1 $O/lb_cfg4_peer4_$M.log
+for N in 2 4; do
+  echo "[final] $N processes on one GPU (IPC transport, owners' rows in place) $(date +%T)"
+  timeout -k 10 300 python -u bench.py --gpus $N --workload cfg4 --no-cpu > $O/bench_cfg4_g${N}_ipc.json 2> $O/bench_cfg4_g${N}_ipc.err
+  tail -c 300 $O/bench_cfg4_g${N}_ipc.json
 done
 echo "[final] done $(date +%T)"
