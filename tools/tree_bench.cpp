@@ -1,7 +1,7 @@
 // tree_bench.cpp -- host-only timing of the restated tree maintenance
 // (tree.cpp) on a churn plan dumped by tools/tree_bench.py: the cfg5 join /
 // leave cost without a GPU.
-//   g++ -O3 -std=c++17 -Iinclude -Igo-libp2p-pubsub_amd/csrc tools/tree_bench.cpp \
+//   g++ -O3 -std=c++17 -Iinclude -Igo-libp2p-pubsub_amd/csrc tools/tree_bench.cpp
 //       go-libp2p-pubsub_amd/csrc/tree.cpp -o /tmp/tree_bench && /tmp/tree_bench plan.bin
 #include <algorithm>
 #include <chrono>
