@@ -12,7 +12,7 @@ SRC="kernels.hip pull.hip flood.hip gbuild.hip graph.cpp plan.cpp run.cpp api.cp
 for f in $SRC; do
   /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -Wall -Iinclude -I$P/csrc "$@" -c $P/csrc/$f -o $O/$f.o &
 done
-wait
+for j in $(jobs -p); do wait $j || { echo "compile failed" >&2; rm -rf $O; exit 1; }; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -fPIC -shared $O/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib \
   -o $P/lib/libpsengine_$N.so
 rm -rf $O $P/lib/libpsengine_$N.so.*
