@@ -388,7 +388,16 @@ class IpcTransport final : public Transport {
 
   // Opens (or creates) the group's segment, exports this rank's flag block and
   // maps every other rank's; all ranks arrive, then rank 0 unlinks the name.
+  // A rank that fails unlinks it too (the other ranks' barrier times out), so
+  // no segment outlives a failed group in /dev/shm.
   bool open(const char* name, uint32_t n_topics, std::string* err) {
+    const bool ok = open_group(name, n_topics, err);
+    if (!ok) shm_unlink(name);
+    return ok;
+  }
+
+ private:
+  bool open_group(const char* name, uint32_t n_topics, std::string* err) {
     topic_words_ = 4 * n_topics;
     shm_bytes_ = sizeof(IpcShm) + static_cast<size_t>(world_) * topic_words_ * 8;
     const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
@@ -438,6 +447,7 @@ class IpcTransport final : public Transport {
     return true;
   }
 
+ public:
   hipError_t exchange(const uint8_t* send, const std::vector<uint64_t>& send_off,
                       const std::vector<uint64_t>& send_len, uint8_t* recv,
                       const std::vector<uint64_t>& recv_off, const std::vector<uint64_t>& recv_len,
