@@ -430,9 +430,11 @@ def general_path(eng, wl, deliv_expected, steps: int, warmup: int = 1, max_start
         # while batch k's kernels run; every batch completes inside the region
         t0 = time.perf_counter()
         tot = 0
+        eng.publish(wl.msg_topics, starts)
         for i in range(n_steps):
-            eng.publish(wl.msg_topics, starts)
             eng.run_async()
+            if i + 1 < n_steps:  # (batch i + 1 published before waiting for i - 1, as steps_pipelined)
+                eng.publish(wl.msg_topics, starts)
             if i:
                 tot += eng.wait().deliveries
         tot += eng.wait().deliveries
